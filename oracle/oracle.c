@@ -1,0 +1,1011 @@
+/*
+ * oracle.c — CPU restatement of dragonboat v4 internal/raft per-shard step, as specified in
+ * DESIGN.md §1 (= SURVEY.md Appendix A with its VERIFY points decided).
+ *
+ * TEST INFRASTRUCTURE ONLY (checker for the HIP engine, and bench.py's cpu_baseline leg).
+ * PARITY UNPINNED against dragonboat (module github.com/lni/dragonboat/v4
+ * v4.0.0-20240618143154-6a1623140f27 is absent; see oracle.h). Function names follow the
+ * upstream functions they restate; each cites the SURVEY Appendix A section it follows.
+ *
+ * Structure: value semantics everywhere. Messages copy their entries (term, type, len, crc,
+ * payload) into the sender's per-tick outbox arena; the receiver reads them in the next tick.
+ * Groups are independent within a tick, so or_tick() runs groups on worker threads with
+ * group g → worker g % T, the arrangement of dragonboat's step workers.
+ */
+#define _GNU_SOURCE
+#include "oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+#include <zlib.h>
+
+typedef struct {
+  uint64_t term;
+  uint32_t type, len, crc;
+} ent_t;
+
+typedef struct {
+  or_msg_view h;
+  uint32_t ent_off; /* first entry in the sender's outbox arena */
+} msg_t;
+
+typedef struct {
+  uint32_t n[OR_MAX_R];       /* enqueued messages per destination slot */
+  uint32_t emitted[OR_MAX_R]; /* emissions per destination incl. lost ones (loss hash input) */
+  msg_t* m;                   /* [R][K_MAX] */
+  ent_t* ents;                /* entry arena for Replicate payload copies */
+  uint8_t* pay;
+  size_t n_ents, cap_ents;
+} outbox_t;
+
+typedef struct {
+  uint64_t term, vote, leader, committed, applied, last, marker, marker_term;
+  uint64_t snap_index, snap_term, cap_base;
+  uint32_t role, election_tick, heartbeat_tick, rand_timeout, rng_ctr;
+  uint32_t granted, responded, active, err, drops;
+  uint64_t match[OR_MAX_R], next[OR_MAX_R], rsnap[OR_MAX_R];
+  uint8_t rstate[OR_MAX_R];
+  /* log ring: index i in (marker, last] lives at slot i & (L-1) */
+  ent_t* log;
+  uint8_t* logpay;
+  outbox_t ob[2];
+  uint32_t g, s; /* group, slot */
+} rep_t;
+
+struct or_engine {
+  or_config c;
+  uint32_t nrep;
+  rep_t* reps;
+  uint64_t t; /* next tick to run */
+  const or_tick_input* in;
+  /* ring-full etc. use log_capacity */
+};
+
+/* ---------------------------------------------------------------- helpers */
+
+uint64_t or_mix64(uint64_t z) {
+  z ^= z >> 30;
+  z *= 0xBF58476D1CE4E5B9ULL;
+  z ^= z >> 27;
+  z *= 0x94D049BB133111EBULL;
+  z ^= z >> 31;
+  return z;
+}
+
+uint32_t or_crc32(const uint8_t* p, size_t n) {
+  /* zlib's crc32 = CRC-32/IEEE (reflected 0xEDB88320, init/xorout 0xFFFFFFFF) */
+  return (uint32_t)crc32(0L, p, (uInt)n);
+}
+
+void or_payload(const or_engine* e, uint32_t slab, uint32_t group, uint32_t entry, uint8_t* out) {
+  /* DESIGN §1.3 payload generator */
+  uint64_t key = or_mix64(((uint64_t)slab << 56) ^ ((uint64_t)group << 16) ^ (uint64_t)entry ^
+                          (e->c.seed * 0x9E3779B97F4A7C15ULL));
+  uint32_t P = e->c.payload_bytes;
+  for (uint32_t w = 0; w < P / 8; ++w) {
+    uint64_t v = or_mix64(key + (uint64_t)(w + 1) * 0xD1B54A32D192ED03ULL);
+    memcpy(out + 8 * w, &v, 8); /* little-endian host */
+  }
+}
+
+static inline uint32_t id_of(uint32_t slot) { return slot + 1; }
+static inline uint32_t slot_of(uint64_t id) { return (uint32_t)(id - 1); }
+static inline uint32_t quorum(const or_engine* e) { return e->c.replicas / 2 + 1; }
+static inline uint32_t popc(uint32_t x) { return (uint32_t)__builtin_popcount(x); }
+static inline uint64_t u64min(uint64_t a, uint64_t b) { return a < b ? a : b; }
+static inline uint64_t u64max(uint64_t a, uint64_t b) { return a > b ? a : b; }
+static inline ent_t* log_at(const or_engine* e, const rep_t* r, uint64_t i) {
+  return &r->log[i & (e->c.log_capacity - 1)];
+}
+static inline uint8_t* logpay_at(const or_engine* e, const rep_t* r, uint64_t i) {
+  return r->logpay + (size_t)(i & (e->c.log_capacity - 1)) * e->c.payload_bytes;
+}
+
+/* entryLog.term: (0, nil) outside [firstIndex-1, lastIndex]  (SURVEY A.9 / DESIGN §1.2) */
+static uint64_t term_of(const or_engine* e, const rep_t* r, uint64_t i) {
+  if (i == r->marker) return r->marker_term;
+  if (i > r->marker && i <= r->last) return log_at(e, r, i)->term;
+  return 0;
+}
+static int match_term(const or_engine* e, const rep_t* r, uint64_t i, uint64_t t) {
+  return term_of(e, r, i) == t;
+}
+static uint64_t last_term(const or_engine* e, const rep_t* r) { return term_of(e, r, r->last); }
+/* entryLog.upToDate (A.8) */
+static int up_to_date(const or_engine* e, const rep_t* r, uint64_t i, uint64_t t) {
+  uint64_t lt = last_term(e, r);
+  return t > lt || (t == lt && i >= r->last);
+}
+
+static uint32_t rand_timeout(const or_engine* e, const rep_t* r) {
+  uint64_t key = ((uint64_t)r->g << 32) | ((uint64_t)r->s << 24) | (uint64_t)(r->rng_ctr & 0xFFFFFF);
+  uint64_t v = or_mix64(e->c.seed ^ or_mix64(key));
+  return e->c.election_rtt + (uint32_t)(v % e->c.election_rtt);
+}
+
+/* ---------------------------------------------------------------- outbox */
+
+static int lost(const or_engine* e, const rep_t* r, uint32_t dst, uint32_t n) {
+  const or_tick_input* in = e->in;
+  uint32_t rid = r->g * e->c.replicas + r->s;
+  if (in && in->isolate) {
+    if (in->isolate[rid] || in->isolate[r->g * e->c.replicas + dst]) return 1;
+  }
+  if (e->c.drop_ppm) {
+    uint64_t h = or_mix64(e->c.seed ^ or_mix64((e->t << 40) ^ ((uint64_t)rid << 8) ^ dst) ^ (uint64_t)(n + 1));
+    if (h % 1000000ULL < e->c.drop_ppm) return 1;
+  }
+  return 0;
+}
+
+static outbox_t* cur_ob(const or_engine* e, rep_t* r) { return &r->ob[e->t & 1]; }
+
+static void arena_reserve(const or_engine* e, outbox_t* ob, size_t need) {
+  if (ob->n_ents + need <= ob->cap_ents) return;
+  size_t nc = ob->cap_ents ? ob->cap_ents * 2 : 256;
+  while (nc < ob->n_ents + need) nc *= 2;
+  ob->ents = (ent_t*)realloc(ob->ents, nc * sizeof(ent_t));
+  if (e->c.payload_bytes) ob->pay = (uint8_t*)realloc(ob->pay, nc * e->c.payload_bytes);
+  ob->cap_ents = nc;
+}
+
+/* raft.send + transport enqueue. Returns the outbox slot or NULL if the message was lost. */
+static msg_t* send_msg(or_engine* e, rep_t* r, or_msg_view* h) {
+  uint32_t dst = slot_of(h->to);
+  h->from = (uint8_t)id_of(r->s);
+  if (h->type != OR_PROPOSE && h->type != OR_REQUEST_VOTE) h->term = r->term;
+  outbox_t* ob = cur_ob(e, r);
+  uint32_t n = ob->emitted[dst]++;
+  if (lost(e, r, dst, n) || ob->n[dst] >= e->c.max_msgs_per_pair) {
+    r->drops++;
+    return NULL;
+  }
+  msg_t* m = &ob->m[dst * e->c.max_msgs_per_pair + ob->n[dst]++];
+  m->h = *h;
+  m->ent_off = 0;
+  return m;
+}
+
+/* ---------------------------------------------------------------- role transitions (A.5) */
+
+static void reset(or_engine* e, rep_t* r, uint64_t t) {
+  if (t != r->term) {
+    r->term = t;
+    r->vote = 0;
+  }
+  r->leader = 0;
+  r->granted = r->responded = 0;
+  r->election_tick = r->heartbeat_tick = 0;
+  r->rng_ctr++;
+  r->rand_timeout = rand_timeout(e, r);
+  for (uint32_t i = 0; i < e->c.replicas; ++i) {
+    r->match[i] = 0;
+    r->next[i] = r->last + 1;
+    r->rsnap[i] = 0;
+    r->rstate[i] = OR_RETRY;
+  }
+  r->match[r->s] = r->last;
+  r->active = 0;
+}
+
+static void become_follower(or_engine* e, rep_t* r, uint64_t t, uint64_t leader) {
+  r->role = OR_FOLLOWER;
+  reset(e, r, t);
+  r->leader = leader;
+}
+
+static void become_candidate(or_engine* e, rep_t* r) {
+  r->role = OR_CANDIDATE;
+  reset(e, r, r->term + 1);
+  r->leader = 0;
+  r->vote = id_of(r->s);
+}
+
+static int try_commit(or_engine* e, rep_t* r);
+static void broadcast_replicate(or_engine* e, rep_t* r);
+
+/* remote.tryUpdate (A.10) */
+static int remote_try_update(rep_t* r, uint32_t i, uint64_t idx) {
+  if (r->next[i] < idx + 1) r->next[i] = idx + 1;
+  if (r->match[i] < idx) {
+    if (r->rstate[i] == OR_WAIT) r->rstate[i] = OR_RETRY;
+    r->match[i] = idx;
+    return 1;
+  }
+  return 0;
+}
+
+/* raft.appendEntries: n entries at term; payload source: slab entries (slab, g, 0..n-1) or
+ * len-0 no-op when slab < 0. Returns 0 when the batch was refused by the capacity rule. */
+static int append_entries(or_engine* e, rep_t* r, uint32_t n, int slab) {
+  uint32_t L = e->c.log_capacity, P = e->c.payload_bytes;
+  if (r->last + n > r->cap_base + L) return 0;
+  for (uint32_t k = 0; k < n; ++k) {
+    uint64_t idx = r->last + 1 + k;
+    ent_t* en = log_at(e, r, idx);
+    en->term = r->term;
+    en->type = OR_ENTRY_APP;
+    if (slab >= 0 && P) {
+      uint8_t* dst = logpay_at(e, r, idx);
+      or_payload(e, (uint32_t)slab, r->g, k, dst);
+      en->len = P;
+      en->crc = or_crc32(dst, P);
+    } else {
+      en->len = 0;
+      en->crc = 0;
+    }
+  }
+  r->last += n;
+  remote_try_update(r, r->s, r->last);
+  if (e->c.replicas == 1) try_commit(e, r);
+  return 1;
+}
+
+static void become_leader(or_engine* e, rep_t* r) {
+  r->role = OR_LEADER;
+  reset(e, r, r->term);
+  r->leader = id_of(r->s);
+  if (!append_entries(e, r, 1, -1)) r->err |= OR_ERR_RING_FULL;
+}
+
+/* ---------------------------------------------------------------- leader replication (A.12) */
+
+static void remote_progress(rep_t* r, uint32_t i, uint64_t last_sent) {
+  if (r->rstate[i] == OR_REPLICATE_ST) r->next[i] = last_sent + 1;
+  else if (r->rstate[i] == OR_RETRY) r->rstate[i] = OR_WAIT;
+}
+
+static void send_replicate(or_engine* e, rep_t* r, uint32_t to) {
+  if (r->rstate[to] == OR_WAIT || r->rstate[to] == OR_SNAPSHOT) return;
+  uint64_t next = r->next[to];
+  or_msg_view h;
+  memset(&h, 0, sizeof h);
+  h.to = (uint8_t)id_of(to);
+  if (next <= r->marker) { /* log compacted below next: InstallSnapshot path */
+    if (!(r->active & (1u << to))) return;
+    if (r->snap_index == 0) {
+      r->err |= OR_ERR_EMPTY_SNAPSHOT;
+      return;
+    }
+    h.type = OR_INSTALL_SNAPSHOT;
+    h.log_index = r->snap_index;
+    h.log_term = r->snap_term;
+    r->rsnap[to] = r->snap_index;
+    r->rstate[to] = OR_SNAPSHOT;
+    send_msg(e, r, &h);
+    return;
+  }
+  uint32_t n = 0;
+  if (next <= r->last) n = (uint32_t)u64min(e->c.max_entries_per_msg, r->last - next + 1);
+  h.type = OR_REPLICATE;
+  h.log_index = next - 1;
+  h.log_term = term_of(e, r, next - 1);
+  h.commit = r->committed;
+  h.nent = n;
+  if (n > 0) remote_progress(r, to, next + n - 1);
+  msg_t* m = send_msg(e, r, &h);
+  if (m && n) {
+    outbox_t* ob = cur_ob(e, r);
+    arena_reserve(e, ob, n);
+    m->ent_off = (uint32_t)ob->n_ents;
+    for (uint32_t k = 0; k < n; ++k) {
+      ob->ents[ob->n_ents + k] = *log_at(e, r, next + k);
+      if (e->c.payload_bytes)
+        memcpy(ob->pay + (ob->n_ents + k) * e->c.payload_bytes, logpay_at(e, r, next + k), e->c.payload_bytes);
+    }
+    ob->n_ents += n;
+  }
+}
+
+static void broadcast_replicate(or_engine* e, rep_t* r) {
+  for (uint32_t i = 0; i < e->c.replicas; ++i)
+    if (i != r->s) send_replicate(e, r, i);
+}
+
+static void broadcast_heartbeat(or_engine* e, rep_t* r) {
+  for (uint32_t i = 0; i < e->c.replicas; ++i) {
+    if (i == r->s) continue;
+    or_msg_view h;
+    memset(&h, 0, sizeof h);
+    h.type = OR_HEARTBEAT;
+    h.to = (uint8_t)id_of(i);
+    h.commit = u64min(r->match[i], r->committed);
+    send_msg(e, r, &h);
+  }
+}
+
+/* raft.tryCommit + sortMatchValues + entryLog.tryCommit (A.13) */
+static int try_commit(or_engine* e, rep_t* r) {
+  uint32_t R = e->c.replicas;
+  uint64_t v[OR_MAX_R];
+  for (uint32_t i = 0; i < R; ++i) v[i] = r->match[i];
+  for (uint32_t i = 1; i < R; ++i) { /* insertion sort ascending */
+    uint64_t x = v[i];
+    int j = (int)i - 1;
+    while (j >= 0 && v[j] > x) {
+      v[j + 1] = v[j];
+      --j;
+    }
+    v[j + 1] = x;
+  }
+  uint64_t q = v[R - quorum(e)];
+  if (q > r->committed && term_of(e, r, q) == r->term) {
+    r->committed = q;
+    return 1;
+  }
+  return 0;
+}
+
+/* ---------------------------------------------------------------- follower side (A.9) */
+
+static void commit_to(rep_t* r, uint64_t i) {
+  if (i <= r->committed) return;
+  if (i > r->last) {
+    r->err |= OR_ERR_COMMIT_BEYOND_LAST;
+    return;
+  }
+  r->committed = i;
+}
+
+typedef struct {
+  or_msg_view h;
+  const ent_t* ents;
+  const uint8_t* pay;
+} msg_in_t;
+
+static void handle_replicate(or_engine* e, rep_t* r, const msg_in_t* m) {
+  uint32_t L = e->c.log_capacity, P = e->c.payload_bytes;
+  or_msg_view resp;
+  memset(&resp, 0, sizeof resp);
+  resp.type = OR_REPLICATE_RESP;
+  resp.to = m->h.from;
+  if (m->h.log_index < r->committed) {
+    resp.log_index = r->committed;
+    send_msg(e, r, &resp);
+    return;
+  }
+  uint32_t n = m->h.nent;
+  if (match_term(e, r, m->h.log_index, m->h.log_term)) {
+    /* entryLog.getConflictIndex */
+    uint64_t ci = 0;
+    uint32_t k0 = 0;
+    for (uint32_t k = 0; k < n; ++k) {
+      uint64_t idx = m->h.log_index + 1 + k;
+      if (!match_term(e, r, idx, m->ents[k].term)) {
+        ci = idx;
+        k0 = k;
+        break;
+      }
+    }
+    uint64_t last_new = m->h.log_index + n;
+    if (ci != 0 && ci > r->committed && last_new > r->cap_base + L) {
+      r->drops++; /* capacity rule: message dropped, no reply */
+      return;
+    }
+    if (ci != 0) {
+      if (ci <= r->committed) {
+        r->err |= OR_ERR_CONFLICT_COMMITTED;
+      } else { /* entryLog.tryAppend → inMemory.merge: truncate at ci, append */
+        for (uint32_t k = k0; k < n; ++k) {
+          uint64_t idx = m->h.log_index + 1 + k;
+          ent_t* en = log_at(e, r, idx);
+          const ent_t* src = &m->ents[k];
+          en->term = src->term;
+          en->type = src->type;
+          en->len = src->len;
+          if (src->len) {
+            uint8_t* dst = logpay_at(e, r, idx);
+            memcpy(dst, m->pay + (size_t)k * P, src->len);
+            en->crc = or_crc32(dst, src->len);
+            if (en->crc != src->crc) r->err |= OR_ERR_CRC;
+          } else {
+            en->crc = 0;
+          }
+        }
+        r->last = last_new;
+      }
+    }
+    commit_to(r, u64min(last_new, m->h.commit));
+    resp.log_index = last_new;
+  } else {
+    resp.reject = 1;
+    resp.log_index = m->h.log_index;
+    resp.hint = r->last;
+  }
+  send_msg(e, r, &resp);
+}
+
+static void handle_heartbeat(or_engine* e, rep_t* r, const or_msg_view* m) {
+  commit_to(r, m->commit);
+  or_msg_view resp;
+  memset(&resp, 0, sizeof resp);
+  resp.type = OR_HEARTBEAT_RESP;
+  resp.to = m->from;
+  resp.hint = m->hint;
+  resp.hint_high = m->hint_high;
+  send_msg(e, r, &resp);
+}
+
+static void handle_install_snapshot(or_engine* e, rep_t* r, const or_msg_view* m) {
+  or_msg_view resp;
+  memset(&resp, 0, sizeof resp);
+  resp.type = OR_REPLICATE_RESP;
+  resp.to = m->from;
+  uint64_t si = m->log_index, st = m->log_term;
+  if (si <= r->committed) {
+    resp.log_index = r->committed;
+  } else if (match_term(e, r, si, st)) {
+    commit_to(r, si);
+    resp.log_index = r->committed;
+  } else { /* raft.restore → entryLog.restore */
+    r->marker = r->last = r->committed = r->snap_index = si;
+    r->marker_term = r->snap_term = st;
+    resp.log_index = r->last;
+  }
+  send_msg(e, r, &resp);
+}
+
+/* ---------------------------------------------------------------- elections (A.7, A.8) */
+
+static void handle_vote_resp(rep_t* r, uint32_t from_slot, int rejected) {
+  uint32_t bit = 1u << from_slot;
+  if (!(r->responded & bit)) {
+    r->responded |= bit;
+    if (!rejected) r->granted |= bit;
+  }
+}
+
+static void campaign(or_engine* e, rep_t* r) {
+  become_candidate(e, r);
+  handle_vote_resp(r, r->s, 0);
+  if (e->c.replicas == 1) {
+    become_leader(e, r);
+    return;
+  }
+  for (uint32_t i = 0; i < e->c.replicas; ++i) {
+    if (i == r->s) continue;
+    or_msg_view h;
+    memset(&h, 0, sizeof h);
+    h.type = OR_REQUEST_VOTE;
+    h.to = (uint8_t)id_of(i);
+    h.term = r->term;
+    h.log_index = r->last;
+    h.log_term = last_term(e, r);
+    send_msg(e, r, &h);
+  }
+}
+
+static void handle_node_election(or_engine* e, rep_t* r) {
+  if (r->role == OR_LEADER) return;
+  if (r->committed > r->applied) return; /* hasConfigChangeToApply */
+  campaign(e, r);
+}
+
+static void handle_node_request_vote(or_engine* e, rep_t* r, const or_msg_view* m) {
+  or_msg_view resp;
+  memset(&resp, 0, sizeof resp);
+  resp.type = OR_REQUEST_VOTE_RESP;
+  resp.to = m->from;
+  int can_grant = r->vote == 0 || r->vote == m->from;
+  if (can_grant && up_to_date(e, r, m->log_index, m->log_term)) {
+    r->election_tick = 0;
+    r->vote = m->from;
+  } else {
+    resp.reject = 1;
+  }
+  send_msg(e, r, &resp);
+}
+
+static void handle_candidate_vote_resp(or_engine* e, rep_t* r, const or_msg_view* m) {
+  handle_vote_resp(r, slot_of(m->from), m->reject);
+  uint32_t granted = popc(r->granted), total = popc(r->responded);
+  if (granted == quorum(e)) {
+    become_leader(e, r);
+    broadcast_replicate(e, r);
+  } else if (total - granted == quorum(e)) {
+    become_follower(e, r, r->term, 0);
+  }
+}
+
+/* ---------------------------------------------------------------- leader responses (A.10, A.11) */
+
+static void handle_leader_replicate_resp(or_engine* e, rep_t* r, const or_msg_view* m) {
+  uint32_t f = slot_of(m->from);
+  r->active |= 1u << f;
+  if (!m->reject) {
+    int paused = r->rstate[f] == OR_WAIT || r->rstate[f] == OR_SNAPSHOT;
+    if (remote_try_update(r, f, m->log_index)) {
+      /* remote.respondedTo */
+      if (r->rstate[f] == OR_RETRY) {
+        r->next[f] = r->match[f] + 1;
+        r->rsnap[f] = 0;
+        r->rstate[f] = OR_REPLICATE_ST;
+      } else if (r->rstate[f] == OR_SNAPSHOT && r->match[f] >= r->rsnap[f]) {
+        r->next[f] = u64max(r->match[f] + 1, r->rsnap[f] + 1);
+        r->rsnap[f] = 0;
+        r->rstate[f] = OR_RETRY;
+      }
+      if (try_commit(e, r)) broadcast_replicate(e, r);
+      else if (paused) send_replicate(e, r, f);
+    }
+  } else {
+    /* remote.decreaseTo */
+    uint64_t rej = m->log_index, hint = m->hint;
+    int ok;
+    if (r->rstate[f] == OR_REPLICATE_ST) {
+      if (rej <= r->match[f]) ok = 0;
+      else {
+        r->next[f] = r->match[f] + 1;
+        ok = 1;
+      }
+    } else if (r->next[f] - 1 != rej) {
+      ok = 0;
+    } else {
+      if (r->rstate[f] == OR_WAIT) r->rstate[f] = OR_RETRY;
+      r->next[f] = u64max(1, u64min(rej, hint + 1));
+      ok = 1;
+    }
+    if (ok) {
+      if (r->rstate[f] == OR_REPLICATE_ST) { /* enterRetryState → becomeRetry */
+        r->next[f] = r->match[f] + 1;
+        r->rsnap[f] = 0;
+        r->rstate[f] = OR_RETRY;
+      }
+      send_replicate(e, r, f);
+    }
+  }
+}
+
+static void handle_leader_heartbeat_resp(or_engine* e, rep_t* r, const or_msg_view* m) {
+  uint32_t f = slot_of(m->from);
+  r->active |= 1u << f;
+  if (r->rstate[f] == OR_WAIT) r->rstate[f] = OR_RETRY;
+  if (r->match[f] < r->last) send_replicate(e, r, f);
+}
+
+static void handle_leader_check_quorum(or_engine* e, rep_t* r) {
+  uint32_t c = 1 + popc(r->active & ~(1u << r->s));
+  r->active = 0;
+  if (c < quorum(e)) become_follower(e, r, r->term, 0);
+}
+
+/* ---------------------------------------------------------------- proposals */
+
+static void handle_propose(or_engine* e, rep_t* r, const or_msg_view* m) {
+  if (r->role == OR_LEADER) {
+    if (!append_entries(e, r, m->nent, (int)m->src_a)) {
+      r->drops++;
+      return;
+    }
+    broadcast_replicate(e, r);
+  } else if (r->role == OR_FOLLOWER && r->leader != 0 && m->src_b == 0) {
+    or_msg_view h = *m;
+    h.to = (uint8_t)r->leader;
+    h.term = 0;
+    h.src_b = m->src_b + 1;
+    send_msg(e, r, &h);
+  } else {
+    r->drops++;
+  }
+}
+
+/* ---------------------------------------------------------------- Handle (A.3) */
+
+static void handle(or_engine* e, rep_t* r, const msg_in_t* mi);
+
+static void local(or_engine* e, rep_t* r, uint32_t type) {
+  msg_in_t mi;
+  memset(&mi, 0, sizeof mi);
+  mi.h.type = (uint8_t)type;
+  mi.h.from = (uint8_t)id_of(r->s);
+  handle(e, r, &mi);
+}
+
+static void tick(or_engine* e, rep_t* r) {
+  if (r->role == OR_LEADER) { /* leaderTick */
+    r->election_tick++;
+    if (r->election_tick >= e->c.election_rtt) {
+      r->election_tick = 0;
+      if (e->c.check_quorum) local(e, r, OR_CHECK_QUORUM);
+    }
+    r->heartbeat_tick++;
+    if (r->heartbeat_tick >= e->c.heartbeat_rtt) {
+      r->heartbeat_tick = 0;
+      local(e, r, OR_LEADER_HEARTBEAT);
+    }
+  } else { /* nonLeaderTick */
+    r->election_tick++;
+    if (r->election_tick >= r->rand_timeout) {
+      r->election_tick = 0;
+      local(e, r, OR_ELECTION);
+    }
+  }
+}
+
+static int is_leader_msg(uint32_t t) {
+  return t == OR_REPLICATE || t == OR_INSTALL_SNAPSHOT || t == OR_HEARTBEAT;
+}
+
+static void handle(or_engine* e, rep_t* r, const msg_in_t* mi) {
+  const or_msg_view* m = &mi->h;
+  if (m->term != 0 && m->term != r->term) {
+    if (m->type == OR_REQUEST_VOTE && e->c.check_quorum && m->term > r->term && m->hint != m->from &&
+        r->leader != 0 && r->election_tick < e->c.election_rtt)
+      return; /* dropRequestVoteFromHighTermNode */
+    if (m->term > r->term) {
+      become_follower(e, r, m->term, is_leader_msg(m->type) ? m->from : 0);
+    } else {
+      if (e->c.check_quorum && is_leader_msg(m->type)) {
+        or_msg_view h;
+        memset(&h, 0, sizeof h);
+        h.type = OR_NOOP;
+        h.to = m->from;
+        send_msg(e, r, &h);
+      }
+      return;
+    }
+  }
+  switch (m->type) {
+    case OR_LOCAL_TICK: tick(e, r); break;
+    case OR_ELECTION: handle_node_election(e, r); break;
+    case OR_LEADER_HEARTBEAT:
+      if (r->role == OR_LEADER) broadcast_heartbeat(e, r);
+      break;
+    case OR_CHECK_QUORUM:
+      if (r->role == OR_LEADER) handle_leader_check_quorum(e, r);
+      break;
+    case OR_PROPOSE: handle_propose(e, r, m); break;
+    case OR_REPLICATE:
+      if (r->role == OR_LEADER) break;
+      if (r->role == OR_CANDIDATE) become_follower(e, r, r->term, m->from);
+      else {
+        r->election_tick = 0;
+        r->leader = m->from;
+      }
+      handle_replicate(e, r, mi);
+      break;
+    case OR_HEARTBEAT:
+      if (r->role == OR_LEADER) break;
+      if (r->role == OR_CANDIDATE) become_follower(e, r, r->term, m->from);
+      else {
+        r->election_tick = 0;
+        r->leader = m->from;
+      }
+      handle_heartbeat(e, r, m);
+      break;
+    case OR_INSTALL_SNAPSHOT:
+      if (r->role == OR_LEADER) break;
+      if (r->role == OR_CANDIDATE) become_follower(e, r, r->term, m->from);
+      else {
+        r->election_tick = 0;
+        r->leader = m->from;
+      }
+      handle_install_snapshot(e, r, m);
+      break;
+    case OR_REPLICATE_RESP:
+      if (r->role == OR_LEADER) handle_leader_replicate_resp(e, r, m);
+      break;
+    case OR_HEARTBEAT_RESP:
+      if (r->role == OR_LEADER) handle_leader_heartbeat_resp(e, r, m);
+      break;
+    case OR_REQUEST_VOTE: handle_node_request_vote(e, r, m); break;
+    case OR_REQUEST_VOTE_RESP:
+      if (r->role == OR_CANDIDATE) handle_candidate_vote_resp(e, r, m);
+      break;
+    default: break;
+  }
+}
+
+/* ---------------------------------------------------------------- tick driver */
+
+static void step_replica(or_engine* e, rep_t* r) {
+  const or_tick_input* in = e->in;
+  uint32_t R = e->c.replicas, K = e->c.max_msgs_per_pair;
+  uint64_t marker_start = r->marker;
+  outbox_t* ob = cur_ob(e, r);
+  memset(ob->n, 0, sizeof ob->n);
+  memset(ob->emitted, 0, sizeof ob->emitted);
+  ob->n_ents = 0;
+  rep_t* grp = &e->reps[r->g * R];
+  /* 1. inbound messages: source slot ascending, emission order */
+  for (uint32_t src = 0; src < R; ++src) {
+    if (src == r->s) continue;
+    const outbox_t* sob = &grp[src].ob[(e->t + 1) & 1];
+    for (uint32_t k = 0; k < sob->n[r->s]; ++k) {
+      const msg_t* m = &sob->m[r->s * K + k];
+      msg_in_t mi;
+      mi.h = m->h;
+      mi.ents = sob->ents + m->ent_off;
+      mi.pay = sob->pay ? sob->pay + (size_t)m->ent_off * e->c.payload_bytes : NULL;
+      handle(e, r, &mi);
+    }
+  }
+  uint32_t rid = r->g * R + r->s;
+  /* 2. campaign input */
+  if (in && in->campaign && in->campaign[rid]) local(e, r, OR_ELECTION);
+  /* 3. LocalTick */
+  if (!(in && (in->flags & OR_TICK_NO_LOCALTICK))) local(e, r, OR_LOCAL_TICK);
+  /* 4. proposals */
+  if (in && in->prop_target && in->prop_target[r->g] == r->s && in->prop_count[r->g] > 0) {
+    msg_in_t mi;
+    memset(&mi, 0, sizeof mi);
+    mi.h.type = OR_PROPOSE;
+    mi.h.from = (uint8_t)id_of(r->s);
+    mi.h.nent = in->prop_count[r->g];
+    mi.h.src_a = (uint32_t)(e->t % e->c.num_slabs);
+    mi.h.src_b = 0;
+    handle(e, r, &mi);
+  }
+  /* 5. apply + snapshot + compaction */
+  r->applied = r->committed;
+  if (e->c.snapshot_entries && r->applied - r->snap_index >= e->c.snapshot_entries) {
+    r->snap_index = r->applied;
+    r->snap_term = term_of(e, r, r->applied);
+    uint64_t c = r->snap_index > e->c.compaction_overhead ? r->snap_index - e->c.compaction_overhead : 0;
+    if (c > r->marker) {
+      r->marker_term = term_of(e, r, c);
+      r->marker = c;
+    }
+  }
+  r->cap_base = marker_start;
+}
+
+typedef struct {
+  or_engine* e;
+  int w, T;
+} worker_arg;
+
+static void* worker(void* p) {
+  worker_arg* a = (worker_arg*)p;
+  or_engine* e = a->e;
+  for (uint32_t g = (uint32_t)a->w; g < e->c.groups; g += (uint32_t)a->T)
+    for (uint32_t s = 0; s < e->c.replicas; ++s) step_replica(e, &e->reps[g * e->c.replicas + s]);
+  return NULL;
+}
+
+int or_tick(or_engine* e, const or_tick_input* in, int nthreads) {
+  e->in = in;
+  if (nthreads <= 1) {
+    worker_arg a = {e, 0, 1};
+    worker(&a);
+  } else {
+    pthread_t th[256];
+    worker_arg args[256];
+    if (nthreads > 256) nthreads = 256;
+    for (int w = 0; w < nthreads; ++w) {
+      args[w].e = e;
+      args[w].w = w;
+      args[w].T = nthreads;
+      pthread_create(&th[w], NULL, worker, &args[w]);
+    }
+    for (int w = 0; w < nthreads; ++w) pthread_join(th[w], NULL);
+  }
+  e->in = NULL;
+  e->t++;
+  return 0;
+}
+
+/* ---------------------------------------------------------------- lifecycle / views */
+
+int or_create(const or_config* cfg, or_engine** out) {
+  const or_config* c = cfg;
+  if (c->replicas < 1 || c->replicas > OR_MAX_R) return -1;
+  if (c->log_capacity < 16 || (c->log_capacity & (c->log_capacity - 1))) return -1;
+  if (c->payload_bytes && (c->payload_bytes < 16 || c->payload_bytes > 1024 ||
+                           (c->payload_bytes & (c->payload_bytes - 1))))
+    return -1;
+  if (c->max_entries_per_msg < 1 || c->max_entries_per_msg > 64) return -1;
+  if (c->max_msgs_per_pair < 1 || c->max_msgs_per_pair > 16) return -1;
+  if (c->num_slabs < 2 || c->election_rtt < 1 || c->heartbeat_rtt < 1) return -1;
+  or_engine* e = (or_engine*)calloc(1, sizeof *e);
+  e->c = *c;
+  e->nrep = c->groups * c->replicas;
+  e->reps = (rep_t*)calloc(e->nrep, sizeof(rep_t));
+  for (uint32_t i = 0; i < e->nrep; ++i) {
+    rep_t* r = &e->reps[i];
+    r->g = i / c->replicas;
+    r->s = i % c->replicas;
+    r->log = (ent_t*)calloc(c->log_capacity, sizeof(ent_t));
+    if (c->payload_bytes) r->logpay = (uint8_t*)calloc((size_t)c->log_capacity, c->payload_bytes);
+    for (int b = 0; b < 2; ++b)
+      r->ob[b].m = (msg_t*)calloc((size_t)c->replicas * c->max_msgs_per_pair, sizeof(msg_t));
+  }
+  *out = e;
+  return 0;
+}
+
+void or_destroy(or_engine* e) {
+  if (!e) return;
+  for (uint32_t i = 0; i < e->nrep; ++i) {
+    rep_t* r = &e->reps[i];
+    free(r->log);
+    free(r->logpay);
+    for (int b = 0; b < 2; ++b) {
+      free(r->ob[b].m);
+      free(r->ob[b].ents);
+      free(r->ob[b].pay);
+    }
+  }
+  free(e->reps);
+  free(e);
+}
+
+/* peer.go Launch(newNode) → becomeFollower(1, NoLeader); bootstrap(addresses) (A.2) */
+int or_bootstrap(or_engine* e) {
+  uint32_t R = e->c.replicas;
+  for (uint32_t i = 0; i < e->nrep; ++i) {
+    rep_t* r = &e->reps[i];
+    r->term = 0;
+    r->last = r->marker = r->marker_term = r->committed = r->applied = 0;
+    r->snap_index = r->snap_term = r->cap_base = 0;
+    r->err = r->drops = 0;
+    r->rng_ctr = 0;
+    become_follower(e, r, 1, 0);
+    for (uint32_t k = 0; k < R; ++k) {
+      ent_t* en = log_at(e, r, k + 1);
+      en->term = 1;
+      en->type = OR_ENTRY_CONFIG;
+      en->len = 0;
+      en->crc = 0;
+    }
+    r->last = R;
+    r->committed = R;
+    for (uint32_t k = 0; k < R; ++k) { /* addNode → setRemote(id, 0, last+1) */
+      r->match[k] = 0;
+      r->next[k] = R + 1;
+      r->rsnap[k] = 0;
+      r->rstate[k] = OR_RETRY;
+    }
+    for (int b = 0; b < 2; ++b) {
+      memset(r->ob[b].n, 0, sizeof r->ob[b].n);
+      r->ob[b].n_ents = 0;
+    }
+  }
+  e->t = 0;
+  return 0;
+}
+
+uint64_t or_tick_count(const or_engine* e) { return e->t; }
+
+int or_get_replica(const or_engine* e, uint32_t rid, or_replica_view* v) {
+  if (rid >= e->nrep) return -1;
+  const rep_t* r = &e->reps[rid];
+  memset(v, 0, sizeof *v);
+  v->term = r->term;
+  v->vote = r->vote;
+  v->leader = r->leader;
+  v->committed = r->committed;
+  v->applied = r->applied;
+  v->last = r->last;
+  v->marker = r->marker;
+  v->marker_term = r->marker_term;
+  v->snap_index = r->snap_index;
+  v->snap_term = r->snap_term;
+  v->cap_base = r->cap_base;
+  v->role = r->role;
+  v->election_tick = r->election_tick;
+  v->heartbeat_tick = r->heartbeat_tick;
+  v->rand_timeout = r->rand_timeout;
+  v->rng_ctr = r->rng_ctr;
+  v->granted = r->granted;
+  v->responded = r->responded;
+  v->active = r->active;
+  v->err = r->err;
+  v->drops = r->drops;
+  for (uint32_t k = 0; k < e->c.replicas; ++k) {
+    v->match[k] = r->match[k];
+    v->next[k] = r->next[k];
+    v->rsnap[k] = r->rsnap[k];
+    v->rstate[k] = r->rstate[k];
+  }
+  return 0;
+}
+
+static const outbox_t* last_ob(const or_engine* e, const rep_t* r) { return &r->ob[(e->t + 1) & 1]; }
+
+int or_get_msgs(const or_engine* e, uint32_t rid, uint32_t dst, or_msg_view* out, uint32_t cap) {
+  if (rid >= e->nrep || dst >= e->c.replicas) return -1;
+  const outbox_t* ob = last_ob(e, &e->reps[rid]);
+  uint32_t n = ob->n[dst];
+  for (uint32_t k = 0; k < n && k < cap; ++k) out[k] = ob->m[dst * e->c.max_msgs_per_pair + k].h;
+  return (int)n;
+}
+
+int or_get_msg_terms(const or_engine* e, uint32_t rid, uint32_t dst, uint32_t k, uint64_t* terms, uint32_t cap) {
+  if (rid >= e->nrep || dst >= e->c.replicas) return -1;
+  const outbox_t* ob = last_ob(e, &e->reps[rid]);
+  if (k >= ob->n[dst]) return -1;
+  const msg_t* m = &ob->m[dst * e->c.max_msgs_per_pair + k];
+  uint32_t n = m->h.type == OR_REPLICATE ? m->h.nent : 0;
+  for (uint32_t i = 0; i < n && i < cap; ++i) terms[i] = ob->ents[m->ent_off + i].term;
+  return (int)n;
+}
+
+int or_get_entry(const or_engine* e, uint32_t rid, uint64_t index, or_entry_view* out, uint8_t* payload) {
+  if (rid >= e->nrep) return -1;
+  const rep_t* r = &e->reps[rid];
+  if (index <= r->marker || index > r->last) return -1;
+  const ent_t* en = log_at(e, r, index);
+  out->term = en->term;
+  out->type = en->type;
+  out->len = en->len;
+  out->crc = en->crc;
+  out->_pad = 0;
+  if (payload && en->len) memcpy(payload, logpay_at(e, r, index), en->len);
+  return 0;
+}
+
+int or_import_replica(or_engine* e, uint32_t rid, const or_replica_view* v, const uint64_t* terms,
+                      const uint32_t* types, const uint8_t* payloads) {
+  if (rid >= e->nrep) return -1;
+  rep_t* r = &e->reps[rid];
+  if (v->last < v->marker || v->last - v->marker > e->c.log_capacity) return -1;
+  r->term = v->term;
+  r->vote = v->vote;
+  r->leader = v->leader;
+  r->committed = v->committed;
+  r->applied = v->applied;
+  r->last = v->last;
+  r->marker = v->marker;
+  r->marker_term = v->marker_term;
+  r->snap_index = v->snap_index;
+  r->snap_term = v->snap_term;
+  r->cap_base = v->cap_base;
+  r->role = v->role;
+  r->election_tick = v->election_tick;
+  r->heartbeat_tick = v->heartbeat_tick;
+  r->rand_timeout = v->rand_timeout;
+  r->rng_ctr = v->rng_ctr;
+  r->granted = v->granted;
+  r->responded = v->responded;
+  r->active = v->active;
+  r->err = v->err;
+  r->drops = v->drops;
+  for (uint32_t k = 0; k < OR_MAX_R; ++k) {
+    r->match[k] = v->match[k];
+    r->next[k] = v->next[k];
+    r->rsnap[k] = v->rsnap[k];
+    r->rstate[k] = v->rstate[k];
+  }
+  uint32_t P = e->c.payload_bytes;
+  for (uint64_t i = v->marker + 1; i <= v->last; ++i) {
+    uint64_t k = i - v->marker - 1;
+    ent_t* en = log_at(e, r, i);
+    en->term = terms[k];
+    en->type = types ? types[k] : OR_ENTRY_APP;
+    if (payloads && P && en->type == OR_ENTRY_APP) {
+      en->len = P;
+      memcpy(logpay_at(e, r, i), payloads + k * P, P);
+      en->crc = or_crc32(logpay_at(e, r, i), P);
+    } else {
+      en->len = 0;
+      en->crc = 0;
+    }
+  }
+  return 0;
+}
+
+int or_deliver(or_engine* e, uint32_t rid_src, const or_msg_view* m) {
+  if (rid_src >= e->nrep) return -1;
+  rep_t* r = &e->reps[rid_src];
+  outbox_t* ob = &r->ob[(e->t + 1) & 1];
+  uint32_t dst = slot_of(m->to);
+  if (dst >= e->c.replicas || ob->n[dst] >= e->c.max_msgs_per_pair) return -1;
+  msg_t* mm = &ob->m[dst * e->c.max_msgs_per_pair + ob->n[dst]++];
+  mm->h = *m;
+  mm->ent_off = 0;
+  if (m->type == OR_REPLICATE && m->nent) {
+    if (m->log_index < r->marker || m->log_index + m->nent > r->last) return -1;
+    arena_reserve(e, ob, m->nent);
+    mm->ent_off = (uint32_t)ob->n_ents;
+    for (uint32_t k = 0; k < m->nent; ++k) {
+      ob->ents[ob->n_ents + k] = *log_at(e, r, m->log_index + 1 + k);
+      if (e->c.payload_bytes)
+        memcpy(ob->pay + (ob->n_ents + k) * e->c.payload_bytes, logpay_at(e, r, m->log_index + 1 + k),
+               e->c.payload_bytes);
+    }
+    ob->n_ents += m->nent;
+  }
+  return 0;
+}

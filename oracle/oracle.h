@@ -1,0 +1,114 @@
+/*
+ * oracle.h — CPU restatement of dragonboat v4's per-shard Raft step (TEST INFRASTRUCTURE).
+ *
+ * This is the parity oracle for raftd-amd's HIP step engine. Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it. It is never a
+ * fallback for the product path.
+ *
+ * PARITY UNPINNED against dragonboat: the algorithm lives in the third-party Go module
+ * github.com/lni/dragonboat/v4 v4.0.0-20240618143154-6a1623140f27 (/root/reference/go.mod:9,
+ * go.sum:268-269), package internal/raft, which is not present in this container and cannot
+ * be built here (no Go toolchain). This file restates it from SURVEY.md Appendix A with the
+ * VERIFY decisions recorded in DESIGN.md §1. It is cross-checked against the independent
+ * Python restatement oracle/pyraft.py and the known-answer tests in tests/golden/.
+ * Call sites in the reference that reach this path: raft/raft_manager.go:92-100 (config),
+ * :109 (NewNodeHost), :142 (StartOnDiskReplica), raft/members.go:21 (GetLeaderID).
+ */
+#ifndef RAFT_ORACLE_H
+#define RAFT_ORACLE_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OR_MAX_R 8
+
+/* raftpb.MessageType numbering as recalled (VERIFY); only the values below are used. */
+enum {
+  OR_LOCAL_TICK = 0, OR_ELECTION = 1, OR_LEADER_HEARTBEAT = 2, OR_NOOP = 4, OR_PROPOSE = 7,
+  OR_CHECK_QUORUM = 10, OR_REPLICATE = 12, OR_REPLICATE_RESP = 13, OR_REQUEST_VOTE = 14,
+  OR_REQUEST_VOTE_RESP = 15, OR_INSTALL_SNAPSHOT = 16, OR_HEARTBEAT = 17, OR_HEARTBEAT_RESP = 18
+};
+enum { OR_FOLLOWER = 0, OR_CANDIDATE = 1, OR_LEADER = 2 };
+enum { OR_RETRY = 0, OR_WAIT = 1, OR_REPLICATE_ST = 2, OR_SNAPSHOT = 3 };
+enum { OR_ENTRY_APP = 0, OR_ENTRY_CONFIG = 1 };
+enum {
+  OR_ERR_CONFLICT_COMMITTED = 1, OR_ERR_COMMIT_BEYOND_LAST = 2, OR_ERR_RING_FULL = 4,
+  OR_ERR_CRC = 8, OR_ERR_EMPTY_SNAPSHOT = 16
+};
+#define OR_TICK_NO_LOCALTICK 1u
+
+typedef struct or_config {
+  uint32_t groups, replicas, log_capacity, payload_bytes;
+  uint32_t max_entries_per_msg, max_msgs_per_pair, num_slabs;
+  uint32_t election_rtt, heartbeat_rtt, check_quorum;
+  uint32_t snapshot_entries, compaction_overhead;
+  uint32_t drop_ppm;
+  uint32_t _pad;
+  uint64_t seed;
+} or_config;
+
+/* Field order identical to rg_replica_view (include/raftgpu.h) so tests compare by name. */
+typedef struct or_replica_view {
+  uint64_t term, vote, leader, committed, applied, last, marker, marker_term;
+  uint64_t snap_index, snap_term, cap_base;
+  uint32_t role, election_tick, heartbeat_tick, rand_timeout, rng_ctr;
+  uint32_t granted, responded, active, err, drops;
+  uint64_t match[OR_MAX_R], next[OR_MAX_R], rsnap[OR_MAX_R];
+  uint8_t rstate[OR_MAX_R];
+} or_replica_view;
+
+typedef struct or_msg_view {
+  uint8_t type, from, to, reject;
+  uint32_t nent;
+  uint64_t term, log_term, log_index, commit, hint, hint_high;
+  uint32_t src_a, src_b; /* Propose: slab id, hop count */
+} or_msg_view;
+
+typedef struct or_entry_view {
+  uint64_t term;
+  uint32_t type, len, crc, _pad;
+} or_entry_view;
+
+typedef struct or_tick_input {
+  const uint8_t* prop_target; /* [G] slot, 0xFF none; NULL = no proposals */
+  const uint32_t* prop_count; /* [G] */
+  const uint8_t* campaign;    /* [G*R] nonzero → Handle(Election) before LocalTick; NULL none */
+  const uint8_t* isolate;     /* [G*R] nonzero → all messages to/from the replica lost */
+  uint32_t flags;
+} or_tick_input;
+
+typedef struct or_engine or_engine;
+
+int or_create(const or_config* cfg, or_engine** out);
+void or_destroy(or_engine* e);
+int or_bootstrap(or_engine* e);
+/* One tick over all groups using `nthreads` worker threads (group g → worker g % nthreads,
+ * dragonboat's step-worker partition). */
+int or_tick(or_engine* e, const or_tick_input* in, int nthreads);
+uint64_t or_tick_count(const or_engine* e);
+
+int or_get_replica(const or_engine* e, uint32_t rid, or_replica_view* out);
+/* Messages emitted by `rid` to slot `dst` in the last tick. Returns count; fills up to cap. */
+int or_get_msgs(const or_engine* e, uint32_t rid, uint32_t dst, or_msg_view* out, uint32_t cap);
+/* Inline entry terms of message k (rid → dst). */
+int or_get_msg_terms(const or_engine* e, uint32_t rid, uint32_t dst, uint32_t k, uint64_t* terms, uint32_t cap);
+/* Log entry at `index` of replica rid (must be in (marker, last]). payload may be NULL. */
+int or_get_entry(const or_engine* e, uint32_t rid, uint64_t index, or_entry_view* out, uint8_t* payload);
+/* Replace a replica's state and log (entries for indices marker+1 .. last). */
+int or_import_replica(or_engine* e, uint32_t rid, const or_replica_view* v,
+                      const uint64_t* terms, const uint32_t* types, const uint8_t* payloads);
+/* Append a message to rid_src's most recent outbox so it is delivered next tick. Replicate
+ * entries are taken from the sender's current log (indices log_index+1 ..). */
+int or_deliver(or_engine* e, uint32_t rid_src, const or_msg_view* m);
+/* Proposal payload generator. */
+void or_payload(const or_engine* e, uint32_t slab, uint32_t group, uint32_t entry, uint8_t* out);
+uint32_t or_crc32(const uint8_t* p, size_t n);
+uint64_t or_mix64(uint64_t z);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

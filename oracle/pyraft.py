@@ -1,0 +1,607 @@
+"""Independent pure-Python restatement of the per-shard Raft step.
+
+TEST INFRASTRUCTURE. Written separately from oracle/oracle.c (different structure: objects,
+dict messages, Python lists as logs) so that tick-by-tick agreement between the two on random
+seeded traces is evidence that the restatement says what DESIGN.md §1 says. It restates
+dragonboat v4 internal/raft (module github.com/lni/dragonboat/v4
+v4.0.0-20240618143154-6a1623140f27, absent here: parity with dragonboat itself is unpinned)
+following SURVEY.md Appendix A:
+  A.3 Handle / onMessageTermNotMatched   -> Replica.handle
+  A.5 reset / become*                    -> Replica.reset / become_*
+  A.6 leaderTick / nonLeaderTick         -> Replica.tick
+  A.7 campaign                           -> Replica.campaign
+  A.8 handleNodeRequestVote / VoteResp   -> Replica.on_request_vote / on_vote_resp
+  A.9 handleReplicateMessage             -> Replica.on_replicate
+  A.10 handleLeaderReplicateResp         -> Replica.on_replicate_resp
+  A.11 handleLeaderHeartbeatResp         -> Replica.on_heartbeat_resp
+  A.12 sendReplicateMessage              -> Replica.send_replicate
+  A.13 tryCommit                         -> Replica.try_commit
+Only for small configurations (it is slow).
+"""
+from __future__ import annotations
+
+import zlib
+
+M64 = (1 << 64) - 1
+
+LOCAL_TICK, ELECTION, LEADER_HEARTBEAT, NOOP, PROPOSE = 0, 1, 2, 4, 7
+CHECK_QUORUM, REPLICATE, REPLICATE_RESP, REQUEST_VOTE, REQUEST_VOTE_RESP = 10, 12, 13, 14, 15
+INSTALL_SNAPSHOT, HEARTBEAT, HEARTBEAT_RESP = 16, 17, 18
+FOLLOWER, CANDIDATE, LEADER = 0, 1, 2
+RETRY, WAIT, REPL, SNAP = 0, 1, 2, 3
+ERR_CONFLICT, ERR_BEYOND, ERR_RING, ERR_CRC, ERR_EMPTY_SNAP = 1, 2, 4, 8, 16
+LEADER_MSGS = (REPLICATE, INSTALL_SNAPSHOT, HEARTBEAT)
+
+
+def mix64(z: int) -> int:
+    z &= M64
+    z ^= z >> 30
+    z = (z * 0xBF58476D1CE4E5B9) & M64
+    z ^= z >> 27
+    z = (z * 0x94D049BB133111EB) & M64
+    z ^= z >> 31
+    return z
+
+
+def payload(seed: int, slab: int, group: int, entry: int, P: int) -> bytes:
+    key = mix64(((slab << 56) ^ (group << 16) ^ entry ^ ((seed * 0x9E3779B97F4A7C15) & M64)) & M64)
+    out = bytearray()
+    for w in range(P // 8):
+        out += mix64((key + (w + 1) * 0xD1B54A32D192ED03) & M64).to_bytes(8, "little")
+    return bytes(out)
+
+
+def msg(type, to, **kw):
+    m = dict(type=type, to=to, frm=0, reject=0, nent=0, term=0, log_term=0, log_index=0, commit=0,
+             hint=0, hint_high=0, src_a=0, src_b=0, ents=())
+    m.update(kw)
+    return m
+
+
+class Entry:
+    __slots__ = ("term", "type", "data", "crc")
+
+    def __init__(self, term, type=0, data=b""):
+        self.term, self.type, self.data = term, type, data
+        self.crc = zlib.crc32(data) if data else 0
+
+
+class Remote:
+    __slots__ = ("match", "next", "snap", "state")
+
+    def __init__(self, match, nxt):
+        self.match, self.next, self.snap, self.state = match, nxt, 0, RETRY
+
+    # remote.go
+    def try_update(self, idx):
+        if self.next < idx + 1:
+            self.next = idx + 1
+        if self.match < idx:
+            if self.state == WAIT:
+                self.state = RETRY
+            self.match = idx
+            return True
+        return False
+
+    def become_retry(self):
+        self.next = max(self.match + 1, self.snap + 1) if self.state == SNAP else self.match + 1
+        self.snap = 0
+        self.state = RETRY
+
+    def responded_to(self):
+        if self.state == RETRY:
+            self.next, self.snap, self.state = self.match + 1, 0, REPL
+        elif self.state == SNAP and self.match >= self.snap:
+            self.become_retry()
+
+    def decrease_to(self, rejected, last):
+        if self.state == REPL:
+            if rejected <= self.match:
+                return False
+            self.next = self.match + 1
+            return True
+        if self.next - 1 != rejected:
+            return False
+        if self.state == WAIT:
+            self.state = RETRY
+        self.next = max(1, min(rejected, last + 1))
+        return True
+
+    def progress(self, last_sent):
+        if self.state == REPL:
+            self.next = last_sent + 1
+        elif self.state == RETRY:
+            self.state = WAIT
+
+    def paused(self):
+        return self.state in (WAIT, SNAP)
+
+
+class Replica:
+    def __init__(self, sim, g, s):
+        self.sim, self.g, self.s, self.id = sim, g, s, s + 1
+        self.term = self.vote = self.leader = 0
+        self.role = FOLLOWER
+        self.committed = self.applied = 0
+        self.marker = self.marker_term = 0
+        self.log = []  # log[k] = entry at index marker+1+k
+        self.snap_index = self.snap_term = self.cap_base = 0
+        self.etick = self.htick = self.rand_to = self.rng = 0
+        self.votes = {}
+        self.active = set()
+        self.err = self.drops = 0
+        self.remotes = []
+        self.out = {}
+        self.emitted = {}
+
+    # -- log (entryLog) --
+    @property
+    def last(self):
+        return self.marker + len(self.log)
+
+    def term_at(self, i):
+        if i == self.marker:
+            return self.marker_term
+        if self.marker < i <= self.last:
+            return self.log[i - self.marker - 1].term
+        return 0
+
+    def up_to_date(self, i, t):
+        lt = self.term_at(self.last)
+        return t > lt or (t == lt and i >= self.last)
+
+    def commit_to(self, i):
+        if i <= self.committed:
+            return
+        if i > self.last:
+            self.err |= ERR_BEYOND
+            return
+        self.committed = i
+
+    # -- transport --
+    def send(self, m):
+        c = self.sim.cfg
+        m["frm"] = self.id
+        if m["type"] not in (PROPOSE, REQUEST_VOTE):
+            m["term"] = self.term
+        d = m["to"] - 1
+        n = self.emitted.get(d, 0)
+        self.emitted[d] = n + 1
+        if self.sim.lost(self, d, n) or len(self.out.setdefault(d, [])) >= c["max_msgs_per_pair"]:
+            self.drops += 1
+            return False
+        self.out[d].append(m)
+        return True
+
+    # -- transitions --
+    def reset(self, t):
+        if t != self.term:
+            self.term, self.vote = t, 0
+        self.leader = 0
+        self.votes = {}
+        self.etick = self.htick = 0
+        self.rng += 1
+        c = self.sim.cfg
+        key = (self.g << 32) | (self.s << 24) | (self.rng & 0xFFFFFF)
+        self.rand_to = c["election_rtt"] + mix64(c["seed"] ^ mix64(key)) % c["election_rtt"]
+        self.remotes = [Remote(0, self.last + 1) for _ in range(self.sim.R)]
+        self.remotes[self.s].match = self.last
+        self.active = set()
+
+    def become_follower(self, t, leader):
+        self.role = FOLLOWER
+        self.reset(t)
+        self.leader = leader
+
+    def become_candidate(self):
+        self.role = CANDIDATE
+        self.reset(self.term + 1)
+        self.leader = 0
+        self.vote = self.id
+
+    def become_leader(self):
+        self.role = LEADER
+        self.reset(self.term)
+        self.leader = self.id
+        if not self.append(1, None):
+            self.err |= ERR_RING
+
+    def append(self, n, slab):
+        c = self.sim.cfg
+        if self.last + n > self.cap_base + c["log_capacity"]:
+            return False
+        for k in range(n):
+            data = b"" if slab is None else self.sim.payload(slab, self.g, k)
+            self.log.append(Entry(self.term, 0, data))
+        self.remotes[self.s].try_update(self.last)
+        if self.sim.R == 1:
+            self.try_commit()
+        return True
+
+    # -- leader --
+    def try_commit(self):
+        vals = sorted(r.match for r in self.remotes)
+        q = vals[self.sim.R - self.sim.quorum]
+        if q > self.committed and self.term_at(q) == self.term:
+            self.committed = q
+            return True
+        return False
+
+    def send_replicate(self, to):
+        rp = self.remotes[to]
+        if rp.paused():
+            return
+        if rp.next <= self.marker:
+            if to not in self.active:
+                return
+            if self.snap_index == 0:
+                self.err |= ERR_EMPTY_SNAP
+                return
+            rp.snap, rp.state = self.snap_index, SNAP
+            self.send(msg(INSTALL_SNAPSHOT, to + 1, log_index=self.snap_index, log_term=self.snap_term))
+            return
+        nxt = rp.next
+        ents = self.log[nxt - self.marker - 1: nxt - self.marker - 1 + self.sim.cfg["max_entries_per_msg"]] \
+            if nxt <= self.last else []
+        if ents:
+            rp.progress(nxt + len(ents) - 1)
+        self.send(msg(REPLICATE, to + 1, log_index=nxt - 1, log_term=self.term_at(nxt - 1),
+                      commit=self.committed, nent=len(ents), ents=tuple(ents)))
+
+    def broadcast_replicate(self):
+        for i in range(self.sim.R):
+            if i != self.s:
+                self.send_replicate(i)
+
+    def on_replicate_resp(self, m):
+        f = m["frm"] - 1
+        rp = self.remotes[f]
+        self.active.add(f)
+        if not m["reject"]:
+            was_paused = rp.paused()
+            if rp.try_update(m["log_index"]):
+                rp.responded_to()
+                if self.try_commit():
+                    self.broadcast_replicate()
+                elif was_paused:
+                    self.send_replicate(f)
+        elif rp.decrease_to(m["log_index"], m["hint"]):
+            if rp.state == REPL:
+                rp.become_retry()
+            self.send_replicate(f)
+
+    def on_heartbeat_resp(self, m):
+        f = m["frm"] - 1
+        self.active.add(f)
+        rp = self.remotes[f]
+        if rp.state == WAIT:
+            rp.state = RETRY
+        if rp.match < self.last:
+            self.send_replicate(f)
+
+    # -- follower --
+    def on_replicate(self, m):
+        resp = msg(REPLICATE_RESP, m["frm"])
+        if m["log_index"] < self.committed:
+            resp["log_index"] = self.committed
+            self.send(resp)
+            return
+        n = m["nent"]
+        if self.term_at(m["log_index"]) == m["log_term"]:
+            conflict = None
+            for k, e in enumerate(m["ents"]):
+                if self.term_at(m["log_index"] + 1 + k) != e.term:
+                    conflict = k
+                    break
+            last_new = m["log_index"] + n
+            if conflict is not None:
+                ci = m["log_index"] + 1 + conflict
+                if ci > self.committed and last_new > self.cap_base + self.sim.cfg["log_capacity"]:
+                    self.drops += 1
+                    return
+                if ci <= self.committed:
+                    self.err |= ERR_CONFLICT
+                else:
+                    del self.log[ci - self.marker - 1:]
+                    for e in m["ents"][conflict:]:
+                        ne = Entry(e.term, e.type, e.data)
+                        if ne.crc != e.crc:
+                            self.err |= ERR_CRC
+                        self.log.append(ne)
+            self.commit_to(min(last_new, m["commit"]))
+            resp["log_index"] = last_new
+        else:
+            resp.update(reject=1, log_index=m["log_index"], hint=self.last)
+        self.send(resp)
+
+    def on_install_snapshot(self, m):
+        resp = msg(REPLICATE_RESP, m["frm"])
+        si, st = m["log_index"], m["log_term"]
+        if si <= self.committed:
+            resp["log_index"] = self.committed
+        elif self.term_at(si) == st:
+            self.commit_to(si)
+            resp["log_index"] = self.committed
+        else:
+            self.log = []
+            self.marker = self.committed = self.snap_index = si
+            self.marker_term = self.snap_term = st
+            resp["log_index"] = self.last
+        self.send(resp)
+
+    # -- elections --
+    def campaign(self):
+        self.become_candidate()
+        self.votes[self.s] = True
+        if self.sim.R == 1:
+            self.become_leader()
+            return
+        for i in range(self.sim.R):
+            if i != self.s:
+                self.send(msg(REQUEST_VOTE, i + 1, term=self.term, log_index=self.last,
+                              log_term=self.term_at(self.last)))
+
+    def on_request_vote(self, m):
+        grant = self.vote in (0, m["frm"]) and self.up_to_date(m["log_index"], m["log_term"])
+        if grant:
+            self.etick = 0
+            self.vote = m["frm"]
+        self.send(msg(REQUEST_VOTE_RESP, m["frm"], reject=0 if grant else 1))
+
+    def on_vote_resp(self, m):
+        f = m["frm"] - 1
+        if f not in self.votes:
+            self.votes[f] = not m["reject"]
+        yes = sum(1 for v in self.votes.values() if v)
+        if yes == self.sim.quorum:
+            self.become_leader()
+            self.broadcast_replicate()
+        elif len(self.votes) - yes == self.sim.quorum:
+            self.become_follower(self.term, 0)
+
+    # -- Handle --
+    def local(self, t):
+        self.handle(msg(t, self.id, frm=self.id))
+
+    def tick(self):
+        c = self.sim.cfg
+        if self.role == LEADER:
+            self.etick += 1
+            if self.etick >= c["election_rtt"]:
+                self.etick = 0
+                if c["check_quorum"]:
+                    self.local(CHECK_QUORUM)
+            self.htick += 1
+            if self.htick >= c["heartbeat_rtt"]:
+                self.htick = 0
+                self.local(LEADER_HEARTBEAT)
+        else:
+            self.etick += 1
+            if self.etick >= self.rand_to:
+                self.etick = 0
+                self.local(ELECTION)
+
+    def handle(self, m):
+        c = self.sim.cfg
+        t, mt = m["type"], m["term"]
+        if mt != 0 and mt != self.term:
+            if (t == REQUEST_VOTE and c["check_quorum"] and mt > self.term and m["hint"] != m["frm"]
+                    and self.leader != 0 and self.etick < c["election_rtt"]):
+                return
+            if mt > self.term:
+                self.become_follower(mt, m["frm"] if t in LEADER_MSGS else 0)
+            else:
+                if c["check_quorum"] and t in LEADER_MSGS:
+                    self.send(msg(NOOP, m["frm"]))
+                return
+        role = self.role
+        if t == LOCAL_TICK:
+            self.tick()
+        elif t == ELECTION:
+            if role != LEADER and not self.committed > self.applied:
+                self.campaign()
+        elif t == LEADER_HEARTBEAT:
+            if role == LEADER:
+                for i in range(self.sim.R):
+                    if i != self.s:
+                        self.send(msg(HEARTBEAT, i + 1, commit=min(self.remotes[i].match, self.committed)))
+        elif t == CHECK_QUORUM:
+            if role == LEADER:
+                c_act = 1 + len(self.active - {self.s})
+                self.active = set()
+                if c_act < self.sim.quorum:
+                    self.become_follower(self.term, 0)
+        elif t == PROPOSE:
+            if role == LEADER:
+                if not self.append(m["nent"], m["src_a"]):
+                    self.drops += 1
+                    return
+                self.broadcast_replicate()
+            elif role == FOLLOWER and self.leader != 0 and m["src_b"] == 0:
+                f = dict(m)
+                f.update(to=self.leader, term=0, src_b=m["src_b"] + 1)
+                self.send(f)
+            else:
+                self.drops += 1
+        elif t in (REPLICATE, HEARTBEAT, INSTALL_SNAPSHOT):
+            if role == LEADER:
+                return
+            if role == CANDIDATE:
+                self.become_follower(self.term, m["frm"])
+            else:
+                self.etick = 0
+                self.leader = m["frm"]
+            if t == REPLICATE:
+                self.on_replicate(m)
+            elif t == HEARTBEAT:
+                self.commit_to(m["commit"])
+                self.send(msg(HEARTBEAT_RESP, m["frm"], hint=m["hint"], hint_high=m["hint_high"]))
+            else:
+                self.on_install_snapshot(m)
+        elif t == REPLICATE_RESP:
+            if role == LEADER:
+                self.on_replicate_resp(m)
+        elif t == HEARTBEAT_RESP:
+            if role == LEADER:
+                self.on_heartbeat_resp(m)
+        elif t == REQUEST_VOTE:
+            self.on_request_vote(m)
+        elif t == REQUEST_VOTE_RESP:
+            if role == CANDIDATE:
+                self.on_vote_resp(m)
+
+    # -- views (same field names as the C views) --
+    def view(self):
+        R = self.sim.R
+        return dict(
+            term=self.term, vote=self.vote, leader=self.leader, committed=self.committed,
+            applied=self.applied, last=self.last, marker=self.marker, marker_term=self.marker_term,
+            snap_index=self.snap_index, snap_term=self.snap_term, cap_base=self.cap_base,
+            role=self.role, election_tick=self.etick, heartbeat_tick=self.htick,
+            rand_timeout=self.rand_to, rng_ctr=self.rng,
+            granted=sum(1 << k for k, v in self.votes.items() if v),
+            responded=sum(1 << k for k in self.votes),
+            active=sum(1 << k for k in self.active), err=self.err, drops=self.drops & 0xFFFFFFFF,
+            match=[r.match for r in self.remotes][:R], next=[r.next for r in self.remotes][:R],
+            rsnap=[r.snap for r in self.remotes][:R], rstate=[r.state for r in self.remotes][:R],
+        )
+
+
+class Sim:
+    """All replicas of all groups, one process, in-memory router."""
+
+    def __init__(self, **cfg):
+        from .pyoracle import default_config  # same defaults; no code shared with oracle.c
+        self.cfg = default_config(**cfg)
+        self.G, self.R = self.cfg["groups"], self.cfg["replicas"]
+        self.quorum = self.R // 2 + 1
+        self.t = 0
+        self.isolate = None
+        self.reps = [Replica(self, g, s) for g in range(self.G) for s in range(self.R)]
+        self._pay = {}
+
+    def payload(self, slab, g, k):
+        key = (slab, g, k)
+        if key not in self._pay:
+            self._pay[key] = payload(self.cfg["seed"], slab, g, k, self.cfg["payload_bytes"])
+        return self._pay[key]
+
+    def lost(self, rep, dst, n):
+        rid = rep.g * self.R + rep.s
+        if self.isolate is not None and (self.isolate[rid] or self.isolate[rep.g * self.R + dst]):
+            return True
+        ppm = self.cfg["drop_ppm"]
+        if ppm:
+            h = mix64(self.cfg["seed"] ^ mix64((self.t << 40) ^ (rid << 8) ^ dst) ^ (n + 1))
+            return h % 1000000 < ppm
+        return False
+
+    def bootstrap(self):
+        R = self.R
+        for r in self.reps:
+            r.rng = 0
+            r.become_follower(1, 0)
+            r.log = [Entry(1, 1) for _ in range(R)]
+            r.committed = R
+            r.remotes = [Remote(0, R + 1) for _ in range(R)]
+            r.out, r.emitted = {}, {}
+        self.t = 0
+
+    def tick(self, prop_target=None, prop_count=None, campaign=None, isolate=None, flags=0):
+        self.isolate = isolate
+        inbox = {id(r): [] for r in self.reps}
+        for r in self.reps:  # deliver last tick's outboxes
+            for d, lst in r.out.items():
+                dst = self.reps[r.g * self.R + d]
+                inbox[id(dst)].append((r.s, lst))
+        for r in self.reps:
+            r._inbox = sorted(inbox[id(r)], key=lambda x: x[0])
+        for r in self.reps:
+            r.out, r.emitted = {}, {}
+        for g in range(self.G):
+            for s in range(self.R):
+                r = self.reps[g * self.R + s]
+                marker_start = r.marker
+                for _, lst in r._inbox:
+                    for m in lst:
+                        r.handle(m)
+                rid = g * self.R + s
+                if campaign is not None and campaign[rid]:
+                    r.local(ELECTION)
+                if not flags & 1:
+                    r.local(LOCAL_TICK)
+                if prop_target is not None and prop_target[g] == s and prop_count[g] > 0:
+                    r.handle(msg(PROPOSE, r.id, frm=r.id, nent=int(prop_count[g]),
+                                 src_a=self.t % self.cfg["num_slabs"], src_b=0))
+                r.applied = r.committed
+                se, co = self.cfg["snapshot_entries"], self.cfg["compaction_overhead"]
+                if se and r.applied - r.snap_index >= se:
+                    r.snap_index, r.snap_term = r.applied, r.term_at(r.applied)
+                    cpt = r.snap_index - co if r.snap_index > co else 0
+                    if cpt > r.marker:
+                        mt = r.term_at(cpt)
+                        del r.log[:cpt - r.marker]
+                        r.marker, r.marker_term = cpt, mt
+                r.cap_base = marker_start
+        self.t += 1
+
+    # views
+    def replica(self, rid):
+        return self.reps[rid].view()
+
+    def msgs(self, rid, dst):
+        out = []
+        for m in self.reps[rid].out.get(dst, []):
+            d = {k: m[k] for k in ("type", "to", "reject", "nent", "term", "log_term", "log_index",
+                                   "commit", "hint", "hint_high", "src_a", "src_b")}
+            d["from"] = m["frm"]
+            d["terms"] = [e.term for e in m["ents"]] if m["type"] == REPLICATE else []
+            out.append(d)
+        return out
+
+    def entry(self, rid, index):
+        r = self.reps[rid]
+        if not (r.marker < index <= r.last):
+            return None
+        e = r.log[index - r.marker - 1]
+        return dict(term=e.term, type=e.type, len=len(e.data), crc=e.crc)
+
+    # -- scenario helpers (KATs): same contract as or_import_replica / or_deliver --
+    def import_replica(self, rid, view: dict, terms, types=None, payloads=None):
+        r = self.reps[rid]
+        P = self.cfg["payload_bytes"]
+        for k in ("term", "vote", "leader", "committed", "applied", "marker", "marker_term",
+                  "snap_index", "snap_term", "cap_base", "role", "err", "drops"):
+            setattr(r, k, view.get(k, 0))
+        r.etick = view.get("election_tick", 0)
+        r.htick = view.get("heartbeat_tick", 0)
+        r.rand_to = view.get("rand_timeout", 0)
+        r.rng = view.get("rng_ctr", 0)
+        g = view.get("granted", 0)
+        resp = view.get("responded", 0)
+        r.votes = {k: bool(g >> k & 1) for k in range(8) if resp >> k & 1}
+        r.active = {k for k in range(8) if view.get("active", 0) >> k & 1}
+        r.log = []
+        for k, t in enumerate(terms):
+            ty = 0 if types is None else types[k]
+            data = payloads[k * P:(k + 1) * P] if (payloads is not None and P and ty == 0) else b""
+            r.log.append(Entry(t, ty, bytes(data)))
+        assert r.last == view.get("last", r.last)
+        r.remotes = []
+        for k in range(self.R):
+            rp = Remote(view.get("match", [0] * 8)[k], view.get("next", [0] * 8)[k])
+            rp.snap = view.get("rsnap", [0] * 8)[k]
+            rp.state = view.get("rstate", [0] * 8)[k]
+            r.remotes.append(rp)
+
+    def deliver(self, rid_src, **f):
+        r = self.reps[rid_src]
+        m = msg(f.get("type"), f.get("to"))
+        for k, v in f.items():
+            m["frm" if k == "from" else k] = v
+        if "from" not in f:
+            m["frm"] = r.id
+        if m["type"] == REPLICATE and m["nent"]:
+            lo = m["log_index"] + 1
+            m["ents"] = tuple(r.log[lo - r.marker - 1: lo - r.marker - 1 + m["nent"]])
+        r.out.setdefault(m["to"] - 1, []).append(m)
