@@ -1,0 +1,104 @@
+"""The C oracle against its pins: CRC check values, the independent Python restatement
+(tick-by-tick on random chaotic traces), and the committed regression traces."""
+import hashlib
+import json
+
+import numpy as np
+import pytest
+
+import kat_scenarios as K
+from engines import make
+from oracle import pyoracle, pyraft
+
+
+def test_crc_kats():
+    d = K.load("crc_kat.json")
+    for v in d["ieee"]:
+        assert pyoracle.crc32(bytes.fromhex(v["hex"])) == v["crc"]
+    assert pyoracle.crc32(b"123456789") == 0xCBF43926
+
+
+def test_mix64_and_payload_agree():
+    o = pyoracle.Oracle(groups=2, replicas=3, payload_bytes=64)
+    for z in (0, 1, 0x5EED, 2**63 + 12345):
+        assert pyoracle.mix64(z) == pyraft.mix64(z)
+    for sl, g, i in ((0, 0, 0), (1, 1, 63), (1, 0, 5)):
+        assert o.payload(sl, g, i) == pyraft.payload(0x5EED, sl, g, i, 64)
+
+
+def random_inputs(rng, G, R, emax):
+    pt = rng.integers(0, R, G).astype(np.uint8)
+    pt[rng.random(G) < 0.3] = 0xFF
+    pc = rng.integers(1, emax + 1, G).astype(np.uint32)
+    camp = (rng.random(G * R) < 0.02).astype(np.uint8)
+    iso = (rng.random(G * R) < 0.05).astype(np.uint8)
+    return pt, pc, camp, iso
+
+
+def cross_check(seed, G, R, T, **cfg):
+    kw = dict(groups=G, replicas=R, payload_bytes=16, max_entries_per_msg=8, log_capacity=64,
+              snapshot_entries=20, compaction_overhead=5, drop_ppm=150000, seed=seed)
+    kw.update(cfg)
+    a, b = make("c", **kw), make("py", **kw)
+    a.bootstrap()
+    b.bootstrap()
+    rng = np.random.default_rng(seed)
+    for t in range(T):
+        ins = random_inputs(rng, G, R, kw["max_entries_per_msg"])
+        a.tick(*ins)
+        b.tick(*ins)
+        for rid in range(G * R):
+            va = a.replica(rid)
+            assert va == b.replica(rid), (seed, t, rid)
+            for d in range(R):
+                assert a.msgs(rid, d) == b.msgs(rid, d), (seed, t, rid, d)
+            for i in range(va["marker"] + 1, va["last"] + 1):
+                assert a.entry(rid, i) == b.entry(rid, i), (seed, t, rid, i)
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_c_oracle_matches_python_restatement(seed):
+    cross_check(seed, G=3, R=[1, 2, 3, 4, 5][seed % 5], T=100)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_c_oracle_matches_python_no_loss_r7(seed):
+    cross_check(100 + seed, G=2, R=7, T=60, drop_ppm=0, max_msgs_per_pair=4)
+
+
+@pytest.mark.parametrize("name", ["trace_r3_chaos.json", "trace_r5_chaos.json"])
+def test_regression_traces(name):
+    fx = K.load(name)
+    o = pyoracle.Oracle(**fx["config"])
+    o.bootstrap()
+    rng = np.random.default_rng(fx["input_seed"])
+    G, R = o.G, o.R
+    for t in range(fx["ticks"]):
+        o.tick(*random_inputs(rng, G, R, fx["config"]["max_entries_per_msg"]))
+        h = hashlib.sha256()
+        for rid in range(G * R):
+            h.update(json.dumps(o.replica(rid), sort_keys=True).encode())
+            for d in range(R):
+                h.update(json.dumps(o.msgs(rid, d), sort_keys=True).encode())
+        assert h.hexdigest()[:16] == fx["digests"][t], t
+    assert [o.replica(r) for r in range(G * R)] == fx["final"]
+
+
+def test_steady_state_throughput_shape():
+    """C2-shaped steady state: every group elects slot 0 and commits every proposal batch."""
+    G, R, E = 8, 3, 16
+    o = pyoracle.Oracle(groups=G, replicas=R, payload_bytes=64, max_entries_per_msg=E)
+    o.bootstrap()
+    o.tick()
+    camp = np.zeros(G * R, np.uint8)
+    camp[0::R] = 1
+    o.tick(campaign=camp)
+    for _ in range(40):
+        o.tick(np.zeros(G, np.uint8), np.full(G, E, np.uint32), threads=4)
+    for g in range(G):
+        v = o.replica(g * R)
+        assert v["role"] == 2 and v["term"] == 2
+        assert v["committed"] >= v["last"] - 2 * E
+        for s in range(1, R):
+            f = o.replica(g * R + s)
+            assert f["role"] == 0 and f["leader"] == 1 and f["err"] == 0
