@@ -1,0 +1,153 @@
+/*
+ * raftgpu.h — C-ABI of the MI355X batched Raft step engine (raftd-amd).
+ *
+ * The engine is the batched analogue of dragonboat v4's internal/raft `Peer`
+ * (Launch/Handle/Tick/GetUpdate/Commit), for every replica of every group that one process
+ * hosts, resident in MI355X HBM. raftd reaches that code only through dragonboat's NodeHost,
+ * which offers no plugin point for the raft step, so these entry points are what
+ * a raftd-side cgo shim re-implementing the NodeHost subset binds:
+ *
+ *   rg_create / rg_destroy        ← dragonboat.NewNodeHost / NodeHost.Close
+ *                                    (/root/reference/raft/raft_manager.go:102-109, :159)
+ *   rg_bootstrap                  ← NodeHost.StartOnDiskReplica(initialMembers, join=false, …, rc)
+ *                                    (raft_manager.go:142-144; rc = ElectionRTT 10, HeartbeatRTT 1,
+ *                                    CheckQuorum, SnapshotEntries 1000, CompactionOverhead 5 at :92-100)
+ *   rg_tick / rg_tick_device      ← the NodeHost tick goroutine (RTTMillisecond 3, raft_manager.go:105)
+ *                                    driving Peer.Tick + Peer.Handle for all shards; proposals ≈
+ *                                    NodeHost.Propose → Peer.ProposeEntries
+ *   rg_leader                     ← NodeHost.GetLeaderID (raft/members.go:21)
+ *   rg_read_replicas              ← NodeHost.SyncGetShardMembership / raftState (raft/members.go:30)
+ *   rg_read_entries               ← committed-range copy-back feeding IOnDiskStateMachine.Update
+ *                                    (raft/state_machine.go:136-166)
+ *   rg_deliver                    ← transport delivery of a pb.Message from another host
+ *
+ * Conventions: plain pointers and sizes; every call returns RG_OK (0) or a negative RG_E*
+ * code, with rg_last_error() (thread-local) describing the failure. An engine handle is not
+ * thread-safe: one host thread drives it, as one dragonboat step worker owns a shard.
+ * The engine owns all device memory. Step semantics: DESIGN.md §1.
+ */
+#ifndef RAFTGPU_H
+#define RAFTGPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RG_MAX_REPLICAS 8
+
+enum {
+  RG_OK = 0,
+  RG_EINVAL = -1,      /* bad argument or configuration */
+  RG_ENOMEM = -2,      /* device allocation failed */
+  RG_EFULL = -3,       /* a bounded buffer is full (e.g. rg_deliver into a full slot) */
+  RG_EHIP = -4,        /* HIP runtime error */
+  RG_EINVARIANT = -5   /* a dragonboat plog.Panicf invariant fired (see rg_replica_view.err) */
+};
+
+/* message types (raftpb.MessageType numbering as recalled) */
+enum {
+  RG_MSG_NOOP = 4, RG_MSG_PROPOSE = 7, RG_MSG_REPLICATE = 12, RG_MSG_REPLICATE_RESP = 13,
+  RG_MSG_REQUEST_VOTE = 14, RG_MSG_REQUEST_VOTE_RESP = 15, RG_MSG_INSTALL_SNAPSHOT = 16,
+  RG_MSG_HEARTBEAT = 17, RG_MSG_HEARTBEAT_RESP = 18
+};
+enum { RG_FOLLOWER = 0, RG_CANDIDATE = 1, RG_LEADER = 2 };
+enum { RG_REMOTE_RETRY = 0, RG_REMOTE_WAIT = 1, RG_REMOTE_REPLICATE = 2, RG_REMOTE_SNAPSHOT = 3 };
+enum { RG_ENTRY_APPLICATION = 0, RG_ENTRY_CONFIG_CHANGE = 1 };
+enum {
+  RG_ERR_CONFLICT_COMMITTED = 1, RG_ERR_COMMIT_BEYOND_LAST = 2, RG_ERR_RING_FULL = 4,
+  RG_ERR_CRC = 8, RG_ERR_EMPTY_SNAPSHOT = 16
+};
+#define RG_TICK_NO_LOCALTICK 1u
+
+typedef struct rg_config {
+  uint32_t groups;              /* shards hosted by this engine */
+  uint32_t replicas;            /* replicas per shard, IDs 1..replicas (1..8) */
+  uint32_t log_capacity;        /* log ring entries per replica (power of two) */
+  uint32_t payload_bytes;       /* bytes per entry: 0 or a power of two in [16, 1024] */
+  uint32_t max_entries_per_msg; /* entries per Replicate / proposal batch (1..64) */
+  uint32_t max_msgs_per_pair;   /* messages per (replica, destination) per tick (1..16) */
+  uint32_t num_slabs;           /* proposal payload slabs, tick t uses slab t % num_slabs (>= 2) */
+  uint32_t election_rtt;        /* config.Config.ElectionRTT (raftd: 10) */
+  uint32_t heartbeat_rtt;       /* config.Config.HeartbeatRTT (raftd: 1) */
+  uint32_t check_quorum;        /* config.Config.CheckQuorum (raftd: true) */
+  uint32_t snapshot_entries;    /* config.Config.SnapshotEntries (raftd: 1000; 0 = off) */
+  uint32_t compaction_overhead; /* config.Config.CompactionOverhead (raftd: 5) */
+  uint32_t drop_ppm;            /* deterministic message loss, parts per million (tests) */
+  int32_t device;               /* HIP device ordinal */
+  uint64_t seed;
+} rg_config;
+
+typedef struct rg_replica_view {
+  uint64_t term, vote, leader, committed, applied, last, marker, marker_term;
+  uint64_t snap_index, snap_term, cap_base;
+  uint32_t role, election_tick, heartbeat_tick, rand_timeout, rng_ctr;
+  uint32_t granted, responded, active, err, drops;
+  uint64_t match[RG_MAX_REPLICAS], next[RG_MAX_REPLICAS], rsnap[RG_MAX_REPLICAS];
+  uint8_t rstate[RG_MAX_REPLICAS];
+} rg_replica_view;
+
+/* 64-byte message header, identical to the in-HBM slot layout. */
+typedef struct rg_msg_view {
+  uint8_t type, from, to, reject;
+  uint32_t nent;
+  uint64_t term, log_term, log_index, commit, hint, hint_high;
+  uint32_t src_a, src_b; /* Propose: slab id, forward hop count */
+} rg_msg_view;
+
+typedef struct rg_entry_view {
+  uint64_t term;
+  uint32_t type, len, crc, bank;
+} rg_entry_view;
+
+typedef struct rg_tick_input {
+  const uint8_t* prop_target; /* [groups] slot receiving this tick's proposal batch, 0xFF none */
+  const uint32_t* prop_count; /* [groups] entries in the batch (<= max_entries_per_msg) */
+  const uint8_t* campaign;    /* [groups*replicas] nonzero: Peer.Campaign before the tick */
+  const uint8_t* isolate;     /* [groups*replicas] nonzero: replica partitioned this tick */
+  uint32_t flags;             /* RG_TICK_* */
+  uint32_t _pad;
+} rg_tick_input;
+
+typedef struct rg_engine rg_engine;
+
+int rg_create(const rg_config* cfg, rg_engine** out);
+void rg_destroy(rg_engine* e);
+/* Every replica: becomeFollower(1) + bootstrap ConfigChange entries 1..R, committed R. */
+int rg_bootstrap(rg_engine* e);
+/* Fill every proposal slab with the deterministic payload generator. */
+int rg_fill_slabs(rg_engine* e);
+/* One tick for every replica. Input arrays are host pointers (copied before launch; NULL =
+ * none). Synchronous with respect to the host buffers, asynchronous on the device. */
+int rg_tick(rg_engine* e, const rg_tick_input* in);
+/* Same, with the input arrays already resident in device memory (no copies). */
+int rg_tick_device(rg_engine* e, const rg_tick_input* in);
+/* Launch work on this HIP stream (hipStream_t) instead of the engine's own. */
+int rg_set_stream(rg_engine* e, void* stream);
+int rg_sync(rg_engine* e);
+uint64_t rg_tick_count(const rg_engine* e);
+
+int rg_read_replicas(rg_engine* e, uint32_t first_rid, uint32_t n, rg_replica_view* out);
+/* Messages `rid` emitted to slot `dst` in the last tick; returns the count, fills up to cap
+ * headers and, if terms != NULL, cap * max_entries_per_msg inline entry terms (bank bit
+ * cleared). */
+int rg_read_msgs(rg_engine* e, uint32_t rid, uint32_t dst, rg_msg_view* out, uint32_t cap, uint64_t* terms);
+/* Log entries first_index .. first_index+n-1 of replica rid (must lie in (marker, last]). */
+int rg_read_entries(rg_engine* e, uint32_t rid, uint64_t first_index, uint32_t n, rg_entry_view* out,
+                    uint8_t* payload);
+int rg_import_replica(rg_engine* e, uint32_t rid, const rg_replica_view* v, const uint64_t* terms,
+                      const uint32_t* types, const uint8_t* payloads);
+/* Enqueue a message as if `rid_src` had emitted it in the last tick (delivered next tick). */
+int rg_deliver(rg_engine* e, uint32_t rid_src, const rg_msg_view* m);
+int rg_leader(rg_engine* e, uint32_t group, uint64_t* leader_id, uint64_t* term, int* valid);
+/* Sum over groups of the highest committed index among the group's replicas. */
+int rg_sum_committed(rg_engine* e, uint64_t* out);
+/* Device bytes held by the engine. */
+uint64_t rg_device_bytes(const rg_engine* e);
+const char* rg_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

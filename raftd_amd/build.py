@@ -1,0 +1,58 @@
+"""Builds the in-tree HIP engine library raftd_amd/libraftgpu.so for gfx950 (hipcc), and the
+test oracle oracle/build/liboracle.so (gcc). Run: python -m raftd_amd.build"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "libraftgpu.so")
+SOURCES = ["raftgpu_kernels.hip", "raftgpu_engine.cpp"]
+HEADERS = ["raftgpu_internal.h", os.path.join("..", "..", "include", "raftgpu.h")]
+ARCH = os.environ.get("RAFTGPU_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def _stale(out: str, deps: list[str]) -> bool:
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_engine(force: bool = False, verbose: bool = False) -> str:
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
+    if not force and not _stale(LIB, deps):
+        return LIB
+    objs = []
+    for src in SOURCES:
+        obj = os.path.join(CSRC, src.rsplit(".", 1)[0] + ".o")
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function",
+               "-c", "-x", "hip", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+        objs.append(obj)
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+    subprocess.run(cmd, check=True)
+    for o in objs:
+        os.remove(o)
+    return LIB
+
+
+def build_oracle() -> str:
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    return os.path.join(ROOT, "oracle", "build", "liboracle.so")
+
+
+def main():
+    force = "--force" in sys.argv
+    print(build_engine(force=force, verbose=True))
+    print(build_oracle())
+
+
+if __name__ == "__main__":
+    main()

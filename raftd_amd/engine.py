@@ -1,0 +1,290 @@
+"""Python host binding of the HIP step engine (include/raftgpu.h) via ctypes.
+
+This is the product path: it loads raftd_amd/libraftgpu.so and fails loudly if the library
+is missing or no GPU is present. There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "libraftgpu.so")
+MAX_R = 8
+
+RG_OK, RG_EINVAL, RG_ENOMEM, RG_EFULL, RG_EHIP, RG_EINVARIANT = 0, -1, -2, -3, -4, -5
+TICK_NO_LOCALTICK = 1
+
+
+class RgError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"raftgpu error {code}: {msg}")
+        self.code = code
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("groups", C.c_uint32), ("replicas", C.c_uint32), ("log_capacity", C.c_uint32),
+        ("payload_bytes", C.c_uint32), ("max_entries_per_msg", C.c_uint32),
+        ("max_msgs_per_pair", C.c_uint32), ("num_slabs", C.c_uint32),
+        ("election_rtt", C.c_uint32), ("heartbeat_rtt", C.c_uint32), ("check_quorum", C.c_uint32),
+        ("snapshot_entries", C.c_uint32), ("compaction_overhead", C.c_uint32),
+        ("drop_ppm", C.c_uint32), ("device", C.c_int32), ("seed", C.c_uint64),
+    ]
+
+
+class ReplicaView(C.Structure):
+    _fields_ = [
+        ("term", C.c_uint64), ("vote", C.c_uint64), ("leader", C.c_uint64),
+        ("committed", C.c_uint64), ("applied", C.c_uint64), ("last", C.c_uint64),
+        ("marker", C.c_uint64), ("marker_term", C.c_uint64), ("snap_index", C.c_uint64),
+        ("snap_term", C.c_uint64), ("cap_base", C.c_uint64),
+        ("role", C.c_uint32), ("election_tick", C.c_uint32), ("heartbeat_tick", C.c_uint32),
+        ("rand_timeout", C.c_uint32), ("rng_ctr", C.c_uint32), ("granted", C.c_uint32),
+        ("responded", C.c_uint32), ("active", C.c_uint32), ("err", C.c_uint32), ("drops", C.c_uint32),
+        ("match", C.c_uint64 * MAX_R), ("next", C.c_uint64 * MAX_R), ("rsnap", C.c_uint64 * MAX_R),
+        ("rstate", C.c_uint8 * MAX_R),
+    ]
+
+
+class MsgView(C.Structure):
+    _fields_ = [
+        ("type", C.c_uint8), ("from_", C.c_uint8), ("to", C.c_uint8), ("reject", C.c_uint8),
+        ("nent", C.c_uint32), ("term", C.c_uint64), ("log_term", C.c_uint64),
+        ("log_index", C.c_uint64), ("commit", C.c_uint64), ("hint", C.c_uint64),
+        ("hint_high", C.c_uint64), ("src_a", C.c_uint32), ("src_b", C.c_uint32),
+    ]
+
+
+class EntryView(C.Structure):
+    _fields_ = [("term", C.c_uint64), ("type", C.c_uint32), ("len", C.c_uint32),
+                ("crc", C.c_uint32), ("bank", C.c_uint32)]
+
+
+class TickInput(C.Structure):
+    _fields_ = [("prop_target", C.c_void_p), ("prop_count", C.c_void_p), ("campaign", C.c_void_p),
+                ("isolate", C.c_void_p), ("flags", C.c_uint32), ("_pad", C.c_uint32)]
+
+
+REPLICA_FIELDS = [f for f, _ in ReplicaView._fields_]
+MSG_FIELDS = [f for f, _ in MsgView._fields_]
+
+# every symbol include/raftgpu.h declares
+EXPORTS = ["rg_create", "rg_destroy", "rg_bootstrap", "rg_fill_slabs", "rg_tick", "rg_tick_device",
+           "rg_set_stream", "rg_sync", "rg_tick_count", "rg_read_replicas", "rg_read_msgs",
+           "rg_read_entries", "rg_import_replica", "rg_deliver", "rg_leader", "rg_sum_committed",
+           "rg_device_bytes", "rg_last_error"]
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libraftgpu.so and declare signatures. Raises if it is missing (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"HIP engine library not built: {path} (run `python -m raftd_amd.build`)")
+    L = C.CDLL(path)
+    vp, u32, u64, i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int
+    sig = {
+        "rg_create": ([C.POINTER(Config), C.POINTER(vp)], i32),
+        "rg_destroy": ([vp], None),
+        "rg_bootstrap": ([vp], i32),
+        "rg_fill_slabs": ([vp], i32),
+        "rg_tick": ([vp, C.POINTER(TickInput)], i32),
+        "rg_tick_device": ([vp, C.POINTER(TickInput)], i32),
+        "rg_set_stream": ([vp, vp], i32),
+        "rg_sync": ([vp], i32),
+        "rg_tick_count": ([vp], u64),
+        "rg_read_replicas": ([vp, u32, u32, C.POINTER(ReplicaView)], i32),
+        "rg_read_msgs": ([vp, u32, u32, C.POINTER(MsgView), u32, C.POINTER(C.c_uint64)], i32),
+        "rg_read_entries": ([vp, u32, u64, u32, C.POINTER(EntryView), vp], i32),
+        "rg_import_replica": ([vp, u32, C.POINTER(ReplicaView), vp, vp, vp], i32),
+        "rg_deliver": ([vp, u32, C.POINTER(MsgView)], i32),
+        "rg_leader": ([vp, u32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_int)], i32),
+        "rg_sum_committed": ([vp, C.POINTER(C.c_uint64)], i32),
+        "rg_device_bytes": ([vp], u64),
+        "rg_last_error": ([], C.c_char_p),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = L
+    return L
+
+
+def default_config(**kw) -> dict:
+    """raftd's Raft parameters (raft/raft_manager.go:92-100) plus the engine's sizing."""
+    c = dict(groups=4, replicas=3, log_capacity=2048, payload_bytes=256, max_entries_per_msg=64,
+             max_msgs_per_pair=8, num_slabs=2, election_rtt=10, heartbeat_rtt=1, check_quorum=1,
+             snapshot_entries=1000, compaction_overhead=5, drop_ppm=0, device=0, seed=0x5EED)
+    c.update(kw)
+    return c
+
+
+class Engine:
+    """One engine = every replica of `groups` Raft shards on one GPU."""
+
+    def __init__(self, **cfg):
+        self.cfg = default_config(**cfg)
+        self.L = load_library()
+        c = Config()
+        for k, v in self.cfg.items():
+            setattr(c, k, v)
+        self.h = C.c_void_p()
+        self._check(self.L.rg_create(C.byref(c), C.byref(self.h)))
+        self.G, self.R = self.cfg["groups"], self.cfg["replicas"]
+        self.nrep = self.G * self.R
+        self._slabs_filled = False
+
+    def _check(self, rc):
+        if rc < 0:
+            raise RgError(rc, self.L.rg_last_error().decode())
+        return rc
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.rg_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # lifecycle
+    def bootstrap(self):
+        self._check(self.L.rg_bootstrap(self.h))
+        if not self._slabs_filled:
+            self.fill_slabs()
+
+    def fill_slabs(self):
+        self._check(self.L.rg_fill_slabs(self.h))
+        self._slabs_filled = True
+
+    def tick(self, prop_target=None, prop_count=None, campaign=None, isolate=None, flags=0, threads=None):
+        ti = TickInput()
+        ti.flags = flags
+        keep = []
+        for name, arr, dt in (("prop_target", prop_target, np.uint8), ("prop_count", prop_count, np.uint32),
+                              ("campaign", campaign, np.uint8), ("isolate", isolate, np.uint8)):
+            if arr is None:
+                setattr(ti, name, None)
+            else:
+                a = np.ascontiguousarray(arr, dtype=dt)
+                keep.append(a)
+                setattr(ti, name, a.ctypes.data)
+        self._check(self.L.rg_tick(self.h, C.byref(ti)))
+
+    def tick_device(self, prop_target_ptr=0, prop_count_ptr=0, campaign_ptr=0, isolate_ptr=0, flags=0):
+        ti = TickInput(prop_target_ptr or None, prop_count_ptr or None, campaign_ptr or None,
+                       isolate_ptr or None, flags, 0)
+        self._check(self.L.rg_tick_device(self.h, C.byref(ti)))
+
+    def set_stream(self, stream_handle: int):
+        self._check(self.L.rg_set_stream(self.h, C.c_void_p(stream_handle)))
+
+    def sync(self):
+        self._check(self.L.rg_sync(self.h))
+
+    @property
+    def t(self) -> int:
+        return self.L.rg_tick_count(self.h)
+
+    @property
+    def device_bytes(self) -> int:
+        return self.L.rg_device_bytes(self.h)
+
+    # views
+    def replicas(self, first=0, n=None):
+        n = self.nrep - first if n is None else n
+        buf = (ReplicaView * n)()
+        self._check(self.L.rg_read_replicas(self.h, first, n, buf))
+        out = []
+        for v in buf:
+            d = {}
+            for f in REPLICA_FIELDS:
+                x = getattr(v, f)
+                d[f] = list(x)[:self.R] if not isinstance(x, int) else x
+            out.append(d)
+        return out
+
+    def replica(self, rid) -> dict:
+        return self.replicas(rid, 1)[0]
+
+    def msgs(self, rid, dst) -> list:
+        K, E = self.cfg["max_msgs_per_pair"], self.cfg["max_entries_per_msg"]
+        buf = (MsgView * K)()
+        terms = (C.c_uint64 * (K * E))()
+        n = self._check(self.L.rg_read_msgs(self.h, rid, dst, buf, K, terms))
+        out = []
+        for k in range(n):
+            m = buf[k]
+            d = {("from" if f == "from_" else f): getattr(m, f) for f in MSG_FIELDS}
+            d["terms"] = list(terms[k * E:k * E + m.nent]) if m.type == 12 else []
+            out.append(d)
+        return out
+
+    def entries(self, rid, first, n, with_payload=False):
+        if n <= 0:
+            return []
+        buf = (EntryView * n)()
+        pay = None
+        P = self.cfg["payload_bytes"]
+        if with_payload and P:
+            pay = (C.c_uint8 * (n * P))()
+        self._check(self.L.rg_read_entries(self.h, rid, first, n, buf, pay))
+        out = []
+        for k, ev in enumerate(buf):
+            d = dict(term=ev.term, type=ev.type, len=ev.len, crc=ev.crc)
+            if pay is not None:
+                d["payload"] = bytes(pay[k * P:k * P + ev.len])
+            out.append(d)
+        return out
+
+    def entry(self, rid, index, with_payload=False):
+        r = self.replica(rid)
+        if not (r["marker"] < index <= r["last"]):
+            return None
+        return self.entries(rid, index, 1, with_payload)[0]
+
+    def import_replica(self, rid, view: dict, terms, types=None, payloads=None):
+        v = ReplicaView()
+        for f in REPLICA_FIELDS:
+            if f in view:
+                x = view[f]
+                if isinstance(x, (list, tuple)):
+                    arr = getattr(v, f)
+                    for i, y in enumerate(x):
+                        arr[i] = y
+                else:
+                    setattr(v, f, x)
+        t = np.ascontiguousarray(np.array(terms, dtype=np.uint64))
+        ty = None if types is None else np.ascontiguousarray(np.array(types, dtype=np.uint32))
+        pl = None if payloads is None else np.ascontiguousarray(np.frombuffer(payloads, dtype=np.uint8))
+        self._check(self.L.rg_import_replica(self.h, rid, C.byref(v), t.ctypes.data if len(t) else None,
+                                             None if ty is None else ty.ctypes.data,
+                                             None if pl is None else pl.ctypes.data))
+
+    def deliver(self, rid_src, **fields):
+        m = MsgView()
+        for k, v in fields.items():
+            setattr(m, "from_" if k == "from" else k, v)
+        if "from" not in fields:
+            m.from_ = rid_src % self.R + 1
+        self._check(self.L.rg_deliver(self.h, rid_src, C.byref(m)))
+
+    def leader(self, group):
+        lid, term, valid = C.c_uint64(), C.c_uint64(), C.c_int()
+        self._check(self.L.rg_leader(self.h, group, C.byref(lid), C.byref(term), C.byref(valid)))
+        return lid.value, term.value, bool(valid.value)
+
+    def sum_committed(self) -> int:
+        v = C.c_uint64()
+        self._check(self.L.rg_sum_committed(self.h, C.byref(v)))
+        return v.value

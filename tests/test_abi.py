@@ -1,0 +1,37 @@
+"""The C-ABI library loads on a CPU-only host and exports every symbol include/raftgpu.h
+declares; host-side argument validation works without a GPU."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "raftgpu.h")).read()
+    return sorted(set(re.findall(r"\b(rg_[a-z_]+)\s*\(", src)))
+
+
+def test_header_declares_expected_api():
+    from raftd_amd.engine import EXPORTS
+    assert sorted(EXPORTS) == declared_symbols()
+
+
+def test_library_exports_every_declared_symbol():
+    from raftd_amd import build
+    lib_path = build.build_engine()
+    lib = C.CDLL(lib_path)
+    for name in declared_symbols():
+        assert hasattr(lib, name), name
+
+
+def test_create_rejects_bad_config_without_gpu():
+    from raftd_amd.engine import Config, load_library
+    L = load_library()
+    c = Config(groups=1, replicas=9, log_capacity=64, payload_bytes=16, max_entries_per_msg=8,
+               max_msgs_per_pair=8, num_slabs=2, election_rtt=10, heartbeat_rtt=1)
+    h = C.c_void_p()
+    assert L.rg_create(C.byref(c), C.byref(h)) == -1
+    assert b"replicas" in L.rg_last_error()

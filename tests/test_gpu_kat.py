@@ -1,0 +1,45 @@
+"""The known-answer tests of tests/test_kat.py, run on the HIP engine."""
+import pytest
+
+import kat_scenarios as K
+
+pytestmark = pytest.mark.gpu
+
+VOTER = K.load("kat_voter.json")
+MSGAPP = K.load("kat_check_msgapp.json")
+APPEND = K.load("kat_append.json")
+FIG7 = K.load("kat_figure7.json")
+CTC = K.load("kat_current_term_commit.json")
+QC = K.load("kat_quorum_commit.json")
+
+
+@pytest.mark.parametrize("case", VOTER["cases"])
+def test_voter_up_to_date(case):
+    assert K.run_voter("gpu", case) == case["reject"]
+
+
+@pytest.mark.parametrize("case", MSGAPP["cases"])
+def test_follower_check_msgapp(case):
+    got = K.run_check_msgapp("gpu", MSGAPP, case)
+    assert got == dict(reject=case["reject"], resp_index=case["resp_index"], hint=case["hint"])
+
+
+@pytest.mark.parametrize("case", APPEND["cases"])
+def test_follower_append_entries(case):
+    assert K.run_append("gpu", APPEND, case) == case["want"]
+
+
+def test_figure7_convergence():
+    logs, views = K.run_figure7("gpu", FIG7)
+    for lg in logs:
+        assert lg == FIG7["want_log"]
+    assert all(v["committed"] == FIG7["want_commit"] for v in views)
+
+
+def test_leader_only_commits_current_term():
+    assert K.run_current_term_commit("gpu", CTC) == [a["want_commit"] for a in CTC["acks"]]
+
+
+@pytest.mark.parametrize("case", QC["cases"])
+def test_quorum_commit(case):
+    assert K.run_quorum_commit("gpu", case) == case["committed"]
