@@ -190,12 +190,8 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
     rg_destroy(e);
     return fail(RG_EHIP, "crc table upload");
   }
-  // grid: as many 256-thread workgroups as are co-resident, capped by the replica count (4 waves each)
-  int cus = 0;
-  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device);
-  int per_cu = tick_blocks_per_cu(c.payload_bytes);
-  uint64_t want = std::min<uint64_t>((n + 3) / 4, (uint64_t)std::max(cus, 1) * std::max(per_cu, 1));
-  e->grid = (int)std::max<uint64_t>(1, want);
+  // grid: one wave per replica, 4 waves per 256-thread workgroup
+  e->grid = (int)((n + 3) / 4);
   *out = e;
   return RG_OK;
 }
@@ -203,10 +199,10 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
 void rg_destroy(rg_engine* e) {
   if (!e) return;
   if (e->own) {
-    hipStreamSynchronize(e->own);
-    hipStreamDestroy(e->own);
+    (void)hipStreamSynchronize(e->own);
+    (void)hipStreamDestroy(e->own);
   }
-  for (void* p : e->allocs) hipFree(p);
+  for (void* p : e->allocs) (void)hipFree(p);
   delete e;
 }
 

@@ -725,10 +725,9 @@ __global__ void __launch_bounds__(256) tick_kernel(TickParams p) {
   }
   __syncthreads();
   Crc crc{lds, lds + CRC_T_WORDS};
-  const uint32_t waves = blockDim.x >> 6;
-  const uint32_t w0 = blockIdx.x * waves + (threadIdx.x >> 6);
-  const uint32_t stride = gridDim.x * waves;
-  for (uint32_t rid = rfl(w0); rid < p.nrep; rid += stride) {
+  // one replica per wave: a grid-stride loop here makes hipcc keep ~2x the VGPRs live
+  const uint32_t rid = rfl(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  if (rid < p.nrep) {
     Step st(p, crc, rid);
     st.run();
   }

@@ -41,6 +41,8 @@ def compare(gpu, ora, t, check_entries=True):
 
 def check_payloads(gpu, ora, sample=4):
     G, R = ora.G, ora.R
+    if not ora.cfg["payload_bytes"]:
+        return
     for rid in range(0, G * R, max(1, G * R // sample)):
         v = ora.replica(rid)
         lo = max(v["marker"] + 1, v["last"] - 31)
