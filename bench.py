@@ -1,0 +1,230 @@
+"""raftd-amd benchmark: batched Raft group-steps/s and commits/s on MI355X.
+
+Workload (BASELINE.json metric "raft group-steps/sec & commits/sec, 64K groups x 3 replicas"):
+65,536 Raft groups x 3 replicas per GPU, steady state (slot 0 leads each group after a real
+election through the engine), every tick each leader receives a 64-entry proposal batch of
+256-B payloads (CRC32 per entry at every replica), raftd's Raft config (ElectionRTT 10,
+HeartbeatRTT 1, CheckQuorum, SnapshotEntries 1000, CompactionOverhead 5). A step = one tick of
+every replica of every group = one launch of the tick kernel. Inputs (proposal descriptors,
+payload slabs) are resident in HBM before the timed region.
+
+N > 1: one process per GPU (torch.distributed.run); each rank hosts its own 65,536 groups with
+all replicas on its GPU (weak scaling, no data-path collective in this round); value = groups
+over all ranks x K / max-over-ranks time.
+
+Prints one JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "raft group-steps/sec & commits/sec, 64K groups×3 replicas, 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--groups", type=int, default=65536)
+    ap.add_argument("--replicas", type=int, default=3)
+    ap.add_argument("--entries", type=int, default=64)
+    ap.add_argument("--payload", type=int, default=256)
+    ap.add_argument("--log-capacity", type=int, default=2048)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def bring_up(eng, G, R):
+    """bootstrap → tick → campaign slot 0 → election completes."""
+    import numpy as np
+    eng.bootstrap()
+    eng.tick()
+    camp = np.zeros(G * R, np.uint8)
+    camp[0::R] = 1
+    eng.tick(campaign=camp)
+    for _ in range(4):
+        eng.tick()
+
+
+def cpu_baseline(args, seconds):
+    """The C oracle (restatement of dragonboat's step) on host threads, dragonboat's step-worker
+    arrangement (group g → worker g % T), same per-group workload, bounded sample."""
+    import numpy as np
+    from oracle.pyoracle import Oracle
+
+    G, R, E = 2048, args.replicas, args.entries
+    try:
+        T = min(16, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        T = min(16, os.cpu_count() or 1)
+    o = Oracle(groups=G, replicas=R, payload_bytes=args.payload, max_entries_per_msg=E,
+               log_capacity=args.log_capacity)
+    o.bootstrap()
+    o.tick(threads=T)
+    camp = np.zeros(G * R, np.uint8)
+    camp[0::R] = 1
+    o.tick(campaign=camp, threads=T)
+    for _ in range(4):
+        o.tick(threads=T)
+    pt, pc = np.zeros(G, np.uint8), np.full(G, E, np.uint32)
+    warm = max(8, args.log_capacity // E + 8)  # wrap the log ring once
+    for _ in range(warm):
+        o.tick(pt, pc, threads=T)
+    c0 = o.replica(0)["committed"]
+    ticks, t0 = 0, time.perf_counter()
+    while True:
+        o.tick(pt, pc, threads=T)
+        ticks += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and ticks >= 5:
+            break
+    c1 = o.replica(0)["committed"]
+    return {
+        "value": G * ticks / el,
+        "unit": "group-steps/s",
+        "cores": T,
+        "kind": "port",
+        "sample": f"{G} groups x {R} replicas, {E} x {args.payload}-B entries per group-tick, {ticks} timed ticks "
+                  f"after {warm} warm ticks ({el:.1f} s); C restatement of dragonboat's step (oracle/oracle.c)",
+        "commits_per_sec": (c1 - c0) * G / el,
+    }
+
+
+def pmc_traffic(kernel="tick_kernel"):
+    """HBM bytes per tick-kernel launch from the committed rocprofv3 PMC summary (profiles/)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_summary.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    k = d.get("kernels", {}).get(kernel)
+    if not k:
+        return None, None
+    return k.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    from raftd_amd import Engine
+
+    G, R, E, P = args.groups, args.replicas, args.entries, args.payload
+    eng = Engine(groups=G, replicas=R, log_capacity=args.log_capacity, payload_bytes=P,
+                 max_entries_per_msg=E, device=local, seed=0x5EED + rank)
+    stream = torch.cuda.current_stream()
+    eng.set_stream(stream.cuda_stream)
+    bring_up(eng, G, R)
+    pt = torch.zeros(G, dtype=torch.uint8, device="cuda")
+    pc = torch.full((G,), E, dtype=torch.int32, device="cuda")  # read as uint32 by the kernel
+    for _ in range(max(args.warmup, 1)):
+        eng.tick_device(pt.data_ptr(), pc.data_ptr())
+    traffic = eng.last_tick_traffic()  # counts of a steady-state tick (outside the timed region)
+    c0 = eng.sum_committed()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        eng.tick_device(pt.data_ptr(), pc.data_ptr())
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    dev_ms = ev0.elapsed_time(ev1)
+    c1 = eng.sum_committed()
+    errs = sum(1 for v in eng.replicas(0, min(eng.nrep, 3 * 4096)) if v["err"])
+    t = torch.tensor([wall, dev_ms, float(c1 - c0)], dtype=torch.float64, device="cuda")
+    if dist:
+        tmax = t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = t.clone()
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        wall, dev_max, commits = tmax[0].item(), tmax[1].item(), tsum[2].item()
+    else:
+        dev_max, commits = dev_ms, float(c1 - c0)
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+    K = args.steps
+    group_steps = world * G * K / wall
+    kern_s = dev_ms / 1e3 / K  # one tick = one tick_kernel launch on this stream
+    achieved = traffic["algorithmic_bytes"] / kern_s / 1e9
+    hbm, src = pmc_traffic()
+    out = {
+        "metric": METRIC,
+        "value": group_steps,
+        "unit": "group-steps/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": args.warmup,
+        "ms_per_step": wall * 1e3 / K,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic",
+        "config": {
+            "workload": f"{G} groups x {R} replicas per GPU, steady-state leaders, {E}-entry batches of "
+                        f"{P}-B payloads + CRC32 per tick, raftd Raft config (ElectionRTT 10, HeartbeatRTT 1, "
+                        f"CheckQuorum, SnapshotEntries 1000, CompactionOverhead 5)",
+            "groups_per_gpu": G, "replicas": R, "entries_per_batch": E, "payload_bytes": P,
+            "log_capacity": args.log_capacity, "parallelism": f"groups sharded over {world} GPU(s), "
+                                                                "replicas co-located (no exchange)",
+        },
+        "commits_per_sec": commits / wall,
+        "replica_steps_per_sec": group_steps * R,
+        "device_ms_per_step": dev_max / K,
+        "invariant_errors_in_sample": errs,
+        "commits_expected_per_step": world * G * E,
+        "commits_measured_per_step": commits / K,
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": hbm,
+            "traffic_source": src,
+            "algorithmic_bytes_per_launch": traffic["algorithmic_bytes"],
+            "per_launch_counts": {k: v for k, v in traffic.items() if k != "algorithmic_bytes"},
+            "kernel": "rg::tick_kernel",
+        },
+        "device_bytes": eng.device_bytes,
+    }
+    if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
+        out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
+    print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

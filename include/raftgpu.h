@@ -110,6 +110,14 @@ typedef struct rg_tick_input {
   uint32_t _pad;
 } rg_tick_input;
 
+/* What the last tick moved, for the roofline numerator. Per SURVEY §8(d):
+ * algorithmic_bytes = 128·replicas + 36·R·leaders + 128·msgs + (16+P)·repl_entries
+ *                     + (12+P)·appended + P·leader_appended                              */
+typedef struct rg_traffic {
+  uint64_t replicas, leaders, msgs, repl_entries, appended, leader_appended;
+  uint64_t algorithmic_bytes;
+} rg_traffic;
+
 typedef struct rg_engine rg_engine;
 
 int rg_create(const rg_config* cfg, rg_engine** out);
@@ -143,6 +151,8 @@ int rg_deliver(rg_engine* e, uint32_t rid_src, const rg_msg_view* m);
 int rg_leader(rg_engine* e, uint32_t group, uint64_t* leader_id, uint64_t* term, int* valid);
 /* Sum over groups of the highest committed index among the group's replicas. */
 int rg_sum_committed(rg_engine* e, uint64_t* out);
+/* Message / entry counts of the last tick and the algorithmic bytes they imply. */
+int rg_last_tick_traffic(rg_engine* e, rg_traffic* out);
 /* Device bytes held by the engine. */
 uint64_t rg_device_bytes(const rg_engine* e);
 const char* rg_last_error(void);

@@ -808,6 +808,9 @@ int or_create(const or_config* cfg, or_engine** out) {
     r->s = i % c->replicas;
     r->log = (ent_t*)calloc(c->log_capacity, sizeof(ent_t));
     if (c->payload_bytes) r->logpay = (uint8_t*)calloc((size_t)c->log_capacity, c->payload_bytes);
+    /* pre-fault the rings so timed ticks do not pay first-touch page faults */
+    memset(r->log, 0, (size_t)c->log_capacity * sizeof(ent_t));
+    if (r->logpay) memset(r->logpay, 0, (size_t)c->log_capacity * c->payload_bytes);
     for (int b = 0; b < 2; ++b)
       r->ob[b].m = (msg_t*)calloc((size_t)c->replicas * c->max_msgs_per_pair, sizeof(msg_t));
   }

@@ -173,7 +173,7 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if (rc == RG_OK) rc = dalloc(e, &e->d_prop_count, c.groups * 4ull);
   if (rc == RG_OK) rc = dalloc(e, &e->d_campaign, n);
   if (rc == RG_OK) rc = dalloc(e, &e->d_isolate, n);
-  if (rc == RG_OK) rc = dalloc(e, &e->d_sum, 8);
+  if (rc == RG_OK) rc = dalloc(e, &e->d_sum, 64);
   if (rc != RG_OK) {
     std::string msg = g_err;
     rg_destroy(e);
@@ -467,6 +467,28 @@ int rg_sum_committed(rg_engine* e, uint64_t* out) {
   HIPCHK(hipMemcpyAsync(&v, e->d_sum, 8, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   *out = v;
+  return RG_OK;
+}
+
+int rg_last_tick_traffic(rg_engine* e, rg_traffic* out) {
+  if (!e || !out) return fail(RG_EINVAL, "rg_last_tick_traffic args");
+  if (e->t == 0) return fail(RG_EINVAL, "no tick has run");
+  // the last tick read st[(t+1)&1] and wrote st[t&1], cnt/hdr[(t+1)&1] ... viewed as a tick input:
+  TickParams p = params(e);  // p.st_in = current state, p.cnt_in/hdr_in = last tick's outbox
+  HIPCHK(hipMemsetAsync(e->d_sum, 0, 64, e->stream));
+  HIPCHK(launch_traffic(p, e->st[(e->t + 1) & 1], e->d_sum, e->stream));
+  unsigned long long v[8] = {0};
+  HIPCHK(hipMemcpyAsync(v, e->d_sum, 64, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  const uint64_t P = e->c.payload_bytes, R = e->c.replicas;
+  out->replicas = e->nrep;
+  out->leaders = v[0];
+  out->msgs = v[1];
+  out->repl_entries = v[2];
+  out->appended = v[3];
+  out->leader_appended = v[4];
+  out->algorithmic_bytes = 128ull * e->nrep + 36ull * R * v[0] + 128ull * v[1] + (16 + P) * v[2] +
+                           (12 + P) * v[3] + P * v[4];
   return RG_OK;
 }
 

@@ -78,6 +78,7 @@ hipError_t launch_fill_slabs(uint8_t* slabs, uint32_t nslab, uint32_t G, uint32_
                              hipStream_t s);
 hipError_t launch_sum_committed(const RepState* st, uint32_t G, uint32_t R, unsigned long long* out,
                                 hipStream_t s);
+hipError_t launch_traffic(const TickParams& p, const RepState* st_prev, unsigned long long* out6, hipStream_t s);
 int tick_lds_bytes(uint32_t P);
 int tick_blocks_per_cu(uint32_t P);
 

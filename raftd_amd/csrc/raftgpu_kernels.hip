@@ -824,4 +824,40 @@ hipError_t launch_sum_committed(const RepState* st, uint32_t G, uint32_t R, unsi
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ last-tick traffic accounting
+// out6: leaders, msgs, repl_entries, appended, leader_appended, (unused)
+__global__ void traffic_kernel(TickParams p, const RepState* st_prev, unsigned long long* out6) {
+  uint64_t v[5] = {0, 0, 0, 0, 0};
+  for (uint32_t rid = blockIdx.x * blockDim.x + threadIdx.x; rid < p.nrep; rid += gridDim.x * blockDim.x) {
+    const RepState& cur = p.st_in[rid];
+    const bool ld = cur.role == LEADER;
+    v[0] += ld;
+    for (uint32_t d = 0; d < p.R; ++d) {
+      const uint32_t n = p.cnt_in[(uint64_t)rid * p.R + d];
+      v[1] += n;
+      for (uint32_t k = 0; k < n; ++k) {
+        const MsgHdr& h = p.hdr_in[((uint64_t)rid * p.R + d) * p.K + k];
+        if ((h.w0 & 0xFF) == M_REPLICATE) v[2] += h.w0 >> 32;
+      }
+    }
+    const uint64_t app = cur.last > st_prev[rid].last ? cur.last - st_prev[rid].last : 0;
+    v[3] += app;
+    if (ld) v[4] += app;
+  }
+  for (int i = 0; i < 5; ++i) {
+    uint64_t a = v[i];
+    for (int off = 32; off > 0; off >>= 1) {
+      uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)a, off, 64);
+      uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(a >> 32), off, 64);
+      a += ((uint64_t)hi << 32) | lo;
+    }
+    if (lane_id() == 0 && a) atomicAdd(out6 + i, (unsigned long long)a);
+  }
+}
+
+hipError_t launch_traffic(const TickParams& p, const RepState* st_prev, unsigned long long* out6, hipStream_t s) {
+  hipLaunchKernelGGL(traffic_kernel, dim3(512), dim3(256), 0, s, p, st_prev, out6);
+  return hipGetLastError();
+}
+
 }  // namespace rg

@@ -63,6 +63,11 @@ class EntryView(C.Structure):
                 ("crc", C.c_uint32), ("bank", C.c_uint32)]
 
 
+class Traffic(C.Structure):
+    _fields_ = [(f, C.c_uint64) for f in ("replicas", "leaders", "msgs", "repl_entries", "appended",
+                                          "leader_appended", "algorithmic_bytes")]
+
+
 class TickInput(C.Structure):
     _fields_ = [("prop_target", C.c_void_p), ("prop_count", C.c_void_p), ("campaign", C.c_void_p),
                 ("isolate", C.c_void_p), ("flags", C.c_uint32), ("_pad", C.c_uint32)]
@@ -75,7 +80,7 @@ MSG_FIELDS = [f for f, _ in MsgView._fields_]
 EXPORTS = ["rg_create", "rg_destroy", "rg_bootstrap", "rg_fill_slabs", "rg_tick", "rg_tick_device",
            "rg_set_stream", "rg_sync", "rg_tick_count", "rg_read_replicas", "rg_read_msgs",
            "rg_read_entries", "rg_import_replica", "rg_deliver", "rg_leader", "rg_sum_committed",
-           "rg_device_bytes", "rg_last_error"]
+           "rg_device_bytes", "rg_last_error", "rg_last_tick_traffic"]
 
 _lib = None
 
@@ -107,6 +112,7 @@ def load_library(path: str = LIB_PATH):
         "rg_leader": ([vp, u32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_int)], i32),
         "rg_sum_committed": ([vp, C.POINTER(C.c_uint64)], i32),
         "rg_device_bytes": ([vp], u64),
+        "rg_last_tick_traffic": ([vp, C.POINTER(Traffic)], i32),
         "rg_last_error": ([], C.c_char_p),
     }
     for name, (args, res) in sig.items():
@@ -288,3 +294,8 @@ class Engine:
         v = C.c_uint64()
         self._check(self.L.rg_sum_committed(self.h, C.byref(v)))
         return v.value
+
+    def last_tick_traffic(self) -> dict:
+        t = Traffic()
+        self._check(self.L.rg_last_tick_traffic(self.h, C.byref(t)))
+        return {f: getattr(t, f) for f, _ in Traffic._fields_}
