@@ -133,7 +133,8 @@ def main():
     G, R, E, P = args.groups, args.replicas, args.entries, args.payload
     eng = Engine(groups=G, replicas=R, log_capacity=args.log_capacity, payload_bytes=P,
                  max_entries_per_msg=E, device=local, seed=0x5EED + rank)
-    stream = torch.cuda.current_stream()
+    stream = torch.cuda.Stream()  # a real (non-null) stream: the engine launches on it, events time it
+    torch.cuda.set_stream(stream)
     eng.set_stream(stream.cuda_stream)
     bring_up(eng, G, R)
     pt = torch.zeros(G, dtype=torch.uint8, device="cuda")

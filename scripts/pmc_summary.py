@@ -1,0 +1,73 @@
+"""Summarise rocprofv3 CSV output (kernel trace + separate FETCH_SIZE / WRITE_SIZE PMC passes)
+into profiles/<tag>_pmc_summary.json and profiles/<tag>_kernel_stats.csv.
+
+HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE (KB) reads exactly half of a
+wide coalesced stream on gfx950, so hbm = (2*FETCH_SIZE + WRITE_SIZE) * 1024; the tick kernel's
+payload traffic is 16 B/lane coalesced, which is the calibrated case.
+usage: python scripts/pmc_summary.py TAG KTRACE_DIR FETCH_DIR WRITE_DIR [last_n]
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+
+def rows(d, pattern):
+    out = []
+    for f in sorted(glob.glob(os.path.join(d, "**", pattern), recursive=True)):
+        with open(f) as fh:
+            out += list(csv.DictReader(fh))
+    return out
+
+
+def short(name):
+    for k in ("tick_kernel", "bootstrap_kernel", "fill_slabs_kernel", "sum_committed_kernel", "traffic_kernel"):
+        if k in name:
+            return k
+    return name[:60]
+
+
+def pmc(d, counter, last_n):
+    vals = {}
+    for r in rows(d, "*counter_collection.csv"):
+        if r.get("Counter_Name") != counter:
+            continue
+        k = short(r.get("Kernel_Name", ""))
+        vals.setdefault(k, []).append((int(r.get("Dispatch_Id", 0)), float(r["Counter_Value"])))
+    return {k: [v for _, v in sorted(x)][-last_n:] for k, x in vals.items()}
+
+
+def main():
+    tag, kdir, fdir, wdir = sys.argv[1:5]
+    last_n = int(sys.argv[5]) if len(sys.argv) > 5 else 5
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prof = os.path.join(root, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    stats = glob.glob(os.path.join(kdir, "**", "*kernel_stats.csv"), recursive=True)
+    if stats:
+        shutil.copy(stats[0], os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    trace = rows(kdir, "*kernel_trace.csv")
+    dur = {}
+    for r in trace:
+        k = short(r.get("Kernel_Name", ""))
+        dur.setdefault(k, []).append((int(r.get("Dispatch_Id", 0)), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+    fetch = pmc(fdir, "FETCH_SIZE", last_n)
+    write = pmc(wdir, "WRITE_SIZE", last_n)
+    out = {"note": __doc__.strip().splitlines()[0], "last_n_dispatches": last_n, "kernels": {}}
+    for k in set(dur) | set(fetch):
+        d = [v for _, v in sorted(dur.get(k, []))][-last_n:]
+        e = {"dispatches_averaged": len(d), "avg_duration_ns": sum(d) / len(d) if d else None}
+        if k in fetch and k in write and fetch[k] and write[k]:
+            fk = sum(fetch[k]) / len(fetch[k])
+            wk = sum(write[k]) / len(write[k])
+            e.update(fetch_size_kb=fk, write_size_kb=wk, hbm_bytes_per_launch=(2 * fk + wk) * 1024)
+        out["kernels"][k] = e
+    with open(os.path.join(prof, f"{tag}_pmc_summary.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Profile the bench's tick kernel on the GPU box: kernel trace + stats, then FETCH_SIZE and
+# WRITE_SIZE in separate PMC passes (MI355X_MICROARCH.md: TCC slots cannot hold both).
+# usage: bash scripts/profile.sh TAG [bench args...]
+set -euo pipefail
+TAG=$1; shift
+ARGS="${@:---steps 10 --warmup 3 --no-cpu-baseline}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/prof_$TAG
+rm -rf $OUT; mkdir -p $OUT
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/ktrace -- python3 bench.py $ARGS > $OUT/ktrace.log 2>&1
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -- python3 bench.py $ARGS > $OUT/fetch.log 2>&1
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -- python3 bench.py $ARGS > $OUT/write.log 2>&1
+python3 scripts/pmc_summary.py $TAG $OUT/ktrace $OUT/fetch $OUT/write 10
