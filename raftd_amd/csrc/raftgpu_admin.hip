@@ -1,0 +1,180 @@
+// raftgpu_admin.hip — small gather / scatter kernels behind rg_read_*, rg_import_replica and
+// rg_deliver: they translate between the device's structure-of-arrays layout (slot-major
+// replica numbering q = s·G + g) and the C-ABI's per-replica views (rid = g·R + s).
+// Not on the tick path.
+#include "../../include/raftgpu.h"
+#include "raftgpu_internal.h"
+
+namespace rg {
+
+__device__ __forceinline__ uint32_t q_of(const TickParams& t, uint32_t rid) {
+  const uint32_t g = rid / t.R, s = rid - g * t.R;
+  return s * t.G + g;
+}
+
+__global__ void gather_replicas_kernel(AdminParams a, uint32_t first, uint32_t n, rg_replica_view* out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const TickParams& t = a.t;
+  const uint32_t q = q_of(t, first + i);
+  const uint64_t N = t.nrep;
+  rg_replica_view v;
+  const uint64_t* s64 = t.s64_in + q;
+  const uint32_t* s32 = t.s32_in + q;
+  v.term = s64[S_TERM * N]; v.vote = s64[S_VOTE * N]; v.leader = s64[S_LEADER * N];
+  v.committed = s64[S_COMMITTED * N]; v.applied = s64[S_APPLIED * N]; v.last = s64[S_LAST * N];
+  v.marker = s64[S_MARKER * N]; v.marker_term = s64[S_MARKER_TERM * N]; v.snap_index = s64[S_SNAP_INDEX * N];
+  v.snap_term = s64[S_SNAP_TERM * N]; v.cap_base = s64[S_CAP_BASE * N];
+  v.role = s32[S_ROLE * N]; v.election_tick = s32[S_ETICK * N]; v.heartbeat_tick = s32[S_HTICK * N];
+  v.rand_timeout = s32[S_RAND_TO * N]; v.rng_ctr = s32[S_RNG_CTR * N]; v.granted = s32[S_GRANTED * N];
+  v.responded = s32[S_RESPONDED * N]; v.active = s32[S_ACTIVE * N];
+  v.err = s32[S_ERR * N] | a.crc_err[q];
+  v.drops = s32[S_DROPS * N];
+  for (uint32_t j = 0; j < RG_MAX_REPLICAS; ++j) {
+    const bool in = j < t.R;
+    v.match[j] = in ? t.rem_in[(0 * t.R + j) * N + q] : 0;
+    v.next[j] = in ? t.rem_in[(1 * t.R + j) * N + q] : 0;
+    v.rsnap[j] = in ? t.rem_in[(2 * t.R + j) * N + q] : 0;
+    v.rstate[j] = in ? t.rst_in[j * N + q] : 0;
+  }
+  out[i] = v;
+}
+
+hipError_t launch_gather_replicas(const AdminParams& a, uint32_t first, uint32_t n, void* out, hipStream_t s) {
+  hipLaunchKernelGGL(gather_replicas_kernel, dim3((n + 63) / 64), dim3(64), 0, s, a, first, n,
+                     (rg_replica_view*)out);
+  return hipGetLastError();
+}
+
+// the last tick's messages rid → dst: the outbox as the next tick will read it (hdr_in / mt_in)
+__global__ void gather_msgs_kernel(AdminParams a, uint32_t rid, uint32_t dst, uint64_t* out_hdr, uint64_t* out_terms,
+                                   uint32_t* out_cnt) {
+  const TickParams& t = a.t;
+  const uint32_t g = rid / t.R, s = rid - g * t.R;
+  const uint64_t plane = (uint64_t)t.R * t.R * t.K * t.G;
+  const uint32_t cnt = t.cnt_in[((uint64_t)s * t.R + dst) * t.G + g];
+  const uint32_t k = threadIdx.x;
+  if (k == 0) *out_cnt = cnt;
+  if (k >= cnt || k >= t.K) return;
+  const uint64_t* h = t.hdr_in + (((uint64_t)s * t.R + dst) * t.K + k) * t.G + g;
+  for (int w = 0; w < 8; ++w) out_hdr[k * 8 + w] = h[w * plane];
+  const uint64_t* mt = t.mt_in + ((((uint64_t)s * t.R + dst) * t.K + k) * t.E) * t.G + g;
+  const uint32_t type = (uint32_t)(h[0] & 0xFF), n = (uint32_t)(h[0] >> 32);
+  for (uint32_t e = 0; e < t.E; ++e)
+    out_terms[(uint64_t)k * t.E + e] = (type == M_REPLICATE && e < n) ? (mt[(uint64_t)e * t.G] & TERM_MASK) : 0;
+}
+
+hipError_t launch_gather_msgs(const AdminParams& a, uint32_t rid, uint32_t dst, void* out_hdr, uint64_t* out_terms,
+                              uint32_t* out_cnt, hipStream_t s) {
+  hipLaunchKernelGGL(gather_msgs_kernel, dim3(1), dim3(64), 0, s, a, rid, dst, (uint64_t*)out_hdr, out_terms,
+                     out_cnt);
+  return hipGetLastError();
+}
+
+__global__ void gather_entries_kernel(AdminParams a, uint32_t rid, uint64_t first, uint32_t n, rg_entry_view* out,
+                                      uint8_t* out_pay) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const TickParams& t = a.t;
+  const uint32_t q = q_of(t, rid);
+  const uint64_t slot = (first + i) & (t.L - 1);
+  const uint64_t w = t.tr[slot * t.nrep + q];
+  const uint64_t bank = w >> 63;
+  const uint2 inf = a.info[(bank * t.nrep + q) * t.L + slot];
+  rg_entry_view v;
+  v.term = w & TERM_MASK;
+  v.type = (uint32_t)((w >> 61) & 1);
+  v.len = inf.y & 0xFFFFFF;
+  v.crc = inf.x;
+  v.bank = (uint32_t)bank;
+  out[i] = v;
+  if (out_pay && t.P && v.len) {
+    const uint8_t* src = a.pay + ((bank * t.nrep + q) * t.L + slot) * t.P;
+    for (uint32_t b = 0; b < v.len; ++b) out_pay[(uint64_t)i * t.P + b] = src[b];
+  }
+}
+
+hipError_t launch_gather_entries(const AdminParams& a, uint32_t rid, uint64_t first, uint32_t n, void* out,
+                                 uint8_t* out_pay, hipStream_t s) {
+  hipLaunchKernelGGL(gather_entries_kernel, dim3((n + 63) / 64), dim3(64), 0, s, a, rid, first, n,
+                     (rg_entry_view*)out, out_pay);
+  return hipGetLastError();
+}
+
+// import: view + entry words (term|type|pay, bank 0) + payloads + CRCs into the current state
+__global__ void scatter_replica_kernel(AdminParams a, uint32_t rid, const rg_replica_view* vv, const uint64_t* words,
+                                       const uint8_t* pays, const uint32_t* crcs, uint32_t nent, uint2* info,
+                                       uint8_t* pay) {
+  const TickParams& t = a.t;
+  const uint32_t q = q_of(t, rid);
+  const uint64_t N = t.nrep;
+  const rg_replica_view& v = *vv;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) {
+    uint64_t* s64 = const_cast<uint64_t*>(t.s64_in) + q;
+    uint32_t* s32 = const_cast<uint32_t*>(t.s32_in) + q;
+    s64[S_TERM * N] = v.term; s64[S_VOTE * N] = v.vote; s64[S_LEADER * N] = v.leader;
+    s64[S_COMMITTED * N] = v.committed; s64[S_APPLIED * N] = v.applied; s64[S_LAST * N] = v.last;
+    s64[S_MARKER * N] = v.marker; s64[S_MARKER_TERM * N] = v.marker_term; s64[S_SNAP_INDEX * N] = v.snap_index;
+    s64[S_SNAP_TERM * N] = v.snap_term; s64[S_CAP_BASE * N] = v.cap_base;
+    s32[S_ROLE * N] = v.role; s32[S_ETICK * N] = v.election_tick; s32[S_HTICK * N] = v.heartbeat_tick;
+    s32[S_RAND_TO * N] = v.rand_timeout; s32[S_RNG_CTR * N] = v.rng_ctr; s32[S_GRANTED * N] = v.granted;
+    s32[S_RESPONDED * N] = v.responded; s32[S_ACTIVE * N] = v.active; s32[S_ERR * N] = v.err;
+    s32[S_DROPS * N] = v.drops;
+    uint64_t* rem = const_cast<uint64_t*>(t.rem_in);
+    uint8_t* rst = const_cast<uint8_t*>(t.rst_in);
+    for (uint32_t j = 0; j < t.R; ++j) {
+      rem[(0 * t.R + j) * N + q] = v.match[j];
+      rem[(1 * t.R + j) * N + q] = v.next[j];
+      rem[(2 * t.R + j) * N + q] = v.rsnap[j];
+      rst[j * N + q] = v.rstate[j];
+    }
+  }
+  if (i >= nent) return;
+  const uint64_t idx = v.marker + 1 + i, slot = idx & (t.L - 1);
+  const uint64_t w = words[i] & ~BANK_BIT;
+  t.tr[slot * N + q] = w;
+  const bool hp = (w >> 62) & 1;
+  info[(uint64_t)q * t.L + slot] = make_uint2(hp ? crcs[i] : 0u, ((uint32_t)((w >> 61) & 1) << 24) | (hp ? t.P : 0u));
+  if (hp)
+    for (uint32_t b = 0; b < t.P; ++b) pay[((uint64_t)q * t.L + slot) * t.P + b] = pays[(uint64_t)i * t.P + b];
+}
+
+hipError_t launch_scatter_replica(const AdminParams& a, uint32_t rid, const void* view, const uint64_t* words,
+                                  const uint8_t* pays, const uint32_t* crcs, uint32_t nent, hipStream_t s,
+                                  uint2* info, uint8_t* pay) {
+  const uint32_t n = nent > 0 ? nent : 1;
+  hipLaunchKernelGGL(scatter_replica_kernel, dim3((n + 63) / 64), dim3(64), 0, s, a, rid,
+                     (const rg_replica_view*)view, words, pays, crcs, nent, info, pay);
+  return hipGetLastError();
+}
+
+// deliver: append a header to rid_src's last-tick outbox (inline terms from the sender's log)
+__global__ void deliver_kernel(AdminParams a, uint32_t rid, const rg_msg_view* m, uint32_t* status) {
+  const TickParams& t = a.t;
+  const uint32_t g = rid / t.R, s = rid - g * t.R, q = s * t.G + g;
+  const uint32_t dst = m->to - 1;
+  uint32_t* cnt = const_cast<uint32_t*>(t.cnt_in) + ((uint64_t)s * t.R + dst) * t.G + g;
+  const uint32_t k = *cnt;
+  if (k >= t.K) {
+    *status = 1;
+    return;
+  }
+  const uint64_t plane = (uint64_t)t.R * t.R * t.K * t.G;
+  uint64_t* h = const_cast<uint64_t*>(t.hdr_in) + (((uint64_t)s * t.R + dst) * t.K + k) * t.G + g;
+  const uint64_t* src = reinterpret_cast<const uint64_t*>(m);
+  for (int w = 0; w < 8; ++w) h[w * plane] = src[w];
+  if (m->type == M_REPLICATE) {
+    uint64_t* mt = const_cast<uint64_t*>(t.mt_in) + ((((uint64_t)s * t.R + dst) * t.K + k) * t.E) * t.G + g;
+    for (uint32_t e = 0; e < m->nent; ++e) mt[(uint64_t)e * t.G] = t.tr[((m->log_index + 1 + e) & (t.L - 1)) * t.nrep + q];
+  }
+  *cnt = k + 1;
+  *status = 0;
+}
+
+hipError_t launch_deliver(const AdminParams& a, uint32_t rid_src, const void* hdr, uint32_t* status, hipStream_t s) {
+  hipLaunchKernelGGL(deliver_kernel, dim3(1), dim3(1), 0, s, a, rid_src, (const rg_msg_view*)hdr, status);
+  return hipGetLastError();
+}
+
+}  // namespace rg

@@ -1,0 +1,635 @@
+// raftgpu_control.h — the per-replica Raft step (control_kernel<R>'s body), kept in a header so
+// the same code compiles for the GPU (RG_FN = __device__ __forceinline__) and, in the test-only
+// host harness tests/native/ctl_host.cpp, for the CPU under AddressSanitizer.
+// Semantics: DESIGN.md §1 (dragonboat v4 internal/raft restated).
+#pragma once
+#include "raftgpu_internal.h"
+
+#include <type_traits>
+
+#ifndef RG_FN
+#define RG_FN __device__ __forceinline__
+#endif
+
+namespace rg {
+
+RG_FN uint64_t mix64(uint64_t z) {
+  z ^= z >> 30;
+  z *= 0xBF58476D1CE4E5B9ULL;
+  z ^= z >> 27;
+  z *= 0x94D049BB133111EBULL;
+  z ^= z >> 31;
+  return z;
+}
+RG_FN uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+RG_FN uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+
+// ================================================================== control kernel
+// Compile-time loop: f(integral_constant<int, J>) for J = B .. E-1, fully unrolled.
+template <int B, int E, class F>
+RG_FN void sfor(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    sfor<B + 1, E>(f);
+  }
+}
+// remote slot f of a per-replica array, with constant indices only (the arrays stay in registers)
+template <int R, class T>
+RG_FN T sel_get(const T (&a)[R], uint32_t f) {
+  T v = a[0];
+  sfor<1, R>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    v = (uint32_t)j == f ? a[j] : v;
+  });
+  return v;
+}
+template <int R, class T, class V>
+RG_FN void sel_set(T (&a)[R], uint32_t f, V val) {
+  sfor<0, R>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    a[j] = (uint32_t)j == f ? (T)val : a[j];
+  });
+}
+
+template <int R>
+struct Ctl {
+  const TickParams p;  // by value: pointer fields stay kernel-argument (global) pointers
+  uint32_t q, g, s, rid;
+  uint64_t term, vote, leader, committed, applied, last, marker, marker_term, snap_index, snap_term, cap_base;
+  uint32_t role, etick, htick, rand_to, rng_ctr, granted, responded, active, err, drops;
+  uint64_t rm[R], rn[R], rs[R];  // remote match / next / snapshot index
+  uint32_t rt[R];                // remote state
+  uint64_t last_start, sent_hi, rw_lo, rw_hi, marker_start;
+  uint64_t oc, em;  // per destination: enqueued / emitted counts, 8 bits each
+  uint32_t nj;      // jobs emitted
+
+  RG_FN Ctl(const TickParams& pp, uint32_t qq) : p(pp), q(qq) {
+    s = q / p.G;
+    g = q - s * p.G;
+    rid = g * R + s;
+    const uint64_t n = p.nrep;
+    const uint64_t* a = p.s64_in + q;
+    term = a[S_TERM * n]; vote = a[S_VOTE * n]; leader = a[S_LEADER * n]; committed = a[S_COMMITTED * n];
+    applied = a[S_APPLIED * n]; last = a[S_LAST * n]; marker = a[S_MARKER * n]; marker_term = a[S_MARKER_TERM * n];
+    snap_index = a[S_SNAP_INDEX * n]; snap_term = a[S_SNAP_TERM * n]; cap_base = a[S_CAP_BASE * n];
+    const uint32_t* b = p.s32_in + q;
+    role = b[S_ROLE * n]; etick = b[S_ETICK * n]; htick = b[S_HTICK * n]; rand_to = b[S_RAND_TO * n];
+    rng_ctr = b[S_RNG_CTR * n]; granted = b[S_GRANTED * n]; responded = b[S_RESPONDED * n];
+    active = b[S_ACTIVE * n]; err = b[S_ERR * n]; drops = b[S_DROPS * n];
+    sfor<0, R>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      rm[j] = p.rem_in[(0 * R + j) * n + q];
+      rn[j] = p.rem_in[(1 * R + j) * n + q];
+      rs[j] = p.rem_in[(2 * R + j) * n + q];
+      rt[j] = p.rst_in[j * n + q];
+    });
+    last_start = last; sent_hi = 0; rw_lo = ~0ull; rw_hi = 0; marker_start = marker;
+    oc = 0; em = 0; nj = 0;
+  }
+
+  RG_FN uint32_t quorum() const { return R / 2 + 1; }
+  RG_FN uint32_t my_id() const { return s + 1; }
+
+  // ---- remotes (compile-time R: selects, no local-memory arrays)
+#define RG_GET(arr, f) sel_get<R>(arr, f)
+#define RG_SET(arr, f, val) sel_set<R>(arr, f, val)
+
+  // ---- log (entryLog)
+  RG_FN uint64_t* tr_at(uint64_t i) const {
+    return p.tr + (uint64_t)(i & (p.L - 1)) * p.nrep + q;
+  }
+  RG_FN uint64_t term_at(uint64_t i) const {
+    if (i == marker) return marker_term;
+    if (i > marker && i <= last) return *tr_at(i) & TERM_MASK;
+    return 0;
+  }
+  RG_FN void commit_to(uint64_t i) {
+    if (i <= committed) return;
+    if (i > last) {
+      err |= ERR_BEYOND;
+      return;
+    }
+    committed = i;
+  }
+
+  // ---- transport
+  RG_FN static uint32_t get8(uint64_t packed, uint32_t d) {
+    return (uint32_t)(packed >> (8 * d)) & 0xFF;
+  }
+  RG_FN bool lost(uint32_t dst, uint32_t n) const {
+    if (p.isolate && (p.isolate[rid] || p.isolate[g * R + dst])) return true;
+    if (p.drop_ppm) {
+      uint64_t h = mix64(p.seed ^ mix64((p.tick << 40) ^ ((uint64_t)rid << 8) ^ dst) ^ (uint64_t)(n + 1));
+      if (h % 1000000ull < p.drop_ppm) return true;
+    }
+    return false;
+  }
+  // raft.send + enqueue into the outbox slot (SoA). Returns slot k, or -1 if lost.
+  RG_FN int send(uint32_t type, uint32_t to, uint64_t mterm, uint32_t reject, uint32_t nent,
+                                      uint64_t log_term, uint64_t log_index, uint64_t commit, uint64_t hint,
+                                      uint64_t hint_high, uint32_t src_a, uint32_t src_b) {
+    const uint32_t dst = to - 1;
+    if (type != M_PROPOSE && type != M_REQUEST_VOTE) mterm = term;
+    const uint32_t n = get8(em, dst);
+    em += 1ull << (8 * dst);
+    const uint32_t k = get8(oc, dst);
+    if (lost(dst, n) || k >= p.K) {
+      drops++;
+      return -1;
+    }
+    oc += 1ull << (8 * dst);
+    const uint64_t plane = (uint64_t)R * R * p.K * p.G;
+    uint64_t* h = p.hdr_out + (((uint64_t)s * R + dst) * p.K + k) * p.G + g;
+    h[0 * plane] = (uint64_t)type | ((uint64_t)my_id() << 8) | ((uint64_t)to << 16) | ((uint64_t)reject << 24) |
+                   ((uint64_t)nent << 32);
+    h[1 * plane] = mterm;
+    h[2 * plane] = log_term;
+    h[3 * plane] = log_index;
+    h[4 * plane] = commit;
+    h[5 * plane] = hint;
+    h[6 * plane] = hint_high;
+    h[7 * plane] = (uint64_t)src_a | ((uint64_t)src_b << 32);
+    return (int)k;
+  }
+  RG_FN int send_simple(uint32_t type, uint32_t to, uint32_t reject = 0, uint64_t log_index = 0,
+                                             uint64_t hint = 0, uint64_t hint_high = 0) {
+    return send(type, to, 0, reject, 0, 0, log_index, 0, hint, hint_high, 0, 0);
+  }
+
+  // ---- role transitions (A.5)
+  RG_FN void reset(uint64_t t) {
+    if (t != term) {
+      term = t;
+      vote = 0;
+    }
+    leader = 0;
+    granted = responded = 0;
+    etick = htick = 0;
+    rng_ctr++;
+    uint64_t key = ((uint64_t)g << 32) | ((uint64_t)s << 24) | (uint64_t)(rng_ctr & 0xFFFFFF);
+    rand_to = p.ET + (uint32_t)(mix64(p.seed ^ mix64(key)) % p.ET);
+    sfor<0, R>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      rm[j] = (uint32_t)j == s ? last : 0;
+      rn[j] = last + 1;
+      rs[j] = 0;
+      rt[j] = RETRY;
+    });
+    active = 0;
+  }
+  RG_FN void become_follower(uint64_t t, uint64_t l) {
+    role = FOLLOWER;
+    reset(t);
+    leader = l;
+  }
+  RG_FN void become_candidate() {
+    role = CANDIDATE;
+    reset(term + 1);
+    leader = 0;
+    vote = my_id();
+  }
+
+  // remote.tryUpdate
+  RG_FN bool remote_try_update(uint32_t f, uint64_t idx) {
+    const uint64_t nx = RG_GET(rn, f), mt = RG_GET(rm, f);
+    const uint32_t st = RG_GET(rt, f);
+    if (nx < idx + 1) RG_SET(rn, f, idx + 1);
+    if (mt < idx) {
+      if (st == WAIT) RG_SET(rt, f, (uint32_t)RETRY);
+      RG_SET(rm, f, idx);
+      return true;
+    }
+    return false;
+  }
+
+  // raft.tryCommit: q = max{m_i : #{j : m_j >= m_i} >= quorum} = sorted_asc[R - quorum]
+  RG_FN bool try_commit() {
+    uint64_t qv = 0;
+    sfor<0, R>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      uint32_t cnt = 0;
+      sfor<0, R>([&](auto jc) { cnt += rm[decltype(jc)::value] >= rm[i] ? 1u : 0u; });
+      if (cnt >= quorum()) qv = umax64(qv, rm[i]);
+    });
+    if (qv > committed && term_at(qv) == term) {
+      committed = qv;
+      return true;
+    }
+    return false;
+  }
+
+  // ---- log writes: term ring + banks, and a job for the bulk kernel
+  // Entry e in [e0, n) goes to index base+e. Words come from the sender's inline terms (RING:
+  // mt points at entry 0, stride G) or are `word` for every entry (SLAB proposals, no-op).
+  RG_FN void write_entries(uint64_t base, uint32_t e0, uint32_t n, uint32_t kind, uint32_t src,
+                                const uint64_t* mt, uint64_t word) {
+    const uint64_t hi_prot = umax64(last_start, sent_hi);
+    uint64_t dm = 0, sm = 0, hm = 0, tm = 0;
+    for (uint32_t e = e0; e < n; ++e) {
+      const uint64_t idx = base + e;
+      const uint64_t w = mt ? mt[(uint64_t)e * p.G] : word;
+      uint64_t* rp = tr_at(idx);
+      uint32_t tb = 0;
+      if (idx <= hi_prot) {  // protected this tick: rewrite goes to the other bank
+        const uint32_t cur = (uint32_t)(*rp >> 63);
+        const bool in_rw = idx >= rw_lo && idx <= rw_hi;
+        tb = in_rw ? cur : cur ^ 1u;
+      }
+      sm |= (w >> 63) << e;
+      hm |= ((w >> 62) & 1ull) << e;
+      tm |= ((w >> 61) & 1ull) << e;
+      dm |= (uint64_t)tb << e;
+      *rp = (w & ~BANK_BIT) | ((uint64_t)tb << 63);
+    }
+    const uint64_t lo_w = base + e0, hi_w = umin64(base + n - 1, hi_prot);
+    if (lo_w <= hi_w) {
+      if (rw_lo > rw_hi) {
+        rw_lo = lo_w;
+        rw_hi = hi_w;
+      } else {
+        for (uint64_t i = hi_w + 1; i < rw_lo; ++i) *tr_at(i) ^= BANK_BIT;  // gap below the hull
+        rw_lo = umin64(rw_lo, lo_w);
+        rw_hi = umax64(rw_hi, hi_w);
+      }
+    }
+    if (nj < p.J) {
+      const uint64_t n64 = p.nrep, JN = (uint64_t)p.J * n64;
+      uint64_t* j64 = p.job64 + (uint64_t)nj * n64 + q;
+      j64[J_FIRST * JN] = base;
+      j64[J_DMASK * JN] = dm;
+      j64[J_SMASK * JN] = sm;
+      j64[J_HMASK * JN] = hm;
+      j64[J_TMASK * JN] = tm;
+      uint32_t* j32 = p.job32 + (uint64_t)nj * n64 + q;
+      j32[J_META * JN] = n | (e0 << 8) | (kind << 16);
+      j32[J_SRC * JN] = src;
+      nj++;
+    }
+  }
+
+  // raft.appendEntries (leader side): n entries at term, from slab (or a len-0 no-op)
+  RG_FN bool append_local(uint32_t n, int slab_id) {
+    if (last + n > cap_base + p.L) return false;
+    const bool pay = slab_id >= 0 && p.P;
+    write_entries(last + 1, 0, n, pay ? SRC_SLAB : SRC_NONE, pay ? (uint32_t)slab_id : 0, nullptr,
+                  term | (pay ? PAY_BIT : 0));
+    last += n;
+    remote_try_update(s, last);
+    if (R == 1) try_commit();
+    return true;
+  }
+  RG_FN void become_leader() {
+    role = LEADER;
+    reset(term);
+    leader = my_id();
+    if (!append_local(1, -1)) err |= ERR_RING;
+  }
+
+  // ---- replication (A.12)
+  RG_FN void send_replicate(uint32_t to) {
+    const uint32_t st = RG_GET(rt, to);
+    if (st == WAIT || st == SNAPSHOT) return;
+    const uint64_t next = RG_GET(rn, to);
+    if (next <= marker) {  // compacted: InstallSnapshot
+      if (!(active & (1u << to))) return;
+      if (snap_index == 0) {
+        err |= ERR_EMPTY_SNAP;
+        return;
+      }
+      RG_SET(rs, to, snap_index);
+      RG_SET(rt, to, (uint32_t)SNAPSHOT);
+      send(M_INSTALL_SNAPSHOT, to + 1, 0, 0, 0, snap_term, snap_index, 0, 0, 0, 0, 0);
+      return;
+    }
+    const uint32_t n = next <= last ? (uint32_t)umin64(p.E, last - next + 1) : 0;
+    const uint64_t lt = term_at(next - 1);
+    if (n > 0) {  // remote.progress
+      if (st == REPLICATE) RG_SET(rn, to, next + n);
+      else if (st == RETRY) RG_SET(rt, to, (uint32_t)WAIT);
+    }
+    const int k = send(M_REPLICATE, to + 1, 0, 0, n, lt, next - 1, committed, 0, 0, 0, 0);
+    if (k >= 0 && n > 0) {
+      uint64_t* mt = p.mt_out + ((((uint64_t)s * R + to) * p.K + (uint32_t)k) * p.E) * p.G + g;
+      for (uint32_t e = 0; e < n; ++e) mt[(uint64_t)e * p.G] = *tr_at(next + e);  // term|type|pay|bank
+      sent_hi = umax64(sent_hi, next + n - 1);
+    }
+  }
+  RG_FN void broadcast_replicate() {
+    for (uint32_t i = 0; i < R; ++i)
+      if (i != s) send_replicate(i);
+  }
+  RG_FN void broadcast_heartbeat() {
+    for (uint32_t i = 0; i < R; ++i)
+      if (i != s) send(M_HEARTBEAT, i + 1, 0, 0, 0, 0, 0, umin64(RG_GET(rm, i), committed), 0, 0, 0, 0);
+  }
+
+  // ---- follower side (A.9)
+  RG_FN void handle_replicate(uint64_t w0, uint64_t log_term, uint64_t li, uint64_t mcommit, uint32_t from,
+                                   uint32_t src, uint32_t k) {
+    if (li < committed) {
+      send_simple(M_REPLICATE_RESP, from, 0, committed);
+      return;
+    }
+    const uint32_t n = (uint32_t)(w0 >> 32);
+    if (term_at(li) == log_term) {
+      const uint64_t* mt = p.mt_in + ((((uint64_t)src * R + s) * p.K + k) * p.E) * p.G + g;
+      uint32_t k0 = n;
+      for (uint32_t e = 0; e < n; ++e) {  // entryLog.getConflictIndex
+        if (term_at(li + 1 + e) != (mt[(uint64_t)e * p.G] & TERM_MASK)) {
+          k0 = e;
+          break;
+        }
+      }
+      const uint64_t last_new = li + n;
+      if (k0 < n) {
+        const uint64_t ci = li + 1 + k0;
+        if (ci > committed && last_new > cap_base + p.L) {
+          drops++;  // capacity rule: dropped, no reply
+          return;
+        }
+        if (ci <= committed) {
+          err |= ERR_CONFLICT;
+        } else {
+          write_entries(li + 1, k0, n, SRC_RING, src * p.G + g, mt, 0);
+          last = last_new;
+        }
+      }
+      commit_to(umin64(last_new, mcommit));
+      send_simple(M_REPLICATE_RESP, from, 0, last_new);
+    } else {
+      send_simple(M_REPLICATE_RESP, from, 1, li, last);
+    }
+  }
+
+  RG_FN void handle_install_snapshot(uint64_t si, uint64_t stt, uint32_t from) {
+    uint64_t li;
+    if (si <= committed) {
+      li = committed;
+    } else if (term_at(si) == stt) {
+      commit_to(si);
+      li = committed;
+    } else {  // restore
+      marker = last = committed = snap_index = si;
+      marker_term = snap_term = stt;
+      li = last;
+    }
+    send_simple(M_REPLICATE_RESP, from, 0, li);
+  }
+
+  // ---- elections (A.7, A.8)
+  RG_FN void campaign() {
+    become_candidate();
+    responded |= 1u << s;
+    granted |= 1u << s;
+    if (R == 1) {
+      become_leader();
+      return;
+    }
+    const uint64_t lt = term_at(last);
+    for (uint32_t i = 0; i < R; ++i)
+      if (i != s) send(M_REQUEST_VOTE, i + 1, term, 0, 0, lt, last, 0, 0, 0, 0, 0);
+  }
+  RG_FN void handle_node_election() {
+    if (role == LEADER) return;
+    if (committed > applied) return;  // hasConfigChangeToApply
+    campaign();
+  }
+  RG_FN void handle_request_vote(uint64_t log_term, uint64_t log_index, uint32_t from) {
+    const bool can = vote == 0 || vote == from;
+    const uint64_t lt = term_at(last);
+    const bool utd = log_term > lt || (log_term == lt && log_index >= last);
+    uint32_t rej = 1;
+    if (can && utd) {
+      etick = 0;
+      vote = from;
+      rej = 0;
+    }
+    send_simple(M_REQUEST_VOTE_RESP, from, rej);
+  }
+  RG_FN void candidate_vote_resp(uint32_t from, uint32_t reject) {
+    const uint32_t bit = 1u << (from - 1);
+    if (!(responded & bit)) {
+      responded |= bit;
+      if (!reject) granted |= bit;
+    }
+    const uint32_t gr = __builtin_popcount(granted), tot = __builtin_popcount(responded);
+    if (gr == quorum()) {
+      become_leader();
+      broadcast_replicate();
+    } else if (tot - gr == quorum()) {
+      become_follower(term, 0);
+    }
+  }
+
+  // ---- leader responses (A.10, A.11)
+  RG_FN void leader_replicate_resp(uint32_t reject, uint64_t li, uint64_t hint, uint32_t from) {
+    const uint32_t f = from - 1;
+    active |= 1u << f;
+    if (!reject) {
+      const uint32_t st0 = RG_GET(rt, f);
+      const bool paused = st0 == WAIT || st0 == SNAPSHOT;
+      if (remote_try_update(f, li)) {
+        const uint32_t st = RG_GET(rt, f);
+        const uint64_t m = RG_GET(rm, f), sn = RG_GET(rs, f);
+        if (st == RETRY) {  // respondedTo → becomeReplicate
+          RG_SET(rn, f, m + 1);
+          RG_SET(rs, f, 0ull);
+          RG_SET(rt, f, (uint32_t)REPLICATE);
+        } else if (st == SNAPSHOT && m >= sn) {  // becomeRetry from Snapshot
+          RG_SET(rn, f, umax64(m + 1, sn + 1));
+          RG_SET(rs, f, 0ull);
+          RG_SET(rt, f, (uint32_t)RETRY);
+        }
+        if (try_commit()) broadcast_replicate();
+        else if (paused) send_replicate(f);
+      }
+    } else {  // remote.decreaseTo
+      const uint32_t st = RG_GET(rt, f);
+      const uint64_t m = RG_GET(rm, f), nx = RG_GET(rn, f);
+      bool ok;
+      if (st == REPLICATE) {
+        if (li <= m) ok = false;
+        else {
+          RG_SET(rn, f, m + 1);
+          ok = true;
+        }
+      } else if (nx - 1 != li) {
+        ok = false;
+      } else {
+        if (st == WAIT) RG_SET(rt, f, (uint32_t)RETRY);
+        RG_SET(rn, f, umax64(1, umin64(li, hint + 1)));
+        ok = true;
+      }
+      if (ok) {
+        if (RG_GET(rt, f) == REPLICATE) {  // enterRetryState → becomeRetry
+          RG_SET(rn, f, m + 1);
+          RG_SET(rs, f, 0ull);
+          RG_SET(rt, f, (uint32_t)RETRY);
+        }
+        send_replicate(f);
+      }
+    }
+  }
+  RG_FN void leader_heartbeat_resp(uint32_t from) {
+    const uint32_t f = from - 1;
+    active |= 1u << f;
+    if (RG_GET(rt, f) == WAIT) RG_SET(rt, f, (uint32_t)RETRY);
+    if (RG_GET(rm, f) < last) send_replicate(f);
+  }
+  RG_FN void check_quorum() {
+    const uint32_t c = 1 + __builtin_popcount(active & ~(1u << s));
+    active = 0;
+    if (c < quorum()) become_follower(term, 0);
+  }
+
+  // ---- proposals
+  RG_FN void handle_propose(uint32_t nent, uint32_t slab_id, uint32_t hop) {
+    if (role == LEADER) {
+      if (!append_local(nent, (int)slab_id)) {
+        drops++;
+        return;
+      }
+      broadcast_replicate();
+    } else if (role == FOLLOWER && leader != 0 && hop == 0) {
+      send(M_PROPOSE, (uint32_t)leader, 0, 0, nent, 0, 0, 0, 0, 0, slab_id, hop + 1);
+    } else {
+      drops++;
+    }
+  }
+
+  // ---- timers (A.6)
+  RG_FN void tick() {
+    if (role == LEADER) {
+      etick++;
+      if (etick >= p.ET) {
+        etick = 0;
+        if (p.CQ) check_quorum();
+      }
+      htick++;
+      if (htick >= p.HT) {
+        htick = 0;
+        if (role == LEADER) broadcast_heartbeat();
+      }
+    } else {
+      etick++;
+      if (etick >= rand_to) {
+        etick = 0;
+        handle_node_election();
+      }
+    }
+  }
+
+  // ---- Handle (A.3): message k from slot src
+  RG_FN void handle(uint32_t src, uint32_t k) {
+    const uint64_t plane = (uint64_t)R * R * p.K * p.G;
+    const uint64_t* h = p.hdr_in + (((uint64_t)src * R + s) * p.K + k) * p.G + g;
+    const uint64_t w0 = h[0];
+    const uint64_t mterm = h[1 * plane];
+    const uint32_t type = (uint32_t)(w0 & 0xFF);
+    const uint32_t from = (uint32_t)(w0 >> 8) & 0xFF;
+    const bool leader_msg = type == M_REPLICATE || type == M_INSTALL_SNAPSHOT || type == M_HEARTBEAT;
+    if (mterm != 0 && mterm != term) {
+      if (type == M_REQUEST_VOTE && p.CQ && mterm > term && h[5 * plane] != from && leader != 0 && etick < p.ET)
+        return;
+      if (mterm > term) {
+        become_follower(mterm, leader_msg ? from : 0);
+      } else {
+        if (p.CQ && leader_msg) send_simple(M_NOOP, from);
+        return;
+      }
+    }
+    switch (type) {
+      case M_PROPOSE: {
+        const uint64_t w7 = h[7 * plane];
+        handle_propose((uint32_t)(w0 >> 32), (uint32_t)w7, (uint32_t)(w7 >> 32));
+        break;
+      }
+      case M_REPLICATE:
+      case M_HEARTBEAT:
+      case M_INSTALL_SNAPSHOT:
+        if (role == LEADER) break;
+        if (role == CANDIDATE) {
+          become_follower(term, from);
+        } else {
+          etick = 0;
+          leader = from;
+        }
+        if (type == M_REPLICATE) {
+          handle_replicate(w0, h[2 * plane], h[3 * plane], h[4 * plane], from, src, k);
+        } else if (type == M_HEARTBEAT) {
+          commit_to(h[4 * plane]);
+          send_simple(M_HEARTBEAT_RESP, from, 0, 0, h[5 * plane], h[6 * plane]);
+        } else {
+          handle_install_snapshot(h[3 * plane], h[2 * plane], from);
+        }
+        break;
+      case M_REPLICATE_RESP:
+        if (role == LEADER) leader_replicate_resp((uint32_t)(w0 >> 24) & 0xFF, h[3 * plane], h[5 * plane], from);
+        break;
+      case M_HEARTBEAT_RESP:
+        if (role == LEADER) leader_heartbeat_resp(from);
+        break;
+      case M_REQUEST_VOTE:
+        handle_request_vote(h[2 * plane], h[3 * plane], from);
+        break;
+      case M_REQUEST_VOTE_RESP:
+        if (role == CANDIDATE) candidate_vote_resp(from, (uint32_t)(w0 >> 24) & 0xFF);
+        break;
+      default:
+        break;
+    }
+  }
+
+  // ---- the whole step
+  RG_FN void run() {
+    for (uint32_t src = 0; src < R; ++src) {
+      if (src == s) continue;
+      const uint32_t cnt = p.cnt_in[((uint64_t)src * R + s) * p.G + g];
+      for (uint32_t k = 0; k < cnt; ++k) handle(src, k);
+    }
+    if (p.campaign && p.campaign[rid]) handle_node_election();
+    if (!(p.flags & 1u)) tick();
+    if (p.prop_target && p.prop_target[g] == s) {
+      const uint32_t n = p.prop_count[g];
+      if (n > 0) handle_propose(n, (uint32_t)(p.tick % p.nslab), 0);
+    }
+    applied = committed;  // apply, snapshot, compaction
+    if (p.SE && applied - snap_index >= p.SE) {
+      snap_index = applied;
+      snap_term = term_at(applied);
+      const uint64_t c = snap_index > p.CO ? snap_index - p.CO : 0;
+      if (c > marker) {
+        marker_term = term_at(c);
+        marker = c;
+      }
+    }
+    cap_base = marker_start;
+    store();
+  }
+
+  RG_FN void store() {
+    const uint64_t n = p.nrep;
+    uint64_t* a = p.s64_out + q;
+    a[S_TERM * n] = term; a[S_VOTE * n] = vote; a[S_LEADER * n] = leader; a[S_COMMITTED * n] = committed;
+    a[S_APPLIED * n] = applied; a[S_LAST * n] = last; a[S_MARKER * n] = marker; a[S_MARKER_TERM * n] = marker_term;
+    a[S_SNAP_INDEX * n] = snap_index; a[S_SNAP_TERM * n] = snap_term; a[S_CAP_BASE * n] = cap_base;
+    uint32_t* b = p.s32_out + q;
+    b[S_ROLE * n] = role; b[S_ETICK * n] = etick; b[S_HTICK * n] = htick; b[S_RAND_TO * n] = rand_to;
+    b[S_RNG_CTR * n] = rng_ctr; b[S_GRANTED * n] = granted; b[S_RESPONDED * n] = responded;
+    b[S_ACTIVE * n] = active; b[S_ERR * n] = err; b[S_DROPS * n] = drops;
+    sfor<0, R>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      p.rem_out[(0 * R + j) * n + q] = rm[j];
+      p.rem_out[(1 * R + j) * n + q] = rn[j];
+      p.rem_out[(2 * R + j) * n + q] = rs[j];
+      p.rst_out[j * n + q] = (uint8_t)rt[j];
+      p.cnt_out[((uint64_t)s * R + j) * p.G + g] = get8(oc, j);
+    });
+    p.jcnt[q] = nj;
+  }
+#undef RG_GET
+#undef RG_SET
+};
+
+
+}  // namespace rg

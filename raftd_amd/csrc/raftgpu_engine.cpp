@@ -1,8 +1,9 @@
 // raftgpu_engine.cpp — host runtime behind the C-ABI in include/raftgpu.h.
 //
-// Owns the device-resident replica table, builds the CRC tables, and launches
-// the tick kernel. The product path has no CPU fallback: every rg_tick runs the HIP kernel and
-// an engine cannot be created without a GPU.
+// Owns the device-resident structure-of-arrays replica table, builds the CRC
+// tables, and issues each tick as two launches on the engine's stream: control_kernel<R>
+// (Raft logic, one lane per replica) then bulk_kernel (payload + CRC). The product path has no
+// CPU fallback: an engine cannot be created without a GPU and every rg_tick runs the kernels.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -22,23 +23,30 @@ static int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
-#define HIPCHK(x)                                                                                   \
-  do {                                                                                              \
-    hipError_t _e = (x);                                                                            \
-    if (_e != hipSuccess) return fail(RG_EHIP, std::string(#x) + ": " + hipGetErrorString(_e));     \
+#define HIPCHK(x)                                                                               \
+  do {                                                                                          \
+    hipError_t _e = (x);                                                                        \
+    if (_e != hipSuccess) return fail(RG_EHIP, std::string(#x) + ": " + hipGetErrorString(_e)); \
   } while (0)
 
 struct rg_engine {
   rg_config c{};
-  uint32_t nrep = 0;
+  uint32_t nrep = 0, J = 0;
   hipStream_t own = nullptr, stream = nullptr;
-  RepState* st[2] = {nullptr, nullptr};
-  uint64_t* term_ring = nullptr;
+  uint64_t* s64[2] = {nullptr, nullptr};
+  uint32_t* s32[2] = {nullptr, nullptr};
+  uint64_t* rem[2] = {nullptr, nullptr};
+  uint8_t* rst[2] = {nullptr, nullptr};
+  uint64_t* tr = nullptr;
   uint2* info = nullptr;
   uint8_t* pay = nullptr;
-  MsgHdr* hdr[2] = {nullptr, nullptr};
+  uint64_t* hdr[2] = {nullptr, nullptr};
   uint64_t* mt[2] = {nullptr, nullptr};
   uint32_t* cnt[2] = {nullptr, nullptr};
+  uint64_t* job64 = nullptr;
+  uint32_t* job32 = nullptr;
+  uint32_t* jcnt = nullptr;
+  uint32_t* crc_err = nullptr;
   uint8_t* slabs = nullptr;
   uint32_t* crc_tab = nullptr;
   uint32_t crc_const = 0;
@@ -47,8 +55,10 @@ struct rg_engine {
   uint8_t* d_campaign = nullptr;
   uint8_t* d_isolate = nullptr;
   unsigned long long* d_sum = nullptr;
+  uint8_t* stage = nullptr;
+  uint64_t stage_bytes = 0;
   uint64_t t = 0;
-  int grid = 0;
+  int bulk_grid = 0;
   uint64_t bytes = 0;
   std::vector<void*> allocs;
   uint32_t T0[256];
@@ -86,50 +96,70 @@ template <class T>
 static int dalloc(rg_engine* e, T** p, uint64_t bytes) {
   if (bytes == 0) bytes = 16;
   hipError_t r = hipMalloc((void**)p, bytes);
-  if (r != hipSuccess) {
-    return fail(RG_ENOMEM, "hipMalloc(" + std::to_string(bytes) + " B) failed: " + hipGetErrorString(r));
-  }
+  if (r != hipSuccess) return fail(RG_ENOMEM, "hipMalloc(" + std::to_string(bytes) + " B) failed: " + hipGetErrorString(r));
   e->allocs.push_back(*p);
   e->bytes += bytes;
   return RG_OK;
 }
 
+static int stage_reserve(rg_engine* e, uint64_t bytes) {
+  if (bytes <= e->stage_bytes) return RG_OK;
+  if (e->stage) {
+    (void)hipStreamSynchronize(e->stream);
+    (void)hipFree(e->stage);
+    e->allocs.erase(std::remove(e->allocs.begin(), e->allocs.end(), (void*)e->stage), e->allocs.end());
+    e->bytes -= e->stage_bytes;
+    e->stage = nullptr;
+    e->stage_bytes = 0;
+  }
+  const uint64_t nb = std::max<uint64_t>(bytes, 1 << 20);
+  int rc = dalloc(e, &e->stage, nb);
+  if (rc == RG_OK) e->stage_bytes = nb;
+  return rc;
+}
+
 static bool pow2(uint32_t x) { return x && !(x & (x - 1)); }
 
+// The parameter block of the tick that runs next (tick e->t): reads parity t&1 state and the
+// outbox written by tick t-1, writes the other parity.
 static TickParams params(rg_engine* e) {
   TickParams p{};
   const rg_config& c = e->c;
-  p.G = c.groups;
-  p.R = c.replicas;
-  p.nrep = e->nrep;
-  p.L = c.log_capacity;
-  p.P = c.payload_bytes;
-  p.E = c.max_entries_per_msg;
-  p.K = c.max_msgs_per_pair;
-  p.nslab = c.num_slabs;
-  p.ET = c.election_rtt;
-  p.HT = c.heartbeat_rtt;
-  p.CQ = c.check_quorum;
-  p.SE = c.snapshot_entries;
-  p.CO = c.compaction_overhead;
-  p.drop_ppm = c.drop_ppm;
-  p.crc_const = e->crc_const;
+  p.G = c.groups; p.R = c.replicas; p.nrep = e->nrep; p.L = c.log_capacity; p.P = c.payload_bytes;
+  p.E = c.max_entries_per_msg; p.K = c.max_msgs_per_pair; p.nslab = c.num_slabs; p.J = e->J;
+  p.ET = c.election_rtt; p.HT = c.heartbeat_rtt; p.CQ = c.check_quorum; p.SE = c.snapshot_entries;
+  p.CO = c.compaction_overhead; p.drop_ppm = c.drop_ppm;
   p.seed = c.seed;
   p.tick = e->t;
-  p.st_in = e->st[e->t & 1];
-  p.st_out = e->st[(e->t + 1) & 1];
-  p.term_ring = e->term_ring;
-  p.info = e->info;
-  p.pay = e->pay;
-  p.hdr_in = e->hdr[(e->t + 1) & 1];
-  p.hdr_out = e->hdr[e->t & 1];
-  p.mt_in = e->mt[(e->t + 1) & 1];
-  p.mt_out = e->mt[e->t & 1];
-  p.cnt_in = e->cnt[(e->t + 1) & 1];
-  p.cnt_out = e->cnt[e->t & 1];
-  p.slabs = e->slabs;
-  p.crc_tab = e->crc_tab;
+  const int a = (int)(e->t & 1), b = a ^ 1;
+  p.s64_in = e->s64[a]; p.s64_out = e->s64[b];
+  p.s32_in = e->s32[a]; p.s32_out = e->s32[b];
+  p.rem_in = e->rem[a]; p.rem_out = e->rem[b];
+  p.rst_in = e->rst[a]; p.rst_out = e->rst[b];
+  p.tr = e->tr;
+  p.hdr_in = e->hdr[b]; p.hdr_out = e->hdr[a];
+  p.mt_in = e->mt[b]; p.mt_out = e->mt[a];
+  p.cnt_in = e->cnt[b]; p.cnt_out = e->cnt[a];
+  p.job64 = e->job64; p.job32 = e->job32; p.jcnt = e->jcnt;
   return p;
+}
+
+static BulkParams bulk_params(rg_engine* e) {
+  BulkParams b{};
+  b.G = e->c.groups; b.nrep = e->nrep; b.L = e->c.log_capacity; b.P = e->c.payload_bytes;
+  b.E = e->c.max_entries_per_msg; b.J = e->J; b.crc_const = e->crc_const;
+  b.job64 = e->job64; b.job32 = e->job32; b.jcnt = e->jcnt;
+  b.info = e->info; b.pay = e->pay; b.slabs = e->slabs; b.crc_err = e->crc_err; b.crc_tab = e->crc_tab;
+  return b;
+}
+
+static AdminParams admin(rg_engine* e) {
+  AdminParams a{};
+  a.t = params(e);
+  a.info = e->info;
+  a.pay = e->pay;
+  a.crc_err = e->crc_err;
+  return a;
 }
 
 extern "C" {
@@ -146,7 +176,7 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if (c.max_entries_per_msg < 1 || c.max_entries_per_msg > 64) return fail(RG_EINVAL, "max_entries_per_msg in 1..64");
   if (c.max_msgs_per_pair < 1 || c.max_msgs_per_pair > 16) return fail(RG_EINVAL, "max_msgs_per_pair in 1..16");
   if (c.num_slabs < 2 || c.election_rtt < 1 || c.heartbeat_rtt < 1) return fail(RG_EINVAL, "num_slabs/rtt");
-  if ((uint64_t)c.groups * c.replicas > 0xFFFFFFFFull / 2) return fail(RG_EINVAL, "too many replicas");
+  if ((uint64_t)c.groups * c.replicas > 0x7FFFFFFFull) return fail(RG_EINVAL, "too many replicas");
   int ndev = 0;
   HIPCHK(hipGetDeviceCount(&ndev));
   if (ndev <= 0 || c.device < 0 || c.device >= ndev) return fail(RG_EINVAL, "no such HIP device");
@@ -155,22 +185,30 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   rg_engine* e = new rg_engine();
   e->c = c;
   e->nrep = c.groups * c.replicas;
+  e->J = (c.replicas - 1) * c.max_msgs_per_pair + 2;  // >= appends one step can make
   const uint64_t n = e->nrep, L = c.log_capacity, P = c.payload_bytes, R = c.replicas, K = c.max_msgs_per_pair,
-                 E = c.max_entries_per_msg;
+                 E = c.max_entries_per_msg, G = c.groups, J = e->J;
   int rc = RG_OK;
   for (int b = 0; b < 2 && rc == RG_OK; ++b) {
-    rc = dalloc(e, &e->st[b], n * sizeof(RepState));
-    if (rc == RG_OK) rc = dalloc(e, &e->hdr[b], n * R * K * sizeof(MsgHdr));
-    if (rc == RG_OK) rc = dalloc(e, &e->mt[b], n * R * K * E * sizeof(uint64_t));
-    if (rc == RG_OK) rc = dalloc(e, &e->cnt[b], n * R * sizeof(uint32_t));
+    rc = dalloc(e, &e->s64[b], S64_ROWS * n * 8);
+    if (rc == RG_OK) rc = dalloc(e, &e->s32[b], S32_ROWS * n * 4);
+    if (rc == RG_OK) rc = dalloc(e, &e->rem[b], 3 * R * n * 8);
+    if (rc == RG_OK) rc = dalloc(e, &e->rst[b], R * n);
+    if (rc == RG_OK) rc = dalloc(e, &e->hdr[b], 8 * R * R * K * G * 8);
+    if (rc == RG_OK) rc = dalloc(e, &e->mt[b], R * R * K * E * G * 8);
+    if (rc == RG_OK) rc = dalloc(e, &e->cnt[b], R * R * G * 4);
   }
-  if (rc == RG_OK) rc = dalloc(e, &e->term_ring, n * L * sizeof(uint64_t));
+  if (rc == RG_OK) rc = dalloc(e, &e->tr, L * n * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->info, 2 * n * L * sizeof(uint2));
   if (rc == RG_OK) rc = dalloc(e, &e->pay, 2 * n * L * P);
-  if (rc == RG_OK) rc = dalloc(e, &e->slabs, (uint64_t)c.num_slabs * c.groups * E * P);
+  if (rc == RG_OK) rc = dalloc(e, &e->job64, J64_ROWS * J * n * 8);
+  if (rc == RG_OK) rc = dalloc(e, &e->job32, J32_ROWS * J * n * 4);
+  if (rc == RG_OK) rc = dalloc(e, &e->jcnt, n * 4);
+  if (rc == RG_OK) rc = dalloc(e, &e->crc_err, n * 4);
+  if (rc == RG_OK) rc = dalloc(e, &e->slabs, (uint64_t)c.num_slabs * G * E * P);
   if (rc == RG_OK) rc = dalloc(e, &e->crc_tab, (CRC_T_WORDS + CRC_S_WORDS) * 4);
-  if (rc == RG_OK) rc = dalloc(e, &e->d_prop_target, c.groups);
-  if (rc == RG_OK) rc = dalloc(e, &e->d_prop_count, c.groups * 4ull);
+  if (rc == RG_OK) rc = dalloc(e, &e->d_prop_target, G);
+  if (rc == RG_OK) rc = dalloc(e, &e->d_prop_count, G * 4);
   if (rc == RG_OK) rc = dalloc(e, &e->d_campaign, n);
   if (rc == RG_OK) rc = dalloc(e, &e->d_isolate, n);
   if (rc == RG_OK) rc = dalloc(e, &e->d_sum, 64);
@@ -190,8 +228,10 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
     rg_destroy(e);
     return fail(RG_EHIP, "crc table upload");
   }
-  // grid: one wave per replica, 4 waves per 256-thread workgroup
-  e->grid = (int)((n + 3) / 4);
+  int cus = 0;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device);
+  const uint64_t per_cu = (uint64_t)std::max(bulk_blocks_per_cu(c.payload_bytes), 1);
+  e->bulk_grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((n + 3) / 4, (uint64_t)std::max(cus, 1) * per_cu));
   *out = e;
   return RG_OK;
 }
@@ -225,12 +265,15 @@ int rg_bootstrap(rg_engine* e) {
   if (!e) return fail(RG_EINVAL, "null engine");
   HIPCHK(hipSetDevice(e->c.device));
   e->t = 0;
-  for (int b = 0; b < 2; ++b) {
-    HIPCHK(hipMemsetAsync(e->cnt[b], 0, (uint64_t)e->nrep * e->c.replicas * 4, e->stream));
-  }
+  const uint64_t R = e->c.replicas, G = e->c.groups;
+  for (int b = 0; b < 2; ++b) HIPCHK(hipMemsetAsync(e->cnt[b], 0, R * R * G * 4, e->stream));
+  HIPCHK(hipMemsetAsync(e->crc_err, 0, (uint64_t)e->nrep * 4, e->stream));
   TickParams p = params(e);
-  p.st_out = e->st[0];
-  HIPCHK(launch_bootstrap(p, e->stream));
+  p.s64_out = e->s64[0];
+  p.s32_out = e->s32[0];
+  p.rem_out = e->rem[0];
+  p.rst_out = e->rst[0];
+  HIPCHK(launch_bootstrap(p, e->info, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   return RG_OK;
 }
@@ -274,7 +317,8 @@ static int tick_impl(rg_engine* e, const rg_tick_input* in, bool device_ptrs) {
       }
     }
   }
-  HIPCHK(launch_tick(p, e->stream, e->grid));
+  HIPCHK(launch_control(p, e->stream));
+  HIPCHK(launch_bulk(bulk_params(e), e->stream, e->bulk_grid));
   e->t++;
   if (!device_ptrs && in) HIPCHK(hipStreamSynchronize(e->stream));  // host buffers may be reused
   return RG_OK;
@@ -290,81 +334,50 @@ int rg_tick_device(rg_engine* e, const rg_tick_input* in) {
   return tick_impl(e, in, true);
 }
 
-static void to_view(const RepState& s, rg_replica_view* v) {
-  memset(v, 0, sizeof *v);
-  v->term = s.term; v->vote = s.vote; v->leader = s.leader; v->committed = s.committed; v->applied = s.applied;
-  v->last = s.last; v->marker = s.marker; v->marker_term = s.marker_term; v->snap_index = s.snap_index;
-  v->snap_term = s.snap_term; v->cap_base = s.cap_base;
-  v->role = s.role; v->election_tick = s.etick; v->heartbeat_tick = s.htick; v->rand_timeout = s.rand_to;
-  v->rng_ctr = s.rng_ctr; v->granted = s.granted; v->responded = s.responded; v->active = s.active;
-  v->err = s.err; v->drops = s.drops;
-  for (int k = 0; k < RG_MAX_REPLICAS; ++k) {
-    v->match[k] = s.match[k];
-    v->next[k] = s.next[k];
-    v->rsnap[k] = s.rsnap[k];
-    v->rstate[k] = s.rstate[k];
-  }
-}
-
 int rg_read_replicas(rg_engine* e, uint32_t first, uint32_t n, rg_replica_view* out) {
   if (!e || !out || (uint64_t)first + n > e->nrep) return fail(RG_EINVAL, "rg_read_replicas range");
-  std::vector<RepState> buf(n);
+  if (n == 0) return RG_OK;
+  int rc = stage_reserve(e, (uint64_t)n * sizeof(rg_replica_view));
+  if (rc) return rc;
+  HIPCHK(launch_gather_replicas(admin(e), first, n, e->stage, e->stream));
+  HIPCHK(hipMemcpyAsync(out, e->stage, (uint64_t)n * sizeof(rg_replica_view), hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
-  HIPCHK(hipMemcpy(buf.data(), e->st[e->t & 1] + first, n * sizeof(RepState), hipMemcpyDeviceToHost));
-  for (uint32_t i = 0; i < n; ++i) {
-    to_view(buf[i], &out[i]);
-    for (uint32_t k = e->c.replicas; k < RG_MAX_REPLICAS; ++k) {
-      out[i].match[k] = out[i].next[k] = out[i].rsnap[k] = 0;
-      out[i].rstate[k] = 0;
-    }
-  }
   return RG_OK;
 }
 
 int rg_read_msgs(rg_engine* e, uint32_t rid, uint32_t dst, rg_msg_view* out, uint32_t cap, uint64_t* terms) {
   if (!e || rid >= e->nrep || dst >= e->c.replicas) return fail(RG_EINVAL, "rg_read_msgs range");
-  const uint32_t R = e->c.replicas, K = e->c.max_msgs_per_pair, E = e->c.max_entries_per_msg;
-  const int ob = (int)((e->t + 1) & 1);
+  const uint32_t K = e->c.max_msgs_per_pair, E = e->c.max_entries_per_msg;
+  const uint64_t hb = (uint64_t)K * 64, tb = (uint64_t)K * E * 8;
+  int rc = stage_reserve(e, hb + tb + 16);
+  if (rc) return rc;
+  uint8_t* d = e->stage;
+  HIPCHK(launch_gather_msgs(admin(e), rid, dst, d, (uint64_t*)(d + hb), (uint32_t*)(d + hb + tb), e->stream));
+  std::vector<uint8_t> h(hb + tb + 4);
+  HIPCHK(hipMemcpyAsync(h.data(), d, h.size(), hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   uint32_t n = 0;
-  HIPCHK(hipMemcpy(&n, e->cnt[ob] + (uint64_t)rid * R + dst, 4, hipMemcpyDeviceToHost));
-  uint32_t m = std::min(n, cap);
-  if (m && out) {
-    static_assert(sizeof(rg_msg_view) == sizeof(MsgHdr), "msg view");
-    HIPCHK(hipMemcpy(out, e->hdr[ob] + ((uint64_t)rid * R + dst) * K, m * sizeof(MsgHdr), hipMemcpyDeviceToHost));
-  }
-  if (m && terms) {
-    HIPCHK(hipMemcpy(terms, e->mt[ob] + ((uint64_t)rid * R + dst) * K * E, (uint64_t)m * E * 8,
-                     hipMemcpyDeviceToHost));
-    for (uint64_t i = 0; i < (uint64_t)m * E; ++i) terms[i] &= TERM_MASK;
-  }
+  memcpy(&n, h.data() + hb + tb, 4);
+  const uint32_t m = std::min(std::min(n, cap), K);
+  if (out && m) memcpy(out, h.data(), (uint64_t)m * sizeof(rg_msg_view));
+  if (terms && m) memcpy(terms, h.data() + hb, (uint64_t)m * E * 8);
   return (int)n;
 }
 
 int rg_read_entries(rg_engine* e, uint32_t rid, uint64_t first, uint32_t n, rg_entry_view* out, uint8_t* payload) {
   if (!e || rid >= e->nrep || !out) return fail(RG_EINVAL, "rg_read_entries args");
+  if (n == 0) return RG_OK;
   rg_replica_view v;
   int rc = rg_read_replicas(e, rid, 1, &v);
   if (rc) return rc;
-  if (n == 0) return RG_OK;
   if (first <= v.marker || first + n - 1 > v.last) return fail(RG_EINVAL, "index outside (marker, last]");
-  const uint64_t L = e->c.log_capacity, P = e->c.payload_bytes;
-  for (uint32_t k = 0; k < n; ++k) {
-    uint64_t idx = first + k, slot = idx & (L - 1);
-    uint64_t tw = 0;
-    uint2 inf;
-    HIPCHK(hipMemcpy(&tw, e->term_ring + (uint64_t)rid * L + slot, 8, hipMemcpyDeviceToHost));
-    uint64_t bank = tw >> 63;
-    HIPCHK(hipMemcpy(&inf, e->info + (bank * e->nrep + rid) * L + slot, 8, hipMemcpyDeviceToHost));
-    out[k].term = tw & TERM_MASK;
-    out[k].type = inf.y >> 24;
-    out[k].len = inf.y & 0xFFFFFF;
-    out[k].crc = inf.x;
-    out[k].bank = (uint32_t)bank;
-    if (payload && P && out[k].len)
-      HIPCHK(hipMemcpy(payload + (uint64_t)k * P, e->pay + ((bank * e->nrep + rid) * L + slot) * P, out[k].len,
-                       hipMemcpyDeviceToHost));
-  }
+  const uint64_t P = e->c.payload_bytes, vb = (uint64_t)n * sizeof(rg_entry_view), pb = payload ? (uint64_t)n * P : 0;
+  rc = stage_reserve(e, vb + pb + 16);
+  if (rc) return rc;
+  HIPCHK(launch_gather_entries(admin(e), rid, first, n, e->stage, payload ? e->stage + vb : nullptr, e->stream));
+  HIPCHK(hipMemcpyAsync(out, e->stage, vb, hipMemcpyDeviceToHost, e->stream));
+  if (payload && pb) HIPCHK(hipMemcpyAsync(payload, e->stage + vb, pb, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
   return RG_OK;
 }
 
@@ -373,69 +386,53 @@ int rg_import_replica(rg_engine* e, uint32_t rid, const rg_replica_view* v, cons
   if (!e || !v || rid >= e->nrep) return fail(RG_EINVAL, "rg_import_replica args");
   const uint64_t L = e->c.log_capacity, P = e->c.payload_bytes;
   if (v->last < v->marker || v->last - v->marker > L) return fail(RG_EINVAL, "log longer than the ring");
+  const uint32_t nent = (uint32_t)(v->last - v->marker);
+  std::vector<uint64_t> words(nent);
+  std::vector<uint32_t> crcs(nent, 0);
+  for (uint32_t k = 0; k < nent; ++k) {
+    const uint32_t type = types ? types[k] : RG_ENTRY_APPLICATION;
+    const bool hp = payloads && P && type == RG_ENTRY_APPLICATION;
+    words[k] = (terms[k] & TERM_MASK) | (type ? TYPE_BIT : 0) | (hp ? PAY_BIT : 0);
+    if (hp) crcs[k] = host_crc(e, payloads + (uint64_t)k * P, P);
+  }
+  const uint64_t vb = 512, wb = (uint64_t)nent * 8, cb = (uint64_t)nent * 4, pb = payloads ? (uint64_t)nent * P : 0;
+  int rc = stage_reserve(e, vb + wb + cb + pb + 64);
+  if (rc) return rc;
+  uint8_t* d = e->stage;
   HIPCHK(hipStreamSynchronize(e->stream));
-  RepState s{};
-  s.term = v->term; s.vote = v->vote; s.leader = v->leader; s.committed = v->committed; s.applied = v->applied;
-  s.last = v->last; s.marker = v->marker; s.marker_term = v->marker_term; s.snap_index = v->snap_index;
-  s.snap_term = v->snap_term; s.cap_base = v->cap_base;
-  s.role = v->role; s.etick = v->election_tick; s.htick = v->heartbeat_tick; s.rand_to = v->rand_timeout;
-  s.rng_ctr = v->rng_ctr; s.granted = v->granted; s.responded = v->responded; s.active = v->active;
-  s.err = v->err; s.drops = v->drops;
-  for (int k = 0; k < RG_MAX_REPLICAS; ++k) {
-    s.match[k] = v->match[k];
-    s.next[k] = v->next[k];
-    s.rsnap[k] = v->rsnap[k];
-    s.rstate[k] = v->rstate[k];
-  }
-  HIPCHK(hipMemcpy(e->st[e->t & 1] + rid, &s, sizeof s, hipMemcpyHostToDevice));
-  for (uint64_t i = v->marker + 1; i <= v->last; ++i) {
-    uint64_t k = i - v->marker - 1, slot = i & (L - 1);
-    uint64_t tw = terms[k] & TERM_MASK;
-    uint32_t type = types ? types[k] : RG_ENTRY_APPLICATION;
-    uint32_t len = 0, crc = 0;
-    if (payloads && P && type == RG_ENTRY_APPLICATION) {
-      len = (uint32_t)P;
-      crc = host_crc(e, payloads + k * P, P);
-      HIPCHK(hipMemcpy(e->pay + ((uint64_t)rid * L + slot) * P, payloads + k * P, P, hipMemcpyHostToDevice));
-    }
-    uint2 inf = make_uint2(crc, (type << 24) | len);
-    HIPCHK(hipMemcpy(e->term_ring + (uint64_t)rid * L + slot, &tw, 8, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(e->info + (uint64_t)rid * L + slot, &inf, 8, hipMemcpyHostToDevice));
-  }
+  HIPCHK(hipMemcpy(d, v, sizeof *v, hipMemcpyHostToDevice));
+  if (wb) HIPCHK(hipMemcpy(d + vb, words.data(), wb, hipMemcpyHostToDevice));
+  if (cb) HIPCHK(hipMemcpy(d + vb + wb, crcs.data(), cb, hipMemcpyHostToDevice));
+  if (pb) HIPCHK(hipMemcpy(d + vb + wb + cb, payloads, pb, hipMemcpyHostToDevice));
+  HIPCHK(launch_scatter_replica(admin(e), rid, d, (const uint64_t*)(d + vb), pb ? d + vb + wb + cb : nullptr,
+                                (const uint32_t*)(d + vb + wb), nent, e->stream, e->info, e->pay));
+  HIPCHK(hipStreamSynchronize(e->stream));
   return RG_OK;
 }
 
 int rg_deliver(rg_engine* e, uint32_t rid_src, const rg_msg_view* m) {
   if (!e || !m || rid_src >= e->nrep) return fail(RG_EINVAL, "rg_deliver args");
-  const uint32_t R = e->c.replicas, K = e->c.max_msgs_per_pair, E = e->c.max_entries_per_msg;
-  const uint64_t L = e->c.log_capacity;
+  const uint32_t R = e->c.replicas;
   if (m->to < 1 || m->to > R) return fail(RG_EINVAL, "rg_deliver: bad destination");
-  const uint32_t dst = m->to - 1;
-  const int ob = (int)((e->t + 1) & 1);
-  HIPCHK(hipStreamSynchronize(e->stream));
-  uint32_t n = 0;
-  uint32_t* cp = e->cnt[ob] + (uint64_t)rid_src * R + dst;
-  HIPCHK(hipMemcpy(&n, cp, 4, hipMemcpyDeviceToHost));
-  if (n >= K) return fail(RG_EFULL, "rg_deliver: outbox slot full");
   rg_msg_view h = *m;
   if (h.from == 0) h.from = (uint8_t)(rid_src % R + 1);
   if (h.type == RG_MSG_REPLICATE && h.nent) {
-    if (h.nent > E) return fail(RG_EINVAL, "rg_deliver: too many entries");
+    if (h.nent > e->c.max_entries_per_msg) return fail(RG_EINVAL, "rg_deliver: too many entries");
     rg_replica_view v;
     int rc = rg_read_replicas(e, rid_src, 1, &v);
     if (rc) return rc;
-    if (h.log_index < v.marker || h.log_index + h.nent > v.last) return fail(RG_EINVAL, "rg_deliver: entries not in sender log");
-    std::vector<uint64_t> tv(h.nent);
-    for (uint32_t k = 0; k < h.nent; ++k) {
-      uint64_t slot = (h.log_index + 1 + k) & (L - 1);
-      HIPCHK(hipMemcpy(&tv[k], e->term_ring + (uint64_t)rid_src * L + slot, 8, hipMemcpyDeviceToHost));
-    }
-    HIPCHK(hipMemcpy(e->mt[ob] + (((uint64_t)rid_src * R + dst) * K + n) * E, tv.data(), h.nent * 8ull,
-                     hipMemcpyHostToDevice));
+    if (h.log_index < v.marker || h.log_index + h.nent > v.last)
+      return fail(RG_EINVAL, "rg_deliver: entries not in sender log");
   }
-  HIPCHK(hipMemcpy(e->hdr[ob] + ((uint64_t)rid_src * R + dst) * K + n, &h, sizeof h, hipMemcpyHostToDevice));
-  n++;
-  HIPCHK(hipMemcpy(cp, &n, 4, hipMemcpyHostToDevice));
+  int rc = stage_reserve(e, 128);
+  if (rc) return rc;
+  HIPCHK(hipStreamSynchronize(e->stream));
+  HIPCHK(hipMemcpy(e->stage, &h, sizeof h, hipMemcpyHostToDevice));
+  HIPCHK(launch_deliver(admin(e), rid_src, e->stage, (uint32_t*)(e->stage + 64), e->stream));
+  uint32_t status = 0;
+  HIPCHK(hipMemcpyAsync(&status, e->stage + 64, 4, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  if (status) return fail(RG_EFULL, "rg_deliver: outbox slot full");
   return RG_OK;
 }
 
@@ -444,25 +441,20 @@ int rg_leader(rg_engine* e, uint32_t group, uint64_t* leader_id, uint64_t* term,
   std::vector<rg_replica_view> v(e->c.replicas);
   int rc = rg_read_replicas(e, group * e->c.replicas, e->c.replicas, v.data());
   if (rc) return rc;
-  uint64_t bl = 0, bt = 0;
-  for (auto& r : v) {
-    if (r.term > bt) bt = r.term;
-    if (r.role == RG_LEADER && r.term >= bt) bl = r.leader;
-  }
-  // the leader is valid only if it holds the highest term seen in the group
-  uint64_t lt = 0;
+  uint64_t bt = 0, bl = 0;
+  for (auto& r : v) bt = std::max(bt, r.term);
   for (auto& r : v)
-    if (r.role == RG_LEADER && r.leader == bl) lt = r.term;
-  if (leader_id) *leader_id = (lt == bt) ? bl : 0;
+    if (r.role == RG_LEADER && r.term == bt) bl = r.leader;  // a leader valid at the group's highest term
+  if (leader_id) *leader_id = bl;
   if (term) *term = bt;
-  if (valid) *valid = (bl != 0 && lt == bt) ? 1 : 0;
+  if (valid) *valid = bl != 0;
   return RG_OK;
 }
 
 int rg_sum_committed(rg_engine* e, uint64_t* out) {
   if (!e || !out) return fail(RG_EINVAL, "rg_sum_committed args");
   HIPCHK(hipMemsetAsync(e->d_sum, 0, 8, e->stream));
-  HIPCHK(launch_sum_committed(e->st[e->t & 1], e->c.groups, e->c.replicas, e->d_sum, e->stream));
+  HIPCHK(launch_sum_committed(params(e), e->d_sum, e->stream));
   unsigned long long v = 0;
   HIPCHK(hipMemcpyAsync(&v, e->d_sum, 8, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
@@ -473,10 +465,8 @@ int rg_sum_committed(rg_engine* e, uint64_t* out) {
 int rg_last_tick_traffic(rg_engine* e, rg_traffic* out) {
   if (!e || !out) return fail(RG_EINVAL, "rg_last_tick_traffic args");
   if (e->t == 0) return fail(RG_EINVAL, "no tick has run");
-  // the last tick read st[(t+1)&1] and wrote st[t&1], cnt/hdr[(t+1)&1] ... viewed as a tick input:
-  TickParams p = params(e);  // p.st_in = current state, p.cnt_in/hdr_in = last tick's outbox
   HIPCHK(hipMemsetAsync(e->d_sum, 0, 64, e->stream));
-  HIPCHK(launch_traffic(p, e->st[(e->t + 1) & 1], e->d_sum, e->stream));
+  HIPCHK(launch_traffic(params(e), e->d_sum, e->stream));
   unsigned long long v[8] = {0};
   HIPCHK(hipMemcpyAsync(v, e->d_sum, 64, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));

@@ -1,5 +1,8 @@
 // raftgpu_internal.h — device-side layout shared by the kernels and the host runtime.
-// Layout rationale: DESIGN.md §2.
+// Layout rationale: DESIGN.md §2. Replicas are numbered slot-major on the device,
+// q = s·G + g (s = replica slot, g = group), so that the 64 lanes of a wave hold the same slot
+// of 64 consecutive groups: every structure-of-arrays access below is coalesced, and in steady
+// state the lanes of a wave take the same branch (same role).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -7,8 +10,11 @@
 namespace rg {
 
 constexpr uint32_t MAX_R = 8;
+// term-ring / inline-term word: term | type<<61 | has_payload<<62 | bank<<63
 constexpr uint64_t BANK_BIT = 1ull << 63;
-constexpr uint64_t TERM_MASK = BANK_BIT - 1;
+constexpr uint64_t PAY_BIT = 1ull << 62;
+constexpr uint64_t TYPE_BIT = 1ull << 61;
+constexpr uint64_t TERM_MASK = TYPE_BIT - 1;
 
 enum : uint32_t {
   M_LOCAL_TICK = 0, M_ELECTION = 1, M_LEADER_HEARTBEAT = 2, M_NOOP = 4, M_PROPOSE = 7,
@@ -20,50 +26,57 @@ enum : uint32_t { RETRY = 0, WAIT = 1, REPLICATE = 2, SNAPSHOT = 3 };
 enum : uint32_t { ENTRY_APP = 0, ENTRY_CONFIG = 1 };
 enum : uint32_t { ERR_CONFLICT = 1, ERR_BEYOND = 2, ERR_RING = 4, ERR_CRC = 8, ERR_EMPTY_SNAP = 16 };
 
-// One replica's scalar + remote state: 384 B, double-buffered across ticks.
-struct __attribute__((aligned(16))) RepState {
-  uint64_t term, vote, leader, committed, applied, last, marker, marker_term;  // 0..63
-  uint64_t snap_index, snap_term, cap_base, _r0;                               // 64..95
-  uint32_t role, etick, htick, rand_to, rng_ctr, granted, responded, active;   // 96..127
-  uint32_t err, drops, _r1[6];                                                 // 128..159
-  uint64_t match[MAX_R];                                                       // 160..223
-  uint64_t next[MAX_R];                                                        // 224..287
-  uint64_t rsnap[MAX_R];                                                       // 288..351
-  uint8_t rstate[MAX_R];                                                       // 352..359
-  uint8_t _pad[24];                                                            // 360..383
+// state field rows ([row][nrep])
+enum : uint32_t {
+  S_TERM, S_VOTE, S_LEADER, S_COMMITTED, S_APPLIED, S_LAST, S_MARKER, S_MARKER_TERM, S_SNAP_INDEX,
+  S_SNAP_TERM, S_CAP_BASE, S64_ROWS
 };
-static_assert(sizeof(RepState) == 384, "RepState layout");
-
-// 64-byte message slot = rg_msg_view.
-struct __attribute__((aligned(16))) MsgHdr {
-  uint64_t w0;  // type | from<<8 | to<<16 | reject<<24 | nent<<32
-  uint64_t term, log_term, log_index, commit, hint, hint_high;
-  uint64_t w7;  // src_a | src_b<<32
+enum : uint32_t {
+  S_ROLE, S_ETICK, S_HTICK, S_RAND_TO, S_RNG_CTR, S_GRANTED, S_RESPONDED, S_ACTIVE, S_ERR, S_DROPS, S32_ROWS
 };
-static_assert(sizeof(MsgHdr) == 64, "MsgHdr layout");
+// job rows
+enum : uint32_t { J_FIRST, J_DMASK, J_SMASK, J_HMASK, J_TMASK, J64_ROWS };
+enum : uint32_t { J_META, J_SRC, J32_ROWS };  // meta = n | e0<<8 | kind<<16
+enum : uint32_t { SRC_NONE = 0, SRC_RING = 1, SRC_SLAB = 2 };
 
 struct TickParams {
-  uint32_t G, R, nrep, L, P, E, K, nslab;
-  uint32_t ET, HT, CQ, SE, CO, drop_ppm;
-  uint32_t flags, crc_const;
+  uint32_t G, R, nrep, L, P, E, K, nslab, J;
+  uint32_t ET, HT, CQ, SE, CO, drop_ppm, flags;
   uint64_t seed, tick;
-  const RepState* st_in;
-  RepState* st_out;
-  uint64_t* term_ring;  // [nrep][L]
-  uint2* info;          // [2][nrep][L] {crc, type<<24 | len}
-  uint8_t* pay;         // [2][nrep][L][P]
-  const MsgHdr* hdr_in;
-  MsgHdr* hdr_out;          // [nrep][R][K]
-  const uint64_t* mt_in;
-  uint64_t* mt_out;         // [nrep][R][K][E]
-  const uint32_t* cnt_in;
-  uint32_t* cnt_out;        // [nrep][R]
-  const uint8_t* slabs;     // [nslab][G][E][P]
+  const uint64_t* s64_in;  // [S64_ROWS][nrep]
+  uint64_t* s64_out;
+  const uint32_t* s32_in;  // [S32_ROWS][nrep]
+  uint32_t* s32_out;
+  const uint64_t* rem_in;  // [3][R][nrep]: match, next, rsnap
+  uint64_t* rem_out;
+  const uint8_t* rst_in;   // [R][nrep]
+  uint8_t* rst_out;
+  uint64_t* tr;            // term ring [L][nrep]
+  const uint64_t* hdr_in;  // [8][R src][R dst][K][G]
+  uint64_t* hdr_out;
+  const uint64_t* mt_in;   // [R src][R dst][K][E][G]
+  uint64_t* mt_out;
+  const uint32_t* cnt_in;  // [R src][R dst][G]
+  uint32_t* cnt_out;
+  uint64_t* job64;         // [J64_ROWS][J][nrep]
+  uint32_t* job32;         // [J32_ROWS][J][nrep]
+  uint32_t* jcnt;          // [nrep]
   const uint8_t* prop_target;
   const uint32_t* prop_count;
   const uint8_t* campaign;
   const uint8_t* isolate;
-  const uint32_t* crc_tab;  // [16][256] slice tables + [6][4][256] shift tables
+};
+
+struct BulkParams {
+  uint32_t G, nrep, L, P, E, J, crc_const, _pad;
+  const uint64_t* job64;
+  const uint32_t* job32;
+  const uint32_t* jcnt;
+  uint2* info;           // [2 banks][nrep][L] {crc, type<<24 | len}
+  uint8_t* pay;          // [2 banks][nrep][L][P]
+  const uint8_t* slabs;  // [nslab][G][E][P]
+  uint32_t* crc_err;     // [nrep] sticky ERR_CRC from payload verification
+  const uint32_t* crc_tab;
 };
 
 // CRC-32/IEEE tables: T[k][b] = raw CRC of byte b followed by k zero bytes (k = 0..15);
@@ -72,14 +85,32 @@ constexpr uint32_t CRC_T_WORDS = 16 * 256;
 constexpr uint32_t CRC_S_WORDS = 6 * 4 * 256;
 
 // host-side launchers (raftgpu_kernels.hip)
-hipError_t launch_tick(const TickParams& p, hipStream_t s, int grid);
-hipError_t launch_bootstrap(const TickParams& p, hipStream_t s);
+hipError_t launch_control(const TickParams& p, hipStream_t s);
+hipError_t launch_bulk(const BulkParams& p, hipStream_t s, int grid);
+hipError_t launch_bootstrap(const TickParams& p, uint2* info, hipStream_t s);
 hipError_t launch_fill_slabs(uint8_t* slabs, uint32_t nslab, uint32_t G, uint32_t E, uint32_t P, uint64_t seed,
                              hipStream_t s);
-hipError_t launch_sum_committed(const RepState* st, uint32_t G, uint32_t R, unsigned long long* out,
-                                hipStream_t s);
-hipError_t launch_traffic(const TickParams& p, const RepState* st_prev, unsigned long long* out6, hipStream_t s);
-int tick_lds_bytes(uint32_t P);
-int tick_blocks_per_cu(uint32_t P);
+hipError_t launch_sum_committed(const TickParams& p, unsigned long long* out, hipStream_t s);
+hipError_t launch_traffic(const TickParams& p, unsigned long long* out6, hipStream_t s);
+// admin gathers / scatters behind the read / import / deliver entry points (raftgpu_admin.hip)
+struct AdminParams {
+  TickParams t;              // the parameter block the next tick would use (s64_in = current state)
+  const uint2* info;
+  const uint8_t* pay;
+  const uint32_t* crc_err;
+};
+hipError_t launch_gather_replicas(const AdminParams& a, uint32_t first_rid, uint32_t n, void* out_views,
+                                  hipStream_t s);
+hipError_t launch_gather_msgs(const AdminParams& a, uint32_t rid, uint32_t dst, void* out_hdr, uint64_t* out_terms,
+                              uint32_t* out_cnt, hipStream_t s);
+hipError_t launch_gather_entries(const AdminParams& a, uint32_t rid, uint64_t first, uint32_t n, void* out_views,
+                                 uint8_t* out_pay, hipStream_t s);
+hipError_t launch_scatter_replica(const AdminParams& a, uint32_t rid, const void* view, const uint64_t* words,
+                                  const uint8_t* pays, const uint32_t* crcs, uint32_t nent, hipStream_t s,
+                                  uint2* info, uint8_t* pay);
+hipError_t launch_deliver(const AdminParams& a, uint32_t rid_src, const void* hdr, uint32_t* status,
+                          hipStream_t s);
+int bulk_lds_bytes(uint32_t P);
+int bulk_blocks_per_cu(uint32_t P);
 
 }  // namespace rg

@@ -30,6 +30,9 @@ def make(kind: str, **cfg):
     if kind == "gpu":
         from raftd_amd.engine import Engine
         return Engine(**cfg)
+    if kind in ("ctl", "ctl-asan"):
+        from native.ctl_host import CtlHost
+        return CtlHost(asan=kind == "ctl-asan", **cfg)
     raise ValueError(kind)
 
 

@@ -1,0 +1,236 @@
+// ctl_host.cpp — TEST HARNESS: runs the engine's control step (raftgpu_control.h, the body of
+// control_kernel<R>) on the CPU over host copies of the device's structure-of-arrays layout, so
+// the exact GPU control code can be checked against the oracle and run under AddressSanitizer
+// without a GPU. The bulk (payload/CRC) kernel is not emulated: entries carry terms/types only.
+#define RG_FN inline
+#include "../../raftd_amd/csrc/raftgpu_control.h"
+#include "../../include/raftgpu.h"
+
+#include <cstring>
+#include <vector>
+
+using namespace rg;
+
+struct Host {
+  rg_config c;
+  uint32_t nrep, J;
+  std::vector<uint64_t> s64[2], rem[2], tr, hdr[2], mt[2], job64;
+  std::vector<uint32_t> s32[2], cnt[2], job32, jcnt;
+  std::vector<uint8_t> rst[2];
+  uint64_t t = 0;
+};
+
+static TickParams params(Host* h) {
+  TickParams p{};
+  const rg_config& c = h->c;
+  p.G = c.groups; p.R = c.replicas; p.nrep = h->nrep; p.L = c.log_capacity; p.P = c.payload_bytes;
+  p.E = c.max_entries_per_msg; p.K = c.max_msgs_per_pair; p.nslab = c.num_slabs; p.J = h->J;
+  p.ET = c.election_rtt; p.HT = c.heartbeat_rtt; p.CQ = c.check_quorum; p.SE = c.snapshot_entries;
+  p.CO = c.compaction_overhead; p.drop_ppm = c.drop_ppm; p.seed = c.seed; p.tick = h->t;
+  const int a = (int)(h->t & 1), b = a ^ 1;
+  p.s64_in = h->s64[a].data(); p.s64_out = h->s64[b].data();
+  p.s32_in = h->s32[a].data(); p.s32_out = h->s32[b].data();
+  p.rem_in = h->rem[a].data(); p.rem_out = h->rem[b].data();
+  p.rst_in = h->rst[a].data(); p.rst_out = h->rst[b].data();
+  p.tr = h->tr.data();
+  p.hdr_in = h->hdr[b].data(); p.hdr_out = h->hdr[a].data();
+  p.mt_in = h->mt[b].data(); p.mt_out = h->mt[a].data();
+  p.cnt_in = h->cnt[b].data(); p.cnt_out = h->cnt[a].data();
+  p.job64 = h->job64.data(); p.job32 = h->job32.data(); p.jcnt = h->jcnt.data();
+  return p;
+}
+
+static uint32_t qof(Host* h, uint32_t rid) {
+  const uint32_t g = rid / h->c.replicas, s = rid % h->c.replicas;
+  return s * h->c.groups + g;
+}
+
+extern "C" {
+
+void* ch_create(const rg_config* c) {
+  Host* h = new Host();
+  h->c = *c;
+  h->nrep = c->groups * c->replicas;
+  h->J = (c->replicas - 1) * c->max_msgs_per_pair + 2;
+  const size_t n = h->nrep, L = c->log_capacity, R = c->replicas, K = c->max_msgs_per_pair,
+               E = c->max_entries_per_msg, G = c->groups, J = h->J;
+  for (int b = 0; b < 2; ++b) {
+    h->s64[b].assign(S64_ROWS * n, 0);
+    h->s32[b].assign(S32_ROWS * n, 0);
+    h->rem[b].assign(3 * R * n, 0);
+    h->rst[b].assign(R * n, 0);
+    h->hdr[b].assign(8 * R * R * K * G, 0);
+    h->mt[b].assign(R * R * K * E * G, 0);
+    h->cnt[b].assign(R * R * G, 0);
+  }
+  h->tr.assign(L * n, 0);
+  h->job64.assign(J64_ROWS * J * n, 0);
+  h->job32.assign(J32_ROWS * J * n, 0);
+  h->jcnt.assign(n, 0);
+  return h;
+}
+
+void ch_destroy(void* hh) { delete (Host*)hh; }
+
+void ch_bootstrap(void* hh) {  // = bootstrap_kernel
+  Host* h = (Host*)hh;
+  h->t = 0;
+  const uint32_t R = h->c.replicas;
+  const uint64_t n = h->nrep;
+  for (int b = 0; b < 2; ++b) std::fill(h->cnt[b].begin(), h->cnt[b].end(), 0u);
+  for (uint32_t q = 0; q < n; ++q) {
+    const uint32_t s = q / h->c.groups, g = q - s * h->c.groups;
+    for (uint32_t f = 0; f < S64_ROWS; ++f) h->s64[0][f * n + q] = 0;
+    for (uint32_t f = 0; f < S32_ROWS; ++f) h->s32[0][f * n + q] = 0;
+    h->s64[0][S_TERM * n + q] = 1;
+    h->s64[0][S_LAST * n + q] = R;
+    h->s64[0][S_COMMITTED * n + q] = R;
+    h->s32[0][S_RNG_CTR * n + q] = 1;
+    const uint64_t key = ((uint64_t)g << 32) | ((uint64_t)s << 24) | 1ull;
+    h->s32[0][S_RAND_TO * n + q] = h->c.election_rtt + (uint32_t)(mix64(h->c.seed ^ mix64(key)) % h->c.election_rtt);
+    for (uint32_t j = 0; j < R; ++j) {
+      h->rem[0][(0 * R + j) * n + q] = 0;
+      h->rem[0][(1 * R + j) * n + q] = R + 1;
+      h->rem[0][(2 * R + j) * n + q] = 0;
+      h->rst[0][j * n + q] = RETRY;
+    }
+    for (uint32_t i = 1; i <= R; ++i) h->tr[(i & (h->c.log_capacity - 1)) * n + q] = 1ull | TYPE_BIT;
+  }
+}
+
+int ch_tick(void* hh, const rg_tick_input* in) {
+  Host* h = (Host*)hh;
+  TickParams p = params(h);
+  if (in) {
+    p.flags = in->flags;
+    p.prop_target = in->prop_target;
+    p.prop_count = in->prop_count;
+    p.campaign = in->campaign;
+    p.isolate = in->isolate;
+  }
+  for (uint32_t q = 0; q < h->nrep; ++q) {
+    switch (h->c.replicas) {
+#define RG_CASE(r) \
+  case r: {        \
+    Ctl<r> c(p, q); \
+    c.run();       \
+    break;         \
+  }
+      RG_CASE(1) RG_CASE(2) RG_CASE(3) RG_CASE(4) RG_CASE(5) RG_CASE(6) RG_CASE(7) RG_CASE(8)
+#undef RG_CASE
+      default: return -1;
+    }
+  }
+  h->t++;
+  return 0;
+}
+
+int ch_read_replica(void* hh, uint32_t rid, rg_replica_view* v) {
+  Host* h = (Host*)hh;
+  const uint32_t q = qof(h, rid);
+  const uint64_t N = h->nrep;
+  const int a = (int)(h->t & 1);
+  const uint64_t* s64 = h->s64[a].data() + q;
+  const uint32_t* s32 = h->s32[a].data() + q;
+  memset(v, 0, sizeof *v);
+  v->term = s64[S_TERM * N]; v->vote = s64[S_VOTE * N]; v->leader = s64[S_LEADER * N];
+  v->committed = s64[S_COMMITTED * N]; v->applied = s64[S_APPLIED * N]; v->last = s64[S_LAST * N];
+  v->marker = s64[S_MARKER * N]; v->marker_term = s64[S_MARKER_TERM * N]; v->snap_index = s64[S_SNAP_INDEX * N];
+  v->snap_term = s64[S_SNAP_TERM * N]; v->cap_base = s64[S_CAP_BASE * N];
+  v->role = s32[S_ROLE * N]; v->election_tick = s32[S_ETICK * N]; v->heartbeat_tick = s32[S_HTICK * N];
+  v->rand_timeout = s32[S_RAND_TO * N]; v->rng_ctr = s32[S_RNG_CTR * N]; v->granted = s32[S_GRANTED * N];
+  v->responded = s32[S_RESPONDED * N]; v->active = s32[S_ACTIVE * N]; v->err = s32[S_ERR * N];
+  v->drops = s32[S_DROPS * N];
+  const uint32_t R = h->c.replicas;
+  for (uint32_t j = 0; j < R; ++j) {
+    v->match[j] = h->rem[a][(0 * R + j) * N + q];
+    v->next[j] = h->rem[a][(1 * R + j) * N + q];
+    v->rsnap[j] = h->rem[a][(2 * R + j) * N + q];
+    v->rstate[j] = h->rst[a][j * N + q];
+  }
+  return 0;
+}
+
+int ch_read_msgs(void* hh, uint32_t rid, uint32_t dst, rg_msg_view* out, uint32_t cap, uint64_t* terms) {
+  Host* h = (Host*)hh;
+  TickParams t = params(h);
+  const uint32_t g = rid / t.R, s = rid % t.R;
+  const uint64_t plane = (uint64_t)t.R * t.R * t.K * t.G;
+  const uint32_t cnt = t.cnt_in[((uint64_t)s * t.R + dst) * t.G + g];
+  for (uint32_t k = 0; k < cnt && k < cap; ++k) {
+    const uint64_t* hp = t.hdr_in + (((uint64_t)s * t.R + dst) * t.K + k) * t.G + g;
+    uint64_t w[8];
+    for (int i = 0; i < 8; ++i) w[i] = hp[i * plane];
+    memcpy(&out[k], w, 64);
+    const uint64_t* mt = t.mt_in + ((((uint64_t)s * t.R + dst) * t.K + k) * t.E) * t.G + g;
+    const uint32_t n = (uint32_t)(w[0] >> 32);
+    for (uint32_t e = 0; e < t.E; ++e)
+      terms[(uint64_t)k * t.E + e] = ((w[0] & 0xFF) == M_REPLICATE && e < n) ? (mt[(uint64_t)e * t.G] & TERM_MASK) : 0;
+  }
+  return (int)cnt;
+}
+
+// term-ring words (term | type<<61 | pay<<62 | bank<<63) of entries first..first+n-1
+int ch_read_words(void* hh, uint32_t rid, uint64_t first, uint32_t n, uint64_t* out) {
+  Host* h = (Host*)hh;
+  const uint32_t q = qof(h, rid);
+  for (uint32_t i = 0; i < n; ++i) out[i] = h->tr[((first + i) & (h->c.log_capacity - 1)) * h->nrep + q];
+  return 0;
+}
+
+int ch_import(void* hh, uint32_t rid, const rg_replica_view* v, const uint64_t* terms, const uint32_t* types,
+              int with_payload) {
+  Host* h = (Host*)hh;
+  const uint32_t q = qof(h, rid);
+  const uint64_t N = h->nrep;
+  const int a = (int)(h->t & 1);
+  uint64_t* s64 = h->s64[a].data() + q;
+  uint32_t* s32 = h->s32[a].data() + q;
+  s64[S_TERM * N] = v->term; s64[S_VOTE * N] = v->vote; s64[S_LEADER * N] = v->leader;
+  s64[S_COMMITTED * N] = v->committed; s64[S_APPLIED * N] = v->applied; s64[S_LAST * N] = v->last;
+  s64[S_MARKER * N] = v->marker; s64[S_MARKER_TERM * N] = v->marker_term; s64[S_SNAP_INDEX * N] = v->snap_index;
+  s64[S_SNAP_TERM * N] = v->snap_term; s64[S_CAP_BASE * N] = v->cap_base;
+  s32[S_ROLE * N] = v->role; s32[S_ETICK * N] = v->election_tick; s32[S_HTICK * N] = v->heartbeat_tick;
+  s32[S_RAND_TO * N] = v->rand_timeout; s32[S_RNG_CTR * N] = v->rng_ctr; s32[S_GRANTED * N] = v->granted;
+  s32[S_RESPONDED * N] = v->responded; s32[S_ACTIVE * N] = v->active; s32[S_ERR * N] = v->err;
+  s32[S_DROPS * N] = v->drops;
+  const uint32_t R = h->c.replicas;
+  for (uint32_t j = 0; j < R; ++j) {
+    h->rem[a][(0 * R + j) * N + q] = v->match[j];
+    h->rem[a][(1 * R + j) * N + q] = v->next[j];
+    h->rem[a][(2 * R + j) * N + q] = v->rsnap[j];
+    h->rst[a][j * N + q] = v->rstate[j];
+  }
+  for (uint64_t i = v->marker + 1; i <= v->last; ++i) {
+    const uint64_t k = i - v->marker - 1;
+    const uint32_t ty = types ? types[k] : 0;
+    const bool hp = with_payload && h->c.payload_bytes && ty == 0;
+    h->tr[(i & (h->c.log_capacity - 1)) * N + q] = (terms[k] & TERM_MASK) | (ty ? TYPE_BIT : 0) | (hp ? PAY_BIT : 0);
+  }
+  return 0;
+}
+
+int ch_deliver(void* hh, uint32_t rid, const rg_msg_view* m) {  // = deliver_kernel
+  Host* h = (Host*)hh;
+  TickParams t = params(h);
+  const uint32_t g = rid / t.R, s = rid % t.R, q = s * t.G + g;
+  const uint32_t dst = m->to - 1;
+  uint32_t* cnt = const_cast<uint32_t*>(t.cnt_in) + ((uint64_t)s * t.R + dst) * t.G + g;
+  const uint32_t k = *cnt;
+  if (k >= t.K) return -3;
+  rg_msg_view mm = *m;
+  if (mm.from == 0) mm.from = (uint8_t)(s + 1);
+  const uint64_t plane = (uint64_t)t.R * t.R * t.K * t.G;
+  uint64_t* hp = const_cast<uint64_t*>(t.hdr_in) + (((uint64_t)s * t.R + dst) * t.K + k) * t.G + g;
+  uint64_t w[8];
+  memcpy(w, &mm, 64);
+  for (int i = 0; i < 8; ++i) hp[i * plane] = w[i];
+  if (mm.type == M_REPLICATE) {
+    uint64_t* mt = const_cast<uint64_t*>(t.mt_in) + ((((uint64_t)s * t.R + dst) * t.K + k) * t.E) * t.G + g;
+    for (uint32_t e = 0; e < mm.nent; ++e) mt[(uint64_t)e * t.G] = t.tr[((mm.log_index + 1 + e) & (t.L - 1)) * t.nrep + q];
+  }
+  *cnt = k + 1;
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,86 @@
+"""The engine's control step (raftgpu_control.h, i.e. control_kernel<R>'s body) compiled for the
+CPU by tests/native/ctl_host.cpp, checked tick by tick against the C oracle: replica state,
+every message (header + inline entry terms) and every log entry's term/type. Payload bytes and
+CRCs belong to the bulk kernel and are covered by the GPU tests. One case runs under
+AddressSanitizer + UBSan in a subprocess."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import kat_scenarios as K
+from engines import make
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def inputs(rng, G, R, emax):
+    pt = rng.integers(0, R, G).astype(np.uint8)
+    pt[rng.random(G) < 0.3] = 0xFF
+    pc = rng.integers(1, emax + 1, G).astype(np.uint32)
+    camp = (rng.random(G * R) < 0.02).astype(np.uint8)
+    iso = (rng.random(G * R) < 0.05).astype(np.uint8)
+    return pt, pc, camp, iso
+
+
+def xcheck(kind, seed, G, R, T, **cfg):
+    kw = dict(groups=G, replicas=R, payload_bytes=16, max_entries_per_msg=8, log_capacity=64,
+              snapshot_entries=20, compaction_overhead=5, drop_ppm=150000, seed=seed)
+    kw.update(cfg)
+    a, b = make(kind, **kw), make("c", **kw)
+    a.bootstrap()
+    b.bootstrap()
+    rng = np.random.default_rng(seed)
+    for t in range(T):
+        ins = inputs(rng, G, R, kw["max_entries_per_msg"])
+        a.tick(*ins)
+        b.tick(*ins)
+        for rid in range(G * R):
+            vb = b.replica(rid)
+            assert a.replica(rid) == vb, (seed, t, rid)
+            for d in range(R):
+                assert a.msgs(rid, d) == b.msgs(rid, d), (seed, t, rid, d)
+            for i in range(vb["marker"] + 1, vb["last"] + 1):
+                eb = b.entry(rid, i)
+                assert a.entry(rid, i) == dict(term=eb["term"], type=eb["type"]), (seed, t, rid, i)
+
+
+@pytest.mark.parametrize("R", [1, 2, 3, 4, 5, 7, 8])
+def test_control_step_matches_oracle(R):
+    xcheck("ctl", 10 + R, G=5, R=R, T=120)
+
+
+def test_control_step_heavy_loss():
+    xcheck("ctl", 77, G=6, R=5, T=200, drop_ppm=300000, max_msgs_per_pair=4)
+
+
+@pytest.mark.parametrize("name,fn", [
+    ("voter", lambda k: [K.run_voter(k, c) == c["reject"] for c in K.load("kat_voter.json")["cases"]]),
+    ("msgapp", lambda k: [K.run_check_msgapp(k, K.load("kat_check_msgapp.json"), c) ==
+                          dict(reject=c["reject"], resp_index=c["resp_index"], hint=c["hint"])
+                          for c in K.load("kat_check_msgapp.json")["cases"]]),
+    ("append", lambda k: [K.run_append(k, K.load("kat_append.json"), c) == c["want"]
+                          for c in K.load("kat_append.json")["cases"]]),
+    ("ctc", lambda k: [K.run_current_term_commit(k, K.load("kat_current_term_commit.json")) ==
+                       [a["want_commit"] for a in K.load("kat_current_term_commit.json")["acks"]]]),
+])
+def test_control_step_kats(name, fn):
+    assert all(fn("ctl"))
+
+
+def test_control_step_under_asan():
+    from native import ctl_host
+    ctl_host.build(asan=True)
+    pre = ":".join(subprocess.check_output(["gcc", f"-print-file-name={lib}"], text=True).strip()
+                   for lib in ("libasan.so", "libubsan.so"))
+    code = ("import sys; sys.path[:0] = [%r, %r]; import test_ctl_host as t; "
+            "t.xcheck('ctl-asan', 5, G=3, R=3, T=60); t.xcheck('ctl-asan', 6, G=2, R=5, T=60); "
+            "import kat_scenarios as K; fx = K.load('kat_check_msgapp.json'); "
+            "[K.run_check_msgapp('ctl-asan', fx, c) for c in fx['cases']]; print('ASAN-CLEAN')"
+            % (HERE, os.path.dirname(HERE)))
+    env = dict(os.environ, LD_PRELOAD=pre, ASAN_OPTIONS="detect_leaks=0:halt_on_error=1",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "ASAN-CLEAN" in r.stdout, r.stderr[-3000:]
