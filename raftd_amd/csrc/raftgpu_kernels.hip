@@ -67,7 +67,10 @@ struct Crc {
   }
 };
 
-constexpr int BULK_U = 8;  // 16-B chunks in flight per lane
+#ifndef RG_BULK_U
+#define RG_BULK_U 8
+#endif
+constexpr int BULK_U = RG_BULK_U;  // 16-B chunks in flight per lane
 
 __device__ __forceinline__ void bulk_job(const BulkParams& p, const Crc& crc, uint32_t q, uint32_t j) {
   const uint64_t n64 = p.nrep, JN = (uint64_t)p.J * n64, jq = (uint64_t)j * n64 + q;
@@ -93,23 +96,30 @@ __device__ __forceinline__ void bulk_job(const BulkParams& p, const Crc& crc, ui
   const uint32_t g = q % p.G;
   bool bad = false;
   for (uint32_t b = e0; b < n; b += epi * BULK_U) {
+    // issue phase: every payload chunk of the batch and, for followers, the sender's stored CRC
     uint4 x[BULK_U];
+    uint32_t want[BULK_U];
 #pragma unroll
     for (int u = 0; u < BULK_U; ++u) {
       const uint32_t e = b + u * epi + ei;
       x[u] = make_uint4(0, 0, 0, 0);
+      want[u] = 0;
       if (e < n && ((hm >> e) & 1ull)) {
         const uint64_t slot = (first + e) & (L - 1);
         const uint8_t* sp;
-        if (kind == SRC_RING)
-          sp = p.pay + ((((sm >> e) & 1ull) * n64 + src) * L + slot) * P + c * 16;
-        else
+        if (kind == SRC_RING) {
+          const uint64_t sb = (sm >> e) & 1ull;
+          sp = p.pay + ((sb * n64 + src) * L + slot) * P + c * 16;
+          if (c == 0) want[u] = p.info[(sb * n64 + src) * L + slot].x;
+        } else {
           sp = p.slabs + (((uint64_t)src * p.G + g) * p.E + e) * P + c * 16;
+        }
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         const u32x4 xv = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(sp));
         x[u] = make_uint4(xv.x, xv.y, xv.z, xv.w);
       }
     }
+    // consume phase: store, CRC, info, verify
 #pragma unroll
     for (int u = 0; u < BULK_U; ++u) {
       const uint32_t e = b + u * epi + ei;
@@ -120,7 +130,9 @@ __device__ __forceinline__ void bulk_job(const BulkParams& p, const Crc& crc, ui
       uint32_t v = 0;
       if (act) {
         *reinterpret_cast<uint4*>(p.pay + (((uint64_t)db * n64 + q) * L + slot) * P + c * 16) = x[u];
+#ifndef RG_BULK_NOCRC
         v = crc.raw16(x[u]);
+#endif
       }
       for (uint32_t l = 0; l < lg; ++l) {  // raw(A||B) = Z^|B|(raw A) ^ raw B
         const uint32_t d = 1u << l;
@@ -131,7 +143,7 @@ __device__ __forceinline__ void bulk_job(const BulkParams& p, const Crc& crc, ui
         const uint32_t cr = act ? (p.crc_const ^ v) : 0u;
         const uint32_t tl = ((uint32_t)((tm >> e) & 1u) << 24) | (act ? (uint32_t)P : 0u);
         p.info[((uint64_t)db * n64 + q) * L + slot] = make_uint2(cr, tl);
-        if (kind == SRC_RING && act) bad |= p.info[(((sm >> e) & 1ull) * n64 + src) * L + slot].x != cr;
+        if (kind == SRC_RING && act) bad |= want[u] != cr;
       }
     }
   }

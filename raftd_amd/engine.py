@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "libraftgpu.so")
+LIB_PATH = os.environ.get("RAFTGPU_LIB") or os.path.join(PKG, "libraftgpu.so")  # override: experiments only
 MAX_R = 8
 
 RG_OK, RG_EINVAL, RG_ENOMEM, RG_EFULL, RG_EHIP, RG_EINVARIANT = 0, -1, -2, -3, -4, -5
