@@ -112,10 +112,14 @@ typedef struct rg_tick_input {
 
 /* What the last tick moved, for the roofline numerator. Per SURVEY §8(d):
  * algorithmic_bytes = 128·replicas + 36·R·leaders + 128·msgs + (16+P)·repl_entries
- *                     + (12+P)·appended + P·leader_appended                              */
+ *                     + (12+P)·appended + P·leader_appended
+ * bulk_bytes = the payload stage's share (bulk_kernel): every appended entry reads its payload
+ * (sender ring or proposal slab) and writes payload + CRC; followers also read the sender's CRC:
+ *   (2P+8)·appended − 4·leader_appended                                                   */
 typedef struct rg_traffic {
   uint64_t replicas, leaders, msgs, repl_entries, appended, leader_appended;
   uint64_t algorithmic_bytes;
+  uint64_t bulk_bytes;
 } rg_traffic;
 
 typedef struct rg_engine rg_engine;
@@ -133,7 +137,17 @@ int rg_tick(rg_engine* e, const rg_tick_input* in);
 int rg_tick_device(rg_engine* e, const rg_tick_input* in);
 /* Launch work on this HIP stream (hipStream_t) instead of the engine's own. */
 int rg_set_stream(rg_engine* e, void* stream);
+/* Make the engine's stream wait, on the device, for every launched tick to finish (a tick's
+ * payload stage runs on a second internal stream); no host synchronisation. */
+int rg_join(rg_engine* e);
+/* rg_join, then block the host until the engine's stream is idle. */
 int rg_sync(rg_engine* e);
+/* Per-launch kernel timing with HIP events on the streams the kernels run on (measurement
+ * only; adds four event records per tick). enable=1 starts it and zeroes the totals. */
+int rg_timing(rg_engine* e, int enable);
+/* Synchronises, then returns the summed durations (ms) and launch counts since rg_timing(e, 1):
+ * index 0 = control_kernel, 1 = bulk_kernel. */
+int rg_kernel_ms(rg_engine* e, double* ms /*[2]*/, uint64_t* launches /*[2]*/);
 uint64_t rg_tick_count(const rg_engine* e);
 
 int rg_read_replicas(rg_engine* e, uint32_t first_rid, uint32_t n, rg_replica_view* out);

@@ -29,10 +29,16 @@ static int fail(int code, const std::string& msg) {
     if (_e != hipSuccess) return fail(RG_EHIP, std::string(#x) + ": " + hipGetErrorString(_e)); \
   } while (0)
 
+#define RGCHK(x)             \
+  do {                       \
+    if (int _rc = (x)) return _rc; \
+  } while (0)
+
 struct rg_engine {
   rg_config c{};
   uint32_t nrep = 0, J = 0;
-  hipStream_t own = nullptr, stream = nullptr;
+  hipStream_t own = nullptr, stream = nullptr, bulk = nullptr;
+  hipEvent_t ctl_done[2] = {nullptr, nullptr}, bulk_done[2] = {nullptr, nullptr};
   uint64_t* s64[2] = {nullptr, nullptr};
   uint32_t* s32[2] = {nullptr, nullptr};
   uint64_t* rem[2] = {nullptr, nullptr};
@@ -43,9 +49,9 @@ struct rg_engine {
   uint64_t* hdr[2] = {nullptr, nullptr};
   uint64_t* mt[2] = {nullptr, nullptr};
   uint32_t* cnt[2] = {nullptr, nullptr};
-  uint64_t* job64 = nullptr;
-  uint32_t* job32 = nullptr;
-  uint32_t* jcnt = nullptr;
+  uint64_t* job64[2] = {nullptr, nullptr};  // double-buffered: control(t+1) overlaps bulk(t)
+  uint32_t* job32[2] = {nullptr, nullptr};
+  uint32_t* jcnt[2] = {nullptr, nullptr};
   uint32_t* crc_err = nullptr;
   uint8_t* slabs = nullptr;
   uint32_t* crc_tab = nullptr;
@@ -59,8 +65,14 @@ struct rg_engine {
   uint64_t stage_bytes = 0;
   uint64_t t = 0;
   int bulk_grid = 0;
+  uint32_t bulk_tile = 1;
   uint64_t bytes = 0;
   std::vector<void*> allocs;
+  // per-launch event timing (rg_timing): [control start, control end, bulk start, bulk end] per tick
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pool, ev_live;
+  double kms[2] = {0, 0};
+  uint64_t klaunch[2] = {0, 0};
   uint32_t T0[256];
 };
 
@@ -140,15 +152,16 @@ static TickParams params(rg_engine* e) {
   p.hdr_in = e->hdr[b]; p.hdr_out = e->hdr[a];
   p.mt_in = e->mt[b]; p.mt_out = e->mt[a];
   p.cnt_in = e->cnt[b]; p.cnt_out = e->cnt[a];
-  p.job64 = e->job64; p.job32 = e->job32; p.jcnt = e->jcnt;
+  p.job64 = e->job64[a]; p.job32 = e->job32[a]; p.jcnt = e->jcnt[a];
   return p;
 }
 
-static BulkParams bulk_params(rg_engine* e) {
+static BulkParams bulk_params(rg_engine* e) {  // for tick e->t
+  const int a = (int)(e->t & 1);
   BulkParams b{};
   b.G = e->c.groups; b.nrep = e->nrep; b.L = e->c.log_capacity; b.P = e->c.payload_bytes;
-  b.E = e->c.max_entries_per_msg; b.J = e->J; b.crc_const = e->crc_const;
-  b.job64 = e->job64; b.job32 = e->job32; b.jcnt = e->jcnt;
+  b.E = e->c.max_entries_per_msg; b.J = e->J; b.crc_const = e->crc_const; b.tile = e->bulk_tile;
+  b.job64 = e->job64[a]; b.job32 = e->job32[a]; b.jcnt = e->jcnt[a];
   b.info = e->info; b.pay = e->pay; b.slabs = e->slabs; b.crc_err = e->crc_err; b.crc_tab = e->crc_tab;
   return b;
 }
@@ -201,9 +214,11 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if (rc == RG_OK) rc = dalloc(e, &e->tr, L * n * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->info, 2 * n * L * sizeof(uint2));
   if (rc == RG_OK) rc = dalloc(e, &e->pay, 2 * n * L * P);
-  if (rc == RG_OK) rc = dalloc(e, &e->job64, J64_ROWS * J * n * 8);
-  if (rc == RG_OK) rc = dalloc(e, &e->job32, J32_ROWS * J * n * 4);
-  if (rc == RG_OK) rc = dalloc(e, &e->jcnt, n * 4);
+  for (int b = 0; b < 2 && rc == RG_OK; ++b) {
+    rc = dalloc(e, &e->job64[b], J64_ROWS * J * n * 8);
+    if (rc == RG_OK) rc = dalloc(e, &e->job32[b], J32_ROWS * J * n * 4);
+    if (rc == RG_OK) rc = dalloc(e, &e->jcnt[b], n * 4);
+  }
   if (rc == RG_OK) rc = dalloc(e, &e->crc_err, n * 4);
   if (rc == RG_OK) rc = dalloc(e, &e->slabs, (uint64_t)c.num_slabs * G * E * P);
   if (rc == RG_OK) rc = dalloc(e, &e->crc_tab, (CRC_T_WORDS + CRC_S_WORDS) * 4);
@@ -217,9 +232,17 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
     rg_destroy(e);
     return fail(rc, msg);
   }
-  if (hipStreamCreateWithFlags(&e->own, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&e->own, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&e->bulk, hipStreamNonBlocking) != hipSuccess) {
     rg_destroy(e);
     return fail(RG_EHIP, "hipStreamCreate");
+  }
+  for (int b = 0; b < 2; ++b) {
+    if (hipEventCreateWithFlags(&e->ctl_done[b], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->bulk_done[b], hipEventDisableTiming) != hipSuccess) {
+      rg_destroy(e);
+      return fail(RG_EHIP, "hipEventCreate");
+    }
   }
   e->stream = e->own;
   std::vector<uint32_t> tab;
@@ -231,7 +254,13 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   int cus = 0;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device);
   const uint64_t per_cu = (uint64_t)std::max(bulk_blocks_per_cu(c.payload_bytes), 1);
-  e->bulk_grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((n + 3) / 4, (uint64_t)std::max(cus, 1) * per_cu));
+  // bulk tiles: the largest power of two <= 64 replicas that still leaves >= 2 tiles per resident wave
+  const uint64_t waves = (uint64_t)std::max(cus, 1) * per_cu * 4;
+  uint32_t tile = 64;
+  while (tile > 1 && (n + tile - 1) / tile < 2 * waves) tile >>= 1;
+  e->bulk_tile = tile;
+  const uint64_t ntiles = (n + tile - 1) / tile;
+  e->bulk_grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((ntiles + 3) / 4, (uint64_t)std::max(cus, 1) * per_cu));
   *out = e;
   return RG_OK;
 }
@@ -242,6 +271,16 @@ void rg_destroy(rg_engine* e) {
     (void)hipStreamSynchronize(e->own);
     (void)hipStreamDestroy(e->own);
   }
+  if (e->bulk) {
+    (void)hipStreamSynchronize(e->bulk);
+    (void)hipStreamDestroy(e->bulk);
+  }
+  for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
+  for (hipEvent_t ev : e->ev_live) (void)hipEventDestroy(ev);
+  for (int b = 0; b < 2; ++b) {
+    if (e->ctl_done[b]) (void)hipEventDestroy(e->ctl_done[b]);
+    if (e->bulk_done[b]) (void)hipEventDestroy(e->bulk_done[b]);
+  }
   for (void* p : e->allocs) (void)hipFree(p);
   delete e;
 }
@@ -251,12 +290,30 @@ uint64_t rg_tick_count(const rg_engine* e) { return e ? e->t : 0; }
 
 int rg_set_stream(rg_engine* e, void* stream) {
   if (!e) return fail(RG_EINVAL, "null engine");
-  e->stream = stream ? (hipStream_t)stream : e->own;
+  hipStream_t ns = stream ? (hipStream_t)stream : e->own;
+  if (ns != e->stream && e->stream) {  // keep tick order across the switch
+    HIPCHK(hipStreamSynchronize(e->stream));
+    HIPCHK(hipStreamSynchronize(e->bulk));
+  }
+  e->stream = ns;
   return RG_OK;
+}
+
+// Make the engine's stream wait (on the device) for the last tick's bulk work.
+static int join(rg_engine* e) {
+  if (e->t > 0) HIPCHK(hipStreamWaitEvent(e->stream, e->bulk_done[(e->t - 1) & 1], 0));
+  return RG_OK;
+}
+
+int rg_join(rg_engine* e) {
+  if (!e) return fail(RG_EINVAL, "null engine");
+  return join(e);
 }
 
 int rg_sync(rg_engine* e) {
   if (!e) return fail(RG_EINVAL, "null engine");
+  int rc = join(e);
+  if (rc) return rc;
   HIPCHK(hipStreamSynchronize(e->stream));
   return RG_OK;
 }
@@ -264,6 +321,8 @@ int rg_sync(rg_engine* e) {
 int rg_bootstrap(rg_engine* e) {
   if (!e) return fail(RG_EINVAL, "null engine");
   HIPCHK(hipSetDevice(e->c.device));
+  HIPCHK(hipStreamSynchronize(e->bulk));
+  HIPCHK(hipStreamSynchronize(e->stream));
   e->t = 0;
   const uint64_t R = e->c.replicas, G = e->c.groups;
   for (int b = 0; b < 2; ++b) HIPCHK(hipMemsetAsync(e->cnt[b], 0, R * R * G * 4, e->stream));
@@ -273,6 +332,7 @@ int rg_bootstrap(rg_engine* e) {
   p.s32_out = e->s32[0];
   p.rem_out = e->rem[0];
   p.rst_out = e->rst[0];
+  for (int b = 0; b < 2; ++b) HIPCHK(hipMemsetAsync(e->jcnt[b], 0, (uint64_t)e->nrep * 4, e->stream));
   HIPCHK(launch_bootstrap(p, e->info, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   return RG_OK;
@@ -280,9 +340,58 @@ int rg_bootstrap(rg_engine* e) {
 
 int rg_fill_slabs(rg_engine* e) {
   if (!e) return fail(RG_EINVAL, "null engine");
+  if (int jrc = join(e)) return jrc;
   HIPCHK(launch_fill_slabs(e->slabs, e->c.num_slabs, e->c.groups, e->c.max_entries_per_msg, e->c.payload_bytes,
                            e->c.seed, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
+  return RG_OK;
+}
+
+static int timing_event(rg_engine* e, hipStream_t s) {
+  hipEvent_t ev;
+  if (e->ev_pool.empty()) {
+    HIPCHK(hipEventCreate(&ev));
+  } else {
+    ev = e->ev_pool.back();
+    e->ev_pool.pop_back();
+  }
+  e->ev_live.push_back(ev);
+  HIPCHK(hipEventRecord(ev, s));
+  return RG_OK;
+}
+
+static int timing_drain(rg_engine* e) {
+  HIPCHK(hipStreamSynchronize(e->stream));
+  HIPCHK(hipStreamSynchronize(e->bulk));
+  for (size_t i = 0; i + 3 < e->ev_live.size(); i += 4) {
+    for (int k = 0; k < 2; ++k) {
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, e->ev_live[i + 2 * k], e->ev_live[i + 2 * k + 1]));
+      e->kms[k] += ms;
+      e->klaunch[k]++;
+    }
+  }
+  e->ev_pool.insert(e->ev_pool.end(), e->ev_live.begin(), e->ev_live.end());
+  e->ev_live.clear();
+  return RG_OK;
+}
+
+int rg_timing(rg_engine* e, int enable) {
+  if (!e) return fail(RG_EINVAL, "null engine");
+  if (int rc = timing_drain(e)) return rc;
+  e->timing = enable != 0;
+  e->kms[0] = e->kms[1] = 0;
+  e->klaunch[0] = e->klaunch[1] = 0;
+  return RG_OK;
+}
+
+int rg_kernel_ms(rg_engine* e, double* ms, uint64_t* launches) {
+  if (!e || !ms || !launches) return fail(RG_EINVAL, "rg_kernel_ms args");
+  if (int rc = timing_drain(e)) return rc;
+  for (int k = 0; k < 2; ++k) {
+    ms[k] = e->kms[k];
+    launches[k] = e->klaunch[k];
+  }
   return RG_OK;
 }
 
@@ -317,8 +426,24 @@ static int tick_impl(rg_engine* e, const rg_tick_input* in, bool device_ptrs) {
       }
     }
   }
+  // control(t) on the engine stream once bulk(t-2) released jobs[t&1]; bulk(t) on the bulk
+  // stream after control(t). control(t+1) then overlaps bulk(t): they touch disjoint data.
+  const int a = (int)(e->t & 1);
+  if (e->t >= 2) HIPCHK(hipStreamWaitEvent(e->stream, e->bulk_done[a], 0));
+  if (e->timing) RGCHK(timing_event(e, e->stream));
   HIPCHK(launch_control(p, e->stream));
-  HIPCHK(launch_bulk(bulk_params(e), e->stream, e->bulk_grid));
+  if (e->timing) RGCHK(timing_event(e, e->stream));
+  HIPCHK(hipEventRecord(e->ctl_done[a], e->stream));
+#ifdef RG_OVERLAP  // ablation: bulk(t) on a second stream beside control(t+1)
+  hipStream_t bs = e->bulk;
+#else  // measured r01: beside bulk the latency-bound control kernel ran 8x slower, a net loss
+  hipStream_t bs = e->stream;
+#endif
+  HIPCHK(hipStreamWaitEvent(bs, e->ctl_done[a], 0));
+  if (e->timing) RGCHK(timing_event(e, bs));
+  HIPCHK(launch_bulk(bulk_params(e), bs, e->bulk_grid));
+  if (e->timing) RGCHK(timing_event(e, bs));
+  HIPCHK(hipEventRecord(e->bulk_done[a], bs));
   e->t++;
   if (!device_ptrs && in) HIPCHK(hipStreamSynchronize(e->stream));  // host buffers may be reused
   return RG_OK;
@@ -336,6 +461,7 @@ int rg_tick_device(rg_engine* e, const rg_tick_input* in) {
 
 int rg_read_replicas(rg_engine* e, uint32_t first, uint32_t n, rg_replica_view* out) {
   if (!e || !out || (uint64_t)first + n > e->nrep) return fail(RG_EINVAL, "rg_read_replicas range");
+  if (int jrc = join(e)) return jrc;
   if (n == 0) return RG_OK;
   int rc = stage_reserve(e, (uint64_t)n * sizeof(rg_replica_view));
   if (rc) return rc;
@@ -347,6 +473,7 @@ int rg_read_replicas(rg_engine* e, uint32_t first, uint32_t n, rg_replica_view* 
 
 int rg_read_msgs(rg_engine* e, uint32_t rid, uint32_t dst, rg_msg_view* out, uint32_t cap, uint64_t* terms) {
   if (!e || rid >= e->nrep || dst >= e->c.replicas) return fail(RG_EINVAL, "rg_read_msgs range");
+  if (int jrc = join(e)) return jrc;
   const uint32_t K = e->c.max_msgs_per_pair, E = e->c.max_entries_per_msg;
   const uint64_t hb = (uint64_t)K * 64, tb = (uint64_t)K * E * 8;
   int rc = stage_reserve(e, hb + tb + 16);
@@ -384,6 +511,7 @@ int rg_read_entries(rg_engine* e, uint32_t rid, uint64_t first, uint32_t n, rg_e
 int rg_import_replica(rg_engine* e, uint32_t rid, const rg_replica_view* v, const uint64_t* terms,
                       const uint32_t* types, const uint8_t* payloads) {
   if (!e || !v || rid >= e->nrep) return fail(RG_EINVAL, "rg_import_replica args");
+  if (int jrc = join(e)) return jrc;
   const uint64_t L = e->c.log_capacity, P = e->c.payload_bytes;
   if (v->last < v->marker || v->last - v->marker > L) return fail(RG_EINVAL, "log longer than the ring");
   const uint32_t nent = (uint32_t)(v->last - v->marker);
@@ -412,6 +540,7 @@ int rg_import_replica(rg_engine* e, uint32_t rid, const rg_replica_view* v, cons
 
 int rg_deliver(rg_engine* e, uint32_t rid_src, const rg_msg_view* m) {
   if (!e || !m || rid_src >= e->nrep) return fail(RG_EINVAL, "rg_deliver args");
+  if (int jrc = join(e)) return jrc;
   const uint32_t R = e->c.replicas;
   if (m->to < 1 || m->to > R) return fail(RG_EINVAL, "rg_deliver: bad destination");
   rg_msg_view h = *m;
@@ -453,6 +582,7 @@ int rg_leader(rg_engine* e, uint32_t group, uint64_t* leader_id, uint64_t* term,
 
 int rg_sum_committed(rg_engine* e, uint64_t* out) {
   if (!e || !out) return fail(RG_EINVAL, "rg_sum_committed args");
+  if (int jrc = join(e)) return jrc;
   HIPCHK(hipMemsetAsync(e->d_sum, 0, 8, e->stream));
   HIPCHK(launch_sum_committed(params(e), e->d_sum, e->stream));
   unsigned long long v = 0;
@@ -465,6 +595,7 @@ int rg_sum_committed(rg_engine* e, uint64_t* out) {
 int rg_last_tick_traffic(rg_engine* e, rg_traffic* out) {
   if (!e || !out) return fail(RG_EINVAL, "rg_last_tick_traffic args");
   if (e->t == 0) return fail(RG_EINVAL, "no tick has run");
+  if (int jrc = join(e)) return jrc;
   HIPCHK(hipMemsetAsync(e->d_sum, 0, 64, e->stream));
   HIPCHK(launch_traffic(params(e), e->d_sum, e->stream));
   unsigned long long v[8] = {0};
@@ -479,6 +610,7 @@ int rg_last_tick_traffic(rg_engine* e, rg_traffic* out) {
   out->leader_appended = v[4];
   out->algorithmic_bytes = 128ull * e->nrep + 36ull * R * v[0] + 128ull * v[1] + (16 + P) * v[2] +
                            (12 + P) * v[3] + P * v[4];
+  out->bulk_bytes = (2 * P + 8) * v[3] - 4 * v[4];
   return RG_OK;
 }
 

@@ -68,7 +68,7 @@ struct TickParams {
 };
 
 struct BulkParams {
-  uint32_t G, nrep, L, P, E, J, crc_const, _pad;
+  uint32_t G, nrep, L, P, E, J, crc_const, tile;  // tile: replicas per wave work item (1..64)
   const uint64_t* job64;
   const uint32_t* job32;
   const uint32_t* jcnt;

@@ -72,13 +72,21 @@ struct Crc {
 #endif
 constexpr int BULK_U = RG_BULK_U;  // 16-B chunks in flight per lane
 
-__device__ __forceinline__ void bulk_job(const BulkParams& p, const Crc& crc, uint32_t q, uint32_t j) {
-  const uint64_t n64 = p.nrep, JN = (uint64_t)p.J * n64, jq = (uint64_t)j * n64 + q;
-  const uint64_t first = p.job64[J_FIRST * JN + jq];
-  const uint64_t dm = p.job64[J_DMASK * JN + jq], sm = p.job64[J_SMASK * JN + jq];
-  const uint64_t hm = p.job64[J_HMASK * JN + jq], tm = p.job64[J_TMASK * JN + jq];
-  const uint32_t meta = p.job32[J_META * JN + jq], src = p.job32[J_SRC * JN + jq];
-  const uint32_t n = meta & 0xFF, e0 = (meta >> 8) & 0xFF, kind = meta >> 16;
+// One copy job, its fields uniform across the wave (SGPRs): n entries from `first`, payloads
+// from the sender's ring or a proposal slab into this replica's ring, CRC per entry.
+struct Job {
+  uint64_t first, dm, sm, hm, tm;
+  uint32_t meta, src;
+};
+
+__device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l) {
+  return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) | __builtin_amdgcn_readlane((uint32_t)v, l);
+}
+
+__device__ __forceinline__ bool bulk_job(const BulkParams& p, const Crc& crc, uint32_t q, const Job& jb) {
+  const uint64_t n64 = p.nrep;
+  const uint64_t first = jb.first, dm = jb.dm, sm = jb.sm, hm = jb.hm, tm = jb.tm;
+  const uint32_t n = jb.meta & 0xFF, e0 = (jb.meta >> 8) & 0xFF, kind = jb.meta >> 16, src = jb.src;
   const uint32_t lane = lane_id();
   const uint64_t L = p.L, P = p.P;
   if (P == 0) {
@@ -88,7 +96,7 @@ __device__ __forceinline__ void bulk_job(const BulkParams& p, const Crc& crc, ui
       const uint32_t db = (uint32_t)(dm >> e) & 1u;
       p.info[((uint64_t)db * n64 + q) * L + slot] = make_uint2(0u, (uint32_t)((tm >> e) & 1u) << 24);
     }
-    return;
+    return false;
   }
   const uint32_t lg = 31 - __clz((uint32_t)(P >> 4));
   const uint32_t nch = 1u << lg, epi = 64u >> lg;
@@ -129,7 +137,13 @@ __device__ __forceinline__ void bulk_job(const BulkParams& p, const Crc& crc, ui
       const uint32_t db = valid ? (uint32_t)(dm >> e) & 1u : 0u;
       uint32_t v = 0;
       if (act) {
-        *reinterpret_cast<uint4*>(p.pay + (((uint64_t)db * n64 + q) * L + slot) * P + c * 16) = x[u];
+        typedef uint32_t u32x4s __attribute__((ext_vector_type(4)));
+        u32x4s xs = {x[u].x, x[u].y, x[u].z, x[u].w};
+#ifdef RG_BULK_PLAIN_STORE
+        *reinterpret_cast<u32x4s*>(p.pay + (((uint64_t)db * n64 + q) * L + slot) * P + c * 16) = xs;
+#else
+        __builtin_nontemporal_store(xs, reinterpret_cast<u32x4s*>(p.pay + (((uint64_t)db * n64 + q) * L + slot) * P + c * 16));
+#endif
 #ifndef RG_BULK_NOCRC
         v = crc.raw16(x[u]);
 #endif
@@ -147,9 +161,25 @@ __device__ __forceinline__ void bulk_job(const BulkParams& p, const Crc& crc, ui
       }
     }
   }
-  if (__ballot(bad) && lane == 0) atomicOr(p.crc_err + q, ERR_CRC);
+  return bad;
 }
 
+__device__ __forceinline__ Job load_job(const BulkParams& p, uint32_t q, uint32_t j) {
+  const uint64_t JN = (uint64_t)p.J * p.nrep, jq = (uint64_t)j * p.nrep + q;
+  Job jb;
+  jb.first = p.job64[J_FIRST * JN + jq];
+  jb.dm = p.job64[J_DMASK * JN + jq];
+  jb.sm = p.job64[J_SMASK * JN + jq];
+  jb.hm = p.job64[J_HMASK * JN + jq];
+  jb.tm = p.job64[J_TMASK * JN + jq];
+  jb.meta = p.job32[J_META * JN + jq];
+  jb.src = p.job32[J_SRC * JN + jq];
+  return jb;
+}
+
+// Each wave owns tiles of p.tile consecutive replicas. Lane i of the tile loads replica i's job
+// count and first job descriptor in one round trip; the wave then runs the tile's jobs back to
+// back with the fields broadcast by readlane, so only the payload loads are on the critical path.
 __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   if (p.P) {
@@ -159,11 +189,28 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p) {
   }
   __syncthreads();
   const Crc crc{lds, lds + CRC_T_WORDS};
-  const uint32_t waves = blockDim.x >> 6;
-  const uint32_t stride = gridDim.x * waves;
-  for (uint32_t q = rfl(blockIdx.x * waves + (threadIdx.x >> 6)); q < p.nrep; q += stride) {
-    const uint32_t nj = p.jcnt[q];
-    for (uint32_t j = 0; j < nj; ++j) bulk_job(p, crc, q, j);
+  const uint32_t waves = blockDim.x >> 6, lane = lane_id();
+  const uint32_t stride = gridDim.x * waves, T = p.tile;
+  const uint32_t ntiles = (p.nrep + T - 1) / T;
+  for (uint32_t t = rfl(blockIdx.x * waves + (threadIdx.x >> 6)); t < ntiles; t += stride) {
+    const uint32_t q = t * T + lane;
+    const bool mine = lane < T && q < p.nrep;
+    const uint32_t nj = mine ? p.jcnt[q] : 0u;
+    Job j0{};
+    if (nj) j0 = load_job(p, q, 0);
+    uint64_t m = __ballot(nj != 0);
+    while (m) {
+      const uint32_t l = rfl((uint32_t)__ffsll((long long)m) - 1);
+      m &= m - 1;
+      const uint32_t qq = t * T + l, njl = __builtin_amdgcn_readlane(nj, l);
+      Job jb;
+      jb.first = rl64(j0.first, l); jb.dm = rl64(j0.dm, l); jb.sm = rl64(j0.sm, l);
+      jb.hm = rl64(j0.hm, l); jb.tm = rl64(j0.tm, l);
+      jb.meta = __builtin_amdgcn_readlane(j0.meta, l); jb.src = __builtin_amdgcn_readlane(j0.src, l);
+      bool bad = bulk_job(p, crc, qq, jb);
+      for (uint32_t j = 1; j < njl; ++j) bad |= bulk_job(p, crc, qq, load_job(p, qq, j));
+      if (__ballot(bad) && lane == 0) atomicOr(p.crc_err + qq, ERR_CRC);
+    }
   }
 }
 

@@ -65,7 +65,7 @@ class EntryView(C.Structure):
 
 class Traffic(C.Structure):
     _fields_ = [(f, C.c_uint64) for f in ("replicas", "leaders", "msgs", "repl_entries", "appended",
-                                          "leader_appended", "algorithmic_bytes")]
+                                          "leader_appended", "algorithmic_bytes", "bulk_bytes")]
 
 
 class TickInput(C.Structure):
@@ -80,7 +80,8 @@ MSG_FIELDS = [f for f, _ in MsgView._fields_]
 EXPORTS = ["rg_create", "rg_destroy", "rg_bootstrap", "rg_fill_slabs", "rg_tick", "rg_tick_device",
            "rg_set_stream", "rg_sync", "rg_tick_count", "rg_read_replicas", "rg_read_msgs",
            "rg_read_entries", "rg_import_replica", "rg_deliver", "rg_leader", "rg_sum_committed",
-           "rg_device_bytes", "rg_last_error", "rg_last_tick_traffic"]
+           "rg_device_bytes", "rg_last_error", "rg_last_tick_traffic", "rg_join",
+           "rg_timing", "rg_kernel_ms"]
 
 _lib = None
 
@@ -103,6 +104,9 @@ def load_library(path: str = LIB_PATH):
         "rg_tick_device": ([vp, C.POINTER(TickInput)], i32),
         "rg_set_stream": ([vp, vp], i32),
         "rg_sync": ([vp], i32),
+        "rg_join": ([vp], i32),
+        "rg_timing": ([vp, i32], i32),
+        "rg_kernel_ms": ([vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64)], i32),
         "rg_tick_count": ([vp], u64),
         "rg_read_replicas": ([vp, u32, u32, C.POINTER(ReplicaView)], i32),
         "rg_read_msgs": ([vp, u32, u32, C.POINTER(MsgView), u32, C.POINTER(C.c_uint64)], i32),
@@ -195,8 +199,22 @@ class Engine:
     def set_stream(self, stream_handle: int):
         self._check(self.L.rg_set_stream(self.h, C.c_void_p(stream_handle)))
 
+    def join(self):
+        self._check(self.L.rg_join(self.h))
+
     def sync(self):
         self._check(self.L.rg_sync(self.h))
+
+    def timing(self, enable: bool = True):
+        """Per-launch HIP-event timing of control_kernel / bulk_kernel (measurement only)."""
+        self._check(self.L.rg_timing(self.h, 1 if enable else 0))
+
+    def kernel_ms(self) -> dict:
+        """{'control': (total_ms, launches), 'bulk': (total_ms, launches)} since timing(True)."""
+        ms = (C.c_double * 2)()
+        n = (C.c_uint64 * 2)()
+        self._check(self.L.rg_kernel_ms(self.h, ms, n))
+        return {"control": (ms[0], n[0]), "bulk": (ms[1], n[1])}
 
     @property
     def t(self) -> int:

@@ -2,7 +2,7 @@
 into profiles/<tag>_pmc_summary.json and profiles/<tag>_kernel_stats.csv.
 
 HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE (KB) reads exactly half of a
-wide coalesced stream on gfx950, so hbm = (2*FETCH_SIZE + WRITE_SIZE) * 1024; the tick kernel's
+wide coalesced stream on gfx950, so hbm = (2*FETCH_SIZE + WRITE_SIZE) * 1024; the bulk kernel's
 payload traffic is 16 B/lane coalesced, which is the calibrated case.
 usage: python scripts/pmc_summary.py TAG KTRACE_DIR FETCH_DIR WRITE_DIR [last_n]
 """
@@ -23,7 +23,7 @@ def rows(d, pattern):
 
 
 def short(name):
-    for k in ("tick_kernel", "bootstrap_kernel", "fill_slabs_kernel", "sum_committed_kernel", "traffic_kernel"):
+    for k in ("control_kernel", "bulk_kernel", "tick_kernel", "bootstrap_kernel", "fill_slabs_kernel", "sum_committed_kernel", "traffic_kernel"):
         if k in name:
             return k
     return name[:60]
