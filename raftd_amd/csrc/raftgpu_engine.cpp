@@ -89,12 +89,19 @@ static void build_crc(rg_engine* e, std::vector<uint32_t>& tab) {
     for (uint32_t i = 0; i < n; ++i) x = Z(x);
     return x;
   };
-  tab.assign(CRC_T_WORDS + CRC_S_WORDS, 0);
+  tab.assign(CRC_TAB_WORDS, 0);
   for (uint32_t k = 0; k < 16; ++k)
     for (uint32_t b = 0; b < 256; ++b) tab[k * 256 + b] = Zn(T0[b], k);
-  for (uint32_t j = 0; j < 6; ++j)
-    for (uint32_t q = 0; q < 4; ++q)
-      for (uint32_t b = 0; b < 256; ++b) tab[CRC_T_WORDS + j * 1024 + q * 256 + b] = Zn(b << (8 * q), 16u << j);
+  for (uint32_t k = 0; k < 16; ++k)
+    for (uint32_t n = 0; n < 16; ++n) {
+      tab[CRC_T_WORDS + (k * 2 + 0) * 16 + n] = tab[k * 256 + n];
+      tab[CRC_T_WORDS + (k * 2 + 1) * 16 + n] = tab[k * 256 + (n << 4)];
+    }
+  const uint32_t nch = e->c.payload_bytes / 16;
+  for (uint32_t c = 0; c < nch; ++c)
+    for (uint32_t j = 0; j < 8; ++j)
+      for (uint32_t n = 0; n < 16; ++n)
+        tab[CRC_T_WORDS + CRC_N_WORDS + c * CRC_SH_STRIDE + j * 16 + n] = Zn(n << (4 * j), 16 * (nch - 1 - c));
   e->crc_const = Zn(0xFFFFFFFFu, e->c.payload_bytes) ^ 0xFFFFFFFFu;
 }
 
@@ -221,7 +228,7 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   }
   if (rc == RG_OK) rc = dalloc(e, &e->crc_err, n * 4);
   if (rc == RG_OK) rc = dalloc(e, &e->slabs, (uint64_t)c.num_slabs * G * E * P);
-  if (rc == RG_OK) rc = dalloc(e, &e->crc_tab, (CRC_T_WORDS + CRC_S_WORDS) * 4);
+  if (rc == RG_OK) rc = dalloc(e, &e->crc_tab, CRC_TAB_WORDS * 4);
   if (rc == RG_OK) rc = dalloc(e, &e->d_prop_target, G);
   if (rc == RG_OK) rc = dalloc(e, &e->d_prop_count, G * 4);
   if (rc == RG_OK) rc = dalloc(e, &e->d_campaign, n);

@@ -81,8 +81,16 @@ struct BulkParams {
 
 // CRC-32/IEEE tables: T[k][b] = raw CRC of byte b followed by k zero bytes (k = 0..15);
 // S[j][q][b] = the raw state (b << 8q) advanced through 16·2^j zero bytes (j = 0..5).
+// CRC-32 tables (device copy in BulkParams::crc_tab, staged into LDS by bulk_kernel):
+//   T  [16][256]  slice-by-16: T[m][b] = raw CRC of byte b followed by m zero bytes
+//   N  [16][2][16] the same split into nibbles (lo, hi) — conflict-free 16-word LDS tables
+//   SH [NCH][8][16] (row stride CRC_SH_STRIDE) per-lane shift: SH[c][j][n] = raw CRC of nibble n
+//      at bit 4j of a 32-bit CRC state followed by 16·(NCH−1−c) zero bytes, NCH = P/16
 constexpr uint32_t CRC_T_WORDS = 16 * 256;
-constexpr uint32_t CRC_S_WORDS = 6 * 4 * 256;
+constexpr uint32_t CRC_N_WORDS = 16 * 2 * 16;
+constexpr uint32_t CRC_SH_STRIDE = 8 * 16 + 2;  // +2 words: lanes' tables start on different banks
+constexpr uint32_t CRC_SH_MAX_WORDS = 64 * CRC_SH_STRIDE;
+constexpr uint32_t CRC_TAB_WORDS = CRC_T_WORDS + CRC_N_WORDS + CRC_SH_MAX_WORDS;
 
 // host-side launchers (raftgpu_kernels.hip)
 hipError_t launch_control(const TickParams& p, hipStream_t s);

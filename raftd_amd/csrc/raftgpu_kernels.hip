@@ -50,25 +50,49 @@ hipError_t launch_control(const TickParams& p, hipStream_t s) {
 
 // ================================================================== bulk kernel
 struct Crc {
-  const uint32_t* T;  // LDS [16][256]
-  const uint32_t* S;  // LDS [lg][4][256]
+  const uint32_t* T;   // LDS [16][256] byte tables
+  const uint32_t* N;   // LDS [16][2][16] nibble tables
+  const uint32_t* SH;  // LDS this lane's [8][16] shift table
+  // raw CRC contribution of a 16-byte chunk taken as the last 16 bytes of a message
   __device__ __forceinline__ uint32_t raw16(uint4 v) const {
     uint32_t r = 0;
     const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#ifdef RG_CRC_NIBBLE  // ablation: twice the lookups into conflict-free 16-word tables (VALU-bound: slower)
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd)
+#pragma unroll
+      for (int h = 0; h < 8; ++h) r ^= N[((15 - (4 * qd + (h >> 1))) * 2 + (h & 1)) * 16 + ((d[qd] >> (4 * h)) & 0xF)];
+#else
 #pragma unroll
     for (int qd = 0; qd < 4; ++qd)
 #pragma unroll
       for (int j = 0; j < 4; ++j) r ^= T[(15 - (4 * qd + j)) * 256 + ((d[qd] >> (8 * j)) & 0xFF)];
+#endif
     return r;
   }
-  __device__ __forceinline__ uint32_t shift(uint32_t v, int lvl) const {
-    const uint32_t* sh = S + lvl * 1024;
-    return sh[v & 0xFF] ^ sh[256 + ((v >> 8) & 0xFF)] ^ sh[512 + ((v >> 16) & 0xFF)] ^ sh[768 + (v >> 24)];
+  // Z^(16·(NCH−1−c))(v): move this lane's chunk contribution to the end of the entry
+  __device__ __forceinline__ uint32_t shift(uint32_t v) const {
+    uint32_t r = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r ^= SH[j * 16 + ((v >> (4 * j)) & 0xF)];
+    return r;
   }
 };
 
+// XOR over the 2^LG lanes of an entry (aligned lane groups); DPP within a row, shuffles across rows
+template <int LG>
+__device__ __forceinline__ uint32_t xor_lanes(uint32_t v) {
+  if constexpr (LG >= 1) v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
+  if constexpr (LG >= 2) v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);   // quad_perm 2,3,0,1
+  if constexpr (LG >= 3) v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  if constexpr (LG >= 4) v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+  if constexpr (LG >= 5) v ^= (uint32_t)__shfl_xor((int)v, 16, 64);
+  if constexpr (LG >= 6) v ^= (uint32_t)__shfl_xor((int)v, 32, 64);
+  return v;
+}
+
 #ifndef RG_BULK_U
-#define RG_BULK_U 8
+#define RG_BULK_U 4
 #endif
 constexpr int BULK_U = RG_BULK_U;  // 16-B chunks in flight per lane
 
@@ -81,87 +105,6 @@ struct Job {
 
 __device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l) {
   return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) | __builtin_amdgcn_readlane((uint32_t)v, l);
-}
-
-__device__ __forceinline__ bool bulk_job(const BulkParams& p, const Crc& crc, uint32_t q, const Job& jb) {
-  const uint64_t n64 = p.nrep;
-  const uint64_t first = jb.first, dm = jb.dm, sm = jb.sm, hm = jb.hm, tm = jb.tm;
-  const uint32_t n = jb.meta & 0xFF, e0 = (jb.meta >> 8) & 0xFF, kind = jb.meta >> 16, src = jb.src;
-  const uint32_t lane = lane_id();
-  const uint64_t L = p.L, P = p.P;
-  if (P == 0) {
-    const uint32_t e = lane;
-    if (e >= e0 && e < n) {
-      const uint64_t slot = (first + e) & (L - 1);
-      const uint32_t db = (uint32_t)(dm >> e) & 1u;
-      p.info[((uint64_t)db * n64 + q) * L + slot] = make_uint2(0u, (uint32_t)((tm >> e) & 1u) << 24);
-    }
-    return false;
-  }
-  const uint32_t lg = 31 - __clz((uint32_t)(P >> 4));
-  const uint32_t nch = 1u << lg, epi = 64u >> lg;
-  const uint32_t c = lane & (nch - 1), ei = lane >> lg;
-  const uint32_t g = q % p.G;
-  bool bad = false;
-  for (uint32_t b = e0; b < n; b += epi * BULK_U) {
-    // issue phase: every payload chunk of the batch and, for followers, the sender's stored CRC
-    uint4 x[BULK_U];
-    uint32_t want[BULK_U];
-#pragma unroll
-    for (int u = 0; u < BULK_U; ++u) {
-      const uint32_t e = b + u * epi + ei;
-      x[u] = make_uint4(0, 0, 0, 0);
-      want[u] = 0;
-      if (e < n && ((hm >> e) & 1ull)) {
-        const uint64_t slot = (first + e) & (L - 1);
-        const uint8_t* sp;
-        if (kind == SRC_RING) {
-          const uint64_t sb = (sm >> e) & 1ull;
-          sp = p.pay + ((sb * n64 + src) * L + slot) * P + c * 16;
-          if (c == 0) want[u] = p.info[(sb * n64 + src) * L + slot].x;
-        } else {
-          sp = p.slabs + (((uint64_t)src * p.G + g) * p.E + e) * P + c * 16;
-        }
-        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4 xv = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(sp));
-        x[u] = make_uint4(xv.x, xv.y, xv.z, xv.w);
-      }
-    }
-    // consume phase: store, CRC, info, verify
-#pragma unroll
-    for (int u = 0; u < BULK_U; ++u) {
-      const uint32_t e = b + u * epi + ei;
-      const bool valid = e < n;
-      const bool act = valid && ((hm >> e) & 1ull);
-      const uint64_t slot = (first + e) & (L - 1);
-      const uint32_t db = valid ? (uint32_t)(dm >> e) & 1u : 0u;
-      uint32_t v = 0;
-      if (act) {
-        typedef uint32_t u32x4s __attribute__((ext_vector_type(4)));
-        u32x4s xs = {x[u].x, x[u].y, x[u].z, x[u].w};
-#ifdef RG_BULK_PLAIN_STORE
-        *reinterpret_cast<u32x4s*>(p.pay + (((uint64_t)db * n64 + q) * L + slot) * P + c * 16) = xs;
-#else
-        __builtin_nontemporal_store(xs, reinterpret_cast<u32x4s*>(p.pay + (((uint64_t)db * n64 + q) * L + slot) * P + c * 16));
-#endif
-#ifndef RG_BULK_NOCRC
-        v = crc.raw16(x[u]);
-#endif
-      }
-      for (uint32_t l = 0; l < lg; ++l) {  // raw(A||B) = Z^|B|(raw A) ^ raw B
-        const uint32_t d = 1u << l;
-        const uint32_t partner = (uint32_t)__shfl_down((int)v, d, 64);
-        if ((c & ((d << 1) - 1)) == 0) v = crc.shift(v, (int)l) ^ partner;
-      }
-      if (valid && c == 0) {
-        const uint32_t cr = act ? (p.crc_const ^ v) : 0u;
-        const uint32_t tl = ((uint32_t)((tm >> e) & 1u) << 24) | (act ? (uint32_t)P : 0u);
-        p.info[((uint64_t)db * n64 + q) * L + slot] = make_uint2(cr, tl);
-        if (kind == SRC_RING && act) bad |= want[u] != cr;
-      }
-    }
-  }
-  return bad;
 }
 
 __device__ __forceinline__ Job load_job(const BulkParams& p, uint32_t q, uint32_t j) {
@@ -177,59 +120,219 @@ __device__ __forceinline__ Job load_job(const BulkParams& p, uint32_t q, uint32_
   return jb;
 }
 
-// Each wave owns tiles of p.tile consecutive replicas. Lane i of the tile loads replica i's job
-// count and first job descriptor in one round trip; the wave then runs the tile's jobs back to
-// back with the fields broadcast by readlane, so only the payload loads are on the critical path.
-__global__ void __launch_bounds__(256) bulk_kernel(BulkParams p) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  if (p.P) {
-    const uint32_t lg = 31 - __clz(p.P >> 4);
-    const uint32_t words = CRC_T_WORDS + lg * 1024;
-    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) lds[i] = p.crc_tab[i];
+// ---- software-pipelined payload stream.
+// A wave walks a flat sequence of steps over the jobs of its tiles; one step = epi entries of one
+// job, 16 B per lane. BULK_U steps are in flight at once in a register ring: slot u is consumed
+// (store, CRC, info, verify) and immediately re-issued with the step BULK_U ahead. All cursor
+// state is wave-uniform (SGPRs).
+struct Cursor {
+  uint32_t t, q, g, njl, j, n, kind, src, b;
+  uint64_t m, first, dm, sm, hm, tm;
+  bool live;
+};
+
+struct TileJobs {  // per lane: job count and first job of replica tile·T + lane
+  uint32_t nj;
+  Job j0;
+};
+
+__device__ __forceinline__ void load_tile(const BulkParams& p, Cursor& cur, TileJobs& tj) {
+  const uint32_t lane = lane_id(), q = cur.t * p.tile + lane;
+  tj.nj = (lane < p.tile && q < p.nrep) ? p.jcnt[q] : 0u;
+  tj.j0 = Job{};
+  if (tj.nj) tj.j0 = load_job(p, q, 0);
+  cur.m = __ballot(tj.nj != 0);
+  cur.j = cur.njl = 0;
+}
+
+__device__ __forceinline__ void set_job(const BulkParams& p, Cursor& cur, const Job& jb) {
+  cur.first = jb.first; cur.dm = jb.dm; cur.sm = jb.sm; cur.hm = jb.hm; cur.tm = jb.tm;
+  cur.n = jb.meta & 0xFF; cur.b = (jb.meta >> 8) & 0xFF; cur.kind = jb.meta >> 16; cur.src = jb.src;
+  cur.g = cur.q % p.G;
+}
+
+// Move the cursor one position: the replica's next job, the tile's next replica, or the next
+// tile (whose descriptors arrive in one round trip; that pass issues nothing). A job with no
+// entries left to write simply yields an empty pass. Returns false once the wave is done.
+__device__ __forceinline__ bool next_job(const BulkParams& p, Cursor& cur, TileJobs& tj, uint32_t stride,
+                                         uint32_t ntiles) {
+  if (cur.j + 1 < cur.njl) {
+    ++cur.j;
+    set_job(p, cur, load_job(p, cur.q, cur.j));
+  } else if (cur.m) {
+    const uint32_t l = rfl((uint32_t)__ffsll((long long)cur.m) - 1);
+    cur.m &= cur.m - 1;
+    cur.q = cur.t * p.tile + l;
+    cur.njl = __builtin_amdgcn_readlane(tj.nj, l);
+    cur.j = 0;
+    Job jb;
+    jb.first = rl64(tj.j0.first, l); jb.dm = rl64(tj.j0.dm, l); jb.sm = rl64(tj.j0.sm, l);
+    jb.hm = rl64(tj.j0.hm, l); jb.tm = rl64(tj.j0.tm, l);
+    jb.meta = __builtin_amdgcn_readlane(tj.j0.meta, l); jb.src = __builtin_amdgcn_readlane(tj.j0.src, l);
+    set_job(p, cur, jb);
+  } else {
+    cur.t += stride;
+    if (cur.t >= ntiles) return false;
+    load_tile(p, cur, tj);
+    cur.b = cur.n = 0;
   }
-  __syncthreads();
-  const Crc crc{lds, lds + CRC_T_WORDS};
+  return true;
+}
+
+enum : uint32_t { F_ACT = 1, F_WRITER = 2, F_TYPE = 4, F_CHECK = 8 };
+
+// metadata-only entries (P = 0): one info word per entry, no payload
+__global__ void __launch_bounds__(256) bulk_meta_kernel(BulkParams p) {
   const uint32_t waves = blockDim.x >> 6, lane = lane_id();
   const uint32_t stride = gridDim.x * waves, T = p.tile;
   const uint32_t ntiles = (p.nrep + T - 1) / T;
-  for (uint32_t t = rfl(blockIdx.x * waves + (threadIdx.x >> 6)); t < ntiles; t += stride) {
-    const uint32_t q = t * T + lane;
-    const bool mine = lane < T && q < p.nrep;
-    const uint32_t nj = mine ? p.jcnt[q] : 0u;
-    Job j0{};
-    if (nj) j0 = load_job(p, q, 0);
-    uint64_t m = __ballot(nj != 0);
-    while (m) {
-      const uint32_t l = rfl((uint32_t)__ffsll((long long)m) - 1);
-      m &= m - 1;
-      const uint32_t qq = t * T + l, njl = __builtin_amdgcn_readlane(nj, l);
-      Job jb;
-      jb.first = rl64(j0.first, l); jb.dm = rl64(j0.dm, l); jb.sm = rl64(j0.sm, l);
-      jb.hm = rl64(j0.hm, l); jb.tm = rl64(j0.tm, l);
-      jb.meta = __builtin_amdgcn_readlane(j0.meta, l); jb.src = __builtin_amdgcn_readlane(j0.src, l);
-      bool bad = bulk_job(p, crc, qq, jb);
-      for (uint32_t j = 1; j < njl; ++j) bad |= bulk_job(p, crc, qq, load_job(p, qq, j));
-      if (__ballot(bad) && lane == 0) atomicOr(p.crc_err + qq, ERR_CRC);
+  const uint64_t n64 = p.nrep, L = p.L;
+  Cursor cur{};
+  TileJobs tj{};
+  cur.t = rfl(blockIdx.x * waves + (threadIdx.x >> 6));
+  if (cur.t >= ntiles) return;
+  load_tile(p, cur, tj);
+  cur.b = cur.n = 0;
+  cur.live = next_job(p, cur, tj, stride, ntiles);
+  while (rfl((uint32_t)cur.live)) {
+    const uint32_t e = cur.b + lane;
+    if (cur.b < cur.n && e < cur.n) {
+      const uint64_t slot = (cur.first + e) & (L - 1);
+      const uint32_t db = (uint32_t)(cur.dm >> e) & 1u;
+      p.info[((uint64_t)db * n64 + cur.q) * L + slot] = make_uint2(0u, (uint32_t)((cur.tm >> e) & 1u) << 24);
     }
+    cur.b = cur.b < cur.n ? cur.b + 64 : cur.b;
+    if (cur.b >= cur.n) cur.live = next_job(p, cur, tj, stride, ntiles);
   }
 }
 
-int bulk_lds_bytes(uint32_t P) {
-  if (!P) return 16;
-  uint32_t lg = 0;
-  while ((1u << lg) < (P >> 4)) ++lg;
-  return (int)((CRC_T_WORDS + lg * 1024) * 4);
+// P = 16 << LG bytes per entry: 2^LG lanes per entry (16 B each), 64 >> LG entries per step.
+template <int LG>
+__global__ void __launch_bounds__(256) bulk_kernel(BulkParams p) {
+  constexpr uint32_t NCH = 1u << LG, EPI = 64u >> LG, P = 16u << LG;
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  for (uint32_t i = threadIdx.x; i < CRC_T_WORDS + CRC_N_WORDS + NCH * CRC_SH_STRIDE; i += blockDim.x)
+    lds[i] = p.crc_tab[i];
+  __syncthreads();
+  const uint32_t waves = blockDim.x >> 6, lane = lane_id();
+  const uint32_t stride = gridDim.x * waves, T = p.tile;
+  const uint32_t ntiles = (p.nrep + T - 1) / T;
+  const uint64_t n64 = p.nrep, L = p.L;
+  const uint32_t c = lane & (NCH - 1), ei = lane >> LG;
+  const Crc crc{lds, lds + CRC_T_WORDS, lds + CRC_T_WORDS + CRC_N_WORDS + c * CRC_SH_STRIDE};
+  Cursor cur{};
+  TileJobs tj{};
+  cur.t = rfl(blockIdx.x * waves + (threadIdx.x >> 6));
+  if (cur.t >= ntiles) return;
+  load_tile(p, cur, tj);
+  cur.b = cur.n = 0;
+  cur.live = next_job(p, cur, tj, stride, ntiles);
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  // ring slot u: payload chunk, destination (slot | bank << 31), flags, sender's CRC
+  u32x4 x[BULK_U];
+  uint32_t ds[BULK_U], fl[BULK_U], want[BULK_U];
+#pragma unroll
+  for (int u = 0; u < BULK_U; ++u) {
+    x[u] = u32x4{0, 0, 0, 0};
+    ds[u] = fl[u] = want[u] = 0;
+  }
+  // Every slot issues exactly two loads per pass (payload chunk + sender CRC word), redirected to a
+  // dummy address when the slot has no work, so the number of memory operations between a load
+  // and its use is the same on every path and the compiler's vmcnt waits keep the ring in flight.
+  // A pass never spans two jobs (the cursor moves once per pass), so the slots consumed in a pass
+  // all belong to the replica `cq` of the previous pass.
+  const uint8_t* dummy = reinterpret_cast<const uint8_t*>(p.crc_tab);
+  uint32_t vmask = 0, iq = 0;
+  do {
+    const uint32_t cq = iq;
+    iq = cur.q;
+    const uint64_t cbase = (uint64_t)cq * L;
+#pragma unroll
+    for (int u = 0; u < BULK_U; ++u) {
+      {  // consume slot u: store, CRC, info, verify (fl = 0 for an empty slot: no stores)
+        const bool act = fl[u] & F_ACT;
+        const uint64_t di = (uint64_t)(ds[u] >> 31) * n64 * L + cbase + (ds[u] & 0x7FFFFFFFu);
+        if (act) {
+#ifdef RG_BULK_PLAIN_STORE
+          *reinterpret_cast<u32x4*>(p.pay + di * P + c * 16) = x[u];
+#else
+          __builtin_nontemporal_store(x[u], reinterpret_cast<u32x4*>(p.pay + di * P + c * 16));
+#endif
+        }
+        uint32_t v = 0;
+#ifndef RG_BULK_NOCRC
+        v = crc.raw16(make_uint4(x[u].x, x[u].y, x[u].z, x[u].w));
+#endif
+        if constexpr (LG > 0) v = xor_lanes<LG>(crc.shift(v));  // raw(entry) = XOR_c Z^(after c)(raw c)
+        if (fl[u] & F_WRITER) {
+          const uint32_t cr = act ? (p.crc_const ^ v) : 0u;
+          const uint32_t tl = ((fl[u] & F_TYPE) ? (1u << 24) : 0u) | (act ? P : 0u);
+          p.info[di] = make_uint2(cr, tl);
+          if ((fl[u] & F_CHECK) && want[u] != cr) atomicOr(p.crc_err + cq, ERR_CRC);
+        }
+      }
+      {  // issue the job's next step (or an empty step) into slot u
+        const bool step = cur.live && cur.b < cur.n;
+        const uint32_t e = cur.b + ei;
+        const bool valid = step && e < cur.n;
+        const bool act = valid && ((cur.hm >> e) & 1ull);
+        const uint32_t slot = (uint32_t)((cur.first + e) & (L - 1));
+        const uint32_t db = valid ? (uint32_t)(cur.dm >> e) & 1u : 0u;
+        const bool ring = cur.kind == SRC_RING;
+        ds[u] = slot | (db << 31);
+        fl[u] = (act ? F_ACT : 0u) | ((valid && c == 0) ? F_WRITER : 0u) | (((cur.tm >> e) & 1ull) ? F_TYPE : 0u) |
+                ((ring && act) ? F_CHECK : 0u);
+        const uint64_t sb = (cur.sm >> e) & 1ull;
+        const uint64_t si = (sb * n64 + cur.src) * L + slot;
+        const uint8_t* sp = ring ? p.pay + si * P : p.slabs + (((uint64_t)cur.src * p.G + cur.g) * p.E + e) * P;
+        sp = act ? sp : dummy;
+        const uint32_t* wp = (ring && act) ? &p.info[si].x : reinterpret_cast<const uint32_t*>(dummy);
+        x[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(sp + c * 16));
+        want[u] = *wp;
+        vmask = step ? (vmask | (1u << u)) : (vmask & ~(1u << u));
+        cur.b += step ? EPI : 0u;
+      }
+    }
+    if (cur.live && cur.b >= cur.n) cur.live = next_job(p, cur, tj, stride, ntiles);
+  } while (rfl((uint32_t)(vmask != 0 || cur.live)));
+}
+
+static int lg_of(uint32_t P) {
+  int lg = 0;
+  while ((16u << lg) < P) ++lg;
+  return lg;
+}
+
+int bulk_lds_bytes(uint32_t P) { return P ? (int)((CRC_T_WORDS + CRC_N_WORDS + (P / 16) * CRC_SH_STRIDE) * 4) : 16; }
+
+template <class F>
+static hipError_t with_bulk(uint32_t P, F f) {
+  if (!P) return f(bulk_meta_kernel);
+  switch (lg_of(P)) {
+    case 0: return f(bulk_kernel<0>);
+    case 1: return f(bulk_kernel<1>);
+    case 2: return f(bulk_kernel<2>);
+    case 3: return f(bulk_kernel<3>);
+    case 4: return f(bulk_kernel<4>);
+    case 5: return f(bulk_kernel<5>);
+    case 6: return f(bulk_kernel<6>);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 int bulk_blocks_per_cu(uint32_t P) {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, bulk_kernel, 256, bulk_lds_bytes(P)) != hipSuccess) n = 4;
-  return n > 0 ? n : 1;
+  const hipError_t r = with_bulk(P, [&](auto k) {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 256, bulk_lds_bytes(P));
+  });
+  return (r == hipSuccess && n > 0) ? n : 1;
 }
 
 hipError_t launch_bulk(const BulkParams& p, hipStream_t s, int grid) {
-  hipLaunchKernelGGL(bulk_kernel, dim3(grid), dim3(256), bulk_lds_bytes(p.P), s, p);
-  return hipGetLastError();
+  return with_bulk(p.P, [&](auto k) {
+    hipLaunchKernelGGL(k, dim3(grid), dim3(256), bulk_lds_bytes(p.P), s, p);
+    return hipGetLastError();
+  });
 }
 
 // ================================================================== bootstrap (peer.go Launch + bootstrap)
