@@ -43,7 +43,7 @@ def main():
     tag, kdir, fdir, wdir = sys.argv[1:5]
     last_n = int(sys.argv[5]) if len(sys.argv) > 5 else 5
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    prof = os.path.join(root, "profiles")
+    prof = os.environ.get("PROFILES_DIR") or os.path.join(root, "profiles")
     os.makedirs(prof, exist_ok=True)
     stats = glob.glob(os.path.join(kdir, "**", "*kernel_stats.csv"), recursive=True)
     if stats:
