@@ -77,6 +77,15 @@ typedef struct rg_config {
   uint32_t drop_ppm;            /* deterministic message loss, parts per million (tests) */
   int32_t device;               /* HIP device ordinal */
   uint64_t seed;
+  /* Placement across ranks (one engine per GPU). Replica slot s of global group g
+   * lives on rank (g mod ranks + s·h(g div ranks)) mod ranks, h cycling over the units mod ranks,
+   * so with ranks >= replicas every replica of a group is on a different GPU. An engine hosts
+   * `groups` local columns; the shard set is ranks·groups global groups. Tick inputs are indexed
+   * by GLOBAL group / replica id. ranks = 0 is read as 1. */
+  uint32_t ranks;               /* 1..16 */
+  uint32_t rank;                /* this engine's rank */
+  uint32_t wire_all;            /* tests: send co-located messages through the wire too */
+  uint32_t _pad;
 } rg_config;
 
 typedef struct rg_replica_view {
@@ -102,6 +111,7 @@ typedef struct rg_entry_view {
 } rg_entry_view;
 
 typedef struct rg_tick_input {
+  /* indexed by GLOBAL group g / replica g·replicas + slot; ranks·groups groups in all */
   const uint8_t* prop_target; /* [groups] slot receiving this tick's proposal batch, 0xFF none */
   const uint32_t* prop_count; /* [groups] entries in the batch (<= max_entries_per_msg) */
   const uint8_t* campaign;    /* [groups*replicas] nonzero: Peer.Campaign before the tick */
@@ -162,11 +172,32 @@ int rg_import_replica(rg_engine* e, uint32_t rid, const rg_replica_view* v, cons
                       const uint32_t* types, const uint8_t* payloads);
 /* Enqueue a message as if `rid_src` had emitted it in the last tick (delivered next tick). */
 int rg_deliver(rg_engine* e, uint32_t rid_src, const rg_msg_view* m);
+/* NodeHost.GetLeaderID for GLOBAL group `group`, as this engine's replicas of it know it: a local
+ * replica that leads at the highest local term, else that replica's known leader. */
 int rg_leader(rg_engine* e, uint32_t group, uint64_t* leader_id, uint64_t* term, int* valid);
-/* Sum over groups of the highest committed index among the group's replicas. */
+/* Sum over groups of the highest committed index among the group's replicas (ranks > 1: over
+ * the slot-0 replicas this engine hosts, so the sum over ranks counts every group once). */
 int rg_sum_committed(rg_engine* e, uint64_t* out);
 /* Message / entry counts of the last tick and the algorithmic bytes they imply. */
 int rg_last_tick_traffic(rg_engine* e, rg_traffic* out);
+/* ---- Inter-rank exchange (ranks > 1 or wire_all): the transport plug (dragonboat ITransport's
+ * place). Messages a replica emitted in the last tick to a replica on another rank travel as one
+ * region per destination rank; the caller moves the regions (RCCL all-to-all over xGMI, or any
+ * transport) between rg_tick calls:
+ *   rg_wire_plan(e, send_bytes)        sizes of this rank's outbound regions (synchronises)
+ *   rg_wire_pack(e, buf, cap)          writes region r at offset send_bytes[0] + … + send_bytes[r-1]
+ *                                      of the device buffer buf (async, on the engine's stream)
+ *   transport                          region r of rank a → rank r; each rank learns recv_bytes
+ *   rg_wire_recv(e, buf, recv_bytes)   regions from every rank, concatenated in rank order in the
+ *                                      device buffer buf, are unpacked for the next tick (async);
+ *                                      buf must stay valid until that tick has completed on the
+ *                                      device (followers read payloads straight out of it).
+ * rg_tick fails with RG_EINVAL if a tick after the first runs without rg_wire_recv. */
+int rg_wire_plan(rg_engine* e, uint64_t* send_bytes /*[ranks]*/);
+int rg_wire_pack(rg_engine* e, void* send_buf, uint64_t send_cap);
+int rg_wire_recv(rg_engine* e, const void* recv_buf, const uint64_t* recv_bytes /*[ranks]*/);
+/* Global group and global replica id (group·replicas + slot) of local replica rid. */
+int rg_global_id(rg_engine* e, uint32_t rid, uint64_t* group, uint64_t* global_rid);
 /* Device bytes held by the engine. */
 uint64_t rg_device_bytes(const rg_engine* e);
 const char* rg_last_error(void);

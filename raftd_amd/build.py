@@ -10,8 +10,8 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libraftgpu.so")
-SOURCES = ["raftgpu_kernels.hip", "raftgpu_admin.hip", "raftgpu_engine.cpp"]
-HEADERS = ["raftgpu_internal.h", os.path.join("..", "..", "include", "raftgpu.h")]
+SOURCES = ["raftgpu_kernels.hip", "raftgpu_admin.hip", "raftgpu_wire.hip", "raftgpu_engine.cpp"]
+HEADERS = ["raftgpu_internal.h", "raftgpu_control.h", "raftgpu_wire.h", os.path.join("..", "..", "include", "raftgpu.h")]
 ARCH = os.environ.get("RAFTGPU_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 

@@ -54,7 +54,8 @@ RG_FN void sel_set(T (&a)[R], uint32_t f, V val) {
 template <int R>
 struct Ctl {
   const TickParams p;  // by value: pointer fields stay kernel-argument (global) pointers
-  uint32_t q, g, s, rid;
+  uint32_t q, g, s;    // g = local column (indexes every device array)
+  uint64_t gg, rid;    // global group and global replica id gg·R + s (RNG keys, tick inputs)
   uint64_t term, vote, leader, committed, applied, last, marker, marker_term, snap_index, snap_term, cap_base;
   uint32_t role, etick, htick, rand_to, rng_ctr, granted, responded, active, err, drops;
   uint64_t rm[R], rn[R], rs[R];  // remote match / next / snapshot index
@@ -66,7 +67,8 @@ struct Ctl {
   RG_FN Ctl(const TickParams& pp, uint32_t qq) : p(pp), q(qq) {
     s = q / p.G;
     g = q - s * p.G;
-    rid = g * R + s;
+    gg = pl_group(p.pl, s, g);
+    rid = gg * R + s;
     const uint64_t n = p.nrep;
     const uint64_t* a = p.s64_in + q;
     term = a[S_TERM * n]; vote = a[S_VOTE * n]; leader = a[S_LEADER * n]; committed = a[S_COMMITTED * n];
@@ -117,7 +119,7 @@ struct Ctl {
     return (uint32_t)(packed >> (8 * d)) & 0xFF;
   }
   RG_FN bool lost(uint32_t dst, uint32_t n) const {
-    if (p.isolate && (p.isolate[rid] || p.isolate[g * R + dst])) return true;
+    if (p.isolate && (p.isolate[rid] || p.isolate[gg * R + dst])) return true;
     if (p.drop_ppm) {
       uint64_t h = mix64(p.seed ^ mix64((p.tick << 40) ^ ((uint64_t)rid << 8) ^ dst) ^ (uint64_t)(n + 1));
       if (h % 1000000ull < p.drop_ppm) return true;
@@ -166,7 +168,7 @@ struct Ctl {
     granted = responded = 0;
     etick = htick = 0;
     rng_ctr++;
-    uint64_t key = ((uint64_t)g << 32) | ((uint64_t)s << 24) | (uint64_t)(rng_ctr & 0xFFFFFF);
+    uint64_t key = (gg << 32) | ((uint64_t)s << 24) | (uint64_t)(rng_ctr & 0xFFFFFF);
     rand_to = p.ET + (uint32_t)(mix64(p.seed ^ mix64(key)) % p.ET);
     sfor<0, R>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
@@ -222,7 +224,7 @@ struct Ctl {
   // Entry e in [e0, n) goes to index base+e. Words come from the sender's inline terms (RING:
   // mt points at entry 0, stride G) or are `word` for every entry (SLAB proposals, no-op).
   RG_FN void write_entries(uint64_t base, uint32_t e0, uint32_t n, uint32_t kind, uint32_t src,
-                                const uint64_t* mt, uint64_t word) {
+                                const uint64_t* mt, uint64_t word, uint64_t wofs = 0) {
     const uint64_t hi_prot = umax64(last_start, sent_hi);
     uint64_t dm = 0, sm = 0, hm = 0, tm = 0;
     for (uint32_t e = e0; e < n; ++e) {
@@ -252,6 +254,7 @@ struct Ctl {
         rw_hi = umax64(rw_hi, hi_w);
       }
     }
+    if (kind == SRC_WIRE) sm = wofs;  // source bank bits are meaningless off-rank
     if (nj < p.J) {
       const uint64_t n64 = p.nrep, JN = (uint64_t)p.J * n64;
       uint64_t* j64 = p.job64 + (uint64_t)nj * n64 + q;
@@ -324,15 +327,16 @@ struct Ctl {
   }
 
   // ---- follower side (A.9)
+  // remote: the message came over the wire (its inline terms are in rmt, its records at wofs)
   RG_FN void handle_replicate(uint64_t w0, uint64_t log_term, uint64_t li, uint64_t mcommit, uint32_t from,
-                                   uint32_t src, uint32_t k) {
+                                   uint32_t src, uint32_t k, bool remote, uint64_t wofs) {
     if (li < committed) {
       send_simple(M_REPLICATE_RESP, from, 0, committed);
       return;
     }
     const uint32_t n = (uint32_t)(w0 >> 32);
     if (term_at(li) == log_term) {
-      const uint64_t* mt = p.mt_in + ((((uint64_t)src * R + s) * p.K + k) * p.E) * p.G + g;
+      const uint64_t* mt = (remote ? p.rmt : p.mt_in) + ((((uint64_t)src * R + s) * p.K + k) * p.E) * p.G + g;
       uint32_t k0 = n;
       for (uint32_t e = 0; e < n; ++e) {  // entryLog.getConflictIndex
         if (term_at(li + 1 + e) != (mt[(uint64_t)e * p.G] & TERM_MASK)) {
@@ -350,7 +354,8 @@ struct Ctl {
         if (ci <= committed) {
           err |= ERR_CONFLICT;
         } else {
-          write_entries(li + 1, k0, n, SRC_RING, src * p.G + g, mt, 0);
+          if (remote) write_entries(li + 1, k0, n, SRC_WIRE, n, mt, 0, wofs);
+          else write_entries(li + 1, k0, n, SRC_RING, src * p.G + g, mt, 0);
           last = last_new;
         }
       }
@@ -519,10 +524,10 @@ struct Ctl {
     }
   }
 
-  // ---- Handle (A.3): message k from slot src
-  RG_FN void handle(uint32_t src, uint32_t k) {
+  // ---- Handle (A.3): message k from slot src (remote: it came over the wire from another rank)
+  RG_FN void handle(uint32_t src, uint32_t k, bool remote) {
     const uint64_t plane = (uint64_t)R * R * p.K * p.G;
-    const uint64_t* h = p.hdr_in + (((uint64_t)src * R + s) * p.K + k) * p.G + g;
+    const uint64_t* h = (remote ? p.rhdr : p.hdr_in) + (((uint64_t)src * R + s) * p.K + k) * p.G + g;
     const uint64_t w0 = h[0];
     const uint64_t mterm = h[1 * plane];
     const uint32_t type = (uint32_t)(w0 & 0xFF);
@@ -555,7 +560,8 @@ struct Ctl {
           leader = from;
         }
         if (type == M_REPLICATE) {
-          handle_replicate(w0, h[2 * plane], h[3 * plane], h[4 * plane], from, src, k);
+          handle_replicate(w0, h[2 * plane], h[3 * plane], h[4 * plane], from, src, k, remote,
+                           remote ? h[7 * plane] : 0);
         } else if (type == M_HEARTBEAT) {
           commit_to(h[4 * plane]);
           send_simple(M_HEARTBEAT_RESP, from, 0, 0, h[5 * plane], h[6 * plane]);
@@ -584,13 +590,14 @@ struct Ctl {
   RG_FN void run() {
     for (uint32_t src = 0; src < R; ++src) {
       if (src == s) continue;
-      const uint32_t cnt = p.cnt_in[((uint64_t)src * R + s) * p.G + g];
-      for (uint32_t k = 0; k < cnt; ++k) handle(src, k);
+      const bool remote = pl_remote(p.pl, src, s, g);
+      const uint32_t cnt = (remote ? p.rcnt : p.cnt_in)[((uint64_t)src * R + s) * p.G + g];
+      for (uint32_t k = 0; k < cnt; ++k) handle(src, k, remote);
     }
     if (p.campaign && p.campaign[rid]) handle_node_election();
     if (!(p.flags & 1u)) tick();
-    if (p.prop_target && p.prop_target[g] == s) {
-      const uint32_t n = p.prop_count[g];
+    if (p.prop_target && p.prop_target[gg] == s) {
+      const uint32_t n = p.prop_count[gg];
       if (n > 0) handle_propose(n, (uint32_t)(p.tick % p.nslab), 0);
     }
     applied = committed;  // apply, snapshot, compaction

@@ -14,6 +14,7 @@
 
 #include "../../include/raftgpu.h"
 #include "raftgpu_internal.h"
+#include "raftgpu_wire.h"
 
 using namespace rg;
 
@@ -74,6 +75,21 @@ struct rg_engine {
   double kms[2] = {0, 0};
   uint64_t klaunch[2] = {0, 0};
   uint32_t T0[256];
+  // placement + inter-rank exchange
+  Placement pl{};
+  bool wire = false;            // some plane crosses ranks (ranks > 1 or wire_all)
+  uint32_t slab_rows = 0;
+  uint32_t *umap = nullptr, *ubeg = nullptr, *rmap = nullptr, *rbeg = nullptr;
+  uint32_t U = 0, RU = 0;
+  std::vector<uint32_t> h_ubeg, h_rbeg;
+  uint32_t* usize = nullptr;
+  uint64_t *uoff = nullptr, *bsum = nullptr, *bounds = nullptr, *h_bounds = nullptr;
+  uint64_t* rhdr = nullptr;
+  uint64_t* rmt = nullptr;
+  uint32_t* rcnt = nullptr;
+  std::vector<uint64_t> send_bytes;
+  bool planned = false, wire_ready = false;
+  const uint8_t* recv = nullptr;  // receive buffer the next tick's SRC_WIRE jobs read
 };
 
 // ---------------------------------------------------------------- CRC-32/IEEE tables
@@ -150,6 +166,7 @@ static TickParams params(rg_engine* e) {
   p.CO = c.compaction_overhead; p.drop_ppm = c.drop_ppm;
   p.seed = c.seed;
   p.tick = e->t;
+  p.pl = e->pl;
   const int a = (int)(e->t & 1), b = a ^ 1;
   p.s64_in = e->s64[a]; p.s64_out = e->s64[b];
   p.s32_in = e->s32[a]; p.s32_out = e->s32[b];
@@ -160,7 +177,22 @@ static TickParams params(rg_engine* e) {
   p.mt_in = e->mt[b]; p.mt_out = e->mt[a];
   p.cnt_in = e->cnt[b]; p.cnt_out = e->cnt[a];
   p.job64 = e->job64[a]; p.job32 = e->job32[a]; p.jcnt = e->jcnt[a];
+  p.rhdr = e->rhdr; p.rmt = e->rmt; p.rcnt = e->rcnt;
   return p;
+}
+
+static WireParams wire_params(rg_engine* e) {
+  const TickParams p = params(e);
+  WireParams w{};
+  w.G = p.G; w.R = p.R; w.nrep = p.nrep; w.L = p.L; w.P = p.P; w.E = p.E; w.K = p.K;
+  w.pl = e->pl;
+  w.hdr = p.hdr_in; w.mt = p.mt_in; w.cnt = p.cnt_in;
+  w.info = e->info; w.pay = e->pay;
+  w.umap = e->umap; w.ubeg = e->ubeg; w.U = e->U;
+  w.usize = e->usize; w.uoff = e->uoff; w.bsum = e->bsum;
+  w.rmap = e->rmap; w.rbeg = e->rbeg; w.RU = e->RU;
+  w.rhdr = e->rhdr; w.rmt = e->rmt; w.rcnt = e->rcnt;
+  return w;
 }
 
 static BulkParams bulk_params(rg_engine* e) {  // for tick e->t
@@ -170,6 +202,8 @@ static BulkParams bulk_params(rg_engine* e) {  // for tick e->t
   b.E = e->c.max_entries_per_msg; b.J = e->J; b.crc_const = e->crc_const; b.tile = e->bulk_tile;
   b.job64 = e->job64[a]; b.job32 = e->job32[a]; b.jcnt = e->jcnt[a];
   b.info = e->info; b.pay = e->pay; b.slabs = e->slabs; b.crc_err = e->crc_err; b.crc_tab = e->crc_tab;
+  b.slab_by_q = e->slab_rows == e->nrep && e->pl.N > 1;
+  b.wire = e->recv;
   return b;
 }
 
@@ -197,6 +231,9 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if (c.max_msgs_per_pair < 1 || c.max_msgs_per_pair > 16) return fail(RG_EINVAL, "max_msgs_per_pair in 1..16");
   if (c.num_slabs < 2 || c.election_rtt < 1 || c.heartbeat_rtt < 1) return fail(RG_EINVAL, "num_slabs/rtt");
   if ((uint64_t)c.groups * c.replicas > 0x7FFFFFFFull) return fail(RG_EINVAL, "too many replicas");
+  const uint32_t N = c.ranks ? c.ranks : 1;
+  if (N > MAX_RANKS || c.rank >= N) return fail(RG_EINVAL, "ranks in 1..16, rank < ranks");
+  if ((N > 1 || c.wire_all) && c.groups >= (1u << 24)) return fail(RG_EINVAL, "groups < 2^24 with ranks > 1");
   int ndev = 0;
   HIPCHK(hipGetDeviceCount(&ndev));
   if (ndev <= 0 || c.device < 0 || c.device >= ndev) return fail(RG_EINVAL, "no such HIP device");
@@ -204,7 +241,10 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
 
   rg_engine* e = new rg_engine();
   e->c = c;
+  e->c.ranks = N;
   e->nrep = c.groups * c.replicas;
+  e->pl = make_placement(N, c.rank, c.wire_all);
+  e->slab_rows = N > 1 ? e->nrep : c.groups;
   e->J = (c.replicas - 1) * c.max_msgs_per_pair + 2;  // >= appends one step can make
   const uint64_t n = e->nrep, L = c.log_capacity, P = c.payload_bytes, R = c.replicas, K = c.max_msgs_per_pair,
                  E = c.max_entries_per_msg, G = c.groups, J = e->J;
@@ -227,13 +267,64 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
     if (rc == RG_OK) rc = dalloc(e, &e->jcnt[b], n * 4);
   }
   if (rc == RG_OK) rc = dalloc(e, &e->crc_err, n * 4);
-  if (rc == RG_OK) rc = dalloc(e, &e->slabs, (uint64_t)c.num_slabs * G * E * P);
+  if (rc == RG_OK) rc = dalloc(e, &e->slabs, (uint64_t)c.num_slabs * e->slab_rows * E * P);
   if (rc == RG_OK) rc = dalloc(e, &e->crc_tab, CRC_TAB_WORDS * 4);
-  if (rc == RG_OK) rc = dalloc(e, &e->d_prop_target, G);
-  if (rc == RG_OK) rc = dalloc(e, &e->d_prop_count, G * 4);
-  if (rc == RG_OK) rc = dalloc(e, &e->d_campaign, n);
-  if (rc == RG_OK) rc = dalloc(e, &e->d_isolate, n);
+  // tick inputs are indexed by global group / replica: ranks × the local sizes
+  if (rc == RG_OK) rc = dalloc(e, &e->d_prop_target, G * N);
+  if (rc == RG_OK) rc = dalloc(e, &e->d_prop_count, G * N * 4);
+  if (rc == RG_OK) rc = dalloc(e, &e->d_campaign, n * N);
+  if (rc == RG_OK) rc = dalloc(e, &e->d_isolate, n * N);
   if (rc == RG_OK) rc = dalloc(e, &e->d_sum, 64);
+  // exchange units: every remote (s, d, j) outbox column, per destination rank (send) and per
+  // source rank (receive), each in (s, d, j) order — the same list on both ends of a link
+  e->wire = N > 1 || c.wire_all;
+  if (rc == RG_OK && e->wire) {
+    std::vector<std::vector<uint32_t>> snd(N), rcv(N);
+    for (uint32_t s = 0; s < R; ++s)
+      for (uint32_t d = 0; d < R; ++d) {
+        if (s == d) continue;
+        for (uint32_t j = 0; j < G; ++j) {
+          if (!pl_remote(e->pl, s, d, j)) continue;
+          const uint32_t off = pl_off(e->pl, s, d, j), code = (s << 28) | (d << 24) | j;
+          snd[(c.rank + off) % N].push_back(code);
+          rcv[(c.rank + N - off) % N].push_back(code);
+        }
+      }
+    std::vector<uint32_t> um, rm;
+    e->h_ubeg.assign(N + 1, 0);
+    e->h_rbeg.assign(N + 1, 0);
+    for (uint32_t r = 0; r < N; ++r) {
+      e->h_ubeg[r] = (uint32_t)um.size();
+      um.insert(um.end(), snd[r].begin(), snd[r].end());
+      e->h_rbeg[r] = (uint32_t)rm.size();
+      rm.insert(rm.end(), rcv[r].begin(), rcv[r].end());
+    }
+    e->h_ubeg[N] = (uint32_t)um.size();
+    e->h_rbeg[N] = (uint32_t)rm.size();
+    e->U = (uint32_t)um.size();
+    e->RU = (uint32_t)rm.size();
+    const uint64_t nb = (e->U + 1023) / 1024 + 1;
+    rc = dalloc(e, &e->umap, (uint64_t)e->U * 4);
+    if (rc == RG_OK) rc = dalloc(e, &e->rmap, (uint64_t)e->RU * 4);
+    if (rc == RG_OK) rc = dalloc(e, &e->ubeg, (N + 1) * 4);
+    if (rc == RG_OK) rc = dalloc(e, &e->rbeg, (N + 1) * 4);
+    if (rc == RG_OK) rc = dalloc(e, &e->usize, (uint64_t)e->U * 4);
+    if (rc == RG_OK) rc = dalloc(e, &e->uoff, ((uint64_t)e->U + 1) * 8);
+    if (rc == RG_OK) rc = dalloc(e, &e->bsum, nb * 8);
+    if (rc == RG_OK) rc = dalloc(e, &e->bounds, (MAX_RANKS + 1) * 8);
+    if (rc == RG_OK) rc = dalloc(e, &e->rhdr, 8 * R * R * K * G * 8);
+    if (rc == RG_OK) rc = dalloc(e, &e->rmt, R * R * K * E * G * 8);
+    if (rc == RG_OK) rc = dalloc(e, &e->rcnt, R * R * G * 4);
+    if (rc == RG_OK && hipHostMalloc((void**)&e->h_bounds, (MAX_RANKS + 1) * 8, 0) != hipSuccess)
+      rc = fail(RG_ENOMEM, "hipHostMalloc");
+    if (rc == RG_OK &&
+        (hipMemcpy(e->umap, um.data(), um.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+         hipMemcpy(e->rmap, rm.data(), rm.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+         hipMemcpy(e->ubeg, e->h_ubeg.data(), (N + 1) * 4, hipMemcpyHostToDevice) != hipSuccess ||
+         hipMemcpy(e->rbeg, e->h_rbeg.data(), (N + 1) * 4, hipMemcpyHostToDevice) != hipSuccess))
+      rc = fail(RG_EHIP, "unit map upload");
+    e->send_bytes.assign(N, 0);
+  }
   if (rc != RG_OK) {
     std::string msg = g_err;
     rg_destroy(e);
@@ -289,6 +380,7 @@ void rg_destroy(rg_engine* e) {
     if (e->bulk_done[b]) (void)hipEventDestroy(e->bulk_done[b]);
   }
   for (void* p : e->allocs) (void)hipFree(p);
+  if (e->h_bounds) (void)hipHostFree(e->h_bounds);
   delete e;
 }
 
@@ -333,6 +425,9 @@ int rg_bootstrap(rg_engine* e) {
   e->t = 0;
   const uint64_t R = e->c.replicas, G = e->c.groups;
   for (int b = 0; b < 2; ++b) HIPCHK(hipMemsetAsync(e->cnt[b], 0, R * R * G * 4, e->stream));
+  if (e->rcnt) HIPCHK(hipMemsetAsync(e->rcnt, 0, R * R * G * 4, e->stream));
+  e->planned = e->wire_ready = false;
+  e->recv = nullptr;
   HIPCHK(hipMemsetAsync(e->crc_err, 0, (uint64_t)e->nrep * 4, e->stream));
   TickParams p = params(e);
   p.s64_out = e->s64[0];
@@ -348,8 +443,8 @@ int rg_bootstrap(rg_engine* e) {
 int rg_fill_slabs(rg_engine* e) {
   if (!e) return fail(RG_EINVAL, "null engine");
   if (int jrc = join(e)) return jrc;
-  HIPCHK(launch_fill_slabs(e->slabs, e->c.num_slabs, e->c.groups, e->c.max_entries_per_msg, e->c.payload_bytes,
-                           e->c.seed, e->stream));
+  HIPCHK(launch_fill_slabs(e->slabs, e->c.num_slabs, e->c.groups, e->slab_rows, e->c.max_entries_per_msg,
+                           e->c.payload_bytes, e->c.seed, e->pl, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   return RG_OK;
 }
@@ -403,6 +498,8 @@ int rg_kernel_ms(rg_engine* e, double* ms, uint64_t* launches) {
 }
 
 static int tick_impl(rg_engine* e, const rg_tick_input* in, bool device_ptrs) {
+  if (e->wire && e->t > 0 && !e->wire_ready)
+    return fail(RG_EINVAL, "rg_tick: the last tick's messages were not exchanged (rg_wire_plan/pack/recv)");
   TickParams p = params(e);
   if (in) {
     p.flags = in->flags;
@@ -412,7 +509,7 @@ static int tick_impl(rg_engine* e, const rg_tick_input* in, bool device_ptrs) {
       p.campaign = in->campaign;
       p.isolate = in->isolate;
     } else {
-      const uint64_t G = e->c.groups, n = e->nrep;
+      const uint64_t G = (uint64_t)e->c.groups * e->pl.N, n = G * e->c.replicas;  // global inputs
       if (in->prop_target) {
         if (!in->prop_count) return fail(RG_EINVAL, "prop_target without prop_count");
         for (uint64_t g = 0; g < G; ++g)
@@ -452,6 +549,7 @@ static int tick_impl(rg_engine* e, const rg_tick_input* in, bool device_ptrs) {
   if (e->timing) RGCHK(timing_event(e, bs));
   HIPCHK(hipEventRecord(e->bulk_done[a], bs));
   e->t++;
+  e->wire_ready = false;
   if (!device_ptrs && in) HIPCHK(hipStreamSynchronize(e->stream));  // host buffers may be reused
   return RG_OK;
 }
@@ -573,17 +671,97 @@ int rg_deliver(rg_engine* e, uint32_t rid_src, const rg_msg_view* m) {
 }
 
 int rg_leader(rg_engine* e, uint32_t group, uint64_t* leader_id, uint64_t* term, int* valid) {
-  if (!e || group >= e->c.groups) return fail(RG_EINVAL, "rg_leader: bad group");
-  std::vector<rg_replica_view> v(e->c.replicas);
-  int rc = rg_read_replicas(e, group * e->c.replicas, e->c.replicas, v.data());
-  if (rc) return rc;
+  const uint32_t N = e ? e->pl.N : 1;
+  if (!e || (uint64_t)group >= (uint64_t)e->c.groups * N) return fail(RG_EINVAL, "rg_leader: bad group");
+  const uint32_t R = e->c.replicas, j = group / N;
+  std::vector<rg_replica_view> v;
+  for (uint32_t s = 0; s < R; ++s) {
+    if ((group % N + s * pl_h(e->pl, j)) % N != e->pl.rank) continue;  // replica hosted elsewhere
+    rg_replica_view x;
+    int rc = rg_read_replicas(e, j * R + s, 1, &x);
+    if (rc) return rc;
+    v.push_back(x);
+  }
+  if (v.empty()) return fail(RG_EINVAL, "rg_leader: no replica of this group on this rank");
   uint64_t bt = 0, bl = 0;
   for (auto& r : v) bt = std::max(bt, r.term);
   for (auto& r : v)
-    if (r.role == RG_LEADER && r.term == bt) bl = r.leader;  // a leader valid at the group's highest term
+    if (r.role == RG_LEADER && r.term == bt) bl = r.leader;  // a leader valid at the highest local term
+  if (!bl)
+    for (auto& r : v)
+      if (r.term == bt && r.leader) bl = r.leader;  // else the leader the replica follows
   if (leader_id) *leader_id = bl;
   if (term) *term = bt;
   if (valid) *valid = bl != 0;
+  return RG_OK;
+}
+
+int rg_global_id(rg_engine* e, uint32_t rid, uint64_t* group, uint64_t* global_rid) {
+  if (!e || rid >= e->nrep) return fail(RG_EINVAL, "rg_global_id: bad replica");
+  const uint32_t R = e->c.replicas, j = rid / R, s = rid % R;
+  const uint64_t gg = pl_group(e->pl, s, j);
+  if (group) *group = gg;
+  if (global_rid) *global_rid = gg * R + s;
+  return RG_OK;
+}
+
+int rg_wire_plan(rg_engine* e, uint64_t* send_bytes) {
+  if (!e || !send_bytes) return fail(RG_EINVAL, "rg_wire_plan args");
+  const uint32_t N = e->pl.N;
+  if (!e->wire) {
+    for (uint32_t r = 0; r < N; ++r) send_bytes[r] = 0;
+    return RG_OK;
+  }
+  if (int jrc = join(e)) return jrc;
+  HIPCHK(hipSetDevice(e->c.device));
+  HIPCHK(launch_wire_plan(wire_params(e), e->bounds, e->stream));
+  HIPCHK(hipMemcpyAsync(e->h_bounds, e->bounds, (N + 1) * 8, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  for (uint32_t r = 0; r < N; ++r) {
+    const uint64_t units = e->h_ubeg[r + 1] - e->h_ubeg[r], data = (e->h_bounds[r + 1] - e->h_bounds[r]) * 16;
+    e->send_bytes[r] = units ? wire_table_bytes(units) + ((data + 255) & ~255ull) : 0;
+    send_bytes[r] = e->send_bytes[r];
+  }
+  e->planned = true;
+  return RG_OK;
+}
+
+int rg_wire_pack(rg_engine* e, void* send_buf, uint64_t send_cap) {
+  if (!e) return fail(RG_EINVAL, "null engine");
+  if (!e->wire) return RG_OK;
+  if (!e->planned) return fail(RG_EINVAL, "rg_wire_pack before rg_wire_plan");
+  WireParams w = wire_params(e);
+  uint64_t off = 0;
+  for (uint32_t r = 0; r < e->pl.N; ++r) {
+    w.send_region[r] = off;
+    off += e->send_bytes[r];
+  }
+  if (off > send_cap) return fail(RG_EFULL, "rg_wire_pack: send buffer smaller than the planned regions");
+  if (off && !send_buf) return fail(RG_EINVAL, "rg_wire_pack: null buffer");
+  w.send = (uint8_t*)send_buf;
+  HIPCHK(launch_wire_pack(w, e->stream));
+  e->planned = false;
+  return RG_OK;
+}
+
+int rg_wire_recv(rg_engine* e, const void* recv_buf, const uint64_t* recv_bytes) {
+  if (!e || !recv_bytes) return fail(RG_EINVAL, "rg_wire_recv args");
+  if (!e->wire) return RG_OK;
+  if (int jrc = join(e)) return jrc;
+  WireParams w = wire_params(e);
+  uint64_t off = 0;
+  for (uint32_t r = 0; r < e->pl.N; ++r) {
+    const uint64_t units = e->h_rbeg[r + 1] - e->h_rbeg[r];
+    if (units ? recv_bytes[r] < wire_table_bytes(units) : recv_bytes[r] != 0)
+      return fail(RG_EINVAL, "rg_wire_recv: region of rank " + std::to_string(r) + " has the wrong size");
+    w.recv_region[r] = off;
+    off += recv_bytes[r];
+  }
+  if (off && !recv_buf) return fail(RG_EINVAL, "rg_wire_recv: null buffer");
+  w.recv = (const uint8_t*)recv_buf;
+  HIPCHK(launch_wire_unpack(w, e->stream));
+  e->recv = (const uint8_t*)recv_buf;
+  e->wire_ready = true;
   return RG_OK;
 }
 

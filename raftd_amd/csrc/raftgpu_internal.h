@@ -7,6 +7,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#ifndef RG_HD_INLINE
+#define RG_HD_INLINE __host__ __device__ inline
+#endif
+
 namespace rg {
 
 constexpr uint32_t MAX_R = 8;
@@ -37,12 +41,56 @@ enum : uint32_t {
 // job rows
 enum : uint32_t { J_FIRST, J_DMASK, J_SMASK, J_HMASK, J_TMASK, J64_ROWS };
 enum : uint32_t { J_META, J_SRC, J32_ROWS };  // meta = n | e0<<8 | kind<<16
-enum : uint32_t { SRC_NONE = 0, SRC_RING = 1, SRC_SLAB = 2 };
+enum : uint32_t { SRC_NONE = 0, SRC_RING = 1, SRC_SLAB = 2, SRC_WIRE = 3 };
+// SRC_WIRE job: the entries arrived over the wire (another rank's replica). J_SMASK holds the byte
+// offset of the message's first entry record in the receive buffer and J_SRC the message's entry
+// count n; record e = {u64 term word, u32 crc, u32 0} at +16e, payload e at +16n + P·e.
+
+// ---- placement across ranks. Replica slot s of global group g lives on rank
+// (g mod N + s·h(j)) mod N, local column j = g div N, h(j) = hs[j mod H] (the units mod N), so all
+// replicas of a group share column j and the plane s→d of column j goes to rank k + (d−s)·h(j).
+constexpr uint32_t MAX_RANKS = 16;
+struct Placement {
+  uint32_t N, rank, H, wire_all;
+  uint8_t hs[MAX_RANKS];
+};
+RG_HD_INLINE uint32_t pl_h(const Placement& pl, uint32_t j) { return pl.hs[j % pl.H]; }
+// rank offset of the plane s→d at column j (0 = co-located)
+RG_HD_INLINE uint32_t pl_off(const Placement& pl, uint32_t s, uint32_t d, uint32_t j) {
+  const uint32_t N = pl.N;
+  return (uint32_t)((((int64_t)d - (int64_t)s) * (int64_t)pl_h(pl, j) % N + N) % N);
+}
+RG_HD_INLINE bool pl_remote(const Placement& pl, uint32_t s, uint32_t d, uint32_t j) {
+  return pl.wire_all || pl_off(pl, s, d, j) != 0;
+}
+inline Placement make_placement(uint32_t N, uint32_t rank, uint32_t wire_all) {
+  Placement pl{};
+  pl.N = N ? N : 1;
+  pl.rank = rank;
+  pl.wire_all = wire_all ? 1 : 0;
+  for (uint32_t h = 1; h < pl.N; ++h) {
+    uint32_t a = h, b = pl.N;
+    while (b) {
+      const uint32_t t = a % b;
+      a = b;
+      b = t;
+    }
+    if (a == 1) pl.hs[pl.H++] = (uint8_t)h;
+  }
+  if (pl.H == 0) pl.hs[pl.H++] = 0;  // one rank: everything co-located
+  return pl;
+}
+// global group of local replica (slot s, column j) on this rank
+RG_HD_INLINE uint64_t pl_group(const Placement& pl, uint32_t s, uint32_t j) {
+  const int64_t N = pl.N;
+  return (uint64_t)N * j + (uint64_t)((((int64_t)pl.rank - (int64_t)s * pl_h(pl, j)) % N + N) % N);
+}
 
 struct TickParams {
   uint32_t G, R, nrep, L, P, E, K, nslab, J;
   uint32_t ET, HT, CQ, SE, CO, drop_ppm, flags;
   uint64_t seed, tick;
+  Placement pl;
   const uint64_t* s64_in;  // [S64_ROWS][nrep]
   uint64_t* s64_out;
   const uint32_t* s32_in;  // [S32_ROWS][nrep]
@@ -58,6 +106,11 @@ struct TickParams {
   uint64_t* mt_out;
   const uint32_t* cnt_in;  // [R src][R dst][G]
   uint32_t* cnt_out;
+  // remote inbox (planes whose sender lives on another rank, written by unpack_kernel; same
+  // layout as hdr/mt/cnt; hdr word 7 of a Replicate = byte offset of its records in the wire)
+  const uint64_t* rhdr;
+  const uint64_t* rmt;
+  const uint32_t* rcnt;
   uint64_t* job64;         // [J64_ROWS][J][nrep]
   uint32_t* job32;         // [J32_ROWS][J][nrep]
   uint32_t* jcnt;          // [nrep]
@@ -69,12 +122,14 @@ struct TickParams {
 
 struct BulkParams {
   uint32_t G, nrep, L, P, E, J, crc_const, tile;  // tile: replicas per wave work item (1..64)
+  uint32_t slab_by_q;    // slab rows per replica (ranks > 1) instead of per group
   const uint64_t* job64;
   const uint32_t* job32;
   const uint32_t* jcnt;
   uint2* info;           // [2 banks][nrep][L] {crc, type<<24 | len}
   uint8_t* pay;          // [2 banks][nrep][L][P]
-  const uint8_t* slabs;  // [nslab][G][E][P]
+  const uint8_t* slabs;  // [nslab][rows][E][P], rows = G (one rank) or nrep (slab_by_q)
+  const uint8_t* wire;   // receive buffer of the last exchange (SRC_WIRE jobs)
   uint32_t* crc_err;     // [nrep] sticky ERR_CRC from payload verification
   const uint32_t* crc_tab;
 };
@@ -96,8 +151,8 @@ constexpr uint32_t CRC_TAB_WORDS = CRC_T_WORDS + CRC_N_WORDS + CRC_SH_MAX_WORDS;
 hipError_t launch_control(const TickParams& p, hipStream_t s);
 hipError_t launch_bulk(const BulkParams& p, hipStream_t s, int grid);
 hipError_t launch_bootstrap(const TickParams& p, uint2* info, hipStream_t s);
-hipError_t launch_fill_slabs(uint8_t* slabs, uint32_t nslab, uint32_t G, uint32_t E, uint32_t P, uint64_t seed,
-                             hipStream_t s);
+hipError_t launch_fill_slabs(uint8_t* slabs, uint32_t nslab, uint32_t G, uint32_t rows, uint32_t E, uint32_t P,
+                             uint64_t seed, const Placement& pl, hipStream_t s);
 hipError_t launch_sum_committed(const TickParams& p, unsigned long long* out, hipStream_t s);
 hipError_t launch_traffic(const TickParams& p, unsigned long long* out6, hipStream_t s);
 // admin gathers / scatters behind the read / import / deliver entry points (raftgpu_admin.hip)

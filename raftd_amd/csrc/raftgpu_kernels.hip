@@ -148,7 +148,7 @@ __device__ __forceinline__ void load_tile(const BulkParams& p, Cursor& cur, Tile
 __device__ __forceinline__ void set_job(const BulkParams& p, Cursor& cur, const Job& jb) {
   cur.first = jb.first; cur.dm = jb.dm; cur.sm = jb.sm; cur.hm = jb.hm; cur.tm = jb.tm;
   cur.n = jb.meta & 0xFF; cur.b = (jb.meta >> 8) & 0xFF; cur.kind = jb.meta >> 16; cur.src = jb.src;
-  cur.g = cur.q % p.G;
+  cur.g = p.slab_by_q ? cur.q : cur.q % p.G;  // proposal slab row
 }
 
 // Move the cursor one position: the replica's next job, the tile's next replica, or the next
@@ -217,7 +217,7 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p) {
   const uint32_t waves = blockDim.x >> 6, lane = lane_id();
   const uint32_t stride = gridDim.x * waves, T = p.tile;
   const uint32_t ntiles = (p.nrep + T - 1) / T;
-  const uint64_t n64 = p.nrep, L = p.L;
+  const uint64_t n64 = p.nrep, L = p.L, rows = p.slab_by_q ? p.nrep : p.G;
   const uint32_t c = lane & (NCH - 1), ei = lane >> LG;
   const Crc crc{lds, lds + CRC_T_WORDS, lds + CRC_T_WORDS + CRC_N_WORDS + c * CRC_SH_STRIDE};
   Cursor cur{};
@@ -278,15 +278,20 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p) {
         const bool act = valid && ((cur.hm >> e) & 1ull);
         const uint32_t slot = (uint32_t)((cur.first + e) & (L - 1));
         const uint32_t db = valid ? (uint32_t)(cur.dm >> e) & 1u : 0u;
-        const bool ring = cur.kind == SRC_RING;
+        const bool ring = cur.kind == SRC_RING, wire = cur.kind == SRC_WIRE;
         ds[u] = slot | (db << 31);
         fl[u] = (act ? F_ACT : 0u) | ((valid && c == 0) ? F_WRITER : 0u) | (((cur.tm >> e) & 1ull) ? F_TYPE : 0u) |
-                ((ring && act) ? F_CHECK : 0u);
+                (((ring || wire) && act) ? F_CHECK : 0u);
         const uint64_t sb = (cur.sm >> e) & 1ull;
         const uint64_t si = (sb * n64 + cur.src) * L + slot;
-        const uint8_t* sp = ring ? p.pay + si * P : p.slabs + (((uint64_t)cur.src * p.G + cur.g) * p.E + e) * P;
+        // wire: records {term word, crc} at sm + 16e, payloads at sm + 16n + P·e (n = src)
+        const uint8_t* sp = ring   ? p.pay + si * P
+                            : wire ? p.wire + cur.sm + 16ull * cur.src + (uint64_t)P * e
+                                   : p.slabs + (((uint64_t)cur.src * rows + cur.g) * p.E + e) * P;
         sp = act ? sp : dummy;
-        const uint32_t* wp = (ring && act) ? &p.info[si].x : reinterpret_cast<const uint32_t*>(dummy);
+        const uint32_t* wp = (ring && act) ? &p.info[si].x
+                             : (wire && act) ? reinterpret_cast<const uint32_t*>(p.wire + cur.sm + 16ull * e + 8)
+                                             : reinterpret_cast<const uint32_t*>(dummy);
         x[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(sp + c * 16));
         want[u] = *wp;
         vmask = step ? (vmask | (1u << u)) : (vmask & ~(1u << u));
@@ -349,7 +354,7 @@ __global__ void bootstrap_kernel(TickParams p, uint2* info) {
   a[S_LAST * n] = R;
   a[S_COMMITTED * n] = R;
   b[S_RNG_CTR * n] = 1;
-  const uint64_t key = ((uint64_t)g << 32) | ((uint64_t)s << 24) | 1ull;
+  const uint64_t key = (pl_group(p.pl, s, g) << 32) | ((uint64_t)s << 24) | 1ull;
   b[S_RAND_TO * n] = p.ET + (uint32_t)(mix64(p.seed ^ mix64(key)) % p.ET);
   for (uint32_t j = 0; j < R; ++j) {  // addNode → setRemote(id, 0, last+1)
     p.rem_out[(0 * R + j) * n + q] = 0;
@@ -371,23 +376,28 @@ hipError_t launch_bootstrap(const TickParams& p, uint2* info, hipStream_t s) {
 }
 
 // ================================================================== proposal payload generator
-__global__ void fill_slabs_kernel(uint8_t* slabs, uint32_t nslab, uint32_t G, uint32_t E, uint32_t P, uint64_t seed) {
+// row r of a slab holds the batch of global group pl_group(s, j): r = j (one rank, rows = G) or
+// r = q = s·G + j (rows = nrep: each rank's replica of a group reads its own row, so a forwarded
+// proposal finds the same bytes on the leader's rank)
+__global__ void fill_slabs_kernel(uint8_t* slabs, uint32_t nslab, uint32_t G, uint32_t rows, uint32_t E, uint32_t P,
+                                  uint64_t seed, Placement pl) {
   const uint64_t wpe = P / 8;
-  const uint64_t total = (uint64_t)nslab * G * E * wpe;
+  const uint64_t total = (uint64_t)nslab * rows * E * wpe;
   for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < total; w += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t ent = w / wpe, wi = w - ent * wpe;
     const uint32_t i = (uint32_t)(ent % E);
     const uint64_t sg = ent / E;
-    const uint32_t gg = (uint32_t)(sg % G), sl = (uint32_t)(sg / G);
-    const uint64_t key = mix64(((uint64_t)sl << 56) ^ ((uint64_t)gg << 16) ^ (uint64_t)i ^ (seed * 0x9E3779B97F4A7C15ULL));
+    const uint32_t r = (uint32_t)(sg % rows), sl = (uint32_t)(sg / rows);
+    const uint64_t gg = pl_group(pl, r / G, r % G);
+    const uint64_t key = mix64(((uint64_t)sl << 56) ^ (gg << 16) ^ (uint64_t)i ^ (seed * 0x9E3779B97F4A7C15ULL));
     reinterpret_cast<uint64_t*>(slabs)[w] = mix64(key + (wi + 1) * 0xD1B54A32D192ED03ULL);
   }
 }
 
-hipError_t launch_fill_slabs(uint8_t* slabs, uint32_t nslab, uint32_t G, uint32_t E, uint32_t P, uint64_t seed,
-                             hipStream_t s) {
+hipError_t launch_fill_slabs(uint8_t* slabs, uint32_t nslab, uint32_t G, uint32_t rows, uint32_t E, uint32_t P,
+                             uint64_t seed, const Placement& pl, hipStream_t s) {
   if (!P) return hipSuccess;
-  hipLaunchKernelGGL(fill_slabs_kernel, dim3(4096), dim3(256), 0, s, slabs, nslab, G, E, P, seed);
+  hipLaunchKernelGGL(fill_slabs_kernel, dim3(4096), dim3(256), 0, s, slabs, nslab, G, rows, E, P, seed, pl);
   return hipGetLastError();
 }
 
@@ -401,12 +411,15 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t a) {
   return a;
 }
 
-// Σ_g max_s committed, on the state a next tick would read (s64_in)
+// Σ_g max_s committed, on the state a next tick would read (s64_in). With ranks > 1 the replicas
+// of a column belong to different groups: sum the slot-0 replicas hosted here (each group's slot 0
+// lives on exactly one rank, so the sum over ranks counts every group once).
 __global__ void sum_committed_kernel(TickParams p, unsigned long long* out) {
   uint64_t acc = 0;
+  const uint32_t ns = p.pl.N > 1 ? 1u : p.R;
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < p.G; g += gridDim.x * blockDim.x) {
     uint64_t m = 0;
-    for (uint32_t s = 0; s < p.R; ++s) m = umax64(m, p.s64_in[(uint64_t)S_COMMITTED * p.nrep + (uint64_t)s * p.G + g]);
+    for (uint32_t s = 0; s < ns; ++s) m = umax64(m, p.s64_in[(uint64_t)S_COMMITTED * p.nrep + (uint64_t)s * p.G + g]);
     acc += m;
   }
   acc = wave_sum64(acc);

@@ -1,0 +1,242 @@
+// raftgpu_wire.hip — the per-tick replica-message exchange between ranks.
+//
+// dragonboat hands each outbound pb.Message to its transport after the step (send-after-step,
+// internal/raft peer.go GetUpdate → transport); here every message a replica emitted in tick t
+// to a replica on another rank travels in one batch before tick t+1, as per-rank regions the
+// caller's transport moves (RCCL all-to-all over xGMI in bench.py, loopback copies in tests).
+//
+// A *unit* is one (sender slot s, destination slot d, column j) outbox column: up to K messages.
+// Units are listed per destination rank in (s, d, j) order (host-built, identical on the sender
+// and the receiver). A region for one rank is
+//     [u64 table: (data offset in 16-B units) << 8 | message count, one per unit, padded to 256 B]
+//     [data: per message a 64-B header, then n 16-B entry records {term word, crc, 0}, then n
+//      payloads of P bytes — n = the Replicate's entry count, 0 for every other type]
+// so a follower's bulk job reads its payloads and sender CRCs straight out of the receive buffer.
+//
+// plan_kernel      thread per unit: bytes of its messages
+// scan_*           exclusive scan of the unit sizes (three passes)
+// pack_kernel      wave per unit: headers, records (term word + the sender's stored CRC), payload
+//                  copied out of the sender's ring bank named by the term word
+// unpack_kernel    thread per received unit: dense remote-inbox planes (rhdr/rmt/rcnt, the layout
+//                  control_kernel reads), header word 7 of a Replicate = its records' byte offset
+#include "raftgpu_wire.h"
+
+namespace rg {
+
+__device__ __forceinline__ uint32_t wl_lane() { return __lane_id(); }
+
+__device__ __forceinline__ void unit_decode(uint32_t u, uint32_t& s, uint32_t& d, uint32_t& j) {
+  s = u >> 28;
+  d = (u >> 24) & 0xF;
+  j = u & 0xFFFFFF;
+}
+
+// 16-B units of one message: header 4, each entry 1 record + P/16 payload
+__device__ __forceinline__ uint32_t msg_units(uint64_t w0, uint32_t P) {
+  const uint32_t n = ((w0 & 0xFF) == M_REPLICATE) ? (uint32_t)(w0 >> 32) : 0u;
+  return 4u + n * (1u + P / 16u);
+}
+
+__global__ void plan_kernel(WireParams w) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= w.U) return;
+  uint32_t s, d, j;
+  unit_decode(w.umap[u], s, d, j);
+  const uint64_t col = (uint64_t)s * w.R + d;
+  const uint32_t c = w.cnt[col * w.G + j];
+  uint32_t sz = 0;
+  for (uint32_t k = 0; k < c; ++k) sz += msg_units(w.hdr[(col * w.K + k) * w.G + j], w.P);
+  w.usize[u] = sz;
+}
+
+// ---- exclusive scan of usize[0..U) into uoff[0..U] (uoff[U] = total), 1024 elements per block
+constexpr uint32_t SCAN_T = 256, SCAN_V = 4, SCAN_B = SCAN_T * SCAN_V;
+
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
+  const uint32_t lane = wl_lane();
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, o, 64);
+    const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), o, 64);
+    if (lane >= o) v += ((uint64_t)hi << 32) | lo;
+  }
+  return v;
+}
+
+// block-wide exclusive scan of one value per thread; returns the exclusive prefix, *total = block sum
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* total) {
+  __shared__ uint64_t wsum[SCAN_T / 64];
+  const uint32_t lane = wl_lane(), wv = threadIdx.x >> 6;
+  const uint64_t inc = wave_incl_scan(v);
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  uint64_t pre = 0, tot = 0;
+  for (uint32_t i = 0; i < SCAN_T / 64; ++i) {
+    pre += i < wv ? wsum[i] : 0;
+    tot += wsum[i];
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + inc - v;
+}
+
+__global__ void scan_reduce_kernel(const uint32_t* in, uint32_t n, uint64_t* bsum) {
+  const uint64_t base = (uint64_t)blockIdx.x * SCAN_B;
+  uint64_t v = 0;
+  for (uint32_t i = 0; i < SCAN_V; ++i) {
+    const uint64_t x = base + (uint64_t)threadIdx.x * SCAN_V + i;
+    v += x < n ? in[x] : 0u;
+  }
+  uint64_t tot;
+  block_excl_scan(v, &tot);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+__global__ void scan_blocks_kernel(uint64_t* bsum, uint32_t nb) {  // one block, exclusive in place
+  uint64_t carry = 0;
+  for (uint32_t b0 = 0; b0 < nb; b0 += SCAN_T) {
+    const uint32_t i = b0 + threadIdx.x;
+    const uint64_t v = i < nb ? bsum[i] : 0;
+    uint64_t tot;
+    const uint64_t ex = block_excl_scan(v, &tot);
+    if (i < nb) bsum[i] = carry + ex;
+    carry += tot;
+  }
+}
+
+__global__ void scan_apply_kernel(const uint32_t* in, uint32_t n, const uint64_t* bsum, uint64_t* out) {
+  const uint64_t base = (uint64_t)blockIdx.x * SCAN_B;
+  uint32_t x[SCAN_V];
+  uint64_t v = 0;
+  for (uint32_t i = 0; i < SCAN_V; ++i) {
+    const uint64_t k = base + (uint64_t)threadIdx.x * SCAN_V + i;
+    x[i] = k < n ? in[k] : 0u;
+    v += x[i];
+  }
+  uint64_t tot;
+  uint64_t run = bsum[blockIdx.x] + block_excl_scan(v, &tot);
+  for (uint32_t i = 0; i < SCAN_V; ++i) {
+    const uint64_t k = base + (uint64_t)threadIdx.x * SCAN_V + i;
+    if (k < n) out[k] = run;
+    run += x[i];
+    if (k + 1 == n) out[n] = run;
+  }
+}
+
+// per-destination data sizes (16-B units) → bounds[r] = uoff[ubeg[r]], r = 0..N
+__global__ void bounds_kernel(WireParams w, uint64_t* bounds) {
+  const uint32_t r = threadIdx.x;
+  if (r <= w.pl.N) bounds[r] = w.U ? w.uoff[w.ubeg[r]] : 0;
+}
+
+__device__ __forceinline__ uint32_t find_rank(const uint32_t* beg, uint32_t N, uint32_t u) {
+  uint32_t r = 0;
+  while (r + 1 < N && u >= beg[r + 1]) ++r;
+  return r;
+}
+
+__device__ __forceinline__ uint64_t table_bytes(uint32_t units) { return ((uint64_t)units * 8 + 255) & ~255ull; }
+
+__device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l) {
+  return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) | __builtin_amdgcn_readlane((uint32_t)v, l);
+}
+
+__global__ void __launch_bounds__(256) pack_kernel(WireParams w) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const uint32_t lane = wl_lane();
+  const uint32_t u = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  if (u >= w.U) return;
+  const uint32_t r = find_rank(w.ubeg, w.pl.N, u);
+  const uint32_t u0 = w.ubeg[r], nu = w.ubeg[r + 1] - u0;
+  uint8_t* region = w.send + w.send_region[r];
+  const uint64_t off16 = w.uoff[u] - w.uoff[u0];
+  uint32_t s, d, j;
+  unit_decode(w.umap[u], s, d, j);
+  const uint64_t col = (uint64_t)s * w.R + d, qs = (uint64_t)s * w.G + j, n64 = w.nrep;
+  const uint64_t plane = (uint64_t)w.R * w.R * w.K * w.G;
+  const uint32_t c = w.cnt[col * w.G + j];
+  if (lane == 0) reinterpret_cast<uint64_t*>(region)[u - u0] = (off16 << 8) | c;
+  uint8_t* out = region + table_bytes(nu) + off16 * 16;
+  const uint32_t P = w.P, nch = P / 16;
+  for (uint32_t k = 0; k < c; ++k) {
+    const uint64_t* hp = w.hdr + (col * w.K + k) * w.G + j;
+    const uint64_t hv = lane < 8 ? hp[lane * plane] : 0;
+    if (lane < 8) reinterpret_cast<uint64_t*>(out)[lane] = hv;
+    const uint64_t w0 = rl64(hv, 0), li = rl64(hv, 3);
+    const uint32_t n = ((w0 & 0xFF) == M_REPLICATE) ? (uint32_t)(w0 >> 32) : 0u;
+    const uint64_t* mtp = w.mt + ((col * w.K + k) * w.E) * w.G + j;
+    if (lane < n) {
+      const uint64_t word = mtp[(uint64_t)lane * w.G];
+      const uint64_t slot = (li + 1 + lane) & (w.L - 1);
+      const uint32_t crc = (word & PAY_BIT) ? w.info[((word >> 63) * n64 + qs) * w.L + slot].x : 0u;
+      *reinterpret_cast<u32x4*>(out + 64 + 16 * lane) = u32x4{(uint32_t)word, (uint32_t)(word >> 32), crc, 0u};
+    }
+    if (P) {
+      uint8_t* po = out + 64 + 16ull * n;
+#pragma unroll 4
+      for (uint32_t t = lane; t < n * nch; t += 64) {
+        const uint32_t e = t / nch, ch = t - e * nch;
+        const uint64_t word = mtp[(uint64_t)e * w.G];
+        if (word & PAY_BIT) {
+          const uint64_t slot = (li + 1 + e) & (w.L - 1);
+          const u32x4 v = __builtin_nontemporal_load(
+              reinterpret_cast<const u32x4*>(w.pay + (((word >> 63) * n64 + qs) * w.L + slot) * P + 16ull * ch));
+          __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(po + 16ull * t));
+        }
+      }
+    }
+    out += 64 + (uint64_t)n * (16 + P);
+  }
+}
+
+__global__ void unpack_kernel(WireParams w) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= w.RU) return;
+  const uint32_t r = find_rank(w.rbeg, w.pl.N, u);
+  const uint32_t u0 = w.rbeg[r], nu = w.rbeg[r + 1] - u0;
+  const uint8_t* region = w.recv + w.recv_region[r];
+  const uint64_t tv = reinterpret_cast<const uint64_t*>(region)[u - u0];
+  const uint32_t c = (uint32_t)(tv & 0xFF);
+  const uint8_t* in = region + table_bytes(nu) + (tv >> 8) * 16;
+  uint32_t s, d, j;
+  unit_decode(w.rmap[u], s, d, j);
+  const uint64_t col = (uint64_t)s * w.R + d;
+  const uint64_t plane = (uint64_t)w.R * w.R * w.K * w.G;
+  w.rcnt[col * w.G + j] = c;
+  for (uint32_t k = 0; k < c && k < w.K; ++k) {
+    const uint64_t* h = reinterpret_cast<const uint64_t*>(in);
+    const uint64_t w0 = h[0];
+    const uint32_t n = ((w0 & 0xFF) == M_REPLICATE) ? (uint32_t)(w0 >> 32) : 0u;
+    uint64_t* ho = w.rhdr + (col * w.K + k) * w.G + j;
+    for (int x = 0; x < 7; ++x) ho[x * plane] = h[x];
+    ho[7 * plane] = (w0 & 0xFF) == M_REPLICATE ? (uint64_t)(in + 64 - w.recv) : h[7];
+    uint64_t* mo = w.rmt + ((col * w.K + k) * w.E) * w.G + j;
+    for (uint32_t e = 0; e < n; ++e) mo[(uint64_t)e * w.G] = h[8 + 2 * e];
+    in += 64 + (uint64_t)n * (16 + w.P);
+  }
+}
+
+hipError_t launch_wire_plan(const WireParams& w, uint64_t* bounds, hipStream_t st) {
+  if (w.U) {
+    hipLaunchKernelGGL(plan_kernel, dim3((w.U + 255) / 256), dim3(256), 0, st, w);
+    const uint32_t nb = (w.U + SCAN_B - 1) / SCAN_B;
+    hipLaunchKernelGGL(scan_reduce_kernel, dim3(nb), dim3(SCAN_T), 0, st, w.usize, w.U, w.bsum);
+    hipLaunchKernelGGL(scan_blocks_kernel, dim3(1), dim3(SCAN_T), 0, st, w.bsum, nb);
+    hipLaunchKernelGGL(scan_apply_kernel, dim3(nb), dim3(SCAN_T), 0, st, w.usize, w.U, w.bsum, w.uoff);
+  }
+  hipLaunchKernelGGL(bounds_kernel, dim3(1), dim3(64), 0, st, w, bounds);
+  return hipGetLastError();
+}
+
+hipError_t launch_wire_pack(const WireParams& w, hipStream_t st) {
+  if (!w.U) return hipSuccess;
+  hipLaunchKernelGGL(pack_kernel, dim3((w.U + 3) / 4), dim3(256), 0, st, w);
+  return hipGetLastError();
+}
+
+hipError_t launch_wire_unpack(const WireParams& w, hipStream_t st) {
+  if (!w.RU) return hipSuccess;
+  hipLaunchKernelGGL(unpack_kernel, dim3((w.RU + 255) / 256), dim3(256), 0, st, w);
+  return hipGetLastError();
+}
+
+}  // namespace rg

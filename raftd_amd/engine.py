@@ -32,6 +32,7 @@ class Config(C.Structure):
         ("election_rtt", C.c_uint32), ("heartbeat_rtt", C.c_uint32), ("check_quorum", C.c_uint32),
         ("snapshot_entries", C.c_uint32), ("compaction_overhead", C.c_uint32),
         ("drop_ppm", C.c_uint32), ("device", C.c_int32), ("seed", C.c_uint64),
+        ("ranks", C.c_uint32), ("rank", C.c_uint32), ("wire_all", C.c_uint32), ("_pad", C.c_uint32),
     ]
 
 
@@ -81,7 +82,7 @@ EXPORTS = ["rg_create", "rg_destroy", "rg_bootstrap", "rg_fill_slabs", "rg_tick"
            "rg_set_stream", "rg_sync", "rg_tick_count", "rg_read_replicas", "rg_read_msgs",
            "rg_read_entries", "rg_import_replica", "rg_deliver", "rg_leader", "rg_sum_committed",
            "rg_device_bytes", "rg_last_error", "rg_last_tick_traffic", "rg_join",
-           "rg_timing", "rg_kernel_ms"]
+           "rg_timing", "rg_kernel_ms", "rg_wire_plan", "rg_wire_pack", "rg_wire_recv", "rg_global_id"]
 
 _lib = None
 
@@ -118,6 +119,10 @@ def load_library(path: str = LIB_PATH):
         "rg_device_bytes": ([vp], u64),
         "rg_last_tick_traffic": ([vp, C.POINTER(Traffic)], i32),
         "rg_last_error": ([], C.c_char_p),
+        "rg_wire_plan": ([vp, C.POINTER(C.c_uint64)], i32),
+        "rg_wire_pack": ([vp, vp, u64], i32),
+        "rg_wire_recv": ([vp, vp, C.POINTER(C.c_uint64)], i32),
+        "rg_global_id": ([vp, u32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -131,13 +136,16 @@ def default_config(**kw) -> dict:
     """raftd's Raft parameters (raft/raft_manager.go:92-100) plus the engine's sizing."""
     c = dict(groups=4, replicas=3, log_capacity=2048, payload_bytes=256, max_entries_per_msg=64,
              max_msgs_per_pair=8, num_slabs=2, election_rtt=10, heartbeat_rtt=1, check_quorum=1,
-             snapshot_entries=1000, compaction_overhead=5, drop_ppm=0, device=0, seed=0x5EED)
+             snapshot_entries=1000, compaction_overhead=5, drop_ppm=0, device=0, seed=0x5EED,
+             ranks=1, rank=0, wire_all=0)
     c.update(kw)
     return c
 
 
 class Engine:
-    """One engine = every replica of `groups` Raft shards on one GPU."""
+    """One engine = the replicas one GPU hosts: with ranks = 1 every replica of `groups` Raft
+    shards; with ranks = N the replicas placed on rank `rank` of N * groups shards.
+    Local replica ids are column * R + slot; tick inputs are indexed by global group / replica."""
 
     def __init__(self, **cfg):
         self.cfg = default_config(**cfg)
@@ -149,6 +157,7 @@ class Engine:
         self._check(self.L.rg_create(C.byref(c), C.byref(self.h)))
         self.G, self.R = self.cfg["groups"], self.cfg["replicas"]
         self.nrep = self.G * self.R
+        self.ranks = max(1, self.cfg["ranks"])
         self._slabs_filled = False
 
     def _check(self, rc):
@@ -312,6 +321,25 @@ class Engine:
         v = C.c_uint64()
         self._check(self.L.rg_sum_committed(self.h, C.byref(v)))
         return v.value
+
+    # inter-rank exchange (include/raftgpu.h rg_wire_*)
+    def wire_plan(self) -> list:
+        out = (C.c_uint64 * self.ranks)()
+        self._check(self.L.rg_wire_plan(self.h, out))
+        return list(out)
+
+    def wire_pack(self, send_ptr: int, send_cap: int):
+        self._check(self.L.rg_wire_pack(self.h, C.c_void_p(send_ptr or None), send_cap))
+
+    def wire_recv(self, recv_ptr: int, recv_bytes):
+        rb = (C.c_uint64 * self.ranks)(*recv_bytes)
+        self._check(self.L.rg_wire_recv(self.h, C.c_void_p(recv_ptr or None), rb))
+
+    def global_id(self, rid: int):
+        """(global group, global replica id) of local replica rid."""
+        g, gr = C.c_uint64(), C.c_uint64()
+        self._check(self.L.rg_global_id(self.h, rid, C.byref(g), C.byref(gr)))
+        return g.value, gr.value
 
     def last_tick_traffic(self) -> dict:
         t = Traffic()

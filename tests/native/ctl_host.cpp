@@ -27,6 +27,7 @@ static TickParams params(Host* h) {
   p.E = c.max_entries_per_msg; p.K = c.max_msgs_per_pair; p.nslab = c.num_slabs; p.J = h->J;
   p.ET = c.election_rtt; p.HT = c.heartbeat_rtt; p.CQ = c.check_quorum; p.SE = c.snapshot_entries;
   p.CO = c.compaction_overhead; p.drop_ppm = c.drop_ppm; p.seed = c.seed; p.tick = h->t;
+  p.pl = make_placement(1, 0, 0);  // one rank: every plane local
   const int a = (int)(h->t & 1), b = a ^ 1;
   p.s64_in = h->s64[a].data(); p.s64_out = h->s64[b].data();
   p.s32_in = h->s32[a].data(); p.s32_out = h->s32[b].data();
@@ -71,6 +72,12 @@ void* ch_create(const rg_config* c) {
 }
 
 void ch_destroy(void* hh) { delete (Host*)hh; }
+
+// placement math of raftgpu_internal.h, for the CPU cross-check with raftd_amd/cluster.py
+uint64_t ch_pl_group(uint32_t N, uint32_t rank, uint32_t s, uint32_t j) {
+  return pl_group(make_placement(N, rank, 0), s, j);
+}
+uint32_t ch_pl_off(uint32_t N, uint32_t s, uint32_t d, uint32_t j) { return pl_off(make_placement(N, 0, 0), s, d, j); }
 
 void ch_bootstrap(void* hh) {  // = bootstrap_kernel
   Host* h = (Host*)hh;

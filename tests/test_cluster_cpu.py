@@ -1,0 +1,104 @@
+"""Multi-rank host logic without a GPU: the placement math (Python vs the C++ of
+raftgpu_internal.h through the host harness), its invariants, and the exchange transport over
+torch.distributed with gloo at world_size 2."""
+import ctypes as C
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from raftd_amd.cluster import (_offsets, all_to_all_bytes, exchange_sizes, global_group, local_rid, rank_of,
+                               units_mod)
+
+
+@pytest.mark.parametrize("N", range(1, 17))
+def test_placement_invariants(N):
+    Gl = 24
+    for R in range(1, 9):
+        hosted = {}
+        for g in range(N * Gl):
+            ranks = [rank_of(g, s, N) for s in range(R)]
+            if N >= R:
+                assert len(set(ranks)) == R, (N, R, g, ranks)  # every replica on its own GPU
+            for s, k in enumerate(ranks):
+                j = local_rid(g, s, N, R) // R
+                assert global_group(k, s, j, N) == g
+                hosted.setdefault((k, s), set()).add(j)
+        for k in range(N):
+            for s in range(R):
+                assert hosted[(k, s)] == set(range(Gl))  # each rank: one replica per (slot, column)
+
+
+def test_units_mod():
+    assert units_mod(1) == [0]
+    assert units_mod(2) == [1]
+    assert units_mod(8) == [1, 3, 5, 7]
+    assert units_mod(6) == [1, 5]
+
+
+def test_placement_matches_cpp():
+    from native.ctl_host import build
+    L = C.CDLL(build())
+    L.ch_pl_group.restype = C.c_uint64
+    L.ch_pl_group.argtypes = [C.c_uint32] * 4
+    L.ch_pl_off.restype = C.c_uint32
+    L.ch_pl_off.argtypes = [C.c_uint32] * 4
+    for N in (1, 2, 3, 4, 5, 7, 8, 12, 16):
+        hs = units_mod(N)
+        for k in range(N):
+            for s in range(8):
+                for j in range(40):
+                    assert L.ch_pl_group(N, k, s, j) == global_group(k, s, j, N)
+        for s in range(8):
+            for d in range(8):
+                for j in range(20):
+                    assert L.ch_pl_off(N, s, d, j) == ((d - s) * hs[j % len(hs)]) % N
+
+
+def _free_port():
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def _transport_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(100 + rank)
+        sizes = [int(x) for x in torch.randint(0, 3000, (world,), generator=g)]
+        sizes[rank] = 0 if rank == 0 else sizes[rank]  # an empty region and a self region
+        offs, tot = _offsets(sizes)
+        send = torch.empty(tot + 17, dtype=torch.uint8)
+        for r in range(world):  # region r of rank a: bytes (a * 31 + r * 7 + i) mod 251
+            i = torch.arange(sizes[r])
+            send[offs[r]:offs[r] + sizes[r]] = ((rank * 31 + r * 7 + i) % 251).to(torch.uint8)
+        rsizes = exchange_sizes(sizes)
+        roffs, rtot = _offsets(rsizes)
+        recv = torch.zeros(rtot + 5, dtype=torch.uint8)
+        all_to_all_bytes(send, sizes, recv, rsizes)
+        ok = True
+        for a in range(world):
+            i = torch.arange(rsizes[a])
+            want = ((a * 31 + rank * 7 + i) % 251).to(torch.uint8)
+            ok &= bool(torch.equal(recv[roffs[a]:roffs[a] + rsizes[a]], want))
+        q.put((rank, ok, rsizes))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_transport_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_transport_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok, _ in res), res
