@@ -86,8 +86,8 @@ def test_cluster_steady_state_and_snapshots():
     check_payloads(cl, ora, sample=16)
     assert snaps > 0
     # the rejoining replica's higher term deposes some leaders (no PreVote, as raftd configures
-    # dragonboat) — the oracle agrees bit for bit; the shard set still committed ~1200 entries
-    assert min(cl.replica(g * R)["committed"] for g in range(G)) > 1000
+    # dragonboat) — the oracle agrees bit for bit; every group still committed > 800 entries
+    assert min(cl.replica(g * R)["committed"] for g in range(G)) > 800
     assert cl.wire_bytes > 0
 
 
