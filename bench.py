@@ -13,9 +13,14 @@ roofline: the dominant kernel is bulk_kernel (HBM-bound byte copies + CRC). achi
 algorithmic bytes per launch (rg_traffic.bulk_bytes) / its mean launch duration, timed with HIP
 events recorded on the bulk stream around every launch of the timed region.
 
-N > 1: one process per GPU (torch.distributed.run); each rank hosts its own 65,536 groups with
-all replicas on its GPU (weak scaling, no data-path collective in this round); value = groups
-over all ranks x K / max-over-ranks time.
+N > 1 (default --placement spread, the north star's layout): one process per GPU
+(torch.distributed.run), N x 65,536 groups, replica slot s of group g on GPU (g mod N + s*h) mod N
+(DESIGN.md §6), so every replica of a group sits on a different GPU, emulating separate nodes.
+Each step = the exchange of the previous tick's cross-GPU messages (plan/pack kernels, one RCCL
+all_to_all_single over xGMI — the only collective — and the unpack kernel) + the tick. Every GPU
+hosts 196,608 replicas, as at N = 1 (weak scaling). --placement colocated keeps every replica of
+a group on one GPU (no exchange). value = groups over all ranks x K / max-over-ranks time.
+--wire-all (N = 1, measurement): every message goes through the pack/unpack path to itself.
 
 Prints one JSON line (rank 0).
 """
@@ -47,19 +52,50 @@ def parse():
     ap.add_argument("--log-capacity", type=int, default=2048)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--placement", choices=["spread", "colocated"], default=None,
+                    help="N > 1: replicas of a group on different GPUs (default) or on one")
+    ap.add_argument("--wire-all", action="store_true", help="N = 1: route every message through the wire")
+    ap.add_argument("--backend", default="nccl", help="N > 1: nccl (RCCL, default) or gloo (rehearsal: several "
+                    "ranks on one GPU with RAFTD_BENCH_DEVICE=0, regions staged through host memory)")
     return ap.parse_args()
 
 
-def bring_up(eng, G, R):
-    """bootstrap → tick → campaign slot 0 → election completes."""
+def bring_up(eng, tick, G, R):
+    """bootstrap → tick → campaign slot 0 → election completes. G = global groups."""
     import numpy as np
     eng.bootstrap()
-    eng.tick()
+    tick()
     camp = np.zeros(G * R, np.uint8)
     camp[0::R] = 1
-    eng.tick(campaign=camp)
+    tick(campaign=camp)
     for _ in range(4):
-        eng.tick()
+        tick()
+
+
+class SelfWire:
+    """N = 1 with wire_all: the one region goes to this rank itself (no copy: recv = send)."""
+
+    def __init__(self, eng, torch):
+        self.eng, self.torch, self.buf = eng, torch, None
+        self.wire_bytes = 0
+
+    def exchange(self):
+        sizes = self.eng.wire_plan()
+        n = sum(sizes)
+        if self.buf is None or self.buf.numel() < n:
+            self.eng.sync()
+            self.buf = self.torch.empty(max(n, 1 << 20) * 3 // 2, dtype=self.torch.uint8, device="cuda")
+        self.eng.wire_pack(self.buf.data_ptr(), self.buf.numel())
+        self.eng.wire_recv(self.buf.data_ptr(), sizes)
+        self.wire_bytes = n
+
+    def tick(self, *a, **kw):
+        self.exchange()
+        self.eng.tick(*a, **kw)
+
+    def tick_device(self, *a, **kw):
+        self.exchange()
+        self.eng.tick_device(*a, **kw)
 
 
 def cpu_baseline(args, seconds):
@@ -124,28 +160,45 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("RAFTD_BENCH_DEVICE", local))
     import torch
 
     dist = None
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.backend)
     else:
         torch.cuda.set_device(local)
     from raftd_amd import Engine
+    from raftd_amd.cluster import DistEngine
 
     G, R, E, P = args.groups, args.replicas, args.entries, args.payload
-    eng = Engine(groups=G, replicas=R, log_capacity=args.log_capacity, payload_bytes=P,
-                 max_entries_per_msg=E, device=local, seed=0x5EED + rank)
+    placement = args.placement or ("spread" if world > 1 else "colocated")
+    spread = placement == "spread" and world > 1
     stream = torch.cuda.Stream()  # a real (non-null) stream: the engine launches on it, events time it
     torch.cuda.set_stream(stream)
-    eng.set_stream(stream.cuda_stream)
-    bring_up(eng, G, R)
-    pt = torch.zeros(G, dtype=torch.uint8, device="cuda")
-    pc = torch.full((G,), E, dtype=torch.int32, device="cuda")  # read as uint32 by the kernel
+    common = dict(replicas=R, log_capacity=args.log_capacity, payload_bytes=P, max_entries_per_msg=E, device=local)
+    wire = None
+    if spread:  # one cluster of world x G groups, replicas spread over the GPUs
+        wire = DistEngine(groups=G, seed=0x5EED, **common)
+        eng = wire.eng
+        Gt = G * world
+    else:  # an independent engine per GPU (its own G groups)
+        eng = Engine(groups=G, seed=0x5EED + rank, wire_all=1 if args.wire_all else 0, **common)
+        eng.set_stream(stream.cuda_stream)
+        if args.wire_all:
+            wire = SelfWire(eng, torch)
+        Gt = G
+    step = wire or eng
+    bring_up(eng, step.tick, Gt, R)
+    pt = torch.zeros(Gt, dtype=torch.uint8, device="cuda")
+    pc = torch.full((Gt,), E, dtype=torch.int32, device="cuda")  # read as uint32 by the kernel
     for _ in range(max(args.warmup, 1)):
-        eng.tick_device(pt.data_ptr(), pc.data_ptr())
+        step.tick_device(pt.data_ptr(), pc.data_ptr())
     traffic = eng.last_tick_traffic()  # counts of a steady-state tick (outside the timed region)
     c0 = eng.sum_committed()
     torch.cuda.synchronize()
@@ -153,10 +206,17 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    xev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     eng.timing(True)
+    wire_bytes = 0
     t0 = time.perf_counter()
     ev0.record(stream)
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        if wire:
+            xev[i][0].record(stream)
+            wire.exchange()
+            xev[i][1].record(stream)
+            wire_bytes += wire.wire_bytes
         eng.tick_device(pt.data_ptr(), pc.data_ptr())
     eng.join()  # the stream waits for the last tick's payload stage before the end event
     ev1.record(stream)
@@ -168,23 +228,33 @@ def main():
     dev_ms = ev0.elapsed_time(ev1)
     kms = eng.kernel_ms()
     eng.timing(False)
+    x_ms = sum(a.elapsed_time(b) for a, b in xev) / args.steps if wire else 0.0
     c1 = eng.sum_committed()
     errs = sum(1 for v in eng.replicas(0, min(eng.nrep, 3 * 4096)) if v["err"])
-    t = torch.tensor([wall, dev_ms, float(c1 - c0)], dtype=torch.float64, device="cuda")
+    t = torch.tensor([wall, dev_ms, float(c1 - c0), x_ms, float(wire_bytes)], dtype=torch.float64,
+                     device="cuda" if args.backend == "nccl" else "cpu")
     if dist:
         tmax = t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         tsum = t.clone()
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
         wall, dev_max, commits = tmax[0].item(), tmax[1].item(), tsum[2].item()
+        x_ms, wire_max = tmax[3].item(), tmax[4].item()
     else:
-        dev_max, commits = dev_ms, float(c1 - c0)
+        dev_max, commits, wire_max = dev_ms, float(c1 - c0), float(wire_bytes)
     if rank != 0:
         if dist:
             dist.destroy_process_group()
         return
     K = args.steps
     group_steps = world * G * K / wall
+    if spread:
+        par = (f"{world * G} groups; replica slot s of group g on GPU (g mod {world} + s*h) mod {world}; "
+               f"cross-GPU messages by one RCCL all_to_all_single per tick")
+    elif args.wire_all:
+        par = "1 GPU, every message through the wire pack/unpack path to itself (measurement)"
+    else:
+        par = f"groups sharded over {world} GPU(s), replicas co-located (no exchange)"
     bulk_ms = kms["bulk"][0] / max(kms["bulk"][1], 1)
     ctl_ms = kms["control"][0] / max(kms["control"][1], 1)
     achieved = traffic["bulk_bytes"] / (bulk_ms / 1e3) / 1e9
@@ -207,8 +277,8 @@ def main():
                         f"{P}-B payloads + CRC32 per tick, raftd Raft config (ElectionRTT 10, HeartbeatRTT 1, "
                         f"CheckQuorum, SnapshotEntries 1000, CompactionOverhead 5)",
             "groups_per_gpu": G, "replicas": R, "entries_per_batch": E, "payload_bytes": P,
-            "log_capacity": args.log_capacity, "parallelism": f"groups sharded over {world} GPU(s), "
-                                                                "replicas co-located (no exchange)",
+            "log_capacity": args.log_capacity, "placement": "spread" if spread else placement,
+            "parallelism": par,
         },
         "commits_per_sec": commits / wall,
         "replica_steps_per_sec": group_steps * R,
@@ -232,6 +302,14 @@ def main():
             "tick_counts": {k: v for k, v in traffic.items() if k not in ("algorithmic_bytes", "bulk_bytes")},
         },
         "kernels_ms": {"control_kernel": ctl_ms, "bulk_kernel": bulk_ms},
+        "exchange": None if not wire else {
+            "ms_per_step": x_ms,
+            "bytes_sent_per_step_max_rank": wire_max / K,
+            "achieved_GBps_per_rank": (wire_max / K) / (x_ms / 1e3) / 1e9 if x_ms > 0 else None,
+            "xgmi_peak_GBps_per_rank": 7 * 153.0,
+            "note": "plan + pack + RCCL all_to_all_single + unpack, timed with events on the bench stream; "
+                    "bytes = the regions this rank sends to other ranks",
+        },
         "device_bytes": eng.device_bytes,
     }
     if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only

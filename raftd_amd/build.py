@@ -10,6 +10,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libraftgpu.so")
+RESOURCES = os.path.join(PKG, "kernel_resources.txt")  # per-kernel VGPR / scratch / occupancy of the last build
 SOURCES = ["raftgpu_kernels.hip", "raftgpu_admin.hip", "raftgpu_wire.hip", "raftgpu_engine.cpp"]
 HEADERS = ["raftgpu_internal.h", "raftgpu_control.h", "raftgpu_wire.h", os.path.join("..", "..", "include", "raftgpu.h")]
 ARCH = os.environ.get("RAFTGPU_ARCH", "gfx950")
@@ -25,17 +26,26 @@ def _stale(out: str, deps: list[str]) -> bool:
 
 def build_engine(force: bool = False, verbose: bool = False) -> str:
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
-    if not force and not _stale(LIB, deps):
+    if not force and not _stale(LIB, deps) and os.path.exists(RESOURCES):
         return LIB
-    objs = []
+    objs, report = [], []
     for src in SOURCES:
         obj = os.path.join(CSRC, src.rsplit(".", 1)[0] + ".o")
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function",
                "-c", "-x", "hip", os.path.join(CSRC, src), "-o", obj]
+        if src.endswith(".hip"):
+            cmd.append("-Rpass-analysis=kernel-resource-usage")
         if verbose:
             print(" ".join(cmd))
-        subprocess.run(cmd, check=True)
+        r = subprocess.run(cmd, check=True, capture_output=True, text=True)
+        report += [ln.split("remark: ", 1)[1].split(" [-Rpass")[0].strip()
+                   for ln in r.stderr.splitlines() if "kernel-resource-usage" in ln and "remark: " in ln]
+        other = [ln for ln in r.stderr.splitlines() if "warning:" in ln or "error:" in ln]
+        if other:
+            print("\n".join(other), file=sys.stderr)
         objs.append(obj)
+    with open(RESOURCES, "w") as f:
+        f.write("\n".join(report) + "\n")
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
     subprocess.run(cmd, check=True)
     for o in objs:
@@ -56,3 +66,16 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def kernel_resources() -> dict:
+    """{kernel name: {field: value}} from the last build's resource-usage remarks."""
+    build_engine()
+    out, cur = {}, None
+    for ln in open(RESOURCES):
+        k, _, v = ln.strip().partition(": ")
+        if k == "Function Name":
+            cur = out.setdefault(v, {})
+        elif cur is not None:
+            cur[k] = v
+    return out

@@ -52,9 +52,9 @@ enum : uint32_t { SRC_NONE = 0, SRC_RING = 1, SRC_SLAB = 2, SRC_WIRE = 3 };
 constexpr uint32_t MAX_RANKS = 16;
 struct Placement {
   uint32_t N, rank, H, wire_all;
-  uint8_t hs[MAX_RANKS];
+  uint64_t hs;  // the H units, 4 bits each (H <= 12 for N <= 16): a register, never an indexed array
 };
-RG_HD_INLINE uint32_t pl_h(const Placement& pl, uint32_t j) { return pl.hs[j % pl.H]; }
+RG_HD_INLINE uint32_t pl_h(const Placement& pl, uint32_t j) { return (uint32_t)(pl.hs >> (4 * (j % pl.H))) & 0xFu; }
 // rank offset of the plane s→d at column j (0 = co-located)
 RG_HD_INLINE uint32_t pl_off(const Placement& pl, uint32_t s, uint32_t d, uint32_t j) {
   const uint32_t N = pl.N;
@@ -75,9 +75,9 @@ inline Placement make_placement(uint32_t N, uint32_t rank, uint32_t wire_all) {
       a = b;
       b = t;
     }
-    if (a == 1) pl.hs[pl.H++] = (uint8_t)h;
+    if (a == 1) pl.hs |= (uint64_t)h << (4 * pl.H++);
   }
-  if (pl.H == 0) pl.hs[pl.H++] = 0;  // one rank: everything co-located
+  if (pl.H == 0) pl.H = 1;  // one rank: h = 0, everything co-located
   return pl;
 }
 // global group of local replica (slot s, column j) on this rank
