@@ -174,7 +174,8 @@ __device__ __forceinline__ bool next_job(const BulkParams& p, Cursor& cur, TileJ
     cur.t += stride;
     if (cur.t >= ntiles) return false;
     load_tile(p, cur, tj);
-    cur.b = cur.n = 0;
+    cur.b = 0;  // two statements: the chained form kept Cursor in scratch
+  cur.n = 0;
   }
   return true;
 }
@@ -192,7 +193,8 @@ __global__ void __launch_bounds__(256) bulk_meta_kernel(BulkParams p) {
   cur.t = rfl(blockIdx.x * waves + (threadIdx.x >> 6));
   if (cur.t >= ntiles) return;
   load_tile(p, cur, tj);
-  cur.b = cur.n = 0;
+  cur.b = 0;  // two statements: the chained form kept Cursor in scratch
+  cur.n = 0;
   cur.live = next_job(p, cur, tj, stride, ntiles);
   while (rfl((uint32_t)cur.live)) {
     const uint32_t e = cur.b + lane;
@@ -225,7 +227,8 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p) {
   cur.t = rfl(blockIdx.x * waves + (threadIdx.x >> 6));
   if (cur.t >= ntiles) return;
   load_tile(p, cur, tj);
-  cur.b = cur.n = 0;
+  cur.b = 0;  // two statements: the chained form kept Cursor in scratch
+  cur.n = 0;
   cur.live = next_job(p, cur, tj, stride, ntiles);
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   // ring slot u: payload chunk, destination (slot | bank << 31), flags, sender's CRC

@@ -11,9 +11,10 @@ step() {  # step NAME TIMEOUT CMD...
   tail -${TAILN:-4} gpurun_out/$name.log
   if [ $rc -ne 0 ] || fault gpurun_out/$name.log; then echo "$name FAILED rc=$rc"; exit 1; fi
 }
-for what in ${STEPS:-smoke tests bench wire rehearse}; do
+for what in ${STEPS:-smoke parity tests bench wire rehearse}; do
   case $what in
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    parity) TAILN=3 step gpu_parity 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 240 --timeout-method thread -p no:cacheprovider ;;
     tests) TAILN=6 step gpu_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -p no:cacheprovider ;;
     bench) step bench 400 python bench.py ${BENCH_ARGS:---cpu-seconds 10} ;;
     wire) step bench_wire 400 python bench.py --wire-all --no-cpu-baseline ;;
