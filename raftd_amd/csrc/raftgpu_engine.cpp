@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -28,6 +29,20 @@ static int fail(int code, const std::string& msg) {
   do {                                                                                          \
     hipError_t _e = (x);                                                                        \
     if (_e != hipSuccess) return fail(RG_EHIP, std::string(#x) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+// RAFTGPU_SYNC_DEBUG=1: synchronise after every launch so a fault names its kernel (debug only)
+static const bool g_sync_debug = [] {
+  const char* v = getenv("RAFTGPU_SYNC_DEBUG");
+  return v && *v == '1';
+}();
+#define LAUNCH(x, st, name)                                                                          \
+  do {                                                                                              \
+    HIPCHK(x);                                                                                      \
+    if (g_sync_debug) {                                                                             \
+      hipError_t _s = hipStreamSynchronize(st);                                                     \
+      if (_s != hipSuccess) return fail(RG_EHIP, std::string(name) + ": " + hipGetErrorString(_s)); \
+    }                                                                                               \
   } while (0)
 
 #define RGCHK(x)             \
@@ -535,7 +550,7 @@ static int tick_impl(rg_engine* e, const rg_tick_input* in, bool device_ptrs) {
   const int a = (int)(e->t & 1);
   if (e->t >= 2) HIPCHK(hipStreamWaitEvent(e->stream, e->bulk_done[a], 0));
   if (e->timing) RGCHK(timing_event(e, e->stream));
-  HIPCHK(launch_control(p, e->stream));
+  LAUNCH(launch_control(p, e->stream), e->stream, "control_kernel");
   if (e->timing) RGCHK(timing_event(e, e->stream));
   HIPCHK(hipEventRecord(e->ctl_done[a], e->stream));
 #ifdef RG_OVERLAP  // ablation: bulk(t) on a second stream beside control(t+1)
@@ -545,7 +560,7 @@ static int tick_impl(rg_engine* e, const rg_tick_input* in, bool device_ptrs) {
 #endif
   HIPCHK(hipStreamWaitEvent(bs, e->ctl_done[a], 0));
   if (e->timing) RGCHK(timing_event(e, bs));
-  HIPCHK(launch_bulk(bulk_params(e), bs, e->bulk_grid));
+  LAUNCH(launch_bulk(bulk_params(e), bs, e->bulk_grid), bs, "bulk_kernel");
   if (e->timing) RGCHK(timing_event(e, bs));
   HIPCHK(hipEventRecord(e->bulk_done[a], bs));
   e->t++;
@@ -714,7 +729,7 @@ int rg_wire_plan(rg_engine* e, uint64_t* send_bytes) {
   }
   if (int jrc = join(e)) return jrc;
   HIPCHK(hipSetDevice(e->c.device));
-  HIPCHK(launch_wire_plan(wire_params(e), e->bounds, e->stream));
+  LAUNCH(launch_wire_plan(wire_params(e), e->bounds, e->stream), e->stream, "wire plan");
   HIPCHK(hipMemcpyAsync(e->h_bounds, e->bounds, (N + 1) * 8, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   for (uint32_t r = 0; r < N; ++r) {
@@ -739,7 +754,7 @@ int rg_wire_pack(rg_engine* e, void* send_buf, uint64_t send_cap) {
   if (off > send_cap) return fail(RG_EFULL, "rg_wire_pack: send buffer smaller than the planned regions");
   if (off && !send_buf) return fail(RG_EINVAL, "rg_wire_pack: null buffer");
   w.send = (uint8_t*)send_buf;
-  HIPCHK(launch_wire_pack(w, e->stream));
+  LAUNCH(launch_wire_pack(w, e->stream), e->stream, "pack_kernel");
   e->planned = false;
   return RG_OK;
 }
@@ -759,7 +774,7 @@ int rg_wire_recv(rg_engine* e, const void* recv_buf, const uint64_t* recv_bytes)
   }
   if (off && !recv_buf) return fail(RG_EINVAL, "rg_wire_recv: null buffer");
   w.recv = (const uint8_t*)recv_buf;
-  HIPCHK(launch_wire_unpack(w, e->stream));
+  LAUNCH(launch_wire_unpack(w, e->stream), e->stream, "unpack_kernel");
   e->recv = (const uint8_t*)recv_buf;
   e->wire_ready = true;
   return RG_OK;

@@ -104,7 +104,10 @@ struct Job {
 };
 
 __device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l) {
-  return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) | __builtin_amdgcn_readlane((uint32_t)v, l);
+  // readlane returns int: widen through uint32_t, or bit 31 of the low word sign-extends over the high word
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  return ((uint64_t)hi << 32) | lo;
 }
 
 __device__ __forceinline__ Job load_job(const BulkParams& p, uint32_t q, uint32_t j) {

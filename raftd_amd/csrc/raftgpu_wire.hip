@@ -137,7 +137,10 @@ __device__ __forceinline__ uint32_t find_rank(const uint32_t* beg, uint32_t N, u
 __device__ __forceinline__ uint64_t table_bytes(uint32_t units) { return ((uint64_t)units * 8 + 255) & ~255ull; }
 
 __device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l) {
-  return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) | __builtin_amdgcn_readlane((uint32_t)v, l);
+  // readlane returns int: widen through uint32_t, or bit 31 of the low word sign-extends over the high word
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  return ((uint64_t)hi << 32) | lo;
 }
 
 __global__ void __launch_bounds__(256) pack_kernel(WireParams w) {

@@ -109,3 +109,8 @@ def test_two_processes_gloo():
                          capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
     assert "dist parity ok" in out.stdout
+
+
+def test_cluster_full_batches():
+    cfg = dict(CHAOS, log_capacity=256, max_entries_per_msg=64, snapshot_entries=120, payload_bytes=16)
+    run_chaos(3, dict(groups=9, replicas=3, seed=37, **cfg), ticks=120, seed=65, p_camp=0.04)

@@ -138,3 +138,11 @@ def test_compaction_and_snapshot_path():
         for rid in range(12):
             snaps += sum(1 for m in ora.msgs(rid, 2) if m["type"] == 16)
     assert snaps > 0
+
+
+def test_chaos_full_batches():
+    """64-entry jobs under loss, elections and truncation: entries 32..63 of a job take their bank
+    bits from the high half of the job's 64-bit masks (a sign-extending lane broadcast once set
+    that half whenever entry 31's bit was set)."""
+    cfg = dict(CHAOS, log_capacity=256, max_entries_per_msg=64, snapshot_entries=120, payload_bytes=16)
+    run_pair(dict(groups=8, replicas=3, seed=31, **cfg), ticks=150, seed=64, p_camp=0.04)
