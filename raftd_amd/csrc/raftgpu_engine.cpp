@@ -217,7 +217,7 @@ static BulkParams bulk_params(rg_engine* e) {  // for tick e->t
   b.E = e->c.max_entries_per_msg; b.J = e->J; b.crc_const = e->crc_const; b.tile = e->bulk_tile;
   b.job64 = e->job64[a]; b.job32 = e->job32[a]; b.jcnt = e->jcnt[a];
   b.info = e->info; b.pay = e->pay; b.slabs = e->slabs; b.crc_err = e->crc_err; b.crc_tab = e->crc_tab;
-  b.slab_by_q = e->slab_rows == e->nrep && e->pl.N > 1;
+  b.wire_mode = e->wire ? 1u : 0u;
   b.wire = e->recv;
   return b;
 }
@@ -259,7 +259,8 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   e->c.ranks = N;
   e->nrep = c.groups * c.replicas;
   e->pl = make_placement(N, c.rank, c.wire_all);
-  e->slab_rows = N > 1 ? e->nrep : c.groups;
+  e->wire = N > 1 || c.wire_all;
+  e->slab_rows = e->wire ? e->nrep : c.groups;  // wire engines: one slab row per replica (bulk_kernel<LG, true>)
   e->J = (c.replicas - 1) * c.max_msgs_per_pair + 2;  // >= appends one step can make
   const uint64_t n = e->nrep, L = c.log_capacity, P = c.payload_bytes, R = c.replicas, K = c.max_msgs_per_pair,
                  E = c.max_entries_per_msg, G = c.groups, J = e->J;
@@ -292,7 +293,6 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if (rc == RG_OK) rc = dalloc(e, &e->d_sum, 64);
   // exchange units: every remote (s, d, j) outbox column, per destination rank (send) and per
   // source rank (receive), each in (s, d, j) order — the same list on both ends of a link
-  e->wire = N > 1 || c.wire_all;
   if (rc == RG_OK && e->wire) {
     std::vector<std::vector<uint32_t>> snd(N), rcv(N);
     for (uint32_t s = 0; s < R; ++s)

@@ -122,13 +122,13 @@ struct TickParams {
 
 struct BulkParams {
   uint32_t G, nrep, L, P, E, J, crc_const, tile;  // tile: replicas per wave work item (1..64)
-  uint32_t slab_by_q;    // slab rows per replica (ranks > 1) instead of per group
+  uint32_t wire_mode;    // wire engine (ranks > 1 or wire_all): SRC_WIRE jobs, one slab row per replica
   const uint64_t* job64;
   const uint32_t* job32;
   const uint32_t* jcnt;
   uint2* info;           // [2 banks][nrep][L] {crc, type<<24 | len}
   uint8_t* pay;          // [2 banks][nrep][L][P]
-  const uint8_t* slabs;  // [nslab][rows][E][P], rows = G (one rank) or nrep (slab_by_q)
+  const uint8_t* slabs;  // [nslab][rows][E][P], rows = G, or nrep in wire_mode
   const uint8_t* wire;   // receive buffer of the last exchange (SRC_WIRE jobs)
   uint32_t* crc_err;     // [nrep] sticky ERR_CRC from payload verification
   const uint32_t* crc_tab;

@@ -148,20 +148,22 @@ __device__ __forceinline__ void load_tile(const BulkParams& p, Cursor& cur, Tile
   cur.j = cur.njl = 0;
 }
 
+template <bool WIRE>
 __device__ __forceinline__ void set_job(const BulkParams& p, Cursor& cur, const Job& jb) {
   cur.first = jb.first; cur.dm = jb.dm; cur.sm = jb.sm; cur.hm = jb.hm; cur.tm = jb.tm;
   cur.n = jb.meta & 0xFF; cur.b = (jb.meta >> 8) & 0xFF; cur.kind = jb.meta >> 16; cur.src = jb.src;
-  cur.g = p.slab_by_q ? cur.q : cur.q % p.G;  // proposal slab row
+  cur.g = WIRE ? cur.q : cur.q % p.G;  // proposal slab row: per replica across ranks, per group on one
 }
 
 // Move the cursor one position: the replica's next job, the tile's next replica, or the next
 // tile (whose descriptors arrive in one round trip; that pass issues nothing). A job with no
 // entries left to write simply yields an empty pass. Returns false once the wave is done.
+template <bool WIRE = false>
 __device__ __forceinline__ bool next_job(const BulkParams& p, Cursor& cur, TileJobs& tj, uint32_t stride,
                                          uint32_t ntiles) {
   if (cur.j + 1 < cur.njl) {
     ++cur.j;
-    set_job(p, cur, load_job(p, cur.q, cur.j));
+    set_job<WIRE>(p, cur, load_job(p, cur.q, cur.j));
   } else if (cur.m) {
     const uint32_t l = rfl((uint32_t)__ffsll((long long)cur.m) - 1);
     cur.m &= cur.m - 1;
@@ -172,7 +174,7 @@ __device__ __forceinline__ bool next_job(const BulkParams& p, Cursor& cur, TileJ
     jb.first = rl64(tj.j0.first, l); jb.dm = rl64(tj.j0.dm, l); jb.sm = rl64(tj.j0.sm, l);
     jb.hm = rl64(tj.j0.hm, l); jb.tm = rl64(tj.j0.tm, l);
     jb.meta = __builtin_amdgcn_readlane(tj.j0.meta, l); jb.src = __builtin_amdgcn_readlane(tj.j0.src, l);
-    set_job(p, cur, jb);
+    set_job<WIRE>(p, cur, jb);
   } else {
     cur.t += stride;
     if (cur.t >= ntiles) return false;
@@ -212,7 +214,9 @@ __global__ void __launch_bounds__(256) bulk_meta_kernel(BulkParams p) {
 }
 
 // P = 16 << LG bytes per entry: 2^LG lanes per entry (16 B each), 64 >> LG entries per step.
-template <int LG>
+// WIRE: the engine exchanges messages with other ranks (SRC_WIRE jobs, slab rows per replica);
+// one-rank engines run the variant without those paths.
+template <int LG, bool WIRE>
 __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p) {
   constexpr uint32_t NCH = 1u << LG, EPI = 64u >> LG, P = 16u << LG;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -222,7 +226,7 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p) {
   const uint32_t waves = blockDim.x >> 6, lane = lane_id();
   const uint32_t stride = gridDim.x * waves, T = p.tile;
   const uint32_t ntiles = (p.nrep + T - 1) / T;
-  const uint64_t n64 = p.nrep, L = p.L, rows = p.slab_by_q ? p.nrep : p.G;
+  const uint64_t n64 = p.nrep, L = p.L, rows = WIRE ? p.nrep : p.G;
   const uint32_t c = lane & (NCH - 1), ei = lane >> LG;
   const Crc crc{lds, lds + CRC_T_WORDS, lds + CRC_T_WORDS + CRC_N_WORDS + c * CRC_SH_STRIDE};
   Cursor cur{};
@@ -232,7 +236,7 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p) {
   load_tile(p, cur, tj);
   cur.b = 0;  // two statements: the chained form kept Cursor in scratch
   cur.n = 0;
-  cur.live = next_job(p, cur, tj, stride, ntiles);
+  cur.live = next_job<WIRE>(p, cur, tj, stride, ntiles);
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   // ring slot u: payload chunk, destination (slot | bank << 31), flags, sender's CRC
   u32x4 x[BULK_U];
@@ -284,7 +288,7 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p) {
         const bool act = valid && ((cur.hm >> e) & 1ull);
         const uint32_t slot = (uint32_t)((cur.first + e) & (L - 1));
         const uint32_t db = valid ? (uint32_t)(cur.dm >> e) & 1u : 0u;
-        const bool ring = cur.kind == SRC_RING, wire = cur.kind == SRC_WIRE;
+        const bool ring = cur.kind == SRC_RING, wire = WIRE && cur.kind == SRC_WIRE;
         ds[u] = slot | (db << 31);
         fl[u] = (act ? F_ACT : 0u) | ((valid && c == 0) ? F_WRITER : 0u) | (((cur.tm >> e) & 1ull) ? F_TYPE : 0u) |
                 (((ring || wire) && act) ? F_CHECK : 0u);
@@ -304,7 +308,7 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p) {
         cur.b += step ? EPI : 0u;
       }
     }
-    if (cur.live && cur.b >= cur.n) cur.live = next_job(p, cur, tj, stride, ntiles);
+    if (cur.live && cur.b >= cur.n) cur.live = next_job<WIRE>(p, cur, tj, stride, ntiles);
   } while (rfl((uint32_t)(vmask != 0 || cur.live)));
 }
 
@@ -316,31 +320,35 @@ static int lg_of(uint32_t P) {
 
 int bulk_lds_bytes(uint32_t P) { return P ? (int)((CRC_T_WORDS + CRC_N_WORDS + (P / 16) * CRC_SH_STRIDE) * 4) : 16; }
 
-template <class F>
-static hipError_t with_bulk(uint32_t P, F f) {
-  if (!P) return f(bulk_meta_kernel);
+template <bool W, class F>
+static hipError_t with_bulk_w(uint32_t P, F f) {
   switch (lg_of(P)) {
-    case 0: return f(bulk_kernel<0>);
-    case 1: return f(bulk_kernel<1>);
-    case 2: return f(bulk_kernel<2>);
-    case 3: return f(bulk_kernel<3>);
-    case 4: return f(bulk_kernel<4>);
-    case 5: return f(bulk_kernel<5>);
-    case 6: return f(bulk_kernel<6>);
+    case 0: return f(bulk_kernel<0, W>);
+    case 1: return f(bulk_kernel<1, W>);
+    case 2: return f(bulk_kernel<2, W>);
+    case 3: return f(bulk_kernel<3, W>);
+    case 4: return f(bulk_kernel<4, W>);
+    case 5: return f(bulk_kernel<5, W>);
+    case 6: return f(bulk_kernel<6, W>);
     default: return hipErrorInvalidValue;
   }
+}
+template <class F>
+static hipError_t with_bulk(uint32_t P, bool wire, F f) {
+  if (!P) return f(bulk_meta_kernel);
+  return wire ? with_bulk_w<true>(P, f) : with_bulk_w<false>(P, f);
 }
 
 int bulk_blocks_per_cu(uint32_t P) {
   int n = 0;
-  const hipError_t r = with_bulk(P, [&](auto k) {
+  const hipError_t r = with_bulk(P, false, [&](auto k) {
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 256, bulk_lds_bytes(P));
   });
   return (r == hipSuccess && n > 0) ? n : 1;
 }
 
 hipError_t launch_bulk(const BulkParams& p, hipStream_t s, int grid) {
-  return with_bulk(p.P, [&](auto k) {
+  return with_bulk(p.P, p.wire_mode != 0, [&](auto k) {
     hipLaunchKernelGGL(k, dim3(grid), dim3(256), bulk_lds_bytes(p.P), s, p);
     return hipGetLastError();
   });
