@@ -132,6 +132,18 @@ typedef struct rg_traffic {
   uint64_t bulk_bytes;
 } rg_traffic;
 
+/* One entry of the committed-entry copy-back (rg_apply_committed): what dragonboat hands to
+ * IOnDiskStateMachine.Update and raftd forwards as {"Index", "Cmd"} to POST /UpdateEntries with
+ * headers raftd-node-id = shard, raftd-replica-id = replica (raft/state_machine.go:63-99,126-166). */
+typedef struct rg_apply_entry {
+  uint64_t index;      /* statemachine.Entry.Index */
+  uint64_t group;      /* global shard id (raftd-node-id) */
+  uint32_t replica_id; /* raftd-replica-id: slot + 1 */
+  uint32_t len;        /* Cmd bytes, at payload + k * payload_bytes */
+  uint32_t crc;        /* CRC-32 of Cmd as stored in the log */
+  uint32_t rid;        /* local replica id */
+} rg_apply_entry;
+
 typedef struct rg_engine rg_engine;
 
 int rg_create(const rg_config* cfg, rg_engine** out);
@@ -196,6 +208,14 @@ int rg_last_tick_traffic(rg_engine* e, rg_traffic* out);
 int rg_wire_plan(rg_engine* e, uint64_t* send_bytes /*[ranks]*/);
 int rg_wire_pack(rg_engine* e, void* send_buf, uint64_t send_cap);
 int rg_wire_recv(rg_engine* e, const void* recv_buf, const uint64_t* recv_bytes /*[ranks]*/);
+/* Committed-entry copy-back: the non-empty application entries that the
+ * replicas whose slot bit is set in slot_mask applied in the last tick — config changes, leader
+ * no-ops and snapshot-restored ranges excluded, as dragonboat's rsm does before Update — in
+ * (local replica, index) order. Compacted on the device, then copied back by one hipMemcpyAsync
+ * per array into entries[cap] and payload[cap * payload_bytes] (host memory; pinned is fastest).
+ * *n = the count; if *n > cap nothing is copied and RG_EFULL is returned. Synchronous. */
+int rg_apply_committed(rg_engine* e, uint32_t slot_mask, rg_apply_entry* entries, uint8_t* payload, uint64_t cap,
+                       uint64_t* n);
 /* Global group and global replica id (group·replicas + slot) of local replica rid. */
 int rg_global_id(rg_engine* e, uint32_t rid, uint64_t* group, uint64_t* global_rid);
 /* Device bytes held by the engine. */

@@ -51,6 +51,9 @@ typedef struct {
   uint8_t* logpay;
   outbox_t ob[2];
   uint32_t g, s; /* group, slot */
+  /* apply window of the last step: entries apply_lo .. applied went to the state machine
+   * (rsm → IOnDiskStateMachine.Update); a range restored from a snapshot does not */
+  uint64_t apply_lo, restored_at;
 } rep_t;
 
 struct or_engine {
@@ -442,6 +445,7 @@ static void handle_install_snapshot(or_engine* e, rep_t* r, const or_msg_view* m
     r->marker = r->last = r->committed = r->snap_index = si;
     r->marker_term = r->snap_term = st;
     resp.log_index = r->last;
+    r->restored_at = si;
   }
   send_msg(e, r, &resp);
 }
@@ -702,7 +706,8 @@ static void handle(or_engine* e, rep_t* r, const msg_in_t* mi) {
 static void step_replica(or_engine* e, rep_t* r) {
   const or_tick_input* in = e->in;
   uint32_t R = e->c.replicas, K = e->c.max_msgs_per_pair;
-  uint64_t marker_start = r->marker;
+  uint64_t marker_start = r->marker, applied_start = r->applied;
+  r->restored_at = 0;
   outbox_t* ob = cur_ob(e, r);
   memset(ob->n, 0, sizeof ob->n);
   memset(ob->emitted, 0, sizeof ob->emitted);
@@ -738,6 +743,7 @@ static void step_replica(or_engine* e, rep_t* r) {
     handle(e, r, &mi);
   }
   /* 5. apply + snapshot + compaction */
+  r->apply_lo = u64max(applied_start, r->restored_at) + 1;
   r->applied = r->committed;
   if (e->c.snapshot_entries && r->applied - r->snap_index >= e->c.snapshot_entries) {
     r->snap_index = r->applied;
@@ -1011,4 +1017,32 @@ int or_deliver(or_engine* e, uint32_t rid_src, const or_msg_view* m) {
     ob->n_ents += m->nent;
   }
   return 0;
+}
+
+/* The non-empty application entries replica rid handed to the state machine in the last step
+ * (dragonboat's rsm skips config changes and empty entries before Update), read from the log ring
+ * where they stay until the next step may reuse their slots (capacity rule). */
+int or_get_applied(const or_engine* e, uint32_t rid, uint64_t* index, or_entry_view* out, uint8_t* payload,
+                   uint32_t cap) {
+  if (rid >= e->nrep) return -1;
+  const rep_t* r = &e->reps[rid];
+  uint32_t n = 0;
+  for (uint64_t i = r->apply_lo ? r->apply_lo : 1; i <= r->applied; ++i) {
+    const ent_t* en = log_at(e, r, i);
+    if (en->type != OR_ENTRY_APP || en->len == 0) continue;
+    if (n < cap) {
+      if (index) index[n] = i;
+      if (out) {
+        out[n].term = en->term;
+        out[n].type = en->type;
+        out[n].len = en->len;
+        out[n].crc = en->crc;
+        out[n]._pad = 0;
+      }
+      if (payload && e->c.payload_bytes)
+        memcpy(payload + (size_t)n * e->c.payload_bytes, logpay_at(e, r, i), e->c.payload_bytes);
+    }
+    n++;
+  }
+  return (int)n;
 }

@@ -103,6 +103,10 @@ int or_import_replica(or_engine* e, uint32_t rid, const or_replica_view* v,
 /* Append a message to rid_src's most recent outbox so it is delivered next tick. Replicate
  * entries are taken from the sender's current log (indices log_index+1 ..). */
 int or_deliver(or_engine* e, uint32_t rid_src, const or_msg_view* m);
+/* Non-empty application entries replica rid applied in the last step (IOnDiskStateMachine.Update
+ * input), in index order. Returns the count; fills up to cap. Any output may be NULL. */
+int or_get_applied(const or_engine* e, uint32_t rid, uint64_t* index, or_entry_view* out, uint8_t* payload,
+                   uint32_t cap);
 /* Proposal payload generator. */
 void or_payload(const or_engine* e, uint32_t slab, uint32_t group, uint32_t entry, uint8_t* out);
 uint32_t or_crc32(const uint8_t* p, size_t n);

@@ -99,6 +99,7 @@ def lib():
         L.or_get_msgs.argtypes = [vp, u32, u32, C.POINTER(MsgView), u32]
         L.or_get_msg_terms.argtypes = [vp, u32, u32, u32, C.POINTER(C.c_uint64), u32]
         L.or_get_entry.argtypes = [vp, u32, u64, C.POINTER(EntryView), C.c_void_p]
+        L.or_get_applied.argtypes = [vp, u32, C.c_void_p, C.c_void_p, C.c_void_p, u32]
         L.or_import_replica.argtypes = [vp, u32, C.POINTER(ReplicaView), C.c_void_p, C.c_void_p, C.c_void_p]
         L.or_deliver.argtypes = [vp, u32, C.POINTER(MsgView)]
         L.or_payload.argtypes = [vp, u32, u32, u32, C.c_void_p]
@@ -222,6 +223,19 @@ class Oracle:
         if pay is not None:
             d["payload"] = bytes(pay[:ev.len])
         return d
+
+    def applied_entries(self, rid):
+        """Non-empty application entries rid handed to the state machine in the last step:
+        [(index, len, crc, payload)] in index order (oracle side of rg_apply_committed)."""
+        n = self.L.or_get_applied(self.h, rid, None, None, None, 0)
+        if n <= 0:
+            return []
+        P = self.cfg["payload_bytes"]
+        idx = (C.c_uint64 * n)()
+        ev = (EntryView * n)()
+        pay = (C.c_uint8 * max(1, n * P))()
+        self.L.or_get_applied(self.h, rid, idx, ev, pay, n)
+        return [(idx[k], ev[k].len, ev[k].crc, bytes(pay[k * P:k * P + ev[k].len])) for k in range(n)]
 
     def log_terms(self, rid):
         r = self.replica(rid)

@@ -61,6 +61,7 @@ struct Ctl {
   uint64_t rm[R], rn[R], rs[R];  // remote match / next / snapshot index
   uint32_t rt[R];                // remote state
   uint64_t last_start, sent_hi, rw_lo, rw_hi, marker_start;
+  uint64_t applied_start, restored_at;  // apply window: entries restored from a snapshot are not Update()d
   uint64_t oc, em;  // per destination: enqueued / emitted counts, 8 bits each
   uint32_t nj;      // jobs emitted
 
@@ -86,6 +87,7 @@ struct Ctl {
       rt[j] = p.rst_in[j * n + q];
     });
     last_start = last; sent_hi = 0; rw_lo = ~0ull; rw_hi = 0; marker_start = marker;
+    applied_start = applied; restored_at = 0;
     oc = 0; em = 0; nj = 0;
   }
 
@@ -377,6 +379,7 @@ struct Ctl {
       marker = last = committed = snap_index = si;
       marker_term = snap_term = stt;
       li = last;
+      restored_at = si;
     }
     send_simple(M_REPLICATE_RESP, from, 0, li);
   }
@@ -633,6 +636,7 @@ struct Ctl {
       p.cnt_out[((uint64_t)s * R + j) * p.G + g] = get8(oc, j);
     });
     p.jcnt[q] = nj;
+    if (p.apply_lo) p.apply_lo[q] = umax64(applied_start, restored_at) + 1;
   }
 #undef RG_GET
 #undef RG_SET

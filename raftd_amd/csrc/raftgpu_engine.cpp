@@ -105,6 +105,12 @@ struct rg_engine {
   std::vector<uint64_t> send_bytes;
   bool planned = false, wire_ready = false;
   const uint8_t* recv = nullptr;  // receive buffer the next tick's SRC_WIRE jobs read
+  // committed-entry copy-back (raftgpu_apply.hip)
+  uint64_t* apply_lo = nullptr;
+  uint32_t* acnt = nullptr;
+  uint64_t *aoff = nullptr, *absum = nullptr;
+  uint8_t* astage = nullptr;
+  uint64_t astage_bytes = 0;
 };
 
 // ---------------------------------------------------------------- CRC-32/IEEE tables
@@ -193,6 +199,7 @@ static TickParams params(rg_engine* e) {
   p.cnt_in = e->cnt[b]; p.cnt_out = e->cnt[a];
   p.job64 = e->job64[a]; p.job32 = e->job32[a]; p.jcnt = e->jcnt[a];
   p.rhdr = e->rhdr; p.rmt = e->rmt; p.rcnt = e->rcnt;
+  p.apply_lo = e->apply_lo;
   return p;
 }
 
@@ -291,6 +298,10 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if (rc == RG_OK) rc = dalloc(e, &e->d_campaign, n * N);
   if (rc == RG_OK) rc = dalloc(e, &e->d_isolate, n * N);
   if (rc == RG_OK) rc = dalloc(e, &e->d_sum, 64);
+  if (rc == RG_OK) rc = dalloc(e, &e->apply_lo, n * 8);
+  if (rc == RG_OK) rc = dalloc(e, &e->acnt, n * 4);
+  if (rc == RG_OK) rc = dalloc(e, &e->aoff, (n + 1) * 8);
+  if (rc == RG_OK) rc = dalloc(e, &e->absum, ((n + 1023) / 1024 + 1) * 8);
   // exchange units: every remote (s, d, j) outbox column, per destination rank (send) and per
   // source rank (receive), each in (s, d, j) order — the same list on both ends of a link
   if (rc == RG_OK && e->wire) {
@@ -441,6 +452,7 @@ int rg_bootstrap(rg_engine* e) {
   const uint64_t R = e->c.replicas, G = e->c.groups;
   for (int b = 0; b < 2; ++b) HIPCHK(hipMemsetAsync(e->cnt[b], 0, R * R * G * 4, e->stream));
   if (e->rcnt) HIPCHK(hipMemsetAsync(e->rcnt, 0, R * R * G * 4, e->stream));
+  HIPCHK(hipMemsetAsync(e->apply_lo, 0, (uint64_t)e->nrep * 8, e->stream));
   e->planned = e->wire_ready = false;
   e->recv = nullptr;
   HIPCHK(hipMemsetAsync(e->crc_err, 0, (uint64_t)e->nrep * 4, e->stream));
@@ -708,6 +720,45 @@ int rg_leader(rg_engine* e, uint32_t group, uint64_t* leader_id, uint64_t* term,
   if (leader_id) *leader_id = bl;
   if (term) *term = bt;
   if (valid) *valid = bl != 0;
+  return RG_OK;
+}
+
+int rg_apply_committed(rg_engine* e, uint32_t slot_mask, rg_apply_entry* entries, uint8_t* payload, uint64_t cap,
+                       uint64_t* n) {
+  if (!e || !n) return fail(RG_EINVAL, "rg_apply_committed args");
+  if (int jrc = join(e)) return jrc;
+  const TickParams t = params(e);
+  ApplyParams a{};
+  a.G = t.G; a.R = t.R; a.nrep = t.nrep; a.L = t.L; a.P = t.P; a.slot_mask = slot_mask; a.pl = e->pl;
+  a.s64 = t.s64_in; a.apply_lo = e->apply_lo; a.tr = e->tr; a.info = e->info; a.pay = e->pay;
+  a.cnt = e->acnt; a.off = e->aoff; a.bsum = e->absum;
+  LAUNCH(launch_apply_count(a, (uint64_t*)e->d_sum, e->stream), e->stream, "apply count");
+  uint64_t total = 0;
+  HIPCHK(hipMemcpyAsync(&total, e->d_sum, 8, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  *n = total;
+  if (total == 0) return RG_OK;
+  if (total > cap) return fail(RG_EFULL, "rg_apply_committed: " + std::to_string(total) + " entries > cap");
+  if (!entries || (a.P && !payload)) return fail(RG_EINVAL, "rg_apply_committed: null output");
+  const uint64_t rb = total * sizeof(rg_apply_entry), pb = total * a.P;
+  if (rb + pb > e->astage_bytes) {
+    if (e->astage) {
+      (void)hipFree(e->astage);
+      e->allocs.erase(std::remove(e->allocs.begin(), e->allocs.end(), (void*)e->astage), e->allocs.end());
+      e->bytes -= e->astage_bytes;
+      e->astage = nullptr;
+      e->astage_bytes = 0;
+    }
+    const uint64_t nb = std::max<uint64_t>((rb + pb) * 5 / 4, 1 << 20);
+    RGCHK(dalloc(e, &e->astage, nb));
+    e->astage_bytes = nb;
+  }
+  a.out_rec = e->astage;
+  a.out_pay = e->astage + rb;
+  LAUNCH(launch_apply_gather(a, e->stream), e->stream, "apply gather");
+  HIPCHK(hipMemcpyAsync(entries, a.out_rec, rb, hipMemcpyDeviceToHost, e->stream));
+  if (pb) HIPCHK(hipMemcpyAsync(payload, a.out_pay, pb, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
   return RG_OK;
 }
 

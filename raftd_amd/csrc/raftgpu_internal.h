@@ -111,6 +111,7 @@ struct TickParams {
   const uint64_t* rhdr;
   const uint64_t* rmt;
   const uint32_t* rcnt;
+  uint64_t* apply_lo;      // [nrep] first index this step hands to the state machine (NULL: skip)
   uint64_t* job64;         // [J64_ROWS][J][nrep]
   uint32_t* job32;         // [J32_ROWS][J][nrep]
   uint32_t* jcnt;          // [nrep]
@@ -155,6 +156,28 @@ hipError_t launch_fill_slabs(uint8_t* slabs, uint32_t nslab, uint32_t G, uint32_
                              uint64_t seed, const Placement& pl, hipStream_t s);
 hipError_t launch_sum_committed(const TickParams& p, unsigned long long* out, hipStream_t s);
 hipError_t launch_traffic(const TickParams& p, unsigned long long* out6, hipStream_t s);
+// committed-entry copy-back (raftgpu_apply.hip): after a tick, the application entries each replica
+// applied in it, (apply_lo - 1, applied], gathered for IOnDiskStateMachine.Update
+struct ApplyParams {
+  uint32_t G, R, nrep, L, P;
+  uint32_t slot_mask;       // replicas whose slot bit is set
+  Placement pl;
+  const uint64_t* s64;      // current state (applied)
+  const uint64_t* apply_lo;
+  const uint64_t* tr;
+  const uint2* info;
+  const uint8_t* pay;
+  uint32_t* cnt;            // [nrep] entries per replica
+  uint64_t* off;            // [nrep + 1] exclusive scan
+  uint64_t* bsum;           // scan scratch
+  uint8_t* out_rec;         // [n] rg_apply_entry
+  uint8_t* out_pay;         // [n][P]
+};
+hipError_t launch_apply_count(const ApplyParams& a, uint64_t* total, hipStream_t s);
+hipError_t launch_apply_gather(const ApplyParams& a, hipStream_t s);
+// exclusive scan of n u32 into out[0..n] (out[n] = total); bsum: (n + 1023) / 1024 + 1 words
+hipError_t launch_scan_u32(const uint32_t* in, uint32_t n, uint64_t* bsum, uint64_t* out, hipStream_t s);
+
 // admin gathers / scatters behind the read / import / deliver entry points (raftgpu_admin.hip)
 struct AdminParams {
   TickParams t;              // the parameter block the next tick would use (s64_in = current state)

@@ -230,6 +230,15 @@ hipError_t launch_wire_plan(const WireParams& w, uint64_t* bounds, hipStream_t s
   return hipGetLastError();
 }
 
+hipError_t launch_scan_u32(const uint32_t* in, uint32_t n, uint64_t* bsum, uint64_t* out, hipStream_t st) {
+  if (!n) return hipMemsetAsync(out, 0, 8, st);
+  const uint32_t nb = (n + SCAN_B - 1) / SCAN_B;
+  hipLaunchKernelGGL(scan_reduce_kernel, dim3(nb), dim3(SCAN_T), 0, st, in, n, bsum);
+  hipLaunchKernelGGL(scan_blocks_kernel, dim3(1), dim3(SCAN_T), 0, st, bsum, nb);
+  hipLaunchKernelGGL(scan_apply_kernel, dim3(nb), dim3(SCAN_T), 0, st, in, n, bsum, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_wire_pack(const WireParams& w, hipStream_t st) {
   if (!w.U) return hipSuccess;
   hipLaunchKernelGGL(pack_kernel, dim3((w.U + 3) / 4), dim3(256), 0, st, w);

@@ -69,6 +69,15 @@ class Traffic(C.Structure):
                                           "leader_appended", "algorithmic_bytes", "bulk_bytes")]
 
 
+class ApplyEntry(C.Structure):
+    _fields_ = [("index", C.c_uint64), ("group", C.c_uint64), ("replica_id", C.c_uint32), ("len", C.c_uint32),
+                ("crc", C.c_uint32), ("rid", C.c_uint32)]
+
+
+APPLY_DTYPE = np.dtype([("index", "<u8"), ("group", "<u8"), ("replica_id", "<u4"), ("len", "<u4"),
+                        ("crc", "<u4"), ("rid", "<u4")])
+
+
 class TickInput(C.Structure):
     _fields_ = [("prop_target", C.c_void_p), ("prop_count", C.c_void_p), ("campaign", C.c_void_p),
                 ("isolate", C.c_void_p), ("flags", C.c_uint32), ("_pad", C.c_uint32)]
@@ -82,7 +91,8 @@ EXPORTS = ["rg_create", "rg_destroy", "rg_bootstrap", "rg_fill_slabs", "rg_tick"
            "rg_set_stream", "rg_sync", "rg_tick_count", "rg_read_replicas", "rg_read_msgs",
            "rg_read_entries", "rg_import_replica", "rg_deliver", "rg_leader", "rg_sum_committed",
            "rg_device_bytes", "rg_last_error", "rg_last_tick_traffic", "rg_join",
-           "rg_timing", "rg_kernel_ms", "rg_wire_plan", "rg_wire_pack", "rg_wire_recv", "rg_global_id"]
+           "rg_timing", "rg_kernel_ms", "rg_wire_plan", "rg_wire_pack", "rg_wire_recv", "rg_global_id",
+           "rg_apply_committed"]
 
 _lib = None
 
@@ -123,6 +133,7 @@ def load_library(path: str = LIB_PATH):
         "rg_wire_pack": ([vp, vp, u64], i32),
         "rg_wire_recv": ([vp, vp, C.POINTER(C.c_uint64)], i32),
         "rg_global_id": ([vp, u32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)], i32),
+        "rg_apply_committed": ([vp, u32, vp, vp, u64, C.POINTER(C.c_uint64)], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -334,6 +345,23 @@ class Engine:
     def wire_recv(self, recv_ptr: int, recv_bytes):
         rb = (C.c_uint64 * self.ranks)(*recv_bytes)
         self._check(self.L.rg_wire_recv(self.h, C.c_void_p(recv_ptr or None), rb))
+
+    def apply_committed(self, slot_mask: int = 0xFF, cap: int = None):
+        """Committed-entry copy-back of the last tick (rg_apply_committed): a structured array
+        (APPLY_DTYPE: index, group, replica_id, len, crc, rid) and the payloads, one row of
+        payload_bytes per entry, as numpy arrays."""
+        P = self.cfg["payload_bytes"]
+        n = C.c_uint64()
+        if cap is None:  # size with a count-only call
+            rc = self.L.rg_apply_committed(self.h, slot_mask, None, None, 0, C.byref(n))
+            if rc < 0 and rc != RG_EFULL:
+                self._check(rc)
+            cap = n.value
+        recs = np.zeros(max(cap, 1), APPLY_DTYPE)
+        pay = np.zeros((max(cap, 1), max(P, 1)), np.uint8)
+        self._check(self.L.rg_apply_committed(self.h, slot_mask, recs.ctypes.data, pay.ctypes.data, cap, C.byref(n)))
+        k = n.value
+        return recs[:k], pay[:k, :P]
 
     def global_id(self, rid: int):
         """(global group, global replica id) of local replica rid."""

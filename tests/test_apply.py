@@ -1,0 +1,100 @@
+"""The /UpdateEntries driver (raftd_amd/apply.py) against raftd's OnDiskStateMachine.Update /
+doReqWithContext (/root/reference/raft/state_machine.go:63-99, 136-166), with a local HTTP app."""
+import base64
+import json
+import threading
+from http.server import BaseHTTPRequestHandler, HTTPServer
+
+import numpy as np
+import pytest
+
+from raftd_amd.apply import Applier, HighStatusCode, batches, parse_results, post_update, update_body
+from raftd_amd.engine import APPLY_DTYPE
+
+
+def fake_batch():
+    recs = np.zeros(5, APPLY_DTYPE)
+    rows = [(7, 3, 2, 5, 4), (8, 3, 2, 5, 4), (9, 3, 2, 3, 4), (12, 17, 1, 4, 9), (13, 17, 1, 2, 9)]
+    for k, (idx, g, rep, ln, rid) in enumerate(rows):
+        recs[k] = (idx, g, rep, ln, 0, rid)
+    pay = np.zeros((5, 16), np.uint8)
+    for k in range(5):
+        pay[k, :recs[k]["len"]] = np.arange(recs[k]["len"]) + 10 * k
+    return recs, pay
+
+
+def test_batches_split_per_replica():
+    bs = batches(*fake_batch())
+    assert [(b.group, b.replica_id, b.rid, b.indices) for b in bs] == [(3, 2, 4, [7, 8, 9]), (17, 1, 9, [12, 13])]
+    assert bs[0].cmds[2] == bytes([20, 21, 22])
+
+
+def test_update_body_matches_go_encoding():
+    # encoding/json of map[string]any{"Entries": []updateEntry{{5, []byte{0,1,2,3}}, {6, "hi?>"}}}
+    body = update_body([5, 6], [b"\x00\x01\x02\x03", b"hi?>"])
+    assert body == b'{"Entries":[{"Index":5,"Cmd":"AAECAw=="},{"Index":6,"Cmd":"aGk/Pg=="}]}'
+
+
+def test_parse_results_only_when_lengths_match():
+    ok = json.dumps({"Results": [{"Value": 1, "Data": base64.b64encode(b"x").decode()}, {"Value": 2, "Data": None}]})
+    assert parse_results(ok.encode(), 2) == [(1, b"x"), (2, b"")]
+    assert parse_results(ok.encode(), 3) is None
+    assert parse_results(b'{"Result": []}', 0) is None  # README's "Result" key is ignored
+
+
+class App(BaseHTTPRequestHandler):
+    seen = []
+    status = 200
+
+    def do_POST(self):
+        n = int(self.headers["content-length"])
+        body = self.rfile.read(n)
+        App.seen.append((self.path, {k.lower(): v for k, v in self.headers.items()}, body))
+        if App.status != 200:
+            self.send_response(App.status)
+            self.end_headers()
+            self.wfile.write(b"boom")
+            return
+        ents = json.loads(body)["Entries"]
+        out = json.dumps({"Results": [{"Value": e["Index"] * 10, "Data": e["Cmd"]} for e in ents]}).encode()
+        self.send_response(200)
+        self.send_header("content-type", "application/json")
+        self.end_headers()
+        self.wfile.write(out)
+
+    def log_message(self, *a):
+        pass
+
+
+@pytest.fixture
+def app():
+    srv = HTTPServer(("127.0.0.1", 0), App)
+    th = threading.Thread(target=srv.serve_forever, daemon=True)
+    th.start()
+    App.seen, App.status = [], 200
+    yield f"http://127.0.0.1:{srv.server_address[1]}"
+    srv.shutdown()
+
+
+class FakeEngine:
+    def apply_committed(self, slot_mask=0xFF):
+        return fake_batch()
+
+
+def test_applier_posts_one_request_per_replica(app):
+    ap = Applier(app, workers=2)
+    out = ap.apply(FakeEngine())
+    ap.close()
+    assert len(App.seen) == 2
+    by = {h["raftd-node-id"]: (p, h, b) for p, h, b in App.seen}
+    p, h, b = by["3"]
+    assert p == "/UpdateEntries" and h["raftd-replica-id"] == "2" and h["content-type"] == "application/json"
+    assert json.loads(b)["Entries"][0] == {"Index": 7, "Cmd": base64.b64encode(bytes(range(0, 5))).decode()}
+    assert out[0].results == [(70, bytes(range(0, 5))), (80, bytes(range(10, 15))), (90, bytes(range(20, 23)))]
+
+
+def test_high_status_code(app):
+    App.status = 500
+    b = batches(*fake_batch())[0]
+    with pytest.raises(HighStatusCode, match="high status code \\(500\\): boom"):
+        post_update(app, b)
