@@ -142,6 +142,49 @@ def cpu_baseline(args, seconds):
     }
 
 
+def hbm_copy_ceiling(torch, nbytes=2 << 30, reps=10):
+    """This box's device-to-device copy rate (read + write bytes / s): context for the roofline,
+    which is priced against the 8 TB/s spec; MI355X boxes differ by ~10% run to run."""
+    a = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    b = torch.empty_like(a)
+    b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    gbs = 2 * nbytes * reps / (e0.elapsed_time(e1) / 1e3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return gbs
+
+
+def apply_copyback(eng, torch, slot_mask=1):
+    """rg_apply_committed after the last timed tick: the entries the node hosting the slot-0
+    replicas hands to /UpdateEntries, gathered on the device and copied back into pinned host
+    buffers. Host wall time of the whole call (count + scan + gather + D2H + sync)."""
+    import ctypes as C
+    n = C.c_uint64()
+    eng.L.rg_apply_committed(eng.h, slot_mask, None, None, 0, C.byref(n))
+    cnt, P = n.value, eng.cfg["payload_bytes"]
+    if cnt == 0:
+        return None
+    recs = torch.empty(cnt * 32, dtype=torch.uint8, pin_memory=True)
+    pay = torch.empty(max(cnt * P, 1), dtype=torch.uint8, pin_memory=True)
+    best = None
+    for _ in range(3):
+        t0 = time.perf_counter()
+        rc = eng.L.rg_apply_committed(eng.h, slot_mask, recs.data_ptr(), pay.data_ptr(), cnt, C.byref(n))
+        dt = time.perf_counter() - t0
+        if rc < 0:
+            return None
+        best = dt if best is None else min(best, dt)
+    nb = cnt * (32 + P)
+    return {"slot_mask": slot_mask, "entries": cnt, "bytes": nb, "ms": best * 1e3, "GBps": nb / best / 1e9,
+            "note": "count + scan + gather kernels, then one hipMemcpyAsync per array into pinned host memory"}
+
+
 def pmc_traffic(kernel="bulk_kernel"):
     """HBM bytes per tick-kernel launch from the committed rocprofv3 PMC summary (profiles/)."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_summary.json")))
@@ -231,6 +274,8 @@ def main():
     x_ms = sum(a.elapsed_time(b) for a, b in xev) / args.steps if wire else 0.0
     c1 = eng.sum_committed()
     errs = sum(1 for v in eng.replicas(0, min(eng.nrep, 3 * 4096)) if v["err"])
+    apply = apply_copyback(eng, torch)
+    copy_gbs = hbm_copy_ceiling(torch)
     t = torch.tensor([wall, dev_ms, float(c1 - c0), x_ms, float(wire_bytes)], dtype=torch.float64,
                      device="cuda" if args.backend == "nccl" else "cpu")
     if dist:
@@ -295,6 +340,8 @@ def main():
             "traffic": hbm,
             "traffic_source": src,
             "kernel": "rg::bulk_kernel",
+            "box_copy_ceiling_GBps": copy_gbs,
+            "frac_of_box_copy_ceiling": achieved / copy_gbs,
             "kernel_ms": bulk_ms,
             "launches_timed": kms["bulk"][1],
             "algorithmic_bytes_per_launch": traffic["bulk_bytes"],
@@ -311,6 +358,7 @@ def main():
                     "bytes = the regions this rank sends to other ranks",
         },
         "device_bytes": eng.device_bytes,
+        "apply_copyback": apply,
     }
     if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
         out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)

@@ -23,7 +23,10 @@ def rows(d, pattern):
 
 
 def short(name):
-    for k in ("control_kernel", "bulk_kernel", "tick_kernel", "bootstrap_kernel", "fill_slabs_kernel", "sum_committed_kernel", "traffic_kernel"):
+    for k in ("control_kernel", "bulk_kernel", "bulk_meta_kernel", "tick_kernel", "bootstrap_kernel",
+              "fill_slabs_kernel", "sum_committed_kernel", "traffic_kernel", "unpack_kernel", "pack_kernel",
+              "plan_kernel", "scan_reduce_kernel", "scan_blocks_kernel", "scan_apply_kernel", "bounds_kernel",
+              "apply_count_kernel", "apply_gather_kernel", "apply_total_kernel"):
         if k in name:
             return k
     return name[:60]
