@@ -142,22 +142,14 @@ def cpu_baseline(args, seconds):
     }
 
 
-def hbm_copy_ceiling(torch, nbytes=2 << 30, reps=10):
-    """This box's device-to-device copy rate (read + write bytes / s): context for the roofline,
-    which is priced against the 8 TB/s spec; MI355X boxes differ by ~10% run to run."""
-    a = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-    b = torch.empty_like(a)
-    b.copy_(a)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        b.copy_(a)
-    e1.record()
-    torch.cuda.synchronize()
-    gbs = 2 * nbytes * reps / (e0.elapsed_time(e1) / 1e3) / 1e9
-    del a, b
-    torch.cuda.empty_cache()
-    return gbs
+def hbm_copy_ceiling(eng, nbytes=2 << 30, reps=10):
+    """This box's streaming-copy rate (read + write bytes / s, rg_probe_copy: 16 B per lane,
+    non-temporal, the bulk kernel's access shape): context for the roofline, which is priced
+    against the 8 TB/s spec; MI355X boxes differ by ~10% run to run."""
+    import ctypes as C
+    g = C.c_double()
+    rc = eng.L.rg_probe_copy(eng.cfg["device"], nbytes, reps, C.byref(g))
+    return g.value if rc == 0 else None
 
 
 def apply_copyback(eng, torch, slot_mask=1):
@@ -185,9 +177,11 @@ def apply_copyback(eng, torch, slot_mask=1):
             "note": "count + scan + gather kernels, then one hipMemcpyAsync per array into pinned host memory"}
 
 
-def pmc_traffic(kernel="bulk_kernel"):
-    """HBM bytes per tick-kernel launch from the committed rocprofv3 PMC summary (profiles/)."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_summary.json")))
+def pmc_traffic(kernel="bulk_kernel", wire=False):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of the
+    same bench mode (profiles/r*_pmc_summary.json; *_wire_* = the --wire-all runs)."""
+    files = [f for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_summary.json")))
+             if ("_wire_" in os.path.basename(f)) == wire]
     if not files:
         return None, None
     with open(files[-1]) as f:
@@ -275,7 +269,7 @@ def main():
     c1 = eng.sum_committed()
     errs = sum(1 for v in eng.replicas(0, min(eng.nrep, 3 * 4096)) if v["err"])
     apply = apply_copyback(eng, torch)
-    copy_gbs = hbm_copy_ceiling(torch)
+    copy_gbs = hbm_copy_ceiling(eng)
     t = torch.tensor([wall, dev_ms, float(c1 - c0), x_ms, float(wire_bytes)], dtype=torch.float64,
                      device="cuda" if args.backend == "nccl" else "cpu")
     if dist:
@@ -303,7 +297,7 @@ def main():
     bulk_ms = kms["bulk"][0] / max(kms["bulk"][1], 1)
     ctl_ms = kms["control"][0] / max(kms["control"][1], 1)
     achieved = traffic["bulk_bytes"] / (bulk_ms / 1e3) / 1e9
-    hbm, src = pmc_traffic()
+    hbm, src = pmc_traffic(wire=bool(args.wire_all))
     out = {
         "metric": METRIC,
         "value": group_steps,
@@ -341,7 +335,7 @@ def main():
             "traffic_source": src,
             "kernel": "rg::bulk_kernel",
             "box_copy_ceiling_GBps": copy_gbs,
-            "frac_of_box_copy_ceiling": achieved / copy_gbs,
+            "frac_of_box_copy_ceiling": achieved / copy_gbs if copy_gbs else None,
             "kernel_ms": bulk_ms,
             "launches_timed": kms["bulk"][1],
             "algorithmic_bytes_per_launch": traffic["bulk_bytes"],

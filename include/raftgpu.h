@@ -218,6 +218,10 @@ int rg_apply_committed(rg_engine* e, uint32_t slot_mask, rg_apply_entry* entries
                        uint64_t* n);
 /* Global group and global replica id (group·replicas + slot) of local replica rid. */
 int rg_global_id(rg_engine* e, uint32_t rid, uint64_t* group, uint64_t* global_rid);
+/* Measurement helper: this device's streaming-copy bandwidth, (read + write bytes) / s, of a
+ * 16-B-per-lane non-temporal grid-stride copy of `bytes` (the bulk kernel's access shape), best
+ * of `reps` launches timed with HIP events. Allocates and frees 2 x bytes. */
+int rg_probe_copy(int32_t device, uint64_t bytes, int32_t reps, double* gbps);
 /* Device bytes held by the engine. */
 uint64_t rg_device_bytes(const rg_engine* e);
 const char* rg_last_error(void);

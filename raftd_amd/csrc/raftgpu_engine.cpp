@@ -411,6 +411,40 @@ void rg_destroy(rg_engine* e) {
 }
 
 uint64_t rg_device_bytes(const rg_engine* e) { return e ? e->bytes : 0; }
+
+int rg_probe_copy(int32_t device, uint64_t bytes, int32_t reps, double* gbps) {
+  if (!gbps || bytes < 16 || reps < 1) return fail(RG_EINVAL, "rg_probe_copy args");
+  HIPCHK(hipSetDevice(device));
+  void *a = nullptr, *b = nullptr;
+  hipStream_t s = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int rc = RG_OK;
+  float best = 0;
+  if (hipMalloc(&a, bytes) != hipSuccess || hipMalloc(&b, bytes) != hipSuccess) {
+    rc = fail(RG_ENOMEM, "rg_probe_copy: hipMalloc");
+  } else if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess ||
+             hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) {
+    rc = fail(RG_EHIP, "rg_probe_copy: stream/events");
+  } else {
+    (void)hipMemsetAsync(a, 1, bytes, s);
+    for (int r = 0; r <= reps && rc == RG_OK; ++r) {  // launch 0 warms up
+      float ms = 0;
+      if (hipEventRecord(e0, s) != hipSuccess || launch_probe_copy(a, b, bytes & ~15ull, s) != hipSuccess ||
+          hipEventRecord(e1, s) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+          hipEventElapsedTime(&ms, e0, e1) != hipSuccess)
+        rc = fail(RG_EHIP, "rg_probe_copy: launch");
+      else if (r > 0 && (best == 0 || ms < best))
+        best = ms;
+    }
+  }
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  if (s) (void)hipStreamDestroy(s);
+  if (a) (void)hipFree(a);
+  if (b) (void)hipFree(b);
+  if (rc == RG_OK) *gbps = 2.0 * (double)(bytes & ~15ull) / (best / 1e3) / 1e9;
+  return rc;
+}
 uint64_t rg_tick_count(const rg_engine* e) { return e ? e->t : 0; }
 
 int rg_set_stream(rg_engine* e, void* stream) {

@@ -154,6 +154,7 @@ hipError_t launch_bulk(const BulkParams& p, hipStream_t s, int grid);
 hipError_t launch_bootstrap(const TickParams& p, uint2* info, hipStream_t s);
 hipError_t launch_fill_slabs(uint8_t* slabs, uint32_t nslab, uint32_t G, uint32_t rows, uint32_t E, uint32_t P,
                              uint64_t seed, const Placement& pl, hipStream_t s);
+hipError_t launch_probe_copy(const void* src, void* dst, uint64_t bytes, hipStream_t s);
 hipError_t launch_sum_committed(const TickParams& p, unsigned long long* out, hipStream_t s);
 hipError_t launch_traffic(const TickParams& p, unsigned long long* out6, hipStream_t s);
 // committed-entry copy-back (raftgpu_apply.hip): after a tick, the application entries each replica

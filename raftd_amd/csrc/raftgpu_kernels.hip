@@ -415,6 +415,32 @@ hipError_t launch_fill_slabs(uint8_t* slabs, uint32_t nslab, uint32_t G, uint32_
   return hipGetLastError();
 }
 
+// ================================================================== copy probe (measurement)
+__global__ void __launch_bounds__(256) probe_copy_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                         uint64_t n) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n; i += 4 * stride) {  // four 16-B loads in flight per lane
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + i + u * stride));
+#pragma unroll
+    for (int u = 0; u < 4; ++u) __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4*>(dst + i + u * stride));
+  }
+  for (; i < n; i += stride)
+    __builtin_nontemporal_store(__builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + i)),
+                                reinterpret_cast<u32x4*>(dst + i));
+}
+
+hipError_t launch_probe_copy(const void* src, void* dst, uint64_t bytes, hipStream_t s) {
+  int dev = 0, cus = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  hipLaunchKernelGGL(probe_copy_kernel, dim3(cus * 8), dim3(256), 0, s, (const uint4*)src, (uint4*)dst, bytes / 16);
+  return hipGetLastError();
+}
+
 // ================================================================== reductions
 __device__ __forceinline__ uint64_t wave_sum64(uint64_t a) {
   for (int off = 32; off > 0; off >>= 1) {

@@ -92,7 +92,7 @@ EXPORTS = ["rg_create", "rg_destroy", "rg_bootstrap", "rg_fill_slabs", "rg_tick"
            "rg_read_entries", "rg_import_replica", "rg_deliver", "rg_leader", "rg_sum_committed",
            "rg_device_bytes", "rg_last_error", "rg_last_tick_traffic", "rg_join",
            "rg_timing", "rg_kernel_ms", "rg_wire_plan", "rg_wire_pack", "rg_wire_recv", "rg_global_id",
-           "rg_apply_committed"]
+           "rg_apply_committed", "rg_probe_copy"]
 
 _lib = None
 
@@ -134,6 +134,7 @@ def load_library(path: str = LIB_PATH):
         "rg_wire_recv": ([vp, vp, C.POINTER(C.c_uint64)], i32),
         "rg_global_id": ([vp, u32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)], i32),
         "rg_apply_committed": ([vp, u32, vp, vp, u64, C.POINTER(C.c_uint64)], i32),
+        "rg_probe_copy": ([C.c_int32, u64, C.c_int32, C.POINTER(C.c_double)], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
