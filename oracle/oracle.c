@@ -121,8 +121,10 @@ static int up_to_date(const or_engine* e, const rep_t* r, uint64_t i, uint64_t t
   return t > lt || (t == lt && i >= r->last);
 }
 
+static inline uint64_t global_group(const or_engine* e, const rep_t* r) { return (uint64_t)e->c.group_base + r->g; }
+
 static uint32_t rand_timeout(const or_engine* e, const rep_t* r) {
-  uint64_t key = ((uint64_t)r->g << 32) | ((uint64_t)r->s << 24) | (uint64_t)(r->rng_ctr & 0xFFFFFF);
+  uint64_t key = (global_group(e, r) << 32) | ((uint64_t)r->s << 24) | (uint64_t)(r->rng_ctr & 0xFFFFFF);
   uint64_t v = or_mix64(e->c.seed ^ or_mix64(key));
   return e->c.election_rtt + (uint32_t)(v % e->c.election_rtt);
 }
@@ -136,7 +138,8 @@ static int lost(const or_engine* e, const rep_t* r, uint32_t dst, uint32_t n) {
     if (in->isolate[rid] || in->isolate[r->g * e->c.replicas + dst]) return 1;
   }
   if (e->c.drop_ppm) {
-    uint64_t h = or_mix64(e->c.seed ^ or_mix64((e->t << 40) ^ ((uint64_t)rid << 8) ^ dst) ^ (uint64_t)(n + 1));
+    uint64_t grid = global_group(e, r) * e->c.replicas + r->s;
+    uint64_t h = or_mix64(e->c.seed ^ or_mix64((e->t << 40) ^ (grid << 8) ^ dst) ^ (uint64_t)(n + 1));
     if (h % 1000000ULL < e->c.drop_ppm) return 1;
   }
   return 0;
@@ -231,7 +234,7 @@ static int append_entries(or_engine* e, rep_t* r, uint32_t n, int slab) {
     en->type = OR_ENTRY_APP;
     if (slab >= 0 && P) {
       uint8_t* dst = logpay_at(e, r, idx);
-      or_payload(e, (uint32_t)slab, r->g, k, dst);
+      or_payload(e, (uint32_t)slab, (uint32_t)global_group(e, r), k, dst);
       en->len = P;
       en->crc = or_crc32(dst, P);
     } else {

@@ -46,7 +46,9 @@ typedef struct or_config {
   uint32_t election_rtt, heartbeat_rtt, check_quorum;
   uint32_t snapshot_entries, compaction_overhead;
   uint32_t drop_ppm;
-  uint32_t _pad;
+  uint32_t group_base; /* global id of group 0: an oracle of a window of groups [base, base+groups)
+                          reproduces that window of a larger run (groups are independent; RNG keys,
+                          loss hashes and payloads use the global id; tick inputs are the window's) */
   uint64_t seed;
 } or_config;
 
