@@ -102,6 +102,16 @@ def load_library(path: str = LIB_PATH):
     global _lib
     if _lib is not None:
         return _lib
+    # One HIP runtime per process. PyTorch-ROCm wheels ship their own libamdhip64.so /
+    # libhsa-runtime64.so (SONAMEs libamdhip64.so.7 / libhsa-runtime64.so.1) and libtorch_hip NEEDs
+    # the unversioned name. If this library pulled /opt/rocm's runtime in first, a later torch
+    # import would load the second copy and two HSA runtimes would share the process's KFD
+    # context (observed: memory-aperture faults, "No HIP GPUs" at torch's lazy init). Importing
+    # torch first lets the dynamic linker satisfy our libamdhip64.so.7 with torch's copy.
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # no torch (e.g. a cgo host): the system runtime is the only one
+        pass
     if not os.path.exists(path):
         raise RuntimeError(f"HIP engine library not built: {path} (run `python -m raftd_amd.build`)")
     L = C.CDLL(path)

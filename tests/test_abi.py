@@ -48,3 +48,14 @@ def test_kernels_use_no_scratch():
     assert len(ctl) == 8
     for k, v in res.items():
         assert int(v["ScratchSize [bytes/lane]"]) == 0, k
+
+
+def test_one_hip_runtime_per_process():
+    """Loading the engine after torch must not bring in a second libamdhip64 / libhsa-runtime64."""
+    import subprocess
+    import sys
+    code = ("import raftd_amd.engine as e; e.load_library(); import torch; "
+            "libs = [l.split()[-1] for l in open('/proc/self/maps') if 'libamdhip64' in l or 'libhsa-runtime64' in l]; "
+            "print(len({p for p in libs if 'amdhip' in p}), len({p for p in libs if 'hsa-runtime' in p}))")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=ROOT, timeout=300)
+    assert out.stdout.split() == ["1", "1"], out.stdout + out.stderr
