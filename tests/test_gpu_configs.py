@@ -6,7 +6,7 @@ with payload. Each test also checks size-independent properties over ALL groups.
 
 - C3: 65,536 groups x 5 replicas spread over 8 ranks (N ranks as N engines on this one GPU, every
   cross-rank message through the wire), 64-entry batches of 256-B entries with CRC32. The log ring
-  is 512 entries instead of 2,048 so that 8 engines fit one GPU's HBM.
+  is 512 entries instead of 2,048 (SnapshotEntries 200) so that 8 engines fit one GPU's HBM.
 - C4: election storm, 65,536 groups x 3, no leader: randomized timeouts, split votes, term bumps;
   10% of the groups start with a follower holding a divergent uncommitted suffix (1-16 entries of
   term 2) and 5% with a second one (term 3), forcing truncation once a leader emerges.
@@ -155,7 +155,8 @@ def test_c5_one_million_groups_zipf_compaction():
 def test_c3_five_replicas_eight_ranks_full_size():
     from raftd_amd.cluster import LoopbackCluster
     G, R, N, W = 65536, 5, 8, 512
-    cfg = dict(replicas=R, log_capacity=512, payload_bytes=256, max_entries_per_msg=64, seed=0xC3)
+    # SnapshotEntries 200: with a 512-entry ring, compaction must keep the window moving
+    cfg = dict(replicas=R, log_capacity=512, payload_bytes=256, max_entries_per_msg=64, snapshot_entries=200, seed=0xC3)
     cl = LoopbackCluster(ranks=N, groups=G, **cfg)
     wins = [(0, W), (G - W, W)]
     oras = [make("c", groups=n, group_base=b, **cfg) for b, n in wins]
