@@ -220,7 +220,7 @@ static WireParams wire_params(rg_engine* e) {
 static BulkParams bulk_params(rg_engine* e) {  // for tick e->t
   const int a = (int)(e->t & 1);
   BulkParams b{};
-  b.G = e->c.groups; b.nrep = e->nrep; b.L = e->c.log_capacity; b.P = e->c.payload_bytes;
+  b.G = e->c.groups; b.R = e->c.replicas; b.nrep = e->nrep; b.L = e->c.log_capacity; b.P = e->c.payload_bytes;
   b.E = e->c.max_entries_per_msg; b.J = e->J; b.crc_const = e->crc_const; b.tile = e->bulk_tile;
   b.job64 = e->job64[a]; b.job32 = e->job32[a]; b.jcnt = e->jcnt[a];
   b.info = e->info; b.pay = e->pay; b.slabs = e->slabs; b.crc_err = e->crc_err; b.crc_tab = e->crc_tab;

@@ -122,7 +122,7 @@ struct TickParams {
 };
 
 struct BulkParams {
-  uint32_t G, nrep, L, P, E, J, crc_const, tile;  // tile: replicas per wave work item (1..64)
+  uint32_t G, R, nrep, L, P, E, J, crc_const, tile;  // tile: groups per wave work item (1..64)
   uint32_t wire_mode;    // wire engine (ranks > 1 or wire_all): SRC_WIRE jobs, one slab row per replica
   const uint64_t* job64;
   const uint32_t* job32;

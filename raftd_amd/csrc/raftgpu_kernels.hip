@@ -24,8 +24,11 @@ namespace rg {
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+#ifndef RG_CTL_MINWAVES
+#define RG_CTL_MINWAVES 1
+#endif
 template <int R>
-__global__ void __launch_bounds__(256) control_kernel(TickParams p) {
+__global__ void __launch_bounds__(256, RG_CTL_MINWAVES) control_kernel(TickParams p) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= p.nrep) return;
   Ctl<R> c(p, q);
@@ -129,23 +132,45 @@ __device__ __forceinline__ Job load_job(const BulkParams& p, uint32_t q, uint32_
 // (store, CRC, info, verify) and immediately re-issued with the step BULK_U ahead. All cursor
 // state is wave-uniform (SGPRs).
 struct Cursor {
-  uint32_t t, q, g, njl, j, n, kind, src, b;
+  uint32_t t, q, qb, g, njl, j, n, kind, src, b;
   uint64_t m, first, dm, sm, hm, tm;
   bool live;
 };
 
-struct TileJobs {  // per lane: job count and first job of replica tile·T + lane
+struct TileJobs {  // per lane: job count and first job of replica qb + lane
   uint32_t nj;
   Job j0;
 };
 
+// Tiles interleave the slots of one block of groups: tile t = (group block t / R, slot t % R), so
+// the R replicas of the same groups are walked by neighbouring waves at the same time and the two
+// followers' reads of their leader's new entries meet in L2 / Infinity Cache instead of both going
+// to HBM (slot-major tiles put them a third of the launch apart). RG_TILE_SLOTMAJOR: ablation.
+__device__ __forceinline__ uint32_t bulk_ntiles(const BulkParams& p) {
+#ifdef RG_TILE_SLOTMAJOR
+  return (p.nrep + p.tile - 1) / p.tile;
+#else
+  return p.R * ((p.G + p.tile - 1) / p.tile);
+#endif
+}
+
 __device__ __forceinline__ void load_tile(const BulkParams& p, Cursor& cur, TileJobs& tj) {
-  const uint32_t lane = lane_id(), q = cur.t * p.tile + lane;
-  tj.nj = (lane < p.tile && q < p.nrep) ? p.jcnt[q] : 0u;
+  const uint32_t lane = lane_id();
+#ifdef RG_TILE_SLOTMAJOR
+  cur.qb = cur.t * p.tile;
+  const bool valid = lane < p.tile && cur.qb + lane < p.nrep;
+#else
+  const uint32_t b = cur.t / p.R, s = cur.t - b * p.R, g0 = b * p.tile;
+  cur.qb = s * p.G + g0;
+  const bool valid = lane < p.tile && g0 + lane < p.G;
+#endif
+  const uint32_t q = cur.qb + lane;
+  tj.nj = valid ? p.jcnt[q] : 0u;
   tj.j0 = Job{};
   if (tj.nj) tj.j0 = load_job(p, q, 0);
   cur.m = __ballot(tj.nj != 0);
-  cur.j = cur.njl = 0;
+  cur.j = 0;
+  cur.njl = 0;
 }
 
 template <bool WIRE>
@@ -167,7 +192,7 @@ __device__ __forceinline__ bool next_job(const BulkParams& p, Cursor& cur, TileJ
   } else if (cur.m) {
     const uint32_t l = rfl((uint32_t)__ffsll((long long)cur.m) - 1);
     cur.m &= cur.m - 1;
-    cur.q = cur.t * p.tile + l;
+    cur.q = cur.qb + l;
     cur.njl = __builtin_amdgcn_readlane(tj.nj, l);
     cur.j = 0;
     Job jb;
@@ -180,7 +205,7 @@ __device__ __forceinline__ bool next_job(const BulkParams& p, Cursor& cur, TileJ
     if (cur.t >= ntiles) return false;
     load_tile(p, cur, tj);
     cur.b = 0;  // two statements: the chained form kept Cursor in scratch
-  cur.n = 0;
+    cur.n = 0;
   }
   return true;
 }
@@ -190,8 +215,8 @@ enum : uint32_t { F_ACT = 1, F_WRITER = 2, F_TYPE = 4, F_CHECK = 8 };
 // metadata-only entries (P = 0): one info word per entry, no payload
 __global__ void __launch_bounds__(256) bulk_meta_kernel(BulkParams p) {
   const uint32_t waves = blockDim.x >> 6, lane = lane_id();
-  const uint32_t stride = gridDim.x * waves, T = p.tile;
-  const uint32_t ntiles = (p.nrep + T - 1) / T;
+  const uint32_t stride = gridDim.x * waves;
+  const uint32_t ntiles = bulk_ntiles(p);
   const uint64_t n64 = p.nrep, L = p.L;
   Cursor cur{};
   TileJobs tj{};
@@ -224,8 +249,8 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p) {
     lds[i] = p.crc_tab[i];
   __syncthreads();
   const uint32_t waves = blockDim.x >> 6, lane = lane_id();
-  const uint32_t stride = gridDim.x * waves, T = p.tile;
-  const uint32_t ntiles = (p.nrep + T - 1) / T;
+  const uint32_t stride = gridDim.x * waves;
+  const uint32_t ntiles = bulk_ntiles(p);
   const uint64_t n64 = p.nrep, L = p.L, rows = WIRE ? p.nrep : p.G;
   const uint32_t c = lane & (NCH - 1), ei = lane >> LG;
   const Crc crc{lds, lds + CRC_T_WORDS, lds + CRC_T_WORDS + CRC_N_WORDS + c * CRC_SH_STRIDE};
@@ -302,7 +327,11 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p) {
         const uint32_t* wp = (ring && act) ? &p.info[si].x
                              : (wire && act) ? reinterpret_cast<const uint32_t*>(p.wire + cur.sm + 16ull * e + 8)
                                              : reinterpret_cast<const uint32_t*>(dummy);
+#ifdef RG_BULK_NT_LOAD  // ablation: non-temporal loads (r01: 1.115 vs 1.090 ms plain)
         x[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(sp + c * 16));
+#else  // temporal: the second follower's read of the same leader entries hits L2 / Infinity Cache
+        x[u] = *reinterpret_cast<const u32x4*>(sp + c * 16);
+#endif
         want[u] = *wp;
         vmask = step ? (vmask | (1u << u)) : (vmask & ~(1u << u));
         cur.b += step ? EPI : 0u;
@@ -416,28 +445,29 @@ hipError_t launch_fill_slabs(uint8_t* slabs, uint32_t nslab, uint32_t G, uint32_
 }
 
 // ================================================================== copy probe (measurement)
+// The fastest of the shapes scripts/copy_probe.hip measured on MI355X (r01: 5.94 TB/s read + write):
+// one block per 32-KB tile, eight 16-B non-temporal loads in flight per lane.
 __global__ void __launch_bounds__(256) probe_copy_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
                                                          uint64_t n) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (; i + 3 * stride < n; i += 4 * stride) {  // four 16-B loads in flight per lane
-    u32x4 v[4];
+  const uint64_t b = (uint64_t)blockIdx.x * 2048;
+  u32x4 v[8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + i + u * stride));
-#pragma unroll
-    for (int u = 0; u < 4; ++u) __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4*>(dst + i + u * stride));
+  for (int u = 0; u < 8; ++u) {
+    const uint64_t i = b + u * 256 + threadIdx.x;
+    v[u] = i < n ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + i)) : u32x4{0, 0, 0, 0};
   }
-  for (; i < n; i += stride)
-    __builtin_nontemporal_store(__builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + i)),
-                                reinterpret_cast<u32x4*>(dst + i));
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const uint64_t i = b + u * 256 + threadIdx.x;
+    if (i < n) __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4*>(dst + i));
+  }
 }
 
 hipError_t launch_probe_copy(const void* src, void* dst, uint64_t bytes, hipStream_t s) {
-  int dev = 0, cus = 0;
-  (void)hipGetDevice(&dev);
-  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  hipLaunchKernelGGL(probe_copy_kernel, dim3(cus * 8), dim3(256), 0, s, (const uint4*)src, (uint4*)dst, bytes / 16);
+  const uint64_t n = bytes / 16;
+  hipLaunchKernelGGL(probe_copy_kernel, dim3((uint32_t)((n + 2047) / 2048)), dim3(256), 0, s, (const uint4*)src,
+                     (uint4*)dst, n);
   return hipGetLastError();
 }
 

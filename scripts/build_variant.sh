@@ -4,7 +4,10 @@
 set -e
 OUT=$1; shift
 cd "$(dirname "$0")/../raftd_amd/csrc"
-for f in raftgpu_kernels.hip raftgpu_admin.hip raftgpu_engine.cpp; do
+SRCS="raftgpu_kernels.hip raftgpu_admin.hip raftgpu_wire.hip raftgpu_apply.hip raftgpu_engine.cpp"
+OBJS=""
+for f in $SRCS; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 "$@" -c -x hip $f -o /tmp/var_${f%.*}.o
+  OBJS="$OBJS /tmp/var_${f%.*}.o"
 done
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT" /tmp/var_raftgpu_kernels.o /tmp/var_raftgpu_admin.o /tmp/var_raftgpu_engine.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT" $OBJS
