@@ -14,7 +14,7 @@ algorithmic bytes per launch (rg_traffic.bulk_bytes) / its mean launch duration,
 events recorded on the bulk stream around every launch of the timed region.
 
 N > 1 (default --placement spread, the north star's layout): one process per GPU
-(torch.distributed.run), N x 65,536 groups, replica slot s of group g on GPU (g mod N + s*h) mod N
+(torch.distributed.run), N x 65,536 groups, replica slot s of group g on GPU (g mod N + off(s)) mod N
 (DESIGN.md §6), so every replica of a group sits on a different GPU, emulating separate nodes.
 Each step = the exchange of the previous tick's cross-GPU messages (plan/pack kernels, one RCCL
 all_to_all_single over xGMI — the only collective — and the unpack kernel) + the tick. Every GPU
@@ -288,7 +288,8 @@ def main():
     K = args.steps
     group_steps = world * G * K / wall
     if spread:
-        par = (f"{world * G} groups; replica slot s of group g on GPU (g mod {world} + s*h) mod {world}; "
+        par = (f"{world * G} groups; replica slot s of group g on GPU (g mod {world} + off(s, g div {world})) mod "
+               f"{world}, every replica of a group on its own GPU, followers spread evenly over the peers; "
                f"cross-GPU messages by one RCCL all_to_all_single per tick")
     elif args.wire_all:
         par = "1 GPU, every message through the wire pack/unpack path to itself (measurement)"

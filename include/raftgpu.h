@@ -78,8 +78,9 @@ typedef struct rg_config {
   int32_t device;               /* HIP device ordinal */
   uint64_t seed;
   /* Placement across ranks (one engine per GPU). Replica slot s of global group g
-   * lives on rank (g mod ranks + s·h(g div ranks)) mod ranks, h cycling over the units mod ranks,
-   * so with ranks >= replicas every replica of a group is on a different GPU. An engine hosts
+   * lives on rank (g mod ranks + off(s, g div ranks)) mod ranks, off(0) = 0, off(s) = ((j mod
+   * (ranks-1)) + s - 1) mod (ranks-1) + 1, so with ranks >= replicas every replica of a group is
+   * on a different GPU and followers spread evenly over the other ranks. An engine hosts
    * `groups` local columns; the shard set is ranks·groups global groups. Tick inputs are indexed
    * by GLOBAL group / replica id. ranks = 0 is read as 1. */
   uint32_t ranks;               /* 1..16 */

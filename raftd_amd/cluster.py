@@ -17,22 +17,21 @@ pair.
 """
 from __future__ import annotations
 
-from math import gcd
-
 from .engine import Engine, default_config
 
 
 # ---------------------------------------------------------------- placement (raftgpu_internal.h)
-def units_mod(n: int) -> list:
-    """h values: the units mod n (h(j) = hs[j % len(hs)]); [0] for one rank."""
-    hs = [h for h in range(1, n) if gcd(h, n) == 1]
-    return hs or [0]
+def slot_offset(s: int, j: int, n: int) -> int:
+    """off_c(s): rank offset of slot s in column j (class c = j mod (n - 1)); 0 for slot 0."""
+    if s == 0 or n < 2:
+        return 0
+    m = n - 1
+    return (j % m + s - 1) % m + 1
 
 
 def rank_of(g: int, s: int, n: int) -> int:
     """Rank hosting slot s of global group g."""
-    hs = units_mod(n)
-    return (g % n + s * hs[(g // n) % len(hs)]) % n
+    return (g % n + slot_offset(s, g // n, n)) % n
 
 
 def local_rid(g: int, s: int, n: int, replicas: int) -> int:
@@ -42,8 +41,12 @@ def local_rid(g: int, s: int, n: int, replicas: int) -> int:
 
 def global_group(rank: int, s: int, j: int, n: int) -> int:
     """Global group of local replica (slot s, column j) on `rank` (pl_group)."""
-    hs = units_mod(n)
-    return n * j + (rank - s * hs[j % len(hs)]) % n
+    return n * j + (rank - slot_offset(s, j, n)) % n
+
+
+def plane_offset(s: int, d: int, j: int, n: int) -> int:
+    """Rank offset of the outbox plane s→d in column j (pl_off; 0 = co-located)."""
+    return (slot_offset(d, j, n) - slot_offset(s, j, n)) % n
 
 
 def _torch():

@@ -737,7 +737,7 @@ int rg_leader(rg_engine* e, uint32_t group, uint64_t* leader_id, uint64_t* term,
   const uint32_t R = e->c.replicas, j = group / N;
   std::vector<rg_replica_view> v;
   for (uint32_t s = 0; s < R; ++s) {
-    if ((group % N + s * pl_h(e->pl, j)) % N != e->pl.rank) continue;  // replica hosted elsewhere
+    if (pl_rank_of(e->pl, group, s) != e->pl.rank) continue;  // replica hosted elsewhere
     rg_replica_view x;
     int rc = rg_read_replicas(e, j * R + s, 1, &x);
     if (rc) return rc;

@@ -47,18 +47,25 @@ enum : uint32_t { SRC_NONE = 0, SRC_RING = 1, SRC_SLAB = 2, SRC_WIRE = 3 };
 // count n; record e = {u64 term word, u32 crc, u32 0} at +16e, payload e at +16n + P·e.
 
 // ---- placement across ranks. Replica slot s of global group g lives on rank
-// (g mod N + s·h(j)) mod N, local column j = g div N, h(j) = hs[j mod H] (the units mod N), so all
-// replicas of a group share column j and the plane s→d of column j goes to rank k + (d−s)·h(j).
+// (g mod N + off_c(s)) mod N, local column j = g div N, column class c = j mod (N − 1), with
+// off_c(0) = 0 and off_c(s) = ((c + s − 1) mod (N − 1)) + 1: every replica of a group shares column
+// j, the plane s→d of column j goes to rank k + off_c(d) − off_c(s), and over N − 1 classes a
+// leader's followers sit at every other rank equally often (the busiest xGMI link carries 2/(N−1)
+// of a rank's leader→follower payload instead of 1/2 with offsets s·h). Arithmetic only: no table
+// that a dynamic index could push into scratch.
 constexpr uint32_t MAX_RANKS = 16;
 struct Placement {
-  uint32_t N, rank, H, wire_all;
-  uint64_t hs;  // the H units, 4 bits each (H <= 12 for N <= 16): a register, never an indexed array
+  uint32_t N, rank, wire_all, _pad;
 };
-RG_HD_INLINE uint32_t pl_h(const Placement& pl, uint32_t j) { return (uint32_t)(pl.hs >> (4 * (j % pl.H))) & 0xFu; }
+RG_HD_INLINE uint32_t pl_soff(const Placement& pl, uint32_t s, uint32_t j) {
+  if (s == 0 || pl.N < 2) return 0;
+  const uint32_t m = pl.N - 1;
+  return (j % m + s - 1) % m + 1;
+}
 // rank offset of the plane s→d at column j (0 = co-located)
 RG_HD_INLINE uint32_t pl_off(const Placement& pl, uint32_t s, uint32_t d, uint32_t j) {
   const uint32_t N = pl.N;
-  return (uint32_t)((((int64_t)d - (int64_t)s) * (int64_t)pl_h(pl, j) % N + N) % N);
+  return (pl_soff(pl, d, j) + N - pl_soff(pl, s, j)) % N;
 }
 RG_HD_INLINE bool pl_remote(const Placement& pl, uint32_t s, uint32_t d, uint32_t j) {
   return pl.wire_all || pl_off(pl, s, d, j) != 0;
@@ -68,22 +75,17 @@ inline Placement make_placement(uint32_t N, uint32_t rank, uint32_t wire_all) {
   pl.N = N ? N : 1;
   pl.rank = rank;
   pl.wire_all = wire_all ? 1 : 0;
-  for (uint32_t h = 1; h < pl.N; ++h) {
-    uint32_t a = h, b = pl.N;
-    while (b) {
-      const uint32_t t = a % b;
-      a = b;
-      b = t;
-    }
-    if (a == 1) pl.hs |= (uint64_t)h << (4 * pl.H++);
-  }
-  if (pl.H == 0) pl.H = 1;  // one rank: h = 0, everything co-located
   return pl;
 }
 // global group of local replica (slot s, column j) on this rank
 RG_HD_INLINE uint64_t pl_group(const Placement& pl, uint32_t s, uint32_t j) {
-  const int64_t N = pl.N;
-  return (uint64_t)N * j + (uint64_t)((((int64_t)pl.rank - (int64_t)s * pl_h(pl, j)) % N + N) % N);
+  const uint32_t N = pl.N;
+  return (uint64_t)N * j + (pl.rank + N - pl_soff(pl, s, j) % N) % N;
+}
+// rank hosting slot s of global group g
+RG_HD_INLINE uint32_t pl_rank_of(const Placement& pl, uint64_t g, uint32_t s) {
+  const uint32_t N = pl.N;
+  return (uint32_t)((g % N + pl_soff(pl, s, (uint32_t)(g / N))) % N);
 }
 
 struct TickParams {

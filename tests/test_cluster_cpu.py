@@ -10,8 +10,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from raftd_amd.cluster import (_offsets, all_to_all_bytes, exchange_sizes, global_group, local_rid, rank_of,
-                               units_mod)
+from raftd_amd.cluster import (_offsets, all_to_all_bytes, exchange_sizes, global_group, local_rid, plane_offset,
+                               rank_of)
 
 
 @pytest.mark.parametrize("N", range(1, 17))
@@ -32,11 +32,13 @@ def test_placement_invariants(N):
                 assert hosted[(k, s)] == set(range(Gl))  # each rank: one replica per (slot, column)
 
 
-def test_units_mod():
-    assert units_mod(1) == [0]
-    assert units_mod(2) == [1]
-    assert units_mod(8) == [1, 3, 5, 7]
-    assert units_mod(6) == [1, 5]
+@pytest.mark.parametrize("N,R", [(8, 3), (8, 5), (4, 3), (16, 3), (7, 7)])
+def test_leader_traffic_spreads_over_every_peer(N, R):
+    """Over N - 1 consecutive columns a leader's followers sit at every other rank equally often,
+    so no xGMI link carries more than (R - 1) / (N - 1) of a rank's leader→follower payload."""
+    from collections import Counter
+    cnt = Counter(plane_offset(0, d, j, N) for j in range(N - 1) for d in range(1, R))
+    assert 0 not in cnt and set(cnt) == set(range(1, N)) and len(set(cnt.values())) == 1
 
 
 def test_placement_matches_cpp():
@@ -47,7 +49,6 @@ def test_placement_matches_cpp():
     L.ch_pl_off.restype = C.c_uint32
     L.ch_pl_off.argtypes = [C.c_uint32] * 4
     for N in (1, 2, 3, 4, 5, 7, 8, 12, 16):
-        hs = units_mod(N)
         for k in range(N):
             for s in range(8):
                 for j in range(40):
@@ -55,7 +56,7 @@ def test_placement_matches_cpp():
         for s in range(8):
             for d in range(8):
                 for j in range(20):
-                    assert L.ch_pl_off(N, s, d, j) == ((d - s) * hs[j % len(hs)]) % N
+                    assert L.ch_pl_off(N, s, d, j) == plane_offset(s, d, j, N)
 
 
 def _free_port():
