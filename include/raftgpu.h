@@ -55,6 +55,9 @@ enum {
 enum { RG_FOLLOWER = 0, RG_CANDIDATE = 1, RG_LEADER = 2 };
 enum { RG_REMOTE_RETRY = 0, RG_REMOTE_WAIT = 1, RG_REMOTE_REPLICATE = 2, RG_REMOTE_SNAPSHOT = 3 };
 enum { RG_ENTRY_APPLICATION = 0, RG_ENTRY_CONFIG_CHANGE = 1 };
+/* rg_import_replica types[] flag: an application entry with an empty Cmd (a leader's no-op),
+ * stored without payload even when payloads are given (WAL restore) */
+#define RG_ENTRY_EMPTY 0x100u
 enum {
   RG_ERR_CONFLICT_COMMITTED = 1, RG_ERR_COMMIT_BEYOND_LAST = 2, RG_ERR_RING_FULL = 4,
   RG_ERR_CRC = 8, RG_ERR_EMPTY_SNAPSHOT = 16
@@ -145,6 +148,24 @@ typedef struct rg_apply_entry {
   uint32_t rid;        /* local replica id */
 } rg_apply_entry;
 
+/* Persistence feed (rg_persist_collect): dragonboat's Update.EntriesToSave + pb.State + snapshot
+ * metadata, which it makes durable (LogDB SaveRaftState, fsync) before a step's messages leave. */
+typedef struct rg_persist_state {
+  uint64_t group;       /* global shard id */
+  uint32_t replica_id;  /* slot + 1 */
+  uint32_t rid;         /* local replica id */
+  uint64_t term, vote, commit;                                 /* pb.State */
+  uint64_t last, marker, marker_term, snap_index, snap_term;   /* log end, compaction / snapshot */
+  uint64_t first;       /* entries first..last follow (none if first > last); the log keeps its
+                           entries below first, drops those above last and at or below marker */
+  uint64_t entry_off;   /* position of this replica's first entry in the entries array */
+} rg_persist_state;
+
+typedef struct rg_persist_entry {
+  uint64_t index, term;
+  uint32_t type, len, crc, rid; /* payload at payload + k * payload_bytes when len > 0 */
+} rg_persist_entry;
+
 typedef struct rg_engine rg_engine;
 
 int rg_create(const rg_config* cfg, rg_engine** out);
@@ -217,6 +238,14 @@ int rg_wire_recv(rg_engine* e, const void* recv_buf, const uint64_t* recv_bytes 
  * *n = the count; if *n > cap nothing is copied and RG_EFULL is returned. Synchronous. */
 int rg_apply_committed(rg_engine* e, uint32_t slot_mask, rg_apply_entry* entries, uint8_t* payload, uint64_t cap,
                        uint64_t* n);
+/* Host WAL feed: for every replica whose log or hard state changed in the last
+ * tick (full != 0, or no tick yet: every replica, whole log window), one rg_persist_state and the
+ * entries it rewrote, gathered on the device and copied back by one hipMemcpyAsync per array. Make
+ * them durable before the next tick delivers the last tick's messages. *n_states / *n_entries =
+ * the counts; if either exceeds its cap nothing is copied and RG_EFULL is returned. Synchronous.
+ * Restart = rg_import_replica of the replayed state. */
+int rg_persist_collect(rg_engine* e, int full, rg_persist_state* states, uint64_t cap_states, uint64_t* n_states,
+                       rg_persist_entry* entries, uint8_t* payload, uint64_t cap_entries, uint64_t* n_entries);
 /* Global group and global replica id (group·replicas + slot) of local replica rid. */
 int rg_global_id(rg_engine* e, uint32_t rid, uint64_t* group, uint64_t* global_rid);
 /* Measurement helper: this device's streaming-copy bandwidth, (read + write bytes) / s, of a

@@ -985,8 +985,8 @@ int or_import_replica(or_engine* e, uint32_t rid, const or_replica_view* v, cons
     uint64_t k = i - v->marker - 1;
     ent_t* en = log_at(e, r, i);
     en->term = terms[k];
-    en->type = types ? types[k] : OR_ENTRY_APP;
-    if (payloads && P && en->type == OR_ENTRY_APP) {
+    en->type = types ? (types[k] & 0xFFu) : OR_ENTRY_APP;
+    if (payloads && P && en->type == OR_ENTRY_APP && !(types && (types[k] & OR_ENTRY_EMPTY))) {
       en->len = P;
       memcpy(logpay_at(e, r, i), payloads + k * P, P);
       en->crc = or_crc32(logpay_at(e, r, i), P);

@@ -34,6 +34,7 @@ enum {
 enum { OR_FOLLOWER = 0, OR_CANDIDATE = 1, OR_LEADER = 2 };
 enum { OR_RETRY = 0, OR_WAIT = 1, OR_REPLICATE_ST = 2, OR_SNAPSHOT = 3 };
 enum { OR_ENTRY_APP = 0, OR_ENTRY_CONFIG = 1 };
+#define OR_ENTRY_EMPTY 0x100u /* import: application entry with an empty Cmd (no payload) */
 enum {
   OR_ERR_CONFLICT_COMMITTED = 1, OR_ERR_COMMIT_BEYOND_LAST = 2, OR_ERR_RING_FULL = 4,
   OR_ERR_CRC = 8, OR_ERR_EMPTY_SNAPSHOT = 16

@@ -89,4 +89,105 @@ hipError_t launch_apply_gather(const ApplyParams& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// ================================================================== persistence (host WAL feed)
+// dragonboat persists Update.EntriesToSave + State{Term, Vote, Commit} (and a snapshot's index)
+// before a step's messages leave. Per replica whose log or hard state changed in the last tick:
+// one state record, and the entries it rewrote, [persist_lo, last] (full: the whole window).
+
+__device__ __forceinline__ uint64_t persist_first(const PersistParams& a, uint32_t q) {
+  const uint64_t n = a.nrep, marker = a.s64[(uint64_t)S_MARKER * n + q];
+  const uint64_t lo = a.full ? marker + 1 : a.persist_lo[q];
+  return lo > marker ? lo : marker + 1;
+}
+
+__global__ void persist_count_kernel(PersistParams a) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= a.nrep) return;
+  const uint64_t n = a.nrep;
+  const uint64_t last = a.s64[(uint64_t)S_LAST * n + q], lo = persist_first(a, q);
+  const uint32_t ne = lo <= last ? (uint32_t)(last - lo + 1) : 0u;
+  const auto diff = [&](uint32_t f) { return a.s64[(uint64_t)f * n + q] != a.s64_prev[(uint64_t)f * n + q]; };
+  const bool changed = a.full || ne > 0 || diff(S_TERM) || diff(S_VOTE) || diff(S_COMMITTED) || diff(S_LAST) ||
+                       diff(S_MARKER) || diff(S_SNAP_INDEX);
+  a.scnt[q] = changed ? 1u : 0u;
+  a.ecnt[q] = ne;
+}
+
+__global__ void persist_total_kernel(const PersistParams a, uint64_t* totals) {
+  totals[0] = a.soff[a.nrep];
+  totals[1] = a.eoff[a.nrep];
+}
+
+hipError_t launch_persist_count(const PersistParams& a, uint64_t* totals, hipStream_t st) {
+  hipLaunchKernelGGL(persist_count_kernel, dim3((a.nrep + 255) / 256), dim3(256), 0, st, a);
+  hipError_t r = launch_scan_u32(a.scnt, a.nrep, a.bsum, a.soff, st);
+  if (r == hipSuccess) r = launch_scan_u32(a.ecnt, a.nrep, a.bsum, a.eoff, st);
+  if (r != hipSuccess) return r;
+  hipLaunchKernelGGL(persist_total_kernel, dim3(1), dim3(1), 0, st, a, totals);
+  return hipGetLastError();
+}
+
+__global__ void persist_state_kernel(PersistParams a) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= a.nrep || !a.scnt[q]) return;
+  const uint64_t n = a.nrep;
+  const uint32_t s = q / a.G, j = q - s * a.G;
+  const uint64_t* v = a.s64 + q;
+  rg_persist_state r;
+  r.group = pl_group(a.pl, s, j);
+  r.replica_id = s + 1;
+  r.rid = j * a.R + s;
+  r.term = v[S_TERM * n];
+  r.vote = v[S_VOTE * n];
+  r.commit = v[S_COMMITTED * n];
+  r.last = v[S_LAST * n];
+  r.marker = v[S_MARKER * n];
+  r.marker_term = v[S_MARKER_TERM * n];
+  r.snap_index = v[S_SNAP_INDEX * n];
+  r.snap_term = v[S_SNAP_TERM * n];
+  r.first = persist_first(a, q);
+  r.entry_off = a.eoff[q];
+  reinterpret_cast<rg_persist_state*>(a.out_state)[a.soff[q]] = r;
+}
+
+__global__ void __launch_bounds__(256) persist_entries_kernel(PersistParams a) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const uint32_t lane = __lane_id();
+  const uint32_t q = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  if (q >= a.nrep || a.ecnt[q] == 0) return;
+  const uint32_t s = q / a.G, j = q - s * a.G;
+  const uint64_t n64 = a.nrep, L = a.L, P = a.P, nch = P / 16;
+  const uint64_t lo = persist_first(a, q), hi = a.s64[(uint64_t)S_LAST * n64 + q];
+  const uint64_t base = a.eoff[q];
+  for (uint64_t i0 = lo; i0 <= hi; i0 += 64) {
+    const uint64_t i = i0 + lane;
+    if (i <= hi) {
+      const uint64_t slot = i & (L - 1), w = a.tr[slot * n64 + q];
+      const uint2 inf = a.info[((w >> 63) * n64 + q) * L + slot];
+      rg_persist_entry r;
+      r.index = i;
+      r.term = w & TERM_MASK;
+      r.type = (uint32_t)((w >> 61) & 1);
+      r.len = inf.y & 0xFFFFFF;
+      r.crc = inf.x;
+      r.rid = j * a.R + s;
+      reinterpret_cast<rg_persist_entry*>(a.out_ent)[base + (i - lo)] = r;
+    }
+    const uint64_t ncand = hi - i0 + 1 < 64 ? hi - i0 + 1 : 64;
+    for (uint64_t t = lane; t < ncand * nch; t += 64) {
+      const uint64_t e = t / nch, ch = t - e * nch, ie = i0 + e, se = ie & (L - 1);
+      const uint64_t we = a.tr[se * n64 + q];
+      if (!(we & PAY_BIT)) continue;
+      const u32x4 v = *reinterpret_cast<const u32x4*>(a.pay + (((we >> 63) * n64 + q) * L + se) * P + 16 * ch);
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(a.out_pay + (base + (ie - lo)) * P + 16 * ch));
+    }
+  }
+}
+
+hipError_t launch_persist_gather(const PersistParams& a, hipStream_t st) {
+  hipLaunchKernelGGL(persist_state_kernel, dim3((a.nrep + 255) / 256), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(persist_entries_kernel, dim3((a.nrep + 3) / 4), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
 }  // namespace rg

@@ -62,6 +62,7 @@ struct Ctl {
   uint32_t rt[R];                // remote state
   uint64_t last_start, sent_hi, rw_lo, rw_hi, marker_start;
   uint64_t applied_start, restored_at;  // apply window: entries restored from a snapshot are not Update()d
+  uint64_t wlo;                         // lowest log index written this step (EntriesToSave from here)
   uint64_t oc, em;  // per destination: enqueued / emitted counts, 8 bits each
   uint32_t nj;      // jobs emitted
 
@@ -87,7 +88,7 @@ struct Ctl {
       rt[j] = p.rst_in[j * n + q];
     });
     last_start = last; sent_hi = 0; rw_lo = ~0ull; rw_hi = 0; marker_start = marker;
-    applied_start = applied; restored_at = 0;
+    applied_start = applied; restored_at = 0; wlo = ~0ull;
     oc = 0; em = 0; nj = 0;
   }
 
@@ -228,6 +229,7 @@ struct Ctl {
   RG_FN void write_entries(uint64_t base, uint32_t e0, uint32_t n, uint32_t kind, uint32_t src,
                                 const uint64_t* mt, uint64_t word, uint64_t wofs = 0) {
     const uint64_t hi_prot = umax64(last_start, sent_hi);
+    wlo = umin64(wlo, base + e0);
     uint64_t dm = 0, sm = 0, hm = 0, tm = 0;
     for (uint32_t e = e0; e < n; ++e) {
       const uint64_t idx = base + e;
@@ -637,6 +639,7 @@ struct Ctl {
     });
     p.jcnt[q] = nj;
     if (p.apply_lo) p.apply_lo[q] = umax64(applied_start, restored_at) + 1;
+    if (p.persist_lo) p.persist_lo[q] = wlo;
   }
 #undef RG_GET
 #undef RG_SET

@@ -111,6 +111,10 @@ struct rg_engine {
   uint64_t *aoff = nullptr, *absum = nullptr;
   uint8_t* astage = nullptr;
   uint64_t astage_bytes = 0;
+  // persistence copy-back
+  uint64_t* persist_lo = nullptr;
+  uint32_t *pscnt = nullptr, *pecnt = nullptr;
+  uint64_t *psoff = nullptr, *peoff = nullptr;
 };
 
 // ---------------------------------------------------------------- CRC-32/IEEE tables
@@ -200,6 +204,7 @@ static TickParams params(rg_engine* e) {
   p.job64 = e->job64[a]; p.job32 = e->job32[a]; p.jcnt = e->jcnt[a];
   p.rhdr = e->rhdr; p.rmt = e->rmt; p.rcnt = e->rcnt;
   p.apply_lo = e->apply_lo;
+  p.persist_lo = e->persist_lo;
   return p;
 }
 
@@ -302,6 +307,11 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if (rc == RG_OK) rc = dalloc(e, &e->acnt, n * 4);
   if (rc == RG_OK) rc = dalloc(e, &e->aoff, (n + 1) * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->absum, ((n + 1023) / 1024 + 1) * 8);
+  if (rc == RG_OK) rc = dalloc(e, &e->persist_lo, n * 8);
+  if (rc == RG_OK) rc = dalloc(e, &e->pscnt, n * 4);
+  if (rc == RG_OK) rc = dalloc(e, &e->pecnt, n * 4);
+  if (rc == RG_OK) rc = dalloc(e, &e->psoff, (n + 1) * 8);
+  if (rc == RG_OK) rc = dalloc(e, &e->peoff, (n + 1) * 8);
   // exchange units: every remote (s, d, j) outbox column, per destination rank (send) and per
   // source rank (receive), each in (s, d, j) order — the same list on both ends of a link
   if (rc == RG_OK && e->wire) {
@@ -487,6 +497,7 @@ int rg_bootstrap(rg_engine* e) {
   for (int b = 0; b < 2; ++b) HIPCHK(hipMemsetAsync(e->cnt[b], 0, R * R * G * 4, e->stream));
   if (e->rcnt) HIPCHK(hipMemsetAsync(e->rcnt, 0, R * R * G * 4, e->stream));
   HIPCHK(hipMemsetAsync(e->apply_lo, 0, (uint64_t)e->nrep * 8, e->stream));
+  HIPCHK(hipMemsetAsync(e->persist_lo, 0xFF, (uint64_t)e->nrep * 8, e->stream));
   e->planned = e->wire_ready = false;
   e->recv = nullptr;
   HIPCHK(hipMemsetAsync(e->crc_err, 0, (uint64_t)e->nrep * 4, e->stream));
@@ -684,8 +695,8 @@ int rg_import_replica(rg_engine* e, uint32_t rid, const rg_replica_view* v, cons
   std::vector<uint64_t> words(nent);
   std::vector<uint32_t> crcs(nent, 0);
   for (uint32_t k = 0; k < nent; ++k) {
-    const uint32_t type = types ? types[k] : RG_ENTRY_APPLICATION;
-    const bool hp = payloads && P && type == RG_ENTRY_APPLICATION;
+    const uint32_t type = types ? (types[k] & 0xFFu) : RG_ENTRY_APPLICATION;
+    const bool hp = payloads && P && type == RG_ENTRY_APPLICATION && !(types && (types[k] & RG_ENTRY_EMPTY));
     words[k] = (terms[k] & TERM_MASK) | (type ? TYPE_BIT : 0) | (hp ? PAY_BIT : 0);
     if (hp) crcs[k] = host_crc(e, payloads + (uint64_t)k * P, P);
   }
@@ -757,6 +768,55 @@ int rg_leader(rg_engine* e, uint32_t group, uint64_t* leader_id, uint64_t* term,
   return RG_OK;
 }
 
+// device staging for the copy-back paths (grown on demand)
+static int astage_reserve(rg_engine* e, uint64_t bytes) {
+  if (bytes <= e->astage_bytes) return RG_OK;
+  if (e->astage) {
+    (void)hipFree(e->astage);
+    e->allocs.erase(std::remove(e->allocs.begin(), e->allocs.end(), (void*)e->astage), e->allocs.end());
+    e->bytes -= e->astage_bytes;
+    e->astage = nullptr;
+    e->astage_bytes = 0;
+  }
+  const uint64_t nb = std::max<uint64_t>(bytes * 5 / 4, 1 << 20);
+  RGCHK(dalloc(e, &e->astage, nb));
+  e->astage_bytes = nb;
+  return RG_OK;
+}
+
+int rg_persist_collect(rg_engine* e, int full, rg_persist_state* states, uint64_t cap_states, uint64_t* n_states,
+                       rg_persist_entry* entries, uint8_t* payload, uint64_t cap_entries, uint64_t* n_entries) {
+  if (!e || !n_states || !n_entries) return fail(RG_EINVAL, "rg_persist_collect args");
+  if (int jrc = join(e)) return jrc;
+  const TickParams t = params(e);
+  PersistParams a{};
+  a.G = t.G; a.R = t.R; a.nrep = t.nrep; a.L = t.L; a.P = t.P; a.pl = e->pl;
+  a.full = (full || e->t == 0) ? 1u : 0u;  // before the first tick there is no previous state
+  a.s64 = t.s64_in; a.s64_prev = t.s64_out; a.persist_lo = e->persist_lo;
+  a.tr = e->tr; a.info = e->info; a.pay = e->pay;
+  a.scnt = e->pscnt; a.ecnt = e->pecnt; a.soff = e->psoff; a.eoff = e->peoff; a.bsum = e->absum;
+  LAUNCH(launch_persist_count(a, (uint64_t*)e->d_sum, e->stream), e->stream, "persist count");
+  uint64_t tot[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(tot, e->d_sum, 16, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  *n_states = tot[0];
+  *n_entries = tot[1];
+  if (tot[0] > cap_states || tot[1] > cap_entries) return fail(RG_EFULL, "rg_persist_collect: buffers too small");
+  if (tot[0] == 0) return RG_OK;
+  if (!states || (tot[1] && (!entries || (a.P && !payload)))) return fail(RG_EINVAL, "rg_persist_collect: null output");
+  const uint64_t sb = tot[0] * sizeof(rg_persist_state), eb = tot[1] * sizeof(rg_persist_entry), pb = tot[1] * a.P;
+  RGCHK(astage_reserve(e, sb + eb + pb));
+  a.out_state = e->astage;
+  a.out_ent = e->astage + sb;
+  a.out_pay = e->astage + sb + eb;
+  LAUNCH(launch_persist_gather(a, e->stream), e->stream, "persist gather");
+  HIPCHK(hipMemcpyAsync(states, a.out_state, sb, hipMemcpyDeviceToHost, e->stream));
+  if (eb) HIPCHK(hipMemcpyAsync(entries, a.out_ent, eb, hipMemcpyDeviceToHost, e->stream));
+  if (pb) HIPCHK(hipMemcpyAsync(payload, a.out_pay, pb, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return RG_OK;
+}
+
 int rg_apply_committed(rg_engine* e, uint32_t slot_mask, rg_apply_entry* entries, uint8_t* payload, uint64_t cap,
                        uint64_t* n) {
   if (!e || !n) return fail(RG_EINVAL, "rg_apply_committed args");
@@ -775,18 +835,7 @@ int rg_apply_committed(rg_engine* e, uint32_t slot_mask, rg_apply_entry* entries
   if (total > cap) return fail(RG_EFULL, "rg_apply_committed: " + std::to_string(total) + " entries > cap");
   if (!entries || (a.P && !payload)) return fail(RG_EINVAL, "rg_apply_committed: null output");
   const uint64_t rb = total * sizeof(rg_apply_entry), pb = total * a.P;
-  if (rb + pb > e->astage_bytes) {
-    if (e->astage) {
-      (void)hipFree(e->astage);
-      e->allocs.erase(std::remove(e->allocs.begin(), e->allocs.end(), (void*)e->astage), e->allocs.end());
-      e->bytes -= e->astage_bytes;
-      e->astage = nullptr;
-      e->astage_bytes = 0;
-    }
-    const uint64_t nb = std::max<uint64_t>((rb + pb) * 5 / 4, 1 << 20);
-    RGCHK(dalloc(e, &e->astage, nb));
-    e->astage_bytes = nb;
-  }
+  RGCHK(astage_reserve(e, rb + pb));
   a.out_rec = e->astage;
   a.out_pay = e->astage + rb;
   LAUNCH(launch_apply_gather(a, e->stream), e->stream, "apply gather");

@@ -114,6 +114,7 @@ struct TickParams {
   const uint64_t* rmt;
   const uint32_t* rcnt;
   uint64_t* apply_lo;      // [nrep] first index this step hands to the state machine (NULL: skip)
+  uint64_t* persist_lo;    // [nrep] lowest index written this step, ~0 if none (NULL: skip)
   uint64_t* job64;         // [J64_ROWS][J][nrep]
   uint32_t* job32;         // [J32_ROWS][J][nrep]
   uint32_t* jcnt;          // [nrep]
@@ -177,6 +178,29 @@ struct ApplyParams {
   uint8_t* out_pay;         // [n][P]
 };
 hipError_t launch_apply_count(const ApplyParams& a, uint64_t* total, hipStream_t s);
+// persistence copy-back (raftgpu_apply.hip): per replica whose log or hard state changed in the
+// last tick, its state record and the entries it rewrote ([persist_lo, last]); full = every
+// replica with its whole log window (marker, last] (a checkpoint)
+struct PersistParams {
+  uint32_t G, R, nrep, L, P, full;
+  Placement pl;
+  const uint64_t* s64;       // current state
+  const uint64_t* s64_prev;  // state at the start of the last tick
+  const uint64_t* persist_lo;
+  const uint64_t* tr;
+  const uint2* info;
+  const uint8_t* pay;
+  uint32_t* scnt;            // [nrep] 1 if the replica has a record
+  uint32_t* ecnt;            // [nrep] entries to save
+  uint64_t* soff;            // [nrep + 1]
+  uint64_t* eoff;            // [nrep + 1]
+  uint64_t* bsum;
+  uint8_t* out_state;        // [ns] rg_persist_state
+  uint8_t* out_ent;          // [ne] rg_persist_entry
+  uint8_t* out_pay;          // [ne][P]
+};
+hipError_t launch_persist_count(const PersistParams& a, uint64_t* totals /*[2]*/, hipStream_t s);
+hipError_t launch_persist_gather(const PersistParams& a, hipStream_t s);
 hipError_t launch_apply_gather(const ApplyParams& a, hipStream_t s);
 // exclusive scan of n u32 into out[0..n] (out[n] = total); bsum: (n + 1023) / 1024 + 1 words
 hipError_t launch_scan_u32(const uint32_t* in, uint32_t n, uint64_t* bsum, uint64_t* out, hipStream_t s);

@@ -78,6 +78,14 @@ APPLY_DTYPE = np.dtype([("index", "<u8"), ("group", "<u8"), ("replica_id", "<u4"
                         ("crc", "<u4"), ("rid", "<u4")])
 
 
+PERSIST_STATE_DTYPE = np.dtype([("group", "<u8"), ("replica_id", "<u4"), ("rid", "<u4"), ("term", "<u8"),
+                                ("vote", "<u8"), ("commit", "<u8"), ("last", "<u8"), ("marker", "<u8"),
+                                ("marker_term", "<u8"), ("snap_index", "<u8"), ("snap_term", "<u8"),
+                                ("first", "<u8"), ("entry_off", "<u8")])
+PERSIST_ENTRY_DTYPE = np.dtype([("index", "<u8"), ("term", "<u8"), ("type", "<u4"), ("len", "<u4"), ("crc", "<u4"),
+                                ("rid", "<u4")])
+
+
 class TickInput(C.Structure):
     _fields_ = [("prop_target", C.c_void_p), ("prop_count", C.c_void_p), ("campaign", C.c_void_p),
                 ("isolate", C.c_void_p), ("flags", C.c_uint32), ("_pad", C.c_uint32)]
@@ -92,7 +100,7 @@ EXPORTS = ["rg_create", "rg_destroy", "rg_bootstrap", "rg_fill_slabs", "rg_tick"
            "rg_read_entries", "rg_import_replica", "rg_deliver", "rg_leader", "rg_sum_committed",
            "rg_device_bytes", "rg_last_error", "rg_last_tick_traffic", "rg_join",
            "rg_timing", "rg_kernel_ms", "rg_wire_plan", "rg_wire_pack", "rg_wire_recv", "rg_global_id",
-           "rg_apply_committed", "rg_probe_copy"]
+           "rg_apply_committed", "rg_probe_copy", "rg_persist_collect"]
 
 _lib = None
 
@@ -145,6 +153,7 @@ def load_library(path: str = LIB_PATH):
         "rg_global_id": ([vp, u32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)], i32),
         "rg_apply_committed": ([vp, u32, vp, vp, u64, C.POINTER(C.c_uint64)], i32),
         "rg_probe_copy": ([C.c_int32, u64, C.c_int32, C.POINTER(C.c_double)], i32),
+        "rg_persist_collect": ([vp, i32, vp, u64, C.POINTER(C.c_uint64), vp, vp, u64, C.POINTER(C.c_uint64)], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -373,6 +382,21 @@ class Engine:
         self._check(self.L.rg_apply_committed(self.h, slot_mask, recs.ctypes.data, pay.ctypes.data, cap, C.byref(n)))
         k = n.value
         return recs[:k], pay[:k, :P]
+
+    def persist_collect(self, full: bool = False):
+        """Host WAL feed of the last tick (rg_persist_collect): (states, entries, payload) numpy
+        arrays — PERSIST_STATE_DTYPE rows, PERSIST_ENTRY_DTYPE rows, payload_bytes per entry."""
+        P = self.cfg["payload_bytes"]
+        ns, ne = C.c_uint64(), C.c_uint64()
+        rc = self.L.rg_persist_collect(self.h, 1 if full else 0, None, 0, C.byref(ns), None, None, 0, C.byref(ne))
+        if rc < 0 and rc != RG_EFULL:
+            self._check(rc)
+        st = np.zeros(max(ns.value, 1), PERSIST_STATE_DTYPE)
+        en = np.zeros(max(ne.value, 1), PERSIST_ENTRY_DTYPE)
+        pay = np.zeros((max(ne.value, 1), max(P, 1)), np.uint8)
+        self._check(self.L.rg_persist_collect(self.h, 1 if full else 0, st.ctypes.data, ns.value, C.byref(ns),
+                                              en.ctypes.data, pay.ctypes.data, ne.value, C.byref(ne)))
+        return st[:ns.value], en[:ne.value], pay[:ne.value, :P]
 
     def global_id(self, rid: int):
         """(global group, global replica id) of local replica rid."""
