@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--placement", choices=["spread", "colocated"], default=None,
                     help="N > 1: replicas of a group on different GPUs (default) or on one")
     ap.add_argument("--wire-all", action="store_true", help="N = 1: route every message through the wire")
+    ap.add_argument("--halves", type=int, default=2, help="N > 1 spread: engines per rank over disjoint column "
+                    "ranges; 2 pipelines one half's all-to-all behind the other half's tick (1 = no overlap)")
     ap.add_argument("--backend", default="nccl", help="N > 1: nccl (RCCL, default) or gloo (rehearsal: several "
                     "ranks on one GPU with RAFTD_BENCH_DEVICE=0, regions staged through host memory)")
     return ap.parse_args()
@@ -221,41 +223,54 @@ def main():
     common = dict(replicas=R, log_capacity=args.log_capacity, payload_bytes=P, max_entries_per_msg=E, device=local)
     wire = None
     if spread:  # one cluster of world x G groups, replicas spread over the GPUs
-        wire = DistEngine(groups=G, seed=0x5EED, **common)
-        eng = wire.eng
+        wire = DistEngine(groups=G, halves=args.halves, seed=0x5EED, **common)
+        host, eng = wire, wire.eng  # host: aggregates over the halves; eng: the first half
         Gt = G * world
     else:  # an independent engine per GPU (its own G groups)
         eng = Engine(groups=G, seed=0x5EED + rank, wire_all=1 if args.wire_all else 0, **common)
         eng.set_stream(stream.cuda_stream)
         if args.wire_all:
             wire = SelfWire(eng, torch)
+        host = eng
         Gt = G
     step = wire or eng
-    bring_up(eng, step.tick, Gt, R)
+    bring_up(host, step.tick, Gt, R)
     pt = torch.zeros(Gt, dtype=torch.uint8, device="cuda")
     pc = torch.full((Gt,), E, dtype=torch.int32, device="cuda")  # read as uint32 by the kernel
     for _ in range(max(args.warmup, 1)):
         step.tick_device(pt.data_ptr(), pc.data_ptr())
-    traffic = eng.last_tick_traffic()  # counts of a steady-state tick (outside the timed region)
-    c0 = eng.sum_committed()
+    traffic = host.last_tick_traffic()  # counts of a steady-state tick (outside the timed region)
+    c0 = host.sum_committed()
+    pipelined = spread and args.halves > 1
+    if pipelined:
+        wire.prime()  # the last warm-up tick's exchange is in flight when the timer starts
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     xev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    eng.timing(True)
+    host.timing(True)
     wire_bytes = 0
     t0 = time.perf_counter()
     ev0.record(stream)
     for i in range(args.steps):
+        if pipelined:  # each half: finish its exchange, tick, start the next exchange
+            wire.step_device(pt.data_ptr(), pc.data_ptr())
+            wire_bytes += wire.wire_bytes
+            continue
         if wire:
             xev[i][0].record(stream)
             wire.exchange()
             xev[i][1].record(stream)
             wire_bytes += wire.wire_bytes
-        eng.tick_device(pt.data_ptr(), pc.data_ptr())
-    eng.join()  # the stream waits for the last tick's payload stage before the end event
+        for e in (wire.parts if spread else [eng]):
+            e = e.eng if spread else e
+            e.tick_device(pt.data_ptr() + (e.cfg["column_base"] * world if spread else 0),
+                          pc.data_ptr() + 4 * (e.cfg["column_base"] * world if spread else 0))
+    if pipelined:
+        wire.drain()  # the last step's exchanges complete inside the timed region
+    host.join()  # the stream waits for the last tick's payload stage before the end event
     ev1.record(stream)
     torch.cuda.synchronize()
     if dist:
@@ -263,10 +278,10 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     dev_ms = ev0.elapsed_time(ev1)
-    kms = eng.kernel_ms()
-    eng.timing(False)
-    x_ms = sum(a.elapsed_time(b) for a, b in xev) / args.steps if wire else 0.0
-    c1 = eng.sum_committed()
+    kms = host.kernel_ms()
+    host.timing(False)
+    x_ms = sum(a.elapsed_time(b) for a, b in xev) / args.steps if wire and not pipelined else 0.0
+    c1 = host.sum_committed()
     errs = sum(1 for v in eng.replicas(0, min(eng.nrep, 3 * 4096)) if v["err"])
     apply = apply_copyback(eng, torch)
     copy_gbs = hbm_copy_ceiling(eng)
@@ -290,7 +305,9 @@ def main():
     if spread:
         par = (f"{world * G} groups; replica slot s of group g on GPU (g mod {world} + off(s, g div {world})) mod "
                f"{world}, every replica of a group on its own GPU, followers spread evenly over the peers; "
-               f"cross-GPU messages by one RCCL all_to_all_single per tick")
+               f"cross-GPU messages by one RCCL all_to_all_single per tick"
+               + (f" and column half ({args.halves} halves per GPU, exchange pipelined behind the other half's tick)"
+                  if args.halves > 1 else ""))
     elif args.wire_all:
         par = "1 GPU, every message through the wire pack/unpack path to itself (measurement)"
     else:
@@ -345,14 +362,17 @@ def main():
         },
         "kernels_ms": {"control_kernel": ctl_ms, "bulk_kernel": bulk_ms},
         "exchange": None if not wire else {
-            "ms_per_step": x_ms,
+            "mode": (f"pipelined over {args.halves} column halves: one half's all-to-all overlaps the other's "
+                     "unpack + tick + pack" if pipelined else "serial: plan + pack + all-to-all + unpack, then tick"),
+            "ms_per_step": x_ms if not pipelined else None,
             "bytes_sent_per_step_max_rank": wire_max / K,
-            "achieved_GBps_per_rank": (wire_max / K) / (x_ms / 1e3) / 1e9 if x_ms > 0 else None,
+            "achieved_GBps_per_rank": ((wire_max / K) / (x_ms / 1e3) / 1e9 if x_ms > 0 else
+                                       (wire_max / K) / (wall / K) / 1e9),
             "xgmi_peak_GBps_per_rank": 7 * 153.0,
-            "note": "plan + pack + RCCL all_to_all_single + unpack, timed with events on the bench stream; "
-                    "bytes = the regions this rank sends to other ranks",
+            "note": "bytes = the regions this rank sends to other ranks per step; serial mode times the exchange "
+                    "with events on the bench stream, pipelined mode reports bytes / step time (a lower bound)",
         },
-        "device_bytes": eng.device_bytes,
+        "device_bytes": host.device_bytes,
         "apply_copyback": apply,
     }
     if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only

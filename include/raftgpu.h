@@ -89,7 +89,9 @@ typedef struct rg_config {
   uint32_t ranks;               /* 1..16 */
   uint32_t rank;                /* this engine's rank */
   uint32_t wire_all;            /* tests: send co-located messages through the wire too */
-  uint32_t _pad;
+  uint32_t column_base;         /* global column of local column 0: a rank may host several engines
+                                   over disjoint column ranges (their tick-input arrays then start
+                                   at global group ranks·column_base) */
 } rg_config;
 
 typedef struct rg_replica_view {
@@ -115,7 +117,8 @@ typedef struct rg_entry_view {
 } rg_entry_view;
 
 typedef struct rg_tick_input {
-  /* indexed by GLOBAL group g / replica g·replicas + slot; ranks·groups groups in all */
+  /* indexed by GLOBAL group g / replica g·replicas + slot, counted from this engine's first group
+   * ranks·column_base; ranks·groups groups in all */
   const uint8_t* prop_target; /* [groups] slot receiving this tick's proposal batch, 0xFF none */
   const uint32_t* prop_count; /* [groups] entries in the batch (<= max_entries_per_msg) */
   const uint8_t* campaign;    /* [groups*replicas] nonzero: Peer.Campaign before the tick */

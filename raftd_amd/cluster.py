@@ -86,20 +86,22 @@ def _offsets(sizes):
 
 
 # ---------------------------------------------------------------- one process per rank
-def all_to_all_bytes(send, send_sizes, recv, recv_sizes, group=None):
+def all_to_all_bytes(send, send_sizes, recv, recv_sizes, group=None, async_op=False):
     """Move region r of `send` (sizes send_sizes, concatenated in rank order) to rank r; the
     regions from every rank land concatenated in rank order in `recv`. nccl: device tensors, one
-    all_to_all_single (RCCL over xGMI). gloo: staged through host memory."""
+    all_to_all_single (RCCL over xGMI); async_op returns its work handle (wait() makes the current
+    stream wait for it). gloo: staged through host memory, always synchronous (returns None)."""
     import torch.distributed as dist
     torch = _torch()
     stot, rtot = sum(send_sizes), sum(recv_sizes)
     if dist.get_backend(group) == "nccl":
-        dist.all_to_all_single(recv[:rtot], send[:stot], list(recv_sizes), list(send_sizes), group=group)
-        return
+        return dist.all_to_all_single(recv[:rtot], send[:stot], list(recv_sizes), list(send_sizes), group=group,
+                                      async_op=async_op)
     hs = send[:stot].cpu() if send.is_cuda else send[:stot]
     hr = torch.empty(rtot, dtype=torch.uint8)
     dist.all_to_all_single(hr, hs, list(recv_sizes), list(send_sizes), group=group)
     recv[:rtot].copy_(hr)
+    return None
 
 
 def exchange_sizes(send_sizes, group=None):
@@ -113,59 +115,167 @@ def exchange_sizes(send_sizes, group=None):
     return [int(x) for x in rt.tolist()]
 
 
-class DistEngine:
-    """This process's engine of an N-rank cluster (rank = torch.distributed rank). `groups` is
-    the number of local columns (the cluster hosts ranks * groups shards). The engine launches
-    on torch's current stream, so the exchange orders itself behind the tick that produced it."""
+class _Half:
+    """One engine of a rank and its exchange state. start() ships the last tick's cross-rank
+    messages (plan, pack, size exchange, all-to-all — asynchronous on nccl); finish() waits for
+    them and unpacks before the engine's next tick."""
 
-    def __init__(self, groups: int, group=None, **cfg):
-        import torch.distributed as dist
-        torch = _torch()
-        self.pg = group
-        self.N, self.rank = dist.get_world_size(group), dist.get_rank(group)
-        self.eng = Engine(groups=groups, ranks=self.N, rank=self.rank, **cfg)
-        torch.cuda.set_device(self.eng.cfg["device"])
-        self.stream = torch.cuda.current_stream()
-        if self.stream.cuda_stream == 0:  # the engine needs a real stream shared with torch's copies
-            self.stream = torch.cuda.Stream()
-            torch.cuda.set_stream(self.stream)
-        self.eng.set_stream(self.stream.cuda_stream)
-        dev = torch.device("cuda", self.eng.cfg["device"])
+    def __init__(self, eng, dev, pg, rank):
+        self.eng, self.pg, self.rank = eng, pg, rank
         self.send, self.recv = _Buf(dev), _Buf(dev)
-        self.wire_bytes = 0  # bytes this rank sent in the last exchange
+        self.work, self.rsizes, self.sent = None, None, 0
 
-    def exchange(self):
-        """Ship the last tick's cross-rank messages (before every tick)."""
+    def start(self, async_op):
         e = self.eng
-        sizes = e.wire_plan()
+        sizes = e.wire_plan()  # host sync: the tick that produced the messages has completed
         _, stot = _offsets(sizes)
         self.send.ensure(stot)
         e.wire_pack(self.send.ptr(), self.send.cap())
         rsizes = exchange_sizes(sizes, self.pg)
         _, rtot = _offsets(rsizes)
-        if rtot > self.recv.cap():
-            e.sync()  # the previous tick's followers may still read the old receive buffer
-        self.recv.ensure(rtot)
-        all_to_all_bytes(self.send.t, sizes, self.recv.t, rsizes, self.pg)
-        e.wire_recv(self.recv.ptr(), rsizes)
-        self.wire_bytes = stot - sizes[self.rank]
+        self.recv.ensure(rtot)  # its previous contents were consumed by the tick wire_plan waited for
+        self.work = all_to_all_bytes(self.send.t, sizes, self.recv.t, rsizes, self.pg, async_op=async_op)
+        self.rsizes, self.sent = rsizes, stot - sizes[self.rank]
 
-    def tick(self, *a, **kw):
-        self.exchange()
-        self.eng.tick(*a, **kw)
+    def finish(self):
+        if self.work is not None:
+            self.work.wait()
+            self.work = None
+        if self.rsizes is not None:
+            self.eng.wire_recv(self.recv.ptr(), self.rsizes)
+            self.rsizes = None
 
-    def tick_device(self, *a, **kw):
-        self.exchange()
-        self.eng.tick_device(*a, **kw)
+
+class DistEngine:
+    """This process's share of an N-rank cluster (rank = torch.distributed rank): `groups` local
+    columns (the cluster hosts ranks * groups shards), as `halves` engines over disjoint column
+    ranges. Engines launch on torch's current stream, so each exchange orders itself behind the
+    tick that produced it. With two halves, step_device() pipelines: while one half's all-to-all
+    is on the wire, the other half unpacks, ticks and packs."""
+
+    def __init__(self, groups: int, group=None, halves: int = 1, **cfg):
+        import torch.distributed as dist
+        torch = _torch()
+        if groups % halves:
+            raise ValueError("groups must be a multiple of halves")
+        self.pg = group
+        self.N, self.rank = dist.get_world_size(group), dist.get_rank(group)
+        hg = groups // halves
+        self.cols = hg
+        engs = [Engine(groups=hg, ranks=self.N, rank=self.rank, column_base=h * hg, **cfg) for h in range(halves)]
+        torch.cuda.set_device(engs[0].cfg["device"])
+        self.stream = torch.cuda.current_stream()
+        if self.stream.cuda_stream == 0:  # the engine needs a real stream shared with torch's copies
+            self.stream = torch.cuda.Stream()
+            torch.cuda.set_stream(self.stream)
+        dev = torch.device("cuda", engs[0].cfg["device"])
+        for e in engs:
+            e.set_stream(self.stream.cuda_stream)
+        self.parts = [_Half(e, dev, self.pg, self.rank) for e in engs]
+        self.eng = engs[0]
+        self.cfg, self.R = engs[0].cfg, engs[0].R
+        self.async_ok = dist.get_backend(group) == "nccl"
+        self.primed = False
+
+    @property
+    def wire_bytes(self) -> int:  # bytes this rank sent in the last exchange of every half
+        return sum(p.sent for p in self.parts)
+
+    def _slices(self, h):
+        """Offsets of half h's tick inputs in the global arrays: groups, replicas."""
+        g0 = self.N * self.cols * h
+        return g0, g0 * self.R
+
+    # ---- plain (exchange, then tick): bring-up, tests
+    def exchange(self):
+        for p in self.parts:
+            p.start(async_op=False)
+            p.finish()
+
+    def tick(self, prop_target=None, prop_count=None, campaign=None, isolate=None, flags=0):
+        self.drain()
+        n = self.N * self.cols
+        for h, p in enumerate(self.parts):
+            p.start(async_op=False)
+            p.finish()
+            g0, r0 = self._slices(h)
+            sl = lambda a, o, k: None if a is None else a[o:o + k]  # noqa: E731
+            p.eng.tick(sl(prop_target, g0, n), sl(prop_count, g0, n), sl(campaign, r0, n * self.R),
+                       sl(isolate, r0, n * self.R), flags)
+
+    def tick_device(self, pt_ptr=0, pc_ptr=0, flags=0):
+        self.drain()
+        for h, p in enumerate(self.parts):
+            p.start(async_op=False)
+            p.finish()
+            g0, _ = self._slices(h)
+            p.eng.tick_device(pt_ptr + g0 if pt_ptr else 0, pc_ptr + 4 * g0 if pc_ptr else 0, flags=flags)
+
+    # ---- pipelined steady state (device-resident proposal inputs)
+    def prime(self):
+        """Start every half's exchange of its last tick (before the first step_device)."""
+        if not self.primed:
+            for p in self.parts:
+                p.start(async_op=self.async_ok)
+            self.primed = True
+
+    def step_device(self, pt_ptr=0, pc_ptr=0, flags=0):
+        self.prime()
+        for h, p in enumerate(self.parts):
+            p.finish()
+            g0, _ = self._slices(h)
+            p.eng.tick_device(pt_ptr + g0 if pt_ptr else 0, pc_ptr + 4 * g0 if pc_ptr else 0, flags=flags)
+            p.start(async_op=self.async_ok)
+
+    def drain(self):
+        """Complete the exchanges in flight so every engine is ready for a plain tick or a read."""
+        if self.primed:
+            for p in self.parts:
+                p.finish()
+            self.primed = False
+
+    # ---- aggregates over the halves (bench)
+    def bootstrap(self):
+        for p in self.parts:
+            p.eng.bootstrap()
+
+    def join(self):
+        for p in self.parts:
+            p.eng.join()
+
+    def sync(self):
+        for p in self.parts:
+            p.eng.sync()
+
+    def timing(self, on=True):
+        for p in self.parts:
+            p.eng.timing(on)
+
+    def kernel_ms(self) -> dict:
+        """Summed over the halves: total ms per kernel, and launches counted per tick."""
+        ks = [p.eng.kernel_ms() for p in self.parts]
+        return {k: (sum(x[k][0] for x in ks), ks[0][k][1]) for k in ks[0]}
+
+    def last_tick_traffic(self) -> dict:
+        ts = [p.eng.last_tick_traffic() for p in self.parts]
+        return {k: sum(t[k] for t in ts) for k in ts[0]}
+
+    def sum_committed(self) -> int:
+        return sum(p.eng.sum_committed() for p in self.parts)
+
+    @property
+    def device_bytes(self) -> int:
+        return sum(p.eng.device_bytes for p in self.parts)
 
 
 # ---------------------------------------------------------------- N ranks in one process
 class LoopbackCluster:
     """N engines (ranks) in one process on one GPU, moving regions with device copies. The
-    interface is the single Engine's, in GLOBAL ids: replica id g * R + s, `groups` = all
-    ranks' shards (a multiple of ranks)."""
+    interface is the single Engine's, in global ids counted from the cluster's first group
+    (ranks * column_base, like an oracle window's group_base): replica id g * R + s, `groups` =
+    all ranks' shards (a multiple of ranks)."""
 
-    def __init__(self, ranks: int, groups: int, **cfg):
+    def __init__(self, ranks: int, groups: int, column_base: int = 0, **cfg):
         torch = _torch()
         if groups % ranks:
             raise ValueError("groups must be a multiple of ranks")
@@ -173,7 +283,8 @@ class LoopbackCluster:
         self.cfg = default_config(groups=groups, **cfg)
         self.G, self.R = groups, self.cfg["replicas"]
         self.nrep = self.G * self.R
-        lc = dict(self.cfg, groups=groups // ranks)
+        self.rid0 = ranks * column_base * self.R  # ids are relative to the first group, as inputs are
+        lc = dict(self.cfg, groups=groups // ranks, column_base=column_base)
         self.engines = [Engine(**dict(lc, ranks=ranks, rank=k)) for k in range(ranks)]
         dev = torch.device("cuda", self.cfg["device"])
         self.send = [_Buf(dev) for _ in range(ranks)]
@@ -182,7 +293,7 @@ class LoopbackCluster:
         for k, e in enumerate(self.engines):
             for lr in range(e.nrep):
                 g, gr = e.global_id(lr)
-                self.loc[gr] = (k, lr)
+                self.loc[gr - self.rid0] = (k, lr)
         self.wire_bytes = 0
 
     def close(self):

@@ -55,7 +55,8 @@ template <int R>
 struct Ctl {
   const TickParams p;  // by value: pointer fields stay kernel-argument (global) pointers
   uint32_t q, g, s;    // g = local column (indexes every device array)
-  uint64_t gg, rid;    // global group and global replica id gg·R + s (RNG keys, tick inputs)
+  uint64_t gg, rid;    // global group and global replica id gg·R + s (RNG keys, loss hash)
+  uint64_t gi, ri;     // the same as indices into this engine's tick-input arrays
   uint64_t term, vote, leader, committed, applied, last, marker, marker_term, snap_index, snap_term, cap_base;
   uint32_t role, etick, htick, rand_to, rng_ctr, granted, responded, active, err, drops;
   uint64_t rm[R], rn[R], rs[R];  // remote match / next / snapshot index
@@ -71,6 +72,8 @@ struct Ctl {
     g = q - s * p.G;
     gg = pl_group(p.pl, s, g);
     rid = gg * R + s;
+    gi = pl_input_index(p.pl, gg);
+    ri = gi * R + s;
     const uint64_t n = p.nrep;
     const uint64_t* a = p.s64_in + q;
     term = a[S_TERM * n]; vote = a[S_VOTE * n]; leader = a[S_LEADER * n]; committed = a[S_COMMITTED * n];
@@ -122,7 +125,7 @@ struct Ctl {
     return (uint32_t)(packed >> (8 * d)) & 0xFF;
   }
   RG_FN bool lost(uint32_t dst, uint32_t n) const {
-    if (p.isolate && (p.isolate[rid] || p.isolate[gg * R + dst])) return true;
+    if (p.isolate && (p.isolate[ri] || p.isolate[gi * R + dst])) return true;
     if (p.drop_ppm) {
       uint64_t h = mix64(p.seed ^ mix64((p.tick << 40) ^ ((uint64_t)rid << 8) ^ dst) ^ (uint64_t)(n + 1));
       if (h % 1000000ull < p.drop_ppm) return true;
@@ -599,10 +602,10 @@ struct Ctl {
       const uint32_t cnt = (remote ? p.rcnt : p.cnt_in)[((uint64_t)src * R + s) * p.G + g];
       for (uint32_t k = 0; k < cnt; ++k) handle(src, k, remote);
     }
-    if (p.campaign && p.campaign[rid]) handle_node_election();
+    if (p.campaign && p.campaign[ri]) handle_node_election();
     if (!(p.flags & 1u)) tick();
-    if (p.prop_target && p.prop_target[gg] == s) {
-      const uint32_t n = p.prop_count[gg];
+    if (p.prop_target && p.prop_target[gi] == s) {
+      const uint32_t n = p.prop_count[gi];
       if (n > 0) handle_propose(n, (uint32_t)(p.tick % p.nslab), 0);
     }
     applied = committed;  // apply, snapshot, compaction

@@ -270,7 +270,7 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   e->c = c;
   e->c.ranks = N;
   e->nrep = c.groups * c.replicas;
-  e->pl = make_placement(N, c.rank, c.wire_all);
+  e->pl = make_placement(N, c.rank, c.wire_all, c.column_base);
   e->wire = N > 1 || c.wire_all;
   e->slab_rows = e->wire ? e->nrep : c.groups;  // wire engines: one slab row per replica (bulk_kernel<LG, true>)
   e->J = (c.replicas - 1) * c.max_msgs_per_pair + 2;  // >= appends one step can make
@@ -744,8 +744,9 @@ int rg_deliver(rg_engine* e, uint32_t rid_src, const rg_msg_view* m) {
 
 int rg_leader(rg_engine* e, uint32_t group, uint64_t* leader_id, uint64_t* term, int* valid) {
   const uint32_t N = e ? e->pl.N : 1;
-  if (!e || (uint64_t)group >= (uint64_t)e->c.groups * N) return fail(RG_EINVAL, "rg_leader: bad group");
-  const uint32_t R = e->c.replicas, j = group / N;
+  const uint64_t g0 = e ? (uint64_t)N * e->pl.col_base : 0;
+  if (!e || group < g0 || (uint64_t)group >= g0 + (uint64_t)e->c.groups * N) return fail(RG_EINVAL, "rg_leader: bad group");
+  const uint32_t R = e->c.replicas, j = group / N - e->pl.col_base;
   std::vector<rg_replica_view> v;
   for (uint32_t s = 0; s < R; ++s) {
     if (pl_rank_of(e->pl, group, s) != e->pl.rank) continue;  // replica hosted elsewhere

@@ -55,12 +55,13 @@ enum : uint32_t { SRC_NONE = 0, SRC_RING = 1, SRC_SLAB = 2, SRC_WIRE = 3 };
 // that a dynamic index could push into scratch.
 constexpr uint32_t MAX_RANKS = 16;
 struct Placement {
-  uint32_t N, rank, wire_all, _pad;
+  uint32_t N, rank, wire_all, col_base;  // col_base: global column of local column 0
 };
+// j: LOCAL column (global column = col_base + j)
 RG_HD_INLINE uint32_t pl_soff(const Placement& pl, uint32_t s, uint32_t j) {
   if (s == 0 || pl.N < 2) return 0;
   const uint32_t m = pl.N - 1;
-  return (j % m + s - 1) % m + 1;
+  return ((pl.col_base + j) % m + s - 1) % m + 1;
 }
 // rank offset of the plane s→d at column j (0 = co-located)
 RG_HD_INLINE uint32_t pl_off(const Placement& pl, uint32_t s, uint32_t d, uint32_t j) {
@@ -70,22 +71,25 @@ RG_HD_INLINE uint32_t pl_off(const Placement& pl, uint32_t s, uint32_t d, uint32
 RG_HD_INLINE bool pl_remote(const Placement& pl, uint32_t s, uint32_t d, uint32_t j) {
   return pl.wire_all || pl_off(pl, s, d, j) != 0;
 }
-inline Placement make_placement(uint32_t N, uint32_t rank, uint32_t wire_all) {
+inline Placement make_placement(uint32_t N, uint32_t rank, uint32_t wire_all, uint32_t col_base = 0) {
   Placement pl{};
   pl.N = N ? N : 1;
   pl.rank = rank;
   pl.wire_all = wire_all ? 1 : 0;
+  pl.col_base = col_base;
   return pl;
 }
 // global group of local replica (slot s, column j) on this rank
 RG_HD_INLINE uint64_t pl_group(const Placement& pl, uint32_t s, uint32_t j) {
   const uint32_t N = pl.N;
-  return (uint64_t)N * j + (pl.rank + N - pl_soff(pl, s, j) % N) % N;
+  return (uint64_t)N * (pl.col_base + j) + (pl.rank + N - pl_soff(pl, s, j) % N) % N;
 }
-// rank hosting slot s of global group g
+// index of global group g in this engine's tick-input arrays (they start at its first group)
+RG_HD_INLINE uint64_t pl_input_index(const Placement& pl, uint64_t g) { return g - (uint64_t)pl.N * pl.col_base; }
+// rank hosting slot s of global group g (g within this engine's columns)
 RG_HD_INLINE uint32_t pl_rank_of(const Placement& pl, uint64_t g, uint32_t s) {
   const uint32_t N = pl.N;
-  return (uint32_t)((g % N + pl_soff(pl, s, (uint32_t)(g / N))) % N);
+  return (uint32_t)((g % N + pl_soff(pl, s, (uint32_t)(g / N - pl.col_base))) % N);
 }
 
 struct TickParams {

@@ -1,6 +1,7 @@
-"""Worker of test_gpu_cluster.test_two_processes_gloo: N processes (one rank each, gloo) step a
-DistEngine on the same GPU; rank 0 compares every replica with the C oracle of all shards.
-usage: python dist_worker.py N"""
+"""Worker of test_gpu_cluster's two-process tests: N processes (one rank each, gloo) step a
+DistEngine (1 or 2 column halves) on the same GPU — chaos ticks through tick(), then steady
+proposal ticks through the pipelined step_device() when there are two halves; rank 0 compares
+every replica with the C oracle of all shards. usage: python dist_worker.py N [halves]"""
 import os
 import sys
 
@@ -12,7 +13,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 import torch.multiprocessing as mp  # noqa: E402
 
-G_LOCAL, R, TICKS = 6, 3, 60
+G_LOCAL, R, TICKS, STEADY = 6, 3, 60, 12
 CFG = dict(replicas=R, log_capacity=64, payload_bytes=32, max_entries_per_msg=8, snapshot_entries=20,
            compaction_overhead=5, drop_ppm=100000, seed=77)
 
@@ -26,25 +27,44 @@ def inputs(rng, G):
     return pt, pc, camp, iso
 
 
-def worker(rank, n):
+def snapshot(de):
+    mine = {}
+    for p in de.parts:
+        e = p.eng
+        for lr, v in enumerate(e.replicas()):
+            _, gr = e.global_id(lr)
+            lo = max(v["marker"] + 1, v["last"] - 7)
+            ents = e.entries(lr, lo, v["last"] - lo + 1, with_payload=True) if v["last"] >= lo else []
+            mine[gr] = (v, [e.msgs(lr, d) for d in range(R)], lo, ents)
+    return mine
+
+
+def worker(rank, n, halves):
     dist.init_process_group("gloo", rank=rank, world_size=n)
     from raftd_amd.cluster import DistEngine
-    de = DistEngine(groups=G_LOCAL, device=0, **CFG)
-    de.eng.bootstrap()
-    G = G_LOCAL * n
+    de = DistEngine(groups=G_LOCAL * halves, halves=halves, device=0, **CFG)
+    de.bootstrap()
+    G = G_LOCAL * halves * n
     rng = np.random.default_rng(3)
     views = []
     for t in range(TICKS):
         de.tick(*inputs(rng, G))
-        mine = {}
-        for lr, v in enumerate(de.eng.replicas()):
-            _, gr = de.eng.global_id(lr)
-            lo = max(v["marker"] + 1, v["last"] - 7)
-            ents = de.eng.entries(lr, lo, v["last"] - lo + 1, with_payload=True) if v["last"] >= lo else []
-            mine[gr] = (v, [de.eng.msgs(lr, d) for d in range(R)], lo, ents)
         allv = [None] * n
-        dist.all_gather_object(allv, mine)
+        dist.all_gather_object(allv, snapshot(de))
         views.append({k: x for d in allv for k, x in d.items()})
+    steady = []
+    if halves > 1:  # pipelined: every half's exchange overlaps the other half's tick
+        pt = np.zeros(G, np.uint8)
+        pc = np.full(G, 5, np.uint32)
+        dpt = torch.tensor(pt, device="cuda")
+        dpc = torch.tensor(pc.astype(np.int32), device="cuda")
+        for _ in range(STEADY):
+            de.step_device(dpt.data_ptr(), dpc.data_ptr())
+        de.drain()
+        de.sync()
+        allv = [None] * n
+        dist.all_gather_object(allv, snapshot(de))
+        steady = {k: x for d in allv for k, x in d.items()}
     if rank == 0:
         from oracle.pyoracle import Oracle
         ora = Oracle(groups=G, **CFG)
@@ -52,18 +72,27 @@ def worker(rank, n):
         rng = np.random.default_rng(3)
         for t in range(TICKS):
             ora.tick(*inputs(rng, G))
-            for gr in range(G * R):
-                v, ms, lo, ents = views[t][gr]
-                ov = ora.replica(gr)
-                assert v == ov, (t, gr, {k: (v[k], ov[k]) for k in ov if v[k] != ov[k]})
-                assert ms == [ora.msgs(gr, d) for d in range(R)], (t, gr)
-                oe = [ora.entry(gr, i, with_payload=True) for i in range(lo, v["last"] + 1)]
-                assert ents == oe, (t, gr)
+            check(ora, views[t], G, t)
+        if halves > 1:
+            for _ in range(STEADY):
+                ora.tick(np.zeros(G, np.uint8), np.full(G, 5, np.uint32))
+            check(ora, steady, G, "steady")
         print("dist parity ok", flush=True)
     dist.barrier()
     dist.destroy_process_group()
 
 
+def check(ora, snap, G, t):
+    for gr in range(G * R):
+        v, ms, lo, ents = snap[gr]
+        ov = ora.replica(gr)
+        assert v == ov, (t, gr, {k: (v[k], ov[k]) for k in ov if v[k] != ov[k]})
+        assert ms == [ora.msgs(gr, d) for d in range(R)], (t, gr)
+        oe = [ora.entry(gr, i, with_payload=True) for i in range(lo, v["last"] + 1)]
+        assert ents == oe, (t, gr)
+
+
 if __name__ == "__main__":
     n = int(sys.argv[1])
-    mp.spawn(worker, args=(n,), nprocs=n, join=True)
+    halves = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    mp.spawn(worker, args=(n, halves), nprocs=n, join=True)

@@ -114,3 +114,33 @@ def test_two_processes_gloo():
 def test_cluster_full_batches():
     cfg = dict(CHAOS, log_capacity=256, max_entries_per_msg=64, snapshot_entries=120, payload_bytes=16)
     run_chaos(3, dict(groups=9, replicas=3, seed=37, **cfg), ticks=120, seed=65, p_camp=0.04)
+
+
+def test_column_halves_match_oracle_windows():
+    """A rank's columns split over two engines (column_base): each half cluster reproduces its
+    window of the oracle of all groups — the layout DistEngine(halves=2) pipelines."""
+    from raftd_amd.cluster import LoopbackCluster
+    N, G, R = 4, 16, 3
+    cfg = dict(replicas=R, seed=71, **CHAOS)
+    halves = [LoopbackCluster(ranks=N, groups=G // 2, column_base=h * (G // 2) // N, **cfg) for h in range(2)]
+    oras = [make("c", groups=G // 2, group_base=h * G // 2, **cfg) for h in range(2)]
+    for x in halves + oras:
+        x.bootstrap()
+    rng = np.random.default_rng(72)
+    for t in range(80):
+        pt, pc, camp, iso = random_inputs(rng, G, R, CHAOS["max_entries_per_msg"])
+        for h in range(2):
+            g0, n = h * G // 2, G // 2
+            ins = (pt[g0:g0 + n], pc[g0:g0 + n], camp[g0 * R:(g0 + n) * R], iso[g0 * R:(g0 + n) * R])
+            halves[h].tick(*ins)
+            oras[h].tick(*ins)
+            compare(halves[h], oras[h], t)
+
+
+def test_two_processes_gloo_halves():
+    """DistEngine(halves=2) in two processes: plain ticks, then pipelined step_device ticks."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29534")
+    out = subprocess.run([sys.executable, "-u", os.path.join(HERE, "dist_worker.py"), "2", "2"], env=env,
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert "dist parity ok" in out.stdout
