@@ -17,7 +17,9 @@ N > 1 (default --placement spread, the north star's layout): one process per GPU
 (torch.distributed.run), N x 65,536 groups, replica slot s of group g on GPU (g mod N + off(s)) mod N
 (DESIGN.md §6), so every replica of a group sits on a different GPU, emulating separate nodes.
 Each step = the exchange of the previous tick's cross-GPU messages (plan/pack kernels, one RCCL
-all_to_all_single over xGMI — the only collective — and the unpack kernel) + the tick. Every GPU
+all_to_all_single over xGMI — the only collective — and the unpack kernel) + the tick; with
+--halves 2 (default) each GPU's columns are two engines whose exchanges are pipelined behind each
+other's ticks. Every GPU
 hosts 196,608 replicas, as at N = 1 (weak scaling). --placement colocated keeps every replica of
 a group on one GPU (no exchange). value = groups over all ranks x K / max-over-ranks time.
 --wire-all (N = 1, measurement): every message goes through the pack/unpack path to itself.
