@@ -169,6 +169,23 @@ typedef struct rg_persist_entry {
   uint32_t type, len, crc, rid; /* payload at payload + k * payload_bytes when len > 0 */
 } rg_persist_entry;
 
+/* Snapshot events of the last tick (rg_snapshot_events): where dragonboat's rsm calls the state
+ * machine's RecoverFromSnapshot (an InstallSnapshot restored the replica's log) and
+ * PrepareSnapshot + SaveSnapshot (SnapshotEntries applied since the last snapshot), which raftd
+ * forwards to the application (raft/state_machine.go:186-275). Host order per replica and tick:
+ * recover to `restored`, Update the tick's applied entries, then save the snapshot at `index`. */
+#define RG_SNAP_TAKEN 1u    /* a snapshot at index/term was taken at the end of the tick */
+#define RG_SNAP_RESTORED 2u /* the log was restored to a snapshot at `restored` during the tick */
+typedef struct rg_snapshot_event {
+  uint64_t group;       /* global shard id */
+  uint32_t replica_id;  /* slot + 1 */
+  uint32_t rid;         /* local replica id */
+  uint32_t kind;        /* RG_SNAP_* bits */
+  uint32_t _pad;
+  uint64_t restored;    /* kind & RG_SNAP_RESTORED: snapshot index the log was restored to */
+  uint64_t index, term; /* kind & RG_SNAP_TAKEN: the new snapshot's index (= applied) and term */
+} rg_snapshot_event;
+
 typedef struct rg_engine rg_engine;
 
 int rg_create(const rg_config* cfg, rg_engine** out);
@@ -235,8 +252,9 @@ int rg_wire_pack(rg_engine* e, void* send_buf, uint64_t send_cap);
 int rg_wire_recv(rg_engine* e, const void* recv_buf, const uint64_t* recv_bytes /*[ranks]*/);
 /* Committed-entry copy-back: the non-empty application entries that the
  * replicas whose slot bit is set in slot_mask applied in the last tick — config changes, leader
- * no-ops and snapshot-restored ranges excluded, as dragonboat's rsm does before Update — in
- * (local replica, index) order. Compacted on the device, then copied back by one hipMemcpyAsync
+ * no-ops and snapshot-restored ranges excluded, as dragonboat's rsm does before Update — grouped
+ * by replica in device order (slot by slot, shards ascending within a slot), each replica's
+ * entries in index order. Compacted on the device, then copied back by one hipMemcpyAsync
  * per array into entries[cap] and payload[cap * payload_bytes] (host memory; pinned is fastest).
  * *n = the count; if *n > cap nothing is copied and RG_EFULL is returned. Synchronous. */
 int rg_apply_committed(rg_engine* e, uint32_t slot_mask, rg_apply_entry* entries, uint8_t* payload, uint64_t cap,
@@ -249,6 +267,10 @@ int rg_apply_committed(rg_engine* e, uint32_t slot_mask, rg_apply_entry* entries
  * Restart = rg_import_replica of the replayed state. */
 int rg_persist_collect(rg_engine* e, int full, rg_persist_state* states, uint64_t cap_states, uint64_t* n_states,
                        rg_persist_entry* entries, uint8_t* payload, uint64_t cap_entries, uint64_t* n_entries);
+/* Snapshot events of the last tick for replicas whose slot bit is set in slot_mask, one per
+ * replica in device order (slot by slot, shards ascending within a slot), compacted on the device and copied back by one hipMemcpyAsync. *n = the count;
+ * if *n > cap nothing is copied and RG_EFULL is returned. Synchronous. */
+int rg_snapshot_events(rg_engine* e, uint32_t slot_mask, rg_snapshot_event* events, uint64_t cap, uint64_t* n);
 /* Global group and global replica id (group·replicas + slot) of local replica rid. */
 int rg_global_id(rg_engine* e, uint32_t rid, uint64_t* group, uint64_t* global_rid);
 /* Measurement helper: this device's streaming-copy bandwidth, (read + write bytes) / s, of a

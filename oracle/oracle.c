@@ -54,6 +54,7 @@ typedef struct {
   /* apply window of the last step: entries apply_lo .. applied went to the state machine
    * (rsm → IOnDiskStateMachine.Update); a range restored from a snapshot does not */
   uint64_t apply_lo, restored_at;
+  int took; /* a snapshot was taken at the end of the last step */
 } rep_t;
 
 struct or_engine {
@@ -711,6 +712,7 @@ static void step_replica(or_engine* e, rep_t* r) {
   uint32_t R = e->c.replicas, K = e->c.max_msgs_per_pair;
   uint64_t marker_start = r->marker, applied_start = r->applied;
   r->restored_at = 0;
+  r->took = 0;
   outbox_t* ob = cur_ob(e, r);
   memset(ob->n, 0, sizeof ob->n);
   memset(ob->emitted, 0, sizeof ob->emitted);
@@ -751,6 +753,7 @@ static void step_replica(or_engine* e, rep_t* r) {
   if (e->c.snapshot_entries && r->applied - r->snap_index >= e->c.snapshot_entries) {
     r->snap_index = r->applied;
     r->snap_term = term_of(e, r, r->applied);
+    r->took = 1;
     uint64_t c = r->snap_index > e->c.compaction_overhead ? r->snap_index - e->c.compaction_overhead : 0;
     if (c > r->marker) {
       r->marker_term = term_of(e, r, c);
@@ -964,6 +967,8 @@ int or_import_replica(or_engine* e, uint32_t rid, const or_replica_view* v, cons
   r->snap_index = v->snap_index;
   r->snap_term = v->snap_term;
   r->cap_base = v->cap_base;
+  r->restored_at = 0;
+  r->took = 0;
   r->role = v->role;
   r->election_tick = v->election_tick;
   r->heartbeat_tick = v->heartbeat_tick;
@@ -1020,6 +1025,17 @@ int or_deliver(or_engine* e, uint32_t rid_src, const or_msg_view* m) {
     ob->n_ents += m->nent;
   }
   return 0;
+}
+
+/* Snapshot events of replica rid's last step (rg_snapshot_events): returns OR_SNAP_* bits;
+ * restored = the index an InstallSnapshot restored the log to, index/term = the snapshot taken. */
+int or_get_snapshot_event(const or_engine* e, uint32_t rid, uint64_t* restored, uint64_t* index, uint64_t* term) {
+  if (rid >= e->nrep) return -1;
+  const rep_t* r = &e->reps[rid];
+  if (restored) *restored = r->restored_at;
+  if (index) *index = r->took ? r->snap_index : 0;
+  if (term) *term = r->took ? r->snap_term : 0;
+  return (r->restored_at ? OR_SNAP_RESTORED : 0) | (r->took ? OR_SNAP_TAKEN : 0);
 }
 
 /* The non-empty application entries replica rid handed to the state machine in the last step

@@ -110,6 +110,10 @@ int or_deliver(or_engine* e, uint32_t rid_src, const or_msg_view* m);
  * input), in index order. Returns the count; fills up to cap. Any output may be NULL. */
 int or_get_applied(const or_engine* e, uint32_t rid, uint64_t* index, or_entry_view* out, uint8_t* payload,
                    uint32_t cap);
+/* Snapshot events of rid's last step (the oracle side of rg_snapshot_events): OR_SNAP_* bits. */
+#define OR_SNAP_TAKEN 1
+#define OR_SNAP_RESTORED 2
+int or_get_snapshot_event(const or_engine* e, uint32_t rid, uint64_t* restored, uint64_t* index, uint64_t* term);
 /* Proposal payload generator. */
 void or_payload(const or_engine* e, uint32_t slab, uint32_t group, uint32_t entry, uint8_t* out);
 uint32_t or_crc32(const uint8_t* p, size_t n);

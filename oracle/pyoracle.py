@@ -100,6 +100,8 @@ def lib():
         L.or_get_msg_terms.argtypes = [vp, u32, u32, u32, C.POINTER(C.c_uint64), u32]
         L.or_get_entry.argtypes = [vp, u32, u64, C.POINTER(EntryView), C.c_void_p]
         L.or_get_applied.argtypes = [vp, u32, C.c_void_p, C.c_void_p, C.c_void_p, u32]
+        L.or_get_snapshot_event.argtypes = [vp, u32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                            C.POINTER(C.c_uint64)]
         L.or_import_replica.argtypes = [vp, u32, C.POINTER(ReplicaView), C.c_void_p, C.c_void_p, C.c_void_p]
         L.or_deliver.argtypes = [vp, u32, C.POINTER(MsgView)]
         L.or_payload.argtypes = [vp, u32, u32, u32, C.c_void_p]
@@ -236,6 +238,12 @@ class Oracle:
         pay = (C.c_uint8 * max(1, n * P))()
         self.L.or_get_applied(self.h, rid, idx, ev, pay, n)
         return [(idx[k], ev[k].len, ev[k].crc, bytes(pay[k * P:k * P + ev[k].len])) for k in range(n)]
+
+    def snapshot_event(self, rid):
+        """(kind, restored, index, term) of rid's last step (oracle side of rg_snapshot_events)."""
+        r, i, t = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        k = self.L.or_get_snapshot_event(self.h, rid, C.byref(r), C.byref(i), C.byref(t))
+        return k, r.value, i.value, t.value
 
     def log_terms(self, rid):
         r = self.replica(rid)

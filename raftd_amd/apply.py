@@ -50,7 +50,7 @@ class UpdateBatch:
 
 
 def batches(recs, pay) -> list:
-    """Split an rg_apply_committed batch (records in (local replica, index) order) per replica."""
+    """Split an rg_apply_committed batch (grouped by replica, each in index order) per replica."""
     out, cur = [], None
     for k in range(len(recs)):
         r = recs[k]

@@ -17,6 +17,8 @@ pair.
 """
 from __future__ import annotations
 
+import numpy as np
+
 from .engine import Engine, default_config
 
 
@@ -146,7 +148,44 @@ class _Half:
             self.rsizes = None
 
 
-class DistEngine:
+class _Feeds:
+    """The per-tick host feeds (rg_snapshot_events, rg_apply_committed) over several engines, in
+    this object's replica ids, replica order (what SnapshotDriver / Applier consume)."""
+
+    _rid_base = 0
+
+    def _feed_engines(self):
+        raise NotImplementedError
+
+    def _feed_maps(self):
+        if getattr(self, "_gmaps", None) is None:  # local rid → id here, once
+            self._gmaps = [np.array([e.global_id(lr)[1] for lr in range(e.nrep)], np.int64) - self._rid_base
+                           for e in self._feed_engines()]
+        return self._gmaps
+
+    def snapshot_events(self, slot_mask: int = 0xFF):
+        parts = []
+        for e, gm in zip(self._feed_engines(), self._feed_maps()):
+            ev = e.snapshot_events(slot_mask).copy()
+            ev["rid"] = gm[ev["rid"].astype(np.int64)]
+            parts.append(ev)
+        out = np.concatenate(parts)
+        return out[np.argsort(out["rid"], kind="stable")]
+
+    def apply_committed(self, slot_mask: int = 0xFF):
+        recs, pays = [], []
+        for e, gm in zip(self._feed_engines(), self._feed_maps()):
+            r, p = e.apply_committed(slot_mask)
+            r = r.copy()
+            r["rid"] = gm[r["rid"].astype(np.int64)]
+            recs.append(r)
+            pays.append(p)
+        recs, pays = np.concatenate(recs), np.concatenate(pays)
+        order = np.argsort(recs["rid"], kind="stable")  # each replica's entries stay in index order
+        return recs[order], pays[order]
+
+
+class DistEngine(_Feeds):
     """This process's share of an N-rank cluster (rank = torch.distributed rank): `groups` local
     columns (the cluster hosts ranks * groups shards), as `halves` engines over disjoint column
     ranges. Engines launch on torch's current stream, so each exchange orders itself behind the
@@ -176,6 +215,10 @@ class DistEngine:
         self.cfg, self.R = engs[0].cfg, engs[0].R
         self.async_ok = dist.get_backend(group) == "nccl"
         self.primed = False
+
+    def _feed_engines(self):  # host feeds in global replica ids
+        self.drain()
+        return [p.eng for p in self.parts]
 
     @property
     def wire_bytes(self) -> int:  # bytes this rank sent in the last exchange of every half
@@ -269,7 +312,7 @@ class DistEngine:
 
 
 # ---------------------------------------------------------------- N ranks in one process
-class LoopbackCluster:
+class LoopbackCluster(_Feeds):
     """N engines (ranks) in one process on one GPU, moving regions with device copies. The
     interface is the single Engine's, in global ids counted from the cluster's first group
     (ranks * column_base, like an oracle window's group_base): replica id g * R + s, `groups` =
@@ -284,6 +327,7 @@ class LoopbackCluster:
         self.G, self.R = groups, self.cfg["replicas"]
         self.nrep = self.G * self.R
         self.rid0 = ranks * column_base * self.R  # ids are relative to the first group, as inputs are
+        self._rid_base = self.rid0
         lc = dict(self.cfg, groups=groups // ranks, column_base=column_base)
         self.engines = [Engine(**dict(lc, ranks=ranks, rank=k)) for k in range(ranks)]
         dev = torch.device("cuda", self.cfg["device"])
@@ -299,6 +343,9 @@ class LoopbackCluster:
     def close(self):
         for e in self.engines:
             e.close()
+
+    def _feed_engines(self):
+        return self.engines
 
     def bootstrap(self):
         for e in self.engines:

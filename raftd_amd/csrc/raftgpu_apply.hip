@@ -190,4 +190,44 @@ hipError_t launch_persist_gather(const PersistParams& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// ================================================================== snapshot events
+// control_kernel leaves snap_ev[q] = restored_at | SNAP_TAKEN_BIT per replica; compact the
+// non-zero ones (thread per replica, coalesced) into rg_snapshot_event records.
+
+__global__ void snap_count_kernel(SnapParams a) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= a.nrep) return;
+  a.cnt[q] = ((a.slot_mask >> (q / a.G)) & 1u) && a.snap_ev[q] != 0 ? 1u : 0u;
+}
+
+hipError_t launch_snap_count(const SnapParams& a, uint64_t* total, hipStream_t st) {
+  hipLaunchKernelGGL(snap_count_kernel, dim3((a.nrep + 255) / 256), dim3(256), 0, st, a);
+  hipError_t r = launch_scan_u32(a.cnt, a.nrep, a.bsum, a.off, st);
+  if (r != hipSuccess) return r;
+  hipLaunchKernelGGL(apply_total_kernel, dim3(1), dim3(1), 0, st, a.off, a.nrep, total);
+  return hipGetLastError();
+}
+
+__global__ void snap_gather_kernel(SnapParams a) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= a.nrep || !a.cnt[q]) return;
+  const uint64_t n = a.nrep, ev = a.snap_ev[q], restored = ev & ~SNAP_TAKEN_BIT;
+  const uint32_t s = q / a.G, j = q - s * a.G;
+  rg_snapshot_event r;
+  r.group = pl_group(a.pl, s, j);
+  r.replica_id = s + 1;
+  r.rid = j * a.R + s;
+  r.kind = (restored ? RG_SNAP_RESTORED : 0u) | ((ev & SNAP_TAKEN_BIT) ? RG_SNAP_TAKEN : 0u);
+  r._pad = 0;
+  r.restored = restored;
+  r.index = (ev & SNAP_TAKEN_BIT) ? a.s64[(uint64_t)S_SNAP_INDEX * n + q] : 0;
+  r.term = (ev & SNAP_TAKEN_BIT) ? a.s64[(uint64_t)S_SNAP_TERM * n + q] : 0;
+  reinterpret_cast<rg_snapshot_event*>(a.out)[a.off[q]] = r;
+}
+
+hipError_t launch_snap_gather(const SnapParams& a, hipStream_t st) {
+  hipLaunchKernelGGL(snap_gather_kernel, dim3((a.nrep + 255) / 256), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
 }  // namespace rg

@@ -63,6 +63,7 @@ struct Ctl {
   uint32_t rt[R];                // remote state
   uint64_t last_start, sent_hi, rw_lo, rw_hi, marker_start;
   uint64_t applied_start, restored_at;  // apply window: entries restored from a snapshot are not Update()d
+  bool took;                            // a snapshot was taken at the end of this step
   uint64_t wlo;                         // lowest log index written this step (EntriesToSave from here)
   uint64_t oc, em;  // per destination: enqueued / emitted counts, 8 bits each
   uint32_t nj;      // jobs emitted
@@ -91,7 +92,7 @@ struct Ctl {
       rt[j] = p.rst_in[j * n + q];
     });
     last_start = last; sent_hi = 0; rw_lo = ~0ull; rw_hi = 0; marker_start = marker;
-    applied_start = applied; restored_at = 0; wlo = ~0ull;
+    applied_start = applied; restored_at = 0; wlo = ~0ull; took = false;
     oc = 0; em = 0; nj = 0;
   }
 
@@ -612,6 +613,7 @@ struct Ctl {
     if (p.SE && applied - snap_index >= p.SE) {
       snap_index = applied;
       snap_term = term_at(applied);
+      took = true;
       const uint64_t c = snap_index > p.CO ? snap_index - p.CO : 0;
       if (c > marker) {
         marker_term = term_at(c);
@@ -643,6 +645,7 @@ struct Ctl {
     p.jcnt[q] = nj;
     if (p.apply_lo) p.apply_lo[q] = umax64(applied_start, restored_at) + 1;
     if (p.persist_lo) p.persist_lo[q] = wlo;
+    if (p.snap_ev) p.snap_ev[q] = restored_at | (took ? SNAP_TAKEN_BIT : 0ull);
   }
 #undef RG_GET
 #undef RG_SET

@@ -113,6 +113,7 @@ struct rg_engine {
   uint64_t astage_bytes = 0;
   // persistence copy-back
   uint64_t* persist_lo = nullptr;
+  uint64_t* snap_ev = nullptr;  // [nrep] restored_at | SNAP_TAKEN_BIT of the last tick
   uint32_t *pscnt = nullptr, *pecnt = nullptr;
   uint64_t *psoff = nullptr, *peoff = nullptr;
 };
@@ -205,6 +206,7 @@ static TickParams params(rg_engine* e) {
   p.rhdr = e->rhdr; p.rmt = e->rmt; p.rcnt = e->rcnt;
   p.apply_lo = e->apply_lo;
   p.persist_lo = e->persist_lo;
+  p.snap_ev = e->snap_ev;
   return p;
 }
 
@@ -308,6 +310,7 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if (rc == RG_OK) rc = dalloc(e, &e->aoff, (n + 1) * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->absum, ((n + 1023) / 1024 + 1) * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->persist_lo, n * 8);
+  if (rc == RG_OK) rc = dalloc(e, &e->snap_ev, n * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->pscnt, n * 4);
   if (rc == RG_OK) rc = dalloc(e, &e->pecnt, n * 4);
   if (rc == RG_OK) rc = dalloc(e, &e->psoff, (n + 1) * 8);
@@ -498,6 +501,7 @@ int rg_bootstrap(rg_engine* e) {
   if (e->rcnt) HIPCHK(hipMemsetAsync(e->rcnt, 0, R * R * G * 4, e->stream));
   HIPCHK(hipMemsetAsync(e->apply_lo, 0, (uint64_t)e->nrep * 8, e->stream));
   HIPCHK(hipMemsetAsync(e->persist_lo, 0xFF, (uint64_t)e->nrep * 8, e->stream));
+  HIPCHK(hipMemsetAsync(e->snap_ev, 0, (uint64_t)e->nrep * 8, e->stream));
   e->planned = e->wire_ready = false;
   e->recv = nullptr;
   HIPCHK(hipMemsetAsync(e->crc_err, 0, (uint64_t)e->nrep * 4, e->stream));
@@ -711,6 +715,7 @@ int rg_import_replica(rg_engine* e, uint32_t rid, const rg_replica_view* v, cons
   if (pb) HIPCHK(hipMemcpy(d + vb + wb + cb, payloads, pb, hipMemcpyHostToDevice));
   HIPCHK(launch_scatter_replica(admin(e), rid, d, (const uint64_t*)(d + vb), pb ? d + vb + wb + cb : nullptr,
                                 (const uint32_t*)(d + vb + wb), nent, e->stream, e->info, e->pay));
+  HIPCHK(hipMemsetAsync(e->snap_ev + rid, 0, 8, e->stream));  // no snapshot events until it steps
   HIPCHK(hipStreamSynchronize(e->stream));
   return RG_OK;
 }
@@ -842,6 +847,31 @@ int rg_apply_committed(rg_engine* e, uint32_t slot_mask, rg_apply_entry* entries
   LAUNCH(launch_apply_gather(a, e->stream), e->stream, "apply gather");
   HIPCHK(hipMemcpyAsync(entries, a.out_rec, rb, hipMemcpyDeviceToHost, e->stream));
   if (pb) HIPCHK(hipMemcpyAsync(payload, a.out_pay, pb, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return RG_OK;
+}
+
+int rg_snapshot_events(rg_engine* e, uint32_t slot_mask, rg_snapshot_event* events, uint64_t cap, uint64_t* n) {
+  if (!e || !n) return fail(RG_EINVAL, "rg_snapshot_events args");
+  if (int jrc = join(e)) return jrc;
+  const TickParams t = params(e);
+  SnapParams a{};
+  a.G = t.G; a.R = t.R; a.nrep = t.nrep; a.slot_mask = slot_mask; a.pl = e->pl;
+  a.s64 = t.s64_in; a.snap_ev = e->snap_ev;
+  a.cnt = e->acnt; a.off = e->aoff; a.bsum = e->absum;
+  LAUNCH(launch_snap_count(a, (uint64_t*)e->d_sum, e->stream), e->stream, "snapshot count");
+  uint64_t total = 0;
+  HIPCHK(hipMemcpyAsync(&total, e->d_sum, 8, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  *n = total;
+  if (total == 0) return RG_OK;
+  if (total > cap) return fail(RG_EFULL, "rg_snapshot_events: " + std::to_string(total) + " events > cap");
+  if (!events) return fail(RG_EINVAL, "rg_snapshot_events: null output");
+  const uint64_t rb = total * sizeof(rg_snapshot_event);
+  RGCHK(astage_reserve(e, rb));
+  a.out = e->astage;
+  LAUNCH(launch_snap_gather(a, e->stream), e->stream, "snapshot gather");
+  HIPCHK(hipMemcpyAsync(events, a.out, rb, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   return RG_OK;
 }

@@ -119,6 +119,7 @@ struct TickParams {
   const uint32_t* rcnt;
   uint64_t* apply_lo;      // [nrep] first index this step hands to the state machine (NULL: skip)
   uint64_t* persist_lo;    // [nrep] lowest index written this step, ~0 if none (NULL: skip)
+  uint64_t* snap_ev;       // [nrep] restored_at | SNAP_TAKEN_BIT (NULL: skip)
   uint64_t* job64;         // [J64_ROWS][J][nrep]
   uint32_t* job32;         // [J32_ROWS][J][nrep]
   uint32_t* jcnt;          // [nrep]
@@ -182,6 +183,20 @@ struct ApplyParams {
   uint8_t* out_pay;         // [n][P]
 };
 hipError_t launch_apply_count(const ApplyParams& a, uint64_t* total, hipStream_t s);
+// snapshot events (raftgpu_apply.hip)
+constexpr uint64_t SNAP_TAKEN_BIT = 1ull << 63;
+struct SnapParams {
+  uint32_t G, R, nrep, slot_mask;
+  Placement pl;
+  const uint64_t* s64;      // current state (snap_index, snap_term)
+  const uint64_t* snap_ev;
+  uint32_t* cnt;
+  uint64_t* off;
+  uint64_t* bsum;
+  uint8_t* out;             // [n] rg_snapshot_event
+};
+hipError_t launch_snap_count(const SnapParams& a, uint64_t* total, hipStream_t s);
+hipError_t launch_snap_gather(const SnapParams& a, hipStream_t s);
 // persistence copy-back (raftgpu_apply.hip): per replica whose log or hard state changed in the
 // last tick, its state record and the entries it rewrote ([persist_lo, last]); full = every
 // replica with its whole log window (marker, last] (a checkpoint)

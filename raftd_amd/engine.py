@@ -85,6 +85,10 @@ PERSIST_STATE_DTYPE = np.dtype([("group", "<u8"), ("replica_id", "<u4"), ("rid",
 PERSIST_ENTRY_DTYPE = np.dtype([("index", "<u8"), ("term", "<u8"), ("type", "<u4"), ("len", "<u4"), ("crc", "<u4"),
                                 ("rid", "<u4")])
 
+SNAP_TAKEN, SNAP_RESTORED = 1, 2  # RG_SNAP_*
+SNAPSHOT_EVENT_DTYPE = np.dtype([("group", "<u8"), ("replica_id", "<u4"), ("rid", "<u4"), ("kind", "<u4"),
+                                 ("_pad", "<u4"), ("restored", "<u8"), ("index", "<u8"), ("term", "<u8")])
+
 
 class TickInput(C.Structure):
     _fields_ = [("prop_target", C.c_void_p), ("prop_count", C.c_void_p), ("campaign", C.c_void_p),
@@ -100,7 +104,7 @@ EXPORTS = ["rg_create", "rg_destroy", "rg_bootstrap", "rg_fill_slabs", "rg_tick"
            "rg_read_entries", "rg_import_replica", "rg_deliver", "rg_leader", "rg_sum_committed",
            "rg_device_bytes", "rg_last_error", "rg_last_tick_traffic", "rg_join",
            "rg_timing", "rg_kernel_ms", "rg_wire_plan", "rg_wire_pack", "rg_wire_recv", "rg_global_id",
-           "rg_apply_committed", "rg_probe_copy", "rg_persist_collect"]
+           "rg_apply_committed", "rg_probe_copy", "rg_persist_collect", "rg_snapshot_events"]
 
 _lib = None
 
@@ -153,6 +157,7 @@ def load_library(path: str = LIB_PATH):
         "rg_global_id": ([vp, u32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)], i32),
         "rg_apply_committed": ([vp, u32, vp, vp, u64, C.POINTER(C.c_uint64)], i32),
         "rg_probe_copy": ([C.c_int32, u64, C.c_int32, C.POINTER(C.c_double)], i32),
+        "rg_snapshot_events": ([vp, u32, vp, u64, C.POINTER(C.c_uint64)], i32),
         "rg_persist_collect": ([vp, i32, vp, u64, C.POINTER(C.c_uint64), vp, vp, u64, C.POINTER(C.c_uint64)], i32),
     }
     for name, (args, res) in sig.items():
@@ -281,6 +286,13 @@ class Engine:
     def replica(self, rid) -> dict:
         return self.replicas(rid, 1)[0]
 
+    def replica_array(self, first=0, n=None):
+        """rg_read_replicas as a numpy structured array (rg_replica_view fields), for bulk checks."""
+        n = self.nrep - first if n is None else n
+        buf = (ReplicaView * n)()
+        self._check(self.L.rg_read_replicas(self.h, first, n, buf))
+        return np.ctypeslib.as_array(buf).copy()
+
     def msgs(self, rid, dst) -> list:
         K, E = self.cfg["max_msgs_per_pair"], self.cfg["max_entries_per_msg"]
         buf = (MsgView * K)()
@@ -397,6 +409,17 @@ class Engine:
         self._check(self.L.rg_persist_collect(self.h, 1 if full else 0, st.ctypes.data, ns.value, C.byref(ns),
                                               en.ctypes.data, pay.ctypes.data, ne.value, C.byref(ne)))
         return st[:ns.value], en[:ne.value], pay[:ne.value, :P]
+
+    def snapshot_events(self, slot_mask: int = 0xFF):
+        """Snapshot events of the last tick (rg_snapshot_events): SNAPSHOT_EVENT_DTYPE rows, one
+        per replica, in device order (slot by slot)."""
+        n = C.c_uint64()
+        rc = self.L.rg_snapshot_events(self.h, slot_mask, None, 0, C.byref(n))
+        if rc < 0 and rc != RG_EFULL:
+            self._check(rc)
+        ev = np.zeros(max(n.value, 1), SNAPSHOT_EVENT_DTYPE)
+        self._check(self.L.rg_snapshot_events(self.h, slot_mask, ev.ctypes.data, n.value, C.byref(n)))
+        return ev[:n.value]
 
     def global_id(self, rid: int):
         """(global group, global replica id) of local replica rid."""

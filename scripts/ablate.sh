@@ -11,3 +11,4 @@ run() {
 }
 run product ""
 for v in "${vs[@]}"; do run $v RAFTGPU_LIB=$PWD/build_variants/$v.so; done
+run product_again ""
