@@ -92,6 +92,8 @@ typedef struct rg_config {
   uint32_t column_base;         /* global column of local column 0: a rank may host several engines
                                    over disjoint column ranges (their tick-input arrays then start
                                    at global group ranks·column_base) */
+  uint32_t crc32c;              /* entry checksum: 0 = CRC-32/IEEE (zlib's, default), 1 = CRC-32C
+                                   (Castagnoli, as pebble/tan WAL records use) */
 } rg_config;
 
 typedef struct rg_replica_view {

@@ -82,6 +82,21 @@ uint32_t or_crc32(const uint8_t* p, size_t n) {
   return (uint32_t)crc32(0L, p, (uInt)n);
 }
 
+uint32_t or_crc32c(const uint8_t* p, size_t n) {
+  /* CRC-32C (Castagnoli): reflected 0x82F63B78, init/xorout 0xFFFFFFFF, bit at a time (the
+   * published definition; Go's hash/crc32 MakeTable(crc32.Castagnoli)) */
+  uint32_t c = 0xFFFFFFFFu;
+  for (size_t i = 0; i < n; ++i) {
+    c ^= p[i];
+    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+  }
+  return c ^ 0xFFFFFFFFu;
+}
+
+static uint32_t entry_crc(const or_engine* e, const uint8_t* p, size_t n) {
+  return e->c.crc32c ? or_crc32c(p, n) : or_crc32(p, n);
+}
+
 void or_payload(const or_engine* e, uint32_t slab, uint32_t group, uint32_t entry, uint8_t* out) {
   /* DESIGN §1.3 payload generator */
   uint64_t key = or_mix64(((uint64_t)slab << 56) ^ ((uint64_t)group << 16) ^ (uint64_t)entry ^
@@ -237,7 +252,7 @@ static int append_entries(or_engine* e, rep_t* r, uint32_t n, int slab) {
       uint8_t* dst = logpay_at(e, r, idx);
       or_payload(e, (uint32_t)slab, (uint32_t)global_group(e, r), k, dst);
       en->len = P;
-      en->crc = or_crc32(dst, P);
+      en->crc = entry_crc(e, dst, P);
     } else {
       en->len = 0;
       en->crc = 0;
@@ -404,7 +419,7 @@ static void handle_replicate(or_engine* e, rep_t* r, const msg_in_t* m) {
           if (src->len) {
             uint8_t* dst = logpay_at(e, r, idx);
             memcpy(dst, m->pay + (size_t)k * P, src->len);
-            en->crc = or_crc32(dst, src->len);
+            en->crc = entry_crc(e, dst, src->len);
             if (en->crc != src->crc) r->err |= OR_ERR_CRC;
           } else {
             en->crc = 0;
@@ -994,7 +1009,7 @@ int or_import_replica(or_engine* e, uint32_t rid, const or_replica_view* v, cons
     if (payloads && P && en->type == OR_ENTRY_APP && !(types && (types[k] & OR_ENTRY_EMPTY))) {
       en->len = P;
       memcpy(logpay_at(e, r, i), payloads + k * P, P);
-      en->crc = or_crc32(logpay_at(e, r, i), P);
+      en->crc = entry_crc(e, logpay_at(e, r, i), P);
     } else {
       en->len = 0;
       en->crc = 0;

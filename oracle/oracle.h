@@ -51,6 +51,8 @@ typedef struct or_config {
                           reproduces that window of a larger run (groups are independent; RNG keys,
                           loss hashes and payloads use the global id; tick inputs are the window's) */
   uint64_t seed;
+  uint32_t crc32c; /* entry checksum: 0 = CRC-32/IEEE (zlib), 1 = CRC-32C (Castagnoli) */
+  uint32_t _pad;
 } or_config;
 
 /* Field order identical to rg_replica_view (include/raftgpu.h) so tests compare by name. */
@@ -117,6 +119,7 @@ int or_get_snapshot_event(const or_engine* e, uint32_t rid, uint64_t* restored, 
 /* Proposal payload generator. */
 void or_payload(const or_engine* e, uint32_t slab, uint32_t group, uint32_t entry, uint8_t* out);
 uint32_t or_crc32(const uint8_t* p, size_t n);
+uint32_t or_crc32c(const uint8_t* p, size_t n);
 uint64_t or_mix64(uint64_t z);
 
 #ifdef __cplusplus

@@ -33,6 +33,7 @@ class Config(C.Structure):
         ("election_rtt", C.c_uint32), ("heartbeat_rtt", C.c_uint32), ("check_quorum", C.c_uint32),
         ("snapshot_entries", C.c_uint32), ("compaction_overhead", C.c_uint32),
         ("drop_ppm", C.c_uint32), ("group_base", C.c_uint32), ("seed", C.c_uint64),
+        ("crc32c", C.c_uint32), ("_pad", C.c_uint32),
     ]
 
 
@@ -107,6 +108,8 @@ def lib():
         L.or_payload.argtypes = [vp, u32, u32, u32, C.c_void_p]
         L.or_crc32.argtypes = [C.c_void_p, C.c_size_t]
         L.or_crc32.restype = u32
+        L.or_crc32c.argtypes = [C.c_void_p, C.c_size_t]
+        L.or_crc32c.restype = u32
         L.or_mix64.argtypes = [u64]
         L.or_mix64.restype = u64
         _lib = L
@@ -117,7 +120,7 @@ def default_config(**kw) -> dict:
     """raftd's Raft parameters (raft/raft_manager.go:92-100) plus the engine's sizing."""
     c = dict(groups=4, replicas=3, log_capacity=2048, payload_bytes=256, max_entries_per_msg=64,
              max_msgs_per_pair=8, num_slabs=2, election_rtt=10, heartbeat_rtt=1, check_quorum=1,
-             snapshot_entries=1000, compaction_overhead=5, drop_ppm=0, seed=0x5EED, group_base=0)
+             snapshot_entries=1000, compaction_overhead=5, drop_ppm=0, seed=0x5EED, group_base=0, crc32c=0)
     c.update(kw)
     return c
 
@@ -288,6 +291,11 @@ class Oracle:
 def crc32(b: bytes) -> int:
     buf = C.create_string_buffer(b, len(b))
     return lib().or_crc32(buf, len(b))
+
+
+def crc32c(b: bytes) -> int:
+    buf = C.create_string_buffer(b, len(b))
+    return lib().or_crc32c(buf, len(b))
 
 
 def mix64(z: int) -> int:

@@ -118,12 +118,16 @@ struct rg_engine {
   uint64_t *psoff = nullptr, *peoff = nullptr;
 };
 
-// ---------------------------------------------------------------- CRC-32/IEEE tables
+// ---------------------------------------------------------------- CRC-32 tables
+// Reflected CRC-32, init and xorout 0xFFFFFFFF: IEEE (zlib) or Castagnoli (rg_config.crc32c).
+// Everything the kernels use (byte, nibble and shift tables, the finalisation constant) is built
+// here, so the device code is the same for both polynomials.
 static void build_crc(rg_engine* e, std::vector<uint32_t>& tab) {
   uint32_t* T0 = e->T0;
+  const uint32_t poly = e->c.crc32c ? 0x82F63B78u : 0xEDB88320u;
   for (uint32_t b = 0; b < 256; ++b) {
     uint32_t c = b;
-    for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
+    for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ poly : c >> 1;
     T0[b] = c;
   }
   auto Z = [&](uint32_t x) { return T0[x & 0xFF] ^ (x >> 8); };  // one zero byte
@@ -262,6 +266,7 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if ((uint64_t)c.groups * c.replicas > 0x7FFFFFFFull) return fail(RG_EINVAL, "too many replicas");
   const uint32_t N = c.ranks ? c.ranks : 1;
   if (N > MAX_RANKS || c.rank >= N) return fail(RG_EINVAL, "ranks in 1..16, rank < ranks");
+  if (c.crc32c > 1) return fail(RG_EINVAL, "crc32c must be 0 (IEEE) or 1 (Castagnoli)");
   if ((N > 1 || c.wire_all) && c.groups >= (1u << 24)) return fail(RG_EINVAL, "groups < 2^24 with ranks > 1");
   int ndev = 0;
   HIPCHK(hipGetDeviceCount(&ndev));

@@ -33,6 +33,7 @@ class Config(C.Structure):
         ("snapshot_entries", C.c_uint32), ("compaction_overhead", C.c_uint32),
         ("drop_ppm", C.c_uint32), ("device", C.c_int32), ("seed", C.c_uint64),
         ("ranks", C.c_uint32), ("rank", C.c_uint32), ("wire_all", C.c_uint32), ("column_base", C.c_uint32),
+        ("crc32c", C.c_uint32),
     ]
 
 
@@ -173,7 +174,7 @@ def default_config(**kw) -> dict:
     c = dict(groups=4, replicas=3, log_capacity=2048, payload_bytes=256, max_entries_per_msg=64,
              max_msgs_per_pair=8, num_slabs=2, election_rtt=10, heartbeat_rtt=1, check_quorum=1,
              snapshot_entries=1000, compaction_overhead=5, drop_ppm=0, device=0, seed=0x5EED,
-             ranks=1, rank=0, wire_all=0, column_base=0)
+             ranks=1, rank=0, wire_all=0, column_base=0, crc32c=0)
     c.update(kw)
     return c
 

@@ -39,6 +39,16 @@ def compare(gpu, ora, t, check_entries=True):
             assert ge == oe, f"tick {t} entries rid {rid}"
 
 
+def crc32c_py(b: bytes) -> int:
+    """CRC-32C (Castagnoli, reflected 0x82F63B78), bit at a time: independent of both engines."""
+    c = 0xFFFFFFFF
+    for x in b:
+        c ^= x
+        for _ in range(8):
+            c = (c >> 1) ^ (0x82F63B78 if c & 1 else 0)
+    return c ^ 0xFFFFFFFF
+
+
 def check_payloads(gpu, ora, sample=4):
     G, R = ora.G, ora.R
     if not ora.cfg["payload_bytes"]:
@@ -52,7 +62,8 @@ def check_payloads(gpu, ora, sample=4):
         for k, i in enumerate(range(lo, v["last"] + 1)):
             oe = ora.entry(rid, i, with_payload=True)
             assert ge[k]["payload"] == oe["payload"], (rid, i)
-            assert ge[k]["crc"] == (zlib.crc32(ge[k]["payload"]) if ge[k]["len"] else 0)
+            want = crc32c_py(ge[k]["payload"]) if ora.cfg.get("crc32c") else zlib.crc32(ge[k]["payload"])
+            assert ge[k]["crc"] == (want if ge[k]["len"] else 0)
 
 
 def run_pair(cfg, ticks, seed, check_every=1, **inkw):
@@ -78,6 +89,13 @@ CHAOS = dict(log_capacity=64, payload_bytes=16, max_entries_per_msg=8, snapshot_
 @pytest.mark.parametrize("R", [1, 2, 3, 4, 5, 7])
 def test_chaos_small(R):
     run_pair(dict(groups=4, replicas=R, seed=7 + R, **CHAOS), ticks=120, seed=R)
+
+
+@pytest.mark.parametrize("P", [16, 256, 1024])
+def test_chaos_crc32c(P):
+    """rg_config.crc32c = 1: every entry CRC is CRC-32C, bit-exact with the oracle."""
+    run_pair(dict(groups=6, replicas=3, seed=17, crc32c=1, **dict(CHAOS, payload_bytes=P)), ticks=100, seed=P,
+             check_every=5)
 
 
 @pytest.mark.parametrize("P", [0, 32, 64, 256, 1024])

@@ -16,6 +16,34 @@ def test_crc_kats():
     for v in d["ieee"]:
         assert pyoracle.crc32(bytes.fromhex(v["hex"])) == v["crc"]
     assert pyoracle.crc32(b"123456789") == 0xCBF43926
+    c = d["castagnoli_check"]
+    assert pyoracle.crc32c(bytes.fromhex(c["hex"])) == c["crc"] == 0xE3069283
+
+
+def test_crc32c_matches_bitwise_restatement():
+    from test_gpu_parity import crc32c_py
+    rng = np.random.default_rng(3)
+    for n in (0, 1, 15, 16, 255, 256, 1024):
+        b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert pyoracle.crc32c(b) == crc32c_py(b)
+
+
+def test_oracle_entry_crcs_follow_config():
+    from test_gpu_parity import crc32c_py
+    import zlib
+    for c32c in (0, 1):
+        o = pyoracle.Oracle(groups=2, replicas=3, payload_bytes=64, max_entries_per_msg=8, crc32c=c32c)
+        o.bootstrap()
+        o.tick()  # the bootstrap ConfigChange entries apply first; a campaign before that is dropped
+        o.tick(campaign=np.array([1, 0, 0, 1, 0, 0], np.uint8))
+        for _ in range(12):
+            o.tick(np.zeros(2, np.uint8), np.full(2, 3, np.uint32))
+        v = o.replica(1)
+        assert v["last"] >= 12, v
+        for i in range(v["marker"] + 1, v["last"] + 1):
+            e = o.entry(1, i, with_payload=True)
+            if e["len"]:
+                assert e["crc"] == (crc32c_py(e["payload"]) if c32c else zlib.crc32(e["payload"]))
 
 
 def test_mix64_and_payload_agree():
