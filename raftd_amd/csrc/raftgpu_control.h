@@ -7,6 +7,11 @@
 
 #include <type_traits>
 
+// entries per load batch in the control kernel's term copies (write_entries, send_replicate)
+#ifndef RG_CTL_BATCH
+#define RG_CTL_BATCH 8
+#endif
+
 #ifndef RG_FN
 #define RG_FN __device__ __forceinline__
 #endif
@@ -235,21 +240,36 @@ struct Ctl {
     const uint64_t hi_prot = umax64(last_start, sent_hi);
     wlo = umin64(wlo, base + e0);
     uint64_t dm = 0, sm = 0, hm = 0, tm = 0;
-    for (uint32_t e = e0; e < n; ++e) {
-      const uint64_t idx = base + e;
-      const uint64_t w = mt ? mt[(uint64_t)e * p.G] : word;
-      uint64_t* rp = tr_at(idx);
-      uint32_t tb = 0;
-      if (idx <= hi_prot) {  // protected this tick: rewrite goes to the other bank
-        const uint32_t cur = (uint32_t)(*rp >> 63);
-        const bool in_rw = idx >= rw_lo && idx <= rw_hi;
-        tb = in_rw ? cur : cur ^ 1u;
+    // RG_CTL_BATCH entries at a time: their loads (sender terms, current ring words of protected
+    // indices) are issued before any of their stores, so a lane waits one memory latency per
+    // batch instead of one per entry (the compiler cannot prove the ring and the inbox disjoint).
+    // The entries of one call occupy distinct ring slots (n <= L by the capacity rule).
+    for (uint32_t e = e0; e < n; e += RG_CTL_BATCH) {
+      uint64_t wv[RG_CTL_BATCH], ov[RG_CTL_BATCH];
+#pragma unroll
+      for (uint32_t k = 0; k < RG_CTL_BATCH; ++k) {
+        const uint64_t idx = base + e + k;
+        const bool in = e + k < n;
+        wv[k] = in && mt ? mt[(uint64_t)(e + k) * p.G] : word;
+        ov[k] = in && idx <= hi_prot ? *tr_at(idx) : 0;
       }
-      sm |= (w >> 63) << e;
-      hm |= ((w >> 62) & 1ull) << e;
-      tm |= ((w >> 61) & 1ull) << e;
-      dm |= (uint64_t)tb << e;
-      *rp = (w & ~BANK_BIT) | ((uint64_t)tb << 63);
+#pragma unroll
+      for (uint32_t k = 0; k < RG_CTL_BATCH; ++k) {
+        if (e + k >= n) break;
+        const uint32_t ek = e + k;
+        const uint64_t idx = base + ek, w = wv[k];
+        uint32_t tb = 0;
+        if (idx <= hi_prot) {  // protected this tick: rewrite goes to the other bank
+          const uint32_t cur = (uint32_t)(ov[k] >> 63);
+          const bool in_rw = idx >= rw_lo && idx <= rw_hi;
+          tb = in_rw ? cur : cur ^ 1u;
+        }
+        sm |= (w >> 63) << ek;
+        hm |= ((w >> 62) & 1ull) << ek;
+        tm |= ((w >> 61) & 1ull) << ek;
+        dm |= (uint64_t)tb << ek;
+        *tr_at(idx) = (w & ~BANK_BIT) | ((uint64_t)tb << 63);
+      }
     }
     const uint64_t lo_w = base + e0, hi_w = umin64(base + n - 1, hi_prot);
     if (lo_w <= hi_w) {
@@ -321,7 +341,14 @@ struct Ctl {
     const int k = send(M_REPLICATE, to + 1, 0, 0, n, lt, next - 1, committed, 0, 0, 0, 0);
     if (k >= 0 && n > 0) {
       uint64_t* mt = p.mt_out + ((((uint64_t)s * R + to) * p.K + (uint32_t)k) * p.E) * p.G + g;
-      for (uint32_t e = 0; e < n; ++e) mt[(uint64_t)e * p.G] = *tr_at(next + e);  // term|type|pay|bank
+      for (uint32_t e = 0; e < n; e += RG_CTL_BATCH) {  // term|type|pay|bank; batched as in write_entries
+        uint64_t v[RG_CTL_BATCH];
+#pragma unroll
+        for (uint32_t k2 = 0; k2 < RG_CTL_BATCH; ++k2) v[k2] = e + k2 < n ? *tr_at(next + e + k2) : 0;
+#pragma unroll
+        for (uint32_t k2 = 0; k2 < RG_CTL_BATCH; ++k2)
+          if (e + k2 < n) mt[(uint64_t)(e + k2) * p.G] = v[k2];
+      }
       sent_hi = umax64(sent_hi, next + n - 1);
     }
   }
