@@ -114,6 +114,7 @@ struct rg_engine {
   // persistence copy-back
   uint64_t* persist_lo = nullptr;
   uint64_t* snap_ev = nullptr;  // [nrep] restored_at | SNAP_TAKEN_BIT of the last tick
+  uint32_t* prof = nullptr;     // RG_CTL_PROFILE builds: control phase stamps of the last tick
   uint32_t *pscnt = nullptr, *pecnt = nullptr;
   uint64_t *psoff = nullptr, *peoff = nullptr;
 };
@@ -211,6 +212,7 @@ static TickParams params(rg_engine* e) {
   p.apply_lo = e->apply_lo;
   p.persist_lo = e->persist_lo;
   p.snap_ev = e->snap_ev;
+  p.prof = e->prof;
   return p;
 }
 
@@ -316,6 +318,9 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if (rc == RG_OK) rc = dalloc(e, &e->absum, ((n + 1023) / 1024 + 1) * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->persist_lo, n * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->snap_ev, n * 8);
+#ifdef RG_CTL_PROFILE
+  if (rc == RG_OK) rc = dalloc(e, &e->prof, n * 6 * 4);
+#endif
   if (rc == RG_OK) rc = dalloc(e, &e->pscnt, n * 4);
   if (rc == RG_OK) rc = dalloc(e, &e->pecnt, n * 4);
   if (rc == RG_OK) rc = dalloc(e, &e->psoff, (n + 1) * 8);
@@ -880,6 +885,16 @@ int rg_snapshot_events(rg_engine* e, uint32_t slot_mask, rg_snapshot_event* even
   HIPCHK(hipStreamSynchronize(e->stream));
   return RG_OK;
 }
+
+#ifdef RG_CTL_PROFILE
+// measurement builds only (not in include/raftgpu.h): the last control launch's phase stamps
+extern "C" int rg_debug_ctl_profile(rg_engine* e, uint32_t* out) {
+  if (!e || !out) return fail(RG_EINVAL, "rg_debug_ctl_profile args");
+  if (int jrc = join(e)) return jrc;
+  HIPCHK(hipMemcpy(out, e->prof, (uint64_t)e->nrep * 6 * 4, hipMemcpyDeviceToHost));
+  return RG_OK;
+}
+#endif
 
 int rg_global_id(rg_engine* e, uint32_t rid, uint64_t* group, uint64_t* global_rid) {
   if (!e || rid >= e->nrep) return fail(RG_EINVAL, "rg_global_id: bad replica");

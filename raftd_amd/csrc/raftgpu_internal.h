@@ -120,6 +120,7 @@ struct TickParams {
   uint64_t* apply_lo;      // [nrep] first index this step hands to the state machine (NULL: skip)
   uint64_t* persist_lo;    // [nrep] lowest index written this step, ~0 if none (NULL: skip)
   uint64_t* snap_ev;       // [nrep] restored_at | SNAP_TAKEN_BIT (NULL: skip)
+  uint32_t* prof;          // RG_CTL_PROFILE builds only: [6][nrep] s_memtime stamps per phase
   uint64_t* job64;         // [J64_ROWS][J][nrep]
   uint32_t* job32;         // [J32_ROWS][J][nrep]
   uint32_t* jcnt;          // [nrep]

@@ -31,7 +31,13 @@ template <int R>
 __global__ void __launch_bounds__(256, RG_CTL_MINWAVES) control_kernel(TickParams p) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= p.nrep) return;
+#ifdef RG_CTL_PROFILE
+  const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memtime();
   Ctl<R> c(p, q);
+  c.stamps[0] = t0;
+#else
+  Ctl<R> c(p, q);
+#endif
   c.run();
 }
 
