@@ -324,28 +324,11 @@ struct Ctl {
   }
 
   // ---- replication (A.12)
-  // A Replicate is built in three steps so that broadcast_replicate can issue every remote's loads
-  // before any store, and copy one batch of ring words into every remote that gets the same range:
-  //   prep  — the range and the term before it (loads only)
-  //   emit  — InstallSnapshot or the header and remote.progress (stores); the message slot or -1
-  //   copy  — the entries' term words into the message (batched as in write_entries)
-  struct Rep {
-    uint64_t next, lt;
-    uint32_t n;
-    int k;
-  };
-  RG_FN Rep rep_prep(uint32_t to) {
-    Rep r;
-    r.next = RG_GET(rn, to);
-    r.n = r.next <= last ? (uint32_t)umin64(p.E, last - r.next + 1) : 0;
-    r.lt = r.next > marker ? term_at(r.next - 1) : 0;
-    r.k = -1;
-    return r;
-  }
-  RG_FN void rep_emit(uint32_t to, Rep& r) {
+  RG_FN void send_replicate(uint32_t to) {
     const uint32_t st = RG_GET(rt, to);
     if (st == WAIT || st == SNAPSHOT) return;
-    if (r.next <= marker) {  // compacted: InstallSnapshot
+    const uint64_t next = RG_GET(rn, to);
+    if (next <= marker) {  // compacted: InstallSnapshot
       if (!(active & (1u << to))) return;
       if (snap_index == 0) {
         err |= ERR_EMPTY_SNAP;
@@ -356,69 +339,29 @@ struct Ctl {
       send(M_INSTALL_SNAPSHOT, to + 1, 0, 0, 0, snap_term, snap_index, 0, 0, 0, 0, 0);
       return;
     }
-    if (r.n > 0) {  // remote.progress
-      if (st == REPLICATE) RG_SET(rn, to, r.next + r.n);
+    const uint32_t n = next <= last ? (uint32_t)umin64(p.E, last - next + 1) : 0;
+    const uint64_t lt = term_at(next - 1);
+    if (n > 0) {  // remote.progress
+      if (st == REPLICATE) RG_SET(rn, to, next + n);
       else if (st == RETRY) RG_SET(rt, to, (uint32_t)WAIT);
     }
-    r.k = send(M_REPLICATE, to + 1, 0, 0, r.n, r.lt, r.next - 1, committed, 0, 0, 0, 0);
-    if (r.k >= 0 && r.n > 0) sent_hi = umax64(sent_hi, r.next + r.n - 1);
-  }
-  RG_FN uint64_t* rep_terms(uint32_t to, int k) {
-    return p.mt_out + ((((uint64_t)s * R + to) * p.K + (uint32_t)k) * p.E) * p.G + g;
-  }
-  RG_FN void send_replicate(uint32_t to) {
-    Rep r = rep_prep(to);
-    rep_emit(to, r);
-    if (r.k < 0 || r.n == 0) return;
-    uint64_t* mt = rep_terms(to, r.k);
-    for (uint32_t e = 0; e < r.n; e += RG_CTL_BATCH) {  // term|type|pay|bank
-      uint64_t v[RG_CTL_BATCH];
+    const int k = send(M_REPLICATE, to + 1, 0, 0, n, lt, next - 1, committed, 0, 0, 0, 0);
+    if (k >= 0 && n > 0) {
+      uint64_t* mt = p.mt_out + ((((uint64_t)s * R + to) * p.K + (uint32_t)k) * p.E) * p.G + g;
+      for (uint32_t e = 0; e < n; e += RG_CTL_BATCH) {  // term|type|pay|bank; batched as in write_entries
+        uint64_t v[RG_CTL_BATCH];
 #pragma unroll
-      for (uint32_t k2 = 0; k2 < RG_CTL_BATCH; ++k2) v[k2] = e + k2 < r.n ? *tr_at(r.next + e + k2) : 0;
+        for (uint32_t k2 = 0; k2 < RG_CTL_BATCH; ++k2) v[k2] = e + k2 < n ? *tr_at(next + e + k2) : 0;
 #pragma unroll
-      for (uint32_t k2 = 0; k2 < RG_CTL_BATCH; ++k2)
-        if (e + k2 < r.n) mt[(uint64_t)(e + k2) * p.G] = v[k2];
+        for (uint32_t k2 = 0; k2 < RG_CTL_BATCH; ++k2)
+          if (e + k2 < n) mt[(uint64_t)(e + k2) * p.G] = v[k2];
+      }
+      sent_hi = umax64(sent_hi, next + n - 1);
     }
   }
   RG_FN void broadcast_replicate() {
-    if constexpr (R > 5) {  // the shared copy's per-remote records would spill at R = 6..8
-      for (uint32_t i = 0; i < R; ++i)
-        if (i != s) send_replicate(i);
-      return;
-    }
-    Rep r[R];
-    sfor<0, R>([&](auto ic) {
-      constexpr int i = decltype(ic)::value;
-      if (i != s) r[i] = rep_prep(i);
-    });
-    sfor<0, R>([&](auto ic) {
-      constexpr int i = decltype(ic)::value;
-      if (i != s) rep_emit(i, r[i]);
-    });
-    uint32_t done = 0;
-    sfor<0, R>([&](auto ic) {
-      constexpr int i = decltype(ic)::value;
-      if (i == s || r[i].k < 0 || r[i].n == 0 || ((done >> i) & 1u)) return;
-      uint32_t share = 0;  // remotes getting the same entries: one load per batch for all of them
-      sfor<i, R>([&](auto jc) {
-        constexpr int j = decltype(jc)::value;
-        if (j != s && r[j].k >= 0 && r[j].n == r[i].n && r[j].next == r[i].next) share |= 1u << j;
-      });
-      done |= share;
-      for (uint32_t e = 0; e < r[i].n; e += RG_CTL_BATCH) {
-        uint64_t v[RG_CTL_BATCH];
-#pragma unroll
-        for (uint32_t k2 = 0; k2 < RG_CTL_BATCH; ++k2) v[k2] = e + k2 < r[i].n ? *tr_at(r[i].next + e + k2) : 0;
-        sfor<i, R>([&](auto jc) {
-          constexpr int j = decltype(jc)::value;
-          if (!((share >> j) & 1u)) return;
-          uint64_t* mt = rep_terms(j, r[j].k);
-#pragma unroll
-          for (uint32_t k2 = 0; k2 < RG_CTL_BATCH; ++k2)
-            if (e + k2 < r[i].n) mt[(uint64_t)(e + k2) * p.G] = v[k2];
-        });
-      }
-    });
+    for (uint32_t i = 0; i < R; ++i)
+      if (i != s) send_replicate(i);
   }
   RG_FN void broadcast_heartbeat() {
     for (uint32_t i = 0; i < R; ++i)
@@ -627,17 +570,14 @@ struct Ctl {
   // ---- Handle (A.3): message k from slot src (remote: it came over the wire from another rank)
   RG_FN void handle(uint32_t src, uint32_t k, bool remote) {
     const uint64_t plane = (uint64_t)R * R * p.K * p.G;
-    const uint64_t* hp = (remote ? p.rhdr : p.hdr_in) + (((uint64_t)src * R + s) * p.K + k) * p.G + g;
-    uint64_t h[8];  // all header words in one round trip (handlers would otherwise load them late)
-#pragma unroll
-    for (int w = 0; w < 8; ++w) h[w] = hp[w * plane];
+    const uint64_t* h = (remote ? p.rhdr : p.hdr_in) + (((uint64_t)src * R + s) * p.K + k) * p.G + g;
     const uint64_t w0 = h[0];
-    const uint64_t mterm = h[1];
+    const uint64_t mterm = h[1 * plane];
     const uint32_t type = (uint32_t)(w0 & 0xFF);
     const uint32_t from = (uint32_t)(w0 >> 8) & 0xFF;
     const bool leader_msg = type == M_REPLICATE || type == M_INSTALL_SNAPSHOT || type == M_HEARTBEAT;
     if (mterm != 0 && mterm != term) {
-      if (type == M_REQUEST_VOTE && p.CQ && mterm > term && h[5] != from && leader != 0 && etick < p.ET)
+      if (type == M_REQUEST_VOTE && p.CQ && mterm > term && h[5 * plane] != from && leader != 0 && etick < p.ET)
         return;
       if (mterm > term) {
         become_follower(mterm, leader_msg ? from : 0);
@@ -648,7 +588,7 @@ struct Ctl {
     }
     switch (type) {
       case M_PROPOSE: {
-        const uint64_t w7 = h[7];
+        const uint64_t w7 = h[7 * plane];
         handle_propose((uint32_t)(w0 >> 32), (uint32_t)w7, (uint32_t)(w7 >> 32));
         break;
       }
@@ -663,23 +603,23 @@ struct Ctl {
           leader = from;
         }
         if (type == M_REPLICATE) {
-          handle_replicate(w0, h[2], h[3], h[4], from, src, k, remote,
-                           remote ? h[7] : 0);
+          handle_replicate(w0, h[2 * plane], h[3 * plane], h[4 * plane], from, src, k, remote,
+                           remote ? h[7 * plane] : 0);
         } else if (type == M_HEARTBEAT) {
-          commit_to(h[4]);
-          send_simple(M_HEARTBEAT_RESP, from, 0, 0, h[5], h[6]);
+          commit_to(h[4 * plane]);
+          send_simple(M_HEARTBEAT_RESP, from, 0, 0, h[5 * plane], h[6 * plane]);
         } else {
-          handle_install_snapshot(h[3], h[2], from);
+          handle_install_snapshot(h[3 * plane], h[2 * plane], from);
         }
         break;
       case M_REPLICATE_RESP:
-        if (role == LEADER) leader_replicate_resp((uint32_t)(w0 >> 24) & 0xFF, h[3], h[5], from);
+        if (role == LEADER) leader_replicate_resp((uint32_t)(w0 >> 24) & 0xFF, h[3 * plane], h[5 * plane], from);
         break;
       case M_HEARTBEAT_RESP:
         if (role == LEADER) leader_heartbeat_resp(from);
         break;
       case M_REQUEST_VOTE:
-        handle_request_vote(h[2], h[3], from);
+        handle_request_vote(h[2 * plane], h[3 * plane], from);
         break;
       case M_REQUEST_VOTE_RESP:
         if (role == CANDIDATE) candidate_vote_resp(from, (uint32_t)(w0 >> 24) & 0xFF);
