@@ -1,7 +1,11 @@
 """Worker of test_gpu_cluster's two-process tests: N processes (one rank each, gloo) step a
 DistEngine (1 or 2 column halves) on the same GPU — chaos ticks through tick(), then steady
 proposal ticks through the pipelined step_device() when there are two halves; rank 0 compares
-every replica with the C oracle of all shards. usage: python dist_worker.py N [halves]"""
+every replica with the C oracle of all shards. usage: python dist_worker.py N [halves [backend]]
+
+backend nccl (N = 1 only: RCCL will not put two ranks on one GPU): the one rank sends every
+message through the wire (wire_all), so each exchange is a real RCCL all_to_all_single — the
+asynchronous one with its work-handle wait in the pipelined steps."""
 import os
 import sys
 
@@ -39,10 +43,17 @@ def snapshot(de):
     return mine
 
 
-def worker(rank, n, halves):
-    dist.init_process_group("gloo", rank=rank, world_size=n)
+def worker(rank, n, halves, backend):
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=rank, world_size=n, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=n)
     from raftd_amd.cluster import DistEngine
-    de = DistEngine(groups=G_LOCAL * halves, halves=halves, device=0, **CFG)
+    extra = dict(wire_all=1) if n == 1 else {}
+    de = DistEngine(groups=G_LOCAL * halves, halves=halves, device=0, **CFG, **extra)
+    if backend == "nccl":
+        assert de.async_ok
     de.bootstrap()
     G = G_LOCAL * halves * n
     rng = np.random.default_rng(3)
@@ -95,4 +106,5 @@ def check(ora, snap, G, t):
 if __name__ == "__main__":
     n = int(sys.argv[1])
     halves = int(sys.argv[2]) if len(sys.argv) > 2 else 1
-    mp.spawn(worker, args=(n, halves), nprocs=n, join=True)
+    backend = sys.argv[3] if len(sys.argv) > 3 else "gloo"
+    mp.spawn(worker, args=(n, halves, backend), nprocs=n, join=True)

@@ -144,3 +144,14 @@ def test_two_processes_gloo_halves():
                          capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
     assert "dist parity ok" in out.stdout
+
+
+def test_one_rank_nccl_wire_halves():
+    """The RCCL path on the one GPU: a world-size-1 nccl group, every message through the wire,
+    two column halves — plain ticks, then pipelined step_device ticks whose exchanges are
+    asynchronous RCCL all_to_all_single calls waited on by the engine stream."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29535")
+    out = subprocess.run([sys.executable, "-u", os.path.join(HERE, "dist_worker.py"), "1", "2", "nccl"], env=env,
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert "dist parity ok" in out.stdout
