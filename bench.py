@@ -56,7 +56,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--placement", choices=["spread", "colocated"], default=None,
                     help="N > 1: replicas of a group on different GPUs (default) or on one")
-    ap.add_argument("--wire-all", action="store_true", help="N = 1: route every message through the wire")
+    ap.add_argument("--wire-all", action="store_true", help="N = 1: route every message through the wire; with "
+                    "--placement spread, through the N > 1 code path (DistEngine, halves, RCCL all-to-all to "
+                    "itself in a one-rank process group): a rehearsal of the multi-GPU step on one GPU")
     ap.add_argument("--halves", type=int, default=2, help="N > 1 spread: engines per rank over disjoint column "
                     "ranges; 2 pipelines one half's all-to-all behind the other half's tick (1 = no overlap)")
     ap.add_argument("--backend", default="nccl", help="N > 1: nccl (RCCL, default) or gloo (rehearsal: several "
@@ -205,7 +207,13 @@ def main():
     import torch
 
     dist = None
-    if world > 1:
+    rehearse = world == 1 and args.placement == "spread" and args.wire_all  # N > 1 path on one rank
+    if rehearse:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29561")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if world > 1 or rehearse:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         if args.backend == "nccl":
@@ -219,13 +227,13 @@ def main():
 
     G, R, E, P = args.groups, args.replicas, args.entries, args.payload
     placement = args.placement or ("spread" if world > 1 else "colocated")
-    spread = placement == "spread" and world > 1
+    spread = placement == "spread" and (world > 1 or rehearse)
     stream = torch.cuda.Stream()  # a real (non-null) stream: the engine launches on it, events time it
     torch.cuda.set_stream(stream)
     common = dict(replicas=R, log_capacity=args.log_capacity, payload_bytes=P, max_entries_per_msg=E, device=local)
     wire = None
     if spread:  # one cluster of world x G groups, replicas spread over the GPUs
-        wire = DistEngine(groups=G, halves=args.halves, seed=0x5EED, **common)
+        wire = DistEngine(groups=G, halves=args.halves, seed=0x5EED, wire_all=1 if rehearse else 0, **common)
         host, eng = wire, wire.eng  # host: aggregates over the halves; eng: the first half
         Gt = G * world
     else:  # an independent engine per GPU (its own G groups)
@@ -309,7 +317,8 @@ def main():
                f"{world}, every replica of a group on its own GPU, followers spread evenly over the peers; "
                f"cross-GPU messages by one RCCL all_to_all_single per tick"
                + (f" and column half ({args.halves} halves per GPU, exchange pipelined behind the other half's tick)"
-                  if args.halves > 1 else ""))
+                  if args.halves > 1 else "")
+               + (" [rehearsal: one rank, every message through the wire to itself]" if rehearse else ""))
     elif args.wire_all:
         par = "1 GPU, every message through the wire pack/unpack path to itself (measurement)"
     else:

@@ -88,17 +88,58 @@ def _offsets(sizes):
 
 
 # ---------------------------------------------------------------- one process per rank
-def all_to_all_bytes(send, send_sizes, recv, recv_sizes, group=None, async_op=False):
+# Largest piece of one peer region moved by a single RCCL call. RCCL 2.26.6 (the one bundled with
+# this PyTorch) corrupted all_to_all_single regions above 1 GiB: from the region's midpoint on, the
+# received bytes were wrong, with no error raised (scripts/a2a_probe.py, one rank, 1100 and 1500 MB;
+# exact up to 1024 MB). At N = 2 a rank's whole follower traffic, ~2.3 GB a tick at 64K groups, goes
+# to its one peer, so every exchange is cut into calls of at most this many bytes per peer region.
+A2A_CHUNK = 256 << 20
+
+
+class _Works:
+    """Work handles of one chunked exchange: wait() orders the current stream after all of them."""
+
+    def __init__(self, works):
+        self.works = works
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+
+
+def a2a_chunks(max_region: int, chunk: int = A2A_CHUNK) -> int:
+    return max(1, -(-max_region // chunk))
+
+
+def all_to_all_bytes(send, send_sizes, recv, recv_sizes, group=None, async_op=False, nchunks=1,
+                     chunk=A2A_CHUNK):
     """Move region r of `send` (sizes send_sizes, concatenated in rank order) to rank r; the
-    regions from every rank land concatenated in rank order in `recv`. nccl: device tensors, one
-    all_to_all_single (RCCL over xGMI); async_op returns its work handle (wait() makes the current
-    stream wait for it). gloo: staged through host memory, always synchronous (returns None)."""
+    regions from every rank land concatenated in rank order in `recv`. nccl: device tensors moved
+    by RCCL over xGMI — one all_to_all_single, or, when a region exceeds `chunk` bytes, `nchunks`
+    all_to_all calls over views of at most `chunk` bytes per region (nchunks must be the same on
+    every rank: a2a_chunks of the largest region of the exchange); async_op returns a handle whose
+    wait() makes the current stream wait. gloo: staged through host memory, always synchronous
+    (returns None)."""
     import torch.distributed as dist
     torch = _torch()
     stot, rtot = sum(send_sizes), sum(recv_sizes)
     if dist.get_backend(group) == "nccl":
-        return dist.all_to_all_single(recv[:rtot], send[:stot], list(recv_sizes), list(send_sizes), group=group,
-                                      async_op=async_op)
+        if nchunks <= 1:
+            return dist.all_to_all_single(recv[:rtot], send[:stot], list(recv_sizes), list(send_sizes), group=group,
+                                          async_op=async_op)
+        so, _ = _offsets(send_sizes)
+        ro, _ = _offsets(recv_sizes)
+        works = []
+        for k in range(nchunks):
+            lo, hi = k * chunk, (k + 1) * chunk
+            ins = [send[so[r] + min(lo, n):so[r] + min(hi, n)] for r, n in enumerate(send_sizes)]
+            outs = [recv[ro[r] + min(lo, n):ro[r] + min(hi, n)] for r, n in enumerate(recv_sizes)]
+            works.append(dist.all_to_all(outs, ins, group=group, async_op=True))
+        h = _Works(works)
+        if async_op:
+            return h
+        h.wait()
+        return None
     hs = send[:stot].cpu() if send.is_cuda else send[:stot]
     hr = torch.empty(rtot, dtype=torch.uint8)
     dist.all_to_all_single(hr, hs, list(recv_sizes), list(send_sizes), group=group)
@@ -107,14 +148,18 @@ def all_to_all_bytes(send, send_sizes, recv, recv_sizes, group=None, async_op=Fa
 
 
 def exchange_sizes(send_sizes, group=None):
-    """Each rank's outbound region sizes → the sizes this rank receives from every rank."""
+    """Each rank's outbound region sizes → (the sizes this rank receives from every rank, the
+    largest region any rank sends this exchange), by one all_gather of the size rows."""
     import torch.distributed as dist
     torch = _torch()
     dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+    n = dist.get_world_size(group)
     st = torch.tensor(send_sizes, dtype=torch.int64, device=dev)
-    rt = torch.empty_like(st)
-    dist.all_to_all_single(rt, st, group=group)
-    return [int(x) for x in rt.tolist()]
+    allt = torch.empty(n * len(send_sizes), dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(allt, st, group=group)
+    m = allt.view(n, len(send_sizes)).tolist()  # m[a][b]: rank a → rank b
+    me = dist.get_rank(group)
+    return [m[a][me] for a in range(n)], max(max(row) for row in m)
 
 
 class _Half:
@@ -133,10 +178,11 @@ class _Half:
         _, stot = _offsets(sizes)
         self.send.ensure(stot)
         e.wire_pack(self.send.ptr(), self.send.cap())
-        rsizes = exchange_sizes(sizes, self.pg)
+        rsizes, biggest = exchange_sizes(sizes, self.pg)
         _, rtot = _offsets(rsizes)
         self.recv.ensure(rtot)  # its previous contents were consumed by the tick wire_plan waited for
-        self.work = all_to_all_bytes(self.send.t, sizes, self.recv.t, rsizes, self.pg, async_op=async_op)
+        self.work = all_to_all_bytes(self.send.t, sizes, self.recv.t, rsizes, self.pg, async_op=async_op,
+                                     nchunks=a2a_chunks(biggest))
         self.rsizes, self.sent = rsizes, stot - sizes[self.rank]
 
     def finish(self):

@@ -77,7 +77,7 @@ def _transport_worker(rank, world, port, q):
         for r in range(world):  # region r of rank a: bytes (a * 31 + r * 7 + i) mod 251
             i = torch.arange(sizes[r])
             send[offs[r]:offs[r] + sizes[r]] = ((rank * 31 + r * 7 + i) % 251).to(torch.uint8)
-        rsizes = exchange_sizes(sizes)
+        rsizes, biggest = exchange_sizes(sizes)
         roffs, rtot = _offsets(rsizes)
         recv = torch.zeros(rtot + 5, dtype=torch.uint8)
         all_to_all_bytes(send, sizes, recv, rsizes)
@@ -86,7 +86,7 @@ def _transport_worker(rank, world, port, q):
             i = torch.arange(rsizes[a])
             want = ((a * 31 + rank * 7 + i) % 251).to(torch.uint8)
             ok &= bool(torch.equal(recv[roffs[a]:roffs[a] + rsizes[a]], want))
-        q.put((rank, ok, rsizes))
+        q.put((rank, ok and biggest >= max(sizes), rsizes))
     finally:
         dist.destroy_process_group()
 

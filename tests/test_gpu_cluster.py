@@ -155,3 +155,13 @@ def test_one_rank_nccl_wire_halves():
                          capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
     assert "dist parity ok" in out.stdout
+
+
+def test_chunked_exchange_rccl():
+    """all_to_all_bytes through RCCL in pieces of at most A2A_CHUNK bytes per region: exact for
+    ragged, empty and 1.5 GB regions (a single RCCL call corrupted regions above 1 GiB)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29536")
+    out = subprocess.run([sys.executable, "-u", os.path.join(HERE, "a2a_worker.py")], env=env,
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert "a2a chunks ok" in out.stdout
