@@ -27,8 +27,10 @@ def slot_offset(s: int, j: int, n: int) -> int:
     """off_c(s): rank offset of slot s in column j (class c = j mod (n - 1)); 0 for slot 0."""
     if s == 0 or n < 2:
         return 0
-    m = n - 1
-    return (j % m + s - 1) % m + 1
+    m, p = n - 1, (s - 1) % n
+    if p == m:  # n < R: every n-th follower shares the leader's rank (fewer copies over xGMI)
+        return 0
+    return (j % m + p) % m + 1
 
 
 def rank_of(g: int, s: int, n: int) -> int:

@@ -52,7 +52,10 @@ enum : uint32_t { SRC_NONE = 0, SRC_RING = 1, SRC_SLAB = 2, SRC_WIRE = 3 };
 // j, the plane s→d of column j goes to rank k + off_c(d) − off_c(s), and over N − 1 classes a
 // leader's followers sit at every other rank equally often (the busiest xGMI link carries 2/(N−1)
 // of a rank's leader→follower payload instead of 1/2 with offsets s·h). Arithmetic only: no table
-// that a dynamic index could push into scratch.
+// that a dynamic index could push into scratch. With N < R co-location is unavoidable: followers
+// s = 1.. take the N − 1 peers, then the leader's own rank, in cycles of N (p = (s − 1) mod N, p = N − 1
+// → offset 0), so the leader's rank hosts ceil(R / N) replicas and fewer follower copies cross xGMI
+// (R 3 at N 2: one remote follower instead of two). For N ≥ R, p < N − 1 and nothing changes.
 constexpr uint32_t MAX_RANKS = 16;
 struct Placement {
   uint32_t N, rank, wire_all, col_base;  // col_base: global column of local column 0
@@ -60,8 +63,9 @@ struct Placement {
 // j: LOCAL column (global column = col_base + j)
 RG_HD_INLINE uint32_t pl_soff(const Placement& pl, uint32_t s, uint32_t j) {
   if (s == 0 || pl.N < 2) return 0;
-  const uint32_t m = pl.N - 1;
-  return ((pl.col_base + j) % m + s - 1) % m + 1;
+  const uint32_t m = pl.N - 1, p = (s - 1) % pl.N;
+  if (p == m) return 0;  // N < R: every N-th follower shares the leader's rank
+  return ((pl.col_base + j) % m + p) % m + 1;
 }
 // rank offset of the plane s→d at column j (0 = co-located)
 RG_HD_INLINE uint32_t pl_off(const Placement& pl, uint32_t s, uint32_t d, uint32_t j) {

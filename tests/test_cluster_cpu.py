@@ -41,6 +41,21 @@ def test_leader_traffic_spreads_over_every_peer(N, R):
     assert 0 not in cnt and set(cnt) == set(range(1, N)) and len(set(cnt.values())) == 1
 
 
+@pytest.mark.parametrize("N,R", [(2, 3), (2, 5), (3, 5), (4, 5), (3, 8), (2, 8), (5, 8)])
+def test_fewer_ranks_than_replicas_keeps_followers_home(N, R):
+    """N < R: the leader's rank hosts ceil(R / N) replicas of each group (the fewest follower
+    copies over xGMI), every rank at most that many, and the remote followers still spread over
+    every peer evenly across N - 1 consecutive columns."""
+    from collections import Counter
+    hi = -(-R // N)
+    for j in range(3 * (N - 1)):
+        per_rank = Counter(plane_offset(0, d, j, N) for d in range(R))
+        assert per_rank[0] == hi and max(per_rank.values()) == hi, (j, per_rank)
+    cnt = Counter(plane_offset(0, d, j, N) for j in range(N - 1) for d in range(1, R))
+    del cnt[0]
+    assert set(cnt) == set(range(1, N)) and len(set(cnt.values())) == 1
+
+
 def test_placement_matches_cpp():
     from native.ctl_host import build
     L = C.CDLL(build())

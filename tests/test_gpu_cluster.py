@@ -43,7 +43,7 @@ def run_chaos(ranks, cfg, ticks, seed, wire_all=0, **inkw):
     return cl, ora
 
 
-@pytest.mark.parametrize("ranks,R", [(2, 3), (3, 3), (4, 3), (8, 3), (8, 5), (4, 5), (2, 2)])
+@pytest.mark.parametrize("ranks,R", [(2, 3), (3, 3), (4, 3), (8, 3), (8, 5), (4, 5), (2, 2), (2, 5), (3, 8)])
 def test_cluster_chaos(ranks, R):
     cfg = dict(groups=2 * ranks, replicas=R, seed=11 + ranks + R, **CHAOS)
     run_chaos(ranks, cfg, ticks=100, seed=ranks * 10 + R)
