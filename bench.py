@@ -40,6 +40,8 @@ sys.path.insert(0, ROOT)
 
 METRIC = "raft group-steps/sec & commits/sec, 64K groups×3 replicas, 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+XGMI_LINK_GBS = 153.0  # one xGMI link per GPU pair, 7 per GPU (≈153 GB/s each)
+CONTROL_TIMING_STEPS = 4
 
 
 def parse():
@@ -260,24 +262,31 @@ def main():
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     xev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    host.timing(True)
-    wire_bytes = 0
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for i in range(args.steps):
+    def one_step(i):
+        """One step; returns the bytes this rank sent to other ranks."""
         if pipelined:  # each half: finish its exchange, tick, start the next exchange
             wire.step_device(pt.data_ptr(), pc.data_ptr())
-            wire_bytes += wire.wire_bytes
-            continue
+            return wire.wire_bytes
+        sent = 0
         if wire:
-            xev[i][0].record(stream)
+            if i is not None:
+                xev[i][0].record(stream)
             wire.exchange()
-            xev[i][1].record(stream)
-            wire_bytes += wire.wire_bytes
+            if i is not None:
+                xev[i][1].record(stream)
+            sent = wire.wire_bytes
         for e in (wire.parts if spread else [eng]):
             e = e.eng if spread else e
             e.tick_device(pt.data_ptr() + (e.cfg["column_base"] * world if spread else 0),
                           pc.data_ptr() + 4 * (e.cfg["column_base"] * world if spread else 0))
+        return sent
+
+    host.timing(True, bulk_only=True)  # the roofline kernel, live; two event records per tick
+    wire_bytes = 0
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for i in range(args.steps):
+        wire_bytes += one_step(i)
     if pipelined:
         wire.drain()  # the last step's exchanges complete inside the timed region
     host.join()  # the stream waits for the last tick's payload stage before the end event
@@ -289,6 +298,14 @@ def main():
     wall = time.perf_counter() - t0
     dev_ms = ev0.elapsed_time(ev1)
     kms = host.kernel_ms()
+    # control_kernel duration from a few more steps after the timed region (timing both kernels
+    # adds two event records per tick, which the timed region does without)
+    host.timing(True)
+    for _ in range(CONTROL_TIMING_STEPS):
+        one_step(None)
+    if pipelined:
+        wire.drain()
+    kms["control"] = host.kernel_ms()["control"]
     host.timing(False)
     x_ms = sum(a.elapsed_time(b) for a, b in xev) / args.steps if wire and not pipelined else 0.0
     c1 = host.sum_committed()
@@ -379,7 +396,7 @@ def main():
             "bytes_sent_per_step_max_rank": wire_max / K,
             "achieved_GBps_per_rank": ((wire_max / K) / (x_ms / 1e3) / 1e9 if x_ms > 0 else
                                        (wire_max / K) / (wall / K) / 1e9),
-            "xgmi_peak_GBps_per_rank": 7 * 153.0,
+            "xgmi_peak_GBps_per_rank": min(max(world - 1, 1), 7) * XGMI_LINK_GBS,
             "note": "bytes = the regions this rank sends to other ranks per step; serial mode times the exchange "
                     "with events on the bench stream, pipelined mode reports bytes / step time (a lower bound)",
         },

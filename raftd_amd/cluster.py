@@ -338,9 +338,9 @@ class DistEngine(_Feeds):
         for p in self.parts:
             p.eng.sync()
 
-    def timing(self, on=True):
+    def timing(self, on=True, bulk_only=False):
         for p in self.parts:
-            p.eng.timing(on)
+            p.eng.timing(on, bulk_only=bulk_only)
 
     def kernel_ms(self) -> dict:
         """Summed over the halves: total ms per kernel, and launches counted per tick."""

@@ -77,6 +77,16 @@ struct Ctl {
   uint64_t applied_start, restored_at;  // apply window: entries restored from a snapshot are not Update()d
   bool took;                            // a snapshot was taken at the end of this step
   uint64_t wlo;                         // lowest log index written this step (EntriesToSave from here)
+  // RG_CTL_FASTREP (ablation, off in the product: it changes control_kernel<5>'s register
+  // allocation, and such a change preceded a memory fault in the full-size C3 test twice).
+  // The leader's last append of this step when it wrote no protected index: entries
+  // [la_base, la_base + la_n) all hold the ring word la_word (bank 0) and term(la_base − 1) = la_pt,
+  // so send_replicate builds a Replicate of them from registers instead of re-reading the ring.
+  // la_n = 0 when any other log write, reset or restore came after it.
+#ifdef RG_CTL_FASTREP
+  uint64_t la_base, la_word, la_pt;
+  uint32_t la_n;
+#endif
   uint64_t oc, em;  // per destination: enqueued / emitted counts, 8 bits each
   uint32_t nj;      // jobs emitted
 
@@ -105,6 +115,9 @@ struct Ctl {
     });
     last_start = last; sent_hi = 0; rw_lo = ~0ull; rw_hi = 0; marker_start = marker;
     applied_start = applied; restored_at = 0; wlo = ~0ull; took = false;
+#ifdef RG_CTL_FASTREP
+    la_base = la_word = la_pt = 0; la_n = 0;
+#endif
     oc = 0; em = 0; nj = 0;
   }
 
@@ -245,6 +258,9 @@ struct Ctl {
   RG_FN void write_entries(uint64_t base, uint32_t e0, uint32_t n, uint32_t kind, uint32_t src,
                                 const uint64_t* mt, uint64_t word, uint64_t wofs = 0) {
     const uint64_t hi_prot = umax64(last_start, sent_hi);
+#ifdef RG_CTL_FASTREP
+    la_n = 0;
+#endif
     wlo = umin64(wlo, base + e0);
     uint64_t dm = 0, sm = 0, hm = 0, tm = 0;
     // RG_CTL_BATCH entries at a time: their loads (sender terms, current ring words of protected
@@ -309,8 +325,20 @@ struct Ctl {
   RG_FN bool append_local(uint32_t n, int slab_id) {
     if (last + n > cap_base + p.L) return false;
     const bool pay = slab_id >= 0 && p.P;
-    write_entries(last + 1, 0, n, pay ? SRC_SLAB : SRC_NONE, pay ? (uint32_t)slab_id : 0, nullptr,
-                  term | (pay ? PAY_BIT : 0));
+    const uint64_t base = last + 1, w = term | (pay ? PAY_BIT : 0);
+#ifdef RG_CTL_FASTREP
+    const bool plain = base > umax64(last_start, sent_hi);  // no protected index: every bank bit 0
+    const uint64_t pt = plain ? term_at(last) : 0;
+#endif
+    write_entries(base, 0, n, pay ? SRC_SLAB : SRC_NONE, pay ? (uint32_t)slab_id : 0, nullptr, w);
+#ifdef RG_CTL_FASTREP
+    if (plain) {
+      la_base = base;
+      la_word = w & ~BANK_BIT;
+      la_pt = pt;
+      la_n = n;
+    }
+#endif
     last += n;
     remote_try_update(s, last);
     if (R == 1) try_commit();
@@ -340,7 +368,12 @@ struct Ctl {
       return;
     }
     const uint32_t n = next <= last ? (uint32_t)umin64(p.E, last - next + 1) : 0;
+#ifdef RG_CTL_FASTREP  // the whole message lies in this step's plain append (the steady-state case)
+    const bool fast = n > 0 && la_n > 0 && next >= la_base && next + n <= la_base + la_n;
+    const uint64_t lt = !fast ? term_at(next - 1) : next == la_base ? la_pt : la_word & TERM_MASK;
+#else
     const uint64_t lt = term_at(next - 1);
+#endif
     if (n > 0) {  // remote.progress
       if (st == REPLICATE) RG_SET(rn, to, next + n);
       else if (st == RETRY) RG_SET(rt, to, (uint32_t)WAIT);
@@ -348,6 +381,11 @@ struct Ctl {
     const int k = send(M_REPLICATE, to + 1, 0, 0, n, lt, next - 1, committed, 0, 0, 0, 0);
     if (k >= 0 && n > 0) {
       uint64_t* mt = p.mt_out + ((((uint64_t)s * R + to) * p.K + (uint32_t)k) * p.E) * p.G + g;
+#ifdef RG_CTL_FASTREP
+      if (fast) {
+        for (uint32_t e = 0; e < n; ++e) mt[(uint64_t)e * p.G] = la_word;
+      } else
+#endif
       for (uint32_t e = 0; e < n; e += RG_CTL_BATCH) {  // term|type|pay|bank; batched as in write_entries
         uint64_t v[RG_CTL_BATCH];
 #pragma unroll
@@ -417,6 +455,9 @@ struct Ctl {
       li = committed;
     } else {  // restore
       marker = last = committed = snap_index = si;
+#ifdef RG_CTL_FASTREP
+      la_n = 0;
+#endif
       marker_term = snap_term = stt;
       li = last;
       restored_at = si;
@@ -575,6 +616,14 @@ struct Ctl {
     const uint64_t mterm = h[1 * plane];
     const uint32_t type = (uint32_t)(w0 & 0xFF);
     const uint32_t from = (uint32_t)(w0 >> 8) & 0xFF;
+#ifdef RG_BOUNDS  // unpack_kernel keeps only well-formed messages
+    if (type == M_REPLICATE && (uint32_t)(w0 >> 32) > p.E) {
+      RG_OOB("RG_BOUNDS control q=%u src=%u k=%u remote=%d replicate n=%u > E=%u\n", q, src, k, (int)remote,
+             (uint32_t)(w0 >> 32), p.E);
+      err |= ERR_WIRE;
+      return;
+    }
+#endif
     const bool leader_msg = type == M_REPLICATE || type == M_INSTALL_SNAPSHOT || type == M_HEARTBEAT;
     if (mterm != 0 && mterm != term) {
       if (type == M_REQUEST_VOTE && p.CQ && mterm > term && h[5 * plane] != from && leader != 0 && etick < p.ET)
@@ -636,7 +685,14 @@ struct Ctl {
     for (uint32_t src = 0; src < R; ++src) {
       if (src == s) continue;
       const bool remote = pl_remote(p.pl, src, s, g);
-      const uint32_t cnt = (remote ? p.rcnt : p.cnt_in)[((uint64_t)src * R + s) * p.G + g];
+      uint32_t cnt = (remote ? p.rcnt : p.cnt_in)[((uint64_t)src * R + s) * p.G + g];
+#ifdef RG_BOUNDS  // unpack_kernel already clamps received counts to K
+      if (cnt > p.K) {  // never produced by a sender: malformed exchange data, ignored
+        RG_OOB("RG_BOUNDS control q=%u src=%u remote=%d cnt=%u > K=%u\n", q, src, (int)remote, cnt, p.K);
+        err |= ERR_WIRE;
+        cnt = 0;
+      }
+#endif
       for (uint32_t k = 0; k < cnt; ++k) handle(src, k, remote);
     }
     RG_STAMP(1);

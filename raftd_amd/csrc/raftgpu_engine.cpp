@@ -84,9 +84,11 @@ struct rg_engine {
   uint32_t bulk_tile = 1;
   uint64_t bytes = 0;
   std::vector<void*> allocs;
-  // per-launch event timing (rg_timing): [control start, control end, bulk start, bulk end] per tick
-  bool timing = false;
+  // per-launch event timing (rg_timing): bit 0 control_kernel, bit 1 bulk_kernel; a start/end
+  // event pair per timed launch
+  int timing = 0;
   std::vector<hipEvent_t> ev_pool, ev_live;
+  std::vector<int> ev_kind;  // kernel (0 control, 1 bulk) of each start/end pair in ev_live
   double kms[2] = {0, 0};
   uint64_t klaunch[2] = {0, 0};
   uint32_t T0[256];
@@ -105,6 +107,7 @@ struct rg_engine {
   std::vector<uint64_t> send_bytes;
   bool planned = false, wire_ready = false;
   const uint8_t* recv = nullptr;  // receive buffer the next tick's SRC_WIRE jobs read
+  uint64_t recv_bytes = 0;         // bytes of it in use (RG_BOUNDS checks)
   // committed-entry copy-back (raftgpu_apply.hip)
   uint64_t* apply_lo = nullptr;
   uint32_t* acnt = nullptr;
@@ -239,6 +242,8 @@ static BulkParams bulk_params(rg_engine* e) {  // for tick e->t
   b.info = e->info; b.pay = e->pay; b.slabs = e->slabs; b.crc_err = e->crc_err; b.crc_tab = e->crc_tab;
   b.wire_mode = e->wire ? 1u : 0u;
   b.wire = e->recv;
+  b.wire_bytes = e->recv_bytes;
+  b.nslab = e->c.num_slabs;
   return b;
 }
 
@@ -535,7 +540,8 @@ int rg_fill_slabs(rg_engine* e) {
   return RG_OK;
 }
 
-static int timing_event(rg_engine* e, hipStream_t s) {
+static int timing_event(rg_engine* e, hipStream_t s, int kind) {
+  if (!(e->timing & (1 << kind))) return RG_OK;
   hipEvent_t ev;
   if (e->ev_pool.empty()) {
     HIPCHK(hipEventCreate(&ev));
@@ -544,6 +550,7 @@ static int timing_event(rg_engine* e, hipStream_t s) {
     e->ev_pool.pop_back();
   }
   e->ev_live.push_back(ev);
+  if (e->ev_live.size() & 1) e->ev_kind.push_back(kind);
   HIPCHK(hipEventRecord(ev, s));
   return RG_OK;
 }
@@ -551,14 +558,14 @@ static int timing_event(rg_engine* e, hipStream_t s) {
 static int timing_drain(rg_engine* e) {
   HIPCHK(hipStreamSynchronize(e->stream));
   HIPCHK(hipStreamSynchronize(e->bulk));
-  for (size_t i = 0; i + 3 < e->ev_live.size(); i += 4) {
-    for (int k = 0; k < 2; ++k) {
-      float ms = 0;
-      HIPCHK(hipEventElapsedTime(&ms, e->ev_live[i + 2 * k], e->ev_live[i + 2 * k + 1]));
-      e->kms[k] += ms;
-      e->klaunch[k]++;
-    }
+  for (size_t i = 0; i + 1 < e->ev_live.size(); i += 2) {
+    float ms = 0;
+    const int k = e->ev_kind[i / 2];
+    HIPCHK(hipEventElapsedTime(&ms, e->ev_live[i], e->ev_live[i + 1]));
+    e->kms[k] += ms;
+    e->klaunch[k]++;
   }
+  e->ev_kind.clear();
   e->ev_pool.insert(e->ev_pool.end(), e->ev_live.begin(), e->ev_live.end());
   e->ev_live.clear();
   return RG_OK;
@@ -567,7 +574,8 @@ static int timing_drain(rg_engine* e) {
 int rg_timing(rg_engine* e, int enable) {
   if (!e) return fail(RG_EINVAL, "null engine");
   if (int rc = timing_drain(e)) return rc;
-  e->timing = enable != 0;
+  // 1: both kernels (4 event records per tick), 2: bulk_kernel only (2 per tick)
+  e->timing = enable == 1 ? 3 : enable == 2 ? 2 : 0;
   e->kms[0] = e->kms[1] = 0;
   e->klaunch[0] = e->klaunch[1] = 0;
   return RG_OK;
@@ -619,20 +627,26 @@ static int tick_impl(rg_engine* e, const rg_tick_input* in, bool device_ptrs) {
   // control(t) on the engine stream once bulk(t-2) released jobs[t&1]; bulk(t) on the bulk
   // stream after control(t). control(t+1) then overlaps bulk(t): they touch disjoint data.
   const int a = (int)(e->t & 1);
-  if (e->t >= 2) HIPCHK(hipStreamWaitEvent(e->stream, e->bulk_done[a], 0));
-  if (e->timing) RGCHK(timing_event(e, e->stream));
-  LAUNCH(launch_control(p, e->stream), e->stream, "control_kernel");
-  if (e->timing) RGCHK(timing_event(e, e->stream));
-  HIPCHK(hipEventRecord(e->ctl_done[a], e->stream));
 #ifdef RG_OVERLAP  // ablation: bulk(t) on a second stream beside control(t+1)
   hipStream_t bs = e->bulk;
 #else  // measured r01: beside bulk the latency-bound control kernel ran 8x slower, a net loss
   hipStream_t bs = e->stream;
 #endif
-  HIPCHK(hipStreamWaitEvent(bs, e->ctl_done[a], 0));
-  if (e->timing) RGCHK(timing_event(e, bs));
+  // One stream (the product): stream order alone sequences control and bulk, so no event
+  // records or waits go between them (each is a packet in the queue, ≈5 µs a tick at 4K groups).
+  // bulk_done is still recorded: join() and a later rg_set_stream() order other streams on it.
+  const bool two = bs != e->stream;
+  if (two && e->t >= 2) HIPCHK(hipStreamWaitEvent(e->stream, e->bulk_done[a], 0));
+  RGCHK(timing_event(e, e->stream, 0));
+  LAUNCH(launch_control(p, e->stream), e->stream, "control_kernel");
+  RGCHK(timing_event(e, e->stream, 0));
+  if (two) {
+    HIPCHK(hipEventRecord(e->ctl_done[a], e->stream));
+    HIPCHK(hipStreamWaitEvent(bs, e->ctl_done[a], 0));
+  }
+  RGCHK(timing_event(e, bs, 1));
   LAUNCH(launch_bulk(bulk_params(e), bs, e->bulk_grid), bs, "bulk_kernel");
-  if (e->timing) RGCHK(timing_event(e, bs));
+  RGCHK(timing_event(e, bs, 1));
   HIPCHK(hipEventRecord(e->bulk_done[a], bs));
   e->t++;
   e->wire_ready = false;
@@ -959,8 +973,10 @@ int rg_wire_recv(rg_engine* e, const void* recv_buf, const uint64_t* recv_bytes)
   }
   if (off && !recv_buf) return fail(RG_EINVAL, "rg_wire_recv: null buffer");
   w.recv = (const uint8_t*)recv_buf;
+  w.recv_total = off;
   LAUNCH(launch_wire_unpack(w, e->stream), e->stream, "unpack_kernel");
   e->recv = (const uint8_t*)recv_buf;
+  e->recv_bytes = off;
   e->wire_ready = true;
   return RG_OK;
 }

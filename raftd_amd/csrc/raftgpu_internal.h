@@ -28,7 +28,15 @@ enum : uint32_t {
 enum : uint32_t { FOLLOWER = 0, CANDIDATE = 1, LEADER = 2 };
 enum : uint32_t { RETRY = 0, WAIT = 1, REPLICATE = 2, SNAPSHOT = 3 };
 enum : uint32_t { ENTRY_APP = 0, ENTRY_CONFIG = 1 };
-enum : uint32_t { ERR_CONFLICT = 1, ERR_BEYOND = 2, ERR_RING = 4, ERR_CRC = 8, ERR_EMPTY_SNAP = 16 };
+enum : uint32_t { ERR_CONFLICT = 1, ERR_BEYOND = 2, ERR_RING = 4, ERR_CRC = 8, ERR_EMPTY_SNAP = 16, ERR_WIRE = 32 };
+// RG_BOUNDS (diagnostic builds): kernels printf and skip any count or offset read from memory that
+// would index outside its buffer (ERR_WIRE in the replica's err word). Product builds check only
+// what arrives over the wire (unpack_kernel keeps the well-formed messages of a unit).
+#ifdef RG_BOUNDS
+#define RG_OOB(...) printf(__VA_ARGS__)
+#else
+#define RG_OOB(...) ((void)0)
+#endif
 
 // state field rows ([row][nrep])
 enum : uint32_t {
@@ -146,6 +154,8 @@ struct BulkParams {
   const uint8_t* wire;   // receive buffer of the last exchange (SRC_WIRE jobs)
   uint32_t* crc_err;     // [nrep] sticky ERR_CRC from payload verification
   const uint32_t* crc_tab;
+  uint64_t wire_bytes;   // RG_BOUNDS checks: bytes of `wire` in use, proposal slabs
+  uint32_t nslab;
 };
 
 // CRC-32/IEEE tables: T[k][b] = raw CRC of byte b followed by k zero bytes (k = 0..15);

@@ -184,6 +184,18 @@ __device__ __forceinline__ void set_job(const BulkParams& p, Cursor& cur, const 
   cur.first = jb.first; cur.dm = jb.dm; cur.sm = jb.sm; cur.hm = jb.hm; cur.tm = jb.tm;
   cur.n = jb.meta & 0xFF; cur.b = (jb.meta >> 8) & 0xFF; cur.kind = jb.meta >> 16; cur.src = jb.src;
   cur.g = WIRE ? cur.q : cur.q % p.G;  // proposal slab row: per replica across ranks, per group on one
+#ifdef RG_BOUNDS
+  const bool bad = cur.n > 64 || cur.b > cur.n || (cur.kind == SRC_RING && cur.src >= p.nrep) ||
+                   (cur.kind == SRC_SLAB && cur.src >= p.nslab) || cur.kind > SRC_WIRE ||
+                   (cur.kind == SRC_WIRE && (!WIRE || cur.n > cur.src ||
+                                             cur.sm + (16ull + p.P) * cur.src > p.wire_bytes));
+  if (bad) {
+    if (lane_id() == 0)
+      printf("RG_BOUNDS bulk q=%u job=%u n=%u b=%u kind=%u src=%u sm=%llu wire_bytes=%llu\n", cur.q, cur.j, cur.n,
+             cur.b, cur.kind, cur.src, (unsigned long long)cur.sm, (unsigned long long)p.wire_bytes);
+    cur.n = cur.b = 0;
+  }
+#endif
 }
 
 // Move the cursor one position: the replica's next job, the tile's next replica, or the next

@@ -28,6 +28,7 @@ struct WireParams {
   uint32_t RU;
   const uint8_t* recv;   // caller's receive buffer
   uint64_t recv_region[MAX_RANKS];
+  uint64_t recv_total;   // bytes of the receive buffer in use (end of the last region)
   uint64_t* rhdr;        // remote inbox, TickParams layout
   uint64_t* rmt;
   uint32_t* rcnt;

@@ -156,7 +156,11 @@ __global__ void __launch_bounds__(256) pack_kernel(WireParams w) {
   unit_decode(w.umap[u], s, d, j);
   const uint64_t col = (uint64_t)s * w.R + d, qs = (uint64_t)s * w.G + j, n64 = w.nrep;
   const uint64_t plane = (uint64_t)w.R * w.R * w.K * w.G;
-  const uint32_t c = w.cnt[col * w.G + j];
+  uint32_t c = w.cnt[col * w.G + j];
+  if (c > w.K) {
+    RG_OOB("RG_BOUNDS pack u=%u s=%u d=%u j=%u cnt=%u > K\n", u, s, d, j, c);
+    c = 0;
+  }
   if (lane == 0) reinterpret_cast<uint64_t*>(region)[u - u0] = (off16 << 8) | c;
   uint8_t* out = region + table_bytes(nu) + off16 * 16;
   const uint32_t P = w.P, nch = P / 16;
@@ -165,7 +169,11 @@ __global__ void __launch_bounds__(256) pack_kernel(WireParams w) {
     const uint64_t hv = lane < 8 ? hp[lane * plane] : 0;
     if (lane < 8) reinterpret_cast<uint64_t*>(out)[lane] = hv;
     const uint64_t w0 = rl64(hv, 0), li = rl64(hv, 3);
-    const uint32_t n = ((w0 & 0xFF) == M_REPLICATE) ? (uint32_t)(w0 >> 32) : 0u;
+    uint32_t n = ((w0 & 0xFF) == M_REPLICATE) ? (uint32_t)(w0 >> 32) : 0u;
+    if (n > w.E) {  // plan_kernel sized the region with the same n: only reachable on corrupt state
+      RG_OOB("RG_BOUNDS pack u=%u k=%u n=%u > E\n", u, k, n);
+      n = 0;
+    }
     const uint64_t* mtp = w.mt + ((col * w.K + k) * w.E) * w.G + j;
     if (lane < n) {
       const uint64_t word = mtp[(uint64_t)lane * w.G];
@@ -198,17 +206,31 @@ __global__ void unpack_kernel(WireParams w) {
   const uint32_t u0 = w.rbeg[r], nu = w.rbeg[r + 1] - u0;
   const uint8_t* region = w.recv + w.recv_region[r];
   const uint64_t tv = reinterpret_cast<const uint64_t*>(region)[u - u0];
-  const uint32_t c = (uint32_t)(tv & 0xFF);
+  uint32_t c = (uint32_t)(tv & 0xFF);
   const uint8_t* in = region + table_bytes(nu) + (tv >> 8) * 16;
+  const uint64_t rend = r + 1 < w.pl.N ? w.recv_region[r + 1] : w.recv_total;
   uint32_t s, d, j;
   unit_decode(w.rmap[u], s, d, j);
   const uint64_t col = (uint64_t)s * w.R + d;
   const uint64_t plane = (uint64_t)w.R * w.R * w.K * w.G;
-  w.rcnt[col * w.G + j] = c;
-  for (uint32_t k = 0; k < c && k < w.K; ++k) {
+  if (c > w.K) {
+    RG_OOB("RG_BOUNDS unpack u=%u r=%u s=%u d=%u j=%u cnt=%u > K\n", u, r, s, d, j, c);
+    c = 0;
+  }
+  // malformed data (a count or size beyond the region): keep only the messages before it
+  uint32_t k = 0;
+  for (; k < c; ++k) {
+    if ((uint64_t)(in - w.recv) + 64 > rend) {
+      RG_OOB("RG_BOUNDS unpack u=%u k=%u header beyond region end %llu\n", u, k, (unsigned long long)rend);
+      break;
+    }
     const uint64_t* h = reinterpret_cast<const uint64_t*>(in);
     const uint64_t w0 = h[0];
     const uint32_t n = ((w0 & 0xFF) == M_REPLICATE) ? (uint32_t)(w0 >> 32) : 0u;
+    if (n > w.E || (uint64_t)(in - w.recv) + 64 + (uint64_t)n * (16 + w.P) > rend) {
+      RG_OOB("RG_BOUNDS unpack u=%u k=%u n=%u region end %llu\n", u, k, n, (unsigned long long)rend);
+      break;
+    }
     uint64_t* ho = w.rhdr + (col * w.K + k) * w.G + j;
     for (int x = 0; x < 7; ++x) ho[x * plane] = h[x];
     ho[7 * plane] = (w0 & 0xFF) == M_REPLICATE ? (uint64_t)(in + 64 - w.recv) : h[7];
@@ -216,6 +238,7 @@ __global__ void unpack_kernel(WireParams w) {
     for (uint32_t e = 0; e < n; ++e) mo[(uint64_t)e * w.G] = h[8 + 2 * e];
     in += 64 + (uint64_t)n * (16 + w.P);
   }
+  w.rcnt[col * w.G + j] = k;
 }
 
 hipError_t launch_wire_plan(const WireParams& w, uint64_t* bounds, hipStream_t st) {

@@ -251,9 +251,10 @@ class Engine:
     def sync(self):
         self._check(self.L.rg_sync(self.h))
 
-    def timing(self, enable: bool = True):
-        """Per-launch HIP-event timing of control_kernel / bulk_kernel (measurement only)."""
-        self._check(self.L.rg_timing(self.h, 1 if enable else 0))
+    def timing(self, enable: bool = True, bulk_only: bool = False):
+        """Per-launch HIP-event timing of control_kernel / bulk_kernel (measurement only);
+        bulk_only: time bulk_kernel alone (two event records per tick instead of four)."""
+        self._check(self.L.rg_timing(self.h, (2 if bulk_only else 1) if enable else 0))
 
     def kernel_ms(self) -> dict:
         """{'control': (total_ms, launches), 'bulk': (total_ms, launches)} since timing(True)."""
