@@ -4,7 +4,8 @@ into profiles/<tag>_pmc_summary.json and profiles/<tag>_kernel_stats.csv.
 HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE (KB) reads exactly half of a
 wide coalesced stream on gfx950, so hbm = (2*FETCH_SIZE + WRITE_SIZE) * 1024; the bulk kernel's
 payload traffic is 16 B/lane coalesced, which is the calibrated case.
-usage: python scripts/pmc_summary.py TAG KTRACE_DIR FETCH_DIR WRITE_DIR [last_n]
+usage: python scripts/pmc_summary.py TAG KTRACE_DIR FETCH_DIR WRITE_DIR [last_n] [skip_tail]
+(skip_tail: tick-kernel dispatches after the timed region, bench.py CONTROL_TIMING_STEPS)
 """
 import csv
 import glob
@@ -32,19 +33,29 @@ def short(name):
     return name[:60]
 
 
-def pmc(d, counter, last_n):
+TICK_KERNELS = ("control_kernel", "bulk_kernel")
+
+
+def window(k, xs, last_n, skip):
+    """The last_n values before the skipped tail (tick kernels only)."""
+    s = skip if k in TICK_KERNELS else 0
+    return xs[max(len(xs) - last_n - s, 0):len(xs) - s]
+
+
+def pmc(d, counter, last_n, skip=0):
     vals = {}
     for r in rows(d, "*counter_collection.csv"):
         if r.get("Counter_Name") != counter:
             continue
         k = short(r.get("Kernel_Name", ""))
         vals.setdefault(k, []).append((int(r.get("Dispatch_Id", 0)), float(r["Counter_Value"])))
-    return {k: [v for _, v in sorted(x)][-last_n:] for k, x in vals.items()}
+    return {k: window(k, [v for _, v in sorted(x)], last_n, skip) for k, x in vals.items()}
 
 
 def main():
     tag, kdir, fdir, wdir = sys.argv[1:5]
     last_n = int(sys.argv[5]) if len(sys.argv) > 5 else 5
+    skip = int(sys.argv[6]) if len(sys.argv) > 6 else 0
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     prof = os.environ.get("PROFILES_DIR") or os.path.join(root, "profiles")
     os.makedirs(prof, exist_ok=True)
@@ -56,11 +67,12 @@ def main():
     for r in trace:
         k = short(r.get("Kernel_Name", ""))
         dur.setdefault(k, []).append((int(r.get("Dispatch_Id", 0)), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
-    fetch = pmc(fdir, "FETCH_SIZE", last_n)
-    write = pmc(wdir, "WRITE_SIZE", last_n)
-    out = {"note": __doc__.strip().splitlines()[0], "last_n_dispatches": last_n, "kernels": {}}
+    fetch = pmc(fdir, "FETCH_SIZE", last_n, skip)
+    write = pmc(wdir, "WRITE_SIZE", last_n, skip)
+    out = {"note": __doc__.strip().splitlines()[0], "last_n_dispatches": last_n, "skipped_tail": skip,
+           "kernels": {}}
     for k in set(dur) | set(fetch):
-        d = [v for _, v in sorted(dur.get(k, []))][-last_n:]
+        d = window(k, [v for _, v in sorted(dur.get(k, []))], last_n, skip)
         e = {"dispatches_averaged": len(d), "avg_duration_ns": sum(d) / len(d) if d else None}
         if k in fetch and k in write and fetch[k] and write[k]:
             fk = sum(fetch[k]) / len(fetch[k])

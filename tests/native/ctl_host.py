@@ -18,14 +18,16 @@ OUT = os.path.join(HERE, "build")
 
 def build(asan: bool = False) -> str:
     os.makedirs(OUT, exist_ok=True)
-    lib = os.path.join(OUT, "libctl_host_asan.so" if asan else "libctl_host.so")
+    extra = os.environ.get("CTL_HOST_CFLAGS", "").split()  # ablations, e.g. -DRG_CTL_FASTREP
+    tag = "".join(f.strip("-").replace("=", "") for f in extra)
+    lib = os.path.join(OUT, ("libctl_host_asan" if asan else "libctl_host") + (f"_{tag}" if tag else "") + ".so")
     src = os.path.join(HERE, "ctl_host.cpp")
     deps = [src, os.path.join(ROOT, "raftd_amd", "csrc", "raftgpu_control.h"),
             os.path.join(ROOT, "raftd_amd", "csrc", "raftgpu_internal.h"), os.path.join(ROOT, "include", "raftgpu.h")]
     if os.path.exists(lib) and all(os.path.getmtime(d) <= os.path.getmtime(lib) for d in deps):
         return lib
     cmd = ["g++", "-O1" if asan else "-O2", "-g", "-std=c++17", "-fPIC", "-shared", "-D__HIP_PLATFORM_AMD__",
-           "-I/opt/rocm/include", src, "-o", lib]
+           "-I/opt/rocm/include", *extra, src, "-o", lib]
     if asan:
         cmd[1:1] = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"]
     subprocess.run(cmd, check=True)
