@@ -397,6 +397,8 @@ def main():
             "achieved_GBps_per_rank": ((wire_max / K) / (x_ms / 1e3) / 1e9 if x_ms > 0 else
                                        (wire_max / K) / (wall / K) / 1e9),
             "xgmi_peak_GBps_per_rank": min(max(world - 1, 1), 7) * XGMI_LINK_GBS,
+            "xgmi_frac": (((wire_max / K) / (x_ms / 1e3) / 1e9 if x_ms > 0 else (wire_max / K) / (wall / K) / 1e9)
+                          / (min(max(world - 1, 1), 7) * XGMI_LINK_GBS)),
             "note": "bytes = the regions this rank sends to other ranks per step; serial mode times the exchange "
                     "with events on the bench stream, pipelined mode reports bytes / step time (a lower bound)",
         },
