@@ -387,6 +387,7 @@ class LoopbackCluster(_Feeds):
                 g, gr = e.global_id(lr)
                 self.loc[gr - self.rid0] = (k, lr)
         self.wire_bytes = 0
+        self.on_recv = None  # callable(rank, recv tensor, region sizes) before unpack (tests)
 
     def close(self):
         for e in self.engines:
@@ -418,6 +419,9 @@ class LoopbackCluster(_Feeds):
                     so = sum(sizes[a][:k])
                     dst[pos:pos + n].copy_(self.send[a].t[so:so + n])
                 pos += n
+        if self.on_recv is not None:  # tests: inspect or damage the received regions
+            for k in range(self.N):
+                self.on_recv(k, self.recv[k].t, [sizes[a][k] for a in range(self.N)])
         torch.cuda.synchronize()
         for k, e in enumerate(self.engines):
             e.wire_recv(self.recv[k].ptr(), [sizes[a][k] for a in range(self.N)])

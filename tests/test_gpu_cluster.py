@@ -165,3 +165,81 @@ def test_chunked_exchange_rccl():
                          capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
     assert "a2a chunks ok" in out.stdout
+
+
+
+def test_malformed_exchange_data_is_dropped():
+    """Exchange data comes from another process: a unit whose message count exceeds K, and a
+    Replicate whose entry count exceeds E, must not make the receiver index outside its planes.
+    unpack_kernel keeps the well-formed messages before them (the rest are lost, as dropped
+    messages are), and Raft's retries bring every replica back to the same log."""
+    import torch
+    from raftd_amd.cluster import LoopbackCluster, plane_offset
+    G, R, E, N, M_REPLICATE = 8, 3, 8, 2, 12
+    cl = LoopbackCluster(ranks=N, groups=G, replicas=R, log_capacity=64, payload_bytes=16, max_entries_per_msg=E)
+    cols = G // N
+
+    def units(a, k):  # receive units of rank k from rank a: (s, d, j) planes a sends to k
+        return sum(1 for j in range(cols) for s_ in range(R) for d in range(R)
+                   if s_ != d and (a + plane_offset(s_, d, j, N)) % N == k)
+
+    cl.bootstrap()
+    cl.tick()
+    camp = np.zeros(G * R, np.uint8)
+    camp[0::R] = 1
+    cl.tick(campaign=camp)
+    pt, pc = np.zeros(G, np.uint8), np.full(G, 4, np.uint32)
+    for _ in range(6):
+        cl.tick(pt, pc)
+    hits = {"count": 0, "entries": 0}
+
+    def regions(k, buf, rsizes):
+        off = 0
+        for a, n in enumerate(rsizes):
+            if n:
+                nu = units(a, k)
+                yield off, n, nu, -(-nu * 8 // 256) * 256
+            off += n
+
+    def put_u64(buf, at, v):
+        buf[at:at + 8].copy_(torch.from_numpy(np.array([v], np.uint64).view(np.uint8)).to(buf.device))
+
+    def bad_count(k, buf, rsizes):
+        for off, n, nu, tb in regions(k, buf, rsizes):
+            tab = buf[off:off + 8 * nu].cpu().numpy().view(np.uint64)
+            for u in range(nu):
+                if int(tab[u]) & 0xFF:  # the first unit with messages claims 255 of them
+                    put_u64(buf, off + 8 * u, (int(tab[u]) & ~0xFF) | 0xFF)
+                    hits["count"] += 1
+                    break
+
+    def bad_entries(k, buf, rsizes):
+        for off, n, nu, tb in regions(k, buf, rsizes):
+            reg = buf[off:off + n].cpu().numpy()
+            tab = reg[:8 * nu].view(np.uint64)
+            for u in range(nu):
+                h = tb + (int(tab[u]) >> 8) * 16
+                for _ in range(int(tab[u]) & 0xFF):  # walk the unit's messages
+                    w0 = int(reg[h:h + 8].view(np.uint64)[0])
+                    if w0 & 0xFF == M_REPLICATE and w0 >> 32:  # the first Replicate claims 2^20 entries
+                        put_u64(buf, off + h, (w0 & 0xFFFFFFFF) | (1 << 52))
+                        hits["entries"] += 1
+                        return
+                    h += 64 + (w0 >> 32 if w0 & 0xFF == M_REPLICATE else 0) * (16 + 16)
+
+    cl.on_recv = bad_count
+    cl.tick(pt, pc)
+    cl.on_recv = bad_entries
+    cl.tick(pt, pc)
+    cl.on_recv = None
+    assert hits["count"] > 0 and hits["entries"] > 0
+    for _ in range(12):
+        cl.tick(pt, pc)
+    for _ in range(6):
+        cl.tick()
+    views = cl.replicas()
+    assert not any(v["err"] for v in views)
+    for g in range(G):
+        lasts = {int(views[g * R + s]["last"]) for s in range(R)}
+        commits = {int(views[g * R + s]["committed"]) for s in range(R)}
+        assert len(lasts) == 1 and len(commits) == 1, (g, lasts, commits)
