@@ -343,7 +343,9 @@ def main():
     bulk_ms = kms["bulk"][0] / max(kms["bulk"][1], 1)
     ctl_ms = kms["control"][0] / max(kms["control"][1], 1)
     achieved = traffic["bulk_bytes"] / (bulk_ms / 1e3) / 1e9
-    hbm, src = pmc_traffic(wire=bool(args.wire_all))
+    # PMC bytes come from a committed profile of the same mode and launch size; the N > 1 spread
+    # engines (column halves, wire jobs) have none, so their traffic is left unmeasured
+    hbm, src = (None, "no PMC profile of the N > 1 spread mode") if spread else pmc_traffic(wire=bool(args.wire_all))
     out = {
         "metric": METRIC,
         "value": group_steps,
