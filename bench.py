@@ -185,11 +185,16 @@ def apply_copyback(eng, torch, slot_mask=1):
             "note": "count + scan + gather kernels, then one hipMemcpyAsync per array into pinned host memory"}
 
 
-def pmc_traffic(kernel="bulk_kernel", wire=False):
+def pmc_traffic(kernel="bulk_kernel", wire=False, spread=False):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of the
-    same bench mode (profiles/r*_pmc_summary.json; *_wire_* = the --wire-all runs)."""
-    files = [f for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_summary.json")))
-             if ("_wire_" in os.path.basename(f)) == wire]
+    same bench mode (profiles/r*_pmc_summary.json; *_wire_* = the --wire-all runs, *_spread_* =
+    the spread placement with column halves, profiled as one rank whose messages all cross the
+    wire — the launch shape of every rank at N > 1)."""
+    def mode(f):
+        b = os.path.basename(f)
+        return "spread" if "_spread_" in b else "wire" if "_wire_" in b else "plain"
+    want = "spread" if spread else "wire" if wire else "plain"
+    files = [f for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_summary.json"))) if mode(f) == want]
     if not files:
         return None, None
     with open(files[-1]) as f:
@@ -345,7 +350,9 @@ def main():
     achieved = traffic["bulk_bytes"] / (bulk_ms / 1e3) / 1e9
     # PMC bytes come from a committed profile of the same mode and launch size; the N > 1 spread
     # engines (column halves, wire jobs) have none, so their traffic is left unmeasured
-    hbm, src = (None, "no PMC profile of the N > 1 spread mode") if spread else pmc_traffic(wire=bool(args.wire_all))
+    hbm, src = pmc_traffic(wire=bool(args.wire_all), spread=spread)
+    if spread and hbm is not None:  # the spread profile is per half (bench default --halves 2); here per tick
+        hbm = hbm * 2 if args.halves == 2 else None
     out = {
         "metric": METRIC,
         "value": group_steps,
@@ -386,6 +393,8 @@ def main():
             "frac_of_box_copy_ceiling": achieved / copy_gbs if copy_gbs else None,
             "kernel_ms": bulk_ms,
             "launches_timed": kms["bulk"][1],
+            "per": "tick: bulk_kernel launches of every column half summed" if pipelined or (spread and args.halves > 1)
+                   else "launch",
             "algorithmic_bytes_per_launch": traffic["bulk_bytes"],
             "tick_algorithmic_bytes": traffic["algorithmic_bytes"],
             "tick_counts": {k: v for k, v in traffic.items() if k not in ("algorithmic_bytes", "bulk_bytes")},
