@@ -303,6 +303,7 @@ def main():
     wall = time.perf_counter() - t0
     dev_ms = ev0.elapsed_time(ev1)
     kms = host.kernel_ms()
+    c1 = host.sum_committed()  # before the control-timing steps below
     # control_kernel duration from a few more steps after the timed region (timing both kernels
     # adds two event records per tick, which the timed region does without)
     host.timing(True)
@@ -313,7 +314,6 @@ def main():
     kms["control"] = host.kernel_ms()["control"]
     host.timing(False)
     x_ms = sum(a.elapsed_time(b) for a, b in xev) / args.steps if wire and not pipelined else 0.0
-    c1 = host.sum_committed()
     errs = sum(1 for v in eng.replicas(0, min(eng.nrep, 3 * 4096)) if v["err"])
     apply = apply_copyback(eng, torch)
     copy_gbs = hbm_copy_ceiling(eng)
@@ -351,6 +351,8 @@ def main():
     # PMC bytes come from a committed profile of the same mode and launch size; the N > 1 spread
     # engines (column halves, wire jobs) have none, so their traffic is left unmeasured
     hbm, src = pmc_traffic(wire=bool(args.wire_all), spread=spread)
+    if (G, R, E, P, args.log_capacity) != (65536, 3, 64, 256, 2048):  # the profiles are of this workload
+        hbm, src = None, "no PMC profile of this workload"
     if spread and hbm is not None:  # the spread profile is per half (bench default --halves 2); here per tick
         hbm = hbm * 2 if args.halves == 2 else None
     out = {
