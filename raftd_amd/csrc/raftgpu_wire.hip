@@ -207,16 +207,17 @@ __global__ void unpack_kernel(WireParams w) {
   const uint8_t* region = w.recv + w.recv_region[r];
   const uint64_t tv = reinterpret_cast<const uint64_t*>(region)[u - u0];
   uint32_t c = (uint32_t)(tv & 0xFF);
-  const uint8_t* in = region + table_bytes(nu) + (tv >> 8) * 16;
   const uint64_t rend = r + 1 < w.pl.N ? w.recv_region[r + 1] : w.recv_total;
   uint32_t s, d, j;
   unit_decode(w.rmap[u], s, d, j);
   const uint64_t col = (uint64_t)s * w.R + d;
   const uint64_t plane = (uint64_t)w.R * w.R * w.K * w.G;
-  if (c > w.K) {
-    RG_OOB("RG_BOUNDS unpack u=%u r=%u s=%u d=%u j=%u cnt=%u > K\n", u, r, s, d, j, c);
+  if (c > w.K || (tv >> 8) > (rend >> 4)) {  // count beyond K, or a data offset beyond the buffer
+    RG_OOB("RG_BOUNDS unpack u=%u r=%u s=%u d=%u j=%u cnt=%u off16=%llu\n", u, r, s, d, j, c,
+           (unsigned long long)(tv >> 8));
     c = 0;
   }
+  const uint8_t* in = region + table_bytes(nu) + (c ? (tv >> 8) * 16 : 0);
   // malformed data (a count or size beyond the region): keep only the messages before it
   uint32_t k = 0;
   for (; k < c; ++k) {

@@ -207,11 +207,11 @@ def test_malformed_exchange_data_is_dropped():
     def bad_count(k, buf, rsizes):
         for off, n, nu, tb in regions(k, buf, rsizes):
             tab = buf[off:off + 8 * nu].cpu().numpy().view(np.uint64)
-            for u in range(nu):
-                if int(tab[u]) & 0xFF:  # the first unit with messages claims 255 of them
-                    put_u64(buf, off + 8 * u, (int(tab[u]) & ~0xFF) | 0xFF)
-                    hits["count"] += 1
-                    break
+            busy = [u for u in range(nu) if int(tab[u]) & 0xFF]
+            if len(busy) >= 2:  # the first unit with messages claims 255, the next one's data lies at 2^54 B
+                put_u64(buf, off + 8 * busy[0], (int(tab[busy[0]]) & ~0xFF) | 0xFF)
+                put_u64(buf, off + 8 * busy[1], (1 << 58) | (int(tab[busy[1]]) & 0xFF))
+                hits["count"] += 1
 
     def bad_entries(k, buf, rsizes):
         for off, n, nu, tb in regions(k, buf, rsizes):
