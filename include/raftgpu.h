@@ -13,8 +13,10 @@
  *                                    (raft_manager.go:142-144; rc = ElectionRTT 10, HeartbeatRTT 1,
  *                                    CheckQuorum, SnapshotEntries 1000, CompactionOverhead 5 at :92-100)
  *   rg_tick / rg_tick_device      ← the NodeHost tick goroutine (RTTMillisecond 3, raft_manager.go:105)
- *                                    driving Peer.Tick + Peer.Handle for all shards; proposals ≈
- *                                    NodeHost.Propose → Peer.ProposeEntries
+ *                                    driving Peer.Tick + Peer.Handle for all shards
+ *   rg_propose                    ← NodeHost.Propose / SyncPropose(session, cmd []byte) → Peer.ProposeEntries:
+ *                                    the client command bytes raftd's state machine later receives
+ *                                    verbatim as statemachine.Entry.Cmd (raft/state_machine.go:126-145)
  *   rg_leader                     ← NodeHost.GetLeaderID (raft/members.go:21)
  *   rg_read_replicas              ← NodeHost.SyncGetShardMembership / raftState (raft/members.go:30)
  *   rg_read_entries               ← committed-range copy-back feeding IOnDiskStateMachine.Update
@@ -60,7 +62,8 @@ enum { RG_ENTRY_APPLICATION = 0, RG_ENTRY_CONFIG_CHANGE = 1 };
 #define RG_ENTRY_EMPTY 0x100u
 enum {
   RG_ERR_CONFLICT_COMMITTED = 1, RG_ERR_COMMIT_BEYOND_LAST = 2, RG_ERR_RING_FULL = 4,
-  RG_ERR_CRC = 8, RG_ERR_EMPTY_SNAPSHOT = 16
+  RG_ERR_CRC = 8, RG_ERR_EMPTY_SNAPSHOT = 16,
+  RG_ERR_MALFORMED = 32 /* a message with an impossible sender / destination was ignored */
 };
 #define RG_TICK_NO_LOCALTICK 1u
 
@@ -68,7 +71,8 @@ typedef struct rg_config {
   uint32_t groups;              /* shards hosted by this engine */
   uint32_t replicas;            /* replicas per shard, IDs 1..replicas (1..8) */
   uint32_t log_capacity;        /* log ring entries per replica (power of two) */
-  uint32_t payload_bytes;       /* bytes per entry: 0 or a power of two in [16, 1024] */
+  uint32_t payload_bytes;       /* largest Cmd (bytes) an entry carries: 0 (metadata only) or a power of
+                                   two in [16, 1024]; each Cmd is 0..payload_bytes bytes */
   uint32_t max_entries_per_msg; /* entries per Replicate / proposal batch (1..64) */
   uint32_t max_msgs_per_pair;   /* messages per (replica, destination) per tick (1..16) */
   uint32_t num_slabs;           /* proposal payload slabs, tick t uses slab t % num_slabs (>= 2) */
@@ -188,14 +192,36 @@ typedef struct rg_snapshot_event {
   uint64_t index, term; /* kind & RG_SNAP_TAKEN: the new snapshot's index (= applied) and term */
 } rg_snapshot_event;
 
+/* One proposal batch (rg_propose): `count` client commands handed to slot `slot` of shard `group`
+ * (the node's local replica; a follower forwards them to its leader, a candidate drops them).
+ * Cmd k of the batch is lens[first + k] bytes; the Cmds of a call are packed back to back in lens
+ * order in its payload buffer (entry j starts at lens[0] + … + lens[j-1]). */
+typedef struct rg_proposal {
+  uint64_t group;  /* GLOBAL shard id */
+  uint32_t slot;   /* replica slot (replica id - 1); must be hosted by this engine */
+  uint32_t count;  /* 1 .. max_entries_per_msg */
+  uint64_t first;  /* index of the batch's first Cmd in lens[] */
+} rg_proposal;
+
 typedef struct rg_engine rg_engine;
 
 int rg_create(const rg_config* cfg, rg_engine** out);
 void rg_destroy(rg_engine* e);
 /* Every replica: becomeFollower(1) + bootstrap ConfigChange entries 1..R, committed R. */
 int rg_bootstrap(rg_engine* e);
-/* Fill every proposal slab with the deterministic payload generator. */
+/* Fill every proposal slab with the deterministic payload generator: the synthetic
+ * Cmds (payload_bytes each) that tick-input proposals (rg_tick_input.prop_target) carry — the
+ * benchmark's fast path. Client commands enter through rg_propose. */
 int rg_fill_slabs(rg_engine* e);
+/* Stage client commands for the next tick (its proposal step): n batches, Cmd bytes
+ * in `payload` (host memory, copied before return; packed in lens order), lengths in `lens`
+ * (each <= payload_bytes; 0 = an empty Cmd, which commits but is not handed to Update). Calls before
+ * one tick accumulate: batches for the same shard and slot are concatenated up to
+ * max_entries_per_msg. All or nothing: RG_EINVAL (bad shard / slot / count / length, a slot hosted
+ * elsewhere), RG_EFULL (a shard's batch would exceed max_entries_per_msg, or a second slot of one
+ * shard in one tick) — nothing is staged then. The next rg_tick / rg_tick_device takes the staged
+ * batches and must not also carry rg_tick_input.prop_target. */
+int rg_propose(rg_engine* e, const rg_proposal* props, size_t n, const uint8_t* payload, const uint32_t* lens);
 /* One tick for every replica. Input arrays are host pointers (copied before launch; NULL =
  * none). Synchronous with respect to the host buffers, asynchronous on the device. */
 int rg_tick(rg_engine* e, const rg_tick_input* in);
@@ -225,8 +251,11 @@ int rg_read_msgs(rg_engine* e, uint32_t rid, uint32_t dst, rg_msg_view* out, uin
 /* Log entries first_index .. first_index+n-1 of replica rid (must lie in (marker, last]). */
 int rg_read_entries(rg_engine* e, uint32_t rid, uint64_t first_index, uint32_t n, rg_entry_view* out,
                     uint8_t* payload);
+/* Replace replica rid's state and its log (marker, last]: terms[k], types[k] (RG_ENTRY_*, | RG_ENTRY_EMPTY),
+ * payloads = one payload_bytes row per entry of which lens[k] bytes are the Cmd (lens NULL: the whole
+ * row for every application entry with a payload). */
 int rg_import_replica(rg_engine* e, uint32_t rid, const rg_replica_view* v, const uint64_t* terms,
-                      const uint32_t* types, const uint8_t* payloads);
+                      const uint32_t* types, const uint8_t* payloads, const uint32_t* lens);
 /* Enqueue a message as if `rid_src` had emitted it in the last tick (delivered next tick). */
 int rg_deliver(rg_engine* e, uint32_t rid_src, const rg_msg_view* m);
 /* NodeHost.GetLeaderID for GLOBAL group `group`, as this engine's replicas of it know it: a local

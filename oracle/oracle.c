@@ -63,7 +63,12 @@ struct or_engine {
   rep_t* reps;
   uint64_t t; /* next tick to run */
   const or_tick_input* in;
-  /* ring-full etc. use log_capacity */
+  /* caller proposals staged for the next tick (or_propose), per window group */
+  uint8_t* stg_slot;  /* [G] target slot, 0xFF none */
+  uint32_t* stg_n;    /* [G] entries */
+  ent_t* stg_ents;    /* [G][E] len per entry */
+  uint8_t* stg_pay;   /* [G][E][P] Cmd bytes, zero-padded */
+  int staged;
 };
 
 /* ---------------------------------------------------------------- helpers */
@@ -238,9 +243,17 @@ static int remote_try_update(rep_t* r, uint32_t i, uint64_t idx) {
   return 0;
 }
 
-/* raft.appendEntries: n entries at term; payload source: slab entries (slab, g, 0..n-1) or
- * len-0 no-op when slab < 0. Returns 0 when the batch was refused by the capacity rule. */
-static int append_entries(or_engine* e, rep_t* r, uint32_t n, int slab) {
+/* Where the Cmds of an append come from: the entries a Propose message
+ * carries (ents / pay, P bytes per entry), or, for a tick-input proposal, the synthetic generator
+ * (slab >= 0: Cmd k = or_payload(slab, group, k), len P). NULL source: one len-0 no-op. */
+typedef struct {
+  int slab;
+  const ent_t* ents;
+  const uint8_t* pay;
+} src_t;
+
+/* raft.appendEntries: n entries at term. Returns 0 when the batch was refused by the capacity rule. */
+static int append_entries(or_engine* e, rep_t* r, uint32_t n, const src_t* src) {
   uint32_t L = e->c.log_capacity, P = e->c.payload_bytes;
   if (r->last + n > r->cap_base + L) return 0;
   for (uint32_t k = 0; k < n; ++k) {
@@ -248,11 +261,13 @@ static int append_entries(or_engine* e, rep_t* r, uint32_t n, int slab) {
     ent_t* en = log_at(e, r, idx);
     en->term = r->term;
     en->type = OR_ENTRY_APP;
-    if (slab >= 0 && P) {
+    uint32_t len = !src || !P ? 0 : src->ents ? src->ents[k].len : P;
+    if (len) {
       uint8_t* dst = logpay_at(e, r, idx);
-      or_payload(e, (uint32_t)slab, (uint32_t)global_group(e, r), k, dst);
-      en->len = P;
-      en->crc = entry_crc(e, dst, P);
+      if (src->ents) memcpy(dst, src->pay + (size_t)k * P, len);
+      else or_payload(e, (uint32_t)src->slab, (uint32_t)global_group(e, r), k, dst);
+      en->len = len;
+      en->crc = entry_crc(e, dst, len);
     } else {
       en->len = 0;
       en->crc = 0;
@@ -268,7 +283,7 @@ static void become_leader(or_engine* e, rep_t* r) {
   r->role = OR_LEADER;
   reset(e, r, r->term);
   r->leader = id_of(r->s);
-  if (!append_entries(e, r, 1, -1)) r->err |= OR_ERR_RING_FULL;
+  if (!append_entries(e, r, 1, NULL)) r->err |= OR_ERR_RING_FULL;
 }
 
 /* ---------------------------------------------------------------- leader replication (A.12) */
@@ -372,7 +387,7 @@ static void commit_to(rep_t* r, uint64_t i) {
 
 typedef struct {
   or_msg_view h;
-  const ent_t* ents;
+  const ent_t* ents; /* Replicate / Propose entries (NULL: a tick-input proposal, synthetic Cmds) */
   const uint8_t* pay;
 } msg_in_t;
 
@@ -595,9 +610,14 @@ static void handle_leader_check_quorum(or_engine* e, rep_t* r) {
 
 /* ---------------------------------------------------------------- proposals */
 
-static void handle_propose(or_engine* e, rep_t* r, const or_msg_view* m) {
+/* leader: appendEntries + broadcast; follower with a known leader: forward the proposal with its
+ * entries (hop limit 1); otherwise dropped */
+static void handle_propose(or_engine* e, rep_t* r, const msg_in_t* mi) {
+  const or_msg_view* m = &mi->h;
+  uint32_t P = e->c.payload_bytes;
+  src_t src = {(int)m->src_a, mi->ents, mi->pay};
   if (r->role == OR_LEADER) {
-    if (!append_entries(e, r, m->nent, (int)m->src_a)) {
+    if (!append_entries(e, r, m->nent, &src)) {
       r->drops++;
       return;
     }
@@ -607,7 +627,26 @@ static void handle_propose(or_engine* e, rep_t* r, const or_msg_view* m) {
     h.to = (uint8_t)r->leader;
     h.term = 0;
     h.src_b = m->src_b + 1;
-    send_msg(e, r, &h);
+    msg_t* fm = send_msg(e, r, &h);
+    if (fm && P && m->nent) { /* the message carries its Cmds */
+      outbox_t* ob = cur_ob(e, r);
+      arena_reserve(e, ob, m->nent);
+      fm->ent_off = (uint32_t)ob->n_ents;
+      for (uint32_t k = 0; k < m->nent; ++k) {
+        ent_t* en = &ob->ents[ob->n_ents + k];
+        uint8_t* pd = ob->pay + (ob->n_ents + k) * P;
+        memset(en, 0, sizeof *en);
+        en->type = OR_ENTRY_APP;
+        if (mi->ents) {
+          en->len = mi->ents[k].len;
+          memcpy(pd, mi->pay + (size_t)k * P, P);
+        } else {
+          en->len = P;
+          or_payload(e, m->src_a, (uint32_t)global_group(e, r), k, pd);
+        }
+      }
+      ob->n_ents += m->nent;
+    }
   } else {
     r->drops++;
   }
@@ -678,7 +717,7 @@ static void handle(or_engine* e, rep_t* r, const msg_in_t* mi) {
     case OR_CHECK_QUORUM:
       if (r->role == OR_LEADER) handle_leader_check_quorum(e, r);
       break;
-    case OR_PROPOSE: handle_propose(e, r, m); break;
+    case OR_PROPOSE: handle_propose(e, r, mi); break;
     case OR_REPLICATE:
       if (r->role == OR_LEADER) break;
       if (r->role == OR_CANDIDATE) become_follower(e, r, r->term, m->from);
@@ -751,15 +790,31 @@ static void step_replica(or_engine* e, rep_t* r) {
   if (in && in->campaign && in->campaign[rid]) local(e, r, OR_ELECTION);
   /* 3. LocalTick */
   if (!(in && (in->flags & OR_TICK_NO_LOCALTICK))) local(e, r, OR_LOCAL_TICK);
-  /* 4. proposals */
-  if (in && in->prop_target && in->prop_target[r->g] == r->s && in->prop_count[r->g] > 0) {
+  /* 4. proposals: tick input (synthetic Cmds of len P) or the batch staged by or_propose */
+  uint32_t pn = 0;
+  const ent_t* pents = NULL;
+  const uint8_t* ppay = NULL;
+  if (in && in->prop_target) {
+    if (in->prop_target[r->g] == r->s) pn = in->prop_count[r->g];
+  } else if (e->staged && e->stg_slot[r->g] == r->s) {
+    pn = e->stg_n[r->g];
+    pents = e->stg_ents + (size_t)r->g * e->c.max_entries_per_msg;
+    ppay = e->stg_pay + (size_t)r->g * e->c.max_entries_per_msg * e->c.payload_bytes;
+  }
+  if (pn > 0) {
     msg_in_t mi;
     memset(&mi, 0, sizeof mi);
     mi.h.type = OR_PROPOSE;
     mi.h.from = (uint8_t)id_of(r->s);
-    mi.h.nent = in->prop_count[r->g];
+    mi.h.nent = pn;
     mi.h.src_a = (uint32_t)(e->t % e->c.num_slabs);
     mi.h.src_b = 0;
+    uint64_t hm = 0; /* entries with a non-empty Cmd */
+    for (uint32_t k = 0; k < pn; ++k)
+      if (e->c.payload_bytes && (!pents || pents[k].len)) hm |= 1ull << k;
+    mi.h.hint = hm;
+    mi.ents = pents;
+    mi.pay = ppay;
     handle(e, r, &mi);
   }
   /* 5. apply + snapshot + compaction */
@@ -792,6 +847,7 @@ static void* worker(void* p) {
 }
 
 int or_tick(or_engine* e, const or_tick_input* in, int nthreads) {
+  if (in && in->prop_target && e->staged) return -1; /* one proposal source per tick */
   e->in = in;
   if (nthreads <= 1) {
     worker_arg a = {e, 0, 1};
@@ -810,7 +866,65 @@ int or_tick(or_engine* e, const or_tick_input* in, int nthreads) {
   }
   e->in = NULL;
   e->t++;
+  if (e->staged) {
+    memset(e->stg_slot, 0xFF, e->c.groups);
+    memset(e->stg_n, 0, (size_t)e->c.groups * 4);
+    e->staged = 0;
+  }
   return 0;
+}
+
+int or_propose(or_engine* e, const or_proposal* p, size_t n, const uint8_t* payload, const uint32_t* lens) {
+  const uint32_t G = e->c.groups, E = e->c.max_entries_per_msg, P = e->c.payload_bytes;
+  uint64_t tot = 0;
+  for (size_t i = 0; i < n; ++i) tot = p[i].first + p[i].count > tot ? p[i].first + p[i].count : tot;
+  /* byte offset of every entry: Cmds packed in lens order */
+  uint64_t* off = (uint64_t*)calloc(tot + 1, 8);
+  for (uint64_t j = 0; j < tot; ++j) off[j + 1] = off[j] + (lens ? lens[j] : 0);
+  /* validate everything before staging anything */
+  uint8_t* slot = (uint8_t*)malloc(G);
+  uint32_t* cnt = (uint32_t*)malloc((size_t)G * 4);
+  memcpy(slot, e->stg_slot, G);
+  memcpy(cnt, e->stg_n, (size_t)G * 4);
+  int rc = 0;
+  for (size_t i = 0; i < n && !rc; ++i) {
+    if (p[i].group < e->c.group_base || p[i].group >= (uint64_t)e->c.group_base + G || p[i].slot >= e->c.replicas ||
+        p[i].count < 1 || p[i].count > E) {
+      rc = -1;
+      break;
+    }
+    for (uint64_t j = p[i].first; j < p[i].first + p[i].count; ++j)
+      if (lens && lens[j] > P) rc = -1;
+    uint32_t g = (uint32_t)(p[i].group - e->c.group_base);
+    if (!rc && cnt[g] && slot[g] != p[i].slot) rc = -3;
+    if (!rc && cnt[g] + p[i].count > E) rc = -3;
+    if (!rc) {
+      slot[g] = (uint8_t)p[i].slot;
+      cnt[g] += p[i].count;
+    }
+  }
+  if (!rc) {
+    for (size_t i = 0; i < n; ++i) {
+      uint32_t g = (uint32_t)(p[i].group - e->c.group_base);
+      e->stg_slot[g] = (uint8_t)p[i].slot;
+      for (uint32_t k = 0; k < p[i].count; ++k) {
+        uint64_t j = p[i].first + k, at = (uint64_t)g * E + e->stg_n[g] + k;
+        uint32_t len = lens ? lens[j] : 0;
+        e->stg_ents[at].len = len;
+        uint8_t* d = e->stg_pay + at * P;
+        if (P) {
+          memset(d, 0, P);
+          if (len) memcpy(d, payload + off[j], len);
+        }
+      }
+      e->stg_n[g] += p[i].count;
+    }
+    e->staged = n > 0 || e->staged;
+  }
+  free(slot);
+  free(cnt);
+  free(off);
+  return rc;
 }
 
 /* ---------------------------------------------------------------- lifecycle / views */
@@ -828,6 +942,11 @@ int or_create(const or_config* cfg, or_engine** out) {
   or_engine* e = (or_engine*)calloc(1, sizeof *e);
   e->c = *c;
   e->nrep = c->groups * c->replicas;
+  e->stg_slot = (uint8_t*)malloc(c->groups);
+  memset(e->stg_slot, 0xFF, c->groups);
+  e->stg_n = (uint32_t*)calloc(c->groups, 4);
+  e->stg_ents = (ent_t*)calloc((size_t)c->groups * c->max_entries_per_msg, sizeof(ent_t));
+  e->stg_pay = (uint8_t*)calloc((size_t)c->groups * c->max_entries_per_msg * (c->payload_bytes ? c->payload_bytes : 1), 1);
   e->reps = (rep_t*)calloc(e->nrep, sizeof(rep_t));
   for (uint32_t i = 0; i < e->nrep; ++i) {
     rep_t* r = &e->reps[i];
@@ -858,6 +977,10 @@ void or_destroy(or_engine* e) {
     }
   }
   free(e->reps);
+  free(e->stg_slot);
+  free(e->stg_n);
+  free(e->stg_ents);
+  free(e->stg_pay);
   free(e);
 }
 
@@ -967,10 +1090,13 @@ int or_get_entry(const or_engine* e, uint32_t rid, uint64_t index, or_entry_view
 }
 
 int or_import_replica(or_engine* e, uint32_t rid, const or_replica_view* v, const uint64_t* terms,
-                      const uint32_t* types, const uint8_t* payloads) {
+                      const uint32_t* types, const uint8_t* payloads, const uint32_t* lens) {
   if (rid >= e->nrep) return -1;
   rep_t* r = &e->reps[rid];
   if (v->last < v->marker || v->last - v->marker > e->c.log_capacity) return -1;
+  if (lens)
+    for (uint64_t k = 0; k < v->last - v->marker; ++k)
+      if (lens[k] > e->c.payload_bytes) return -1;
   r->term = v->term;
   r->vote = v->vote;
   r->leader = v->leader;
@@ -1006,10 +1132,12 @@ int or_import_replica(or_engine* e, uint32_t rid, const or_replica_view* v, cons
     ent_t* en = log_at(e, r, i);
     en->term = terms[k];
     en->type = types ? (types[k] & 0xFFu) : OR_ENTRY_APP;
-    if (payloads && P && en->type == OR_ENTRY_APP && !(types && (types[k] & OR_ENTRY_EMPTY))) {
-      en->len = P;
-      memcpy(logpay_at(e, r, i), payloads + k * P, P);
-      en->crc = entry_crc(e, logpay_at(e, r, i), P);
+    uint32_t len = lens ? lens[k] : P;
+    if (payloads && P && len && en->type == OR_ENTRY_APP && !(types && (types[k] & OR_ENTRY_EMPTY))) {
+      en->len = len;
+      memset(logpay_at(e, r, i), 0, P);
+      memcpy(logpay_at(e, r, i), payloads + k * P, len);
+      en->crc = entry_crc(e, logpay_at(e, r, i), len);
     } else {
       en->len = 0;
       en->crc = 0;

@@ -71,6 +71,18 @@ typedef struct or_msg_view {
   uint64_t term, log_term, log_index, commit, hint, hint_high;
   uint32_t src_a, src_b; /* Propose: slab id, hop count */
 } or_msg_view;
+/* A Propose message carries its nent entries (Cmd bytes + length, like pb.Message.Entries of a
+ * forwarded MsgProp); its header `hint` is the mask of entries with a non-empty Cmd (bit k). */
+
+/* One proposal batch handed to a shard's replica (NodeHost.Propose → Peer.ProposeEntries):
+ * `count` Cmds whose lengths are lens[first .. first+count) and whose bytes are packed back to back
+ * in lens order in the payload buffer of or_propose. */
+typedef struct or_proposal {
+  uint64_t group;  /* global shard id (group_base + window-local id) */
+  uint32_t slot;   /* replica slot the node hands the batch to */
+  uint32_t count;  /* entries, 1 .. max_entries_per_msg */
+  uint64_t first;  /* its first entry in lens[] */
+} or_proposal;
 
 typedef struct or_entry_view {
   uint64_t term;
@@ -102,9 +114,19 @@ int or_get_msgs(const or_engine* e, uint32_t rid, uint32_t dst, or_msg_view* out
 int or_get_msg_terms(const or_engine* e, uint32_t rid, uint32_t dst, uint32_t k, uint64_t* terms, uint32_t cap);
 /* Log entry at `index` of replica rid (must be in (marker, last]). payload may be NULL. */
 int or_get_entry(const or_engine* e, uint32_t rid, uint64_t index, or_entry_view* out, uint8_t* payload);
-/* Replace a replica's state and log (entries for indices marker+1 .. last). */
+/* Replace a replica's state and log (entries for indices marker+1 .. last). payloads: one row of
+ * payload_bytes per entry; lens (NULL = payload_bytes for every application entry with a payload)
+ * = the Cmd length of each entry, its first lens[k] bytes of row k. */
 int or_import_replica(or_engine* e, uint32_t rid, const or_replica_view* v,
-                      const uint64_t* terms, const uint32_t* types, const uint8_t* payloads);
+                      const uint64_t* terms, const uint32_t* types, const uint8_t* payloads,
+                      const uint32_t* lens);
+/* Stage caller proposals for the next tick (its step 4 instead of tick-input prop_target; a tick
+ * given both fails). Batches for the same group and slot are concatenated (at most
+ * max_entries_per_msg in all); a second slot of one group in one tick, an empty or oversized batch,
+ * a Cmd longer than payload_bytes or a group outside the window fail the whole call, staging
+ * nothing: -1 invalid, -3 batch full. Cmd bytes packed in lens order (entry j at the sum of
+ * lens[0..j)). */
+int or_propose(or_engine* e, const or_proposal* p, size_t n, const uint8_t* payload, const uint32_t* lens);
 /* Append a message to rid_src's most recent outbox so it is delivered next tick. Replicate
  * entries are taken from the sender's current log (indices log_index+1 ..). */
 int or_deliver(or_engine* e, uint32_t rid_src, const or_msg_view* m);
@@ -116,7 +138,7 @@ int or_get_applied(const or_engine* e, uint32_t rid, uint64_t* index, or_entry_v
 #define OR_SNAP_TAKEN 1
 #define OR_SNAP_RESTORED 2
 int or_get_snapshot_event(const or_engine* e, uint32_t rid, uint64_t* restored, uint64_t* index, uint64_t* term);
-/* Proposal payload generator. */
+/* Proposal payload generator: the synthetic Cmd of a tick-input proposal, len payload_bytes. */
 void or_payload(const or_engine* e, uint32_t slab, uint32_t group, uint32_t entry, uint8_t* out);
 uint32_t or_crc32(const uint8_t* p, size_t n);
 uint32_t or_crc32c(const uint8_t* p, size_t n);

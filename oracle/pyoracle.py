@@ -65,6 +65,10 @@ class EntryView(C.Structure):
                 ("crc", C.c_uint32), ("_pad", C.c_uint32)]
 
 
+class Proposal(C.Structure):
+    _fields_ = [("group", C.c_uint64), ("slot", C.c_uint32), ("count", C.c_uint32), ("first", C.c_uint64)]
+
+
 class TickInput(C.Structure):
     _fields_ = [("prop_target", C.c_void_p), ("prop_count", C.c_void_p), ("campaign", C.c_void_p),
                 ("isolate", C.c_void_p), ("flags", C.c_uint32)]
@@ -103,7 +107,10 @@ def lib():
         L.or_get_applied.argtypes = [vp, u32, C.c_void_p, C.c_void_p, C.c_void_p, u32]
         L.or_get_snapshot_event.argtypes = [vp, u32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                             C.POINTER(C.c_uint64)]
-        L.or_import_replica.argtypes = [vp, u32, C.POINTER(ReplicaView), C.c_void_p, C.c_void_p, C.c_void_p]
+        L.or_import_replica.argtypes = [vp, u32, C.POINTER(ReplicaView), C.c_void_p, C.c_void_p, C.c_void_p,
+                                        C.c_void_p]
+        L.or_propose.argtypes = [vp, C.POINTER(Proposal), C.c_size_t, C.c_void_p, C.c_void_p]
+        L.or_tick.restype = C.c_int
         L.or_deliver.argtypes = [vp, u32, C.POINTER(MsgView)]
         L.or_payload.argtypes = [vp, u32, u32, u32, C.c_void_p]
         L.or_crc32.argtypes = [C.c_void_p, C.c_size_t]
@@ -189,7 +196,15 @@ class Oracle:
 
     def tick(self, prop_target=None, prop_count=None, campaign=None, isolate=None, flags=0, threads=1):
         ti = TickInputs(self.G, self.R, prop_target, prop_count, campaign, isolate, flags)
-        self.L.or_tick(self.h, C.byref(ti.ti), threads)
+        if self.L.or_tick(self.h, C.byref(ti.ti), threads) != 0:
+            raise ValueError("or_tick: tick-input proposals while caller proposals are staged")
+
+    def propose(self, batches):
+        """Stage caller proposals for the next tick (or_propose): batches = [(global group, slot,
+        [Cmd bytes, ...]), ...]. Returns the oracle's code (0, -1 invalid, -3 batch full)."""
+        props, lens, blob = pack_proposals(batches)
+        return self.L.or_propose(self.h, props, len(batches), blob.ctypes.data if blob.size else None,
+                                 lens.ctypes.data if lens.size else None)
 
     @property
     def t(self) -> int:
@@ -252,7 +267,7 @@ class Oracle:
         r = self.replica(rid)
         return [self.entry(rid, i)["term"] for i in range(r["marker"] + 1, r["last"] + 1)]
 
-    def import_replica(self, rid, view: dict, terms, types=None, payloads=None):
+    def import_replica(self, rid, view: dict, terms, types=None, payloads=None, lens=None):
         v = ReplicaView()
         for f in REPLICA_FIELDS:
             if f in view:
@@ -266,9 +281,11 @@ class Oracle:
         t = np.ascontiguousarray(np.array(terms, dtype=np.uint64))
         ty = None if types is None else np.ascontiguousarray(np.array(types, dtype=np.uint32))
         pl = None if payloads is None else np.ascontiguousarray(np.frombuffer(payloads, dtype=np.uint8))
+        ln = None if lens is None else np.ascontiguousarray(np.array(lens, dtype=np.uint32))
         rc = self.L.or_import_replica(self.h, rid, C.byref(v), t.ctypes.data if len(t) else None,
                                       None if ty is None else ty.ctypes.data,
-                                      None if pl is None else pl.ctypes.data)
+                                      None if pl is None else pl.ctypes.data,
+                                      None if ln is None or not ln.size else ln.ctypes.data)
         if rc != 0:
             raise ValueError("or_import_replica failed")
 
@@ -286,6 +303,21 @@ class Oracle:
         buf = (C.c_uint8 * max(self.cfg["payload_bytes"], 1))()
         self.L.or_payload(self.h, slab, group, entry, buf)
         return bytes(buf[:self.cfg["payload_bytes"]])
+
+
+def pack_proposals(batches):
+    """[(group, slot, [cmd bytes])] → (Proposal array, u32 lens, packed u8 Cmd bytes): the layout
+    or_propose and rg_propose take (Cmds back to back in lens order)."""
+    props = (Proposal * max(len(batches), 1))()
+    lens, chunks, first = [], [], 0
+    for i, (g, s, cmds) in enumerate(batches):
+        props[i].group, props[i].slot, props[i].count, props[i].first = g, s, len(cmds), first
+        for c in cmds:
+            lens.append(len(c))
+            chunks.append(bytes(c))
+        first += len(cmds)
+    blob = np.frombuffer(b"".join(chunks), dtype=np.uint8).copy() if chunks else np.zeros(0, np.uint8)
+    return props, np.array(lens, dtype=np.uint32), blob
 
 
 def crc32(b: bytes) -> int:

@@ -203,16 +203,17 @@ class Replica:
         self.role = LEADER
         self.reset(self.term)
         self.leader = self.id
-        if not self.append(1, None):
+        if not self.append(1, ()):
             self.err |= ERR_RING
 
-    def append(self, n, slab):
+    def append(self, n, cmds):
+        """appendEntries of n entries at the current term; cmds[k] = Cmd bytes of entry k (() for
+        the leader's empty no-op)."""
         c = self.sim.cfg
         if self.last + n > self.cap_base + c["log_capacity"]:
             return False
         for k in range(n):
-            data = b"" if slab is None else self.sim.payload(slab, self.g, k)
-            self.log.append(Entry(self.term, 0, data))
+            self.log.append(Entry(self.term, 0, cmds[k] if k < len(cmds) else b""))
         self.remotes[self.s].try_update(self.last)
         if self.sim.R == 1:
             self.try_commit()
@@ -411,9 +412,9 @@ class Replica:
                 self.active = set()
                 if c_act < self.sim.quorum:
                     self.become_follower(self.term, 0)
-        elif t == PROPOSE:
+        elif t == PROPOSE:  # the message carries its Cmds (m["ents"])
             if role == LEADER:
-                if not self.append(m["nent"], m["src_a"]):
+                if not self.append(m["nent"], [e.data for e in m["ents"]]):
                     self.drops += 1
                     return
                 self.broadcast_replicate()
@@ -479,6 +480,28 @@ class Sim:
         self.isolate = None
         self.reps = [Replica(self, g, s) for g in range(self.G) for s in range(self.R)]
         self._pay = {}
+        self.staged = {}  # window group -> (slot, [cmd bytes]) for the next tick (propose)
+
+    def propose(self, batches):
+        """Stage caller proposals (group, slot, [cmds]) for the next tick; all or nothing:
+        0, -1 (invalid) or -3 (a group's batch is full / has a second slot)."""
+        c = self.cfg
+        E, P, base = c["max_entries_per_msg"], c["payload_bytes"], c["group_base"]
+        new = {g: (s, list(v)) for g, (s, v) in self.staged.items()}
+        for g, s, cmds in batches:
+            if not (base <= g < base + self.G) or s >= self.R or not 1 <= len(cmds) <= E:
+                return -1
+            if any(len(x) > P for x in cmds):
+                return -1
+            lg = g - base
+            if lg in new and new[lg][1] and new[lg][0] != s:
+                return -3
+            cur = new.setdefault(lg, (s, []))[1]
+            if len(cur) + len(cmds) > E:
+                return -3
+            cur.extend(bytes(x) for x in cmds)
+        self.staged = new
+        return 0
 
     def payload(self, slab, g, k):
         key = (slab, g, k)
@@ -508,6 +531,9 @@ class Sim:
         self.t = 0
 
     def tick(self, prop_target=None, prop_count=None, campaign=None, isolate=None, flags=0):
+        if prop_target is not None and self.staged:
+            raise ValueError("tick-input proposals while caller proposals are staged")
+        staged, self.staged = self.staged, {}
         self.isolate = isolate
         inbox = {id(r): [] for r in self.reps}
         for r in self.reps:  # deliver last tick's outboxes
@@ -530,9 +556,17 @@ class Sim:
                     r.local(ELECTION)
                 if not flags & 1:
                     r.local(LOCAL_TICK)
+                slab = self.t % self.cfg["num_slabs"]
+                cmds = None
                 if prop_target is not None and prop_target[g] == s and prop_count[g] > 0:
-                    r.handle(msg(PROPOSE, r.id, frm=r.id, nent=int(prop_count[g]),
-                                 src_a=self.t % self.cfg["num_slabs"], src_b=0))
+                    P = self.cfg["payload_bytes"]
+                    cmds = [self.payload(slab, g, k) if P else b"" for k in range(int(prop_count[g]))]
+                elif g in staged and staged[g][0] == s:
+                    cmds = staged[g][1]
+                if cmds:
+                    hm = sum(1 << k for k, x in enumerate(cmds) if x)
+                    r.handle(msg(PROPOSE, r.id, frm=r.id, nent=len(cmds), hint=hm, src_a=slab, src_b=0,
+                                 ents=tuple(Entry(0, 0, x) for x in cmds)))
                 r.applied = r.committed
                 se, co = self.cfg["snapshot_entries"], self.cfg["compaction_overhead"]
                 if se and r.applied - r.snap_index >= se:
@@ -567,7 +601,7 @@ class Sim:
         return dict(term=e.term, type=e.type, len=len(e.data), crc=e.crc)
 
     # -- scenario helpers (KATs): same contract as or_import_replica / or_deliver --
-    def import_replica(self, rid, view: dict, terms, types=None, payloads=None):
+    def import_replica(self, rid, view: dict, terms, types=None, payloads=None, lens=None):
         r = self.reps[rid]
         P = self.cfg["payload_bytes"]
         for k in ("term", "vote", "leader", "committed", "applied", "marker", "marker_term",
@@ -584,7 +618,8 @@ class Sim:
         r.log = []
         for k, t in enumerate(terms):
             ty = 0 if types is None else types[k]
-            data = payloads[k * P:(k + 1) * P] if (payloads is not None and P and ty == 0) else b""
+            ln = P if lens is None else lens[k]
+            data = payloads[k * P:k * P + ln] if (payloads is not None and P and ty == 0) else b""
             r.log.append(Entry(t, ty, bytes(data)))
         assert r.last == view.get("last", r.last)
         r.remotes = []

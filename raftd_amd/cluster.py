@@ -457,9 +457,19 @@ class LoopbackCluster(_Feeds):
         k, lr = self.loc[rid]
         return self.engines[k].entry(lr, index, with_payload)
 
-    def import_replica(self, rid, view, terms, types=None, payloads=None):
+    def import_replica(self, rid, view, terms, types=None, payloads=None, lens=None):
         k, lr = self.loc[rid]
-        self.engines[k].import_replica(lr, view, terms, types, payloads)
+        self.engines[k].import_replica(lr, view, terms, types, payloads, lens)
+
+    def propose(self, batches):
+        """rg_propose on the rank hosting each batch's replica (global group, slot)."""
+        per = [[] for _ in range(self.N)]
+        for g, s, cmds in batches:
+            gg = g + self.rid0 // self.R  # global group
+            per[rank_of(gg, s, self.N)].append((gg, s, cmds))
+        for k, b in enumerate(per):
+            if b:
+                self.engines[k].propose(b)
 
     def deliver(self, rid_src, **fields):
         k, lr = self.loc[rid_src]

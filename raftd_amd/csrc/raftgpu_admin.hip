@@ -84,8 +84,8 @@ __global__ void gather_entries_kernel(AdminParams a, uint32_t rid, uint64_t firs
   rg_entry_view v;
   v.term = w & TERM_MASK;
   v.type = (uint32_t)((w >> 61) & 1);
-  v.len = inf.y & 0xFFFFFF;
-  v.crc = inf.x;
+  v.len = (w & PAY_BIT) ? word_len(w) : 0u;
+  v.crc = (w & PAY_BIT) ? crc_of_cmd(inf.x, v.len, t.P, a.zi) : 0u;  // the ring keeps the slot CRC
   v.bank = (uint32_t)bank;
   out[i] = v;
   if (out_pay && t.P && v.len) {
@@ -101,7 +101,8 @@ hipError_t launch_gather_entries(const AdminParams& a, uint32_t rid, uint64_t fi
   return hipGetLastError();
 }
 
-// import: view + entry words (term|type|pay, bank 0) + payloads + CRCs into the current state
+// import: view + entry words (term|len|type|pay, bank 0) + payloads (zero-padded P-byte rows) + slot
+// CRCs into the current state
 __global__ void scatter_replica_kernel(AdminParams a, uint32_t rid, const rg_replica_view* vv, const uint64_t* words,
                                        const uint8_t* pays, const uint32_t* crcs, uint32_t nent, uint2* info,
                                        uint8_t* pay) {

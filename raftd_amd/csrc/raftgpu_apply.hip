@@ -64,8 +64,8 @@ __global__ void __launch_bounds__(256) apply_gather_kernel(ApplyParams a) {
       r.index = i;
       r.group = group;
       r.replica_id = s + 1;
-      r.len = inf.y & 0xFFFFFF;
-      r.crc = inf.x;
+      r.len = word_len(w);
+      r.crc = crc_of_cmd(inf.x, r.len, a.P, a.zi);  // the ring keeps the slot CRC
       r.rid = j * a.R + s;
       reinterpret_cast<rg_apply_entry*>(a.out_rec)[k] = r;
     }
@@ -168,8 +168,8 @@ __global__ void __launch_bounds__(256) persist_entries_kernel(PersistParams a) {
       r.index = i;
       r.term = w & TERM_MASK;
       r.type = (uint32_t)((w >> 61) & 1);
-      r.len = inf.y & 0xFFFFFF;
-      r.crc = inf.x;
+      r.len = (w & PAY_BIT) ? word_len(w) : 0u;
+      r.crc = (w & PAY_BIT) ? crc_of_cmd(inf.x, r.len, a.P, a.zi) : 0u;
       r.rid = j * a.R + s;
       reinterpret_cast<rg_persist_entry*>(a.out_ent)[base + (i - lo)] = r;
     }

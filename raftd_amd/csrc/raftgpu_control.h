@@ -163,6 +163,10 @@ struct Ctl {
                                       uint64_t log_term, uint64_t log_index, uint64_t commit, uint64_t hint,
                                       uint64_t hint_high, uint32_t src_a, uint32_t src_b) {
     const uint32_t dst = to - 1;
+    if (dst >= (uint32_t)R) {  // unreachable with validated inputs (handle() and unpack check ids)
+      err |= ERR_WIRE;
+      return -1;
+    }
     if (type != M_PROPOSE && type != M_REQUEST_VOTE) mterm = term;
     const uint32_t n = get8(em, dst);
     em += 1ull << (8 * dst);
@@ -253,10 +257,11 @@ struct Ctl {
   }
 
   // ---- log writes: term ring + banks, and a job for the bulk kernel
-  // Entry e in [e0, n) goes to index base+e. Words come from the sender's inline terms (RING:
-  // mt points at entry 0, stride G) or are `word` for every entry (SLAB proposals, no-op).
+  // Entry e in [e0, n) goes to index base+e with ring word `word` | (the inline word mt[e·G] of a
+  // Replicate or remote Propose, when mt is set) | (len_bits of slab Cmd e, li[e].y, when li is set).
+  // aux: the J_SMASK of a WIRE job (record offset) or a SLAB job (slab row).
   RG_FN void write_entries(uint64_t base, uint32_t e0, uint32_t n, uint32_t kind, uint32_t src,
-                                const uint64_t* mt, uint64_t word, uint64_t wofs = 0) {
+                                const uint64_t* mt, uint64_t word, uint64_t aux = 0, const uint2* li = nullptr) {
     const uint64_t hi_prot = umax64(last_start, sent_hi);
 #ifdef RG_CTL_FASTREP
     la_n = 0;
@@ -273,7 +278,7 @@ struct Ctl {
       for (uint32_t k = 0; k < RG_CTL_BATCH; ++k) {
         const uint64_t idx = base + e + k;
         const bool in = e + k < n;
-        wv[k] = in && mt ? mt[(uint64_t)(e + k) * p.G] : word;
+        wv[k] = word | (!in ? 0ull : mt ? mt[(uint64_t)(e + k) * p.G] : li ? len_bits(li[e + k].y) : 0ull);
         ov[k] = in && idx <= hi_prot ? *tr_at(idx) : 0;
       }
 #pragma unroll
@@ -305,7 +310,7 @@ struct Ctl {
         rw_hi = umax64(rw_hi, hi_w);
       }
     }
-    if (kind == SRC_WIRE) sm = wofs;  // source bank bits are meaningless off-rank
+    if (kind == SRC_WIRE || kind == SRC_WIRE_PROP) sm = aux;  // source bank bits are meaningless off-rank
     if (nj < p.J) {
       const uint64_t n64 = p.nrep, JN = (uint64_t)p.J * n64;
       uint64_t* j64 = p.job64 + (uint64_t)nj * n64 + q;
@@ -321,20 +326,27 @@ struct Ctl {
     }
   }
 
-  // raft.appendEntries (leader side): n entries at term, from slab (or a len-0 no-op)
-  RG_FN bool append_local(uint32_t n, int slab_id) {
+  // raft.appendEntries (leader side): n entries at term. slab_id < 0: the leader's empty no-op.
+  // Otherwise Cmds of a proposal: in slab `slab_id`, row of replica slot `rslot` in this column,
+  // with lengths li[0..n) (li NULL: synthetic Cmds, P bytes each), or — rmt set: forwarded from
+  // another rank — their inline words rmt[e·G] (length bits) and bytes in the receive buffer at
+  // record offset wofs.
+  RG_FN bool append_local(uint32_t n, int slab_id, uint32_t rslot = 0, const uint2* li = nullptr,
+                          const uint64_t* rmt = nullptr, uint64_t wofs = 0) {
     if (last + n > cap_base + p.L) return false;
-    const bool pay = slab_id >= 0 && p.P;
-    const uint64_t base = last + 1, w = term | (pay ? PAY_BIT : 0);
+    const uint64_t base = last + 1;
 #ifdef RG_CTL_FASTREP
     const bool plain = base > umax64(last_start, sent_hi);  // no protected index: every bank bit 0
     const uint64_t pt = plain ? term_at(last) : 0;
 #endif
-    write_entries(base, 0, n, pay ? SRC_SLAB : SRC_NONE, pay ? (uint32_t)slab_id : 0, nullptr, w);
+    const uint64_t w = slab_id >= 0 && !li && !rmt ? term | len_bits(p.P) : term;
+    if (slab_id < 0 || !p.P) write_entries(base, 0, n, SRC_NONE, 0, nullptr, w);
+    else if (rmt) write_entries(base, 0, n, SRC_WIRE_PROP, n, rmt, w, wofs);
+    else write_entries(base, 0, n, SRC_SLAB, (uint32_t)slab_id | (rslot << 16), nullptr, w, 0, li);
 #ifdef RG_CTL_FASTREP
-    if (plain) {
+    if (plain && !li && !rmt) {  // every entry holds the same word
       la_base = base;
-      la_word = w & ~BANK_BIT;
+      la_word = w;
       la_pt = pt;
       la_n = n;
     }
@@ -348,7 +360,7 @@ struct Ctl {
     role = LEADER;
     reset(term);
     leader = my_id();
-    if (!append_local(1, -1)) err |= ERR_RING;
+    if (!append_local(1, -1)) err |= ERR_RING;  // the empty no-op
   }
 
   // ---- replication (A.12)
@@ -571,16 +583,18 @@ struct Ctl {
     if (c < quorum()) become_follower(term, 0);
   }
 
-  // ---- proposals
-  RG_FN void handle_propose(uint32_t nent, uint32_t slab_id, uint32_t hop) {
+  // ---- proposals: nent Cmds (hm = those with a non-empty Cmd, the forwarded header's hint); their
+  // bytes and lengths as append_local takes them
+  RG_FN void handle_propose(uint32_t nent, uint32_t slab_id, uint32_t hop, uint64_t hm, uint32_t rslot,
+                            const uint2* li, const uint64_t* rmt, uint64_t wofs) {
     if (role == LEADER) {
-      if (!append_local(nent, (int)slab_id)) {
+      if (!append_local(nent, (int)slab_id, rslot, li, rmt, wofs)) {
         drops++;
         return;
       }
       broadcast_replicate();
     } else if (role == FOLLOWER && leader != 0 && hop == 0) {
-      send(M_PROPOSE, (uint32_t)leader, 0, 0, nent, 0, 0, 0, 0, 0, slab_id, hop + 1);
+      send(M_PROPOSE, (uint32_t)leader, 0, 0, nent, 0, 0, 0, hm, 0, slab_id, hop + 1);
     } else {
       drops++;
     }
@@ -616,6 +630,10 @@ struct Ctl {
     const uint64_t mterm = h[1 * plane];
     const uint32_t type = (uint32_t)(w0 & 0xFF);
     const uint32_t from = (uint32_t)(w0 >> 8) & 0xFF;
+    if (from - 1 >= (uint32_t)R) {  // unreachable: local senders stamp their id, unpack checks remote ones
+      err |= ERR_WIRE;
+      return;
+    }
 #ifdef RG_BOUNDS  // unpack_kernel keeps only well-formed messages
     if (type == M_REPLICATE && (uint32_t)(w0 >> 32) > p.E) {
       RG_OOB("RG_BOUNDS control q=%u src=%u k=%u remote=%d replicate n=%u > E=%u\n", q, src, k, (int)remote,
@@ -636,9 +654,23 @@ struct Ctl {
       }
     }
     switch (type) {
-      case M_PROPOSE: {
+      case M_PROPOSE: {  // forwarded (hop 1). Local: the Cmds are in the forwarder's row of slab w7;
+        // remote: unpack put their length words in rmt and their records' offset in word 7
         const uint64_t w7 = h[7 * plane];
-        handle_propose((uint32_t)(w0 >> 32), (uint32_t)w7, (uint32_t)(w7 >> 32));
+        const uint32_t nent = (uint32_t)(w0 >> 32);
+        if (nent - 1 >= p.E || (!remote && (uint32_t)w7 >= p.nslab)) {  // unreachable: senders forward
+          err |= ERR_WIRE;                                               // 1..E entries of a slab
+          break;
+        }
+        if (remote) {
+          const uint64_t* rm = p.rmt + ((((uint64_t)src * R + s) * p.K + k) * p.E) * p.G + g;
+          handle_propose(nent, 0, 1, h[5 * plane], 0, nullptr, rm, w7);
+        } else {
+          const uint64_t row = p.wire ? (uint64_t)src * p.G + g : g;  // the forwarder's slab row (same rank)
+          const uint64_t rows = p.wire ? p.nrep : p.G;
+          const uint2* li = p.slab_info + ((uint64_t)(uint32_t)w7 * rows + row) * p.E;
+          handle_propose(nent, (uint32_t)w7, (uint32_t)(w7 >> 32), h[5 * plane], src, li, nullptr, 0);
+        }
         break;
       }
       case M_REPLICATE:
@@ -701,7 +733,16 @@ struct Ctl {
     RG_STAMP(2);
     if (p.prop_target && p.prop_target[gi] == s) {
       const uint32_t n = p.prop_count[gi];
-      if (n > 0) handle_propose(n, (uint32_t)(p.tick % p.nslab), 0);
+      if (n > p.E) {  // rg_tick_device's contract: batches of at most E entries (the host path checks)
+        drops++;
+      } else if (n > 0) {
+        // caller batch (rg_propose): lengths in slab_info; tick-input batch: synthetic Cmds of P bytes
+        const uint32_t sl = (uint32_t)(p.tick % p.nslab);
+        const uint64_t row = p.wire ? q : g, rows = p.wire ? p.nrep : p.G;
+        const uint64_t hm = !p.P ? 0ull : p.prop_hmask ? p.prop_hmask[gi] : (n >= 64 ? ~0ull : (1ull << n) - 1);
+        const uint2* li = p.prop_hmask && p.P ? p.slab_info + ((uint64_t)sl * rows + row) * p.E : nullptr;
+        handle_propose(n, sl, 0, hm, s, li, nullptr, 0);
+      }
     }
     RG_STAMP(3);
     applied = committed;  // apply, snapshot, compaction

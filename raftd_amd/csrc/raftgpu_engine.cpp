@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <unordered_map>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -70,6 +71,22 @@ struct rg_engine {
   uint32_t* jcnt[2] = {nullptr, nullptr};
   uint32_t* crc_err = nullptr;
   uint8_t* slabs = nullptr;
+  uint2* slab_info = nullptr;  // [nslab][rows][E] {0, Cmd length}
+  bool slabs_synthetic = false;  // every slab holds the generator's bytes (rg_fill_slabs, no rg_propose since)
+  // caller proposals staged for the next tick (rg_propose): pinned host tables indexed by global input
+  // index, uploaded by the tick; Cmd bytes + per-entry descriptors staged through pinned buffers
+  uint8_t* h_pt = nullptr;
+  uint32_t* h_pc = nullptr;
+  uint64_t* h_hm = nullptr;
+  uint64_t* d_prop_hmask = nullptr;
+  std::vector<uint64_t> touched;  // input indices set in h_* since the last upload
+  bool staged = false, stg_reset_pending = false;
+  hipEvent_t stg_ev = nullptr;    // the last upload of h_* (host may rewrite them once it completed)
+  hipEvent_t prop_ev = nullptr;   // the last H2D out of the pinned Cmd staging below
+  uint8_t* h_cmd = nullptr;       // pinned: Cmd bytes, then off / dst (u64) and len (u32) per entry
+  uint64_t h_cmd_cap = 0;
+  uint8_t* d_cmd = nullptr;
+  uint64_t d_cmd_cap = 0;
   uint32_t* crc_tab = nullptr;
   uint32_t crc_const = 0;
   uint8_t* d_prop_target = nullptr;
@@ -122,6 +139,8 @@ struct rg_engine {
   uint64_t *psoff = nullptr, *peoff = nullptr;
 };
 
+static int stage_reset(rg_engine* e);
+
 // ---------------------------------------------------------------- CRC-32 tables
 // Reflected CRC-32, init and xorout 0xFFFFFFFF: IEEE (zlib) or Castagnoli (rg_config.crc32c).
 // Everything the kernels use (byte, nibble and shift tables, the finalisation constant) is built
@@ -153,6 +172,20 @@ static void build_crc(rg_engine* e, std::vector<uint32_t>& tab) {
       for (uint32_t n = 0; n < 16; ++n)
         tab[CRC_T_WORDS + CRC_N_WORDS + c * CRC_SH_STRIDE + j * 16 + n] = Zn(n << (4 * j), 16 * (nch - 1 - c));
   e->crc_const = Zn(0xFFFFFFFFu, e->c.payload_bytes) ^ 0xFFFFFFFFu;
+  // inverse shifts: Z(x) = T0[x & 0xFF] ^ (x >> 8) is invertible (the top byte of T0[b] names b)
+  uint32_t top[256];
+  for (uint32_t b = 0; b < 256; ++b) top[T0[b] >> 24] = b;
+  auto Zi = [&](uint32_t y) {
+    const uint32_t b = top[y >> 24];
+    return ((y ^ T0[b]) << 8) | b;
+  };
+  for (uint32_t b = 0; b < CRC_ZI_BITS; ++b)
+    for (uint32_t j = 0; j < 8; ++j)
+      for (uint32_t n = 0; n < 16; ++n) {
+        uint32_t x = n << (4 * j);
+        for (uint32_t i = 0; i < (1u << b); ++i) x = Zi(x);
+        tab[CRC_ZI_OFF + (b * 8 + j) * 16 + n] = x;
+      }
 }
 
 static uint32_t host_crc(const rg_engine* e, const uint8_t* p, size_t n) {
@@ -198,6 +231,7 @@ static TickParams params(rg_engine* e) {
   p.E = c.max_entries_per_msg; p.K = c.max_msgs_per_pair; p.nslab = c.num_slabs; p.J = e->J;
   p.ET = c.election_rtt; p.HT = c.heartbeat_rtt; p.CQ = c.check_quorum; p.SE = c.snapshot_entries;
   p.CO = c.compaction_overhead; p.drop_ppm = c.drop_ppm;
+  p.wire = e->wire ? 1u : 0u;
   p.seed = c.seed;
   p.tick = e->t;
   p.pl = e->pl;
@@ -212,6 +246,7 @@ static TickParams params(rg_engine* e) {
   p.cnt_in = e->cnt[b]; p.cnt_out = e->cnt[a];
   p.job64 = e->job64[a]; p.job32 = e->job32[a]; p.jcnt = e->jcnt[a];
   p.rhdr = e->rhdr; p.rmt = e->rmt; p.rcnt = e->rcnt;
+  p.slab_info = e->slab_info;
   p.apply_lo = e->apply_lo;
   p.persist_lo = e->persist_lo;
   p.snap_ev = e->snap_ev;
@@ -226,6 +261,7 @@ static WireParams wire_params(rg_engine* e) {
   w.pl = e->pl;
   w.hdr = p.hdr_in; w.mt = p.mt_in; w.cnt = p.cnt_in;
   w.info = e->info; w.pay = e->pay;
+  w.slabs = e->slabs; w.slab_info = e->slab_info; w.nslab = e->c.num_slabs;
   w.umap = e->umap; w.ubeg = e->ubeg; w.U = e->U;
   w.usize = e->usize; w.uoff = e->uoff; w.bsum = e->bsum;
   w.rmap = e->rmap; w.rbeg = e->rbeg; w.RU = e->RU;
@@ -253,6 +289,7 @@ static AdminParams admin(rg_engine* e) {
   a.info = e->info;
   a.pay = e->pay;
   a.crc_err = e->crc_err;
+  a.zi = e->crc_tab + CRC_ZI_OFF;
   return a;
 }
 
@@ -310,6 +347,17 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   }
   if (rc == RG_OK) rc = dalloc(e, &e->crc_err, n * 4);
   if (rc == RG_OK) rc = dalloc(e, &e->slabs, (uint64_t)c.num_slabs * e->slab_rows * E * P);
+  if (rc == RG_OK) rc = dalloc(e, &e->slab_info, (uint64_t)c.num_slabs * e->slab_rows * E * sizeof(uint2));
+  if (rc == RG_OK) rc = dalloc(e, &e->d_prop_hmask, G * N * 8);
+  if (rc == RG_OK && (hipHostMalloc((void**)&e->h_pt, G * N, 0) != hipSuccess ||
+                      hipHostMalloc((void**)&e->h_pc, G * N * 4, 0) != hipSuccess ||
+                      hipHostMalloc((void**)&e->h_hm, G * N * 8, 0) != hipSuccess))
+    rc = fail(RG_ENOMEM, "hipHostMalloc (proposal tables)");
+  if (rc == RG_OK) {
+    memset(e->h_pt, 0xFF, G * N);
+    memset(e->h_pc, 0, G * N * 4);
+    memset(e->h_hm, 0, G * N * 8);
+  }
   if (rc == RG_OK) rc = dalloc(e, &e->crc_tab, CRC_TAB_WORDS * 4);
   // tick inputs are indexed by global group / replica: ranks × the local sizes
   if (rc == RG_OK) rc = dalloc(e, &e->d_prop_target, G * N);
@@ -396,6 +444,11 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
       return fail(RG_EHIP, "hipEventCreate");
     }
   }
+  if (hipEventCreateWithFlags(&e->stg_ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&e->prop_ev, hipEventDisableTiming) != hipSuccess) {
+    rg_destroy(e);
+    return fail(RG_EHIP, "hipEventCreate");
+  }
   e->stream = e->own;
   std::vector<uint32_t> tab;
   build_crc(e, tab);
@@ -433,8 +486,12 @@ void rg_destroy(rg_engine* e) {
     if (e->ctl_done[b]) (void)hipEventDestroy(e->ctl_done[b]);
     if (e->bulk_done[b]) (void)hipEventDestroy(e->bulk_done[b]);
   }
+  if (e->stg_ev) (void)hipEventDestroy(e->stg_ev);
+  if (e->prop_ev) (void)hipEventDestroy(e->prop_ev);
   for (void* p : e->allocs) (void)hipFree(p);
   if (e->h_bounds) (void)hipHostFree(e->h_bounds);
+  for (void* h : {(void*)e->h_pt, (void*)e->h_pc, (void*)e->h_hm, (void*)e->h_cmd})
+    if (h) (void)hipHostFree(h);
   delete e;
 }
 
@@ -519,6 +576,14 @@ int rg_bootstrap(rg_engine* e) {
   HIPCHK(hipMemsetAsync(e->snap_ev, 0, (uint64_t)e->nrep * 8, e->stream));
   e->planned = e->wire_ready = false;
   e->recv = nullptr;
+  RGCHK(stage_reset(e));
+  for (uint64_t gi : e->touched) {
+    e->h_pt[gi] = 0xFF;
+    e->h_pc[gi] = 0;
+    e->h_hm[gi] = 0;
+  }
+  e->touched.clear();
+  e->staged = false;
   HIPCHK(hipMemsetAsync(e->crc_err, 0, (uint64_t)e->nrep * 4, e->stream));
   TickParams p = params(e);
   p.s64_out = e->s64[0];
@@ -534,9 +599,120 @@ int rg_bootstrap(rg_engine* e) {
 int rg_fill_slabs(rg_engine* e) {
   if (!e) return fail(RG_EINVAL, "null engine");
   if (int jrc = join(e)) return jrc;
-  HIPCHK(launch_fill_slabs(e->slabs, e->c.num_slabs, e->c.groups, e->slab_rows, e->c.max_entries_per_msg,
-                           e->c.payload_bytes, e->c.seed, e->pl, e->stream));
+  HIPCHK(launch_fill_slabs(e->slabs, e->slab_info, e->c.num_slabs, e->c.groups, e->slab_rows,
+                           e->c.max_entries_per_msg, e->c.payload_bytes, e->c.seed, e->pl, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
+  e->slabs_synthetic = true;
+  return RG_OK;
+}
+
+// The host proposal tables still hold the batches the last tick uploaded: once that upload has
+// completed, put the touched rows back to "no proposal".
+static int stage_reset(rg_engine* e) {
+  if (!e->stg_reset_pending) return RG_OK;
+  HIPCHK(hipEventSynchronize(e->stg_ev));
+  for (uint64_t gi : e->touched) {
+    e->h_pt[gi] = 0xFF;
+    e->h_pc[gi] = 0;
+    e->h_hm[gi] = 0;
+  }
+  e->touched.clear();
+  e->stg_reset_pending = false;
+  return RG_OK;
+}
+
+int rg_propose(rg_engine* e, const rg_proposal* props, size_t n, const uint8_t* payload, const uint32_t* lens) {
+  if (!e || (n && !props)) return fail(RG_EINVAL, "rg_propose args");
+  RGCHK(stage_reset(e));
+  const uint32_t N = e->pl.N, R = e->c.replicas, E = e->c.max_entries_per_msg, P = e->c.payload_bytes;
+  const uint64_t g0 = (uint64_t)N * e->pl.col_base, gn = (uint64_t)N * e->c.groups;
+  // validate every batch against the tables plus this call's earlier batches (all or nothing)
+  std::unordered_map<uint64_t, std::pair<uint32_t, uint32_t>> add;  // input index -> (slot, count)
+  uint64_t nent = 0, nbytes = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const rg_proposal& b = props[i];
+    if (b.group < g0 || b.group >= g0 + gn || b.slot >= R || b.count < 1 || b.count > E)
+      return fail(RG_EINVAL, "rg_propose: batch " + std::to_string(i) + ": bad shard, slot or count");
+    if (pl_rank_of(e->pl, b.group, b.slot) != e->pl.rank)
+      return fail(RG_EINVAL, "rg_propose: batch " + std::to_string(i) + ": that replica is hosted by another rank");
+    const uint64_t gi = b.group - g0;
+    auto it = add.find(gi);
+    const uint32_t have = e->h_pc[gi] + (it == add.end() ? 0u : it->second.second);
+    const uint32_t slot = it != add.end() ? it->second.first : e->h_pc[gi] ? e->h_pt[gi] : b.slot;
+    if (have && slot != b.slot) return fail(RG_EFULL, "rg_propose: a second slot of one shard in one tick");
+    if (have + b.count > E) return fail(RG_EFULL, "rg_propose: batch larger than max_entries_per_msg");
+    add[gi] = {b.slot, have - e->h_pc[gi] + b.count};
+    nent = std::max<uint64_t>(nent, b.first + b.count);
+  }
+  if (nent && !lens) return fail(RG_EINVAL, "rg_propose: null lens");
+  for (uint64_t j = 0; j < nent; ++j) {
+    if (lens[j] > P) return fail(RG_EINVAL, "rg_propose: Cmd longer than payload_bytes");
+    nbytes += lens[j];
+  }
+  if (nbytes && !payload) return fail(RG_EINVAL, "rg_propose: null payload");
+  // stage: pinned [Cmd bytes | off u64 | dst u64 | len u32] for the entries of the batches
+  uint64_t nstage = 0;
+  for (size_t i = 0; i < n; ++i) nstage += props[i].count;
+  const uint64_t cb = (nbytes + 15) & ~15ull, need = cb + nstage * 20 + 64;
+  if (P && nstage) {
+    HIPCHK(hipEventSynchronize(e->prop_ev));  // the last H2D out of h_cmd has completed
+    if (need > e->h_cmd_cap) {
+      if (e->h_cmd) (void)hipHostFree(e->h_cmd);
+      e->h_cmd = nullptr;
+      e->h_cmd_cap = 0;
+      if (hipHostMalloc((void**)&e->h_cmd, need * 3 / 2, 0) != hipSuccess) return fail(RG_ENOMEM, "hipHostMalloc");
+      e->h_cmd_cap = need * 3 / 2;
+    }
+    if (need > e->d_cmd_cap) {
+      HIPCHK(hipStreamSynchronize(e->stream));  // the last stage kernel read the old buffer
+      if (e->d_cmd) {
+        (void)hipFree(e->d_cmd);
+        e->allocs.erase(std::remove(e->allocs.begin(), e->allocs.end(), (void*)e->d_cmd), e->allocs.end());
+        e->bytes -= e->d_cmd_cap;
+        e->d_cmd = nullptr;
+      }
+      e->d_cmd_cap = 0;
+      RGCHK(dalloc(e, &e->d_cmd, need * 3 / 2));
+      e->d_cmd_cap = need * 3 / 2;
+    }
+    if (nbytes) memcpy(e->h_cmd, payload, nbytes);
+  }
+  std::vector<uint64_t> boff(nent + 1, 0);
+  for (uint64_t j = 0; j < nent; ++j) boff[j + 1] = boff[j] + lens[j];
+  uint64_t* off = (uint64_t*)(e->h_cmd + cb);
+  uint64_t* dst = off + nstage;
+  uint32_t* len = (uint32_t*)(dst + nstage);
+  const uint64_t slab = e->t % e->c.num_slabs, rows = e->slab_rows;
+  uint64_t k = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const rg_proposal& b = props[i];
+    const uint64_t gi = b.group - g0;
+    const uint32_t j = (uint32_t)(b.group / N - e->pl.col_base);
+    const uint64_t row = e->wire ? (uint64_t)b.slot * e->c.groups + j : j;
+    for (uint32_t x = 0; x < b.count; ++x) {
+      const uint32_t at = e->h_pc[gi] + x;  // position in the shard's batch
+      if (lens[b.first + x] && P) e->h_hm[gi] |= 1ull << at;
+      if (P) {
+        off[k] = boff[b.first + x];
+        dst[k] = (slab * rows + row) * E + at;
+        len[k] = lens[b.first + x];
+        ++k;
+      }
+    }
+    if (!e->h_pc[gi]) e->touched.push_back(gi);
+    e->h_pt[gi] = (uint8_t)b.slot;
+    e->h_pc[gi] += b.count;
+  }
+  if (P && k) {
+    uint8_t* d = e->d_cmd;
+    HIPCHK(hipMemcpyAsync(d, e->h_cmd, cb + k * 20, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipEventRecord(e->prop_ev, e->stream));
+    LAUNCH(launch_stage_cmds(e->slabs, e->slab_info, P, d, (const uint64_t*)(d + cb), (const uint64_t*)(d + cb) + k,
+                             (const uint32_t*)((const uint64_t*)(d + cb) + 2 * k), k, e->stream),
+           e->stream, "stage_cmds");
+    e->slabs_synthetic = false;
+  }
+  if (n) e->staged = true;
   return RG_OK;
 }
 
@@ -595,6 +771,9 @@ static int tick_impl(rg_engine* e, const rg_tick_input* in, bool device_ptrs) {
   if (e->wire && e->t > 0 && !e->wire_ready)
     return fail(RG_EINVAL, "rg_tick: the last tick's messages were not exchanged (rg_wire_plan/pack/recv)");
   TickParams p = params(e);
+  if (e->staged && in && in->prop_target)
+    return fail(RG_EINVAL, "rg_tick: proposals staged by rg_propose and tick-input proposals in one tick");
+  if (in && in->prop_target && !e->slabs_synthetic && e->c.payload_bytes) RGCHK(rg_fill_slabs(e));
   if (in) {
     p.flags = in->flags;
     if (device_ptrs) {
@@ -623,6 +802,18 @@ static int tick_impl(rg_engine* e, const rg_tick_input* in, bool device_ptrs) {
         p.isolate = e->d_isolate;
       }
     }
+  }
+  if (e->staged) {  // rg_propose's batches: upload the tables (pinned; reset once the copy completed)
+    const uint64_t GN = (uint64_t)e->c.groups * e->pl.N;
+    HIPCHK(hipMemcpyAsync(e->d_prop_target, e->h_pt, GN, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipMemcpyAsync(e->d_prop_count, e->h_pc, GN * 4, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipMemcpyAsync(e->d_prop_hmask, e->h_hm, GN * 8, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipEventRecord(e->stg_ev, e->stream));
+    p.prop_target = e->d_prop_target;
+    p.prop_count = e->d_prop_count;
+    p.prop_hmask = e->d_prop_hmask;
+    e->staged = false;
+    e->stg_reset_pending = true;
   }
   // control(t) on the engine stream once bulk(t-2) released jobs[t&1]; bulk(t) on the bulk
   // stream after control(t). control(t+1) then overlaps bulk(t): they touch disjoint data.
@@ -714,21 +905,28 @@ int rg_read_entries(rg_engine* e, uint32_t rid, uint64_t first, uint32_t n, rg_e
 }
 
 int rg_import_replica(rg_engine* e, uint32_t rid, const rg_replica_view* v, const uint64_t* terms,
-                      const uint32_t* types, const uint8_t* payloads) {
+                      const uint32_t* types, const uint8_t* payloads, const uint32_t* lens) {
   if (!e || !v || rid >= e->nrep) return fail(RG_EINVAL, "rg_import_replica args");
   if (int jrc = join(e)) return jrc;
   const uint64_t L = e->c.log_capacity, P = e->c.payload_bytes;
   if (v->last < v->marker || v->last - v->marker > L) return fail(RG_EINVAL, "log longer than the ring");
   const uint32_t nent = (uint32_t)(v->last - v->marker);
+  if (nent && !terms) return fail(RG_EINVAL, "rg_import_replica: null terms");
   std::vector<uint64_t> words(nent);
   std::vector<uint32_t> crcs(nent, 0);
+  std::vector<uint8_t> rows(payloads ? (uint64_t)nent * P : 0, 0);  // Cmds zero-padded to P bytes
   for (uint32_t k = 0; k < nent; ++k) {
     const uint32_t type = types ? (types[k] & 0xFFu) : RG_ENTRY_APPLICATION;
-    const bool hp = payloads && P && type == RG_ENTRY_APPLICATION && !(types && (types[k] & RG_ENTRY_EMPTY));
-    words[k] = (terms[k] & TERM_MASK) | (type ? TYPE_BIT : 0) | (hp ? PAY_BIT : 0);
-    if (hp) crcs[k] = host_crc(e, payloads + (uint64_t)k * P, P);
+    const uint32_t len = lens ? lens[k] : (uint32_t)P;
+    if (len > P) return fail(RG_EINVAL, "rg_import_replica: Cmd longer than payload_bytes");
+    const bool hp = payloads && P && len && type == RG_ENTRY_APPLICATION && !(types && (types[k] & RG_ENTRY_EMPTY));
+    words[k] = (terms[k] & TERM_MASK) | (type ? TYPE_BIT : 0) | (hp ? len_bits(len) : 0);
+    if (hp) {
+      memcpy(rows.data() + (uint64_t)k * P, payloads + (uint64_t)k * P, len);
+      crcs[k] = host_crc(e, rows.data() + (uint64_t)k * P, P);  // the slot CRC
+    }
   }
-  const uint64_t vb = 512, wb = (uint64_t)nent * 8, cb = (uint64_t)nent * 4, pb = payloads ? (uint64_t)nent * P : 0;
+  const uint64_t vb = 512, wb = (uint64_t)nent * 8, cb = (uint64_t)nent * 4, pb = rows.size();
   int rc = stage_reserve(e, vb + wb + cb + pb + 64);
   if (rc) return rc;
   uint8_t* d = e->stage;
@@ -736,7 +934,7 @@ int rg_import_replica(rg_engine* e, uint32_t rid, const rg_replica_view* v, cons
   HIPCHK(hipMemcpy(d, v, sizeof *v, hipMemcpyHostToDevice));
   if (wb) HIPCHK(hipMemcpy(d + vb, words.data(), wb, hipMemcpyHostToDevice));
   if (cb) HIPCHK(hipMemcpy(d + vb + wb, crcs.data(), cb, hipMemcpyHostToDevice));
-  if (pb) HIPCHK(hipMemcpy(d + vb + wb + cb, payloads, pb, hipMemcpyHostToDevice));
+  if (pb) HIPCHK(hipMemcpy(d + vb + wb + cb, rows.data(), pb, hipMemcpyHostToDevice));
   HIPCHK(launch_scatter_replica(admin(e), rid, d, (const uint64_t*)(d + vb), pb ? d + vb + wb + cb : nullptr,
                                 (const uint32_t*)(d + vb + wb), nent, e->stream, e->info, e->pay));
   HIPCHK(hipMemsetAsync(e->snap_ev + rid, 0, 8, e->stream));  // no snapshot events until it steps
@@ -823,7 +1021,7 @@ int rg_persist_collect(rg_engine* e, int full, rg_persist_state* states, uint64_
   a.G = t.G; a.R = t.R; a.nrep = t.nrep; a.L = t.L; a.P = t.P; a.pl = e->pl;
   a.full = (full || e->t == 0) ? 1u : 0u;  // before the first tick there is no previous state
   a.s64 = t.s64_in; a.s64_prev = t.s64_out; a.persist_lo = e->persist_lo;
-  a.tr = e->tr; a.info = e->info; a.pay = e->pay;
+  a.tr = e->tr; a.info = e->info; a.pay = e->pay; a.zi = e->crc_tab + CRC_ZI_OFF;
   a.scnt = e->pscnt; a.ecnt = e->pecnt; a.soff = e->psoff; a.eoff = e->peoff; a.bsum = e->absum;
   LAUNCH(launch_persist_count(a, (uint64_t*)e->d_sum, e->stream), e->stream, "persist count");
   uint64_t tot[2] = {0, 0};
@@ -855,6 +1053,7 @@ int rg_apply_committed(rg_engine* e, uint32_t slot_mask, rg_apply_entry* entries
   ApplyParams a{};
   a.G = t.G; a.R = t.R; a.nrep = t.nrep; a.L = t.L; a.P = t.P; a.slot_mask = slot_mask; a.pl = e->pl;
   a.s64 = t.s64_in; a.apply_lo = e->apply_lo; a.tr = e->tr; a.info = e->info; a.pay = e->pay;
+  a.zi = e->crc_tab + CRC_ZI_OFF;
   a.cnt = e->acnt; a.off = e->aoff; a.bsum = e->absum;
   LAUNCH(launch_apply_count(a, (uint64_t*)e->d_sum, e->stream), e->stream, "apply count");
   uint64_t total = 0;

@@ -14,11 +14,16 @@
 namespace rg {
 
 constexpr uint32_t MAX_R = 8;
-// term-ring / inline-term word: term | type<<61 | has_payload<<62 | bank<<63
+// term-ring / inline-term word: term | cmd_len<<48 | type<<61 | has_payload<<62 | bank<<63
+// (terms < 2^48; cmd_len = the entry's Cmd bytes, 0..payload_bytes; has_payload ⇔ an application
+// entry with cmd_len > 0)
 constexpr uint64_t BANK_BIT = 1ull << 63;
 constexpr uint64_t PAY_BIT = 1ull << 62;
 constexpr uint64_t TYPE_BIT = 1ull << 61;
-constexpr uint64_t TERM_MASK = TYPE_BIT - 1;
+constexpr uint32_t LEN_SHIFT = 48;
+constexpr uint64_t TERM_MASK = (1ull << LEN_SHIFT) - 1;
+RG_HD_INLINE uint32_t word_len(uint64_t w) { return (uint32_t)(w >> LEN_SHIFT) & 0x1FFFu; }
+RG_HD_INLINE uint64_t len_bits(uint32_t len) { return ((uint64_t)len << LEN_SHIFT) | (len ? PAY_BIT : 0ull); }
 
 enum : uint32_t {
   M_LOCAL_TICK = 0, M_ELECTION = 1, M_LEADER_HEARTBEAT = 2, M_NOOP = 4, M_PROPOSE = 7,
@@ -49,10 +54,18 @@ enum : uint32_t {
 // job rows
 enum : uint32_t { J_FIRST, J_DMASK, J_SMASK, J_HMASK, J_TMASK, J64_ROWS };
 enum : uint32_t { J_META, J_SRC, J32_ROWS };  // meta = n | e0<<8 | kind<<16
-enum : uint32_t { SRC_NONE = 0, SRC_RING = 1, SRC_SLAB = 2, SRC_WIRE = 3 };
+// SRC_WIRE_PROP: a proposal forwarded from another rank — its Cmds in the receive buffer like
+// SRC_WIRE's entries, but with no sender CRC to verify
+enum : uint32_t { SRC_NONE = 0, SRC_RING = 1, SRC_SLAB = 2, SRC_WIRE = 3, SRC_WIRE_PROP = 4 };
+// SRC_RING job: J_SRC = the sender's replica q, J_SMASK = per-entry source bank bits.
+// SRC_SLAB job (a proposal): J_SRC = slab id | row slot << 16: the Cmds are in slab row = column
+// (one rank) or row slot · G + column (wire engines: the proposing replica's row).
 // SRC_WIRE job: the entries arrived over the wire (another rank's replica). J_SMASK holds the byte
 // offset of the message's first entry record in the receive buffer and J_SRC the message's entry
-// count n; record e = {u64 term word, u32 crc, u32 0} at +16e, payload e at +16n + P·e.
+// count n; record e = {u64 term word, u32 crc, u32 len} at +16e, payload e at +16n + P·e.
+// Entry Cmds are variable-length, len in [0, P] (in the term word): a payload slot holds the Cmd
+// zero-padded to P bytes, and its info word {crc, type << 24 | slot bytes} carries the CRC-32 of
+// the whole padded slot ("slot CRC"; equal to the Cmd's CRC when len = P). crc_of_cmd converts.
 
 // ---- placement across ranks. Replica slot s of global group g lives on rank
 // (g mod N + off_c(s)) mod N, local column j = g div N, column class c = j mod (N − 1), with
@@ -107,6 +120,7 @@ RG_HD_INLINE uint32_t pl_rank_of(const Placement& pl, uint64_t g, uint32_t s) {
 struct TickParams {
   uint32_t G, R, nrep, L, P, E, K, nslab, J;
   uint32_t ET, HT, CQ, SE, CO, drop_ppm, flags;
+  uint32_t wire;           // wire engine: slab rows per replica (q), else per column (g)
   uint64_t seed, tick;
   Placement pl;
   const uint64_t* s64_in;  // [S64_ROWS][nrep]
@@ -138,6 +152,8 @@ struct TickParams {
   uint32_t* jcnt;          // [nrep]
   const uint8_t* prop_target;
   const uint32_t* prop_count;
+  const uint64_t* prop_hmask;  // caller proposals: entries with a non-empty Cmd (NULL: synthetic, all of len P)
+  const uint2* slab_info;      // [nslab][rows][E] {0, Cmd length} of the proposal slabs
   const uint8_t* campaign;
   const uint8_t* isolate;
 };
@@ -165,18 +181,45 @@ struct BulkParams {
 //   N  [16][2][16] the same split into nibbles (lo, hi) — conflict-free 16-word LDS tables
 //   SH [NCH][8][16] (row stride CRC_SH_STRIDE) per-lane shift: SH[c][j][n] = raw CRC of nibble n
 //      at bit 4j of a 32-bit CRC state followed by 16·(NCH−1−c) zero bytes, NCH = P/16
+//   ZI [10][8][16] (global memory only, after SH) inverse shifts: ZI[b][j][n] = nibble n at bit 4j of
+//      a raw state moved back through 2^b zero bytes (Z^-(2^b)); crc_of_cmd uses them
 constexpr uint32_t CRC_T_WORDS = 16 * 256;
 constexpr uint32_t CRC_N_WORDS = 16 * 2 * 16;
 constexpr uint32_t CRC_SH_STRIDE = 8 * 16 + 2;  // +2 words: lanes' tables start on different banks
 constexpr uint32_t CRC_SH_MAX_WORDS = 64 * CRC_SH_STRIDE;
-constexpr uint32_t CRC_TAB_WORDS = CRC_T_WORDS + CRC_N_WORDS + CRC_SH_MAX_WORDS;
+constexpr uint32_t CRC_ZI_BITS = 10;  // P − len < 1024
+constexpr uint32_t CRC_ZI_WORDS = CRC_ZI_BITS * 8 * 16;
+constexpr uint32_t CRC_ZI_OFF = CRC_T_WORDS + CRC_N_WORDS + CRC_SH_MAX_WORDS;
+constexpr uint32_t CRC_TAB_WORDS = CRC_ZI_OFF + CRC_ZI_WORDS;
+
+// CRC-32 of a Cmd of len bytes from its slot CRC (the CRC of the Cmd zero-padded to P bytes):
+// slot = crc_const ^ raw(slot), raw(slot) = Z^(P−len) raw(Cmd), so
+// crc(Cmd) = Z^-(P−len)(slot ^ ~0) ^ ~0 (init / xorout ~0; Z = one zero byte, invertible).
+RG_HD_INLINE uint32_t crc_of_cmd(uint32_t slot_crc, uint32_t len, uint32_t P, const uint32_t* zi) {
+  if (!len) return 0;
+  if (len >= P) return slot_crc;
+  uint32_t v = slot_crc ^ 0xFFFFFFFFu;
+  const uint32_t k = P - len;
+  for (uint32_t b = 0; b < CRC_ZI_BITS; ++b) {
+    if ((k >> b) & 1u) {
+      uint32_t r = 0;
+      for (uint32_t j = 0; j < 8; ++j) r ^= zi[(b * 8 + j) * 16 + ((v >> (4 * j)) & 0xF)];
+      v = r;
+    }
+  }
+  return v ^ 0xFFFFFFFFu;
+}
 
 // host-side launchers (raftgpu_kernels.hip)
 hipError_t launch_control(const TickParams& p, hipStream_t s);
 hipError_t launch_bulk(const BulkParams& p, hipStream_t s, int grid);
 hipError_t launch_bootstrap(const TickParams& p, uint2* info, hipStream_t s);
-hipError_t launch_fill_slabs(uint8_t* slabs, uint32_t nslab, uint32_t G, uint32_t rows, uint32_t E, uint32_t P,
-                             uint64_t seed, const Placement& pl, hipStream_t s);
+hipError_t launch_fill_slabs(uint8_t* slabs, uint2* slab_info, uint32_t nslab, uint32_t G, uint32_t rows, uint32_t E,
+                             uint32_t P, uint64_t seed, const Placement& pl, hipStream_t s);
+// caller proposals (rg_propose): Cmd e of the batch is copied from src + off[e] (len[e] bytes, zero-padded
+// to P) into slab entry dst[e] = (slab · rows + row) · E + k, and slab_info[dst[e]] = {0, len[e]}
+hipError_t launch_stage_cmds(uint8_t* slabs, uint2* slab_info, uint32_t P, const uint8_t* src, const uint64_t* off,
+                             const uint64_t* dst, const uint32_t* len, uint64_t n, hipStream_t s);
 hipError_t launch_probe_copy(const void* src, void* dst, uint64_t bytes, hipStream_t s);
 hipError_t launch_sum_committed(const TickParams& p, unsigned long long* out, hipStream_t s);
 hipError_t launch_traffic(const TickParams& p, unsigned long long* out6, hipStream_t s);
@@ -191,6 +234,7 @@ struct ApplyParams {
   const uint64_t* tr;
   const uint2* info;
   const uint8_t* pay;
+  const uint32_t* zi;       // CRC inverse-shift tables (crc_of_cmd)
   uint32_t* cnt;            // [nrep] entries per replica
   uint64_t* off;            // [nrep + 1] exclusive scan
   uint64_t* bsum;           // scan scratch
@@ -224,6 +268,7 @@ struct PersistParams {
   const uint64_t* tr;
   const uint2* info;
   const uint8_t* pay;
+  const uint32_t* zi;
   uint32_t* scnt;            // [nrep] 1 if the replica has a record
   uint32_t* ecnt;            // [nrep] entries to save
   uint64_t* soff;            // [nrep + 1]
@@ -245,6 +290,7 @@ struct AdminParams {
   const uint2* info;
   const uint8_t* pay;
   const uint32_t* crc_err;
+  const uint32_t* zi;
 };
 hipError_t launch_gather_replicas(const AdminParams& a, uint32_t first_rid, uint32_t n, void* out_views,
                                   hipStream_t s);

@@ -17,6 +17,8 @@
 //   check the result against the sender's stored CRC. Payloads are read straight from the
 //   sender's ring (no staging copy); DESIGN.md §2 explains the two payload banks that keep the
 //   same-launch reads and rewrites disjoint.
+#include <algorithm>
+
 #include "raftgpu_control.h"
 
 namespace rg {
@@ -182,11 +184,13 @@ __device__ __forceinline__ void load_tile(const BulkParams& p, Cursor& cur, Tile
 template <bool WIRE>
 __device__ __forceinline__ void set_job(const BulkParams& p, Cursor& cur, const Job& jb) {
   cur.first = jb.first; cur.dm = jb.dm; cur.sm = jb.sm; cur.hm = jb.hm; cur.tm = jb.tm;
-  cur.n = jb.meta & 0xFF; cur.b = (jb.meta >> 8) & 0xFF; cur.kind = jb.meta >> 16; cur.src = jb.src;
-  cur.g = WIRE ? cur.q : cur.q % p.G;  // proposal slab row: per replica across ranks, per group on one
+  cur.n = jb.meta & 0xFF; cur.b = (jb.meta >> 8) & 0xFF; cur.kind = (jb.meta >> 16) & 0xF; cur.src = jb.src;
+  cur.g = WIRE ? (cur.src >> 16) * p.G + cur.q % p.G : cur.q % p.G;  // SRC_SLAB: the proposal's slab row
+  cur.src &= cur.kind == SRC_SLAB ? 0xFFFFu : 0xFFFFFFFFu;
 #ifdef RG_BOUNDS
   const bool bad = cur.n > 64 || cur.b > cur.n || (cur.kind == SRC_RING && cur.src >= p.nrep) ||
-                   (cur.kind == SRC_SLAB && cur.src >= p.nslab) || cur.kind > SRC_WIRE ||
+                   (cur.kind == SRC_SLAB && (cur.src >= p.nslab || cur.g >= (WIRE ? p.nrep : p.G))) ||
+                   cur.kind > SRC_WIRE_PROP ||
                    (cur.kind == SRC_WIRE && (!WIRE || cur.n > cur.src ||
                                              cur.sm + (16ull + p.P) * cur.src > p.wire_bytes));
   if (bad) {
@@ -281,7 +285,7 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p) {
   cur.n = 0;
   cur.live = next_job<WIRE>(p, cur, tj, stride, ntiles);
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  // ring slot u: payload chunk, destination (slot | bank << 31), flags, sender's CRC
+  // ring slot u: payload chunk, destination (slot | bank << 31), flags, sender's slot CRC
   u32x4 x[BULK_U];
   uint32_t ds[BULK_U], fl[BULK_U], want[BULK_U];
 #pragma unroll
@@ -302,7 +306,9 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p) {
     const uint64_t cbase = (uint64_t)cq * L;
 #pragma unroll
     for (int u = 0; u < BULK_U; ++u) {
-      {  // consume slot u: store, CRC, info, verify (fl = 0 for an empty slot: no stores)
+      {  // consume slot u: store, CRC, info, verify (fl = 0 for an empty slot: no stores). A payload
+        // slot holds the Cmd zero-padded to P bytes (every writer copies whole slots), so the CRC is
+        // the slot CRC; the Cmd's length lives in the term word, not here.
         const bool act = fl[u] & F_ACT;
         const uint64_t di = (uint64_t)(ds[u] >> 31) * n64 * L + cbase + (ds[u] & 0x7FFFFFFFu);
         if (act) {
@@ -316,7 +322,7 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p) {
 #ifndef RG_BULK_NOCRC
         v = crc.raw16(make_uint4(x[u].x, x[u].y, x[u].z, x[u].w));
 #endif
-        if constexpr (LG > 0) v = xor_lanes<LG>(crc.shift(v));  // raw(entry) = XOR_c Z^(after c)(raw c)
+        if constexpr (LG > 0) v = xor_lanes<LG>(crc.shift(v));  // raw(slot) = XOR_c Z^(after c)(raw c)
         if (fl[u] & F_WRITER) {
           const uint32_t cr = act ? (p.crc_const ^ v) : 0u;
           const uint32_t tl = ((fl[u] & F_TYPE) ? (1u << 24) : 0u) | (act ? P : 0u);
@@ -331,13 +337,13 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p) {
         const bool act = valid && ((cur.hm >> e) & 1ull);
         const uint32_t slot = (uint32_t)((cur.first + e) & (L - 1));
         const uint32_t db = valid ? (uint32_t)(cur.dm >> e) & 1u : 0u;
-        const bool ring = cur.kind == SRC_RING, wire = WIRE && cur.kind == SRC_WIRE;
+        const bool ring = cur.kind == SRC_RING, wire = WIRE && (cur.kind == SRC_WIRE || cur.kind == SRC_WIRE_PROP);
         ds[u] = slot | (db << 31);
         fl[u] = (act ? F_ACT : 0u) | ((valid && c == 0) ? F_WRITER : 0u) | (((cur.tm >> e) & 1ull) ? F_TYPE : 0u) |
-                (((ring || wire) && act) ? F_CHECK : 0u);
+                (((ring || (WIRE && cur.kind == SRC_WIRE)) && act) ? F_CHECK : 0u);
         const uint64_t sb = (cur.sm >> e) & 1ull;
         const uint64_t si = (sb * n64 + cur.src) * L + slot;
-        // wire: records {term word, crc} at sm + 16e, payloads at sm + 16n + P·e (n = src)
+        // wire: records {term word, slot crc, 0} at sm + 16e, payloads at sm + 16n + P·e (n = src)
         const uint8_t* sp = ring   ? p.pay + si * P
                             : wire ? p.wire + cur.sm + 16ull * cur.src + (uint64_t)P * e
                                    : p.slabs + (((uint64_t)cur.src * rows + cur.g) * p.E + e) * P;
@@ -440,8 +446,8 @@ hipError_t launch_bootstrap(const TickParams& p, uint2* info, hipStream_t s) {
 // row r of a slab holds the batch of global group pl_group(s, j): r = j (one rank, rows = G) or
 // r = q = s·G + j (rows = nrep: each rank's replica of a group reads its own row, so a forwarded
 // proposal finds the same bytes on the leader's rank)
-__global__ void fill_slabs_kernel(uint8_t* slabs, uint32_t nslab, uint32_t G, uint32_t rows, uint32_t E, uint32_t P,
-                                  uint64_t seed, Placement pl) {
+__global__ void fill_slabs_kernel(uint8_t* slabs, uint2* slab_info, uint32_t nslab, uint32_t G, uint32_t rows,
+                                  uint32_t E, uint32_t P, uint64_t seed, Placement pl) {
   const uint64_t wpe = P / 8;
   const uint64_t total = (uint64_t)nslab * rows * E * wpe;
   for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < total; w += (uint64_t)gridDim.x * blockDim.x) {
@@ -452,13 +458,46 @@ __global__ void fill_slabs_kernel(uint8_t* slabs, uint32_t nslab, uint32_t G, ui
     const uint64_t gg = pl_group(pl, r / G, r % G);
     const uint64_t key = mix64(((uint64_t)sl << 56) ^ (gg << 16) ^ (uint64_t)i ^ (seed * 0x9E3779B97F4A7C15ULL));
     reinterpret_cast<uint64_t*>(slabs)[w] = mix64(key + (wi + 1) * 0xD1B54A32D192ED03ULL);
+    if (wi == 0) slab_info[ent] = make_uint2(0u, P);  // a synthetic Cmd is P bytes
   }
 }
 
-hipError_t launch_fill_slabs(uint8_t* slabs, uint32_t nslab, uint32_t G, uint32_t rows, uint32_t E, uint32_t P,
-                             uint64_t seed, const Placement& pl, hipStream_t s) {
+hipError_t launch_fill_slabs(uint8_t* slabs, uint2* slab_info, uint32_t nslab, uint32_t G, uint32_t rows, uint32_t E,
+                             uint32_t P, uint64_t seed, const Placement& pl, hipStream_t s) {
   if (!P) return hipSuccess;
-  hipLaunchKernelGGL(fill_slabs_kernel, dim3(4096), dim3(256), 0, s, slabs, nslab, G, rows, E, P, seed, pl);
+  hipLaunchKernelGGL(fill_slabs_kernel, dim3(4096), dim3(256), 0, s, slabs, slab_info, nslab, G, rows, E, P, seed, pl);
+  return hipGetLastError();
+}
+
+// ================================================================== caller proposals (rg_propose)
+// One wave per Cmd: lane c writes bytes [16c, 16c + 16) of the Cmd's P-byte slab slot from the caller's
+// packed bytes (unaligned, read byte by byte: an H2D-staged batch, not the tick path), zero past len.
+__global__ void __launch_bounds__(256) stage_cmds_kernel(uint8_t* slabs, uint2* slab_info, uint32_t P,
+                                                         const uint8_t* src, const uint64_t* off, const uint64_t* dst,
+                                                         const uint32_t* len, uint64_t n) {
+  const uint32_t lane = __lane_id(), nch = P / 16;
+  for (uint64_t i = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < n;
+       i += (uint64_t)gridDim.x * (blockDim.x >> 6)) {
+    const uint64_t d = dst[i], o = off[i];
+    const uint32_t ln = len[i];
+    for (uint32_t c = lane; c < nch; c += 64) {
+      uint32_t w[4] = {0, 0, 0, 0};
+      for (uint32_t b = 0; b < 16; ++b) {
+        const uint32_t k = 16 * c + b;
+        if (k < ln) w[b >> 2] |= (uint32_t)src[o + k] << (8 * (b & 3));
+      }
+      *reinterpret_cast<uint4*>(slabs + d * P + 16ull * c) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    if (lane == 0) slab_info[d] = make_uint2(0u, ln);
+  }
+}
+
+hipError_t launch_stage_cmds(uint8_t* slabs, uint2* slab_info, uint32_t P, const uint8_t* src, const uint64_t* off,
+                             const uint64_t* dst, const uint32_t* len, uint64_t n, hipStream_t s) {
+  if (!n || !P) return hipSuccess;
+  const uint64_t blocks = std::min<uint64_t>((n + 3) / 4, 65536);
+  hipLaunchKernelGGL(stage_cmds_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, slabs, slab_info, P, src, off, dst,
+                     len, n);
   return hipGetLastError();
 }
 

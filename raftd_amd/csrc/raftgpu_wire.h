@@ -14,6 +14,9 @@ struct WireParams {
   const uint32_t* cnt;
   const uint2* info;
   const uint8_t* pay;
+  const uint8_t* slabs;     // proposal slabs [nslab][nrep][E][P]: a forwarded Propose ships its Cmds
+  const uint2* slab_info;   // [nslab][nrep][E] {0, len}
+  uint32_t nslab;
   const uint32_t* umap;  // [U] send units s<<28 | d<<24 | j, grouped by destination rank
   const uint32_t* ubeg;  // [N+1] first send unit of each destination
   uint32_t U;

@@ -9,9 +9,12 @@
 // Units are listed per destination rank in (s, d, j) order (host-built, identical on the sender
 // and the receiver). A region for one rank is
 //     [u64 table: (data offset in 16-B units) << 8 | message count, one per unit, padded to 256 B]
-//     [data: per message a 64-B header, then n 16-B entry records {term word, crc, 0}, then n
-//      payloads of P bytes — n = the Replicate's entry count, 0 for every other type]
-// so a follower's bulk job reads its payloads and sender CRCs straight out of the receive buffer.
+//     [data: per message a 64-B header, then n 16-B entry records {ring word, slot crc, 0}, then n
+//      payloads of P bytes — n = the entry count of a Replicate, or of a forwarded Propose when
+//      P > 0 (its Cmds: records {len bits, 0, 0}); 0 for every other type]
+// so a follower's (or a leader's, for a proposal) bulk job reads the payloads and sender CRCs
+// straight out of the receive buffer. A payload is the Cmd zero-padded to P bytes; the ring word
+// carries its length (raftgpu_internal.h).
 //
 // plan_kernel      thread per unit: bytes of its messages
 // scan_*           exclusive scan of the unit sizes (three passes)
@@ -31,10 +34,15 @@ __device__ __forceinline__ void unit_decode(uint32_t u, uint32_t& s, uint32_t& d
   j = u & 0xFFFFFF;
 }
 
+// entries a message carries on the wire: a Replicate's, and a forwarded Propose's Cmds (P > 0)
+__device__ __forceinline__ uint32_t wire_entries(uint64_t w0, uint32_t P) {
+  const uint32_t t = (uint32_t)(w0 & 0xFF);
+  return (t == M_REPLICATE || (t == M_PROPOSE && P)) ? (uint32_t)(w0 >> 32) : 0u;
+}
+
 // 16-B units of one message: header 4, each entry 1 record + P/16 payload
 __device__ __forceinline__ uint32_t msg_units(uint64_t w0, uint32_t P) {
-  const uint32_t n = ((w0 & 0xFF) == M_REPLICATE) ? (uint32_t)(w0 >> 32) : 0u;
-  return 4u + n * (1u + P / 16u);
+  return 4u + wire_entries(w0, P) * (1u + P / 16u);
 }
 
 __global__ void plan_kernel(WireParams w) {
@@ -168,29 +176,45 @@ __global__ void __launch_bounds__(256) pack_kernel(WireParams w) {
     const uint64_t* hp = w.hdr + (col * w.K + k) * w.G + j;
     const uint64_t hv = lane < 8 ? hp[lane * plane] : 0;
     if (lane < 8) reinterpret_cast<uint64_t*>(out)[lane] = hv;
-    const uint64_t w0 = rl64(hv, 0), li = rl64(hv, 3);
-    uint32_t n = ((w0 & 0xFF) == M_REPLICATE) ? (uint32_t)(w0 >> 32) : 0u;
+    const uint64_t w0 = rl64(hv, 0), li = rl64(hv, 3), w7 = rl64(hv, 7);
+    const bool prop = (w0 & 0xFF) == M_PROPOSE;
+    uint32_t n = wire_entries(w0, P);
     if (n > w.E) {  // plan_kernel sized the region with the same n: only reachable on corrupt state
       RG_OOB("RG_BOUNDS pack u=%u k=%u n=%u > E\n", u, k, n);
       n = 0;
     }
+    // a forwarded Propose: its Cmds are in this replica's row of slab w7 (the bytes its tick staged)
+    const uint32_t sl = (uint32_t)w7;
+    const bool slab_ok = prop && sl < w.nslab;
+    const uint64_t se0 = ((uint64_t)sl * n64 + qs) * w.E;
     const uint64_t* mtp = w.mt + ((col * w.K + k) * w.E) * w.G + j;
     if (lane < n) {
-      const uint64_t word = mtp[(uint64_t)lane * w.G];
-      const uint64_t slot = (li + 1 + lane) & (w.L - 1);
-      const uint32_t crc = (word & PAY_BIT) ? w.info[((word >> 63) * n64 + qs) * w.L + slot].x : 0u;
-      *reinterpret_cast<u32x4*>(out + 64 + 16 * lane) = u32x4{(uint32_t)word, (uint32_t)(word >> 32), crc, 0u};
+      u32x4 rec = u32x4{0u, 0u, 0u, 0u};
+      if (prop) {
+        const uint64_t word = len_bits(slab_ok ? min(w.slab_info[se0 + lane].y, P) : 0u);
+        rec = u32x4{(uint32_t)word, (uint32_t)(word >> 32), 0u, 0u};
+      } else {
+        const uint64_t word = mtp[(uint64_t)lane * w.G];
+        const uint64_t slot = (li + 1 + lane) & (w.L - 1);
+        const uint32_t crc = (word & PAY_BIT) ? w.info[((word >> 63) * n64 + qs) * w.L + slot].x : 0u;
+        rec = u32x4{(uint32_t)word, (uint32_t)(word >> 32), crc, 0u};
+      }
+      *reinterpret_cast<u32x4*>(out + 64 + 16 * lane) = rec;
     }
     if (P) {
       uint8_t* po = out + 64 + 16ull * n;
 #pragma unroll 4
       for (uint32_t t = lane; t < n * nch; t += 64) {
         const uint32_t e = t / nch, ch = t - e * nch;
-        const uint64_t word = mtp[(uint64_t)e * w.G];
-        if (word & PAY_BIT) {
-          const uint64_t slot = (li + 1 + e) & (w.L - 1);
-          const u32x4 v = __builtin_nontemporal_load(
-              reinterpret_cast<const u32x4*>(w.pay + (((word >> 63) * n64 + qs) * w.L + slot) * P + 16ull * ch));
+        const uint8_t* src = nullptr;
+        if (prop) {
+          if (slab_ok && w.slab_info[se0 + e].y) src = w.slabs + (se0 + e) * P;
+        } else {
+          const uint64_t word = mtp[(uint64_t)e * w.G];
+          if (word & PAY_BIT) src = w.pay + (((word >> 63) * n64 + qs) * w.L + ((li + 1 + e) & (w.L - 1))) * P;
+        }
+        if (src) {
+          const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + 16ull * ch));
           __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(po + 16ull * t));
         }
       }
@@ -227,16 +251,35 @@ __global__ void unpack_kernel(WireParams w) {
     }
     const uint64_t* h = reinterpret_cast<const uint64_t*>(in);
     const uint64_t w0 = h[0];
-    const uint32_t n = ((w0 & 0xFF) == M_REPLICATE) ? (uint32_t)(w0 >> 32) : 0u;
-    if (n > w.E || (uint64_t)(in - w.recv) + 64 + (uint64_t)n * (16 + w.P) > rend) {
-      RG_OOB("RG_BOUNDS unpack u=%u k=%u n=%u region end %llu\n", u, k, n, (unsigned long long)rend);
+    const uint32_t type = (uint32_t)(w0 & 0xFF), n = wire_entries(w0, w.P);
+    // exchange data comes from another process: keep a message only if this plane can carry it —
+    // a known type, from the unit's sender slot s to its destination slot d, at most E entries (a
+    // Propose 1..E), inside the region; the unit's messages from the first bad one on are dropped
+    const bool known = type == M_NOOP || type == M_PROPOSE || type == M_REPLICATE || type == M_REPLICATE_RESP ||
+                       type == M_REQUEST_VOTE || type == M_REQUEST_VOTE_RESP || type == M_INSTALL_SNAPSHOT ||
+                       type == M_HEARTBEAT || type == M_HEARTBEAT_RESP;
+    const uint32_t from = (uint32_t)(w0 >> 8) & 0xFF, to = (uint32_t)(w0 >> 16) & 0xFF, nent = (uint32_t)(w0 >> 32);
+    if (!known || from != s + 1 || to != d + 1 || n > w.E || (type == M_PROPOSE && (nent < 1 || nent > w.E)) ||
+        (uint64_t)(in - w.recv) + 64 + (uint64_t)n * (16 + w.P) > rend) {
+      RG_OOB("RG_BOUNDS unpack u=%u k=%u type=%u from=%u to=%u n=%u region end %llu\n", u, k, type, from, to, n,
+             (unsigned long long)rend);
+      break;
+    }
+    bool sane = true;  // every entry word: length <= P, payload bit exactly when the length is non-zero
+    for (uint32_t e = 0; e < n; ++e) {
+      const uint64_t rw = h[8 + 2 * e];
+      const uint32_t ln = word_len(rw);
+      sane = sane && ln <= w.P && ((rw & PAY_BIT) != 0) == (ln != 0);
+    }
+    if (!sane) {
+      RG_OOB("RG_BOUNDS unpack u=%u k=%u: entry word with a bad length\n", u, k);
       break;
     }
     uint64_t* ho = w.rhdr + (col * w.K + k) * w.G + j;
     for (int x = 0; x < 7; ++x) ho[x * plane] = h[x];
-    ho[7 * plane] = (w0 & 0xFF) == M_REPLICATE ? (uint64_t)(in + 64 - w.recv) : h[7];
-    uint64_t* mo = w.rmt + ((col * w.K + k) * w.E) * w.G + j;
-    for (uint32_t e = 0; e < n; ++e) mo[(uint64_t)e * w.G] = h[8 + 2 * e];
+    ho[7 * plane] = n ? (uint64_t)(in + 64 - w.recv) : h[7];  // entries: word 7 = their records' offset
+    uint64_t* mo = w.rmt + ((col * w.K + k) * w.E) * w.G + j;  // inline ring words (a Propose: length bits)
+    for (uint32_t e = 0; e < n; ++e) mo[(uint64_t)e * w.G] = h[8 + 2 * e] & (type == M_PROPOSE ? ~TERM_MASK & ~BANK_BIT & ~TYPE_BIT : ~0ull);
     in += 64 + (uint64_t)n * (16 + w.P);
   }
   w.rcnt[col * w.G + j] = k;

@@ -91,6 +91,25 @@ SNAPSHOT_EVENT_DTYPE = np.dtype([("group", "<u8"), ("replica_id", "<u4"), ("rid"
                                  ("_pad", "<u4"), ("restored", "<u8"), ("index", "<u8"), ("term", "<u8")])
 
 
+class Proposal(C.Structure):
+    _fields_ = [("group", C.c_uint64), ("slot", C.c_uint32), ("count", C.c_uint32), ("first", C.c_uint64)]
+
+
+def pack_proposals(batches):
+    """[(global group, slot, [Cmd bytes, ...]), ...] → (rg_proposal array, u32 lens, packed u8 Cmd
+    bytes): rg_propose's layout (Cmds back to back in lens order)."""
+    props = (Proposal * max(len(batches), 1))()
+    lens, chunks, first = [], [], 0
+    for i, (g, s, cmds) in enumerate(batches):
+        props[i].group, props[i].slot, props[i].count, props[i].first = g, s, len(cmds), first
+        for c in cmds:
+            lens.append(len(c))
+            chunks.append(bytes(c))
+        first += len(cmds)
+    blob = np.frombuffer(b"".join(chunks), dtype=np.uint8).copy() if chunks else np.zeros(0, np.uint8)
+    return props, np.array(lens, dtype=np.uint32), blob
+
+
 class TickInput(C.Structure):
     _fields_ = [("prop_target", C.c_void_p), ("prop_count", C.c_void_p), ("campaign", C.c_void_p),
                 ("isolate", C.c_void_p), ("flags", C.c_uint32), ("_pad", C.c_uint32)]
@@ -105,7 +124,7 @@ EXPORTS = ["rg_create", "rg_destroy", "rg_bootstrap", "rg_fill_slabs", "rg_tick"
            "rg_read_entries", "rg_import_replica", "rg_deliver", "rg_leader", "rg_sum_committed",
            "rg_device_bytes", "rg_last_error", "rg_last_tick_traffic", "rg_join",
            "rg_timing", "rg_kernel_ms", "rg_wire_plan", "rg_wire_pack", "rg_wire_recv", "rg_global_id",
-           "rg_apply_committed", "rg_probe_copy", "rg_persist_collect", "rg_snapshot_events"]
+           "rg_apply_committed", "rg_probe_copy", "rg_persist_collect", "rg_snapshot_events", "rg_propose"]
 
 _lib = None
 
@@ -145,7 +164,8 @@ def load_library(path: str = LIB_PATH):
         "rg_read_replicas": ([vp, u32, u32, C.POINTER(ReplicaView)], i32),
         "rg_read_msgs": ([vp, u32, u32, C.POINTER(MsgView), u32, C.POINTER(C.c_uint64)], i32),
         "rg_read_entries": ([vp, u32, u64, u32, C.POINTER(EntryView), vp], i32),
-        "rg_import_replica": ([vp, u32, C.POINTER(ReplicaView), vp, vp, vp], i32),
+        "rg_import_replica": ([vp, u32, C.POINTER(ReplicaView), vp, vp, vp, vp], i32),
+        "rg_propose": ([vp, C.POINTER(Proposal), C.c_size_t, vp, vp], i32),
         "rg_deliver": ([vp, u32, C.POINTER(MsgView)], i32),
         "rg_leader": ([vp, u32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_int)], i32),
         "rg_sum_committed": ([vp, C.POINTER(C.c_uint64)], i32),
@@ -162,6 +182,8 @@ def load_library(path: str = LIB_PATH):
         "rg_persist_collect": ([vp, i32, vp, u64, C.POINTER(C.c_uint64), vp, vp, u64, C.POINTER(C.c_uint64)], i32),
     }
     for name, (args, res) in sig.items():
+        if os.environ.get("RAFTGPU_LIB") and not hasattr(L, name):
+            continue  # an experiment's library (ablations of an older build) may lack newer entry points
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res
@@ -236,6 +258,13 @@ class Engine:
                 keep.append(a)
                 setattr(ti, name, a.ctypes.data)
         self._check(self.L.rg_tick(self.h, C.byref(ti)))
+
+    def propose(self, batches):
+        """Stage client commands for the next tick (rg_propose): batches = [(global group, slot,
+        [Cmd bytes, ...]), ...]. Raises RgError (RG_EINVAL / RG_EFULL) and stages nothing on failure."""
+        props, lens, blob = pack_proposals(batches)
+        self._check(self.L.rg_propose(self.h, props, len(batches), blob.ctypes.data if blob.size else None,
+                                      lens.ctypes.data if lens.size else None))
 
     def tick_device(self, prop_target_ptr=0, prop_count_ptr=0, campaign_ptr=0, isolate_ptr=0, flags=0):
         ti = TickInput(prop_target_ptr or None, prop_count_ptr or None, campaign_ptr or None,
@@ -331,7 +360,7 @@ class Engine:
             return None
         return self.entries(rid, index, 1, with_payload)[0]
 
-    def import_replica(self, rid, view: dict, terms, types=None, payloads=None):
+    def import_replica(self, rid, view: dict, terms, types=None, payloads=None, lens=None):
         v = ReplicaView()
         for f in REPLICA_FIELDS:
             if f in view:
@@ -345,9 +374,11 @@ class Engine:
         t = np.ascontiguousarray(np.array(terms, dtype=np.uint64))
         ty = None if types is None else np.ascontiguousarray(np.array(types, dtype=np.uint32))
         pl = None if payloads is None else np.ascontiguousarray(np.frombuffer(payloads, dtype=np.uint8))
+        ln = None if lens is None else np.ascontiguousarray(np.array(lens, dtype=np.uint32))
         self._check(self.L.rg_import_replica(self.h, rid, C.byref(v), t.ctypes.data if len(t) else None,
                                              None if ty is None else ty.ctypes.data,
-                                             None if pl is None else pl.ctypes.data))
+                                             None if pl is None else pl.ctypes.data,
+                                             None if ln is None or not ln.size else ln.ctypes.data))
 
     def deliver(self, rid_src, **fields):
         m = MsgView()

@@ -144,4 +144,5 @@ def restore(engine, wal_logs: dict, cfg: dict, global_rids):
         # RG_ENTRY_EMPTY: an application entry whose Cmd is empty (a leader's no-op) stays empty
         types = [rl.log[i][1] | (0x100 if rl.log[i][1] == 0 and rl.log[i][2] == 0 else 0) for i in idx]
         pays = b"".join((rl.log[i][4] if rl.log[i][2] else b"").ljust(P, b"\0") for i in idx) if P else None
-        engine.import_replica(rid, v, terms, types, pays)
+        lens = [rl.log[i][2] for i in idx]
+        engine.import_replica(rid, v, terms, types, pays, lens)

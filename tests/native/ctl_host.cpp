@@ -17,6 +17,7 @@ struct Host {
   std::vector<uint64_t> s64[2], rem[2], tr, hdr[2], mt[2], job64;
   std::vector<uint32_t> s32[2], cnt[2], job32, jcnt;
   std::vector<uint8_t> rst[2];
+  std::vector<uint2> slab_info;  // [nslab][G][E] {0, P}: synthetic Cmds (forwarded proposals read their lengths)
   uint64_t t = 0;
 };
 
@@ -38,6 +39,7 @@ static TickParams params(Host* h) {
   p.mt_in = h->mt[b].data(); p.mt_out = h->mt[a].data();
   p.cnt_in = h->cnt[b].data(); p.cnt_out = h->cnt[a].data();
   p.job64 = h->job64.data(); p.job32 = h->job32.data(); p.jcnt = h->jcnt.data();
+  p.slab_info = h->slab_info.data();
   return p;
 }
 
@@ -68,6 +70,7 @@ void* ch_create(const rg_config* c) {
   h->job64.assign(J64_ROWS * J * n, 0);
   h->job32.assign(J32_ROWS * J * n, 0);
   h->jcnt.assign(n, 0);
+  h->slab_info.assign((size_t)c->num_slabs * G * E, make_uint2(0u, c->payload_bytes));
   return h;
 }
 
@@ -212,7 +215,8 @@ int ch_import(void* hh, uint32_t rid, const rg_replica_view* v, const uint64_t* 
     const uint64_t k = i - v->marker - 1;
     const uint32_t ty = types ? types[k] : 0;
     const bool hp = with_payload && h->c.payload_bytes && ty == 0;
-    h->tr[(i & (h->c.log_capacity - 1)) * N + q] = (terms[k] & TERM_MASK) | (ty ? TYPE_BIT : 0) | (hp ? PAY_BIT : 0);
+    h->tr[(i & (h->c.log_capacity - 1)) * N + q] = (terms[k] & TERM_MASK) | (ty ? TYPE_BIT : 0) |
+                                                   (hp ? len_bits(h->c.payload_bytes) : 0);
   }
   return 0;
 }

@@ -111,9 +111,9 @@ class CtlHost:
             return None
         w = (C.c_uint64 * 1)()
         self.L.ch_read_words(C.c_void_p(self.h), C.c_uint32(rid), C.c_uint64(index), C.c_uint32(1), w)
-        return dict(term=w[0] & ((1 << 61) - 1), type=(w[0] >> 61) & 1)
+        return dict(term=w[0] & ((1 << 48) - 1), type=(w[0] >> 61) & 1)
 
-    def import_replica(self, rid, view: dict, terms, types=None, payloads=None):
+    def import_replica(self, rid, view: dict, terms, types=None, payloads=None, lens=None):
         from raftd_amd.engine import REPLICA_FIELDS
         v = self._ReplicaView()
         for f in REPLICA_FIELDS:

@@ -1,0 +1,167 @@
+"""Client commands through the C-ABI (rg_propose) against the oracle (or_propose), tick by tick.
+
+raftd hands every client command to the shard as an opaque `Cmd []byte`, and the state machine
+gets it back verbatim as statemachine.Entry.Cmd (/root/reference/raft/state_machine.go:126-145).
+Here variable-length Cmds (0, 1, 17 and payload_bytes bytes, and random lengths) enter through
+rg_propose, are appended by leaders, forwarded by followers with their bytes, replicated, CRC'd over
+exactly their length, compacted and copied back; every replica view, message, entry (term, type,
+length, CRC, bytes) and applied batch must equal the oracle's. Parity with dragonboat itself is
+unpinned.
+"""
+import zlib
+
+import numpy as np
+import pytest
+
+from engines import make
+from test_gpu_parity import CHAOS, compare, crc32c_py
+from test_oracle import random_batches
+
+pytestmark = pytest.mark.gpu
+
+
+def check_cmds(gpu, ora, crc32c=False):
+    """Every log entry's bytes and CRC (the ring holds len bytes; the CRC covers exactly them)."""
+    lens = set()
+    for rid in range(ora.nrep):
+        v = ora.replica(rid)
+        if v["last"] <= v["marker"]:
+            continue
+        ge = gpu.entries(rid, v["marker"] + 1, v["last"] - v["marker"], with_payload=True)
+        for k, i in enumerate(range(v["marker"] + 1, v["last"] + 1)):
+            oe = ora.entry(rid, i, with_payload=True)
+            assert ge[k] == oe, (rid, i)
+            lens.add(oe["len"])
+            want = crc32c_py(oe["payload"]) if crc32c else zlib.crc32(oe["payload"])
+            assert ge[k]["crc"] == (want if oe["len"] else 0)
+    return lens
+
+
+def check_applied(gpu, ora):
+    recs, pay = gpu.apply_committed()
+    got = {}
+    for r, p in zip(recs, pay):
+        got.setdefault(int(r["rid"]), []).append((int(r["index"]), int(r["len"]), int(r["crc"]),
+                                                  bytes(p[:int(r["len"])])))
+    for rid in range(ora.nrep):
+        assert got.get(rid, []) == ora.applied_entries(rid), rid
+
+
+def run_caller(cfg, ticks, seed, make_gpu=None, check_every=1, p_none=0.3, applied=True):
+    gpu = make_gpu() if make_gpu else make("gpu", **cfg)
+    ora = make("c", **cfg)
+    gpu.bootstrap()
+    ora.bootstrap()
+    rng = np.random.default_rng(seed)
+    G, R, E, P = ora.G, ora.R, cfg["max_entries_per_msg"], cfg["payload_bytes"]
+    for t in range(ticks):
+        batches = random_batches(rng, G, R, E, P, p_none=p_none)
+        gpu.propose(batches)
+        assert ora.propose(batches) == 0
+        camp = (rng.random(G * R) < 0.02).astype(np.uint8)
+        iso = (rng.random(G * R) < 0.05).astype(np.uint8)
+        gpu.tick(None, None, camp, iso)
+        ora.tick(None, None, camp, iso)
+        if t % check_every == 0 or t == ticks - 1:
+            compare(gpu, ora, t)
+            if applied and hasattr(gpu, "apply_committed"):
+                check_applied(gpu, ora)
+    lens = check_cmds(gpu, ora, cfg.get("crc32c", 0))
+    return gpu, ora, lens
+
+
+@pytest.mark.parametrize("R,P", [(1, 64), (3, 16), (3, 256), (3, 1024), (5, 64), (4, 32)])
+def test_caller_cmds_chaos(R, P):
+    """Random-length Cmds under message loss, isolation, elections, truncation and snapshots."""
+    cfg = dict(CHAOS, groups=4, replicas=R, payload_bytes=P, max_entries_per_msg=8, seed=40 + R)
+    _, _, lens = run_caller(cfg, ticks=100, seed=R * 100 + P)
+    assert {0, 1, P} <= lens and len(lens) > 4, lens
+
+
+def test_caller_cmds_crc32c():
+    cfg = dict(CHAOS, groups=4, replicas=3, payload_bytes=256, max_entries_per_msg=8, seed=5, crc32c=1)
+    run_caller(cfg, ticks=80, seed=77)
+
+
+def test_caller_cmds_full_batches():
+    """64-Cmd batches: the upper half of the jobs' 64-bit masks, all lengths in one batch."""
+    cfg = dict(CHAOS, groups=4, replicas=3, payload_bytes=64, max_entries_per_msg=64, log_capacity=512,
+               snapshot_entries=200, seed=8)
+    run_caller(cfg, ticks=60, seed=64, check_every=3)
+
+
+@pytest.mark.parametrize("ranks,R", [(2, 3), (3, 3), (4, 5), (2, 5)])
+def test_caller_cmds_cluster(ranks, R):
+    """Replicas on different ranks: a follower's forwarded proposal carries its Cmds over the wire
+    to a leader on another rank (pack reads them from the forwarder's slab row)."""
+    from raftd_amd.cluster import LoopbackCluster
+    cfg = dict(CHAOS, groups=2 * ranks, replicas=R, payload_bytes=64, max_entries_per_msg=8, seed=3 + ranks)
+    run_caller(cfg, ticks=80, seed=ranks * 7 + R, make_gpu=lambda: LoopbackCluster(ranks=ranks, **cfg))
+
+
+def test_caller_cmds_metadata_only():
+    """payload_bytes 0: every Cmd is empty; proposals still commit (no payload stage)."""
+    cfg = dict(CHAOS, groups=4, replicas=3, payload_bytes=0, max_entries_per_msg=8, seed=2)
+    from engines import make as mk
+    gpu, ora = mk("gpu", **cfg), mk("c", **cfg)
+    gpu.bootstrap()
+    ora.bootstrap()
+    rng = np.random.default_rng(1)
+    for t in range(60):
+        b = [(g, int(rng.integers(0, 3)), [b""] * int(rng.integers(1, 9))) for g in range(4)]
+        gpu.propose(b)
+        assert ora.propose(b) == 0
+        gpu.tick()
+        ora.tick()
+        compare(gpu, ora, t)
+
+
+def test_propose_errors_stage_nothing():
+    from raftd_amd.engine import RG_EFULL, RG_EINVAL, RgError
+    cfg = dict(groups=2, replicas=3, payload_bytes=16, max_entries_per_msg=4, log_capacity=64)
+    gpu, ora = make("gpu", **cfg), make("c", **cfg)
+    for e in (gpu, ora):
+        e.bootstrap()
+    gpu.propose([(0, 1, [b"a"] * 3)])
+    assert ora.propose([(0, 1, [b"a"] * 3)]) == 0
+    cases = [([(0, 1, [b"b"] * 2)], RG_EFULL), ([(0, 2, [b"c"])], RG_EFULL), ([(1, 0, [b"b"] * 5)], RG_EINVAL),
+             ([(0, 1, [b"x" * 17])], RG_EINVAL), ([(2, 0, [b"x"])], RG_EINVAL),
+             ([(1, 0, [])], RG_EINVAL), ([(1, 0, [b"ok"]), (1, 2, [b"no"])], RG_EFULL)]
+    for batch, code in cases:
+        with pytest.raises(RgError) as ei:
+            gpu.propose(batch)
+        assert ei.value.code == code, batch
+        assert ora.propose(batch) == code
+    gpu.propose([(0, 1, [b""])])  # 4 = E
+    assert ora.propose([(0, 1, [b""])]) == 0
+    with pytest.raises(RgError):
+        gpu.tick(np.zeros(2, np.uint8), np.ones(2, np.uint32))  # staged + tick-input proposals
+    for e in (gpu, ora):
+        e.tick()
+    compare(gpu, ora, 0)
+
+
+def test_caller_then_synthetic():
+    """A synthetic (tick-input) proposal after caller proposals regenerates the slab bytes first."""
+    cfg = dict(groups=4, replicas=3, payload_bytes=64, max_entries_per_msg=8, log_capacity=256)
+    gpu, ora = make("gpu", **cfg), make("c", **cfg)
+    camp = np.zeros(12, np.uint8)
+    camp[0::3] = 1
+    for e in (gpu, ora):
+        e.bootstrap()
+        e.tick()
+        e.tick(campaign=camp)
+    rng = np.random.default_rng(9)
+    for t in range(12):
+        if t % 3 == 2:
+            ins = (np.zeros(4, np.uint8), np.full(4, 8, np.uint32))
+            gpu.tick(*ins)
+            ora.tick(*ins)
+        else:
+            b = random_batches(rng, 4, 3, 8, 64, p_none=0.0)
+            gpu.propose(b)
+            ora.propose(b)
+            gpu.tick()
+            ora.tick()
+        compare(gpu, ora, t)
+    check_cmds(gpu, ora)

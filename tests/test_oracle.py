@@ -84,6 +84,84 @@ def cross_check(seed, G, R, T, **cfg):
                 assert a.entry(rid, i) == b.entry(rid, i), (seed, t, rid, i)
 
 
+def random_batches(rng, G, R, E, P, base=0, p_none=0.3):
+    """Caller proposals for one tick: per group (with probability 1 - p_none) a batch of 1..E Cmds
+    to a random slot, lengths drawn from the edge cases 0, 1, 17, P and uniform [0, P]."""
+    out = []
+    for g in range(G):
+        if rng.random() < p_none:
+            continue
+        n = int(rng.integers(1, E + 1))
+        lens = [int(x) for x in rng.choice([0, 1, min(17, P), P, int(rng.integers(0, P + 1))], n)]
+        cmds = [rng.integers(0, 256, ln, dtype=np.uint8).tobytes() for ln in lens]
+        out.append((base + g, int(rng.integers(0, R)), cmds))
+    return out
+
+
+def cross_check_caller(seed, G, R, T, **cfg):
+    kw = dict(groups=G, replicas=R, payload_bytes=64, max_entries_per_msg=8, log_capacity=64,
+              snapshot_entries=20, compaction_overhead=5, drop_ppm=100000, seed=seed)
+    kw.update(cfg)
+    a, b = make("c", **kw), make("py", **kw)
+    a.bootstrap()
+    b.bootstrap()
+    rng = np.random.default_rng(seed)
+    P = kw["payload_bytes"]
+    for t in range(T):
+        batches = random_batches(rng, G, R, kw["max_entries_per_msg"], P)
+        assert a.propose(batches) == 0 and b.propose(batches) == 0
+        _, _, camp, iso = random_inputs(rng, G, R, kw["max_entries_per_msg"])
+        a.tick(None, None, camp, iso)
+        b.tick(None, None, camp, iso)
+        for rid in range(G * R):
+            va = a.replica(rid)
+            assert va == b.replica(rid), (seed, t, rid)
+            for d in range(R):
+                assert a.msgs(rid, d) == b.msgs(rid, d), (seed, t, rid, d)
+            for i in range(va["marker"] + 1, va["last"] + 1):
+                ea = a.entry(rid, i, with_payload=True)
+                eb = b.entry(rid, i)
+                eb["payload"] = b.reps[rid].log[i - b.reps[rid].marker - 1].data
+                assert ea == eb, (seed, t, rid, i)
+    return a
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_caller_proposals_c_matches_python(seed):
+    """Variable-length caller Cmds (0, 1, 17, max and random bytes), forwarded by followers to
+    their leader with the entries riding in the Propose message: both restatements agree on every
+    state, message and entry (payload bytes and CRC over exactly len bytes)."""
+    a = cross_check_caller(200 + seed, G=3, R=[1, 2, 3, 5, 3, 4][seed], T=80,
+                           payload_bytes=[16, 64, 256, 64, 1024, 32][seed])
+    lens = set()
+    for rid in range(a.nrep):
+        v = a.replica(rid)
+        for i in range(v["marker"] + 1, v["last"] + 1):
+            e = a.entry(rid, i, with_payload=True)
+            lens.add(e["len"])
+            if e["len"]:
+                import zlib
+                assert e["crc"] == zlib.crc32(e["payload"])
+    assert 0 in lens and 1 in lens and len(lens) > 3
+
+
+def test_propose_validation():
+    o = pyoracle.Oracle(groups=2, replicas=3, payload_bytes=16, max_entries_per_msg=4)
+    py = make("py", groups=2, replicas=3, payload_bytes=16, max_entries_per_msg=4)
+    for e in (o, py):
+        e.bootstrap()
+        assert e.propose([(0, 1, [b"a"] * 3)]) == 0
+        assert e.propose([(0, 1, [b"b"] * 2)]) == -3  # 5 > E in one tick
+        assert e.propose([(0, 2, [b"c"])]) == -3      # second slot of one group
+        assert e.propose([(1, 0, [b"x" * 17])]) == -1  # Cmd longer than payload_bytes
+        assert e.propose([(2, 0, [b"x"])]) == -1       # no such group
+        assert e.propose([(1, 0, [])]) == -1           # empty batch
+        assert e.propose([(1, 0, [b"ok"]), (1, 0, [b"x" * 99])]) == -1  # all or nothing
+        assert e.propose([(0, 1, [b"d"])]) == 0        # 4 = E
+    with pytest.raises(ValueError):
+        o.tick(np.zeros(2, np.uint8), np.ones(2, np.uint32))  # one proposal source per tick
+
+
 @pytest.mark.parametrize("seed", range(10))
 def test_c_oracle_matches_python_restatement(seed):
     cross_check(seed, G=3, R=[1, 2, 3, 4, 5][seed % 5], T=100)
