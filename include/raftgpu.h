@@ -98,11 +98,15 @@ typedef struct rg_config {
                                    at global group ranks·column_base) */
   uint32_t crc32c;              /* entry checksum: 0 = CRC-32/IEEE (zlib's, default), 1 = CRC-32C
                                    (Castagnoli, as pebble/tan WAL records use) */
+  uint32_t apply_feedback;      /* 0: `applied` follows `processed` at the end of every tick (the state
+                                   machine keeps up); 1: it moves only by rg_notify_applied
+                                   (dragonboat's NotifyRaftLastApplied, raft/state_machine.go:101-166) */
 } rg_config;
 
 typedef struct rg_replica_view {
   uint64_t term, vote, leader, committed, applied, last, marker, marker_term;
   uint64_t snap_index, snap_term, cap_base;
+  uint64_t processed; /* committed entries handed to the state machine (entryLog.processed) */
   uint32_t role, election_tick, heartbeat_tick, rand_timeout, rng_ctr;
   uint32_t granted, responded, active, err, drops;
   uint64_t match[RG_MAX_REPLICAS], next[RG_MAX_REPLICAS], rsnap[RG_MAX_REPLICAS];
@@ -303,6 +307,12 @@ int rg_persist_collect(rg_engine* e, int full, rg_persist_state* states, uint64_
  * replica in device order (slot by slot, shards ascending within a slot), compacted on the device and copied back by one hipMemcpyAsync. *n = the count;
  * if *n > cap nothing is copied and RG_EFULL is returned. Synchronous. */
 int rg_snapshot_events(rg_engine* e, uint32_t slot_mask, rg_snapshot_event* events, uint64_t cap, uint64_t* n);
+/* Peer.NotifyRaftLastApplied for n local replicas: replica rids[k]'s state machine has applied
+ * through index[k] (<= its processed index — config changes and empty entries included, which the
+ * state machine never sees). With rg_config.apply_feedback = 1 this is how `applied` moves: it gates
+ * campaigns (hasConfigChangeToApply: committed > applied) and snapshots (SnapshotEntries applied
+ * since the last one). RG_EINVAL (nothing changed) if an index exceeds processed or a rid is bad. */
+int rg_notify_applied(rg_engine* e, const uint32_t* rids, const uint64_t* index, size_t n);
 /* Global group and global replica id (group·replicas + slot) of local replica rid. */
 int rg_global_id(rg_engine* e, uint32_t rid, uint64_t* group, uint64_t* global_rid);
 /* Measurement helper: this device's streaming-copy bandwidth, (read + write bytes) / s, of a

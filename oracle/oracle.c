@@ -42,6 +42,7 @@ typedef struct {
 typedef struct {
   uint64_t term, vote, leader, committed, applied, last, marker, marker_term;
   uint64_t snap_index, snap_term, cap_base;
+  uint64_t processed; /* committed entries handed to the state machine (entryLog.processed) */
   uint32_t role, election_tick, heartbeat_tick, rand_timeout, rng_ctr;
   uint32_t granted, responded, active, err, drops;
   uint64_t match[OR_MAX_R], next[OR_MAX_R], rsnap[OR_MAX_R];
@@ -51,7 +52,7 @@ typedef struct {
   uint8_t* logpay;
   outbox_t ob[2];
   uint32_t g, s; /* group, slot */
-  /* apply window of the last step: entries apply_lo .. applied went to the state machine
+  /* apply window of the last step: entries apply_lo .. processed went to the state machine
    * (rsm → IOnDiskStateMachine.Update); a range restored from a snapshot does not */
   uint64_t apply_lo, restored_at;
   int took; /* a snapshot was taken at the end of the last step */
@@ -475,9 +476,10 @@ static void handle_install_snapshot(or_engine* e, rep_t* r, const or_msg_view* m
   } else if (match_term(e, r, si, st)) {
     commit_to(r, si);
     resp.log_index = r->committed;
-  } else { /* raft.restore → entryLog.restore */
-    r->marker = r->last = r->committed = r->snap_index = si;
+  } else { /* raft.restore → entryLog.restore; the state machine recovers from the snapshot */
+    r->marker = r->last = r->committed = r->snap_index = r->processed = si;
     r->marker_term = r->snap_term = st;
+    r->applied = u64max(r->applied, si);
     resp.log_index = r->last;
     r->restored_at = si;
   }
@@ -764,7 +766,7 @@ static void handle(or_engine* e, rep_t* r, const msg_in_t* mi) {
 static void step_replica(or_engine* e, rep_t* r) {
   const or_tick_input* in = e->in;
   uint32_t R = e->c.replicas, K = e->c.max_msgs_per_pair;
-  uint64_t marker_start = r->marker, applied_start = r->applied;
+  uint64_t marker_start = r->marker, processed_start = r->processed;
   r->restored_at = 0;
   r->took = 0;
   outbox_t* ob = cur_ob(e, r);
@@ -818,9 +820,12 @@ static void step_replica(or_engine* e, rep_t* r) {
     handle(e, r, &mi);
   }
   /* 5. apply + snapshot + compaction */
-  r->apply_lo = u64max(applied_start, r->restored_at) + 1;
-  r->applied = r->committed;
-  if (e->c.snapshot_entries && r->applied - r->snap_index >= e->c.snapshot_entries) {
+  /* GetUpdate.CommittedEntries = (processed, committed] (a restored range excluded), then
+   * commitUpdate: processed = committed; applied follows unless the state machine reports it */
+  r->apply_lo = u64max(processed_start, r->restored_at) + 1;
+  r->processed = r->committed;
+  if (!e->c.apply_feedback) r->applied = r->processed;
+  if (e->c.snapshot_entries && r->applied >= r->snap_index && r->applied - r->snap_index >= e->c.snapshot_entries) {
     r->snap_index = r->applied;
     r->snap_term = term_of(e, r, r->applied);
     r->took = 1;
@@ -990,7 +995,7 @@ int or_bootstrap(or_engine* e) {
   for (uint32_t i = 0; i < e->nrep; ++i) {
     rep_t* r = &e->reps[i];
     r->term = 0;
-    r->last = r->marker = r->marker_term = r->committed = r->applied = 0;
+    r->last = r->marker = r->marker_term = r->committed = r->applied = r->processed = 0;
     r->snap_index = r->snap_term = r->cap_base = 0;
     r->err = r->drops = 0;
     r->rng_ctr = 0;
@@ -1030,6 +1035,7 @@ int or_get_replica(const or_engine* e, uint32_t rid, or_replica_view* v) {
   v->leader = r->leader;
   v->committed = r->committed;
   v->applied = r->applied;
+  v->processed = r->processed;
   v->last = r->last;
   v->marker = r->marker;
   v->marker_term = r->marker_term;
@@ -1102,6 +1108,7 @@ int or_import_replica(or_engine* e, uint32_t rid, const or_replica_view* v, cons
   r->leader = v->leader;
   r->committed = v->committed;
   r->applied = v->applied;
+  r->processed = v->processed;
   r->last = v->last;
   r->marker = v->marker;
   r->marker_term = v->marker_term;
@@ -1170,6 +1177,14 @@ int or_deliver(or_engine* e, uint32_t rid_src, const or_msg_view* m) {
   return 0;
 }
 
+int or_notify_applied(or_engine* e, uint32_t rid, uint64_t index) {
+  if (rid >= e->nrep) return -1;
+  rep_t* r = &e->reps[rid];
+  if (index > r->processed) return -1;
+  r->applied = index;
+  return 0;
+}
+
 /* Snapshot events of replica rid's last step (rg_snapshot_events): returns OR_SNAP_* bits;
  * restored = the index an InstallSnapshot restored the log to, index/term = the snapshot taken. */
 int or_get_snapshot_event(const or_engine* e, uint32_t rid, uint64_t* restored, uint64_t* index, uint64_t* term) {
@@ -1189,7 +1204,7 @@ int or_get_applied(const or_engine* e, uint32_t rid, uint64_t* index, or_entry_v
   if (rid >= e->nrep) return -1;
   const rep_t* r = &e->reps[rid];
   uint32_t n = 0;
-  for (uint64_t i = r->apply_lo ? r->apply_lo : 1; i <= r->applied; ++i) {
+  for (uint64_t i = r->apply_lo ? r->apply_lo : 1; i <= r->processed; ++i) {
     const ent_t* en = log_at(e, r, i);
     if (en->type != OR_ENTRY_APP || en->len == 0) continue;
     if (n < cap) {

@@ -52,13 +52,14 @@ typedef struct or_config {
                           loss hashes and payloads use the global id; tick inputs are the window's) */
   uint64_t seed;
   uint32_t crc32c; /* entry checksum: 0 = CRC-32/IEEE (zlib), 1 = CRC-32C (Castagnoli) */
-  uint32_t _pad;
+  uint32_t apply_feedback; /* 0: applied follows processed at the end of every step (the state machine
+                              keeps up); 1: applied moves only by or_notify_applied (NotifyRaftLastApplied) */
 } or_config;
 
 /* Field order identical to rg_replica_view (include/raftgpu.h) so tests compare by name. */
 typedef struct or_replica_view {
   uint64_t term, vote, leader, committed, applied, last, marker, marker_term;
-  uint64_t snap_index, snap_term, cap_base;
+  uint64_t snap_index, snap_term, cap_base, processed;
   uint32_t role, election_tick, heartbeat_tick, rand_timeout, rng_ctr;
   uint32_t granted, responded, active, err, drops;
   uint64_t match[OR_MAX_R], next[OR_MAX_R], rsnap[OR_MAX_R];
@@ -134,6 +135,10 @@ int or_deliver(or_engine* e, uint32_t rid_src, const or_msg_view* m);
  * input), in index order. Returns the count; fills up to cap. Any output may be NULL. */
 int or_get_applied(const or_engine* e, uint32_t rid, uint64_t* index, or_entry_view* out, uint8_t* payload,
                    uint32_t cap);
+/* Peer.NotifyRaftLastApplied: the state machine of replica rid has applied through `index`
+ * (<= processed, else -1). With apply_feedback = 1 this is the only way `applied` moves (besides a
+ * restored snapshot); it gates campaigns (hasConfigChangeToApply) and snapshots. */
+int or_notify_applied(or_engine* e, uint32_t rid, uint64_t index);
 /* Snapshot events of rid's last step (the oracle side of rg_snapshot_events): OR_SNAP_* bits. */
 #define OR_SNAP_TAKEN 1
 #define OR_SNAP_RESTORED 2

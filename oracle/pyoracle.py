@@ -33,7 +33,7 @@ class Config(C.Structure):
         ("election_rtt", C.c_uint32), ("heartbeat_rtt", C.c_uint32), ("check_quorum", C.c_uint32),
         ("snapshot_entries", C.c_uint32), ("compaction_overhead", C.c_uint32),
         ("drop_ppm", C.c_uint32), ("group_base", C.c_uint32), ("seed", C.c_uint64),
-        ("crc32c", C.c_uint32), ("_pad", C.c_uint32),
+        ("crc32c", C.c_uint32), ("apply_feedback", C.c_uint32),
     ]
 
 
@@ -42,7 +42,7 @@ class ReplicaView(C.Structure):
         ("term", C.c_uint64), ("vote", C.c_uint64), ("leader", C.c_uint64),
         ("committed", C.c_uint64), ("applied", C.c_uint64), ("last", C.c_uint64),
         ("marker", C.c_uint64), ("marker_term", C.c_uint64), ("snap_index", C.c_uint64),
-        ("snap_term", C.c_uint64), ("cap_base", C.c_uint64),
+        ("snap_term", C.c_uint64), ("cap_base", C.c_uint64), ("processed", C.c_uint64),
         ("role", C.c_uint32), ("election_tick", C.c_uint32), ("heartbeat_tick", C.c_uint32),
         ("rand_timeout", C.c_uint32), ("rng_ctr", C.c_uint32), ("granted", C.c_uint32),
         ("responded", C.c_uint32), ("active", C.c_uint32), ("err", C.c_uint32), ("drops", C.c_uint32),
@@ -110,6 +110,7 @@ def lib():
         L.or_import_replica.argtypes = [vp, u32, C.POINTER(ReplicaView), C.c_void_p, C.c_void_p, C.c_void_p,
                                         C.c_void_p]
         L.or_propose.argtypes = [vp, C.POINTER(Proposal), C.c_size_t, C.c_void_p, C.c_void_p]
+        L.or_notify_applied.argtypes = [vp, u32, u64]
         L.or_tick.restype = C.c_int
         L.or_deliver.argtypes = [vp, u32, C.POINTER(MsgView)]
         L.or_payload.argtypes = [vp, u32, u32, u32, C.c_void_p]
@@ -127,7 +128,8 @@ def default_config(**kw) -> dict:
     """raftd's Raft parameters (raft/raft_manager.go:92-100) plus the engine's sizing."""
     c = dict(groups=4, replicas=3, log_capacity=2048, payload_bytes=256, max_entries_per_msg=64,
              max_msgs_per_pair=8, num_slabs=2, election_rtt=10, heartbeat_rtt=1, check_quorum=1,
-             snapshot_entries=1000, compaction_overhead=5, drop_ppm=0, seed=0x5EED, group_base=0, crc32c=0)
+             snapshot_entries=1000, compaction_overhead=5, drop_ppm=0, seed=0x5EED, group_base=0, crc32c=0,
+             apply_feedback=0)
     c.update(kw)
     return c
 
@@ -288,6 +290,10 @@ class Oracle:
                                       None if ln is None or not ln.size else ln.ctypes.data)
         if rc != 0:
             raise ValueError("or_import_replica failed")
+
+    def notify_applied(self, rid, index) -> int:
+        """or_notify_applied (Peer.NotifyRaftLastApplied): 0, or -1 if index > processed."""
+        return self.L.or_notify_applied(self.h, rid, index)
 
     def deliver(self, rid_src, **fields):
         m = MsgView()

@@ -122,7 +122,7 @@ class Replica:
         self.sim, self.g, self.s, self.id = sim, g, s, s + 1
         self.term = self.vote = self.leader = 0
         self.role = FOLLOWER
-        self.committed = self.applied = 0
+        self.committed = self.applied = self.processed = 0
         self.marker = self.marker_term = 0
         self.log = []  # log[k] = entry at index marker+1+k
         self.snap_index = self.snap_term = self.cap_base = 0
@@ -325,8 +325,9 @@ class Replica:
             resp["log_index"] = self.committed
         else:
             self.log = []
-            self.marker = self.committed = self.snap_index = si
+            self.marker = self.committed = self.snap_index = self.processed = si
             self.marker_term = self.snap_term = st
+            self.applied = max(self.applied, si)
             resp["log_index"] = self.last
         self.send(resp)
 
@@ -457,7 +458,7 @@ class Replica:
         return dict(
             term=self.term, vote=self.vote, leader=self.leader, committed=self.committed,
             applied=self.applied, last=self.last, marker=self.marker, marker_term=self.marker_term,
-            snap_index=self.snap_index, snap_term=self.snap_term, cap_base=self.cap_base,
+            snap_index=self.snap_index, snap_term=self.snap_term, cap_base=self.cap_base, processed=self.processed,
             role=self.role, election_tick=self.etick, heartbeat_tick=self.htick,
             rand_timeout=self.rand_to, rng_ctr=self.rng,
             granted=sum(1 << k for k, v in self.votes.items() if v),
@@ -567,9 +568,11 @@ class Sim:
                     hm = sum(1 << k for k, x in enumerate(cmds) if x)
                     r.handle(msg(PROPOSE, r.id, frm=r.id, nent=len(cmds), hint=hm, src_a=slab, src_b=0,
                                  ents=tuple(Entry(0, 0, x) for x in cmds)))
-                r.applied = r.committed
+                r.processed = r.committed  # handed to the state machine this step
+                if not self.cfg["apply_feedback"]:
+                    r.applied = r.processed
                 se, co = self.cfg["snapshot_entries"], self.cfg["compaction_overhead"]
-                if se and r.applied - r.snap_index >= se:
+                if se and r.applied >= r.snap_index and r.applied - r.snap_index >= se:
                     r.snap_index, r.snap_term = r.applied, r.term_at(r.applied)
                     cpt = r.snap_index - co if r.snap_index > co else 0
                     if cpt > r.marker:
@@ -604,7 +607,7 @@ class Sim:
     def import_replica(self, rid, view: dict, terms, types=None, payloads=None, lens=None):
         r = self.reps[rid]
         P = self.cfg["payload_bytes"]
-        for k in ("term", "vote", "leader", "committed", "applied", "marker", "marker_term",
+        for k in ("term", "vote", "leader", "committed", "applied", "processed", "marker", "marker_term",
                   "snap_index", "snap_term", "cap_base", "role", "err", "drops"):
             setattr(r, k, view.get(k, 0))
         r.etick = view.get("election_tick", 0)
@@ -628,6 +631,14 @@ class Sim:
             rp.snap = view.get("rsnap", [0] * 8)[k]
             rp.state = view.get("rstate", [0] * 8)[k]
             r.remotes.append(rp)
+
+    def notify_applied(self, rid, index):
+        """Peer.NotifyRaftLastApplied (index <= processed)."""
+        r = self.reps[rid]
+        if index > r.processed:
+            return -1
+        r.applied = index
+        return 0
 
     def deliver(self, rid_src, **f):
         r = self.reps[rid_src]

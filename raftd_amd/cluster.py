@@ -461,6 +461,12 @@ class LoopbackCluster(_Feeds):
         k, lr = self.loc[rid]
         self.engines[k].import_replica(lr, view, terms, types, payloads, lens)
 
+    def notify_applied(self, rids, index):
+        """rg_notify_applied on the ranks hosting replicas rids (cluster ids)."""
+        for r, i in zip(np.atleast_1d(rids), np.atleast_1d(index)):
+            k, lr = self.loc[int(r)]
+            self.engines[k].notify_applied([lr], [int(i)])
+
     def propose(self, batches):
         """rg_propose on the rank hosting each batch's replica (global group, slot)."""
         per = [[] for _ in range(self.N)]

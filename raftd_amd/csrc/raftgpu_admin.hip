@@ -24,7 +24,7 @@ __global__ void gather_replicas_kernel(AdminParams a, uint32_t first, uint32_t n
   v.term = s64[S_TERM * N]; v.vote = s64[S_VOTE * N]; v.leader = s64[S_LEADER * N];
   v.committed = s64[S_COMMITTED * N]; v.applied = s64[S_APPLIED * N]; v.last = s64[S_LAST * N];
   v.marker = s64[S_MARKER * N]; v.marker_term = s64[S_MARKER_TERM * N]; v.snap_index = s64[S_SNAP_INDEX * N];
-  v.snap_term = s64[S_SNAP_TERM * N]; v.cap_base = s64[S_CAP_BASE * N];
+  v.snap_term = s64[S_SNAP_TERM * N]; v.cap_base = s64[S_CAP_BASE * N]; v.processed = s64[S_PROCESSED * N];
   v.role = s32[S_ROLE * N]; v.election_tick = s32[S_ETICK * N]; v.heartbeat_tick = s32[S_HTICK * N];
   v.rand_timeout = s32[S_RAND_TO * N]; v.rng_ctr = s32[S_RNG_CTR * N]; v.granted = s32[S_GRANTED * N];
   v.responded = s32[S_RESPONDED * N]; v.active = s32[S_ACTIVE * N];
@@ -117,7 +117,7 @@ __global__ void scatter_replica_kernel(AdminParams a, uint32_t rid, const rg_rep
     s64[S_TERM * N] = v.term; s64[S_VOTE * N] = v.vote; s64[S_LEADER * N] = v.leader;
     s64[S_COMMITTED * N] = v.committed; s64[S_APPLIED * N] = v.applied; s64[S_LAST * N] = v.last;
     s64[S_MARKER * N] = v.marker; s64[S_MARKER_TERM * N] = v.marker_term; s64[S_SNAP_INDEX * N] = v.snap_index;
-    s64[S_SNAP_TERM * N] = v.snap_term; s64[S_CAP_BASE * N] = v.cap_base;
+    s64[S_SNAP_TERM * N] = v.snap_term; s64[S_CAP_BASE * N] = v.cap_base; s64[S_PROCESSED * N] = v.processed;
     s32[S_ROLE * N] = v.role; s32[S_ETICK * N] = v.election_tick; s32[S_HTICK * N] = v.heartbeat_tick;
     s32[S_RAND_TO * N] = v.rand_timeout; s32[S_RNG_CTR * N] = v.rng_ctr; s32[S_GRANTED * N] = v.granted;
     s32[S_RESPONDED * N] = v.responded; s32[S_ACTIVE * N] = v.active; s32[S_ERR * N] = v.err;
@@ -175,6 +175,31 @@ __global__ void deliver_kernel(AdminParams a, uint32_t rid, const rg_msg_view* m
 
 hipError_t launch_deliver(const AdminParams& a, uint32_t rid_src, const void* hdr, uint32_t* status, hipStream_t s) {
   hipLaunchKernelGGL(deliver_kernel, dim3(1), dim3(1), 0, s, a, rid_src, (const rg_msg_view*)hdr, status);
+  return hipGetLastError();
+}
+
+__global__ void notify_applied_kernel(AdminParams a, const uint32_t* rids, const uint64_t* index, uint32_t n, int pass,
+                                      uint32_t* bad) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const TickParams& t = a.t;
+  if (rids[i] >= t.nrep) {
+    atomicAdd(bad, 1u);
+    return;
+  }
+  const uint64_t q = q_of(t, rids[i]), N = t.nrep;
+  uint64_t* s64 = const_cast<uint64_t*>(t.s64_in) + q;
+  if (pass == 0) {
+    if (index[i] > s64[S_PROCESSED * N]) atomicAdd(bad, 1u);
+  } else {
+    s64[S_APPLIED * N] = index[i];
+  }
+}
+
+hipError_t launch_notify_applied(const AdminParams& a, const uint32_t* rids, const uint64_t* index, uint32_t n,
+                                 int pass, uint32_t* bad, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(notify_applied_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, rids, index, n, pass, bad);
   return hipGetLastError();
 }
 

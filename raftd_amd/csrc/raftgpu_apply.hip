@@ -24,7 +24,7 @@ __global__ void apply_count_kernel(ApplyParams a) {
   const uint32_t s = q / a.G;
   uint32_t c = 0;
   if ((a.slot_mask >> s) & 1u) {
-    const uint64_t hi = a.s64[(uint64_t)S_APPLIED * a.nrep + q];
+    const uint64_t hi = a.s64[(uint64_t)S_PROCESSED * a.nrep + q];
     for (uint64_t i = a.apply_lo[q] > 0 ? a.apply_lo[q] : 1; i <= hi; ++i)
       c += applies(a.tr[(i & (a.L - 1)) * a.nrep + q]) ? 1u : 0u;
   }
@@ -49,7 +49,7 @@ __global__ void __launch_bounds__(256) apply_gather_kernel(ApplyParams a) {
   const uint32_t s = q / a.G, j = q - s * a.G;
   const uint64_t n64 = a.nrep, L = a.L, P = a.P, nch = P / 16;
   const uint64_t group = pl_group(a.pl, s, j);
-  const uint64_t hi = a.s64[(uint64_t)S_APPLIED * n64 + q];
+  const uint64_t hi = a.s64[(uint64_t)S_PROCESSED * n64 + q];
   uint64_t pos = a.off[q];
   for (uint64_t i0 = a.apply_lo[q] > 0 ? a.apply_lo[q] : 1; i0 <= hi; i0 += 64) {
     const uint64_t i = i0 + lane;

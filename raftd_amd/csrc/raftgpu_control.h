@@ -70,11 +70,12 @@ struct Ctl {
   uint64_t gg, rid;    // global group and global replica id gg·R + s (RNG keys, loss hash)
   uint64_t gi, ri;     // the same as indices into this engine's tick-input arrays
   uint64_t term, vote, leader, committed, applied, last, marker, marker_term, snap_index, snap_term, cap_base;
+  uint64_t processed;  // committed entries handed to the state machine (entryLog.processed)
   uint32_t role, etick, htick, rand_to, rng_ctr, granted, responded, active, err, drops;
   uint64_t rm[R], rn[R], rs[R];  // remote match / next / snapshot index
   uint32_t rt[R];                // remote state
   uint64_t last_start, sent_hi, rw_lo, rw_hi, marker_start;
-  uint64_t applied_start, restored_at;  // apply window: entries restored from a snapshot are not Update()d
+  uint64_t processed_start, restored_at;  // apply window: entries restored from a snapshot are not Update()d
   bool took;                            // a snapshot was taken at the end of this step
   uint64_t wlo;                         // lowest log index written this step (EntriesToSave from here)
   // RG_CTL_FASTREP (ablation, off in the product: it changes control_kernel<5>'s register
@@ -102,6 +103,7 @@ struct Ctl {
     term = a[S_TERM * n]; vote = a[S_VOTE * n]; leader = a[S_LEADER * n]; committed = a[S_COMMITTED * n];
     applied = a[S_APPLIED * n]; last = a[S_LAST * n]; marker = a[S_MARKER * n]; marker_term = a[S_MARKER_TERM * n];
     snap_index = a[S_SNAP_INDEX * n]; snap_term = a[S_SNAP_TERM * n]; cap_base = a[S_CAP_BASE * n];
+    processed = a[S_PROCESSED * n];
     const uint32_t* b = p.s32_in + q;
     role = b[S_ROLE * n]; etick = b[S_ETICK * n]; htick = b[S_HTICK * n]; rand_to = b[S_RAND_TO * n];
     rng_ctr = b[S_RNG_CTR * n]; granted = b[S_GRANTED * n]; responded = b[S_RESPONDED * n];
@@ -114,7 +116,7 @@ struct Ctl {
       rt[j] = p.rst_in[j * n + q];
     });
     last_start = last; sent_hi = 0; rw_lo = ~0ull; rw_hi = 0; marker_start = marker;
-    applied_start = applied; restored_at = 0; wlo = ~0ull; took = false;
+    processed_start = processed; restored_at = 0; wlo = ~0ull; took = false;
 #ifdef RG_CTL_FASTREP
     la_base = la_word = la_pt = 0; la_n = 0;
 #endif
@@ -465,8 +467,9 @@ struct Ctl {
     } else if (term_at(si) == stt) {
       commit_to(si);
       li = committed;
-    } else {  // restore
-      marker = last = committed = snap_index = si;
+    } else {  // restore; the state machine recovers from the snapshot
+      marker = last = committed = snap_index = processed = si;
+      applied = umax64(applied, si);
 #ifdef RG_CTL_FASTREP
       la_n = 0;
 #endif
@@ -745,8 +748,11 @@ struct Ctl {
       }
     }
     RG_STAMP(3);
-    applied = committed;  // apply, snapshot, compaction
-    if (p.SE && applied - snap_index >= p.SE) {
+    // GetUpdate.CommittedEntries = (processed, committed], then commitUpdate; applied follows unless
+    // the state machine reports it (rg_notify_applied); snapshot + compaction on applied
+    processed = committed;
+    if (!p.AF) applied = processed;
+    if (p.SE && applied >= snap_index && applied - snap_index >= p.SE) {
       snap_index = applied;
       snap_term = term_at(applied);
       took = true;
@@ -772,6 +778,7 @@ struct Ctl {
     a[S_TERM * n] = term; a[S_VOTE * n] = vote; a[S_LEADER * n] = leader; a[S_COMMITTED * n] = committed;
     a[S_APPLIED * n] = applied; a[S_LAST * n] = last; a[S_MARKER * n] = marker; a[S_MARKER_TERM * n] = marker_term;
     a[S_SNAP_INDEX * n] = snap_index; a[S_SNAP_TERM * n] = snap_term; a[S_CAP_BASE * n] = cap_base;
+    a[S_PROCESSED * n] = processed;
     uint32_t* b = p.s32_out + q;
     b[S_ROLE * n] = role; b[S_ETICK * n] = etick; b[S_HTICK * n] = htick; b[S_RAND_TO * n] = rand_to;
     b[S_RNG_CTR * n] = rng_ctr; b[S_GRANTED * n] = granted; b[S_RESPONDED * n] = responded;
@@ -785,7 +792,7 @@ struct Ctl {
       p.cnt_out[((uint64_t)s * R + j) * p.G + g] = get8(oc, j);
     });
     p.jcnt[q] = nj;
-    if (p.apply_lo) p.apply_lo[q] = umax64(applied_start, restored_at) + 1;
+    if (p.apply_lo) p.apply_lo[q] = umax64(processed_start, restored_at) + 1;
     if (p.persist_lo) p.persist_lo[q] = wlo;
     if (p.snap_ev) p.snap_ev[q] = restored_at | (took ? SNAP_TAKEN_BIT : 0ull);
   }

@@ -72,7 +72,7 @@ struct rg_engine {
   uint32_t* crc_err = nullptr;
   uint8_t* slabs = nullptr;
   uint2* slab_info = nullptr;  // [nslab][rows][E] {0, Cmd length}
-  bool slabs_synthetic = false;  // every slab holds the generator's bytes (rg_fill_slabs, no rg_propose since)
+  uint64_t slab_synth = 0;  // bit s: slab s holds the generator's bytes (rg_fill_slabs, no rg_propose into it since)
   // caller proposals staged for the next tick (rg_propose): pinned host tables indexed by global input
   // index, uploaded by the tick; Cmd bytes + per-entry descriptors staged through pinned buffers
   uint8_t* h_pt = nullptr;
@@ -232,6 +232,7 @@ static TickParams params(rg_engine* e) {
   p.ET = c.election_rtt; p.HT = c.heartbeat_rtt; p.CQ = c.check_quorum; p.SE = c.snapshot_entries;
   p.CO = c.compaction_overhead; p.drop_ppm = c.drop_ppm;
   p.wire = e->wire ? 1u : 0u;
+  p.AF = c.apply_feedback;
   p.seed = c.seed;
   p.tick = e->t;
   p.pl = e->pl;
@@ -306,11 +307,13 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
     return fail(RG_EINVAL, "payload_bytes must be 0 or a power of two in [16, 1024]");
   if (c.max_entries_per_msg < 1 || c.max_entries_per_msg > 64) return fail(RG_EINVAL, "max_entries_per_msg in 1..64");
   if (c.max_msgs_per_pair < 1 || c.max_msgs_per_pair > 16) return fail(RG_EINVAL, "max_msgs_per_pair in 1..16");
-  if (c.num_slabs < 2 || c.election_rtt < 1 || c.heartbeat_rtt < 1) return fail(RG_EINVAL, "num_slabs/rtt");
+  if (c.num_slabs < 2 || c.num_slabs > 64 || c.election_rtt < 1 || c.heartbeat_rtt < 1)
+    return fail(RG_EINVAL, "num_slabs in 2..64, rtt >= 1");
   if ((uint64_t)c.groups * c.replicas > 0x7FFFFFFFull) return fail(RG_EINVAL, "too many replicas");
   const uint32_t N = c.ranks ? c.ranks : 1;
   if (N > MAX_RANKS || c.rank >= N) return fail(RG_EINVAL, "ranks in 1..16, rank < ranks");
   if (c.crc32c > 1) return fail(RG_EINVAL, "crc32c must be 0 (IEEE) or 1 (Castagnoli)");
+  if (c.apply_feedback > 1) return fail(RG_EINVAL, "apply_feedback must be 0 or 1");
   if ((N > 1 || c.wire_all) && c.groups >= (1u << 24)) return fail(RG_EINVAL, "groups < 2^24 with ranks > 1");
   int ndev = 0;
   HIPCHK(hipGetDeviceCount(&ndev));
@@ -599,10 +602,10 @@ int rg_bootstrap(rg_engine* e) {
 int rg_fill_slabs(rg_engine* e) {
   if (!e) return fail(RG_EINVAL, "null engine");
   if (int jrc = join(e)) return jrc;
-  HIPCHK(launch_fill_slabs(e->slabs, e->slab_info, e->c.num_slabs, e->c.groups, e->slab_rows,
+  HIPCHK(launch_fill_slabs(e->slabs, e->slab_info, 0, e->c.num_slabs, e->c.groups, e->slab_rows,
                            e->c.max_entries_per_msg, e->c.payload_bytes, e->c.seed, e->pl, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
-  e->slabs_synthetic = true;
+  e->slab_synth = ~0ull;
   return RG_OK;
 }
 
@@ -710,7 +713,7 @@ int rg_propose(rg_engine* e, const rg_proposal* props, size_t n, const uint8_t* 
     LAUNCH(launch_stage_cmds(e->slabs, e->slab_info, P, d, (const uint64_t*)(d + cb), (const uint64_t*)(d + cb) + k,
                              (const uint32_t*)((const uint64_t*)(d + cb) + 2 * k), k, e->stream),
            e->stream, "stage_cmds");
-    e->slabs_synthetic = false;
+    e->slab_synth &= ~(1ull << slab);
   }
   if (n) e->staged = true;
   return RG_OK;
@@ -773,7 +776,14 @@ static int tick_impl(rg_engine* e, const rg_tick_input* in, bool device_ptrs) {
   TickParams p = params(e);
   if (e->staged && in && in->prop_target)
     return fail(RG_EINVAL, "rg_tick: proposals staged by rg_propose and tick-input proposals in one tick");
-  if (in && in->prop_target && !e->slabs_synthetic && e->c.payload_bytes) RGCHK(rg_fill_slabs(e));
+  const uint32_t sl = (uint32_t)(e->t % e->c.num_slabs);
+  if (in && in->prop_target && !((e->slab_synth >> sl) & 1) && e->c.payload_bytes) {
+    // a tick-input (synthetic) batch into a slab rg_propose wrote: regenerate that slab only (the
+    // others may still hold forwarded proposals' Cmds)
+    HIPCHK(launch_fill_slabs(e->slabs, e->slab_info, sl, 1, e->c.groups, e->slab_rows, e->c.max_entries_per_msg,
+                             e->c.payload_bytes, e->c.seed, e->pl, e->stream));
+    e->slab_synth |= 1ull << sl;
+  }
   if (in) {
     p.flags = in->flags;
     if (device_ptrs) {
@@ -1108,6 +1118,29 @@ extern "C" int rg_debug_ctl_profile(rg_engine* e, uint32_t* out) {
   return RG_OK;
 }
 #endif
+
+int rg_notify_applied(rg_engine* e, const uint32_t* rids, const uint64_t* index, size_t n) {
+  if (!e || (n && (!rids || !index))) return fail(RG_EINVAL, "rg_notify_applied args");
+  if (n == 0) return RG_OK;
+  if (n > 0x7FFFFFFFull) return fail(RG_EINVAL, "rg_notify_applied: too many");
+  if (int jrc = join(e)) return jrc;
+  const uint64_t rb = (n * 4 + 15) & ~15ull, ib = n * 8;
+  RGCHK(stage_reserve(e, rb + ib + 16));
+  uint8_t* d = e->stage;
+  HIPCHK(hipStreamSynchronize(e->stream));
+  HIPCHK(hipMemcpy(d, rids, n * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d + rb, index, ib, hipMemcpyHostToDevice));
+  uint32_t* bad = (uint32_t*)(d + rb + ib);
+  HIPCHK(hipMemsetAsync(bad, 0, 4, e->stream));
+  HIPCHK(launch_notify_applied(admin(e), (const uint32_t*)d, (const uint64_t*)(d + rb), (uint32_t)n, 0, bad, e->stream));
+  uint32_t nbad = 0;
+  HIPCHK(hipMemcpyAsync(&nbad, bad, 4, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  if (nbad) return fail(RG_EINVAL, "rg_notify_applied: " + std::to_string(nbad) + " replica(s) bad or past processed");
+  HIPCHK(launch_notify_applied(admin(e), (const uint32_t*)d, (const uint64_t*)(d + rb), (uint32_t)n, 1, bad, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return RG_OK;
+}
 
 int rg_global_id(rg_engine* e, uint32_t rid, uint64_t* group, uint64_t* global_rid) {
   if (!e || rid >= e->nrep) return fail(RG_EINVAL, "rg_global_id: bad replica");

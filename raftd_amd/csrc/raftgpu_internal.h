@@ -46,7 +46,7 @@ enum : uint32_t { ERR_CONFLICT = 1, ERR_BEYOND = 2, ERR_RING = 4, ERR_CRC = 8, E
 // state field rows ([row][nrep])
 enum : uint32_t {
   S_TERM, S_VOTE, S_LEADER, S_COMMITTED, S_APPLIED, S_LAST, S_MARKER, S_MARKER_TERM, S_SNAP_INDEX,
-  S_SNAP_TERM, S_CAP_BASE, S64_ROWS
+  S_SNAP_TERM, S_CAP_BASE, S_PROCESSED, S64_ROWS
 };
 enum : uint32_t {
   S_ROLE, S_ETICK, S_HTICK, S_RAND_TO, S_RNG_CTR, S_GRANTED, S_RESPONDED, S_ACTIVE, S_ERR, S_DROPS, S32_ROWS
@@ -121,6 +121,7 @@ struct TickParams {
   uint32_t G, R, nrep, L, P, E, K, nslab, J;
   uint32_t ET, HT, CQ, SE, CO, drop_ppm, flags;
   uint32_t wire;           // wire engine: slab rows per replica (q), else per column (g)
+  uint32_t AF;             // apply feedback: applied moves only by rg_notify_applied
   uint64_t seed, tick;
   Placement pl;
   const uint64_t* s64_in;  // [S64_ROWS][nrep]
@@ -214,8 +215,9 @@ RG_HD_INLINE uint32_t crc_of_cmd(uint32_t slot_crc, uint32_t len, uint32_t P, co
 hipError_t launch_control(const TickParams& p, hipStream_t s);
 hipError_t launch_bulk(const BulkParams& p, hipStream_t s, int grid);
 hipError_t launch_bootstrap(const TickParams& p, uint2* info, hipStream_t s);
-hipError_t launch_fill_slabs(uint8_t* slabs, uint2* slab_info, uint32_t nslab, uint32_t G, uint32_t rows, uint32_t E,
-                             uint32_t P, uint64_t seed, const Placement& pl, hipStream_t s);
+// synthetic Cmds into slabs [slab0, slab0 + nslab)
+hipError_t launch_fill_slabs(uint8_t* slabs, uint2* slab_info, uint32_t slab0, uint32_t nslab, uint32_t G, uint32_t rows,
+                             uint32_t E, uint32_t P, uint64_t seed, const Placement& pl, hipStream_t s);
 // caller proposals (rg_propose): Cmd e of the batch is copied from src + off[e] (len[e] bytes, zero-padded
 // to P) into slab entry dst[e] = (slab · rows + row) · E + k, and slab_info[dst[e]] = {0, len[e]}
 hipError_t launch_stage_cmds(uint8_t* slabs, uint2* slab_info, uint32_t P, const uint8_t* src, const uint64_t* off,
@@ -303,6 +305,9 @@ hipError_t launch_scatter_replica(const AdminParams& a, uint32_t rid, const void
                                   uint2* info, uint8_t* pay);
 hipError_t launch_deliver(const AdminParams& a, uint32_t rid_src, const void* hdr, uint32_t* status,
                           hipStream_t s);
+// rg_notify_applied: check (pass 0: *bad = number of rids / indices out of range) or set (pass 1) applied
+hipError_t launch_notify_applied(const AdminParams& a, const uint32_t* rids, const uint64_t* index, uint32_t n,
+                                 int pass, uint32_t* bad, hipStream_t s);
 int bulk_lds_bytes(uint32_t P);
 int bulk_blocks_per_cu(uint32_t P);
 

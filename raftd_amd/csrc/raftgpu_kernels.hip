@@ -446,26 +446,28 @@ hipError_t launch_bootstrap(const TickParams& p, uint2* info, hipStream_t s) {
 // row r of a slab holds the batch of global group pl_group(s, j): r = j (one rank, rows = G) or
 // r = q = s·G + j (rows = nrep: each rank's replica of a group reads its own row, so a forwarded
 // proposal finds the same bytes on the leader's rank)
-__global__ void fill_slabs_kernel(uint8_t* slabs, uint2* slab_info, uint32_t nslab, uint32_t G, uint32_t rows,
-                                  uint32_t E, uint32_t P, uint64_t seed, Placement pl) {
+__global__ void fill_slabs_kernel(uint8_t* slabs, uint2* slab_info, uint32_t slab0, uint32_t nslab, uint32_t G,
+                                  uint32_t rows, uint32_t E, uint32_t P, uint64_t seed, Placement pl) {
   const uint64_t wpe = P / 8;
   const uint64_t total = (uint64_t)nslab * rows * E * wpe;
   for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < total; w += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t ent = w / wpe, wi = w - ent * wpe;
     const uint32_t i = (uint32_t)(ent % E);
     const uint64_t sg = ent / E;
-    const uint32_t r = (uint32_t)(sg % rows), sl = (uint32_t)(sg / rows);
+    const uint32_t r = (uint32_t)(sg % rows), sl = slab0 + (uint32_t)(sg / rows);
     const uint64_t gg = pl_group(pl, r / G, r % G);
     const uint64_t key = mix64(((uint64_t)sl << 56) ^ (gg << 16) ^ (uint64_t)i ^ (seed * 0x9E3779B97F4A7C15ULL));
-    reinterpret_cast<uint64_t*>(slabs)[w] = mix64(key + (wi + 1) * 0xD1B54A32D192ED03ULL);
-    if (wi == 0) slab_info[ent] = make_uint2(0u, P);  // a synthetic Cmd is P bytes
+    const uint64_t at = (uint64_t)slab0 * rows * E * wpe + w;  // slabs [slab0, slab0 + nslab) only
+    reinterpret_cast<uint64_t*>(slabs)[at] = mix64(key + (wi + 1) * 0xD1B54A32D192ED03ULL);
+    if (wi == 0) slab_info[at / wpe] = make_uint2(0u, P);  // a synthetic Cmd is P bytes
   }
 }
 
-hipError_t launch_fill_slabs(uint8_t* slabs, uint2* slab_info, uint32_t nslab, uint32_t G, uint32_t rows, uint32_t E,
-                             uint32_t P, uint64_t seed, const Placement& pl, hipStream_t s) {
+hipError_t launch_fill_slabs(uint8_t* slabs, uint2* slab_info, uint32_t slab0, uint32_t nslab, uint32_t G, uint32_t rows,
+                             uint32_t E, uint32_t P, uint64_t seed, const Placement& pl, hipStream_t s) {
   if (!P) return hipSuccess;
-  hipLaunchKernelGGL(fill_slabs_kernel, dim3(4096), dim3(256), 0, s, slabs, slab_info, nslab, G, rows, E, P, seed, pl);
+  hipLaunchKernelGGL(fill_slabs_kernel, dim3(4096), dim3(256), 0, s, slabs, slab_info, slab0, nslab, G, rows, E, P,
+                     seed, pl);
   return hipGetLastError();
 }
 

@@ -33,7 +33,7 @@ class Config(C.Structure):
         ("snapshot_entries", C.c_uint32), ("compaction_overhead", C.c_uint32),
         ("drop_ppm", C.c_uint32), ("device", C.c_int32), ("seed", C.c_uint64),
         ("ranks", C.c_uint32), ("rank", C.c_uint32), ("wire_all", C.c_uint32), ("column_base", C.c_uint32),
-        ("crc32c", C.c_uint32),
+        ("crc32c", C.c_uint32), ("apply_feedback", C.c_uint32),
     ]
 
 
@@ -42,7 +42,7 @@ class ReplicaView(C.Structure):
         ("term", C.c_uint64), ("vote", C.c_uint64), ("leader", C.c_uint64),
         ("committed", C.c_uint64), ("applied", C.c_uint64), ("last", C.c_uint64),
         ("marker", C.c_uint64), ("marker_term", C.c_uint64), ("snap_index", C.c_uint64),
-        ("snap_term", C.c_uint64), ("cap_base", C.c_uint64),
+        ("snap_term", C.c_uint64), ("cap_base", C.c_uint64), ("processed", C.c_uint64),
         ("role", C.c_uint32), ("election_tick", C.c_uint32), ("heartbeat_tick", C.c_uint32),
         ("rand_timeout", C.c_uint32), ("rng_ctr", C.c_uint32), ("granted", C.c_uint32),
         ("responded", C.c_uint32), ("active", C.c_uint32), ("err", C.c_uint32), ("drops", C.c_uint32),
@@ -124,7 +124,8 @@ EXPORTS = ["rg_create", "rg_destroy", "rg_bootstrap", "rg_fill_slabs", "rg_tick"
            "rg_read_entries", "rg_import_replica", "rg_deliver", "rg_leader", "rg_sum_committed",
            "rg_device_bytes", "rg_last_error", "rg_last_tick_traffic", "rg_join",
            "rg_timing", "rg_kernel_ms", "rg_wire_plan", "rg_wire_pack", "rg_wire_recv", "rg_global_id",
-           "rg_apply_committed", "rg_probe_copy", "rg_persist_collect", "rg_snapshot_events", "rg_propose"]
+           "rg_apply_committed", "rg_probe_copy", "rg_persist_collect", "rg_snapshot_events", "rg_propose",
+           "rg_notify_applied"]
 
 _lib = None
 
@@ -166,6 +167,7 @@ def load_library(path: str = LIB_PATH):
         "rg_read_entries": ([vp, u32, u64, u32, C.POINTER(EntryView), vp], i32),
         "rg_import_replica": ([vp, u32, C.POINTER(ReplicaView), vp, vp, vp, vp], i32),
         "rg_propose": ([vp, C.POINTER(Proposal), C.c_size_t, vp, vp], i32),
+        "rg_notify_applied": ([vp, vp, vp, C.c_size_t], i32),
         "rg_deliver": ([vp, u32, C.POINTER(MsgView)], i32),
         "rg_leader": ([vp, u32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_int)], i32),
         "rg_sum_committed": ([vp, C.POINTER(C.c_uint64)], i32),
@@ -196,7 +198,7 @@ def default_config(**kw) -> dict:
     c = dict(groups=4, replicas=3, log_capacity=2048, payload_bytes=256, max_entries_per_msg=64,
              max_msgs_per_pair=8, num_slabs=2, election_rtt=10, heartbeat_rtt=1, check_quorum=1,
              snapshot_entries=1000, compaction_overhead=5, drop_ppm=0, device=0, seed=0x5EED,
-             ranks=1, rank=0, wire_all=0, column_base=0, crc32c=0)
+             ranks=1, rank=0, wire_all=0, column_base=0, crc32c=0, apply_feedback=0)
     c.update(kw)
     return c
 
@@ -387,6 +389,13 @@ class Engine:
         if "from" not in fields:
             m.from_ = rid_src % self.R + 1
         self._check(self.L.rg_deliver(self.h, rid_src, C.byref(m)))
+
+    def notify_applied(self, rids, index):
+        """rg_notify_applied (Peer.NotifyRaftLastApplied) for local replicas rids."""
+        r = np.ascontiguousarray(np.atleast_1d(rids), dtype=np.uint32)
+        i = np.ascontiguousarray(np.atleast_1d(index), dtype=np.uint64)
+        assert r.shape == i.shape
+        self._check(self.L.rg_notify_applied(self.h, r.ctypes.data, i.ctypes.data, r.size))
 
     def leader(self, group):
         lid, term, valid = C.c_uint64(), C.c_uint64(), C.c_int()

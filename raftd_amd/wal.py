@@ -116,29 +116,36 @@ def mix64(z: int) -> int:
     return z ^ (z >> 31)
 
 
-def restart_view(rl: ReplicaLog, group: int, slot: int, cfg: dict) -> dict:
-    """The replica view a restarted node starts from (becomeFollower(term, NoLeader))."""
+def restart_view(rl: ReplicaLog, group: int, slot: int, cfg: dict, app_applied=None) -> dict:
+    """The replica view a restarted node starts from (becomeFollower(term, NoLeader)).
+
+    applied = processed = the index the state machine reports as applied (raftd's Open returns the
+    app's /LastLogIndex, raft/state_machine.go:101-124), at least the snapshot index (the snapshot is
+    recovered first) and at most the persisted commit; None = the commit (a state machine that kept
+    up). The committed entries above it are handed to Update again by the first tick."""
     s, R, ET = rl.state, cfg["replicas"], cfg["election_rtt"]
     last = s["last"]
+    applied = s["commit"] if app_applied is None else min(max(int(app_applied), s["snap_index"]), s["commit"])
     key = (group << 32) | (slot << 24) | 1
     rto = ET + mix64(cfg["seed"] ^ mix64(key)) % ET
     match = [0] * R
     match[slot] = last
-    return dict(term=s["term"], vote=s["vote"], leader=0, committed=s["commit"], applied=s["commit"], last=last,
-                marker=s["marker"], marker_term=s["marker_term"], snap_index=s["snap_index"],
+    return dict(term=s["term"], vote=s["vote"], leader=0, committed=s["commit"], applied=applied, processed=applied,
+                last=last, marker=s["marker"], marker_term=s["marker_term"], snap_index=s["snap_index"],
                 snap_term=s["snap_term"], cap_base=s["marker"], role=0, election_tick=0, heartbeat_tick=0,
                 rand_timeout=rto, rng_ctr=1, granted=0, responded=0, active=0, err=0, drops=0,
                 match=match, next=[last + 1] * R, rsnap=[0] * R, rstate=[0] * R)
 
 
-def restore(engine, wal_logs: dict, cfg: dict, global_rids):
+def restore(engine, wal_logs: dict, cfg: dict, global_rids, app_applied=None):
     """Import every replica of `engine` (Engine, LoopbackCluster or Oracle: anything with
-    import_replica(rid, view, terms, types, payloads)) from replayed WAL logs. global_rids maps
-    the engine's replica ids to global ones (identity for one rank)."""
+    import_replica(rid, view, terms, types, payloads, lens)) from replayed WAL logs. global_rids maps
+    the engine's replica ids to global ones (identity for one rank). app_applied(global rid) -> the
+    index the replica's state machine has applied (its /LastLogIndex), or None for the commit."""
     R, P = cfg["replicas"], cfg["payload_bytes"]
     for rid, gr in global_rids:
         rl = wal_logs[gr]
-        v = restart_view(rl, gr // R, gr % R, cfg)
+        v = restart_view(rl, gr // R, gr % R, cfg, None if app_applied is None else app_applied(gr))
         idx = range(v["marker"] + 1, v["last"] + 1)
         terms = [rl.log[i][0] for i in idx]
         # RG_ENTRY_EMPTY: an application entry whose Cmd is empty (a leader's no-op) stays empty

@@ -28,6 +28,7 @@ static TickParams params(Host* h) {
   p.E = c.max_entries_per_msg; p.K = c.max_msgs_per_pair; p.nslab = c.num_slabs; p.J = h->J;
   p.ET = c.election_rtt; p.HT = c.heartbeat_rtt; p.CQ = c.check_quorum; p.SE = c.snapshot_entries;
   p.CO = c.compaction_overhead; p.drop_ppm = c.drop_ppm; p.seed = c.seed; p.tick = h->t;
+  p.AF = c.apply_feedback;
   p.pl = make_placement(1, 0, 0);  // one rank: every plane local
   const int a = (int)(h->t & 1), b = a ^ 1;
   p.s64_in = h->s64[a].data(); p.s64_out = h->s64[b].data();
@@ -146,7 +147,7 @@ int ch_read_replica(void* hh, uint32_t rid, rg_replica_view* v) {
   v->term = s64[S_TERM * N]; v->vote = s64[S_VOTE * N]; v->leader = s64[S_LEADER * N];
   v->committed = s64[S_COMMITTED * N]; v->applied = s64[S_APPLIED * N]; v->last = s64[S_LAST * N];
   v->marker = s64[S_MARKER * N]; v->marker_term = s64[S_MARKER_TERM * N]; v->snap_index = s64[S_SNAP_INDEX * N];
-  v->snap_term = s64[S_SNAP_TERM * N]; v->cap_base = s64[S_CAP_BASE * N];
+  v->snap_term = s64[S_SNAP_TERM * N]; v->cap_base = s64[S_CAP_BASE * N]; v->processed = s64[S_PROCESSED * N];
   v->role = s32[S_ROLE * N]; v->election_tick = s32[S_ETICK * N]; v->heartbeat_tick = s32[S_HTICK * N];
   v->rand_timeout = s32[S_RAND_TO * N]; v->rng_ctr = s32[S_RNG_CTR * N]; v->granted = s32[S_GRANTED * N];
   v->responded = s32[S_RESPONDED * N]; v->active = s32[S_ACTIVE * N]; v->err = s32[S_ERR * N];
@@ -199,7 +200,7 @@ int ch_import(void* hh, uint32_t rid, const rg_replica_view* v, const uint64_t* 
   s64[S_TERM * N] = v->term; s64[S_VOTE * N] = v->vote; s64[S_LEADER * N] = v->leader;
   s64[S_COMMITTED * N] = v->committed; s64[S_APPLIED * N] = v->applied; s64[S_LAST * N] = v->last;
   s64[S_MARKER * N] = v->marker; s64[S_MARKER_TERM * N] = v->marker_term; s64[S_SNAP_INDEX * N] = v->snap_index;
-  s64[S_SNAP_TERM * N] = v->snap_term; s64[S_CAP_BASE * N] = v->cap_base;
+  s64[S_SNAP_TERM * N] = v->snap_term; s64[S_CAP_BASE * N] = v->cap_base; s64[S_PROCESSED * N] = v->processed;
   s32[S_ROLE * N] = v->role; s32[S_ETICK * N] = v->election_tick; s32[S_HTICK * N] = v->heartbeat_tick;
   s32[S_RAND_TO * N] = v->rand_timeout; s32[S_RNG_CTR * N] = v->rng_ctr; s32[S_GRANTED * N] = v->granted;
   s32[S_RESPONDED * N] = v->responded; s32[S_ACTIVE * N] = v->active; s32[S_ERR * N] = v->err;

@@ -145,6 +145,45 @@ def test_caller_proposals_c_matches_python(seed):
     assert 0 in lens and 1 in lens and len(lens) > 3
 
 
+def lagging_apply(rng, e, nrep, p_notify=0.4):
+    """Notify-applied inputs for one tick: each replica, with probability p_notify, reports an
+    applied index drawn from [applied, processed] (a state machine that lags, then catches up)."""
+    out = []
+    for rid in range(nrep):
+        v = e.replica(rid)
+        if rng.random() < p_notify and v["processed"] >= v["applied"]:
+            out.append((rid, int(rng.integers(v["applied"], v["processed"] + 1))))
+    return out
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_apply_feedback_c_matches_python(seed):
+    """apply_feedback = 1: `applied` moves only by notify_applied (NotifyRaftLastApplied), so a lagging
+    state machine delays campaigns (hasConfigChangeToApply) and snapshots; both restatements agree."""
+    kw = dict(groups=3, replicas=[3, 5, 3, 2][seed], payload_bytes=16, max_entries_per_msg=8, log_capacity=64,
+              snapshot_entries=20, compaction_overhead=5, drop_ppm=100000, seed=300 + seed, apply_feedback=1)
+    a, b = make("c", **kw), make("py", **kw)
+    a.bootstrap()
+    b.bootstrap()
+    rng = np.random.default_rng(seed)
+    G, R = kw["groups"], kw["replicas"]
+    lagged = 0
+    for t in range(120):
+        for rid, idx in lagging_apply(rng, a, G * R):
+            assert a.notify_applied(rid, idx) == 0 and b.notify_applied(rid, idx) == 0
+        assert a.notify_applied(0, a.replica(0)["processed"] + 1) == -1
+        ins = random_inputs(rng, G, R, 8)
+        a.tick(*ins)
+        b.tick(*ins)
+        for rid in range(G * R):
+            va = a.replica(rid)
+            assert va == b.replica(rid), (seed, t, rid)
+            for d in range(R):
+                assert a.msgs(rid, d) == b.msgs(rid, d), (seed, t, rid, d)
+            lagged += va["applied"] < va["committed"]
+    assert lagged > 0
+
+
 def test_propose_validation():
     o = pyoracle.Oracle(groups=2, replicas=3, payload_bytes=16, max_entries_per_msg=4)
     py = make("py", groups=2, replicas=3, payload_bytes=16, max_entries_per_msg=4)
