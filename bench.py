@@ -139,10 +139,19 @@ def cpu_baseline(args, seconds):
         if el >= seconds and ticks >= 5:
             break
     c1 = o.replica(0)["committed"]
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), None)
+    except OSError:
+        pass
     return {
         "value": G * ticks / el,
         "unit": "group-steps/s",
         "cores": T,
+        "nproc": os.cpu_count(),
+        "affinity_cpus": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
+        "cpu_model": model,
         "kind": "port",
         "sample": f"{G} groups x {R} replicas, {E} x {args.payload}-B entries per group-tick, {ticks} timed ticks "
                   f"after {warm} warm ticks ({el:.1f} s); C restatement of dragonboat's step (oracle/oracle.c)",
@@ -183,6 +192,34 @@ def apply_copyback(eng, torch, slot_mask=1):
     nb = cnt * (32 + P)
     return {"slot_mask": slot_mask, "entries": cnt, "bytes": nb, "ms": best * 1e3, "GBps": nb / best / 1e9,
             "note": "count + scan + gather kernels, then one hipMemcpyAsync per array into pinned host memory"}
+
+
+def e2e_with_apply(eng, tick, G, steps, slot_mask=1):
+    """Ticks with the committed-entry copy-back the daemon needs for /UpdateEntries: after every tick
+    rg_apply_async gathers the slot-0 replicas' applied entries (one node's share) and starts their
+    D2H copy on the copy stream, double-buffered, so copies overlap the next ticks; the host waits
+    for each tick's copy one tick later. Bounded by min(tick rate, PCIe rate)."""
+    import torch
+    n = nb = 0
+    P = eng.cfg["payload_bytes"]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        tick()
+        eng.apply_async(slot_mask, i & 1)
+        if i:
+            r, _ = eng.apply_wait((i - 1) & 1, copy=False)
+            n += len(r)
+    r, _ = eng.apply_wait((steps - 1) & 1, copy=False)
+    n += len(r)
+    el = time.perf_counter() - t0
+    nb = n * (32 + P)
+    return {"value": G * steps / el, "unit": "group-steps/s", "steps": steps, "ms_per_step": el * 1e3 / steps,
+            "entries_per_step": n / steps, "bytes_per_step": nb / steps, "pcie_GBps": nb / el / 1e9,
+            "slot_mask": slot_mask,
+            "note": "tick + gather of the applied entries of one node (slot-0 replicas) + D2H into pinned memory "
+                    "on a copy stream, overlapped with the next tick (rg_apply_async / rg_apply_wait); the copy "
+                    "is PCIe-bound, so this is min(tick rate, PCIe rate)"}
 
 
 def pmc_traffic(kernel="bulk_kernel", wire=False, spread=False):
@@ -314,7 +351,11 @@ def main():
     kms["control"] = host.kernel_ms()["control"]
     host.timing(False)
     x_ms = sum(a.elapsed_time(b) for a, b in xev) / args.steps if wire and not pipelined else 0.0
-    errs = sum(1 for v in eng.replicas(0, min(eng.nrep, 3 * 4096)) if v["err"])
+    va = eng.replica_array()  # every replica of this rank's first engine: invariant bits and drops
+    errs, drops = int((va["err"] != 0).sum()), int(va["drops"].sum())
+    e2e = None
+    if not spread:
+        e2e = e2e_with_apply(eng, lambda: one_step(None), G, steps=max(4, min(args.steps, 12)))
     apply = apply_copyback(eng, torch)
     copy_gbs = hbm_copy_ceiling(eng)
     t = torch.tensor([wall, dev_ms, float(c1 - c0), x_ms, float(wire_bytes)], dtype=torch.float64,
@@ -379,7 +420,10 @@ def main():
         "commits_per_sec": commits / wall,
         "replica_steps_per_sec": group_steps * R,
         "device_ms_per_step": dev_max / K,
-        "invariant_errors_in_sample": errs,
+        "replicas_with_invariant_errors": errs,
+        "drops_total": drops,
+        "drops_note": "messages / batches the engine dropped by its own bounded-buffer rules (K_MAX per pair per "
+                      "tick, ring capacity, forward hop limit) since bootstrap, summed over this rank's replicas",
         "commits_expected_per_step": world * G * E,
         "commits_measured_per_step": commits / K,
         "roofline": {
@@ -417,6 +461,7 @@ def main():
         },
         "device_bytes": host.device_bytes,
         "apply_copyback": apply,
+        "e2e_with_apply": e2e,
     }
     if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
         out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)

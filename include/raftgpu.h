@@ -295,6 +295,16 @@ int rg_wire_recv(rg_engine* e, const void* recv_buf, const uint64_t* recv_bytes 
  * *n = the count; if *n > cap nothing is copied and RG_EFULL is returned. Synchronous. */
 int rg_apply_committed(rg_engine* e, uint32_t slot_mask, rg_apply_entry* entries, uint8_t* payload, uint64_t cap,
                        uint64_t* n);
+/* Asynchronous, double-buffered copy-back (the same batch as rg_apply_committed): gathers the last
+ * tick's applied entries into device staging buffer `buf` (0 or 1) on the engine's stream — before
+ * the next tick can reuse their ring slots — and starts one D2H copy per array into engine-owned
+ * pinned host memory on a separate copy stream, so the copy overlaps the next ticks. A gather into
+ * `buf` first waits (on the device) for that buffer's previous copy: a driver that alternates
+ * buffers runs at min(tick rate, PCIe rate). Synchronises the host only on the entry count. */
+int rg_apply_async(rg_engine* e, uint32_t slot_mask, int buf);
+/* Wait for buffer `buf`'s copy; *entries / *payload (payload_bytes per entry) point into
+ * engine-owned pinned memory, valid until the next rg_apply_async into `buf`; *n = the count. */
+int rg_apply_wait(rg_engine* e, int buf, const rg_apply_entry** entries, const uint8_t** payload, uint64_t* n);
 /* Host WAL feed: for every replica whose log or hard state changed in the last
  * tick (full != 0, or no tick yet: every replica, whole log window), one rg_persist_state and the
  * entries it rewrote, gathered on the device and copied back by one hipMemcpyAsync per array. Make

@@ -58,10 +58,26 @@ def build_oracle() -> str:
     return os.path.join(ROOT, "oracle", "build", "liboracle.so")
 
 
+def build_abi_harness() -> str:
+    """gcc the plain-C ABI harness tests/native/abi_c.c (the call sequence a cgo shim makes) against
+    the in-tree libraftgpu.so: tests/native/abi_c.bin (test infrastructure, run by tests/test_abi.py)."""
+    src = os.path.join(ROOT, "tests", "native", "abi_c.c")
+    out = os.path.join(ROOT, "tests", "native", "abi_c.bin")
+    lib = build_engine()
+    deps = [src, lib, os.path.join(ROOT, "include", "raftgpu.h")]
+    if not _stale(out, deps):
+        return out
+    subprocess.run(["gcc", "-O2", "-std=c11", "-Wall", "-Wextra", "-Werror", src, "-I", os.path.join(ROOT, "include"),
+                    "-L", PKG, "-lraftgpu", "-lz", "-Wl,-rpath,$ORIGIN/../../raftd_amd", "-Wl,-rpath,/opt/rocm/lib",
+                    "-o", out], check=True)
+    return out
+
+
 def main():
     force = "--force" in sys.argv
     print(build_engine(force=force, verbose=True))
     print(build_oracle())
+    print(build_abi_harness())
 
 
 if __name__ == "__main__":

@@ -131,6 +131,14 @@ struct rg_engine {
   uint64_t *aoff = nullptr, *absum = nullptr;
   uint8_t* astage = nullptr;
   uint64_t astage_bytes = 0;
+  // asynchronous copy-back (rg_apply_async): per buffer a device staging area, pinned host memory,
+  // and events for "gathered" and "copied"; copies run on their own stream
+  hipStream_t copy = nullptr;
+  hipEvent_t a_gath[2] = {nullptr, nullptr}, a_copy[2] = {nullptr, nullptr};
+  uint8_t* a_dev[2] = {nullptr, nullptr};
+  uint8_t* a_host[2] = {nullptr, nullptr};
+  uint64_t a_dcap[2] = {0, 0}, a_hcap[2] = {0, 0}, a_n[2] = {0, 0};
+  bool a_used[2] = {false, false};
   // persistence copy-back
   uint64_t* persist_lo = nullptr;
   uint64_t* snap_ev = nullptr;  // [nrep] restored_at | SNAP_TAKEN_BIT of the last tick
@@ -448,10 +456,17 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
     }
   }
   if (hipEventCreateWithFlags(&e->stg_ev, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&e->prop_ev, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&e->prop_ev, hipEventDisableTiming) != hipSuccess ||
+      hipStreamCreateWithFlags(&e->copy, hipStreamNonBlocking) != hipSuccess) {
     rg_destroy(e);
-    return fail(RG_EHIP, "hipEventCreate");
+    return fail(RG_EHIP, "hipEventCreate / hipStreamCreate");
   }
+  for (int b = 0; b < 2; ++b)
+    if (hipEventCreateWithFlags(&e->a_gath[b], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->a_copy[b], hipEventDisableTiming) != hipSuccess) {
+      rg_destroy(e);
+      return fail(RG_EHIP, "hipEventCreate");
+    }
   e->stream = e->own;
   std::vector<uint32_t> tab;
   build_crc(e, tab);
@@ -488,6 +503,15 @@ void rg_destroy(rg_engine* e) {
   for (int b = 0; b < 2; ++b) {
     if (e->ctl_done[b]) (void)hipEventDestroy(e->ctl_done[b]);
     if (e->bulk_done[b]) (void)hipEventDestroy(e->bulk_done[b]);
+  }
+  if (e->copy) {
+    (void)hipStreamSynchronize(e->copy);
+    (void)hipStreamDestroy(e->copy);
+  }
+  for (int b = 0; b < 2; ++b) {
+    if (e->a_gath[b]) (void)hipEventDestroy(e->a_gath[b]);
+    if (e->a_copy[b]) (void)hipEventDestroy(e->a_copy[b]);
+    if (e->a_host[b]) (void)hipHostFree(e->a_host[b]);
   }
   if (e->stg_ev) (void)hipEventDestroy(e->stg_ev);
   if (e->prop_ev) (void)hipEventDestroy(e->prop_ev);
@@ -1081,6 +1105,68 @@ int rg_apply_committed(rg_engine* e, uint32_t slot_mask, rg_apply_entry* entries
   HIPCHK(hipMemcpyAsync(entries, a.out_rec, rb, hipMemcpyDeviceToHost, e->stream));
   if (pb) HIPCHK(hipMemcpyAsync(payload, a.out_pay, pb, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
+  return RG_OK;
+}
+
+int rg_apply_async(rg_engine* e, uint32_t slot_mask, int buf) {
+  if (!e || buf < 0 || buf > 1) return fail(RG_EINVAL, "rg_apply_async args");
+  if (int jrc = join(e)) return jrc;
+  const TickParams t = params(e);
+  ApplyParams a{};
+  a.G = t.G; a.R = t.R; a.nrep = t.nrep; a.L = t.L; a.P = t.P; a.slot_mask = slot_mask; a.pl = e->pl;
+  a.s64 = t.s64_in; a.apply_lo = e->apply_lo; a.tr = e->tr; a.info = e->info; a.pay = e->pay;
+  a.zi = e->crc_tab + CRC_ZI_OFF;
+  a.cnt = e->acnt; a.off = e->aoff; a.bsum = e->absum;
+  LAUNCH(launch_apply_count(a, (uint64_t*)e->d_sum, e->stream), e->stream, "apply count");
+  uint64_t total = 0;
+  HIPCHK(hipMemcpyAsync(&total, e->d_sum, 8, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  const uint64_t rb = total * sizeof(rg_apply_entry), need = rb + total * a.P;
+  if (need > e->a_dcap[buf] || need > e->a_hcap[buf]) {  // grow: the buffer's last copy must be done
+    HIPCHK(hipEventSynchronize(e->a_copy[buf]));
+    const uint64_t nb = std::max<uint64_t>(need * 5 / 4, 1 << 20);
+    if (need > e->a_dcap[buf]) {
+      if (e->a_dev[buf]) {
+        (void)hipFree(e->a_dev[buf]);
+        e->allocs.erase(std::remove(e->allocs.begin(), e->allocs.end(), (void*)e->a_dev[buf]), e->allocs.end());
+        e->bytes -= e->a_dcap[buf];
+        e->a_dev[buf] = nullptr;
+      }
+      e->a_dcap[buf] = 0;
+      RGCHK(dalloc(e, &e->a_dev[buf], nb));
+      e->a_dcap[buf] = nb;
+    }
+    if (need > e->a_hcap[buf]) {
+      if (e->a_host[buf]) (void)hipHostFree(e->a_host[buf]);
+      e->a_host[buf] = nullptr;
+      e->a_hcap[buf] = 0;
+      if (hipHostMalloc((void**)&e->a_host[buf], nb, 0) != hipSuccess) return fail(RG_ENOMEM, "hipHostMalloc (apply)");
+      e->a_hcap[buf] = nb;
+    }
+  }
+  const bool prev = e->a_used[buf];
+  e->a_n[buf] = total;
+  e->a_used[buf] = true;
+  if (total) {
+    if (prev) HIPCHK(hipStreamWaitEvent(e->stream, e->a_copy[buf], 0));  // its last copy has read the staging
+    a.out_rec = e->a_dev[buf];
+    a.out_pay = e->a_dev[buf] + rb;
+    LAUNCH(launch_apply_gather(a, e->stream), e->stream, "apply gather");
+  }
+  HIPCHK(hipEventRecord(e->a_gath[buf], e->stream));
+  HIPCHK(hipStreamWaitEvent(e->copy, e->a_gath[buf], 0));
+  if (total) HIPCHK(hipMemcpyAsync(e->a_host[buf], e->a_dev[buf], need, hipMemcpyDeviceToHost, e->copy));
+  HIPCHK(hipEventRecord(e->a_copy[buf], e->copy));
+  return RG_OK;
+}
+
+int rg_apply_wait(rg_engine* e, int buf, const rg_apply_entry** entries, const uint8_t** payload, uint64_t* n) {
+  if (!e || buf < 0 || buf > 1 || !n) return fail(RG_EINVAL, "rg_apply_wait args");
+  if (!e->a_used[buf]) return fail(RG_EINVAL, "rg_apply_wait: no rg_apply_async into this buffer");
+  HIPCHK(hipEventSynchronize(e->a_copy[buf]));
+  *n = e->a_n[buf];
+  if (entries) *entries = (const rg_apply_entry*)e->a_host[buf];
+  if (payload) *payload = e->a_host[buf] ? e->a_host[buf] + e->a_n[buf] * sizeof(rg_apply_entry) : nullptr;
   return RG_OK;
 }
 

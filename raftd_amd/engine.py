@@ -125,7 +125,7 @@ EXPORTS = ["rg_create", "rg_destroy", "rg_bootstrap", "rg_fill_slabs", "rg_tick"
            "rg_device_bytes", "rg_last_error", "rg_last_tick_traffic", "rg_join",
            "rg_timing", "rg_kernel_ms", "rg_wire_plan", "rg_wire_pack", "rg_wire_recv", "rg_global_id",
            "rg_apply_committed", "rg_probe_copy", "rg_persist_collect", "rg_snapshot_events", "rg_propose",
-           "rg_notify_applied"]
+           "rg_notify_applied", "rg_apply_async", "rg_apply_wait"]
 
 _lib = None
 
@@ -168,6 +168,8 @@ def load_library(path: str = LIB_PATH):
         "rg_import_replica": ([vp, u32, C.POINTER(ReplicaView), vp, vp, vp, vp], i32),
         "rg_propose": ([vp, C.POINTER(Proposal), C.c_size_t, vp, vp], i32),
         "rg_notify_applied": ([vp, vp, vp, C.c_size_t], i32),
+        "rg_apply_async": ([vp, u32, i32], i32),
+        "rg_apply_wait": ([vp, i32, C.POINTER(vp), C.POINTER(vp), C.POINTER(C.c_uint64)], i32),
         "rg_deliver": ([vp, u32, C.POINTER(MsgView)], i32),
         "rg_leader": ([vp, u32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_int)], i32),
         "rg_sum_committed": ([vp, C.POINTER(C.c_uint64)], i32),
@@ -436,6 +438,24 @@ class Engine:
         self._check(self.L.rg_apply_committed(self.h, slot_mask, recs.ctypes.data, pay.ctypes.data, cap, C.byref(n)))
         k = n.value
         return recs[:k], pay[:k, :P]
+
+    def apply_async(self, slot_mask: int = 0xFF, buf: int = 0):
+        """rg_apply_async: gather the last tick's applied entries and start their D2H copy into
+        pinned buffer `buf` (0/1), overlapping the next ticks."""
+        self._check(self.L.rg_apply_async(self.h, slot_mask, buf))
+
+    def apply_wait(self, buf: int = 0, copy: bool = True):
+        """rg_apply_wait: (records, payloads) of buffer `buf` as numpy arrays (copies unless copy=False:
+        then views into engine-owned pinned memory, valid until the next apply_async into `buf`)."""
+        ents, pay, n = C.c_void_p(), C.c_void_p(), C.c_uint64()
+        self._check(self.L.rg_apply_wait(self.h, buf, C.byref(ents), C.byref(pay), C.byref(n)))
+        k, P = n.value, self.cfg["payload_bytes"]
+        if k == 0:
+            return np.zeros(0, APPLY_DTYPE), np.zeros((0, P), np.uint8)
+        recs = np.ctypeslib.as_array(C.cast(ents, C.POINTER(C.c_uint8)), (k * APPLY_DTYPE.itemsize,)).view(APPLY_DTYPE)
+        pays = (np.ctypeslib.as_array(C.cast(pay, C.POINTER(C.c_uint8)), (k * P,)).reshape(k, P) if P
+                else np.zeros((k, 0), np.uint8))
+        return (recs.copy(), pays.copy()) if copy else (recs, pays)
 
     def persist_collect(self, full: bool = False):
         """Host WAL feed of the last tick (rg_persist_collect): (states, entries, payload) numpy

@@ -1,0 +1,191 @@
+/*
+ * abi_c.c — TEST HARNESS: drives libraftgpu.so through include/raftgpu.h from plain C, in the
+ * call sequence the cgo NodeHost shim of INTEGRATION.md makes, with C-owned buffers only (cgo
+ * forbids C from keeping Go pointers, so the shim copies into buffers like these):
+ *
+ *   rg_create / rg_bootstrap            NewNodeHost + StartOnDiskReplica (raft/raft_manager.go:109,142)
+ *   rg_tick (campaign, then plain)      the NodeHost tick loop
+ *   rg_propose                          NodeHost.SyncPropose(cmd) (the /raft/update handler's job)
+ *   rg_persist_collect                  LogDB SaveRaftState before the messages leave
+ *   rg_apply_committed                  IOnDiskStateMachine.Update → POST /UpdateEntries
+ *   rg_notify_applied                   NotifyRaftLastApplied once the app answered
+ *   rg_leader / rg_read_replicas        GetLeaderID / SyncGetShardMembership (raft/members.go:21,30)
+ *   rg_destroy                          NodeHost.Close (raft_manager.go:159)
+ *
+ * Checks: every proposed Cmd reaches Update exactly once per replica, in proposal order, byte for
+ * byte, with its zlib CRC-32; every shard has one leader; errors come back as RG_E* codes.
+ * Exit 0 and "ABI_C OK" on success. Built by tests/test_abi.py (gcc, -lraftgpu -lz); run by the
+ * -m gpu test there.
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <zlib.h>
+
+#include "../../include/raftgpu.h"
+
+#define G 16
+#define R 3
+#define TICKS 40
+#define PER_TICK 4 /* Cmds per shard per tick */
+
+#define CHECK(x)                                                                              \
+  do {                                                                                        \
+    int _rc = (x);                                                                            \
+    if (_rc < 0) {                                                                            \
+      fprintf(stderr, "%s:%d: %s = %d (%s)\n", __FILE__, __LINE__, #x, _rc, rg_last_error()); \
+      exit(1);                                                                                \
+    }                                                                                         \
+  } while (0)
+#define EXPECT(c)                                                      \
+  do {                                                                 \
+    if (!(c)) {                                                        \
+      fprintf(stderr, "%s:%d: expectation failed: %s\n", __FILE__, __LINE__, #c); \
+      exit(1);                                                         \
+    }                                                                  \
+  } while (0)
+
+/* deterministic Cmd k of shard g at tick t: "put g/t/k" + filler, 1..200 bytes */
+static uint32_t make_cmd(uint32_t g, uint32_t t, uint32_t k, uint8_t* out) {
+  uint32_t n = (uint32_t)snprintf((char*)out, 256, "put shard=%u tick=%u k=%u;", g, t, k);
+  uint32_t len = 1 + (g * 131 + t * 31 + k * 7) % 200;
+  for (uint32_t i = n; i < len; ++i) out[i] = (uint8_t)('a' + (g + t + k + i) % 26);
+  return len;
+}
+
+int main(void) {
+  rg_config c;
+  memset(&c, 0, sizeof c);
+  c.groups = G; c.replicas = R; c.log_capacity = 1024; c.payload_bytes = 256;
+  c.max_entries_per_msg = 16; c.max_msgs_per_pair = 8; c.num_slabs = 2;
+  c.election_rtt = 10; c.heartbeat_rtt = 1; c.check_quorum = 1; /* raftd's config (raft_manager.go:92-100) */
+  c.snapshot_entries = 1000; c.compaction_overhead = 5; c.seed = 0x5EED; c.ranks = 1;
+  c.apply_feedback = 1;
+  rg_engine* e = NULL;
+  CHECK(rg_create(&c, &e));
+  CHECK(rg_bootstrap(e));
+
+  /* errors are codes, not crashes */
+  rg_proposal bad = {G + 5, 0, 1, 0};
+  uint32_t one = 1;
+  EXPECT(rg_propose(e, &bad, 1, (const uint8_t*)"x", &one) == RG_EINVAL);
+  EXPECT(rg_last_error()[0] != 0);
+
+  uint8_t campaign[G * R];
+  memset(campaign, 0, sizeof campaign);
+  rg_tick_input in;
+  memset(&in, 0, sizeof in);
+  CHECK(rg_tick(e, &in));
+  for (uint32_t g = 0; g < G; ++g) campaign[g * R + (g % R)] = 1;  /* leaders spread over the slots */
+  in.campaign = campaign;
+  /* every replica reports the bootstrap entries applied (the rsm applies config changes itself) */
+  uint32_t rids[G * R];
+  uint64_t idx[G * R];
+  for (uint32_t r = 0; r < G * R; ++r) { rids[r] = r; idx[r] = R; }
+  CHECK(rg_notify_applied(e, rids, idx, G * R));
+  CHECK(rg_tick(e, &in));
+  in.campaign = NULL;
+  for (int t = 0; t < 6; ++t) CHECK(rg_tick(e, &in));
+
+  /* C-owned buffers for the copy-back and the WAL feed */
+  const uint64_t cap = 1u << 16;
+  rg_apply_entry* ents = (rg_apply_entry*)malloc(cap * sizeof *ents);
+  uint8_t* pay = (uint8_t*)malloc(cap * c.payload_bytes);
+  rg_persist_state* ps = (rg_persist_state*)malloc(cap * sizeof *ps);
+  rg_persist_entry* pe = (rg_persist_entry*)malloc(cap * sizeof *pe);
+  uint8_t* ppay = (uint8_t*)malloc(cap * c.payload_bytes);
+  /* what each replica's state machine received, as a running CRC over (index, Cmd) */
+  uint64_t got[G * R];
+  uint32_t got_crc[G * R];
+  uint64_t last_idx[G * R];
+  memset(got, 0, sizeof got);
+  memset(got_crc, 0, sizeof got_crc);
+  memset(last_idx, 0, sizeof last_idx);
+
+  uint8_t* blob = (uint8_t*)malloc(G * PER_TICK * 256);
+  uint32_t lens[G * PER_TICK];
+  rg_proposal props[G];
+  uint32_t want_crc[G];
+  uint64_t want_n[G];
+  memset(want_crc, 0, sizeof want_crc);
+  memset(want_n, 0, sizeof want_n);
+  for (uint32_t t = 0; t < TICKS; ++t) {
+    uint64_t off = 0;
+    for (uint32_t g = 0; g < G; ++g) {
+      uint64_t leader = 0, term = 0;
+      int valid = 0;
+      CHECK(rg_leader(e, g, &leader, &term, &valid));
+      props[g].group = g;
+      props[g].slot = valid ? (uint32_t)(leader - 1) : 0;
+      props[g].count = PER_TICK;
+      props[g].first = (uint64_t)g * PER_TICK;
+      for (uint32_t k = 0; k < PER_TICK; ++k) {
+        uint32_t n = make_cmd(g, t, k, blob + off);
+        lens[g * PER_TICK + k] = n;
+        off += n;
+      }
+    }
+    CHECK(rg_propose(e, props, G, blob, lens));
+    off = 0;
+    for (uint32_t g = 0; g < G; ++g)
+      for (uint32_t k = 0; k < PER_TICK; ++k) {
+        uint32_t n = lens[g * PER_TICK + k];
+        want_crc[g] = (uint32_t)crc32(want_crc[g], blob + off, n);
+        want_n[g]++;
+        off += n;
+      }
+    CHECK(rg_tick(e, &in));
+    uint64_t ns = 0, ne = 0, na = 0;
+    CHECK(rg_persist_collect(e, 0, ps, cap, &ns, pe, ppay, cap, &ne)); /* the shim fsyncs these */
+    CHECK(rg_apply_committed(e, 0xFF, ents, pay, cap, &na));
+    for (uint64_t i = 0; i < na; ++i) {
+      const rg_apply_entry* a = &ents[i];
+      const uint8_t* cmd = pay + i * c.payload_bytes;
+      EXPECT(a->crc == (uint32_t)crc32(0, cmd, a->len));
+      EXPECT(a->index > last_idx[a->rid]);
+      last_idx[a->rid] = a->index;
+      got_crc[a->rid] = (uint32_t)crc32(got_crc[a->rid], cmd, a->len);
+      got[a->rid]++;
+    }
+    /* the app answered: applied = processed (config changes and no-ops included) */
+    rg_replica_view v[G * R];
+    CHECK(rg_read_replicas(e, 0, G * R, v));
+    for (uint32_t r = 0; r < G * R; ++r) idx[r] = v[r].processed;
+    CHECK(rg_notify_applied(e, rids, idx, G * R));
+  }
+  for (int t = 0; t < 4; ++t) { /* drain: the last Cmds commit everywhere */
+    uint64_t na = 0;
+    CHECK(rg_tick(e, &in));
+    CHECK(rg_apply_committed(e, 0xFF, ents, pay, cap, &na));
+    for (uint64_t i = 0; i < na; ++i) {
+      got_crc[ents[i].rid] = (uint32_t)crc32(got_crc[ents[i].rid], pay + i * c.payload_bytes, ents[i].len);
+      got[ents[i].rid]++;
+    }
+    rg_replica_view v[G * R];
+    CHECK(rg_read_replicas(e, 0, G * R, v));
+    for (uint32_t r = 0; r < G * R; ++r) idx[r] = v[r].processed;
+    CHECK(rg_notify_applied(e, rids, idx, G * R));
+  }
+  rg_replica_view v[G * R];
+  CHECK(rg_read_replicas(e, 0, G * R, v));
+  for (uint32_t g = 0; g < G; ++g) {
+    uint32_t leaders = 0;
+    for (uint32_t s = 0; s < R; ++s) {
+      const uint32_t r = g * R + s;
+      leaders += v[r].role == RG_LEADER;
+      EXPECT(v[r].err == 0);
+      if (got[r] != want_n[g] || got_crc[r] != want_crc[g]) {
+        fprintf(stderr, "shard %u replica %u: %llu Cmds crc %08x, want %llu crc %08x\n", g, s + 1,
+                (unsigned long long)got[r], got_crc[r], (unsigned long long)want_n[g], want_crc[g]);
+        return 1;
+      }
+    }
+    EXPECT(leaders == 1);
+  }
+  printf("ABI_C OK: %u shards x %u replicas, %llu Cmds per shard applied on every replica, device %.1f MB\n", G, R,
+         (unsigned long long)want_n[0], rg_device_bytes(e) / 1e6);
+  rg_destroy(e);
+  free(ents); free(pay); free(ps); free(pe); free(ppay); free(blob);
+  return 0;
+}

@@ -21,7 +21,9 @@ def test_header_declares_expected_api():
 
 def test_library_exports_every_declared_symbol():
     from raftd_amd import build
+    from raftd_amd.engine import load_library
     lib_path = build.build_engine()
+    load_library()  # torch's HIP runtime first (raftd_amd/engine.py): one runtime per process
     lib = C.CDLL(lib_path)
     for name in declared_symbols():
         assert hasattr(lib, name), name
@@ -59,3 +61,24 @@ def test_one_hip_runtime_per_process():
             "print(len({p for p in libs if 'amdhip' in p}), len({p for p in libs if 'hsa-runtime' in p}))")
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=ROOT, timeout=300)
     assert out.stdout.split() == ["1", "1"], out.stdout + out.stderr
+
+
+def build_c_harness() -> str:
+    from raftd_amd.build import build_abi_harness
+    return build_abi_harness()
+
+
+def test_c_harness_builds_and_links():
+    """A plain C program (what a cgo shim compiles to) includes raftgpu.h and links libraftgpu.so."""
+    import subprocess
+    exe = build_c_harness()
+    out = subprocess.run(["ldd", exe], capture_output=True, text=True)
+    assert "libraftgpu.so" in out.stdout and "not found" not in out.stdout, out.stdout
+
+
+@pytest.mark.gpu
+def test_c_harness_runs_the_cgo_call_sequence():
+    import subprocess
+    exe = build_c_harness()
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and "ABI_C OK" in out.stdout, out.stdout + out.stderr

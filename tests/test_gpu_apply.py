@@ -87,3 +87,27 @@ def test_apply_copyback_full_size():
     assert np.all(np.diff(recs["index"].reshape(G, E), axis=1) == 1)
     for k in range(0, len(recs), 9973):
         assert int(recs[k]["crc"]) == zlib.crc32(bytes(pay[k]))
+
+
+def test_async_copyback_matches_sync():
+    """rg_apply_async / rg_apply_wait (double-buffered, copy stream) return exactly what
+    rg_apply_committed returns for the same tick, also when a buffer is re-used two ticks later."""
+    from test_gpu_parity import CHAOS, random_inputs
+    cfg = dict(CHAOS, groups=8, replicas=3, payload_bytes=64, max_entries_per_msg=16, seed=4)
+    eng = make("gpu", **cfg)
+    eng.bootstrap()
+    rng = np.random.default_rng(4)
+    total = 0
+    for t in range(60):
+        eng.tick(*random_inputs(rng, 8, 3, 16))
+        want_r, want_p = eng.apply_committed()
+        eng.apply_async(0xFF, t & 1)
+        if t % 5 == 4:  # sometimes read the other buffer first: it must still hold the previous tick
+            eng.apply_wait((t - 1) & 1)
+        got_r, got_p = eng.apply_wait(t & 1)
+        assert np.array_equal(got_r, want_r), t
+        for k in range(len(want_r)):
+            n = int(want_r[k]["len"])
+            assert bytes(got_p[k, :n]) == bytes(want_p[k, :n]), (t, k)
+        total += len(want_r)
+    assert total > 0
