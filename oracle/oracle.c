@@ -1061,6 +1061,12 @@ int or_get_replica(const or_engine* e, uint32_t rid, or_replica_view* v) {
   return 0;
 }
 
+int or_get_replicas(const or_engine* e, uint32_t first, uint32_t n, or_replica_view* out) {
+  if ((uint64_t)first + n > e->nrep) return -1;
+  for (uint32_t i = 0; i < n; ++i) or_get_replica(e, first + i, &out[i]);
+  return 0;
+}
+
 static const outbox_t* last_ob(const or_engine* e, const rep_t* r) { return &r->ob[(e->t + 1) & 1]; }
 
 int or_get_msgs(const or_engine* e, uint32_t rid, uint32_t dst, or_msg_view* out, uint32_t cap) {

@@ -109,6 +109,8 @@ int or_tick(or_engine* e, const or_tick_input* in, int nthreads);
 uint64_t or_tick_count(const or_engine* e);
 
 int or_get_replica(const or_engine* e, uint32_t rid, or_replica_view* out);
+/* Views of replicas first .. first+n-1 (bulk comparisons at full size). */
+int or_get_replicas(const or_engine* e, uint32_t first, uint32_t n, or_replica_view* out);
 /* Messages emitted by `rid` to slot `dst` in the last tick. Returns count; fills up to cap. */
 int or_get_msgs(const or_engine* e, uint32_t rid, uint32_t dst, or_msg_view* out, uint32_t cap);
 /* Inline entry terms of message k (rid → dst). */

@@ -101,6 +101,7 @@ def lib():
         L.or_tick_count.argtypes = [vp]
         L.or_tick_count.restype = u64
         L.or_get_replica.argtypes = [vp, u32, C.POINTER(ReplicaView)]
+        L.or_get_replicas.argtypes = [vp, u32, u32, C.POINTER(ReplicaView)]
         L.or_get_msgs.argtypes = [vp, u32, u32, C.POINTER(MsgView), u32]
         L.or_get_msg_terms.argtypes = [vp, u32, u32, u32, C.POINTER(C.c_uint64), u32]
         L.or_get_entry.argtypes = [vp, u32, u64, C.POINTER(EntryView), C.c_void_p]
@@ -220,6 +221,13 @@ class Oracle:
         for f in ("match", "next", "rsnap", "rstate"):
             d[f] = d[f][:R]
         return d
+
+    def replica_array(self, first=0, n=None):
+        """Views of replicas first .. first+n-1 as a numpy structured array (bulk comparisons)."""
+        n = self.nrep - first if n is None else n
+        buf = (ReplicaView * n)()
+        assert self.L.or_get_replicas(self.h, first, n, buf) == 0
+        return np.ctypeslib.as_array(buf).copy()
 
     def msgs(self, rid, dst) -> list:
         buf = (MsgView * 16)()

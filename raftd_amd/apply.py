@@ -96,18 +96,48 @@ def post_update(app_url: str, b: UpdateBatch, timeout: float = TIMEOUT_S) -> Upd
     return b
 
 
+class ApplyFailed(RuntimeError):
+    """An Update failed earlier: the node must restart (dragonboat stops a node whose state machine
+    Update returns an error); further batches are refused so none is silently skipped."""
+
+
 class Applier:
-    """Drives /UpdateEntries from the engine's committed-entry copy-back after each tick."""
+    """Drives /UpdateEntries from the engine's committed-entry copy-back after each tick.
+
+    Failure contract: the first failed POST (timeout, transport error, status > 299) is
+    fatal — apply() re-raises it and every later call raises ApplyFailed, because the device has
+    already moved past that batch. The node restarts through the WAL path: with
+    rg_config.apply_feedback = 1 and notify=True the engine's `applied` only ever moved for batches
+    the application acknowledged, the restart view starts from the app's /LastLogIndex, and the
+    first tick hands the unacknowledged entries to Update again (raftd_amd/wal.py restart_view)."""
 
     def __init__(self, app_url: str, workers: int = 16, timeout: float = TIMEOUT_S):
         self.app_url = app_url.rstrip("/")
         self.timeout = timeout
         self.pool = ThreadPoolExecutor(max_workers=workers)
+        self.failed = None
 
-    def apply(self, engine, slot_mask: int = 0xFF) -> list:
+    def apply(self, engine, slot_mask: int = 0xFF, notify: bool = False) -> list:
+        """POST the last tick's applied entries of the replicas in slot_mask (one request per
+        replica). notify: once every POST succeeded, report applied = processed for those replicas
+        (rg_notify_applied; config changes and empty entries included — the state machine never
+        sees them, dragonboat's rsm applies them itself)."""
+        if self.failed is not None:
+            raise ApplyFailed(f"an earlier Update failed ({self.failed}); restart the node from its WAL")
         recs, pay = engine.apply_committed(slot_mask)
         bs = batches(recs, pay)
-        return list(self.pool.map(lambda b: post_update(self.app_url, b, self.timeout), bs))
+        try:
+            out = list(self.pool.map(lambda b: post_update(self.app_url, b, self.timeout), bs))
+        except Exception as ex:
+            self.failed = ex
+            raise
+        if notify:
+            import numpy as np
+            va = engine.replica_array()
+            rids = np.array([r for r in range(len(va)) if (slot_mask >> (r % engine.R)) & 1], np.uint32)
+            if len(rids):
+                engine.notify_applied(rids, va["processed"][rids])
+        return out
 
     def close(self):
         self.pool.shutdown(wait=True)

@@ -310,12 +310,18 @@ class DistEngine(_Feeds):
                 p.start(async_op=self.async_ok)
             self.primed = True
 
-    def step_device(self, pt_ptr=0, pc_ptr=0, flags=0):
+    def step_device(self, pt_ptr=0, pc_ptr=0, flags=0, persist=None):
+        """One pipelined step. persist(engine), if given, runs after each half's tick and before
+        that tick's messages are packed and leave the rank: the place for rg_persist_collect + WAL
+        fsync (dragonboat persists a step's Update before its messages go out). Without
+        it this path is not durable (the benchmark's mode)."""
         self.prime()
         for h, p in enumerate(self.parts):
             p.finish()
             g0, _ = self._slices(h)
             p.eng.tick_device(pt_ptr + g0 if pt_ptr else 0, pc_ptr + 4 * g0 if pc_ptr else 0, flags=flags)
+            if persist is not None:
+                persist(p.eng)
             p.start(async_op=self.async_ok)
 
     def drain(self):

@@ -69,10 +69,31 @@ def worker(rank, n, halves, backend):
         pc = np.full(G, 5, np.uint32)
         dpt = torch.tensor(pt, device="cuda")
         dpc = torch.tensor(pc.astype(np.int32), device="cuda")
-        for _ in range(STEADY):
-            de.step_device(dpt.data_ptr(), dpc.data_ptr())
+        # durable pipelined steps: each half's persistence feed is appended to its WAL (fsync) after
+        # its tick and before its messages leave the rank (DistEngine.step_device's persist hook)
+        import tempfile
+        from raftd_amd.wal import WAL, replay
+        tmp = tempfile.mkdtemp(prefix=f"rgwal{rank}_")
+        wals = {id(p.eng): WAL(os.path.join(tmp, f"half{h}.wal")) for h, p in enumerate(de.parts)}
+        de.drain()
+        for p in de.parts:
+            wals[id(p.eng)].append(0, *p.eng.persist_collect(full=True), CFG["payload_bytes"])
+        steps = [0]
+
+        def persist(e):
+            wals[id(e)].append(steps[0] + 1, *e.persist_collect(), CFG["payload_bytes"])
+
+        for k in range(STEADY):
+            steps[0] = k
+            de.step_device(dpt.data_ptr(), dpc.data_ptr(), persist=persist)
         de.drain()
         de.sync()
+        for p in de.parts:  # the WAL holds every replica's hard state and log as the engine does
+            logs = replay(wals[id(p.eng)].path, R)
+            for lr, v in enumerate(p.eng.replicas()):
+                s = logs[p.eng.global_id(lr)[1]].state
+                assert (s["term"], s["vote"], s["commit"], s["last"], s["marker"]) == \
+                    (v["term"], v["vote"], v["committed"], v["last"], v["marker"]), (rank, lr)
         allv = [None] * n
         dist.all_gather_object(allv, snapshot(de))
         steady = {k: x for d in allv for k, x in d.items()}

@@ -98,3 +98,40 @@ def test_high_status_code(app):
     b = batches(*fake_batch())[0]
     with pytest.raises(HighStatusCode, match="high status code \\(500\\): boom"):
         post_update(app, b)
+
+
+def test_failed_update_is_fatal(app):
+    """after a failed Update the applier refuses every later batch (the device has moved
+    past it; the node restarts through the WAL, which hands the batch to Update again)."""
+    from raftd_amd.apply import ApplyFailed
+    ap = Applier(app, workers=2)
+    App.status = 500
+    with pytest.raises(HighStatusCode):
+        ap.apply(FakeEngine())
+    App.status = 200
+    n = len(App.seen)
+    with pytest.raises(ApplyFailed):
+        ap.apply(FakeEngine())
+    assert len(App.seen) == n  # nothing posted after the failure
+    ap.close()
+
+
+def test_notify_after_acknowledged_updates(app):
+    """notify=True reports applied = processed for the replicas of the slot mask, and only after every
+    POST of the tick succeeded."""
+    class Eng(FakeEngine):
+        R = 3
+        notified = None
+
+        def replica_array(self):
+            a = np.zeros(12, [("processed", "<u8")])
+            a["processed"] = np.arange(12) + 100
+            return a
+
+        def notify_applied(self, rids, idx):
+            Eng.notified = (list(rids), list(idx))
+
+    ap = Applier(app, workers=2)
+    ap.apply(Eng(), slot_mask=0b010, notify=True)
+    assert Eng.notified == ([1, 4, 7, 10], [101, 104, 107, 110])
+    ap.close()

@@ -178,3 +178,75 @@ def test_c3_five_replicas_eight_ranks_full_size():
                                b, n, R, t, check_entries=(t == 15))
     assert cl.wire_bytes > 4 * G * 64 * 256  # every follower entry crossed ranks
     assert cl.sum_committed() >= G * (R + 1 + 8 * 64)  # slot-0 replicas committed the batches
+
+
+def test_c2_steady_state_full_shard_set():
+    """C2 at its stated size: 4,096 groups x 3, steady-state leaders, 64-entry batches of 256-B
+    entries every tick, against the oracle of ALL 4,096 groups — every replica view every tick,
+    messages and the newest entries (with payload) on sampled groups — for 48 ticks, past one wrap
+    of the 2,048-entry log ring."""
+    G, R, E, L = 4096, 3, 64, 2048
+    cfg = dict(groups=G, replicas=R, log_capacity=L, payload_bytes=256, max_entries_per_msg=E, seed=0xC2)
+    gpu, ora = make("gpu", **cfg), make("c", **cfg)
+    camp = np.zeros(G * R, np.uint8)
+    camp[0::R] = 1
+    for e in (gpu, ora):
+        e.bootstrap()
+    for t, ins in enumerate([{}, dict(campaign=camp), {}, {}, {}, {}]):
+        gpu.tick(**ins)
+        ora.tick(threads=16, **ins)
+    pt, pc = np.zeros(G, np.uint8), np.full(G, E, np.uint32)
+    sample = list(range(0, G, 97))
+    for t in range(48):
+        gpu.tick(pt, pc)
+        ora.tick(pt, pc, threads=16)
+        ga, oa = gpu.replica_array(), ora.replica_array()
+        if ga.tobytes() != oa.tobytes():
+            bad = [r for r in range(G * R) if ga[r].tobytes() != oa[r].tobytes()][:3]
+            raise AssertionError(f"tick {t}: replicas {bad} differ: {[(gpu.replica(r), ora.replica(r)) for r in bad]}")
+        if t % 8 == 7:
+            for g in sample:
+                for s in range(R):
+                    for d in range(R):
+                        assert gpu.msgs(g * R + s, d) == ora.msgs(g * R + s, d), (t, g, s, d)
+            for g in sample[::4]:
+                for s in range(R):
+                    v = ora.replica(g * R + s)
+                    lo = max(v["marker"] + 1, v["last"] - NEWEST + 1)
+                    got = gpu.entries(g * R + s, lo, v["last"] - lo + 1, with_payload=True)
+                    assert got == [ora.entry(g * R + s, i, with_payload=True) for i in range(lo, v["last"] + 1)]
+    v = gpu.replica_array()
+    assert (v["err"] == 0).all() and (v["last"] > L).all()  # every log wrapped the ring
+    assert (v["committed"][0::R] >= R + 1 + 46 * E).all()  # slot-0 leaders committed the batches (one in flight)
+
+
+def test_c3_snapshot_entries_1000():
+    """C3's shape with raftd's SnapshotEntries 1000 / CompactionOverhead 5 and a 2,048-entry ring
+    (5 replicas spread over 8 ranks, 64 x 256-B entries per tick): snapshots and compaction happen
+    twice per replica within the run. 8,192 groups (1,024 columns per rank) so that the eight ranks'
+    engines fit this one GPU; on an 8-GPU node each rank holds 8,192 columns at the same ring size."""
+    from raftd_amd.cluster import LoopbackCluster
+    G, R, N, W = 8192, 5, 8, 256
+    cfg = dict(replicas=R, log_capacity=2048, payload_bytes=256, max_entries_per_msg=64, snapshot_entries=1000,
+               compaction_overhead=5, seed=0xC35)
+    cl = LoopbackCluster(ranks=N, groups=G, **cfg)
+    wins = [(0, W), (G - W, W)]
+    oras = [make("c", groups=n, group_base=b, **cfg) for b, n in wins]
+    cl.bootstrap()
+    for o in oras:
+        o.bootstrap()
+    camp = np.zeros(G * R, np.uint8)
+    camp[0::R] = 1
+    pt, pc = np.zeros(G, np.uint8), np.full(G, 64, np.uint32)
+    for t in range(44):
+        ins = dict(campaign=camp) if t == 1 else (dict(prop_target=pt, prop_count=pc) if t >= 6 else {})
+        cl.tick(**ins)
+        for (b, n), o in zip(wins, oras):
+            o.tick(**{k: v[b * (R if k == "campaign" else 1):(b + n) * (R if k == "campaign" else 1)]
+                      for k, v in ins.items()}, threads=8)
+        if t in (20, 43):
+            for (b, n), o in zip(wins, oras):
+                compare_window(cl.replica, cl.msgs, lambda gr, lo, k: cl.entries(gr, lo, k, with_payload=True), o,
+                               b, n, R, t, check_entries=(t == 43))
+    v = cl.replica(0)
+    assert v["snap_index"] >= 2000 and v["marker"] == v["snap_index"] - 5 and v["last"] > 2048, v
