@@ -11,7 +11,7 @@ run() {  # run NAME ARGS...
 import json;d=json.loads(open('gpurun_out/shape_$n.log').read().strip().splitlines()[-1])
 r=d['roofline']
 print('$n', '$*', 'value', round(d['value']/1e6,2), 'M ms', round(d['ms_per_step'],4), {k: round(v,4) for k,v in d['kernels_ms'].items()},
-      'bulkGBs', round(r['achieved']), 'frac', round(r['frac'],3), 'commits/s', round(d['commits_per_sec']/1e9,3), 'G err', d['invariant_errors_in_sample'],
+      'bulkGBs', round(r['achieved']), 'frac', round(r['frac'],3), 'commits/s', round(d['commits_per_sec']/1e9,3), 'G err', d['replicas_with_invariant_errors'],
       'dev GB', round(d['device_bytes']/1e9,1))"
 }
 run c2 --groups 4096 --steps 100 --warmup 10
