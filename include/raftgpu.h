@@ -52,7 +52,7 @@ enum {
 enum {
   RG_MSG_NOOP = 4, RG_MSG_PROPOSE = 7, RG_MSG_REPLICATE = 12, RG_MSG_REPLICATE_RESP = 13,
   RG_MSG_REQUEST_VOTE = 14, RG_MSG_REQUEST_VOTE_RESP = 15, RG_MSG_INSTALL_SNAPSHOT = 16,
-  RG_MSG_HEARTBEAT = 17, RG_MSG_HEARTBEAT_RESP = 18
+  RG_MSG_HEARTBEAT = 17, RG_MSG_HEARTBEAT_RESP = 18, RG_MSG_READ_INDEX = 19, RG_MSG_READ_INDEX_RESP = 20
 };
 enum { RG_FOLLOWER = 0, RG_CANDIDATE = 1, RG_LEADER = 2 };
 enum { RG_REMOTE_RETRY = 0, RG_REMOTE_WAIT = 1, RG_REMOTE_REPLICATE = 2, RG_REMOTE_SNAPSHOT = 3 };
@@ -207,6 +207,22 @@ typedef struct rg_proposal {
   uint64_t first;  /* index of the batch's first Cmd in lens[] */
 } rg_proposal;
 
+/* ReadIndex (rg_read_index): replica `slot` of shard `group` asks for a linearizable read point
+ * under a non-zero context (dragonboat's SystemCtx; the shim batches the tick's client reads of a
+ * replica under one context). */
+typedef struct rg_read_request {
+  uint64_t group; /* GLOBAL shard id */
+  uint32_t slot, _pad;
+  uint64_t ctx;
+} rg_read_request;
+/* A read made ready (dragonboat's ReadyToRead): serve the reads of `ctx` — IOnDiskStateMachine.Lookup,
+ * raftd's POST /Read (raft/state_machine.go:168-184) — once the replica has applied `index`. */
+typedef struct rg_read_ready {
+  uint64_t group;
+  uint32_t replica_id, rid;
+  uint64_t ctx, index;
+} rg_read_ready;
+
 typedef struct rg_engine rg_engine;
 
 int rg_create(const rg_config* cfg, rg_engine** out);
@@ -317,6 +333,17 @@ int rg_persist_collect(rg_engine* e, int full, rg_persist_state* states, uint64_
  * replica in device order (slot by slot, shards ascending within a slot), compacted on the device and copied back by one hipMemcpyAsync. *n = the count;
  * if *n > cap nothing is copied and RG_EFULL is returned. Synchronous. */
 int rg_snapshot_events(rg_engine* e, uint32_t slot_mask, rg_snapshot_event* events, uint64_t cap, uint64_t* n);
+/* Stage ReadIndex requests for the next tick (dragonboat's NodeHost.ReadIndex → Peer.ReadIndex): a
+ * leader that has committed an entry in its term records its commit index and confirms leadership
+ * with one heartbeat round carrying the context; a follower forwards the request to its leader,
+ * which answers with a ReadIndexResp once confirmed. One pending request per leader (another is
+ * dropped, counted in drops; the shim retries). RG_EINVAL: bad shard / slot, ctx 0, or a replica
+ * hosted by another rank (nothing staged). A later request for the same replica in the same tick
+ * replaces the earlier one. */
+int rg_read_index(rg_engine* e, const rg_read_request* reqs, size_t n);
+/* Reads made ready in the last tick for replicas whose slot bit is set, one per replica at most, in
+ * device order; compacted on the device, one hipMemcpyAsync. *n = count; RG_EFULL if > cap. */
+int rg_read_index_results(rg_engine* e, uint32_t slot_mask, rg_read_ready* out, uint64_t cap, uint64_t* n);
 /* Peer.NotifyRaftLastApplied for n local replicas: replica rids[k]'s state machine has applied
  * through index[k] (<= its processed index — config changes and empty entries included, which the
  * state machine never sees). With rg_config.apply_feedback = 1 this is how `applied` moves: it gates

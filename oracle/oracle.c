@@ -56,6 +56,10 @@ typedef struct {
    * (rsm → IOnDiskStateMachine.Update); a range restored from a snapshot does not */
   uint64_t apply_lo, restored_at;
   int took; /* a snapshot was taken at the end of the last step */
+  /* ReadIndex: the leader's pending request (ctx 0 = none), and the read made ready in a step */
+  uint64_t ri_ctx, ri_index;
+  uint32_t ri_acks, ri_from;
+  uint64_t rd_ctx, rd_index, rd_tick; /* rd_tick = step + 1 when it became ready */
 } rep_t;
 
 struct or_engine {
@@ -70,6 +74,8 @@ struct or_engine {
   ent_t* stg_ents;    /* [G][E] len per entry */
   uint8_t* stg_pay;   /* [G][E][P] Cmd bytes, zero-padded */
   int staged;
+  uint64_t* rd_req;   /* [G*R] ReadIndex contexts staged for the next tick (0 none) */
+  int rd_staged;
 };
 
 /* ---------------------------------------------------------------- helpers */
@@ -182,7 +188,7 @@ static void arena_reserve(const or_engine* e, outbox_t* ob, size_t need) {
 static msg_t* send_msg(or_engine* e, rep_t* r, or_msg_view* h) {
   uint32_t dst = slot_of(h->to);
   h->from = (uint8_t)id_of(r->s);
-  if (h->type != OR_PROPOSE && h->type != OR_REQUEST_VOTE) h->term = r->term;
+  if (h->type != OR_PROPOSE && h->type != OR_REQUEST_VOTE && h->type != OR_READ_INDEX) h->term = r->term;
   outbox_t* ob = cur_ob(e, r);
   uint32_t n = ob->emitted[dst]++;
   if (lost(e, r, dst, n) || ob->n[dst] >= e->c.max_msgs_per_pair) {
@@ -215,6 +221,7 @@ static void reset(or_engine* e, rep_t* r, uint64_t t) {
   }
   r->match[r->s] = r->last;
   r->active = 0;
+  r->ri_ctx = 0; /* readIndex.reset */
 }
 
 static void become_follower(or_engine* e, rep_t* r, uint64_t t, uint64_t leader) {
@@ -597,11 +604,74 @@ static void handle_leader_replicate_resp(or_engine* e, rep_t* r, const or_msg_vi
   }
 }
 
+static void read_ready(or_engine* e, rep_t* r, uint64_t ctx, uint64_t index) { /* addReadyToRead */
+  r->rd_ctx = ctx;
+  r->rd_index = index;
+  r->rd_tick = e->t + 1;
+}
+
+/* the leader's confirmed read goes to its requester: itself, or a follower (ReadIndexResp) */
+static void read_confirmed(or_engine* e, rep_t* r, uint64_t ctx, uint64_t index, uint32_t from_slot) {
+  if (from_slot == r->s) {
+    read_ready(e, r, ctx, index);
+  } else {
+    or_msg_view h;
+    memset(&h, 0, sizeof h);
+    h.type = OR_READ_INDEX_RESP;
+    h.to = (uint8_t)id_of(from_slot);
+    h.log_index = index;
+    h.hint = ctx;
+    send_msg(e, r, &h);
+  }
+}
+
 static void handle_leader_heartbeat_resp(or_engine* e, rep_t* r, const or_msg_view* m) {
   uint32_t f = slot_of(m->from);
   r->active |= 1u << f;
   if (r->rstate[f] == OR_WAIT) r->rstate[f] = OR_RETRY;
   if (r->match[f] < r->last) send_replicate(e, r, f);
+  if (m->hint != 0 && m->hint == r->ri_ctx) { /* readIndex.confirm */
+    r->ri_acks |= 1u << f;
+    if (popc(r->ri_acks) >= quorum(e)) {
+      uint64_t ctx = r->ri_ctx;
+      r->ri_ctx = 0;
+      read_confirmed(e, r, ctx, r->ri_index, r->ri_from);
+    }
+  }
+}
+
+/* ReadIndex{hint = ctx} from slot m->from (itself, or a follower that forwarded it) */
+static void handle_read_index(or_engine* e, rep_t* r, const or_msg_view* m) {
+  uint32_t f = slot_of(m->from);
+  if (r->role == OR_LEADER) {
+    if (e->c.replicas == 1) {
+      read_confirmed(e, r, m->hint, r->committed, f);
+    } else if (term_of(e, r, r->committed) != r->term || r->ri_ctx != 0) {
+      r->drops++; /* no entry committed in this term yet (thesis §6.4), or a read already pending */
+    } else {
+      r->ri_ctx = m->hint;
+      r->ri_index = r->committed;
+      r->ri_acks = 1u << r->s;
+      r->ri_from = f;
+      for (uint32_t i = 0; i < e->c.replicas; ++i) { /* broadcastHeartbeatMessageWithHint */
+        if (i == r->s) continue;
+        or_msg_view h;
+        memset(&h, 0, sizeof h);
+        h.type = OR_HEARTBEAT;
+        h.to = (uint8_t)id_of(i);
+        h.commit = u64min(r->match[i], r->committed);
+        h.hint = m->hint;
+        send_msg(e, r, &h);
+      }
+    }
+  } else if (r->role == OR_FOLLOWER && r->leader != 0 && f == r->s) {
+    or_msg_view h = *m;
+    h.to = (uint8_t)r->leader;
+    h.term = 0;
+    send_msg(e, r, &h);
+  } else {
+    r->drops++;
+  }
 }
 
 static void handle_leader_check_quorum(or_engine* e, rep_t* r) {
@@ -688,7 +758,7 @@ static void tick(or_engine* e, rep_t* r) {
 }
 
 static int is_leader_msg(uint32_t t) {
-  return t == OR_REPLICATE || t == OR_INSTALL_SNAPSHOT || t == OR_HEARTBEAT;
+  return t == OR_REPLICATE || t == OR_INSTALL_SNAPSHOT || t == OR_HEARTBEAT || t == OR_READ_INDEX_RESP;
 }
 
 static void handle(or_engine* e, rep_t* r, const msg_in_t* mi) {
@@ -752,6 +822,14 @@ static void handle(or_engine* e, rep_t* r, const msg_in_t* mi) {
       break;
     case OR_HEARTBEAT_RESP:
       if (r->role == OR_LEADER) handle_leader_heartbeat_resp(e, r, m);
+      break;
+    case OR_READ_INDEX: handle_read_index(e, r, m); break;
+    case OR_READ_INDEX_RESP:
+      if (r->role == OR_FOLLOWER) {
+        r->election_tick = 0; /* a leader message: like Heartbeat */
+        r->leader = m->from;
+        read_ready(e, r, m->hint, m->log_index);
+      }
       break;
     case OR_REQUEST_VOTE: handle_node_request_vote(e, r, m); break;
     case OR_REQUEST_VOTE_RESP:
@@ -819,6 +897,15 @@ static void step_replica(or_engine* e, rep_t* r) {
     mi.pay = ppay;
     handle(e, r, &mi);
   }
+  /* 4b. ReadIndex input */
+  if (e->rd_staged && e->rd_req[rid]) {
+    msg_in_t mi;
+    memset(&mi, 0, sizeof mi);
+    mi.h.type = OR_READ_INDEX;
+    mi.h.from = (uint8_t)id_of(r->s);
+    mi.h.hint = e->rd_req[rid];
+    handle(e, r, &mi);
+  }
   /* 5. apply + snapshot + compaction */
   /* GetUpdate.CommittedEntries = (processed, committed] (a restored range excluded), then
    * commitUpdate: processed = committed; applied follows unless the state machine reports it */
@@ -876,7 +963,30 @@ int or_tick(or_engine* e, const or_tick_input* in, int nthreads) {
     memset(e->stg_n, 0, (size_t)e->c.groups * 4);
     e->staged = 0;
   }
+  if (e->rd_staged) {
+    memset(e->rd_req, 0, (size_t)e->nrep * 8);
+    e->rd_staged = 0;
+  }
   return 0;
+}
+
+int or_read_index(or_engine* e, const or_read_request* q, size_t n) {
+  for (size_t i = 0; i < n; ++i)
+    if (q[i].group < e->c.group_base || q[i].group >= (uint64_t)e->c.group_base + e->c.groups ||
+        q[i].slot >= e->c.replicas || q[i].ctx == 0)
+      return -1;
+  for (size_t i = 0; i < n; ++i) e->rd_req[(q[i].group - e->c.group_base) * e->c.replicas + q[i].slot] = q[i].ctx;
+  if (n) e->rd_staged = 1;
+  return 0;
+}
+
+int or_get_read_ready(const or_engine* e, uint32_t rid, uint64_t* ctx, uint64_t* index) {
+  if (rid >= e->nrep) return -1;
+  const rep_t* r = &e->reps[rid];
+  if (r->rd_tick != e->t) return 0; /* not made ready in the last step */
+  if (ctx) *ctx = r->rd_ctx;
+  if (index) *index = r->rd_index;
+  return 1;
 }
 
 int or_propose(or_engine* e, const or_proposal* p, size_t n, const uint8_t* payload, const uint32_t* lens) {
@@ -952,6 +1062,7 @@ int or_create(const or_config* cfg, or_engine** out) {
   e->stg_n = (uint32_t*)calloc(c->groups, 4);
   e->stg_ents = (ent_t*)calloc((size_t)c->groups * c->max_entries_per_msg, sizeof(ent_t));
   e->stg_pay = (uint8_t*)calloc((size_t)c->groups * c->max_entries_per_msg * (c->payload_bytes ? c->payload_bytes : 1), 1);
+  e->rd_req = (uint64_t*)calloc((size_t)c->groups * c->replicas, 8);
   e->reps = (rep_t*)calloc(e->nrep, sizeof(rep_t));
   for (uint32_t i = 0; i < e->nrep; ++i) {
     rep_t* r = &e->reps[i];
@@ -986,6 +1097,7 @@ void or_destroy(or_engine* e) {
   free(e->stg_n);
   free(e->stg_ents);
   free(e->stg_pay);
+  free(e->rd_req);
   free(e);
 }
 
@@ -1123,6 +1235,7 @@ int or_import_replica(or_engine* e, uint32_t rid, const or_replica_view* v, cons
   r->cap_base = v->cap_base;
   r->restored_at = 0;
   r->took = 0;
+  r->ri_ctx = r->rd_tick = 0;
   r->role = v->role;
   r->election_tick = v->election_tick;
   r->heartbeat_tick = v->heartbeat_tick;

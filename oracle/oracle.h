@@ -29,7 +29,8 @@ extern "C" {
 enum {
   OR_LOCAL_TICK = 0, OR_ELECTION = 1, OR_LEADER_HEARTBEAT = 2, OR_NOOP = 4, OR_PROPOSE = 7,
   OR_CHECK_QUORUM = 10, OR_REPLICATE = 12, OR_REPLICATE_RESP = 13, OR_REQUEST_VOTE = 14,
-  OR_REQUEST_VOTE_RESP = 15, OR_INSTALL_SNAPSHOT = 16, OR_HEARTBEAT = 17, OR_HEARTBEAT_RESP = 18
+  OR_REQUEST_VOTE_RESP = 15, OR_INSTALL_SNAPSHOT = 16, OR_HEARTBEAT = 17, OR_HEARTBEAT_RESP = 18,
+  OR_READ_INDEX = 19, OR_READ_INDEX_RESP = 20
 };
 enum { OR_FOLLOWER = 0, OR_CANDIDATE = 1, OR_LEADER = 2 };
 enum { OR_RETRY = 0, OR_WAIT = 1, OR_REPLICATE_ST = 2, OR_SNAPSHOT = 3 };
@@ -141,6 +142,18 @@ int or_get_applied(const or_engine* e, uint32_t rid, uint64_t* index, or_entry_v
  * (<= processed, else -1). With apply_feedback = 1 this is the only way `applied` moves (besides a
  * restored snapshot); it gates campaigns (hasConfigChangeToApply) and snapshots. */
 int or_notify_applied(or_engine* e, uint32_t rid, uint64_t index);
+/* ReadIndex (dragonboat's ReadIndex protocol, Raft thesis §6.4) for the next tick: replica `slot` of
+ * shard `group` asks for a linearizable read point under context ctx (non-zero). At most one request
+ * per replica per tick (a later one replaces an earlier). -1 invalid. */
+typedef struct or_read_request {
+  uint64_t group; /* global shard id */
+  uint32_t slot, _pad;
+  uint64_t ctx;   /* non-zero request context (dragonboat's SystemCtx) */
+} or_read_request;
+int or_read_index(or_engine* e, const or_read_request* reqs, size_t n);
+/* The read replica rid's last step made ready (ReadyToRead): returns 1 with its ctx and read index
+ * (serve it once applied >= index), 0 if none. */
+int or_get_read_ready(const or_engine* e, uint32_t rid, uint64_t* ctx, uint64_t* index);
 /* Snapshot events of rid's last step (the oracle side of rg_snapshot_events): OR_SNAP_* bits. */
 #define OR_SNAP_TAKEN 1
 #define OR_SNAP_RESTORED 2

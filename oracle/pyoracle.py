@@ -69,6 +69,10 @@ class Proposal(C.Structure):
     _fields_ = [("group", C.c_uint64), ("slot", C.c_uint32), ("count", C.c_uint32), ("first", C.c_uint64)]
 
 
+class ReadRequest(C.Structure):
+    _fields_ = [("group", C.c_uint64), ("slot", C.c_uint32), ("_pad", C.c_uint32), ("ctx", C.c_uint64)]
+
+
 class TickInput(C.Structure):
     _fields_ = [("prop_target", C.c_void_p), ("prop_count", C.c_void_p), ("campaign", C.c_void_p),
                 ("isolate", C.c_void_p), ("flags", C.c_uint32)]
@@ -112,6 +116,8 @@ def lib():
                                         C.c_void_p]
         L.or_propose.argtypes = [vp, C.POINTER(Proposal), C.c_size_t, C.c_void_p, C.c_void_p]
         L.or_notify_applied.argtypes = [vp, u32, u64]
+        L.or_read_index.argtypes = [vp, C.POINTER(ReadRequest), C.c_size_t]
+        L.or_get_read_ready.argtypes = [vp, u32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.or_tick.restype = C.c_int
         L.or_deliver.argtypes = [vp, u32, C.POINTER(MsgView)]
         L.or_payload.argtypes = [vp, u32, u32, u32, C.c_void_p]
@@ -298,6 +304,18 @@ class Oracle:
                                       None if ln is None or not ln.size else ln.ctypes.data)
         if rc != 0:
             raise ValueError("or_import_replica failed")
+
+    def read_index(self, reqs) -> int:
+        """Stage ReadIndex requests [(global group, slot, ctx)] for the next tick (or_read_index)."""
+        arr = (ReadRequest * max(len(reqs), 1))()
+        for i, (g, s, ctx) in enumerate(reqs):
+            arr[i].group, arr[i].slot, arr[i].ctx = g, s, ctx
+        return self.L.or_read_index(self.h, arr, len(reqs))
+
+    def read_ready(self, rid):
+        """(ctx, index) of the read replica rid made ready in the last tick, or None."""
+        c, i = C.c_uint64(), C.c_uint64()
+        return (c.value, i.value) if self.L.or_get_read_ready(self.h, rid, C.byref(c), C.byref(i)) == 1 else None
 
     def notify_applied(self, rid, index) -> int:
         """or_notify_applied (Peer.NotifyRaftLastApplied): 0, or -1 if index > processed."""

@@ -27,10 +27,11 @@ M64 = (1 << 64) - 1
 LOCAL_TICK, ELECTION, LEADER_HEARTBEAT, NOOP, PROPOSE = 0, 1, 2, 4, 7
 CHECK_QUORUM, REPLICATE, REPLICATE_RESP, REQUEST_VOTE, REQUEST_VOTE_RESP = 10, 12, 13, 14, 15
 INSTALL_SNAPSHOT, HEARTBEAT, HEARTBEAT_RESP = 16, 17, 18
+READ_INDEX, READ_INDEX_RESP = 19, 20
 FOLLOWER, CANDIDATE, LEADER = 0, 1, 2
 RETRY, WAIT, REPL, SNAP = 0, 1, 2, 3
 ERR_CONFLICT, ERR_BEYOND, ERR_RING, ERR_CRC, ERR_EMPTY_SNAP = 1, 2, 4, 8, 16
-LEADER_MSGS = (REPLICATE, INSTALL_SNAPSHOT, HEARTBEAT)
+LEADER_MSGS = (REPLICATE, INSTALL_SNAPSHOT, HEARTBEAT, READ_INDEX_RESP)
 
 
 def mix64(z: int) -> int:
@@ -133,6 +134,8 @@ class Replica:
         self.remotes = []
         self.out = {}
         self.emitted = {}
+        self.pending_read = None  # leader: [ctx, index, acks set, requester slot]
+        self.ready_read = None    # (tick, ctx, index) of the read made ready in a step
 
     # -- log (entryLog) --
     @property
@@ -162,7 +165,7 @@ class Replica:
     def send(self, m):
         c = self.sim.cfg
         m["frm"] = self.id
-        if m["type"] not in (PROPOSE, REQUEST_VOTE):
+        if m["type"] not in (PROPOSE, REQUEST_VOTE, READ_INDEX):
             m["term"] = self.term
         d = m["to"] - 1
         n = self.emitted.get(d, 0)
@@ -187,6 +190,7 @@ class Replica:
         self.remotes = [Remote(0, self.last + 1) for _ in range(self.sim.R)]
         self.remotes[self.s].match = self.last
         self.active = set()
+        self.pending_read = None
 
     def become_follower(self, t, leader):
         self.role = FOLLOWER
@@ -279,6 +283,39 @@ class Replica:
             rp.state = RETRY
         if rp.match < self.last:
             self.send_replicate(f)
+        pr = self.pending_read
+        if m["hint"] and pr is not None and m["hint"] == pr[0]:
+            pr[2].add(f)
+            if len(pr[2]) >= self.sim.quorum:
+                self.pending_read = None
+                self.read_confirmed(pr[0], pr[1], pr[3])
+
+    # -- ReadIndex (Raft thesis §6.4) --
+    def read_confirmed(self, ctx, index, slot):
+        if slot == self.s:
+            self.ready_read = (self.sim.t, ctx, index)
+        else:
+            self.send(msg(READ_INDEX_RESP, slot + 1, log_index=index, hint=ctx))
+
+    def on_read_index(self, m):
+        f = m["frm"] - 1
+        if self.role == LEADER:
+            if self.sim.R == 1:
+                self.read_confirmed(m["hint"], self.committed, f)
+            elif self.term_at(self.committed) != self.term or self.pending_read is not None:
+                self.drops += 1
+            else:
+                self.pending_read = [m["hint"], self.committed, {self.s}, f]
+                for i in range(self.sim.R):
+                    if i != self.s:
+                        self.send(msg(HEARTBEAT, i + 1, commit=min(self.remotes[i].match, self.committed),
+                                      hint=m["hint"]))
+        elif self.role == FOLLOWER and self.leader != 0 and f == self.s:
+            fw = dict(m)
+            fw.update(to=self.leader, term=0)
+            self.send(fw)
+        else:
+            self.drops += 1
 
     # -- follower --
     def on_replicate(self, m):
@@ -446,6 +483,13 @@ class Replica:
         elif t == HEARTBEAT_RESP:
             if role == LEADER:
                 self.on_heartbeat_resp(m)
+        elif t == READ_INDEX:
+            self.on_read_index(m)
+        elif t == READ_INDEX_RESP:
+            if role == FOLLOWER:
+                self.etick = 0
+                self.leader = m["frm"]
+                self.ready_read = (self.sim.t, m["hint"], m["log_index"])
         elif t == REQUEST_VOTE:
             self.on_request_vote(m)
         elif t == REQUEST_VOTE_RESP:
@@ -482,6 +526,20 @@ class Sim:
         self.reps = [Replica(self, g, s) for g in range(self.G) for s in range(self.R)]
         self._pay = {}
         self.staged = {}  # window group -> (slot, [cmd bytes]) for the next tick (propose)
+        self.reads = {}   # window rid -> ReadIndex ctx for the next tick
+
+    def read_index(self, reqs):
+        base = self.cfg["group_base"]
+        for g, s, ctx in reqs:
+            if not (base <= g < base + self.G) or s >= self.R or ctx == 0:
+                return -1
+        for g, s, ctx in reqs:
+            self.reads[(g - base) * self.R + s] = ctx
+        return 0
+
+    def read_ready(self, rid):
+        rr = self.reps[rid].ready_read
+        return (rr[1], rr[2]) if rr is not None and rr[0] == self.t - 1 else None
 
     def propose(self, batches):
         """Stage caller proposals (group, slot, [cmds]) for the next tick; all or nothing:
@@ -535,6 +593,7 @@ class Sim:
         if prop_target is not None and self.staged:
             raise ValueError("tick-input proposals while caller proposals are staged")
         staged, self.staged = self.staged, {}
+        reads, self.reads = self.reads, {}
         self.isolate = isolate
         inbox = {id(r): [] for r in self.reps}
         for r in self.reps:  # deliver last tick's outboxes
@@ -568,6 +627,8 @@ class Sim:
                     hm = sum(1 << k for k, x in enumerate(cmds) if x)
                     r.handle(msg(PROPOSE, r.id, frm=r.id, nent=len(cmds), hint=hm, src_a=slab, src_b=0,
                                  ents=tuple(Entry(0, 0, x) for x in cmds)))
+                if reads.get(rid):
+                    r.handle(msg(READ_INDEX, r.id, frm=r.id, hint=reads[rid]))
                 r.processed = r.committed  # handed to the state machine this step
                 if not self.cfg["apply_feedback"]:
                     r.applied = r.processed
@@ -618,6 +679,7 @@ class Sim:
         resp = view.get("responded", 0)
         r.votes = {k: bool(g >> k & 1) for k in range(8) if resp >> k & 1}
         r.active = {k for k in range(8) if view.get("active", 0) >> k & 1}
+        r.pending_read = r.ready_read = None
         r.log = []
         for k, t in enumerate(terms):
             ty = 0 if types is None else types[k]

@@ -473,6 +473,29 @@ class LoopbackCluster(_Feeds):
             k, lr = self.loc[int(r)]
             self.engines[k].notify_applied([lr], [int(i)])
 
+    def read_index(self, reqs):
+        """rg_read_index on the rank hosting each request's replica (cluster group ids)."""
+        per = [[] for _ in range(self.N)]
+        for g, s, ctx in reqs:
+            gg = g + self.rid0 // self.R
+            per[rank_of(gg, s, self.N)].append((gg, s, ctx))
+        for k, b in enumerate(per):
+            if b:
+                self.engines[k].read_index(b)
+
+    def read_ready_all(self) -> dict:
+        """{cluster rid: (ctx, index)} for the reads made ready in the last tick, over all ranks."""
+        back = {kl: r for r, kl in enumerate(self.loc)}
+        out = {}
+        for k, e in enumerate(self.engines):
+            for lr, v in e.read_ready_all().items():
+                out[back[(k, lr)]] = v
+        return out
+
+    def read_ready(self, rid):
+        """(ctx, index) made ready for cluster replica rid in the last tick, or None."""
+        return self.read_ready_all().get(rid)
+
     def propose(self, batches):
         """rg_propose on the rank hosting each batch's replica (global group, slot)."""
         per = [[] for _ in range(self.N)]

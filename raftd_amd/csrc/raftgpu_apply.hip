@@ -230,4 +230,38 @@ hipError_t launch_snap_gather(const SnapParams& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// ================================================================== ReadIndex results
+// reads made ready in the last tick: RD_TICK == the number of ticks run (read_ready stores tick + 1)
+__global__ void read_count_kernel(SnapParams a) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= a.nrep) return;
+  a.cnt[q] = ((a.slot_mask >> (q / a.G)) & 1u) && a.rdst[(uint64_t)RD_TICK * a.nrep + q] == a.tick ? 1u : 0u;
+}
+
+hipError_t launch_read_count(const SnapParams& a, uint64_t* total, hipStream_t st) {
+  hipLaunchKernelGGL(read_count_kernel, dim3((a.nrep + 255) / 256), dim3(256), 0, st, a);
+  hipError_t r = launch_scan_u32(a.cnt, a.nrep, a.bsum, a.off, st);
+  if (r != hipSuccess) return r;
+  hipLaunchKernelGGL(apply_total_kernel, dim3(1), dim3(1), 0, st, a.off, a.nrep, total);
+  return hipGetLastError();
+}
+
+__global__ void read_gather_kernel(SnapParams a) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= a.nrep || !a.cnt[q]) return;
+  const uint32_t s = q / a.G, j = q - s * a.G;
+  rg_read_ready r;
+  r.group = pl_group(a.pl, s, j);
+  r.replica_id = s + 1;
+  r.rid = j * a.R + s;
+  r.ctx = a.rdst[(uint64_t)RD_CTX * a.nrep + q];
+  r.index = a.rdst[(uint64_t)RD_INDEX * a.nrep + q];
+  reinterpret_cast<rg_read_ready*>(a.out)[a.off[q]] = r;
+}
+
+hipError_t launch_read_gather(const SnapParams& a, hipStream_t st) {
+  hipLaunchKernelGGL(read_gather_kernel, dim3((a.nrep + 255) / 256), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
 }  // namespace rg

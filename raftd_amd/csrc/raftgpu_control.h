@@ -7,6 +7,13 @@
 
 #include <type_traits>
 
+// Measurement variants of the control step, off in the product (each changes the
+// kernel's register allocation, and builds with them faulted on the GPU while the same code
+// replayed clean on the CPU under ASan, UBSan and MSan; the product keeps the r01 allocation):
+//   RG_CTL_FASTREP   a leader builds the Replicate of its own same-step append from registers
+//   RG_CTL_FRESH     write_entries' fresh-index path (pointer-stepped ring slots, no hull)
+//   RG_CTL_HDRBATCH  handle() loads all eight header words of a message up front
+
 // entries per load batch in the control kernel's term copies (write_entries, send_replicate)
 #ifndef RG_CTL_BATCH
 #define RG_CTL_BATCH 8
@@ -15,8 +22,13 @@
 // RG_CTL_PROFILE (measurement builds): shader-clock stamps at the phase boundaries of a step
 #if defined(RG_CTL_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
 #define RG_STAMP(i) (stamps[i] = (uint32_t)__builtin_amdgcn_s_memtime())
+// accumulated time of a sub-phase (acc[i] += cycles since t0), rows 6.. of the profile
+#define RG_T0(v) const uint32_t v = (uint32_t)__builtin_amdgcn_s_memtime()
+#define RG_ACC(i, t0) (stamps[6 + (i)] += (uint32_t)__builtin_amdgcn_s_memtime() - (t0))
 #else
 #define RG_STAMP(i) ((void)0)
+#define RG_T0(v) ((void)0)
+#define RG_ACC(i, t0) ((void)0)
 #endif
 
 #ifndef RG_FN
@@ -78,9 +90,8 @@ struct Ctl {
   uint64_t processed_start, restored_at;  // apply window: entries restored from a snapshot are not Update()d
   bool took;                            // a snapshot was taken at the end of this step
   uint64_t wlo;                         // lowest log index written this step (EntriesToSave from here)
-  // RG_CTL_FASTREP (ablation, off in the product: it changes control_kernel<5>'s register
-  // allocation, and such a change preceded a memory fault in the full-size C3 test twice).
-  // The leader's last append of this step when it wrote no protected index: entries
+  // RG_CTL_FASTREP (ablation, see the top of this file). The leader's last append
+  // of this step when it wrote no protected index: entries
   // [la_base, la_base + la_n) all hold the ring word la_word (bank 0) and term(la_base − 1) = la_pt,
   // so send_replicate builds a Replicate of them from registers instead of re-reading the ring.
   // la_n = 0 when any other log write, reset or restore came after it.
@@ -169,7 +180,7 @@ struct Ctl {
       err |= ERR_WIRE;
       return -1;
     }
-    if (type != M_PROPOSE && type != M_REQUEST_VOTE) mterm = term;
+    if (type != M_PROPOSE && type != M_REQUEST_VOTE && type != M_READ_INDEX) mterm = term;
     const uint32_t n = get8(em, dst);
     em += 1ull << (8 * dst);
     const uint32_t k = get8(oc, dst);
@@ -216,6 +227,7 @@ struct Ctl {
       rt[j] = RETRY;
     });
     active = 0;
+    if (p.rdst) p.rdst[(uint64_t)RI_CTX * p.nrep + q] = 0;  // readIndex.reset
   }
   RG_FN void become_follower(uint64_t t, uint64_t l) {
     role = FOLLOWER;
@@ -264,12 +276,67 @@ struct Ctl {
   // aux: the J_SMASK of a WIRE job (record offset) or a SLAB job (slab row).
   RG_FN void write_entries(uint64_t base, uint32_t e0, uint32_t n, uint32_t kind, uint32_t src,
                                 const uint64_t* mt, uint64_t word, uint64_t aux = 0, const uint2* li = nullptr) {
+    RG_T0(t0);
+    write_entries_(base, e0, n, kind, src, mt, word, aux, li);
+    RG_ACC(3, t0);
+  }
+  RG_FN void write_entries_(uint64_t base, uint32_t e0, uint32_t n, uint32_t kind, uint32_t src,
+                                const uint64_t* mt, uint64_t word, uint64_t aux, const uint2* li) {
     const uint64_t hi_prot = umax64(last_start, sent_hi);
 #ifdef RG_CTL_FASTREP
     la_n = 0;
 #endif
     wlo = umin64(wlo, base + e0);
     uint64_t dm = 0, sm = 0, hm = 0, tm = 0;
+#ifdef RG_CTL_FRESH
+    if (base + e0 > hi_prot) {
+      // Fast path (the steady state): every index is fresh — bank 0, no old word to load, no hull.
+      // The ring slot advances by one row per entry (pointer increment, wrap at L) instead of a
+      // 64-bit multiply per entry; masks from the words with single-bit selects. (A lane steps one
+      // replica; at occupancy 1 this loop is issue-bound)
+      uint64_t* dst = tr_at(base + e0);
+      uint32_t slot = (uint32_t)((base + e0) & (p.L - 1));
+      const uint64_t step = p.nrep, wrap = (uint64_t)p.L * p.nrep;
+      if (!mt && !li) {  // one word for every entry: a leader's batch of synthetic Cmds, or its no-op
+        const uint64_t M = (n - e0 >= 64 ? ~0ull : (1ull << (n - e0)) - 1) << e0;
+        sm = (word & BANK_BIT) ? M : 0ull;
+        hm = (word & PAY_BIT) ? M : 0ull;
+        tm = (word & TYPE_BIT) ? M : 0ull;
+        const uint64_t wr = word & ~BANK_BIT;
+        for (uint32_t e = e0; e < n; ++e) {
+          *dst = wr;
+          dst += step;
+          if (++slot == p.L) {
+            slot = 0;
+            dst -= wrap;
+          }
+        }
+      } else {
+        uint64_t bit = 1ull << e0;
+        for (uint32_t e = e0; e < n; e += RG_CTL_BATCH) {
+          uint64_t wv[RG_CTL_BATCH];
+#pragma unroll
+          for (uint32_t k = 0; k < RG_CTL_BATCH; ++k)
+            wv[k] = word | (e + k >= n ? 0ull : mt ? mt[(uint64_t)(e + k) * p.G] : len_bits(li[e + k].y));
+#pragma unroll
+          for (uint32_t k = 0; k < RG_CTL_BATCH; ++k) {
+            if (e + k >= n) break;
+            const uint64_t w = wv[k];
+            sm |= (w & BANK_BIT) ? bit : 0ull;
+            hm |= (w & PAY_BIT) ? bit : 0ull;
+            tm |= (w & TYPE_BIT) ? bit : 0ull;
+            *dst = w & ~BANK_BIT;
+            dst += step;
+            if (++slot == p.L) {
+              slot = 0;
+              dst -= wrap;
+            }
+            bit <<= 1;
+          }
+        }
+      }
+    } else
+#endif
     // RG_CTL_BATCH entries at a time: their loads (sender terms, current ring words of protected
     // indices) are issued before any of their stores, so a lane waits one memory latency per
     // batch instead of one per entry (the compiler cannot prove the ring and the inbox disjoint).
@@ -383,7 +450,8 @@ struct Ctl {
     }
     const uint32_t n = next <= last ? (uint32_t)umin64(p.E, last - next + 1) : 0;
 #ifdef RG_CTL_FASTREP  // the whole message lies in this step's plain append (the steady-state case)
-    const bool fast = n > 0 && la_n > 0 && next >= la_base && next + n <= la_base + la_n;
+    // (at R = 8 the three extra live registers push the lane past 512 and into scratch: off there)
+    const bool fast = R <= 7 && n > 0 && la_n > 0 && next >= la_base && next + n <= la_base + la_n;
     const uint64_t lt = !fast ? term_at(next - 1) : next == la_base ? la_pt : la_word & TERM_MASK;
 #else
     const uint64_t lt = term_at(next - 1);
@@ -423,6 +491,12 @@ struct Ctl {
   // ---- follower side (A.9)
   // remote: the message came over the wire (its inline terms are in rmt, its records at wofs)
   RG_FN void handle_replicate(uint64_t w0, uint64_t log_term, uint64_t li, uint64_t mcommit, uint32_t from,
+                                   uint32_t src, uint32_t k, bool remote, uint64_t wofs) {
+    RG_T0(t0);
+    handle_replicate_(w0, log_term, li, mcommit, from, src, k, remote, wofs);
+    RG_ACC(2, t0);
+  }
+  RG_FN void handle_replicate_(uint64_t w0, uint64_t log_term, uint64_t li, uint64_t mcommit, uint32_t from,
                                    uint32_t src, uint32_t k, bool remote, uint64_t wofs) {
     if (li < committed) {
       send_simple(M_REPLICATE_RESP, from, 0, committed);
@@ -574,11 +648,58 @@ struct Ctl {
       }
     }
   }
-  RG_FN void leader_heartbeat_resp(uint32_t from) {
+  RG_FN void leader_heartbeat_resp(uint32_t from, uint64_t hint) {
     const uint32_t f = from - 1;
     active |= 1u << f;
     if (RG_GET(rt, f) == WAIT) RG_SET(rt, f, (uint32_t)RETRY);
     if (RG_GET(rm, f) < last) send_replicate(f);
+    if (hint != 0 && p.rdst) {  // readIndex.confirm: only read heartbeats carry a context
+      uint64_t* rd = p.rdst + q;
+      const uint64_t n = p.nrep;
+      if (rd[RI_CTX * n] == hint) {
+        const uint64_t a = rd[RI_ACKS * n] | (1ull << f);
+        if ((uint32_t)__builtin_popcount((uint32_t)a) >= quorum()) {
+          rd[RI_CTX * n] = 0;
+          read_confirmed(hint, rd[RI_INDEX * n], (uint32_t)(a >> 32));
+        } else {
+          rd[RI_ACKS * n] = a;
+        }
+      }
+    }
+  }
+  // ---- ReadIndex (Raft thesis §6.4; dragonboat's readIndex), state in p.rdst, not in registers
+  RG_FN void read_ready(uint64_t ctx, uint64_t index) {  // addReadyToRead
+    uint64_t* rd = p.rdst + q;
+    rd[RD_CTX * (uint64_t)p.nrep] = ctx;
+    rd[RD_INDEX * (uint64_t)p.nrep] = index;
+    rd[RD_TICK * (uint64_t)p.nrep] = p.tick + 1;
+  }
+  RG_FN void read_confirmed(uint64_t ctx, uint64_t index, uint32_t slot) {
+    if (slot == s) read_ready(ctx, index);
+    else send(M_READ_INDEX_RESP, slot + 1, 0, 0, 0, 0, index, 0, ctx, 0, 0, 0);
+  }
+  RG_FN void handle_read_index(uint32_t from, uint64_t ctx) {
+    const uint32_t f = from - 1;
+    if (!p.rdst) return;
+    if (role == LEADER) {
+      uint64_t* rd = p.rdst + q;
+      const uint64_t n = p.nrep;
+      if (R == 1) {
+        read_confirmed(ctx, committed, f);
+      } else if (term_at(committed) != term || rd[RI_CTX * n] != 0) {
+        drops++;  // nothing committed in this term yet, or a read already pending
+      } else {
+        rd[RI_CTX * n] = ctx;
+        rd[RI_INDEX * n] = committed;
+        rd[RI_ACKS * n] = (1ull << s) | ((uint64_t)f << 32);
+        for (uint32_t i = 0; i < R; ++i)  // broadcastHeartbeatMessageWithHint
+          if (i != s) send(M_HEARTBEAT, i + 1, 0, 0, 0, 0, 0, umin64(RG_GET(rm, i), committed), ctx, 0, 0, 0);
+      }
+    } else if (role == FOLLOWER && leader != 0 && f == s) {
+      send(M_READ_INDEX, (uint32_t)leader, 0, 0, 0, 0, 0, 0, ctx, 0, 0, 0);
+    } else {
+      drops++;
+    }
   }
   RG_FN void check_quorum() {
     const uint32_t c = 1 + __builtin_popcount(active & ~(1u << s));
@@ -591,11 +712,15 @@ struct Ctl {
   RG_FN void handle_propose(uint32_t nent, uint32_t slab_id, uint32_t hop, uint64_t hm, uint32_t rslot,
                             const uint2* li, const uint64_t* rmt, uint64_t wofs) {
     if (role == LEADER) {
+      RG_T0(t0);
       if (!append_local(nent, (int)slab_id, rslot, li, rmt, wofs)) {
         drops++;
         return;
       }
+      RG_ACC(0, t0);
+      RG_T0(t1);
       broadcast_replicate();
+      RG_ACC(1, t1);
     } else if (role == FOLLOWER && leader != 0 && hop == 0) {
       send(M_PROPOSE, (uint32_t)leader, 0, 0, nent, 0, 0, 0, hm, 0, slab_id, hop + 1);
     } else {
@@ -627,10 +752,26 @@ struct Ctl {
 
   // ---- Handle (A.3): message k from slot src (remote: it came over the wire from another rank)
   RG_FN void handle(uint32_t src, uint32_t k, bool remote) {
+    RG_T0(t0);
+    handle_(src, k, remote);
+    RG_ACC(5, t0);
+  }
+  RG_FN void handle_(uint32_t src, uint32_t k, bool remote) {
     const uint64_t plane = (uint64_t)R * R * p.K * p.G;
     const uint64_t* h = (remote ? p.rhdr : p.hdr_in) + (((uint64_t)src * R + s) * p.K + k) * p.G + g;
-    const uint64_t w0 = h[0];
-    const uint64_t mterm = h[1 * plane];
+    // words 0 and 1 (type, ids, term) up front; the others where a handler uses them
+    // (RG_CTL_HDRBATCH: all eight in one round trip; at R >= 6 there is no room for them)
+#ifdef RG_CTL_HDRBATCH
+    constexpr int NB = R <= 5 ? 8 : 2;
+#else
+    constexpr int NB = 2;
+#endif
+    uint64_t hb[NB];
+#pragma unroll
+    for (int x = 0; x < NB; ++x) hb[x] = h[(uint64_t)x * plane];
+    auto hw = [&](int x) -> uint64_t { return x < NB ? hb[x < NB ? x : 0] : h[(uint64_t)x * plane]; };
+    const uint64_t w0 = hw(0);
+    const uint64_t mterm = hw(1);
     const uint32_t type = (uint32_t)(w0 & 0xFF);
     const uint32_t from = (uint32_t)(w0 >> 8) & 0xFF;
     if (from - 1 >= (uint32_t)R) {  // unreachable: local senders stamp their id, unpack checks remote ones
@@ -645,9 +786,10 @@ struct Ctl {
       return;
     }
 #endif
-    const bool leader_msg = type == M_REPLICATE || type == M_INSTALL_SNAPSHOT || type == M_HEARTBEAT;
+    const bool leader_msg =
+        type == M_REPLICATE || type == M_INSTALL_SNAPSHOT || type == M_HEARTBEAT || type == M_READ_INDEX_RESP;
     if (mterm != 0 && mterm != term) {
-      if (type == M_REQUEST_VOTE && p.CQ && mterm > term && h[5 * plane] != from && leader != 0 && etick < p.ET)
+      if (type == M_REQUEST_VOTE && p.CQ && mterm > term && hw(5) != from && leader != 0 && etick < p.ET)
         return;
       if (mterm > term) {
         become_follower(mterm, leader_msg ? from : 0);
@@ -659,7 +801,7 @@ struct Ctl {
     switch (type) {
       case M_PROPOSE: {  // forwarded (hop 1). Local: the Cmds are in the forwarder's row of slab w7;
         // remote: unpack put their length words in rmt and their records' offset in word 7
-        const uint64_t w7 = h[7 * plane];
+        const uint64_t w7 = hw(7);
         const uint32_t nent = (uint32_t)(w0 >> 32);
         if (nent - 1 >= p.E || (!remote && (uint32_t)w7 >= p.nslab)) {  // unreachable: senders forward
           err |= ERR_WIRE;                                               // 1..E entries of a slab
@@ -667,12 +809,12 @@ struct Ctl {
         }
         if (remote) {
           const uint64_t* rm = p.rmt + ((((uint64_t)src * R + s) * p.K + k) * p.E) * p.G + g;
-          handle_propose(nent, 0, 1, h[5 * plane], 0, nullptr, rm, w7);
+          handle_propose(nent, 0, 1, hw(5), 0, nullptr, rm, w7);
         } else {
           const uint64_t row = p.wire ? (uint64_t)src * p.G + g : g;  // the forwarder's slab row (same rank)
           const uint64_t rows = p.wire ? p.nrep : p.G;
           const uint2* li = p.slab_info + ((uint64_t)(uint32_t)w7 * rows + row) * p.E;
-          handle_propose(nent, (uint32_t)w7, (uint32_t)(w7 >> 32), h[5 * plane], src, li, nullptr, 0);
+          handle_propose(nent, (uint32_t)w7, (uint32_t)(w7 >> 32), hw(5), src, li, nullptr, 0);
         }
         break;
       }
@@ -687,23 +829,33 @@ struct Ctl {
           leader = from;
         }
         if (type == M_REPLICATE) {
-          handle_replicate(w0, h[2 * plane], h[3 * plane], h[4 * plane], from, src, k, remote,
-                           remote ? h[7 * plane] : 0);
+          handle_replicate(w0, hw(2), hw(3), hw(4), from, src, k, remote,
+                           remote ? hw(7) : 0);
         } else if (type == M_HEARTBEAT) {
-          commit_to(h[4 * plane]);
-          send_simple(M_HEARTBEAT_RESP, from, 0, 0, h[5 * plane], h[6 * plane]);
+          commit_to(hw(4));
+          send_simple(M_HEARTBEAT_RESP, from, 0, 0, hw(5), hw(6));
         } else {
-          handle_install_snapshot(h[3 * plane], h[2 * plane], from);
+          handle_install_snapshot(hw(3), hw(2), from);
         }
         break;
       case M_REPLICATE_RESP:
-        if (role == LEADER) leader_replicate_resp((uint32_t)(w0 >> 24) & 0xFF, h[3 * plane], h[5 * plane], from);
+        if (role == LEADER) leader_replicate_resp((uint32_t)(w0 >> 24) & 0xFF, hw(3), hw(5), from);
         break;
       case M_HEARTBEAT_RESP:
-        if (role == LEADER) leader_heartbeat_resp(from);
+        if (role == LEADER) leader_heartbeat_resp(from, hw(5));
+        break;
+      case M_READ_INDEX:
+        handle_read_index(from, hw(5));
+        break;
+      case M_READ_INDEX_RESP:
+        if (role == FOLLOWER && p.rdst) {
+          etick = 0;
+          leader = from;
+          read_ready(hw(5), hw(3));
+        }
         break;
       case M_REQUEST_VOTE:
-        handle_request_vote(h[2 * plane], h[3 * plane], from);
+        handle_request_vote(hw(2), hw(3), from);
         break;
       case M_REQUEST_VOTE_RESP:
         if (role == CANDIDATE) candidate_vote_resp(from, (uint32_t)(w0 >> 24) & 0xFF);
@@ -714,7 +866,7 @@ struct Ctl {
   }
 
   // ---- the whole step
-  uint32_t stamps[6];
+  uint32_t stamps[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 
   RG_FN void run() {
     for (uint32_t src = 0; src < R; ++src) {
@@ -747,6 +899,10 @@ struct Ctl {
         handle_propose(n, sl, 0, hm, s, li, nullptr, 0);
       }
     }
+    if (p.read_ctx) {  // 4b: ReadIndex input (rg_read_index)
+      const uint64_t ctx = p.read_ctx[ri];
+      if (ctx) handle_read_index(my_id(), ctx);
+    }
     RG_STAMP(3);
     // GetUpdate.CommittedEntries = (processed, committed], then commitUpdate; applied follows unless
     // the state machine reports it (rg_notify_applied); snapshot + compaction on applied
@@ -768,7 +924,7 @@ struct Ctl {
     RG_STAMP(5);
 #if defined(RG_CTL_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
     if (p.prof)
-      for (int k = 0; k < 6; ++k) p.prof[(uint64_t)k * p.nrep + q] = stamps[k];
+      for (int k = 0; k < 12; ++k) p.prof[(uint64_t)k * p.nrep + q] = stamps[k];
 #endif
   }
 

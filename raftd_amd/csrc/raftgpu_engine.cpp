@@ -87,6 +87,14 @@ struct rg_engine {
   uint64_t h_cmd_cap = 0;
   uint8_t* d_cmd = nullptr;
   uint64_t d_cmd_cap = 0;
+  // ReadIndex: device state rows, and the requests staged for the next tick (pinned table indexed
+  // by global replica id, uploaded by the tick like the proposal tables)
+  uint64_t* rdst = nullptr;
+  uint64_t* h_rd = nullptr;
+  uint64_t* d_read_ctx = nullptr;
+  std::vector<uint64_t> rd_touched;
+  bool rd_staged = false, rd_reset_pending = false;
+  hipEvent_t rd_ev = nullptr;
   uint32_t* crc_tab = nullptr;
   uint32_t crc_const = 0;
   uint8_t* d_prop_target = nullptr;
@@ -256,6 +264,7 @@ static TickParams params(rg_engine* e) {
   p.job64 = e->job64[a]; p.job32 = e->job32[a]; p.jcnt = e->jcnt[a];
   p.rhdr = e->rhdr; p.rmt = e->rmt; p.rcnt = e->rcnt;
   p.slab_info = e->slab_info;
+  p.rdst = e->rdst;
   p.apply_lo = e->apply_lo;
   p.persist_lo = e->persist_lo;
   p.snap_ev = e->snap_ev;
@@ -307,6 +316,9 @@ extern "C" {
 const char* rg_last_error(void) { return g_err.c_str(); }
 
 int rg_create(const rg_config* cfg, rg_engine** out) {
+  // Kernel arguments in host memory: effective when this is the process's first
+  // HIP call; a host that initialised HIP earlier sets HIP_FORCE_DEV_KERNARG=0 itself
+  setenv("HIP_FORCE_DEV_KERNARG", "0", 0);
   if (!cfg || !out) return fail(RG_EINVAL, "null argument");
   const rg_config& c = *cfg;
   if (c.groups < 1 || c.replicas < 1 || c.replicas > RG_MAX_REPLICAS) return fail(RG_EINVAL, "groups/replicas");
@@ -360,6 +372,10 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if (rc == RG_OK) rc = dalloc(e, &e->slabs, (uint64_t)c.num_slabs * e->slab_rows * E * P);
   if (rc == RG_OK) rc = dalloc(e, &e->slab_info, (uint64_t)c.num_slabs * e->slab_rows * E * sizeof(uint2));
   if (rc == RG_OK) rc = dalloc(e, &e->d_prop_hmask, G * N * 8);
+  if (rc == RG_OK) rc = dalloc(e, &e->rdst, (uint64_t)RD_ROWS * n * 8);
+  if (rc == RG_OK) rc = dalloc(e, &e->d_read_ctx, n * N * 8);
+  if (rc == RG_OK && hipHostMalloc((void**)&e->h_rd, n * N * 8, 0) != hipSuccess) rc = fail(RG_ENOMEM, "hipHostMalloc");
+  if (rc == RG_OK) memset(e->h_rd, 0, n * N * 8);
   if (rc == RG_OK && (hipHostMalloc((void**)&e->h_pt, G * N, 0) != hipSuccess ||
                       hipHostMalloc((void**)&e->h_pc, G * N * 4, 0) != hipSuccess ||
                       hipHostMalloc((void**)&e->h_hm, G * N * 8, 0) != hipSuccess))
@@ -383,7 +399,7 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if (rc == RG_OK) rc = dalloc(e, &e->persist_lo, n * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->snap_ev, n * 8);
 #ifdef RG_CTL_PROFILE
-  if (rc == RG_OK) rc = dalloc(e, &e->prof, n * 6 * 4);
+  if (rc == RG_OK) rc = dalloc(e, &e->prof, n * 12 * 4);
 #endif
   if (rc == RG_OK) rc = dalloc(e, &e->pscnt, n * 4);
   if (rc == RG_OK) rc = dalloc(e, &e->pecnt, n * 4);
@@ -455,7 +471,8 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
       return fail(RG_EHIP, "hipEventCreate");
     }
   }
-  if (hipEventCreateWithFlags(&e->stg_ev, hipEventDisableTiming) != hipSuccess ||
+  if (hipEventCreateWithFlags(&e->rd_ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&e->stg_ev, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&e->prop_ev, hipEventDisableTiming) != hipSuccess ||
       hipStreamCreateWithFlags(&e->copy, hipStreamNonBlocking) != hipSuccess) {
     rg_destroy(e);
@@ -514,6 +531,8 @@ void rg_destroy(rg_engine* e) {
     if (e->a_host[b]) (void)hipHostFree(e->a_host[b]);
   }
   if (e->stg_ev) (void)hipEventDestroy(e->stg_ev);
+  if (e->rd_ev) (void)hipEventDestroy(e->rd_ev);
+  if (e->h_rd) (void)hipHostFree(e->h_rd);
   if (e->prop_ev) (void)hipEventDestroy(e->prop_ev);
   for (void* p : e->allocs) (void)hipFree(p);
   if (e->h_bounds) (void)hipHostFree(e->h_bounds);
@@ -611,6 +630,11 @@ int rg_bootstrap(rg_engine* e) {
   }
   e->touched.clear();
   e->staged = false;
+  if (e->rd_reset_pending) HIPCHK(hipEventSynchronize(e->rd_ev));
+  for (uint64_t i : e->rd_touched) e->h_rd[i] = 0;
+  e->rd_touched.clear();
+  e->rd_staged = e->rd_reset_pending = false;
+  HIPCHK(hipMemsetAsync(e->rdst, 0, (uint64_t)RD_ROWS * e->nrep * 8, e->stream));
   HIPCHK(hipMemsetAsync(e->crc_err, 0, (uint64_t)e->nrep * 4, e->stream));
   TickParams p = params(e);
   p.s64_out = e->s64[0];
@@ -804,8 +828,9 @@ static int tick_impl(rg_engine* e, const rg_tick_input* in, bool device_ptrs) {
   if (in && in->prop_target && !((e->slab_synth >> sl) & 1) && e->c.payload_bytes) {
     // a tick-input (synthetic) batch into a slab rg_propose wrote: regenerate that slab only (the
     // others may still hold forwarded proposals' Cmds)
-    HIPCHK(launch_fill_slabs(e->slabs, e->slab_info, sl, 1, e->c.groups, e->slab_rows, e->c.max_entries_per_msg,
-                             e->c.payload_bytes, e->c.seed, e->pl, e->stream));
+    LAUNCH(launch_fill_slabs(e->slabs, e->slab_info, sl, 1, e->c.groups, e->slab_rows, e->c.max_entries_per_msg,
+                             e->c.payload_bytes, e->c.seed, e->pl, e->stream),
+           e->stream, "fill_slabs");
     e->slab_synth |= 1ull << sl;
   }
   if (in) {
@@ -848,6 +873,13 @@ static int tick_impl(rg_engine* e, const rg_tick_input* in, bool device_ptrs) {
     p.prop_hmask = e->d_prop_hmask;
     e->staged = false;
     e->stg_reset_pending = true;
+  }
+  if (e->rd_staged) {  // rg_read_index's requests
+    HIPCHK(hipMemcpyAsync(e->d_read_ctx, e->h_rd, (uint64_t)e->nrep * e->pl.N * 8, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipEventRecord(e->rd_ev, e->stream));
+    p.read_ctx = e->d_read_ctx;
+    e->rd_staged = false;
+    e->rd_reset_pending = true;
   }
   // control(t) on the engine stream once bulk(t-2) released jobs[t&1]; bulk(t) on the bulk
   // stream after control(t). control(t+1) then overlaps bulk(t): they touch disjoint data.
@@ -971,7 +1003,12 @@ int rg_import_replica(rg_engine* e, uint32_t rid, const rg_replica_view* v, cons
   if (pb) HIPCHK(hipMemcpy(d + vb + wb + cb, rows.data(), pb, hipMemcpyHostToDevice));
   HIPCHK(launch_scatter_replica(admin(e), rid, d, (const uint64_t*)(d + vb), pb ? d + vb + wb + cb : nullptr,
                                 (const uint32_t*)(d + vb + wb), nent, e->stream, e->info, e->pay));
-  HIPCHK(hipMemsetAsync(e->snap_ev + rid, 0, 8, e->stream));  // no snapshot events until it steps
+  {  // no snapshot event, pending or ready read until it steps (device rows are indexed by q = s·G + g)
+    const uint64_t q = (uint64_t)(rid % e->c.replicas) * e->c.groups + rid / e->c.replicas;
+    HIPCHK(hipMemsetAsync(e->snap_ev + q, 0, 8, e->stream));
+    HIPCHK(hipMemsetAsync(e->rdst + (uint64_t)RI_CTX * e->nrep + q, 0, 8, e->stream));
+    HIPCHK(hipMemsetAsync(e->rdst + (uint64_t)RD_TICK * e->nrep + q, 0, 8, e->stream));
+  }
   HIPCHK(hipStreamSynchronize(e->stream));
   return RG_OK;
 }
@@ -1200,10 +1237,83 @@ int rg_snapshot_events(rg_engine* e, uint32_t slot_mask, rg_snapshot_event* even
 extern "C" int rg_debug_ctl_profile(rg_engine* e, uint32_t* out) {
   if (!e || !out) return fail(RG_EINVAL, "rg_debug_ctl_profile args");
   if (int jrc = join(e)) return jrc;
-  HIPCHK(hipMemcpy(out, e->prof, (uint64_t)e->nrep * 6 * 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(out, e->prof, (uint64_t)e->nrep * 12 * 4, hipMemcpyDeviceToHost));
   return RG_OK;
 }
 #endif
+
+// tests only (not in include/raftgpu.h): where this process's kernel arguments live.
+// *is_device = 1 device memory, 0 host memory, -1 unknown (the runtime does not track the address)
+extern "C" int rg_debug_kernarg_placement(int32_t device, uint64_t* addr, int32_t* is_device) {
+  if (!addr || !is_device) return fail(RG_EINVAL, "rg_debug_kernarg_placement args");
+  HIPCHK(hipSetDevice(device));
+  uint64_t* d = nullptr;
+  HIPCHK(hipMalloc((void**)&d, 16));
+  uint64_t h[2] = {0, 0};
+  hipError_t r = launch_kernarg_probe(d, 0x5EEDull, nullptr);
+  if (r == hipSuccess) r = hipMemcpy(h, d, 16, hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (r != hipSuccess) return fail(RG_EHIP, std::string("kernarg probe: ") + hipGetErrorString(r));
+  if (h[1] != 0x5EEDull) return fail(RG_EHIP, "kernarg probe: bad tag");
+  *addr = h[0];
+  hipPointerAttribute_t at{};
+  *is_device = -1;
+  if (hipPointerGetAttributes(&at, (void*)(uintptr_t)h[0]) == hipSuccess)
+    *is_device = at.type == hipMemoryTypeDevice ? 1 : at.type == hipMemoryTypeHost ? 0 : -1;
+  (void)hipGetLastError();
+  return RG_OK;
+}
+
+int rg_read_index(rg_engine* e, const rg_read_request* reqs, size_t n) {
+  if (!e || (n && !reqs)) return fail(RG_EINVAL, "rg_read_index args");
+  if (e->rd_reset_pending) {  // the last upload has completed: clear what it carried
+    HIPCHK(hipEventSynchronize(e->rd_ev));
+    for (uint64_t i : e->rd_touched) e->h_rd[i] = 0;
+    e->rd_touched.clear();
+    e->rd_reset_pending = false;
+  }
+  const uint32_t N = e->pl.N, R = e->c.replicas;
+  const uint64_t g0 = (uint64_t)N * e->pl.col_base, gn = (uint64_t)N * e->c.groups;
+  for (size_t i = 0; i < n; ++i) {
+    const rg_read_request& q = reqs[i];
+    if (q.group < g0 || q.group >= g0 + gn || q.slot >= R || q.ctx == 0)
+      return fail(RG_EINVAL, "rg_read_index: request " + std::to_string(i) + ": bad shard, slot or ctx 0");
+    if (pl_rank_of(e->pl, q.group, q.slot) != e->pl.rank)
+      return fail(RG_EINVAL, "rg_read_index: request " + std::to_string(i) + ": replica hosted by another rank");
+  }
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t at = (reqs[i].group - g0) * R + reqs[i].slot;
+    if (!e->h_rd[at]) e->rd_touched.push_back(at);
+    e->h_rd[at] = reqs[i].ctx;
+  }
+  if (n) e->rd_staged = true;
+  return RG_OK;
+}
+
+int rg_read_index_results(rg_engine* e, uint32_t slot_mask, rg_read_ready* out, uint64_t cap, uint64_t* n) {
+  if (!e || !n) return fail(RG_EINVAL, "rg_read_index_results args");
+  if (int jrc = join(e)) return jrc;
+  const TickParams t = params(e);
+  SnapParams a{};
+  a.G = t.G; a.R = t.R; a.nrep = t.nrep; a.slot_mask = slot_mask; a.pl = e->pl;
+  a.s64 = t.s64_in; a.rdst = e->rdst; a.tick = e->t;
+  a.cnt = e->acnt; a.off = e->aoff; a.bsum = e->absum;
+  LAUNCH(launch_read_count(a, (uint64_t*)e->d_sum, e->stream), e->stream, "read count");
+  uint64_t total = 0;
+  HIPCHK(hipMemcpyAsync(&total, e->d_sum, 8, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  *n = total;
+  if (total == 0) return RG_OK;
+  if (total > cap) return fail(RG_EFULL, "rg_read_index_results: " + std::to_string(total) + " > cap");
+  if (!out) return fail(RG_EINVAL, "rg_read_index_results: null output");
+  const uint64_t rb = total * sizeof(rg_read_ready);
+  RGCHK(astage_reserve(e, rb));
+  a.out = e->astage;
+  LAUNCH(launch_read_gather(a, e->stream), e->stream, "read gather");
+  HIPCHK(hipMemcpyAsync(out, a.out, rb, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return RG_OK;
+}
 
 int rg_notify_applied(rg_engine* e, const uint32_t* rids, const uint64_t* index, size_t n) {
   if (!e || (n && (!rids || !index))) return fail(RG_EINVAL, "rg_notify_applied args");

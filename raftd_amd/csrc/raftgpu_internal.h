@@ -28,8 +28,12 @@ RG_HD_INLINE uint64_t len_bits(uint32_t len) { return ((uint64_t)len << LEN_SHIF
 enum : uint32_t {
   M_LOCAL_TICK = 0, M_ELECTION = 1, M_LEADER_HEARTBEAT = 2, M_NOOP = 4, M_PROPOSE = 7,
   M_CHECK_QUORUM = 10, M_REPLICATE = 12, M_REPLICATE_RESP = 13, M_REQUEST_VOTE = 14,
-  M_REQUEST_VOTE_RESP = 15, M_INSTALL_SNAPSHOT = 16, M_HEARTBEAT = 17, M_HEARTBEAT_RESP = 18
+  M_REQUEST_VOTE_RESP = 15, M_INSTALL_SNAPSHOT = 16, M_HEARTBEAT = 17, M_HEARTBEAT_RESP = 18,
+  M_READ_INDEX = 19, M_READ_INDEX_RESP = 20
 };
+// ReadIndex state rows ([row][nrep], updated in place by the replica's own lane, touched only on
+// read traffic): the leader's pending request and the read made ready in a step
+enum : uint32_t { RI_CTX, RI_INDEX, RI_ACKS /* acks | requester slot << 32 */, RD_CTX, RD_INDEX, RD_TICK, RD_ROWS };
 enum : uint32_t { FOLLOWER = 0, CANDIDATE = 1, LEADER = 2 };
 enum : uint32_t { RETRY = 0, WAIT = 1, REPLICATE = 2, SNAPSHOT = 3 };
 enum : uint32_t { ENTRY_APP = 0, ENTRY_CONFIG = 1 };
@@ -157,6 +161,8 @@ struct TickParams {
   const uint2* slab_info;      // [nslab][rows][E] {0, Cmd length} of the proposal slabs
   const uint8_t* campaign;
   const uint8_t* isolate;
+  const uint64_t* read_ctx;    // [global rid] ReadIndex request contexts of this tick (NULL: none)
+  uint64_t* rdst;              // [RD_ROWS][nrep] ReadIndex state
 };
 
 struct BulkParams {
@@ -216,6 +222,8 @@ hipError_t launch_control(const TickParams& p, hipStream_t s);
 hipError_t launch_bulk(const BulkParams& p, hipStream_t s, int grid);
 hipError_t launch_bootstrap(const TickParams& p, uint2* info, hipStream_t s);
 // synthetic Cmds into slabs [slab0, slab0 + nslab)
+// the address of a launch's kernel-argument segment (where the runtime put the arguments)
+hipError_t launch_kernarg_probe(uint64_t* out, uint64_t tag, hipStream_t s);
 hipError_t launch_fill_slabs(uint8_t* slabs, uint2* slab_info, uint32_t slab0, uint32_t nslab, uint32_t G, uint32_t rows,
                              uint32_t E, uint32_t P, uint64_t seed, const Placement& pl, hipStream_t s);
 // caller proposals (rg_propose): Cmd e of the batch is copied from src + off[e] (len[e] bytes, zero-padded
@@ -251,6 +259,8 @@ struct SnapParams {
   Placement pl;
   const uint64_t* s64;      // current state (snap_index, snap_term)
   const uint64_t* snap_ev;
+  const uint64_t* rdst;     // ReadIndex state (read results)
+  uint64_t tick;            // the ticks run so far (a read made ready in the last one has RD_TICK == tick)
   uint32_t* cnt;
   uint64_t* off;
   uint64_t* bsum;
@@ -258,6 +268,9 @@ struct SnapParams {
 };
 hipError_t launch_snap_count(const SnapParams& a, uint64_t* total, hipStream_t s);
 hipError_t launch_snap_gather(const SnapParams& a, hipStream_t s);
+// reads made ready in the last tick (rg_read_index_results), same count / scan / gather shape
+hipError_t launch_read_count(const SnapParams& a, uint64_t* total, hipStream_t s);
+hipError_t launch_read_gather(const SnapParams& a, hipStream_t s);
 // persistence copy-back (raftgpu_apply.hip): per replica whose log or hard state changed in the
 // last tick, its state record and the entries it rewrote ([persist_lo, last]); full = every
 // replica with its whole log window (marker, last] (a checkpoint)

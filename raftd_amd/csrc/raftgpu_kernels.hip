@@ -503,6 +503,19 @@ hipError_t launch_stage_cmds(uint8_t* slabs, uint2* slab_info, uint32_t P, const
   return hipGetLastError();
 }
 
+// ================================================================== kernel-argument placement probe (tests)
+__global__ void kernarg_probe_kernel(uint64_t* out, uint64_t tag) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    out[0] = (uint64_t)(uintptr_t)__builtin_amdgcn_kernarg_segment_ptr();
+    out[1] = tag;
+  }
+}
+
+hipError_t launch_kernarg_probe(uint64_t* out, uint64_t tag, hipStream_t s) {
+  hipLaunchKernelGGL(kernarg_probe_kernel, dim3(1), dim3(64), 0, s, out, tag);
+  return hipGetLastError();
+}
+
 // ================================================================== copy probe (measurement)
 // The fastest of the shapes scripts/copy_probe.hip measured on MI355X (r01: 5.94 TB/s read + write):
 // one block per 32-KB tile, eight 16-B non-temporal loads in flight per lane.

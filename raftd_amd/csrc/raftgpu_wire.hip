@@ -257,7 +257,8 @@ __global__ void unpack_kernel(WireParams w) {
     // Propose 1..E), inside the region; the unit's messages from the first bad one on are dropped
     const bool known = type == M_NOOP || type == M_PROPOSE || type == M_REPLICATE || type == M_REPLICATE_RESP ||
                        type == M_REQUEST_VOTE || type == M_REQUEST_VOTE_RESP || type == M_INSTALL_SNAPSHOT ||
-                       type == M_HEARTBEAT || type == M_HEARTBEAT_RESP;
+                       type == M_HEARTBEAT || type == M_HEARTBEAT_RESP || type == M_READ_INDEX ||
+                       type == M_READ_INDEX_RESP;
     const uint32_t from = (uint32_t)(w0 >> 8) & 0xFF, to = (uint32_t)(w0 >> 16) & 0xFF, nent = (uint32_t)(w0 >> 32);
     if (!known || from != s + 1 || to != d + 1 || n > w.E || (type == M_PROPOSE && (nent < 1 || nent > w.E)) ||
         (uint64_t)(in - w.recv) + 64 + (uint64_t)n * (16 + w.P) > rend) {

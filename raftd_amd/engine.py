@@ -110,6 +110,13 @@ def pack_proposals(batches):
     return props, np.array(lens, dtype=np.uint32), blob
 
 
+class ReadRequest(C.Structure):
+    _fields_ = [("group", C.c_uint64), ("slot", C.c_uint32), ("_pad", C.c_uint32), ("ctx", C.c_uint64)]
+
+
+READ_READY_DTYPE = np.dtype([("group", "<u8"), ("replica_id", "<u4"), ("rid", "<u4"), ("ctx", "<u8"), ("index", "<u8")])
+
+
 class TickInput(C.Structure):
     _fields_ = [("prop_target", C.c_void_p), ("prop_count", C.c_void_p), ("campaign", C.c_void_p),
                 ("isolate", C.c_void_p), ("flags", C.c_uint32), ("_pad", C.c_uint32)]
@@ -125,7 +132,7 @@ EXPORTS = ["rg_create", "rg_destroy", "rg_bootstrap", "rg_fill_slabs", "rg_tick"
            "rg_device_bytes", "rg_last_error", "rg_last_tick_traffic", "rg_join",
            "rg_timing", "rg_kernel_ms", "rg_wire_plan", "rg_wire_pack", "rg_wire_recv", "rg_global_id",
            "rg_apply_committed", "rg_probe_copy", "rg_persist_collect", "rg_snapshot_events", "rg_propose",
-           "rg_notify_applied", "rg_apply_async", "rg_apply_wait"]
+           "rg_notify_applied", "rg_apply_async", "rg_apply_wait", "rg_read_index", "rg_read_index_results"]
 
 _lib = None
 
@@ -169,6 +176,8 @@ def load_library(path: str = LIB_PATH):
         "rg_propose": ([vp, C.POINTER(Proposal), C.c_size_t, vp, vp], i32),
         "rg_notify_applied": ([vp, vp, vp, C.c_size_t], i32),
         "rg_apply_async": ([vp, u32, i32], i32),
+        "rg_read_index": ([vp, C.POINTER(ReadRequest), C.c_size_t], i32),
+        "rg_read_index_results": ([vp, u32, vp, u64, C.POINTER(C.c_uint64)], i32),
         "rg_apply_wait": ([vp, i32, C.POINTER(vp), C.POINTER(vp), C.POINTER(C.c_uint64)], i32),
         "rg_deliver": ([vp, u32, C.POINTER(MsgView)], i32),
         "rg_leader": ([vp, u32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_int)], i32),
@@ -391,6 +400,31 @@ class Engine:
         if "from" not in fields:
             m.from_ = rid_src % self.R + 1
         self._check(self.L.rg_deliver(self.h, rid_src, C.byref(m)))
+
+    def read_index(self, reqs):
+        """Stage ReadIndex requests [(global group, slot, ctx)] for the next tick (rg_read_index)."""
+        arr = (ReadRequest * max(len(reqs), 1))()
+        for i, (g, s, ctx) in enumerate(reqs):
+            arr[i].group, arr[i].slot, arr[i].ctx = g, s, ctx
+        self._check(self.L.rg_read_index(self.h, arr, len(reqs)))
+
+    def read_index_results(self, slot_mask: int = 0xFF):
+        """Reads made ready in the last tick (rg_read_index_results): READ_READY_DTYPE rows."""
+        n = C.c_uint64()
+        rc = self.L.rg_read_index_results(self.h, slot_mask, None, 0, C.byref(n))
+        if rc < 0 and rc != RG_EFULL:
+            self._check(rc)
+        out = np.zeros(max(n.value, 1), READ_READY_DTYPE)
+        self._check(self.L.rg_read_index_results(self.h, slot_mask, out.ctypes.data, n.value, C.byref(n)))
+        return out[:n.value]
+
+    def read_ready_all(self) -> dict:
+        """{local rid: (ctx, index)} for the reads made ready in the last tick."""
+        return {int(r["rid"]): (int(r["ctx"]), int(r["index"])) for r in self.read_index_results()}
+
+    def read_ready(self, rid):
+        """(ctx, index) made ready for local replica rid in the last tick, or None."""
+        return self.read_ready_all().get(rid)
 
     def notify_applied(self, rids, index):
         """rg_notify_applied (Peer.NotifyRaftLastApplied) for local replicas rids."""

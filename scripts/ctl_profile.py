@@ -21,11 +21,13 @@ eng.tick(campaign=camp)
 pt, pc = np.zeros(G, np.uint8), np.full(G, E, np.uint32)
 for _ in range(12):
     eng.tick(pt, pc)
-prof = np.zeros((6, G * R), np.uint32)
+prof = np.zeros((12, G * R), np.uint32)
 fn = eng.L.rg_debug_ctl_profile
 fn.argtypes = [C.c_void_p, C.c_void_p]
 assert fn(eng.h, prof.ctypes.data) == 0
-d = (np.diff(prof.astype(np.int64), axis=0) % 2**32).astype(np.float64)
+d = (np.diff(prof[:6].astype(np.int64), axis=0) % 2**32).astype(np.float64)
+acc = prof[6:].astype(np.float64)
+accn = ["propose:append", "propose:broadcast", "handle_replicate", "write_entries", "-", "handle (all msgs)"]
 names = ["load+inbox", "campaign+tick", "propose", "apply/snap", "store"]
 roles = np.array([v for v in eng.replica_array()["role"]])
 for s in range(R):
@@ -34,3 +36,4 @@ for s in range(R):
     print(f"slot {s} (role {np.bincount(roles[s::R], minlength=3).tolist()} F/C/L): total {tot.mean():8.0f} cyc "
           f"(p50 {np.median(tot):.0f}, p99 {np.percentile(tot, 99):.0f})  " +
           "  ".join(f"{n} {d[k, sl].mean():7.0f}" for k, n in enumerate(names)))
+    print("    sub-phases: " + "  ".join(f"{n} {acc[k, sl].mean():7.0f}" for k, n in enumerate(accn) if n != "-"))

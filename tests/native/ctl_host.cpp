@@ -17,7 +17,12 @@ struct Host {
   std::vector<uint64_t> s64[2], rem[2], tr, hdr[2], mt[2], job64;
   std::vector<uint32_t> s32[2], cnt[2], job32, jcnt;
   std::vector<uint8_t> rst[2];
-  std::vector<uint2> slab_info;  // [nslab][G][E] {0, P}: synthetic Cmds (forwarded proposals read their lengths)
+  std::vector<uint2> slab_info;  // [nslab][G][E] {0, len}: synthetic Cmds are P bytes; ch_propose sets lengths
+  std::vector<uint64_t> rdst;     // ReadIndex state rows
+  std::vector<uint8_t> pt;        // rg_propose staging: target slot, count, non-empty mask per group
+  std::vector<uint32_t> pc;
+  std::vector<uint64_t> hm;
+  bool staged = false;
   uint64_t t = 0;
 };
 
@@ -41,6 +46,7 @@ static TickParams params(Host* h) {
   p.cnt_in = h->cnt[b].data(); p.cnt_out = h->cnt[a].data();
   p.job64 = h->job64.data(); p.job32 = h->job32.data(); p.jcnt = h->jcnt.data();
   p.slab_info = h->slab_info.data();
+  p.rdst = h->rdst.data();
   return p;
 }
 
@@ -72,6 +78,10 @@ void* ch_create(const rg_config* c) {
   h->job32.assign(J32_ROWS * J * n, 0);
   h->jcnt.assign(n, 0);
   h->slab_info.assign((size_t)c->num_slabs * G * E, make_uint2(0u, c->payload_bytes));
+  h->rdst.assign((size_t)RD_ROWS * n, 0);
+  h->pt.assign(G, 0xFF);
+  h->pc.assign(G, 0);
+  h->hm.assign(G, 0);
   return h;
 }
 
@@ -119,6 +129,11 @@ int ch_tick(void* hh, const rg_tick_input* in) {
     p.campaign = in->campaign;
     p.isolate = in->isolate;
   }
+  if (h->staged) {
+    p.prop_target = h->pt.data();
+    p.prop_count = h->pc.data();
+    p.prop_hmask = h->hm.data();
+  }
   for (uint32_t q = 0; q < h->nrep; ++q) {
     switch (h->c.replicas) {
 #define RG_CASE(r) \
@@ -133,6 +148,40 @@ int ch_tick(void* hh, const rg_tick_input* in) {
     }
   }
   h->t++;
+  if (h->staged) {
+    std::fill(h->pt.begin(), h->pt.end(), 0xFF);
+    std::fill(h->pc.begin(), h->pc.end(), 0u);
+    std::fill(h->hm.begin(), h->hm.end(), 0ull);
+    h->staged = false;
+  }
+  return 0;
+}
+
+// = rg_propose's staging (lengths only: the bulk kernel is not emulated); no validation
+int ch_propose(void* hh, const rg_proposal* props, uint64_t n, const uint32_t* lens) {
+  Host* h = (Host*)hh;
+  const uint64_t E = h->c.max_entries_per_msg, slab = h->t % h->c.num_slabs, P = h->c.payload_bytes;
+  for (uint64_t i = 0; i < n; ++i) {
+    const rg_proposal& b = props[i];
+    for (uint32_t x = 0; x < b.count; ++x) {
+      const uint32_t at = h->pc[b.group] + x, ln = lens[b.first + x];
+      if (ln && P) h->hm[b.group] |= 1ull << at;
+      h->slab_info[(slab * h->c.groups + b.group) * E + at] = make_uint2(0u, ln);
+    }
+    h->pt[b.group] = (uint8_t)b.slot;
+    h->pc[b.group] += b.count;
+  }
+  h->staged = n > 0;
+  return 0;
+}
+
+// = notify_applied_kernel's second pass
+int ch_notify_applied(void* hh, uint32_t rid, uint64_t index) {
+  Host* h = (Host*)hh;
+  const uint64_t q = qof(h, rid), N = h->nrep;
+  uint64_t* s64 = h->s64[h->t & 1].data() + q;
+  if (index > s64[S_PROCESSED * N]) return -1;
+  s64[S_APPLIED * N] = index;
   return 0;
 }
 

@@ -82,3 +82,20 @@ def test_c_harness_runs_the_cgo_call_sequence():
     exe = build_c_harness()
     out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0 and "ABI_C OK" in out.stdout, out.stdout + out.stderr
+
+
+@pytest.mark.gpu
+def test_kernel_arguments_live_in_host_memory():
+    """the engine runs with HIP_FORCE_DEV_KERNARG=0 (set by the package, the test
+    session and rg_create before HIP initialises), so kernels read their arguments from host memory.
+    The probe kernel reports its kernel-argument segment address; the runtime must not place it
+    in device memory."""
+    from raftd_amd.engine import load_library
+    assert os.environ.get("HIP_FORCE_DEV_KERNARG") == "0"
+    L = load_library()
+    fn = L.rg_debug_kernarg_placement
+    fn.argtypes = [C.c_int32, C.POINTER(C.c_uint64), C.POINTER(C.c_int32)]
+    addr, dev = C.c_uint64(), C.c_int32()
+    assert fn(0, C.byref(addr), C.byref(dev)) == 0, L.rg_last_error()
+    print(f"kernarg segment at {addr.value:#x}, device memory: {dev.value}")
+    assert addr.value != 0 and dev.value != 1

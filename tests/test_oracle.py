@@ -184,6 +184,42 @@ def test_apply_feedback_c_matches_python(seed):
     assert lagged > 0
 
 
+def random_reads(rng, G, R, t, p=0.15):
+    """ReadIndex requests for one tick: each replica with probability p, a unique non-zero ctx."""
+    return [(g, s, (t << 20) | (g * R + s) + 1) for g in range(G) for s in range(R) if rng.random() < p]
+
+
+@pytest.mark.parametrize("seed", range(5))
+def test_read_index_c_matches_python(seed):
+    """ReadIndex (Raft thesis §6.4, dragonboat's readIndex): a leader confirms its commit index with a
+    heartbeat round carrying the request context, followers forward their requests and get a
+    ReadIndexResp; both restatements agree on every message, state and ready read."""
+    G, R = 3, [3, 5, 1, 2, 3][seed]
+    kw = dict(groups=G, replicas=R, payload_bytes=16, max_entries_per_msg=8, log_capacity=64, snapshot_entries=20,
+              compaction_overhead=5, drop_ppm=[100000, 50000, 0, 100000, 0][seed], seed=400 + seed)
+    a, b = make("c", **kw), make("py", **kw)
+    a.bootstrap()
+    b.bootstrap()
+    rng = np.random.default_rng(seed)
+    ready = 0
+    for t in range(120):
+        reqs = random_reads(rng, G, R, t)
+        assert a.read_index(reqs) == 0 and b.read_index(reqs) == 0
+        ins = random_inputs(rng, G, R, 8)
+        a.tick(*ins)
+        b.tick(*ins)
+        for rid in range(G * R):
+            assert a.replica(rid) == b.replica(rid), (seed, t, rid)
+            for d in range(R):
+                assert a.msgs(rid, d) == b.msgs(rid, d), (seed, t, rid, d)
+            ra = a.read_ready(rid)
+            assert ra == b.read_ready(rid), (seed, t, rid)
+            if ra is not None:
+                ready += 1
+                assert ra[1] <= a.replica(rid)["committed"] or a.replica(rid)["role"] != 2
+    assert ready > 0
+
+
 def test_propose_validation():
     o = pyoracle.Oracle(groups=2, replicas=3, payload_bytes=16, max_entries_per_msg=4)
     py = make("py", groups=2, replicas=3, payload_bytes=16, max_entries_per_msg=4)
