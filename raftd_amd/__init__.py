@@ -5,9 +5,9 @@ is its Python binding. See DESIGN.md.
 """
 import os
 
-# Kernel arguments in host memory (HIP_FORCE_DEV_KERNARG=0), set before anything initialises HIP:
-# DESIGN.md §3.4 — with device-memory kernargs the control kernel intermittently ran on garbage
-# parameters. setdefault: an explicit setting in the environment wins.
+# Kernel arguments in host memory (HIP_FORCE_DEV_KERNARG=0), set before anything initialises HIP.
+# Device-memory kernel arguments are the suspected cause of the intermittent control-kernel
+# faults (DESIGN.md §3 "The control-kernel fault"). An explicit setting in the environment wins.
 os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "0")
 
 from .engine import Engine, RgError, default_config, load_library  # noqa: F401

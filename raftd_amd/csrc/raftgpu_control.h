@@ -7,9 +7,9 @@
 
 #include <type_traits>
 
-// Measurement variants of the control step, off in the product (each changes the
-// kernel's register allocation, and builds with them faulted on the GPU while the same code
-// replayed clean on the CPU under ASan, UBSan and MSan; the product keeps the r01 allocation):
+// Measurement variants of the control step, off in the product until the intermittent GPU fault
+// is closed (DESIGN.md §3 "The control-kernel fault"; the same code replays clean on the CPU
+// under ASan, UBSan and MSan):
 //   RG_CTL_FASTREP   a leader builds the Replicate of its own same-step append from registers
 //   RG_CTL_FRESH     write_entries' fresh-index path (pointer-stepped ring slots, no hull)
 //   RG_CTL_HDRBATCH  handle() loads all eight header words of a message up front

@@ -316,8 +316,9 @@ extern "C" {
 const char* rg_last_error(void) { return g_err.c_str(); }
 
 int rg_create(const rg_config* cfg, rg_engine** out) {
-  // Kernel arguments in host memory: effective when this is the process's first
-  // HIP call; a host that initialised HIP earlier sets HIP_FORCE_DEV_KERNARG=0 itself
+  // Kernel arguments in host memory (DESIGN.md §3 "The control-kernel fault"): effective when this
+  // is the process's first HIP call; a host that initialised HIP earlier sets
+  // HIP_FORCE_DEV_KERNARG=0 itself
   setenv("HIP_FORCE_DEV_KERNARG", "0", 0);
   if (!cfg || !out) return fail(RG_EINVAL, "null argument");
   const rg_config& c = *cfg;

@@ -86,8 +86,9 @@ def test_c_harness_runs_the_cgo_call_sequence():
 
 @pytest.mark.gpu
 def test_kernel_arguments_live_in_host_memory():
-    """the engine runs with HIP_FORCE_DEV_KERNARG=0 (set by the package, the test
-    session and rg_create before HIP initialises), so kernels read their arguments from host memory.
+    """DESIGN.md §3 "The control-kernel fault": the engine runs with HIP_FORCE_DEV_KERNARG=0 (set
+    by the package, the test session and rg_create before HIP initialises), so kernels read their
+    arguments from host memory.
     The probe kernel reports its kernel-argument segment address; the runtime must not place it
     in device memory."""
     from raftd_amd.engine import load_library
