@@ -101,6 +101,9 @@ typedef struct rg_config {
   uint32_t apply_feedback;      /* 0: `applied` follows `processed` at the end of every tick (the state
                                    machine keeps up); 1: it moves only by rg_notify_applied
                                    (dragonboat's NotifyRaftLastApplied, raft/state_machine.go:101-166) */
+  uint32_t initial_members;     /* bootstrap voting membership, bit s = slot s: StartOnDiskReplica's
+                                   initialMembers (raft/raft_manager.go:114-144); 0 = every slot */
+  uint32_t _reserved;
 } rg_config;
 
 typedef struct rg_replica_view {
@@ -109,6 +112,10 @@ typedef struct rg_replica_view {
   uint64_t processed; /* committed entries handed to the state machine (entryLog.processed) */
   uint32_t role, election_tick, heartbeat_tick, rand_timeout, rng_ctr;
   uint32_t granted, responded, active, err, drops;
+  uint32_t members;      /* voting membership as this replica applied it, bit s = slot s */
+  uint32_t snap_members; /* the membership its latest snapshot records */
+  uint32_t cc_pending;   /* leader: a config change is in flight (pendingConfigChange) */
+  uint32_t _mpad;
   uint64_t match[RG_MAX_REPLICAS], next[RG_MAX_REPLICAS], rsnap[RG_MAX_REPLICAS];
   uint8_t rstate[RG_MAX_REPLICAS];
 } rg_replica_view;
@@ -172,6 +179,7 @@ typedef struct rg_persist_state {
   uint64_t first;       /* entries first..last follow (none if first > last); the log keeps its
                            entries below first, drops those above last and at or below marker */
   uint64_t entry_off;   /* position of this replica's first entry in the entries array */
+  uint32_t members, snap_members; /* voting membership now and at the snapshot */
 } rg_persist_state;
 
 typedef struct rg_persist_entry {
@@ -344,6 +352,17 @@ int rg_read_index(rg_engine* e, const rg_read_request* reqs, size_t n);
 /* Reads made ready in the last tick for replicas whose slot bit is set, one per replica at most, in
  * device order; compacted on the device, one hipMemcpyAsync. *n = count; RG_EFULL if > cap. */
 int rg_read_index_results(rg_engine* e, uint32_t slot_mask, rg_read_ready* out, uint64_t cap, uint64_t* n);
+/* Stage a membership change for the next tick: NodeHost.SyncRequestAddReplica (op RG_CC_ADD) /
+ * SyncRequestDeleteReplica (RG_CC_REMOVE) of slot `target` of global shard `group`
+ * (raft/raft_manager.go:165-185), proposed at the local replica `slot` after that tick's Cmd batch.
+ * The leader appends one ConfigChange entry (a follower forwards it; a second change while one is
+ * in flight becomes an empty entry and counts a drop); every replica applies it when the entry is
+ * handed to its state machine: quorum, elections, replication and snapshots then follow the new
+ * membership. RG_EINVAL: bad shard / slot / target / op, or a replica hosted by
+ * another rank; RG_EFULL: a change is already staged for the shard this tick. */
+#define RG_CC_ADD 1u
+#define RG_CC_REMOVE 2u
+int rg_config_change(rg_engine* e, uint64_t group, uint32_t slot, uint32_t op, uint32_t target);
 /* Peer.NotifyRaftLastApplied for n local replicas: replica rids[k]'s state machine has applied
  * through index[k] (<= its processed index — config changes and empty entries included, which the
  * state machine never sees). With rg_config.apply_feedback = 1 this is how `applied` moves: it gates

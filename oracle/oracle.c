@@ -45,6 +45,7 @@ typedef struct {
   uint64_t processed; /* committed entries handed to the state machine (entryLog.processed) */
   uint32_t role, election_tick, heartbeat_tick, rand_timeout, rng_ctr;
   uint32_t granted, responded, active, err, drops;
+  uint32_t members, snap_members, cc_pending; /* DESIGN §1.8 */
   uint64_t match[OR_MAX_R], next[OR_MAX_R], rsnap[OR_MAX_R];
   uint8_t rstate[OR_MAX_R];
   /* log ring: index i in (marker, last] lives at slot i & (L-1) */
@@ -76,6 +77,9 @@ struct or_engine {
   int staged;
   uint64_t* rd_req;   /* [G*R] ReadIndex contexts staged for the next tick (0 none) */
   int rd_staged;
+  uint8_t* cc_slot;   /* [G] membership change staged for the next tick: proposing slot (0xFF none) */
+  uint8_t* cc_desc;   /* [G] its descriptor OR_CC(op, target) */
+  int cc_staged;
 };
 
 /* ---------------------------------------------------------------- helpers */
@@ -122,8 +126,10 @@ void or_payload(const or_engine* e, uint32_t slab, uint32_t group, uint32_t entr
 
 static inline uint32_t id_of(uint32_t slot) { return slot + 1; }
 static inline uint32_t slot_of(uint64_t id) { return (uint32_t)(id - 1); }
-static inline uint32_t quorum(const or_engine* e) { return e->c.replicas / 2 + 1; }
 static inline uint32_t popc(uint32_t x) { return (uint32_t)__builtin_popcount(x); }
+/* raft.quorum over the voting members (numVotingMembers / 2 + 1) */
+static inline uint32_t quorum(const rep_t* r) { return popc(r->members) / 2 + 1; }
+static inline int is_member(const rep_t* r, uint32_t slot) { return (r->members >> slot) & 1u; }
 static inline uint64_t u64min(uint64_t a, uint64_t b) { return a < b ? a : b; }
 static inline uint64_t u64max(uint64_t a, uint64_t b) { return a > b ? a : b; }
 static inline ent_t* log_at(const or_engine* e, const rep_t* r, uint64_t i) {
@@ -221,7 +227,8 @@ static void reset(or_engine* e, rep_t* r, uint64_t t) {
   }
   r->match[r->s] = r->last;
   r->active = 0;
-  r->ri_ctx = 0; /* readIndex.reset */
+  r->ri_ctx = 0;     /* readIndex.reset */
+  r->cc_pending = 0; /* clearPendingConfigChange */
 }
 
 static void become_follower(or_engine* e, rep_t* r, uint64_t t, uint64_t leader) {
@@ -253,11 +260,13 @@ static int remote_try_update(rep_t* r, uint32_t i, uint64_t idx) {
 
 /* Where the Cmds of an append come from: the entries a Propose message
  * carries (ents / pay, P bytes per entry), or, for a tick-input proposal, the synthetic generator
- * (slab >= 0: Cmd k = or_payload(slab, group, k), len P). NULL source: one len-0 no-op. */
+ * (slab >= 0: Cmd k = or_payload(slab, group, k), len P). NULL source: len-0 no-ops. cc != 0: one
+ * ConfigChange entry with that descriptor. */
 typedef struct {
   int slab;
   const ent_t* ents;
   const uint8_t* pay;
+  uint32_t cc;
 } src_t;
 
 /* raft.appendEntries: n entries at term. Returns 0 when the batch was refused by the capacity rule. */
@@ -269,6 +278,12 @@ static int append_entries(or_engine* e, rep_t* r, uint32_t n, const src_t* src) 
     ent_t* en = log_at(e, r, idx);
     en->term = r->term;
     en->type = OR_ENTRY_APP;
+    if (src && src->cc) { /* a ConfigChange entry: no Cmd, its descriptor in len */
+      en->type = OR_ENTRY_CONFIG;
+      en->len = src->cc;
+      en->crc = 0;
+      continue;
+    }
     uint32_t len = !src || !P ? 0 : src->ents ? src->ents[k].len : P;
     if (len) {
       uint8_t* dst = logpay_at(e, r, idx);
@@ -283,7 +298,7 @@ static int append_entries(or_engine* e, rep_t* r, uint32_t n, const src_t* src) 
   }
   r->last += n;
   remote_try_update(r, r->s, r->last);
-  if (e->c.replicas == 1) try_commit(e, r);
+  if (popc(r->members) == 1) try_commit(e, r); /* isSingleNodeQuorum */
   return 1;
 }
 
@@ -291,6 +306,9 @@ static void become_leader(or_engine* e, rep_t* r) {
   r->role = OR_LEADER;
   reset(e, r, r->term);
   r->leader = id_of(r->s);
+  /* preLeaderPromotionHandleConfigChange: a ConfigChange entry in (committed, last] is in flight */
+  for (uint64_t i = r->committed + 1; i <= r->last; ++i)
+    if (log_at(e, r, i)->type == OR_ENTRY_CONFIG) r->cc_pending = 1;
   if (!append_entries(e, r, 1, NULL)) r->err |= OR_ERR_RING_FULL;
 }
 
@@ -316,6 +334,7 @@ static void send_replicate(or_engine* e, rep_t* r, uint32_t to) {
     h.type = OR_INSTALL_SNAPSHOT;
     h.log_index = r->snap_index;
     h.log_term = r->snap_term;
+    h.hint_high = r->snap_members; /* the snapshot's membership */
     r->rsnap[to] = r->snap_index;
     r->rstate[to] = OR_SNAPSHOT;
     send_msg(e, r, &h);
@@ -345,12 +364,12 @@ static void send_replicate(or_engine* e, rep_t* r, uint32_t to) {
 
 static void broadcast_replicate(or_engine* e, rep_t* r) {
   for (uint32_t i = 0; i < e->c.replicas; ++i)
-    if (i != r->s) send_replicate(e, r, i);
+    if (i != r->s && is_member(r, i)) send_replicate(e, r, i);
 }
 
 static void broadcast_heartbeat(or_engine* e, rep_t* r) {
   for (uint32_t i = 0; i < e->c.replicas; ++i) {
-    if (i == r->s) continue;
+    if (i == r->s || !is_member(r, i)) continue;
     or_msg_view h;
     memset(&h, 0, sizeof h);
     h.type = OR_HEARTBEAT;
@@ -362,9 +381,11 @@ static void broadcast_heartbeat(or_engine* e, rep_t* r) {
 
 /* raft.tryCommit + sortMatchValues + entryLog.tryCommit (A.13) */
 static int try_commit(or_engine* e, rep_t* r) {
-  uint32_t R = e->c.replicas;
+  uint32_t R = 0; /* the voting members' match values */
   uint64_t v[OR_MAX_R];
-  for (uint32_t i = 0; i < R; ++i) v[i] = r->match[i];
+  for (uint32_t i = 0; i < e->c.replicas; ++i)
+    if (is_member(r, i)) v[R++] = r->match[i];
+  if (R == 0) return 0;
   for (uint32_t i = 1; i < R; ++i) { /* insertion sort ascending */
     uint64_t x = v[i];
     int j = (int)i - 1;
@@ -374,7 +395,7 @@ static int try_commit(or_engine* e, rep_t* r) {
     }
     v[j + 1] = x;
   }
-  uint64_t q = v[R - quorum(e)];
+  uint64_t q = v[R - quorum(r)];
   if (q > r->committed && term_of(e, r, q) == r->term) {
     r->committed = q;
     return 1;
@@ -439,7 +460,7 @@ static void handle_replicate(or_engine* e, rep_t* r, const msg_in_t* m) {
           en->term = src->term;
           en->type = src->type;
           en->len = src->len;
-          if (src->len) {
+          if (src->len && src->type == OR_ENTRY_APP) {
             uint8_t* dst = logpay_at(e, r, idx);
             memcpy(dst, m->pay + (size_t)k * P, src->len);
             en->crc = entry_crc(e, dst, src->len);
@@ -487,6 +508,7 @@ static void handle_install_snapshot(or_engine* e, rep_t* r, const or_msg_view* m
     r->marker = r->last = r->committed = r->snap_index = r->processed = si;
     r->marker_term = r->snap_term = st;
     r->applied = u64max(r->applied, si);
+    r->members = r->snap_members = (uint32_t)m->hint_high; /* the snapshot's membership */
     resp.log_index = r->last;
     r->restored_at = si;
   }
@@ -506,12 +528,12 @@ static void handle_vote_resp(rep_t* r, uint32_t from_slot, int rejected) {
 static void campaign(or_engine* e, rep_t* r) {
   become_candidate(e, r);
   handle_vote_resp(r, r->s, 0);
-  if (e->c.replicas == 1) {
+  if (popc(r->granted & r->members) == quorum(r)) { /* single-node quorum */
     become_leader(e, r);
     return;
   }
   for (uint32_t i = 0; i < e->c.replicas; ++i) {
-    if (i == r->s) continue;
+    if (i == r->s || !is_member(r, i)) continue;
     or_msg_view h;
     memset(&h, 0, sizeof h);
     h.type = OR_REQUEST_VOTE;
@@ -525,6 +547,7 @@ static void campaign(or_engine* e, rep_t* r) {
 
 static void handle_node_election(or_engine* e, rep_t* r) {
   if (r->role == OR_LEADER) return;
+  if (!is_member(r, r->s)) return; /* selfRemoved: no elections */
   if (r->committed > r->applied) return; /* hasConfigChangeToApply */
   campaign(e, r);
 }
@@ -546,11 +569,11 @@ static void handle_node_request_vote(or_engine* e, rep_t* r, const or_msg_view* 
 
 static void handle_candidate_vote_resp(or_engine* e, rep_t* r, const or_msg_view* m) {
   handle_vote_resp(r, slot_of(m->from), m->reject);
-  uint32_t granted = popc(r->granted), total = popc(r->responded);
-  if (granted == quorum(e)) {
+  uint32_t granted = popc(r->granted & r->members), total = popc(r->responded & r->members);
+  if (granted == quorum(r)) {
     become_leader(e, r);
     broadcast_replicate(e, r);
-  } else if (total - granted == quorum(e)) {
+  } else if (total - granted == quorum(r)) {
     become_follower(e, r, r->term, 0);
   }
 }
@@ -559,6 +582,7 @@ static void handle_candidate_vote_resp(or_engine* e, rep_t* r, const or_msg_view
 
 static void handle_leader_replicate_resp(or_engine* e, rep_t* r, const or_msg_view* m) {
   uint32_t f = slot_of(m->from);
+  if (!is_member(r, f)) return; /* no remote for it */
   r->active |= 1u << f;
   if (!m->reject) {
     int paused = r->rstate[f] == OR_WAIT || r->rstate[f] == OR_SNAPSHOT;
@@ -627,12 +651,13 @@ static void read_confirmed(or_engine* e, rep_t* r, uint64_t ctx, uint64_t index,
 
 static void handle_leader_heartbeat_resp(or_engine* e, rep_t* r, const or_msg_view* m) {
   uint32_t f = slot_of(m->from);
+  if (!is_member(r, f)) return; /* no remote for it */
   r->active |= 1u << f;
   if (r->rstate[f] == OR_WAIT) r->rstate[f] = OR_RETRY;
   if (r->match[f] < r->last) send_replicate(e, r, f);
   if (m->hint != 0 && m->hint == r->ri_ctx) { /* readIndex.confirm */
     r->ri_acks |= 1u << f;
-    if (popc(r->ri_acks) >= quorum(e)) {
+    if (popc(r->ri_acks & r->members) >= quorum(r)) {
       uint64_t ctx = r->ri_ctx;
       r->ri_ctx = 0;
       read_confirmed(e, r, ctx, r->ri_index, r->ri_from);
@@ -644,7 +669,7 @@ static void handle_leader_heartbeat_resp(or_engine* e, rep_t* r, const or_msg_vi
 static void handle_read_index(or_engine* e, rep_t* r, const or_msg_view* m) {
   uint32_t f = slot_of(m->from);
   if (r->role == OR_LEADER) {
-    if (e->c.replicas == 1) {
+    if (quorum(r) == 1) { /* isSingleNodeQuorum */
       read_confirmed(e, r, m->hint, r->committed, f);
     } else if (term_of(e, r, r->committed) != r->term || r->ri_ctx != 0) {
       r->drops++; /* no entry committed in this term yet (thesis §6.4), or a read already pending */
@@ -654,7 +679,7 @@ static void handle_read_index(or_engine* e, rep_t* r, const or_msg_view* m) {
       r->ri_acks = 1u << r->s;
       r->ri_from = f;
       for (uint32_t i = 0; i < e->c.replicas; ++i) { /* broadcastHeartbeatMessageWithHint */
-        if (i == r->s) continue;
+        if (i == r->s || !is_member(r, i)) continue;
         or_msg_view h;
         memset(&h, 0, sizeof h);
         h.type = OR_HEARTBEAT;
@@ -675,9 +700,9 @@ static void handle_read_index(or_engine* e, rep_t* r, const or_msg_view* m) {
 }
 
 static void handle_leader_check_quorum(or_engine* e, rep_t* r) {
-  uint32_t c = 1 + popc(r->active & ~(1u << r->s));
+  uint32_t c = popc((r->active | (1u << r->s)) & r->members); /* leaderHasQuorum */
   r->active = 0;
-  if (c < quorum(e)) become_follower(e, r, r->term, 0);
+  if (c < quorum(r)) become_follower(e, r, r->term, 0);
 }
 
 /* ---------------------------------------------------------------- proposals */
@@ -687,12 +712,22 @@ static void handle_leader_check_quorum(or_engine* e, rep_t* r) {
 static void handle_propose(or_engine* e, rep_t* r, const msg_in_t* mi) {
   const or_msg_view* m = &mi->h;
   uint32_t P = e->c.payload_bytes;
-  src_t src = {(int)m->src_a, mi->ents, mi->pay};
+  const uint32_t cc = (uint32_t)m->hint_high; /* a membership change: one entry */
+  src_t src = {(int)m->src_a, mi->ents, mi->pay, cc};
   if (r->role == OR_LEADER) {
-    if (!append_entries(e, r, m->nent, &src)) {
+    int dropped_cc = 0;
+    if (cc && r->cc_pending) { /* one change at a time: it becomes an empty application entry */
+      src.cc = 0;
+      src.ents = NULL;
+      src.slab = -1;
+      dropped_cc = 1;
+    }
+    if (!append_entries(e, r, m->nent, dropped_cc ? NULL : &src)) {
       r->drops++;
       return;
     }
+    if (dropped_cc) r->drops++;          /* reportDroppedConfigChange */
+    else if (cc) r->cc_pending = 1;      /* setPendingConfigChange */
     broadcast_replicate(e, r);
   } else if (r->role == OR_FOLLOWER && r->leader != 0 && m->src_b == 0) {
     or_msg_view h = *m;
@@ -700,7 +735,7 @@ static void handle_propose(or_engine* e, rep_t* r, const msg_in_t* mi) {
     h.term = 0;
     h.src_b = m->src_b + 1;
     msg_t* fm = send_msg(e, r, &h);
-    if (fm && P && m->nent) { /* the message carries its Cmds */
+    if (fm && P && m->nent && !cc) { /* the message carries its Cmds */
       outbox_t* ob = cur_ob(e, r);
       arena_reserve(e, ob, m->nent);
       fm->ent_off = (uint32_t)ob->n_ents;
@@ -748,9 +783,9 @@ static void tick(or_engine* e, rep_t* r) {
       r->heartbeat_tick = 0;
       local(e, r, OR_LEADER_HEARTBEAT);
     }
-  } else { /* nonLeaderTick */
+  } else { /* nonLeaderTick: a replica outside the membership never starts an election */
     r->election_tick++;
-    if (r->election_tick >= r->rand_timeout) {
+    if (is_member(r, r->s) && r->election_tick >= r->rand_timeout) {
       r->election_tick = 0;
       local(e, r, OR_ELECTION);
     }
@@ -839,6 +874,29 @@ static void handle(or_engine* e, rep_t* r, const msg_in_t* mi) {
   }
 }
 
+/* ---------------------------------------------------------------- membership */
+
+/* raft.addNode / raft.removeNode, reached through the rsm's ApplyConfigChange */
+static void apply_config_change(or_engine* e, rep_t* r, uint32_t cc) {
+  uint32_t op = cc >> 4, slot = (cc & 0xFu) - 1u;
+  r->cc_pending = 0; /* clearPendingConfigChange */
+  if (slot >= e->c.replicas) return;
+  uint32_t bit = 1u << slot;
+  if (op == OR_CC_ADD) {
+    if (r->members & bit) return;
+    r->members |= bit; /* setRemote(id, 0, lastIndex + 1) */
+    r->match[slot] = 0;
+    r->next[slot] = r->last + 1;
+    r->rsnap[slot] = 0;
+    r->rstate[slot] = OR_RETRY;
+  } else if (op == OR_CC_REMOVE) {
+    r->members &= ~bit; /* deleteRemote */
+    r->active &= ~bit;
+    if (slot == r->s && r->role == OR_LEADER) become_follower(e, r, r->term, 0);
+    if (r->role == OR_LEADER && r->members && try_commit(e, r)) broadcast_replicate(e, r);
+  }
+}
+
 /* ---------------------------------------------------------------- tick driver */
 
 static void step_replica(or_engine* e, rep_t* r) {
@@ -897,6 +955,17 @@ static void step_replica(or_engine* e, rep_t* r) {
     mi.pay = ppay;
     handle(e, r, &mi);
   }
+  /* 4a. membership change input (or_config_change): one ConfigChange entry */
+  if (e->cc_staged && e->cc_slot[r->g] == r->s) {
+    msg_in_t mi;
+    memset(&mi, 0, sizeof mi);
+    mi.h.type = OR_PROPOSE;
+    mi.h.from = (uint8_t)id_of(r->s);
+    mi.h.nent = 1;
+    mi.h.src_a = (uint32_t)(e->t % e->c.num_slabs);
+    mi.h.hint_high = e->cc_desc[r->g];
+    handle(e, r, &mi);
+  }
   /* 4b. ReadIndex input */
   if (e->rd_staged && e->rd_req[rid]) {
     msg_in_t mi;
@@ -910,11 +979,17 @@ static void step_replica(or_engine* e, rep_t* r) {
   /* GetUpdate.CommittedEntries = (processed, committed] (a restored range excluded), then
    * commitUpdate: processed = committed; applied follows unless the state machine reports it */
   r->apply_lo = u64max(processed_start, r->restored_at) + 1;
+  /* the rsm applies the ConfigChange entries it is handed */
+  for (uint64_t i = r->apply_lo; i <= r->committed; ++i) {
+    const ent_t* en = log_at(e, r, i);
+    if (en->type == OR_ENTRY_CONFIG && en->len) apply_config_change(e, r, en->len);
+  }
   r->processed = r->committed;
   if (!e->c.apply_feedback) r->applied = r->processed;
   if (e->c.snapshot_entries && r->applied >= r->snap_index && r->applied - r->snap_index >= e->c.snapshot_entries) {
     r->snap_index = r->applied;
     r->snap_term = term_of(e, r, r->applied);
+    r->snap_members = r->members;
     r->took = 1;
     uint64_t c = r->snap_index > e->c.compaction_overhead ? r->snap_index - e->c.compaction_overhead : 0;
     if (c > r->marker) {
@@ -967,6 +1042,22 @@ int or_tick(or_engine* e, const or_tick_input* in, int nthreads) {
     memset(e->rd_req, 0, (size_t)e->nrep * 8);
     e->rd_staged = 0;
   }
+  if (e->cc_staged) {
+    memset(e->cc_slot, 0xFF, e->c.groups);
+    e->cc_staged = 0;
+  }
+  return 0;
+}
+
+int or_config_change(or_engine* e, uint64_t group, uint32_t slot, uint32_t op, uint32_t target) {
+  if (group < e->c.group_base || group >= (uint64_t)e->c.group_base + e->c.groups || slot >= e->c.replicas ||
+      target >= e->c.replicas || (op != OR_CC_ADD && op != OR_CC_REMOVE))
+    return -1;
+  uint32_t g = (uint32_t)(group - e->c.group_base);
+  if (e->cc_slot[g] != 0xFF) return -3;
+  e->cc_slot[g] = (uint8_t)slot;
+  e->cc_desc[g] = (uint8_t)OR_CC(op, target);
+  e->cc_staged = 1;
   return 0;
 }
 
@@ -1054,6 +1145,7 @@ int or_create(const or_config* cfg, or_engine** out) {
   if (c->max_entries_per_msg < 1 || c->max_entries_per_msg > 64) return -1;
   if (c->max_msgs_per_pair < 1 || c->max_msgs_per_pair > 16) return -1;
   if (c->num_slabs < 2 || c->election_rtt < 1 || c->heartbeat_rtt < 1) return -1;
+  if (c->initial_members >> c->replicas) return -1;
   or_engine* e = (or_engine*)calloc(1, sizeof *e);
   e->c = *c;
   e->nrep = c->groups * c->replicas;
@@ -1063,6 +1155,9 @@ int or_create(const or_config* cfg, or_engine** out) {
   e->stg_ents = (ent_t*)calloc((size_t)c->groups * c->max_entries_per_msg, sizeof(ent_t));
   e->stg_pay = (uint8_t*)calloc((size_t)c->groups * c->max_entries_per_msg * (c->payload_bytes ? c->payload_bytes : 1), 1);
   e->rd_req = (uint64_t*)calloc((size_t)c->groups * c->replicas, 8);
+  e->cc_slot = (uint8_t*)malloc(c->groups);
+  memset(e->cc_slot, 0xFF, c->groups);
+  e->cc_desc = (uint8_t*)calloc(c->groups, 1);
   e->reps = (rep_t*)calloc(e->nrep, sizeof(rep_t));
   for (uint32_t i = 0; i < e->nrep; ++i) {
     rep_t* r = &e->reps[i];
@@ -1098,6 +1193,8 @@ void or_destroy(or_engine* e) {
   free(e->stg_ents);
   free(e->stg_pay);
   free(e->rd_req);
+  free(e->cc_slot);
+  free(e->cc_desc);
   free(e);
 }
 
@@ -1111,6 +1208,7 @@ int or_bootstrap(or_engine* e) {
     r->snap_index = r->snap_term = r->cap_base = 0;
     r->err = r->drops = 0;
     r->rng_ctr = 0;
+    r->members = r->snap_members = e->c.initial_members ? e->c.initial_members : (1u << R) - 1u;
     become_follower(e, r, 1, 0);
     for (uint32_t k = 0; k < R; ++k) {
       ent_t* en = log_at(e, r, k + 1);
@@ -1164,6 +1262,9 @@ int or_get_replica(const or_engine* e, uint32_t rid, or_replica_view* v) {
   v->active = r->active;
   v->err = r->err;
   v->drops = r->drops;
+  v->members = r->members;
+  v->snap_members = r->snap_members;
+  v->cc_pending = r->cc_pending;
   for (uint32_t k = 0; k < e->c.replicas; ++k) {
     v->match[k] = r->match[k];
     v->next[k] = r->next[k];
@@ -1209,7 +1310,7 @@ int or_get_entry(const or_engine* e, uint32_t rid, uint64_t index, or_entry_view
   out->len = en->len;
   out->crc = en->crc;
   out->_pad = 0;
-  if (payload && en->len) memcpy(payload, logpay_at(e, r, index), en->len);
+  if (payload && en->len && en->type == OR_ENTRY_APP) memcpy(payload, logpay_at(e, r, index), en->len);
   return 0;
 }
 
@@ -1220,7 +1321,7 @@ int or_import_replica(or_engine* e, uint32_t rid, const or_replica_view* v, cons
   if (v->last < v->marker || v->last - v->marker > e->c.log_capacity) return -1;
   if (lens)
     for (uint64_t k = 0; k < v->last - v->marker; ++k)
-      if (lens[k] > e->c.payload_bytes) return -1;
+      if (lens[k] > e->c.payload_bytes && !(types && (types[k] & 0xFFu) == OR_ENTRY_CONFIG)) return -1;
   r->term = v->term;
   r->vote = v->vote;
   r->leader = v->leader;
@@ -1246,6 +1347,9 @@ int or_import_replica(or_engine* e, uint32_t rid, const or_replica_view* v, cons
   r->active = v->active;
   r->err = v->err;
   r->drops = v->drops;
+  r->members = v->members;
+  r->snap_members = v->snap_members;
+  r->cc_pending = v->cc_pending;
   for (uint32_t k = 0; k < OR_MAX_R; ++k) {
     r->match[k] = v->match[k];
     r->next[k] = v->next[k];
@@ -1265,7 +1369,7 @@ int or_import_replica(or_engine* e, uint32_t rid, const or_replica_view* v, cons
       memcpy(logpay_at(e, r, i), payloads + k * P, len);
       en->crc = entry_crc(e, logpay_at(e, r, i), len);
     } else {
-      en->len = 0;
+      en->len = en->type == OR_ENTRY_CONFIG && lens ? lens[k] : 0; /* a ConfigChange keeps its descriptor */
       en->crc = 0;
     }
   }

@@ -35,6 +35,10 @@ enum {
 enum { OR_FOLLOWER = 0, OR_CANDIDATE = 1, OR_LEADER = 2 };
 enum { OR_RETRY = 0, OR_WAIT = 1, OR_REPLICATE_ST = 2, OR_SNAPSHOT = 3 };
 enum { OR_ENTRY_APP = 0, OR_ENTRY_CONFIG = 1 };
+/* A ConfigChange entry's descriptor, kept in its `len` field (it has no Cmd): op << 4 | (slot + 1);
+ * 0 = the bootstrap entries, which change nothing */
+enum { OR_CC_ADD = 1, OR_CC_REMOVE = 2 };
+#define OR_CC(op, slot) ((uint32_t)(op) << 4 | ((uint32_t)(slot) + 1u))
 #define OR_ENTRY_EMPTY 0x100u /* import: application entry with an empty Cmd (no payload) */
 enum {
   OR_ERR_CONFLICT_COMMITTED = 1, OR_ERR_COMMIT_BEYOND_LAST = 2, OR_ERR_RING_FULL = 4,
@@ -55,6 +59,8 @@ typedef struct or_config {
   uint32_t crc32c; /* entry checksum: 0 = CRC-32/IEEE (zlib), 1 = CRC-32C (Castagnoli) */
   uint32_t apply_feedback; /* 0: applied follows processed at the end of every step (the state machine
                               keeps up); 1: applied moves only by or_notify_applied (NotifyRaftLastApplied) */
+  uint32_t initial_members; /* bootstrap membership, bit s = slot s (StartOnDiskReplica's initialMembers);
+                               0 = every slot */
 } or_config;
 
 /* Field order identical to rg_replica_view (include/raftgpu.h) so tests compare by name. */
@@ -63,6 +69,10 @@ typedef struct or_replica_view {
   uint64_t snap_index, snap_term, cap_base, processed;
   uint32_t role, election_tick, heartbeat_tick, rand_timeout, rng_ctr;
   uint32_t granted, responded, active, err, drops;
+  uint32_t members;      /* voting membership as this replica applied it, bit s = slot s */
+  uint32_t snap_members; /* the membership its latest snapshot records */
+  uint32_t cc_pending;   /* leader: a config change is in flight (pendingConfigChange) */
+  uint32_t _mpad;
   uint64_t match[OR_MAX_R], next[OR_MAX_R], rsnap[OR_MAX_R];
   uint8_t rstate[OR_MAX_R];
 } or_replica_view;
@@ -131,6 +141,11 @@ int or_import_replica(or_engine* e, uint32_t rid, const or_replica_view* v,
  * nothing: -1 invalid, -3 batch full. Cmd bytes packed in lens order (entry j at the sum of
  * lens[0..j)). */
 int or_propose(or_engine* e, const or_proposal* p, size_t n, const uint8_t* payload, const uint32_t* lens);
+/* Stage a membership change for the next tick (SyncRequestAddReplica / SyncRequestDeleteReplica,
+ * raft/raft_manager.go:165-185): a ConfigChange entry adding (OR_CC_ADD) or removing (OR_CC_REMOVE)
+ * slot `target`, proposed at replica `slot` of shard `group` after that tick's Cmd batch. -1 invalid,
+ * -3 a change is already staged for the shard this tick. */
+int or_config_change(or_engine* e, uint64_t group, uint32_t slot, uint32_t op, uint32_t target);
 /* Append a message to rid_src's most recent outbox so it is delivered next tick. Replicate
  * entries are taken from the sender's current log (indices log_index+1 ..). */
 int or_deliver(or_engine* e, uint32_t rid_src, const or_msg_view* m);

@@ -33,7 +33,7 @@ class Config(C.Structure):
         ("election_rtt", C.c_uint32), ("heartbeat_rtt", C.c_uint32), ("check_quorum", C.c_uint32),
         ("snapshot_entries", C.c_uint32), ("compaction_overhead", C.c_uint32),
         ("drop_ppm", C.c_uint32), ("group_base", C.c_uint32), ("seed", C.c_uint64),
-        ("crc32c", C.c_uint32), ("apply_feedback", C.c_uint32),
+        ("crc32c", C.c_uint32), ("apply_feedback", C.c_uint32), ("initial_members", C.c_uint32),
     ]
 
 
@@ -46,6 +46,7 @@ class ReplicaView(C.Structure):
         ("role", C.c_uint32), ("election_tick", C.c_uint32), ("heartbeat_tick", C.c_uint32),
         ("rand_timeout", C.c_uint32), ("rng_ctr", C.c_uint32), ("granted", C.c_uint32),
         ("responded", C.c_uint32), ("active", C.c_uint32), ("err", C.c_uint32), ("drops", C.c_uint32),
+        ("members", C.c_uint32), ("snap_members", C.c_uint32), ("cc_pending", C.c_uint32), ("_mpad", C.c_uint32),
         ("match", C.c_uint64 * MAX_R), ("next", C.c_uint64 * MAX_R), ("rsnap", C.c_uint64 * MAX_R),
         ("rstate", C.c_uint8 * MAX_R),
     ]
@@ -78,7 +79,17 @@ class TickInput(C.Structure):
                 ("isolate", C.c_void_p), ("flags", C.c_uint32)]
 
 
-REPLICA_FIELDS = [f for f, _ in ReplicaView._fields_]
+REPLICA_FIELDS = [f for f, _ in ReplicaView._fields_ if not f.startswith("_")]
+CC_ADD, CC_REMOVE = 1, 2  # OR_CC_ADD / OR_CC_REMOVE
+
+
+def with_members(view: dict, R: int) -> dict:
+    """A view for import: a dict without membership fields means every slot is a member."""
+    if "members" not in view:
+        view = dict(view, members=(1 << R) - 1)
+    if "snap_members" not in view:
+        view = dict(view, snap_members=view["members"])
+    return view
 MSG_FIELDS = [f for f, _ in MsgView._fields_]
 
 
@@ -116,6 +127,7 @@ def lib():
                                         C.c_void_p]
         L.or_propose.argtypes = [vp, C.POINTER(Proposal), C.c_size_t, C.c_void_p, C.c_void_p]
         L.or_notify_applied.argtypes = [vp, u32, u64]
+        L.or_config_change.argtypes = [vp, u64, u32, u32, u32]
         L.or_read_index.argtypes = [vp, C.POINTER(ReadRequest), C.c_size_t]
         L.or_get_read_ready.argtypes = [vp, u32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.or_tick.restype = C.c_int
@@ -136,7 +148,7 @@ def default_config(**kw) -> dict:
     c = dict(groups=4, replicas=3, log_capacity=2048, payload_bytes=256, max_entries_per_msg=64,
              max_msgs_per_pair=8, num_slabs=2, election_rtt=10, heartbeat_rtt=1, check_quorum=1,
              snapshot_entries=1000, compaction_overhead=5, drop_ppm=0, seed=0x5EED, group_base=0, crc32c=0,
-             apply_feedback=0)
+             apply_feedback=0, initial_members=0)
     c.update(kw)
     return c
 
@@ -284,6 +296,7 @@ class Oracle:
         return [self.entry(rid, i)["term"] for i in range(r["marker"] + 1, r["last"] + 1)]
 
     def import_replica(self, rid, view: dict, terms, types=None, payloads=None, lens=None):
+        view = with_members(view, self.R)
         v = ReplicaView()
         for f in REPLICA_FIELDS:
             if f in view:
@@ -316,6 +329,11 @@ class Oracle:
         """(ctx, index) of the read replica rid made ready in the last tick, or None."""
         c, i = C.c_uint64(), C.c_uint64()
         return (c.value, i.value) if self.L.or_get_read_ready(self.h, rid, C.byref(c), C.byref(i)) == 1 else None
+
+    def config_change(self, group, slot, op, target) -> int:
+        """Stage a membership change for the next tick (or_config_change): 0, -1 invalid, -3 one
+        already staged for the shard."""
+        return self.L.or_config_change(self.h, group, slot, op, target)
 
     def notify_applied(self, rid, index) -> int:
         """or_notify_applied (Peer.NotifyRaftLastApplied): 0, or -1 if index > processed."""

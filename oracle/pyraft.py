@@ -32,6 +32,7 @@ FOLLOWER, CANDIDATE, LEADER = 0, 1, 2
 RETRY, WAIT, REPL, SNAP = 0, 1, 2, 3
 ERR_CONFLICT, ERR_BEYOND, ERR_RING, ERR_CRC, ERR_EMPTY_SNAP = 1, 2, 4, 8, 16
 LEADER_MSGS = (REPLICATE, INSTALL_SNAPSHOT, HEARTBEAT, READ_INDEX_RESP)
+CC_ADD, CC_REMOVE = 1, 2  # membership change ops: descriptor op << 4 | (slot + 1)
 
 
 def mix64(z: int) -> int:
@@ -60,11 +61,16 @@ def msg(type, to, **kw):
 
 
 class Entry:
-    __slots__ = ("term", "type", "data", "crc")
+    __slots__ = ("term", "type", "data", "crc", "cc")
 
-    def __init__(self, term, type=0, data=b""):
-        self.term, self.type, self.data = term, type, data
+    def __init__(self, term, type=0, data=b"", cc=0):
+        self.term, self.type, self.data, self.cc = term, type, data, cc
         self.crc = zlib.crc32(data) if data else 0
+
+    @property
+    def len(self):
+        """Cmd length; a ConfigChange entry reports its descriptor."""
+        return self.cc if self.type == 1 else len(self.data)
 
 
 class Remote:
@@ -136,6 +142,14 @@ class Replica:
         self.emitted = {}
         self.pending_read = None  # leader: [ctx, index, acks set, requester slot]
         self.ready_read = None    # (tick, ctx, index) of the read made ready in a step
+        self.members = set(range(sim.R))  # voting membership as applied here
+        self.snap_members = set(range(sim.R))
+        self.cc_pending = False
+        self.restored_at = 0
+
+    @property
+    def quorum(self):
+        return len(self.members) // 2 + 1
 
     # -- log (entryLog) --
     @property
@@ -191,6 +205,7 @@ class Replica:
         self.remotes[self.s].match = self.last
         self.active = set()
         self.pending_read = None
+        self.cc_pending = False  # clearPendingConfigChange
 
     def become_follower(self, t, leader):
         self.role = FOLLOWER
@@ -207,26 +222,33 @@ class Replica:
         self.role = LEADER
         self.reset(self.term)
         self.leader = self.id
+        # a ConfigChange entry not yet committed is still in flight
+        self.cc_pending = any(self.log[i - self.marker - 1].type == 1 for i in range(self.committed + 1, self.last + 1))
         if not self.append(1, ()):
             self.err |= ERR_RING
 
-    def append(self, n, cmds):
+    def append(self, n, cmds, cc=0):
         """appendEntries of n entries at the current term; cmds[k] = Cmd bytes of entry k (() for
-        the leader's empty no-op)."""
+        the leader's empty no-op); cc: one ConfigChange entry with that descriptor."""
         c = self.sim.cfg
         if self.last + n > self.cap_base + c["log_capacity"]:
             return False
         for k in range(n):
-            self.log.append(Entry(self.term, 0, cmds[k] if k < len(cmds) else b""))
+            if cc:
+                self.log.append(Entry(self.term, 1, b"", cc))
+            else:
+                self.log.append(Entry(self.term, 0, cmds[k] if k < len(cmds) else b""))
         self.remotes[self.s].try_update(self.last)
-        if self.sim.R == 1:
+        if len(self.members) == 1:
             self.try_commit()
         return True
 
     # -- leader --
     def try_commit(self):
-        vals = sorted(r.match for r in self.remotes)
-        q = vals[self.sim.R - self.sim.quorum]
+        vals = sorted(self.remotes[i].match for i in self.members)
+        if not vals:
+            return False
+        q = vals[len(vals) - self.quorum]
         if q > self.committed and self.term_at(q) == self.term:
             self.committed = q
             return True
@@ -243,7 +265,8 @@ class Replica:
                 self.err |= ERR_EMPTY_SNAP
                 return
             rp.snap, rp.state = self.snap_index, SNAP
-            self.send(msg(INSTALL_SNAPSHOT, to + 1, log_index=self.snap_index, log_term=self.snap_term))
+            self.send(msg(INSTALL_SNAPSHOT, to + 1, log_index=self.snap_index, log_term=self.snap_term,
+                          hint_high=sum(1 << k for k in self.snap_members)))
             return
         nxt = rp.next
         ents = self.log[nxt - self.marker - 1: nxt - self.marker - 1 + self.sim.cfg["max_entries_per_msg"]] \
@@ -255,11 +278,13 @@ class Replica:
 
     def broadcast_replicate(self):
         for i in range(self.sim.R):
-            if i != self.s:
+            if i != self.s and i in self.members:
                 self.send_replicate(i)
 
     def on_replicate_resp(self, m):
         f = m["frm"] - 1
+        if f not in self.members:
+            return
         rp = self.remotes[f]
         self.active.add(f)
         if not m["reject"]:
@@ -277,6 +302,8 @@ class Replica:
 
     def on_heartbeat_resp(self, m):
         f = m["frm"] - 1
+        if f not in self.members:
+            return
         self.active.add(f)
         rp = self.remotes[f]
         if rp.state == WAIT:
@@ -286,7 +313,7 @@ class Replica:
         pr = self.pending_read
         if m["hint"] and pr is not None and m["hint"] == pr[0]:
             pr[2].add(f)
-            if len(pr[2]) >= self.sim.quorum:
+            if len(pr[2] & self.members) >= self.quorum:
                 self.pending_read = None
                 self.read_confirmed(pr[0], pr[1], pr[3])
 
@@ -300,14 +327,14 @@ class Replica:
     def on_read_index(self, m):
         f = m["frm"] - 1
         if self.role == LEADER:
-            if self.sim.R == 1:
+            if self.quorum == 1:
                 self.read_confirmed(m["hint"], self.committed, f)
             elif self.term_at(self.committed) != self.term or self.pending_read is not None:
                 self.drops += 1
             else:
                 self.pending_read = [m["hint"], self.committed, {self.s}, f]
                 for i in range(self.sim.R):
-                    if i != self.s:
+                    if i != self.s and i in self.members:
                         self.send(msg(HEARTBEAT, i + 1, commit=min(self.remotes[i].match, self.committed),
                                       hint=m["hint"]))
         elif self.role == FOLLOWER and self.leader != 0 and f == self.s:
@@ -342,7 +369,7 @@ class Replica:
                 else:
                     del self.log[ci - self.marker - 1:]
                     for e in m["ents"][conflict:]:
-                        ne = Entry(e.term, e.type, e.data)
+                        ne = Entry(e.term, e.type, e.data, e.cc)
                         if ne.crc != e.crc:
                             self.err |= ERR_CRC
                         self.log.append(ne)
@@ -365,6 +392,9 @@ class Replica:
             self.marker = self.committed = self.snap_index = self.processed = si
             self.marker_term = self.snap_term = st
             self.applied = max(self.applied, si)
+            self.members = {k for k in range(8) if m["hint_high"] >> k & 1}  # the snapshot's membership
+            self.snap_members = set(self.members)
+            self.restored_at = si
             resp["log_index"] = self.last
         self.send(resp)
 
@@ -372,11 +402,11 @@ class Replica:
     def campaign(self):
         self.become_candidate()
         self.votes[self.s] = True
-        if self.sim.R == 1:
+        if sum(1 for k, v in self.votes.items() if v and k in self.members) == self.quorum:
             self.become_leader()
             return
         for i in range(self.sim.R):
-            if i != self.s:
+            if i != self.s and i in self.members:
                 self.send(msg(REQUEST_VOTE, i + 1, term=self.term, log_index=self.last,
                               log_term=self.term_at(self.last)))
 
@@ -391,11 +421,12 @@ class Replica:
         f = m["frm"] - 1
         if f not in self.votes:
             self.votes[f] = not m["reject"]
-        yes = sum(1 for v in self.votes.values() if v)
-        if yes == self.sim.quorum:
+        yes = sum(1 for k, v in self.votes.items() if v and k in self.members)
+        total = sum(1 for k in self.votes if k in self.members)
+        if yes == self.quorum:
             self.become_leader()
             self.broadcast_replicate()
-        elif len(self.votes) - yes == self.sim.quorum:
+        elif total - yes == self.quorum:
             self.become_follower(self.term, 0)
 
     # -- Handle --
@@ -416,7 +447,7 @@ class Replica:
                 self.local(LEADER_HEARTBEAT)
         else:
             self.etick += 1
-            if self.etick >= self.rand_to:
+            if self.s in self.members and self.etick >= self.rand_to:  # selfRemoved: no elections
                 self.etick = 0
                 self.local(ELECTION)
 
@@ -437,24 +468,30 @@ class Replica:
         if t == LOCAL_TICK:
             self.tick()
         elif t == ELECTION:
-            if role != LEADER and not self.committed > self.applied:
+            if role != LEADER and self.s in self.members and not self.committed > self.applied:
                 self.campaign()
         elif t == LEADER_HEARTBEAT:
             if role == LEADER:
                 for i in range(self.sim.R):
-                    if i != self.s:
+                    if i != self.s and i in self.members:
                         self.send(msg(HEARTBEAT, i + 1, commit=min(self.remotes[i].match, self.committed)))
         elif t == CHECK_QUORUM:
             if role == LEADER:
-                c_act = 1 + len(self.active - {self.s})
+                c_act = len((self.active | {self.s}) & self.members)
                 self.active = set()
-                if c_act < self.sim.quorum:
+                if c_act < self.quorum:
                     self.become_follower(self.term, 0)
-        elif t == PROPOSE:  # the message carries its Cmds (m["ents"])
+        elif t == PROPOSE:  # the message carries its Cmds (m["ents"]), or a membership change
+            cc = m["hint_high"]
             if role == LEADER:
-                if not self.append(m["nent"], [e.data for e in m["ents"]]):
+                dropped = bool(cc) and self.cc_pending  # one change at a time: an empty entry instead
+                if not self.append(m["nent"], [] if cc else [e.data for e in m["ents"]], 0 if dropped else cc):
                     self.drops += 1
                     return
+                if dropped:
+                    self.drops += 1
+                elif cc:
+                    self.cc_pending = True
                 self.broadcast_replicate()
             elif role == FOLLOWER and self.leader != 0 and m["src_b"] == 0:
                 f = dict(m)
@@ -496,6 +533,25 @@ class Replica:
             if role == CANDIDATE:
                 self.on_vote_resp(m)
 
+    # -- membership: raft.addNode / removeNode through the rsm's ApplyConfigChange --
+    def apply_config_change(self, cc):
+        op, slot = cc >> 4, (cc & 0xF) - 1
+        self.cc_pending = False
+        if slot >= self.sim.R:
+            return
+        if op == CC_ADD:
+            if slot in self.members:
+                return
+            self.members.add(slot)
+            self.remotes[slot] = Remote(0, self.last + 1)
+        elif op == CC_REMOVE:
+            self.members.discard(slot)
+            self.active.discard(slot)
+            if slot == self.s and self.role == LEADER:
+                self.become_follower(self.term, 0)
+            if self.role == LEADER and self.members and self.try_commit():
+                self.broadcast_replicate()
+
     # -- views (same field names as the C views) --
     def view(self):
         R = self.sim.R
@@ -508,6 +564,8 @@ class Replica:
             granted=sum(1 << k for k, v in self.votes.items() if v),
             responded=sum(1 << k for k in self.votes),
             active=sum(1 << k for k in self.active), err=self.err, drops=self.drops & 0xFFFFFFFF,
+            members=sum(1 << k for k in self.members), snap_members=sum(1 << k for k in self.snap_members),
+            cc_pending=int(self.cc_pending),
             match=[r.match for r in self.remotes][:R], next=[r.next for r in self.remotes][:R],
             rsnap=[r.snap for r in self.remotes][:R], rstate=[r.state for r in self.remotes][:R],
         )
@@ -520,13 +578,22 @@ class Sim:
         from .pyoracle import default_config  # same defaults; no code shared with oracle.c
         self.cfg = default_config(**cfg)
         self.G, self.R = self.cfg["groups"], self.cfg["replicas"]
-        self.quorum = self.R // 2 + 1
         self.t = 0
         self.isolate = None
         self.reps = [Replica(self, g, s) for g in range(self.G) for s in range(self.R)]
         self._pay = {}
         self.staged = {}  # window group -> (slot, [cmd bytes]) for the next tick (propose)
         self.reads = {}   # window rid -> ReadIndex ctx for the next tick
+        self.ccs = {}     # window group -> (slot, descriptor) membership change for the next tick
+
+    def config_change(self, group, slot, op, target):
+        base = self.cfg["group_base"]
+        if not (base <= group < base + self.G) or slot >= self.R or target >= self.R or op not in (CC_ADD, CC_REMOVE):
+            return -1
+        if group - base in self.ccs:
+            return -3
+        self.ccs[group - base] = (slot, op << 4 | (target + 1))
+        return 0
 
     def read_index(self, reqs):
         base = self.cfg["group_base"]
@@ -580,8 +647,11 @@ class Sim:
 
     def bootstrap(self):
         R = self.R
+        im = self.cfg.get("initial_members", 0) or (1 << R) - 1
         for r in self.reps:
             r.rng = 0
+            r.members = {k for k in range(R) if im >> k & 1}
+            r.snap_members = set(r.members)
             r.become_follower(1, 0)
             r.log = [Entry(1, 1) for _ in range(R)]
             r.committed = R
@@ -594,6 +664,7 @@ class Sim:
             raise ValueError("tick-input proposals while caller proposals are staged")
         staged, self.staged = self.staged, {}
         reads, self.reads = self.reads, {}
+        ccs, self.ccs = self.ccs, {}
         self.isolate = isolate
         inbox = {id(r): [] for r in self.reps}
         for r in self.reps:  # deliver last tick's outboxes
@@ -607,7 +678,8 @@ class Sim:
         for g in range(self.G):
             for s in range(self.R):
                 r = self.reps[g * self.R + s]
-                marker_start = r.marker
+                marker_start, processed_start = r.marker, r.processed
+                r.restored_at = 0
                 for _, lst in r._inbox:
                     for m in lst:
                         r.handle(m)
@@ -627,14 +699,24 @@ class Sim:
                     hm = sum(1 << k for k, x in enumerate(cmds) if x)
                     r.handle(msg(PROPOSE, r.id, frm=r.id, nent=len(cmds), hint=hm, src_a=slab, src_b=0,
                                  ents=tuple(Entry(0, 0, x) for x in cmds)))
+                if g in ccs and ccs[g][0] == s:
+                    r.handle(msg(PROPOSE, r.id, frm=r.id, nent=1, hint=0, hint_high=ccs[g][1], src_a=slab,
+                                 src_b=0, ents=()))
                 if reads.get(rid):
                     r.handle(msg(READ_INDEX, r.id, frm=r.id, hint=reads[rid]))
+                i = max(processed_start, r.restored_at) + 1
+                while i <= r.committed:  # a removal may commit more: those are handed over too
+                    e = r.log[i - r.marker - 1]
+                    if e.type == 1 and e.cc:
+                        r.apply_config_change(e.cc)
+                    i += 1
                 r.processed = r.committed  # handed to the state machine this step
                 if not self.cfg["apply_feedback"]:
                     r.applied = r.processed
                 se, co = self.cfg["snapshot_entries"], self.cfg["compaction_overhead"]
                 if se and r.applied >= r.snap_index and r.applied - r.snap_index >= se:
                     r.snap_index, r.snap_term = r.applied, r.term_at(r.applied)
+                    r.snap_members = set(r.members)
                     cpt = r.snap_index - co if r.snap_index > co else 0
                     if cpt > r.marker:
                         mt = r.term_at(cpt)
@@ -662,7 +744,7 @@ class Sim:
         if not (r.marker < index <= r.last):
             return None
         e = r.log[index - r.marker - 1]
-        return dict(term=e.term, type=e.type, len=len(e.data), crc=e.crc)
+        return dict(term=e.term, type=e.type, len=e.len, crc=e.crc)
 
     # -- scenario helpers (KATs): same contract as or_import_replica / or_deliver --
     def import_replica(self, rid, view: dict, terms, types=None, payloads=None, lens=None):
@@ -680,12 +762,16 @@ class Sim:
         r.votes = {k: bool(g >> k & 1) for k in range(8) if resp >> k & 1}
         r.active = {k for k in range(8) if view.get("active", 0) >> k & 1}
         r.pending_read = r.ready_read = None
+        r.members = {k for k in range(8) if view.get("members", (1 << self.R) - 1) >> k & 1}
+        r.snap_members = {k for k in range(8) if view.get("snap_members", view.get("members", (1 << self.R) - 1)) >> k & 1}
+        r.cc_pending = bool(view.get("cc_pending", 0))
         r.log = []
         for k, t in enumerate(terms):
-            ty = 0 if types is None else types[k]
+            ty = 0 if types is None else types[k] & 0xFF
             ln = P if lens is None else lens[k]
-            data = payloads[k * P:k * P + ln] if (payloads is not None and P and ty == 0) else b""
-            r.log.append(Entry(t, ty, bytes(data)))
+            empty = types is not None and types[k] & 0x100
+            data = payloads[k * P:k * P + ln] if (payloads is not None and P and ty == 0 and not empty) else b""
+            r.log.append(Entry(t, ty, bytes(data), ln if ty == 1 and lens is not None else 0))
         assert r.last == view.get("last", r.last)
         r.remotes = []
         for k in range(self.R):

@@ -473,6 +473,11 @@ class LoopbackCluster(_Feeds):
             k, lr = self.loc[int(r)]
             self.engines[k].notify_applied([lr], [int(i)])
 
+    def config_change(self, group, slot, op, target):
+        """rg_config_change on the rank hosting replica `slot` of cluster group `group`."""
+        gg = group + self.rid0 // self.R
+        self.engines[rank_of(gg, slot, self.N)].config_change(gg, slot, op, target)
+
     def read_index(self, reqs):
         """rg_read_index on the rank hosting each request's replica (cluster group ids)."""
         per = [[] for _ in range(self.N)]

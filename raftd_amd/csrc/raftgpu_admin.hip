@@ -30,6 +30,8 @@ __global__ void gather_replicas_kernel(AdminParams a, uint32_t first, uint32_t n
   v.responded = s32[S_RESPONDED * N]; v.active = s32[S_ACTIVE * N];
   v.err = s32[S_ERR * N] | a.crc_err[q];
   v.drops = s32[S_DROPS * N];
+  v.members = s32[S_MEMBERS * N]; v.snap_members = s32[S_SNAP_MEMBERS * N]; v.cc_pending = s32[S_CC_PENDING * N];
+  v._mpad = 0;
   for (uint32_t j = 0; j < RG_MAX_REPLICAS; ++j) {
     const bool in = j < t.R;
     v.match[j] = in ? t.rem_in[(0 * t.R + j) * N + q] : 0;
@@ -84,7 +86,7 @@ __global__ void gather_entries_kernel(AdminParams a, uint32_t rid, uint64_t firs
   rg_entry_view v;
   v.term = w & TERM_MASK;
   v.type = (uint32_t)((w >> 61) & 1);
-  v.len = (w & PAY_BIT) ? word_len(w) : 0u;
+  v.len = (w & (PAY_BIT | TYPE_BIT)) ? word_len(w) : 0u;  // a ConfigChange reports its descriptor
   v.crc = (w & PAY_BIT) ? crc_of_cmd(inf.x, v.len, t.P, a.zi) : 0u;  // the ring keeps the slot CRC
   v.bank = (uint32_t)bank;
   out[i] = v;
@@ -122,6 +124,8 @@ __global__ void scatter_replica_kernel(AdminParams a, uint32_t rid, const rg_rep
     s32[S_RAND_TO * N] = v.rand_timeout; s32[S_RNG_CTR * N] = v.rng_ctr; s32[S_GRANTED * N] = v.granted;
     s32[S_RESPONDED * N] = v.responded; s32[S_ACTIVE * N] = v.active; s32[S_ERR * N] = v.err;
     s32[S_DROPS * N] = v.drops;
+    s32[S_MEMBERS * N] = v.members; s32[S_SNAP_MEMBERS * N] = v.snap_members; s32[S_CC_PENDING * N] = v.cc_pending;
+    s64[S_CC_HI * N] = v.last;  // any imported entry may be a ConfigChange
     uint64_t* rem = const_cast<uint64_t*>(t.rem_in);
     uint8_t* rst = const_cast<uint8_t*>(t.rst_in);
     for (uint32_t j = 0; j < t.R; ++j) {

@@ -147,6 +147,8 @@ __global__ void persist_state_kernel(PersistParams a) {
   r.snap_term = v[S_SNAP_TERM * n];
   r.first = persist_first(a, q);
   r.entry_off = a.eoff[q];
+  r.members = a.s32[(uint64_t)S_MEMBERS * n + q];
+  r.snap_members = a.s32[(uint64_t)S_SNAP_MEMBERS * n + q];
   reinterpret_cast<rg_persist_state*>(a.out_state)[a.soff[q]] = r;
 }
 
@@ -168,7 +170,7 @@ __global__ void __launch_bounds__(256) persist_entries_kernel(PersistParams a) {
       r.index = i;
       r.term = w & TERM_MASK;
       r.type = (uint32_t)((w >> 61) & 1);
-      r.len = (w & PAY_BIT) ? word_len(w) : 0u;
+      r.len = (w & (PAY_BIT | TYPE_BIT)) ? word_len(w) : 0u;  // a ConfigChange: its descriptor
       r.crc = (w & PAY_BIT) ? crc_of_cmd(inf.x, r.len, a.P, a.zi) : 0u;
       r.rid = j * a.R + s;
       reinterpret_cast<rg_persist_entry*>(a.out_ent)[base + (i - lo)] = r;

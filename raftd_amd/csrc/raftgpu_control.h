@@ -80,11 +80,16 @@ struct Ctl {
   const TickParams p;  // by value: pointer fields stay kernel-argument (global) pointers
   uint32_t q, g, s;    // g = local column (indexes every device array)
   uint64_t gg, rid;    // global group and global replica id gg·R + s (RNG keys, loss hash)
-  uint64_t gi, ri;     // the same as indices into this engine's tick-input arrays
+  uint32_t gi;         // the global group as an index into this engine's tick-input arrays (< 2^32)
   uint64_t term, vote, leader, committed, applied, last, marker, marker_term, snap_index, snap_term, cap_base;
   uint64_t processed;  // committed entries handed to the state machine (entryLog.processed)
   uint32_t role, etick, htick, rand_to, rng_ctr, granted, responded, active, err, drops;
-  uint64_t rm[R], rn[R], rs[R];  // remote match / next / snapshot index
+  uint32_t members, snap_members, cc_pending;  // membership
+  uint64_t cc_hi;                              // highest index a ConfigChange entry was written to
+  // remote match / next / snapshot index; at R = 8 the snapshot indices (touched only on the
+  // snapshot path) stay in this step's output rows instead of registers
+  static constexpr bool RS_MEM = R >= 8;
+  uint64_t rm[R], rn[R], rs[RS_MEM ? 1 : R];
   uint32_t rt[R];                // remote state
   uint64_t last_start, sent_hi, rw_lo, rw_hi, marker_start;
   uint64_t processed_start, restored_at;  // apply window: entries restored from a snapshot are not Update()d
@@ -107,23 +112,24 @@ struct Ctl {
     g = q - s * p.G;
     gg = pl_group(p.pl, s, g);
     rid = gg * R + s;
-    gi = pl_input_index(p.pl, gg);
-    ri = gi * R + s;
+    gi = (uint32_t)pl_input_index(p.pl, gg);
     const uint64_t n = p.nrep;
     const uint64_t* a = p.s64_in + q;
     term = a[S_TERM * n]; vote = a[S_VOTE * n]; leader = a[S_LEADER * n]; committed = a[S_COMMITTED * n];
     applied = a[S_APPLIED * n]; last = a[S_LAST * n]; marker = a[S_MARKER * n]; marker_term = a[S_MARKER_TERM * n];
     snap_index = a[S_SNAP_INDEX * n]; snap_term = a[S_SNAP_TERM * n]; cap_base = a[S_CAP_BASE * n];
-    processed = a[S_PROCESSED * n];
+    processed = a[S_PROCESSED * n]; cc_hi = a[S_CC_HI * n];
     const uint32_t* b = p.s32_in + q;
     role = b[S_ROLE * n]; etick = b[S_ETICK * n]; htick = b[S_HTICK * n]; rand_to = b[S_RAND_TO * n];
     rng_ctr = b[S_RNG_CTR * n]; granted = b[S_GRANTED * n]; responded = b[S_RESPONDED * n];
     active = b[S_ACTIVE * n]; err = b[S_ERR * n]; drops = b[S_DROPS * n];
+    members = b[S_MEMBERS * n]; snap_members = b[S_SNAP_MEMBERS * n]; cc_pending = b[S_CC_PENDING * n];
     sfor<0, R>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       rm[j] = p.rem_in[(0 * R + j) * n + q];
       rn[j] = p.rem_in[(1 * R + j) * n + q];
-      rs[j] = p.rem_in[(2 * R + j) * n + q];
+      if constexpr (RS_MEM) p.rem_out[(2 * R + j) * n + q] = p.rem_in[(2 * R + j) * n + q];
+      else rs[j] = p.rem_in[(2 * R + j) * n + q];
       rt[j] = p.rst_in[j * n + q];
     });
     last_start = last; sent_hi = 0; rw_lo = ~0ull; rw_hi = 0; marker_start = marker;
@@ -134,12 +140,24 @@ struct Ctl {
     oc = 0; em = 0; nj = 0;
   }
 
-  RG_FN uint32_t quorum() const { return R / 2 + 1; }
+  // entries per load batch (RG_CTL_BATCH); at R >= 7 the remote arrays leave room for half as many
+  static constexpr uint32_t CB = R >= 7 ? (RG_CTL_BATCH > 4 ? 4 : RG_CTL_BATCH) : RG_CTL_BATCH;
+  RG_FN uint64_t ri() const { return (uint64_t)gi * R + s; }  // the replica's tick-input index
+  RG_FN uint32_t quorum() const { return (uint32_t)__builtin_popcount(members) / 2 + 1; }  // voting members
+  RG_FN bool is_member(uint32_t i) const { return (members >> i) & 1u; }
   RG_FN uint32_t my_id() const { return s + 1; }
 
   // ---- remotes (compile-time R: selects, no local-memory arrays)
 #define RG_GET(arr, f) sel_get<R>(arr, f)
 #define RG_SET(arr, f, val) sel_set<R>(arr, f, val)
+  RG_FN uint64_t rs_get(uint32_t f) const {
+    if constexpr (RS_MEM) return p.rem_out[((uint64_t)(2 * R) + f) * p.nrep + q];
+    else return sel_get<R>(rs, f);
+  }
+  RG_FN void rs_set(uint32_t f, uint64_t v) {
+    if constexpr (RS_MEM) p.rem_out[((uint64_t)(2 * R) + f) * p.nrep + q] = v;
+    else sel_set<R>(rs, f, v);
+  }
 
   // ---- log (entryLog)
   RG_FN uint64_t* tr_at(uint64_t i) const {
@@ -164,7 +182,7 @@ struct Ctl {
     return (uint32_t)(packed >> (8 * d)) & 0xFF;
   }
   RG_FN bool lost(uint32_t dst, uint32_t n) const {
-    if (p.isolate && (p.isolate[ri] || p.isolate[gi * R + dst])) return true;
+    if (p.isolate && (p.isolate[ri()] || p.isolate[(uint64_t)gi * R + dst])) return true;
     if (p.drop_ppm) {
       uint64_t h = mix64(p.seed ^ mix64((p.tick << 40) ^ ((uint64_t)rid << 8) ^ dst) ^ (uint64_t)(n + 1));
       if (h % 1000000ull < p.drop_ppm) return true;
@@ -223,10 +241,11 @@ struct Ctl {
       constexpr int j = decltype(jc)::value;
       rm[j] = (uint32_t)j == s ? last : 0;
       rn[j] = last + 1;
-      rs[j] = 0;
+      rs_set(j, 0);
       rt[j] = RETRY;
     });
     active = 0;
+    cc_pending = 0;  // clearPendingConfigChange
     if (p.rdst) p.rdst[(uint64_t)RI_CTX * p.nrep + q] = 0;  // readIndex.reset
   }
   RG_FN void become_follower(uint64_t t, uint64_t l) {
@@ -255,13 +274,17 @@ struct Ctl {
   }
 
   // raft.tryCommit: q = max{m_i : #{j : m_j >= m_i} >= quorum} = sorted_asc[R - quorum]
-  RG_FN bool try_commit() {
+  RG_FN bool try_commit() {  // over the voting members only
     uint64_t qv = 0;
+    const uint32_t qn = quorum();
     sfor<0, R>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
       uint32_t cnt = 0;
-      sfor<0, R>([&](auto jc) { cnt += rm[decltype(jc)::value] >= rm[i] ? 1u : 0u; });
-      if (cnt >= quorum()) qv = umax64(qv, rm[i]);
+      sfor<0, R>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        cnt += ((members >> j) & 1u) && rm[j] >= rm[i] ? 1u : 0u;
+      });
+      if (((members >> i) & 1u) && cnt >= qn) qv = umax64(qv, rm[i]);
     });
     if (qv > committed && term_at(qv) == term) {
       committed = qv;
@@ -313,13 +336,13 @@ struct Ctl {
         }
       } else {
         uint64_t bit = 1ull << e0;
-        for (uint32_t e = e0; e < n; e += RG_CTL_BATCH) {
-          uint64_t wv[RG_CTL_BATCH];
+        for (uint32_t e = e0; e < n; e += CB) {
+          uint64_t wv[CB];
 #pragma unroll
-          for (uint32_t k = 0; k < RG_CTL_BATCH; ++k)
+          for (uint32_t k = 0; k < CB; ++k)
             wv[k] = word | (e + k >= n ? 0ull : mt ? mt[(uint64_t)(e + k) * p.G] : len_bits(li[e + k].y));
 #pragma unroll
-          for (uint32_t k = 0; k < RG_CTL_BATCH; ++k) {
+          for (uint32_t k = 0; k < CB; ++k) {
             if (e + k >= n) break;
             const uint64_t w = wv[k];
             sm |= (w & BANK_BIT) ? bit : 0ull;
@@ -337,21 +360,21 @@ struct Ctl {
       }
     } else
 #endif
-    // RG_CTL_BATCH entries at a time: their loads (sender terms, current ring words of protected
+    // CB entries at a time: their loads (sender terms, current ring words of protected
     // indices) are issued before any of their stores, so a lane waits one memory latency per
     // batch instead of one per entry (the compiler cannot prove the ring and the inbox disjoint).
     // The entries of one call occupy distinct ring slots (n <= L by the capacity rule).
-    for (uint32_t e = e0; e < n; e += RG_CTL_BATCH) {
-      uint64_t wv[RG_CTL_BATCH], ov[RG_CTL_BATCH];
+    for (uint32_t e = e0; e < n; e += CB) {
+      uint64_t wv[CB], ov[CB];
 #pragma unroll
-      for (uint32_t k = 0; k < RG_CTL_BATCH; ++k) {
+      for (uint32_t k = 0; k < CB; ++k) {
         const uint64_t idx = base + e + k;
         const bool in = e + k < n;
         wv[k] = word | (!in ? 0ull : mt ? mt[(uint64_t)(e + k) * p.G] : li ? len_bits(li[e + k].y) : 0ull);
         ov[k] = in && idx <= hi_prot ? *tr_at(idx) : 0;
       }
 #pragma unroll
-      for (uint32_t k = 0; k < RG_CTL_BATCH; ++k) {
+      for (uint32_t k = 0; k < CB; ++k) {
         if (e + k >= n) break;
         const uint32_t ek = e + k;
         const uint64_t idx = base + ek, w = wv[k];
@@ -379,6 +402,7 @@ struct Ctl {
         rw_hi = umax64(rw_hi, hi_w);
       }
     }
+    if (tm) cc_hi = umax64(cc_hi, base + n - 1);  // a ConfigChange entry may be among them
     if (kind == SRC_WIRE || kind == SRC_WIRE_PROP) sm = aux;  // source bank bits are meaningless off-rank
     if (nj < p.J) {
       const uint64_t n64 = p.nrep, JN = (uint64_t)p.J * n64;
@@ -401,9 +425,16 @@ struct Ctl {
   // another rank — their inline words rmt[e·G] (length bits) and bytes in the receive buffer at
   // record offset wofs.
   RG_FN bool append_local(uint32_t n, int slab_id, uint32_t rslot = 0, const uint2* li = nullptr,
-                          const uint64_t* rmt = nullptr, uint64_t wofs = 0) {
+                          const uint64_t* rmt = nullptr, uint64_t wofs = 0, uint32_t cc = 0) {
     if (last + n > cap_base + p.L) return false;
     const uint64_t base = last + 1;
+    if (cc) {  // one ConfigChange entry: no Cmd, the descriptor in its length field
+      write_entries(base, 0, 1, SRC_NONE, 0, nullptr, term | TYPE_BIT | cc_bits(cc));
+      last += 1;
+      remote_try_update(s, last);
+      if (__builtin_popcount(members) == 1) try_commit();  // isSingleNodeQuorum
+      return true;
+    }
 #ifdef RG_CTL_FASTREP
     const bool plain = base > umax64(last_start, sent_hi);  // no protected index: every bank bit 0
     const uint64_t pt = plain ? term_at(last) : 0;
@@ -422,13 +453,16 @@ struct Ctl {
 #endif
     last += n;
     remote_try_update(s, last);
-    if (R == 1) try_commit();
+    if (__builtin_popcount(members) == 1) try_commit();  // isSingleNodeQuorum
     return true;
   }
   RG_FN void become_leader() {
     role = LEADER;
     reset(term);
     leader = my_id();
+    // preLeaderPromotionHandleConfigChange: a ConfigChange entry in (committed, last] is in flight
+    for (uint64_t i = committed + 1; i <= umin64(last, cc_hi); ++i)
+      if (*tr_at(i) & TYPE_BIT) cc_pending = 1;
     if (!append_local(1, -1)) err |= ERR_RING;  // the empty no-op
   }
 
@@ -443,9 +477,9 @@ struct Ctl {
         err |= ERR_EMPTY_SNAP;
         return;
       }
-      RG_SET(rs, to, snap_index);
+      rs_set(to, snap_index);
       RG_SET(rt, to, (uint32_t)SNAPSHOT);
-      send(M_INSTALL_SNAPSHOT, to + 1, 0, 0, 0, snap_term, snap_index, 0, 0, 0, 0, 0);
+      send(M_INSTALL_SNAPSHOT, to + 1, 0, 0, 0, snap_term, snap_index, 0, 0, snap_members, 0, 0);
       return;
     }
     const uint32_t n = next <= last ? (uint32_t)umin64(p.E, last - next + 1) : 0;
@@ -468,12 +502,12 @@ struct Ctl {
         for (uint32_t e = 0; e < n; ++e) mt[(uint64_t)e * p.G] = la_word;
       } else
 #endif
-      for (uint32_t e = 0; e < n; e += RG_CTL_BATCH) {  // term|type|pay|bank; batched as in write_entries
-        uint64_t v[RG_CTL_BATCH];
+      for (uint32_t e = 0; e < n; e += CB) {  // term|type|pay|bank; batched as in write_entries
+        uint64_t v[CB];
 #pragma unroll
-        for (uint32_t k2 = 0; k2 < RG_CTL_BATCH; ++k2) v[k2] = e + k2 < n ? *tr_at(next + e + k2) : 0;
+        for (uint32_t k2 = 0; k2 < CB; ++k2) v[k2] = e + k2 < n ? *tr_at(next + e + k2) : 0;
 #pragma unroll
-        for (uint32_t k2 = 0; k2 < RG_CTL_BATCH; ++k2)
+        for (uint32_t k2 = 0; k2 < CB; ++k2)
           if (e + k2 < n) mt[(uint64_t)(e + k2) * p.G] = v[k2];
       }
       sent_hi = umax64(sent_hi, next + n - 1);
@@ -481,11 +515,11 @@ struct Ctl {
   }
   RG_FN void broadcast_replicate() {
     for (uint32_t i = 0; i < R; ++i)
-      if (i != s) send_replicate(i);
+      if (i != s && is_member(i)) send_replicate(i);
   }
   RG_FN void broadcast_heartbeat() {
     for (uint32_t i = 0; i < R; ++i)
-      if (i != s) send(M_HEARTBEAT, i + 1, 0, 0, 0, 0, 0, umin64(RG_GET(rm, i), committed), 0, 0, 0, 0);
+      if (i != s && is_member(i)) send(M_HEARTBEAT, i + 1, 0, 0, 0, 0, 0, umin64(RG_GET(rm, i), committed), 0, 0, 0, 0);
   }
 
   // ---- follower side (A.9)
@@ -534,7 +568,7 @@ struct Ctl {
     }
   }
 
-  RG_FN void handle_install_snapshot(uint64_t si, uint64_t stt, uint32_t from) {
+  RG_FN void handle_install_snapshot(uint64_t si, uint64_t stt, uint32_t from, uint32_t smembers) {
     uint64_t li;
     if (si <= committed) {
       li = committed;
@@ -548,6 +582,7 @@ struct Ctl {
       la_n = 0;
 #endif
       marker_term = snap_term = stt;
+      members = snap_members = smembers;  // the snapshot's membership
       li = last;
       restored_at = si;
     }
@@ -559,16 +594,17 @@ struct Ctl {
     become_candidate();
     responded |= 1u << s;
     granted |= 1u << s;
-    if (R == 1) {
+    if ((uint32_t)__builtin_popcount(granted & members) == quorum()) {  // single-node quorum
       become_leader();
       return;
     }
     const uint64_t lt = term_at(last);
     for (uint32_t i = 0; i < R; ++i)
-      if (i != s) send(M_REQUEST_VOTE, i + 1, term, 0, 0, lt, last, 0, 0, 0, 0, 0);
+      if (i != s && is_member(i)) send(M_REQUEST_VOTE, i + 1, term, 0, 0, lt, last, 0, 0, 0, 0, 0);
   }
   RG_FN void handle_node_election() {
     if (role == LEADER) return;
+    if (!is_member(s)) return;        // selfRemoved: no elections
     if (committed > applied) return;  // hasConfigChangeToApply
     campaign();
   }
@@ -590,7 +626,7 @@ struct Ctl {
       responded |= bit;
       if (!reject) granted |= bit;
     }
-    const uint32_t gr = __builtin_popcount(granted), tot = __builtin_popcount(responded);
+    const uint32_t gr = __builtin_popcount(granted & members), tot = __builtin_popcount(responded & members);
     if (gr == quorum()) {
       become_leader();
       broadcast_replicate();
@@ -602,20 +638,21 @@ struct Ctl {
   // ---- leader responses (A.10, A.11)
   RG_FN void leader_replicate_resp(uint32_t reject, uint64_t li, uint64_t hint, uint32_t from) {
     const uint32_t f = from - 1;
+    if (!is_member(f)) return;  // no remote for it
     active |= 1u << f;
     if (!reject) {
       const uint32_t st0 = RG_GET(rt, f);
       const bool paused = st0 == WAIT || st0 == SNAPSHOT;
       if (remote_try_update(f, li)) {
         const uint32_t st = RG_GET(rt, f);
-        const uint64_t m = RG_GET(rm, f), sn = RG_GET(rs, f);
+        const uint64_t m = RG_GET(rm, f), sn = rs_get(f);
         if (st == RETRY) {  // respondedTo → becomeReplicate
           RG_SET(rn, f, m + 1);
-          RG_SET(rs, f, 0ull);
+          rs_set(f, 0ull);
           RG_SET(rt, f, (uint32_t)REPLICATE);
         } else if (st == SNAPSHOT && m >= sn) {  // becomeRetry from Snapshot
           RG_SET(rn, f, umax64(m + 1, sn + 1));
-          RG_SET(rs, f, 0ull);
+          rs_set(f, 0ull);
           RG_SET(rt, f, (uint32_t)RETRY);
         }
         if (try_commit()) broadcast_replicate();
@@ -641,7 +678,7 @@ struct Ctl {
       if (ok) {
         if (RG_GET(rt, f) == REPLICATE) {  // enterRetryState → becomeRetry
           RG_SET(rn, f, m + 1);
-          RG_SET(rs, f, 0ull);
+          rs_set(f, 0ull);
           RG_SET(rt, f, (uint32_t)RETRY);
         }
         send_replicate(f);
@@ -650,6 +687,7 @@ struct Ctl {
   }
   RG_FN void leader_heartbeat_resp(uint32_t from, uint64_t hint) {
     const uint32_t f = from - 1;
+    if (!is_member(f)) return;  // no remote for it
     active |= 1u << f;
     if (RG_GET(rt, f) == WAIT) RG_SET(rt, f, (uint32_t)RETRY);
     if (RG_GET(rm, f) < last) send_replicate(f);
@@ -658,7 +696,7 @@ struct Ctl {
       const uint64_t n = p.nrep;
       if (rd[RI_CTX * n] == hint) {
         const uint64_t a = rd[RI_ACKS * n] | (1ull << f);
-        if ((uint32_t)__builtin_popcount((uint32_t)a) >= quorum()) {
+        if ((uint32_t)__builtin_popcount((uint32_t)a & members) >= quorum()) {
           rd[RI_CTX * n] = 0;
           read_confirmed(hint, rd[RI_INDEX * n], (uint32_t)(a >> 32));
         } else {
@@ -684,7 +722,7 @@ struct Ctl {
     if (role == LEADER) {
       uint64_t* rd = p.rdst + q;
       const uint64_t n = p.nrep;
-      if (R == 1) {
+      if (quorum() == 1) {  // isSingleNodeQuorum
         read_confirmed(ctx, committed, f);
       } else if (term_at(committed) != term || rd[RI_CTX * n] != 0) {
         drops++;  // nothing committed in this term yet, or a read already pending
@@ -693,7 +731,7 @@ struct Ctl {
         rd[RI_INDEX * n] = committed;
         rd[RI_ACKS * n] = (1ull << s) | ((uint64_t)f << 32);
         for (uint32_t i = 0; i < R; ++i)  // broadcastHeartbeatMessageWithHint
-          if (i != s) send(M_HEARTBEAT, i + 1, 0, 0, 0, 0, 0, umin64(RG_GET(rm, i), committed), ctx, 0, 0, 0);
+          if (i != s && is_member(i)) send(M_HEARTBEAT, i + 1, 0, 0, 0, 0, 0, umin64(RG_GET(rm, i), committed), ctx, 0, 0, 0);
       }
     } else if (role == FOLLOWER && leader != 0 && f == s) {
       send(M_READ_INDEX, (uint32_t)leader, 0, 0, 0, 0, 0, 0, ctx, 0, 0, 0);
@@ -702,27 +740,32 @@ struct Ctl {
     }
   }
   RG_FN void check_quorum() {
-    const uint32_t c = 1 + __builtin_popcount(active & ~(1u << s));
+    const uint32_t c = __builtin_popcount((active | (1u << s)) & members);  // leaderHasQuorum
     active = 0;
     if (c < quorum()) become_follower(term, 0);
   }
 
   // ---- proposals: nent Cmds (hm = those with a non-empty Cmd, the forwarded header's hint); their
   // bytes and lengths as append_local takes them
+  // cc != 0: a membership change (one ConfigChange entry)
   RG_FN void handle_propose(uint32_t nent, uint32_t slab_id, uint32_t hop, uint64_t hm, uint32_t rslot,
-                            const uint2* li, const uint64_t* rmt, uint64_t wofs) {
+                            const uint2* li, const uint64_t* rmt, uint64_t wofs, uint32_t cc = 0) {
     if (role == LEADER) {
       RG_T0(t0);
-      if (!append_local(nent, (int)slab_id, rslot, li, rmt, wofs)) {
+      const bool dropped = cc && cc_pending;  // one change at a time: an empty entry instead
+      if (!(cc ? (dropped ? append_local(1, -1) : append_local(1, -1, 0, nullptr, nullptr, 0, cc))
+               : append_local(nent, (int)slab_id, rslot, li, rmt, wofs))) {
         drops++;
         return;
       }
+      if (dropped) drops++;        // reportDroppedConfigChange
+      else if (cc) cc_pending = 1;  // setPendingConfigChange
       RG_ACC(0, t0);
       RG_T0(t1);
       broadcast_replicate();
       RG_ACC(1, t1);
     } else if (role == FOLLOWER && leader != 0 && hop == 0) {
-      send(M_PROPOSE, (uint32_t)leader, 0, 0, nent, 0, 0, 0, hm, 0, slab_id, hop + 1);
+      send(M_PROPOSE, (uint32_t)leader, 0, 0, nent, 0, 0, 0, hm, cc, slab_id, hop + 1);
     } else {
       drops++;
     }
@@ -743,10 +786,31 @@ struct Ctl {
       }
     } else {
       etick++;
-      if (etick >= rand_to) {
+      if (is_member(s) && etick >= rand_to) {  // selfRemoved: no elections
         etick = 0;
         handle_node_election();
       }
+    }
+  }
+
+  // ---- membership: raft.addNode / removeNode through the rsm's ApplyConfigChange
+  RG_FN void apply_config_change(uint32_t cc) {
+    cc_pending = 0;  // clearPendingConfigChange
+    const uint32_t op = cc >> 4, slot = (cc & 0xFu) - 1u;
+    if (slot >= (uint32_t)R) return;
+    const uint32_t bit = 1u << slot;
+    if (op == CC_ADD) {
+      if (members & bit) return;
+      members |= bit;  // setRemote(id, 0, lastIndex + 1)
+      RG_SET(rm, slot, 0ull);
+      RG_SET(rn, slot, last + 1);
+      rs_set(slot, 0ull);
+      RG_SET(rt, slot, (uint32_t)RETRY);
+    } else if (op == CC_REMOVE) {
+      members &= ~bit;  // deleteRemote
+      active &= ~bit;
+      if (slot == s && role == LEADER) become_follower(term, 0);
+      if (role == LEADER && members && try_commit()) broadcast_replicate();
     }
   }
 
@@ -809,12 +873,12 @@ struct Ctl {
         }
         if (remote) {
           const uint64_t* rm = p.rmt + ((((uint64_t)src * R + s) * p.K + k) * p.E) * p.G + g;
-          handle_propose(nent, 0, 1, hw(5), 0, nullptr, rm, w7);
+          handle_propose(nent, 0, 1, hw(5), 0, nullptr, rm, w7, (uint32_t)hw(6));
         } else {
           const uint64_t row = p.wire ? (uint64_t)src * p.G + g : g;  // the forwarder's slab row (same rank)
           const uint64_t rows = p.wire ? p.nrep : p.G;
           const uint2* li = p.slab_info + ((uint64_t)(uint32_t)w7 * rows + row) * p.E;
-          handle_propose(nent, (uint32_t)w7, (uint32_t)(w7 >> 32), hw(5), src, li, nullptr, 0);
+          handle_propose(nent, (uint32_t)w7, (uint32_t)(w7 >> 32), hw(5), src, li, nullptr, 0, (uint32_t)hw(6));
         }
         break;
       }
@@ -835,7 +899,7 @@ struct Ctl {
           commit_to(hw(4));
           send_simple(M_HEARTBEAT_RESP, from, 0, 0, hw(5), hw(6));
         } else {
-          handle_install_snapshot(hw(3), hw(2), from);
+          handle_install_snapshot(hw(3), hw(2), from, (uint32_t)hw(6));
         }
         break;
       case M_REPLICATE_RESP:
@@ -883,7 +947,7 @@ struct Ctl {
       for (uint32_t k = 0; k < cnt; ++k) handle(src, k, remote);
     }
     RG_STAMP(1);
-    if (p.campaign && p.campaign[ri]) handle_node_election();
+    if (p.campaign && p.campaign[ri()]) handle_node_election();
     if (!(p.flags & 1u)) tick();
     RG_STAMP(2);
     if (p.prop_target && p.prop_target[gi] == s) {
@@ -899,18 +963,28 @@ struct Ctl {
         handle_propose(n, sl, 0, hm, s, li, nullptr, 0);
       }
     }
+    if (p.cc_in) {  // 4a: membership change input (rg_config_change)
+      const uint32_t v = p.cc_in[gi];
+      if (v && (v & 0xFFu) == s) handle_propose(1, (uint32_t)(p.tick % p.nslab), 0, 0, s, nullptr, nullptr, 0, v >> 8);
+    }
     if (p.read_ctx) {  // 4b: ReadIndex input (rg_read_index)
-      const uint64_t ctx = p.read_ctx[ri];
+      const uint64_t ctx = p.read_ctx[ri()];
       if (ctx) handle_read_index(my_id(), ctx);
     }
     RG_STAMP(3);
     // GetUpdate.CommittedEntries = (processed, committed], then commitUpdate; applied follows unless
     // the state machine reports it (rg_notify_applied); snapshot + compaction on applied
+    // the rsm applies the ConfigChange entries it is handed (none past cc_hi)
+    for (uint64_t i = umax64(processed_start, restored_at) + 1; i <= umin64(committed, cc_hi); ++i) {
+      const uint64_t w = *tr_at(i);
+      if ((w & TYPE_BIT) && word_len(w)) apply_config_change(word_len(w));
+    }
     processed = committed;
     if (!p.AF) applied = processed;
     if (p.SE && applied >= snap_index && applied - snap_index >= p.SE) {
       snap_index = applied;
       snap_term = term_at(applied);
+      snap_members = members;
       took = true;
       const uint64_t c = snap_index > p.CO ? snap_index - p.CO : 0;
       if (c > marker) {
@@ -934,16 +1008,17 @@ struct Ctl {
     a[S_TERM * n] = term; a[S_VOTE * n] = vote; a[S_LEADER * n] = leader; a[S_COMMITTED * n] = committed;
     a[S_APPLIED * n] = applied; a[S_LAST * n] = last; a[S_MARKER * n] = marker; a[S_MARKER_TERM * n] = marker_term;
     a[S_SNAP_INDEX * n] = snap_index; a[S_SNAP_TERM * n] = snap_term; a[S_CAP_BASE * n] = cap_base;
-    a[S_PROCESSED * n] = processed;
+    a[S_PROCESSED * n] = processed; a[S_CC_HI * n] = cc_hi;
     uint32_t* b = p.s32_out + q;
     b[S_ROLE * n] = role; b[S_ETICK * n] = etick; b[S_HTICK * n] = htick; b[S_RAND_TO * n] = rand_to;
     b[S_RNG_CTR * n] = rng_ctr; b[S_GRANTED * n] = granted; b[S_RESPONDED * n] = responded;
     b[S_ACTIVE * n] = active; b[S_ERR * n] = err; b[S_DROPS * n] = drops;
+    b[S_MEMBERS * n] = members; b[S_SNAP_MEMBERS * n] = snap_members; b[S_CC_PENDING * n] = cc_pending;
     sfor<0, R>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       p.rem_out[(0 * R + j) * n + q] = rm[j];
       p.rem_out[(1 * R + j) * n + q] = rn[j];
-      p.rem_out[(2 * R + j) * n + q] = rs[j];
+      if constexpr (!RS_MEM) p.rem_out[(2 * R + j) * n + q] = rs[j];
       p.rst_out[j * n + q] = (uint8_t)rt[j];
       p.cnt_out[((uint64_t)s * R + j) * p.G + g] = get8(oc, j);
     });

@@ -95,6 +95,12 @@ struct rg_engine {
   std::vector<uint64_t> rd_touched;
   bool rd_staged = false, rd_reset_pending = false;
   hipEvent_t rd_ev = nullptr;
+  // rg_config_change staging: [global group] slot | descriptor << 8 (pinned), uploaded by the tick
+  uint16_t* h_cc = nullptr;
+  uint16_t* d_cc = nullptr;
+  std::vector<uint64_t> cc_touched;
+  bool cc_staged = false, cc_reset_pending = false;
+  hipEvent_t cc_ev = nullptr;
   uint32_t* crc_tab = nullptr;
   uint32_t crc_const = 0;
   uint8_t* d_prop_target = nullptr;
@@ -249,6 +255,7 @@ static TickParams params(rg_engine* e) {
   p.CO = c.compaction_overhead; p.drop_ppm = c.drop_ppm;
   p.wire = e->wire ? 1u : 0u;
   p.AF = c.apply_feedback;
+  p.IM = c.initial_members;
   p.seed = c.seed;
   p.tick = e->t;
   p.pl = e->pl;
@@ -335,6 +342,7 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if (N > MAX_RANKS || c.rank >= N) return fail(RG_EINVAL, "ranks in 1..16, rank < ranks");
   if (c.crc32c > 1) return fail(RG_EINVAL, "crc32c must be 0 (IEEE) or 1 (Castagnoli)");
   if (c.apply_feedback > 1) return fail(RG_EINVAL, "apply_feedback must be 0 or 1");
+  if (c.initial_members >> c.replicas) return fail(RG_EINVAL, "initial_members names a slot >= replicas");
   if ((N > 1 || c.wire_all) && c.groups >= (1u << 24)) return fail(RG_EINVAL, "groups < 2^24 with ranks > 1");
   int ndev = 0;
   HIPCHK(hipGetDeviceCount(&ndev));
@@ -377,6 +385,9 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if (rc == RG_OK) rc = dalloc(e, &e->d_read_ctx, n * N * 8);
   if (rc == RG_OK && hipHostMalloc((void**)&e->h_rd, n * N * 8, 0) != hipSuccess) rc = fail(RG_ENOMEM, "hipHostMalloc");
   if (rc == RG_OK) memset(e->h_rd, 0, n * N * 8);
+  if (rc == RG_OK) rc = dalloc(e, &e->d_cc, G * N * 2);
+  if (rc == RG_OK && hipHostMalloc((void**)&e->h_cc, G * N * 2, 0) != hipSuccess) rc = fail(RG_ENOMEM, "hipHostMalloc");
+  if (rc == RG_OK) memset(e->h_cc, 0, G * N * 2);
   if (rc == RG_OK && (hipHostMalloc((void**)&e->h_pt, G * N, 0) != hipSuccess ||
                       hipHostMalloc((void**)&e->h_pc, G * N * 4, 0) != hipSuccess ||
                       hipHostMalloc((void**)&e->h_hm, G * N * 8, 0) != hipSuccess))
@@ -473,6 +484,7 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
     }
   }
   if (hipEventCreateWithFlags(&e->rd_ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&e->cc_ev, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&e->stg_ev, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&e->prop_ev, hipEventDisableTiming) != hipSuccess ||
       hipStreamCreateWithFlags(&e->copy, hipStreamNonBlocking) != hipSuccess) {
@@ -533,6 +545,8 @@ void rg_destroy(rg_engine* e) {
   }
   if (e->stg_ev) (void)hipEventDestroy(e->stg_ev);
   if (e->rd_ev) (void)hipEventDestroy(e->rd_ev);
+  if (e->cc_ev) (void)hipEventDestroy(e->cc_ev);
+  if (e->h_cc) (void)hipHostFree(e->h_cc);
   if (e->h_rd) (void)hipHostFree(e->h_rd);
   if (e->prop_ev) (void)hipEventDestroy(e->prop_ev);
   for (void* p : e->allocs) (void)hipFree(p);
@@ -634,6 +648,10 @@ int rg_bootstrap(rg_engine* e) {
   if (e->rd_reset_pending) HIPCHK(hipEventSynchronize(e->rd_ev));
   for (uint64_t i : e->rd_touched) e->h_rd[i] = 0;
   e->rd_touched.clear();
+  if (e->cc_reset_pending) HIPCHK(hipEventSynchronize(e->cc_ev));
+  for (uint64_t i : e->cc_touched) e->h_cc[i] = 0;
+  e->cc_touched.clear();
+  e->cc_staged = e->cc_reset_pending = false;
   e->rd_staged = e->rd_reset_pending = false;
   HIPCHK(hipMemsetAsync(e->rdst, 0, (uint64_t)RD_ROWS * e->nrep * 8, e->stream));
   HIPCHK(hipMemsetAsync(e->crc_err, 0, (uint64_t)e->nrep * 4, e->stream));
@@ -882,6 +900,13 @@ static int tick_impl(rg_engine* e, const rg_tick_input* in, bool device_ptrs) {
     e->rd_staged = false;
     e->rd_reset_pending = true;
   }
+  if (e->cc_staged) {  // rg_config_change's membership changes
+    HIPCHK(hipMemcpyAsync(e->d_cc, e->h_cc, (uint64_t)e->c.groups * e->pl.N * 2, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipEventRecord(e->cc_ev, e->stream));
+    p.cc_in = e->d_cc;
+    e->cc_staged = false;
+    e->cc_reset_pending = true;
+  }
   // control(t) on the engine stream once bulk(t-2) released jobs[t&1]; bulk(t) on the bulk
   // stream after control(t). control(t+1) then overlaps bulk(t): they touch disjoint data.
   const int a = (int)(e->t & 1);
@@ -985,9 +1010,15 @@ int rg_import_replica(rg_engine* e, uint32_t rid, const rg_replica_view* v, cons
   for (uint32_t k = 0; k < nent; ++k) {
     const uint32_t type = types ? (types[k] & 0xFFu) : RG_ENTRY_APPLICATION;
     const uint32_t len = lens ? lens[k] : (uint32_t)P;
+    if (type != RG_ENTRY_APPLICATION) {  // a ConfigChange keeps its descriptor, no Cmd
+      const uint32_t cc = lens ? lens[k] : 0u;
+      if (cc > 0x1FFFu) return fail(RG_EINVAL, "rg_import_replica: ConfigChange descriptor out of range");
+      words[k] = (terms[k] & TERM_MASK) | TYPE_BIT | cc_bits(cc);
+      continue;
+    }
     if (len > P) return fail(RG_EINVAL, "rg_import_replica: Cmd longer than payload_bytes");
-    const bool hp = payloads && P && len && type == RG_ENTRY_APPLICATION && !(types && (types[k] & RG_ENTRY_EMPTY));
-    words[k] = (terms[k] & TERM_MASK) | (type ? TYPE_BIT : 0) | (hp ? len_bits(len) : 0);
+    const bool hp = payloads && P && len && !(types && (types[k] & RG_ENTRY_EMPTY));
+    words[k] = (terms[k] & TERM_MASK) | (hp ? len_bits(len) : 0);
     if (hp) {
       memcpy(rows.data() + (uint64_t)k * P, payloads + (uint64_t)k * P, len);
       crcs[k] = host_crc(e, rows.data() + (uint64_t)k * P, P);  // the slot CRC
@@ -1092,7 +1123,7 @@ int rg_persist_collect(rg_engine* e, int full, rg_persist_state* states, uint64_
   PersistParams a{};
   a.G = t.G; a.R = t.R; a.nrep = t.nrep; a.L = t.L; a.P = t.P; a.pl = e->pl;
   a.full = (full || e->t == 0) ? 1u : 0u;  // before the first tick there is no previous state
-  a.s64 = t.s64_in; a.s64_prev = t.s64_out; a.persist_lo = e->persist_lo;
+  a.s64 = t.s64_in; a.s64_prev = t.s64_out; a.s32 = t.s32_in; a.persist_lo = e->persist_lo;
   a.tr = e->tr; a.info = e->info; a.pay = e->pay; a.zi = e->crc_tab + CRC_ZI_OFF;
   a.scnt = e->pscnt; a.ecnt = e->pecnt; a.soff = e->psoff; a.eoff = e->peoff; a.bsum = e->absum;
   LAUNCH(launch_persist_count(a, (uint64_t*)e->d_sum, e->stream), e->stream, "persist count");
@@ -1262,6 +1293,28 @@ extern "C" int rg_debug_kernarg_placement(int32_t device, uint64_t* addr, int32_
   if (hipPointerGetAttributes(&at, (void*)(uintptr_t)h[0]) == hipSuccess)
     *is_device = at.type == hipMemoryTypeDevice ? 1 : at.type == hipMemoryTypeHost ? 0 : -1;
   (void)hipGetLastError();
+  return RG_OK;
+}
+
+int rg_config_change(rg_engine* e, uint64_t group, uint32_t slot, uint32_t op, uint32_t target) {
+  if (!e) return fail(RG_EINVAL, "rg_config_change args");
+  const uint32_t N = e->pl.N, R = e->c.replicas;
+  const uint64_t g0 = (uint64_t)N * e->pl.col_base, gn = (uint64_t)N * e->c.groups;
+  if (group < g0 || group >= g0 + gn || slot >= R || target >= R || (op != RG_CC_ADD && op != RG_CC_REMOVE))
+    return fail(RG_EINVAL, "rg_config_change: bad shard, slot, target or op");
+  if (pl_rank_of(e->pl, group, slot) != e->pl.rank)
+    return fail(RG_EINVAL, "rg_config_change: replica hosted by another rank");
+  if (e->cc_reset_pending) {  // the last upload has completed: clear what it carried
+    HIPCHK(hipEventSynchronize(e->cc_ev));
+    for (uint64_t i : e->cc_touched) e->h_cc[i] = 0;
+    e->cc_touched.clear();
+    e->cc_reset_pending = false;
+  }
+  const uint64_t gi = group - g0;
+  if (e->h_cc[gi]) return fail(RG_EFULL, "rg_config_change: a change is already staged for this shard");
+  e->h_cc[gi] = (uint16_t)(slot | ((op << 4 | (target + 1u)) << 8));
+  e->cc_touched.push_back(gi);
+  e->cc_staged = true;
   return RG_OK;
 }
 

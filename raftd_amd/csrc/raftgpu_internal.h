@@ -24,6 +24,10 @@ constexpr uint32_t LEN_SHIFT = 48;
 constexpr uint64_t TERM_MASK = (1ull << LEN_SHIFT) - 1;
 RG_HD_INLINE uint32_t word_len(uint64_t w) { return (uint32_t)(w >> LEN_SHIFT) & 0x1FFFu; }
 RG_HD_INLINE uint64_t len_bits(uint32_t len) { return ((uint64_t)len << LEN_SHIFT) | (len ? PAY_BIT : 0ull); }
+// A ConfigChange entry (TYPE_BIT, no payload) keeps its descriptor op << 4 | (slot + 1) in the
+// length field; 0 = the bootstrap entries
+enum : uint32_t { CC_ADD = 1, CC_REMOVE = 2 };
+RG_HD_INLINE uint64_t cc_bits(uint32_t cc) { return ((uint64_t)cc << LEN_SHIFT); }
 
 enum : uint32_t {
   M_LOCAL_TICK = 0, M_ELECTION = 1, M_LEADER_HEARTBEAT = 2, M_NOOP = 4, M_PROPOSE = 7,
@@ -50,10 +54,14 @@ enum : uint32_t { ERR_CONFLICT = 1, ERR_BEYOND = 2, ERR_RING = 4, ERR_CRC = 8, E
 // state field rows ([row][nrep])
 enum : uint32_t {
   S_TERM, S_VOTE, S_LEADER, S_COMMITTED, S_APPLIED, S_LAST, S_MARKER, S_MARKER_TERM, S_SNAP_INDEX,
-  S_SNAP_TERM, S_CAP_BASE, S_PROCESSED, S64_ROWS
+  S_SNAP_TERM, S_CAP_BASE, S_PROCESSED,
+  S_CC_HI,  // highest index a ConfigChange entry was written to (the apply scan stops there)
+  S64_ROWS
 };
 enum : uint32_t {
-  S_ROLE, S_ETICK, S_HTICK, S_RAND_TO, S_RNG_CTR, S_GRANTED, S_RESPONDED, S_ACTIVE, S_ERR, S_DROPS, S32_ROWS
+  S_ROLE, S_ETICK, S_HTICK, S_RAND_TO, S_RNG_CTR, S_GRANTED, S_RESPONDED, S_ACTIVE, S_ERR, S_DROPS,
+  S_MEMBERS, S_SNAP_MEMBERS, S_CC_PENDING,  // membership
+  S32_ROWS
 };
 // job rows
 enum : uint32_t { J_FIRST, J_DMASK, J_SMASK, J_HMASK, J_TMASK, J64_ROWS };
@@ -162,6 +170,8 @@ struct TickParams {
   const uint8_t* campaign;
   const uint8_t* isolate;
   const uint64_t* read_ctx;    // [global rid] ReadIndex request contexts of this tick (NULL: none)
+  const uint16_t* cc_in;       // [global group] membership change of this tick: slot | descriptor << 8 (0 none)
+  uint32_t IM;                 // bootstrap membership (rg_config.initial_members, 0 read as every slot)
   uint64_t* rdst;              // [RD_ROWS][nrep] ReadIndex state
 };
 
@@ -279,6 +289,7 @@ struct PersistParams {
   Placement pl;
   const uint64_t* s64;       // current state
   const uint64_t* s64_prev;  // state at the start of the last tick
+  const uint32_t* s32;       // current state (membership)
   const uint64_t* persist_lo;
   const uint64_t* tr;
   const uint2* info;

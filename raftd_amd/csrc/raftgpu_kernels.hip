@@ -421,6 +421,9 @@ __global__ void bootstrap_kernel(TickParams p, uint2* info) {
   a[S_LAST * n] = R;
   a[S_COMMITTED * n] = R;
   b[S_RNG_CTR * n] = 1;
+  const uint32_t im = p.IM ? p.IM : (1u << R) - 1u;  // initialMembers
+  b[S_MEMBERS * n] = im;
+  b[S_SNAP_MEMBERS * n] = im;
   const uint64_t key = (pl_group(p.pl, s, g) << 32) | ((uint64_t)s << 24) | 1ull;
   b[S_RAND_TO * n] = p.ET + (uint32_t)(mix64(p.seed ^ mix64(key)) % p.ET);
   for (uint32_t j = 0; j < R; ++j) {  // addNode → setRemote(id, 0, last+1)

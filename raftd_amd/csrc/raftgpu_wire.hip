@@ -266,11 +266,12 @@ __global__ void unpack_kernel(WireParams w) {
              (unsigned long long)rend);
       break;
     }
-    bool sane = true;  // every entry word: length <= P, payload bit exactly when the length is non-zero
-    for (uint32_t e = 0; e < n; ++e) {
+    bool sane = true;  // every entry word: an application entry's length <= P with the payload bit
+    for (uint32_t e = 0; e < n; ++e) {  // exactly when non-zero; a ConfigChange: no payload, a descriptor
       const uint64_t rw = h[8 + 2 * e];
       const uint32_t ln = word_len(rw);
-      sane = sane && ln <= w.P && ((rw & PAY_BIT) != 0) == (ln != 0);
+      sane = sane && ((rw & TYPE_BIT) ? !(rw & PAY_BIT) && ln <= 0x2Fu
+                                      : ln <= w.P && ((rw & PAY_BIT) != 0) == (ln != 0));
     }
     if (!sane) {
       RG_OOB("RG_BOUNDS unpack u=%u k=%u: entry word with a bad length\n", u, k);

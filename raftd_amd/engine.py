@@ -33,7 +33,8 @@ class Config(C.Structure):
         ("snapshot_entries", C.c_uint32), ("compaction_overhead", C.c_uint32),
         ("drop_ppm", C.c_uint32), ("device", C.c_int32), ("seed", C.c_uint64),
         ("ranks", C.c_uint32), ("rank", C.c_uint32), ("wire_all", C.c_uint32), ("column_base", C.c_uint32),
-        ("crc32c", C.c_uint32), ("apply_feedback", C.c_uint32),
+        ("crc32c", C.c_uint32), ("apply_feedback", C.c_uint32), ("initial_members", C.c_uint32),
+        ("_cpad", C.c_uint32),
     ]
 
 
@@ -46,6 +47,7 @@ class ReplicaView(C.Structure):
         ("role", C.c_uint32), ("election_tick", C.c_uint32), ("heartbeat_tick", C.c_uint32),
         ("rand_timeout", C.c_uint32), ("rng_ctr", C.c_uint32), ("granted", C.c_uint32),
         ("responded", C.c_uint32), ("active", C.c_uint32), ("err", C.c_uint32), ("drops", C.c_uint32),
+        ("members", C.c_uint32), ("snap_members", C.c_uint32), ("cc_pending", C.c_uint32), ("_mpad", C.c_uint32),
         ("match", C.c_uint64 * MAX_R), ("next", C.c_uint64 * MAX_R), ("rsnap", C.c_uint64 * MAX_R),
         ("rstate", C.c_uint8 * MAX_R),
     ]
@@ -82,7 +84,7 @@ APPLY_DTYPE = np.dtype([("index", "<u8"), ("group", "<u8"), ("replica_id", "<u4"
 PERSIST_STATE_DTYPE = np.dtype([("group", "<u8"), ("replica_id", "<u4"), ("rid", "<u4"), ("term", "<u8"),
                                 ("vote", "<u8"), ("commit", "<u8"), ("last", "<u8"), ("marker", "<u8"),
                                 ("marker_term", "<u8"), ("snap_index", "<u8"), ("snap_term", "<u8"),
-                                ("first", "<u8"), ("entry_off", "<u8")])
+                                ("first", "<u8"), ("entry_off", "<u8"), ("members", "<u4"), ("snap_members", "<u4")])
 PERSIST_ENTRY_DTYPE = np.dtype([("index", "<u8"), ("term", "<u8"), ("type", "<u4"), ("len", "<u4"), ("crc", "<u4"),
                                 ("rid", "<u4")])
 
@@ -122,7 +124,17 @@ class TickInput(C.Structure):
                 ("isolate", C.c_void_p), ("flags", C.c_uint32), ("_pad", C.c_uint32)]
 
 
-REPLICA_FIELDS = [f for f, _ in ReplicaView._fields_]
+REPLICA_FIELDS = [f for f, _ in ReplicaView._fields_ if not f.startswith("_")]
+CC_ADD, CC_REMOVE = 1, 2  # rg_config_change ops
+
+
+def with_members(view: dict, R: int) -> dict:
+    """A view for import: a dict without membership fields means every slot is a member."""
+    if "members" not in view:
+        view = dict(view, members=(1 << R) - 1)
+    if "snap_members" not in view:
+        view = dict(view, snap_members=view["members"])
+    return view
 MSG_FIELDS = [f for f, _ in MsgView._fields_]
 
 # every symbol include/raftgpu.h declares
@@ -132,7 +144,8 @@ EXPORTS = ["rg_create", "rg_destroy", "rg_bootstrap", "rg_fill_slabs", "rg_tick"
            "rg_device_bytes", "rg_last_error", "rg_last_tick_traffic", "rg_join",
            "rg_timing", "rg_kernel_ms", "rg_wire_plan", "rg_wire_pack", "rg_wire_recv", "rg_global_id",
            "rg_apply_committed", "rg_probe_copy", "rg_persist_collect", "rg_snapshot_events", "rg_propose",
-           "rg_notify_applied", "rg_apply_async", "rg_apply_wait", "rg_read_index", "rg_read_index_results"]
+           "rg_notify_applied", "rg_apply_async", "rg_apply_wait", "rg_read_index", "rg_read_index_results",
+           "rg_config_change"]
 
 _lib = None
 
@@ -177,6 +190,7 @@ def load_library(path: str = LIB_PATH):
         "rg_notify_applied": ([vp, vp, vp, C.c_size_t], i32),
         "rg_apply_async": ([vp, u32, i32], i32),
         "rg_read_index": ([vp, C.POINTER(ReadRequest), C.c_size_t], i32),
+        "rg_config_change": ([vp, u64, u32, u32, u32], i32),
         "rg_read_index_results": ([vp, u32, vp, u64, C.POINTER(C.c_uint64)], i32),
         "rg_apply_wait": ([vp, i32, C.POINTER(vp), C.POINTER(vp), C.POINTER(C.c_uint64)], i32),
         "rg_deliver": ([vp, u32, C.POINTER(MsgView)], i32),
@@ -209,7 +223,8 @@ def default_config(**kw) -> dict:
     c = dict(groups=4, replicas=3, log_capacity=2048, payload_bytes=256, max_entries_per_msg=64,
              max_msgs_per_pair=8, num_slabs=2, election_rtt=10, heartbeat_rtt=1, check_quorum=1,
              snapshot_entries=1000, compaction_overhead=5, drop_ppm=0, device=0, seed=0x5EED,
-             ranks=1, rank=0, wire_all=0, column_base=0, crc32c=0, apply_feedback=0)
+             ranks=1, rank=0, wire_all=0, column_base=0, crc32c=0, apply_feedback=0,
+             initial_members=0)
     c.update(kw)
     return c
 
@@ -374,6 +389,7 @@ class Engine:
         return self.entries(rid, index, 1, with_payload)[0]
 
     def import_replica(self, rid, view: dict, terms, types=None, payloads=None, lens=None):
+        view = with_members(view, self.R)
         v = ReplicaView()
         for f in REPLICA_FIELDS:
             if f in view:
@@ -417,6 +433,11 @@ class Engine:
         out = np.zeros(max(n.value, 1), READ_READY_DTYPE)
         self._check(self.L.rg_read_index_results(self.h, slot_mask, out.ctypes.data, n.value, C.byref(n)))
         return out[:n.value]
+
+    def config_change(self, group, slot, op, target):
+        """Stage a membership change for the next tick (rg_config_change): ConfigChange entry adding
+        (CC_ADD) or removing (CC_REMOVE) slot `target` of global shard `group`, proposed at `slot`."""
+        self._check(self.L.rg_config_change(self.h, group, slot, op, target))
 
     def read_ready_all(self) -> dict:
         """{local rid: (ctx, index)} for the reads made ready in the last tick."""

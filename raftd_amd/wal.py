@@ -32,7 +32,7 @@ import numpy as np
 from .engine import PERSIST_ENTRY_DTYPE, PERSIST_STATE_DTYPE
 
 MAGIC = b"RGWL"
-VERSION = 1
+VERSION = 2  # 2: state records carry the membership (members, snap_members)
 HDR = struct.Struct("<4sIQQQIIQ")
 
 
@@ -134,6 +134,7 @@ def restart_view(rl: ReplicaLog, group: int, slot: int, cfg: dict, app_applied=N
                 last=last, marker=s["marker"], marker_term=s["marker_term"], snap_index=s["snap_index"],
                 snap_term=s["snap_term"], cap_base=s["marker"], role=0, election_tick=0, heartbeat_tick=0,
                 rand_timeout=rto, rng_ctr=1, granted=0, responded=0, active=0, err=0, drops=0,
+                members=s["members"], snap_members=s["snap_members"], cc_pending=0,
                 match=match, next=[last + 1] * R, rsnap=[0] * R, rstate=[0] * R)
 
 

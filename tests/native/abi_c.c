@@ -9,11 +9,14 @@
  *   rg_persist_collect                  LogDB SaveRaftState before the messages leave
  *   rg_apply_committed                  IOnDiskStateMachine.Update → POST /UpdateEntries
  *   rg_notify_applied                   NotifyRaftLastApplied once the app answered
+ *   rg_config_change                    SyncRequestDeleteReplica / SyncRequestAddReplica (:165-185)
  *   rg_leader / rg_read_replicas        GetLeaderID / SyncGetShardMembership (raft/members.go:21,30)
  *   rg_destroy                          NodeHost.Close (raft_manager.go:159)
  *
  * Checks: every proposed Cmd reaches Update exactly once per replica, in proposal order, byte for
- * byte, with its zlib CRC-32; every shard has one leader; errors come back as RG_E* codes.
+ * byte, with its zlib CRC-32 — including a follower removed from the membership for six ticks and
+ * added back, which catches up; every shard has one leader and full membership at the end; errors
+ * come back as RG_E* codes.
  * Exit 0 and "ABI_C OK" on success. Built by tests/test_abi.py (gcc, -lraftgpu -lz); run by the
  * -m gpu test there.
  */
@@ -70,6 +73,7 @@ int main(void) {
   rg_proposal bad = {G + 5, 0, 1, 0};
   uint32_t one = 1;
   EXPECT(rg_propose(e, &bad, 1, (const uint8_t*)"x", &one) == RG_EINVAL);
+  EXPECT(rg_config_change(e, 0, 0, 7, 1) == RG_EINVAL);
   EXPECT(rg_last_error()[0] != 0);
 
   uint8_t campaign[G * R];
@@ -127,6 +131,12 @@ int main(void) {
       }
     }
     CHECK(rg_propose(e, props, G, blob, lens));
+    /* a follower leaves the membership and comes back six ticks later — within its election timeout
+     * (no heartbeats reach a removed replica; one that timed out would campaign at a higher term and
+     * depose the leader when re-added, as without PreVote in dragonboat) */
+    if (t == 10 || t == 16)
+      for (uint32_t g = 0; g < G; ++g)
+        CHECK(rg_config_change(e, g, props[g].slot, t == 10 ? RG_CC_REMOVE : RG_CC_ADD, (props[g].slot + 2) % R));
     off = 0;
     for (uint32_t g = 0; g < G; ++g)
       for (uint32_t k = 0; k < PER_TICK; ++k) {
@@ -154,7 +164,7 @@ int main(void) {
     for (uint32_t r = 0; r < G * R; ++r) idx[r] = v[r].processed;
     CHECK(rg_notify_applied(e, rids, idx, G * R));
   }
-  for (int t = 0; t < 4; ++t) { /* drain: the last Cmds commit everywhere */
+  for (int t = 0; t < 16; ++t) { /* drain: the last Cmds commit everywhere, the re-added follower catches up */
     uint64_t na = 0;
     CHECK(rg_tick(e, &in));
     CHECK(rg_apply_committed(e, 0xFF, ents, pay, cap, &na));
@@ -175,6 +185,7 @@ int main(void) {
       const uint32_t r = g * R + s;
       leaders += v[r].role == RG_LEADER;
       EXPECT(v[r].err == 0);
+      EXPECT(v[r].members == (1u << R) - 1u);
       if (got[r] != want_n[g] || got_crc[r] != want_crc[g]) {
         fprintf(stderr, "shard %u replica %u: %llu Cmds crc %08x, want %llu crc %08x\n", g, s + 1,
                 (unsigned long long)got[r], got_crc[r], (unsigned long long)want_n[g], want_crc[g]);

@@ -23,6 +23,8 @@ struct Host {
   std::vector<uint32_t> pc;
   std::vector<uint64_t> hm;
   bool staged = false;
+  std::vector<uint16_t> cc;  // membership change staging: slot | descriptor << 8
+  bool cc_staged = false;
   uint64_t t = 0;
 };
 
@@ -82,6 +84,7 @@ void* ch_create(const rg_config* c) {
   h->pt.assign(G, 0xFF);
   h->pc.assign(G, 0);
   h->hm.assign(G, 0);
+  h->cc.assign(G, 0);
   return h;
 }
 
@@ -107,6 +110,9 @@ void ch_bootstrap(void* hh) {  // = bootstrap_kernel
     h->s64[0][S_LAST * n + q] = R;
     h->s64[0][S_COMMITTED * n + q] = R;
     h->s32[0][S_RNG_CTR * n + q] = 1;
+    const uint32_t im = h->c.initial_members ? h->c.initial_members : (1u << R) - 1u;
+    h->s32[0][S_MEMBERS * n + q] = im;
+    h->s32[0][S_SNAP_MEMBERS * n + q] = im;
     const uint64_t key = ((uint64_t)g << 32) | ((uint64_t)s << 24) | 1ull;
     h->s32[0][S_RAND_TO * n + q] = h->c.election_rtt + (uint32_t)(mix64(h->c.seed ^ mix64(key)) % h->c.election_rtt);
     for (uint32_t j = 0; j < R; ++j) {
@@ -134,6 +140,7 @@ int ch_tick(void* hh, const rg_tick_input* in) {
     p.prop_count = h->pc.data();
     p.prop_hmask = h->hm.data();
   }
+  if (h->cc_staged) p.cc_in = h->cc.data();
   for (uint32_t q = 0; q < h->nrep; ++q) {
     switch (h->c.replicas) {
 #define RG_CASE(r) \
@@ -154,6 +161,19 @@ int ch_tick(void* hh, const rg_tick_input* in) {
     std::fill(h->hm.begin(), h->hm.end(), 0ull);
     h->staged = false;
   }
+  if (h->cc_staged) {
+    std::fill(h->cc.begin(), h->cc.end(), (uint16_t)0);
+    h->cc_staged = false;
+  }
+  return 0;
+}
+
+// = rg_config_change's staging (no validation beyond one change per group)
+int ch_config_change(void* hh, uint32_t group, uint32_t slot, uint32_t op, uint32_t target) {
+  Host* h = (Host*)hh;
+  if (h->cc[group]) return -3;
+  h->cc[group] = (uint16_t)(slot | ((op << 4 | (target + 1)) << 8));
+  h->cc_staged = true;
   return 0;
 }
 
@@ -201,6 +221,7 @@ int ch_read_replica(void* hh, uint32_t rid, rg_replica_view* v) {
   v->rand_timeout = s32[S_RAND_TO * N]; v->rng_ctr = s32[S_RNG_CTR * N]; v->granted = s32[S_GRANTED * N];
   v->responded = s32[S_RESPONDED * N]; v->active = s32[S_ACTIVE * N]; v->err = s32[S_ERR * N];
   v->drops = s32[S_DROPS * N];
+  v->members = s32[S_MEMBERS * N]; v->snap_members = s32[S_SNAP_MEMBERS * N]; v->cc_pending = s32[S_CC_PENDING * N];
   const uint32_t R = h->c.replicas;
   for (uint32_t j = 0; j < R; ++j) {
     v->match[j] = h->rem[a][(0 * R + j) * N + q];
@@ -239,7 +260,7 @@ int ch_read_words(void* hh, uint32_t rid, uint64_t first, uint32_t n, uint64_t* 
 }
 
 int ch_import(void* hh, uint32_t rid, const rg_replica_view* v, const uint64_t* terms, const uint32_t* types,
-              int with_payload) {
+              int with_payload, const uint32_t* lens) {
   Host* h = (Host*)hh;
   const uint32_t q = qof(h, rid);
   const uint64_t N = h->nrep;
@@ -254,6 +275,8 @@ int ch_import(void* hh, uint32_t rid, const rg_replica_view* v, const uint64_t* 
   s32[S_RAND_TO * N] = v->rand_timeout; s32[S_RNG_CTR * N] = v->rng_ctr; s32[S_GRANTED * N] = v->granted;
   s32[S_RESPONDED * N] = v->responded; s32[S_ACTIVE * N] = v->active; s32[S_ERR * N] = v->err;
   s32[S_DROPS * N] = v->drops;
+  s32[S_MEMBERS * N] = v->members; s32[S_SNAP_MEMBERS * N] = v->snap_members; s32[S_CC_PENDING * N] = v->cc_pending;
+  s64[S_CC_HI * N] = v->last;  // any imported entry may be a ConfigChange
   const uint32_t R = h->c.replicas;
   for (uint32_t j = 0; j < R; ++j) {
     h->rem[a][(0 * R + j) * N + q] = v->match[j];
@@ -263,10 +286,11 @@ int ch_import(void* hh, uint32_t rid, const rg_replica_view* v, const uint64_t* 
   }
   for (uint64_t i = v->marker + 1; i <= v->last; ++i) {
     const uint64_t k = i - v->marker - 1;
-    const uint32_t ty = types ? types[k] : 0;
-    const bool hp = with_payload && h->c.payload_bytes && ty == 0;
+    const uint32_t ty = types ? types[k] & 0xFFu : 0;
+    const bool hp = with_payload && h->c.payload_bytes && ty == 0 && !(types && (types[k] & 0x100u));
+    const uint32_t ln = lens ? lens[k] : h->c.payload_bytes;
     h->tr[(i & (h->c.log_capacity - 1)) * N + q] = (terms[k] & TERM_MASK) | (ty ? TYPE_BIT : 0) |
-                                                   (hp ? len_bits(h->c.payload_bytes) : 0);
+                                                   (ty ? cc_bits(lens ? lens[k] : 0) : hp ? len_bits(ln) : 0);
   }
   return 0;
 }

@@ -114,7 +114,8 @@ class CtlHost:
         return dict(term=w[0] & ((1 << 48) - 1), type=(w[0] >> 61) & 1)
 
     def import_replica(self, rid, view: dict, terms, types=None, payloads=None, lens=None):
-        from raftd_amd.engine import REPLICA_FIELDS
+        from raftd_amd.engine import REPLICA_FIELDS, with_members
+        view = with_members(view, self.R)
         v = self._ReplicaView()
         for f in REPLICA_FIELDS:
             if f in view:
@@ -127,8 +128,16 @@ class CtlHost:
                     setattr(v, f, x)
         t = np.ascontiguousarray(np.array(list(terms) + [0], dtype=np.uint64))
         ty = None if types is None else np.ascontiguousarray(np.array(types, dtype=np.uint32))
+        ln = None if lens is None else np.ascontiguousarray(np.array(list(lens) + [0], dtype=np.uint32))
         self.L.ch_import(C.c_void_p(self.h), C.c_uint32(rid), C.byref(v), C.c_void_p(t.ctypes.data),
-                         None if ty is None else C.c_void_p(ty.ctypes.data), C.c_int(1 if payloads is not None else 0))
+                         None if ty is None else C.c_void_p(ty.ctypes.data), C.c_int(1 if payloads is not None else 0),
+                         None if ln is None else C.c_void_p(ln.ctypes.data))
+
+    def config_change(self, group, slot, op, target) -> int:
+        """rg_config_change's staging on the CPU harness (the caller validates)."""
+        fn = self.L.ch_config_change
+        fn.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
+        return fn(C.c_void_p(self.h), group, slot, op, target)
 
     def deliver(self, rid_src, **fields):
         m = self._MsgView()

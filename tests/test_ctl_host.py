@@ -25,7 +25,8 @@ def inputs(rng, G, R, emax):
     return pt, pc, camp, iso
 
 
-def xcheck(kind, seed, G, R, T, **cfg):
+def xcheck(kind, seed, G, R, T, p_cc=0.0, **cfg):
+    """p_cc: per group and tick, the probability of a membership change."""
     kw = dict(groups=G, replicas=R, payload_bytes=16, max_entries_per_msg=8, log_capacity=64,
               snapshot_entries=20, compaction_overhead=5, drop_ppm=150000, seed=seed)
     kw.update(cfg)
@@ -34,6 +35,10 @@ def xcheck(kind, seed, G, R, T, **cfg):
     b.bootstrap()
     rng = np.random.default_rng(seed)
     for t in range(T):
+        if p_cc:
+            from test_oracle import random_ccs
+            for c in random_ccs(rng, G, R, p_cc):
+                assert b.config_change(*c) == 0 and a.config_change(*c) == 0
         ins = inputs(rng, G, R, kw["max_entries_per_msg"])
         a.tick(*ins)
         b.tick(*ins)
@@ -54,6 +59,12 @@ def test_control_step_matches_oracle(R):
 
 def test_control_step_heavy_loss():
     xcheck("ctl", 77, G=6, R=5, T=200, drop_ppm=300000, max_msgs_per_pair=4)
+
+
+@pytest.mark.parametrize("R,im", [(3, 0), (5, 0b01011), (8, 0), (2, 0b01), (7, 0b1110111)])
+def test_control_step_membership_matches_oracle(R, im):
+    """ConfigChange proposals through the kernel's step: members, quorum, elections, snapshots."""
+    xcheck("ctl", 200 + R, G=5, R=R, T=160, p_cc=0.06, initial_members=im)
 
 
 @pytest.mark.parametrize("name,fn", [
@@ -77,6 +88,7 @@ def test_control_step_under_asan():
                    for lib in ("libasan.so", "libubsan.so"))
     code = ("import sys; sys.path[:0] = [%r, %r]; import test_ctl_host as t; "
             "t.xcheck('ctl-asan', 5, G=3, R=3, T=60); t.xcheck('ctl-asan', 6, G=2, R=5, T=60); "
+            "t.xcheck('ctl-asan', 7, G=3, R=8, T=80, p_cc=0.08); "
             "import kat_scenarios as K; fx = K.load('kat_check_msgapp.json'); "
             "[K.run_check_msgapp('ctl-asan', fx, c) for c in fx['cases']]; print('ASAN-CLEAN')"
             % (HERE, os.path.dirname(HERE)))

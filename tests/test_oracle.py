@@ -220,6 +220,113 @@ def test_read_index_c_matches_python(seed):
     assert ready > 0
 
 
+def random_ccs(rng, G, R, p=0.05):
+    """Membership changes for one tick: per group, with probability p, add or remove a random slot,
+    proposed at a random slot. Removing the last members is a legal input (the group then stalls)."""
+    return [(g, int(rng.integers(0, R)), int(rng.choice([1, 2])), int(rng.integers(0, R)))
+            for g in range(G) if rng.random() < p]
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_membership_c_matches_python(seed):
+    """ConfigChange proposals (add / remove a slot) under loss, elections and snapshots, from full
+    and partial initial memberships: both restatements agree on every view (members, snapshot
+    members, pending change), message and entry."""
+    G, R = 3, [3, 5, 4, 2, 3, 5, 7, 3][seed]
+    kw = dict(groups=G, replicas=R, payload_bytes=16, max_entries_per_msg=8, log_capacity=64, snapshot_entries=20,
+              compaction_overhead=5, drop_ppm=[100000, 50000, 0, 100000, 0, 150000, 0, 50000][seed], seed=500 + seed,
+              initial_members=[0, 0b01111, 0b0111, 0, 0b011, 0, 0b1011011, 0][seed])
+    a, b = make("c", **kw), make("py", **kw)
+    a.bootstrap()
+    b.bootstrap()
+    rng = np.random.default_rng(seed)
+    changed = dropped = 0
+    for t in range(160):
+        for c in random_ccs(rng, G, R):
+            ra, rb = a.config_change(*c), b.config_change(*c)
+            assert ra == rb == 0, (t, c)
+        ins = random_inputs(rng, G, R, 8)
+        a.tick(*ins)
+        b.tick(*ins)
+        for rid in range(G * R):
+            va = a.replica(rid)
+            assert va == b.replica(rid), (seed, t, rid)
+            for d in range(R):
+                assert a.msgs(rid, d) == b.msgs(rid, d), (seed, t, rid, d)
+            for i in range(va["marker"] + 1, va["last"] + 1):
+                assert a.entry(rid, i) == b.entry(rid, i), (seed, t, rid, i)
+            changed += va["members"] != (kw["initial_members"] or (1 << R) - 1)
+    assert changed > 0
+
+
+def test_membership_scenario():
+    """Remove a follower, then the leader, then add both back (3 slots, one group): quorum follows
+    the membership, a removed leader steps down, a removed replica never campaigns, an added one
+    catches up."""
+    from oracle.pyoracle import CC_ADD, CC_REMOVE
+    o = make("c", groups=1, replicas=3, payload_bytes=16, max_entries_per_msg=8, log_capacity=256,
+             snapshot_entries=0)
+    o.bootstrap()
+    o.tick()
+    o.tick(campaign=np.array([1, 0, 0], np.uint8))
+    for _ in range(3):
+        o.tick()
+    assert o.replica(0)["role"] == 2
+    pt, pc = np.zeros(1, np.uint8), np.ones(1, np.uint32)
+    assert o.config_change(0, 0, CC_REMOVE, 2) == 0
+    assert o.config_change(0, 0, CC_ADD, 1) == -3  # one change per shard per tick
+    for _ in range(4):
+        o.tick()
+    assert [o.replica(r)["members"] for r in range(3)] == [0b011, 0b011, 0b011]  # slot 2 applied it too
+    iso = np.array([0, 0, 1], np.uint8)
+    c0 = o.replica(0)["committed"]
+    for _ in range(4):  # slot 2 cut off: the 2-member quorum {0, 1} still commits
+        o.tick(pt, pc, isolate=iso)
+    assert o.replica(0)["committed"] >= c0 + 2
+    iso = np.array([0, 1, 0], np.uint8)
+    for _ in range(2):  # responses slot 1 sent before the cut still arrive
+        o.tick(pt, pc, isolate=iso)
+    c0 = o.replica(0)["committed"]
+    for _ in range(4):  # slot 1 cut off: no quorum of {0, 1}, though slot 2 is reachable
+        o.tick(pt, pc, isolate=iso)
+    assert o.replica(0)["committed"] == c0
+    for _ in range(3):
+        o.tick()
+    assert o.config_change(0, 1, CC_REMOVE, 0) == 0  # proposed at a follower: forwarded
+    for _ in range(5):
+        o.tick()
+    v = [o.replica(r) for r in range(3)]
+    assert v[0]["members"] == 0b010 and v[0]["role"] == 0  # the removed leader stepped down
+    for _ in range(40):
+        o.tick()
+    v = [o.replica(r) for r in range(3)]
+    assert v[1]["role"] == 2 and v[0]["role"] != 2 and v[2]["role"] != 2  # sole member leads itself
+    c1 = v[1]["committed"]
+    o.tick(np.array([1], np.uint8), np.ones(1, np.uint32))
+    assert o.replica(1)["committed"] == c1 + 1  # single-node quorum commits on append
+    assert o.config_change(0, 1, CC_ADD, 2) == 0
+    for _ in range(6):
+        o.tick()
+    assert o.replica(1)["members"] == 0b110
+    o.tick(np.array([1], np.uint8), np.full(1, 4, np.uint32))
+    for _ in range(4):
+        o.tick()
+    assert o.replica(2)["last"] == o.replica(1)["last"] and o.replica(2)["committed"] == o.replica(1)["committed"]
+
+
+def test_config_change_validation():
+    for kind in ("c", "py"):
+        o = make(kind, groups=2, replicas=3, payload_bytes=16)
+        o.bootstrap()
+        assert o.config_change(2, 0, 1, 0) == -1   # no such group
+        assert o.config_change(0, 3, 1, 0) == -1   # no such slot
+        assert o.config_change(0, 0, 1, 3) == -1   # no such target
+        assert o.config_change(0, 0, 3, 0) == -1   # no such op
+        assert o.config_change(0, 0, 2, 1) == 0
+        assert o.config_change(0, 1, 1, 1) == -3   # one per shard per tick
+        assert o.config_change(1, 1, 1, 1) == 0
+
+
 def test_propose_validation():
     o = pyoracle.Oracle(groups=2, replicas=3, payload_bytes=16, max_entries_per_msg=4)
     py = make("py", groups=2, replicas=3, payload_bytes=16, max_entries_per_msg=4)

@@ -10,7 +10,7 @@ P = 16
 
 def rec(group, slot, term, commit, first, last, marker=0, ents=(), vote=0):
     st = np.zeros(1, PERSIST_STATE_DTYPE)
-    st[0] = (group, slot + 1, 0, term, vote, commit, last, marker, term if marker else 0, marker, 0, first, 0)
+    st[0] = (group, slot + 1, 0, term, vote, commit, last, marker, term if marker else 0, marker, 0, first, 0, 7, 7)
     en = np.zeros(len(ents), PERSIST_ENTRY_DTYPE)
     pay = np.zeros((len(ents), P), np.uint8)
     for k, (i, t, ln) in enumerate(ents):
@@ -56,9 +56,11 @@ def test_restart_view_is_a_fresh_follower():
     from raftd_amd.wal import ReplicaLog
     from oracle.pyoracle import mix64
     rl = ReplicaLog()
-    rl.state = dict(term=7, vote=2, commit=40, last=44, marker=30, marker_term=6, snap_index=35, snap_term=6)
+    rl.state = dict(term=7, vote=2, commit=40, last=44, marker=30, marker_term=6, snap_index=35, snap_term=6,
+                    members=0b011, snap_members=0b111)
     cfg = dict(replicas=3, election_rtt=10, seed=0x5EED)
     v = restart_view(rl, group=9, slot=1, cfg=cfg)
     assert (v["term"], v["vote"], v["committed"], v["applied"], v["role"], v["leader"]) == (7, 2, 40, 40, 0, 0)
     assert v["match"] == [0, 44, 0] and v["next"] == [45] * 3 and v["cap_base"] == 30
+    assert (v["members"], v["snap_members"], v["cc_pending"]) == (0b011, 0b111, 0)
     assert v["rand_timeout"] == 10 + mix64(0x5EED ^ mix64((9 << 32) | (1 << 24) | 1)) % 10
