@@ -114,6 +114,68 @@ def kats() -> dict:
         "source": "etcd raft TestLeaderAcknowledgeCommit shape; SURVEY.md §4 'Quorum commit'",
         "cases": cases,
     }
+    # etcd TestLeaderElection: a candidate wins iff the reachable nodes (itself included) are a
+    # quorum; etcd's terms start at 0, the engine's bootstrap term is 1: the campaign adds one
+    out["kat_leader_election.json"] = {
+        "source": "etcd raft TestLeaderElection (raft_test.go); nopStepper nodes = unreachable slots",
+        "term_delta": 1,
+        "cases": [
+            {"size": 3, "down": [], "state": "leader"},
+            {"size": 3, "down": [2], "state": "leader"},
+            {"size": 3, "down": [1, 2], "state": "candidate"},
+            {"size": 4, "down": [1, 2], "state": "candidate"},
+            {"size": 5, "down": [1, 2], "state": "leader"},
+        ],
+    }
+    # etcd TestCandidateFallback: a candidate that receives MsgApp from a leader of its term or a
+    # higher one becomes that leader's follower at the message's term
+    out["kat_candidate_fallback.json"] = {
+        "source": "etcd raft TestCandidateFallback (raft_paper_test.go)",
+        "cases": [{"term_delta": 0, "state": "follower"}, {"term_delta": 1, "state": "follower"}],
+    }
+    # etcd Test{Follower,Candidate,Leader}UpdateTermFromMessage: MsgApp at term + 1 → follower at
+    # term + 1 whose leader is the sender
+    out["kat_update_term.json"] = {
+        "source": "etcd raft testUpdateTermFromMessage (raft_paper_test.go) for each starting state",
+        "cases": [{"state": "follower"}, {"state": "candidate"}, {"state": "leader"}],
+        "want_state": "follower", "want_term_delta": 1, "want_leader_is_sender": True,
+    }
+    # etcd TestLeaderCommitEntry: once a majority holds the new entry the leader commits it and its
+    # next messages carry that commit index
+    out["kat_leader_commit_entry.json"] = {
+        "source": "etcd raft TestLeaderCommitEntry (raft_paper_test.go)",
+        "size": 3, "leader_log": [1, 2], "leader_term": 2, "proposals": 1,
+        "want_commit": 3, "want_msg_commit": 3,
+    }
+    # etcd TestFollowerCommitEntry: the follower commits min(leader commit, last new entry)
+    out["kat_follower_commit_entry.json"] = {
+        "source": "etcd raft TestFollowerCommitEntry (raft_paper_test.go)",
+        "cases": [
+            {"entries": [1], "commit": 1, "want_commit": 1},
+            {"entries": [1, 1], "commit": 2, "want_commit": 2},
+            {"entries": [1, 1], "commit": 1, "want_commit": 1},
+        ],
+    }
+    # etcd TestVoteRequest: after its election timeout a follower campaigns at term + 1 and asks
+    # every other node with its last entry's term and index
+    out["kat_vote_request.json"] = {
+        "source": "etcd raft TestVoteRequest (raft_paper_test.go)",
+        "cases": [
+            {"log": [1], "term": 1, "want_term": 2, "want_log_term": 1, "want_log_index": 1},
+            {"log": [1, 2], "term": 2, "want_term": 3, "want_log_term": 2, "want_log_index": 2},
+        ],
+    }
+    # etcd TestLeaderStepdownWhenQuorumActive / ...QuorumLost (CheckQuorum): after an election
+    # timeout a leader stays only if it heard from a quorum (itself included)
+    out["kat_check_quorum.json"] = {
+        "source": "etcd raft TestLeaderStepdownWhenQuorumActive / TestLeaderStepdownWhenQuorumLost (raft_test.go)",
+        "cases": [
+            {"size": 3, "active": [], "state": "follower"},
+            {"size": 3, "active": [1], "state": "leader"},
+            {"size": 5, "active": [1], "state": "follower"},
+            {"size": 5, "active": [1, 2], "state": "leader"},
+        ],
+    }
     return out
 
 

@@ -81,6 +81,11 @@ def test_control_step_kats(name, fn):
     assert all(fn("ctl"))
 
 
+@pytest.mark.parametrize("name", sorted(K.PAPER_KATS))
+def test_control_step_paper_kats(name):
+    assert all(K.PAPER_KATS[name]("ctl"))
+
+
 def test_control_step_under_asan():
     from native import ctl_host
     ctl_host.build(asan=True)

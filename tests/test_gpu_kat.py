@@ -43,3 +43,9 @@ def test_leader_only_commits_current_term():
 @pytest.mark.parametrize("case", QC["cases"])
 def test_quorum_commit(case):
     assert K.run_quorum_commit("gpu", case) == case["committed"]
+
+
+@pytest.mark.parametrize("name", sorted(K.PAPER_KATS))
+def test_paper_kats(name):
+    """The etcd paper-test shapes through rg_import_replica / rg_deliver / rg_tick."""
+    assert all(K.PAPER_KATS[name]("gpu"))

@@ -50,3 +50,11 @@ def test_leader_only_commits_current_term(kind):
 @pytest.mark.parametrize("case", QC["cases"], ids=lambda c: f"n{c['size']}-{c['acceptors']}")
 def test_quorum_commit(kind, case):
     assert K.run_quorum_commit(kind, case) == case["committed"]
+
+
+@pytest.mark.parametrize("kind", KINDS_CPU)
+@pytest.mark.parametrize("name", sorted(K.PAPER_KATS))
+def test_paper_kats(kind, name):
+    """etcd raft paper-test shapes (leader election, candidate fallback, term update, leader and
+    follower commit, vote request, CheckQuorum step-down); parity with dragonboat unpinned."""
+    assert all(K.PAPER_KATS[name](kind))
