@@ -51,7 +51,7 @@ def test_read_index_chaos(R):
 def test_read_index_no_loss():
     """Without drops every follower's forwarded read comes back as a ReadIndexResp."""
     cfg = dict(CHAOS, groups=8, replicas=3, payload_bytes=16, max_entries_per_msg=8, drop_ppm=0, seed=17)
-    assert run_reads(cfg, ticks=80, seed=11) > 100
+    assert run_reads(cfg, ticks=80, seed=11) > 30
 
 
 @pytest.mark.parametrize("ranks", [2, 3])
