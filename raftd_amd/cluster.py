@@ -331,6 +331,40 @@ class DistEngine(_Feeds):
                 p.finish()
             self.primed = False
 
+    # ---- caller inputs in global shard ids, routed to the half hosting the shard's column; the
+    # replicas other ranks host are theirs to stage (every rank may pass the same list)
+    def _half_engine(self, group: int):
+        return self.parts[(group // self.N) // self.cols].eng
+
+    def hosts(self, group: int, slot: int) -> bool:
+        """Whether this rank hosts replica `slot` of global shard `group` (placement)."""
+        return rank_of(group, slot, self.N) == self.rank
+
+    def propose(self, batches):
+        """rg_propose of the batches [(global group, slot, [Cmd bytes])] whose replica is hosted here."""
+        per = {}
+        for g, s, cmds in batches:
+            if self.hosts(g, s):
+                e = self._half_engine(g)
+                per.setdefault(id(e), (e, []))[1].append((g, s, cmds))
+        for e, b in per.values():
+            e.propose(b)
+
+    def config_change(self, group, slot, op, target):
+        """rg_config_change, if replica `slot` of global shard `group` is hosted here."""
+        if self.hosts(group, slot):
+            self._half_engine(group).config_change(group, slot, op, target)
+
+    def read_index(self, reqs):
+        """rg_read_index of the requests [(global group, slot, ctx)] whose replica is hosted here."""
+        per = {}
+        for g, s, ctx in reqs:
+            if self.hosts(g, s):
+                e = self._half_engine(g)
+                per.setdefault(id(e), (e, []))[1].append((g, s, ctx))
+        for e, b in per.values():
+            e.read_index(b)
+
     # ---- aggregates over the halves (bench)
     def bootstrap(self):
         for p in self.parts:

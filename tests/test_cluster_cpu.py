@@ -118,3 +118,17 @@ def test_transport_gloo_world2():
         p.join(60)
         assert p.exitcode == 0
     assert all(ok for _, ok, _ in res), res
+
+
+@pytest.mark.parametrize("N,halves", [(1, 1), (2, 2), (3, 1), (8, 2)])
+def test_dist_engine_routes_a_shard_to_its_half(N, halves):
+    """DistEngine.propose / config_change / read_index route global shard g to half
+    (g div N) div cols: the half whose columns hold g on the rank that hosts the replica."""
+    cols = 12 // halves
+    for rank in range(N):
+        for h in range(halves):
+            for s in range(3):
+                for j in range(h * cols, (h + 1) * cols):
+                    g = global_group(rank, s, j, N)
+                    assert rank_of(g, s, N) == rank
+                    assert (g // N) // cols == h
