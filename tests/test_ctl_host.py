@@ -101,3 +101,26 @@ def test_control_step_under_asan():
                UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and "ASAN-CLEAN" in r.stdout, r.stderr[-3000:]
+
+
+def test_control_step_c3_shape():
+    """C3's per-rank shape (8,192 columns x 5, L 512, 64-entry batches of 256 B, SnapshotEntries
+    200) for 24 ticks, past a ring wrap and snapshots, against the oracle on sampled replicas: the
+    index arithmetic at the size where the GPU fault appeared."""
+    G, R = 8192, 5
+    cfg = dict(groups=G, replicas=R, log_capacity=512, payload_bytes=256, max_entries_per_msg=64,
+               snapshot_entries=200, seed=0xC3)
+    a, b = make("ctl", **cfg), make("c", **cfg)
+    a.bootstrap()
+    b.bootstrap()
+    camp = np.zeros(G * R, np.uint8)
+    camp[0::R] = 1
+    pt, pc = np.zeros(G, np.uint8), np.full(G, 64, np.uint32)
+    for t in range(24):
+        ins = dict(campaign=camp) if t == 1 else (dict(prop_target=pt, prop_count=pc) if t >= 6 else {})
+        a.tick(**ins)
+        b.tick(threads=8, **ins)
+        if t % 4 == 3:
+            for rid in range(0, G * R, 997):
+                assert a.replica(rid) == b.replica(rid), (t, rid)
+    assert b.replica(0)["committed"] > 512 and b.replica(0)["marker"] > 0
