@@ -35,10 +35,6 @@ import os
 import sys
 import time
 
-# Kernel arguments in host memory (HIP_FORCE_DEV_KERNARG=0), set before anything initialises HIP.
-# Device-memory kernel arguments are the suspected cause of the intermittent control-kernel
-# faults (DESIGN.md §3 "The control-kernel fault"). An explicit setting in the environment wins.
-os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "0")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)

@@ -31,8 +31,12 @@ def build_engine(force: bool = False, verbose: bool = False) -> str:
     objs, report = [], []
     for src in SOURCES:
         obj = os.path.join(CSRC, src.rsplit(".", 1)[0] + ".o")
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function",
-               "-c", "-x", "hip", os.path.join(CSRC, src), "-o", obj]
+        if src.endswith(".hip"):
+            lang = [f"--offload-arch={ARCH}", "-x", "hip"]
+        else:  # host-only runtime (no device pass: TickParams' device-side address spaces stay out of it)
+            lang = ["-x", "c++", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include"]
+        cmd = [HIPCC] + lang + ["-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function",
+                                "-c", os.path.join(CSRC, src), "-o", obj]
         if src.endswith(".hip"):
             cmd.append("-Rpass-analysis=kernel-resource-usage")
         if verbose:

@@ -114,8 +114,8 @@ __global__ void scatter_replica_kernel(AdminParams a, uint32_t rid, const rg_rep
   const rg_replica_view& v = *vv;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) {
-    uint64_t* s64 = const_cast<uint64_t*>(t.s64_in) + q;
-    uint32_t* s32 = const_cast<uint32_t*>(t.s32_in) + q;
+    uint64_t* s64 = ((uint64_t*)(t.s64_in)) + q;
+    uint32_t* s32 = ((uint32_t*)(t.s32_in)) + q;
     s64[S_TERM * N] = v.term; s64[S_VOTE * N] = v.vote; s64[S_LEADER * N] = v.leader;
     s64[S_COMMITTED * N] = v.committed; s64[S_APPLIED * N] = v.applied; s64[S_LAST * N] = v.last;
     s64[S_MARKER * N] = v.marker; s64[S_MARKER_TERM * N] = v.marker_term; s64[S_SNAP_INDEX * N] = v.snap_index;
@@ -126,8 +126,8 @@ __global__ void scatter_replica_kernel(AdminParams a, uint32_t rid, const rg_rep
     s32[S_DROPS * N] = v.drops;
     s32[S_MEMBERS * N] = v.members; s32[S_SNAP_MEMBERS * N] = v.snap_members; s32[S_CC_PENDING * N] = v.cc_pending;
     s64[S_CC_HI * N] = v.last;  // any imported entry may be a ConfigChange
-    uint64_t* rem = const_cast<uint64_t*>(t.rem_in);
-    uint8_t* rst = const_cast<uint8_t*>(t.rst_in);
+    uint64_t* rem = ((uint64_t*)(t.rem_in));
+    uint8_t* rst = ((uint8_t*)(t.rst_in));
     for (uint32_t j = 0; j < t.R; ++j) {
       rem[(0 * t.R + j) * N + q] = v.match[j];
       rem[(1 * t.R + j) * N + q] = v.next[j];
@@ -159,18 +159,18 @@ __global__ void deliver_kernel(AdminParams a, uint32_t rid, const rg_msg_view* m
   const TickParams& t = a.t;
   const uint32_t g = rid / t.R, s = rid - g * t.R, q = s * t.G + g;
   const uint32_t dst = m->to - 1;
-  uint32_t* cnt = const_cast<uint32_t*>(t.cnt_in) + ((uint64_t)s * t.R + dst) * t.G + g;
+  uint32_t* cnt = ((uint32_t*)(t.cnt_in)) + ((uint64_t)s * t.R + dst) * t.G + g;
   const uint32_t k = *cnt;
   if (k >= t.K) {
     *status = 1;
     return;
   }
   const uint64_t plane = (uint64_t)t.R * t.R * t.K * t.G;
-  uint64_t* h = const_cast<uint64_t*>(t.hdr_in) + (((uint64_t)s * t.R + dst) * t.K + k) * t.G + g;
+  uint64_t* h = ((uint64_t*)(t.hdr_in)) + (((uint64_t)s * t.R + dst) * t.K + k) * t.G + g;
   const uint64_t* src = reinterpret_cast<const uint64_t*>(m);
   for (int w = 0; w < 8; ++w) h[w * plane] = src[w];
   if (m->type == M_REPLICATE) {
-    uint64_t* mt = const_cast<uint64_t*>(t.mt_in) + ((((uint64_t)s * t.R + dst) * t.K + k) * t.E) * t.G + g;
+    uint64_t* mt = ((uint64_t*)(t.mt_in)) + ((((uint64_t)s * t.R + dst) * t.K + k) * t.E) * t.G + g;
     for (uint32_t e = 0; e < m->nent; ++e) mt[(uint64_t)e * t.G] = t.tr[((m->log_index + 1 + e) & (t.L - 1)) * t.nrep + q];
   }
   *cnt = k + 1;
@@ -192,7 +192,7 @@ __global__ void notify_applied_kernel(AdminParams a, const uint32_t* rids, const
     return;
   }
   const uint64_t q = q_of(t, rids[i]), N = t.nrep;
-  uint64_t* s64 = const_cast<uint64_t*>(t.s64_in) + q;
+  uint64_t* s64 = ((uint64_t*)(t.s64_in)) + q;
   if (pass == 0) {
     if (index[i] > s64[S_PROCESSED * N]) atomicAdd(bad, 1u);
   } else {

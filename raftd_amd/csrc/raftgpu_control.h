@@ -842,14 +842,14 @@ struct Ctl {
       err |= ERR_WIRE;
       return;
     }
-#ifdef RG_BOUNDS  // unpack_kernel keeps only well-formed messages
+    // unreachable (senders write at most E entries, unpack_kernel keeps only well-formed messages):
+    // checked anyway, so that a damaged inbox shows up as ERR_WIRE instead of a wild address
     if (type == M_REPLICATE && (uint32_t)(w0 >> 32) > p.E) {
       RG_OOB("RG_BOUNDS control q=%u src=%u k=%u remote=%d replicate n=%u > E=%u\n", q, src, k, (int)remote,
              (uint32_t)(w0 >> 32), p.E);
       err |= ERR_WIRE;
       return;
     }
-#endif
     const bool leader_msg =
         type == M_REPLICATE || type == M_INSTALL_SNAPSHOT || type == M_HEARTBEAT || type == M_READ_INDEX_RESP;
     if (mterm != 0 && mterm != term) {
@@ -937,13 +937,11 @@ struct Ctl {
       if (src == s) continue;
       const bool remote = pl_remote(p.pl, src, s, g);
       uint32_t cnt = (remote ? p.rcnt : p.cnt_in)[((uint64_t)src * R + s) * p.G + g];
-#ifdef RG_BOUNDS  // unpack_kernel already clamps received counts to K
-      if (cnt > p.K) {  // never produced by a sender: malformed exchange data, ignored
+      if (cnt > p.K) {  // never produced by a sender (unpack_kernel clamps received counts): ERR_WIRE
         RG_OOB("RG_BOUNDS control q=%u src=%u remote=%d cnt=%u > K=%u\n", q, src, (int)remote, cnt, p.K);
         err |= ERR_WIRE;
         cnt = 0;
       }
-#endif
       for (uint32_t k = 0; k < cnt; ++k) handle(src, k, remote);
     }
     RG_STAMP(1);

@@ -51,6 +51,8 @@ static const bool g_sync_debug = [] {
     if (int _rc = (x)) return _rc; \
   } while (0)
 
+constexpr uint32_t TP_SLOTS = 128, TP_CHUNK = 32;
+
 struct rg_engine {
   rg_config c{};
   uint32_t nrep = 0, J = 0;
@@ -108,6 +110,15 @@ struct rg_engine {
   uint8_t* d_campaign = nullptr;
   uint8_t* d_isolate = nullptr;
   unsigned long long* d_sum = nullptr;
+  // control_kernel's parameter block, passed by pointer (DESIGN.md §3 "The control-kernel fault"):
+  // TP_SLOTS device slots, each written by a stream-ordered H2D copy from the pinned host slot of
+  // the same index; tp_ev[c] follows the last copy of chunk c, so a host slot is rewritten only
+  // after the copy out of it (TP_SLOTS launches earlier) has completed
+  TickParams* d_tp = nullptr;
+  TickParams* h_tp = nullptr;
+  hipEvent_t tp_ev[TP_SLOTS / TP_CHUNK] = {};
+  bool tp_used[TP_SLOTS / TP_CHUNK] = {};
+  uint64_t tp_next = 0;
   uint8_t* stage = nullptr;
   uint64_t stage_bytes = 0;
   uint64_t t = 0;
@@ -323,10 +334,6 @@ extern "C" {
 const char* rg_last_error(void) { return g_err.c_str(); }
 
 int rg_create(const rg_config* cfg, rg_engine** out) {
-  // Kernel arguments in host memory (DESIGN.md §3 "The control-kernel fault"): effective when this
-  // is the process's first HIP call; a host that initialised HIP earlier sets
-  // HIP_FORCE_DEV_KERNARG=0 itself
-  setenv("HIP_FORCE_DEV_KERNARG", "0", 0);
   if (!cfg || !out) return fail(RG_EINVAL, "null argument");
   const rg_config& c = *cfg;
   if (c.groups < 1 || c.replicas < 1 || c.replicas > RG_MAX_REPLICAS) return fail(RG_EINVAL, "groups/replicas");
@@ -404,6 +411,9 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if (rc == RG_OK) rc = dalloc(e, &e->d_campaign, n * N);
   if (rc == RG_OK) rc = dalloc(e, &e->d_isolate, n * N);
   if (rc == RG_OK) rc = dalloc(e, &e->d_sum, 64);
+  if (rc == RG_OK) rc = dalloc(e, &e->d_tp, (uint64_t)TP_SLOTS * sizeof(TickParams));
+  if (rc == RG_OK && hipHostMalloc((void**)&e->h_tp, (uint64_t)TP_SLOTS * sizeof(TickParams), 0) != hipSuccess)
+    rc = fail(RG_ENOMEM, "hipHostMalloc (parameter blocks)");
   if (rc == RG_OK) rc = dalloc(e, &e->apply_lo, n * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->acnt, n * 4);
   if (rc == RG_OK) rc = dalloc(e, &e->aoff, (n + 1) * 8);
@@ -487,6 +497,11 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
       hipEventCreateWithFlags(&e->cc_ev, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&e->stg_ev, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&e->prop_ev, hipEventDisableTiming) != hipSuccess ||
+      [&] {
+        for (hipEvent_t& ev : e->tp_ev)
+          if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return false;
+        return true;
+      }() == false ||
       hipStreamCreateWithFlags(&e->copy, hipStreamNonBlocking) != hipSuccess) {
     rg_destroy(e);
     return fail(RG_EHIP, "hipEventCreate / hipStreamCreate");
@@ -549,6 +564,9 @@ void rg_destroy(rg_engine* e) {
   if (e->h_cc) (void)hipHostFree(e->h_cc);
   if (e->h_rd) (void)hipHostFree(e->h_rd);
   if (e->prop_ev) (void)hipEventDestroy(e->prop_ev);
+  for (hipEvent_t ev : e->tp_ev)
+    if (ev) (void)hipEventDestroy(ev);
+  if (e->h_tp) (void)hipHostFree(e->h_tp);
   for (void* p : e->allocs) (void)hipFree(p);
   if (e->h_bounds) (void)hipHostFree(e->h_bounds);
   for (void* h : {(void*)e->h_pt, (void*)e->h_pc, (void*)e->h_hm, (void*)e->h_cmd})
@@ -837,6 +855,21 @@ int rg_kernel_ms(rg_engine* e, double* ms, uint64_t* launches) {
   return RG_OK;
 }
 
+// control_kernel(t) reads its parameter block from a device slot written by a copy on the same
+// stream just before the launch, so the launch's own kernel arguments are one pointer
+static int launch_control_slot(rg_engine* e, const TickParams& p) {
+  const uint32_t k = (uint32_t)(e->tp_next++ % TP_SLOTS), c = k / TP_CHUNK;
+  if (k % TP_CHUNK == 0 && e->tp_used[c]) HIPCHK(hipEventSynchronize(e->tp_ev[c]));
+  e->h_tp[k] = p;
+  HIPCHK(hipMemcpyAsync(e->d_tp + k, e->h_tp + k, sizeof(TickParams), hipMemcpyHostToDevice, e->stream));
+  if (k % TP_CHUNK == TP_CHUNK - 1) {
+    HIPCHK(hipEventRecord(e->tp_ev[c], e->stream));
+    e->tp_used[c] = true;
+  }
+  LAUNCH(launch_control(e->d_tp + k, p.R, p.nrep, e->stream), e->stream, "control_kernel");
+  return RG_OK;
+}
+
 static int tick_impl(rg_engine* e, const rg_tick_input* in, bool device_ptrs) {
   if (e->wire && e->t > 0 && !e->wire_ready)
     return fail(RG_EINVAL, "rg_tick: the last tick's messages were not exchanged (rg_wire_plan/pack/recv)");
@@ -921,7 +954,7 @@ static int tick_impl(rg_engine* e, const rg_tick_input* in, bool device_ptrs) {
   const bool two = bs != e->stream;
   if (two && e->t >= 2) HIPCHK(hipStreamWaitEvent(e->stream, e->bulk_done[a], 0));
   RGCHK(timing_event(e, e->stream, 0));
-  LAUNCH(launch_control(p, e->stream), e->stream, "control_kernel");
+  RGCHK(launch_control_slot(e, p));
   RGCHK(timing_event(e, e->stream, 0));
   if (two) {
     HIPCHK(hipEventRecord(e->ctl_done[a], e->stream));

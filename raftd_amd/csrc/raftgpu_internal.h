@@ -129,6 +129,15 @@ RG_HD_INLINE uint32_t pl_rank_of(const Placement& pl, uint64_t g, uint32_t s) {
   return (uint32_t)((g % N + pl_soff(pl, s, (uint32_t)(g / N - pl.col_base))) % N);
 }
 
+// TickParams reaches control_kernel through a pointer (a device slot, not kernel arguments), so its
+// pointer fields are loaded from memory: declared in the global address space on the device, they
+// keep every access a global_load / global_store instead of a flat one (same bits and layout as
+// the host's plain pointers)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RG_G(T) __attribute__((address_space(1))) T*
+#else
+#define RG_G(T) T*
+#endif
 struct TickParams {
   uint32_t G, R, nrep, L, P, E, K, nslab, J;
   uint32_t ET, HT, CQ, SE, CO, drop_ppm, flags;
@@ -136,43 +145,43 @@ struct TickParams {
   uint32_t AF;             // apply feedback: applied moves only by rg_notify_applied
   uint64_t seed, tick;
   Placement pl;
-  const uint64_t* s64_in;  // [S64_ROWS][nrep]
-  uint64_t* s64_out;
-  const uint32_t* s32_in;  // [S32_ROWS][nrep]
-  uint32_t* s32_out;
-  const uint64_t* rem_in;  // [3][R][nrep]: match, next, rsnap
-  uint64_t* rem_out;
-  const uint8_t* rst_in;   // [R][nrep]
-  uint8_t* rst_out;
-  uint64_t* tr;            // term ring [L][nrep]
-  const uint64_t* hdr_in;  // [8][R src][R dst][K][G]
-  uint64_t* hdr_out;
-  const uint64_t* mt_in;   // [R src][R dst][K][E][G]
-  uint64_t* mt_out;
-  const uint32_t* cnt_in;  // [R src][R dst][G]
-  uint32_t* cnt_out;
+  RG_G(const uint64_t) s64_in;  // [S64_ROWS][nrep]
+  RG_G(uint64_t) s64_out;
+  RG_G(const uint32_t) s32_in;  // [S32_ROWS][nrep]
+  RG_G(uint32_t) s32_out;
+  RG_G(const uint64_t) rem_in;  // [3][R][nrep]: match, next, rsnap
+  RG_G(uint64_t) rem_out;
+  RG_G(const uint8_t) rst_in;   // [R][nrep]
+  RG_G(uint8_t) rst_out;
+  RG_G(uint64_t) tr;            // term ring [L][nrep]
+  RG_G(const uint64_t) hdr_in;  // [8][R src][R dst][K][G]
+  RG_G(uint64_t) hdr_out;
+  RG_G(const uint64_t) mt_in;   // [R src][R dst][K][E][G]
+  RG_G(uint64_t) mt_out;
+  RG_G(const uint32_t) cnt_in;  // [R src][R dst][G]
+  RG_G(uint32_t) cnt_out;
   // remote inbox (planes whose sender lives on another rank, written by unpack_kernel; same
   // layout as hdr/mt/cnt; hdr word 7 of a Replicate = byte offset of its records in the wire)
-  const uint64_t* rhdr;
-  const uint64_t* rmt;
-  const uint32_t* rcnt;
-  uint64_t* apply_lo;      // [nrep] first index this step hands to the state machine (NULL: skip)
-  uint64_t* persist_lo;    // [nrep] lowest index written this step, ~0 if none (NULL: skip)
-  uint64_t* snap_ev;       // [nrep] restored_at | SNAP_TAKEN_BIT (NULL: skip)
-  uint32_t* prof;          // RG_CTL_PROFILE builds only: [6][nrep] s_memtime stamps per phase
-  uint64_t* job64;         // [J64_ROWS][J][nrep]
-  uint32_t* job32;         // [J32_ROWS][J][nrep]
-  uint32_t* jcnt;          // [nrep]
-  const uint8_t* prop_target;
-  const uint32_t* prop_count;
-  const uint64_t* prop_hmask;  // caller proposals: entries with a non-empty Cmd (NULL: synthetic, all of len P)
-  const uint2* slab_info;      // [nslab][rows][E] {0, Cmd length} of the proposal slabs
-  const uint8_t* campaign;
-  const uint8_t* isolate;
-  const uint64_t* read_ctx;    // [global rid] ReadIndex request contexts of this tick (NULL: none)
-  const uint16_t* cc_in;       // [global group] membership change of this tick: slot | descriptor << 8 (0 none)
+  RG_G(const uint64_t) rhdr;
+  RG_G(const uint64_t) rmt;
+  RG_G(const uint32_t) rcnt;
+  RG_G(uint64_t) apply_lo;      // [nrep] first index this step hands to the state machine (NULL: skip)
+  RG_G(uint64_t) persist_lo;    // [nrep] lowest index written this step, ~0 if none (NULL: skip)
+  RG_G(uint64_t) snap_ev;       // [nrep] restored_at | SNAP_TAKEN_BIT (NULL: skip)
+  RG_G(uint32_t) prof;          // RG_CTL_PROFILE builds only: [6][nrep] s_memtime stamps per phase
+  RG_G(uint64_t) job64;         // [J64_ROWS][J][nrep]
+  RG_G(uint32_t) job32;         // [J32_ROWS][J][nrep]
+  RG_G(uint32_t) jcnt;          // [nrep]
+  RG_G(const uint8_t) prop_target;
+  RG_G(const uint32_t) prop_count;
+  RG_G(const uint64_t) prop_hmask;  // caller proposals: entries with a non-empty Cmd (NULL: synthetic, all of len P)
+  RG_G(const uint2) slab_info;      // [nslab][rows][E] {0, Cmd length} of the proposal slabs
+  RG_G(const uint8_t) campaign;
+  RG_G(const uint8_t) isolate;
+  RG_G(const uint64_t) read_ctx;    // [global rid] ReadIndex request contexts of this tick (NULL: none)
+  RG_G(const uint16_t) cc_in;       // [global group] membership change of this tick: slot | descriptor << 8 (0 none)
   uint32_t IM;                 // bootstrap membership (rg_config.initial_members, 0 read as every slot)
-  uint64_t* rdst;              // [RD_ROWS][nrep] ReadIndex state
+  RG_G(uint64_t) rdst;              // [RD_ROWS][nrep] ReadIndex state
 };
 
 struct BulkParams {
@@ -228,7 +237,8 @@ RG_HD_INLINE uint32_t crc_of_cmd(uint32_t slot_crc, uint32_t len, uint32_t P, co
 }
 
 // host-side launchers (raftgpu_kernels.hip)
-hipError_t launch_control(const TickParams& p, hipStream_t s);
+// control_kernel<R> over nrep lanes; *p: the tick's parameter block in device memory
+hipError_t launch_control(const TickParams* p, uint32_t R, uint32_t nrep, hipStream_t s);
 hipError_t launch_bulk(const BulkParams& p, hipStream_t s, int grid);
 hipError_t launch_bootstrap(const TickParams& p, uint2* info, hipStream_t s);
 // synthetic Cmds into slabs [slab0, slab0 + nslab)

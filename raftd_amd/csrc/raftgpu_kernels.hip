@@ -29,9 +29,12 @@ __device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_re
 #ifndef RG_CTL_MINWAVES
 #define RG_CTL_MINWAVES 1
 #endif
+// The parameter block comes by pointer from a device slot the host filled with a stream-ordered
+// copy (DESIGN.md §3 "The control-kernel fault"); Ctl copies it (scalar loads, uniform address).
 template <int R>
-__global__ void __launch_bounds__(256, RG_CTL_MINWAVES) control_kernel(TickParams p) {
+__global__ void __launch_bounds__(256, RG_CTL_MINWAVES) control_kernel(const TickParams* __restrict__ pp) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  const TickParams p = *pp;
   if (q >= p.nrep) return;
 #ifdef RG_CTL_PROFILE
   const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memtime();
@@ -43,9 +46,9 @@ __global__ void __launch_bounds__(256, RG_CTL_MINWAVES) control_kernel(TickParam
   c.run();
 }
 
-hipError_t launch_control(const TickParams& p, hipStream_t s) {
-  dim3 grid((p.nrep + 255) / 256), block(256);
-  switch (p.R) {
+hipError_t launch_control(const TickParams* p, uint32_t R, uint32_t nrep, hipStream_t s) {
+  dim3 grid((nrep + 255) / 256), block(256);
+  switch (R) {
     case 1: hipLaunchKernelGGL(control_kernel<1>, grid, block, 0, s, p); break;
     case 2: hipLaunchKernelGGL(control_kernel<2>, grid, block, 0, s, p); break;
     case 3: hipLaunchKernelGGL(control_kernel<3>, grid, block, 0, s, p); break;
@@ -187,19 +190,22 @@ __device__ __forceinline__ void set_job(const BulkParams& p, Cursor& cur, const 
   cur.n = jb.meta & 0xFF; cur.b = (jb.meta >> 8) & 0xFF; cur.kind = (jb.meta >> 16) & 0xF; cur.src = jb.src;
   cur.g = WIRE ? (cur.src >> 16) * p.G + cur.q % p.G : cur.q % p.G;  // SRC_SLAB: the proposal's slab row
   cur.src &= cur.kind == SRC_SLAB ? 0xFFFFu : 0xFFFFFFFFu;
-#ifdef RG_BOUNDS
+  // a malformed job (never produced by control_kernel) is skipped and marks its replica ERR_WIRE
   const bool bad = cur.n > 64 || cur.b > cur.n || (cur.kind == SRC_RING && cur.src >= p.nrep) ||
                    (cur.kind == SRC_SLAB && (cur.src >= p.nslab || cur.g >= (WIRE ? p.nrep : p.G))) ||
                    cur.kind > SRC_WIRE_PROP ||
                    (cur.kind == SRC_WIRE && (!WIRE || cur.n > cur.src ||
                                              cur.sm + (16ull + p.P) * cur.src > p.wire_bytes));
   if (bad) {
+#ifdef RG_BOUNDS
     if (lane_id() == 0)
       printf("RG_BOUNDS bulk q=%u job=%u n=%u b=%u kind=%u src=%u sm=%llu wire_bytes=%llu\n", cur.q, cur.j, cur.n,
              cur.b, cur.kind, cur.src, (unsigned long long)cur.sm, (unsigned long long)p.wire_bytes);
-    cur.n = cur.b = 0;
-  }
 #endif
+    if (lane_id() == 0) atomicOr(p.crc_err + cur.q, ERR_WIRE);
+    cur.n = 0;
+    cur.b = 0;
+  }
 }
 
 // Move the cursor one position: the replica's next job, the tile's next replica, or the next

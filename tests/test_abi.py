@@ -85,18 +85,16 @@ def test_c_harness_runs_the_cgo_call_sequence():
 
 
 @pytest.mark.gpu
-def test_kernel_arguments_live_in_host_memory():
-    """DESIGN.md §3 "The control-kernel fault": the engine runs with HIP_FORCE_DEV_KERNARG=0 (set
-    by the package, the test session and rg_create before HIP initialises), so kernels read their
-    arguments from host memory.
-    The probe kernel reports its kernel-argument segment address; the runtime must not place it
-    in device memory."""
+def test_kernarg_probe_reports_placement():
+    """DESIGN.md §3 "The control-kernel fault": this runtime places kernel arguments in device memory
+    whatever HIP_FORCE_DEV_KERNARG says (measured r02), which is why control_kernel takes its
+    parameter block from a stream-ordered device slot instead. The probe kernel reports its
+    kernel-argument segment address and the runtime's view of it."""
     from raftd_amd.engine import load_library
-    assert os.environ.get("HIP_FORCE_DEV_KERNARG") == "0"
     L = load_library()
     fn = L.rg_debug_kernarg_placement
     fn.argtypes = [C.c_int32, C.POINTER(C.c_uint64), C.POINTER(C.c_int32)]
     addr, dev = C.c_uint64(), C.c_int32()
     assert fn(0, C.byref(addr), C.byref(dev)) == 0, L.rg_last_error()
     print(f"kernarg segment at {addr.value:#x}, device memory: {dev.value}")
-    assert addr.value != 0 and dev.value != 1
+    assert addr.value != 0 and dev.value in (-1, 0, 1)
