@@ -194,7 +194,7 @@ __device__ __forceinline__ void set_job(const BulkParams& p, Cursor& cur, const 
   const bool bad = cur.n > 64 || cur.b > cur.n || (cur.kind == SRC_RING && cur.src >= p.nrep) ||
                    (cur.kind == SRC_SLAB && (cur.src >= p.nslab || cur.g >= (WIRE ? p.nrep : p.G))) ||
                    cur.kind > SRC_WIRE_PROP ||
-                   (cur.kind == SRC_WIRE && (!WIRE || cur.n > cur.src ||
+                   (cur.kind == SRC_WIRE && (!p.wire_mode || cur.n > cur.src ||
                                              cur.sm + (16ull + p.P) * cur.src > p.wire_bytes));
   if (bad) {
 #ifdef RG_BOUNDS
