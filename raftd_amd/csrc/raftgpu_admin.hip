@@ -59,11 +59,14 @@ __global__ void gather_msgs_kernel(AdminParams a, uint32_t rid, uint32_t dst, ui
   if (k == 0) *out_cnt = cnt;
   if (k >= cnt || k >= t.K) return;
   const uint64_t* h = t.hdr_in + (((uint64_t)s * t.R + dst) * t.K + k) * t.G + g;
-  for (int w = 0; w < 8; ++w) out_hdr[k * 8 + w] = h[w * plane];
   const uint64_t* mt = t.mt_in + ((((uint64_t)s * t.R + dst) * t.K + k) * t.E) * t.G + g;
   const uint32_t type = (uint32_t)(h[0] & 0xFF), n = (uint32_t)(h[0] >> 32);
+  // a uniform Replicate (RG_UNIFORM in word 7) is shown expanded, as the message it encodes
+  const bool uni = type == M_REPLICATE && ((uint32_t)h[7 * plane] & RG_UNIFORM);
+  for (int w = 0; w < 8; ++w) out_hdr[k * 8 + w] = h[w * plane] & (w == 7 && uni ? ~(uint64_t)RG_UNIFORM : ~0ull);
   for (uint32_t e = 0; e < t.E; ++e)
-    out_terms[(uint64_t)k * t.E + e] = (type == M_REPLICATE && e < n) ? (mt[(uint64_t)e * t.G] & TERM_MASK) : 0;
+    out_terms[(uint64_t)k * t.E + e] =
+        (type == M_REPLICATE && e < n) ? (mt[uni ? 0 : (uint64_t)e * t.G] & TERM_MASK) : 0;
 }
 
 hipError_t launch_gather_msgs(const AdminParams& a, uint32_t rid, uint32_t dst, void* out_hdr, uint64_t* out_terms,
@@ -169,7 +172,8 @@ __global__ void deliver_kernel(AdminParams a, uint32_t rid, const rg_msg_view* m
   uint64_t* h = ((uint64_t*)(t.hdr_in)) + (((uint64_t)s * t.R + dst) * t.K + k) * t.G + g;
   const uint64_t* src = reinterpret_cast<const uint64_t*>(m);
   for (int w = 0; w < 8; ++w) h[w * plane] = src[w];
-  if (m->type == M_REPLICATE) {
+  if (m->type == M_REPLICATE) {  // every inline word written below: never a uniform Replicate
+    h[7 * plane] = src[7] & ~(uint64_t)RG_UNIFORM;
     uint64_t* mt = ((uint64_t*)(t.mt_in)) + ((((uint64_t)s * t.R + dst) * t.K + k) * t.E) * t.G + g;
     for (uint32_t e = 0; e < m->nent; ++e) mt[(uint64_t)e * t.G] = t.tr[((m->log_index + 1 + e) & (t.L - 1)) * t.nrep + q];
   }

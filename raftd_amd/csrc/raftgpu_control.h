@@ -7,12 +7,25 @@
 
 #include <type_traits>
 
-// Measurement variants of the control step, off in the product until the intermittent GPU fault
-// is closed (DESIGN.md §3 "The control-kernel fault"; the same code replays clean on the CPU
-// under ASan, UBSan and MSan):
-//   RG_CTL_FASTREP   a leader builds the Replicate of its own same-step append from registers
+// Fast paths of the control step (on; RG_CTL_SLOW turns all three off for A/B runs):
+//   RG_CTL_FASTREP   a leader builds the Replicate of its own same-step append from registers and
+//                    sends it as a uniform Replicate (one inline word for all n entries, below)
 //   RG_CTL_FRESH     write_entries' fresh-index path (pointer-stepped ring slots, no hull)
 //   RG_CTL_HDRBATCH  handle() loads all eight header words of a message up front
+// Uniform Replicate: header word 7 = RG_UNIFORM marks a local Replicate whose n entries all carry
+// the ring word mt[0] (only mt[0] is written). Remote Replicates never carry it: unpack_kernel
+// replaces word 7 with the records' offset, and pack_kernel expands the word into n records.
+#ifndef RG_CTL_SLOW
+#ifndef RG_CTL_FASTREP
+#define RG_CTL_FASTREP
+#endif
+#ifndef RG_CTL_FRESH
+#define RG_CTL_FRESH
+#endif
+#ifndef RG_CTL_HDRBATCH
+#define RG_CTL_HDRBATCH
+#endif
+#endif
 
 // entries per load batch in the control kernel's term copies (write_entries, send_replicate)
 #ifndef RG_CTL_BATCH
@@ -484,8 +497,8 @@ struct Ctl {
     }
     const uint32_t n = next <= last ? (uint32_t)umin64(p.E, last - next + 1) : 0;
 #ifdef RG_CTL_FASTREP  // the whole message lies in this step's plain append (the steady-state case)
-    // (at R = 8 the three extra live registers push the lane past 512 and into scratch: off there)
-    const bool fast = R <= 7 && n > 0 && la_n > 0 && next >= la_base && next + n <= la_base + la_n;
+    // (at R >= 7 the three extra live registers push the lane past 512 and into scratch: off there)
+    const bool fast = R <= 6 && n > 0 && la_n > 0 && next >= la_base && next + n <= la_base + la_n;
     const uint64_t lt = !fast ? term_at(next - 1) : next == la_base ? la_pt : la_word & TERM_MASK;
 #else
     const uint64_t lt = term_at(next - 1);
@@ -494,12 +507,17 @@ struct Ctl {
       if (st == REPLICATE) RG_SET(rn, to, next + n);
       else if (st == RETRY) RG_SET(rt, to, (uint32_t)WAIT);
     }
-    const int k = send(M_REPLICATE, to + 1, 0, 0, n, lt, next - 1, committed, 0, 0, 0, 0);
+#ifdef RG_CTL_FASTREP
+    const uint32_t uni = fast ? RG_UNIFORM : 0u;
+#else
+    const uint32_t uni = 0;
+#endif
+    const int k = send(M_REPLICATE, to + 1, 0, 0, n, lt, next - 1, committed, 0, 0, uni, 0);
     if (k >= 0 && n > 0) {
       uint64_t* mt = p.mt_out + ((((uint64_t)s * R + to) * p.K + (uint32_t)k) * p.E) * p.G + g;
 #ifdef RG_CTL_FASTREP
       if (fast) {
-        for (uint32_t e = 0; e < n; ++e) mt[(uint64_t)e * p.G] = la_word;
+        mt[0] = la_word;  // uniform: one word for every entry
       } else
 #endif
       for (uint32_t e = 0; e < n; e += CB) {  // term|type|pay|bank; batched as in write_entries
@@ -539,9 +557,12 @@ struct Ctl {
     const uint32_t n = (uint32_t)(w0 >> 32);
     if (term_at(li) == log_term) {
       const uint64_t* mt = (remote ? p.rmt : p.mt_in) + ((((uint64_t)src * R + s) * p.K + k) * p.E) * p.G + g;
+      // a uniform Replicate (local only): every entry carries the word mt[0]
+      const bool uni = !remote && ((uint32_t)wofs & RG_UNIFORM) && n > 0;
+      const uint64_t uw = uni ? mt[0] : 0ull;
       uint32_t k0 = n;
       for (uint32_t e = 0; e < n; ++e) {  // entryLog.getConflictIndex
-        if (term_at(li + 1 + e) != (mt[(uint64_t)e * p.G] & TERM_MASK)) {
+        if (term_at(li + 1 + e) != ((uni ? uw : mt[(uint64_t)e * p.G]) & TERM_MASK)) {
           k0 = e;
           break;
         }
@@ -557,6 +578,7 @@ struct Ctl {
           err |= ERR_CONFLICT;
         } else {
           if (remote) write_entries(li + 1, k0, n, SRC_WIRE, n, mt, 0, wofs);
+          else if (uni) write_entries(li + 1, k0, n, SRC_RING, src * p.G + g, nullptr, uw);
           else write_entries(li + 1, k0, n, SRC_RING, src * p.G + g, mt, 0);
           last = last_new;
         }
@@ -893,8 +915,7 @@ struct Ctl {
           leader = from;
         }
         if (type == M_REPLICATE) {
-          handle_replicate(w0, hw(2), hw(3), hw(4), from, src, k, remote,
-                           remote ? hw(7) : 0);
+          handle_replicate(w0, hw(2), hw(3), hw(4), from, src, k, remote, hw(7));  // local: RG_UNIFORM
         } else if (type == M_HEARTBEAT) {
           commit_to(hw(4));
           send_simple(M_HEARTBEAT_RESP, from, 0, 0, hw(5), hw(6));

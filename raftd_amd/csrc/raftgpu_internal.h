@@ -39,6 +39,8 @@ enum : uint32_t {
 // read traffic): the leader's pending request and the read made ready in a step
 enum : uint32_t { RI_CTX, RI_INDEX, RI_ACKS /* acks | requester slot << 32 */, RD_CTX, RD_INDEX, RD_TICK, RD_ROWS };
 enum : uint32_t { FOLLOWER = 0, CANDIDATE = 1, LEADER = 2 };
+// header word 7 of a local Replicate: its n entries all carry the inline word mt[0] (raftgpu_control.h)
+constexpr uint32_t RG_UNIFORM = 1;
 enum : uint32_t { RETRY = 0, WAIT = 1, REPLICATE = 2, SNAPSHOT = 3 };
 enum : uint32_t { ENTRY_APP = 0, ENTRY_CONFIG = 1 };
 enum : uint32_t { ERR_CONFLICT = 1, ERR_BEYOND = 2, ERR_RING = 4, ERR_CRC = 8, ERR_EMPTY_SNAP = 16, ERR_WIRE = 32 };

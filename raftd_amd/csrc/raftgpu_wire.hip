@@ -178,6 +178,8 @@ __global__ void __launch_bounds__(256) pack_kernel(WireParams w) {
     if (lane < 8) reinterpret_cast<uint64_t*>(out)[lane] = hv;
     const uint64_t w0 = rl64(hv, 0), li = rl64(hv, 3), w7 = rl64(hv, 7);
     const bool prop = (w0 & 0xFF) == M_PROPOSE;
+    // a uniform Replicate: one inline word for every entry; expanded into n records on the wire
+    const uint64_t est = (w0 & 0xFF) == M_REPLICATE && ((uint32_t)w7 & RG_UNIFORM) ? 0ull : (uint64_t)w.G;
     uint32_t n = wire_entries(w0, P);
     if (n > w.E) {  // plan_kernel sized the region with the same n: only reachable on corrupt state
       RG_OOB("RG_BOUNDS pack u=%u k=%u n=%u > E\n", u, k, n);
@@ -194,7 +196,7 @@ __global__ void __launch_bounds__(256) pack_kernel(WireParams w) {
         const uint64_t word = len_bits(slab_ok ? min(w.slab_info[se0 + lane].y, P) : 0u);
         rec = u32x4{(uint32_t)word, (uint32_t)(word >> 32), 0u, 0u};
       } else {
-        const uint64_t word = mtp[(uint64_t)lane * w.G];
+        const uint64_t word = mtp[(uint64_t)lane * est];
         const uint64_t slot = (li + 1 + lane) & (w.L - 1);
         const uint32_t crc = (word & PAY_BIT) ? w.info[((word >> 63) * n64 + qs) * w.L + slot].x : 0u;
         rec = u32x4{(uint32_t)word, (uint32_t)(word >> 32), crc, 0u};
@@ -210,7 +212,7 @@ __global__ void __launch_bounds__(256) pack_kernel(WireParams w) {
         if (prop) {
           if (slab_ok && w.slab_info[se0 + e].y) src = w.slabs + (se0 + e) * P;
         } else {
-          const uint64_t word = mtp[(uint64_t)e * w.G];
+          const uint64_t word = mtp[(uint64_t)e * est];
           if (word & PAY_BIT) src = w.pay + (((word >> 63) * n64 + qs) * w.L + ((li + 1 + e) & (w.L - 1))) * P;
         }
         if (src) {

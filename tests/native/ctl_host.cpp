@@ -242,11 +242,14 @@ int ch_read_msgs(void* hh, uint32_t rid, uint32_t dst, rg_msg_view* out, uint32_
     const uint64_t* hp = t.hdr_in + (((uint64_t)s * t.R + dst) * t.K + k) * t.G + g;
     uint64_t w[8];
     for (int i = 0; i < 8; ++i) w[i] = hp[i * plane];
+    const bool uni = (w[0] & 0xFF) == M_REPLICATE && ((uint32_t)w[7] & RG_UNIFORM);  // shown expanded
+    if (uni) w[7] &= ~(uint64_t)RG_UNIFORM;
     memcpy(&out[k], w, 64);
     const uint64_t* mt = t.mt_in + ((((uint64_t)s * t.R + dst) * t.K + k) * t.E) * t.G + g;
     const uint32_t n = (uint32_t)(w[0] >> 32);
     for (uint32_t e = 0; e < t.E; ++e)
-      terms[(uint64_t)k * t.E + e] = ((w[0] & 0xFF) == M_REPLICATE && e < n) ? (mt[(uint64_t)e * t.G] & TERM_MASK) : 0;
+      terms[(uint64_t)k * t.E + e] =
+          ((w[0] & 0xFF) == M_REPLICATE && e < n) ? (mt[uni ? 0 : (uint64_t)e * t.G] & TERM_MASK) : 0;
   }
   return (int)cnt;
 }
