@@ -64,6 +64,9 @@ def parse():
                     "itself in a one-rank process group): a rehearsal of the multi-GPU step on one GPU")
     ap.add_argument("--halves", type=int, default=2, help="N > 1 spread: engines per rank over disjoint column "
                     "ranges; 2 pipelines one half's all-to-all behind the other half's tick (1 = no overlap)")
+    ap.add_argument("--exchange", choices=["torch", "c"], default="torch", help="N > 1 spread: move the regions "
+                    "with torch.distributed from Python (default) or with the library's rg_wire_exchange (built-in "
+                    "RCCL transport on nccl; each half on its own stream)")
     ap.add_argument("--backend", default="nccl", help="N > 1: nccl (RCCL, default) or gloo (rehearsal: several "
                     "ranks on one GPU with RAFTD_BENCH_DEVICE=0, regions staged through host memory)")
     return ap.parse_args()
@@ -278,7 +281,8 @@ def main():
     common = dict(replicas=R, log_capacity=args.log_capacity, payload_bytes=P, max_entries_per_msg=E, device=local)
     wire = None
     if spread:  # one cluster of world x G groups, replicas spread over the GPUs
-        wire = DistEngine(groups=G, halves=args.halves, seed=0x5EED, wire_all=1 if rehearse else 0, **common)
+        wire = DistEngine(groups=G, halves=args.halves, seed=0x5EED, wire_all=1 if rehearse else 0,
+                          exchange=args.exchange, **common)
         host, eng = wire, wire.eng  # host: aggregates over the halves; eng: the first half
         Gt = G * world
     else:  # an independent engine per GPU (its own G groups)
@@ -451,6 +455,8 @@ def main():
             "mode": (f"pipelined over {args.halves} column halves: one half's all-to-all overlaps the other's "
                      "unpack + tick + pack" if pipelined else "serial: plan + pack + all-to-all + unpack, then tick"),
             "ms_per_step": x_ms if not pipelined else None,
+            "transport": ("rg_wire_exchange (C-ABI, built-in RCCL transport)" if spread and args.exchange == "c"
+                          else "torch.distributed all_to_all_single" if spread else "device copy (one engine)"),
             "bytes_sent_per_step_max_rank": wire_max / K,
             "achieved_GBps_per_rank": ((wire_max / K) / (x_ms / 1e3) / 1e9 if x_ms > 0 else
                                        (wire_max / K) / (wall / K) / 1e9),

@@ -310,6 +310,34 @@ int rg_last_tick_traffic(rg_engine* e, rg_traffic* out);
 int rg_wire_plan(rg_engine* e, uint64_t* send_bytes /*[ranks]*/);
 int rg_wire_pack(rg_engine* e, void* send_buf, uint64_t send_cap);
 int rg_wire_recv(rg_engine* e, const void* recv_buf, const uint64_t* recv_bytes /*[ranks]*/);
+/* The whole exchange in one call: rg_wire_plan, the region sizes through t->allgather_u64, pack
+ * into an engine-owned send buffer, t->alltoallv into an engine-owned receive buffer, and
+ * rg_wire_recv. Every rank of the cluster calls it between the same two ticks. A host in any
+ * language gets multi-GPU replication from this call plus a transport: the built-in RCCL one
+ * (rg_rccl_open) or its own.
+ * *sent_bytes (if not NULL) = the bytes this rank sent to other ranks. The transport's callbacks return 0 on success. alltoallv gets device buffers and the engine's
+ * HIP stream. Its transfers must come after the work already on `stream` (the pack), and the
+ * work enqueued on `stream` after it returns (the unpack) must come after its transfers. It can
+ * enqueue on `stream` itself, order a stream of its own by events both ways (the RCCL transport),
+ * or synchronise `stream` and complete before returning (a host-staged transport). Region r of `send`
+ * (send + soff[r], ssize[r] bytes) goes to rank r; region r of `recv`
+ * (recv + roff[r], rsize[r] bytes) comes from rank r. allgather_u64 is a host-memory, blocking
+ * all-gather of n values per rank: all[r * n + i] = value i of rank r. */
+typedef struct rg_transport {
+  void* user;
+  int (*allgather_u64)(void* user, const uint64_t* mine, uint64_t* all, uint32_t n);
+  int (*alltoallv)(void* user, const void* send, const uint64_t* soff, const uint64_t* ssize, void* recv,
+                   const uint64_t* roff, const uint64_t* rsize, void* stream);
+} rg_transport;
+int rg_wire_exchange(rg_engine* e, const rg_transport* t, uint64_t* sent_bytes /* nullable: bytes to other ranks */);
+/* Built-in RCCL transport (librccl loaded at run time; the one a PyTorch process already holds
+ * is reused). Rank 0 calls rg_rccl_unique_id and hands the 128 bytes to every rank out of band
+ * (raftd: over its own control channel); each rank then calls rg_rccl_open with its device.
+ * Each peer region moves in pieces of at most 256 MiB ("The 1 GiB contract").
+ * rg_rccl_close destroys the communicator. */
+int rg_rccl_unique_id(uint8_t id[128]);
+int rg_rccl_open(const uint8_t id[128], int32_t nranks, int32_t rank, int32_t device, rg_transport* out);
+int rg_rccl_close(rg_transport* t);
 /* Committed-entry copy-back: the non-empty application entries that the
  * replicas whose slot bit is set in slot_mask applied in the last tick — config changes, leader
  * no-ops and snapshot-restored ranges excluded, as dragonboat's rsm does before Update — grouped

@@ -11,7 +11,8 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libraftgpu.so")
 RESOURCES = os.path.join(PKG, "kernel_resources.txt")  # per-kernel VGPR / scratch / occupancy of the last build
-SOURCES = ["raftgpu_kernels.hip", "raftgpu_admin.hip", "raftgpu_wire.hip", "raftgpu_apply.hip", "raftgpu_engine.cpp"]
+SOURCES = ["raftgpu_kernels.hip", "raftgpu_admin.hip", "raftgpu_wire.hip", "raftgpu_apply.hip", "raftgpu_engine.cpp",
+           "raftgpu_rccl.cpp"]
 HEADERS = ["raftgpu_internal.h", "raftgpu_control.h", "raftgpu_wire.h", os.path.join("..", "..", "include", "raftgpu.h")]
 ARCH = os.environ.get("RAFTGPU_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -50,7 +51,7 @@ def build_engine(force: bool = False, verbose: bool = False) -> str:
         objs.append(obj)
     with open(RESOURCES, "w") as f:
         f.write("\n".join(report) + "\n")
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + ["-ldl"]
     subprocess.run(cmd, check=True)
     for o in objs:
         os.remove(o)

@@ -164,18 +164,60 @@ def exchange_sizes(send_sizes, group=None):
     return [m[a][me] for a in range(n)], max(max(row) for row in m)
 
 
+def _dev_bytes(ptr: int, n: int, device):
+    """A uint8 torch tensor over n bytes of device memory the engine owns (no copy)."""
+    torch = _torch()
+
+    class _Arr:
+        __cuda_array_interface__ = {"shape": (n,), "typestr": "|u1", "data": (ptr, False), "version": 3,
+                                    "strides": None}
+
+    return torch.as_tensor(_Arr(), device=device) if n else torch.empty(0, dtype=torch.uint8, device=device)
+
+
+def gloo_transport(pg, device):
+    """rg_transport over a gloo (or any host) process group, for rg_wire_exchange: sizes by
+    all_gather, regions staged through host memory by all_to_all_bytes. Synchronous: it waits
+    for the engine stream before reading and completes before returning (include/raftgpu.h)."""
+    import torch.distributed as dist
+    from .engine import PyTransport
+    torch = _torch()
+    n = dist.get_world_size(pg)
+
+    def allgather(vals):
+        t = torch.tensor(vals, dtype=torch.int64)
+        out = [torch.empty_like(t) for _ in range(n)]
+        dist.all_gather(out, t, group=pg)
+        return [int(v) for o in out for v in o.tolist()]
+
+    def alltoallv(send, soff, ssize, recv, roff, rsize, stream):
+        torch.cuda.synchronize(device)
+        st, rt = sum(ssize), sum(rsize)
+        sb, rb = _dev_bytes(send, st, device), _dev_bytes(recv, rt, device)
+        all_to_all_bytes(sb, list(ssize), rb, list(rsize), pg, nchunks=a2a_chunks(max(list(ssize) + list(rsize))))
+        torch.cuda.synchronize(device)
+
+    pt = PyTransport(allgather, alltoallv)
+    pt.nranks = n
+    return pt
+
+
 class _Half:
     """One engine of a rank and its exchange state. start() ships the last tick's cross-rank
     messages (plan, pack, size exchange, all-to-all — asynchronous on nccl); finish() waits for
-    them and unpacks before the engine's next tick."""
+    them and unpacks before the engine's next tick. With a C transport (exchange="c") start() is
+    one rg_wire_exchange call, ordered on the device, and finish() has nothing left to do."""
 
-    def __init__(self, eng, dev, pg, rank):
-        self.eng, self.pg, self.rank = eng, pg, rank
+    def __init__(self, eng, dev, pg, rank, xt=None):
+        self.eng, self.pg, self.rank, self.xt = eng, pg, rank, xt
         self.send, self.recv = _Buf(dev), _Buf(dev)
         self.work, self.rsizes, self.sent = None, None, 0
 
     def start(self, async_op):
         e = self.eng
+        if self.xt is not None:
+            self.sent = e.wire_exchange(self.xt)
+            return
         sizes = e.wire_plan()  # host sync: the tick that produced the messages has completed
         _, stot = _offsets(sizes)
         self.send.ensure(stot)
@@ -240,11 +282,16 @@ class DistEngine(_Feeds):
     tick that produced it. With two halves, step_device() pipelines: while one half's all-to-all
     is on the wire, the other half unpacks, ticks and packs."""
 
-    def __init__(self, groups: int, group=None, halves: int = 1, **cfg):
+    def __init__(self, groups: int, group=None, halves: int = 1, exchange: str = "torch", **cfg):
+        """exchange: "torch" moves the regions with torch.distributed from Python; "c" with the
+        library's rg_wire_exchange (RCCL transport on an nccl group, a host-staged one on gloo),
+        each half on a stream of its own so one half's transfer overlaps the other's tick."""
         import torch.distributed as dist
         torch = _torch()
         if groups % halves:
             raise ValueError("groups must be a multiple of halves")
+        if exchange not in ("torch", "c"):
+            raise ValueError("exchange is 'torch' or 'c'")
         self.pg = group
         self.N, self.rank = dist.get_world_size(group), dist.get_rank(group)
         hg = groups // halves
@@ -256,9 +303,22 @@ class DistEngine(_Feeds):
             self.stream = torch.cuda.Stream()
             torch.cuda.set_stream(self.stream)
         dev = torch.device("cuda", engs[0].cfg["device"])
-        for e in engs:
-            e.set_stream(self.stream.cuda_stream)
-        self.parts = [_Half(e, dev, self.pg, self.rank) for e in engs]
+        self.xchg, self.xt, self._xclose = exchange, None, None
+        self.streams = [self.stream] + ([torch.cuda.Stream(device=dev) for _ in engs[1:]] if exchange == "c"
+                                        else [self.stream] * (len(engs) - 1))
+        for e, st in zip(engs, self.streams):
+            e.set_stream(st.cuda_stream)
+        if exchange == "c":
+            from .engine import rccl_close, rccl_transport, rccl_unique_id
+            if dist.get_backend(group) == "nccl":
+                uid = [rccl_unique_id() if self.rank == 0 else None]
+                dist.broadcast_object_list(uid, src=0, group=group)
+                t = rccl_transport(uid[0], self.N, self.rank, engs[0].cfg["device"])
+                self.xt, self._xclose = t, (lambda: rccl_close(t))
+            else:
+                self._pyxt = gloo_transport(group, dev)
+                self.xt = self._pyxt.t
+        self.parts = [_Half(e, dev, self.pg, self.rank, self.xt) for e in engs]
         self.eng = engs[0]
         self.cfg, self.R = engs[0].cfg, engs[0].R
         self.async_ok = dist.get_backend(group) == "nccl"
@@ -371,12 +431,26 @@ class DistEngine(_Feeds):
             p.eng.bootstrap()
 
     def join(self):
-        for p in self.parts:
+        """torch's current stream waits (on the device) for every half's last tick."""
+        torch = _torch()
+        cur = torch.cuda.current_stream()
+        for p, st in zip(self.parts, self.streams):
             p.eng.join()
+            if st.cuda_stream != cur.cuda_stream:
+                ev = torch.cuda.Event()
+                ev.record(st)
+                cur.wait_event(ev)
 
     def sync(self):
         for p in self.parts:
             p.eng.sync()
+
+    def close(self):
+        """Release the RCCL communicator of exchange="c" (after the last exchange completed)."""
+        self.sync()
+        if self._xclose is not None:
+            self._xclose()
+            self._xclose, self.xt = None, None
 
     def timing(self, on=True, bulk_only=False):
         for p in self.parts:

@@ -150,6 +150,10 @@ struct rg_engine {
   bool planned = false, wire_ready = false;
   const uint8_t* recv = nullptr;  // receive buffer the next tick's SRC_WIRE jobs read
   uint64_t recv_bytes = 0;         // bytes of it in use (RG_BOUNDS checks)
+  // rg_wire_exchange's own buffers (grown on demand; stream order keeps one of each enough: the
+  // next exchange is enqueued after the tick that reads the receive buffer)
+  uint8_t *x_send = nullptr, *x_recv = nullptr;
+  uint64_t x_send_cap = 0, x_recv_cap = 0;
   // committed-entry copy-back (raftgpu_apply.hip)
   uint64_t* apply_lo = nullptr;
   uint32_t* acnt = nullptr;
@@ -1528,6 +1532,52 @@ int rg_last_tick_traffic(rg_engine* e, rg_traffic* out) {
                            (12 + P) * v[3] + P * v[4];
   out->bulk_bytes = (2 * P + 8) * v[3] - 4 * v[4];
   return RG_OK;
+}
+
+
+// One exchange between two ticks (include/raftgpu.h): plan, sizes, pack, transport, unpack.
+static int xgrow(rg_engine* e, uint8_t** buf, uint64_t* cap, uint64_t need) {
+  if (need <= *cap) return RG_OK;
+  if (*buf) {
+    HIPCHK(hipStreamSynchronize(e->stream));  // the last tick or transfer may still read it
+    (void)hipFree(*buf);
+    e->allocs.erase(std::remove(e->allocs.begin(), e->allocs.end(), (void*)*buf), e->allocs.end());
+    e->bytes -= *cap;
+    *buf = nullptr;
+    *cap = 0;
+  }
+  const uint64_t nb = ((need + need / 4) + 4095) & ~4095ull;  // 25 % headroom against regrowth
+  RGCHK(dalloc(e, buf, nb));
+  *cap = nb;
+  return RG_OK;
+}
+
+int rg_wire_exchange(rg_engine* e, const rg_transport* t, uint64_t* sent_bytes) {
+  if (!e || !t || !t->allgather_u64 || !t->alltoallv) return fail(RG_EINVAL, "rg_wire_exchange args");
+  if (sent_bytes) *sent_bytes = 0;
+  if (!e->wire) return RG_OK;
+  const uint32_t N = e->pl.N, me = e->pl.rank;
+  std::vector<uint64_t> ssize(N), soff(N), all((uint64_t)N * N), rsize(N), roff(N);
+  RGCHK(rg_wire_plan(e, ssize.data()));
+  if (t->allgather_u64(t->user, ssize.data(), all.data(), N) != 0)
+    return fail(RG_EHIP, "rg_wire_exchange: transport allgather_u64 failed");
+  uint64_t st = 0, rt = 0;
+  for (uint32_t r = 0; r < N; ++r) {
+    if (all[(uint64_t)me * N + r] != ssize[r]) return fail(RG_EINVAL, "rg_wire_exchange: allgather returned another rank's sizes");
+    soff[r] = st;
+    st += ssize[r];
+    rsize[r] = all[(uint64_t)r * N + me];
+    roff[r] = rt;
+    rt += rsize[r];
+  }
+  RGCHK(xgrow(e, &e->x_send, &e->x_send_cap, std::max<uint64_t>(st, 256)));
+  RGCHK(xgrow(e, &e->x_recv, &e->x_recv_cap, std::max<uint64_t>(rt, 256)));
+  RGCHK(rg_wire_pack(e, e->x_send, e->x_send_cap));
+  if (t->alltoallv(t->user, e->x_send, soff.data(), ssize.data(), e->x_recv, roff.data(), rsize.data(),
+                   (void*)e->stream) != 0)
+    return fail(RG_EHIP, "rg_wire_exchange: transport alltoallv failed");
+  if (sent_bytes) *sent_bytes = st - ssize[me];
+  return rg_wire_recv(e, e->x_recv, rsize.data());
 }
 
 }  // extern "C"

@@ -119,6 +119,16 @@ class ReadRequest(C.Structure):
 READ_READY_DTYPE = np.dtype([("group", "<u8"), ("replica_id", "<u4"), ("rid", "<u4"), ("ctx", "<u8"), ("index", "<u8")])
 
 
+_ALLGATHER = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_uint32)
+_ALLTOALLV = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_void_p,
+                         C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_void_p)
+
+
+class Transport(C.Structure):
+    """rg_transport (include/raftgpu.h): what rg_wire_exchange moves the regions with."""
+    _fields_ = [("user", C.c_void_p), ("allgather_u64", _ALLGATHER), ("alltoallv", _ALLTOALLV)]
+
+
 class TickInput(C.Structure):
     _fields_ = [("prop_target", C.c_void_p), ("prop_count", C.c_void_p), ("campaign", C.c_void_p),
                 ("isolate", C.c_void_p), ("flags", C.c_uint32), ("_pad", C.c_uint32)]
@@ -145,7 +155,7 @@ EXPORTS = ["rg_create", "rg_destroy", "rg_bootstrap", "rg_fill_slabs", "rg_tick"
            "rg_timing", "rg_kernel_ms", "rg_wire_plan", "rg_wire_pack", "rg_wire_recv", "rg_global_id",
            "rg_apply_committed", "rg_probe_copy", "rg_persist_collect", "rg_snapshot_events", "rg_propose",
            "rg_notify_applied", "rg_apply_async", "rg_apply_wait", "rg_read_index", "rg_read_index_results",
-           "rg_config_change"]
+           "rg_config_change", "rg_wire_exchange", "rg_rccl_unique_id", "rg_rccl_open", "rg_rccl_close"]
 
 _lib = None
 
@@ -202,6 +212,10 @@ def load_library(path: str = LIB_PATH):
         "rg_wire_plan": ([vp, C.POINTER(C.c_uint64)], i32),
         "rg_wire_pack": ([vp, vp, u64], i32),
         "rg_wire_recv": ([vp, vp, C.POINTER(C.c_uint64)], i32),
+        "rg_wire_exchange": ([vp, C.POINTER(Transport), C.POINTER(C.c_uint64)], i32),
+        "rg_rccl_unique_id": ([C.c_char_p], i32),
+        "rg_rccl_open": ([C.c_char_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(Transport)], i32),
+        "rg_rccl_close": ([C.POINTER(Transport)], i32),
         "rg_global_id": ([vp, u32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)], i32),
         "rg_apply_committed": ([vp, u32, vp, vp, u64, C.POINTER(C.c_uint64)], i32),
         "rg_probe_copy": ([C.c_int32, u64, C.c_int32, C.POINTER(C.c_double)], i32),
@@ -477,6 +491,14 @@ class Engine:
         rb = (C.c_uint64 * self.ranks)(*recv_bytes)
         self._check(self.L.rg_wire_recv(self.h, C.c_void_p(recv_ptr or None), rb))
 
+    def wire_exchange(self, transport: "Transport") -> int:
+        """rg_wire_exchange: plan, sizes, pack, transport, unpack in one call (the C-ABI path a
+        non-Python host uses; transport = rccl_transport(...) or PyTransport(...).t). Returns the
+        bytes sent to other ranks."""
+        sent = C.c_uint64()
+        self._check(self.L.rg_wire_exchange(self.h, C.byref(transport), C.byref(sent)))
+        return sent.value
+
     def apply_committed(self, slot_mask: int = 0xFF, cap: int = None):
         """Committed-entry copy-back of the last tick (rg_apply_committed): a structured array
         (APPLY_DTYPE: index, group, replica_id, len, crc, rid) and the payloads, one row of
@@ -548,3 +570,58 @@ class Engine:
         t = Traffic()
         self._check(self.L.rg_last_tick_traffic(self.h, C.byref(t)))
         return {f: getattr(t, f) for f, _ in Traffic._fields_}
+
+
+def rccl_unique_id() -> bytes:
+    """rg_rccl_unique_id: 128 bytes rank 0 creates and hands to every rank out of band."""
+    L = load_library()
+    buf = C.create_string_buffer(128)
+    if L.rg_rccl_unique_id(buf) != 0:
+        raise RgError(-4, "rg_rccl_unique_id: librccl unavailable")
+    return buf.raw
+
+
+def rccl_transport(uid: bytes, nranks: int, rank: int, device: int = 0) -> Transport:
+    """The library's built-in RCCL transport (rg_rccl_open); close with rccl_close(t)."""
+    L = load_library()
+    t = Transport()
+    rc = L.rg_rccl_open(C.create_string_buffer(bytes(uid), 128), nranks, rank, device, C.byref(t))
+    if rc != 0:
+        raise RgError(rc, "rg_rccl_open failed")
+    return t
+
+
+def rccl_close(t: Transport):
+    load_library().rg_rccl_close(C.byref(t))
+
+
+class PyTransport:
+    """An rg_transport whose callbacks are Python: allgather(list of n ints) -> list of ranks*n
+    ints; alltoallv(send_ptr, soff, ssize, recv_ptr, roff, rsize, stream) moves device regions and
+    must respect the ordering rule of include/raftgpu.h. Exceptions become a failed call."""
+
+    def __init__(self, allgather, alltoallv):
+        def ag(_user, mine, all_, n):
+            try:
+                vals = allgather([mine[i] for i in range(n)])
+                for i, v in enumerate(vals):
+                    all_[i] = v
+                return 0
+            except Exception as exc:  # noqa: BLE001 - reported through the C return code
+                self.error = exc
+                return -1
+
+        def a2a(_user, send, soff, ssize, recv, roff, rsize, stream):
+            try:
+                k = self.nranks
+                alltoallv(send or 0, [soff[i] for i in range(k)], [ssize[i] for i in range(k)], recv or 0,
+                          [roff[i] for i in range(k)], [rsize[i] for i in range(k)], stream or 0)
+                return 0
+            except Exception as exc:  # noqa: BLE001
+                self.error = exc
+                return -1
+
+        self.error = None
+        self.nranks = 0
+        self._cb = (_ALLGATHER(ag), _ALLTOALLV(a2a))  # keep the trampolines alive
+        self.t = Transport(None, self._cb[0], self._cb[1])

@@ -1,11 +1,15 @@
 """Worker of test_gpu_cluster's two-process tests: N processes (one rank each, gloo) step a
 DistEngine (1 or 2 column halves) on the same GPU — chaos ticks through tick(), then steady
 proposal ticks through the pipelined step_device() when there are two halves; rank 0 compares
-every replica with the C oracle of all shards. usage: python dist_worker.py N [halves [backend]]
+every replica with the C oracle of all shards.
+usage: python dist_worker.py N [halves [backend [exchange]]]   (exchange: torch | c)
 
 backend nccl (N = 1 only: RCCL will not put two ranks on one GPU): the one rank sends every
 message through the wire (wire_all), so each exchange is a real RCCL all_to_all_single — the
-asynchronous one with its work-handle wait in the pipelined steps."""
+asynchronous one with its work-handle wait in the pipelined steps.
+
+exchange c: the library's rg_wire_exchange moves the regions (the C-ABI path a Go host uses):
+through its built-in RCCL transport on nccl, through a host-staged Python transport on gloo."""
 import os
 import sys
 
@@ -43,7 +47,7 @@ def snapshot(de):
     return mine
 
 
-def worker(rank, n, halves, backend):
+def worker(rank, n, halves, backend, exchange="torch"):
     if backend == "nccl":
         torch.cuda.set_device(0)
         dist.init_process_group("nccl", rank=rank, world_size=n, device_id=torch.device("cuda", 0))
@@ -51,7 +55,7 @@ def worker(rank, n, halves, backend):
         dist.init_process_group("gloo", rank=rank, world_size=n)
     from raftd_amd.cluster import DistEngine
     extra = dict(wire_all=1) if n == 1 else {}
-    de = DistEngine(groups=G_LOCAL * halves, halves=halves, device=0, **CFG, **extra)
+    de = DistEngine(groups=G_LOCAL * halves, halves=halves, device=0, exchange=exchange, **CFG, **extra)
     if backend == "nccl":
         assert de.async_ok
     de.bootstrap()
@@ -110,6 +114,7 @@ def worker(rank, n, halves, backend):
                 ora.tick(np.zeros(G, np.uint8), np.full(G, 5, np.uint32))
             check(ora, steady, G, "steady")
         print("dist parity ok", flush=True)
+    de.close()
     dist.barrier()
     dist.destroy_process_group()
 
@@ -128,4 +133,5 @@ if __name__ == "__main__":
     n = int(sys.argv[1])
     halves = int(sys.argv[2]) if len(sys.argv) > 2 else 1
     backend = sys.argv[3] if len(sys.argv) > 3 else "gloo"
-    mp.spawn(worker, args=(n, halves, backend), nprocs=n, join=True)
+    exchange = sys.argv[4] if len(sys.argv) > 4 else "torch"
+    mp.spawn(worker, args=(n, halves, backend, exchange), nprocs=n, join=True)

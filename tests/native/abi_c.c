@@ -12,6 +12,9 @@
  *   rg_config_change                    SyncRequestDeleteReplica / SyncRequestAddReplica (:165-185)
  *   rg_leader / rg_read_replicas        GetLeaderID / SyncGetShardMembership (raft/members.go:21,30)
  *   rg_destroy                          NodeHost.Close (raft_manager.go:159)
+ *   rg_wire_exchange + rg_rccl_*        (argument "rccl") every message through the wire and the
+ *                                       library's RCCL transport at world size 1: the multi-GPU
+ *                                       replication path of a non-Python host
  *
  * Checks: every proposed Cmd reaches Update exactly once per replica, in proposal order, byte for
  * byte, with its zlib CRC-32 — including a follower removed from the membership for six ticks and
@@ -57,7 +60,24 @@ static uint32_t make_cmd(uint32_t g, uint32_t t, uint32_t k, uint8_t* out) {
   return len;
 }
 
-int main(void) {
+static rg_transport xt;
+static int use_wire = 0;
+static int ticks = 0;
+
+/* the NodeHost tick: with the wire, the last tick's messages are exchanged first */
+static int tick(rg_engine* e, const rg_tick_input* in) {
+  if (use_wire && ticks > 0) {
+    uint64_t sent = 0;
+    int rc = rg_wire_exchange(e, &xt, &sent);
+    if (rc < 0) return rc;
+    if (sent != 0) return RG_EINVAL; /* one rank: its only region is its own */
+  }
+  ++ticks;
+  return rg_tick(e, in);
+}
+
+int main(int argc, char** argv) {
+  use_wire = argc > 1 && strcmp(argv[1], "rccl") == 0;
   rg_config c;
   memset(&c, 0, sizeof c);
   c.groups = G; c.replicas = R; c.log_capacity = 1024; c.payload_bytes = 256;
@@ -65,6 +85,12 @@ int main(void) {
   c.election_rtt = 10; c.heartbeat_rtt = 1; c.check_quorum = 1; /* raftd's config (raft_manager.go:92-100) */
   c.snapshot_entries = 1000; c.compaction_overhead = 5; c.seed = 0x5EED; c.ranks = 1;
   c.apply_feedback = 1;
+  c.wire_all = (uint32_t)use_wire;
+  if (use_wire) {
+    uint8_t uid[128];
+    CHECK(rg_rccl_unique_id(uid));
+    CHECK(rg_rccl_open(uid, 1, 0, 0, &xt));
+  }
   rg_engine* e = NULL;
   CHECK(rg_create(&c, &e));
   CHECK(rg_bootstrap(e));
@@ -80,7 +106,7 @@ int main(void) {
   memset(campaign, 0, sizeof campaign);
   rg_tick_input in;
   memset(&in, 0, sizeof in);
-  CHECK(rg_tick(e, &in));
+  CHECK(tick(e, &in));
   for (uint32_t g = 0; g < G; ++g) campaign[g * R + (g % R)] = 1;  /* leaders spread over the slots */
   in.campaign = campaign;
   /* every replica reports the bootstrap entries applied (the rsm applies config changes itself) */
@@ -88,9 +114,9 @@ int main(void) {
   uint64_t idx[G * R];
   for (uint32_t r = 0; r < G * R; ++r) { rids[r] = r; idx[r] = R; }
   CHECK(rg_notify_applied(e, rids, idx, G * R));
-  CHECK(rg_tick(e, &in));
+  CHECK(tick(e, &in));
   in.campaign = NULL;
-  for (int t = 0; t < 6; ++t) CHECK(rg_tick(e, &in));
+  for (int t = 0; t < 6; ++t) CHECK(tick(e, &in));
 
   /* C-owned buffers for the copy-back and the WAL feed */
   const uint64_t cap = 1u << 16;
@@ -145,7 +171,7 @@ int main(void) {
         want_n[g]++;
         off += n;
       }
-    CHECK(rg_tick(e, &in));
+    CHECK(tick(e, &in));
     uint64_t ns = 0, ne = 0, na = 0;
     CHECK(rg_persist_collect(e, 0, ps, cap, &ns, pe, ppay, cap, &ne)); /* the shim fsyncs these */
     CHECK(rg_apply_committed(e, 0xFF, ents, pay, cap, &na));
@@ -166,7 +192,7 @@ int main(void) {
   }
   for (int t = 0; t < 16; ++t) { /* drain: the last Cmds commit everywhere, the re-added follower catches up */
     uint64_t na = 0;
-    CHECK(rg_tick(e, &in));
+    CHECK(tick(e, &in));
     CHECK(rg_apply_committed(e, 0xFF, ents, pay, cap, &na));
     for (uint64_t i = 0; i < na; ++i) {
       got_crc[ents[i].rid] = (uint32_t)crc32(got_crc[ents[i].rid], pay + i * c.payload_bytes, ents[i].len);
@@ -194,9 +220,10 @@ int main(void) {
     }
     EXPECT(leaders == 1);
   }
-  printf("ABI_C OK: %u shards x %u replicas, %llu Cmds per shard applied on every replica, device %.1f MB\n", G, R,
-         (unsigned long long)want_n[0], rg_device_bytes(e) / 1e6);
+  printf("ABI_C OK%s: %u shards x %u replicas, %llu Cmds per shard applied on every replica, device %.1f MB\n",
+         use_wire ? " (wire + RCCL exchange)" : "", G, R, (unsigned long long)want_n[0], rg_device_bytes(e) / 1e6);
   rg_destroy(e);
+  if (use_wire) CHECK(rg_rccl_close(&xt));
   free(ents); free(pay); free(ps); free(pe); free(ppay); free(blob);
   return 0;
 }

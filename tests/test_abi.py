@@ -85,6 +85,17 @@ def test_c_harness_runs_the_cgo_call_sequence():
 
 
 @pytest.mark.gpu
+def test_c_harness_wire_through_rccl_exchange():
+    """The same call sequence with every message through the wire and rg_wire_exchange over the
+    library's RCCL transport (rg_rccl_unique_id / rg_rccl_open at world size 1): a C host's
+    multi-GPU replication path, end to end, with no Python in the process."""
+    import subprocess
+    exe = build_c_harness()
+    out = subprocess.run([exe, "rccl"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and "ABI_C OK (wire + RCCL exchange)" in out.stdout, out.stdout + out.stderr
+
+
+@pytest.mark.gpu
 def test_kernarg_probe_reports_placement():
     """DESIGN.md §3 "The control-kernel fault": this runtime places kernel arguments in device memory
     whatever HIP_FORCE_DEV_KERNARG says (measured r02), which is why control_kernel takes its

@@ -243,3 +243,51 @@ def test_malformed_exchange_data_is_dropped():
         lasts = {int(views[g * R + s]["last"]) for s in range(R)}
         commits = {int(views[g * R + s]["committed"]) for s in range(R)}
         assert len(lasts) == 1 and len(commits) == 1, (g, lasts, commits)
+
+
+def _worker(args, port):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    out = subprocess.run([sys.executable, "-u", os.path.join(HERE, "dist_worker.py")] + args, env=env,
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert "dist parity ok" in out.stdout
+
+
+def test_two_processes_gloo_c_exchange():
+    """rg_wire_exchange (the C-ABI exchange a Go host calls) with a host-staged transport over
+    gloo: two processes, two column halves each on its own stream — plain ticks, then pipelined
+    durable step_device ticks, every replica bit-exact against the oracle."""
+    _worker(["2", "2", "gloo", "c"], 29537)
+
+
+def test_one_rank_rccl_c_exchange():
+    """rg_wire_exchange with the library's built-in RCCL transport (librccl loaded at run time,
+    communicator from rg_rccl_unique_id / rg_rccl_open): one rank, every message through the
+    wire, two halves on their own streams."""
+    _worker(["1", "2", "nccl", "c"], 29538)
+
+
+def test_c_exchange_one_engine_vs_oracle():
+    """A bare engine (no torch.distributed) exchanging through the built-in RCCL transport at
+    world size 1, every plane through the wire: chaos ticks bit-exact against the oracle."""
+    from raftd_amd.engine import Engine, rccl_close, rccl_transport, rccl_unique_id
+    cfg = dict(groups=16, replicas=3, seed=91, **CHAOS)
+    eng = Engine(wire_all=1, **cfg)
+    ora = make("c", **cfg)
+    t = rccl_transport(rccl_unique_id(), 1, 0, 0)
+    try:
+        eng.bootstrap()
+        ora.bootstrap()
+        rng = np.random.default_rng(92)
+        sent = 0
+        for k in range(60):
+            if k:
+                sent += eng.wire_exchange(t)
+            ins = random_inputs(rng, 16, 3, CHAOS["max_entries_per_msg"])
+            eng.tick(*ins)
+            ora.tick(*ins)
+            compare(eng, ora, k)
+        assert sent == 0  # one rank: its only region is its own
+    finally:
+        eng.sync()
+        rccl_close(t)
