@@ -12,6 +12,7 @@
 //                    sends it as a uniform Replicate (one inline word for all n entries, below)
 //   RG_CTL_FRESH     write_entries' fresh-index path (pointer-stepped ring slots, no hull)
 //   RG_CTL_HDRBATCH  handle() loads all eight header words of a message up front
+//   RG_CTL_LTCACHE   term_at keeps the term of one index (at first `last`) in registers
 // Uniform Replicate: header word 7 = RG_UNIFORM marks a local Replicate whose n entries all carry
 // the ring word mt[0] (only mt[0] is written). Remote Replicates never carry it: unpack_kernel
 // replaces word 7 with the records' offset, and pack_kernel expands the word into n records.
@@ -24,6 +25,9 @@
 #endif
 #ifndef RG_CTL_HDRBATCH
 #define RG_CTL_HDRBATCH
+#endif
+#ifndef RG_CTL_LTCACHE
+#define RG_CTL_LTCACHE
 #endif
 #endif
 
@@ -119,6 +123,7 @@ struct Ctl {
 #endif
   uint64_t oc, em;  // per destination: enqueued / emitted counts, 8 bits each
   uint32_t nj;      // jobs emitted
+  uint64_t lt_i = ~0ull, lt_v = 0;  // term_at cache: index lt_i has term lt_v (~0: none)
 
   RG_FN Ctl(const TickParams& pp, uint32_t qq) : p(pp), q(qq) {
     s = q / p.G;
@@ -145,6 +150,7 @@ struct Ctl {
       else rs[j] = p.rem_in[(2 * R + j) * n + q];
       rt[j] = p.rst_in[j * n + q];
     });
+    if (last > marker) lt_set(last, *tr_at(last) & TERM_MASK);  // issued early, used after the inbox headers
     last_start = last; sent_hi = 0; rw_lo = ~0ull; rw_hi = 0; marker_start = marker;
     processed_start = processed; restored_at = 0; wlo = ~0ull; took = false;
 #ifdef RG_CTL_FASTREP
@@ -178,8 +184,22 @@ struct Ctl {
   }
   RG_FN uint64_t term_at(uint64_t i) const {
     if (i == marker) return marker_term;
-    if (i > marker && i <= last) return *tr_at(i) & TERM_MASK;
+    if (i > marker && i <= last) return i == lt_i ? lt_v : *tr_at(i) & TERM_MASK;
     return 0;
+  }
+  // the term of one index kept in registers (RG_CTL_LTCACHE): the step's own writes keep it
+  // current (write_entries_), so the repeated term_at(last) of a leader's commit checks and
+  // empty Replicates and a follower's log-matching check cost no ring round trip
+  RG_FN void lt_set(uint64_t i, uint64_t t) {
+#ifdef RG_CTL_LTCACHE
+    if constexpr (R < 8) {  // at R = 8 the two registers push the lane into scratch: off there
+      lt_i = i;
+      lt_v = t;
+    }
+#else
+    (void)i;
+    (void)t;
+#endif
   }
   RG_FN void commit_to(uint64_t i) {
     if (i <= committed) return;
@@ -339,6 +359,7 @@ struct Ctl {
         hm = (word & PAY_BIT) ? M : 0ull;
         tm = (word & TYPE_BIT) ? M : 0ull;
         const uint64_t wr = word & ~BANK_BIT;
+        if (n > e0) lt_set(base + n - 1, word & TERM_MASK);
         for (uint32_t e = e0; e < n; ++e) {
           *dst = wr;
           dst += step;
@@ -358,6 +379,7 @@ struct Ctl {
           for (uint32_t k = 0; k < CB; ++k) {
             if (e + k >= n) break;
             const uint64_t w = wv[k];
+            if (e + k == n - 1) lt_set(base + n - 1, w & TERM_MASK);
             sm |= (w & BANK_BIT) ? bit : 0ull;
             hm |= (w & PAY_BIT) ? bit : 0ull;
             tm |= (w & TYPE_BIT) ? bit : 0ull;
@@ -391,6 +413,7 @@ struct Ctl {
         if (e + k >= n) break;
         const uint32_t ek = e + k;
         const uint64_t idx = base + ek, w = wv[k];
+        if (ek == n - 1) lt_set(idx, w & TERM_MASK);
         uint32_t tb = 0;
         if (idx <= hi_prot) {  // protected this tick: rewrite goes to the other bank
           const uint32_t cur = (uint32_t)(ov[k] >> 63);
