@@ -526,10 +526,16 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   int cus = 0;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device);
   const uint64_t per_cu = (uint64_t)std::max(bulk_blocks_per_cu(c.payload_bytes), 1);
-  // bulk tiles: the largest power of two <= 64 replicas that still leaves >= 2 tiles per resident wave
+  // bulk tiles: the largest power of two <= 64 replicas that still leaves a tile per resident wave
+  // (r02 sweep, scripts/tile_sweep.sh: 64K x 3 picks 32, 1.160 -> 1.137 ms; C2 4,096 x 3 picks 2,
+  // 0.094 -> 0.085 ms; the r01 rule asked for two tiles per wave and picked 16 and 1)
   const uint64_t waves = (uint64_t)std::max(cus, 1) * per_cu * 4;
   uint32_t tile = 64;
-  while (tile > 1 && (n + tile - 1) / tile < 2 * waves) tile >>= 1;
+  while (tile > 1 && (n + tile - 1) / tile < waves) tile >>= 1;
+  if (const char* tv = getenv("RAFTGPU_BULK_TILE")) {  // measurement override (a power of two, 1..64)
+    const uint32_t t = (uint32_t)atoi(tv);
+    if (pow2(t) && t <= 64) tile = t;
+  }
   e->bulk_tile = tile;
   const uint64_t ntiles = (n + tile - 1) / tile;
   e->bulk_grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((ntiles + 3) / 4, (uint64_t)std::max(cus, 1) * per_cu));
