@@ -194,7 +194,9 @@ def gloo_transport(pg, device):
         torch.cuda.synchronize(device)
         st, rt = sum(ssize), sum(rsize)
         sb, rb = _dev_bytes(send, st, device), _dev_bytes(recv, rt, device)
-        all_to_all_bytes(sb, list(ssize), rb, list(rsize), pg, nchunks=a2a_chunks(max(list(ssize) + list(rsize))))
+        big = torch.tensor([max(list(ssize) + list(rsize))], dtype=torch.int64)
+        dist.all_reduce(big, op=dist.ReduceOp.MAX, group=pg)  # every rank issues the same chunk count
+        all_to_all_bytes(sb, list(ssize), rb, list(rsize), pg, nchunks=a2a_chunks(int(big.item())))
         torch.cuda.synchronize(device)
 
     pt = PyTransport(allgather, alltoallv)
