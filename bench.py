@@ -198,7 +198,7 @@ def apply_copyback(eng, torch, slot_mask=1):
             "note": "count + scan + gather kernels, then one hipMemcpyAsync per array into pinned host memory"}
 
 
-def e2e_with_apply(eng, tick, G, steps, slot_mask=1):
+def e2e_with_apply(eng, tick, G, steps, slot_mask=1, serial=False):
     """Ticks with the committed-entry copy-back the daemon needs for /UpdateEntries: after every tick
     rg_apply_async gathers the slot-0 replicas' applied entries (one node's share) and starts their
     D2H copy on the copy stream, double-buffered, so copies overlap the next ticks; the host waits
@@ -211,16 +211,20 @@ def e2e_with_apply(eng, tick, G, steps, slot_mask=1):
     for i in range(steps):
         tick()
         eng.apply_async(slot_mask, i & 1)
-        if i:
+        if serial:  # the copy completes before the next tick is issued
+            r, _ = eng.apply_wait(i & 1, copy=False)
+            n += len(r)
+        elif i:
             r, _ = eng.apply_wait((i - 1) & 1, copy=False)
             n += len(r)
-    r, _ = eng.apply_wait((steps - 1) & 1, copy=False)
-    n += len(r)
+    if not serial:
+        r, _ = eng.apply_wait((steps - 1) & 1, copy=False)
+        n += len(r)
     el = time.perf_counter() - t0
     nb = n * (32 + P)
     return {"value": G * steps / el, "unit": "group-steps/s", "steps": steps, "ms_per_step": el * 1e3 / steps,
             "entries_per_step": n / steps, "bytes_per_step": nb / steps, "pcie_GBps": nb / el / 1e9,
-            "slot_mask": slot_mask,
+            "slot_mask": slot_mask, "schedule": "serial" if serial else "overlapped",
             "note": "tick + gather of the applied entries of one node (slot-0 replicas) + D2H into pinned memory "
                     "on a copy stream, overlapped with the next tick (rg_apply_async / rg_apply_wait); the copy "
                     "is PCIe-bound, so this is min(tick rate, PCIe rate)"}
@@ -361,6 +365,10 @@ def main():
     e2e = None
     if not spread:
         e2e = e2e_with_apply(eng, lambda: one_step(None), G, steps=max(4, min(args.steps, 12)))
+        # the same with each copy finished before the next tick: the copy kernels and the tick
+        # kernels slow each other down when they share the GPU
+        e2e["serial"] = e2e_with_apply(eng, lambda: one_step(None), G, steps=max(4, min(args.steps, 12)),
+                                       serial=True)
     apply = apply_copyback(eng, torch)
     copy_gbs = hbm_copy_ceiling(eng)
     t = torch.tensor([wall, dev_ms, float(c1 - c0), x_ms, float(wire_bytes)], dtype=torch.float64,
