@@ -539,6 +539,10 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   e->bulk_tile = tile;
   const uint64_t ntiles = (n + tile - 1) / tile;
   e->bulk_grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((ntiles + 3) / 4, (uint64_t)std::max(cus, 1) * per_cu));
+  if (const char* gv = getenv("RAFTGPU_BULK_GRID")) {  // measurement override (blocks)
+    const int gb = atoi(gv);
+    if (gb > 0) e->bulk_grid = gb;
+  }
   *out = e;
   return RG_OK;
 }
