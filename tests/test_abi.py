@@ -29,6 +29,16 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, name), name
 
 
+def test_transport_struct_matches_header():
+    """rg_transport as ctypes sees it: a user pointer and two callback pointers, in header order."""
+    from raftd_amd.engine import Transport
+    src = open(os.path.join(ROOT, "include", "raftgpu.h")).read()
+    body = src[src.index("typedef struct rg_transport {"):src.index("} rg_transport;")]
+    order = re.findall(r"\(\*(\w+)\)|void\* (user);", body)
+    assert [a or b for a, b in order] == [f for f, _ in Transport._fields_]
+    assert C.sizeof(Transport) == 3 * C.sizeof(C.c_void_p)
+
+
 def test_create_rejects_bad_config_without_gpu():
     from raftd_amd.engine import Config, load_library
     L = load_library()

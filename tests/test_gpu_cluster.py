@@ -291,3 +291,27 @@ def test_c_exchange_one_engine_vs_oracle():
     finally:
         eng.sync()
         rccl_close(t)
+
+
+def test_c_exchange_transport_failures_surface_as_errors():
+    """A transport callback that fails (raises, or returns sizes that are not this rank's own)
+    makes rg_wire_exchange fail with RG_EHIP / RG_EINVAL instead of unpacking anything."""
+    from raftd_amd.engine import Engine, PyTransport, RgError
+    cfg = dict(groups=8, replicas=3, seed=93, **CHAOS)
+    eng = Engine(wire_all=1, **cfg)
+    eng.bootstrap()
+    eng.tick(*random_inputs(np.random.default_rng(94), 8, 3, CHAOS["max_entries_per_msg"]))
+
+    def a2a_raises(*_):
+        raise RuntimeError("link down")
+
+    bad = PyTransport(lambda vals: list(vals), a2a_raises)
+    bad.nranks = 1
+    with pytest.raises(RgError, match="alltoallv failed"):
+        eng.wire_exchange(bad.t)
+    assert isinstance(bad.error, RuntimeError)
+    liar = PyTransport(lambda vals: [v + 16 for v in vals], lambda *a: None)
+    liar.nranks = 1
+    with pytest.raises(RgError, match="another rank's sizes"):
+        eng.wire_exchange(liar.t)
+    eng.sync()
