@@ -1,7 +1,7 @@
 """Where the HIP runtime puts kernel arguments in this process ("The
 control-kernel fault").
-usage: python scripts/kernarg_probe.py   (the package sets HIP_FORCE_DEV_KERNARG=0 unless the
-environment already names a value)"""
+usage: [HIP_FORCE_DEV_KERNARG=0|1] python scripts/kernarg_probe.py (r02: this runtime put them in
+device memory either way, so control_kernel takes its parameter block from a device slot)"""
 import ctypes as C
 import os
 import sys
