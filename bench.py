@@ -401,7 +401,11 @@ def main():
         par = f"groups sharded over {world} GPU(s), replicas co-located (no exchange)"
     bulk_ms = kms["bulk"][0] / max(kms["bulk"][1], 1)
     ctl_ms = kms["control"][0] / max(kms["control"][1], 1)
-    achieved = traffic["bulk_bytes"] / (bulk_ms / 1e3) / 1e9
+    # metadata-only (P = 0): no payload stage is launched, the control kernel is the tick
+    meta_only = kms["bulk"][1] == 0
+    rk_ms = ctl_ms if meta_only else bulk_ms
+    rk_bytes = traffic["algorithmic_bytes"] if meta_only else traffic["bulk_bytes"]
+    achieved = rk_bytes / (rk_ms / 1e3) / 1e9 if rk_ms > 0 else 0.0
     # PMC bytes come from a committed profile of the same mode and launch size; the N > 1 spread
     # engines (column halves, wire jobs) have none, so their traffic is left unmeasured
     hbm, src = pmc_traffic(wire=bool(args.wire_all), spread=spread)
@@ -447,14 +451,14 @@ def main():
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": hbm,
             "traffic_source": src,
-            "kernel": "rg::bulk_kernel",
+            "kernel": "rg::control_kernel" if meta_only else "rg::bulk_kernel",
             "box_copy_ceiling_GBps": copy_gbs,
             "frac_of_box_copy_ceiling": achieved / copy_gbs if copy_gbs else None,
-            "kernel_ms": bulk_ms,
+            "kernel_ms": rk_ms,
             "launches_timed": kms["bulk"][1],
             "per": "tick: bulk_kernel launches of every column half summed" if pipelined or (spread and args.halves > 1)
                    else "launch",
-            "algorithmic_bytes_per_launch": traffic["bulk_bytes"],
+            "algorithmic_bytes_per_launch": rk_bytes,
             "tick_algorithmic_bytes": traffic["algorithmic_bytes"],
             "tick_counts": {k: v for k, v in traffic.items() if k not in ("algorithmic_bytes", "bulk_bytes")},
         },
