@@ -6,12 +6,14 @@ election through the engine), every tick each leader receives a 64-entry proposa
 256-B payloads (CRC32 per entry at every replica), raftd's Raft config (ElectionRTT 10,
 HeartbeatRTT 1, CheckQuorum, SnapshotEntries 1000, CompactionOverhead 5). A step = one tick of
 every replica of every group = one control_kernel launch (Raft logic) + one bulk_kernel launch
-(payload copies + CRC32); control of tick t+1 overlaps bulk of tick t on a second stream. Inputs
-(proposal descriptors, payload slabs) are resident in HBM before the timed region.
+(payload copies + CRC32), in that order on one stream. Inputs (proposal descriptors, payload
+slabs) are resident in HBM before the timed region.
 
 roofline: the dominant kernel is bulk_kernel (HBM-bound byte copies + CRC). achieved = its
 algorithmic bytes per launch (rg_traffic.bulk_bytes) / its mean launch duration, timed with HIP
-events recorded on the bulk stream around every launch of the timed region.
+events recorded on the engine stream around every launch of the timed region. With
+--payload 0 there is no payload stage and the control kernel (the whole tick's algorithmic bytes)
+is reported instead.
 
 N > 1 (default --placement spread, the north star's layout): one process per GPU
 (torch.distributed.run), N x 65,536 groups, replica slot s of group g on GPU (g mod N + off(s)) mod N
