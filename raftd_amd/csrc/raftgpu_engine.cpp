@@ -975,8 +975,8 @@ static int tick_impl(rg_engine* e, const rg_tick_input* in, bool device_ptrs) {
     HIPCHK(hipStreamWaitEvent(bs, e->ctl_done[a], 0));
   }
   // metadata-only engines (P = 0) have no payload stage: every reader of an entry takes its type
-  // from the term word and its CRC is 0 (no Cmd bytes), so the info words bulk_meta_kernel would
-  // write are never read and the tick is the control launch alone
+  // from the term word and its CRC is 0 (no Cmd bytes), so no info word needs writing and the tick
+  // is the control launch alone
   if (e->c.payload_bytes) {
     RGCHK(timing_event(e, bs, 1));
     LAUNCH(launch_bulk(bulk_params(e), bs, e->bulk_grid), bs, "bulk_kernel");

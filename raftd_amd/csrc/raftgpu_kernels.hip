@@ -244,31 +244,6 @@ __device__ __forceinline__ bool next_job(const BulkParams& p, Cursor& cur, TileJ
 
 enum : uint32_t { F_ACT = 1, F_WRITER = 2, F_TYPE = 4, F_CHECK = 8 };
 
-// metadata-only entries (P = 0): one info word per entry, no payload
-__global__ void __launch_bounds__(256) bulk_meta_kernel(BulkParams p) {
-  const uint32_t waves = blockDim.x >> 6, lane = lane_id();
-  const uint32_t stride = gridDim.x * waves;
-  const uint32_t ntiles = bulk_ntiles(p);
-  const uint64_t n64 = p.nrep, L = p.L;
-  Cursor cur{};
-  TileJobs tj{};
-  cur.t = rfl(blockIdx.x * waves + (threadIdx.x >> 6));
-  if (cur.t >= ntiles) return;
-  load_tile(p, cur, tj);
-  cur.b = 0;  // two statements: the chained form kept Cursor in scratch
-  cur.n = 0;
-  cur.live = next_job(p, cur, tj, stride, ntiles);
-  while (rfl((uint32_t)cur.live)) {
-    const uint32_t e = cur.b + lane;
-    if (cur.b < cur.n && e < cur.n) {
-      const uint64_t slot = (cur.first + e) & (L - 1);
-      const uint32_t db = (uint32_t)(cur.dm >> e) & 1u;
-      p.info[((uint64_t)db * n64 + cur.q) * L + slot] = make_uint2(0u, (uint32_t)((cur.tm >> e) & 1u) << 24);
-    }
-    cur.b = cur.b < cur.n ? cur.b + 64 : cur.b;
-    if (cur.b >= cur.n) cur.live = next_job(p, cur, tj, stride, ntiles);
-  }
-}
 
 // P = 16 << LG bytes per entry: 2^LG lanes per entry (16 B each), 64 >> LG entries per step.
 // WIRE: the engine exchanges messages with other ranks (SRC_WIRE jobs, slab rows per replica);
@@ -398,7 +373,7 @@ static hipError_t with_bulk_w(uint32_t P, F f) {
 }
 template <class F>
 static hipError_t with_bulk(uint32_t P, bool wire, F f) {
-  if (!P) return f(bulk_meta_kernel);
+  if (!P) return hipSuccess;  // metadata-only engines have no payload stage (tick_impl)
   return wire ? with_bulk_w<true>(P, f) : with_bulk_w<false>(P, f);
 }
 
