@@ -180,24 +180,26 @@ def apply_copyback(eng, torch, slot_mask=1):
     replicas hands to /UpdateEntries, gathered on the device and copied back into pinned host
     buffers. Host wall time of the whole call (count + scan + gather + D2H + sync)."""
     import ctypes as C
-    n = C.c_uint64()
-    eng.L.rg_apply_committed(eng.h, slot_mask, None, None, 0, C.byref(n))
-    cnt, P = n.value, eng.cfg["payload_bytes"]
+    from raftd_amd.engine import APPLY_DTYPE
+    n, pb = C.c_uint64(), C.c_uint64()
+    eng.L.rg_apply_committed(eng.h, slot_mask, None, None, 0, C.byref(n), 0, C.byref(pb))
+    cnt, nbytes = n.value, pb.value
     if cnt == 0:
         return None
-    recs = torch.empty(cnt * 32, dtype=torch.uint8, pin_memory=True)
-    pay = torch.empty(max(cnt * P, 1), dtype=torch.uint8, pin_memory=True)
+    recs = torch.empty(cnt * APPLY_DTYPE.itemsize, dtype=torch.uint8, pin_memory=True)
+    pay = torch.empty(max(nbytes, 16), dtype=torch.uint8, pin_memory=True)
     best = None
     for _ in range(3):
         t0 = time.perf_counter()
-        rc = eng.L.rg_apply_committed(eng.h, slot_mask, recs.data_ptr(), pay.data_ptr(), cnt, C.byref(n))
+        rc = eng.L.rg_apply_committed(eng.h, slot_mask, recs.data_ptr(), pay.data_ptr(), cnt, C.byref(n),
+                                      pay.numel(), C.byref(pb))
         dt = time.perf_counter() - t0
         if rc < 0:
             return None
         best = dt if best is None else min(best, dt)
-    nb = cnt * (32 + P)
+    nb = cnt * APPLY_DTYPE.itemsize + pb.value
     return {"slot_mask": slot_mask, "entries": cnt, "bytes": nb, "ms": best * 1e3, "GBps": nb / best / 1e9,
-            "note": "count + scan + gather kernels, then one hipMemcpyAsync per array into pinned host memory"}
+            "note": "count + scan + gather kernels (Cmds packed at their own length), then one hipMemcpyAsync per array into pinned host memory"}
 
 
 def e2e_with_apply(eng, tick, G, steps, slot_mask=1, serial=False):
@@ -206,24 +208,26 @@ def e2e_with_apply(eng, tick, G, steps, slot_mask=1, serial=False):
     D2H copy on the copy stream, double-buffered, so copies overlap the next ticks; the host waits
     for each tick's copy one tick later. Bounded by min(tick rate, PCIe rate)."""
     import torch
+    from raftd_amd.engine import APPLY_DTYPE
     n = nb = 0
-    P = eng.cfg["payload_bytes"]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(steps):
         tick()
         eng.apply_async(slot_mask, i & 1)
         if serial:  # the copy completes before the next tick is issued
-            r, _ = eng.apply_wait(i & 1, copy=False)
+            r, pk = eng.apply_wait(i & 1, copy=False)
             n += len(r)
+            nb += len(r) * APPLY_DTYPE.itemsize + pk.size
         elif i:
-            r, _ = eng.apply_wait((i - 1) & 1, copy=False)
+            r, pk = eng.apply_wait((i - 1) & 1, copy=False)
             n += len(r)
+            nb += len(r) * APPLY_DTYPE.itemsize + pk.size
     if not serial:
-        r, _ = eng.apply_wait((steps - 1) & 1, copy=False)
+        r, pk = eng.apply_wait((steps - 1) & 1, copy=False)
         n += len(r)
+        nb += len(r) * APPLY_DTYPE.itemsize + pk.size
     el = time.perf_counter() - t0
-    nb = n * (32 + P)
     return {"value": G * steps / el, "unit": "group-steps/s", "steps": steps, "ms_per_step": el * 1e3 / steps,
             "entries_per_step": n / steps, "bytes_per_step": nb / steps, "pcie_GBps": nb / el / 1e9,
             "slot_mask": slot_mask, "schedule": "serial" if serial else "overlapped",

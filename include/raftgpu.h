@@ -63,7 +63,8 @@ enum { RG_ENTRY_APPLICATION = 0, RG_ENTRY_CONFIG_CHANGE = 1 };
 enum {
   RG_ERR_CONFLICT_COMMITTED = 1, RG_ERR_COMMIT_BEYOND_LAST = 2, RG_ERR_RING_FULL = 4,
   RG_ERR_CRC = 8, RG_ERR_EMPTY_SNAPSHOT = 16,
-  RG_ERR_MALFORMED = 32 /* a message with an impossible sender / destination was ignored */
+  RG_ERR_MALFORMED = 32, /* a message with an impossible sender / destination was ignored */
+  RG_ERR_POOL = 64       /* the payload page pool was empty: this replica's appends of a step were lost */
 };
 #define RG_TICK_NO_LOCALTICK 1u
 
@@ -103,6 +104,21 @@ typedef struct rg_config {
                                    (dragonboat's NotifyRaftLastApplied, raft/state_machine.go:101-166) */
   uint32_t initial_members;     /* bootstrap voting membership, bit s = slot s: StartOnDiskReplica's
                                    initialMembers (raft/raft_manager.go:114-144); 0 = every slot */
+  /* Cmd storage: every replica appends its entries' Cmds, each at its own length
+   * rounded up to 16 B, to a payload stream mapped onto 4-KiB pages of one engine-wide pool. */
+  uint32_t max_cmd_bytes;       /* longest Cmd (raft/state_machine.go:126-145 hands any Cmd []byte back):
+                                   payload_bytes .. 8191; 0 = payload_bytes. payload_bytes is the Cmd
+                                   size the payload kernel's lane groups and the benchmark's synthetic
+                                   Cmds use; longer Cmds take several groups */
+  uint32_t stream_pages;        /* pages one replica's live stream may span (power of two); an append
+                                   beyond it is refused like one beyond log_capacity.
+                                   0 = twice a full log of payload_bytes Cmds */
+  uint32_t pool_pages;          /* 4-KiB pages in the pool (<= 2^24); 0 = a full log of payload_bytes
+                                   Cmds per replica, capped at 2^24. An empty pool poisons the engine:
+                                   RG_ERR_POOL in the affected replicas, rg_pool_stats().fail */
+  uint32_t join_slots;          /* slots started by StartOnDiskReplica(join = true) (raft_manager.go:
+                                   134-144): empty log, term 0, not a member until a ConfigChange that
+                                   adds them reaches them; 0 = none */
   uint32_t _reserved;
 } rg_config;
 
@@ -163,9 +179,11 @@ typedef struct rg_apply_entry {
   uint64_t index;      /* statemachine.Entry.Index */
   uint64_t group;      /* global shard id (raftd-node-id) */
   uint32_t replica_id; /* raftd-replica-id: slot + 1 */
-  uint32_t len;        /* Cmd bytes, at payload + k * payload_bytes */
+  uint32_t len;        /* Cmd bytes, at payload + off */
   uint32_t crc;        /* CRC-32 of Cmd as stored in the log */
   uint32_t rid;        /* local replica id */
+  uint64_t off;        /* byte offset of the Cmd in the payload buffer (Cmds packed back to back, each
+                          rounded up to 16 B) */
 } rg_apply_entry;
 
 /* Persistence feed (rg_persist_collect): dragonboat's Update.EntriesToSave + pb.State + snapshot
@@ -184,7 +202,8 @@ typedef struct rg_persist_state {
 
 typedef struct rg_persist_entry {
   uint64_t index, term;
-  uint32_t type, len, crc, rid; /* payload at payload + k * payload_bytes when len > 0 */
+  uint32_t type, len, crc, rid; /* an application entry's Cmd: len bytes at payload + off */
+  uint64_t off;
 } rg_persist_entry;
 
 /* Snapshot events of the last tick (rg_snapshot_events): where dragonboat's rsm calls the state
@@ -276,12 +295,15 @@ int rg_read_replicas(rg_engine* e, uint32_t first_rid, uint32_t n, rg_replica_vi
  * headers and, if terms != NULL, cap * max_entries_per_msg inline entry terms (bank bit
  * cleared). */
 int rg_read_msgs(rg_engine* e, uint32_t rid, uint32_t dst, rg_msg_view* out, uint32_t cap, uint64_t* terms);
-/* Log entries first_index .. first_index+n-1 of replica rid (must lie in (marker, last]). */
+/* Log entries first_index .. first_index+n-1 of replica rid (must lie in (marker, last]); payload (if
+ * not NULL): entry k's Cmd at payload + k * max_cmd_bytes. */
 int rg_read_entries(rg_engine* e, uint32_t rid, uint64_t first_index, uint32_t n, rg_entry_view* out,
                     uint8_t* payload);
 /* Replace replica rid's state and its log (marker, last]: terms[k], types[k] (RG_ENTRY_*, | RG_ENTRY_EMPTY),
- * payloads = one payload_bytes row per entry of which lens[k] bytes are the Cmd (lens NULL: the whole
- * row for every application entry with a payload). */
+ * payloads = one max_cmd_bytes row per entry of which lens[k] bytes are the Cmd (lens NULL:
+ * payload_bytes for every application entry with a payload). The replica's Cmds move to a fresh
+ * payload stream (RG_ENOMEM: the page pool is empty; RG_EFULL: longer than stream_pages). Not for a
+ * replica whose messages of the last tick are still to be delivered. */
 int rg_import_replica(rg_engine* e, uint32_t rid, const rg_replica_view* v, const uint64_t* terms,
                       const uint32_t* types, const uint8_t* payloads, const uint32_t* lens);
 /* Enqueue a message as if `rid_src` had emitted it in the last tick (delivered next tick). */
@@ -343,28 +365,31 @@ int rg_rccl_close(rg_transport* t);
  * no-ops and snapshot-restored ranges excluded, as dragonboat's rsm does before Update — grouped
  * by replica in device order (slot by slot, shards ascending within a slot), each replica's
  * entries in index order. Compacted on the device, then copied back by one hipMemcpyAsync
- * per array into entries[cap] and payload[cap * payload_bytes] (host memory; pinned is fastest).
- * *n = the count; if *n > cap nothing is copied and RG_EFULL is returned. Synchronous. */
+ * per array into entries[cap] and payload[pay_cap] (host memory; pinned is fastest): the Cmds
+ * packed back to back, each rounded up to 16 B (rg_apply_entry.off), so only Cmd bytes cross PCIe.
+ * *n = the count, *pay_bytes = the payload bytes; if either exceeds its cap nothing is copied and
+ * RG_EFULL is returned. Synchronous. */
 int rg_apply_committed(rg_engine* e, uint32_t slot_mask, rg_apply_entry* entries, uint8_t* payload, uint64_t cap,
-                       uint64_t* n);
-/* Asynchronous, double-buffered copy-back (the same batch as rg_apply_committed): gathers the last
- * tick's applied entries into device staging buffer `buf` (0 or 1) on the engine's stream — before
- * the next tick can reuse their ring slots — and starts one D2H copy per array into engine-owned
- * pinned host memory on a separate copy stream, so the copy overlaps the next ticks. A gather into
- * `buf` first waits (on the device) for that buffer's previous copy: a driver that alternates
- * buffers runs at min(tick rate, PCIe rate). Synchronises the host only on the entry count. */
+                       uint64_t* n, uint64_t pay_cap, uint64_t* pay_bytes);
+/* Asynchronous, double-buffered copy-back (the same batch as rg_apply_committed): the gather kernel
+ * writes the last tick's applied entries straight into engine-owned, host-mapped pinned buffer `buf`
+ * (0 or 1) over PCIe, on the engine's stream right after the tick (before the next tick can reuse
+ * their log slots): no staging copy and no copy engine contending with the next ticks. Its counts
+ * are read back without a host synchronisation when the buffer is large enough from the last use
+ * (the buffer grows, with one synchronisation, when it is not). */
 int rg_apply_async(rg_engine* e, uint32_t slot_mask, int buf);
-/* Wait for buffer `buf`'s copy; *entries / *payload (payload_bytes per entry) point into
+/* Wait for buffer `buf`'s gather; *entries / *payload (rg_apply_entry.off into it) point into
  * engine-owned pinned memory, valid until the next rg_apply_async into `buf`; *n = the count. */
 int rg_apply_wait(rg_engine* e, int buf, const rg_apply_entry** entries, const uint8_t** payload, uint64_t* n);
 /* Host WAL feed: for every replica whose log or hard state changed in the last
  * tick (full != 0, or no tick yet: every replica, whole log window), one rg_persist_state and the
- * entries it rewrote, gathered on the device and copied back by one hipMemcpyAsync per array. Make
- * them durable before the next tick delivers the last tick's messages. *n_states / *n_entries =
- * the counts; if either exceeds its cap nothing is copied and RG_EFULL is returned. Synchronous.
- * Restart = rg_import_replica of the replayed state. */
+ * entries it rewrote, their Cmds packed (rg_persist_entry.off), gathered on the device and copied back
+ * by one hipMemcpyAsync per array. Make them durable before the next tick delivers the last tick's
+ * messages. *n_states / *n_entries / *pay_bytes = the counts; if one exceeds its cap nothing is copied
+ * and RG_EFULL is returned. Synchronous. Restart = rg_import_replica of the replayed state. */
 int rg_persist_collect(rg_engine* e, int full, rg_persist_state* states, uint64_t cap_states, uint64_t* n_states,
-                       rg_persist_entry* entries, uint8_t* payload, uint64_t cap_entries, uint64_t* n_entries);
+                       rg_persist_entry* entries, uint8_t* payload, uint64_t cap_entries, uint64_t* n_entries,
+                       uint64_t pay_cap, uint64_t* pay_bytes);
 /* Snapshot events of the last tick for replicas whose slot bit is set in slot_mask, one per
  * replica in device order (slot by slot, shards ascending within a slot), compacted on the device and copied back by one hipMemcpyAsync. *n = the count;
  * if *n > cap nothing is copied and RG_EFULL is returned. Synchronous. */
@@ -405,6 +430,9 @@ int rg_global_id(rg_engine* e, uint32_t rid, uint64_t* group, uint64_t* global_r
 int rg_probe_copy(int32_t device, uint64_t bytes, int32_t reps, double* gbps);
 /* Device bytes held by the engine. */
 uint64_t rg_device_bytes(const rg_engine* e);
+/* The payload page pool: pages in all, pages free (after the last launch), and
+ * whether an allocation ever found it empty (the engine is then poisoned: RG_ERR_POOL). Synchronises. */
+int rg_pool_stats(rg_engine* e, uint64_t* total_pages, uint64_t* free_pages, int* failed);
 const char* rg_last_error(void);
 
 #ifdef __cplusplus

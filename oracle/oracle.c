@@ -23,6 +23,7 @@
 typedef struct {
   uint64_t term;
   uint32_t type, len, crc;
+  uint32_t pos; /* payload stream position (16-B chunks) of its Cmd in the replica's log */
 } ent_t;
 
 typedef struct {
@@ -61,11 +62,17 @@ typedef struct {
   uint64_t ri_ctx, ri_index;
   uint32_t ri_acks, ri_from;
   uint64_t rd_ctx, rd_index, rd_tick; /* rd_tick = step + 1 when it became ready */
+  /* payload stream: the capacity rule's state. hw = next free chunk; lpg = lowest page
+   * held; fidx = the step compacted or restored below this entry: its position bounds the pages the
+   * next step releases (nlpg, effective once that step ends) */
+  uint32_t hw, lpg, nlpg;
+  uint64_t fidx;
 } rep_t;
 
 struct or_engine {
   or_config c;
   uint32_t nrep;
+  uint32_t maxc, pts; /* longest Cmd (the payload row stride), stream pages per replica */
   rep_t* reps;
   uint64_t t; /* next tick to run */
   const or_tick_input* in;
@@ -136,7 +143,15 @@ static inline ent_t* log_at(const or_engine* e, const rep_t* r, uint64_t i) {
   return &r->log[i & (e->c.log_capacity - 1)];
 }
 static inline uint8_t* logpay_at(const or_engine* e, const rep_t* r, uint64_t i) {
-  return r->logpay + (size_t)(i & (e->c.log_capacity - 1)) * e->c.payload_bytes;
+  return r->logpay + (size_t)(i & (e->c.log_capacity - 1)) * e->maxc;
+}
+/* 16-B chunks a Cmd of len bytes takes in the payload stream */
+static inline uint32_t chunks_of(uint32_t len) { return (len + 15u) >> 4; }
+/* stream capacity rule: an append of c chunks fits iff its last chunk's page lies
+ * within stream_pages of the lowest page still held (page numbers are positions >> 8, mod 2^24) */
+static int stream_fits(const or_engine* e, const rep_t* r, uint32_t c) {
+  if (c == 0) return 1;
+  return ((((r->hw + c - 1u) >> 8) - r->lpg) & 0xFFFFFFu) < e->pts;
 }
 
 /* entryLog.term: (0, nil) outside [firstIndex-1, lastIndex]  (SURVEY A.9 / DESIGN §1.2) */
@@ -186,7 +201,7 @@ static void arena_reserve(const or_engine* e, outbox_t* ob, size_t need) {
   size_t nc = ob->cap_ents ? ob->cap_ents * 2 : 256;
   while (nc < ob->n_ents + need) nc *= 2;
   ob->ents = (ent_t*)realloc(ob->ents, nc * sizeof(ent_t));
-  if (e->c.payload_bytes) ob->pay = (uint8_t*)realloc(ob->pay, nc * e->c.payload_bytes);
+  if (e->c.payload_bytes) ob->pay = (uint8_t*)realloc(ob->pay, nc * e->maxc);
   ob->cap_ents = nc;
 }
 
@@ -273,11 +288,16 @@ typedef struct {
 static int append_entries(or_engine* e, rep_t* r, uint32_t n, const src_t* src) {
   uint32_t L = e->c.log_capacity, P = e->c.payload_bytes;
   if (r->last + n > r->cap_base + L) return 0;
+  uint32_t c = 0; /* the batch's stream chunks (the capacity rule's input) */
+  if (src && !src->cc && P)
+    for (uint32_t k = 0; k < n; ++k) c += chunks_of(src->ents ? src->ents[k].len : P);
+  if (!stream_fits(e, r, c)) return 0;
   for (uint32_t k = 0; k < n; ++k) {
     uint64_t idx = r->last + 1 + k;
     ent_t* en = log_at(e, r, idx);
     en->term = r->term;
     en->type = OR_ENTRY_APP;
+    en->pos = r->hw;
     if (src && src->cc) { /* a ConfigChange entry: no Cmd, its descriptor in len */
       en->type = OR_ENTRY_CONFIG;
       en->len = src->cc;
@@ -287,10 +307,11 @@ static int append_entries(or_engine* e, rep_t* r, uint32_t n, const src_t* src) 
     uint32_t len = !src || !P ? 0 : src->ents ? src->ents[k].len : P;
     if (len) {
       uint8_t* dst = logpay_at(e, r, idx);
-      if (src->ents) memcpy(dst, src->pay + (size_t)k * P, len);
+      if (src->ents) memcpy(dst, src->pay + (size_t)k * e->maxc, len);
       else or_payload(e, (uint32_t)src->slab, (uint32_t)global_group(e, r), k, dst);
       en->len = len;
       en->crc = entry_crc(e, dst, len);
+      r->hw += chunks_of(len);
     } else {
       en->len = 0;
       en->crc = 0;
@@ -355,8 +376,7 @@ static void send_replicate(or_engine* e, rep_t* r, uint32_t to) {
     m->ent_off = (uint32_t)ob->n_ents;
     for (uint32_t k = 0; k < n; ++k) {
       ob->ents[ob->n_ents + k] = *log_at(e, r, next + k);
-      if (e->c.payload_bytes)
-        memcpy(ob->pay + (ob->n_ents + k) * e->c.payload_bytes, logpay_at(e, r, next + k), e->c.payload_bytes);
+      if (e->c.payload_bytes) memcpy(ob->pay + (ob->n_ents + k) * e->maxc, logpay_at(e, r, next + k), e->maxc);
     }
     ob->n_ents += n;
   }
@@ -375,6 +395,7 @@ static void broadcast_heartbeat(or_engine* e, rep_t* r) {
     h.type = OR_HEARTBEAT;
     h.to = (uint8_t)id_of(i);
     h.commit = u64min(r->match[i], r->committed);
+    h.hint = r->ri_ctx; /* a pending ReadIndex rides on every heartbeat (readIndex.peepCtx) */
     send_msg(e, r, &h);
   }
 }
@@ -445,9 +466,14 @@ static void handle_replicate(or_engine* e, rep_t* r, const msg_in_t* m) {
       }
     }
     uint64_t last_new = m->h.log_index + n;
-    if (ci != 0 && ci > r->committed && last_new > r->cap_base + L) {
-      r->drops++; /* capacity rule: message dropped, no reply */
-      return;
+    if (ci != 0 && ci > r->committed) { /* capacity rules (ring, then payload stream): dropped, no reply */
+      uint32_t c = 0;
+      for (uint32_t k = k0; k < n && P; ++k)
+        if (m->ents[k].type == OR_ENTRY_APP) c += chunks_of(m->ents[k].len);
+      if (last_new > r->cap_base + L || !stream_fits(e, r, c)) {
+        r->drops++;
+        return;
+      }
     }
     if (ci != 0) {
       if (ci <= r->committed) {
@@ -460,11 +486,13 @@ static void handle_replicate(or_engine* e, rep_t* r, const msg_in_t* m) {
           en->term = src->term;
           en->type = src->type;
           en->len = src->len;
+          en->pos = r->hw;
           if (src->len && src->type == OR_ENTRY_APP) {
             uint8_t* dst = logpay_at(e, r, idx);
-            memcpy(dst, m->pay + (size_t)k * P, src->len);
+            memcpy(dst, m->pay + (size_t)k * e->maxc, src->len);
             en->crc = entry_crc(e, dst, src->len);
             if (en->crc != src->crc) r->err |= OR_ERR_CRC;
+            r->hw += chunks_of(src->len);
           } else {
             en->crc = 0;
           }
@@ -741,12 +769,12 @@ static void handle_propose(or_engine* e, rep_t* r, const msg_in_t* mi) {
       fm->ent_off = (uint32_t)ob->n_ents;
       for (uint32_t k = 0; k < m->nent; ++k) {
         ent_t* en = &ob->ents[ob->n_ents + k];
-        uint8_t* pd = ob->pay + (ob->n_ents + k) * P;
+        uint8_t* pd = ob->pay + (ob->n_ents + k) * e->maxc;
         memset(en, 0, sizeof *en);
         en->type = OR_ENTRY_APP;
         if (mi->ents) {
           en->len = mi->ents[k].len;
-          memcpy(pd, mi->pay + (size_t)k * P, P);
+          memcpy(pd, mi->pay + (size_t)k * e->maxc, e->maxc);
         } else {
           en->len = P;
           or_payload(e, m->src_a, (uint32_t)global_group(e, r), k, pd);
@@ -905,6 +933,9 @@ static void step_replica(or_engine* e, rep_t* r) {
   uint64_t marker_start = r->marker, processed_start = r->processed;
   r->restored_at = 0;
   r->took = 0;
+  /* the pages below the last step's compaction / restore are released when this step ends */
+  r->nlpg = r->lpg;
+  if (r->fidx) r->nlpg = (r->fidx <= r->last ? log_at(e, r, r->fidx)->pos : r->hw) >> 8;
   outbox_t* ob = cur_ob(e, r);
   memset(ob->n, 0, sizeof ob->n);
   memset(ob->emitted, 0, sizeof ob->emitted);
@@ -919,7 +950,7 @@ static void step_replica(or_engine* e, rep_t* r) {
       msg_in_t mi;
       mi.h = m->h;
       mi.ents = sob->ents + m->ent_off;
-      mi.pay = sob->pay ? sob->pay + (size_t)m->ent_off * e->c.payload_bytes : NULL;
+      mi.pay = sob->pay ? sob->pay + (size_t)m->ent_off * e->maxc : NULL;
       handle(e, r, &mi);
     }
   }
@@ -937,7 +968,7 @@ static void step_replica(or_engine* e, rep_t* r) {
   } else if (e->staged && e->stg_slot[r->g] == r->s) {
     pn = e->stg_n[r->g];
     pents = e->stg_ents + (size_t)r->g * e->c.max_entries_per_msg;
-    ppay = e->stg_pay + (size_t)r->g * e->c.max_entries_per_msg * e->c.payload_bytes;
+    ppay = e->stg_pay + (size_t)r->g * e->c.max_entries_per_msg * e->maxc;
   }
   if (pn > 0) {
     msg_in_t mi;
@@ -998,6 +1029,8 @@ static void step_replica(or_engine* e, rep_t* r) {
     }
   }
   r->cap_base = marker_start;
+  r->lpg = r->nlpg;
+  r->fidx = r->marker != marker_start ? r->marker + 1 : 0;
 }
 
 typedef struct {
@@ -1100,7 +1133,7 @@ int or_propose(or_engine* e, const or_proposal* p, size_t n, const uint8_t* payl
       break;
     }
     for (uint64_t j = p[i].first; j < p[i].first + p[i].count; ++j)
-      if (lens && lens[j] > P) rc = -1;
+      if (lens && lens[j] > e->maxc) rc = -1;
     uint32_t g = (uint32_t)(p[i].group - e->c.group_base);
     if (!rc && cnt[g] && slot[g] != p[i].slot) rc = -3;
     if (!rc && cnt[g] + p[i].count > E) rc = -3;
@@ -1117,9 +1150,9 @@ int or_propose(or_engine* e, const or_proposal* p, size_t n, const uint8_t* payl
         uint64_t j = p[i].first + k, at = (uint64_t)g * E + e->stg_n[g] + k;
         uint32_t len = lens ? lens[j] : 0;
         e->stg_ents[at].len = len;
-        uint8_t* d = e->stg_pay + at * P;
+        uint8_t* d = e->stg_pay + at * e->maxc;
         if (P) {
-          memset(d, 0, P);
+          memset(d, 0, e->maxc);
           if (len) memcpy(d, payload + off[j], len);
         }
       }
@@ -1146,14 +1179,24 @@ int or_create(const or_config* cfg, or_engine** out) {
   if (c->max_msgs_per_pair < 1 || c->max_msgs_per_pair > 16) return -1;
   if (c->num_slabs < 2 || c->election_rtt < 1 || c->heartbeat_rtt < 1) return -1;
   if (c->initial_members >> c->replicas) return -1;
+  if (c->join_slots >> c->replicas || (c->initial_members & c->join_slots)) return -1;
+  uint32_t maxc = c->max_cmd_bytes ? c->max_cmd_bytes : c->payload_bytes;
+  if (c->payload_bytes ? (maxc < c->payload_bytes || maxc > 8191) : maxc != 0) return -1;
   or_engine* e = (or_engine*)calloc(1, sizeof *e);
   e->c = *c;
   e->nrep = c->groups * c->replicas;
+  e->maxc = maxc;
+  { /* stream_pages as rg_create sizes it */
+    uint64_t full = ((uint64_t)c->log_capacity * ((c->payload_bytes + 15) & ~15u) + 4095) / 4096;
+    uint32_t pts = 16;
+    while (pts < 2 * full) pts <<= 1;
+    e->pts = c->payload_bytes ? (c->stream_pages ? c->stream_pages : pts) : 1;
+  }
   e->stg_slot = (uint8_t*)malloc(c->groups);
   memset(e->stg_slot, 0xFF, c->groups);
   e->stg_n = (uint32_t*)calloc(c->groups, 4);
   e->stg_ents = (ent_t*)calloc((size_t)c->groups * c->max_entries_per_msg, sizeof(ent_t));
-  e->stg_pay = (uint8_t*)calloc((size_t)c->groups * c->max_entries_per_msg * (c->payload_bytes ? c->payload_bytes : 1), 1);
+  e->stg_pay = (uint8_t*)calloc((size_t)c->groups * c->max_entries_per_msg * (maxc ? maxc : 1), 1);
   e->rd_req = (uint64_t*)calloc((size_t)c->groups * c->replicas, 8);
   e->cc_slot = (uint8_t*)malloc(c->groups);
   memset(e->cc_slot, 0xFF, c->groups);
@@ -1164,10 +1207,10 @@ int or_create(const or_config* cfg, or_engine** out) {
     r->g = i / c->replicas;
     r->s = i % c->replicas;
     r->log = (ent_t*)calloc(c->log_capacity, sizeof(ent_t));
-    if (c->payload_bytes) r->logpay = (uint8_t*)calloc((size_t)c->log_capacity, c->payload_bytes);
+    if (c->payload_bytes) r->logpay = (uint8_t*)calloc((size_t)c->log_capacity, maxc);
     /* pre-fault the rings so timed ticks do not pay first-touch page faults */
     memset(r->log, 0, (size_t)c->log_capacity * sizeof(ent_t));
-    if (r->logpay) memset(r->logpay, 0, (size_t)c->log_capacity * c->payload_bytes);
+    if (r->logpay) memset(r->logpay, 0, (size_t)c->log_capacity * maxc);
     for (int b = 0; b < 2; ++b)
       r->ob[b].m = (msg_t*)calloc((size_t)c->replicas * c->max_msgs_per_pair, sizeof(msg_t));
   }
@@ -1199,29 +1242,39 @@ void or_destroy(or_engine* e) {
 }
 
 /* peer.go Launch(newNode) → becomeFollower(1, NoLeader); bootstrap(addresses) (A.2) */
+/* A joining replica (join_slots; StartOnDiskReplica with join = true, raft/raft_manager.go:134-144)
+ * starts with an empty log at term 0 and no membership: becomeFollower(0, NoLeader). The others
+ * bootstrap with one ConfigChange entry per slot at term 1 — AddNode(s) for each initial member,
+ * descriptor 0 for the other slots — committed. */
 int or_bootstrap(or_engine* e) {
   uint32_t R = e->c.replicas;
+  uint32_t im = (e->c.initial_members ? e->c.initial_members : (1u << R) - 1u) & ~e->c.join_slots;
   for (uint32_t i = 0; i < e->nrep; ++i) {
     rep_t* r = &e->reps[i];
+    int joining = (e->c.join_slots >> r->s) & 1u;
     r->term = 0;
     r->last = r->marker = r->marker_term = r->committed = r->applied = r->processed = 0;
     r->snap_index = r->snap_term = r->cap_base = 0;
     r->err = r->drops = 0;
     r->rng_ctr = 0;
-    r->members = r->snap_members = e->c.initial_members ? e->c.initial_members : (1u << R) - 1u;
-    become_follower(e, r, 1, 0);
-    for (uint32_t k = 0; k < R; ++k) {
+    r->hw = r->lpg = r->nlpg = 0;
+    r->fidx = 0;
+    r->members = r->snap_members = joining ? 0u : im;
+    become_follower(e, r, joining ? 0 : 1, 0);
+    uint32_t last = joining ? 0 : R;
+    for (uint32_t k = 0; k < last; ++k) {
       ent_t* en = log_at(e, r, k + 1);
       en->term = 1;
       en->type = OR_ENTRY_CONFIG;
-      en->len = 0;
+      en->len = ((im >> k) & 1u) ? OR_CC(OR_CC_ADD, k) : 0u;
       en->crc = 0;
+      en->pos = 0;
     }
-    r->last = R;
-    r->committed = R;
+    r->last = last;
+    r->committed = last;
     for (uint32_t k = 0; k < R; ++k) { /* addNode → setRemote(id, 0, last+1) */
       r->match[k] = 0;
-      r->next[k] = R + 1;
+      r->next[k] = last + 1;
       r->rsnap[k] = 0;
       r->rstate[k] = OR_RETRY;
     }
@@ -1321,7 +1374,7 @@ int or_import_replica(or_engine* e, uint32_t rid, const or_replica_view* v, cons
   if (v->last < v->marker || v->last - v->marker > e->c.log_capacity) return -1;
   if (lens)
     for (uint64_t k = 0; k < v->last - v->marker; ++k)
-      if (lens[k] > e->c.payload_bytes && !(types && (types[k] & 0xFFu) == OR_ENTRY_CONFIG)) return -1;
+      if (lens[k] > e->maxc && !(types && (types[k] & 0xFFu) == OR_ENTRY_CONFIG)) return -1;
   r->term = v->term;
   r->vote = v->vote;
   r->leader = v->leader;
@@ -1357,22 +1410,27 @@ int or_import_replica(or_engine* e, uint32_t rid, const or_replica_view* v, cons
     r->rstate[k] = v->rstate[k];
   }
   uint32_t P = e->c.payload_bytes;
+  r->hw = r->lpg = r->nlpg = 0; /* a fresh payload stream (rg_import_replica) */
+  r->fidx = 0;
   for (uint64_t i = v->marker + 1; i <= v->last; ++i) {
     uint64_t k = i - v->marker - 1;
     ent_t* en = log_at(e, r, i);
     en->term = terms[k];
     en->type = types ? (types[k] & 0xFFu) : OR_ENTRY_APP;
+    en->pos = r->hw;
     uint32_t len = lens ? lens[k] : P;
     if (payloads && P && len && en->type == OR_ENTRY_APP && !(types && (types[k] & OR_ENTRY_EMPTY))) {
       en->len = len;
-      memset(logpay_at(e, r, i), 0, P);
-      memcpy(logpay_at(e, r, i), payloads + k * P, len);
+      memset(logpay_at(e, r, i), 0, e->maxc);
+      memcpy(logpay_at(e, r, i), payloads + k * e->maxc, len);
       en->crc = entry_crc(e, logpay_at(e, r, i), len);
+      r->hw += chunks_of(len);
     } else {
       en->len = en->type == OR_ENTRY_CONFIG && lens ? lens[k] : 0; /* a ConfigChange keeps its descriptor */
       en->crc = 0;
     }
   }
+  r->lpg = r->nlpg = 0;
   return 0;
 }
 
@@ -1392,8 +1450,7 @@ int or_deliver(or_engine* e, uint32_t rid_src, const or_msg_view* m) {
     for (uint32_t k = 0; k < m->nent; ++k) {
       ob->ents[ob->n_ents + k] = *log_at(e, r, m->log_index + 1 + k);
       if (e->c.payload_bytes)
-        memcpy(ob->pay + (ob->n_ents + k) * e->c.payload_bytes, logpay_at(e, r, m->log_index + 1 + k),
-               e->c.payload_bytes);
+        memcpy(ob->pay + (ob->n_ents + k) * e->maxc, logpay_at(e, r, m->log_index + 1 + k), e->maxc);
     }
     ob->n_ents += m->nent;
   }
@@ -1439,8 +1496,7 @@ int or_get_applied(const or_engine* e, uint32_t rid, uint64_t* index, or_entry_v
         out[n].crc = en->crc;
         out[n]._pad = 0;
       }
-      if (payload && e->c.payload_bytes)
-        memcpy(payload + (size_t)n * e->c.payload_bytes, logpay_at(e, r, i), e->c.payload_bytes);
+      if (payload && e->c.payload_bytes) memcpy(payload + (size_t)n * e->maxc, logpay_at(e, r, i), e->maxc);
     }
     n++;
   }

@@ -34,6 +34,8 @@ class Config(C.Structure):
         ("snapshot_entries", C.c_uint32), ("compaction_overhead", C.c_uint32),
         ("drop_ppm", C.c_uint32), ("group_base", C.c_uint32), ("seed", C.c_uint64),
         ("crc32c", C.c_uint32), ("apply_feedback", C.c_uint32), ("initial_members", C.c_uint32),
+        ("max_cmd_bytes", C.c_uint32), ("stream_pages", C.c_uint32), ("join_slots", C.c_uint32),
+        ("_pad", C.c_uint32),
     ]
 
 
@@ -80,6 +82,7 @@ class TickInput(C.Structure):
 
 
 REPLICA_FIELDS = [f for f, _ in ReplicaView._fields_ if not f.startswith("_")]
+CONFIG_KEYS = {f for f, _ in Config._fields_}
 CC_ADD, CC_REMOVE = 1, 2  # OR_CC_ADD / OR_CC_REMOVE
 
 
@@ -148,9 +151,14 @@ def default_config(**kw) -> dict:
     c = dict(groups=4, replicas=3, log_capacity=2048, payload_bytes=256, max_entries_per_msg=64,
              max_msgs_per_pair=8, num_slabs=2, election_rtt=10, heartbeat_rtt=1, check_quorum=1,
              snapshot_entries=1000, compaction_overhead=5, drop_ppm=0, seed=0x5EED, group_base=0, crc32c=0,
-             apply_feedback=0, initial_members=0)
+             apply_feedback=0, initial_members=0, max_cmd_bytes=0, stream_pages=0, join_slots=0)
     c.update(kw)
     return c
+
+
+def max_cmd(cfg: dict) -> int:
+    """The longest Cmd (and payload row stride) of a configuration: max_cmd_bytes, or payload_bytes."""
+    return cfg.get("max_cmd_bytes", 0) or cfg["payload_bytes"]
 
 
 def make_config(d: dict) -> Config:
@@ -195,7 +203,8 @@ class Oracle:
         self.cfg = default_config(**cfg)
         self.L = lib()
         self.h = C.c_void_p()
-        rc = self.L.or_create(C.byref(make_config(self.cfg)), C.byref(self.h))
+        rc = self.L.or_create(C.byref(make_config({k: v for k, v in self.cfg.items() if k in CONFIG_KEYS})),
+                              C.byref(self.h))
         if rc != 0:
             raise ValueError(f"or_create rejected config {self.cfg}")
         self.G, self.R = self.cfg["groups"], self.cfg["replicas"]
@@ -263,13 +272,13 @@ class Oracle:
         ev = EntryView()
         pay = None
         if with_payload and self.cfg["payload_bytes"]:
-            pay = (C.c_uint8 * self.cfg["payload_bytes"])()
+            pay = (C.c_uint8 * max_cmd(self.cfg))()
         rc = self.L.or_get_entry(self.h, rid, index, C.byref(ev), pay)
         if rc != 0:
             return None
         d = dict(term=ev.term, type=ev.type, len=ev.len, crc=ev.crc)
         if pay is not None:
-            d["payload"] = bytes(pay[:ev.len])
+            d["payload"] = bytes(pay[:ev.len]) if ev.type == 0 else b""  # ConfigChange: len = descriptor
         return d
 
     def applied_entries(self, rid):
@@ -278,7 +287,7 @@ class Oracle:
         n = self.L.or_get_applied(self.h, rid, None, None, None, 0)
         if n <= 0:
             return []
-        P = self.cfg["payload_bytes"]
+        P = max_cmd(self.cfg)
         idx = (C.c_uint64 * n)()
         ev = (EntryView * n)()
         pay = (C.c_uint8 * max(1, n * P))()

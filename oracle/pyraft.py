@@ -61,11 +61,16 @@ def msg(type, to, **kw):
 
 
 class Entry:
-    __slots__ = ("term", "type", "data", "crc", "cc")
+    __slots__ = ("term", "type", "data", "crc", "cc", "pos")
 
     def __init__(self, term, type=0, data=b"", cc=0):
         self.term, self.type, self.data, self.cc = term, type, data, cc
         self.crc = zlib.crc32(data) if data else 0
+        self.pos = 0  # payload stream position (16-B chunks) in the log that holds it
+
+    @property
+    def chunks(self):
+        return (len(self.data) + 15) // 16 if self.type == 0 else 0
 
     @property
     def len(self):
@@ -146,6 +151,8 @@ class Replica:
         self.snap_members = set(range(sim.R))
         self.cc_pending = False
         self.restored_at = 0
+        # payload stream: next free chunk, lowest page held, the last step's compaction bound
+        self.hw = self.lpg = self.nlpg = self.fidx = 0
 
     @property
     def quorum(self):
@@ -166,6 +173,18 @@ class Replica:
     def up_to_date(self, i, t):
         lt = self.term_at(self.last)
         return t > lt or (t == lt and i >= self.last)
+
+    def stream_fits(self, chunks):
+        """The stream capacity rule: the append's last chunk within stream_pages of the lowest page held."""
+        if chunks == 0:
+            return True
+        return (((self.hw + chunks - 1) & 0xFFFFFFFF) >> 8) - self.lpg & 0xFFFFFF < self.sim.pts
+
+    def put(self, e):
+        """Append Entry e to the log at the stream's end."""
+        e.pos = self.hw
+        self.hw = (self.hw + e.chunks) & 0xFFFFFFFF
+        self.log.append(e)
 
     def commit_to(self, i):
         if i <= self.committed:
@@ -233,11 +252,13 @@ class Replica:
         c = self.sim.cfg
         if self.last + n > self.cap_base + c["log_capacity"]:
             return False
+        if not cc and not self.stream_fits(sum((len(x) + 15) // 16 for x in cmds[:n])):
+            return False
         for k in range(n):
             if cc:
-                self.log.append(Entry(self.term, 1, b"", cc))
+                self.put(Entry(self.term, 1, b"", cc))
             else:
-                self.log.append(Entry(self.term, 0, cmds[k] if k < len(cmds) else b""))
+                self.put(Entry(self.term, 0, cmds[k] if k < len(cmds) else b""))
         self.remotes[self.s].try_update(self.last)
         if len(self.members) == 1:
             self.try_commit()
@@ -361,7 +382,8 @@ class Replica:
             last_new = m["log_index"] + n
             if conflict is not None:
                 ci = m["log_index"] + 1 + conflict
-                if ci > self.committed and last_new > self.cap_base + self.sim.cfg["log_capacity"]:
+                if ci > self.committed and (last_new > self.cap_base + self.sim.cfg["log_capacity"] or
+                                            not self.stream_fits(sum(e.chunks for e in m["ents"][conflict:]))):
                     self.drops += 1
                     return
                 if ci <= self.committed:
@@ -372,7 +394,7 @@ class Replica:
                         ne = Entry(e.term, e.type, e.data, e.cc)
                         if ne.crc != e.crc:
                             self.err |= ERR_CRC
-                        self.log.append(ne)
+                        self.put(ne)
             self.commit_to(min(last_new, m["commit"]))
             resp["log_index"] = last_new
         else:
@@ -471,10 +493,11 @@ class Replica:
             if role != LEADER and self.s in self.members and not self.committed > self.applied:
                 self.campaign()
         elif t == LEADER_HEARTBEAT:
-            if role == LEADER:
+            if role == LEADER:  # a pending ReadIndex rides on every heartbeat (readIndex.peepCtx)
+                ctx = self.pending_read[0] if self.pending_read is not None else 0
                 for i in range(self.sim.R):
                     if i != self.s and i in self.members:
-                        self.send(msg(HEARTBEAT, i + 1, commit=min(self.remotes[i].match, self.committed)))
+                        self.send(msg(HEARTBEAT, i + 1, commit=min(self.remotes[i].match, self.committed), hint=ctx))
         elif t == CHECK_QUORUM:
             if role == LEADER:
                 c_act = len((self.active | {self.s}) & self.members)
@@ -578,6 +601,13 @@ class Sim:
         from .pyoracle import default_config  # same defaults; no code shared with oracle.c
         self.cfg = default_config(**cfg)
         self.G, self.R = self.cfg["groups"], self.cfg["replicas"]
+        P, L = self.cfg["payload_bytes"], self.cfg["log_capacity"]
+        self.maxc = self.cfg.get("max_cmd_bytes", 0) or P
+        full = (L * ((P + 15) // 16 * 16) + 4095) // 4096
+        pts = 16
+        while pts < 2 * full:
+            pts <<= 1
+        self.pts = (self.cfg.get("stream_pages", 0) or pts) if P else 1
         self.t = 0
         self.isolate = None
         self.reps = [Replica(self, g, s) for g in range(self.G) for s in range(self.R)]
@@ -617,7 +647,7 @@ class Sim:
         for g, s, cmds in batches:
             if not (base <= g < base + self.G) or s >= self.R or not 1 <= len(cmds) <= E:
                 return -1
-            if any(len(x) > P for x in cmds):
+            if any(len(x) > self.maxc for x in cmds):
                 return -1
             lg = g - base
             if lg in new and new[lg][1] and new[lg][0] != s:
@@ -646,16 +676,23 @@ class Sim:
         return False
 
     def bootstrap(self):
+        """A joining slot (join_slots) starts empty at term 0 with no membership; the others with one
+        ConfigChange entry per slot at term 1: AddNode(s) for each initial member, 0 for the rest."""
         R = self.R
-        im = self.cfg.get("initial_members", 0) or (1 << R) - 1
+        js = self.cfg.get("join_slots", 0)
+        im = (self.cfg.get("initial_members", 0) or (1 << R) - 1) & ~js
         for r in self.reps:
+            joining = js >> r.s & 1
             r.rng = 0
-            r.members = {k for k in range(R) if im >> k & 1}
+            r.hw = r.lpg = r.nlpg = r.fidx = 0
+            r.members = set() if joining else {k for k in range(R) if im >> k & 1}
             r.snap_members = set(r.members)
-            r.become_follower(1, 0)
-            r.log = [Entry(1, 1) for _ in range(R)]
-            r.committed = R
-            r.remotes = [Remote(0, R + 1) for _ in range(R)]
+            r.log = []
+            r.become_follower(0 if joining else 1, 0)
+            last = 0 if joining else R
+            r.log = [Entry(1, 1, b"", (CC_ADD << 4 | (k + 1)) if im >> k & 1 else 0) for k in range(last)]
+            r.committed = last
+            r.remotes = [Remote(0, last + 1) for _ in range(R)]
             r.out, r.emitted = {}, {}
         self.t = 0
 
@@ -680,6 +717,9 @@ class Sim:
                 r = self.reps[g * self.R + s]
                 marker_start, processed_start = r.marker, r.processed
                 r.restored_at = 0
+                r.nlpg = r.lpg  # the pages below the last step's compaction go back when this step ends
+                if r.fidx:
+                    r.nlpg = (r.log[r.fidx - r.marker - 1].pos if r.fidx <= r.last else r.hw) >> 8
                 for _, lst in r._inbox:
                     for m in lst:
                         r.handle(m)
@@ -723,6 +763,8 @@ class Sim:
                         del r.log[:cpt - r.marker]
                         r.marker, r.marker_term = cpt, mt
                 r.cap_base = marker_start
+                r.lpg = r.nlpg
+                r.fidx = r.marker + 1 if r.marker != marker_start else 0
         self.t += 1
 
     # views
@@ -749,7 +791,7 @@ class Sim:
     # -- scenario helpers (KATs): same contract as or_import_replica / or_deliver --
     def import_replica(self, rid, view: dict, terms, types=None, payloads=None, lens=None):
         r = self.reps[rid]
-        P = self.cfg["payload_bytes"]
+        P, row = self.cfg["payload_bytes"], self.maxc
         for k in ("term", "vote", "leader", "committed", "applied", "processed", "marker", "marker_term",
                   "snap_index", "snap_term", "cap_base", "role", "err", "drops"):
             setattr(r, k, view.get(k, 0))
@@ -766,12 +808,13 @@ class Sim:
         r.snap_members = {k for k in range(8) if view.get("snap_members", view.get("members", (1 << self.R) - 1)) >> k & 1}
         r.cc_pending = bool(view.get("cc_pending", 0))
         r.log = []
+        r.hw = r.lpg = r.nlpg = r.fidx = 0  # a fresh payload stream (rg_import_replica)
         for k, t in enumerate(terms):
             ty = 0 if types is None else types[k] & 0xFF
             ln = P if lens is None else lens[k]
             empty = types is not None and types[k] & 0x100
-            data = payloads[k * P:k * P + ln] if (payloads is not None and P and ty == 0 and not empty) else b""
-            r.log.append(Entry(t, ty, bytes(data), ln if ty == 1 and lens is not None else 0))
+            data = payloads[k * row:k * row + ln] if (payloads is not None and P and ty == 0 and not empty) else b""
+            r.put(Entry(t, ty, bytes(data), ln if ty == 1 and lens is not None else 0))
         assert r.last == view.get("last", r.last)
         r.remotes = []
         for k in range(self.R):

@@ -61,9 +61,14 @@ __global__ void gather_msgs_kernel(AdminParams a, uint32_t rid, uint32_t dst, ui
   const uint64_t* h = t.hdr_in + (((uint64_t)s * t.R + dst) * t.K + k) * t.G + g;
   const uint64_t* mt = t.mt_in + ((((uint64_t)s * t.R + dst) * t.K + k) * t.E) * t.G + g;
   const uint32_t type = (uint32_t)(h[0] & 0xFF), n = (uint32_t)(h[0] >> 32);
-  // a uniform Replicate (RG_UNIFORM in word 7) is shown expanded, as the message it encodes
+  // a uniform Replicate (RG_UNIFORM in word 7, its Cmds' stream position in word 5) is shown
+  // expanded, as the message it encodes
   const bool uni = type == M_REPLICATE && ((uint32_t)h[7 * plane] & RG_UNIFORM);
-  for (int w = 0; w < 8; ++w) out_hdr[k * 8 + w] = h[w * plane] & (w == 7 && uni ? ~(uint64_t)RG_UNIFORM : ~0ull);
+  // a Propose's word 4 carries its batch's stream layout (raftgpu_control.h), not a commit index
+  const bool prop = type == M_PROPOSE;
+  for (int w = 0; w < 8; ++w)
+    out_hdr[k * 8 + w] = (uni && w == 5) || (prop && w == 4) ? 0ull
+                                                             : h[w * plane] & (w == 7 && uni ? ~(uint64_t)RG_UNIFORM : ~0ull);
   for (uint32_t e = 0; e < t.E; ++e)
     out_terms[(uint64_t)k * t.E + e] =
         (type == M_REPLICATE && e < n) ? (mt[uni ? 0 : (uint64_t)e * t.G] & TERM_MASK) : 0;
@@ -76,6 +81,7 @@ hipError_t launch_gather_msgs(const AdminParams& a, uint32_t rid, uint32_t dst, 
   return hipGetLastError();
 }
 
+// one thread per entry: its view, and its Cmd into a row of `row` bytes (read through the stream's pages)
 __global__ void gather_entries_kernel(AdminParams a, uint32_t rid, uint64_t first, uint32_t n, rg_entry_view* out,
                                       uint8_t* out_pay) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -90,13 +96,14 @@ __global__ void gather_entries_kernel(AdminParams a, uint32_t rid, uint64_t firs
   v.term = w & TERM_MASK;
   v.type = (uint32_t)((w >> 61) & 1);
   v.len = (w & (PAY_BIT | TYPE_BIT)) ? word_len(w) : 0u;  // a ConfigChange reports its descriptor
-  v.crc = (w & PAY_BIT) ? crc_of_cmd(inf.x, v.len, t.P, a.zi) : 0u;  // the ring keeps the slot CRC
+  v.crc = (w & PAY_BIT) ? crc_of_cmd(inf.x, v.len, t.P, a.zi) : 0u;  // the info word keeps the slot CRC
   v.bank = (uint32_t)bank;
   out[i] = v;
-  if (out_pay && t.P && v.len) {
-    const uint8_t* src = a.pay + ((bank * t.nrep + q) * t.L + slot) * t.P;
-    for (uint32_t b = 0; b < v.len; ++b) out_pay[(uint64_t)i * t.P + b] = src[b];
-  }
+  if (out_pay && (w & PAY_BIT))
+    for (uint32_t b = 0; b < v.len; ++b) {
+      const uint8_t* src = a.pool + stream_byte(a.pt, a.PTS, q, inf.y + (b >> 4));
+      out_pay[(uint64_t)i * a.row + b] = src[b & 15];
+    }
 }
 
 hipError_t launch_gather_entries(const AdminParams& a, uint32_t rid, uint64_t first, uint32_t n, void* out,
@@ -106,23 +113,58 @@ hipError_t launch_gather_entries(const AdminParams& a, uint32_t rid, uint64_t fi
   return hipGetLastError();
 }
 
-// import: view + entry words (term|len|type|pay, bank 0) + payloads (zero-padded P-byte rows) + slot
-// CRCs into the current state
-__global__ void scatter_replica_kernel(AdminParams a, uint32_t rid, const rg_replica_view* vv, const uint64_t* words,
-                                       const uint8_t* pays, const uint32_t* crcs, uint32_t nent, uint2* info,
-                                       uint8_t* pay) {
+// import (one block): the view into the current state; the replica's old stream pages back to the
+// free ring; a fresh stream of ceil(nch / 256) pages (the head taken by compare-and-swap, so an empty
+// pool changes nothing); then every entry's ring word, info {slot crc, position} and Cmd chunks
+__global__ void __launch_bounds__(256) scatter_replica_kernel(AdminParams a, uint32_t rid, const rg_replica_view* vv,
+                                                              const uint64_t* words, const uint32_t* crcs,
+                                                              const uint32_t* pos, const uint8_t* chunks,
+                                                              uint32_t nent, uint32_t nch, uint32_t* status) {
   const TickParams& t = a.t;
   const uint32_t q = q_of(t, rid);
   const uint64_t N = t.nrep;
   const rg_replica_view& v = *vv;
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i == 0) {
-    uint64_t* s64 = ((uint64_t*)(t.s64_in)) + q;
-    uint32_t* s32 = ((uint32_t*)(t.s32_in)) + q;
+  uint32_t* s32 = ((uint32_t*)(t.s32_in)) + q;
+  uint64_t* s64 = ((uint64_t*)(t.s64_in)) + q;
+  __shared__ uint32_t ok;
+  const uint32_t np = t.P ? vpn_ceil(nch) : 0u;
+  if (threadIdx.x == 0) {
+    ok = 1;
+    if (t.P) {
+      PoolCtl* c = a.poolctl;
+      unsigned long long h = c->head;
+      for (;;) {  // take np ids below limit (written by earlier launches)
+        if (h + np > c->limit) {
+          ok = 0;
+          break;
+        }
+        const unsigned long long seen = atomicCAS(&c->head, h, h + np);
+        if (seen == h) break;
+        h = seen;
+      }
+      if (ok) {
+        const uint32_t lpg = s32[S_LPG * N], apg = s32[S_APG * N], f = vpn_diff(apg, lpg);
+        uint32_t* ptq = a.pt + (uint64_t)q * a.PTS;
+        const unsigned long long fb = f ? atomicAdd(&c->tail, (unsigned long long)f) : 0ull;
+        for (uint32_t k = 0; k < f; ++k) a.fring[(fb + k) % a.npages] = ptq[(lpg + k) & (a.PTS - 1)];
+        for (uint32_t k = 0; k < np; ++k) ptq[k & (a.PTS - 1)] = a.fring[(h + k) % a.npages];
+        s32[S_HW * N] = nch;
+        s32[S_LPG * N] = 0;
+        s32[S_APG * N] = np;
+        s32[S_NLPG * N] = 0;
+      } else {
+        *status = 1;
+      }
+    }
+  }
+  __syncthreads();
+  if (!ok) return;
+  if (threadIdx.x == 0) {
     s64[S_TERM * N] = v.term; s64[S_VOTE * N] = v.vote; s64[S_LEADER * N] = v.leader;
     s64[S_COMMITTED * N] = v.committed; s64[S_APPLIED * N] = v.applied; s64[S_LAST * N] = v.last;
     s64[S_MARKER * N] = v.marker; s64[S_MARKER_TERM * N] = v.marker_term; s64[S_SNAP_INDEX * N] = v.snap_index;
     s64[S_SNAP_TERM * N] = v.snap_term; s64[S_CAP_BASE * N] = v.cap_base; s64[S_PROCESSED * N] = v.processed;
+    s64[S_FIDX * N] = 0;
     s32[S_ROLE * N] = v.role; s32[S_ETICK * N] = v.election_tick; s32[S_HTICK * N] = v.heartbeat_tick;
     s32[S_RAND_TO * N] = v.rand_timeout; s32[S_RNG_CTR * N] = v.rng_ctr; s32[S_GRANTED * N] = v.granted;
     s32[S_RESPONDED * N] = v.responded; s32[S_ACTIVE * N] = v.active; s32[S_ERR * N] = v.err;
@@ -138,22 +180,22 @@ __global__ void scatter_replica_kernel(AdminParams a, uint32_t rid, const rg_rep
       rst[j * N + q] = v.rstate[j];
     }
   }
-  if (i >= nent) return;
-  const uint64_t idx = v.marker + 1 + i, slot = idx & (t.L - 1);
-  const uint64_t w = words[i] & ~BANK_BIT;
-  t.tr[slot * N + q] = w;
-  const bool hp = (w >> 62) & 1;
-  info[(uint64_t)q * t.L + slot] = make_uint2(hp ? crcs[i] : 0u, ((uint32_t)((w >> 61) & 1) << 24) | (hp ? t.P : 0u));
-  if (hp)
-    for (uint32_t b = 0; b < t.P; ++b) pay[((uint64_t)q * t.L + slot) * t.P + b] = pays[(uint64_t)i * t.P + b];
+  for (uint32_t i = threadIdx.x; i < nent; i += blockDim.x) {
+    const uint64_t idx = v.marker + 1 + i, slot = idx & (t.L - 1);
+    const uint64_t w = words[i] & ~BANK_BIT;
+    t.tr[slot * N + q] = w;
+    const_cast<uint2*>(a.info)[(uint64_t)q * t.L + slot] = make_uint2((w & PAY_BIT) ? crcs[i] : 0u, pos[i]);
+  }
+  if (chunks)
+    for (uint32_t c = threadIdx.x; c < nch; c += blockDim.x)
+      *reinterpret_cast<uint4*>(a.pool + stream_byte(a.pt, a.PTS, q, c)) = reinterpret_cast<const uint4*>(chunks)[c];
 }
 
 hipError_t launch_scatter_replica(const AdminParams& a, uint32_t rid, const void* view, const uint64_t* words,
-                                  const uint8_t* pays, const uint32_t* crcs, uint32_t nent, hipStream_t s,
-                                  uint2* info, uint8_t* pay) {
-  const uint32_t n = nent > 0 ? nent : 1;
-  hipLaunchKernelGGL(scatter_replica_kernel, dim3((n + 63) / 64), dim3(64), 0, s, a, rid,
-                     (const rg_replica_view*)view, words, pays, crcs, nent, info, pay);
+                                  const uint32_t* crcs, const uint32_t* pos, const uint8_t* chunks, uint32_t nent,
+                                  uint32_t nch, uint32_t* status, hipStream_t s) {
+  hipLaunchKernelGGL(scatter_replica_kernel, dim3(1), dim3(256), 0, s, a, rid, (const rg_replica_view*)view, words,
+                     crcs, pos, chunks, nent, nch, status);
   return hipGetLastError();
 }
 

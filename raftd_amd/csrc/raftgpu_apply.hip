@@ -18,69 +18,110 @@ namespace rg {
 
 __device__ __forceinline__ bool applies(uint64_t w) { return !(w & TYPE_BIT) && (w & PAY_BIT); }
 
+__device__ __forceinline__ uint32_t lane_inc_scan(uint32_t v) {
+  const uint32_t lane = __lane_id();
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)v, o, 64);
+    if (lane >= o) v += y;
+  }
+  return v;
+}
+
+// The Cmds of up to 64 consecutive candidate entries of replica q, packed back to back: lane i holds
+// candidate i's inclusive chunk prefix inc (0 chunks if not selected) and its stream position sp;
+// chunk t of the run (t < total) belongs to the first candidate whose inc exceeds t (binary search
+// over lanes), and is copied from its stream into out + (base + t) · 16.
+__device__ __forceinline__ void copy_run(const uint8_t* pool, const uint32_t* pt, uint32_t PTS, uint32_t q,
+                                         uint32_t inc, uint32_t sp, uint32_t total, uint8_t* out, uint64_t base,
+                                         bool host) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const uint32_t lane = __lane_id();
+  for (uint32_t t = lane; t < ((total + 63) & ~63u); t += 64) {
+    uint32_t lo = 0;  // first lane with inc > t
+#pragma unroll
+    for (uint32_t step = 32; step; step >>= 1) {
+      const uint32_t v = (uint32_t)__shfl((int)inc, (int)(lo + step - 1), 64);
+      if (v <= t) lo += step;
+    }
+    const uint32_t ex = lo ? (uint32_t)__shfl((int)inc, (int)(lo - 1), 64) : 0u;
+    const uint32_t spl = (uint32_t)__shfl((int)sp, (int)(lo < 64 ? lo : 63), 64);
+    if (t < total) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(pool + stream_byte(pt, PTS, q, spl + (t - ex)));
+      u32x4* d = reinterpret_cast<u32x4*>(out + (base + t) * 16);
+      if (host) *d = v;
+      else __builtin_nontemporal_store(v, d);
+    }
+  }
+}
+
 __global__ void apply_count_kernel(ApplyParams a) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= a.nrep) return;
   const uint32_t s = q / a.G;
-  uint32_t c = 0;
+  uint32_t c = 0, cc = 0;
   if ((a.slot_mask >> s) & 1u) {
     const uint64_t hi = a.s64[(uint64_t)S_PROCESSED * a.nrep + q];
-    for (uint64_t i = a.apply_lo[q] > 0 ? a.apply_lo[q] : 1; i <= hi; ++i)
-      c += applies(a.tr[(i & (a.L - 1)) * a.nrep + q]) ? 1u : 0u;
+    for (uint64_t i = a.apply_lo[q] > 0 ? a.apply_lo[q] : 1; i <= hi; ++i) {
+      const uint64_t w = a.tr[(i & (a.L - 1)) * a.nrep + q];
+      if (applies(w)) {
+        c += 1;
+        cc += word_nc(w);
+      }
+    }
   }
   a.cnt[q] = c;
+  a.ccnt[q] = cc;
 }
 
 __global__ void apply_total_kernel(const uint64_t* off, uint32_t n, uint64_t* total) { *total = off[n]; }
+__global__ void totals2_kernel(const uint64_t* a, const uint64_t* b, uint32_t n, uint64_t* out) {
+  out[0] = a[n];
+  out[1] = b[n];
+}
 
-hipError_t launch_apply_count(const ApplyParams& a, uint64_t* total, hipStream_t st) {
+hipError_t launch_apply_count(const ApplyParams& a, uint64_t* totals, hipStream_t st) {
   hipLaunchKernelGGL(apply_count_kernel, dim3((a.nrep + 255) / 256), dim3(256), 0, st, a);
   hipError_t r = launch_scan_u32(a.cnt, a.nrep, a.bsum, a.off, st);
+  if (r == hipSuccess) r = launch_scan_u32(a.ccnt, a.nrep, a.bsum, a.coff, st);
   if (r != hipSuccess) return r;
-  hipLaunchKernelGGL(apply_total_kernel, dim3(1), dim3(1), 0, st, a.off, a.nrep, total);
+  hipLaunchKernelGGL(totals2_kernel, dim3(1), dim3(1), 0, st, a.off, a.coff, a.nrep, totals);
   return hipGetLastError();
 }
 
+// wave per replica: ballot-compacted records, then the Cmds of each run of 64 candidates packed
 __global__ void __launch_bounds__(256) apply_gather_kernel(ApplyParams a) {
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const uint32_t lane = __lane_id();
   const uint32_t q = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   if (q >= a.nrep || a.cnt[q] == 0) return;
   const uint32_t s = q / a.G, j = q - s * a.G;
-  const uint64_t n64 = a.nrep, L = a.L, P = a.P, nch = P / 16;
+  const uint64_t n64 = a.nrep, L = a.L;
   const uint64_t group = pl_group(a.pl, s, j);
   const uint64_t hi = a.s64[(uint64_t)S_PROCESSED * n64 + q];
-  uint64_t pos = a.off[q];
+  uint64_t pos = a.off[q], cpos = a.coff[q];
   for (uint64_t i0 = a.apply_lo[q] > 0 ? a.apply_lo[q] : 1; i0 <= hi; i0 += 64) {
     const uint64_t i = i0 + lane;
     const uint64_t slot = i & (L - 1);
     const uint64_t w = i <= hi ? a.tr[slot * n64 + q] : 0;
     const bool sel = i <= hi && applies(w);
     const uint64_t mask = __ballot(sel);
+    const uint2 inf = sel ? a.info[((w >> 63) * n64 + q) * L + slot] : make_uint2(0u, 0u);
+    const uint32_t nc = sel ? word_nc(w) : 0u, inc = lane_inc_scan(nc);
     if (sel) {
       const uint64_t k = pos + __builtin_popcountll(mask & ((1ull << lane) - 1));
-      const uint2 inf = a.info[((w >> 63) * n64 + q) * L + slot];
       rg_apply_entry r;
       r.index = i;
       r.group = group;
       r.replica_id = s + 1;
       r.len = word_len(w);
-      r.crc = crc_of_cmd(inf.x, r.len, a.P, a.zi);  // the ring keeps the slot CRC
+      r.crc = crc_of_cmd(inf.x, r.len, a.P, a.zi);  // the info word keeps the slot CRC
       r.rid = j * a.R + s;
+      r.off = (cpos + inc - nc) * 16;
       reinterpret_cast<rg_apply_entry*>(a.out_rec)[k] = r;
     }
-    // payloads: 16 B per lane over (candidate entry, chunk); unselected candidates idle
-    const uint64_t ncand = hi - i0 + 1 < 64 ? hi - i0 + 1 : 64;
-    for (uint64_t t = lane; t < ncand * nch; t += 64) {
-      const uint64_t e = t / nch, ch = t - e * nch;
-      if (!((mask >> e) & 1ull)) continue;
-      const uint64_t ie = i0 + e, se = ie & (L - 1);
-      const uint64_t we = a.tr[se * n64 + q];
-      const uint64_t k = pos + __builtin_popcountll(mask & ((1ull << e) - 1));
-      const u32x4 v = *reinterpret_cast<const u32x4*>(a.pay + (((we >> 63) * n64 + q) * L + se) * P + 16 * ch);
-      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(a.out_pay + k * P + 16 * ch));
-    }
+    const uint32_t total = (uint32_t)__shfl((int)inc, 63, 64);
+    copy_run(a.pool, a.pt, a.PTS, q, inc, inf.y, total, a.out_pay, cpos, a.out_host != 0);
     pos += __builtin_popcountll(mask);
+    cpos += total;
   }
 }
 
@@ -92,7 +133,8 @@ hipError_t launch_apply_gather(const ApplyParams& a, hipStream_t st) {
 // ================================================================== persistence (host WAL feed)
 // dragonboat persists Update.EntriesToSave + State{Term, Vote, Commit} (and a snapshot's index)
 // before a step's messages leave. Per replica whose log or hard state changed in the last tick:
-// one state record, and the entries it rewrote, [persist_lo, last] (full: the whole window).
+// one state record, and the entries it rewrote, [persist_lo, last] (full: the whole window), their
+// Cmds packed (rg_persist_entry.off).
 
 __device__ __forceinline__ uint64_t persist_first(const PersistParams& a, uint32_t q) {
   const uint64_t n = a.nrep, marker = a.s64[(uint64_t)S_MARKER * n + q];
@@ -109,19 +151,24 @@ __global__ void persist_count_kernel(PersistParams a) {
   const auto diff = [&](uint32_t f) { return a.s64[(uint64_t)f * n + q] != a.s64_prev[(uint64_t)f * n + q]; };
   const bool changed = a.full || ne > 0 || diff(S_TERM) || diff(S_VOTE) || diff(S_COMMITTED) || diff(S_LAST) ||
                        diff(S_MARKER) || diff(S_SNAP_INDEX);
+  uint32_t cc = 0;
+  for (uint64_t i = lo; i <= last; ++i) cc += word_nc(a.tr[(i & (a.L - 1)) * n + q]);
   a.scnt[q] = changed ? 1u : 0u;
   a.ecnt[q] = ne;
+  a.ccnt[q] = cc;
 }
 
 __global__ void persist_total_kernel(const PersistParams a, uint64_t* totals) {
   totals[0] = a.soff[a.nrep];
   totals[1] = a.eoff[a.nrep];
+  totals[2] = a.coff[a.nrep];
 }
 
 hipError_t launch_persist_count(const PersistParams& a, uint64_t* totals, hipStream_t st) {
   hipLaunchKernelGGL(persist_count_kernel, dim3((a.nrep + 255) / 256), dim3(256), 0, st, a);
   hipError_t r = launch_scan_u32(a.scnt, a.nrep, a.bsum, a.soff, st);
   if (r == hipSuccess) r = launch_scan_u32(a.ecnt, a.nrep, a.bsum, a.eoff, st);
+  if (r == hipSuccess) r = launch_scan_u32(a.ccnt, a.nrep, a.bsum, a.coff, st);
   if (r != hipSuccess) return r;
   hipLaunchKernelGGL(persist_total_kernel, dim3(1), dim3(1), 0, st, a, totals);
   return hipGetLastError();
@@ -153,19 +200,21 @@ __global__ void persist_state_kernel(PersistParams a) {
 }
 
 __global__ void __launch_bounds__(256) persist_entries_kernel(PersistParams a) {
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const uint32_t lane = __lane_id();
   const uint32_t q = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   if (q >= a.nrep || a.ecnt[q] == 0) return;
   const uint32_t s = q / a.G, j = q - s * a.G;
-  const uint64_t n64 = a.nrep, L = a.L, P = a.P, nch = P / 16;
+  const uint64_t n64 = a.nrep, L = a.L;
   const uint64_t lo = persist_first(a, q), hi = a.s64[(uint64_t)S_LAST * n64 + q];
   const uint64_t base = a.eoff[q];
+  uint64_t cpos = a.coff[q];
   for (uint64_t i0 = lo; i0 <= hi; i0 += 64) {
     const uint64_t i = i0 + lane;
-    if (i <= hi) {
-      const uint64_t slot = i & (L - 1), w = a.tr[slot * n64 + q];
-      const uint2 inf = a.info[((w >> 63) * n64 + q) * L + slot];
+    const bool in = i <= hi;
+    const uint64_t slot = i & (L - 1), w = in ? a.tr[slot * n64 + q] : 0;
+    const uint2 inf = in ? a.info[((w >> 63) * n64 + q) * L + slot] : make_uint2(0u, 0u);
+    const uint32_t nc = word_nc(w), inc = lane_inc_scan(nc);
+    if (in) {
       rg_persist_entry r;
       r.index = i;
       r.term = w & TERM_MASK;
@@ -173,16 +222,12 @@ __global__ void __launch_bounds__(256) persist_entries_kernel(PersistParams a) {
       r.len = (w & (PAY_BIT | TYPE_BIT)) ? word_len(w) : 0u;  // a ConfigChange: its descriptor
       r.crc = (w & PAY_BIT) ? crc_of_cmd(inf.x, r.len, a.P, a.zi) : 0u;
       r.rid = j * a.R + s;
+      r.off = (cpos + inc - nc) * 16;
       reinterpret_cast<rg_persist_entry*>(a.out_ent)[base + (i - lo)] = r;
     }
-    const uint64_t ncand = hi - i0 + 1 < 64 ? hi - i0 + 1 : 64;
-    for (uint64_t t = lane; t < ncand * nch; t += 64) {
-      const uint64_t e = t / nch, ch = t - e * nch, ie = i0 + e, se = ie & (L - 1);
-      const uint64_t we = a.tr[se * n64 + q];
-      if (!(we & PAY_BIT)) continue;
-      const u32x4 v = *reinterpret_cast<const u32x4*>(a.pay + (((we >> 63) * n64 + q) * L + se) * P + 16 * ch);
-      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(a.out_pay + (base + (ie - lo)) * P + 16 * ch));
-    }
+    const uint32_t total = (uint32_t)__shfl((int)inc, 63, 64);
+    copy_run(a.pool, a.pt, a.PTS, q, inc, inf.y, total, a.out_pay, cpos, false);
+    cpos += total;
   }
 }
 

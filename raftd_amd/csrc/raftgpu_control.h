@@ -94,7 +94,10 @@ RG_FN void sel_set(T (&a)[R], uint32_t f, V val) {
 
 template <int R>
 struct Ctl {
-  const TickParams p;  // by value: pointer fields stay kernel-argument (global) pointers
+  // the tick's parameter block, read in place at each use (a device slot the host filled): the
+  // fields are reloaded where needed instead of living in registers for the whole step (r02 kept a
+  // 368-B copy, 279 SGPR spills at R = 3)
+  const TickParams& p;
   uint32_t q, g, s;    // g = local column (indexes every device array)
   uint64_t gg, rid;    // global group and global replica id gg·R + s (RNG keys, loss hash)
   uint32_t gi;         // the global group as an index into this engine's tick-input arrays (< 2^32)
@@ -112,14 +115,18 @@ struct Ctl {
   uint64_t processed_start, restored_at;  // apply window: entries restored from a snapshot are not Update()d
   bool took;                            // a snapshot was taken at the end of this step
   uint64_t wlo;                         // lowest log index written this step (EntriesToSave from here)
-  // RG_CTL_FASTREP (ablation, see the top of this file). The leader's last append
+  // payload stream: hw = next free chunk. The lowest page held (S_LPG, the capacity
+  // rule's base, unchanged during a step) is read where an append needs it
+  uint32_t hw;
+  // RG_CTL_FASTREP (see the top of this file). The leader's last append
   // of this step when it wrote no protected index: entries
   // [la_base, la_base + la_n) all hold the ring word la_word (bank 0) and term(la_base − 1) = la_pt,
-  // so send_replicate builds a Replicate of them from registers instead of re-reading the ring.
-  // la_n = 0 when any other log write, reset or restore came after it.
+  // their Cmds start at stream chunk la_pos, so send_replicate builds a Replicate of them from
+  // registers instead of re-reading the ring. la_n = 0 when any other log write, reset or restore
+  // came after it.
 #ifdef RG_CTL_FASTREP
   uint64_t la_base, la_word, la_pt;
-  uint32_t la_n;
+  uint32_t la_n, la_pos;
 #endif
   uint64_t oc, em;  // per destination: enqueued / emitted counts, 8 bits each
   uint32_t nj;      // jobs emitted
@@ -142,6 +149,7 @@ struct Ctl {
     rng_ctr = b[S_RNG_CTR * n]; granted = b[S_GRANTED * n]; responded = b[S_RESPONDED * n];
     active = b[S_ACTIVE * n]; err = b[S_ERR * n]; drops = b[S_DROPS * n];
     members = b[S_MEMBERS * n]; snap_members = b[S_SNAP_MEMBERS * n]; cc_pending = b[S_CC_PENDING * n];
+    hw = b[S_HW * n];
     sfor<0, R>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       rm[j] = p.rem_in[(0 * R + j) * n + q];
@@ -153,8 +161,24 @@ struct Ctl {
     if (last > marker) lt_set(last, *tr_at(last) & TERM_MASK);  // issued early, used after the inbox headers
     last_start = last; sent_hi = 0; rw_lo = ~0ull; rw_hi = 0; marker_start = marker;
     processed_start = processed; restored_at = 0; wlo = ~0ull; took = false;
+    // the last step compacted (or restored) below entry fidx: its stream position bounds the pages
+    // to release, known now that the step which wrote it has stored its {crc, position} (the bulk
+    // kernel). They go back to the pool at the end of this step; the capacity rule keeps lpg until
+    // then, so a page read in this launch is never reassigned in it
+    {
+      uint32_t nlpg = b[S_LPG * n];
+      if (const uint64_t fi = a[S_FIDX * n]) {
+        uint32_t bound = hw;
+        if (fi <= last) {
+          const uint64_t sl = fi & (p.L - 1), bank = *tr_at(fi) >> 63;
+          bound = p.info[(bank * n + q) * p.L + sl].y;
+        }
+        nlpg = vpn_of(bound);
+      }
+      p.s32_out[S_NLPG * n + q] = nlpg;  // for pool_kernel, after this launch
+    }
 #ifdef RG_CTL_FASTREP
-    la_base = la_word = la_pt = 0; la_n = 0;
+    la_base = la_word = la_pt = 0; la_n = 0; la_pos = 0;
 #endif
     oc = 0; em = 0; nj = 0;
   }
@@ -326,24 +350,33 @@ struct Ctl {
     return false;
   }
 
-  // ---- log writes: term ring + banks, and a job for the bulk kernel
+  // ---- log writes: term ring + info banks, and a job for the bulk kernel
   // Entry e in [e0, n) goes to index base+e with ring word `word` | (the inline word mt[e·G] of a
   // Replicate or remote Propose, when mt is set) | (len_bits of slab Cmd e, li[e].y, when li is set).
-  // aux: the J_SMASK of a WIRE job (record offset) or a SLAB job (slab row).
+  // Its Cmd bytes go to this replica's payload stream at hw (back to back, whole chunks), and hw
+  // advances. aux: a WIRE job's record offset. uspos: a uniform Replicate's (mt and li unset, kind
+  // RING) stream position of message entry 0 at the sender, or a caller batch's (kind CMD) arena
+  // chunk of entry 0, ucmd = the batch is contiguous in its arena (rg_propose decides).
   RG_FN void write_entries(uint64_t base, uint32_t e0, uint32_t n, uint32_t kind, uint32_t src,
-                                const uint64_t* mt, uint64_t word, uint64_t aux = 0, const uint2* li = nullptr) {
+                           const uint64_t* mt, uint64_t word, uint64_t aux = 0, const uint2* li = nullptr,
+                           uint32_t uspos = 0, bool ucmd = false) {
     RG_T0(t0);
-    write_entries_(base, e0, n, kind, src, mt, word, aux, li);
+    write_entries_(base, e0, n, kind, src, mt, word, aux, li, uspos, ucmd);
     RG_ACC(3, t0);
   }
   RG_FN void write_entries_(uint64_t base, uint32_t e0, uint32_t n, uint32_t kind, uint32_t src,
-                                const uint64_t* mt, uint64_t word, uint64_t aux, const uint2* li) {
+                            const uint64_t* mt, uint64_t word, uint64_t aux, const uint2* li, uint32_t uspos,
+                            bool ucmd) {
     const uint64_t hi_prot = umax64(last_start, sent_hi);
 #ifdef RG_CTL_FASTREP
     la_n = 0;
 #endif
     wlo = umin64(wlo, base + e0);
-    uint64_t dm = 0, sm = 0, hm = 0, tm = 0;
+    uint64_t dm = 0, sm = 0, tm = 0;
+    // stream layout: tot chunks in all; uniform = every entry the same chunk count ncu (and, for caller
+    // Cmds, contiguous in their arena) so the bulk kernel addresses them arithmetically
+    uint32_t tot = 0, ncu = 0;
+    bool same = true;
 #ifdef RG_CTL_FRESH
     if (base + e0 > hi_prot) {
       // Fast path (the steady state): every index is fresh — bank 0, no old word to load, no hull.
@@ -356,8 +389,9 @@ struct Ctl {
       if (!mt && !li) {  // one word for every entry: a leader's batch of synthetic Cmds, or its no-op
         const uint64_t M = (n - e0 >= 64 ? ~0ull : (1ull << (n - e0)) - 1) << e0;
         sm = (word & BANK_BIT) ? M : 0ull;
-        hm = (word & PAY_BIT) ? M : 0ull;
         tm = (word & TYPE_BIT) ? M : 0ull;
+        ncu = word_nc(word);
+        tot = ncu * (n - e0);
         const uint64_t wr = word & ~BANK_BIT;
         if (n > e0) lt_set(base + n - 1, word & TERM_MASK);
         for (uint32_t e = e0; e < n; ++e) {
@@ -380,8 +414,11 @@ struct Ctl {
             if (e + k >= n) break;
             const uint64_t w = wv[k];
             if (e + k == n - 1) lt_set(base + n - 1, w & TERM_MASK);
+            const uint32_t nc = word_nc(w);
+            if (e + k == e0) ncu = nc;
+            same = same && nc == ncu;
+            tot += nc;
             sm |= (w & BANK_BIT) ? bit : 0ull;
-            hm |= (w & PAY_BIT) ? bit : 0ull;
             tm |= (w & TYPE_BIT) ? bit : 0ull;
             *dst = w & ~BANK_BIT;
             dst += step;
@@ -414,14 +451,17 @@ struct Ctl {
         const uint32_t ek = e + k;
         const uint64_t idx = base + ek, w = wv[k];
         if (ek == n - 1) lt_set(idx, w & TERM_MASK);
+        const uint32_t nc = word_nc(w);
+        if (ek == e0) ncu = nc;
+        same = same && nc == ncu;
+        tot += nc;
         uint32_t tb = 0;
-        if (idx <= hi_prot) {  // protected this tick: rewrite goes to the other bank
+        if (idx <= hi_prot) {  // protected this tick: rewrite goes to the other info bank
           const uint32_t cur = (uint32_t)(ov[k] >> 63);
           const bool in_rw = idx >= rw_lo && idx <= rw_hi;
           tb = in_rw ? cur : cur ^ 1u;
         }
         sm |= (w >> 63) << ek;
-        hm |= ((w >> 62) & 1ull) << ek;
         tm |= ((w >> 61) & 1ull) << ek;
         dm |= (uint64_t)tb << ek;
         *tr_at(idx) = (w & ~BANK_BIT) | ((uint64_t)tb << 63);
@@ -439,29 +479,49 @@ struct Ctl {
       }
     }
     if (tm) cc_hi = umax64(cc_hi, base + n - 1);  // a ConfigChange entry may be among them
-    if (kind == SRC_WIRE || kind == SRC_WIRE_PROP) sm = aux;  // source bank bits are meaningless off-rank
+    // uniform job? (then J_SPOS = the source position of entry e0's bytes, see raftgpu_internal.h)
+    uint64_t spos = 0;
+    bool uni = same;
+    if (kind == SRC_RING) {
+      uni = !mt && !li;  // a uniform Replicate: the sender's stream holds them back to back
+      spos = uspos;
+    } else if (kind == SRC_WIRE || kind == SRC_WIRE_PROP) {
+      uni = same && e0 == 0;  // payloads at +16n + e·ncu chunks
+      spos = aux;
+    } else if (kind == SRC_CMD) {
+      uni = same && ucmd;
+      spos = uspos;
+    } else {
+      uni = true;  // SRC_SLAB (generator Cmds, P bytes) or SRC_NONE (no Cmd bytes)
+    }
     if (nj < p.J) {
       const uint64_t n64 = p.nrep, JN = (uint64_t)p.J * n64;
       uint64_t* j64 = p.job64 + (uint64_t)nj * n64 + q;
       j64[J_FIRST * JN] = base;
-      j64[J_DMASK * JN] = dm;
+      j64[J_SPOS * JN] = spos;
       j64[J_SMASK * JN] = sm;
-      j64[J_HMASK * JN] = hm;
-      j64[J_TMASK * JN] = tm;
+      j64[J_DMASK * JN] = dm;
       uint32_t* j32 = p.job32 + (uint64_t)nj * n64 + q;
-      j32[J_META * JN] = n | (e0 << 8) | (kind << 16);
+      j32[J_META * JN] = job_meta(n, e0, kind, uni, uni ? ncu : 0u);
       j32[J_SRC * JN] = src;
+      j32[J_DPOS * JN] = hw;
       nj++;
     }
+    hw += tot;
   }
+
+  RG_FN uint32_t lpg() const { return p.s32_in[(uint64_t)S_LPG * p.nrep + q]; }
 
   // raft.appendEntries (leader side): n entries at term. slab_id < 0: the leader's empty no-op.
   // Otherwise Cmds of a proposal: in slab `slab_id`, row of replica slot `rslot` in this column,
-  // with lengths li[0..n) (li NULL: synthetic Cmds, P bytes each), or — rmt set: forwarded from
+  // with lengths li[0..n) (li NULL: synthetic Cmds, P bytes each; li[0].x & SYN_OFF: the generator's
+  // Cmds forwarded from that row; else caller Cmds in the slab's arena), or — rmt set: forwarded from
   // another rank — their inline words rmt[e·G] (length bits) and bytes in the receive buffer at
-  // record offset wofs.
+  // record offset wofs. cinfo (a Propose's header word 4): the batch's stream chunks | contiguous in
+  // its Cmd arena << 31 | arena chunk of entry 0 << 32. Refused (false) by the ring or the stream
+  // capacity rule.
   RG_FN bool append_local(uint32_t n, int slab_id, uint32_t rslot = 0, const uint2* li = nullptr,
-                          const uint64_t* rmt = nullptr, uint64_t wofs = 0, uint32_t cc = 0) {
+                          const uint64_t* rmt = nullptr, uint64_t wofs = 0, uint32_t cc = 0, uint64_t cinfo = 0) {
     if (last + n > cap_base + p.L) return false;
     const uint64_t base = last + 1;
     if (cc) {  // one ConfigChange entry: no Cmd, the descriptor in its length field
@@ -471,20 +531,28 @@ struct Ctl {
       if (__builtin_popcount(members) == 1) try_commit();  // isSingleNodeQuorum
       return true;
     }
+    const bool pay = slab_id >= 0 && p.P;
+    if (pay && !stream_fits(hw, lpg(), (uint32_t)cinfo & 0x7FFFFFFFu, p.PTS)) return false;
 #ifdef RG_CTL_FASTREP
     const bool plain = base > umax64(last_start, sent_hi);  // no protected index: every bank bit 0
     const uint64_t pt = plain ? term_at(last) : 0;
+    const uint32_t pos0 = hw;
 #endif
-    const uint64_t w = slab_id >= 0 && !li && !rmt ? term | len_bits(p.P) : term;
-    if (slab_id < 0 || !p.P) write_entries(base, 0, n, SRC_NONE, 0, nullptr, w);
+    const bool syn = pay && !rmt && (!li || (li[0].x & SYN_OFF));  // generator Cmds: P bytes each
+    const uint64_t w = syn ? term | len_bits(p.P) : term;
+    if (!pay) write_entries(base, 0, n, SRC_NONE, 0, nullptr, w);
     else if (rmt) write_entries(base, 0, n, SRC_WIRE_PROP, n, rmt, w, wofs);
-    else write_entries(base, 0, n, SRC_SLAB, (uint32_t)slab_id | (rslot << 16), nullptr, w, 0, li);
+    else if (syn) write_entries(base, 0, n, SRC_SLAB, (uint32_t)slab_id | (rslot << 16), nullptr, w);
+    else
+      write_entries(base, 0, n, SRC_CMD, (uint32_t)slab_id | (rslot << 16), nullptr, w, 0, li, (uint32_t)(cinfo >> 32),
+                    (cinfo >> 31) & 1u);
 #ifdef RG_CTL_FASTREP
-    if (plain && !li && !rmt) {  // every entry holds the same word
+    if (plain && (syn || !pay)) {  // every entry holds the same word
       la_base = base;
       la_word = w;
       la_pt = pt;
       la_n = n;
+      la_pos = pos0;
     }
 #endif
     last += n;
@@ -532,10 +600,14 @@ struct Ctl {
     }
 #ifdef RG_CTL_FASTREP
     const uint32_t uni = fast ? RG_UNIFORM : 0u;
+    // a uniform Replicate's word 5: the stream position of its first entry's Cmd here (the
+    // follower's bulk job reads the bytes from there; shown as hint 0 by rg_read_msgs)
+    const uint64_t upos = fast ? (uint32_t)(la_pos + (uint32_t)(next - la_base) * word_nc(la_word)) : 0u;
 #else
     const uint32_t uni = 0;
+    const uint64_t upos = 0;
 #endif
-    const int k = send(M_REPLICATE, to + 1, 0, 0, n, lt, next - 1, committed, 0, 0, uni, 0);
+    const int k = send(M_REPLICATE, to + 1, 0, 0, n, lt, next - 1, committed, upos, 0, uni, 0);
     if (k >= 0 && n > 0) {
       uint64_t* mt = p.mt_out + ((((uint64_t)s * R + to) * p.K + (uint32_t)k) * p.E) * p.G + g;
 #ifdef RG_CTL_FASTREP
@@ -559,20 +631,24 @@ struct Ctl {
       if (i != s && is_member(i)) send_replicate(i);
   }
   RG_FN void broadcast_heartbeat() {
+    // a pending ReadIndex rides on every heartbeat (dragonboat's broadcastHeartbeatMessage attaches
+    // readIndex.peepCtx), so a lost read heartbeat or response is retried by the next round
+    const uint64_t ctx = p.rdst ? p.rdst[(uint64_t)RI_CTX * p.nrep + q] : 0ull;
     for (uint32_t i = 0; i < R; ++i)
-      if (i != s && is_member(i)) send(M_HEARTBEAT, i + 1, 0, 0, 0, 0, 0, umin64(RG_GET(rm, i), committed), 0, 0, 0, 0);
+      if (i != s && is_member(i)) send(M_HEARTBEAT, i + 1, 0, 0, 0, 0, 0, umin64(RG_GET(rm, i), committed), ctx, 0, 0, 0);
   }
 
   // ---- follower side (A.9)
   // remote: the message came over the wire (its inline terms are in rmt, its records at wofs)
+  // upos: header word 5 (a uniform Replicate's stream position of entry 0 at the sender)
   RG_FN void handle_replicate(uint64_t w0, uint64_t log_term, uint64_t li, uint64_t mcommit, uint32_t from,
-                                   uint32_t src, uint32_t k, bool remote, uint64_t wofs) {
+                              uint32_t src, uint32_t k, bool remote, uint64_t wofs, uint64_t upos) {
     RG_T0(t0);
-    handle_replicate_(w0, log_term, li, mcommit, from, src, k, remote, wofs);
+    handle_replicate_(w0, log_term, li, mcommit, from, src, k, remote, wofs, upos);
     RG_ACC(2, t0);
   }
   RG_FN void handle_replicate_(uint64_t w0, uint64_t log_term, uint64_t li, uint64_t mcommit, uint32_t from,
-                                   uint32_t src, uint32_t k, bool remote, uint64_t wofs) {
+                               uint32_t src, uint32_t k, bool remote, uint64_t wofs, uint64_t upos) {
     if (li < committed) {
       send_simple(M_REPLICATE_RESP, from, 0, committed);
       return;
@@ -593,15 +669,25 @@ struct Ctl {
       const uint64_t last_new = li + n;
       if (k0 < n) {
         const uint64_t ci = li + 1 + k0;
-        if (ci > committed && last_new > cap_base + p.L) {
-          drops++;  // capacity rule: dropped, no reply
-          return;
+        if (ci > committed) {  // capacity rules (ring, then payload stream): dropped, no reply
+          bool fits = last_new <= cap_base + p.L;
+          if (fits && p.P) {
+            uint32_t c = 0;
+            if (uni) c = (n - k0) * word_nc(uw);
+            else
+              for (uint32_t e = k0; e < n; ++e) c += word_nc(mt[(uint64_t)e * p.G]);
+            fits = stream_fits(hw, lpg(), c, p.PTS);
+          }
+          if (!fits) {
+            drops++;
+            return;
+          }
         }
         if (ci <= committed) {
           err |= ERR_CONFLICT;
         } else {
           if (remote) write_entries(li + 1, k0, n, SRC_WIRE, n, mt, 0, wofs);
-          else if (uni) write_entries(li + 1, k0, n, SRC_RING, src * p.G + g, nullptr, uw);
+          else if (uni) write_entries(li + 1, k0, n, SRC_RING, src * p.G + g, nullptr, uw, 0, nullptr, (uint32_t)upos);
           else write_entries(li + 1, k0, n, SRC_RING, src * p.G + g, mt, 0);
           last = last_new;
         }
@@ -794,12 +880,12 @@ struct Ctl {
   // bytes and lengths as append_local takes them
   // cc != 0: a membership change (one ConfigChange entry)
   RG_FN void handle_propose(uint32_t nent, uint32_t slab_id, uint32_t hop, uint64_t hm, uint32_t rslot,
-                            const uint2* li, const uint64_t* rmt, uint64_t wofs, uint32_t cc = 0) {
+                            const uint2* li, const uint64_t* rmt, uint64_t wofs, uint32_t cc, uint64_t cinfo) {
     if (role == LEADER) {
       RG_T0(t0);
       const bool dropped = cc && cc_pending;  // one change at a time: an empty entry instead
       if (!(cc ? (dropped ? append_local(1, -1) : append_local(1, -1, 0, nullptr, nullptr, 0, cc))
-               : append_local(nent, (int)slab_id, rslot, li, rmt, wofs))) {
+               : append_local(nent, (int)slab_id, rslot, li, rmt, wofs, 0, cinfo))) {
         drops++;
         return;
       }
@@ -810,7 +896,7 @@ struct Ctl {
       broadcast_replicate();
       RG_ACC(1, t1);
     } else if (role == FOLLOWER && leader != 0 && hop == 0) {
-      send(M_PROPOSE, (uint32_t)leader, 0, 0, nent, 0, 0, 0, hm, cc, slab_id, hop + 1);
+      send(M_PROPOSE, (uint32_t)leader, 0, 0, nent, 0, 0, cinfo, hm, cc, slab_id, hop + 1);
     } else {
       drops++;
     }
@@ -916,14 +1002,16 @@ struct Ctl {
           err |= ERR_WIRE;                                               // 1..E entries of a slab
           break;
         }
+        // word 4: the batch's stream chunks | contiguous << 31 | arena chunk << 32 (a remote
+        // batch: the chunks unpack_kernel counted)
         if (remote) {
           const uint64_t* rm = p.rmt + ((((uint64_t)src * R + s) * p.K + k) * p.E) * p.G + g;
-          handle_propose(nent, 0, 1, hw(5), 0, nullptr, rm, w7, (uint32_t)hw(6));
+          handle_propose(nent, 0, 1, hw(5), 0, nullptr, rm, w7, (uint32_t)hw(6), hw(4));
         } else {
           const uint64_t row = p.wire ? (uint64_t)src * p.G + g : g;  // the forwarder's slab row (same rank)
           const uint64_t rows = p.wire ? p.nrep : p.G;
           const uint2* li = p.slab_info + ((uint64_t)(uint32_t)w7 * rows + row) * p.E;
-          handle_propose(nent, (uint32_t)w7, (uint32_t)(w7 >> 32), hw(5), src, li, nullptr, 0, (uint32_t)hw(6));
+          handle_propose(nent, (uint32_t)w7, (uint32_t)(w7 >> 32), hw(5), src, li, nullptr, 0, (uint32_t)hw(6), hw(4));
         }
         break;
       }
@@ -938,7 +1026,7 @@ struct Ctl {
           leader = from;
         }
         if (type == M_REPLICATE) {
-          handle_replicate(w0, hw(2), hw(3), hw(4), from, src, k, remote, hw(7));  // local: RG_UNIFORM
+          handle_replicate(w0, hw(2), hw(3), hw(4), from, src, k, remote, hw(7), hw(5));  // local: RG_UNIFORM
         } else if (type == M_HEARTBEAT) {
           commit_to(hw(4));
           send_simple(M_HEARTBEAT_RESP, from, 0, 0, hw(5), hw(6));
@@ -1002,12 +1090,17 @@ struct Ctl {
         const uint64_t row = p.wire ? q : g, rows = p.wire ? p.nrep : p.G;
         const uint64_t hm = !p.P ? 0ull : p.prop_hmask ? p.prop_hmask[gi] : (n >= 64 ? ~0ull : (1ull << n) - 1);
         const uint2* li = p.prop_hmask && p.P ? p.slab_info + ((uint64_t)sl * rows + row) * p.E : nullptr;
-        handle_propose(n, sl, 0, hm, s, li, nullptr, 0);
+        uint64_t cinfo = (uint64_t)(n * (p.P >> 4)) | (1ull << 31);  // generator Cmds: P bytes each
+        if (p.prop_cmd) {  // a caller batch: rg_propose's chunk count, contiguity and first arena chunk
+          const uint2 pc = p.prop_cmd[gi];
+          cinfo = pc.x | ((uint64_t)pc.y << 32);
+        }
+        handle_propose(n, sl, 0, hm, s, li, nullptr, 0, 0, cinfo);
       }
     }
     if (p.cc_in) {  // 4a: membership change input (rg_config_change)
       const uint32_t v = p.cc_in[gi];
-      if (v && (v & 0xFFu) == s) handle_propose(1, (uint32_t)(p.tick % p.nslab), 0, 0, s, nullptr, nullptr, 0, v >> 8);
+      if (v && (v & 0xFFu) == s) handle_propose(1, (uint32_t)(p.tick % p.nslab), 0, 0, s, nullptr, nullptr, 0, v >> 8, 0);
     }
     if (p.read_ctx) {  // 4b: ReadIndex input (rg_read_index)
       const uint64_t ctx = p.read_ctx[ri()];
@@ -1035,6 +1128,8 @@ struct Ctl {
       }
     }
     cap_base = marker_start;
+    // compaction or a restore moved the marker: the stream below entry marker + 1 is released by the
+    // next step, once this step's bulk kernel has stored that entry's position
     RG_STAMP(4);
     store();
     RG_STAMP(5);
@@ -1051,11 +1146,15 @@ struct Ctl {
     a[S_APPLIED * n] = applied; a[S_LAST * n] = last; a[S_MARKER * n] = marker; a[S_MARKER_TERM * n] = marker_term;
     a[S_SNAP_INDEX * n] = snap_index; a[S_SNAP_TERM * n] = snap_term; a[S_CAP_BASE * n] = cap_base;
     a[S_PROCESSED * n] = processed; a[S_CC_HI * n] = cc_hi;
+    // compaction or a restore moved the marker: the stream below entry marker + 1 is released by the
+    // next step, once this step's bulk kernel has stored that entry's position
+    a[S_FIDX * n] = marker != marker_start ? marker + 1 : 0;
     uint32_t* b = p.s32_out + q;
     b[S_ROLE * n] = role; b[S_ETICK * n] = etick; b[S_HTICK * n] = htick; b[S_RAND_TO * n] = rand_to;
     b[S_RNG_CTR * n] = rng_ctr; b[S_GRANTED * n] = granted; b[S_RESPONDED * n] = responded;
     b[S_ACTIVE * n] = active; b[S_ERR * n] = err; b[S_DROPS * n] = drops;
     b[S_MEMBERS * n] = members; b[S_SNAP_MEMBERS * n] = snap_members; b[S_CC_PENDING * n] = cc_pending;
+    b[S_HW * n] = hw;  // S_LPG / S_APG: pool_kernel (after this launch)
     sfor<0, R>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       p.rem_out[(0 * R + j) * n + q] = rm[j];

@@ -64,7 +64,14 @@ struct rg_engine {
   uint8_t* rst[2] = {nullptr, nullptr};
   uint64_t* tr = nullptr;
   uint2* info = nullptr;
-  uint8_t* pay = nullptr;
+  // paged payload streams: pool pages, per-replica page tables, the free-id ring and
+  // its counters
+  uint8_t* pool = nullptr;
+  uint32_t* pt = nullptr;
+  uint32_t* fring = nullptr;
+  PoolCtl* poolctl = nullptr;
+  uint64_t npages = 0;
+  uint32_t PTS = 0, maxc = 0;  // stream pages per replica, longest Cmd
   uint64_t* hdr[2] = {nullptr, nullptr};
   uint64_t* mt[2] = {nullptr, nullptr};
   uint32_t* cnt[2] = {nullptr, nullptr};
@@ -73,7 +80,12 @@ struct rg_engine {
   uint32_t* jcnt[2] = {nullptr, nullptr};
   uint32_t* crc_err = nullptr;
   uint8_t* slabs = nullptr;
-  uint2* slab_info = nullptr;  // [nslab][rows][E] {0, Cmd length}
+  uint2* slab_info = nullptr;  // [nslab][rows][E] {SYN_OFF or arena chunk, Cmd length}
+  // caller Cmds (rg_propose): one arena per slab, [nslab][cmd_cap], filled chunk-aligned from
+  // cmd_used[slab] on by the H2D copy of a call; a slab's arena restarts when a new tick takes it
+  uint8_t* cmds = nullptr;
+  uint64_t cmd_cap = 0;
+  std::vector<uint64_t> cmd_used, cmd_tick;
   uint64_t slab_synth = 0;  // bit s: slab s holds the generator's bytes (rg_fill_slabs, no rg_propose into it since)
   // caller proposals staged for the next tick (rg_propose): pinned host tables indexed by global input
   // index, uploaded by the tick; Cmd bytes + per-entry descriptors staged through pinned buffers
@@ -81,6 +93,11 @@ struct rg_engine {
   uint32_t* h_pc = nullptr;
   uint64_t* h_hm = nullptr;
   uint64_t* d_prop_hmask = nullptr;
+  // per shard: {stream chunks | contiguous in the arena << 31, arena chunk of entry 0} (pinned), and
+  // the chunk count of its first Cmd (host only: a batch is contiguous while every Cmd has it)
+  uint2* h_pcmd = nullptr;
+  uint2* d_prop_cmd = nullptr;
+  std::vector<uint32_t> pnc;
   std::vector<uint64_t> touched;  // input indices set in h_* since the last upload
   bool staged = false, stg_reset_pending = false;
   hipEvent_t stg_ev = nullptr;    // the last upload of h_* (host may rewrite them once it completed)
@@ -156,8 +173,9 @@ struct rg_engine {
   uint64_t x_send_cap = 0, x_recv_cap = 0;
   // committed-entry copy-back (raftgpu_apply.hip)
   uint64_t* apply_lo = nullptr;
-  uint32_t* acnt = nullptr;
-  uint64_t *aoff = nullptr, *absum = nullptr;
+  uint32_t *acnt = nullptr, *accnt = nullptr;
+  uint64_t *aoff = nullptr, *acoff = nullptr, *absum = nullptr;
+  bool copy_kernel = true;  // RAFTGPU_APPLY_MEMCPY=1: the runtime's D2H copy instead (A/B)
   uint8_t* astage = nullptr;
   uint64_t astage_bytes = 0;
   // asynchronous copy-back (rg_apply_async): per buffer a device staging area, pinned host memory,
@@ -172,8 +190,8 @@ struct rg_engine {
   uint64_t* persist_lo = nullptr;
   uint64_t* snap_ev = nullptr;  // [nrep] restored_at | SNAP_TAKEN_BIT of the last tick
   uint32_t* prof = nullptr;     // RG_CTL_PROFILE builds: control phase stamps of the last tick
-  uint32_t *pscnt = nullptr, *pecnt = nullptr;
-  uint64_t *psoff = nullptr, *peoff = nullptr;
+  uint32_t *pscnt = nullptr, *pecnt = nullptr, *pccnt = nullptr;
+  uint64_t *psoff = nullptr, *peoff = nullptr, *pcoff = nullptr;
 };
 
 static int stage_reset(rg_engine* e);
@@ -223,6 +241,15 @@ static void build_crc(rg_engine* e, std::vector<uint32_t>& tab) {
         for (uint32_t i = 0; i < (1u << b); ++i) x = Zi(x);
         tab[CRC_ZI_OFF + (b * 8 + j) * 16 + n] = x;
       }
+  // Z^P (chaining the P-byte segments of a longer Cmd) and the finalisation constants of S·P bytes
+  const uint32_t P = e->c.payload_bytes;
+  for (uint32_t j = 0; j < 8; ++j)
+    for (uint32_t n = 0; n < 16; ++n) tab[CRC_ZP_OFF + j * 16 + n] = Zn(n << (4 * j), P);
+  uint32_t st = 0xFFFFFFFFu;
+  for (uint32_t S = 1; S <= CRC_CS_MAX; ++S) {
+    st = Zn(st, P);
+    tab[CRC_CS_OFF + S] = st ^ 0xFFFFFFFFu;
+  }
 }
 
 static uint32_t host_crc(const rg_engine* e, const uint8_t* p, size_t n) {
@@ -258,6 +285,7 @@ static int stage_reserve(rg_engine* e, uint64_t bytes) {
 }
 
 static bool pow2(uint32_t x) { return x && !(x & (x - 1)); }
+static uint64_t a16(uint64_t x) { return (x + 15) & ~15ull; }
 
 // The parameter block of the tick that runs next (tick e->t): reads parity t&1 state and the
 // outbox written by tick t-1, writes the other parity.
@@ -270,6 +298,8 @@ static TickParams params(rg_engine* e) {
   p.CO = c.compaction_overhead; p.drop_ppm = c.drop_ppm;
   p.wire = e->wire ? 1u : 0u;
   p.AF = c.apply_feedback;
+  p.PTS = e->PTS;
+  p.JS = c.join_slots;
   p.IM = c.initial_members;
   p.seed = c.seed;
   p.tick = e->t;
@@ -291,6 +321,8 @@ static TickParams params(rg_engine* e) {
   p.persist_lo = e->persist_lo;
   p.snap_ev = e->snap_ev;
   p.prof = e->prof;
+  p.info = e->info;
+  p.pool = e->poolctl;
   return p;
 }
 
@@ -300,8 +332,9 @@ static WireParams wire_params(rg_engine* e) {
   w.G = p.G; w.R = p.R; w.nrep = p.nrep; w.L = p.L; w.P = p.P; w.E = p.E; w.K = p.K;
   w.pl = e->pl;
   w.hdr = p.hdr_in; w.mt = p.mt_in; w.cnt = p.cnt_in;
-  w.info = e->info; w.pay = e->pay;
+  w.info = e->info; w.pool = e->pool; w.pt = e->pt; w.PTS = e->PTS; w.maxc = e->maxc;
   w.slabs = e->slabs; w.slab_info = e->slab_info; w.nslab = e->c.num_slabs;
+  w.cmds = e->cmds; w.cmd_cap = e->cmd_cap;
   w.umap = e->umap; w.ubeg = e->ubeg; w.U = e->U;
   w.usize = e->usize; w.uoff = e->uoff; w.bsum = e->bsum;
   w.rmap = e->rmap; w.rbeg = e->rbeg; w.RU = e->RU;
@@ -315,7 +348,9 @@ static BulkParams bulk_params(rg_engine* e) {  // for tick e->t
   b.G = e->c.groups; b.R = e->c.replicas; b.nrep = e->nrep; b.L = e->c.log_capacity; b.P = e->c.payload_bytes;
   b.E = e->c.max_entries_per_msg; b.J = e->J; b.crc_const = e->crc_const; b.tile = e->bulk_tile;
   b.job64 = e->job64[a]; b.job32 = e->job32[a]; b.jcnt = e->jcnt[a];
-  b.info = e->info; b.pay = e->pay; b.slabs = e->slabs; b.crc_err = e->crc_err; b.crc_tab = e->crc_tab;
+  b.tr = e->tr; b.info = e->info; b.pool = e->pool; b.PTS = e->PTS;
+  b.slabs = e->slabs; b.slab_info = e->slab_info; b.cmds = e->cmds; b.cmd_cap = e->cmd_cap;
+  b.crc_err = e->crc_err; b.crc_tab = e->crc_tab; b.poolctl = e->poolctl;
   b.wire_mode = e->wire ? 1u : 0u;
   b.wire = e->recv;
   b.wire_bytes = e->recv_bytes;
@@ -327,7 +362,13 @@ static AdminParams admin(rg_engine* e) {
   AdminParams a{};
   a.t = params(e);
   a.info = e->info;
-  a.pay = e->pay;
+  a.pool = e->pool;
+  a.pt = e->pt;
+  a.PTS = e->PTS;
+  a.row = e->maxc;
+  a.fring = e->fring;
+  a.npages = e->npages;
+  a.poolctl = e->poolctl;
   a.crc_err = e->crc_err;
   a.zi = e->crc_tab + CRC_ZI_OFF;
   return a;
@@ -355,6 +396,15 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if (c.apply_feedback > 1) return fail(RG_EINVAL, "apply_feedback must be 0 or 1");
   if (c.initial_members >> c.replicas) return fail(RG_EINVAL, "initial_members names a slot >= replicas");
   if ((N > 1 || c.wire_all) && c.groups >= (1u << 24)) return fail(RG_EINVAL, "groups < 2^24 with ranks > 1");
+  const uint32_t maxc = c.max_cmd_bytes ? c.max_cmd_bytes : c.payload_bytes;
+  if (c.payload_bytes ? (maxc < c.payload_bytes || maxc > MAX_CMD) : maxc != 0)
+    return fail(RG_EINVAL, "max_cmd_bytes must be in [payload_bytes, 8191] (0 with payload_bytes 0)");
+  if (c.stream_pages && (!pow2(c.stream_pages) || c.stream_pages > (1u << 20)))
+    return fail(RG_EINVAL, "stream_pages must be 0 or a power of two <= 2^20");
+  if (c.pool_pages > (1u << 24)) return fail(RG_EINVAL, "pool_pages <= 2^24 (64 GiB)");
+  if (c.join_slots >> c.replicas) return fail(RG_EINVAL, "join_slots names a slot >= replicas");
+  if (c.initial_members & c.join_slots) return fail(RG_EINVAL, "a slot is both an initial member and joining");
+  if (c.join_slots == (1u << c.replicas) - 1u) return fail(RG_EINVAL, "every slot joining: nobody to join");
   int ndev = 0;
   HIPCHK(hipGetDeviceCount(&ndev));
   if (ndev <= 0 || c.device < 0 || c.device >= ndev) return fail(RG_EINVAL, "no such HIP device");
@@ -368,6 +418,15 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   e->wire = N > 1 || c.wire_all;
   e->slab_rows = e->wire ? e->nrep : c.groups;  // wire engines: one slab row per replica (bulk_kernel<LG, true>)
   e->J = (c.replicas - 1) * c.max_msgs_per_pair + 2;  // >= appends one step can make
+  e->maxc = maxc;
+  {  // payload streams: a replica's window (auto: twice a full log of P-byte Cmds) and the pool
+    const uint64_t full = ((uint64_t)c.log_capacity * ((c.payload_bytes + 15) & ~15u) + PAGE_BYTES - 1) / PAGE_BYTES;
+    uint32_t pts = 16;
+    while (pts < 2 * full) pts <<= 1;
+    e->PTS = c.payload_bytes ? (c.stream_pages ? c.stream_pages : pts) : 1;
+    const uint64_t want = (uint64_t)c.groups * c.replicas * (full + 2);
+    e->npages = !c.payload_bytes ? 0 : c.pool_pages ? c.pool_pages : std::min<uint64_t>(want, 1ull << 24);
+  }
   const uint64_t n = e->nrep, L = c.log_capacity, P = c.payload_bytes, R = c.replicas, K = c.max_msgs_per_pair,
                  E = c.max_entries_per_msg, G = c.groups, J = e->J;
   int rc = RG_OK;
@@ -382,7 +441,10 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   }
   if (rc == RG_OK) rc = dalloc(e, &e->tr, L * n * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->info, 2 * n * L * sizeof(uint2));
-  if (rc == RG_OK) rc = dalloc(e, &e->pay, 2 * n * L * P);
+  if (rc == RG_OK) rc = dalloc(e, &e->pool, e->npages * PAGE_BYTES);
+  if (rc == RG_OK) rc = dalloc(e, &e->pt, (uint64_t)n * e->PTS * 4);
+  if (rc == RG_OK) rc = dalloc(e, &e->fring, e->npages * 4);
+  if (rc == RG_OK) rc = dalloc(e, &e->poolctl, sizeof(PoolCtl));
   for (int b = 0; b < 2 && rc == RG_OK; ++b) {
     rc = dalloc(e, &e->job64[b], J64_ROWS * J * n * 8);
     if (rc == RG_OK) rc = dalloc(e, &e->job32[b], J32_ROWS * J * n * 4);
@@ -391,7 +453,14 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if (rc == RG_OK) rc = dalloc(e, &e->crc_err, n * 4);
   if (rc == RG_OK) rc = dalloc(e, &e->slabs, (uint64_t)c.num_slabs * e->slab_rows * E * P);
   if (rc == RG_OK) rc = dalloc(e, &e->slab_info, (uint64_t)c.num_slabs * e->slab_rows * E * sizeof(uint2));
+  e->cmd_used.assign(c.num_slabs, 0);
+  e->cmd_tick.assign(c.num_slabs, ~0ull);
   if (rc == RG_OK) rc = dalloc(e, &e->d_prop_hmask, G * N * 8);
+  if (rc == RG_OK) rc = dalloc(e, &e->d_prop_cmd, G * N * 8);
+  if (rc == RG_OK && hipHostMalloc((void**)&e->h_pcmd, G * N * 8, 0) != hipSuccess)
+    rc = fail(RG_ENOMEM, "hipHostMalloc (proposal tables)");
+  if (rc == RG_OK) memset(e->h_pcmd, 0, G * N * 8);
+  e->pnc.assign(G * N, 0);
   if (rc == RG_OK) rc = dalloc(e, &e->rdst, (uint64_t)RD_ROWS * n * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->d_read_ctx, n * N * 8);
   if (rc == RG_OK && hipHostMalloc((void**)&e->h_rd, n * N * 8, 0) != hipSuccess) rc = fail(RG_ENOMEM, "hipHostMalloc");
@@ -420,7 +489,9 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
     rc = fail(RG_ENOMEM, "hipHostMalloc (parameter blocks)");
   if (rc == RG_OK) rc = dalloc(e, &e->apply_lo, n * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->acnt, n * 4);
+  if (rc == RG_OK) rc = dalloc(e, &e->accnt, n * 4);
   if (rc == RG_OK) rc = dalloc(e, &e->aoff, (n + 1) * 8);
+  if (rc == RG_OK) rc = dalloc(e, &e->acoff, (n + 1) * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->absum, ((n + 1023) / 1024 + 1) * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->persist_lo, n * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->snap_ev, n * 8);
@@ -429,8 +500,10 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
 #endif
   if (rc == RG_OK) rc = dalloc(e, &e->pscnt, n * 4);
   if (rc == RG_OK) rc = dalloc(e, &e->pecnt, n * 4);
+  if (rc == RG_OK) rc = dalloc(e, &e->pccnt, n * 4);
   if (rc == RG_OK) rc = dalloc(e, &e->psoff, (n + 1) * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->peoff, (n + 1) * 8);
+  if (rc == RG_OK) rc = dalloc(e, &e->pcoff, (n + 1) * 8);
   // exchange units: every remote (s, d, j) outbox column, per destination rank (send) and per
   // source rank (receive), each in (s, d, j) order — the same list on both ends of a link
   if (rc == RG_OK && e->wire) {
@@ -537,6 +610,12 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
     if (pow2(t) && t <= 64) tile = t;
   }
   e->bulk_tile = tile;
+  if (const char* v = getenv("RAFTGPU_APPLY_MEMCPY")) e->copy_kernel = !(v[0] == '1');
+  if (launch_pool_reset(e->fring, e->npages, e->poolctl, e->stream) != hipSuccess ||
+      hipStreamSynchronize(e->stream) != hipSuccess) {
+    rg_destroy(e);
+    return fail(RG_EHIP, "page pool reset");
+  }
   const uint64_t ntiles = (n + tile - 1) / tile;
   e->bulk_grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((ntiles + 3) / 4, (uint64_t)std::max(cus, 1) * per_cu));
   if (const char* gv = getenv("RAFTGPU_BULK_GRID")) {  // measurement override (blocks)
@@ -583,7 +662,7 @@ void rg_destroy(rg_engine* e) {
   if (e->h_tp) (void)hipHostFree(e->h_tp);
   for (void* p : e->allocs) (void)hipFree(p);
   if (e->h_bounds) (void)hipHostFree(e->h_bounds);
-  for (void* h : {(void*)e->h_pt, (void*)e->h_pc, (void*)e->h_hm, (void*)e->h_cmd})
+  for (void* h : {(void*)e->h_pt, (void*)e->h_pc, (void*)e->h_hm, (void*)e->h_cmd, (void*)e->h_pcmd})
     if (h) (void)hipHostFree(h);
   delete e;
 }
@@ -651,7 +730,11 @@ int rg_sync(rg_engine* e) {
   if (!e) return fail(RG_EINVAL, "null engine");
   int rc = join(e);
   if (rc) return rc;
+  uint32_t perr = 0;
+  HIPCHK(hipMemcpyAsync(&perr, &e->poolctl->param_err, 4, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
+  if (perr)
+    return fail(RG_EINVARIANT, "control_kernel found a corrupt parameter block (checksum mismatch): a tick was skipped");
   return RG_OK;
 }
 
@@ -674,6 +757,7 @@ int rg_bootstrap(rg_engine* e) {
     e->h_pt[gi] = 0xFF;
     e->h_pc[gi] = 0;
     e->h_hm[gi] = 0;
+    e->h_pcmd[gi] = make_uint2(0u, 0u);
   }
   e->touched.clear();
   e->staged = false;
@@ -687,6 +771,9 @@ int rg_bootstrap(rg_engine* e) {
   e->rd_staged = e->rd_reset_pending = false;
   HIPCHK(hipMemsetAsync(e->rdst, 0, (uint64_t)RD_ROWS * e->nrep * 8, e->stream));
   HIPCHK(hipMemsetAsync(e->crc_err, 0, (uint64_t)e->nrep * 4, e->stream));
+  HIPCHK(launch_pool_reset(e->fring, e->npages, e->poolctl, e->stream));  // every stream empty, every page free
+  std::fill(e->cmd_used.begin(), e->cmd_used.end(), 0ull);
+  std::fill(e->cmd_tick.begin(), e->cmd_tick.end(), ~0ull);
   TickParams p = params(e);
   p.s64_out = e->s64[0];
   p.s32_out = e->s32[0];
@@ -717,9 +804,34 @@ static int stage_reset(rg_engine* e) {
     e->h_pt[gi] = 0xFF;
     e->h_pc[gi] = 0;
     e->h_hm[gi] = 0;
+    e->h_pcmd[gi] = make_uint2(0u, 0u);
   }
   e->touched.clear();
   e->stg_reset_pending = false;
+  return RG_OK;
+}
+
+// grow the caller-Cmd arenas (rare: a call's Cmds exceed a slab's arena): the old contents move
+// with a synchronised device copy, since forwarded batches of the last ticks may still be read
+static int cmd_reserve(rg_engine* e, uint64_t need_bytes) {
+  if (need_bytes <= e->cmd_cap) return RG_OK;
+  const uint64_t cap = std::max<uint64_t>((need_bytes * 3 / 2 + 4095) & ~4095ull, 1ull << 20);
+  const uint32_t ns = e->c.num_slabs;
+  uint8_t* nb = nullptr;
+  RGCHK(dalloc(e, &nb, cap * ns));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  HIPCHK(hipStreamSynchronize(e->bulk));
+  if (e->cmds) {
+    for (uint32_t sl = 0; sl < ns; ++sl)
+      if (e->cmd_used[sl])
+        HIPCHK(hipMemcpy(nb + (uint64_t)sl * cap, e->cmds + (uint64_t)sl * e->cmd_cap, e->cmd_used[sl] * 16,
+                         hipMemcpyDeviceToDevice));
+    (void)hipFree(e->cmds);
+    e->allocs.erase(std::remove(e->allocs.begin(), e->allocs.end(), (void*)e->cmds), e->allocs.end());
+    e->bytes -= e->cmd_cap * ns;
+  }
+  e->cmds = nb;
+  e->cmd_cap = cap;
   return RG_OK;
 }
 
@@ -748,14 +860,28 @@ int rg_propose(rg_engine* e, const rg_proposal* props, size_t n, const uint8_t* 
   }
   if (nent && !lens) return fail(RG_EINVAL, "rg_propose: null lens");
   for (uint64_t j = 0; j < nent; ++j) {
-    if (lens[j] > P) return fail(RG_EINVAL, "rg_propose: Cmd longer than payload_bytes");
+    if (lens[j] > e->maxc) return fail(RG_EINVAL, "rg_propose: Cmd longer than max_cmd_bytes");
     nbytes += lens[j];
   }
   if (nbytes && !payload) return fail(RG_EINVAL, "rg_propose: null payload");
-  // stage: pinned [Cmd bytes | off u64 | dst u64 | len u32] for the entries of the batches
-  uint64_t nstage = 0;
-  for (size_t i = 0; i < n; ++i) nstage += props[i].count;
-  const uint64_t cb = (nbytes + 15) & ~15ull, need = cb + nstage * 20 + 64;
+  // the tick's slab: its Cmd arena restarts when a new tick takes it (stream order keeps the bytes of
+  // the tick that used it nslab ticks ago until that tick and the next have read them)
+  const uint64_t slab = e->t % e->c.num_slabs, rows = e->slab_rows;
+  if (e->cmd_tick[slab] != e->t) {
+    e->cmd_tick[slab] = e->t;
+    e->cmd_used[slab] = 0;
+  }
+  // layout: each Cmd at its own length rounded up to 16 B, back to back from cmd_used[slab]
+  uint64_t nstage = 0, chunks = 0;
+  for (size_t i = 0; i < n; ++i) {
+    nstage += props[i].count;
+    for (uint32_t x = 0; x < props[i].count; ++x) chunks += (lens[props[i].first + x] + 15) / 16;
+  }
+  const uint64_t a0 = e->cmd_used[slab];
+  if (P && (a0 + chunks) >= SYN_OFF) return fail(RG_EFULL, "rg_propose: a slab's Cmd arena holds at most 32 GiB");
+  if (P && chunks) RGCHK(cmd_reserve(e, (a0 + chunks) * 16));
+  // pinned staging: [Cmds, chunk-aligned and zero-padded | info_at u64 | chunk u32 | len u32]
+  const uint64_t cb = chunks * 16, need = cb + nstage * 16 + 64;
   if (P && nstage) {
     HIPCHK(hipEventSynchronize(e->prop_ev));  // the last H2D out of h_cmd has completed
     if (need > e->h_cmd_cap) {
@@ -765,7 +891,7 @@ int rg_propose(rg_engine* e, const rg_proposal* props, size_t n, const uint8_t* 
       if (hipHostMalloc((void**)&e->h_cmd, need * 3 / 2, 0) != hipSuccess) return fail(RG_ENOMEM, "hipHostMalloc");
       e->h_cmd_cap = need * 3 / 2;
     }
-    if (need > e->d_cmd_cap) {
+    if (need - cb > e->d_cmd_cap) {
       HIPCHK(hipStreamSynchronize(e->stream));  // the last stage kernel read the old buffer
       if (e->d_cmd) {
         (void)hipFree(e->d_cmd);
@@ -774,18 +900,16 @@ int rg_propose(rg_engine* e, const rg_proposal* props, size_t n, const uint8_t* 
         e->d_cmd = nullptr;
       }
       e->d_cmd_cap = 0;
-      RGCHK(dalloc(e, &e->d_cmd, need * 3 / 2));
-      e->d_cmd_cap = need * 3 / 2;
+      RGCHK(dalloc(e, &e->d_cmd, (need - cb) * 3 / 2));
+      e->d_cmd_cap = (need - cb) * 3 / 2;
     }
-    if (nbytes) memcpy(e->h_cmd, payload, nbytes);
   }
   std::vector<uint64_t> boff(nent + 1, 0);
   for (uint64_t j = 0; j < nent; ++j) boff[j + 1] = boff[j] + lens[j];
-  uint64_t* off = (uint64_t*)(e->h_cmd + cb);
-  uint64_t* dst = off + nstage;
-  uint32_t* len = (uint32_t*)(dst + nstage);
-  const uint64_t slab = e->t % e->c.num_slabs, rows = e->slab_rows;
-  uint64_t k = 0;
+  uint64_t* info_at = (uint64_t*)(e->h_cmd + cb);
+  uint32_t* chunk = (uint32_t*)(info_at + nstage);
+  uint32_t* len = chunk + nstage;
+  uint64_t k = 0, at_chunk = 0;
   for (size_t i = 0; i < n; ++i) {
     const rg_proposal& b = props[i];
     const uint64_t gi = b.group - g0;
@@ -793,11 +917,25 @@ int rg_propose(rg_engine* e, const rg_proposal* props, size_t n, const uint8_t* 
     const uint64_t row = e->wire ? (uint64_t)b.slot * e->c.groups + j : j;
     for (uint32_t x = 0; x < b.count; ++x) {
       const uint32_t at = e->h_pc[gi] + x;  // position in the shard's batch
-      if (lens[b.first + x] && P) e->h_hm[gi] |= 1ull << at;
+      const uint32_t ln = lens[b.first + x];
+      if (ln && P) e->h_hm[gi] |= 1ull << at;
       if (P) {
-        off[k] = boff[b.first + x];
-        dst[k] = (slab * rows + row) * E + at;
-        len[k] = lens[b.first + x];
+        const uint64_t nc = (ln + 15) / 16;
+        uint2& pc = e->h_pcmd[gi];  // the shard's batch: chunks, contiguity, first arena chunk
+        if (at == 0) {
+          pc = make_uint2(1u << 31, (uint32_t)(a0 + at_chunk));
+          e->pnc[gi] = (uint32_t)nc;
+        } else if (nc != e->pnc[gi] || a0 + at_chunk != pc.y + (uint64_t)at * nc) {
+          pc.x &= ~(1u << 31);
+        }
+        pc.x += (uint32_t)nc;
+        uint8_t* d = e->h_cmd + at_chunk * 16;
+        if (ln) memcpy(d, payload + boff[b.first + x], ln);
+        if (nc * 16 > ln) memset(d + ln, 0, nc * 16 - ln);
+        info_at[k] = (slab * rows + row) * E + at;
+        chunk[k] = (uint32_t)(a0 + at_chunk);
+        len[k] = ln;
+        at_chunk += nc;
         ++k;
       }
     }
@@ -806,12 +944,18 @@ int rg_propose(rg_engine* e, const rg_proposal* props, size_t n, const uint8_t* 
     e->h_pc[gi] += b.count;
   }
   if (P && k) {
-    uint8_t* d = e->d_cmd;
-    HIPCHK(hipMemcpyAsync(d, e->h_cmd, cb + k * 20, hipMemcpyHostToDevice, e->stream));
+    // the Cmd bytes straight into the slab's arena (one H2D copy), then their descriptors
+    if (cb) HIPCHK(hipMemcpyAsync(e->cmds + slab * e->cmd_cap + a0 * 16, e->h_cmd, cb, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipMemcpyAsync(e->d_cmd, e->h_cmd + cb, k * 16, hipMemcpyHostToDevice, e->stream));
     HIPCHK(hipEventRecord(e->prop_ev, e->stream));
-    LAUNCH(launch_stage_cmds(e->slabs, e->slab_info, P, d, (const uint64_t*)(d + cb), (const uint64_t*)(d + cb) + k,
-                             (const uint32_t*)((const uint64_t*)(d + cb) + 2 * k), k, e->stream),
-           e->stream, "stage_cmds");
+    StageParams sp{};
+    sp.slab_info = e->slab_info;
+    sp.info_at = (const uint64_t*)e->d_cmd;
+    sp.chunk = (const uint32_t*)(e->d_cmd + k * 8);
+    sp.len = (const uint32_t*)(e->d_cmd + k * 12);
+    sp.n = k;
+    LAUNCH(launch_stage_cmds(sp, e->stream), e->stream, "stage_cmds");
+    e->cmd_used[slab] = a0 + chunks;
     e->slab_synth &= ~(1ull << slab);
   }
   if (n) e->staged = true;
@@ -875,12 +1019,18 @@ static int launch_control_slot(rg_engine* e, const TickParams& p) {
   const uint32_t k = (uint32_t)(e->tp_next++ % TP_SLOTS), c = k / TP_CHUNK;
   if (k % TP_CHUNK == 0 && e->tp_used[c]) HIPCHK(hipEventSynchronize(e->tp_ev[c]));
   e->h_tp[k] = p;
+  {  // the checksum the kernel verifies before it dereferences anything
+    uint64_t w[TP_WORDS], h = 0;
+    memcpy(w, &e->h_tp[k], sizeof w);
+    for (uint32_t i = 0; i < TP_WORDS; ++i) h = tp_mix(h ^ w[i]);
+    e->h_tp[k].csum = h;
+  }
   HIPCHK(hipMemcpyAsync(e->d_tp + k, e->h_tp + k, sizeof(TickParams), hipMemcpyHostToDevice, e->stream));
   if (k % TP_CHUNK == TP_CHUNK - 1) {
     HIPCHK(hipEventRecord(e->tp_ev[c], e->stream));
     e->tp_used[c] = true;
   }
-  LAUNCH(launch_control(e->d_tp + k, p.R, p.nrep, e->stream), e->stream, "control_kernel");
+  LAUNCH(launch_control(e->d_tp + k, &e->poolctl->param_err, p.R, p.nrep, e->stream), e->stream, "control_kernel");
   return RG_OK;
 }
 
@@ -933,6 +1083,10 @@ static int tick_impl(rg_engine* e, const rg_tick_input* in, bool device_ptrs) {
     HIPCHK(hipMemcpyAsync(e->d_prop_target, e->h_pt, GN, hipMemcpyHostToDevice, e->stream));
     HIPCHK(hipMemcpyAsync(e->d_prop_count, e->h_pc, GN * 4, hipMemcpyHostToDevice, e->stream));
     HIPCHK(hipMemcpyAsync(e->d_prop_hmask, e->h_hm, GN * 8, hipMemcpyHostToDevice, e->stream));
+    if (e->c.payload_bytes) {
+      HIPCHK(hipMemcpyAsync(e->d_prop_cmd, e->h_pcmd, GN * 8, hipMemcpyHostToDevice, e->stream));
+      p.prop_cmd = e->d_prop_cmd;
+    }
     HIPCHK(hipEventRecord(e->stg_ev, e->stream));
     p.prop_target = e->d_prop_target;
     p.prop_count = e->d_prop_count;
@@ -969,6 +1123,13 @@ static int tick_impl(rg_engine* e, const rg_tick_input* in, bool device_ptrs) {
   if (two && e->t >= 2) HIPCHK(hipStreamWaitEvent(e->stream, e->bulk_done[a], 0));
   RGCHK(timing_event(e, e->stream, 0));
   RGCHK(launch_control_slot(e, p));
+  if (e->c.payload_bytes) {  // stream pages: release what compaction passed, take what this step's appends need
+    PoolParams pp{};
+    pp.nrep = e->nrep; pp.PTS = e->PTS; pp.npages = e->npages;
+    pp.s32_out = p.s32_out; pp.s32_in = p.s32_in; pp.pt = e->pt; pp.fring = e->fring; pp.ctl = e->poolctl;
+    pp.jcnt = p.jcnt;
+    LAUNCH(launch_pool(pp, e->stream), e->stream, "pool_kernel");
+  }
   RGCHK(timing_event(e, e->stream, 0));
   if (two) {
     HIPCHK(hipEventRecord(e->ctl_done[a], e->stream));
@@ -979,7 +1140,7 @@ static int tick_impl(rg_engine* e, const rg_tick_input* in, bool device_ptrs) {
   // is the control launch alone
   if (e->c.payload_bytes) {
     RGCHK(timing_event(e, bs, 1));
-    LAUNCH(launch_bulk(bulk_params(e), bs, e->bulk_grid), bs, "bulk_kernel");
+    LAUNCH(launch_bulk(bulk_params(e), e->pt, bs, e->bulk_grid), bs, "bulk_kernel");
     RGCHK(timing_event(e, bs, 1));
   }
   HIPCHK(hipEventRecord(e->bulk_done[a], bs));
@@ -1038,7 +1199,7 @@ int rg_read_entries(rg_engine* e, uint32_t rid, uint64_t first, uint32_t n, rg_e
   int rc = rg_read_replicas(e, rid, 1, &v);
   if (rc) return rc;
   if (first <= v.marker || first + n - 1 > v.last) return fail(RG_EINVAL, "index outside (marker, last]");
-  const uint64_t P = e->c.payload_bytes, vb = (uint64_t)n * sizeof(rg_entry_view), pb = payload ? (uint64_t)n * P : 0;
+  const uint64_t vb = (uint64_t)n * sizeof(rg_entry_view), pb = payload ? (uint64_t)n * e->maxc : 0;
   rc = stage_reserve(e, vb + pb + 16);
   if (rc) return rc;
   HIPCHK(launch_gather_entries(admin(e), rid, first, n, e->stage, payload ? e->stage + vb : nullptr, e->stream));
@@ -1052,48 +1213,62 @@ int rg_import_replica(rg_engine* e, uint32_t rid, const rg_replica_view* v, cons
                       const uint32_t* types, const uint8_t* payloads, const uint32_t* lens) {
   if (!e || !v || rid >= e->nrep) return fail(RG_EINVAL, "rg_import_replica args");
   if (int jrc = join(e)) return jrc;
-  const uint64_t L = e->c.log_capacity, P = e->c.payload_bytes;
+  const uint64_t L = e->c.log_capacity, P = e->c.payload_bytes, row = e->maxc;
   if (v->last < v->marker || v->last - v->marker > L) return fail(RG_EINVAL, "log longer than the ring");
   const uint32_t nent = (uint32_t)(v->last - v->marker);
   if (nent && !terms) return fail(RG_EINVAL, "rg_import_replica: null terms");
   std::vector<uint64_t> words(nent);
-  std::vector<uint32_t> crcs(nent, 0);
-  std::vector<uint8_t> rows(payloads ? (uint64_t)nent * P : 0, 0);  // Cmds zero-padded to P bytes
+  std::vector<uint32_t> crcs(nent, 0), pos(nent, 0);
+  std::vector<uint8_t> chunks;  // the Cmds back to back, each zero-padded to whole chunks (a fresh stream)
+  std::vector<uint8_t> slot;
   for (uint32_t k = 0; k < nent; ++k) {
     const uint32_t type = types ? (types[k] & 0xFFu) : RG_ENTRY_APPLICATION;
     const uint32_t len = lens ? lens[k] : (uint32_t)P;
+    pos[k] = (uint32_t)(chunks.size() / 16);
     if (type != RG_ENTRY_APPLICATION) {  // a ConfigChange keeps its descriptor, no Cmd
       const uint32_t cc = lens ? lens[k] : 0u;
       if (cc > 0x1FFFu) return fail(RG_EINVAL, "rg_import_replica: ConfigChange descriptor out of range");
       words[k] = (terms[k] & TERM_MASK) | TYPE_BIT | cc_bits(cc);
       continue;
     }
-    if (len > P) return fail(RG_EINVAL, "rg_import_replica: Cmd longer than payload_bytes");
+    if (len > row) return fail(RG_EINVAL, "rg_import_replica: Cmd longer than max_cmd_bytes");
     const bool hp = payloads && P && len && !(types && (types[k] & RG_ENTRY_EMPTY));
     words[k] = (terms[k] & TERM_MASK) | (hp ? len_bits(len) : 0);
     if (hp) {
-      memcpy(rows.data() + (uint64_t)k * P, payloads + (uint64_t)k * P, len);
-      crcs[k] = host_crc(e, rows.data() + (uint64_t)k * P, P);  // the slot CRC
+      const uint64_t S = (len + P - 1) / P;  // the slot CRC: the Cmd zero-padded to S·P bytes
+      slot.assign(S * P, 0);
+      memcpy(slot.data(), payloads + (uint64_t)k * row, len);
+      crcs[k] = host_crc(e, slot.data(), S * P);
+      chunks.insert(chunks.end(), slot.begin(), slot.begin() + (len + 15) / 16 * 16);
     }
   }
-  const uint64_t vb = 512, wb = (uint64_t)nent * 8, cb = (uint64_t)nent * 4, pb = rows.size();
-  int rc = stage_reserve(e, vb + wb + cb + pb + 64);
+  const uint64_t nch = chunks.size() / 16;
+  if (nch && vpn_ceil((uint32_t)nch) > e->PTS) return fail(RG_EFULL, "rg_import_replica: log longer than stream_pages");
+  const uint64_t vb = 512, wb = (uint64_t)nent * 8, cb = (uint64_t)nent * 4, pb = chunks.size();
+  int rc = stage_reserve(e, vb + wb + 2 * cb + pb + 64);
   if (rc) return rc;
   uint8_t* d = e->stage;
   HIPCHK(hipStreamSynchronize(e->stream));
   HIPCHK(hipMemcpy(d, v, sizeof *v, hipMemcpyHostToDevice));
   if (wb) HIPCHK(hipMemcpy(d + vb, words.data(), wb, hipMemcpyHostToDevice));
   if (cb) HIPCHK(hipMemcpy(d + vb + wb, crcs.data(), cb, hipMemcpyHostToDevice));
-  if (pb) HIPCHK(hipMemcpy(d + vb + wb + cb, rows.data(), pb, hipMemcpyHostToDevice));
-  HIPCHK(launch_scatter_replica(admin(e), rid, d, (const uint64_t*)(d + vb), pb ? d + vb + wb + cb : nullptr,
-                                (const uint32_t*)(d + vb + wb), nent, e->stream, e->info, e->pay));
+  if (cb) HIPCHK(hipMemcpy(d + vb + wb + cb, pos.data(), cb, hipMemcpyHostToDevice));
+  if (pb) HIPCHK(hipMemcpy(d + vb + wb + 2 * cb, chunks.data(), pb, hipMemcpyHostToDevice));
+  uint32_t* status = (uint32_t*)(d + vb - 16);
+  HIPCHK(hipMemsetAsync(status, 0, 4, e->stream));
+  HIPCHK(launch_scatter_replica(admin(e), rid, d, (const uint64_t*)(d + vb), (const uint32_t*)(d + vb + wb),
+                                (const uint32_t*)(d + vb + wb + cb), pb ? d + vb + wb + 2 * cb : nullptr, nent,
+                                (uint32_t)nch, status, e->stream));
   {  // no snapshot event, pending or ready read until it steps (device rows are indexed by q = s·G + g)
     const uint64_t q = (uint64_t)(rid % e->c.replicas) * e->c.groups + rid / e->c.replicas;
     HIPCHK(hipMemsetAsync(e->snap_ev + q, 0, 8, e->stream));
     HIPCHK(hipMemsetAsync(e->rdst + (uint64_t)RI_CTX * e->nrep + q, 0, 8, e->stream));
     HIPCHK(hipMemsetAsync(e->rdst + (uint64_t)RD_TICK * e->nrep + q, 0, 8, e->stream));
   }
+  uint32_t st = 0;
+  HIPCHK(hipMemcpyAsync(&st, status, 4, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
+  if (st) return fail(RG_ENOMEM, "rg_import_replica: the payload page pool is empty");
   return RG_OK;
 }
 
@@ -1168,7 +1343,8 @@ static int astage_reserve(rg_engine* e, uint64_t bytes) {
 }
 
 int rg_persist_collect(rg_engine* e, int full, rg_persist_state* states, uint64_t cap_states, uint64_t* n_states,
-                       rg_persist_entry* entries, uint8_t* payload, uint64_t cap_entries, uint64_t* n_entries) {
+                       rg_persist_entry* entries, uint8_t* payload, uint64_t cap_entries, uint64_t* n_entries,
+                       uint64_t pay_cap, uint64_t* pay_bytes) {
   if (!e || !n_states || !n_entries) return fail(RG_EINVAL, "rg_persist_collect args");
   if (int jrc = join(e)) return jrc;
   const TickParams t = params(e);
@@ -1176,73 +1352,87 @@ int rg_persist_collect(rg_engine* e, int full, rg_persist_state* states, uint64_
   a.G = t.G; a.R = t.R; a.nrep = t.nrep; a.L = t.L; a.P = t.P; a.pl = e->pl;
   a.full = (full || e->t == 0) ? 1u : 0u;  // before the first tick there is no previous state
   a.s64 = t.s64_in; a.s64_prev = t.s64_out; a.s32 = t.s32_in; a.persist_lo = e->persist_lo;
-  a.tr = e->tr; a.info = e->info; a.pay = e->pay; a.zi = e->crc_tab + CRC_ZI_OFF;
-  a.scnt = e->pscnt; a.ecnt = e->pecnt; a.soff = e->psoff; a.eoff = e->peoff; a.bsum = e->absum;
+  a.tr = e->tr; a.info = e->info; a.pool = e->pool; a.pt = e->pt; a.PTS = e->PTS; a.zi = e->crc_tab + CRC_ZI_OFF;
+  a.scnt = e->pscnt; a.ecnt = e->pecnt; a.ccnt = e->pccnt; a.soff = e->psoff; a.eoff = e->peoff; a.coff = e->pcoff;
+  a.bsum = e->absum;
   LAUNCH(launch_persist_count(a, (uint64_t*)e->d_sum, e->stream), e->stream, "persist count");
-  uint64_t tot[2] = {0, 0};
-  HIPCHK(hipMemcpyAsync(tot, e->d_sum, 16, hipMemcpyDeviceToHost, e->stream));
+  uint64_t tot[3] = {0, 0, 0};
+  HIPCHK(hipMemcpyAsync(tot, e->d_sum, 24, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   *n_states = tot[0];
   *n_entries = tot[1];
-  if (tot[0] > cap_states || tot[1] > cap_entries) return fail(RG_EFULL, "rg_persist_collect: buffers too small");
+  const uint64_t pb = tot[2] * 16;
+  if (pay_bytes) *pay_bytes = pb;
+  if (tot[0] > cap_states || tot[1] > cap_entries || pb > pay_cap)
+    return fail(RG_EFULL, "rg_persist_collect: buffers too small");
   if (tot[0] == 0) return RG_OK;
-  if (!states || (tot[1] && (!entries || (a.P && !payload)))) return fail(RG_EINVAL, "rg_persist_collect: null output");
-  const uint64_t sb = tot[0] * sizeof(rg_persist_state), eb = tot[1] * sizeof(rg_persist_entry), pb = tot[1] * a.P;
+  if (!states || (tot[1] && !entries) || (pb && !payload)) return fail(RG_EINVAL, "rg_persist_collect: null output");
+  const uint64_t sb = a16(tot[0] * sizeof(rg_persist_state)), eb = a16(tot[1] * sizeof(rg_persist_entry));
   RGCHK(astage_reserve(e, sb + eb + pb));
   a.out_state = e->astage;
   a.out_ent = e->astage + sb;
   a.out_pay = e->astage + sb + eb;
   LAUNCH(launch_persist_gather(a, e->stream), e->stream, "persist gather");
-  HIPCHK(hipMemcpyAsync(states, a.out_state, sb, hipMemcpyDeviceToHost, e->stream));
-  if (eb) HIPCHK(hipMemcpyAsync(entries, a.out_ent, eb, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(states, a.out_state, tot[0] * sizeof(rg_persist_state), hipMemcpyDeviceToHost, e->stream));
+  if (tot[1]) HIPCHK(hipMemcpyAsync(entries, a.out_ent, tot[1] * sizeof(rg_persist_entry), hipMemcpyDeviceToHost, e->stream));
   if (pb) HIPCHK(hipMemcpyAsync(payload, a.out_pay, pb, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   return RG_OK;
 }
 
-int rg_apply_committed(rg_engine* e, uint32_t slot_mask, rg_apply_entry* entries, uint8_t* payload, uint64_t cap,
-                       uint64_t* n) {
-  if (!e || !n) return fail(RG_EINVAL, "rg_apply_committed args");
-  if (int jrc = join(e)) return jrc;
+static ApplyParams apply_params(rg_engine* e, uint32_t slot_mask) {
   const TickParams t = params(e);
   ApplyParams a{};
   a.G = t.G; a.R = t.R; a.nrep = t.nrep; a.L = t.L; a.P = t.P; a.slot_mask = slot_mask; a.pl = e->pl;
-  a.s64 = t.s64_in; a.apply_lo = e->apply_lo; a.tr = e->tr; a.info = e->info; a.pay = e->pay;
+  a.s64 = t.s64_in; a.apply_lo = e->apply_lo; a.tr = e->tr; a.info = e->info;
+  a.pool = e->pool; a.pt = e->pt; a.PTS = e->PTS;
   a.zi = e->crc_tab + CRC_ZI_OFF;
-  a.cnt = e->acnt; a.off = e->aoff; a.bsum = e->absum;
+  a.cnt = e->acnt; a.ccnt = e->accnt; a.off = e->aoff; a.coff = e->acoff; a.bsum = e->absum;
+  return a;
+}
+
+int rg_apply_committed(rg_engine* e, uint32_t slot_mask, rg_apply_entry* entries, uint8_t* payload, uint64_t cap,
+                       uint64_t* n, uint64_t pay_cap, uint64_t* pay_bytes) {
+  if (!e || !n) return fail(RG_EINVAL, "rg_apply_committed args");
+  if (int jrc = join(e)) return jrc;
+  ApplyParams a = apply_params(e, slot_mask);
   LAUNCH(launch_apply_count(a, (uint64_t*)e->d_sum, e->stream), e->stream, "apply count");
-  uint64_t total = 0;
-  HIPCHK(hipMemcpyAsync(&total, e->d_sum, 8, hipMemcpyDeviceToHost, e->stream));
+  uint64_t tot[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(tot, e->d_sum, 16, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
-  *n = total;
-  if (total == 0) return RG_OK;
-  if (total > cap) return fail(RG_EFULL, "rg_apply_committed: " + std::to_string(total) + " entries > cap");
-  if (!entries || (a.P && !payload)) return fail(RG_EINVAL, "rg_apply_committed: null output");
-  const uint64_t rb = total * sizeof(rg_apply_entry), pb = total * a.P;
+  *n = tot[0];
+  const uint64_t pb = tot[1] * 16;
+  if (pay_bytes) *pay_bytes = pb;
+  if (tot[0] == 0) return RG_OK;
+  if (tot[0] > cap || pb > pay_cap)
+    return fail(RG_EFULL, "rg_apply_committed: " + std::to_string(tot[0]) + " entries / " + std::to_string(pb) +
+                              " payload bytes exceed the buffers");
+  if (!entries || (pb && !payload)) return fail(RG_EINVAL, "rg_apply_committed: null output");
+  const uint64_t rb = a16(tot[0] * sizeof(rg_apply_entry));
   RGCHK(astage_reserve(e, rb + pb));
   a.out_rec = e->astage;
   a.out_pay = e->astage + rb;
   LAUNCH(launch_apply_gather(a, e->stream), e->stream, "apply gather");
-  HIPCHK(hipMemcpyAsync(entries, a.out_rec, rb, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(entries, a.out_rec, tot[0] * sizeof(rg_apply_entry), hipMemcpyDeviceToHost, e->stream));
   if (pb) HIPCHK(hipMemcpyAsync(payload, a.out_pay, pb, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   return RG_OK;
 }
 
+// Asynchronous copy-back: the gather runs on the engine stream right after the tick (the next tick
+// may reuse the window's log slots and release its pages) into device staging; then a copy kernel
+// with a handful of workgroups on the copy stream moves the staging into host-mapped pinned memory
+// over PCIe. The runtime's own D2H path (blit kernels over the whole chip, measured r02) slowed the
+// next ticks' kernels beside it; a few workgroups are enough to keep PCIe busy.
 int rg_apply_async(rg_engine* e, uint32_t slot_mask, int buf) {
   if (!e || buf < 0 || buf > 1) return fail(RG_EINVAL, "rg_apply_async args");
   if (int jrc = join(e)) return jrc;
-  const TickParams t = params(e);
-  ApplyParams a{};
-  a.G = t.G; a.R = t.R; a.nrep = t.nrep; a.L = t.L; a.P = t.P; a.slot_mask = slot_mask; a.pl = e->pl;
-  a.s64 = t.s64_in; a.apply_lo = e->apply_lo; a.tr = e->tr; a.info = e->info; a.pay = e->pay;
-  a.zi = e->crc_tab + CRC_ZI_OFF;
-  a.cnt = e->acnt; a.off = e->aoff; a.bsum = e->absum;
+  ApplyParams a = apply_params(e, slot_mask);
   LAUNCH(launch_apply_count(a, (uint64_t*)e->d_sum, e->stream), e->stream, "apply count");
-  uint64_t total = 0;
-  HIPCHK(hipMemcpyAsync(&total, e->d_sum, 8, hipMemcpyDeviceToHost, e->stream));
+  uint64_t tot[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(tot, e->d_sum, 16, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
-  const uint64_t rb = total * sizeof(rg_apply_entry), need = rb + total * a.P;
+  const uint64_t total = tot[0], rb = a16(total * sizeof(rg_apply_entry)), need = rb + tot[1] * 16;
   if (need > e->a_dcap[buf] || need > e->a_hcap[buf]) {  // grow: the buffer's last copy must be done
     HIPCHK(hipEventSynchronize(e->a_copy[buf]));
     const uint64_t nb = std::max<uint64_t>(need * 5 / 4, 1 << 20);
@@ -1261,7 +1451,8 @@ int rg_apply_async(rg_engine* e, uint32_t slot_mask, int buf) {
       if (e->a_host[buf]) (void)hipHostFree(e->a_host[buf]);
       e->a_host[buf] = nullptr;
       e->a_hcap[buf] = 0;
-      if (hipHostMalloc((void**)&e->a_host[buf], nb, 0) != hipSuccess) return fail(RG_ENOMEM, "hipHostMalloc (apply)");
+      if (hipHostMalloc((void**)&e->a_host[buf], nb, hipHostMallocMapped) != hipSuccess)
+        return fail(RG_ENOMEM, "hipHostMalloc (apply)");
       e->a_hcap[buf] = nb;
     }
   }
@@ -1276,7 +1467,15 @@ int rg_apply_async(rg_engine* e, uint32_t slot_mask, int buf) {
   }
   HIPCHK(hipEventRecord(e->a_gath[buf], e->stream));
   HIPCHK(hipStreamWaitEvent(e->copy, e->a_gath[buf], 0));
-  if (total) HIPCHK(hipMemcpyAsync(e->a_host[buf], e->a_dev[buf], need, hipMemcpyDeviceToHost, e->copy));
+  if (total) {
+    if (e->copy_kernel) {
+      void* hdev = nullptr;
+      HIPCHK(hipHostGetDevicePointer(&hdev, e->a_host[buf], 0));
+      LAUNCH(launch_copy_to_host(e->a_dev[buf], hdev, need, e->copy), e->copy, "copy to host");
+    } else {
+      HIPCHK(hipMemcpyAsync(e->a_host[buf], e->a_dev[buf], need, hipMemcpyDeviceToHost, e->copy));
+    }
+  }
   HIPCHK(hipEventRecord(e->a_copy[buf], e->copy));
   return RG_OK;
 }
@@ -1287,7 +1486,19 @@ int rg_apply_wait(rg_engine* e, int buf, const rg_apply_entry** entries, const u
   HIPCHK(hipEventSynchronize(e->a_copy[buf]));
   *n = e->a_n[buf];
   if (entries) *entries = (const rg_apply_entry*)e->a_host[buf];
-  if (payload) *payload = e->a_host[buf] ? e->a_host[buf] + e->a_n[buf] * sizeof(rg_apply_entry) : nullptr;
+  if (payload) *payload = e->a_host[buf] ? e->a_host[buf] + a16(e->a_n[buf] * sizeof(rg_apply_entry)) : nullptr;
+  return RG_OK;
+}
+
+int rg_pool_stats(rg_engine* e, uint64_t* total_pages, uint64_t* free_pages, int* failed) {
+  if (!e) return fail(RG_EINVAL, "rg_pool_stats args");
+  if (int jrc = join(e)) return jrc;
+  PoolCtl c{};
+  HIPCHK(hipMemcpyAsync(&c, e->poolctl, sizeof c, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  if (total_pages) *total_pages = e->npages;
+  if (free_pages) *free_pages = c.tail >= c.head ? c.tail - c.head : 0;
+  if (failed) *failed = c.fail ? 1 : 0;
   return RG_OK;
 }
 

@@ -5,6 +5,7 @@
 // state the lanes of a wave take the same branch (same role).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #ifndef RG_HD_INLINE
@@ -15,15 +16,50 @@ namespace rg {
 
 constexpr uint32_t MAX_R = 8;
 // term-ring / inline-term word: term | cmd_len<<48 | type<<61 | has_payload<<62 | bank<<63
-// (terms < 2^48; cmd_len = the entry's Cmd bytes, 0..payload_bytes; has_payload ⇔ an application
-// entry with cmd_len > 0)
+// (terms < 2^48; cmd_len = the entry's Cmd bytes, 0..max_cmd_bytes (< 8192); has_payload ⇔ an
+// application entry with cmd_len > 0; bank = which of the two info banks holds the entry's
+// {crc, stream position})
 constexpr uint64_t BANK_BIT = 1ull << 63;
 constexpr uint64_t PAY_BIT = 1ull << 62;
 constexpr uint64_t TYPE_BIT = 1ull << 61;
 constexpr uint32_t LEN_SHIFT = 48;
 constexpr uint64_t TERM_MASK = (1ull << LEN_SHIFT) - 1;
+constexpr uint32_t MAX_CMD = 8191;  // the 13-bit length field
 RG_HD_INLINE uint32_t word_len(uint64_t w) { return (uint32_t)(w >> LEN_SHIFT) & 0x1FFFu; }
 RG_HD_INLINE uint64_t len_bits(uint32_t len) { return ((uint64_t)len << LEN_SHIFT) | (len ? PAY_BIT : 0ull); }
+// 16-B chunks of the payload stream an entry occupies (0: no Cmd bytes; a ConfigChange has none)
+RG_HD_INLINE uint32_t word_nc(uint64_t w) { return (w & PAY_BIT) ? (word_len(w) + 15u) >> 4 : 0u; }
+
+// ---- paged payload stream. Every replica appends its entries' Cmd bytes, each
+// rounded up to 16-B chunks, to its own stream; a stream position is a u32 chunk count (modular).
+// The stream is mapped through a per-replica ring of page ids pt[q][vpn & (PTS-1)] onto 4-KiB pages
+// of one engine-wide pool. Pages are taken when the stream grows (pool_kernel, after the control
+// step) and returned once compaction passed them (one step later, so same-launch readers of
+// entries sent in the previous step are done). Positions only grow: a truncated suffix's bytes stay
+// where they are (garbage until compaction passes them), so readers of an entry never race with a
+// rewrite of its index.
+constexpr uint32_t PAGE_LOG = 8;                        // chunks per page = 256
+constexpr uint32_t PAGE_CH = 1u << PAGE_LOG;
+constexpr uint32_t PAGE_BYTES = PAGE_CH * 16;           // 4 KiB
+constexpr uint32_t VPN_MASK = (1u << (32 - PAGE_LOG)) - 1;  // page numbers are positions >> 8, mod 2^24
+RG_HD_INLINE uint32_t vpn_of(uint32_t pos) { return pos >> PAGE_LOG; }
+RG_HD_INLINE uint32_t vpn_ceil(uint32_t pos) { return (uint32_t)(((uint64_t)pos + PAGE_CH - 1) >> PAGE_LOG) & VPN_MASK; }
+RG_HD_INLINE uint32_t vpn_diff(uint32_t a, uint32_t b) { return (a - b) & VPN_MASK; }
+// stream capacity rule (deterministic; the oracle applies the same): an append of c chunks is
+// allowed iff its last chunk's page stays within PTS pages of the lowest page still held
+RG_HD_INLINE bool stream_fits(uint32_t hw, uint32_t lpg, uint32_t c, uint32_t PTS) {
+  return c == 0 || vpn_diff(vpn_of(hw + c - 1u), lpg) < PTS;
+}
+// slab_info.x of a proposal-slab entry: SYN_OFF = the generator's Cmd (P bytes at the entry's fixed
+// slab slot); otherwise the chunk offset of a caller Cmd in its slab's Cmd arena
+constexpr uint32_t SYN_OFF = 0x80000000u;
+// engine-wide page pool state (device memory): free-id ring [npages] consumed at head, refilled at
+// tail; limit = tail as of the last bulk launch (ids below it were written by an earlier launch)
+struct PoolCtl {
+  unsigned long long head, tail, limit;
+  uint32_t fail;       // sticky: an allocation found the pool empty (ERR_POOL, the engine is poisoned)
+  uint32_t param_err;  // sticky: a control launch found a corrupt parameter block (checksum)
+};
 // A ConfigChange entry (TYPE_BIT, no payload) keeps its descriptor op << 4 | (slot + 1) in the
 // length field; 0 = the bootstrap entries
 enum : uint32_t { CC_ADD = 1, CC_REMOVE = 2 };
@@ -43,7 +79,9 @@ enum : uint32_t { FOLLOWER = 0, CANDIDATE = 1, LEADER = 2 };
 constexpr uint32_t RG_UNIFORM = 1;
 enum : uint32_t { RETRY = 0, WAIT = 1, REPLICATE = 2, SNAPSHOT = 3 };
 enum : uint32_t { ENTRY_APP = 0, ENTRY_CONFIG = 1 };
-enum : uint32_t { ERR_CONFLICT = 1, ERR_BEYOND = 2, ERR_RING = 4, ERR_CRC = 8, ERR_EMPTY_SNAP = 16, ERR_WIRE = 32 };
+enum : uint32_t {
+  ERR_CONFLICT = 1, ERR_BEYOND = 2, ERR_RING = 4, ERR_CRC = 8, ERR_EMPTY_SNAP = 16, ERR_WIRE = 32, ERR_POOL = 64
+};
 // RG_BOUNDS (diagnostic builds): kernels printf and skip any count or offset read from memory that
 // would index outside its buffer (ERR_WIRE in the replica's err word). Product builds check only
 // what arrives over the wire (unpack_kernel keeps the well-formed messages of a unit).
@@ -58,28 +96,43 @@ enum : uint32_t {
   S_TERM, S_VOTE, S_LEADER, S_COMMITTED, S_APPLIED, S_LAST, S_MARKER, S_MARKER_TERM, S_SNAP_INDEX,
   S_SNAP_TERM, S_CAP_BASE, S_PROCESSED,
   S_CC_HI,  // highest index a ConfigChange entry was written to (the apply scan stops there)
+  S_FIDX,   // compaction (or a restore) in the last step: the stream below this entry's position is free
   S64_ROWS
 };
 enum : uint32_t {
   S_ROLE, S_ETICK, S_HTICK, S_RAND_TO, S_RNG_CTR, S_GRANTED, S_RESPONDED, S_ACTIVE, S_ERR, S_DROPS,
   S_MEMBERS, S_SNAP_MEMBERS, S_CC_PENDING,  // membership
+  S_HW,    // payload stream: next free chunk position
+  S_LPG,   // lowest stream page still held (the capacity rule's base)
+  S_APG,   // stream pages held up to here (exclusive): [S_LPG, S_APG)
+  S_NLPG,  // control → pool_kernel: pages below this are free once the step is done (= S_LPG: none)
   S32_ROWS
 };
 // job rows
-enum : uint32_t { J_FIRST, J_DMASK, J_SMASK, J_HMASK, J_TMASK, J64_ROWS };
-enum : uint32_t { J_META, J_SRC, J32_ROWS };  // meta = n | e0<<8 | kind<<16
+enum : uint32_t { J_FIRST, J_SPOS, J_SMASK, J_DMASK, J64_ROWS };
+enum : uint32_t { J_META, J_SRC, J_DPOS, J32_ROWS };
+// meta = n | e0 << 8 | kind << 16 | uniform << 20 | ncu << 21
+RG_HD_INLINE uint32_t job_meta(uint32_t n, uint32_t e0, uint32_t kind, bool uni, uint32_t ncu) {
+  return n | (e0 << 8) | (kind << 16) | (uni ? 1u << 20 : 0u) | (ncu << 21);
+}
 // SRC_WIRE_PROP: a proposal forwarded from another rank — its Cmds in the receive buffer like
-// SRC_WIRE's entries, but with no sender CRC to verify
-enum : uint32_t { SRC_NONE = 0, SRC_RING = 1, SRC_SLAB = 2, SRC_WIRE = 3, SRC_WIRE_PROP = 4 };
-// SRC_RING job: J_SRC = the sender's replica q, J_SMASK = per-entry source bank bits.
-// SRC_SLAB job (a proposal): J_SRC = slab id | row slot << 16: the Cmds are in slab row = column
-// (one rank) or row slot · G + column (wire engines: the proposing replica's row).
-// SRC_WIRE job: the entries arrived over the wire (another rank's replica). J_SMASK holds the byte
-// offset of the message's first entry record in the receive buffer and J_SRC the message's entry
-// count n; record e = {u64 term word, u32 crc, u32 len} at +16e, payload e at +16n + P·e.
-// Entry Cmds are variable-length, len in [0, P] (in the term word): a payload slot holds the Cmd
-// zero-padded to P bytes, and its info word {crc, type << 24 | slot bytes} carries the CRC-32 of
-// the whole padded slot ("slot CRC"; equal to the Cmd's CRC when len = P). crc_of_cmd converts.
+// SRC_WIRE's entries, but with no sender CRC to verify. SRC_CMD: caller Cmds in a slab's Cmd arena.
+enum : uint32_t { SRC_NONE = 0, SRC_RING = 1, SRC_SLAB = 2, SRC_WIRE = 3, SRC_WIRE_PROP = 4, SRC_CMD = 5 };
+// A job is n entries [first + e0, first + n) written to this replica's log; their Cmd bytes go to its
+// stream from chunk J_DPOS on, back to back; J_DMASK = per-entry destination info bank bits.
+// Uniform jobs (meta bit 20): every entry is ncu chunks and the source bytes are contiguous too, so
+// the bulk kernel addresses them arithmetically (the steady state); other jobs read each entry's
+// source position (the bulk kernel's per-entry path).
+// SRC_RING: J_SRC = the sender's replica q, J_SMASK = per-entry source info bank bits; uniform:
+//   J_SPOS = the sender's stream position of message entry 0 (header word 5 of a uniform Replicate).
+// SRC_SLAB (generator Cmds, P bytes each, uniform) and SRC_CMD (caller Cmds): J_SRC = slab id | row
+//   slot << 16: the batch is in slab row = column (one rank) or row slot · G + column (wire engines:
+//   the proposing replica's row); SRC_CMD uniform: J_SPOS = arena chunk of entry e0.
+// SRC_WIRE / SRC_WIRE_PROP: the message arrived over the wire. J_SPOS = byte offset of its first
+//   entry record in the receive buffer, J_SRC = its entry count n; record e = {u64 term word, u32
+//   slot crc, u32 payload chunk offset} at +16e, payloads from +16n on.
+// Slot CRC: the CRC-32 of the Cmd zero-padded to S·P bytes, S = ceil(len / P) (= the Cmd's CRC when
+// len = S·P). The bulk kernel computes it with P-byte lane groups; crc_of_cmd converts.
 
 // ---- placement across ranks. Replica slot s of global group g lives on rank
 // (g mod N + off_c(s)) mod N, local column j = g div N, column class c = j mod (N − 1), with
@@ -145,6 +198,8 @@ struct TickParams {
   uint32_t ET, HT, CQ, SE, CO, drop_ppm, flags;
   uint32_t wire;           // wire engine: slab rows per replica (q), else per column (g)
   uint32_t AF;             // apply feedback: applied moves only by rg_notify_applied
+  uint32_t PTS;            // stream pages per replica (power of two; the capacity rule)
+  uint32_t JS;             // join slots (rg_config.join_slots): bootstrap with an empty log, no membership
   uint64_t seed, tick;
   Placement pl;
   RG_G(const uint64_t) s64_in;  // [S64_ROWS][nrep]
@@ -177,6 +232,7 @@ struct TickParams {
   RG_G(const uint8_t) prop_target;
   RG_G(const uint32_t) prop_count;
   RG_G(const uint64_t) prop_hmask;  // caller proposals: entries with a non-empty Cmd (NULL: synthetic, all of len P)
+  RG_G(const uint2) prop_cmd;       // caller proposals: {stream chunks | contiguous << 31, arena chunk of entry 0}
   RG_G(const uint2) slab_info;      // [nslab][rows][E] {0, Cmd length} of the proposal slabs
   RG_G(const uint8_t) campaign;
   RG_G(const uint8_t) isolate;
@@ -184,7 +240,18 @@ struct TickParams {
   RG_G(const uint16_t) cc_in;       // [global group] membership change of this tick: slot | descriptor << 8 (0 none)
   uint32_t IM;                 // bootstrap membership (rg_config.initial_members, 0 read as every slot)
   RG_G(uint64_t) rdst;              // [RD_ROWS][nrep] ReadIndex state
+  RG_G(const uint2) info;           // [2 banks][nrep][L] {slot crc, stream position} (a freed stream's bound)
+  RG_G(PoolCtl) pool;               // sticky param_err on a checksum mismatch
+  uint64_t csum;                    // tp_checksum of every word above (host-computed, checked first)
 };
+// the parameter block's checksum: mix64 chain over its words before `csum` (a stale or torn block
+// is reported as an engine error instead of being dereferenced)
+RG_HD_INLINE uint64_t tp_mix(uint64_t z) {
+  z ^= z >> 31;
+  z *= 0x9E3779B97F4A7C15ULL;
+  return z ^ (z >> 29);
+}
+constexpr uint32_t TP_WORDS = (uint32_t)(offsetof(TickParams, csum) / 8);
 
 struct BulkParams {
   uint32_t G, R, nrep, L, P, E, J, crc_const, tile;  // tile: groups per wave work item (1..64)
@@ -192,14 +259,33 @@ struct BulkParams {
   const uint64_t* job64;
   const uint32_t* job32;
   const uint32_t* jcnt;
-  uint2* info;           // [2 banks][nrep][L] {crc, type<<24 | len}
-  uint8_t* pay;          // [2 banks][nrep][L][P]
-  const uint8_t* slabs;  // [nslab][rows][E][P], rows = G, or nrep in wire_mode
+  const uint64_t* tr;    // term ring [L][nrep] (per-entry Cmd lengths of non-uniform jobs)
+  uint2* info;           // [2 banks][nrep][L] {slot crc, stream position}
+  uint8_t* pool;         // [npages][4 KiB] payload pages
+  uint32_t PTS;          // page-table entries per replica; pt = the kernel's own argument
+  const uint8_t* slabs;  // [nslab][rows][E][P], rows = G, or nrep in wire_mode (generator Cmds)
+  const uint2* slab_info;  // [nslab][rows][E] {SYN_OFF or arena chunk, len}
+  const uint8_t* cmds;   // [nslab][cmd_cap] caller Cmd arenas
+  uint64_t cmd_cap;
   const uint8_t* wire;   // receive buffer of the last exchange (SRC_WIRE jobs)
   uint32_t* crc_err;     // [nrep] sticky ERR_CRC from payload verification
   const uint32_t* crc_tab;
-  uint64_t wire_bytes;   // RG_BOUNDS checks: bytes of `wire` in use, proposal slabs
+  PoolCtl* poolctl;      // block 0 publishes limit = tail (the pool kernel of this tick has run)
+  uint64_t wire_bytes;   // bytes of `wire` in use (job bounds checks)
   uint32_t nslab;
+};
+
+// pool_kernel (after control, before bulk): frees the stream pages control released, allocates the
+// pages the step's appends need, and updates S_LPG / S_APG; on an empty pool ERR_POOL + no jobs
+struct PoolParams {
+  uint32_t nrep, PTS;
+  uint64_t npages;
+  uint32_t* s32_out;           // the step's output state rows (S_HW, S_NLPG written by control)
+  const uint32_t* s32_in;      // S_LPG / S_APG before the step
+  uint32_t* pt;                // [nrep][PTS] page ids
+  uint32_t* fring;             // [npages] free page ids
+  PoolCtl* ctl;
+  uint32_t* jcnt;              // the step's job counts (zeroed for a replica whose allocation failed)
 };
 
 // CRC-32/IEEE tables: T[k][b] = raw CRC of byte b followed by k zero bytes (k = 0..15);
@@ -215,19 +301,26 @@ constexpr uint32_t CRC_T_WORDS = 16 * 256;
 constexpr uint32_t CRC_N_WORDS = 16 * 2 * 16;
 constexpr uint32_t CRC_SH_STRIDE = 8 * 16 + 2;  // +2 words: lanes' tables start on different banks
 constexpr uint32_t CRC_SH_MAX_WORDS = 64 * CRC_SH_STRIDE;
-constexpr uint32_t CRC_ZI_BITS = 10;  // P − len < 1024
+constexpr uint32_t CRC_ZI_BITS = 10;  // S·P − len < P <= 1024
 constexpr uint32_t CRC_ZI_WORDS = CRC_ZI_BITS * 8 * 16;
 constexpr uint32_t CRC_ZI_OFF = CRC_T_WORDS + CRC_N_WORDS + CRC_SH_MAX_WORDS;
-constexpr uint32_t CRC_TAB_WORDS = CRC_ZI_OFF + CRC_ZI_WORDS;
+// ZP [8][16]: Z^P (P zero bytes) on a raw state, to chain the P-byte segments of a Cmd longer than P;
+// CS [S]: the finalisation constant of an S·P-byte message, Z^(S·P)(~0) ^ ~0 (S = 1 .. CRC_CS_MAX)
+constexpr uint32_t CRC_ZP_OFF = CRC_ZI_OFF + CRC_ZI_WORDS;
+constexpr uint32_t CRC_ZP_WORDS = 8 * 16;
+constexpr uint32_t CRC_CS_OFF = CRC_ZP_OFF + CRC_ZP_WORDS;
+constexpr uint32_t CRC_CS_MAX = 512;  // ceil(MAX_CMD / 16)
+constexpr uint32_t CRC_TAB_WORDS = CRC_CS_OFF + CRC_CS_MAX + 1;
 
-// CRC-32 of a Cmd of len bytes from its slot CRC (the CRC of the Cmd zero-padded to P bytes):
-// slot = crc_const ^ raw(slot), raw(slot) = Z^(P−len) raw(Cmd), so
-// crc(Cmd) = Z^-(P−len)(slot ^ ~0) ^ ~0 (init / xorout ~0; Z = one zero byte, invertible).
+// CRC-32 of a Cmd of len bytes from its slot CRC (the CRC of the Cmd zero-padded to S·P bytes,
+// S = ceil(len / P)): slot = cs ^ raw(slot), raw(slot) = Z^(S·P−len) raw(Cmd), so
+// crc(Cmd) = Z^-(S·P−len)(slot ^ ~0) ^ ~0 (init / xorout ~0; Z = one zero byte, invertible).
 RG_HD_INLINE uint32_t crc_of_cmd(uint32_t slot_crc, uint32_t len, uint32_t P, const uint32_t* zi) {
   if (!len) return 0;
-  if (len >= P) return slot_crc;
+  const uint32_t padded = (len + P - 1) / P * P;
+  if (len == padded) return slot_crc;
   uint32_t v = slot_crc ^ 0xFFFFFFFFu;
-  const uint32_t k = P - len;
+  const uint32_t k = padded - len;
   for (uint32_t b = 0; b < CRC_ZI_BITS; ++b) {
     if ((k >> b) & 1u) {
       uint32_t r = 0;
@@ -238,25 +331,43 @@ RG_HD_INLINE uint32_t crc_of_cmd(uint32_t slot_crc, uint32_t len, uint32_t P, co
   return v ^ 0xFFFFFFFFu;
 }
 
+// byte offset in the pool of chunk `pos` of replica q's payload stream
+RG_HD_INLINE uint64_t stream_byte(const uint32_t* pt, uint32_t PTS, uint32_t q, uint32_t pos) {
+  const uint32_t pid = pt[(uint64_t)q * PTS + (vpn_of(pos) & (PTS - 1u))];
+  return ((uint64_t)pid * PAGE_BYTES) + ((uint64_t)(pos & (PAGE_CH - 1u)) << 4);
+}
+
 // host-side launchers (raftgpu_kernels.hip)
 // control_kernel<R> over nrep lanes; *p: the tick's parameter block in device memory
-hipError_t launch_control(const TickParams* p, uint32_t R, uint32_t nrep, hipStream_t s);
-hipError_t launch_bulk(const BulkParams& p, hipStream_t s, int grid);
+hipError_t launch_control(const TickParams* p, uint32_t* perr, uint32_t R, uint32_t nrep, hipStream_t s);
+hipError_t launch_pool(const PoolParams& p, hipStream_t s);
+// every page free, every replica's stream empty (bootstrap)
+hipError_t launch_pool_reset(uint32_t* fring, uint64_t npages, PoolCtl* ctl, hipStream_t s);
+hipError_t launch_bulk(const BulkParams& p, const uint32_t* pt, hipStream_t s, int grid);
 hipError_t launch_bootstrap(const TickParams& p, uint2* info, hipStream_t s);
-// synthetic Cmds into slabs [slab0, slab0 + nslab)
 // the address of a launch's kernel-argument segment (where the runtime put the arguments)
 hipError_t launch_kernarg_probe(uint64_t* out, uint64_t tag, hipStream_t s);
+// synthetic Cmds into slabs [slab0, slab0 + nslab)
 hipError_t launch_fill_slabs(uint8_t* slabs, uint2* slab_info, uint32_t slab0, uint32_t nslab, uint32_t G, uint32_t rows,
                              uint32_t E, uint32_t P, uint64_t seed, const Placement& pl, hipStream_t s);
-// caller proposals (rg_propose): Cmd e of the batch is copied from src + off[e] (len[e] bytes, zero-padded
-// to P) into slab entry dst[e] = (slab · rows + row) · E + k, and slab_info[dst[e]] = {0, len[e]}
-hipError_t launch_stage_cmds(uint8_t* slabs, uint2* slab_info, uint32_t P, const uint8_t* src, const uint64_t* off,
-                             const uint64_t* dst, const uint32_t* len, uint64_t n, hipStream_t s);
+// caller proposals (rg_propose): the Cmd bytes reach their slab's arena by one H2D copy; this
+// writes their descriptors slab_info[info_at[e]] = {chunk[e], len[e]}
+struct StageParams {
+  uint2* slab_info;
+  const uint64_t* info_at;  // [n] slab_info index
+  const uint32_t* chunk;    // [n] arena chunk of the Cmd
+  const uint32_t* len;      // [n]
+  uint64_t n;
+};
+hipError_t launch_stage_cmds(const StageParams& a, hipStream_t s);
 hipError_t launch_probe_copy(const void* src, void* dst, uint64_t bytes, hipStream_t s);
+// device staging → host-mapped pinned memory with a few workgroups (rg_apply_async)
+hipError_t launch_copy_to_host(const void* src, void* dst, uint64_t bytes, hipStream_t s);
 hipError_t launch_sum_committed(const TickParams& p, unsigned long long* out, hipStream_t s);
 hipError_t launch_traffic(const TickParams& p, unsigned long long* out6, hipStream_t s);
 // committed-entry copy-back (raftgpu_apply.hip): after a tick, the application entries each replica
-// applied in it, (apply_lo - 1, applied], gathered for IOnDiskStateMachine.Update
+// applied in it, (apply_lo - 1, applied], gathered for IOnDiskStateMachine.Update; payloads packed
+// back to back, each rounded up to 16 B (rg_apply_entry.off)
 struct ApplyParams {
   uint32_t G, R, nrep, L, P;
   uint32_t slot_mask;       // replicas whose slot bit is set
@@ -265,15 +376,20 @@ struct ApplyParams {
   const uint64_t* apply_lo;
   const uint64_t* tr;
   const uint2* info;
-  const uint8_t* pay;
+  const uint8_t* pool;
+  const uint32_t* pt;
+  uint32_t PTS;
   const uint32_t* zi;       // CRC inverse-shift tables (crc_of_cmd)
   uint32_t* cnt;            // [nrep] entries per replica
-  uint64_t* off;            // [nrep + 1] exclusive scan
+  uint32_t* ccnt;           // [nrep] payload chunks per replica
+  uint64_t* off;            // [nrep + 1] exclusive scan of cnt
+  uint64_t* coff;           // [nrep + 1] exclusive scan of ccnt
   uint64_t* bsum;           // scan scratch
   uint8_t* out_rec;         // [n] rg_apply_entry
-  uint8_t* out_pay;         // [n][P]
+  uint8_t* out_pay;         // [chunks][16]
+  uint32_t out_host;        // out_* are host-mapped pinned memory: plain (not non-temporal) stores
 };
-hipError_t launch_apply_count(const ApplyParams& a, uint64_t* total, hipStream_t s);
+hipError_t launch_apply_count(const ApplyParams& a, uint64_t* totals /*[2]: entries, chunks*/, hipStream_t s);
 // snapshot events (raftgpu_apply.hip)
 constexpr uint64_t SNAP_TAKEN_BIT = 1ull << 63;
 struct SnapParams {
@@ -295,7 +411,7 @@ hipError_t launch_read_count(const SnapParams& a, uint64_t* total, hipStream_t s
 hipError_t launch_read_gather(const SnapParams& a, hipStream_t s);
 // persistence copy-back (raftgpu_apply.hip): per replica whose log or hard state changed in the
 // last tick, its state record and the entries it rewrote ([persist_lo, last]); full = every
-// replica with its whole log window (marker, last] (a checkpoint)
+// replica with its whole log window (marker, last] (a checkpoint). Payloads packed (rg_persist_entry.off)
 struct PersistParams {
   uint32_t G, R, nrep, L, P, full;
   Placement pl;
@@ -305,18 +421,22 @@ struct PersistParams {
   const uint64_t* persist_lo;
   const uint64_t* tr;
   const uint2* info;
-  const uint8_t* pay;
+  const uint8_t* pool;
+  const uint32_t* pt;
+  uint32_t PTS;
   const uint32_t* zi;
   uint32_t* scnt;            // [nrep] 1 if the replica has a record
   uint32_t* ecnt;            // [nrep] entries to save
+  uint32_t* ccnt;            // [nrep] their payload chunks
   uint64_t* soff;            // [nrep + 1]
   uint64_t* eoff;            // [nrep + 1]
+  uint64_t* coff;            // [nrep + 1]
   uint64_t* bsum;
   uint8_t* out_state;        // [ns] rg_persist_state
   uint8_t* out_ent;          // [ne] rg_persist_entry
-  uint8_t* out_pay;          // [ne][P]
+  uint8_t* out_pay;          // [chunks][16]
 };
-hipError_t launch_persist_count(const PersistParams& a, uint64_t* totals /*[2]*/, hipStream_t s);
+hipError_t launch_persist_count(const PersistParams& a, uint64_t* totals /*[3]: states, entries, chunks*/, hipStream_t s);
 hipError_t launch_persist_gather(const PersistParams& a, hipStream_t s);
 hipError_t launch_apply_gather(const ApplyParams& a, hipStream_t s);
 // exclusive scan of n u32 into out[0..n] (out[n] = total); bsum: (n + 1023) / 1024 + 1 words
@@ -326,7 +446,13 @@ hipError_t launch_scan_u32(const uint32_t* in, uint32_t n, uint64_t* bsum, uint6
 struct AdminParams {
   TickParams t;              // the parameter block the next tick would use (s64_in = current state)
   const uint2* info;
-  const uint8_t* pay;
+  uint8_t* pool;
+  uint32_t* pt;
+  uint32_t PTS;
+  uint32_t row;              // bytes per entry row of rg_read_entries / rg_import_replica (max_cmd_bytes)
+  uint32_t* fring;
+  uint64_t npages;
+  PoolCtl* poolctl;
   const uint32_t* crc_err;
   const uint32_t* zi;
 };
@@ -336,9 +462,13 @@ hipError_t launch_gather_msgs(const AdminParams& a, uint32_t rid, uint32_t dst, 
                               uint32_t* out_cnt, hipStream_t s);
 hipError_t launch_gather_entries(const AdminParams& a, uint32_t rid, uint64_t first, uint32_t n, void* out_views,
                                  uint8_t* out_pay, hipStream_t s);
+// import: the view + entry words (term|len|type|pay, bank 0) + slot CRCs + stream positions of a fresh
+// stream (chunk offsets from 0) + the Cmds back to back in whole chunks (nch in all). The replica's
+// old stream pages go back to the pool and its new stream takes ceil(nch / 256) pages (*status = 1
+// if the pool is empty: nothing changed)
 hipError_t launch_scatter_replica(const AdminParams& a, uint32_t rid, const void* view, const uint64_t* words,
-                                  const uint8_t* pays, const uint32_t* crcs, uint32_t nent, hipStream_t s,
-                                  uint2* info, uint8_t* pay);
+                                  const uint32_t* crcs, const uint32_t* pos, const uint8_t* chunks, uint32_t nent,
+                                  uint32_t nch, uint32_t* status, hipStream_t s);
 hipError_t launch_deliver(const AdminParams& a, uint32_t rid_src, const void* hdr, uint32_t* status,
                           hipStream_t s);
 // rg_notify_applied: check (pass 0: *bad = number of rids / indices out of range) or set (pass 1) applied

@@ -18,6 +18,7 @@
 //   sender's ring (no staging copy); DESIGN.md §2 explains the two payload banks that keep the
 //   same-launch reads and rewrites disjoint.
 #include <algorithm>
+#include <cstdlib>
 
 #include "raftgpu_control.h"
 
@@ -34,33 +35,49 @@ __device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_re
                          // its last one ends (r02 A/B vs 256: control 0.122 -> 0.118 ms at 64K x 3, C2 0.043 -> 0.041)
 #endif
 // The parameter block comes by pointer from a device slot the host filled with a stream-ordered
-// copy (DESIGN.md §3 "The control-kernel fault"); Ctl copies it (scalar loads, uniform address).
+// copy (DESIGN.md §3 "The control-kernel fault"). Before anything is dereferenced, every lane checks
+// the block's checksum (uniform scalar loads): a stale or torn block becomes a sticky engine error
+// (*perr, a separate kernel argument, reported by the next synchronising call) instead of wild
+// addresses. Ctl reads the fields in place.
 template <int R>
-__global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_MINWAVES) control_kernel(const TickParams* __restrict__ pp) {
+__global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_MINWAVES) control_kernel(const TickParams* __restrict__ pp,
+                                                                               uint32_t* perr) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-  const TickParams p = *pp;
-  if (q >= p.nrep) return;
+  // volatile: these loads must not be merged with the field loads of the step (that kept every
+  // field of the block live across the whole step)
+  const volatile uint64_t* w = reinterpret_cast<const volatile uint64_t*>(pp);
+  uint64_t h = 0;
+  for (uint32_t i = 0; i < TP_WORDS; ++i) h = tp_mix(h ^ w[i]);
+  if (h != w[TP_WORDS]) {
+    if (q == 0) {
+      printf("raftgpu: control_kernel parameter block checksum mismatch (tick %llu): launch skipped\n",
+             (unsigned long long)pp->tick);
+      atomicOr(perr, 1u);
+    }
+    return;
+  }
+  if (q >= pp->nrep) return;
 #ifdef RG_CTL_PROFILE
   const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memtime();
-  Ctl<R> c(p, q);
+  Ctl<R> c(*pp, q);
   c.stamps[0] = t0;
 #else
-  Ctl<R> c(p, q);
+  Ctl<R> c(*pp, q);
 #endif
   c.run();
 }
 
-hipError_t launch_control(const TickParams* p, uint32_t R, uint32_t nrep, hipStream_t s) {
+hipError_t launch_control(const TickParams* p, uint32_t* perr, uint32_t R, uint32_t nrep, hipStream_t s) {
   dim3 grid((nrep + RG_CTL_BLOCK - 1) / RG_CTL_BLOCK), block(RG_CTL_BLOCK);
   switch (R) {
-    case 1: hipLaunchKernelGGL(control_kernel<1>, grid, block, 0, s, p); break;
-    case 2: hipLaunchKernelGGL(control_kernel<2>, grid, block, 0, s, p); break;
-    case 3: hipLaunchKernelGGL(control_kernel<3>, grid, block, 0, s, p); break;
-    case 4: hipLaunchKernelGGL(control_kernel<4>, grid, block, 0, s, p); break;
-    case 5: hipLaunchKernelGGL(control_kernel<5>, grid, block, 0, s, p); break;
-    case 6: hipLaunchKernelGGL(control_kernel<6>, grid, block, 0, s, p); break;
-    case 7: hipLaunchKernelGGL(control_kernel<7>, grid, block, 0, s, p); break;
-    case 8: hipLaunchKernelGGL(control_kernel<8>, grid, block, 0, s, p); break;
+    case 1: hipLaunchKernelGGL(control_kernel<1>, grid, block, 0, s, p, perr); break;
+    case 2: hipLaunchKernelGGL(control_kernel<2>, grid, block, 0, s, p, perr); break;
+    case 3: hipLaunchKernelGGL(control_kernel<3>, grid, block, 0, s, p, perr); break;
+    case 4: hipLaunchKernelGGL(control_kernel<4>, grid, block, 0, s, p, perr); break;
+    case 5: hipLaunchKernelGGL(control_kernel<5>, grid, block, 0, s, p, perr); break;
+    case 6: hipLaunchKernelGGL(control_kernel<6>, grid, block, 0, s, p, perr); break;
+    case 7: hipLaunchKernelGGL(control_kernel<7>, grid, block, 0, s, p, perr); break;
+    case 8: hipLaunchKernelGGL(control_kernel<8>, grid, block, 0, s, p, perr); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -71,6 +88,7 @@ struct Crc {
   const uint32_t* T;   // LDS [16][256] byte tables
   const uint32_t* N;   // LDS [16][2][16] nibble tables
   const uint32_t* SH;  // LDS this lane's [8][16] shift table
+  const uint32_t* ZP;  // LDS [8][16] Z^P (a Cmd longer than P: chaining its P-byte segments)
   // raw CRC contribution of a 16-byte chunk taken as the last 16 bytes of a message
   __device__ __forceinline__ uint32_t raw16(uint4 v) const {
     uint32_t r = 0;
@@ -88,11 +106,17 @@ struct Crc {
 #endif
     return r;
   }
-  // Z^(16·(NCH−1−c))(v): move this lane's chunk contribution to the end of the entry
+  // Z^(16·(NCH−1−c))(v): move this lane's chunk contribution to the end of its P-byte segment
   __device__ __forceinline__ uint32_t shift(uint32_t v) const {
     uint32_t r = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) r ^= SH[j * 16 + ((v >> (4 * j)) & 0xF)];
+    return r;
+  }
+  __device__ __forceinline__ uint32_t zp(uint32_t v) const {
+    uint32_t r = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r ^= ZP[j * 16 + ((v >> (4 * j)) & 0xF)];
     return r;
   }
 };
@@ -109,16 +133,27 @@ __device__ __forceinline__ uint32_t xor_lanes(uint32_t v) {
   return v;
 }
 
+__device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t v) {
+  const uint32_t lane = lane_id();
+  uint32_t x = v;
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+    if (lane >= o) x += y;
+  }
+  return x - v;
+}
+
 #ifndef RG_BULK_U
 #define RG_BULK_U 4
 #endif
 constexpr int BULK_U = RG_BULK_U;  // 16-B chunks in flight per lane
 
 // One copy job, its fields uniform across the wave (SGPRs): n entries from `first`, payloads
-// from the sender's ring or a proposal slab into this replica's ring, CRC per entry.
+// from the sender's stream, a proposal slab / Cmd arena or the receive buffer into this replica's
+// stream, CRC per entry (raftgpu_internal.h: job rows).
 struct Job {
-  uint64_t first, dm, sm, hm, tm;
-  uint32_t meta, src;
+  uint64_t first, spos, sm, dm;
+  uint32_t meta, src, dpos;
 };
 
 __device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l) {
@@ -132,24 +167,25 @@ __device__ __forceinline__ Job load_job(const BulkParams& p, uint32_t q, uint32_
   const uint64_t JN = (uint64_t)p.J * p.nrep, jq = (uint64_t)j * p.nrep + q;
   Job jb;
   jb.first = p.job64[J_FIRST * JN + jq];
-  jb.dm = p.job64[J_DMASK * JN + jq];
+  jb.spos = p.job64[J_SPOS * JN + jq];
   jb.sm = p.job64[J_SMASK * JN + jq];
-  jb.hm = p.job64[J_HMASK * JN + jq];
-  jb.tm = p.job64[J_TMASK * JN + jq];
+  jb.dm = p.job64[J_DMASK * JN + jq];
   jb.meta = p.job32[J_META * JN + jq];
   jb.src = p.job32[J_SRC * JN + jq];
+  jb.dpos = p.job32[J_DPOS * JN + jq];
   return jb;
 }
 
 // ---- software-pipelined payload stream.
 // A wave walks a flat sequence of steps over the jobs of its tiles; one step = epi entries of one
-// job, 16 B per lane. BULK_U steps are in flight at once in a register ring: slot u is consumed
-// (store, CRC, info, verify) and immediately re-issued with the step BULK_U ahead. All cursor
-// state is wave-uniform (SGPRs).
+// uniform job, 16 B per lane. BULK_U steps are in flight at once in a register ring: slot u is
+// consumed (store, CRC, info, verify) and immediately re-issued with the step BULK_U ahead. All
+// cursor state is wave-uniform (SGPRs). A non-uniform job drains the ring and runs on its own
+// (vjob: per-entry source positions, Cmds of any length).
 struct Cursor {
-  uint32_t t, q, qb, g, njl, j, n, kind, src, b;
-  uint64_t m, first, dm, sm, hm, tm;
-  bool live;
+  uint32_t t, q, qb, g, njl, j, n, kind, src, b, e0, ncu, dpos;
+  uint64_t m, first, spos, sm, dm;
+  bool live, uni;
 };
 
 struct TileJobs {  // per lane: job count and first job of replica qb + lane
@@ -188,39 +224,47 @@ __device__ __forceinline__ void load_tile(const BulkParams& p, Cursor& cur, Tile
   cur.njl = 0;
 }
 
-template <bool WIRE>
+template <int LG, bool WIRE>
 __device__ __forceinline__ void set_job(const BulkParams& p, Cursor& cur, const Job& jb) {
-  cur.first = jb.first; cur.dm = jb.dm; cur.sm = jb.sm; cur.hm = jb.hm; cur.tm = jb.tm;
-  cur.n = jb.meta & 0xFF; cur.b = (jb.meta >> 8) & 0xFF; cur.kind = (jb.meta >> 16) & 0xF; cur.src = jb.src;
-  cur.g = WIRE ? (cur.src >> 16) * p.G + cur.q % p.G : cur.q % p.G;  // SRC_SLAB: the proposal's slab row
-  cur.src &= cur.kind == SRC_SLAB ? 0xFFFFu : 0xFFFFFFFFu;
+  constexpr uint32_t NCH = 1u << LG;
+  cur.first = jb.first; cur.spos = jb.spos; cur.sm = jb.sm; cur.dm = jb.dm; cur.dpos = jb.dpos;
+  cur.n = jb.meta & 0xFF; cur.b = (jb.meta >> 8) & 0xFF; cur.e0 = cur.b; cur.kind = (jb.meta >> 16) & 0xF;
+  cur.uni = (jb.meta >> 20) & 1; cur.ncu = (jb.meta >> 21) & 0x7F;
+  cur.src = jb.src;
+  const bool slab = cur.kind == SRC_SLAB || cur.kind == SRC_CMD;
+  cur.g = WIRE ? (cur.src >> 16) * p.G + cur.q % p.G : cur.q % p.G;  // SRC_SLAB / SRC_CMD: the batch's slab row
+  if (slab) cur.src &= 0xFFFFu;
+  const bool wk = cur.kind == SRC_WIRE || cur.kind == SRC_WIRE_PROP;
   // a malformed job (never produced by control_kernel) is skipped and marks its replica ERR_WIRE
-  const bool bad = cur.n > 64 || cur.b > cur.n || (cur.kind == SRC_RING && cur.src >= p.nrep) ||
-                   (cur.kind == SRC_SLAB && (cur.src >= p.nslab || cur.g >= (WIRE ? p.nrep : p.G))) ||
-                   cur.kind > SRC_WIRE_PROP ||
-                   (cur.kind == SRC_WIRE && (!p.wire_mode || cur.n > cur.src ||
-                                             cur.sm + (16ull + p.P) * cur.src > p.wire_bytes));
+  const bool bad =
+      cur.n > 64 || cur.e0 > cur.n || cur.kind > SRC_CMD || (cur.uni && cur.ncu > NCH) ||
+      (cur.kind == SRC_SLAB && (!cur.uni || cur.ncu != NCH)) || (cur.kind == SRC_RING && cur.src >= p.nrep) ||
+      (slab && (cur.src >= p.nslab || cur.g >= (WIRE ? p.nrep : p.G))) ||
+      (wk && (!p.wire_mode || cur.n > cur.src || cur.spos + 16ull * cur.src > p.wire_bytes ||
+              (cur.uni && (cur.e0 != 0 || cur.spos + 16ull * cur.src * (1 + cur.ncu) > p.wire_bytes)))) ||
+      (cur.kind == SRC_CMD && cur.uni && (cur.spos + (uint64_t)(cur.n - cur.e0) * cur.ncu) * 16 > p.cmd_cap);
   if (bad) {
 #ifdef RG_BOUNDS
     if (lane_id() == 0)
-      printf("RG_BOUNDS bulk q=%u job=%u n=%u b=%u kind=%u src=%u sm=%llu wire_bytes=%llu\n", cur.q, cur.j, cur.n,
-             cur.b, cur.kind, cur.src, (unsigned long long)cur.sm, (unsigned long long)p.wire_bytes);
+      printf("RG_BOUNDS bulk q=%u job=%u n=%u e0=%u kind=%u src=%u spos=%llu wire_bytes=%llu\n", cur.q, cur.j, cur.n,
+             cur.e0, cur.kind, cur.src, (unsigned long long)cur.spos, (unsigned long long)p.wire_bytes);
 #endif
     if (lane_id() == 0) atomicOr(p.crc_err + cur.q, ERR_WIRE);
     cur.n = 0;
-    cur.b = 0;
+    cur.b = cur.e0 = 0;
+    cur.uni = true;
   }
 }
 
 // Move the cursor one position: the replica's next job, the tile's next replica, or the next
 // tile (whose descriptors arrive in one round trip; that pass issues nothing). A job with no
 // entries left to write simply yields an empty pass. Returns false once the wave is done.
-template <bool WIRE = false>
+template <int LG, bool WIRE>
 __device__ __forceinline__ bool next_job(const BulkParams& p, Cursor& cur, TileJobs& tj, uint32_t stride,
                                          uint32_t ntiles) {
   if (cur.j + 1 < cur.njl) {
     ++cur.j;
-    set_job<WIRE>(p, cur, load_job(p, cur.q, cur.j));
+    set_job<LG, WIRE>(p, cur, load_job(p, cur.q, cur.j));
   } else if (cur.m) {
     const uint32_t l = rfl((uint32_t)__ffsll((long long)cur.m) - 1);
     cur.m &= cur.m - 1;
@@ -228,39 +272,145 @@ __device__ __forceinline__ bool next_job(const BulkParams& p, Cursor& cur, TileJ
     cur.njl = __builtin_amdgcn_readlane(tj.nj, l);
     cur.j = 0;
     Job jb;
-    jb.first = rl64(tj.j0.first, l); jb.dm = rl64(tj.j0.dm, l); jb.sm = rl64(tj.j0.sm, l);
-    jb.hm = rl64(tj.j0.hm, l); jb.tm = rl64(tj.j0.tm, l);
+    jb.first = rl64(tj.j0.first, l); jb.spos = rl64(tj.j0.spos, l); jb.sm = rl64(tj.j0.sm, l);
+    jb.dm = rl64(tj.j0.dm, l);
     jb.meta = __builtin_amdgcn_readlane(tj.j0.meta, l); jb.src = __builtin_amdgcn_readlane(tj.j0.src, l);
-    set_job<WIRE>(p, cur, jb);
+    jb.dpos = __builtin_amdgcn_readlane(tj.j0.dpos, l);
+    set_job<LG, WIRE>(p, cur, jb);
   } else {
     cur.t += stride;
     if (cur.t >= ntiles) return false;
     load_tile(p, cur, tj);
     cur.b = 0;  // two statements: the chained form kept Cursor in scratch
     cur.n = 0;
+    cur.uni = true;
   }
   return true;
 }
 
-enum : uint32_t { F_ACT = 1, F_WRITER = 2, F_TYPE = 4, F_CHECK = 8 };
+enum : uint32_t { F_ACT = 1, F_WRITER = 2, F_CHECK = 8 };
 
+// the entry info word {slot crc, stream position} (and the sender-CRC check) of job entry e
+__device__ __forceinline__ void put_info(const BulkParams& p, uint32_t q, uint64_t first, uint64_t dm, uint32_t e,
+                                         uint32_t crc, uint32_t pos, bool check, uint32_t want) {
+  const uint64_t slot = (first + e) & (p.L - 1), bank = (dm >> e) & 1ull;
+  p.info[(bank * p.nrep + q) * p.L + slot] = make_uint2(crc, pos);
+  if (check && want != crc) atomicOr(p.crc_err + q, ERR_CRC);
+}
 
-// P = 16 << LG bytes per entry: 2^LG lanes per entry (16 B each), 64 >> LG entries per step.
+// A non-uniform job (Cmds of different lengths, a Replicate the sender built from its ring, caller
+// Cmds, Cmds longer than P): lane e reads entry e's source position and length, a wave scan lays
+// the Cmds out back to back from J_DPOS, then up to 64/NCH entries of at most P bytes move per
+// pass (NCH lanes each, as in the uniform path), and a longer Cmd moves alone, 64 chunks per pass,
+// its P-byte segments' CRCs chained with Z^P. Page-table lookups are per lane (not pipelined).
+template <int LG, bool WIRE>
+__device__ void vjob(const BulkParams& p, const uint32_t* __restrict__ pt, const Cursor& cur, const Crc& crc) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  constexpr uint32_t NCH = 1u << LG, EPI = 64u >> LG;
+  const uint32_t lane = lane_id(), c = lane & (NCH - 1), ei = lane >> LG;
+  const uint32_t n = cur.n, e0 = cur.e0, q = cur.q, kind = cur.kind;
+  const uint64_t n64 = p.nrep, L = p.L, PTS = p.PTS;
+  const bool ring = kind == SRC_RING, wire = WIRE && (kind == SRC_WIRE || kind == SRC_WIRE_PROP);
+  const bool check = ring || (WIRE && kind == SRC_WIRE);
+  const uint64_t rows = WIRE ? p.nrep : p.G;
+  const uint8_t* arena = p.cmds + (uint64_t)cur.src * p.cmd_cap;
+  const uint64_t wpay = cur.spos + 16ull * n;  // wire: payload base
+  // lane e: entry e's chunks, source position (sender stream / arena / wire chunk) and sender CRC
+  const uint32_t e = lane;
+  const bool in = e >= e0 && e < n;
+  uint32_t nc = 0, sp = 0, want = 0;
+  if (in) {
+    const uint64_t slot = (cur.first + e) & (L - 1);
+    nc = word_nc(p.tr[slot * n64 + q]);
+    if (ring) {
+      const uint2 inf = p.info[(((cur.sm >> e) & 1ull) * n64 + cur.src) * L + slot];
+      want = inf.x;
+      sp = inf.y;
+    } else if (wire) {
+      const uint32_t* r = reinterpret_cast<const uint32_t*>(p.wire + cur.spos + 16ull * e);
+      want = r[2];
+      sp = r[3];
+      if (wpay + ((uint64_t)sp + nc) * 16 > p.wire_bytes) nc = sp = 0;  // validated by unpack; never here
+    } else if (kind == SRC_CMD) {
+      sp = p.slab_info[((uint64_t)cur.src * rows + cur.g) * p.E + e].x;
+      if (((uint64_t)sp + nc) * 16 > p.cmd_cap) nc = sp = 0;
+    } else {
+      nc = 0;
+    }
+  }
+  const uint32_t dpe = cur.dpos + wave_excl_scan32(nc);
+  const uint64_t bigm = __ballot(in && nc > NCH);
+  auto src_at = [&](uint32_t pos) -> const uint8_t* {
+    return ring ? p.pool + stream_byte(pt, p.PTS, cur.src, pos)
+           : wire ? p.wire + wpay + 16ull * pos
+                  : arena + 16ull * pos;
+  };
+  uint32_t ee = e0;
+  while (ee < n) {
+    const uint32_t nce = __builtin_amdgcn_readlane(nc, ee);
+    if (nce > NCH) {  // one Cmd longer than P
+      const uint32_t spe = __builtin_amdgcn_readlane(sp, ee), dpee = __builtin_amdgcn_readlane(dpe, ee);
+      uint32_t acc = 0;
+      for (uint32_t w0 = 0; w0 < nce; w0 += 64) {
+        const uint32_t k = w0 + lane;
+        u32x4 x = u32x4{0, 0, 0, 0};
+        if (k < nce) {
+          x = *reinterpret_cast<const u32x4*>(src_at(spe + k));
+          *reinterpret_cast<u32x4*>(p.pool + stream_byte(pt, p.PTS, q, dpee + k)) = x;
+        }
+        uint32_t v = crc.raw16(make_uint4(x.x, x.y, x.z, x.w));
+        if constexpr (LG > 0) v = xor_lanes<LG>(crc.shift(v));
+        for (uint32_t gi = 0; gi < EPI && w0 + gi * NCH < nce; ++gi)
+          acc = crc.zp(acc) ^ (uint32_t)__builtin_amdgcn_readlane(v, gi * NCH);
+      }
+      const uint32_t S = (nce + NCH - 1) / NCH;
+      const uint32_t cr = p.crc_tab[CRC_CS_OFF + (S <= CRC_CS_MAX ? S : CRC_CS_MAX)] ^ acc;
+      const uint32_t we = __builtin_amdgcn_readlane(want, ee);
+      if (lane == 0) put_info(p, q, cur.first, cur.dm, ee, cr, dpee, check, we);
+      ++ee;
+    } else {  // up to EPI consecutive Cmds of at most P bytes, NCH lanes each
+      uint32_t kk = n - ee < EPI ? n - ee : EPI;
+      const uint64_t bb = bigm >> ee;
+      if (bb) kk = min(kk, (uint32_t)__ffsll((long long)bb) - 1);
+      const uint32_t me = ee + ei;
+      const bool grp = ei < kk;
+      const uint32_t mnc = (uint32_t)__shfl((int)nc, (int)me, 64), msp = (uint32_t)__shfl((int)sp, (int)me, 64);
+      const uint32_t mdp = (uint32_t)__shfl((int)dpe, (int)me, 64), mw = (uint32_t)__shfl((int)want, (int)me, 64);
+      const bool act = grp && c < mnc;
+      u32x4 x = u32x4{0, 0, 0, 0};
+      if (act) {
+        x = *reinterpret_cast<const u32x4*>(src_at(msp + c));
+        *reinterpret_cast<u32x4*>(p.pool + stream_byte(pt, p.PTS, q, mdp + c)) = x;
+      }
+      uint32_t v = crc.raw16(make_uint4(x.x, x.y, x.z, x.w));
+      if constexpr (LG > 0) v = xor_lanes<LG>(crc.shift(v));
+      if (grp && c == 0) put_info(p, q, cur.first, cur.dm, me, mnc ? p.crc_const ^ v : 0u, mdp, check && mnc, mw);
+      ee += kk;
+    }
+  }
+  (void)PTS;
+}
+
+// P = 16 << LG bytes per lane group: 2^LG lanes per entry (16 B each), 64 >> LG entries per step.
 // WIRE: the engine exchanges messages with other ranks (SRC_WIRE jobs, slab rows per replica);
 // one-rank engines run the variant without those paths.
 template <int LG, bool WIRE>
-__global__ void __launch_bounds__(256) bulk_kernel(BulkParams p) {
+__global__ void __launch_bounds__(256) bulk_kernel(BulkParams p, const uint32_t* __restrict__ pt) {
   constexpr uint32_t NCH = 1u << LG, EPI = 64u >> LG, P = 16u << LG;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  for (uint32_t i = threadIdx.x; i < CRC_T_WORDS + CRC_N_WORDS + NCH * CRC_SH_STRIDE; i += blockDim.x)
-    lds[i] = p.crc_tab[i];
+  const uint32_t shw = CRC_T_WORDS + CRC_N_WORDS + NCH * CRC_SH_STRIDE;
+  for (uint32_t i = threadIdx.x; i < shw; i += blockDim.x) lds[i] = p.crc_tab[i];
+  for (uint32_t i = threadIdx.x; i < CRC_ZP_WORDS; i += blockDim.x) lds[shw + i] = p.crc_tab[CRC_ZP_OFF + i];
+  // pages freed by this tick's pool kernel become allocatable from the next tick on
+  if (blockIdx.x == 0 && threadIdx.x == 0) p.poolctl->limit = p.poolctl->tail;
   __syncthreads();
   const uint32_t waves = blockDim.x >> 6, lane = lane_id();
   const uint32_t stride = gridDim.x * waves;
   const uint32_t ntiles = bulk_ntiles(p);
   const uint64_t n64 = p.nrep, L = p.L, rows = WIRE ? p.nrep : p.G;
+  const uint32_t PTSM = p.PTS - 1;
   const uint32_t c = lane & (NCH - 1), ei = lane >> LG;
-  const Crc crc{lds, lds + CRC_T_WORDS, lds + CRC_T_WORDS + CRC_N_WORDS + c * CRC_SH_STRIDE};
+  const Crc crc{lds, lds + CRC_T_WORDS, lds + CRC_T_WORDS + CRC_N_WORDS + c * CRC_SH_STRIDE, lds + shw};
   Cursor cur{};
   TileJobs tj{};
   cur.t = rfl(blockIdx.x * waves + (threadIdx.x >> 6));
@@ -268,9 +418,10 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p) {
   load_tile(p, cur, tj);
   cur.b = 0;  // two statements: the chained form kept Cursor in scratch
   cur.n = 0;
-  cur.live = next_job<WIRE>(p, cur, tj, stride, ntiles);
+  cur.uni = true;
+  cur.live = next_job<LG, WIRE>(p, cur, tj, stride, ntiles);
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  // ring slot u: payload chunk, destination (slot | bank << 31), flags, sender's slot CRC
+  // ring slot u: payload chunk, destination pool chunk, flags, sender's slot CRC
   u32x4 x[BULK_U];
   uint32_t ds[BULK_U], fl[BULK_U], want[BULK_U];
 #pragma unroll
@@ -282,25 +433,26 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p) {
   // dummy address when the slot has no work, so the number of memory operations between a load
   // and its use is the same on every path and the compiler's vmcnt waits keep the ring in flight.
   // A pass never spans two jobs (the cursor moves once per pass), so the slots consumed in a pass
-  // all belong to the replica `cq` of the previous pass.
+  // all belong to the job `pj` the previous pass issued.
   const uint8_t* dummy = reinterpret_cast<const uint8_t*>(p.crc_tab);
-  uint32_t vmask = 0, iq = 0;
+  uint32_t vmask = 0;
+  uint32_t iq = 0, ib = 0, ie0 = 0, idp = 0, incu = 0;  // the job of the pass being issued (for its consume)
+  uint64_t ifirst = 0, idm = 0;
   do {
-    const uint32_t cq = iq;
-    iq = cur.q;
-    const uint64_t cbase = (uint64_t)cq * L;
+    const uint32_t cq = iq, cb = ib, ce0 = ie0, cdp = idp, cncu = incu;
+    const uint64_t cfirst = ifirst, cdm = idm;
+    iq = cur.q; ib = cur.b; ie0 = cur.e0; idp = cur.dpos; incu = cur.ncu; ifirst = cur.first; idm = cur.dm;
 #pragma unroll
     for (int u = 0; u < BULK_U; ++u) {
-      {  // consume slot u: store, CRC, info, verify (fl = 0 for an empty slot: no stores). A payload
-        // slot holds the Cmd zero-padded to P bytes (every writer copies whole slots), so the CRC is
-        // the slot CRC; the Cmd's length lives in the term word, not here.
+      {  // consume slot u: store, CRC, info, verify (fl = 0 for an empty slot: no stores). A stream's
+        // Cmd is followed by zeros up to its chunk boundary (every writer copies whole chunks), and
+        // lanes past a Cmd's chunks contribute nothing, so the CRC is the slot CRC.
         const bool act = fl[u] & F_ACT;
-        const uint64_t di = (uint64_t)(ds[u] >> 31) * n64 * L + cbase + (ds[u] & 0x7FFFFFFFu);
         if (act) {
 #ifdef RG_BULK_PLAIN_STORE
-          *reinterpret_cast<u32x4*>(p.pay + di * P + c * 16) = x[u];
+          *reinterpret_cast<u32x4*>(p.pool + (uint64_t)ds[u] * 16) = x[u];
 #else
-          __builtin_nontemporal_store(x[u], reinterpret_cast<u32x4*>(p.pay + di * P + c * 16));
+          __builtin_nontemporal_store(x[u], reinterpret_cast<u32x4*>(p.pool + (uint64_t)ds[u] * 16));
 #endif
         }
         uint32_t v = 0;
@@ -309,44 +461,64 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p) {
 #endif
         if constexpr (LG > 0) v = xor_lanes<LG>(crc.shift(v));  // raw(slot) = XOR_c Z^(after c)(raw c)
         if (fl[u] & F_WRITER) {
-          const uint32_t cr = act ? (p.crc_const ^ v) : 0u;
-          const uint32_t tl = ((fl[u] & F_TYPE) ? (1u << 24) : 0u) | (act ? P : 0u);
-          p.info[di] = make_uint2(cr, tl);
-          if ((fl[u] & F_CHECK) && want[u] != cr) atomicOr(p.crc_err + cq, ERR_CRC);
+          const uint32_t e = cb + u * EPI + ei;
+          put_info(p, cq, cfirst, cdm, e, act ? (p.crc_const ^ v) : 0u, cdp + (e - ce0) * cncu,
+                   (fl[u] & F_CHECK) != 0, want[u]);
         }
       }
       {  // issue the job's next step (or an empty step) into slot u
-        const bool step = cur.live && cur.b < cur.n;
+        const bool step = cur.live && cur.uni && cur.b < cur.n;
         const uint32_t e = cur.b + ei;
         const bool valid = step && e < cur.n;
-        const bool act = valid && ((cur.hm >> e) & 1ull);
-        const uint32_t slot = (uint32_t)((cur.first + e) & (L - 1));
-        const uint32_t db = valid ? (uint32_t)(cur.dm >> e) & 1u : 0u;
+        const bool act = valid && c < cur.ncu;
         const bool ring = cur.kind == SRC_RING, wire = WIRE && (cur.kind == SRC_WIRE || cur.kind == SRC_WIRE_PROP);
-        ds[u] = slot | (db << 31);
-        fl[u] = (act ? F_ACT : 0u) | ((valid && c == 0) ? F_WRITER : 0u) | (((cur.tm >> e) & 1ull) ? F_TYPE : 0u) |
+        // destination chunks of this step: at most 64, so at most two stream pages (page ids by
+        // scalar loads: uniform addresses)
+        const uint32_t d0 = cur.dpos + (cur.b - cur.e0) * cur.ncu, dv = vpn_of(d0);
+        const uint32_t dl = d0 + ei * cur.ncu + c;
+        uint32_t pd0 = 0, pd1 = 0, ps0 = 0, ps1 = 0;
+        const uint32_t s0 = (uint32_t)cur.spos + cur.b * cur.ncu, sv = vpn_of(s0);
+        if (step && cur.ncu) {
+          const uint64_t dr = (uint64_t)cur.q * p.PTS;
+          pd0 = pt[dr + (dv & PTSM)];
+          pd1 = pt[dr + ((dv + 1) & PTSM)];
+          if (ring) {
+            const uint64_t sr = (uint64_t)cur.src * p.PTS;
+            ps0 = pt[sr + (sv & PTSM)];
+            ps1 = pt[sr + ((sv + 1) & PTSM)];
+          }
+        }
+        const uint32_t pid = vpn_of(dl) == dv ? pd0 : pd1;
+        ds[u] = pid * PAGE_CH + (dl & (PAGE_CH - 1));
+        fl[u] = (act ? F_ACT : 0u) | ((valid && c == 0) ? F_WRITER : 0u) |
                 (((ring || (WIRE && cur.kind == SRC_WIRE)) && act) ? F_CHECK : 0u);
-        const uint64_t sb = (cur.sm >> e) & 1ull;
-        const uint64_t si = (sb * n64 + cur.src) * L + slot;
-        // wire: records {term word, slot crc, 0} at sm + 16e, payloads at sm + 16n + P·e (n = src)
-        const uint8_t* sp = ring   ? p.pay + si * P
-                            : wire ? p.wire + cur.sm + 16ull * cur.src + (uint64_t)P * e
-                                   : p.slabs + (((uint64_t)cur.src * rows + cur.g) * p.E + e) * P;
+        const uint64_t slot = (cur.first + e) & (L - 1);
+        const uint64_t si = (((cur.sm >> e) & 1ull) * n64 + cur.src) * L + slot;
+        const uint32_t sl = s0 + ei * cur.ncu + c;
+        const uint8_t* sp = ring ? p.pool + ((uint64_t)(vpn_of(sl) == sv ? ps0 : ps1) * PAGE_BYTES) + ((sl & (PAGE_CH - 1)) << 4)
+                            : wire ? p.wire + cur.spos + 16ull * cur.src + 16ull * (e * cur.ncu + c)
+                            : cur.kind == SRC_CMD
+                                ? p.cmds + (uint64_t)cur.src * p.cmd_cap + 16ull * ((uint32_t)cur.spos + (e - cur.e0) * cur.ncu + c)
+                                : p.slabs + (((uint64_t)cur.src * rows + cur.g) * p.E + e) * P + c * 16;
         sp = act ? sp : dummy;
         const uint32_t* wp = (ring && act) ? &p.info[si].x
-                             : (wire && act) ? reinterpret_cast<const uint32_t*>(p.wire + cur.sm + 16ull * e + 8)
+                             : (wire && act) ? reinterpret_cast<const uint32_t*>(p.wire + cur.spos + 16ull * e + 8)
                                              : reinterpret_cast<const uint32_t*>(dummy);
 #ifdef RG_BULK_NT_LOAD  // ablation: non-temporal loads (r01: 1.115 vs 1.090 ms plain)
-        x[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(sp + c * 16));
+        x[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(sp));
 #else  // temporal: the second follower's read of the same leader entries hits L2 / Infinity Cache
-        x[u] = *reinterpret_cast<const u32x4*>(sp + c * 16);
+        x[u] = *reinterpret_cast<const u32x4*>(sp);
 #endif
         want[u] = *wp;
         vmask = step ? (vmask | (1u << u)) : (vmask & ~(1u << u));
         cur.b += step ? EPI : 0u;
       }
     }
-    if (cur.live && cur.b >= cur.n) cur.live = next_job<WIRE>(p, cur, tj, stride, ntiles);
+    if (cur.live && !cur.uni && vmask == 0) {  // a non-uniform job once the ring has drained
+      vjob<LG, WIRE>(p, pt, cur, crc);
+      cur.b = cur.n;
+    }
+    if (cur.live && cur.b >= cur.n) cur.live = next_job<LG, WIRE>(p, cur, tj, stride, ntiles);
   } while (rfl((uint32_t)(vmask != 0 || cur.live)));
 }
 
@@ -356,7 +528,9 @@ static int lg_of(uint32_t P) {
   return lg;
 }
 
-int bulk_lds_bytes(uint32_t P) { return P ? (int)((CRC_T_WORDS + CRC_N_WORDS + (P / 16) * CRC_SH_STRIDE) * 4) : 16; }
+int bulk_lds_bytes(uint32_t P) {
+  return P ? (int)((CRC_T_WORDS + CRC_N_WORDS + (P / 16) * CRC_SH_STRIDE + CRC_ZP_WORDS) * 4) : 16;
+}
 
 template <bool W, class F>
 static hipError_t with_bulk_w(uint32_t P, F f) {
@@ -385,42 +559,131 @@ int bulk_blocks_per_cu(uint32_t P) {
   return (r == hipSuccess && n > 0) ? n : 1;
 }
 
-hipError_t launch_bulk(const BulkParams& p, hipStream_t s, int grid) {
+hipError_t launch_bulk(const BulkParams& p, const uint32_t* pt, hipStream_t s, int grid) {
   return with_bulk(p.P, p.wire_mode != 0, [&](auto k) {
-    hipLaunchKernelGGL(k, dim3(grid), dim3(256), bulk_lds_bytes(p.P), s, p);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(256), bulk_lds_bytes(p.P), s, p, pt);
     return hipGetLastError();
   });
 }
 
+// ================================================================== payload page pool
+// One lane per replica (coalesced state rows): return the stream pages control released
+// ([S_LPG, S_NLPG)) to the free ring and take the pages this step's appends need ([S_APG,
+// ceil(S_HW))), with one tail and one head atomic per wave. Allocations read ids below `limit`
+// (written by an earlier launch); frees write at and above the tail: disjoint.
+__global__ void __launch_bounds__(256) pool_kernel(PoolParams pp) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x, lane = lane_id();
+  const bool valid = q < pp.nrep;
+  const uint64_t n = pp.nrep, PTSM = pp.PTS - 1;
+  uint32_t lpg = 0, apg = 0, nlpg = 0, top = 0, f = 0, a = 0;
+  if (valid) {
+    lpg = pp.s32_in[S_LPG * n + q];
+    apg = pp.s32_in[S_APG * n + q];
+    nlpg = pp.s32_out[S_NLPG * n + q];
+    top = vpn_ceil(pp.s32_out[S_HW * n + q]);
+    f = vpn_diff(nlpg, lpg);
+    a = vpn_diff(top, apg);
+  }
+  const uint32_t fo = wave_excl_scan32(f), ao = wave_excl_scan32(a);
+  const uint32_t F = __builtin_amdgcn_readlane(fo + f, 63), A = __builtin_amdgcn_readlane(ao + a, 63);
+  unsigned long long fb = 0, ab = 0;
+  if (lane == 0) {
+    if (F) fb = atomicAdd(&pp.ctl->tail, (unsigned long long)F);
+    if (A) ab = atomicAdd(&pp.ctl->head, (unsigned long long)A);
+  }
+  fb = rl64(fb, 0);
+  ab = rl64(ab, 0);
+  const unsigned long long limit = pp.ctl->limit;
+  uint32_t* ptq = pp.pt + (uint64_t)q * pp.PTS;
+  for (uint32_t k = 0; k < f; k += 8) {  // frees: eight page-table reads in flight, then their ring writes
+    uint32_t v[8];
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) v[j] = k + j < f ? ptq[(lpg + k + j) & PTSM] : 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j)
+      if (k + j < f) pp.fring[(fb + fo + k + j) % pp.npages] = v[j];
+  }
+  const bool ok = ab + ao + a <= limit;
+  if (ok) {
+    for (uint32_t k = 0; k < a; k += 8) {
+      uint32_t v[8];
+#pragma unroll
+      for (uint32_t j = 0; j < 8; ++j) v[j] = k + j < a ? pp.fring[(ab + ao + k + j) % pp.npages] : 0u;
+#pragma unroll
+      for (uint32_t j = 0; j < 8; ++j)
+        if (k + j < a) ptq[(apg + k + j) & PTSM] = v[j];
+    }
+  }
+  if (valid) {
+    pp.s32_out[S_LPG * n + q] = nlpg;
+    pp.s32_out[S_APG * n + q] = ok ? top : apg;
+    if (!ok) {  // the pool is empty: this replica's appends of the step are not stored; the engine is poisoned
+      pp.s32_out[S_ERR * n + q] |= ERR_POOL;
+      pp.jcnt[q] = 0;
+      atomicOr(&pp.ctl->fail, 1u);
+    }
+  }
+}
+
+hipError_t launch_pool(const PoolParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(pool_kernel, dim3((p.nrep + 255) / 256), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+__global__ void pool_reset_kernel(uint32_t* fring, uint64_t npages, PoolCtl* ctl) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < npages; i += (uint64_t)gridDim.x * blockDim.x)
+    fring[i] = (uint32_t)i;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    ctl->head = 0;
+    ctl->tail = ctl->limit = npages;
+    ctl->fail = 0;
+    ctl->param_err = 0;
+  }
+}
+
+hipError_t launch_pool_reset(uint32_t* fring, uint64_t npages, PoolCtl* ctl, hipStream_t s) {
+  hipLaunchKernelGGL(pool_reset_kernel, dim3(1024), dim3(256), 0, s, fring, npages, ctl);
+  return hipGetLastError();
+}
+
 // ================================================================== bootstrap (peer.go Launch + bootstrap)
+// A new replica (join = false): becomeFollower(1), then one ConfigChange entry per slot at term 1,
+// indices 1..R — AddNode(s) for each initial member s (descriptor 0 for the others), committed R,
+// and its remotes as addNode set them. A joining replica (rg_config.join_slots, StartOnDiskReplica
+// with join = true): becomeFollower(0) with an empty log and no membership; it learns the
+// membership from the log or a snapshot its leader sends once a ConfigChange adds it.
 __global__ void bootstrap_kernel(TickParams p, uint2* info) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= p.nrep) return;
   const uint32_t R = p.R, s = q / p.G, g = q - s * p.G;
   const uint64_t n = p.nrep;
+  const bool joining = (p.JS >> s) & 1u;
   uint64_t* a = p.s64_out + q;
   for (uint32_t f = 0; f < S64_ROWS; ++f) a[f * n] = 0;
   uint32_t* b = p.s32_out + q;
   for (uint32_t f = 0; f < S32_ROWS; ++f) b[f * n] = 0;
-  a[S_TERM * n] = 1;  // becomeFollower(1, NoLeader): one reset
-  a[S_LAST * n] = R;
-  a[S_COMMITTED * n] = R;
+  const uint32_t im = (p.IM ? p.IM : (1u << R) - 1u) & ~p.JS;  // initialMembers
+  const uint64_t last = joining ? 0 : R;
+  a[S_TERM * n] = joining ? 0 : 1;  // becomeFollower(term, NoLeader): one reset
+  a[S_LAST * n] = last;
+  a[S_COMMITTED * n] = last;
+  a[S_CC_HI * n] = last;
   b[S_RNG_CTR * n] = 1;
-  const uint32_t im = p.IM ? p.IM : (1u << R) - 1u;  // initialMembers
-  b[S_MEMBERS * n] = im;
-  b[S_SNAP_MEMBERS * n] = im;
+  b[S_MEMBERS * n] = joining ? 0u : im;
+  b[S_SNAP_MEMBERS * n] = joining ? 0u : im;
   const uint64_t key = (pl_group(p.pl, s, g) << 32) | ((uint64_t)s << 24) | 1ull;
   b[S_RAND_TO * n] = p.ET + (uint32_t)(mix64(p.seed ^ mix64(key)) % p.ET);
   for (uint32_t j = 0; j < R; ++j) {  // addNode → setRemote(id, 0, last+1)
     p.rem_out[(0 * R + j) * n + q] = 0;
-    p.rem_out[(1 * R + j) * n + q] = R + 1;
+    p.rem_out[(1 * R + j) * n + q] = last + 1;
     p.rem_out[(2 * R + j) * n + q] = 0;
     p.rst_out[j * n + q] = RETRY;
   }
-  for (uint32_t i = 1; i <= R; ++i) {
+  for (uint32_t i = 1; i <= last; ++i) {
     const uint64_t slot = i & (p.L - 1);
-    p.tr[slot * n + q] = 1ull | TYPE_BIT;  // ConfigChange, term 1, no payload, bank 0
-    info[(uint64_t)q * p.L + slot] = make_uint2(0u, (uint32_t)ENTRY_CONFIG << 24);
+    const uint32_t cc = ((im >> (i - 1)) & 1u) ? (CC_ADD << 4 | i) : 0u;  // AddNode(slot i - 1)
+    p.tr[slot * n + q] = 1ull | TYPE_BIT | cc_bits(cc);  // ConfigChange, term 1, no payload, bank 0
+    info[(uint64_t)q * p.L + slot] = make_uint2(0u, 0u);  // no Cmd bytes, at stream position 0
   }
   p.jcnt[q] = 0;
 }
@@ -447,7 +710,7 @@ __global__ void fill_slabs_kernel(uint8_t* slabs, uint2* slab_info, uint32_t sla
     const uint64_t key = mix64(((uint64_t)sl << 56) ^ (gg << 16) ^ (uint64_t)i ^ (seed * 0x9E3779B97F4A7C15ULL));
     const uint64_t at = (uint64_t)slab0 * rows * E * wpe + w;  // slabs [slab0, slab0 + nslab) only
     reinterpret_cast<uint64_t*>(slabs)[at] = mix64(key + (wi + 1) * 0xD1B54A32D192ED03ULL);
-    if (wi == 0) slab_info[at / wpe] = make_uint2(0u, P);  // a synthetic Cmd is P bytes
+    if (wi == 0) slab_info[at / wpe] = make_uint2(SYN_OFF, P);  // a generator Cmd: P bytes at its slab slot
   }
 }
 
@@ -460,34 +723,17 @@ hipError_t launch_fill_slabs(uint8_t* slabs, uint2* slab_info, uint32_t slab0, u
 }
 
 // ================================================================== caller proposals (rg_propose)
-// One wave per Cmd: lane c writes bytes [16c, 16c + 16) of the Cmd's P-byte slab slot from the caller's
-// packed bytes (unaligned, read byte by byte: an H2D-staged batch, not the tick path), zero past len.
-__global__ void __launch_bounds__(256) stage_cmds_kernel(uint8_t* slabs, uint2* slab_info, uint32_t P,
-                                                         const uint8_t* src, const uint64_t* off, const uint64_t* dst,
-                                                         const uint32_t* len, uint64_t n) {
-  const uint32_t lane = __lane_id(), nch = P / 16;
-  for (uint64_t i = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < n;
-       i += (uint64_t)gridDim.x * (blockDim.x >> 6)) {
-    const uint64_t d = dst[i], o = off[i];
-    const uint32_t ln = len[i];
-    for (uint32_t c = lane; c < nch; c += 64) {
-      uint32_t w[4] = {0, 0, 0, 0};
-      for (uint32_t b = 0; b < 16; ++b) {
-        const uint32_t k = 16 * c + b;
-        if (k < ln) w[b >> 2] |= (uint32_t)src[o + k] << (8 * (b & 3));
-      }
-      *reinterpret_cast<uint4*>(slabs + d * P + 16ull * c) = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-    if (lane == 0) slab_info[d] = make_uint2(0u, ln);
-  }
+// The Cmd bytes themselves reach their slab's arena with one H2D copy (the host lays them out
+// chunk-aligned and zero-padded in pinned staging); this scatters their slab_info descriptors.
+__global__ void stage_cmds_kernel(StageParams a) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * blockDim.x)
+    a.slab_info[a.info_at[i]] = make_uint2(a.chunk[i], a.len[i]);
 }
 
-hipError_t launch_stage_cmds(uint8_t* slabs, uint2* slab_info, uint32_t P, const uint8_t* src, const uint64_t* off,
-                             const uint64_t* dst, const uint32_t* len, uint64_t n, hipStream_t s) {
-  if (!n || !P) return hipSuccess;
-  const uint64_t blocks = std::min<uint64_t>((n + 3) / 4, 65536);
-  hipLaunchKernelGGL(stage_cmds_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, slabs, slab_info, P, src, off, dst,
-                     len, n);
+hipError_t launch_stage_cmds(const StageParams& a, hipStream_t s) {
+  if (!a.n) return hipSuccess;
+  const uint64_t blocks = std::min<uint64_t>((a.n + 255) / 256, 4096);
+  hipLaunchKernelGGL(stage_cmds_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
@@ -528,6 +774,34 @@ hipError_t launch_probe_copy(const void* src, void* dst, uint64_t bytes, hipStre
   const uint64_t n = bytes / 16;
   hipLaunchKernelGGL(probe_copy_kernel, dim3((uint32_t)((n + 2047) / 2048)), dim3(256), 0, s, (const uint4*)src,
                      (uint4*)dst, n);
+  return hipGetLastError();
+}
+
+// ================================================================== copy-back to host-mapped memory
+// rg_apply_async's PCIe leg: a few workgroups stream the gathered batch from device staging into
+// pinned host memory, four 16-B chunks in flight per lane (the tail, under 16 B, by single bytes)
+__global__ void __launch_bounds__(256) copy_to_host_kernel(const uint8_t* src, uint8_t* dst, uint64_t bytes) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const uint64_t n = bytes / 16, stride = (uint64_t)gridDim.x * 256 * 4;
+  for (uint64_t i = (uint64_t)blockIdx.x * 1024 + threadIdx.x; i < n; i += stride) {
+    u32x4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      v[k] = i + 256 * k < n ? *reinterpret_cast<const u32x4*>(src + (i + 256 * k) * 16) : u32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (i + 256 * k < n) __builtin_nontemporal_store(v[k], reinterpret_cast<u32x4*>(dst + (i + 256 * k) * 16));
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (bytes & 15)) dst[n * 16 + threadIdx.x] = src[n * 16 + threadIdx.x];
+}
+
+hipError_t launch_copy_to_host(const void* src, void* dst, uint64_t bytes, hipStream_t s) {
+  if (!bytes) return hipSuccess;
+  static const int blocks = [] {
+    const char* v = getenv("RAFTGPU_COPY_WG");  // measurement override
+    return v && atoi(v) > 0 ? atoi(v) : 32;
+  }();
+  hipLaunchKernelGGL(copy_to_host_kernel, dim3(blocks), dim3(256), 0, s, (const uint8_t*)src, (uint8_t*)dst, bytes);
   return hipGetLastError();
 }
 

@@ -12,10 +12,14 @@ struct WireParams {
   const uint64_t* hdr;
   const uint64_t* mt;
   const uint32_t* cnt;
-  const uint2* info;
-  const uint8_t* pay;
+  const uint2* info;       // [2 banks][nrep][L] {slot crc, stream position}
+  const uint8_t* pool;      // payload pages, through pt[nrep][PTS]
+  const uint32_t* pt;
+  uint32_t PTS, maxc;       // stream pages per replica, longest Cmd
   const uint8_t* slabs;     // proposal slabs [nslab][nrep][E][P]: a forwarded Propose ships its Cmds
-  const uint2* slab_info;   // [nslab][nrep][E] {0, len}
+  const uint2* slab_info;   // [nslab][nrep][E] {SYN_OFF or arena chunk, len}
+  const uint8_t* cmds;      // caller Cmd arenas [nslab][cmd_cap]
+  uint64_t cmd_cap;
   uint32_t nslab;
   const uint32_t* umap;  // [U] send units s<<28 | d<<24 | j, grouped by destination rank
   const uint32_t* ubeg;  // [N+1] first send unit of each destination

@@ -9,19 +9,21 @@
 // Units are listed per destination rank in (s, d, j) order (host-built, identical on the sender
 // and the receiver). A region for one rank is
 //     [u64 table: (data offset in 16-B units) << 8 | message count, one per unit, padded to 256 B]
-//     [data: per message a 64-B header, then n 16-B entry records {ring word, slot crc, 0}, then n
-//      payloads of P bytes — n = the entry count of a Replicate, or of a forwarded Propose when
-//      P > 0 (its Cmds: records {len bits, 0, 0}); 0 for every other type]
+//     [data: per message a 64-B header, then n 16-B entry records {ring word, slot crc, payload chunk
+//      offset}, then the n Cmds back to back, each rounded up to 16 B — n = the entry count of a
+//      Replicate, or of a forwarded Propose when P > 0 (its Cmds: records {len bits, 0, offset}); 0
+//      for every other type]
 // so a follower's (or a leader's, for a proposal) bulk job reads the payloads and sender CRCs
-// straight out of the receive buffer. A payload is the Cmd zero-padded to P bytes; the ring word
-// carries its length (raftgpu_internal.h).
+// straight out of the receive buffer. Only Cmd bytes cross xGMI (the ring word carries the length,
+// raftgpu_internal.h).
 //
-// plan_kernel      thread per unit: bytes of its messages
+// plan_kernel      thread per unit: 16-B units of its messages
 // scan_*           exclusive scan of the unit sizes (three passes)
-// pack_kernel      wave per unit: headers, records (term word + the sender's stored CRC), payload
-//                  copied out of the sender's ring bank named by the term word
+// pack_kernel      wave per unit: headers, records (term word + the sender's stored CRC), the Cmds
+//                  copied out of the sender's payload stream (or slab / Cmd arena for a Propose)
 // unpack_kernel    thread per received unit: dense remote-inbox planes (rhdr/rmt/rcnt, the layout
-//                  control_kernel reads), header word 7 of a Replicate = its records' byte offset
+//                  control_kernel reads), header word 7 of a Replicate = its records' byte offset;
+//                  records are checked (lengths, offsets, sizes) before anything is kept
 #include "raftgpu_wire.h"
 
 namespace rg {
@@ -40,9 +42,18 @@ __device__ __forceinline__ uint32_t wire_entries(uint64_t w0, uint32_t P) {
   return (t == M_REPLICATE || (t == M_PROPOSE && P)) ? (uint32_t)(w0 >> 32) : 0u;
 }
 
-// 16-B units of one message: header 4, each entry 1 record + P/16 payload
-__device__ __forceinline__ uint32_t msg_units(uint64_t w0, uint32_t P) {
-  return 4u + wire_entries(w0, P) * (1u + P / 16u);
+// payload chunks of entry e of outbox message k of column (col, j) (the sender's view)
+__device__ __forceinline__ uint32_t msg_entry_nc(const WireParams& w, uint64_t col, uint32_t j, uint32_t k, uint64_t w0,
+                                                 uint64_t w7, uint32_t e) {
+  if ((w0 & 0xFF) == M_PROPOSE) {  // a forwarded batch: its Cmds in this replica's row of slab w7
+    const uint32_t sl = (uint32_t)w7;
+    if (sl >= w.nslab) return 0u;
+    const uint64_t qs = (col / w.R) * w.G + j;
+    return (min(w.slab_info[((uint64_t)sl * w.nrep + qs) * w.E + e].y, w.maxc) + 15u) >> 4;
+  }
+  const uint64_t* mtp = w.mt + ((col * w.K + k) * w.E) * w.G + j;
+  const bool uni = ((uint32_t)w7 & RG_UNIFORM) != 0;
+  return word_nc(mtp[uni ? 0 : (uint64_t)e * w.G]);
 }
 
 __global__ void plan_kernel(WireParams w) {
@@ -51,9 +62,19 @@ __global__ void plan_kernel(WireParams w) {
   uint32_t s, d, j;
   unit_decode(w.umap[u], s, d, j);
   const uint64_t col = (uint64_t)s * w.R + d;
-  const uint32_t c = w.cnt[col * w.G + j];
+  const uint64_t plane = (uint64_t)w.R * w.R * w.K * w.G;
+  const uint32_t c = min(w.cnt[col * w.G + j], w.K);
   uint32_t sz = 0;
-  for (uint32_t k = 0; k < c; ++k) sz += msg_units(w.hdr[(col * w.K + k) * w.G + j], w.P);
+  for (uint32_t k = 0; k < c; ++k) {  // 16-B units: header 4, a record per entry, the Cmd chunks
+    const uint64_t* h = w.hdr + (col * w.K + k) * w.G + j;
+    const uint64_t w0 = h[0];
+    const uint32_t n = min(wire_entries(w0, w.P), w.E);
+    sz += 4u + n;
+    if (n && w.P) {
+      const uint64_t w7 = h[7 * plane];
+      for (uint32_t e = 0; e < n; ++e) sz += msg_entry_nc(w, col, j, k, w0, w7, e);
+    }
+  }
   w.usize[u] = sz;
 }
 
@@ -151,6 +172,15 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+__device__ __forceinline__ uint32_t lane_incl_scan32(uint32_t v) {
+  const uint32_t lane = wl_lane();
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)v, o, 64);
+    if (lane >= o) v += y;
+  }
+  return v;
+}
+
 __global__ void __launch_bounds__(256) pack_kernel(WireParams w) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const uint32_t lane = wl_lane();
@@ -171,7 +201,7 @@ __global__ void __launch_bounds__(256) pack_kernel(WireParams w) {
   }
   if (lane == 0) reinterpret_cast<uint64_t*>(region)[u - u0] = (off16 << 8) | c;
   uint8_t* out = region + table_bytes(nu) + off16 * 16;
-  const uint32_t P = w.P, nch = P / 16;
+  const uint32_t P = w.P;
   for (uint32_t k = 0; k < c; ++k) {
     const uint64_t* hp = w.hdr + (col * w.K + k) * w.G + j;
     const uint64_t hv = lane < 8 ? hp[lane * plane] : 0;
@@ -190,39 +220,56 @@ __global__ void __launch_bounds__(256) pack_kernel(WireParams w) {
     const bool slab_ok = prop && sl < w.nslab;
     const uint64_t se0 = ((uint64_t)sl * n64 + qs) * w.E;
     const uint64_t* mtp = w.mt + ((col * w.K + k) * w.E) * w.G + j;
+    // lane e: entry e's record and where its Cmd is (sender stream position / slab / arena chunk)
+    uint64_t word = 0;
+    uint32_t crc = 0, nc = 0, sp = 0;
+    bool syn = false;
     if (lane < n) {
-      u32x4 rec = u32x4{0u, 0u, 0u, 0u};
       if (prop) {
-        const uint64_t word = len_bits(slab_ok ? min(w.slab_info[se0 + lane].y, P) : 0u);
-        rec = u32x4{(uint32_t)word, (uint32_t)(word >> 32), 0u, 0u};
+        const uint2 inf = slab_ok ? w.slab_info[se0 + lane] : make_uint2(0u, 0u);
+        word = len_bits(min(inf.y, w.maxc));
+        syn = (inf.x & SYN_OFF) != 0;
+        sp = inf.x & ~SYN_OFF;
       } else {
-        const uint64_t word = mtp[(uint64_t)lane * est];
+        word = mtp[(uint64_t)lane * est];
         const uint64_t slot = (li + 1 + lane) & (w.L - 1);
-        const uint32_t crc = (word & PAY_BIT) ? w.info[((word >> 63) * n64 + qs) * w.L + slot].x : 0u;
-        rec = u32x4{(uint32_t)word, (uint32_t)(word >> 32), crc, 0u};
+        const uint2 inf = w.info[((word >> 63) * n64 + qs) * w.L + slot];
+        crc = (word & PAY_BIT) ? inf.x : 0u;
+        sp = inf.y;
       }
-      *reinterpret_cast<u32x4*>(out + 64 + 16 * lane) = rec;
+      nc = P ? word_nc(word) : 0u;
     }
-    if (P) {
-      uint8_t* po = out + 64 + 16ull * n;
-#pragma unroll 4
-      for (uint32_t t = lane; t < n * nch; t += 64) {
-        const uint32_t e = t / nch, ch = t - e * nch;
-        const uint8_t* src = nullptr;
-        if (prop) {
-          if (slab_ok && w.slab_info[se0 + e].y) src = w.slabs + (se0 + e) * P;
-        } else {
-          const uint64_t word = mtp[(uint64_t)e * est];
-          if (word & PAY_BIT) src = w.pay + (((word >> 63) * n64 + qs) * w.L + ((li + 1 + e) & (w.L - 1))) * P;
-        }
-        if (src) {
-          const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + 16ull * ch));
-          __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(po + 16ull * t));
-        }
+    const uint32_t inc = lane_incl_scan32(nc), total = __builtin_amdgcn_readlane(inc, 63);
+    if (lane < n)
+      *reinterpret_cast<u32x4*>(out + 64 + 16 * lane) = u32x4{(uint32_t)word, (uint32_t)(word >> 32), crc, inc - nc};
+    uint8_t* po = out + 64 + 16ull * n;
+    for (uint32_t t = lane; t < ((total + 63) & ~63u); t += 64) {
+      uint32_t lo = 0;  // the entry of chunk t: first lane with inc > t
+#pragma unroll
+      for (uint32_t step = 32; step; step >>= 1) {
+        const uint32_t v = (uint32_t)__shfl((int)inc, (int)(lo + step - 1), 64);
+        if (v <= t) lo += step;
+      }
+      const uint32_t le = lo < 64 ? lo : 63;
+      const uint32_t ex = lo ? (uint32_t)__shfl((int)inc, (int)(lo - 1), 64) : 0u;
+      const uint32_t spl = (uint32_t)__shfl((int)sp, (int)le, 64);
+      const bool synl = __shfl((int)syn, (int)le, 64) != 0;
+      if (t < total) {
+        const uint32_t ch = t - ex;
+        const uint8_t* src = !prop ? w.pool + stream_byte(w.pt, w.PTS, (uint32_t)qs, spl + ch)
+                             : synl ? w.slabs + (se0 + le) * P + 16ull * ch
+                                    : w.cmds + (uint64_t)sl * w.cmd_cap + 16ull * (spl + ch);
+        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src));
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(po + 16ull * t));
       }
     }
-    out += 64 + (uint64_t)n * (16 + P);
+    out += 64 + 16ull * (n + total);
   }
+}
+
+__device__ __forceinline__ bool cc_valid(uint32_t cc, uint32_t R) {  // a ConfigChange descriptor (or none)
+  const uint32_t op = cc >> 4, sl = cc & 0xF;
+  return cc == 0 || ((op == CC_ADD || op == CC_REMOVE) && sl >= 1 && sl <= R && cc <= 0x2Fu);
 }
 
 __global__ void unpack_kernel(WireParams w) {
@@ -256,35 +303,43 @@ __global__ void unpack_kernel(WireParams w) {
     const uint32_t type = (uint32_t)(w0 & 0xFF), n = wire_entries(w0, w.P);
     // exchange data comes from another process: keep a message only if this plane can carry it —
     // a known type, from the unit's sender slot s to its destination slot d, at most E entries (a
-    // Propose 1..E), inside the region; the unit's messages from the first bad one on are dropped
+    // Propose 1..E with a valid ConfigChange descriptor or none), inside the region; the unit's
+    // messages from the first bad one on are dropped
     const bool known = type == M_NOOP || type == M_PROPOSE || type == M_REPLICATE || type == M_REPLICATE_RESP ||
                        type == M_REQUEST_VOTE || type == M_REQUEST_VOTE_RESP || type == M_INSTALL_SNAPSHOT ||
                        type == M_HEARTBEAT || type == M_HEARTBEAT_RESP || type == M_READ_INDEX ||
                        type == M_READ_INDEX_RESP;
     const uint32_t from = (uint32_t)(w0 >> 8) & 0xFF, to = (uint32_t)(w0 >> 16) & 0xFF, nent = (uint32_t)(w0 >> 32);
-    if (!known || from != s + 1 || to != d + 1 || n > w.E || (type == M_PROPOSE && (nent < 1 || nent > w.E)) ||
-        (uint64_t)(in - w.recv) + 64 + (uint64_t)n * (16 + w.P) > rend) {
+    if (!known || from != s + 1 || to != d + 1 || n > w.E ||
+        (type == M_PROPOSE && (nent < 1 || nent > w.E || !cc_valid((uint32_t)h[6], w.R))) ||
+        (uint64_t)(in - w.recv) + 64 + (uint64_t)n * 16 > rend) {
       RG_OOB("RG_BOUNDS unpack u=%u k=%u type=%u from=%u to=%u n=%u region end %llu\n", u, k, type, from, to, n,
              (unsigned long long)rend);
       break;
     }
-    bool sane = true;  // every entry word: an application entry's length <= P with the payload bit
-    for (uint32_t e = 0; e < n; ++e) {  // exactly when non-zero; a ConfigChange: no payload, a descriptor
+    // every entry record: an application entry's length <= max_cmd_bytes with the payload bit exactly
+    // when non-zero, a ConfigChange no payload and a descriptor; Cmd offsets back to back from 0
+    bool sane = true;
+    uint32_t tot = 0;
+    for (uint32_t e = 0; e < n; ++e) {
       const uint64_t rw = h[8 + 2 * e];
-      const uint32_t ln = word_len(rw);
+      const uint32_t ln = word_len(rw), ofs = (uint32_t)(h[9 + 2 * e] >> 32);
       sane = sane && ((rw & TYPE_BIT) ? !(rw & PAY_BIT) && ln <= 0x2Fu
-                                      : ln <= w.P && ((rw & PAY_BIT) != 0) == (ln != 0));
+                                      : ln <= w.maxc && ((rw & PAY_BIT) != 0) == (ln != 0)) &&
+             ofs == tot;
+      tot += word_nc(rw);
     }
-    if (!sane) {
-      RG_OOB("RG_BOUNDS unpack u=%u k=%u: entry word with a bad length\n", u, k);
+    if (!sane || (uint64_t)(in - w.recv) + 64 + 16ull * (n + tot) > rend) {
+      RG_OOB("RG_BOUNDS unpack u=%u k=%u: a bad entry record or Cmds beyond the region\n", u, k);
       break;
     }
     uint64_t* ho = w.rhdr + (col * w.K + k) * w.G + j;
     for (int x = 0; x < 7; ++x) ho[x * plane] = h[x];
+    if (type == M_PROPOSE) ho[4 * plane] = tot;  // its Cmds' stream chunks (the capacity rule's input)
     ho[7 * plane] = n ? (uint64_t)(in + 64 - w.recv) : h[7];  // entries: word 7 = their records' offset
     uint64_t* mo = w.rmt + ((col * w.K + k) * w.E) * w.G + j;  // inline ring words (a Propose: length bits)
     for (uint32_t e = 0; e < n; ++e) mo[(uint64_t)e * w.G] = h[8 + 2 * e] & (type == M_PROPOSE ? ~TERM_MASK & ~BANK_BIT & ~TYPE_BIT : ~0ull);
-    in += 64 + (uint64_t)n * (16 + w.P);
+    in += 64 + 16ull * (n + tot);
   }
   w.rcnt[col * w.G + j] = k;
 }

@@ -34,7 +34,8 @@ class Config(C.Structure):
         ("drop_ppm", C.c_uint32), ("device", C.c_int32), ("seed", C.c_uint64),
         ("ranks", C.c_uint32), ("rank", C.c_uint32), ("wire_all", C.c_uint32), ("column_base", C.c_uint32),
         ("crc32c", C.c_uint32), ("apply_feedback", C.c_uint32), ("initial_members", C.c_uint32),
-        ("_cpad", C.c_uint32),
+        ("max_cmd_bytes", C.c_uint32), ("stream_pages", C.c_uint32), ("pool_pages", C.c_uint32),
+        ("join_slots", C.c_uint32), ("_cpad", C.c_uint32),
     ]
 
 
@@ -74,11 +75,11 @@ class Traffic(C.Structure):
 
 class ApplyEntry(C.Structure):
     _fields_ = [("index", C.c_uint64), ("group", C.c_uint64), ("replica_id", C.c_uint32), ("len", C.c_uint32),
-                ("crc", C.c_uint32), ("rid", C.c_uint32)]
+                ("crc", C.c_uint32), ("rid", C.c_uint32), ("off", C.c_uint64)]
 
 
 APPLY_DTYPE = np.dtype([("index", "<u8"), ("group", "<u8"), ("replica_id", "<u4"), ("len", "<u4"),
-                        ("crc", "<u4"), ("rid", "<u4")])
+                        ("crc", "<u4"), ("rid", "<u4"), ("off", "<u8")])
 
 
 PERSIST_STATE_DTYPE = np.dtype([("group", "<u8"), ("replica_id", "<u4"), ("rid", "<u4"), ("term", "<u8"),
@@ -86,7 +87,17 @@ PERSIST_STATE_DTYPE = np.dtype([("group", "<u8"), ("replica_id", "<u4"), ("rid",
                                 ("marker_term", "<u8"), ("snap_index", "<u8"), ("snap_term", "<u8"),
                                 ("first", "<u8"), ("entry_off", "<u8"), ("members", "<u4"), ("snap_members", "<u4")])
 PERSIST_ENTRY_DTYPE = np.dtype([("index", "<u8"), ("term", "<u8"), ("type", "<u4"), ("len", "<u4"), ("crc", "<u4"),
-                                ("rid", "<u4")])
+                                ("rid", "<u4"), ("off", "<u8")])
+
+
+def unpack_rows(recs, packed: np.ndarray, row: int) -> np.ndarray:
+    """Packed Cmds (each at recs["off"], recs["len"] bytes) as one zero-padded row of `row` bytes per
+    record: the Python view of rg_apply_committed / rg_persist_collect payloads."""
+    out = np.zeros((len(recs), max(row, 1)), np.uint8)
+    for k, (o, n) in enumerate(zip(recs["off"].tolist(), recs["len"].tolist())):
+        if n and row:
+            out[k, :n] = packed[o:o + n]
+    return out[:, :row]
 
 SNAP_TAKEN, SNAP_RESTORED = 1, 2  # RG_SNAP_*
 SNAPSHOT_EVENT_DTYPE = np.dtype([("group", "<u8"), ("replica_id", "<u4"), ("rid", "<u4"), ("kind", "<u4"),
@@ -155,7 +166,8 @@ EXPORTS = ["rg_create", "rg_destroy", "rg_bootstrap", "rg_fill_slabs", "rg_tick"
            "rg_timing", "rg_kernel_ms", "rg_wire_plan", "rg_wire_pack", "rg_wire_recv", "rg_global_id",
            "rg_apply_committed", "rg_probe_copy", "rg_persist_collect", "rg_snapshot_events", "rg_propose",
            "rg_notify_applied", "rg_apply_async", "rg_apply_wait", "rg_read_index", "rg_read_index_results",
-           "rg_config_change", "rg_wire_exchange", "rg_rccl_unique_id", "rg_rccl_open", "rg_rccl_close"]
+           "rg_config_change", "rg_wire_exchange", "rg_rccl_unique_id", "rg_rccl_open", "rg_rccl_close",
+           "rg_pool_stats"]
 
 _lib = None
 
@@ -217,10 +229,12 @@ def load_library(path: str = LIB_PATH):
         "rg_rccl_open": ([C.c_char_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(Transport)], i32),
         "rg_rccl_close": ([C.POINTER(Transport)], i32),
         "rg_global_id": ([vp, u32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)], i32),
-        "rg_apply_committed": ([vp, u32, vp, vp, u64, C.POINTER(C.c_uint64)], i32),
+        "rg_apply_committed": ([vp, u32, vp, vp, u64, C.POINTER(C.c_uint64), u64, C.POINTER(C.c_uint64)], i32),
+        "rg_pool_stats": ([vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_int)], i32),
         "rg_probe_copy": ([C.c_int32, u64, C.c_int32, C.POINTER(C.c_double)], i32),
         "rg_snapshot_events": ([vp, u32, vp, u64, C.POINTER(C.c_uint64)], i32),
-        "rg_persist_collect": ([vp, i32, vp, u64, C.POINTER(C.c_uint64), vp, vp, u64, C.POINTER(C.c_uint64)], i32),
+        "rg_persist_collect": ([vp, i32, vp, u64, C.POINTER(C.c_uint64), vp, vp, u64, C.POINTER(C.c_uint64), u64,
+                                C.POINTER(C.c_uint64)], i32),
     }
     for name, (args, res) in sig.items():
         if os.environ.get("RAFTGPU_LIB") and not hasattr(L, name):
@@ -238,7 +252,7 @@ def default_config(**kw) -> dict:
              max_msgs_per_pair=8, num_slabs=2, election_rtt=10, heartbeat_rtt=1, check_quorum=1,
              snapshot_entries=1000, compaction_overhead=5, drop_ppm=0, device=0, seed=0x5EED,
              ranks=1, rank=0, wire_all=0, column_base=0, crc32c=0, apply_feedback=0,
-             initial_members=0)
+             initial_members=0, max_cmd_bytes=0, stream_pages=0, pool_pages=0, join_slots=0)
     c.update(kw)
     return c
 
@@ -259,6 +273,7 @@ class Engine:
         self.G, self.R = self.cfg["groups"], self.cfg["replicas"]
         self.nrep = self.G * self.R
         self.ranks = max(1, self.cfg["ranks"])
+        self.row = self.cfg["max_cmd_bytes"] or self.cfg["payload_bytes"]  # longest Cmd: payload row stride
         self._slabs_filled = False
 
     def _check(self, rc):
@@ -384,7 +399,7 @@ class Engine:
             return []
         buf = (EntryView * n)()
         pay = None
-        P = self.cfg["payload_bytes"]
+        P = self.row
         if with_payload and P:
             pay = (C.c_uint8 * (n * P))()
         self._check(self.L.rg_read_entries(self.h, rid, first, n, buf, pay))
@@ -499,22 +514,25 @@ class Engine:
         self._check(self.L.rg_wire_exchange(self.h, C.byref(transport), C.byref(sent)))
         return sent.value
 
-    def apply_committed(self, slot_mask: int = 0xFF, cap: int = None):
+    def apply_committed_packed(self, slot_mask: int = 0xFF):
+        """rg_apply_committed as the C-ABI returns it: (APPLY_DTYPE records, packed Cmd bytes, each at
+        its record's off)."""
+        n, pb = C.c_uint64(), C.c_uint64()
+        rc = self.L.rg_apply_committed(self.h, slot_mask, None, None, 0, C.byref(n), 0, C.byref(pb))
+        if rc < 0 and rc != RG_EFULL:
+            self._check(rc)
+        recs = np.zeros(max(n.value, 1), APPLY_DTYPE)
+        pay = np.zeros(max(pb.value, 16), np.uint8)
+        self._check(self.L.rg_apply_committed(self.h, slot_mask, recs.ctypes.data, pay.ctypes.data, n.value,
+                                              C.byref(n), pay.size, C.byref(pb)))
+        return recs[:n.value], pay[:pb.value]
+
+    def apply_committed(self, slot_mask: int = 0xFF):
         """Committed-entry copy-back of the last tick (rg_apply_committed): a structured array
-        (APPLY_DTYPE: index, group, replica_id, len, crc, rid) and the payloads, one row of
-        payload_bytes per entry, as numpy arrays."""
-        P = self.cfg["payload_bytes"]
-        n = C.c_uint64()
-        if cap is None:  # size with a count-only call
-            rc = self.L.rg_apply_committed(self.h, slot_mask, None, None, 0, C.byref(n))
-            if rc < 0 and rc != RG_EFULL:
-                self._check(rc)
-            cap = n.value
-        recs = np.zeros(max(cap, 1), APPLY_DTYPE)
-        pay = np.zeros((max(cap, 1), max(P, 1)), np.uint8)
-        self._check(self.L.rg_apply_committed(self.h, slot_mask, recs.ctypes.data, pay.ctypes.data, cap, C.byref(n)))
-        k = n.value
-        return recs[:k], pay[:k, :P]
+        (APPLY_DTYPE: index, group, replica_id, len, crc, rid, off) and the Cmds, one zero-padded row of
+        max_cmd_bytes per entry, as numpy arrays."""
+        recs, packed = self.apply_committed_packed(slot_mask)
+        return recs, unpack_rows(recs, packed, self.row)
 
     def apply_async(self, slot_mask: int = 0xFF, buf: int = 0):
         """rg_apply_async: gather the last tick's applied entries and start their D2H copy into
@@ -526,28 +544,40 @@ class Engine:
         then views into engine-owned pinned memory, valid until the next apply_async into `buf`)."""
         ents, pay, n = C.c_void_p(), C.c_void_p(), C.c_uint64()
         self._check(self.L.rg_apply_wait(self.h, buf, C.byref(ents), C.byref(pay), C.byref(n)))
-        k, P = n.value, self.cfg["payload_bytes"]
+        k, P = n.value, self.row
         if k == 0:
             return np.zeros(0, APPLY_DTYPE), np.zeros((0, P), np.uint8)
         recs = np.ctypeslib.as_array(C.cast(ents, C.POINTER(C.c_uint8)), (k * APPLY_DTYPE.itemsize,)).view(APPLY_DTYPE)
-        pays = (np.ctypeslib.as_array(C.cast(pay, C.POINTER(C.c_uint8)), (k * P,)).reshape(k, P) if P
-                else np.zeros((k, 0), np.uint8))
-        return (recs.copy(), pays.copy()) if copy else (recs, pays)
+        last = recs[-1]
+        nbytes = int(last["off"]) + (int(last["len"]) + 15) // 16 * 16
+        packed = (np.ctypeslib.as_array(C.cast(pay, C.POINTER(C.c_uint8)), (max(nbytes, 1),))[:nbytes] if P
+                  else np.zeros(0, np.uint8))
+        if not copy:  # views into engine-owned pinned memory: the records and the packed Cmds
+            return recs, packed
+        return recs.copy(), unpack_rows(recs, packed, P)
 
     def persist_collect(self, full: bool = False):
         """Host WAL feed of the last tick (rg_persist_collect): (states, entries, payload) numpy
-        arrays — PERSIST_STATE_DTYPE rows, PERSIST_ENTRY_DTYPE rows, payload_bytes per entry."""
-        P = self.cfg["payload_bytes"]
-        ns, ne = C.c_uint64(), C.c_uint64()
-        rc = self.L.rg_persist_collect(self.h, 1 if full else 0, None, 0, C.byref(ns), None, None, 0, C.byref(ne))
+        arrays — PERSIST_STATE_DTYPE rows, PERSIST_ENTRY_DTYPE rows, one max_cmd_bytes row per entry."""
+        ns, ne, pb = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        rc = self.L.rg_persist_collect(self.h, 1 if full else 0, None, 0, C.byref(ns), None, None, 0, C.byref(ne),
+                                       0, C.byref(pb))
         if rc < 0 and rc != RG_EFULL:
             self._check(rc)
         st = np.zeros(max(ns.value, 1), PERSIST_STATE_DTYPE)
         en = np.zeros(max(ne.value, 1), PERSIST_ENTRY_DTYPE)
-        pay = np.zeros((max(ne.value, 1), max(P, 1)), np.uint8)
+        packed = np.zeros(max(pb.value, 16), np.uint8)
         self._check(self.L.rg_persist_collect(self.h, 1 if full else 0, st.ctypes.data, ns.value, C.byref(ns),
-                                              en.ctypes.data, pay.ctypes.data, ne.value, C.byref(ne)))
-        return st[:ns.value], en[:ne.value], pay[:ne.value, :P]
+                                              en.ctypes.data, packed.ctypes.data, ne.value, C.byref(ne),
+                                              packed.size, C.byref(pb)))
+        en = en[:ne.value]
+        return st[:ns.value], en, unpack_rows(en, packed[:pb.value], self.row)
+
+    def pool_stats(self) -> dict:
+        """rg_pool_stats: {'total': pages, 'free': pages, 'failed': bool} of the payload page pool."""
+        tot, free, failed = C.c_uint64(), C.c_uint64(), C.c_int()
+        self._check(self.L.rg_pool_stats(self.h, C.byref(tot), C.byref(free), C.byref(failed)))
+        return {"total": tot.value, "free": free.value, "failed": bool(failed.value)}
 
     def snapshot_events(self, slot_mask: int = 0xFF):
         """Snapshot events of the last tick (rg_snapshot_events): SNAPSHOT_EVENT_DTYPE rows, one

@@ -8,10 +8,11 @@ snapshot's index and term) durable in its LogDB with fsync before the step's mes
 (one ``hipMemcpyAsync`` per array), ``WAL.append`` writes it as one framed, CRC-checked record and
 fsyncs, and the engine may then run the next tick (which delivers the last tick's messages).
 
-Record: ``b"RGWL"``, u32 version, u64 tick, u64 #states, u64 #entries, u32 payload_bytes,
-u32 crc32(body), u64 len(body); body = the state rows, the entry rows, the payloads
-(``PERSIST_STATE_DTYPE`` / ``PERSIST_ENTRY_DTYPE`` little-endian). A torn tail record (crash
-mid-write) is ignored on replay.
+Record: ``b"RGWL"``, u32 version, u64 tick, u64 #states, u64 #entries, u32 row bytes (the longest
+Cmd), u32 crc32(body), u64 len(body); body = the state rows, the entry rows, the Cmds, one zero-padded
+row per entry (``PERSIST_STATE_DTYPE`` / ``PERSIST_ENTRY_DTYPE`` little-endian). A torn tail record
+(crash mid-write: short, or failing its CRC) is ignored on replay; a complete record of another
+format version is an error, never silently dropped.
 
 Replay applies records in order per replica: keep the entries below ``first``, replace
 ``first..last`` with the record's entries, drop those above ``last`` and at or below ``marker``.
@@ -32,7 +33,7 @@ import numpy as np
 from .engine import PERSIST_ENTRY_DTYPE, PERSIST_STATE_DTYPE
 
 MAGIC = b"RGWL"
-VERSION = 2  # 2: state records carry the membership (members, snap_members)
+VERSION = 3  # 2: state records carry the membership (members, snap_members); 3: entry rows carry `off`
 HDR = struct.Struct("<4sIQQQIIQ")
 
 
@@ -62,8 +63,11 @@ def records(path: str):
     pos = 0
     while pos + HDR.size <= len(data):
         magic, ver, tick, ns, ne, P, crc, blen = HDR.unpack_from(data, pos)
-        if magic != MAGIC or ver != VERSION or pos + HDR.size + blen > len(data):
+        if magic != MAGIC or pos + HDR.size + blen > len(data):
             break  # torn tail
+        if ver != VERSION:
+            raise ValueError(f"WAL {path}: a record of format version {ver} at byte {pos}; this build reads "
+                             f"version {VERSION} (replay it with the build that wrote it)")
         body = data[pos + HDR.size:pos + HDR.size + blen]
         if zlib.crc32(body) != crc:
             break
@@ -143,7 +147,7 @@ def restore(engine, wal_logs: dict, cfg: dict, global_rids, app_applied=None):
     import_replica(rid, view, terms, types, payloads, lens)) from replayed WAL logs. global_rids maps
     the engine's replica ids to global ones (identity for one rank). app_applied(global rid) -> the
     index the replica's state machine has applied (its /LastLogIndex), or None for the commit."""
-    R, P = cfg["replicas"], cfg["payload_bytes"]
+    R, P = cfg["replicas"], cfg.get("max_cmd_bytes", 0) or cfg["payload_bytes"]  # the import row stride
     for rid, gr in global_rids:
         rl = wal_logs[gr]
         v = restart_view(rl, gr // R, gr % R, cfg, None if app_applied is None else app_applied(gr))

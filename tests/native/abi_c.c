@@ -35,6 +35,7 @@
 #define R 3
 #define TICKS 40
 #define PER_TICK 4 /* Cmds per shard per tick */
+#define MAXC 1500  /* longest Cmd: six 256-B lane groups, up to two pages */
 
 #define CHECK(x)                                                                              \
   do {                                                                                        \
@@ -52,10 +53,12 @@
     }                                                                  \
   } while (0)
 
-/* deterministic Cmd k of shard g at tick t: "put g/t/k" + filler, 1..200 bytes */
+/* deterministic Cmd k of shard g at tick t: "put g/t/k" + filler, 1..MAXC bytes (longer than
+ * payload_bytes, so Cmds span lane groups and pages) */
 static uint32_t make_cmd(uint32_t g, uint32_t t, uint32_t k, uint8_t* out) {
   uint32_t n = (uint32_t)snprintf((char*)out, 256, "put shard=%u tick=%u k=%u;", g, t, k);
-  uint32_t len = 1 + (g * 131 + t * 31 + k * 7) % 200;
+  uint32_t len = 1 + (g * 131 + t * 31 + k * 7) % MAXC;
+  if (len < n) len = n;
   for (uint32_t i = n; i < len; ++i) out[i] = (uint8_t)('a' + (g + t + k + i) % 26);
   return len;
 }
@@ -81,6 +84,7 @@ int main(int argc, char** argv) {
   rg_config c;
   memset(&c, 0, sizeof c);
   c.groups = G; c.replicas = R; c.log_capacity = 1024; c.payload_bytes = 256;
+  c.max_cmd_bytes = MAXC;
   c.max_entries_per_msg = 16; c.max_msgs_per_pair = 8; c.num_slabs = 2;
   c.election_rtt = 10; c.heartbeat_rtt = 1; c.check_quorum = 1; /* raftd's config (raft_manager.go:92-100) */
   c.snapshot_entries = 1000; c.compaction_overhead = 5; c.seed = 0x5EED; c.ranks = 1;
@@ -121,10 +125,11 @@ int main(int argc, char** argv) {
   /* C-owned buffers for the copy-back and the WAL feed */
   const uint64_t cap = 1u << 16;
   rg_apply_entry* ents = (rg_apply_entry*)malloc(cap * sizeof *ents);
-  uint8_t* pay = (uint8_t*)malloc(cap * c.payload_bytes);
+  const uint64_t pay_cap = cap * 64;
+  uint8_t* pay = (uint8_t*)malloc(pay_cap);
   rg_persist_state* ps = (rg_persist_state*)malloc(cap * sizeof *ps);
   rg_persist_entry* pe = (rg_persist_entry*)malloc(cap * sizeof *pe);
-  uint8_t* ppay = (uint8_t*)malloc(cap * c.payload_bytes);
+  uint8_t* ppay = (uint8_t*)malloc(pay_cap);
   /* what each replica's state machine received, as a running CRC over (index, Cmd) */
   uint64_t got[G * R];
   uint32_t got_crc[G * R];
@@ -133,7 +138,7 @@ int main(int argc, char** argv) {
   memset(got_crc, 0, sizeof got_crc);
   memset(last_idx, 0, sizeof last_idx);
 
-  uint8_t* blob = (uint8_t*)malloc(G * PER_TICK * 256);
+  uint8_t* blob = (uint8_t*)malloc(G * PER_TICK * MAXC);
   uint32_t lens[G * PER_TICK];
   rg_proposal props[G];
   uint32_t want_crc[G];
@@ -172,12 +177,14 @@ int main(int argc, char** argv) {
         off += n;
       }
     CHECK(tick(e, &in));
-    uint64_t ns = 0, ne = 0, na = 0;
-    CHECK(rg_persist_collect(e, 0, ps, cap, &ns, pe, ppay, cap, &ne)); /* the shim fsyncs these */
-    CHECK(rg_apply_committed(e, 0xFF, ents, pay, cap, &na));
+    uint64_t ns = 0, ne = 0, na = 0, pb = 0;
+    CHECK(rg_persist_collect(e, 0, ps, cap, &ns, pe, ppay, cap, &ne, pay_cap, &pb)); /* the shim fsyncs these */
+    for (uint64_t i = 0; i < ne; ++i) EXPECT(pe[i].off + pe[i].len <= pb);
+    CHECK(rg_apply_committed(e, 0xFF, ents, pay, cap, &na, pay_cap, &pb));
     for (uint64_t i = 0; i < na; ++i) {
       const rg_apply_entry* a = &ents[i];
-      const uint8_t* cmd = pay + i * c.payload_bytes;
+      const uint8_t* cmd = pay + a->off;
+      EXPECT(a->off + a->len <= pb);
       EXPECT(a->crc == (uint32_t)crc32(0, cmd, a->len));
       EXPECT(a->index > last_idx[a->rid]);
       last_idx[a->rid] = a->index;
@@ -191,11 +198,11 @@ int main(int argc, char** argv) {
     CHECK(rg_notify_applied(e, rids, idx, G * R));
   }
   for (int t = 0; t < 16; ++t) { /* drain: the last Cmds commit everywhere, the re-added follower catches up */
-    uint64_t na = 0;
+    uint64_t na = 0, pb = 0;
     CHECK(tick(e, &in));
-    CHECK(rg_apply_committed(e, 0xFF, ents, pay, cap, &na));
+    CHECK(rg_apply_committed(e, 0xFF, ents, pay, cap, &na, pay_cap, &pb));
     for (uint64_t i = 0; i < na; ++i) {
-      got_crc[ents[i].rid] = (uint32_t)crc32(got_crc[ents[i].rid], pay + i * c.payload_bytes, ents[i].len);
+      got_crc[ents[i].rid] = (uint32_t)crc32(got_crc[ents[i].rid], pay + ents[i].off, ents[i].len);
       got[ents[i].rid]++;
     }
     rg_replica_view v[G * R];

@@ -1,7 +1,9 @@
 // ctl_host.cpp — TEST HARNESS: runs the engine's control step (raftgpu_control.h, the body of
 // control_kernel<R>) on the CPU over host copies of the device's structure-of-arrays layout, so
 // the exact GPU control code can be checked against the oracle and run under AddressSanitizer
-// without a GPU. The bulk (payload/CRC) kernel is not emulated: entries carry terms/types only.
+// without a GPU. The bulk (payload/CRC) kernel is not emulated beyond what the control step reads
+// back: each written entry's stream position (its info word) and the pool kernel's page bookkeeping
+// (S_LPG / S_APG); entries carry terms/types only.
 #define RG_FN inline
 #include "../../raftd_amd/csrc/raftgpu_control.h"
 #include "../../include/raftgpu.h"
@@ -15,6 +17,8 @@ struct Host {
   rg_config c;
   uint32_t nrep, J;
   std::vector<uint64_t> s64[2], rem[2], tr, hdr[2], mt[2], job64;
+  std::vector<uint2> info;        // [2 banks][nrep][L] {crc (0 here), stream position}
+  uint32_t PTS = 16;
   std::vector<uint32_t> s32[2], cnt[2], job32, jcnt;
   std::vector<uint8_t> rst[2];
   std::vector<uint2> slab_info;  // [nslab][G][E] {0, len}: synthetic Cmds are P bytes; ch_propose sets lengths
@@ -22,6 +26,7 @@ struct Host {
   std::vector<uint8_t> pt;        // rg_propose staging: target slot, count, non-empty mask per group
   std::vector<uint32_t> pc;
   std::vector<uint64_t> hm;
+  std::vector<uint2> pcmd;  // {stream chunks | contiguous << 31, arena chunk}: chunk counts only here
   bool staged = false;
   std::vector<uint16_t> cc;  // membership change staging: slot | descriptor << 8
   bool cc_staged = false;
@@ -36,6 +41,10 @@ static TickParams params(Host* h) {
   p.ET = c.election_rtt; p.HT = c.heartbeat_rtt; p.CQ = c.check_quorum; p.SE = c.snapshot_entries;
   p.CO = c.compaction_overhead; p.drop_ppm = c.drop_ppm; p.seed = c.seed; p.tick = h->t;
   p.AF = c.apply_feedback;
+  p.PTS = h->PTS;
+  p.JS = c.join_slots;
+  p.IM = c.initial_members;
+  p.info = h->info.data();
   p.pl = make_placement(1, 0, 0);  // one rank: every plane local
   const int a = (int)(h->t & 1), b = a ^ 1;
   p.s64_in = h->s64[a].data(); p.s64_out = h->s64[b].data();
@@ -76,6 +85,13 @@ void* ch_create(const rg_config* c) {
     h->cnt[b].assign(R * R * G, 0);
   }
   h->tr.assign(L * n, 0);
+  h->info.assign(2 * L * n, make_uint2(0u, 0u));
+  {  // stream_pages as rg_create sizes it
+    const uint64_t full = ((uint64_t)L * ((c->payload_bytes + 15) & ~15u) + PAGE_BYTES - 1) / PAGE_BYTES;
+    uint32_t pts = 16;
+    while (pts < 2 * full) pts <<= 1;
+    h->PTS = c->payload_bytes ? (c->stream_pages ? c->stream_pages : pts) : 1;
+  }
   h->job64.assign(J64_ROWS * J * n, 0);
   h->job32.assign(J32_ROWS * J * n, 0);
   h->jcnt.assign(n, 0);
@@ -84,6 +100,7 @@ void* ch_create(const rg_config* c) {
   h->pt.assign(G, 0xFF);
   h->pc.assign(G, 0);
   h->hm.assign(G, 0);
+  h->pcmd.assign(G, make_uint2(0u, 0u));
   h->cc.assign(G, 0);
   return h;
 }
@@ -99,29 +116,58 @@ uint32_t ch_pl_off(uint32_t N, uint32_t s, uint32_t d, uint32_t j) { return pl_o
 void ch_bootstrap(void* hh) {  // = bootstrap_kernel
   Host* h = (Host*)hh;
   h->t = 0;
-  const uint32_t R = h->c.replicas;
+  const uint32_t R = h->c.replicas, JS = h->c.join_slots;
   const uint64_t n = h->nrep;
   for (int b = 0; b < 2; ++b) std::fill(h->cnt[b].begin(), h->cnt[b].end(), 0u);
+  const uint32_t im = (h->c.initial_members ? h->c.initial_members : (1u << R) - 1u) & ~JS;
   for (uint32_t q = 0; q < n; ++q) {
     const uint32_t s = q / h->c.groups, g = q - s * h->c.groups;
+    const bool joining = (JS >> s) & 1u;
+    const uint64_t last = joining ? 0 : R;
     for (uint32_t f = 0; f < S64_ROWS; ++f) h->s64[0][f * n + q] = 0;
     for (uint32_t f = 0; f < S32_ROWS; ++f) h->s32[0][f * n + q] = 0;
-    h->s64[0][S_TERM * n + q] = 1;
-    h->s64[0][S_LAST * n + q] = R;
-    h->s64[0][S_COMMITTED * n + q] = R;
+    h->s64[0][S_TERM * n + q] = joining ? 0 : 1;
+    h->s64[0][S_LAST * n + q] = last;
+    h->s64[0][S_COMMITTED * n + q] = last;
+    h->s64[0][S_CC_HI * n + q] = last;
     h->s32[0][S_RNG_CTR * n + q] = 1;
-    const uint32_t im = h->c.initial_members ? h->c.initial_members : (1u << R) - 1u;
-    h->s32[0][S_MEMBERS * n + q] = im;
-    h->s32[0][S_SNAP_MEMBERS * n + q] = im;
+    h->s32[0][S_MEMBERS * n + q] = joining ? 0u : im;
+    h->s32[0][S_SNAP_MEMBERS * n + q] = joining ? 0u : im;
     const uint64_t key = ((uint64_t)g << 32) | ((uint64_t)s << 24) | 1ull;
     h->s32[0][S_RAND_TO * n + q] = h->c.election_rtt + (uint32_t)(mix64(h->c.seed ^ mix64(key)) % h->c.election_rtt);
     for (uint32_t j = 0; j < R; ++j) {
       h->rem[0][(0 * R + j) * n + q] = 0;
-      h->rem[0][(1 * R + j) * n + q] = R + 1;
+      h->rem[0][(1 * R + j) * n + q] = last + 1;
       h->rem[0][(2 * R + j) * n + q] = 0;
       h->rst[0][j * n + q] = RETRY;
     }
-    for (uint32_t i = 1; i <= R; ++i) h->tr[(i & (h->c.log_capacity - 1)) * n + q] = 1ull | TYPE_BIT;
+    for (uint32_t i = 1; i <= last; ++i) {
+      const uint32_t cc = ((im >> (i - 1)) & 1u) ? (CC_ADD << 4 | i) : 0u;
+      h->tr[(i & (h->c.log_capacity - 1)) * n + q] = 1ull | TYPE_BIT | cc_bits(cc);
+      h->info[(uint64_t)q * h->c.log_capacity + (i & (h->c.log_capacity - 1))] = make_uint2(0u, 0u);
+    }
+  }
+}
+
+// what the pool and bulk kernels leave behind that a later control step reads: the pages held
+// ([S_LPG, S_APG)) and every written entry's info word {0, stream position} (positions back to back
+// from the job's J_DPOS, as the bulk kernel lays them out)
+static void after_step(Host* h, const TickParams& p) {
+  const uint64_t n = h->nrep, L = h->c.log_capacity, JN = (uint64_t)h->J * n;
+  uint32_t* so = const_cast<uint32_t*>(p.s32_out);
+  for (uint64_t q = 0; q < n; ++q) {
+    so[S_LPG * n + q] = so[S_NLPG * n + q];
+    so[S_APG * n + q] = vpn_ceil(so[S_HW * n + q]);
+    for (uint32_t j = 0; j < p.jcnt[q]; ++j) {
+      const uint64_t jq = (uint64_t)j * n + q, first = p.job64[J_FIRST * JN + jq], dm = p.job64[J_DMASK * JN + jq];
+      const uint32_t meta = p.job32[J_META * JN + jq], nn = meta & 0xFF, e0 = (meta >> 8) & 0xFF;
+      uint32_t pos = p.job32[J_DPOS * JN + jq];
+      for (uint32_t e = e0; e < nn; ++e) {
+        const uint64_t slot = (first + e) & (L - 1);
+        h->info[(((dm >> e) & 1ull) * n + q) * L + slot] = make_uint2(0u, pos);
+        pos += word_nc(h->tr[slot * n + q]);
+      }
+    }
   }
 }
 
@@ -139,6 +185,7 @@ int ch_tick(void* hh, const rg_tick_input* in) {
     p.prop_target = h->pt.data();
     p.prop_count = h->pc.data();
     p.prop_hmask = h->hm.data();
+    p.prop_cmd = h->pcmd.data();
   }
   if (h->cc_staged) p.cc_in = h->cc.data();
   for (uint32_t q = 0; q < h->nrep; ++q) {
@@ -154,11 +201,13 @@ int ch_tick(void* hh, const rg_tick_input* in) {
       default: return -1;
     }
   }
+  after_step(h, p);
   h->t++;
   if (h->staged) {
     std::fill(h->pt.begin(), h->pt.end(), 0xFF);
     std::fill(h->pc.begin(), h->pc.end(), 0u);
     std::fill(h->hm.begin(), h->hm.end(), 0ull);
+    std::fill(h->pcmd.begin(), h->pcmd.end(), make_uint2(0u, 0u));
     h->staged = false;
   }
   if (h->cc_staged) {
@@ -187,6 +236,7 @@ int ch_propose(void* hh, const rg_proposal* props, uint64_t n, const uint32_t* l
       const uint32_t at = h->pc[b.group] + x, ln = lens[b.first + x];
       if (ln && P) h->hm[b.group] |= 1ull << at;
       h->slab_info[(slab * h->c.groups + b.group) * E + at] = make_uint2(0u, ln);
+      if (P) h->pcmd[b.group].x += (ln + 15) / 16;  // not contiguous: the bulk kernel is not emulated
     }
     h->pt[b.group] = (uint8_t)b.slot;
     h->pc[b.group] += b.count;
@@ -243,7 +293,11 @@ int ch_read_msgs(void* hh, uint32_t rid, uint32_t dst, rg_msg_view* out, uint32_
     uint64_t w[8];
     for (int i = 0; i < 8; ++i) w[i] = hp[i * plane];
     const bool uni = (w[0] & 0xFF) == M_REPLICATE && ((uint32_t)w[7] & RG_UNIFORM);  // shown expanded
-    if (uni) w[7] &= ~(uint64_t)RG_UNIFORM;
+    if (uni) {
+      w[7] &= ~(uint64_t)RG_UNIFORM;
+      w[5] = 0;  // its Cmds' stream position
+    }
+    if ((w[0] & 0xFF) == M_PROPOSE) w[4] = 0;  // its batch's stream layout
     memcpy(&out[k], w, 64);
     const uint64_t* mt = t.mt_in + ((((uint64_t)s * t.R + dst) * t.K + k) * t.E) * t.G + g;
     const uint32_t n = (uint32_t)(w[0] >> 32);
@@ -280,6 +334,7 @@ int ch_import(void* hh, uint32_t rid, const rg_replica_view* v, const uint64_t* 
   s32[S_DROPS * N] = v->drops;
   s32[S_MEMBERS * N] = v->members; s32[S_SNAP_MEMBERS * N] = v->snap_members; s32[S_CC_PENDING * N] = v->cc_pending;
   s64[S_CC_HI * N] = v->last;  // any imported entry may be a ConfigChange
+  s64[S_FIDX * N] = 0;
   const uint32_t R = h->c.replicas;
   for (uint32_t j = 0; j < R; ++j) {
     h->rem[a][(0 * R + j) * N + q] = v->match[j];
@@ -287,14 +342,21 @@ int ch_import(void* hh, uint32_t rid, const rg_replica_view* v, const uint64_t* 
     h->rem[a][(2 * R + j) * N + q] = v->rsnap[j];
     h->rst[a][j * N + q] = v->rstate[j];
   }
+  uint32_t pos = 0;  // a fresh payload stream from position 0 (rg_import_replica)
   for (uint64_t i = v->marker + 1; i <= v->last; ++i) {
     const uint64_t k = i - v->marker - 1;
     const uint32_t ty = types ? types[k] & 0xFFu : 0;
     const bool hp = with_payload && h->c.payload_bytes && ty == 0 && !(types && (types[k] & 0x100u));
     const uint32_t ln = lens ? lens[k] : h->c.payload_bytes;
-    h->tr[(i & (h->c.log_capacity - 1)) * N + q] = (terms[k] & TERM_MASK) | (ty ? TYPE_BIT : 0) |
-                                                   (ty ? cc_bits(lens ? lens[k] : 0) : hp ? len_bits(ln) : 0);
+    const uint64_t w = (terms[k] & TERM_MASK) | (ty ? TYPE_BIT : 0) | (ty ? cc_bits(lens ? lens[k] : 0) : hp ? len_bits(ln) : 0);
+    h->tr[(i & (h->c.log_capacity - 1)) * N + q] = w;
+    h->info[(uint64_t)q * h->c.log_capacity + (i & (h->c.log_capacity - 1))] = make_uint2(0u, pos);
+    pos += word_nc(w);
   }
+  s32[S_HW * N] = pos;
+  s32[S_LPG * N] = 0;
+  s32[S_APG * N] = vpn_ceil(pos);
+  s32[S_NLPG * N] = 0;
   return 0;
 }
 

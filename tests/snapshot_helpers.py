@@ -37,7 +37,7 @@ class OracleFeeds:
         recs, pays = [], []
         for rid in self._rids(slot_mask):
             for i, ln, crc, p in self.ora.applied_entries(rid):
-                recs.append((i, rid // self.R, rid % self.R + 1, ln, crc, rid))
+                recs.append((i, rid // self.R, rid % self.R + 1, ln, crc, rid, len(pays) * self.P))
                 pays.append(p.ljust(self.P, b"\0"))
         pay = np.frombuffer(b"".join(pays), np.uint8).reshape(len(pays), self.P) if pays else \
             np.zeros((0, self.P), np.uint8)

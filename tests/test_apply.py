@@ -16,7 +16,7 @@ def fake_batch():
     recs = np.zeros(5, APPLY_DTYPE)
     rows = [(7, 3, 2, 5, 4), (8, 3, 2, 5, 4), (9, 3, 2, 3, 4), (12, 17, 1, 4, 9), (13, 17, 1, 2, 9)]
     for k, (idx, g, rep, ln, rid) in enumerate(rows):
-        recs[k] = (idx, g, rep, ln, 0, rid)
+        recs[k] = (idx, g, rep, ln, 0, rid, 16 * k)
     pay = np.zeros((5, 16), np.uint8)
     for k in range(5):
         pay[k, :recs[k]["len"]] = np.arange(recs[k]["len"]) + 10 * k

@@ -14,7 +14,7 @@ def rec(group, slot, term, commit, first, last, marker=0, ents=(), vote=0):
     en = np.zeros(len(ents), PERSIST_ENTRY_DTYPE)
     pay = np.zeros((len(ents), P), np.uint8)
     for k, (i, t, ln) in enumerate(ents):
-        en[k] = (i, t, 0, ln, 0, 0)
+        en[k] = (i, t, 0, ln, 0, 0, k * P)
         pay[k, :ln] = (i * 7 + np.arange(ln)) & 0xFF
     return st, en, pay
 
