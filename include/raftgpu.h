@@ -72,8 +72,9 @@ typedef struct rg_config {
   uint32_t groups;              /* shards hosted by this engine */
   uint32_t replicas;            /* replicas per shard, IDs 1..replicas (1..8) */
   uint32_t log_capacity;        /* log ring entries per replica (power of two) */
-  uint32_t payload_bytes;       /* largest Cmd (bytes) an entry carries: 0 (metadata only) or a power of
-                                   two in [16, 1024]; each Cmd is 0..payload_bytes bytes */
+  uint32_t payload_bytes;       /* Cmd lane-group size P (bytes): 0 (metadata only) or a power of two in
+                                   [16, 1024]; the size of the generator's synthetic Cmds. Caller Cmds
+                                   are 0..max_cmd_bytes bytes (below) */
   uint32_t max_entries_per_msg; /* entries per Replicate / proposal batch (1..64) */
   uint32_t max_msgs_per_pair;   /* messages per (replica, destination) per tick (1..16) */
   uint32_t num_slabs;           /* proposal payload slabs, tick t uses slab t % num_slabs (>= 2) */
@@ -254,7 +255,8 @@ typedef struct rg_engine rg_engine;
 
 int rg_create(const rg_config* cfg, rg_engine** out);
 void rg_destroy(rg_engine* e);
-/* Every replica: becomeFollower(1) + bootstrap ConfigChange entries 1..R, committed R. */
+/* Every replica: becomeFollower(1) + bootstrap ConfigChange entries 1..R (AddNode for each initial
+ * member), committed R; a join slot (rg_config.join_slots): becomeFollower(0), empty log. */
 int rg_bootstrap(rg_engine* e);
 /* Fill every proposal slab with the deterministic payload generator: the synthetic
  * Cmds (payload_bytes each) that tick-input proposals (rg_tick_input.prop_target) carry — the
@@ -262,7 +264,7 @@ int rg_bootstrap(rg_engine* e);
 int rg_fill_slabs(rg_engine* e);
 /* Stage client commands for the next tick (its proposal step): n batches, Cmd bytes
  * in `payload` (host memory, copied before return; packed in lens order), lengths in `lens`
- * (each <= payload_bytes; 0 = an empty Cmd, which commits but is not handed to Update). Calls before
+ * (each <= max_cmd_bytes; 0 = an empty Cmd, which commits but is not handed to Update). Calls before
  * one tick accumulate: batches for the same shard and slot are concatenated up to
  * max_entries_per_msg. All or nothing: RG_EINVAL (bad shard / slot / count / length, a slot hosted
  * elsewhere), RG_EFULL (a shard's batch would exceed max_entries_per_msg, or a second slot of one

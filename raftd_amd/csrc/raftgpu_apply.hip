@@ -43,7 +43,10 @@ __device__ __forceinline__ void copy_run(const uint8_t* pool, const uint32_t* pt
       const uint32_t v = (uint32_t)__shfl((int)inc, (int)(lo + step - 1), 64);
       if (v <= t) lo += step;
     }
-    const uint32_t ex = lo ? (uint32_t)__shfl((int)inc, (int)(lo - 1), 64) : 0u;
+    // every lane takes part in the permute: a lane masked off by a branch supplies no data, and a
+    // reader of it (lane lo - 1 with its own lo = 0) would get 0
+    const uint32_t exl = (uint32_t)__shfl((int)inc, (int)(lo ? lo - 1 : 0), 64);
+    const uint32_t ex = lo ? exl : 0u;
     const uint32_t spl = (uint32_t)__shfl((int)sp, (int)(lo < 64 ? lo : 63), 64);
     if (t < total) {
       const u32x4 v = *reinterpret_cast<const u32x4*>(pool + stream_byte(pt, PTS, q, spl + (t - ex)));

@@ -494,6 +494,7 @@ struct Ctl {
     } else {
       uni = true;  // SRC_SLAB (generator Cmds, P bytes) or SRC_NONE (no Cmd bytes)
     }
+    uni = uni && ncu <= (p.P >> 4);  // the pipelined path moves at most one lane group (P bytes) per entry
     if (nj < p.J) {
       const uint64_t n64 = p.nrep, JN = (uint64_t)p.J * n64;
       uint64_t* j64 = p.job64 + (uint64_t)nj * n64 + q;

@@ -310,7 +310,10 @@ constexpr uint32_t CRC_ZP_OFF = CRC_ZI_OFF + CRC_ZI_WORDS;
 constexpr uint32_t CRC_ZP_WORDS = 8 * 16;
 constexpr uint32_t CRC_CS_OFF = CRC_ZP_OFF + CRC_ZP_WORDS;
 constexpr uint32_t CRC_CS_MAX = 512;  // ceil(MAX_CMD / 16)
-constexpr uint32_t CRC_TAB_WORDS = CRC_CS_OFF + CRC_CS_MAX + 1;
+// 16 zero bytes (16-B aligned): where the bulk kernel's idle lanes load from, so a lane past its
+// entry's chunks adds nothing to the lane group's CRC
+constexpr uint32_t CRC_ZERO_OFF = (CRC_CS_OFF + CRC_CS_MAX + 1 + 3) & ~3u;
+constexpr uint32_t CRC_TAB_WORDS = CRC_ZERO_OFF + 4;
 
 // CRC-32 of a Cmd of len bytes from its slot CRC (the CRC of the Cmd zero-padded to S·P bytes,
 // S = ceil(len / P)): slot = cs ^ raw(slot), raw(slot) = Z^(S·P−len) raw(Cmd), so

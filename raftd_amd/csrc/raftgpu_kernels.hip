@@ -434,7 +434,7 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p, const uint32_t*
   // and its use is the same on every path and the compiler's vmcnt waits keep the ring in flight.
   // A pass never spans two jobs (the cursor moves once per pass), so the slots consumed in a pass
   // all belong to the job `pj` the previous pass issued.
-  const uint8_t* dummy = reinterpret_cast<const uint8_t*>(p.crc_tab);
+  const uint8_t* dummy = reinterpret_cast<const uint8_t*>(p.crc_tab + CRC_ZERO_OFF);  // 16 zero bytes
   uint32_t vmask = 0;
   uint32_t iq = 0, ib = 0, ie0 = 0, idp = 0, incu = 0;  // the job of the pass being issued (for its consume)
   uint64_t ifirst = 0, idm = 0;

@@ -104,6 +104,7 @@ int alltoallv(void* user, const void* send, const uint64_t* soff, const uint64_t
   const Api* a = api();
   if (!a) return -1;
   hipStream_t st = (hipStream_t)stream, xs = c->xs;
+  if (hipSetDevice(c->device) != hipSuccess) return -1;
   if (hipEventRecord(c->ev_in, st) != hipSuccess || hipStreamWaitEvent(xs, c->ev_in, 0) != hipSuccess) return -1;
   uint64_t most = 0;
   for (int r = 0; r < c->nranks; ++r) most = std::max(most, std::max(ssize[r], rsize[r]));
@@ -113,16 +114,17 @@ int alltoallv(void* user, const void* send, const uint64_t* soff, const uint64_t
   const uint64_t pieces = (most + CHUNK - 1) / CHUNK;
   for (uint64_t k = 0; k < pieces; ++k) {
     if (a->GroupStart() != 0) return -1;
-    for (int r = 0; r < c->nranks; ++r) {
+    bool ok = true;  // a failed Send / Recv still closes the group, or every later call on the comm breaks
+    for (int r = 0; r < c->nranks && ok; ++r) {
       const uint64_t o = k * CHUNK;
       if (ssize[r] > o &&
           a->Send((const uint8_t*)send + soff[r] + o, std::min(CHUNK, ssize[r] - o), ncclUint8, r, c->comm, xs) != 0)
-        return -1;
-      if (rsize[r] > o &&
+        ok = false;
+      if (ok && rsize[r] > o &&
           a->Recv((uint8_t*)recv + roff[r] + o, std::min(CHUNK, rsize[r] - o), ncclUint8, r, c->comm, xs) != 0)
-        return -1;
+        ok = false;
     }
-    if (a->GroupEnd() != 0) return -1;
+    if (a->GroupEnd() != 0 || !ok) return -1;
   }
   // the engine stream's next work (unpack) waits for the transfers
   if (hipEventRecord(c->ev_out, xs) != hipSuccess || hipStreamWaitEvent(st, c->ev_out, 0) != hipSuccess) return -1;

@@ -251,7 +251,10 @@ __global__ void __launch_bounds__(256) pack_kernel(WireParams w) {
         if (v <= t) lo += step;
       }
       const uint32_t le = lo < 64 ? lo : 63;
-      const uint32_t ex = lo ? (uint32_t)__shfl((int)inc, (int)(lo - 1), 64) : 0u;
+      // every lane takes part in the permute: a lane masked off by a branch supplies no data, and a
+      // reader of it (lane lo - 1 with its own lo = 0) would get 0
+      const uint32_t exl = (uint32_t)__shfl((int)inc, (int)(lo ? lo - 1 : 0), 64);
+      const uint32_t ex = lo ? exl : 0u;
       const uint32_t spl = (uint32_t)__shfl((int)sp, (int)le, 64);
       const bool synl = __shfl((int)syn, (int)le, 64) != 0;
       if (t < total) {

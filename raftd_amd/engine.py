@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("RAFTGPU_LIB") or os.path.join(PKG, "libraftgpu.so")  
 MAX_R = 8
 
 RG_OK, RG_EINVAL, RG_ENOMEM, RG_EFULL, RG_EHIP, RG_EINVARIANT = 0, -1, -2, -3, -4, -5
+RG_ERR_CRC, RG_ERR_MALFORMED, RG_ERR_POOL = 8, 32, 64  # rg_replica_view.err bits
 TICK_NO_LOCALTICK = 1
 
 
@@ -94,8 +95,9 @@ def unpack_rows(recs, packed: np.ndarray, row: int) -> np.ndarray:
     """Packed Cmds (each at recs["off"], recs["len"] bytes) as one zero-padded row of `row` bytes per
     record: the Python view of rg_apply_committed / rg_persist_collect payloads."""
     out = np.zeros((len(recs), max(row, 1)), np.uint8)
+    app = (recs["type"] == 0).tolist() if "type" in recs.dtype.names else [True] * len(recs)
     for k, (o, n) in enumerate(zip(recs["off"].tolist(), recs["len"].tolist())):
-        if n and row:
+        if n and row and app[k]:  # a ConfigChange entry's len is its descriptor: no Cmd bytes
             out[k, :n] = packed[o:o + n]
     return out[:, :row]
 
@@ -407,7 +409,8 @@ class Engine:
         for k, ev in enumerate(buf):
             d = dict(term=ev.term, type=ev.type, len=ev.len, crc=ev.crc)
             if pay is not None:
-                d["payload"] = bytes(pay[k * P:k * P + ev.len])
+                # a ConfigChange entry's len is its descriptor: no Cmd bytes
+                d["payload"] = bytes(pay[k * P:k * P + ev.len]) if ev.type == 0 else b""
             out.append(d)
         return out
 

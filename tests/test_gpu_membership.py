@@ -64,6 +64,36 @@ def test_membership_with_caller_cmds():
     run_members(cfg, ticks=120, seed=9, caller=True)
 
 
+@pytest.mark.parametrize("R,js,im", [(4, 0b1000, 0), (5, 0b11000, 0), (3, 0b100, 0b011)])
+def test_join_slots(R, js, im):
+    """join_slots (StartOnDiskReplica join = true): empty joiners at term 0 outside the membership,
+    added by ConfigChanges every 10 ticks, catch up through probing (or a snapshot) bit-exact with
+    the oracle."""
+    cfg = dict(CHAOS, groups=4, replicas=R, payload_bytes=16, max_entries_per_msg=8, seed=950 + R,
+               initial_members=im, join_slots=js, drop_ppm=50000)
+    gpu, ora = make("gpu", **cfg), make("c", **cfg)
+    gpu.bootstrap()
+    ora.bootstrap()
+    compare(gpu, ora, -1)
+    rng = np.random.default_rng(R)
+    G = 4
+    joiners = [k for k in range(R) if js >> k & 1]
+    for t in range(150):
+        ccs = random_ccs(rng, G, R, 0.04)
+        if t % 10 == 5:
+            ccs = [(g, int(rng.integers(0, R)), 1, int(rng.choice(joiners))) for g in range(G)]
+        for c in ccs:
+            assert ora.config_change(*c) == 0
+            gpu.config_change(*c)
+        ins = random_inputs(rng, G, R, cfg["max_entries_per_msg"])
+        gpu.tick(*ins)
+        ora.tick(*ins)
+        compare(gpu, ora, t)
+    joined = sum(1 for r in range(G * R) if js >> (r % R) & 1 and ora.replica(r)["members"] >> (r % R) & 1
+                 and ora.replica(r)["last"] > 0)
+    assert joined > 0
+
+
 @pytest.mark.parametrize("ranks,R", [(2, 3), (3, 5)])
 def test_membership_cluster(ranks, R):
     """Changes proposed at followers on other ranks are forwarded over the wire; InstallSnapshot

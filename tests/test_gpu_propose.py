@@ -55,7 +55,7 @@ def run_caller(cfg, ticks, seed, make_gpu=None, check_every=1, p_none=0.3, appli
     rng = np.random.default_rng(seed)
     G, R, E, P = ora.G, ora.R, cfg["max_entries_per_msg"], cfg["payload_bytes"]
     for t in range(ticks):
-        batches = random_batches(rng, G, R, E, P, p_none=p_none)
+        batches = random_batches(rng, G, R, E, P, p_none=p_none, maxc=cfg.get("max_cmd_bytes"))
         gpu.propose(batches)
         assert ora.propose(batches) == 0
         camp = (rng.random(G * R) < 0.02).astype(np.uint8)
@@ -76,6 +76,60 @@ def test_caller_cmds_chaos(R, P):
     cfg = dict(CHAOS, groups=4, replicas=R, payload_bytes=P, max_entries_per_msg=8, seed=40 + R)
     _, _, lens = run_caller(cfg, ticks=100, seed=R * 100 + P)
     assert {0, 1, P} <= lens and len(lens) > 4, lens
+
+
+@pytest.mark.parametrize("R,P,maxc,pages", [(3, 64, 1000, 0), (5, 16, 300, 0), (3, 256, 8191, 0), (3, 64, 2000, 16),
+                                            (1, 1024, 4096, 0), (4, 32, 700, 0)])
+def test_caller_long_cmds_chaos(R, P, maxc, pages):
+    """Cmds longer than payload_bytes (P - 1, P + 1, max_cmd_bytes, random up to it) through the paged
+    payload stream: appended, forwarded, replicated, CRC'd, compacted (pages freed and reused) and
+    copied back bit-exact with the oracle; pages = 16: the stream capacity rule refuses appends."""
+    # a pool of stream_pages per replica never runs dry (the stream rule bounds live + pending pages);
+    # the default pool (a full log of P-byte Cmds per replica) is sized for the benchmark's Cmds
+    cfg = dict(CHAOS, groups=4, replicas=R, payload_bytes=P, max_entries_per_msg=8, seed=60 + R,
+               max_cmd_bytes=maxc, stream_pages=pages, pool_pages=4 * R * (pages or 16))
+    gpu, _, lens = run_caller(cfg, ticks=100, seed=R * 1000 + maxc)
+    assert max(lens) > P and {0, 1} <= lens, lens
+    st = gpu.pool_stats()
+    assert not st["failed"] and 0 < st["free"] < st["total"], st
+
+
+def test_caller_long_cmds_crc32c():
+    cfg = dict(CHAOS, groups=4, replicas=3, payload_bytes=64, max_entries_per_msg=8, seed=6, crc32c=1,
+               max_cmd_bytes=900, pool_pages=4 * 3 * 16)
+    run_caller(cfg, ticks=80, seed=78)
+
+
+@pytest.mark.parametrize("ranks,R", [(2, 3), (3, 5)])
+def test_caller_long_cmds_cluster(ranks, R):
+    """Long Cmds over the wire: a forwarded Propose and Replicate carry packed Cmds of any length."""
+    from raftd_amd.cluster import LoopbackCluster
+    cfg = dict(CHAOS, groups=2 * ranks, replicas=R, payload_bytes=64, max_entries_per_msg=8, seed=9 + ranks,
+               max_cmd_bytes=1500, pool_pages=2 * ranks * R * 16)
+    run_caller(cfg, ticks=80, seed=ranks * 11 + R, make_gpu=lambda: LoopbackCluster(ranks=ranks, **cfg))
+
+
+def test_pool_exhaustion_poisons_the_engine():
+    """A pool too small for the Cmds: the replicas whose pages could not be taken get RG_ERR_POOL
+    (sticky), rg_pool_stats reports the failure, and nothing is written out of bounds."""
+    from raftd_amd.engine import RG_ERR_POOL
+    cfg = dict(groups=4, replicas=3, payload_bytes=64, max_entries_per_msg=8, log_capacity=64, max_cmd_bytes=4000,
+               pool_pages=24)
+    gpu = make("gpu", **cfg)
+    gpu.bootstrap()
+    camp = np.zeros(12, np.uint8)
+    camp[0::3] = 1
+    gpu.tick()
+    gpu.tick(campaign=camp)
+    for _ in range(3):
+        gpu.tick()
+    big = bytes(range(256)) * 15
+    for t in range(6):
+        gpu.propose([(g, 0, [big] * 8) for g in range(4)])
+        gpu.tick()
+    st = gpu.pool_stats()
+    errs = [gpu.replica(r)["err"] for r in range(12)]
+    assert st["failed"] and any(e & RG_ERR_POOL for e in errs), (st, errs)
 
 
 def test_caller_cmds_crc32c():

@@ -62,6 +62,16 @@ def test_read_index_cluster(ranks):
     run_reads(cfg, ticks=80, seed=ranks, make_gpu=lambda: LoopbackCluster(ranks=ranks, **cfg))
 
 
+def test_read_index_survives_dropped_heartbeat():
+    """The leader's read heartbeat is lost; the next regular heartbeat carries the pending ctx."""
+    from test_oracle import read_heartbeat_drop
+    cfg = dict(groups=1, replicas=3, payload_bytes=16, max_entries_per_msg=8, log_capacity=256, snapshot_entries=0,
+               heartbeat_rtt=2, election_rtt=20)
+    gpu, ora = make("gpu", **cfg), make("c", **cfg)
+    assert read_heartbeat_drop(gpu) == read_heartbeat_drop(ora)
+    compare(gpu, ora, -1)
+
+
 def test_read_index_errors():
     from raftd_amd.engine import RgError
     gpu = make("gpu", groups=2, replicas=3, payload_bytes=16)

@@ -84,15 +84,20 @@ def cross_check(seed, G, R, T, **cfg):
                 assert a.entry(rid, i) == b.entry(rid, i), (seed, t, rid, i)
 
 
-def random_batches(rng, G, R, E, P, base=0, p_none=0.3):
+def random_batches(rng, G, R, E, P, base=0, p_none=0.3, maxc=None):
     """Caller proposals for one tick: per group (with probability 1 - p_none) a batch of 1..E Cmds
-    to a random slot, lengths drawn from the edge cases 0, 1, 17, P and uniform [0, P]."""
+    to a random slot, lengths drawn from the edge cases 0, 1, 17, P and uniform [0, P]; with
+    maxc > P (max_cmd_bytes) also P - 1, P + 1, maxc and uniform [0, maxc]."""
+    M = maxc or P
     out = []
     for g in range(G):
         if rng.random() < p_none:
             continue
         n = int(rng.integers(1, E + 1))
-        lens = [int(x) for x in rng.choice([0, 1, min(17, P), P, int(rng.integers(0, P + 1))], n)]
+        pool = [0, 1, min(17, P), P, int(rng.integers(0, P + 1))]
+        if M > P:
+            pool += [P - 1, P + 1, M, int(rng.integers(0, M + 1)), int(rng.integers(P, M + 1))]
+        lens = [int(x) for x in rng.choice(pool, n)]
         cmds = [rng.integers(0, 256, ln, dtype=np.uint8).tobytes() for ln in lens]
         out.append((base + g, int(rng.integers(0, R)), cmds))
     return out
@@ -108,7 +113,7 @@ def cross_check_caller(seed, G, R, T, **cfg):
     rng = np.random.default_rng(seed)
     P = kw["payload_bytes"]
     for t in range(T):
-        batches = random_batches(rng, G, R, kw["max_entries_per_msg"], P)
+        batches = random_batches(rng, G, R, kw["max_entries_per_msg"], P, maxc=kw.get("max_cmd_bytes"))
         assert a.propose(batches) == 0 and b.propose(batches) == 0
         _, _, camp, iso = random_inputs(rng, G, R, kw["max_entries_per_msg"])
         a.tick(None, None, camp, iso)
@@ -143,6 +148,25 @@ def test_caller_proposals_c_matches_python(seed):
                 import zlib
                 assert e["crc"] == zlib.crc32(e["payload"])
     assert 0 in lens and 1 in lens and len(lens) > 3
+
+
+@pytest.mark.parametrize("seed,R,P,maxc,pages", [(0, 3, 64, 1000, 0), (1, 5, 16, 300, 0), (2, 3, 256, 8191, 0),
+                                                  (3, 3, 64, 2000, 16), (4, 1, 1024, 4096, 0)])
+def test_long_cmds_c_matches_python(seed, R, P, maxc, pages):
+    """Cmds longer than payload_bytes (P - 1, P + 1, max_cmd_bytes, random up to it) in the paged
+    payload stream; pages = 16: a short stream, so appends hit the stream capacity rule (DESIGN.md
+    §1.7) and both restatements must refuse the same ones."""
+    a = cross_check_caller(500 + seed, G=3, R=R, T=60, payload_bytes=P, max_cmd_bytes=maxc, stream_pages=pages)
+    lens = set()
+    for rid in range(a.nrep):
+        v = a.replica(rid)
+        for i in range(v["marker"] + 1, v["last"] + 1):
+            e = a.entry(rid, i, with_payload=True)
+            lens.add(e["len"] if e["type"] == 0 else 0)
+            if e["len"] and e["type"] == 0:
+                import zlib
+                assert e["crc"] == zlib.crc32(e["payload"])
+    assert max(lens) > P, lens
 
 
 def lagging_apply(rng, e, nrep, p_notify=0.4):
@@ -257,6 +281,113 @@ def test_membership_c_matches_python(seed):
                 assert a.entry(rid, i) == b.entry(rid, i), (seed, t, rid, i)
             changed += va["members"] != (kw["initial_members"] or (1 << R) - 1)
     assert changed > 0
+
+
+@pytest.mark.parametrize("seed,R,js,im", [(0, 4, 0b1000, 0), (1, 5, 0b11000, 0), (2, 3, 0b100, 0b011),
+                                          (3, 4, 0b0110, 0)])
+def test_join_slots_c_matches_python(seed, R, js, im):
+    """join_slots (StartOnDiskReplica join = true, raft_manager.go:134-144): those slots start empty
+    at term 0 outside the membership; random ConfigChanges add them (and remove others) under loss
+    and elections; both restatements agree on every view, message and entry."""
+    G = 3
+    kw = dict(groups=G, replicas=R, payload_bytes=16, max_entries_per_msg=8, log_capacity=64, snapshot_entries=20,
+              compaction_overhead=5, drop_ppm=50000, seed=900 + seed, initial_members=im, join_slots=js)
+    a, b = make("c", **kw), make("py", **kw)
+    a.bootstrap()
+    b.bootstrap()
+    for rid in range(G * R):
+        v = a.replica(rid)
+        if js >> (rid % R) & 1:
+            assert v["term"] == 0 and v["last"] == 0 and v["members"] == 0, v
+        else:
+            assert v["members"] == (im or (1 << R) - 1) & ~js and v["last"] == R, v
+    rng = np.random.default_rng(seed)
+    joiners = [k for k in range(R) if js >> k & 1]
+    joined = 0
+    for t in range(160):
+        ccs = random_ccs(rng, G, R, p=0.05)
+        if t % 10 == 5:  # every shard is asked (at a random slot) to add one of its joining slots
+            ccs = [(g, int(rng.integers(0, R)), 1, int(rng.choice(joiners))) for g in range(G)]
+        for c in ccs:
+            assert a.config_change(*c) == b.config_change(*c) == 0, (t, c)
+        ins = random_inputs(rng, G, R, 8)
+        a.tick(*ins)
+        b.tick(*ins)
+        for rid in range(G * R):
+            va = a.replica(rid)
+            assert va == b.replica(rid), (seed, t, rid)
+            for d in range(R):
+                assert a.msgs(rid, d) == b.msgs(rid, d), (seed, t, rid, d)
+            for i in range(va["marker"] + 1, va["last"] + 1):
+                assert a.entry(rid, i) == b.entry(rid, i), (seed, t, rid, i)
+    for rid in range(G * R):
+        v = a.replica(rid)
+        joined += (js >> (rid % R) & 1) and (v["members"] >> (rid % R) & 1) and v["last"] > 0
+    assert joined > 0
+
+
+def test_join_scenario():
+    """A 2-member shard adds a joining third slot: the joiner stays silent at term 0 until the
+    leader's Replicate (or snapshot) reaches it, then holds the leader's log and membership and
+    counts toward quorum."""
+    from oracle.pyoracle import CC_ADD
+    o = make("c", groups=1, replicas=3, payload_bytes=16, max_entries_per_msg=8, log_capacity=256,
+             snapshot_entries=0, join_slots=0b100)
+    o.bootstrap()
+    o.tick()
+    o.tick(campaign=np.array([1, 0, 0], np.uint8))
+    for _ in range(3):
+        o.tick()
+    assert o.replica(0)["role"] == 2 and o.replica(0)["members"] == 0b011
+    assert o.replica(2)["term"] == 0 and o.replica(2)["last"] == 0
+    for _ in range(30):  # not a member: nobody sends it anything, and it never campaigns
+        o.tick()
+    assert o.replica(2)["term"] == 0 and o.replica(2)["role"] == 0
+    assert o.config_change(0, 0, CC_ADD, 2) == 0
+    for _ in range(12):  # commit, apply, then a probe round (reject, back to index 1) before the log flows
+        o.tick()
+    v = [o.replica(r) for r in range(3)]
+    assert all(x["members"] == 0b111 for x in v), [x["members"] for x in v]
+    assert v[2]["last"] == v[0]["last"] and v[2]["term"] == v[0]["term"]
+    iso = np.array([0, 1, 0], np.uint8)  # slot 1 cut off: {0, 2} is a quorum of three
+    c0 = v[0]["committed"]
+    pt, pc = np.zeros(1, np.uint8), np.ones(1, np.uint32)
+    for _ in range(4):
+        o.tick(pt, pc, isolate=iso)
+    assert o.replica(0)["committed"] >= c0 + 2
+
+
+def read_heartbeat_drop(o):
+    """the leader's read heartbeat is lost (both followers cut off for the tick it is
+    sent); the next regular heartbeat carries the pending ctx (dragonboat broadcastHeartbeatMessage
+    attaches readIndex.peepCtx), so the read still becomes ready. Returns the ready (ctx, index)."""
+    o.bootstrap()
+    o.tick()
+    o.tick(campaign=np.array([1, 0, 0], np.uint8))
+    for _ in range(5):
+        o.tick()
+    assert o.replica(0)["role"] == 2
+    assert o.read_index([(0, 0, 77)]) in (0, None)
+    o.tick(isolate=np.array([0, 1, 1], np.uint8))
+    assert o.read_ready(0) is None
+    hint = None
+    for _ in range(6):
+        o.tick()
+        hb = [m for m in o.msgs(0, 1) if m["type"] == 17]
+        if hb and hint is None:
+            hint = hb[0]["hint"]
+        r = o.read_ready(0)
+        if r is not None:
+            assert hint == 77  # the regular heartbeat carried the ctx
+            return r
+    raise AssertionError("the read never became ready")
+
+
+@pytest.mark.parametrize("kind", ["c", "py"])
+def test_read_index_survives_dropped_heartbeat(kind):
+    o = make(kind, groups=1, replicas=3, payload_bytes=16, max_entries_per_msg=8, log_capacity=256,
+             snapshot_entries=0, heartbeat_rtt=2, election_rtt=20)
+    assert read_heartbeat_drop(o)[0] == 77
 
 
 def test_membership_scenario():
