@@ -551,6 +551,10 @@ class LoopbackCluster(_Feeds):
     def t(self) -> int:
         return self.engines[0].t
 
+    @property
+    def device_bytes(self) -> int:
+        return sum(e.device_bytes for e in self.engines)
+
     # ---- views in global ids
     def replicas(self, first=0, n=None):
         n = self.nrep - first if n is None else n

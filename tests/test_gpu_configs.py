@@ -5,14 +5,16 @@ reproduce that window of a full-size run — every replica view, outbound messag
 with payload. Each test also checks size-independent properties over ALL groups.
 
 - C3: 65,536 groups x 5 replicas spread over 8 ranks (N ranks as N engines on this one GPU, every
-  cross-rank message through the wire), 64-entry batches of 256-B entries with CRC32. The log ring
-  is 512 entries instead of 2,048 (SnapshotEntries 200) so that 8 engines fit one GPU's HBM.
+  cross-rank message through the wire), 64-entry batches of 256-B entries with CRC32, a 2,048-entry
+  log ring and raftd's SnapshotEntries 1000 / CompactionOverhead 5: every replica snapshots and
+  compacts twice within the run. The paged payload store holds only live Cmds, so the eight ranks'
+  engines fit this one GPU.
 - C4: election storm, 65,536 groups x 3, no leader: randomized timeouts, split votes, term bumps;
   10% of the groups start with a follower holding a divergent uncommitted suffix (1-16 entries of
   term 2) and 5% with a second one (term 3), forcing truncation once a leader emerges.
 - C5: 1,048,576 groups x 3, Zipf(1.1)-skewed proposals (mean 1 entry per group per tick) with
-  snapshot/compaction index advance on the hot groups. P = 16, L = 1,024, E = 16, K = 4 so that
-  3.1 M replicas fit HBM (the payload ring holds the whole log window).
+  snapshot/compaction index advance on the hot groups, 256-B Cmds, L = 2,048, E = 16,
+  K = 4. 3.1 M replicas fit one GPU's HBM because payload pages hold only live Cmds.
 """
 import zlib
 
@@ -108,9 +110,10 @@ def zipf_rates(G, rng, s=1.1):
 
 def test_c5_one_million_groups_zipf_compaction():
     G, R, E = 1 << 20, 3, 16
-    cfg = dict(replicas=R, log_capacity=1024, payload_bytes=16, max_entries_per_msg=E, max_msgs_per_pair=4,
+    cfg = dict(replicas=R, log_capacity=2048, payload_bytes=256, max_entries_per_msg=E, max_msgs_per_pair=4,
                snapshot_entries=1000, compaction_overhead=5, seed=0xC5)
     eng = make("gpu", groups=G, **cfg)
+    assert eng.device_bytes < 288e9, eng.device_bytes  # the "288 GB HBM sizing" of BASELINE config 5
     rng = np.random.default_rng(5)
     lam = zipf_rates(G, rng)
     hot = int(np.argmax(lam))
@@ -149,15 +152,22 @@ def test_c5_one_million_groups_zipf_compaction():
     lead = eng.replica(hot * R)
     for s in range(R):
         e = eng.entry(hot * R + s, lead["last"], with_payload=True)
-        assert e["crc"] == zlib.crc32(e["payload"]) and e["len"] == 16
+        assert e["crc"] == zlib.crc32(e["payload"]) and e["len"] == 256
+    ps = eng.pool_stats()
+    assert not ps["failed"] and ps["free"] < ps["total"], ps
 
 
 def test_c3_five_replicas_eight_ranks_full_size():
+    """C3 at its stated size with raftd's snapshot settings: 65,536 groups x 5 spread over 8 ranks,
+    64 x 256-B entries per leader per tick, L 2,048, SnapshotEntries 1000, CompactionOverhead 5 —
+    every replica snapshots and compacts twice, and every follower entry crosses ranks."""
     from raftd_amd.cluster import LoopbackCluster
-    G, R, N, W = 65536, 5, 8, 512
-    # SnapshotEntries 200: with a 512-entry ring, compaction must keep the window moving
-    cfg = dict(replicas=R, log_capacity=512, payload_bytes=256, max_entries_per_msg=64, snapshot_entries=200, seed=0xC3)
-    cl = LoopbackCluster(ranks=N, groups=G, **cfg)
+    G, R, N, W = 65536, 5, 8, 256
+    cfg = dict(replicas=R, log_capacity=2048, payload_bytes=256, max_entries_per_msg=64, snapshot_entries=1000,
+               compaction_overhead=5, seed=0xC3)
+    # 40,960 replicas per rank, each holding ~1,100 live 256-B Cmds (70 pages) at most
+    cl = LoopbackCluster(ranks=N, groups=G, pool_pages=1 << 22, **cfg)
+    assert cl.device_bytes < 288e9, cl.device_bytes
     wins = [(0, W), (G - W, W)]
     oras = [make("c", groups=n, group_base=b, **cfg) for b, n in wins]
     cl.bootstrap()
@@ -166,18 +176,23 @@ def test_c3_five_replicas_eight_ranks_full_size():
     camp = np.zeros(G * R, np.uint8)
     camp[0::R] = 1
     pt, pc = np.zeros(G, np.uint8), np.full(G, 64, np.uint32)
-    for t in range(16):
+    for t in range(44):
         ins = dict(campaign=camp) if t == 1 else (dict(prop_target=pt, prop_count=pc) if t >= 6 else {})
         cl.tick(**ins)
         for (b, n), o in zip(wins, oras):
             o.tick(**{k: v[b * (R if k == "campaign" else 1):(b + n) * (R if k == "campaign" else 1)]
-                      for k, v in ins.items()})
-        if t in (7, 15):
+                      for k, v in ins.items()}, threads=8)
+        if t in (7, 24, 43):
             for (b, n), o in zip(wins, oras):
                 compare_window(cl.replica, cl.msgs, lambda gr, lo, k: cl.entries(gr, lo, k, with_payload=True), o,
-                               b, n, R, t, check_entries=(t == 15))
+                               b, n, R, t, check_entries=(t != 7))
     assert cl.wire_bytes > 4 * G * 64 * 256  # every follower entry crossed ranks
-    assert cl.sum_committed() >= G * (R + 1 + 8 * 64)  # slot-0 replicas committed the batches
+    assert cl.sum_committed() >= G * (R + 1 + 36 * 64)  # slot-0 replicas committed the batches
+    for g in (0, G // 2 + 3, G - 1):
+        for s in range(R):
+            v = cl.replica(g * R + s)
+            assert v["snap_index"] >= 2000 and v["marker"] == v["snap_index"] - 5 and v["last"] > 2048, v
+            assert v["err"] == 0
 
 
 def test_c2_steady_state_full_shard_set():
@@ -218,35 +233,3 @@ def test_c2_steady_state_full_shard_set():
     v = gpu.replica_array()
     assert (v["err"] == 0).all() and (v["last"] > L).all()  # every log wrapped the ring
     assert (v["committed"][0::R] >= R + 1 + 46 * E).all()  # slot-0 leaders committed the batches (one in flight)
-
-
-def test_c3_snapshot_entries_1000():
-    """C3's shape with raftd's SnapshotEntries 1000 / CompactionOverhead 5 and a 2,048-entry ring
-    (5 replicas spread over 8 ranks, 64 x 256-B entries per tick): snapshots and compaction happen
-    twice per replica within the run. 8,192 groups (1,024 columns per rank) so that the eight ranks'
-    engines fit this one GPU; on an 8-GPU node each rank holds 8,192 columns at the same ring size."""
-    from raftd_amd.cluster import LoopbackCluster
-    G, R, N, W = 8192, 5, 8, 256
-    cfg = dict(replicas=R, log_capacity=2048, payload_bytes=256, max_entries_per_msg=64, snapshot_entries=1000,
-               compaction_overhead=5, seed=0xC35)
-    cl = LoopbackCluster(ranks=N, groups=G, **cfg)
-    wins = [(0, W), (G - W, W)]
-    oras = [make("c", groups=n, group_base=b, **cfg) for b, n in wins]
-    cl.bootstrap()
-    for o in oras:
-        o.bootstrap()
-    camp = np.zeros(G * R, np.uint8)
-    camp[0::R] = 1
-    pt, pc = np.zeros(G, np.uint8), np.full(G, 64, np.uint32)
-    for t in range(44):
-        ins = dict(campaign=camp) if t == 1 else (dict(prop_target=pt, prop_count=pc) if t >= 6 else {})
-        cl.tick(**ins)
-        for (b, n), o in zip(wins, oras):
-            o.tick(**{k: v[b * (R if k == "campaign" else 1):(b + n) * (R if k == "campaign" else 1)]
-                      for k, v in ins.items()}, threads=8)
-        if t in (20, 43):
-            for (b, n), o in zip(wins, oras):
-                compare_window(cl.replica, cl.msgs, lambda gr, lo, k: cl.entries(gr, lo, k, with_payload=True), o,
-                               b, n, R, t, check_entries=(t == 43))
-    v = cl.replica(0)
-    assert v["snap_index"] >= 2000 and v["marker"] == v["snap_index"] - 5 and v["last"] > 2048, v
