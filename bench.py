@@ -69,6 +69,9 @@ def parse():
     ap.add_argument("--exchange", choices=["torch", "c"], default="torch", help="N > 1 spread: move the regions "
                     "with torch.distributed from Python (default) or with the library's rg_wire_exchange (built-in "
                     "RCCL transport on nccl; each half on its own stream)")
+    ap.add_argument("--ingest", action="store_true", help="N = 1: also time the client ingest path: every step "
+                    "the G x E Cmds enter through rg_propose from host memory (NodeHost.Propose) instead of the "
+                    "HBM-resident proposal slabs; reported beside the headline line as `ingest`")
     ap.add_argument("--backend", default="nccl", help="N > 1: nccl (RCCL, default) or gloo (rehearsal: several "
                     "ranks on one GPU with RAFTD_BENCH_DEVICE=0, regions staged through host memory)")
     return ap.parse_args()
@@ -236,6 +239,54 @@ def e2e_with_apply(eng, tick, G, steps, slot_mask=1, serial=False):
                     "is PCIe-bound, so this is min(tick rate, PCIe rate)"}
 
 
+def ingest(eng, G, E, P, steps, seed=7):
+    """The client ingest path (SURVEY §8b rg_propose ≈ NodeHost.Propose): every step each leader's
+    E Cmds of P bytes (host memory, pageable, the way a cgo shim hands Go []byte over) are staged by
+    one rg_propose call for all G shards, then the tick runs; host wall time per step, so the
+    figure includes the host-side staging and the H2D copy of the Cmd bytes."""
+    import ctypes as C
+    import numpy as np
+    import torch
+    from raftd_amd.engine import Proposal
+    props = (Proposal * G)()
+    a = np.frombuffer(props, dtype=np.dtype([("group", "<u8"), ("slot", "<u4"), ("count", "<u4"), ("first", "<u8")]))
+    a["group"] = np.arange(G)
+    a["slot"] = 0
+    a["count"] = E
+    a["first"] = np.arange(G, dtype=np.uint64) * E
+    lens = np.full(G * E, P, np.uint32)
+    blob = np.random.default_rng(seed).integers(0, 256, G * E * P, dtype=np.uint8)
+    c0 = eng.sum_committed()
+
+    def step():
+        rc = eng.L.rg_propose(eng.h, props, G, blob.ctypes.data, lens.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(f"rg_propose: {eng.L.rg_last_error().decode()}")
+        eng.tick_device()
+
+    step()  # warm: staging buffers grow once
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tp = 0.0
+    for _ in range(steps):
+        a0 = time.perf_counter()
+        rc = eng.L.rg_propose(eng.h, props, G, blob.ctypes.data, lens.ctypes.data)
+        tp += time.perf_counter() - a0
+        if rc != 0:
+            raise RuntimeError(f"rg_propose: {eng.L.rg_last_error().decode()}")
+        eng.tick_device()
+    eng.sync()
+    el = time.perf_counter() - t0
+    committed = eng.sum_committed() - c0
+    nb = G * E * P
+    return {"value": G * steps / el, "unit": "group-steps/s", "steps": steps, "ms_per_step": el * 1e3 / steps,
+            "propose_ms_per_step": tp * 1e3 / steps, "cmd_bytes_per_step": nb, "ingest_GBps": nb * steps / el / 1e9,
+            "propose_GBps": nb * steps / tp / 1e9 if tp else None, "commits_per_step": committed / (steps + 1),
+            "note": "per step: one rg_propose of G batches x E Cmds from pageable host memory (validation, staging "
+                    "into pinned memory, one H2D copy, descriptor kernel), then rg_tick_device with no tick-input "
+                    "proposals; host wall time"}
+
+
 def pmc_traffic(kernel="bulk_kernel", wire=False, spread=False):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of the
     same bench mode (profiles/r*_pmc_summary.json; *_wire_* = the --wire-all runs, *_spread_* =
@@ -376,6 +427,7 @@ def main():
         e2e["serial"] = e2e_with_apply(eng, lambda: one_step(None), G, steps=max(4, min(args.steps, 12)),
                                        serial=True)
     apply = apply_copyback(eng, torch)
+    ing = ingest(eng, G, E, P, steps=max(3, min(args.steps, 8))) if args.ingest and not spread and P else None
     copy_gbs = hbm_copy_ceiling(eng)
     t = torch.tensor([wall, dev_ms, float(c1 - c0), x_ms, float(wire_bytes)], dtype=torch.float64,
                      device="cuda" if args.backend == "nccl" else "cpu")
@@ -488,6 +540,8 @@ def main():
         "apply_copyback": apply,
         "e2e_with_apply": e2e,
     }
+    if ing:
+        out["ingest"] = ing
     if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
         out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
     print(json.dumps(out), flush=True)

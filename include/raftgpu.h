@@ -396,6 +396,46 @@ int rg_persist_collect(rg_engine* e, int full, rg_persist_state* states, uint64_
  * replica in device order (slot by slot, shards ascending within a slot), compacted on the device and copied back by one hipMemcpyAsync. *n = the count;
  * if *n > cap nothing is copied and RG_EFULL is returned. Synchronous. */
 int rg_snapshot_events(rg_engine* e, uint32_t slot_mask, rg_snapshot_event* events, uint64_t cap, uint64_t* n);
+/* ---- One hand-off per tick (dragonboat Peer.GetUpdate / Peer.Commit): everything the
+ * host must act on after a tick, gathered on the device in one pass — the persistence feed
+ * (rg_persist_collect), the committed entries for IOnDiskStateMachine.Update (rg_apply_committed),
+ * the snapshot events (rg_snapshot_events) and the reads made ready (rg_read_index_results) — with
+ * one host synchronisation for the counts and one D2H copy of all sections. The pointers are
+ * engine-owned pinned memory, valid until the next rg_get_update or rg_destroy. slot_mask selects
+ * the replicas whose committed entries, snapshot events and reads are reported (the node's slots);
+ * the persistence section covers every replica whose log or hard state changed (every replica and
+ * its whole log window with RG_UPDATE_FULL_STATE: a checkpoint). Sections not asked for are empty. */
+#define RG_UPDATE_PERSIST 1u     /* EntriesToSave + State (rg_persist_collect) */
+#define RG_UPDATE_COMMITTED 2u   /* CommittedEntries for Update (rg_apply_committed) */
+#define RG_UPDATE_SNAPSHOTS 4u   /* snapshot events (rg_snapshot_events) */
+#define RG_UPDATE_READS 8u       /* ReadyToReads (rg_read_index_results) */
+#define RG_UPDATE_ALL 15u
+#define RG_UPDATE_FULL_STATE 16u /* persistence section: every replica, whole log window */
+typedef struct rg_update {
+  uint64_t tick;                          /* ticks run when the update was taken */
+  const rg_persist_state* states;
+  uint64_t n_states;
+  const rg_persist_entry* entries;        /* grouped by replica; rg_persist_state.entry_off indexes it */
+  uint64_t n_entries;
+  const uint8_t* entry_payload;           /* rg_persist_entry.off into it */
+  uint64_t entry_payload_bytes;
+  const rg_apply_entry* committed;
+  uint64_t n_committed;
+  const uint8_t* committed_payload;       /* rg_apply_entry.off into it */
+  uint64_t committed_payload_bytes;
+  const rg_snapshot_event* snapshots;
+  uint64_t n_snapshots;
+  const rg_read_ready* reads;
+  uint64_t n_reads;
+  uint32_t slot_mask, flags;
+} rg_update;
+int rg_get_update(rg_engine* e, uint32_t slot_mask, uint32_t flags, rg_update* out);
+/* Peer.Commit for an update the host has made durable and handed to the state machine: with
+ * RG_COMMIT_APPLIED, every replica of u->slot_mask reports applied = its processed index
+ * (NotifyRaftLastApplied; meaningful with rg_config.apply_feedback = 1). The update's buffers may
+ * be reused afterwards. */
+#define RG_COMMIT_APPLIED 1u
+int rg_commit_update(rg_engine* e, const rg_update* u, uint32_t flags);
 /* Stage ReadIndex requests for the next tick (dragonboat's NodeHost.ReadIndex → Peer.ReadIndex): a
  * leader that has committed an entry in its term records its commit index and confirms leadership
  * with one heartbeat round carrying the context; a follower forwards the request to its leader,

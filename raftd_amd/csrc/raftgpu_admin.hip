@@ -253,4 +253,19 @@ hipError_t launch_notify_applied(const AdminParams& a, const uint32_t* rids, con
   return hipGetLastError();
 }
 
+// rg_commit_update(RG_COMMIT_APPLIED): every replica of the slot mask has applied what it was handed
+// (applied = processed), one lane per replica
+__global__ void applied_all_kernel(AdminParams a, uint32_t slot_mask) {
+  const TickParams& t = a.t;
+  const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, N = t.nrep;
+  if (q >= N || !((slot_mask >> (q / t.G)) & 1u)) return;
+  uint64_t* s64 = ((uint64_t*)(t.s64_in)) + q;
+  s64[S_APPLIED * N] = s64[S_PROCESSED * N];
+}
+
+hipError_t launch_applied_all(const AdminParams& a, uint32_t slot_mask, hipStream_t s) {
+  hipLaunchKernelGGL(applied_all_kernel, dim3((a.t.nrep + 255) / 256), dim3(256), 0, s, a, slot_mask);
+  return hipGetLastError();
+}
+
 }  // namespace rg

@@ -92,12 +92,23 @@ RG_FN void sel_set(T (&a)[R], uint32_t f, V val) {
   });
 }
 
+// The parameter block is read through the constant address space on the device: it does not
+// change during a launch, so every field read is a scalar (s_load) read served by the scalar cache,
+// wherever it sits in the step (stores to global memory cannot clobber it), and no copy of the
+// block has to stay live in registers.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RG_CONST(T) __attribute__((address_space(4))) T
+#else
+#define RG_CONST(T) T
+#endif
+using CTickParams = RG_CONST(const TickParams);
+
 template <int R>
 struct Ctl {
   // the tick's parameter block, read in place at each use (a device slot the host filled): the
   // fields are reloaded where needed instead of living in registers for the whole step (r02 kept a
   // 368-B copy, 279 SGPR spills at R = 3)
-  const TickParams& p;
+  CTickParams& p;
   uint32_t q, g, s;    // g = local column (indexes every device array)
   uint64_t gg, rid;    // global group and global replica id gg·R + s (RNG keys, loss hash)
   uint32_t gi;         // the global group as an index into this engine's tick-input arrays (< 2^32)
@@ -132,7 +143,7 @@ struct Ctl {
   uint32_t nj;      // jobs emitted
   uint64_t lt_i = ~0ull, lt_v = 0;  // term_at cache: index lt_i has term lt_v (~0: none)
 
-  RG_FN Ctl(const TickParams& pp, uint32_t qq) : p(pp), q(qq) {
+  RG_FN Ctl(CTickParams& pp, uint32_t qq) : p(pp), q(qq) {
     s = q / p.G;
     g = q - s * p.G;
     gg = pl_group(p.pl, s, g);

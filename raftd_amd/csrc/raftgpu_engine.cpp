@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <thread>
 #include <unordered_map>
 #include <cstdlib>
 #include <cstring>
@@ -98,6 +99,10 @@ struct rg_engine {
   uint2* h_pcmd = nullptr;
   uint2* d_prop_cmd = nullptr;
   std::vector<uint32_t> pnc;
+  // rg_propose scratch, kept across calls: per input index this call's additions (validation),
+  // the indices set, the callers' Cmd offsets, and per staged Cmd its source offset
+  std::vector<uint32_t> padd;
+  std::vector<uint64_t> pset, pboff, psrc;
   std::vector<uint64_t> touched;  // input indices set in h_* since the last upload
   bool staged = false, stg_reset_pending = false;
   hipEvent_t stg_ev = nullptr;    // the last upload of h_* (host may rewrite them once it completed)
@@ -192,6 +197,13 @@ struct rg_engine {
   uint32_t* prof = nullptr;     // RG_CTL_PROFILE builds: control phase stamps of the last tick
   uint32_t *pscnt = nullptr, *pecnt = nullptr, *pccnt = nullptr;
   uint64_t *psoff = nullptr, *peoff = nullptr, *pcoff = nullptr;
+  // rg_get_update: count / offset rows of the snapshot and read sections (the committed section
+  // uses acnt / aoff, the persistence section pscnt / psoff, so every count runs before any gather),
+  // and the pinned host buffer all sections land in
+  uint32_t *uscnt = nullptr, *urcnt = nullptr;
+  uint64_t *usoff = nullptr, *uroff = nullptr;
+  uint8_t* u_host = nullptr;
+  uint64_t u_hcap = 0;
 };
 
 static int stage_reset(rg_engine* e);
@@ -504,6 +516,10 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if (rc == RG_OK) rc = dalloc(e, &e->psoff, (n + 1) * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->peoff, (n + 1) * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->pcoff, (n + 1) * 8);
+  if (rc == RG_OK) rc = dalloc(e, &e->uscnt, n * 4);
+  if (rc == RG_OK) rc = dalloc(e, &e->urcnt, n * 4);
+  if (rc == RG_OK) rc = dalloc(e, &e->usoff, (n + 1) * 8);
+  if (rc == RG_OK) rc = dalloc(e, &e->uroff, (n + 1) * 8);
   // exchange units: every remote (s, d, j) outbox column, per destination rank (send) and per
   // source rank (receive), each in (s, d, j) order — the same list on both ends of a link
   if (rc == RG_OK && e->wire) {
@@ -840,24 +856,44 @@ int rg_propose(rg_engine* e, const rg_proposal* props, size_t n, const uint8_t* 
   RGCHK(stage_reset(e));
   const uint32_t N = e->pl.N, R = e->c.replicas, E = e->c.max_entries_per_msg, P = e->c.payload_bytes;
   const uint64_t g0 = (uint64_t)N * e->pl.col_base, gn = (uint64_t)N * e->c.groups;
-  // validate every batch against the tables plus this call's earlier batches (all or nothing)
-  std::unordered_map<uint64_t, std::pair<uint32_t, uint32_t>> add;  // input index -> (slot, count)
+  // validate every batch against the tables plus this call's earlier batches (all or nothing):
+  // padd[input index] = this call's additions (count | slot << 8 | 1 << 16), cleared on the way out
+  std::vector<uint32_t>& padd = e->padd;
+  if (padd.size() < gn) padd.assign(gn, 0u);
+  std::vector<uint64_t>& pset = e->pset;
+  pset.clear();
+  auto clear_add = [&] {
+    for (uint64_t gi : pset) padd[gi] = 0;
+    pset.clear();
+  };
   uint64_t nent = 0, nbytes = 0;
   for (size_t i = 0; i < n; ++i) {
     const rg_proposal& b = props[i];
-    if (b.group < g0 || b.group >= g0 + gn || b.slot >= R || b.count < 1 || b.count > E)
+    if (b.group < g0 || b.group >= g0 + gn || b.slot >= R || b.count < 1 || b.count > E) {
+      clear_add();
       return fail(RG_EINVAL, "rg_propose: batch " + std::to_string(i) + ": bad shard, slot or count");
-    if (pl_rank_of(e->pl, b.group, b.slot) != e->pl.rank)
+    }
+    if (pl_rank_of(e->pl, b.group, b.slot) != e->pl.rank) {
+      clear_add();
       return fail(RG_EINVAL, "rg_propose: batch " + std::to_string(i) + ": that replica is hosted by another rank");
+    }
     const uint64_t gi = b.group - g0;
-    auto it = add.find(gi);
-    const uint32_t have = e->h_pc[gi] + (it == add.end() ? 0u : it->second.second);
-    const uint32_t slot = it != add.end() ? it->second.first : e->h_pc[gi] ? e->h_pt[gi] : b.slot;
-    if (have && slot != b.slot) return fail(RG_EFULL, "rg_propose: a second slot of one shard in one tick");
-    if (have + b.count > E) return fail(RG_EFULL, "rg_propose: batch larger than max_entries_per_msg");
-    add[gi] = {b.slot, have - e->h_pc[gi] + b.count};
+    const uint32_t ad = padd[gi], added = ad & 0xFFu;
+    const uint32_t have = e->h_pc[gi] + added;
+    const uint32_t slot = ad ? (ad >> 8) & 0xFFu : e->h_pc[gi] ? e->h_pt[gi] : b.slot;
+    if (have && slot != b.slot) {
+      clear_add();
+      return fail(RG_EFULL, "rg_propose: a second slot of one shard in one tick");
+    }
+    if (have + b.count > E) {
+      clear_add();
+      return fail(RG_EFULL, "rg_propose: batch larger than max_entries_per_msg");
+    }
+    if (!ad) pset.push_back(gi);
+    padd[gi] = (added + b.count) | (b.slot << 8) | (1u << 16);
     nent = std::max<uint64_t>(nent, b.first + b.count);
   }
+  clear_add();
   if (nent && !lens) return fail(RG_EINVAL, "rg_propose: null lens");
   for (uint64_t j = 0; j < nent; ++j) {
     if (lens[j] > e->maxc) return fail(RG_EINVAL, "rg_propose: Cmd longer than max_cmd_bytes");
@@ -904,11 +940,15 @@ int rg_propose(rg_engine* e, const rg_proposal* props, size_t n, const uint8_t* 
       e->d_cmd_cap = (need - cb) * 3 / 2;
     }
   }
-  std::vector<uint64_t> boff(nent + 1, 0);
+  std::vector<uint64_t>& boff = e->pboff;
+  boff.assign(nent + 1, 0);
   for (uint64_t j = 0; j < nent; ++j) boff[j + 1] = boff[j] + lens[j];
   uint64_t* info_at = (uint64_t*)(e->h_cmd + cb);
   uint32_t* chunk = (uint32_t*)(info_at + nstage);
   uint32_t* len = chunk + nstage;
+  std::vector<uint64_t>& srcoff = e->psrc;  // per staged Cmd: its offset in the caller's payload
+  if (P) srcoff.resize(nstage);
+  // pass 1 (serial, tables + descriptors): each Cmd's place in the arena and the shard's batch
   uint64_t k = 0, at_chunk = 0;
   for (size_t i = 0; i < n; ++i) {
     const rg_proposal& b = props[i];
@@ -929,9 +969,7 @@ int rg_propose(rg_engine* e, const rg_proposal* props, size_t n, const uint8_t* 
           pc.x &= ~(1u << 31);
         }
         pc.x += (uint32_t)nc;
-        uint8_t* d = e->h_cmd + at_chunk * 16;
-        if (ln) memcpy(d, payload + boff[b.first + x], ln);
-        if (nc * 16 > ln) memset(d + ln, 0, nc * 16 - ln);
+        srcoff[k] = boff[b.first + x];
         info_at[k] = (slab * rows + row) * E + at;
         chunk[k] = (uint32_t)(a0 + at_chunk);
         len[k] = ln;
@@ -942,6 +980,36 @@ int rg_propose(rg_engine* e, const rg_proposal* props, size_t n, const uint8_t* 
     if (!e->h_pc[gi]) e->touched.push_back(gi);
     e->h_pt[gi] = (uint8_t)b.slot;
     e->h_pc[gi] += b.count;
+  }
+  // pass 2 (the bytes): every Cmd into its chunk-aligned place in pinned staging, zero-padded to its
+  // chunk boundary. Runs of Cmds that are back to back in both buffers (lengths multiples of 16 B,
+  // the common case) move with one memcpy; large calls split over host threads (≈ 1 GiB per tick at
+  // 64K shards x 64 Cmds of 256 B: one thread copies it at host-memcpy speed).
+  if (P && k) {
+    auto copy_range = [&](uint64_t lo, uint64_t hi) {
+      uint64_t r = lo;
+      while (r < hi) {
+        uint64_t q = r, bytes = len[r];
+        while (q + 1 < hi && (len[q] & 15u) == 0 && srcoff[q + 1] == srcoff[q] + len[q] &&
+               chunk[q + 1] == chunk[q] + len[q] / 16) {
+          ++q;
+          bytes += len[q];
+        }
+        uint8_t* d = e->h_cmd + (uint64_t)(chunk[r] - a0) * 16;
+        if (bytes) memcpy(d, payload + srcoff[r], bytes);
+        const uint64_t span = (uint64_t)(chunk[q] - chunk[r]) * 16 + ((len[q] + 15) & ~15u);
+        if (span > bytes) memset(d + bytes, 0, span - bytes);
+        r = q + 1;
+      }
+    };
+    const uint64_t T = std::min<uint64_t>({16, std::max(1u, std::thread::hardware_concurrency()), 1 + cb / (64ull << 20)});
+    if (T <= 1) {
+      copy_range(0, k);
+    } else {
+      std::vector<std::thread> th;
+      for (uint64_t t = 0; t < T; ++t) th.emplace_back(copy_range, k * t / T, k * (t + 1) / T);
+      for (auto& x : th) x.join();
+    }
   }
   if (P && k) {
     // the Cmd bytes straight into the slab's arena (one H2D copy), then their descriptors
@@ -1629,6 +1697,106 @@ int rg_read_index_results(rg_engine* e, uint32_t slot_mask, rg_read_ready* out, 
   LAUNCH(launch_read_gather(a, e->stream), e->stream, "read gather");
   HIPCHK(hipMemcpyAsync(out, a.out, rb, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
+  return RG_OK;
+}
+
+// rg_get_update: every section's count kernels first (their totals side by side in d_sum), one
+// synchronisation, every section's gather into one device staging area, one D2H copy, one
+// synchronisation — instead of a count, sync, gather, copy and sync per section
+int rg_get_update(rg_engine* e, uint32_t slot_mask, uint32_t flags, rg_update* out) {
+  if (!e || !out || (flags & ~(RG_UPDATE_ALL | RG_UPDATE_FULL_STATE))) return fail(RG_EINVAL, "rg_get_update args");
+  if (int jrc = join(e)) return jrc;
+  *out = rg_update{};
+  out->tick = e->t;
+  out->slot_mask = slot_mask;
+  out->flags = flags;
+  const TickParams t = params(e);
+  uint64_t* sum = (uint64_t*)e->d_sum;  // [0..2] persist, [3..4] committed, [5] snapshots, [6] reads
+  PersistParams pa{};
+  pa.G = t.G; pa.R = t.R; pa.nrep = t.nrep; pa.L = t.L; pa.P = t.P; pa.pl = e->pl;
+  pa.full = ((flags & RG_UPDATE_FULL_STATE) || e->t == 0) ? 1u : 0u;
+  pa.s64 = t.s64_in; pa.s64_prev = t.s64_out; pa.s32 = t.s32_in; pa.persist_lo = e->persist_lo;
+  pa.tr = e->tr; pa.info = e->info; pa.pool = e->pool; pa.pt = e->pt; pa.PTS = e->PTS; pa.zi = e->crc_tab + CRC_ZI_OFF;
+  pa.scnt = e->pscnt; pa.ecnt = e->pecnt; pa.ccnt = e->pccnt; pa.soff = e->psoff; pa.eoff = e->peoff; pa.coff = e->pcoff;
+  pa.bsum = e->absum;
+  ApplyParams aa = apply_params(e, slot_mask);
+  SnapParams sa{};
+  sa.G = t.G; sa.R = t.R; sa.nrep = t.nrep; sa.slot_mask = slot_mask; sa.pl = e->pl;
+  sa.s64 = t.s64_in; sa.snap_ev = e->snap_ev; sa.rdst = e->rdst; sa.tick = e->t;
+  sa.cnt = e->uscnt; sa.off = e->usoff; sa.bsum = e->absum;
+  SnapParams ra = sa;
+  ra.cnt = e->urcnt; ra.off = e->uroff;
+  HIPCHK(hipMemsetAsync(sum, 0, 64, e->stream));
+  if (flags & RG_UPDATE_PERSIST) LAUNCH(launch_persist_count(pa, sum, e->stream), e->stream, "persist count");
+  if (flags & RG_UPDATE_COMMITTED) LAUNCH(launch_apply_count(aa, sum + 3, e->stream), e->stream, "apply count");
+  if (flags & RG_UPDATE_SNAPSHOTS) LAUNCH(launch_snap_count(sa, sum + 5, e->stream), e->stream, "snapshot count");
+  if (flags & RG_UPDATE_READS) LAUNCH(launch_read_count(ra, sum + 6, e->stream), e->stream, "read count");
+  uint64_t tot[8] = {};
+  HIPCHK(hipMemcpyAsync(tot, sum, 64, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  // one staging layout for every section, each 16-B aligned
+  const uint64_t sb = a16(tot[0] * sizeof(rg_persist_state)), eb = a16(tot[1] * sizeof(rg_persist_entry)),
+                 epb = tot[2] * 16, cb = a16(tot[3] * sizeof(rg_apply_entry)), cpb = tot[4] * 16,
+                 snb = a16(tot[5] * sizeof(rg_snapshot_event)), rdb = a16(tot[6] * sizeof(rg_read_ready));
+  const uint64_t o_e = sb, o_ep = o_e + eb, o_c = o_ep + epb, o_cp = o_c + cb, o_s = o_cp + cpb, o_r = o_s + snb,
+                 total = o_r + rdb;
+  if (total == 0) return RG_OK;
+  RGCHK(astage_reserve(e, total));
+  if (total > e->u_hcap) {
+    if (e->u_host) (void)hipHostFree(e->u_host);
+    e->u_host = nullptr;
+    e->u_hcap = 0;
+    const uint64_t nb = std::max<uint64_t>(total * 5 / 4, 1 << 20);
+    if (hipHostMalloc((void**)&e->u_host, nb, 0) != hipSuccess) return fail(RG_ENOMEM, "hipHostMalloc (update)");
+    e->u_hcap = nb;
+  }
+  uint8_t* d = e->astage;
+  if (tot[0]) {
+    pa.out_state = d;
+    pa.out_ent = d + o_e;
+    pa.out_pay = d + o_ep;
+    LAUNCH(launch_persist_gather(pa, e->stream), e->stream, "persist gather");
+  }
+  if (tot[3]) {
+    aa.out_rec = d + o_c;
+    aa.out_pay = d + o_cp;
+    LAUNCH(launch_apply_gather(aa, e->stream), e->stream, "apply gather");
+  }
+  if (tot[5]) {
+    sa.out = d + o_s;
+    LAUNCH(launch_snap_gather(sa, e->stream), e->stream, "snapshot gather");
+  }
+  if (tot[6]) {
+    ra.out = d + o_r;
+    LAUNCH(launch_read_gather(ra, e->stream), e->stream, "read gather");
+  }
+  HIPCHK(hipMemcpyAsync(e->u_host, d, total, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  uint8_t* h = e->u_host;
+  out->states = (const rg_persist_state*)h;
+  out->n_states = tot[0];
+  out->entries = (const rg_persist_entry*)(h + o_e);
+  out->n_entries = tot[1];
+  out->entry_payload = h + o_ep;
+  out->entry_payload_bytes = epb;
+  out->committed = (const rg_apply_entry*)(h + o_c);
+  out->n_committed = tot[3];
+  out->committed_payload = h + o_cp;
+  out->committed_payload_bytes = cpb;
+  out->snapshots = (const rg_snapshot_event*)(h + o_s);
+  out->n_snapshots = tot[5];
+  out->reads = (const rg_read_ready*)(h + o_r);
+  out->n_reads = tot[6];
+  return RG_OK;
+}
+
+int rg_commit_update(rg_engine* e, const rg_update* u, uint32_t flags) {
+  if (!e || !u || (flags & ~RG_COMMIT_APPLIED)) return fail(RG_EINVAL, "rg_commit_update args");
+  if (u->tick != e->t) return fail(RG_EINVAL, "rg_commit_update: the update is not of the last tick");
+  if (flags & RG_COMMIT_APPLIED) {
+    if (int jrc = join(e)) return jrc;
+    LAUNCH(launch_applied_all(admin(e), u->slot_mask, e->stream), e->stream, "applied all");
+  }
   return RG_OK;
 }
 

@@ -43,10 +43,16 @@ template <int R>
 __global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_MINWAVES) control_kernel(const TickParams* __restrict__ pp,
                                                                                uint32_t* perr) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-  // volatile: these loads must not be merged with the field loads of the step (that kept every
-  // field of the block live across the whole step)
-  const volatile uint64_t* w = reinterpret_cast<const volatile uint64_t*>(pp);
+  // The block is read through the constant address space: scalar loads, a handful of 64-B
+  // s_load_dwordx16 for the checksum (r03: a volatile flat-load loop here cost 53 dependent,
+  // cache-bypassing round trips per wave). The empty asm launders the pointer so these loads stay
+  // separate from the step's field reads (which would otherwise keep the whole block live).
+  const TickParams* pc = pp;
+  asm volatile("" : "+s"(pc));
+  typedef RG_CONST(const uint64_t) cu64;
+  cu64* w = (cu64*)pc;  // a C cast: the address-space conversion
   uint64_t h = 0;
+#pragma unroll
   for (uint32_t i = 0; i < TP_WORDS; ++i) h = tp_mix(h ^ w[i]);
   if (h != w[TP_WORDS]) {
     if (q == 0) {
@@ -56,19 +62,24 @@ __global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_MINWAVES) control_kernel(
     }
     return;
   }
-  if (q >= pp->nrep) return;
+  CTickParams& cp = *(CTickParams*)pp;
+  if (q >= cp.nrep) return;
 #ifdef RG_CTL_PROFILE
   const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memtime();
-  Ctl<R> c(*pp, q);
+  Ctl<R> c(cp, q);
   c.stamps[0] = t0;
 #else
-  Ctl<R> c(*pp, q);
+  Ctl<R> c(cp, q);
 #endif
   c.run();
 }
 
 hipError_t launch_control(const TickParams* p, uint32_t* perr, uint32_t R, uint32_t nrep, hipStream_t s) {
   dim3 grid((nrep + RG_CTL_BLOCK - 1) / RG_CTL_BLOCK), block(RG_CTL_BLOCK);
+#ifdef RG_DEV_NO_CONTROL  // development builds of the other kernels only (ISA / resource checks)
+  (void)grid; (void)block; (void)p; (void)perr; (void)R; (void)s;
+  return hipErrorInvalidValue;
+#endif
   switch (R) {
     case 1: hipLaunchKernelGGL(control_kernel<1>, grid, block, 0, s, p, perr); break;
     case 2: hipLaunchKernelGGL(control_kernel<2>, grid, block, 0, s, p, perr); break;
@@ -288,8 +299,6 @@ __device__ __forceinline__ bool next_job(const BulkParams& p, Cursor& cur, TileJ
   return true;
 }
 
-enum : uint32_t { F_ACT = 1, F_WRITER = 2, F_CHECK = 8 };
-
 // the entry info word {slot crc, stream position} (and the sender-CRC check) of job entry e
 __device__ __forceinline__ void put_info(const BulkParams& p, uint32_t q, uint64_t first, uint64_t dm, uint32_t e,
                                          uint32_t crc, uint32_t pos, bool check, uint32_t want) {
@@ -421,13 +430,15 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p, const uint32_t*
   cur.uni = true;
   cur.live = next_job<LG, WIRE>(p, cur, tj, stride, ntiles);
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  // ring slot u: payload chunk, destination pool chunk, flags, sender's slot CRC
+  // ring slot u: payload chunk, destination pool chunk, sender's slot CRC (per lane); the entries
+  // each slot's step holds are wave-uniform: 8 bits per slot in one scalar (ikv / ckv), so the
+  // per-lane flags need no registers of their own (r03: 99 -> 95 VGPRs, occupancy 4 -> 5)
   u32x4 x[BULK_U];
-  uint32_t ds[BULK_U], fl[BULK_U], want[BULK_U];
+  uint32_t ds[BULK_U], want[BULK_U];
 #pragma unroll
   for (int u = 0; u < BULK_U; ++u) {
     x[u] = u32x4{0, 0, 0, 0};
-    ds[u] = fl[u] = want[u] = 0;
+    ds[u] = want[u] = 0;
   }
   // Every slot issues exactly two loads per pass (payload chunk + sender CRC word), redirected to a
   // dummy address when the slot has no work, so the number of memory operations between a load
@@ -436,18 +447,23 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p, const uint32_t*
   // all belong to the job `pj` the previous pass issued.
   const uint8_t* dummy = reinterpret_cast<const uint8_t*>(p.crc_tab + CRC_ZERO_OFF);  // 16 zero bytes
   uint32_t vmask = 0;
-  uint32_t iq = 0, ib = 0, ie0 = 0, idp = 0, incu = 0;  // the job of the pass being issued (for its consume)
+  uint32_t iq = 0, ib = 0, ie0 = 0, idp = 0, incu = 0, ikv = 0;  // the job of the pass being issued (for its consume)
+  bool ichk = false;
   uint64_t ifirst = 0, idm = 0;
   do {
-    const uint32_t cq = iq, cb = ib, ce0 = ie0, cdp = idp, cncu = incu;
+    const uint32_t cq = iq, cb = ib, ce0 = ie0, cdp = idp, cncu = incu, ckv = ikv;
+    const bool cchk = ichk;
     const uint64_t cfirst = ifirst, cdm = idm;
     iq = cur.q; ib = cur.b; ie0 = cur.e0; idp = cur.dpos; incu = cur.ncu; ifirst = cur.first; idm = cur.dm;
+    ichk = cur.kind == SRC_RING || (WIRE && cur.kind == SRC_WIRE);  // followers verify the sender's CRC
+    ikv = 0;
 #pragma unroll
     for (int u = 0; u < BULK_U; ++u) {
       {  // consume slot u: store, CRC, info, verify (fl = 0 for an empty slot: no stores). A stream's
         // Cmd is followed by zeros up to its chunk boundary (every writer copies whole chunks), and
         // lanes past a Cmd's chunks contribute nothing, so the CRC is the slot CRC.
-        const bool act = fl[u] & F_ACT;
+        const bool valid = ei < ((ckv >> (8 * u)) & 0xFFu);
+        const bool act = valid && c < cncu;
         if (act) {
 #ifdef RG_BULK_PLAIN_STORE
           *reinterpret_cast<u32x4*>(p.pool + (uint64_t)ds[u] * 16) = x[u];
@@ -460,10 +476,9 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p, const uint32_t*
         v = crc.raw16(make_uint4(x[u].x, x[u].y, x[u].z, x[u].w));
 #endif
         if constexpr (LG > 0) v = xor_lanes<LG>(crc.shift(v));  // raw(slot) = XOR_c Z^(after c)(raw c)
-        if (fl[u] & F_WRITER) {
+        if (valid && c == 0) {
           const uint32_t e = cb + u * EPI + ei;
-          put_info(p, cq, cfirst, cdm, e, act ? (p.crc_const ^ v) : 0u, cdp + (e - ce0) * cncu,
-                   (fl[u] & F_CHECK) != 0, want[u]);
+          put_info(p, cq, cfirst, cdm, e, act ? (p.crc_const ^ v) : 0u, cdp + (e - ce0) * cncu, cchk && act, want[u]);
         }
       }
       {  // issue the job's next step (or an empty step) into slot u
@@ -490,8 +505,7 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p, const uint32_t*
         }
         const uint32_t pid = vpn_of(dl) == dv ? pd0 : pd1;
         ds[u] = pid * PAGE_CH + (dl & (PAGE_CH - 1));
-        fl[u] = (act ? F_ACT : 0u) | ((valid && c == 0) ? F_WRITER : 0u) |
-                (((ring || (WIRE && cur.kind == SRC_WIRE)) && act) ? F_CHECK : 0u);
+        ikv |= (step ? min(EPI, cur.n - cur.b) : 0u) << (8 * u);
         const uint64_t slot = (cur.first + e) & (L - 1);
         const uint64_t si = (((cur.sm >> e) & 1ull) * n64 + cur.src) * L + slot;
         const uint32_t sl = s0 + ei * cur.ncu + c;
@@ -534,6 +548,10 @@ int bulk_lds_bytes(uint32_t P) {
 
 template <bool W, class F>
 static hipError_t with_bulk_w(uint32_t P, F f) {
+#ifdef RG_DEV_ONLY_LG  // development builds: one payload size only (ISA / resource checks)
+  if (W || lg_of(P) != RG_DEV_ONLY_LG) return hipErrorInvalidValue;
+  return f(bulk_kernel<RG_DEV_ONLY_LG, false>);
+#endif
   switch (lg_of(P)) {
     case 0: return f(bulk_kernel<0, W>);
     case 1: return f(bulk_kernel<1, W>);

@@ -142,6 +142,19 @@ class Transport(C.Structure):
     _fields_ = [("user", C.c_void_p), ("allgather_u64", _ALLGATHER), ("alltoallv", _ALLTOALLV)]
 
 
+class Update(C.Structure):
+    """rg_update (include/raftgpu.h): rg_get_update's sections, pointers into engine-owned pinned memory."""
+    _fields_ = [("tick", C.c_uint64), ("states", C.c_void_p), ("n_states", C.c_uint64), ("entries", C.c_void_p),
+                ("n_entries", C.c_uint64), ("entry_payload", C.c_void_p), ("entry_payload_bytes", C.c_uint64),
+                ("committed", C.c_void_p), ("n_committed", C.c_uint64), ("committed_payload", C.c_void_p),
+                ("committed_payload_bytes", C.c_uint64), ("snapshots", C.c_void_p), ("n_snapshots", C.c_uint64),
+                ("reads", C.c_void_p), ("n_reads", C.c_uint64), ("slot_mask", C.c_uint32), ("flags", C.c_uint32)]
+
+
+UPDATE_PERSIST, UPDATE_COMMITTED, UPDATE_SNAPSHOTS, UPDATE_READS, UPDATE_ALL, UPDATE_FULL_STATE = 1, 2, 4, 8, 15, 16
+COMMIT_APPLIED = 1
+
+
 class TickInput(C.Structure):
     _fields_ = [("prop_target", C.c_void_p), ("prop_count", C.c_void_p), ("campaign", C.c_void_p),
                 ("isolate", C.c_void_p), ("flags", C.c_uint32), ("_pad", C.c_uint32)]
@@ -169,7 +182,7 @@ EXPORTS = ["rg_create", "rg_destroy", "rg_bootstrap", "rg_fill_slabs", "rg_tick"
            "rg_apply_committed", "rg_probe_copy", "rg_persist_collect", "rg_snapshot_events", "rg_propose",
            "rg_notify_applied", "rg_apply_async", "rg_apply_wait", "rg_read_index", "rg_read_index_results",
            "rg_config_change", "rg_wire_exchange", "rg_rccl_unique_id", "rg_rccl_open", "rg_rccl_close",
-           "rg_pool_stats"]
+           "rg_pool_stats", "rg_get_update", "rg_commit_update"]
 
 _lib = None
 
@@ -233,6 +246,8 @@ def load_library(path: str = LIB_PATH):
         "rg_global_id": ([vp, u32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)], i32),
         "rg_apply_committed": ([vp, u32, vp, vp, u64, C.POINTER(C.c_uint64), u64, C.POINTER(C.c_uint64)], i32),
         "rg_pool_stats": ([vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_int)], i32),
+        "rg_get_update": ([vp, u32, u32, C.POINTER(Update)], i32),
+        "rg_commit_update": ([vp, C.POINTER(Update), u32], i32),
         "rg_probe_copy": ([C.c_int32, u64, C.c_int32, C.POINTER(C.c_double)], i32),
         "rg_snapshot_events": ([vp, u32, vp, u64, C.POINTER(C.c_uint64)], i32),
         "rg_persist_collect": ([vp, i32, vp, u64, C.POINTER(C.c_uint64), vp, vp, u64, C.POINTER(C.c_uint64), u64,
@@ -575,6 +590,30 @@ class Engine:
                                               packed.size, C.byref(pb)))
         en = en[:ne.value]
         return st[:ns.value], en, unpack_rows(en, packed[:pb.value], self.row)
+
+    def get_update(self, slot_mask: int = 0xFF, flags: int = UPDATE_ALL):
+        """rg_get_update: the last tick's whole hand-off in one call. Returns (raw rg_update, dict of
+        numpy copies: states, entries, entry_payload, committed, committed_payload, snapshots, reads)."""
+        u = Update()
+        self._check(self.L.rg_get_update(self.h, slot_mask, flags, C.byref(u)))
+
+        def arr(ptr, n, dt):
+            if not n:
+                return np.zeros(0, dt)
+            return np.frombuffer((C.c_uint8 * (n * dt.itemsize)).from_address(ptr), dtype=dt).copy()
+
+        out = {"states": arr(u.states, u.n_states, PERSIST_STATE_DTYPE),
+               "entries": arr(u.entries, u.n_entries, PERSIST_ENTRY_DTYPE),
+               "entry_payload": arr(u.entry_payload, u.entry_payload_bytes, np.dtype(np.uint8)),
+               "committed": arr(u.committed, u.n_committed, APPLY_DTYPE),
+               "committed_payload": arr(u.committed_payload, u.committed_payload_bytes, np.dtype(np.uint8)),
+               "snapshots": arr(u.snapshots, u.n_snapshots, SNAPSHOT_EVENT_DTYPE),
+               "reads": arr(u.reads, u.n_reads, READ_READY_DTYPE)}
+        return u, out
+
+    def commit_update(self, u, applied: bool = True):
+        """rg_commit_update (Peer.Commit); applied: the slot mask's replicas report applied = processed."""
+        self._check(self.L.rg_commit_update(self.h, C.byref(u), COMMIT_APPLIED if applied else 0))
 
     def pool_stats(self) -> dict:
         """rg_pool_stats: {'total': pages, 'free': pages, 'failed': bool} of the payload page pool."""

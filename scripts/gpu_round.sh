@@ -16,7 +16,9 @@ for what in ${STEPS:-smoke parity tests bench wire rehearse}; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     parity) TAILN=3 step gpu_parity 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 240 --timeout-method thread -p no:cacheprovider ;;
     tests) TAILN=6 step gpu_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -p no:cacheprovider ;;
-    bench) step bench 400 python bench.py ${BENCH_ARGS:---cpu-seconds 10} ;;
+    bench) step bench 400 python bench.py ${BENCH_ARGS:---cpu-seconds 10 --ingest} ;;
+    profile) step profile 1000 bash scripts/profile.sh ${PTAG:-r03} ;;
+    shapes) step shapes 600 bash scripts/shapes.sh ;;
     wire) step bench_wire 400 python bench.py --wire-all --no-cpu-baseline ;;
     rehearse) step rehearse 400 env RAFTD_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                 --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --backend gloo --groups 8192 \

@@ -1,5 +1,7 @@
 """Summarise rocprofv3 CSV output (kernel trace + separate FETCH_SIZE / WRITE_SIZE PMC passes)
-into profiles/<tag>_pmc_summary.json and profiles/<tag>_kernel_stats.csv.
+into profiles/<tag>_pmc_summary.json, profiles/<tag>_kernel_stats.csv (rocprofv3 --stats: every
+dispatch of the run, warm-up and copy-back runs included) and profiles/<tag>_kernel_stats_timed.csv
+(the same statistics over the timed window only: the last_n tick launches before the skipped tail).
 
 HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE (KB) reads exactly half of a
 wide coalesced stream on gfx950, so hbm = (2*FETCH_SIZE + WRITE_SIZE) * 1024; the bulk kernel's
@@ -27,13 +29,13 @@ def short(name):
     for k in ("control_kernel", "bulk_kernel", "bulk_meta_kernel", "tick_kernel", "bootstrap_kernel",
               "fill_slabs_kernel", "sum_committed_kernel", "traffic_kernel", "unpack_kernel", "pack_kernel",
               "plan_kernel", "scan_reduce_kernel", "scan_blocks_kernel", "scan_apply_kernel", "bounds_kernel",
-              "apply_count_kernel", "apply_gather_kernel", "apply_total_kernel"):
+              "apply_count_kernel", "apply_gather_kernel", "apply_total_kernel", "pool_kernel"):
         if k in name:
             return k
     return name[:60]
 
 
-TICK_KERNELS = ("control_kernel", "bulk_kernel")
+TICK_KERNELS = ("control_kernel", "bulk_kernel", "pool_kernel")
 
 
 def window(k, xs, last_n, skip):
@@ -67,6 +69,13 @@ def main():
     for r in trace:
         k = short(r.get("Kernel_Name", ""))
         dur.setdefault(k, []).append((int(r.get("Dispatch_Id", 0)), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+    with open(os.path.join(prof, f"{tag}_kernel_stats_timed.csv"), "w") as f:
+        f.write("Name,Calls,AverageNs,MinNs,MaxNs,Window\n")
+        for k in sorted(dur):
+            d = window(k, [v for _, v in sorted(dur[k])], last_n, skip)
+            if d:
+                f.write(f"{k},{len(d)},{sum(d) / len(d):.1f},{min(d)},{max(d)},"
+                        f"{'timed tick launches' if k in TICK_KERNELS else 'last dispatches'}\n")
     fetch = pmc(fdir, "FETCH_SIZE", last_n, skip)
     write = pmc(wdir, "WRITE_SIZE", last_n, skip)
     out = {"note": __doc__.strip().splitlines()[0], "last_n_dispatches": last_n, "skipped_tail": skip,

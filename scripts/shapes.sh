@@ -1,6 +1,7 @@
 #!/bin/bash
 # bench.py at the other BASELINE.json shapes on one GPU (steady-state leaders; not the headline
-# line): C2 4,096 x 3 (and P = 0), 64K x 3 P = 0, C3's 64K x 5 co-located, C5's 1M x 3 at P = 16.
+# line): C2 4,096 x 3 (and P = 0), 64K x 3 P = 0, C3's 64K x 5 co-located (L 1,024: at L 2,048 its live Cmds exceed the 64-GiB page pool of one engine),
+# C5's 1M x 3 at P = 256, L = 2,048 (the paged store, r03).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -18,4 +19,4 @@ run c2 --groups 4096 --steps 100 --warmup 10
 run c2p0 --groups 4096 --payload 0 --steps 100 --warmup 10
 run m64p0 --payload 0 --steps 50 --warmup 10
 run c3shape --replicas 5 --steps 20 --warmup 5 --log-capacity 1024
-run c5shape --groups 1048576 --payload 16 --log-capacity 1024 --steps 10 --warmup 3
+run c5shape --groups 1048576 --entries 1 --steps 10 --warmup 3  # mean 1 entry per group per tick

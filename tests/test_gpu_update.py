@@ -1,0 +1,94 @@
+"""rg_get_update / rg_commit_update (dragonboat Peer.GetUpdate / Peer.Commit): the one
+hand-off per tick must carry exactly what the four separate calls return — the persistence feed
+(rg_persist_collect), the committed entries for Update (rg_apply_committed), the snapshot events
+(rg_snapshot_events) and the reads made ready (rg_read_index_results) — and rg_commit_update's
+applied report must move the engine exactly as rg_notify_applied does.
+
+Two identical engines run the same chaos trace (caller Cmds of 0..300 bytes, elections, message
+loss, an isolated replica that falls behind compaction and is restored by InstallSnapshot, ReadIndex
+requests, apply feedback on); engine A uses the separate calls, engine B rg_get_update."""
+import numpy as np
+import pytest
+
+from engines import make
+from raftd_amd.engine import unpack_rows
+
+pytestmark = pytest.mark.gpu
+
+
+def test_get_update_equals_the_separate_calls():
+    G, R, MASK = 12, 3, 0b011
+    cfg = dict(groups=G, replicas=R, log_capacity=256, payload_bytes=64, max_cmd_bytes=300, max_entries_per_msg=8,
+               snapshot_entries=24, compaction_overhead=3, drop_ppm=30000, apply_feedback=1, seed=0xB0B)
+    a, b = make("gpu", **cfg), make("gpu", **cfg)
+    for e in (a, b):
+        e.bootstrap()
+    rng = np.random.default_rng(11)
+    camp = np.zeros(G * R, np.uint8)
+    camp[0::R] = 1
+    seen = {"committed": 0, "snapshots": 0, "restored": 0, "reads": 0, "states": 0}
+    for t in range(90):
+        iso = np.zeros(G * R, np.uint8)
+        if 20 <= t < 60:
+            iso[1 * R + 2] = 1  # group 1's slot 2 misses compaction, then gets InstallSnapshot
+        batches = []
+        if t >= 4:
+            for g in range(G):
+                if rng.random() < 0.7:
+                    n = int(rng.integers(1, 6))
+                    cmds = [bytes(rng.integers(0, 256, int(rng.integers(0, 301)), dtype=np.uint8)) for _ in range(n)]
+                    batches.append((g, int(rng.integers(0, R)), cmds))
+        reads = [(g, int(rng.integers(0, R)), int(rng.integers(1, 1 << 40))) for g in range(G) if rng.random() < 0.3]
+        for e in (a, b):
+            if batches:
+                e.propose(batches)
+            if t >= 4 and reads:
+                e.read_index(reads)
+            e.tick(campaign=camp if t == 1 else None, isolate=iso)
+        st, en, rows = a.persist_collect()
+        recs, arows = a.apply_committed(MASK)
+        ev = a.snapshot_events(MASK)
+        rd = a.read_index_results(MASK)
+        u, out = b.get_update(MASK)
+        assert u.tick == b.t
+        assert out["states"].tobytes() == st.tobytes(), t
+        assert out["entries"].tobytes() == en.tobytes(), t
+        assert np.array_equal(unpack_rows(out["entries"], out["entry_payload"], b.row), rows), t
+        assert out["committed"].tobytes() == recs.tobytes(), t
+        assert np.array_equal(unpack_rows(out["committed"], out["committed_payload"], b.row), arows), t
+        assert out["snapshots"].tobytes() == ev.tobytes(), t
+        assert out["reads"].tobytes() == rd.tobytes(), t
+        # Peer.Commit: the node's replicas applied what they were handed
+        va = a.replica_array()
+        rids = np.array([r for r in range(G * R) if (MASK >> (r % R)) & 1], np.uint32)
+        a.notify_applied(rids, va["processed"][rids])
+        b.commit_update(u, applied=True)
+        assert a.replica_array().tobytes() == b.replica_array().tobytes(), t
+        seen["committed"] += len(recs)
+        seen["snapshots"] += int((ev["kind"] & 1).sum()) if len(ev) else 0
+        seen["restored"] += int((ev["kind"] & 2).sum() != 0) if len(ev) else 0
+        seen["reads"] += len(rd)
+        seen["states"] += len(st)
+    # the trace exercised every section
+    assert all(v > 0 for v in seen.values()), seen
+
+
+def test_get_update_sections_and_full_state():
+    """flags select sections; RG_UPDATE_FULL_STATE = rg_persist_collect(full=1)."""
+    from raftd_amd.engine import UPDATE_COMMITTED, UPDATE_FULL_STATE, UPDATE_PERSIST
+    G, R = 8, 3
+    e = make("gpu", groups=G, replicas=R, log_capacity=128, payload_bytes=32, max_entries_per_msg=8, seed=5)
+    e.bootstrap()
+    camp = np.zeros(G * R, np.uint8)
+    camp[0::R] = 1
+    for t in range(8):
+        e.tick(np.zeros(G, np.uint8) if t >= 4 else None, np.full(G, 3, np.uint32) if t >= 4 else None,
+               campaign=camp if t == 1 else None)
+    _, only_c = e.get_update(0xFF, UPDATE_COMMITTED)
+    assert len(only_c["committed"]) > 0 and len(only_c["states"]) == 0 and len(only_c["reads"]) == 0
+    _, full = e.get_update(0xFF, UPDATE_PERSIST | UPDATE_FULL_STATE)
+    st, en, rows = e.persist_collect(full=True)
+    assert full["states"].tobytes() == st.tobytes() and len(st) == G * R
+    assert full["entries"].tobytes() == en.tobytes()
+    assert np.array_equal(unpack_rows(full["entries"], full["entry_payload"], e.row), rows)
+    assert len(full["committed"]) == 0
