@@ -287,6 +287,24 @@ def ingest(eng, G, E, P, steps, seed=7):
                     "proposals; host wall time"}
 
 
+def graph_ticks(eng, pt, pc, G, k=10, reps=4):
+    """The multi-tick path (rg_tick_device_n, RG_TICKN_GRAPH): the same steady-state ticks, k per
+    captured HIP graph, one hipGraphLaunch per k ticks; host wall time per tick."""
+    import torch
+    eng.tick_device_n(k, pt.data_ptr(), pc.data_ptr())  # capture + first replay
+    eng.sync()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        eng.tick_device_n(k, pt.data_ptr(), pc.data_ptr())
+    eng.sync()
+    el = time.perf_counter() - t0
+    return {"value": G * k * reps / el, "unit": "group-steps/s", "ticks": k * reps, "ticks_per_graph": k,
+            "ms_per_step": el * 1e3 / (k * reps),
+            "note": "rg_tick_device_n(k, RG_TICKN_GRAPH): k ticks per hipGraphLaunch, parameter blocks written "
+                    "into the graph's pinned slots before each launch; host wall time"}
+
+
 def pmc_traffic(kernel="bulk_kernel", wire=False, spread=False):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of the
     same bench mode (profiles/r*_pmc_summary.json; *_wire_* = the --wire-all runs, *_spread_* =
@@ -416,6 +434,7 @@ def main():
         wire.drain()
     kms["control"] = host.kernel_ms()["control"]
     host.timing(False)
+    graph = graph_ticks(eng, pt, pc, G) if not spread and not args.wire_all else None
     x_ms = sum(a.elapsed_time(b) for a, b in xev) / args.steps if wire and not pipelined else 0.0
     va = eng.replica_array()  # every replica of this rank's first engine: invariant bits and drops
     errs, drops = int((va["err"] != 0).sum()), int(va["drops"].sum())
@@ -539,6 +558,7 @@ def main():
         "device_bytes": host.device_bytes,
         "apply_copyback": apply,
         "e2e_with_apply": e2e,
+        "graph": graph,
     }
     if ing:
         out["ingest"] = ing

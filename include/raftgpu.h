@@ -276,6 +276,16 @@ int rg_propose(rg_engine* e, const rg_proposal* props, size_t n, const uint8_t* 
 int rg_tick(rg_engine* e, const rg_tick_input* in);
 /* Same, with the input arrays already resident in device memory (no copies). */
 int rg_tick_device(rg_engine* e, const rg_tick_input* in);
+/* k ticks with the same device-resident inputs (the steady-state pattern of a batch driver): without
+ * flags, k rg_tick_device calls; with RG_TICKN_GRAPH, one captured HIP graph of the k ticks, replayed
+ * with one launch (the parameter blocks are written into the graph's pinned slots before each
+ * replay, so results equal k rg_tick_device calls bit for bit). The graph needs a one-rank engine
+ * (ranks 1, wire_all 0), nothing staged by rg_propose / rg_read_index / rg_config_change, timing off,
+ * and k a multiple of lcm(2, num_slabs), at most 64 (slabs rg_propose wrote get the generator's Cmds
+ * back first, as a tick-input batch would; the last tick's slab must not be one); it is captured
+ * on first use and again whenever k, the inputs, the stream or the parity of the tick count change. */
+#define RG_TICKN_GRAPH 1u
+int rg_tick_device_n(rg_engine* e, const rg_tick_input* in, uint32_t k, uint32_t flags);
 /* Launch work on this HIP stream (hipStream_t) instead of the engine's own. */
 int rg_set_stream(rg_engine* e, void* stream);
 /* Make the engine's stream wait, on the device, for every launched tick to finish (a tick's

@@ -1077,10 +1077,24 @@ struct Ctl {
   uint32_t stamps[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 
   RG_FN void run() {
+    // The step's inputs that no step logic feeds — the inbox counts of every sender and the tick
+    // inputs — are loaded together up front: the lane then waits one memory latency for all of them
+    // instead of one per use (at C2 a wave per SIMD, so nothing hides these waits)
+    uint32_t cnt_pf[R];
+    sfor<0, R>([&](auto jc) {
+      constexpr int src = decltype(jc)::value;
+      cnt_pf[src] = (uint32_t)src == s ? 0u
+                    : (pl_remote(p.pl, src, s, g) ? p.rcnt : p.cnt_in)[((uint64_t)src * R + s) * p.G + g];
+    });
+    const uint32_t in_pt = p.prop_target ? p.prop_target[gi] : 0xFFu;
+    const uint32_t in_pc = p.prop_target ? p.prop_count[gi] : 0u;
+    const bool in_camp = p.campaign && p.campaign[ri()];
+    const uint32_t in_cc = p.cc_in ? p.cc_in[gi] : 0u;
+    const uint64_t in_rd = p.read_ctx ? p.read_ctx[ri()] : 0ull;
     for (uint32_t src = 0; src < R; ++src) {
       if (src == s) continue;
       const bool remote = pl_remote(p.pl, src, s, g);
-      uint32_t cnt = (remote ? p.rcnt : p.cnt_in)[((uint64_t)src * R + s) * p.G + g];
+      uint32_t cnt = sel_get<R>(cnt_pf, src);
       if (cnt > p.K) {  // never produced by a sender (unpack_kernel clamps received counts): ERR_WIRE
         RG_OOB("RG_BOUNDS control q=%u src=%u remote=%d cnt=%u > K=%u\n", q, src, (int)remote, cnt, p.K);
         err |= ERR_WIRE;
@@ -1089,11 +1103,11 @@ struct Ctl {
       for (uint32_t k = 0; k < cnt; ++k) handle(src, k, remote);
     }
     RG_STAMP(1);
-    if (p.campaign && p.campaign[ri()]) handle_node_election();
+    if (in_camp) handle_node_election();
     if (!(p.flags & 1u)) tick();
     RG_STAMP(2);
-    if (p.prop_target && p.prop_target[gi] == s) {
-      const uint32_t n = p.prop_count[gi];
+    if (in_pt == s) {
+      const uint32_t n = in_pc;
       if (n > p.E) {  // rg_tick_device's contract: batches of at most E entries (the host path checks)
         drops++;
       } else if (n > 0) {
@@ -1110,14 +1124,11 @@ struct Ctl {
         handle_propose(n, sl, 0, hm, s, li, nullptr, 0, 0, cinfo);
       }
     }
-    if (p.cc_in) {  // 4a: membership change input (rg_config_change)
-      const uint32_t v = p.cc_in[gi];
+    {  // 4a: membership change input (rg_config_change)
+      const uint32_t v = in_cc;
       if (v && (v & 0xFFu) == s) handle_propose(1, (uint32_t)(p.tick % p.nslab), 0, 0, s, nullptr, nullptr, 0, v >> 8, 0);
     }
-    if (p.read_ctx) {  // 4b: ReadIndex input (rg_read_index)
-      const uint64_t ctx = p.read_ctx[ri()];
-      if (ctx) handle_read_index(my_id(), ctx);
-    }
+    if (in_rd) handle_read_index(my_id(), in_rd);  // 4b: ReadIndex input (rg_read_index)
     RG_STAMP(3);
     // GetUpdate.CommittedEntries = (processed, committed], then commitUpdate; applied follows unless
     // the state machine reports it (rg_notify_applied); snapshot + compaction on applied

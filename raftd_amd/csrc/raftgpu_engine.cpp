@@ -204,7 +204,20 @@ struct rg_engine {
   uint64_t *usoff = nullptr, *uroff = nullptr;
   uint8_t* u_host = nullptr;
   uint64_t u_hcap = 0;
+  // rg_tick_device_n's HIP graphs ("Multi-tick path"): two captured graphs of g_k ticks,
+  // each over its own set of parameter slots, used alternately so the host refills one set while
+  // the other graph may still be reading its slots; g_ev[i] follows the last launch of graph i
+  hipGraph_t gg[2] = {nullptr, nullptr};
+  hipGraphExec_t gx[2] = {nullptr, nullptr};
+  hipEvent_t g_ev[2] = {nullptr, nullptr};
+  bool g_used[2] = {false, false}, g_valid = false;
+  uint32_t g_k = 0, g_par = 0, g_flip = 0;
+  rg_tick_input g_in{};
+  hipStream_t g_stream = nullptr;
+  TickParams* g_dtp = nullptr;  // [2][G_MAXK] device slots
+  TickParams* g_htp = nullptr;  // [2][G_MAXK] pinned host slots
 };
+constexpr uint32_t G_MAXK = 64;
 
 static int stage_reset(rg_engine* e);
 
@@ -301,7 +314,9 @@ static uint64_t a16(uint64_t x) { return (x + 15) & ~15ull; }
 
 // The parameter block of the tick that runs next (tick e->t): reads parity t&1 state and the
 // outbox written by tick t-1, writes the other parity.
-static TickParams params(rg_engine* e) {
+static TickParams params_at(rg_engine* e, uint64_t t);
+static TickParams params(rg_engine* e) { return params_at(e, e->t); }
+static TickParams params_at(rg_engine* e, uint64_t tk) {
   TickParams p{};
   const rg_config& c = e->c;
   p.G = c.groups; p.R = c.replicas; p.nrep = e->nrep; p.L = c.log_capacity; p.P = c.payload_bytes;
@@ -314,9 +329,9 @@ static TickParams params(rg_engine* e) {
   p.JS = c.join_slots;
   p.IM = c.initial_members;
   p.seed = c.seed;
-  p.tick = e->t;
+  p.tick = tk;
   p.pl = e->pl;
-  const int a = (int)(e->t & 1), b = a ^ 1;
+  const int a = (int)(tk & 1), b = a ^ 1;
   p.s64_in = e->s64[a]; p.s64_out = e->s64[b];
   p.s32_in = e->s32[a]; p.s32_out = e->s32[b];
   p.rem_in = e->rem[a]; p.rem_out = e->rem[b];
@@ -354,8 +369,10 @@ static WireParams wire_params(rg_engine* e) {
   return w;
 }
 
-static BulkParams bulk_params(rg_engine* e) {  // for tick e->t
-  const int a = (int)(e->t & 1);
+static BulkParams bulk_params_at(rg_engine* e, uint64_t tk);
+static BulkParams bulk_params(rg_engine* e) { return bulk_params_at(e, e->t); }
+static BulkParams bulk_params_at(rg_engine* e, uint64_t tk) {
+  const int a = (int)(tk & 1);
   BulkParams b{};
   b.G = e->c.groups; b.R = e->c.replicas; b.nrep = e->nrep; b.L = e->c.log_capacity; b.P = e->c.payload_bytes;
   b.E = e->c.max_entries_per_msg; b.J = e->J; b.crc_const = e->crc_const; b.tile = e->bulk_tile;
@@ -644,6 +661,15 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
 
 void rg_destroy(rg_engine* e) {
   if (!e) return;
+  for (int i = 0; i < 2; ++i) {
+    if (e->gx[i]) (void)hipGraphExecDestroy(e->gx[i]);
+    if (e->gg[i]) (void)hipGraphDestroy(e->gg[i]);
+    if (e->g_ev[i]) {
+      (void)hipEventSynchronize(e->g_ev[i]);
+      (void)hipEventDestroy(e->g_ev[i]);
+    }
+  }
+  if (e->g_htp) (void)hipHostFree(e->g_htp);
   if (e->own) {
     (void)hipStreamSynchronize(e->own);
     (void)hipStreamDestroy(e->own);
@@ -847,6 +873,7 @@ static int cmd_reserve(rg_engine* e, uint64_t need_bytes) {
     e->bytes -= e->cmd_cap * ns;
   }
   e->cmds = nb;
+  e->g_valid = false;  // captured bulk launches name the old arena
   e->cmd_cap = cap;
   return RG_OK;
 }
@@ -1083,16 +1110,19 @@ int rg_kernel_ms(rg_engine* e, double* ms, uint64_t* launches) {
 
 // control_kernel(t) reads its parameter block from a device slot written by a copy on the same
 // stream just before the launch, so the launch's own kernel arguments are one pointer
+// the checksum the kernel verifies before it dereferences anything
+static void seal(TickParams& p) {
+  uint64_t w[TP_WORDS], h = 0;
+  memcpy(w, &p, sizeof w);
+  for (uint32_t i = 0; i < TP_WORDS; ++i) h = tp_mix(h ^ w[i]);
+  p.csum = h;
+}
+
 static int launch_control_slot(rg_engine* e, const TickParams& p) {
   const uint32_t k = (uint32_t)(e->tp_next++ % TP_SLOTS), c = k / TP_CHUNK;
   if (k % TP_CHUNK == 0 && e->tp_used[c]) HIPCHK(hipEventSynchronize(e->tp_ev[c]));
   e->h_tp[k] = p;
-  {  // the checksum the kernel verifies before it dereferences anything
-    uint64_t w[TP_WORDS], h = 0;
-    memcpy(w, &e->h_tp[k], sizeof w);
-    for (uint32_t i = 0; i < TP_WORDS; ++i) h = tp_mix(h ^ w[i]);
-    e->h_tp[k].csum = h;
-  }
+  seal(e->h_tp[k]);
   HIPCHK(hipMemcpyAsync(e->d_tp + k, e->h_tp + k, sizeof(TickParams), hipMemcpyHostToDevice, e->stream));
   if (k % TP_CHUNK == TP_CHUNK - 1) {
     HIPCHK(hipEventRecord(e->tp_ev[c], e->stream));
@@ -1120,6 +1150,7 @@ static int tick_impl(rg_engine* e, const rg_tick_input* in, bool device_ptrs) {
   if (in) {
     p.flags = in->flags;
     if (device_ptrs) {
+      if (in->prop_target && !in->prop_count) return fail(RG_EINVAL, "prop_target without prop_count");
       p.prop_target = in->prop_target;
       p.prop_count = in->prop_count;
       p.campaign = in->campaign;
@@ -1221,6 +1252,114 @@ static int tick_impl(rg_engine* e, const rg_tick_input* in, bool device_ptrs) {
 int rg_tick(rg_engine* e, const rg_tick_input* in) {
   if (!e) return fail(RG_EINVAL, "null engine");
   return tick_impl(e, in, false);
+}
+
+// ---- the multi-tick path: k ticks with the same device-resident inputs. With
+// RG_TICKN_GRAPH the k ticks are one captured HIP graph — per tick a parameter-slot copy and the
+// control / pool / bulk launches — replayed with one hipGraphLaunch; the host writes the k parameter
+// blocks into the graph's pinned slots before each launch (the copy nodes read them when they run).
+static int tick_graph(rg_engine* e, const rg_tick_input* in, uint32_t k) {
+  const uint64_t t0 = e->t;
+  const bool same = e->g_valid && e->g_k == k && e->g_par == (uint32_t)(t0 & 1) && e->g_stream == e->stream &&
+                    !memcmp(&e->g_in, in, sizeof *in);
+  if (!same) {
+    HIPCHK(hipStreamSynchronize(e->stream));
+    for (int i = 0; i < 2; ++i) {
+      if (e->gx[i]) (void)hipGraphExecDestroy(e->gx[i]);
+      if (e->gg[i]) (void)hipGraphDestroy(e->gg[i]);
+      e->gx[i] = nullptr;
+      e->gg[i] = nullptr;
+      e->g_used[i] = false;
+    }
+    e->g_valid = false;
+    if (!e->g_dtp) {
+      RGCHK(dalloc(e, &e->g_dtp, 2ull * G_MAXK * sizeof(TickParams)));
+      if (hipHostMalloc((void**)&e->g_htp, 2ull * G_MAXK * sizeof(TickParams), 0) != hipSuccess)
+        return fail(RG_ENOMEM, "hipHostMalloc (graph parameter slots)");
+      for (int i = 0; i < 2; ++i) HIPCHK(hipEventCreateWithFlags(&e->g_ev[i], hipEventDisableTiming));
+    }
+    for (int set = 0; set < 2; ++set) {
+      HIPCHK(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+      for (uint32_t i = 0; i < k; ++i) {
+        TickParams p = params_at(e, t0 + i);
+        p.flags = in->flags;
+        p.prop_target = in->prop_target;
+        p.prop_count = in->prop_count;
+        p.campaign = in->campaign;
+        p.isolate = in->isolate;
+        TickParams* hs = e->g_htp + set * G_MAXK + i;
+        TickParams* ds = e->g_dtp + set * G_MAXK + i;
+        HIPCHK(hipMemcpyAsync(ds, hs, sizeof(TickParams), hipMemcpyHostToDevice, e->stream));
+        HIPCHK(launch_control(ds, &e->poolctl->param_err, p.R, p.nrep, e->stream));
+        if (e->c.payload_bytes) {
+          PoolParams pp{};
+          pp.nrep = e->nrep; pp.PTS = e->PTS; pp.npages = e->npages;
+          pp.s32_out = p.s32_out; pp.s32_in = p.s32_in; pp.pt = e->pt; pp.fring = e->fring; pp.ctl = e->poolctl;
+          pp.jcnt = p.jcnt;
+          HIPCHK(launch_pool(pp, e->stream));
+          HIPCHK(launch_bulk(bulk_params_at(e, t0 + i), e->pt, e->stream, e->bulk_grid));
+        }
+      }
+      hipError_t r = hipStreamEndCapture(e->stream, &e->gg[set]);
+      if (r != hipSuccess) return fail(RG_EHIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(r));
+      HIPCHK(hipGraphInstantiate(&e->gx[set], e->gg[set], nullptr, nullptr, 0));
+    }
+    e->g_k = k;
+    e->g_par = (uint32_t)(t0 & 1);
+    e->g_stream = e->stream;
+    e->g_in = *in;
+    e->g_flip = 0;
+    e->g_valid = true;
+  }
+  const uint32_t set = e->g_flip;
+  if (e->g_used[set]) HIPCHK(hipEventSynchronize(e->g_ev[set]));  // its copy nodes have read the slots
+  for (uint32_t i = 0; i < k; ++i) {
+    TickParams p = params_at(e, t0 + i);
+    p.flags = in->flags;
+    p.prop_target = in->prop_target;
+    p.prop_count = in->prop_count;
+    p.campaign = in->campaign;
+    p.isolate = in->isolate;
+    seal(p);
+    e->g_htp[set * G_MAXK + i] = p;
+  }
+  HIPCHK(hipGraphLaunch(e->gx[set], e->stream));
+  HIPCHK(hipEventRecord(e->g_ev[set], e->stream));
+  e->g_used[set] = true;
+  e->g_flip ^= 1u;
+  e->t += k;
+  HIPCHK(hipEventRecord(e->bulk_done[(e->t - 1) & 1], e->stream));
+  return RG_OK;
+}
+
+int rg_tick_device_n(rg_engine* e, const rg_tick_input* in, uint32_t k, uint32_t flags) {
+  if (!e || !in || k == 0 || (flags & ~RG_TICKN_GRAPH)) return fail(RG_EINVAL, "rg_tick_device_n args");
+  if (in->prop_target && !in->prop_count) return fail(RG_EINVAL, "prop_target without prop_count");
+  if (!(flags & RG_TICKN_GRAPH)) {
+    for (uint32_t i = 0; i < k; ++i) RGCHK(tick_impl(e, in, true));
+    return RG_OK;
+  }
+  const uint32_t ns = e->c.num_slabs, period = ns % 2 ? 2 * ns : ns;
+  if (k > G_MAXK || k % period)
+    return fail(RG_EINVAL, "rg_tick_device_n: a graph runs a multiple of lcm(2, num_slabs) ticks, at most 64");
+  if (e->wire || e->staged || e->rd_staged || e->cc_staged || e->timing)
+    return fail(RG_EINVAL, "rg_tick_device_n: graphs need a one-rank engine with nothing staged and timing off");
+  HIPCHK(hipSetDevice(e->c.device));
+  if (in->prop_target && e->c.payload_bytes) {
+    // tick-input batches carry generator Cmds: regenerate every slab rg_propose wrote, as tick_impl
+    // would when a tick-input batch takes it — except the last tick's, whose forwarded batches the
+    // first graph tick may still read (then one plain tick first)
+    const uint64_t prev = e->t ? (e->t - 1) % ns : ~0ull;
+    for (uint32_t sl = 0; sl < ns; ++sl) {
+      if ((e->slab_synth >> sl) & 1) continue;
+      if (sl == prev) return fail(RG_EINVAL, "rg_tick_device_n: the last tick's slab holds caller Cmds (tick once first)");
+      LAUNCH(launch_fill_slabs(e->slabs, e->slab_info, sl, 1, e->c.groups, e->slab_rows, e->c.max_entries_per_msg,
+                               e->c.payload_bytes, e->c.seed, e->pl, e->stream),
+             e->stream, "fill_slabs");
+      e->slab_synth |= 1ull << sl;
+    }
+  }
+  return tick_graph(e, in, k);
 }
 
 int rg_tick_device(rg_engine* e, const rg_tick_input* in) {

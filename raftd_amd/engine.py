@@ -182,7 +182,7 @@ EXPORTS = ["rg_create", "rg_destroy", "rg_bootstrap", "rg_fill_slabs", "rg_tick"
            "rg_apply_committed", "rg_probe_copy", "rg_persist_collect", "rg_snapshot_events", "rg_propose",
            "rg_notify_applied", "rg_apply_async", "rg_apply_wait", "rg_read_index", "rg_read_index_results",
            "rg_config_change", "rg_wire_exchange", "rg_rccl_unique_id", "rg_rccl_open", "rg_rccl_close",
-           "rg_pool_stats", "rg_get_update", "rg_commit_update"]
+           "rg_pool_stats", "rg_get_update", "rg_commit_update", "rg_tick_device_n"]
 
 _lib = None
 
@@ -213,6 +213,7 @@ def load_library(path: str = LIB_PATH):
         "rg_fill_slabs": ([vp], i32),
         "rg_tick": ([vp, C.POINTER(TickInput)], i32),
         "rg_tick_device": ([vp, C.POINTER(TickInput)], i32),
+        "rg_tick_device_n": ([vp, C.POINTER(TickInput), u32, u32], i32),
         "rg_set_stream": ([vp, vp], i32),
         "rg_sync": ([vp], i32),
         "rg_join": ([vp], i32),
@@ -344,6 +345,14 @@ class Engine:
         ti = TickInput(prop_target_ptr or None, prop_count_ptr or None, campaign_ptr or None,
                        isolate_ptr or None, flags, 0)
         self._check(self.L.rg_tick_device(self.h, C.byref(ti)))
+
+    def tick_device_n(self, k, prop_target_ptr=0, prop_count_ptr=0, campaign_ptr=0, isolate_ptr=0, flags=0,
+                      graph=True):
+        """rg_tick_device_n: k ticks with the same device-resident inputs; graph: one captured HIP graph
+        of the k ticks per call (RG_TICKN_GRAPH)."""
+        ti = TickInput(prop_target_ptr or None, prop_count_ptr or None, campaign_ptr or None,
+                       isolate_ptr or None, flags, 0)
+        self._check(self.L.rg_tick_device_n(self.h, C.byref(ti), k, 1 if graph else 0))
 
     def set_stream(self, stream_handle: int):
         self._check(self.L.rg_set_stream(self.h, C.c_void_p(stream_handle)))
