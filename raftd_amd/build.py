@@ -25,9 +25,23 @@ def _stale(out: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def _digest(deps: list[str]) -> str:
+    """Content hash of the sources a library was built from (a build that raced an edit shows up as
+    a mismatch, which mtimes alone miss)."""
+    import hashlib
+    h = hashlib.sha256()
+    for d in deps:
+        with open(d, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
 def build_engine(force: bool = False, verbose: bool = False) -> str:
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
-    if not force and not _stale(LIB, deps) and os.path.exists(RESOURCES):
+    stamp = LIB + ".sha256"
+    digest = _digest(deps)  # taken before compiling: an edit during the build leaves the stamp stale
+    if (not force and not _stale(LIB, deps) and os.path.exists(RESOURCES) and os.path.exists(stamp)
+            and open(stamp).read().strip() == digest):
         return LIB
     objs, report = [], []
     for src in SOURCES:
@@ -55,6 +69,8 @@ def build_engine(force: bool = False, verbose: bool = False) -> str:
     subprocess.run(cmd, check=True)
     for o in objs:
         os.remove(o)
+    with open(stamp, "w") as f:
+        f.write(digest + "\n")
     return LIB
 
 
