@@ -474,6 +474,13 @@ int rg_config_change(rg_engine* e, uint64_t group, uint32_t slot, uint32_t op, u
  * campaigns (hasConfigChangeToApply: committed > applied) and snapshots (SnapshotEntries applied
  * since the last one). RG_EINVAL (nothing changed) if an index exceeds processed or a rid is bad. */
 int rg_notify_applied(rg_engine* e, const uint32_t* rids, const uint64_t* index, size_t n);
+/* Whole-table digest of this engine's replicas: out[0] = the sum over replicas of an
+ * fmix64 chain over the replica's rg_replica_view fields (remotes of slots < replicas), out[1] = the
+ * sum of a chain over its log entries (marker, last] (term, then type | len << 8 | crc << 32), each
+ * chain seeded by the global replica id. Order-independent, so the digests of several ranks add up to
+ * the cluster's; the oracle's or_digest is the same function — a parity check of every replica and
+ * every log entry at any size, in one pass on the device. */
+int rg_digest(rg_engine* e, uint64_t* out /*[2]*/);
 /* Global group and global replica id (group·replicas + slot) of local replica rid. */
 int rg_global_id(rg_engine* e, uint32_t rid, uint64_t* group, uint64_t* global_rid);
 /* Measurement helper: this device's streaming-copy bandwidth, (read + write bytes) / s, of a

@@ -1502,3 +1502,47 @@ int or_get_applied(const or_engine* e, uint32_t rid, uint64_t* index, or_entry_v
   }
   return (int)n;
 }
+
+/* ---- whole-table digest (or_digest, oracle.h; rg_digest restates it on the device) */
+static inline uint64_t dg_mix(uint64_t z) {  /* fmix64 */
+  z ^= z >> 33;
+  z *= 0xFF51AFD7ED558CCDULL;
+  z ^= z >> 33;
+  z *= 0xC4CEB9FE1A85EC53ULL;
+  z ^= z >> 33;
+  return z;
+}
+
+int or_digest(const or_engine* e, uint64_t out[2]) {
+  uint64_t a = 0, b = 0;
+  const uint32_t R = e->c.replicas;
+  for (uint32_t rid = 0; rid < e->nrep; ++rid) {
+    const rep_t* r = &e->reps[rid];
+    or_replica_view v;
+    or_get_replica(e, rid, &v);
+    const uint64_t gid = global_group(e, r) * R + r->s;
+    uint64_t h = dg_mix(gid + 0x9E3779B97F4A7C15ULL);
+    const uint64_t f[25] = {v.term, v.vote, v.leader, v.committed, v.applied, v.last, v.marker, v.marker_term,
+                            v.snap_index, v.snap_term, v.cap_base, v.processed, v.role, v.election_tick,
+                            v.heartbeat_tick, v.rand_timeout, v.rng_ctr, v.granted, v.responded, v.active, v.err,
+                            v.drops, v.members, v.snap_members, v.cc_pending};
+    for (int k = 0; k < 25; ++k) h = dg_mix(h ^ f[k]);
+    for (uint32_t j = 0; j < R; ++j) {
+      h = dg_mix(h ^ v.match[j]);
+      h = dg_mix(h ^ v.next[j]);
+      h = dg_mix(h ^ v.rsnap[j]);
+      h = dg_mix(h ^ v.rstate[j]);
+    }
+    a += h;
+    uint64_t h2 = dg_mix(gid ^ 0x5851F42D4C957F2DULL);
+    for (uint64_t i = r->marker + 1; i <= r->last; ++i) {
+      const ent_t* en = log_at(e, r, i);
+      h2 = dg_mix(h2 ^ en->term);
+      h2 = dg_mix(h2 ^ ((uint64_t)en->type | ((uint64_t)en->len << 8) | ((uint64_t)en->crc << 32)));
+    }
+    b += h2;
+  }
+  out[0] = a;
+  out[1] = b;
+  return 0;
+}

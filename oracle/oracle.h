@@ -179,6 +179,12 @@ int or_get_read_ready(const or_engine* e, uint32_t rid, uint64_t* ctx, uint64_t*
 /* Snapshot events of rid's last step (the oracle side of rg_snapshot_events): OR_SNAP_* bits. */
 #define OR_SNAP_TAKEN 1
 #define OR_SNAP_RESTORED 2
+/* Whole-table digest: out[0] = Σ over replicas of an fmix64 chain over the replica's
+ * view (the or_replica_view fields, remotes of slots < R), out[1] = Σ of a chain over its log entries
+ * (marker, last] (term, then type | len << 8 | crc << 32); each chain seeded by the global replica id.
+ * Order-independent: the sum over ranks / windows is the digest of their union. Same function as
+ * rg_digest. */
+int or_digest(const or_engine* e, uint64_t out[2]);
 int or_get_snapshot_event(const or_engine* e, uint32_t rid, uint64_t* restored, uint64_t* index, uint64_t* term);
 /* Proposal payload generator: the synthetic Cmd of a tick-input proposal, len payload_bytes. */
 void or_payload(const or_engine* e, uint32_t slab, uint32_t group, uint32_t entry, uint8_t* out);

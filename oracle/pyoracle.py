@@ -119,6 +119,7 @@ def lib():
         L.or_tick_count.argtypes = [vp]
         L.or_tick_count.restype = u64
         L.or_get_replica.argtypes = [vp, u32, C.POINTER(ReplicaView)]
+        L.or_digest.argtypes = [vp, C.POINTER(C.c_uint64)]
         L.or_get_replicas.argtypes = [vp, u32, u32, C.POINTER(ReplicaView)]
         L.or_get_msgs.argtypes = [vp, u32, u32, C.POINTER(MsgView), u32]
         L.or_get_msg_terms.argtypes = [vp, u32, u32, u32, C.POINTER(C.c_uint64), u32]
@@ -333,6 +334,12 @@ class Oracle:
         for i, (g, s, ctx) in enumerate(reqs):
             arr[i].group, arr[i].slot, arr[i].ctx = g, s, ctx
         return self.L.or_read_index(self.h, arr, len(reqs))
+
+    def digest(self):
+        """or_digest: (view digest, log digest) of every replica."""
+        out = (C.c_uint64 * 2)()
+        self.L.or_digest(self.h, out)
+        return out[0], out[1]
 
     def read_ready(self, rid):
         """(ctx, index) of the read replica rid made ready in the last tick, or None."""

@@ -2,6 +2,8 @@
 // rg_deliver: they translate between the device's structure-of-arrays layout (slot-major
 // replica numbering q = s·G + g) and the C-ABI's per-replica views (rid = g·R + s).
 // Not on the tick path.
+#include <algorithm>
+
 #include "../../include/raftgpu.h"
 #include "raftgpu_internal.h"
 
@@ -250,6 +252,75 @@ hipError_t launch_notify_applied(const AdminParams& a, const uint32_t* rids, con
                                  int pass, uint32_t* bad, hipStream_t s) {
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(notify_applied_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, rids, index, n, pass, bad);
+  return hipGetLastError();
+}
+
+// ---- rg_digest (the same function as the oracle's or_digest): per replica an fmix64
+// chain over its view and one over its log (marker, last], seeded by the global replica id, summed
+__device__ __forceinline__ uint64_t dg_mix(uint64_t z) {
+  z ^= z >> 33;
+  z *= 0xFF51AFD7ED558CCDULL;
+  z ^= z >> 33;
+  z *= 0xC4CEB9FE1A85EC53ULL;
+  z ^= z >> 33;
+  return z;
+}
+
+__global__ void __launch_bounds__(256) digest_kernel(AdminParams a, unsigned long long* out) {
+  const TickParams& t = a.t;
+  const uint64_t N = t.nrep;
+  uint64_t sa = 0, sb = 0;
+  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < N; q += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t s = (uint32_t)(q / t.G), g = (uint32_t)(q - (uint64_t)s * t.G);
+    const uint64_t gid = pl_group(t.pl, s, g) * t.R + s;
+    const uint64_t* s64 = t.s64_in + q;
+    const uint32_t* s32 = t.s32_in + q;
+    uint64_t h = dg_mix(gid + 0x9E3779B97F4A7C15ULL);
+    for (uint32_t k = 0; k <= S_PROCESSED; ++k) {  // term .. processed, in rg_replica_view order
+      const uint32_t row = k <= S_CAP_BASE ? k : S_PROCESSED;
+      h = dg_mix(h ^ s64[row * N]);
+    }
+    const uint32_t rows32[13] = {S_ROLE, S_ETICK, S_HTICK, S_RAND_TO, S_RNG_CTR, S_GRANTED, S_RESPONDED, S_ACTIVE,
+                                 S_ERR, S_DROPS, S_MEMBERS, S_SNAP_MEMBERS, S_CC_PENDING};
+    for (uint32_t k = 0; k < 13; ++k) {
+      uint32_t x = s32[rows32[k] * N];
+      if (rows32[k] == S_ERR) x |= a.crc_err[q];
+      h = dg_mix(h ^ x);
+    }
+    for (uint32_t j = 0; j < t.R; ++j) {
+      h = dg_mix(h ^ t.rem_in[(0 * t.R + j) * N + q]);
+      h = dg_mix(h ^ t.rem_in[(1 * t.R + j) * N + q]);
+      h = dg_mix(h ^ t.rem_in[(2 * t.R + j) * N + q]);
+      h = dg_mix(h ^ t.rst_in[j * N + q]);
+    }
+    sa += h;
+    const uint64_t marker = s64[S_MARKER * N], last = s64[S_LAST * N];
+    uint64_t h2 = dg_mix(gid ^ 0x5851F42D4C957F2DULL);
+    for (uint64_t i = marker + 1; i <= last; ++i) {
+      const uint64_t slot = i & (t.L - 1);
+      const uint64_t w = t.tr[slot * N + q];
+      const uint32_t type = (uint32_t)((w >> 61) & 1);
+      const uint32_t len = (w & (PAY_BIT | TYPE_BIT)) ? word_len(w) : 0u;
+      uint32_t crc = 0;
+      if (w & PAY_BIT) crc = crc_of_cmd(a.info[((w >> 63) * N + q) * t.L + slot].x, len, t.P, a.zi);
+      h2 = dg_mix(h2 ^ (w & TERM_MASK));
+      h2 = dg_mix(h2 ^ ((uint64_t)type | ((uint64_t)len << 8) | ((uint64_t)crc << 32)));
+    }
+    sb += h2;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    sa += ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(sa >> 32), off, 64) << 32) | (uint32_t)__shfl_xor((int)(uint32_t)sa, off, 64);
+    sb += ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(sb >> 32), off, 64) << 32) | (uint32_t)__shfl_xor((int)(uint32_t)sb, off, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(out, (unsigned long long)sa);
+    atomicAdd(out + 1, (unsigned long long)sb);
+  }
+}
+
+hipError_t launch_digest(const AdminParams& a, unsigned long long* out, hipStream_t s) {
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((a.t.nrep + 255) / 256, 4096);
+  hipLaunchKernelGGL(digest_kernel, dim3(blocks), dim3(256), 0, s, a, out);
   return hipGetLastError();
 }
 

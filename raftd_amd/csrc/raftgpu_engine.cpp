@@ -1929,6 +1929,16 @@ int rg_get_update(rg_engine* e, uint32_t slot_mask, uint32_t flags, rg_update* o
   return RG_OK;
 }
 
+int rg_digest(rg_engine* e, uint64_t* out) {
+  if (!e || !out) return fail(RG_EINVAL, "rg_digest args");
+  if (int jrc = join(e)) return jrc;
+  HIPCHK(hipMemsetAsync(e->d_sum, 0, 16, e->stream));
+  LAUNCH(launch_digest(admin(e), e->d_sum, e->stream), e->stream, "digest");
+  HIPCHK(hipMemcpyAsync(out, e->d_sum, 16, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return RG_OK;
+}
+
 int rg_commit_update(rg_engine* e, const rg_update* u, uint32_t flags) {
   if (!e || !u || (flags & ~RG_COMMIT_APPLIED)) return fail(RG_EINVAL, "rg_commit_update args");
   if (u->tick != e->t) return fail(RG_EINVAL, "rg_commit_update: the update is not of the last tick");

@@ -477,6 +477,8 @@ hipError_t launch_deliver(const AdminParams& a, uint32_t rid_src, const void* hd
 // rg_notify_applied: check (pass 0: *bad = number of rids / indices out of range) or set (pass 1) applied
 hipError_t launch_notify_applied(const AdminParams& a, const uint32_t* rids, const uint64_t* index, uint32_t n,
                                  int pass, uint32_t* bad, hipStream_t s);
+// rg_digest: out[0] += Σ view chains, out[1] += Σ log chains (out zeroed by the caller)
+hipError_t launch_digest(const AdminParams& a, unsigned long long* out, hipStream_t s);
 // rg_commit_update(RG_COMMIT_APPLIED): applied = processed for every replica of the slot mask
 hipError_t launch_applied_all(const AdminParams& a, uint32_t slot_mask, hipStream_t s);
 int bulk_lds_bytes(uint32_t P);

@@ -182,7 +182,7 @@ EXPORTS = ["rg_create", "rg_destroy", "rg_bootstrap", "rg_fill_slabs", "rg_tick"
            "rg_apply_committed", "rg_probe_copy", "rg_persist_collect", "rg_snapshot_events", "rg_propose",
            "rg_notify_applied", "rg_apply_async", "rg_apply_wait", "rg_read_index", "rg_read_index_results",
            "rg_config_change", "rg_wire_exchange", "rg_rccl_unique_id", "rg_rccl_open", "rg_rccl_close",
-           "rg_pool_stats", "rg_get_update", "rg_commit_update", "rg_tick_device_n"]
+           "rg_pool_stats", "rg_get_update", "rg_commit_update", "rg_tick_device_n", "rg_digest"]
 
 _lib = None
 
@@ -248,6 +248,7 @@ def load_library(path: str = LIB_PATH):
         "rg_apply_committed": ([vp, u32, vp, vp, u64, C.POINTER(C.c_uint64), u64, C.POINTER(C.c_uint64)], i32),
         "rg_pool_stats": ([vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_int)], i32),
         "rg_get_update": ([vp, u32, u32, C.POINTER(Update)], i32),
+        "rg_digest": ([vp, C.POINTER(C.c_uint64)], i32),
         "rg_commit_update": ([vp, C.POINTER(Update), u32], i32),
         "rg_probe_copy": ([C.c_int32, u64, C.c_int32, C.POINTER(C.c_double)], i32),
         "rg_snapshot_events": ([vp, u32, vp, u64, C.POINTER(C.c_uint64)], i32),
@@ -623,6 +624,12 @@ class Engine:
     def commit_update(self, u, applied: bool = True):
         """rg_commit_update (Peer.Commit); applied: the slot mask's replicas report applied = processed."""
         self._check(self.L.rg_commit_update(self.h, C.byref(u), COMMIT_APPLIED if applied else 0))
+
+    def digest(self):
+        """rg_digest: (view digest, log digest) of this engine's replicas."""
+        out = (C.c_uint64 * 2)()
+        self._check(self.L.rg_digest(self.h, out))
+        return out[0], out[1]
 
     def pool_stats(self) -> dict:
         """rg_pool_stats: {'total': pages, 'free': pages, 'failed': bool} of the payload page pool."""

@@ -521,3 +521,67 @@ def test_steady_state_throughput_shape():
         for s in range(1, R):
             f = o.replica(g * R + s)
             assert f["role"] == 0 and f["leader"] == 1 and f["err"] == 0
+
+
+def _digest_py(o, R):
+    """or_digest restated from the oracle's public views."""
+    M = (1 << 64) - 1
+
+    def mix(z):
+        z ^= z >> 33
+        z = (z * 0xFF51AFD7ED558CCD) & M
+        z ^= z >> 33
+        z = (z * 0xC4CEB9FE1A85EC53) & M
+        return z ^ (z >> 33)
+
+    a = b = 0
+    base = o.cfg["group_base"]
+    for rid in range(o.nrep):
+        v = o.replica(rid)
+        gid = (base + rid // R) * R + rid % R
+        h = mix((gid + 0x9E3779B97F4A7C15) & M)
+        for f in ("term", "vote", "leader", "committed", "applied", "last", "marker", "marker_term", "snap_index",
+                  "snap_term", "cap_base", "processed", "role", "election_tick", "heartbeat_tick", "rand_timeout",
+                  "rng_ctr", "granted", "responded", "active", "err", "drops", "members", "snap_members",
+                  "cc_pending"):
+            h = mix(h ^ v[f])
+        for j in range(R):
+            for f in ("match", "next", "rsnap", "rstate"):
+                h = mix(h ^ v[f][j])
+        a = (a + h) & M
+        h2 = mix(gid ^ 0x5851F42D4C957F2D)
+        for i in range(v["marker"] + 1, v["last"] + 1):
+            en = o.entry(rid, i)
+            h2 = mix(h2 ^ en["term"])
+            h2 = mix(h2 ^ (en["type"] | (en["len"] << 8) | (en["crc"] << 32)))
+        b = (b + h2) & M
+    return a, b
+
+
+def test_digest_definition_and_windows():
+    """or_digest equals its restatement from the public views, and the digests of group windows add
+    up to the digest of their union (what lets a rank or a window be checked on its own)."""
+    import numpy as np
+    G, R = 8, 3
+    cfg = dict(replicas=R, log_capacity=64, payload_bytes=32, max_entries_per_msg=8, snapshot_entries=20,
+               compaction_overhead=3, drop_ppm=30000, seed=0xD16)
+    whole = make("c", groups=G, **cfg)
+    halves = [make("c", groups=G // 2, group_base=b, **cfg) for b in (0, G // 2)]
+    for o in [whole] + halves:
+        o.bootstrap()
+    rng = np.random.default_rng(2)
+    camp = np.zeros(G * R, np.uint8)
+    camp[0::R] = 1
+    for t in range(40):
+        pt = rng.integers(0, R, G).astype(np.uint8)
+        pc = rng.integers(1, 9, G).astype(np.uint32)
+        ins = dict(campaign=camp) if t == 1 else dict(prop_target=pt, prop_count=pc) if t > 4 else {}
+        whole.tick(**ins)
+        for k, o in enumerate(halves):
+            sl = slice(k * G // 2, (k + 1) * G // 2)
+            o.tick(**{n: (v[k * G // 2 * R:(k + 1) * G // 2 * R] if n == "campaign" else v[sl]) for n, v in ins.items()})
+    d = whole.digest()
+    assert d == _digest_py(whole, R)
+    s = [sum(x) & ((1 << 64) - 1) for x in zip(*(o.digest() for o in halves))]
+    assert tuple(s) == d
+    assert whole.replica(0)["snap_index"] > 0  # compaction happened: the log chains start above a marker
