@@ -129,6 +129,7 @@ struct Ctl {
   // payload stream: hw = next free chunk. The lowest page held (S_LPG, the capacity
   // rule's base, unchanged during a step) is read where an append needs it
   uint32_t hw;
+  uint32_t lpg_;  // S_LPG at step start (read with the state; the capacity rule's base)
   // RG_CTL_FASTREP (see the top of this file). The leader's last append
   // of this step when it wrote no protected index: entries
   // [la_base, la_base + la_n) all hold the ring word la_word (bank 0) and term(la_base − 1) = la_pt,
@@ -176,8 +177,9 @@ struct Ctl {
     // to release, known now that the step which wrote it has stored its {crc, position} (the bulk
     // kernel). They go back to the pool at the end of this step; the capacity rule keeps lpg until
     // then, so a page read in this launch is never reassigned in it
+    lpg_ = b[S_LPG * n];
     {
-      uint32_t nlpg = b[S_LPG * n];
+      uint32_t nlpg = lpg_;
       if (const uint64_t fi = a[S_FIDX * n]) {
         uint32_t bound = hw;
         if (fi <= last) {
@@ -522,7 +524,7 @@ struct Ctl {
     hw += tot;
   }
 
-  RG_FN uint32_t lpg() const { return p.s32_in[(uint64_t)S_LPG * p.nrep + q]; }
+  RG_FN uint32_t lpg() const { return lpg_; }
 
   // raft.appendEntries (leader side): n entries at term. slab_id < 0: the leader's empty no-op.
   // Otherwise Cmds of a proposal: in slab `slab_id`, row of replica slot `rslot` in this column,
@@ -654,13 +656,13 @@ struct Ctl {
   // remote: the message came over the wire (its inline terms are in rmt, its records at wofs)
   // upos: header word 5 (a uniform Replicate's stream position of entry 0 at the sender)
   RG_FN void handle_replicate(uint64_t w0, uint64_t log_term, uint64_t li, uint64_t mcommit, uint32_t from,
-                              uint32_t src, uint32_t k, bool remote, uint64_t wofs, uint64_t upos) {
+                              uint32_t src, uint32_t k, bool remote, uint64_t wofs, uint64_t upos, uint64_t mt0) {
     RG_T0(t0);
-    handle_replicate_(w0, log_term, li, mcommit, from, src, k, remote, wofs, upos);
+    handle_replicate_(w0, log_term, li, mcommit, from, src, k, remote, wofs, upos, mt0);
     RG_ACC(2, t0);
   }
   RG_FN void handle_replicate_(uint64_t w0, uint64_t log_term, uint64_t li, uint64_t mcommit, uint32_t from,
-                               uint32_t src, uint32_t k, bool remote, uint64_t wofs, uint64_t upos) {
+                               uint32_t src, uint32_t k, bool remote, uint64_t wofs, uint64_t upos, uint64_t mt0) {
     if (li < committed) {
       send_simple(M_REPLICATE_RESP, from, 0, committed);
       return;
@@ -670,7 +672,7 @@ struct Ctl {
       const uint64_t* mt = (remote ? p.rmt : p.mt_in) + ((((uint64_t)src * R + s) * p.K + k) * p.E) * p.G + g;
       // a uniform Replicate (local only): every entry carries the word mt[0]
       const bool uni = !remote && ((uint32_t)wofs & RG_UNIFORM) && n > 0;
-      const uint64_t uw = uni ? mt[0] : 0ull;
+      const uint64_t uw = uni ? mt0 : 0ull;  // loaded with the header (handle_)
       uint32_t k0 = n;
       for (uint32_t e = 0; e < n; ++e) {  // entryLog.getConflictIndex
         if (term_at(li + 1 + e) != ((uni ? uw : mt[(uint64_t)e * p.G]) & TERM_MASK)) {
@@ -976,6 +978,9 @@ struct Ctl {
     uint64_t hb[NB];
 #pragma unroll
     for (int x = 0; x < NB; ++x) hb[x] = h[(uint64_t)x * plane];
+    // a local Replicate's first inline word travels in the same round trip (a uniform Replicate
+    // needs only it); for other messages the slot holds stale words, which nothing reads
+    const uint64_t mt0 = remote ? 0ull : p.mt_in[((((uint64_t)src * R + s) * p.K + k) * p.E) * p.G + g];
     auto hw = [&](int x) -> uint64_t { return x < NB ? hb[x < NB ? x : 0] : h[(uint64_t)x * plane]; };
     const uint64_t w0 = hw(0);
     const uint64_t mterm = hw(1);
@@ -1038,7 +1043,7 @@ struct Ctl {
           leader = from;
         }
         if (type == M_REPLICATE) {
-          handle_replicate(w0, hw(2), hw(3), hw(4), from, src, k, remote, hw(7), hw(5));  // local: RG_UNIFORM
+          handle_replicate(w0, hw(2), hw(3), hw(4), from, src, k, remote, hw(7), hw(5), mt0);  // local: RG_UNIFORM
         } else if (type == M_HEARTBEAT) {
           commit_to(hw(4));
           send_simple(M_HEARTBEAT_RESP, from, 0, 0, hw(5), hw(6));

@@ -1217,7 +1217,8 @@ static int tick_impl(rg_engine* e, const rg_tick_input* in, bool device_ptrs) {
 #endif
   // One stream (the product): stream order alone sequences control and bulk, so no event
   // records or waits go between them (each is a packet in the queue, ≈5 µs a tick at 4K groups).
-  // bulk_done is still recorded: join() and a later rg_set_stream() order other streams on it.
+  // (r03: bulk_done, which only orders a second stream, is no longer recorded every tick either;
+  // rg_set_stream synchronises before it switches streams.)
   const bool two = bs != e->stream;
   if (two && e->t >= 2) HIPCHK(hipStreamWaitEvent(e->stream, e->bulk_done[a], 0));
   RGCHK(timing_event(e, e->stream, 0));
@@ -1242,7 +1243,9 @@ static int tick_impl(rg_engine* e, const rg_tick_input* in, bool device_ptrs) {
     LAUNCH(launch_bulk(bulk_params(e), e->pt, bs, e->bulk_grid), bs, "bulk_kernel");
     RGCHK(timing_event(e, bs, 1));
   }
-  HIPCHK(hipEventRecord(e->bulk_done[a], bs));
+  // bulk_done orders other streams behind the payload stage (join, the overlap ablation); with one
+  // stream, stream order already does, and an event record is one more packet per tick
+  if (two) HIPCHK(hipEventRecord(e->bulk_done[a], bs));
   e->t++;
   e->wire_ready = false;
   if (!device_ptrs && in) HIPCHK(hipStreamSynchronize(e->stream));  // host buffers may be reused

@@ -587,10 +587,15 @@ hipError_t launch_bulk(const BulkParams& p, const uint32_t* pt, hipStream_t s, i
 // ================================================================== payload page pool
 // One lane per replica (coalesced state rows): return the stream pages control released
 // ([S_LPG, S_NLPG)) to the free ring and take the pages this step's appends need ([S_APG,
-// ceil(S_HW))), with one tail and one head atomic per wave. Allocations read ids below `limit`
-// (written by an earlier launch); frees write at and above the tail: disjoint.
-__global__ void __launch_bounds__(256) pool_kernel(PoolParams pp) {
-  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x, lane = lane_id();
+// ceil(S_HW))). The ring positions come from a block-wide scan and ONE tail and ONE head atomic
+// per 1,024-lane block (r03: an atomic pair per wave, 3,072 pairs on two addresses at 64K x 3, made
+// this a 55 µs kernel). Allocations read ids below `limit` (written by an earlier launch); frees
+// write at and above the tail: disjoint.
+constexpr uint32_t POOL_BLOCK = 1024;
+__global__ void __launch_bounds__(POOL_BLOCK) pool_kernel(PoolParams pp) {
+  __shared__ uint32_t wf[POOL_BLOCK / 64], wa[POOL_BLOCK / 64];
+  __shared__ unsigned long long base[2];
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x, lane = lane_id(), w = threadIdx.x >> 6;
   const bool valid = q < pp.nrep;
   const uint64_t n = pp.nrep, PTSM = pp.PTS - 1;
   uint32_t lpg = 0, apg = 0, nlpg = 0, top = 0, f = 0, a = 0;
@@ -602,15 +607,26 @@ __global__ void __launch_bounds__(256) pool_kernel(PoolParams pp) {
     f = vpn_diff(nlpg, lpg);
     a = vpn_diff(top, apg);
   }
-  const uint32_t fo = wave_excl_scan32(f), ao = wave_excl_scan32(a);
-  const uint32_t F = __builtin_amdgcn_readlane(fo + f, 63), A = __builtin_amdgcn_readlane(ao + a, 63);
-  unsigned long long fb = 0, ab = 0;
-  if (lane == 0) {
-    if (F) fb = atomicAdd(&pp.ctl->tail, (unsigned long long)F);
-    if (A) ab = atomicAdd(&pp.ctl->head, (unsigned long long)A);
+  uint32_t fo = wave_excl_scan32(f), ao = wave_excl_scan32(a);
+  if (lane == 63) {
+    wf[w] = fo + f;
+    wa[w] = ao + a;
   }
-  fb = rl64(fb, 0);
-  ab = rl64(ab, 0);
+  __syncthreads();
+  if (threadIdx.x == 0) {  // the block's wave totals → offsets, and the block's two ring reservations
+    uint32_t sf = 0, sa = 0;
+    for (uint32_t i = 0; i < blockDim.x / 64; ++i) {
+      const uint32_t tf = wf[i], ta = wa[i];
+      wf[i] = sf;
+      wa[i] = sa;
+      sf += tf;
+      sa += ta;
+    }
+    base[0] = sf ? atomicAdd(&pp.ctl->tail, (unsigned long long)sf) : 0ull;
+    base[1] = sa ? atomicAdd(&pp.ctl->head, (unsigned long long)sa) : 0ull;
+  }
+  __syncthreads();
+  const unsigned long long fb = base[0] + wf[w], ab = base[1] + wa[w];
   const unsigned long long limit = pp.ctl->limit;
   uint32_t* ptq = pp.pt + (uint64_t)q * pp.PTS;
   for (uint32_t k = 0; k < f; k += 8) {  // frees: eight page-table reads in flight, then their ring writes
@@ -644,7 +660,7 @@ __global__ void __launch_bounds__(256) pool_kernel(PoolParams pp) {
 }
 
 hipError_t launch_pool(const PoolParams& p, hipStream_t s) {
-  hipLaunchKernelGGL(pool_kernel, dim3((p.nrep + 255) / 256), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(pool_kernel, dim3((p.nrep + POOL_BLOCK - 1) / POOL_BLOCK), dim3(POOL_BLOCK), 0, s, p);
   return hipGetLastError();
 }
 

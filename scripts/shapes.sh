@@ -1,6 +1,6 @@
 #!/bin/bash
 # bench.py at the other BASELINE.json shapes on one GPU (steady-state leaders; not the headline
-# line): C2 4,096 x 3 (and P = 0), 64K x 3 P = 0, C3's 64K x 5 co-located (L 1,024: at L 2,048 its live Cmds exceed the 64-GiB page pool of one engine),
+# line): C2 4,096 x 3 (and P = 0), 64K x 3 P = 0, C3's shape co-located at 32K x 5 (64K x 5 at L 2,048 holds more live Cmds than one engine's 64-GiB page pool),
 # C5's 1M x 3 at P = 256, L = 2,048 (the paged store, r03).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -18,5 +18,5 @@ print('$n', '$*', 'value', round(d['value']/1e6,2), 'M ms', round(d['ms_per_step
 run c2 --groups 4096 --steps 100 --warmup 10
 run c2p0 --groups 4096 --payload 0 --steps 100 --warmup 10
 run m64p0 --payload 0 --steps 50 --warmup 10
-run c3shape --replicas 5 --steps 20 --warmup 5 --log-capacity 1024
+run c3shape --replicas 5 --groups 32768 --steps 20 --warmup 5  # 32K x 5 = C3's 8,192 columns x 5 per GPU, four times over
 run c5shape --groups 1048576 --entries 1 --steps 10 --warmup 3  # mean 1 entry per group per tick
