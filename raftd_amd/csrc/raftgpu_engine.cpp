@@ -1114,7 +1114,7 @@ int rg_kernel_ms(rg_engine* e, double* ms, uint64_t* launches) {
 static void seal(TickParams& p) {
   uint64_t w[TP_WORDS], h = 0;
   memcpy(w, &p, sizeof w);
-  for (uint32_t i = 0; i < TP_WORDS; ++i) h = tp_mix(h ^ w[i]);
+  for (uint32_t i = 0; i < TP_WORDS; ++i) h += tp_term(w[i], i);
   p.csum = h;
 }
 

@@ -244,14 +244,17 @@ struct TickParams {
   RG_G(PoolCtl) pool;               // sticky param_err on a checksum mismatch
   uint64_t csum;                    // tp_checksum of every word above (host-computed, checked first)
 };
-// the parameter block's checksum: mix64 chain over its words before `csum` (a stale or torn block
-// is reported as an engine error instead of being dereferenced)
+// the parameter block's checksum: Σ_i tp_mix(word_i + (i + 1)·φ) mod 2^64 over its words before `csum`
+// (a stale or torn block is reported as an engine error instead of being dereferenced).
+// A sum, not a chain, so a wave checks it with one coalesced load (lane i, word i) and a reduction.
 RG_HD_INLINE uint64_t tp_mix(uint64_t z) {
   z ^= z >> 31;
   z *= 0x9E3779B97F4A7C15ULL;
   return z ^ (z >> 29);
 }
+RG_HD_INLINE uint64_t tp_term(uint64_t word, uint32_t i) { return tp_mix(word + (uint64_t)(i + 1) * 0x9E3779B97F4A7C15ULL); }
 constexpr uint32_t TP_WORDS = (uint32_t)(offsetof(TickParams, csum) / 8);
+static_assert(TP_WORDS <= 64, "the checksum is verified with one word per lane of a wave");
 
 struct BulkParams {
   uint32_t G, R, nrep, L, P, E, J, crc_const, tile;  // tile: groups per wave work item (1..64)

@@ -43,18 +43,23 @@ template <int R>
 __global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_MINWAVES) control_kernel(const TickParams* __restrict__ pp,
                                                                                uint32_t* perr) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-  // The block is read through the constant address space: scalar loads, a handful of 64-B
-  // s_load_dwordx16 for the checksum (r03: a volatile flat-load loop here cost 53 dependent,
-  // cache-bypassing round trips per wave). The empty asm launders the pointer so these loads stay
-  // separate from the step's field reads (which would otherwise keep the whole block live).
+  // The checksum: lane i loads word i (one coalesced 424-B wave load, through a laundered pointer so
+  // it stays separate from the step's scalar field reads) and the wave sums the terms with a
+  // butterfly. r03a's volatile chain cost 53 dependent cache-bypassing loads per wave; a chain of
+  // seven s_load_dwordx16 (r03b) still waited seven scalar round trips at the head of every wave.
   const TickParams* pc = pp;
   asm volatile("" : "+s"(pc));
-  typedef RG_CONST(const uint64_t) cu64;
-  cu64* w = (cu64*)pc;  // a C cast: the address-space conversion
-  uint64_t h = 0;
+  const uint32_t lane = threadIdx.x & 63u;
+  typedef __attribute__((address_space(1))) const uint64_t gu64;
+  gu64* wv = (gu64*)pc;  // a C cast: the address-space conversion (global_load, not flat_load)
+  uint64_t h = lane < TP_WORDS ? tp_term(wv[lane], lane) : 0ull;
 #pragma unroll
-  for (uint32_t i = 0; i < TP_WORDS; ++i) h = tp_mix(h ^ w[i]);
-  if (h != w[TP_WORDS]) {
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)h, off, 64);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(h >> 32), off, 64);
+    h += ((uint64_t)hi << 32) | lo;
+  }
+  if (h != wv[TP_WORDS]) {
     if (q == 0) {
       printf("raftgpu: control_kernel parameter block checksum mismatch (tick %llu): launch skipped\n",
              (unsigned long long)pp->tick);

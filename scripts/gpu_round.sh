@@ -19,6 +19,7 @@ for what in ${STEPS:-smoke parity tests bench wire rehearse}; do
     bench) step bench 400 python bench.py ${BENCH_ARGS:---cpu-seconds 10 --ingest} ;;
     profile) step profile 1000 bash scripts/profile.sh ${PTAG:-r03} ;;
     shapes) step shapes 600 bash scripts/shapes.sh ;;
+    copywg) step copywg 900 bash scripts/e2e_copywg.sh ;;
     wire) step bench_wire 400 python bench.py --wire-all --no-cpu-baseline ;;
     rehearse) step rehearse 400 env RAFTD_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                 --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --backend gloo --groups 8192 \
