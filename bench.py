@@ -434,6 +434,17 @@ def main():
         wire.drain()
     kms["control"] = host.kernel_ms()["control"]
     host.timing(False)
+    # the same steps once more with no timing events at all (the roofline's bulk events are two
+    # event records per tick in the timed region): what the event records themselves cost
+    torch.cuda.synchronize()
+    u0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_step(None)
+    if pipelined:
+        wire.drain()
+    host.join()
+    torch.cuda.synchronize()
+    untimed_ms = (time.perf_counter() - u0) * 1e3 / args.steps
     graph = graph_ticks(eng, pt, pc, G) if not spread and not args.wire_all else None
     x_ms = sum(a.elapsed_time(b) for a, b in xev) / args.steps if wire and not pipelined else 0.0
     va = eng.replica_array()  # every replica of this rank's first engine: invariant bits and drops
@@ -514,6 +525,7 @@ def main():
         "commits_per_sec": commits / wall,
         "replica_steps_per_sec": group_steps * R,
         "device_ms_per_step": dev_max / K,
+        "ms_per_step_without_timing_events": untimed_ms,
         "replicas_with_invariant_errors": errs,
         "drops_total": drops,
         "drops_note": "messages / batches the engine dropped by its own bounded-buffer rules (K_MAX per pair per "
