@@ -295,7 +295,8 @@ int rg_join(rg_engine* e);
 int rg_sync(rg_engine* e);
 /* Per-launch kernel timing with HIP events on the streams the kernels run on (measurement
  * only). enable=1 times both kernels (four event records per tick), enable=2 bulk_kernel only
- * (two), 0 stops; a non-zero value zeroes the totals. */
+ * (two), 0 stops; a non-zero value zeroes the totals. enable | (n << 8): only every n-th tick
+ * (tick count divisible by n) is timed — each timed event record costs its tick tens of µs. */
 int rg_timing(rg_engine* e, int enable);
 /* Synchronises, then returns the summed durations (ms) and launch counts since rg_timing(e, 1):
  * index 0 = control_kernel, 1 = bulk_kernel. */

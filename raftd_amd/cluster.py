@@ -454,9 +454,9 @@ class DistEngine(_Feeds):
             self._xclose()
             self._xclose, self.xt = None, None
 
-    def timing(self, on=True, bulk_only=False):
+    def timing(self, on=True, bulk_only=False, every=1):
         for p in self.parts:
-            p.eng.timing(on, bulk_only=bulk_only)
+            p.eng.timing(on, bulk_only=bulk_only, every=every)
 
     def kernel_ms(self) -> dict:
         """Summed over the halves: total ms per kernel, and launches counted per tick."""

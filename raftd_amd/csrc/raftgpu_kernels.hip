@@ -304,6 +304,23 @@ __device__ __forceinline__ bool next_job(const BulkParams& p, Cursor& cur, TileJ
   return true;
 }
 
+// The tile's next replica, from the first-job descriptors the tile load left in registers: no
+// memory round trip, so the cursor can take it in the middle of a pass (small jobs share a pass).
+template <int LG, bool WIRE>
+__device__ __forceinline__ void next_replica(const BulkParams& p, Cursor& cur, const TileJobs& tj) {
+  const uint32_t l = rfl((uint32_t)__ffsll((long long)cur.m) - 1);
+  cur.m &= cur.m - 1;
+  cur.q = cur.qb + l;
+  cur.njl = __builtin_amdgcn_readlane(tj.nj, l);
+  cur.j = 0;
+  Job jb;
+  jb.first = rl64(tj.j0.first, l); jb.spos = rl64(tj.j0.spos, l); jb.sm = rl64(tj.j0.sm, l);
+  jb.dm = rl64(tj.j0.dm, l);
+  jb.meta = __builtin_amdgcn_readlane(tj.j0.meta, l); jb.src = __builtin_amdgcn_readlane(tj.j0.src, l);
+  jb.dpos = __builtin_amdgcn_readlane(tj.j0.dpos, l);
+  set_job<LG, WIRE>(p, cur, jb);
+}
+
 // the entry info word {slot crc, stream position} (and the sender-CRC check) of job entry e
 __device__ __forceinline__ void put_info(const BulkParams& p, uint32_t q, uint64_t first, uint64_t dm, uint32_t e,
                                          uint32_t crc, uint32_t pos, bool check, uint32_t want) {
@@ -435,40 +452,38 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p, const uint32_t*
   cur.uni = true;
   cur.live = next_job<LG, WIRE>(p, cur, tj, stride, ntiles);
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  // ring slot u: payload chunk, destination pool chunk, sender's slot CRC (per lane); the entries
-  // each slot's step holds are wave-uniform: 8 bits per slot in one scalar (ikv / ckv), so the
-  // per-lane flags need no registers of their own (r03: 99 -> 95 VGPRs, occupancy 4 -> 5)
+  // ring slot u: payload chunk, destination pool chunk, sender's slot CRC (per lane). The job a slot's
+  // step belongs to is wave-uniform and kept per slot (scalars): replica sq, first index sfirst, bank
+  // mask sdm, first entry of the step sb, job start se0 / destination chunk sdp / chunks per entry
+  // sncu, entries in the step skv (0 = empty), whether followers check the sender CRC schk. A slot
+  // may take the tile's next replica's job in the middle of a pass (from registers, no round trip),
+  // so a pass of small jobs (C5: one entry per job) fills all BULK_U slots instead of one.
   u32x4 x[BULK_U];
   uint32_t ds[BULK_U], want[BULK_U];
+  uint32_t sq[BULK_U], sb[BULK_U], se0[BULK_U], sdp[BULK_U], sncu[BULK_U], skv[BULK_U];
+  uint64_t sfirst[BULK_U], sdm[BULK_U];
+  bool schk[BULK_U];
 #pragma unroll
   for (int u = 0; u < BULK_U; ++u) {
     x[u] = u32x4{0, 0, 0, 0};
     ds[u] = want[u] = 0;
+    sq[u] = sb[u] = se0[u] = sdp[u] = sncu[u] = skv[u] = 0;
+    sfirst[u] = sdm[u] = 0;
+    schk[u] = false;
   }
   // Every slot issues exactly two loads per pass (payload chunk + sender CRC word), redirected to a
   // dummy address when the slot has no work, so the number of memory operations between a load
   // and its use is the same on every path and the compiler's vmcnt waits keep the ring in flight.
-  // A pass never spans two jobs (the cursor moves once per pass), so the slots consumed in a pass
-  // all belong to the job `pj` the previous pass issued.
   const uint8_t* dummy = reinterpret_cast<const uint8_t*>(p.crc_tab + CRC_ZERO_OFF);  // 16 zero bytes
   uint32_t vmask = 0;
-  uint32_t iq = 0, ib = 0, ie0 = 0, idp = 0, incu = 0, ikv = 0;  // the job of the pass being issued (for its consume)
-  bool ichk = false;
-  uint64_t ifirst = 0, idm = 0;
   do {
-    const uint32_t cq = iq, cb = ib, ce0 = ie0, cdp = idp, cncu = incu, ckv = ikv;
-    const bool cchk = ichk;
-    const uint64_t cfirst = ifirst, cdm = idm;
-    iq = cur.q; ib = cur.b; ie0 = cur.e0; idp = cur.dpos; incu = cur.ncu; ifirst = cur.first; idm = cur.dm;
-    ichk = cur.kind == SRC_RING || (WIRE && cur.kind == SRC_WIRE);  // followers verify the sender's CRC
-    ikv = 0;
 #pragma unroll
     for (int u = 0; u < BULK_U; ++u) {
-      {  // consume slot u: store, CRC, info, verify (fl = 0 for an empty slot: no stores). A stream's
-        // Cmd is followed by zeros up to its chunk boundary (every writer copies whole chunks), and
-        // lanes past a Cmd's chunks contribute nothing, so the CRC is the slot CRC.
-        const bool valid = ei < ((ckv >> (8 * u)) & 0xFFu);
-        const bool act = valid && c < cncu;
+      {  // consume slot u: store, CRC, info, verify (no entries: no stores). A stream's Cmd is followed
+        // by zeros up to its chunk boundary (every writer copies whole chunks), and lanes past a Cmd's
+        // chunks contribute nothing, so the CRC is the slot CRC.
+        const bool valid = ei < skv[u];
+        const bool act = valid && c < sncu[u];
         if (act) {
 #ifdef RG_BULK_PLAIN_STORE
           *reinterpret_cast<u32x4*>(p.pool + (uint64_t)ds[u] * 16) = x[u];
@@ -482,11 +497,16 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p, const uint32_t*
 #endif
         if constexpr (LG > 0) v = xor_lanes<LG>(crc.shift(v));  // raw(slot) = XOR_c Z^(after c)(raw c)
         if (valid && c == 0) {
-          const uint32_t e = cb + u * EPI + ei;
-          put_info(p, cq, cfirst, cdm, e, act ? (p.crc_const ^ v) : 0u, cdp + (e - ce0) * cncu, cchk && act, want[u]);
+          const uint32_t e = sb[u] + ei;
+          put_info(p, sq[u], sfirst[u], sdm[u], e, act ? (p.crc_const ^ v) : 0u, sdp[u] + (e - se0[u]) * sncu[u],
+                   schk[u] && act, want[u]);
         }
       }
       {  // issue the job's next step (or an empty step) into slot u
+#ifndef RG_BULK_ONEJOB
+        // a uniform job fully issued: take the tile's next replica now if that costs no round trip
+        if (cur.live && cur.uni && cur.b >= cur.n && cur.j + 1 >= cur.njl && cur.m) next_replica<LG, WIRE>(p, cur, tj);
+#endif
         const bool step = cur.live && cur.uni && cur.b < cur.n;
         const uint32_t e = cur.b + ei;
         const bool valid = step && e < cur.n;
@@ -510,7 +530,6 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p, const uint32_t*
         }
         const uint32_t pid = vpn_of(dl) == dv ? pd0 : pd1;
         ds[u] = pid * PAGE_CH + (dl & (PAGE_CH - 1));
-        ikv |= (step ? min(EPI, cur.n - cur.b) : 0u) << (8 * u);
         const uint64_t slot = (cur.first + e) & (L - 1);
         const uint64_t si = (((cur.sm >> e) & 1ull) * n64 + cur.src) * L + slot;
         const uint32_t sl = s0 + ei * cur.ncu + c;
@@ -529,6 +548,11 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p, const uint32_t*
         x[u] = *reinterpret_cast<const u32x4*>(sp);
 #endif
         want[u] = *wp;
+        // the slot's job, for its consume in the next pass
+        sq[u] = cur.q; sb[u] = cur.b; se0[u] = cur.e0; sdp[u] = cur.dpos; sncu[u] = cur.ncu;
+        sfirst[u] = cur.first; sdm[u] = cur.dm;
+        schk[u] = ring || (WIRE && cur.kind == SRC_WIRE);  // followers verify the sender's CRC
+        skv[u] = step ? min(EPI, cur.n - cur.b) : 0u;
         vmask = step ? (vmask | (1u << u)) : (vmask & ~(1u << u));
         cur.b += step ? EPI : 0u;
       }

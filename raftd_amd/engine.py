@@ -364,10 +364,12 @@ class Engine:
     def sync(self):
         self._check(self.L.rg_sync(self.h))
 
-    def timing(self, enable: bool = True, bulk_only: bool = False):
+    def timing(self, enable: bool = True, bulk_only: bool = False, every: int = 1):
         """Per-launch HIP-event timing of control_kernel / bulk_kernel (measurement only);
-        bulk_only: time bulk_kernel alone (two event records per tick instead of four)."""
-        self._check(self.L.rg_timing(self.h, (2 if bulk_only else 1) if enable else 0))
+        bulk_only: time bulk_kernel alone (two event records per tick instead of four); every: time
+        only the ticks whose count is a multiple of it."""
+        mode = (2 if bulk_only else 1) if enable else 0
+        self._check(self.L.rg_timing(self.h, mode | (max(int(every), 1) << 8) if mode else 0))
 
     def kernel_ms(self) -> dict:
         """{'control': (total_ms, launches), 'bulk': (total_ms, launches)} since timing(True)."""
