@@ -12,8 +12,9 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libraftgpu.so")
 RESOURCES = os.path.join(PKG, "kernel_resources.txt")  # per-kernel VGPR / scratch / occupancy of the last build
 SOURCES = ["raftgpu_kernels.hip", "raftgpu_admin.hip", "raftgpu_wire.hip", "raftgpu_apply.hip", "raftgpu_engine.cpp",
-           "raftgpu_rccl.cpp"]
-HEADERS = ["raftgpu_internal.h", "raftgpu_control.h", "raftgpu_wire.h", os.path.join("..", "..", "include", "raftgpu.h")]
+           "raftgpu_rccl.cpp", "raftgpu_sdma.cpp"]
+HEADERS = ["raftgpu_internal.h", "raftgpu_control.h", "raftgpu_wire.h", "raftgpu_sdma.h",
+           os.path.join("..", "..", "include", "raftgpu.h")]
 ARCH = os.environ.get("RAFTGPU_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 

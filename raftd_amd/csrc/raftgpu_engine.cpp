@@ -17,6 +17,7 @@
 
 #include "../../include/raftgpu.h"
 #include "raftgpu_internal.h"
+#include "raftgpu_sdma.h"
 #include "raftgpu_wire.h"
 
 using namespace rg;
@@ -182,6 +183,7 @@ struct rg_engine {
   uint32_t *acnt = nullptr, *accnt = nullptr;
   uint64_t *aoff = nullptr, *acoff = nullptr, *absum = nullptr;
   bool copy_kernel = true;  // RAFTGPU_APPLY_MEMCPY=1: the runtime's D2H copy instead (A/B)
+  SdmaCopier* sdma = nullptr;  // RAFTGPU_APPLY_SDMA=1: the D2H leg on an SDMA engine (raftgpu_sdma.cpp)
   uint8_t* astage = nullptr;
   uint64_t astage_bytes = 0;
   // asynchronous copy-back (rg_apply_async): per buffer a device staging area, pinned host memory,
@@ -645,6 +647,14 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   }
   e->bulk_tile = tile;
   if (const char* v = getenv("RAFTGPU_APPLY_MEMCPY")) e->copy_kernel = !(v[0] == '1');
+  if (const char* v = getenv("RAFTGPU_APPLY_SDMA"))
+    if (v[0] == '1') {
+      std::string why;
+      if (sdma_open(c.device, &e->sdma, &why) != 0) {
+        rg_destroy(e);
+        return fail(RG_EHIP, "RAFTGPU_APPLY_SDMA: " + why);
+      }
+    }
   if (launch_pool_reset(e->fring, e->npages, e->poolctl, e->stream) != hipSuccess ||
       hipStreamSynchronize(e->stream) != hipSuccess) {
     rg_destroy(e);
@@ -662,6 +672,7 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
 
 void rg_destroy(rg_engine* e) {
   if (!e) return;
+  if (e->sdma) sdma_close(e->sdma);
   for (int i = 0; i < 2; ++i) {
     if (e->gx[i]) (void)hipGraphExecDestroy(e->gx[i]);
     if (e->gg[i]) (void)hipGraphDestroy(e->gg[i]);
@@ -1649,6 +1660,7 @@ int rg_apply_async(rg_engine* e, uint32_t slot_mask, int buf) {
   const uint64_t total = tot[0], rb = a16(total * sizeof(rg_apply_entry)), need = rb + tot[1] * 16;
   if (need > e->a_dcap[buf] || need > e->a_hcap[buf]) {  // grow: the buffer's last copy must be done
     HIPCHK(hipEventSynchronize(e->a_copy[buf]));
+    if (e->sdma) sdma_wait(e->sdma, buf);
     const uint64_t nb = std::max<uint64_t>(need * 5 / 4, 1 << 20);
     if (need > e->a_dcap[buf]) {
       if (e->a_dev[buf]) {
@@ -1674,12 +1686,21 @@ int rg_apply_async(rg_engine* e, uint32_t slot_mask, int buf) {
   e->a_n[buf] = total;
   e->a_used[buf] = true;
   if (total) {
-    if (prev) HIPCHK(hipStreamWaitEvent(e->stream, e->a_copy[buf], 0));  // its last copy has read the staging
+    if (prev && e->sdma) sdma_wait(e->sdma, buf);  // its last copy has read the staging
+    else if (prev) HIPCHK(hipStreamWaitEvent(e->stream, e->a_copy[buf], 0));
     a.out_rec = e->a_dev[buf];
     a.out_pay = e->a_dev[buf] + rb;
     LAUNCH(launch_apply_gather(a, e->stream), e->stream, "apply gather");
   }
   HIPCHK(hipEventRecord(e->a_gath[buf], e->stream));
+  if (e->sdma) {  // the DMA engine takes the batch once the gather is done (no shader code on the copy)
+    if (total) {
+      HIPCHK(hipEventSynchronize(e->a_gath[buf]));
+      if (sdma_copy(e->sdma, buf, e->a_host[buf], e->a_dev[buf], need) != 0)
+        return fail(RG_EHIP, "rg_apply_async: hsa_amd_memory_async_copy failed");
+    }
+    return RG_OK;
+  }
   HIPCHK(hipStreamWaitEvent(e->copy, e->a_gath[buf], 0));
   if (total) {
     if (e->copy_kernel) {
@@ -1697,7 +1718,8 @@ int rg_apply_async(rg_engine* e, uint32_t slot_mask, int buf) {
 int rg_apply_wait(rg_engine* e, int buf, const rg_apply_entry** entries, const uint8_t** payload, uint64_t* n) {
   if (!e || buf < 0 || buf > 1 || !n) return fail(RG_EINVAL, "rg_apply_wait args");
   if (!e->a_used[buf]) return fail(RG_EINVAL, "rg_apply_wait: no rg_apply_async into this buffer");
-  HIPCHK(hipEventSynchronize(e->a_copy[buf]));
+  if (e->sdma) sdma_wait(e->sdma, buf);
+  else HIPCHK(hipEventSynchronize(e->a_copy[buf]));
   *n = e->a_n[buf];
   if (entries) *entries = (const rg_apply_entry*)e->a_host[buf];
   if (payload) *payload = e->a_host[buf] ? e->a_host[buf] + a16(e->a_n[buf] * sizeof(rg_apply_entry)) : nullptr;

@@ -9,7 +9,7 @@ for f in raftgpu_kernels.hip raftgpu_admin.hip raftgpu_wire.hip raftgpu_apply.hi
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 "$@" -c -x hip $f -o /tmp/var_${f%.*}.o
   OBJS="$OBJS /tmp/var_${f%.*}.o"
 done
-for f in raftgpu_engine.cpp raftgpu_rccl.cpp; do  # host-only runtime (raftd_amd/build.py)
+for f in raftgpu_engine.cpp raftgpu_rccl.cpp raftgpu_sdma.cpp; do  # host-only runtime (raftd_amd/build.py)
   /opt/rocm/bin/hipcc -x c++ -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -O3 -fPIC -std=c++17 "$@" -c $f -o /tmp/var_${f%.*}.o
   OBJS="$OBJS /tmp/var_${f%.*}.o"
 done
