@@ -300,10 +300,23 @@ def graph_ticks(eng, pt, pc, G, k=10, reps=4):
         eng.tick_device_n(k, pt.data_ptr(), pc.data_ptr())
     eng.sync()
     el = time.perf_counter() - t0
-    return {"value": G * k * reps / el, "unit": "group-steps/s", "ticks": k * reps, "ticks_per_graph": k,
-            "ms_per_step": el * 1e3 / (k * reps),
-            "note": "rg_tick_device_n(k, RG_TICKN_GRAPH): k ticks per hipGraphLaunch, parameter blocks written "
-                    "into the graph's pinned slots before each launch; host wall time"}
+    out = {"value": G * k * reps / el, "unit": "group-steps/s", "ticks": k * reps, "ticks_per_graph": k,
+           "ms_per_step": el * 1e3 / (k * reps),
+           "note": "rg_tick_device_n(k, RG_TICKN_GRAPH): k ticks per hipGraphLaunch, parameter blocks written "
+                   "into the graph's pinned slots before each launch; host wall time"}
+    if eng.cfg["payload_bytes"] == 0 and eng.cfg["replicas"] <= 4:  # the resident control kernel
+        kr = 32
+        eng.tick_device_n(kr, pt.data_ptr(), pc.data_ptr(), resident=True)
+        eng.sync()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            eng.tick_device_n(kr, pt.data_ptr(), pc.data_ptr(), resident=True)
+        eng.sync()
+        el = time.perf_counter() - t0
+        out["resident"] = {"value": G * kr * reps / el, "ms_per_step": el * 1e3 / (kr * reps), "ticks_per_launch": kr,
+                           "note": "rg_tick_device_n(k, RG_TICKN_RESIDENT): k ticks in one launch of the resident "
+                                   "control kernel (metadata-only engines); host wall time"}
+    return out
 
 
 def pmc_traffic(kernel="bulk_kernel", wire=False, spread=False):

@@ -285,6 +285,11 @@ int rg_tick_device(rg_engine* e, const rg_tick_input* in);
  * back first, as a tick-input batch would; the last tick's slab must not be one); it is captured
  * on first use and again whenever k, the inputs, the stream or the parity of the tick count change. */
 #define RG_TICKN_GRAPH 1u
+/* RG_TICKN_RESIDENT (metadata-only engines, payload_bytes 0, one rank, replicas <= 4): the k ticks
+ * in ONE launch of a resident control kernel — a workgroup holds every replica of 64 groups, so a
+ * tick's messages stay inside it, and a workgroup barrier replaces the kernel boundary between
+ * ticks. Same results as k rg_tick_device calls; k <= 64; the other conditions as for a graph. */
+#define RG_TICKN_RESIDENT 2u
 int rg_tick_device_n(rg_engine* e, const rg_tick_input* in, uint32_t k, uint32_t flags);
 /* Launch work on this HIP stream (hipStream_t) instead of the engine's own. */
 int rg_set_stream(rg_engine* e, void* stream);

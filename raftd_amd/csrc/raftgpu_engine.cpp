@@ -1350,9 +1350,52 @@ static int tick_graph(rg_engine* e, const rg_tick_input* in, uint32_t k) {
   return RG_OK;
 }
 
+// RG_TICKN_RESIDENT: the k ticks of a metadata-only one-rank engine in ONE launch of the resident
+// control kernel (a workgroup per 64 groups holding all their replicas, a barrier between ticks)
+static int tick_resident(rg_engine* e, const rg_tick_input* in, uint32_t k) {
+  if (!e->g_dtp) {
+    RGCHK(dalloc(e, &e->g_dtp, 2ull * G_MAXK * sizeof(TickParams)));
+    if (hipHostMalloc((void**)&e->g_htp, 2ull * G_MAXK * sizeof(TickParams), 0) != hipSuccess)
+      return fail(RG_ENOMEM, "hipHostMalloc (graph parameter slots)");
+    for (int i = 0; i < 2; ++i) HIPCHK(hipEventCreateWithFlags(&e->g_ev[i], hipEventDisableTiming));
+  }
+  const uint32_t set = e->g_flip;
+  if (e->g_used[set]) HIPCHK(hipEventSynchronize(e->g_ev[set]));  // its copy has read the slots
+  for (uint32_t i = 0; i < k; ++i) {
+    TickParams p = params_at(e, e->t + i);
+    p.flags = in->flags;
+    p.prop_target = in->prop_target;
+    p.prop_count = in->prop_count;
+    p.campaign = in->campaign;
+    p.isolate = in->isolate;
+    seal(p);
+    e->g_htp[set * G_MAXK + i] = p;
+  }
+  TickParams* ds = e->g_dtp + set * G_MAXK;
+  HIPCHK(hipMemcpyAsync(ds, e->g_htp + set * G_MAXK, k * sizeof(TickParams), hipMemcpyHostToDevice, e->stream));
+  HIPCHK(hipEventRecord(e->g_ev[set], e->stream));
+  LAUNCH(launch_control_resident(ds, k, &e->poolctl->param_err, e->c.replicas, e->c.groups, e->stream), e->stream,
+         "control_resident_kernel");
+  e->g_used[set] = true;
+  e->g_flip ^= 1u;
+  e->g_valid = false;  // the graph path's slots were reused
+  e->t += k;
+  return RG_OK;
+}
+
 int rg_tick_device_n(rg_engine* e, const rg_tick_input* in, uint32_t k, uint32_t flags) {
-  if (!e || !in || k == 0 || (flags & ~RG_TICKN_GRAPH)) return fail(RG_EINVAL, "rg_tick_device_n args");
+  if (!e || !in || k == 0 || (flags & ~(RG_TICKN_GRAPH | RG_TICKN_RESIDENT)) ||
+      (flags & RG_TICKN_GRAPH && flags & RG_TICKN_RESIDENT))
+    return fail(RG_EINVAL, "rg_tick_device_n args");
   if (in->prop_target && !in->prop_count) return fail(RG_EINVAL, "prop_target without prop_count");
+  if (flags & RG_TICKN_RESIDENT) {
+    if (e->c.payload_bytes || e->wire || e->c.replicas > 4 || k > G_MAXK || e->staged || e->rd_staged ||
+        e->cc_staged || e->timing)
+      return fail(RG_EINVAL, "rg_tick_device_n: resident ticks need a metadata-only one-rank engine with at most 4 "
+                             "replicas, nothing staged, timing off, k <= 64");
+    HIPCHK(hipSetDevice(e->c.device));
+    return tick_resident(e, in, k);
+  }
   if (!(flags & RG_TICKN_GRAPH)) {
     for (uint32_t i = 0; i < k; ++i) RGCHK(tick_impl(e, in, true));
     return RG_OK;

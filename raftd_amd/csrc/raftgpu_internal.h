@@ -346,6 +346,9 @@ RG_HD_INLINE uint64_t stream_byte(const uint32_t* pt, uint32_t PTS, uint32_t q, 
 // host-side launchers (raftgpu_kernels.hip)
 // control_kernel<R> over nrep lanes; *p: the tick's parameter block in device memory
 hipError_t launch_control(const TickParams* p, uint32_t* perr, uint32_t R, uint32_t nrep, hipStream_t s);
+// k ticks of a metadata-only one-rank engine in one launch (p = k consecutive sealed blocks)
+hipError_t launch_control_resident(const TickParams* p, uint32_t k, uint32_t* perr, uint32_t R, uint32_t G,
+                                   hipStream_t s);
 hipError_t launch_pool(const PoolParams& p, hipStream_t s);
 // every page free, every replica's stream empty (bootstrap)
 hipError_t launch_pool_reset(uint32_t* fring, uint64_t npages, PoolCtl* ctl, hipStream_t s);

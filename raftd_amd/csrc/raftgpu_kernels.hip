@@ -18,6 +18,7 @@
 //   sender's ring (no staging copy); DESIGN.md §2 explains the two payload banks that keep the
 //   same-launch reads and rewrites disjoint.
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 #include "raftgpu_control.h"
@@ -77,6 +78,69 @@ __global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_MINWAVES) control_kernel(
   Ctl<R> c(cp, q);
 #endif
   c.run();
+}
+
+// ---- the resident multi-tick control kernel (metadata-only, one-rank engines). A
+// workgroup holds every replica of 64 groups — wave w is slot w of groups [64·b, 64·b + 64) — so a
+// tick's messages never leave it, and k ticks run in one launch with a workgroup barrier between
+// them instead of a kernel boundary: the state, outboxes and ring words a tick reads were written
+// by this workgroup one tick earlier and are still in its CU's caches. Block i of pp is tick t0 + i
+// (the host seals each); all k checksums are verified before anything is dereferenced.
+__device__ __forceinline__ bool tp_check(const TickParams* pp, uint32_t i) {
+  const TickParams* pc = pp + i;
+  asm volatile("" : "+s"(pc));
+  typedef __attribute__((address_space(1))) const uint64_t gu64;
+  gu64* wv = (gu64*)pc;
+  const uint32_t lane = threadIdx.x & 63u;
+  uint64_t h = lane < TP_WORDS ? tp_term(wv[lane], lane) : 0ull;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)h, off, 64);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(h >> 32), off, 64);
+    h += ((uint64_t)hi << 32) | lo;
+  }
+  return h == wv[TP_WORDS];
+}
+
+template <int R>
+__global__ void __launch_bounds__(64 * R, 1) control_resident_kernel(const TickParams* __restrict__ pp, uint32_t k,
+                                                                     uint32_t* perr) {
+  for (uint32_t i = 0; i < k; ++i)
+    if (!tp_check(pp, i)) {  // the same verdict in every wave: the whole workgroup leaves together
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        printf("raftgpu: control_resident_kernel parameter block %u checksum mismatch: launch skipped\n", i);
+        atomicOr(perr, 1u);
+      }
+      return;
+    }
+  CTickParams* cp = (CTickParams*)pp;
+  const uint32_t G = cp[0].G, w = threadIdx.x >> 6, g = blockIdx.x * 64 + (threadIdx.x & 63u);
+  const uint32_t q = w * G + g;
+  for (uint32_t i = 0; i < k; ++i) {
+    if (g < G) {
+      Ctl<R> c(cp[i], q);
+      c.run();
+    }
+    __syncthreads();  // tick i's outboxes and state, written by this workgroup, before tick i + 1 reads them
+  }
+}
+
+hipError_t launch_control_resident(const TickParams* p, uint32_t k, uint32_t* perr, uint32_t R, uint32_t G,
+                                   hipStream_t s) {
+#ifdef RG_DEV_NO_CONTROL
+  (void)p; (void)k; (void)perr; (void)R; (void)G; (void)s;
+  return hipErrorInvalidValue;
+#endif
+  dim3 grid((G + 63) / 64), block(64 * R);
+  switch (R) {
+    case 1: hipLaunchKernelGGL(control_resident_kernel<1>, grid, block, 0, s, p, k, perr); break;
+    case 2: hipLaunchKernelGGL(control_resident_kernel<2>, grid, block, 0, s, p, k, perr); break;
+    case 3: hipLaunchKernelGGL(control_resident_kernel<3>, grid, block, 0, s, p, k, perr); break;
+    case 4: hipLaunchKernelGGL(control_resident_kernel<4>, grid, block, 0, s, p, k, perr); break;
+    // R > 4: a control wave needs a SIMD of its own (occupancy 1), and a CU has four
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
 
 hipError_t launch_control(const TickParams* p, uint32_t* perr, uint32_t R, uint32_t nrep, hipStream_t s) {
@@ -321,6 +385,14 @@ __device__ __forceinline__ void next_replica(const BulkParams& p, Cursor& cur, c
   set_job<LG, WIRE>(p, cur, jb);
 }
 
+// the entry info word {slot crc, stream position} (and the sender-CRC check) at ring slot `slot`,
+// info bank `bank`
+__device__ __forceinline__ void put_info_at(const BulkParams& p, uint32_t q, uint64_t slot, uint64_t bank, uint32_t crc,
+                                            uint32_t pos, bool check, uint32_t want) {
+  p.info[(bank * p.nrep + q) * p.L + slot] = make_uint2(crc, pos);
+  if (check && want != crc) atomicOr(p.crc_err + q, ERR_CRC);
+}
+
 // the entry info word {slot crc, stream position} (and the sender-CRC check) of job entry e
 __device__ __forceinline__ void put_info(const BulkParams& p, uint32_t q, uint64_t first, uint64_t dm, uint32_t e,
                                          uint32_t crc, uint32_t pos, bool check, uint32_t want) {
@@ -460,16 +532,19 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p, const uint32_t*
   // so a pass of small jobs (C5: one entry per job) fills all BULK_U slots instead of one.
   u32x4 x[BULK_U];
   uint32_t ds[BULK_U], want[BULK_U];
-  uint32_t sq[BULK_U], sb[BULK_U], se0[BULK_U], sdp[BULK_U], sncu[BULK_U], skv[BULK_U];
-  uint64_t sfirst[BULK_U], sdm[BULK_U];
-  bool schk[BULK_U];
+  // sm[u] packs the small fields: step's first entry b (7 bits) | job start e0 << 7 | chunks per
+  // entry ncu << 14 | entries in the step << 21 | check << 28 (fewer scalars: fewer SGPR spills)
+  // ss[u] = the ring slot of the step's first entry, sbk[u] = the step's destination bank bits (one
+  // per entry, EPI of them)
+  typedef std::conditional_t<(EPI <= 32), uint32_t, uint64_t> Banks;
+  uint32_t sq[BULK_U], sdp[BULK_U], sm[BULK_U], ss[BULK_U];
+  Banks sbk[BULK_U];
 #pragma unroll
   for (int u = 0; u < BULK_U; ++u) {
     x[u] = u32x4{0, 0, 0, 0};
     ds[u] = want[u] = 0;
-    sq[u] = sb[u] = se0[u] = sdp[u] = sncu[u] = skv[u] = 0;
-    sfirst[u] = sdm[u] = 0;
-    schk[u] = false;
+    sq[u] = sdp[u] = sm[u] = ss[u] = 0;
+    sbk[u] = 0;
   }
   // Every slot issues exactly two loads per pass (payload chunk + sender CRC word), redirected to a
   // dummy address when the slot has no work, so the number of memory operations between a load
@@ -482,8 +557,11 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p, const uint32_t*
       {  // consume slot u: store, CRC, info, verify (no entries: no stores). A stream's Cmd is followed
         // by zeros up to its chunk boundary (every writer copies whole chunks), and lanes past a Cmd's
         // chunks contribute nothing, so the CRC is the slot CRC.
-        const bool valid = ei < skv[u];
-        const bool act = valid && c < sncu[u];
+        const uint32_t sb = sm[u] & 0x7Fu, se0 = (sm[u] >> 7) & 0x7Fu, sncu = (sm[u] >> 14) & 0x7Fu;
+        const uint32_t skv = (sm[u] >> 21) & 0x7Fu;
+        const bool schk = (sm[u] >> 28) & 1u;
+        const bool valid = ei < skv;
+        const bool act = valid && c < sncu;
         if (act) {
 #ifdef RG_BULK_PLAIN_STORE
           *reinterpret_cast<u32x4*>(p.pool + (uint64_t)ds[u] * 16) = x[u];
@@ -497,9 +575,9 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p, const uint32_t*
 #endif
         if constexpr (LG > 0) v = xor_lanes<LG>(crc.shift(v));  // raw(slot) = XOR_c Z^(after c)(raw c)
         if (valid && c == 0) {
-          const uint32_t e = sb[u] + ei;
-          put_info(p, sq[u], sfirst[u], sdm[u], e, act ? (p.crc_const ^ v) : 0u, sdp[u] + (e - se0[u]) * sncu[u],
-                   schk[u] && act, want[u]);
+          const uint32_t e = sb + ei;
+          put_info_at(p, sq[u], (ss[u] + ei) & (L - 1), (sbk[u] >> ei) & 1u, act ? (p.crc_const ^ v) : 0u,
+                      sdp[u] + (e - se0) * sncu, schk && act, want[u]);
         }
       }
       {  // issue the job's next step (or an empty step) into slot u
@@ -549,10 +627,12 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p, const uint32_t*
 #endif
         want[u] = *wp;
         // the slot's job, for its consume in the next pass
-        sq[u] = cur.q; sb[u] = cur.b; se0[u] = cur.e0; sdp[u] = cur.dpos; sncu[u] = cur.ncu;
-        sfirst[u] = cur.first; sdm[u] = cur.dm;
-        schk[u] = ring || (WIRE && cur.kind == SRC_WIRE);  // followers verify the sender's CRC
-        skv[u] = step ? min(EPI, cur.n - cur.b) : 0u;
+        sq[u] = cur.q; sdp[u] = cur.dpos;
+        ss[u] = (uint32_t)((cur.first + cur.b) & (L - 1));
+        sbk[u] = (Banks)(cur.dm >> (cur.b & 63u));
+        sm[u] = (cur.b & 0x7Fu) | ((cur.e0 & 0x7Fu) << 7) | ((cur.ncu & 0x7Fu) << 14) |
+                ((step ? min(EPI, cur.n - cur.b) : 0u) << 21) |
+                ((ring || (WIRE && cur.kind == SRC_WIRE)) ? 1u << 28 : 0u);  // followers verify the sender's CRC
         vmask = step ? (vmask | (1u << u)) : (vmask & ~(1u << u));
         cur.b += step ? EPI : 0u;
       }

@@ -348,12 +348,14 @@ class Engine:
         self._check(self.L.rg_tick_device(self.h, C.byref(ti)))
 
     def tick_device_n(self, k, prop_target_ptr=0, prop_count_ptr=0, campaign_ptr=0, isolate_ptr=0, flags=0,
-                      graph=True):
+                      graph=True, resident=False):
         """rg_tick_device_n: k ticks with the same device-resident inputs; graph: one captured HIP graph
-        of the k ticks per call (RG_TICKN_GRAPH)."""
+        of the k ticks per call (RG_TICKN_GRAPH); resident: one launch of the resident control kernel
+        (RG_TICKN_RESIDENT, metadata-only engines)."""
         ti = TickInput(prop_target_ptr or None, prop_count_ptr or None, campaign_ptr or None,
                        isolate_ptr or None, flags, 0)
-        self._check(self.L.rg_tick_device_n(self.h, C.byref(ti), k, 1 if graph else 0))
+        mode = 2 if resident else (1 if graph else 0)
+        self._check(self.L.rg_tick_device_n(self.h, C.byref(ti), k, mode))
 
     def set_stream(self, stream_handle: int):
         self._check(self.L.rg_set_stream(self.h, C.c_void_p(stream_handle)))

@@ -60,3 +60,42 @@ def test_graph_refuses_what_it_cannot_capture():
     e.propose([(0, 0, [b"x"])])
     with pytest.raises(RgError):
         e.tick_device_n(2)  # a caller batch is staged
+
+
+@pytest.mark.parametrize("R", [1, 3, 4])
+def test_resident_ticks_equal_single_ticks(R):
+    """RG_TICKN_RESIDENT (metadata-only engines): k ticks in one launch of the resident control kernel
+    equal k rg_tick_device calls — elections from scratch inside the launch, message loss, isolation,
+    snapshots and compaction; a group count that leaves the last workgroup partly empty."""
+    G, K = 100, 16
+    cfg = dict(groups=G, replicas=R, log_capacity=128, payload_bytes=0, max_entries_per_msg=16,
+               snapshot_entries=30, compaction_overhead=4, drop_ppm=30000, seed=0x7E5 + R)
+    a, b = make("gpu", **cfg), make("gpu", **cfg)
+    for e in (a, b):
+        e.bootstrap()
+    rng = np.random.default_rng(R)
+    pt = torch.tensor(rng.integers(0, R, G), dtype=torch.uint8, device="cuda")
+    pc = torch.tensor(rng.integers(1, 9, G), dtype=torch.int32, device="cuda")
+    iso = torch.tensor((rng.random(G * R) < 0.02).astype(np.uint8), device="cuda")
+    for rep in range(6):
+        for _ in range(K):
+            a.tick_device(pt.data_ptr(), pc.data_ptr(), 0, iso.data_ptr())
+        b.tick_device_n(K, pt.data_ptr(), pc.data_ptr(), 0, iso.data_ptr(), resident=True)
+        a.sync()
+        b.sync()
+        assert a.t == b.t
+        assert a.replica_array().tobytes() == b.replica_array().tobytes(), rep
+        for rid in range(0, G * R, 11):
+            for d in range(R):
+                assert a.msgs(rid, d) == b.msgs(rid, d), (rep, rid, d)
+    assert a.digest() == b.digest()
+    v = b.replica_array()
+    assert (v["role"] == 2).sum() > G // 2 and v["snap_index"].max() > 0  # elected, and snapshots ran
+
+
+def test_resident_refuses_payload_engines():
+    from raftd_amd.engine import RgError
+    e = make("gpu", groups=8, replicas=3, log_capacity=64, payload_bytes=16, max_entries_per_msg=4)
+    e.bootstrap()
+    with pytest.raises(RgError):
+        e.tick_device_n(4, resident=True)
