@@ -960,28 +960,39 @@ struct Ctl {
   }
 
   // ---- Handle (A.3): message k from slot src (remote: it came over the wire from another rank)
-  RG_FN void handle(uint32_t src, uint32_t k, bool remote) {
+  // words 0 and 1 (type, ids, term) up front; the others where a handler uses them
+  // (RG_CTL_HDRBATCH: all eight in one round trip; at R >= 6 there is no room for them)
+#ifdef RG_CTL_HDRBATCH
+  static constexpr int NB = R <= 5 ? 8 : 2;
+#else
+  static constexpr int NB = 2;
+#endif
+  struct Hdr {
+    uint64_t w[NB];
+    uint64_t mt0;  // a local Replicate's first inline word (a uniform Replicate needs only it)
+  };
+  RG_FN const uint64_t* hdr_ptr(uint32_t src, uint32_t k, bool remote) const {
+    return (remote ? p.rhdr : p.hdr_in) + (((uint64_t)src * R + s) * p.K + k) * p.G + g;
+  }
+  // one round trip: the header words and, for a local message, its first inline word (for other
+  // messages the slot holds stale words, which nothing reads)
+  RG_FN void load_hdr(uint32_t src, uint32_t k, bool remote, Hdr& o) const {
+    const uint64_t plane = (uint64_t)R * R * p.K * p.G;
+    const uint64_t* h = hdr_ptr(src, k, remote);
+#pragma unroll
+    for (int x = 0; x < NB; ++x) o.w[x] = h[(uint64_t)x * plane];
+    o.mt0 = remote ? 0ull : p.mt_in[((((uint64_t)src * R + s) * p.K + k) * p.E) * p.G + g];
+  }
+  RG_FN void handle(uint32_t src, uint32_t k, bool remote, const Hdr& hd) {
     RG_T0(t0);
-    handle_(src, k, remote);
+    handle_(src, k, remote, hd);
     RG_ACC(5, t0);
   }
-  RG_FN void handle_(uint32_t src, uint32_t k, bool remote) {
+  RG_FN void handle_(uint32_t src, uint32_t k, bool remote, const Hdr& hd) {
     const uint64_t plane = (uint64_t)R * R * p.K * p.G;
-    const uint64_t* h = (remote ? p.rhdr : p.hdr_in) + (((uint64_t)src * R + s) * p.K + k) * p.G + g;
-    // words 0 and 1 (type, ids, term) up front; the others where a handler uses them
-    // (RG_CTL_HDRBATCH: all eight in one round trip; at R >= 6 there is no room for them)
-#ifdef RG_CTL_HDRBATCH
-    constexpr int NB = R <= 5 ? 8 : 2;
-#else
-    constexpr int NB = 2;
-#endif
-    uint64_t hb[NB];
-#pragma unroll
-    for (int x = 0; x < NB; ++x) hb[x] = h[(uint64_t)x * plane];
-    // a local Replicate's first inline word travels in the same round trip (a uniform Replicate
-    // needs only it); for other messages the slot holds stale words, which nothing reads
-    const uint64_t mt0 = remote ? 0ull : p.mt_in[((((uint64_t)src * R + s) * p.K + k) * p.E) * p.G + g];
-    auto hw = [&](int x) -> uint64_t { return x < NB ? hb[x < NB ? x : 0] : h[(uint64_t)x * plane]; };
+    const uint64_t* h = hdr_ptr(src, k, remote);
+    const uint64_t mt0 = hd.mt0;
+    auto hw = [&](int x) -> uint64_t { return x < NB ? hd.w[x < NB ? x : 0] : h[(uint64_t)x * plane]; };
     const uint64_t w0 = hw(0);
     const uint64_t mterm = hw(1);
     const uint32_t type = (uint32_t)(w0 & 0xFF);
@@ -1096,16 +1107,42 @@ struct Ctl {
     const bool in_camp = p.campaign && p.campaign[ri()];
     const uint32_t in_cc = p.cc_in ? p.cc_in[gi] : 0u;
     const uint64_t in_rd = p.read_ctx ? p.read_ctx[ri()] : 0ull;
-    for (uint32_t src = 0; src < R; ++src) {
-      if (src == s) continue;
-      const bool remote = pl_remote(p.pl, src, s, g);
-      uint32_t cnt = sel_get<R>(cnt_pf, src);
-      if (cnt > p.K) {  // never produced by a sender (unpack_kernel clamps received counts): ERR_WIRE
-        RG_OOB("RG_BOUNDS control q=%u src=%u remote=%d cnt=%u > K=%u\n", q, src, (int)remote, cnt, p.K);
+    sfor<0, R>([&](auto jc) {
+      constexpr int src = decltype(jc)::value;
+      if (cnt_pf[src] > p.K) {  // never produced by a sender (unpack_kernel clamps received counts): ERR_WIRE
+        RG_OOB("RG_BOUNDS control q=%u src=%u cnt=%u > K=%u\n", q, (uint32_t)src, cnt_pf[src], p.K);
         err |= ERR_WIRE;
-        cnt = 0;
+        cnt_pf[src] = 0;
       }
-      for (uint32_t k = 0; k < cnt; ++k) handle(src, k, remote);
+    });
+    // The inbox in sender order, software-pipelined: the next message's header is loaded before the
+    // current one is handled (the inbox is read-only in this launch), so a lane waits about one
+    // round trip for its whole inbox instead of one per message.
+    auto next_msg = [&](uint32_t src, uint32_t k, uint32_t& ns, uint32_t& nk) -> bool {
+      for (uint32_t x = src, y = k + 1; x < R; ++x, y = 0) {
+        if (x == s) continue;
+        if (y < sel_get<R>(cnt_pf, x)) {
+          ns = x;
+          nk = y;
+          return true;
+        }
+      }
+      return false;
+    };
+    uint32_t cs = 0, ck = 0;
+    bool have = next_msg(0, ~0u, cs, ck);
+    Hdr cur{};
+    if (have) load_hdr(cs, ck, pl_remote(p.pl, cs, s, g), cur);
+    while (have) {
+      uint32_t ns = 0, nk = 0;
+      const bool more = next_msg(cs, ck, ns, nk);
+      Hdr nxt{};
+      if (more) load_hdr(ns, nk, pl_remote(p.pl, ns, s, g), nxt);
+      handle(cs, ck, pl_remote(p.pl, cs, s, g), cur);
+      cur = nxt;
+      cs = ns;
+      ck = nk;
+      have = more;
     }
     RG_STAMP(1);
     if (in_camp) handle_node_election();

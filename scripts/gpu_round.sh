@@ -22,6 +22,7 @@ for what in ${STEPS:-smoke parity tests bench wire rehearse}; do
     copywg) step copywg 900 bash scripts/e2e_copywg.sh ;;
     ab) step ab 700 env LIBS="raftd_amd/libraftgpu.so ablib/onejob.so" bash scripts/ab_lib.sh --steps 20 --warmup 5 ;;
     ab_c5) step ab_c5 700 env LIBS="raftd_amd/libraftgpu.so ablib/onejob.so" bash scripts/ab_lib.sh --groups 1048576 --entries 1 --steps 10 --warmup 3 ;;
+    rehearse_c) step rehearse_c 400 python bench.py --placement spread --wire-all --exchange c --no-cpu-baseline --steps 10 --warmup 3 ;;
     sdma) step sdma 300 env RAFTGPU_APPLY_SDMA=1 python bench.py --steps 12 --warmup 3 --no-cpu-baseline ;;
     wire) step bench_wire 400 python bench.py --wire-all --no-cpu-baseline ;;
     rehearse) step rehearse 400 env RAFTD_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
