@@ -147,6 +147,10 @@ struct rg_engine {
   uint64_t t = 0;
   int bulk_grid = 0;
   uint32_t bulk_tile = 1;
+  // small jobs share a bulk ring pass (bulk_kernel<.., MJ = true>): when Replicates and proposal
+  // batches carry at most 16 entries (max_entries_per_msg), jobs are small; the 64-entry jobs of
+  // full batches run faster without it. RAFTGPU_BULK_MULTIJOB=0/1 overrides (A/B).
+  bool bulk_mj = false;
   uint64_t bytes = 0;
   std::vector<void*> allocs;
   // per-launch event timing (rg_timing): bit 0 control_kernel, bit 1 bulk_kernel; a start/end
@@ -387,6 +391,7 @@ static BulkParams bulk_params_at(rg_engine* e, uint64_t tk) {
   b.wire = e->recv;
   b.wire_bytes = e->recv_bytes;
   b.nslab = e->c.num_slabs;
+  b.multijob = e->bulk_mj ? 1u : 0u;
   return b;
 }
 
@@ -647,6 +652,8 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   }
   e->bulk_tile = tile;
   if (const char* v = getenv("RAFTGPU_APPLY_MEMCPY")) e->copy_kernel = !(v[0] == '1');
+  e->bulk_mj = c.max_entries_per_msg <= 16;
+  if (const char* v = getenv("RAFTGPU_BULK_MULTIJOB")) e->bulk_mj = v[0] == '1';
   if (const char* v = getenv("RAFTGPU_APPLY_SDMA"))
     if (v[0] == '1') {
       std::string why;

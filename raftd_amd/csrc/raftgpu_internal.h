@@ -276,6 +276,7 @@ struct BulkParams {
   PoolCtl* poolctl;      // block 0 publishes limit = tail (the pool kernel of this tick has run)
   uint64_t wire_bytes;   // bytes of `wire` in use (job bounds checks)
   uint32_t nslab;
+  uint32_t multijob;     // small jobs share a ring pass (bulk_kernel<.., MJ>; the engine's choice)
 };
 
 // pool_kernel (after control, before bulk): frees the stream pages control released, allocates the

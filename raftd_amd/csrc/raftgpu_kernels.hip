@@ -497,7 +497,10 @@ __device__ void vjob(const BulkParams& p, const uint32_t* __restrict__ pt, const
 // P = 16 << LG bytes per lane group: 2^LG lanes per entry (16 B each), 64 >> LG entries per step.
 // WIRE: the engine exchanges messages with other ranks (SRC_WIRE jobs, slab rows per replica);
 // one-rank engines run the variant without those paths.
-template <int LG, bool WIRE>
+// MJ: small jobs share a pass — a ring slot takes the tile's next replica's job as soon as the current
+// one is issued (C5's one-entry jobs: bulk 3.99 -> 1.67 ms). It costs the 64-entry jobs of the
+// 64K x 3 workload 8% (1.26 -> 1.36 ms, r03f A/B), so the host picks it per engine (launch_bulk).
+template <int LG, bool WIRE, bool MJ>
 __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p, const uint32_t* __restrict__ pt) {
   constexpr uint32_t NCH = 1u << LG, EPI = 64u >> LG, P = 16u << LG;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -581,10 +584,9 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p, const uint32_t*
         }
       }
       {  // issue the job's next step (or an empty step) into slot u
-#ifndef RG_BULK_ONEJOB
         // a uniform job fully issued: take the tile's next replica now if that costs no round trip
-        if (cur.live && cur.uni && cur.b >= cur.n && cur.j + 1 >= cur.njl && cur.m) next_replica<LG, WIRE>(p, cur, tj);
-#endif
+        if (MJ && cur.live && cur.uni && cur.b >= cur.n && cur.j + 1 >= cur.njl && cur.m)
+          next_replica<LG, WIRE>(p, cur, tj);
         const bool step = cur.live && cur.uni && cur.b < cur.n;
         const uint32_t e = cur.b + ei;
         const bool valid = step && e < cur.n;
@@ -655,39 +657,40 @@ int bulk_lds_bytes(uint32_t P) {
   return P ? (int)((CRC_T_WORDS + CRC_N_WORDS + (P / 16) * CRC_SH_STRIDE + CRC_ZP_WORDS) * 4) : 16;
 }
 
-template <bool W, class F>
+template <bool W, bool MJ, class F>
 static hipError_t with_bulk_w(uint32_t P, F f) {
 #ifdef RG_DEV_ONLY_LG  // development builds: one payload size only (ISA / resource checks)
-  if (W || lg_of(P) != RG_DEV_ONLY_LG) return hipErrorInvalidValue;
-  return f(bulk_kernel<RG_DEV_ONLY_LG, false>);
+  if (W || MJ || lg_of(P) != RG_DEV_ONLY_LG) return hipErrorInvalidValue;
+  return f(bulk_kernel<RG_DEV_ONLY_LG, false, false>);
 #endif
   switch (lg_of(P)) {
-    case 0: return f(bulk_kernel<0, W>);
-    case 1: return f(bulk_kernel<1, W>);
-    case 2: return f(bulk_kernel<2, W>);
-    case 3: return f(bulk_kernel<3, W>);
-    case 4: return f(bulk_kernel<4, W>);
-    case 5: return f(bulk_kernel<5, W>);
-    case 6: return f(bulk_kernel<6, W>);
+    case 0: return f(bulk_kernel<0, W, MJ>);
+    case 1: return f(bulk_kernel<1, W, MJ>);
+    case 2: return f(bulk_kernel<2, W, MJ>);
+    case 3: return f(bulk_kernel<3, W, MJ>);
+    case 4: return f(bulk_kernel<4, W, MJ>);
+    case 5: return f(bulk_kernel<5, W, MJ>);
+    case 6: return f(bulk_kernel<6, W, MJ>);
     default: return hipErrorInvalidValue;
   }
 }
 template <class F>
-static hipError_t with_bulk(uint32_t P, bool wire, F f) {
+static hipError_t with_bulk(uint32_t P, bool wire, bool mj, F f) {
   if (!P) return hipSuccess;  // metadata-only engines have no payload stage (tick_impl)
-  return wire ? with_bulk_w<true>(P, f) : with_bulk_w<false>(P, f);
+  if (mj) return wire ? with_bulk_w<true, true>(P, f) : with_bulk_w<false, true>(P, f);
+  return wire ? with_bulk_w<true, false>(P, f) : with_bulk_w<false, false>(P, f);
 }
 
 int bulk_blocks_per_cu(uint32_t P) {
   int n = 0;
-  const hipError_t r = with_bulk(P, false, [&](auto k) {
+  const hipError_t r = with_bulk(P, false, false, [&](auto k) {
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 256, bulk_lds_bytes(P));
   });
   return (r == hipSuccess && n > 0) ? n : 1;
 }
 
 hipError_t launch_bulk(const BulkParams& p, const uint32_t* pt, hipStream_t s, int grid) {
-  return with_bulk(p.P, p.wire_mode != 0, [&](auto k) {
+  return with_bulk(p.P, p.wire_mode != 0, p.multijob != 0, [&](auto k) {
     hipLaunchKernelGGL(k, dim3(grid), dim3(256), bulk_lds_bytes(p.P), s, p, pt);
     return hipGetLastError();
   });
