@@ -527,6 +527,10 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p, const uint32_t*
   cur.uni = true;
   cur.live = next_job<LG, WIRE>(p, cur, tj, stride, ntiles);
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  // Two ring walks: MJ keeps each slot's job in scalars and lets a slot take the tile's next
+  // replica mid-pass (small jobs); without MJ the slots of a pass share one job (per-pass scalars,
+  // fewer SGPRs: the 64-entry jobs of full batches run faster so).
+  if constexpr (MJ) {
   // ring slot u: payload chunk, destination pool chunk, sender's slot CRC (per lane). The job a slot's
   // step belongs to is wave-uniform and kept per slot (scalars): replica sq, first index sfirst, bank
   // mask sdm, first entry of the step sb, job start se0 / destination chunk sdp / chunks per entry
@@ -585,7 +589,7 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p, const uint32_t*
       }
       {  // issue the job's next step (or an empty step) into slot u
         // a uniform job fully issued: take the tile's next replica now if that costs no round trip
-        if (MJ && cur.live && cur.uni && cur.b >= cur.n && cur.j + 1 >= cur.njl && cur.m)
+        if (cur.live && cur.uni && cur.b >= cur.n && cur.j + 1 >= cur.njl && cur.m)
           next_replica<LG, WIRE>(p, cur, tj);
         const bool step = cur.live && cur.uni && cur.b < cur.n;
         const uint32_t e = cur.b + ei;
@@ -645,6 +649,112 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p, const uint32_t*
     }
     if (cur.live && cur.b >= cur.n) cur.live = next_job<LG, WIRE>(p, cur, tj, stride, ntiles);
   } while (rfl((uint32_t)(vmask != 0 || cur.live)));
+  } else {
+  // ring slot u: payload chunk, destination pool chunk, sender's slot CRC (per lane); the entries
+  // each slot's step holds are wave-uniform: 8 bits per slot in one scalar (ikv / ckv), so the
+  // per-lane flags need no registers of their own (r03: 99 -> 95 VGPRs, occupancy 4 -> 5)
+  u32x4 x[BULK_U];
+  uint32_t ds[BULK_U], want[BULK_U];
+#pragma unroll
+  for (int u = 0; u < BULK_U; ++u) {
+    x[u] = u32x4{0, 0, 0, 0};
+    ds[u] = want[u] = 0;
+  }
+  // Every slot issues exactly two loads per pass (payload chunk + sender CRC word), redirected to a
+  // dummy address when the slot has no work, so the number of memory operations between a load
+  // and its use is the same on every path and the compiler's vmcnt waits keep the ring in flight.
+  // A pass never spans two jobs (the cursor moves once per pass), so the slots consumed in a pass
+  // all belong to the job `pj` the previous pass issued.
+  const uint8_t* dummy = reinterpret_cast<const uint8_t*>(p.crc_tab + CRC_ZERO_OFF);  // 16 zero bytes
+  uint32_t vmask = 0;
+  uint32_t iq = 0, ib = 0, ie0 = 0, idp = 0, incu = 0, ikv = 0;  // the job of the pass being issued (for its consume)
+  bool ichk = false;
+  uint64_t ifirst = 0, idm = 0;
+  do {
+    const uint32_t cq = iq, cb = ib, ce0 = ie0, cdp = idp, cncu = incu, ckv = ikv;
+    const bool cchk = ichk;
+    const uint64_t cfirst = ifirst, cdm = idm;
+    iq = cur.q; ib = cur.b; ie0 = cur.e0; idp = cur.dpos; incu = cur.ncu; ifirst = cur.first; idm = cur.dm;
+    ichk = cur.kind == SRC_RING || (WIRE && cur.kind == SRC_WIRE);  // followers verify the sender's CRC
+    ikv = 0;
+#pragma unroll
+    for (int u = 0; u < BULK_U; ++u) {
+      {  // consume slot u: store, CRC, info, verify (fl = 0 for an empty slot: no stores). A stream's
+        // Cmd is followed by zeros up to its chunk boundary (every writer copies whole chunks), and
+        // lanes past a Cmd's chunks contribute nothing, so the CRC is the slot CRC.
+        const bool valid = ei < ((ckv >> (8 * u)) & 0xFFu);
+        const bool act = valid && c < cncu;
+        if (act) {
+#ifdef RG_BULK_PLAIN_STORE
+          *reinterpret_cast<u32x4*>(p.pool + (uint64_t)ds[u] * 16) = x[u];
+#else
+          __builtin_nontemporal_store(x[u], reinterpret_cast<u32x4*>(p.pool + (uint64_t)ds[u] * 16));
+#endif
+        }
+        uint32_t v = 0;
+#ifndef RG_BULK_NOCRC
+        v = crc.raw16(make_uint4(x[u].x, x[u].y, x[u].z, x[u].w));
+#endif
+        if constexpr (LG > 0) v = xor_lanes<LG>(crc.shift(v));  // raw(slot) = XOR_c Z^(after c)(raw c)
+        if (valid && c == 0) {
+          const uint32_t e = cb + u * EPI + ei;
+          put_info(p, cq, cfirst, cdm, e, act ? (p.crc_const ^ v) : 0u, cdp + (e - ce0) * cncu, cchk && act, want[u]);
+        }
+      }
+      {  // issue the job's next step (or an empty step) into slot u
+        const bool step = cur.live && cur.uni && cur.b < cur.n;
+        const uint32_t e = cur.b + ei;
+        const bool valid = step && e < cur.n;
+        const bool act = valid && c < cur.ncu;
+        const bool ring = cur.kind == SRC_RING, wire = WIRE && (cur.kind == SRC_WIRE || cur.kind == SRC_WIRE_PROP);
+        // destination chunks of this step: at most 64, so at most two stream pages (page ids by
+        // scalar loads: uniform addresses)
+        const uint32_t d0 = cur.dpos + (cur.b - cur.e0) * cur.ncu, dv = vpn_of(d0);
+        const uint32_t dl = d0 + ei * cur.ncu + c;
+        uint32_t pd0 = 0, pd1 = 0, ps0 = 0, ps1 = 0;
+        const uint32_t s0 = (uint32_t)cur.spos + cur.b * cur.ncu, sv = vpn_of(s0);
+        if (step && cur.ncu) {
+          const uint64_t dr = (uint64_t)cur.q * p.PTS;
+          pd0 = pt[dr + (dv & PTSM)];
+          pd1 = pt[dr + ((dv + 1) & PTSM)];
+          if (ring) {
+            const uint64_t sr = (uint64_t)cur.src * p.PTS;
+            ps0 = pt[sr + (sv & PTSM)];
+            ps1 = pt[sr + ((sv + 1) & PTSM)];
+          }
+        }
+        const uint32_t pid = vpn_of(dl) == dv ? pd0 : pd1;
+        ds[u] = pid * PAGE_CH + (dl & (PAGE_CH - 1));
+        ikv |= (step ? min(EPI, cur.n - cur.b) : 0u) << (8 * u);
+        const uint64_t slot = (cur.first + e) & (L - 1);
+        const uint64_t si = (((cur.sm >> e) & 1ull) * n64 + cur.src) * L + slot;
+        const uint32_t sl = s0 + ei * cur.ncu + c;
+        const uint8_t* sp = ring ? p.pool + ((uint64_t)(vpn_of(sl) == sv ? ps0 : ps1) * PAGE_BYTES) + ((sl & (PAGE_CH - 1)) << 4)
+                            : wire ? p.wire + cur.spos + 16ull * cur.src + 16ull * (e * cur.ncu + c)
+                            : cur.kind == SRC_CMD
+                                ? p.cmds + (uint64_t)cur.src * p.cmd_cap + 16ull * ((uint32_t)cur.spos + (e - cur.e0) * cur.ncu + c)
+                                : p.slabs + (((uint64_t)cur.src * rows + cur.g) * p.E + e) * P + c * 16;
+        sp = act ? sp : dummy;
+        const uint32_t* wp = (ring && act) ? &p.info[si].x
+                             : (wire && act) ? reinterpret_cast<const uint32_t*>(p.wire + cur.spos + 16ull * e + 8)
+                                             : reinterpret_cast<const uint32_t*>(dummy);
+#ifdef RG_BULK_NT_LOAD  // ablation: non-temporal loads (r01: 1.115 vs 1.090 ms plain)
+        x[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(sp));
+#else  // temporal: the second follower's read of the same leader entries hits L2 / Infinity Cache
+        x[u] = *reinterpret_cast<const u32x4*>(sp);
+#endif
+        want[u] = *wp;
+        vmask = step ? (vmask | (1u << u)) : (vmask & ~(1u << u));
+        cur.b += step ? EPI : 0u;
+      }
+    }
+    if (cur.live && !cur.uni && vmask == 0) {  // a non-uniform job once the ring has drained
+      vjob<LG, WIRE>(p, pt, cur, crc);
+      cur.b = cur.n;
+    }
+    if (cur.live && cur.b >= cur.n) cur.live = next_job<LG, WIRE>(p, cur, tj, stride, ntiles);
+  } while (rfl((uint32_t)(vmask != 0 || cur.live)));
+  }
 }
 
 static int lg_of(uint32_t P) {
