@@ -89,10 +89,14 @@ def test_apply_copyback_full_size():
         assert int(recs[k]["crc"]) == zlib.crc32(bytes(pay[k]))
 
 
-def test_async_copyback_matches_sync():
+@pytest.mark.parametrize("d2h", ["kernel", "sdma"])
+def test_async_copyback_matches_sync(d2h, monkeypatch):
     """rg_apply_async / rg_apply_wait (double-buffered, copy stream) return exactly what
-    rg_apply_committed returns for the same tick, also when a buffer is re-used two ticks later."""
+    rg_apply_committed returns for the same tick, also when a buffer is re-used two ticks later —
+    with the copy kernel (default) and with the D2H leg on an SDMA engine (RAFTGPU_APPLY_SDMA=1)."""
     from test_gpu_parity import CHAOS, random_inputs
+    if d2h == "sdma":
+        monkeypatch.setenv("RAFTGPU_APPLY_SDMA", "1")  # read by rg_create
     cfg = dict(CHAOS, groups=8, replicas=3, payload_bytes=64, max_entries_per_msg=16, seed=4)
     eng = make("gpu", **cfg)
     eng.bootstrap()
