@@ -650,8 +650,6 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p, const uint32_t*
     if (cur.live && cur.b >= cur.n) cur.live = next_job<LG, WIRE>(p, cur, tj, stride, ntiles);
   } while (rfl((uint32_t)(vmask != 0 || cur.live)));
   } else {
-  // page ids of the current destination / source page pair (scalars; see the issue step)
-  uint32_t c_dq = ~0u, c_dv = 0, c_pd0 = 0, c_pd1 = 0, c_sq = ~0u, c_sv = 0, c_ps0 = 0, c_ps1 = 0;
   // ring slot u: payload chunk, destination pool chunk, sender's slot CRC (per lane); the entries
   // each slot's step holds are wave-uniform: 8 bits per slot in one scalar (ikv / ckv), so the
   // per-lane flags need no registers of their own (r03: 99 -> 95 VGPRs, occupancy 4 -> 5)
@@ -716,31 +714,6 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p, const uint32_t*
         uint32_t pd0 = 0, pd1 = 0, ps0 = 0, ps1 = 0;
         const uint32_t s0 = (uint32_t)cur.spos + cur.b * cur.ncu, sv = vpn_of(s0);
         if (step && cur.ncu) {
-#ifndef RG_BULK_NO_PTCACHE
-          // a step covers a quarter page or less: consecutive steps mostly need the page ids the
-          // last one loaded, so they stay in scalars and are reloaded (one wait) only when the
-          // replica or the page changes (the page tables are fixed during the launch)
-          if (cur.q != c_dq || dv != c_dv) {
-            const uint64_t dr = (uint64_t)cur.q * p.PTS;
-            c_dq = cur.q;
-            c_dv = dv;
-            c_pd0 = pt[dr + (dv & PTSM)];
-            c_pd1 = pt[dr + ((dv + 1) & PTSM)];
-          }
-          pd0 = c_pd0;
-          pd1 = c_pd1;
-          if (ring) {
-            if (cur.src != c_sq || sv != c_sv) {
-              const uint64_t sr = (uint64_t)cur.src * p.PTS;
-              c_sq = cur.src;
-              c_sv = sv;
-              c_ps0 = pt[sr + (sv & PTSM)];
-              c_ps1 = pt[sr + ((sv + 1) & PTSM)];
-            }
-            ps0 = c_ps0;
-            ps1 = c_ps1;
-          }
-#else
           const uint64_t dr = (uint64_t)cur.q * p.PTS;
           pd0 = pt[dr + (dv & PTSM)];
           pd1 = pt[dr + ((dv + 1) & PTSM)];
@@ -749,7 +722,6 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p, const uint32_t*
             ps0 = pt[sr + (sv & PTSM)];
             ps1 = pt[sr + ((sv + 1) & PTSM)];
           }
-#endif
         }
         const uint32_t pid = vpn_of(dl) == dv ? pd0 : pd1;
         ds[u] = pid * PAGE_CH + (dl & (PAGE_CH - 1));
