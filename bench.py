@@ -240,6 +240,33 @@ def e2e_with_apply(eng, tick, G, steps, slot_mask=1, serial=False):
                     "is PCIe-bound, so this is min(tick rate, PCIe rate)"}
 
 
+def hand_off(eng, tick, G, steps, slot_mask=1):
+    """Ticks with dragonboat's per-step hand-off: after every tick one rg_get_update
+    (slot-0 replicas = one node's share; UPDATE_ALL: hard states + appended entries to persist,
+    committed entries to apply, snapshot events, ready reads, all in one staging pass and one D2H)
+    and one rg_commit_update(RG_COMMIT_APPLIED), the host reading the sections in place. Host wall time."""
+    import ctypes as C
+    import torch
+    from raftd_amd.engine import Update, UPDATE_ALL, COMMIT_APPLIED
+    u = Update()
+    nb = ne = 0
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tick()
+        if eng.L.rg_get_update(eng.h, slot_mask, UPDATE_ALL, C.byref(u)) != 0:
+            raise RuntimeError(f"rg_get_update: {eng.L.rg_last_error().decode()}")
+        ne += u.n_entries + u.n_committed
+        nb += u.entry_payload_bytes + u.committed_payload_bytes
+        if eng.L.rg_commit_update(eng.h, C.byref(u), COMMIT_APPLIED) != 0:
+            raise RuntimeError(f"rg_commit_update: {eng.L.rg_last_error().decode()}")
+    el = time.perf_counter() - t0
+    return {"value": G * steps / el, "unit": "group-steps/s", "steps": steps, "ms_per_step": el * 1e3 / steps,
+            "entry_rows_per_step": ne / steps, "payload_bytes_per_step": nb / steps,
+            "note": "tick + rg_get_update(slot-0 replicas, UPDATE_ALL) + rg_commit_update(RG_COMMIT_APPLIED) per "
+                    "step: the single GetUpdate / Commit hand-off, sections read in place from pinned memory"}
+
+
 def ingest(eng, G, E, P, steps, seed=7):
     """The client ingest path (SURVEY §8b rg_propose ≈ NodeHost.Propose): every step each leader's
     E Cmds of P bytes (host memory, pageable, the way a cgo shim hands Go []byte over) are staged by
@@ -473,6 +500,7 @@ def main():
         # kernels slow each other down when they share the GPU
         e2e["serial"] = e2e_with_apply(eng, lambda: one_step(None), G, steps=max(4, min(args.steps, 12)),
                                        serial=True)
+        e2e["hand_off"] = hand_off(eng, lambda: one_step(None), G, steps=max(3, min(args.steps, 8)))
     apply = apply_copyback(eng, torch)
     ing = ingest(eng, G, E, P, steps=max(3, min(args.steps, 8))) if args.ingest and not spread and P else None
     copy_gbs = hbm_copy_ceiling(eng)

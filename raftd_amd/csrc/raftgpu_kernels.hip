@@ -500,8 +500,13 @@ __device__ void vjob(const BulkParams& p, const uint32_t* __restrict__ pt, const
 // MJ: small jobs share a pass — a ring slot takes the tile's next replica's job as soon as the current
 // one is issued (C5's one-entry jobs: bulk 3.99 -> 1.67 ms). It costs the 64-entry jobs of the
 // 64K x 3 workload 8% (1.26 -> 1.36 ms, r03f A/B), so the host picks it per engine (launch_bulk).
+#ifdef RG_BULK_WPE  // A/B: hold the compiler to RG_BULK_WPE waves per SIMD
+#define RG_BULK_ATTR __attribute__((amdgpu_waves_per_eu(RG_BULK_WPE, RG_BULK_WPE)))
+#else
+#define RG_BULK_ATTR
+#endif
 template <int LG, bool WIRE, bool MJ>
-__global__ void __launch_bounds__(256) bulk_kernel(BulkParams p, const uint32_t* __restrict__ pt) {
+__global__ void __launch_bounds__(256) RG_BULK_ATTR bulk_kernel(BulkParams p, const uint32_t* __restrict__ pt) {
   constexpr uint32_t NCH = 1u << LG, EPI = 64u >> LG, P = 16u << LG;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const uint32_t shw = CRC_T_WORDS + CRC_N_WORDS + NCH * CRC_SH_STRIDE;
@@ -677,6 +682,25 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p, const uint32_t*
     iq = cur.q; ib = cur.b; ie0 = cur.e0; idp = cur.dpos; incu = cur.ncu; ifirst = cur.first; idm = cur.dm;
     ichk = cur.kind == SRC_RING || (WIRE && cur.kind == SRC_WIRE);  // followers verify the sender's CRC
     ikv = 0;
+#ifndef RG_BULK_STEP_PT
+    // the pass's page ids: its BULK_U steps are consecutive in the job, at most 64 chunks each, so the
+    // pass covers at most BULK_U * 64 = PAGE_CH destination (and source) chunks: two pages each. Four
+    // scalar loads per pass, issued together, instead of four per step.
+    static_assert(BULK_U * 64 <= PAGE_CH, "a pass spans at most two stream pages");
+    const uint32_t qdv = vpn_of(cur.dpos + (cur.b - cur.e0) * cur.ncu);
+    const uint32_t qsv = vpn_of((uint32_t)cur.spos + cur.b * cur.ncu);
+    uint32_t qd0 = 0, qd1 = 0, qs0 = 0, qs1 = 0;
+    if (cur.live && cur.uni && cur.b < cur.n && cur.ncu) {
+      const uint64_t dr = (uint64_t)cur.q * p.PTS;
+      qd0 = pt[dr + (qdv & PTSM)];
+      qd1 = pt[dr + ((qdv + 1) & PTSM)];
+      if (cur.kind == SRC_RING) {
+        const uint64_t sr = (uint64_t)cur.src * p.PTS;
+        qs0 = pt[sr + (qsv & PTSM)];
+        qs1 = pt[sr + ((qsv + 1) & PTSM)];
+      }
+    }
+#endif
 #pragma unroll
     for (int u = 0; u < BULK_U; ++u) {
       {  // consume slot u: store, CRC, info, verify (fl = 0 for an empty slot: no stores). A stream's
@@ -709,10 +733,12 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p, const uint32_t*
         const bool ring = cur.kind == SRC_RING, wire = WIRE && (cur.kind == SRC_WIRE || cur.kind == SRC_WIRE_PROP);
         // destination chunks of this step: at most 64, so at most two stream pages (page ids by
         // scalar loads: uniform addresses)
-        const uint32_t d0 = cur.dpos + (cur.b - cur.e0) * cur.ncu, dv = vpn_of(d0);
+        const uint32_t d0 = cur.dpos + (cur.b - cur.e0) * cur.ncu;
         const uint32_t dl = d0 + ei * cur.ncu + c;
+        const uint32_t s0 = (uint32_t)cur.spos + cur.b * cur.ncu;
+#ifdef RG_BULK_STEP_PT  // A/B: the step's own page ids (r03h product)
+        const uint32_t dv = vpn_of(d0), sv = vpn_of(s0);
         uint32_t pd0 = 0, pd1 = 0, ps0 = 0, ps1 = 0;
-        const uint32_t s0 = (uint32_t)cur.spos + cur.b * cur.ncu, sv = vpn_of(s0);
         if (step && cur.ncu) {
           const uint64_t dr = (uint64_t)cur.q * p.PTS;
           pd0 = pt[dr + (dv & PTSM)];
@@ -723,6 +749,9 @@ __global__ void __launch_bounds__(256) bulk_kernel(BulkParams p, const uint32_t*
             ps1 = pt[sr + ((sv + 1) & PTSM)];
           }
         }
+#else
+        const uint32_t dv = qdv, sv = qsv, pd0 = qd0, pd1 = qd1, ps0 = qs0, ps1 = qs1;
+#endif
         const uint32_t pid = vpn_of(dl) == dv ? pd0 : pd1;
         ds[u] = pid * PAGE_CH + (dl & (PAGE_CH - 1));
         ikv |= (step ? min(EPI, cur.n - cur.b) : 0u) << (8 * u);
