@@ -263,8 +263,10 @@ def hand_off(eng, tick, G, steps, slot_mask=1):
     el = time.perf_counter() - t0
     return {"value": G * steps / el, "unit": "group-steps/s", "steps": steps, "ms_per_step": el * 1e3 / steps,
             "entry_rows_per_step": ne / steps, "payload_bytes_per_step": nb / steps,
-            "note": "tick + rg_get_update(slot-0 replicas, UPDATE_ALL) + rg_commit_update(RG_COMMIT_APPLIED) per "
-                    "step: the single GetUpdate / Commit hand-off, sections read in place from pinned memory"}
+            "note": "tick + rg_get_update(UPDATE_ALL, slot mask 1) + rg_commit_update(RG_COMMIT_APPLIED) per step: "
+                    "the single GetUpdate / Commit hand-off (entries to persist: every replica of the engine; committed "
+                    "entries, snapshots, reads: the slot-0 replicas), sections read in place from pinned memory; "
+                    "PCIe-bound at full batches"}
 
 
 def ingest(eng, G, E, P, steps, seed=7):
