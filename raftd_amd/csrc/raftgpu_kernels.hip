@@ -271,7 +271,27 @@ struct Cursor {
 struct TileJobs {  // per lane: job count and first job of replica qb + lane
   uint32_t nj;
   Job j0;
+  uint32_t pd0, pd1, ps0, ps1;  // MJ: page ids of that job's first step
 };
+
+// the page ids a job's first step needs: destination pages vpn(dpos), +1; a ring job's source
+// pages vpn(spos + e0 * ncu), +1 (the page tables are fixed during the launch)
+__device__ __forceinline__ void first_step_pages(const BulkParams& p, const uint32_t* __restrict__ pt, uint32_t q,
+                                                 const Job& jb, uint32_t& pd0, uint32_t& pd1, uint32_t& ps0,
+                                                 uint32_t& ps1) {
+  const uint32_t PTSM = p.PTS - 1, ncu = (jb.meta >> 21) & 0x7F, e0 = (jb.meta >> 8) & 0xFF;
+  const uint32_t kind = (jb.meta >> 16) & 0xF, dv = vpn_of(jb.dpos);
+  const uint64_t dr = (uint64_t)q * p.PTS;
+  pd0 = pt[dr + (dv & PTSM)];
+  pd1 = pt[dr + ((dv + 1) & PTSM)];
+  ps0 = ps1 = 0;
+  if (kind == SRC_RING && jb.src < p.nrep) {
+    const uint32_t sv = vpn_of((uint32_t)jb.spos + e0 * ncu);
+    const uint64_t sr = (uint64_t)jb.src * p.PTS;
+    ps0 = pt[sr + (sv & PTSM)];
+    ps1 = pt[sr + ((sv + 1) & PTSM)];
+  }
+}
 
 // Tiles interleave the slots of one block of groups: tile t = (group block t / R, slot t % R), so
 // the R replicas of the same groups are walked by neighbouring waves at the same time and the two
@@ -285,7 +305,9 @@ __device__ __forceinline__ uint32_t bulk_ntiles(const BulkParams& p) {
 #endif
 }
 
-__device__ __forceinline__ void load_tile(const BulkParams& p, Cursor& cur, TileJobs& tj) {
+template <bool MJ = false>
+__device__ __forceinline__ void load_tile(const BulkParams& p, Cursor& cur, TileJobs& tj,
+                                          const uint32_t* __restrict__ pt = nullptr) {
   const uint32_t lane = lane_id();
 #ifdef RG_TILE_SLOTMAJOR
   cur.qb = cur.t * p.tile;
@@ -299,6 +321,10 @@ __device__ __forceinline__ void load_tile(const BulkParams& p, Cursor& cur, Tile
   tj.nj = valid ? p.jcnt[q] : 0u;
   tj.j0 = Job{};
   if (tj.nj) tj.j0 = load_job(p, q, 0);
+  tj.pd0 = tj.pd1 = tj.ps0 = tj.ps1 = 0;
+  if constexpr (MJ) {  // one more round trip per tile instead of one per job (C5: one-entry jobs)
+    if (tj.nj) first_step_pages(p, pt, q, tj.j0, tj.pd0, tj.pd1, tj.ps0, tj.ps1);
+  }
   cur.m = __ballot(tj.nj != 0);
   cur.j = 0;
   cur.njl = 0;
@@ -339,9 +365,9 @@ __device__ __forceinline__ void set_job(const BulkParams& p, Cursor& cur, const 
 // Move the cursor one position: the replica's next job, the tile's next replica, or the next
 // tile (whose descriptors arrive in one round trip; that pass issues nothing). A job with no
 // entries left to write simply yields an empty pass. Returns false once the wave is done.
-template <int LG, bool WIRE>
+template <int LG, bool WIRE, bool MJ = false>
 __device__ __forceinline__ bool next_job(const BulkParams& p, Cursor& cur, TileJobs& tj, uint32_t stride,
-                                         uint32_t ntiles) {
+                                         uint32_t ntiles, const uint32_t* __restrict__ pt = nullptr) {
   if (cur.j + 1 < cur.njl) {
     ++cur.j;
     set_job<LG, WIRE>(p, cur, load_job(p, cur.q, cur.j));
@@ -360,7 +386,7 @@ __device__ __forceinline__ bool next_job(const BulkParams& p, Cursor& cur, TileJ
   } else {
     cur.t += stride;
     if (cur.t >= ntiles) return false;
-    load_tile(p, cur, tj);
+    load_tile<MJ>(p, cur, tj, pt);
     cur.b = 0;  // two statements: the chained form kept Cursor in scratch
     cur.n = 0;
     cur.uni = true;
@@ -526,11 +552,11 @@ __global__ void __launch_bounds__(256) RG_BULK_ATTR bulk_kernel(BulkParams p, co
   TileJobs tj{};
   cur.t = rfl(blockIdx.x * waves + (threadIdx.x >> 6));
   if (cur.t >= ntiles) return;
-  load_tile(p, cur, tj);
+  load_tile<MJ>(p, cur, tj, pt);
   cur.b = 0;  // two statements: the chained form kept Cursor in scratch
   cur.n = 0;
   cur.uni = true;
-  cur.live = next_job<LG, WIRE>(p, cur, tj, stride, ntiles);
+  cur.live = next_job<LG, WIRE, MJ>(p, cur, tj, stride, ntiles, pt);
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   // Two ring walks: MJ keeps each slot's job in scalars and lets a slot take the tile's next
   // replica mid-pass (small jobs); without MJ the slots of a pass share one job (per-pass scalars,
@@ -607,6 +633,18 @@ __global__ void __launch_bounds__(256) RG_BULK_ATTR bulk_kernel(BulkParams p, co
         const uint32_t dl = d0 + ei * cur.ncu + c;
         uint32_t pd0 = 0, pd1 = 0, ps0 = 0, ps1 = 0;
         const uint32_t s0 = (uint32_t)cur.spos + cur.b * cur.ncu, sv = vpn_of(s0);
+#ifndef RG_BULK_MJ_NOPF
+        // a replica's first job (cur.j 0) came from the tile load, which also fetched its first
+        // step's page ids (lane q - qb of tj): no scalar round trip when this step is that step's pages
+        if (step && cur.ncu && cur.j == 0 && dv == vpn_of(cur.dpos) &&
+            (!ring || sv == vpn_of((uint32_t)cur.spos + cur.e0 * cur.ncu))) {
+          const uint32_t l = cur.q - cur.qb;
+          pd0 = __builtin_amdgcn_readlane(tj.pd0, l);
+          pd1 = __builtin_amdgcn_readlane(tj.pd1, l);
+          ps0 = __builtin_amdgcn_readlane(tj.ps0, l);
+          ps1 = __builtin_amdgcn_readlane(tj.ps1, l);
+        } else
+#endif
         if (step && cur.ncu) {
           const uint64_t dr = (uint64_t)cur.q * p.PTS;
           pd0 = pt[dr + (dv & PTSM)];
@@ -652,7 +690,7 @@ __global__ void __launch_bounds__(256) RG_BULK_ATTR bulk_kernel(BulkParams p, co
       vjob<LG, WIRE>(p, pt, cur, crc);
       cur.b = cur.n;
     }
-    if (cur.live && cur.b >= cur.n) cur.live = next_job<LG, WIRE>(p, cur, tj, stride, ntiles);
+    if (cur.live && cur.b >= cur.n) cur.live = next_job<LG, WIRE, true>(p, cur, tj, stride, ntiles, pt);
   } while (rfl((uint32_t)(vmask != 0 || cur.live)));
   } else {
   // ring slot u: payload chunk, destination pool chunk, sender's slot CRC (per lane); the entries
