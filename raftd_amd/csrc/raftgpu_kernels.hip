@@ -633,7 +633,7 @@ __global__ void __launch_bounds__(256) RG_BULK_ATTR bulk_kernel(BulkParams p, co
         const uint32_t dl = d0 + ei * cur.ncu + c;
         uint32_t pd0 = 0, pd1 = 0, ps0 = 0, ps1 = 0;
         const uint32_t s0 = (uint32_t)cur.spos + cur.b * cur.ncu, sv = vpn_of(s0);
-#ifndef RG_BULK_MJ_NOPF
+#ifdef RG_BULK_MJ_PF
         // a replica's first job (cur.j 0) came from the tile load, which also fetched its first
         // step's page ids (lane q - qb of tj): no scalar round trip when this step is that step's pages
         if (step && cur.ncu && cur.j == 0 && dv == vpn_of(cur.dpos) &&
