@@ -322,9 +322,13 @@ __device__ __forceinline__ void load_tile(const BulkParams& p, Cursor& cur, Tile
   tj.j0 = Job{};
   if (tj.nj) tj.j0 = load_job(p, q, 0);
   tj.pd0 = tj.pd1 = tj.ps0 = tj.ps1 = 0;
+#ifdef RG_BULK_MJ_PF
   if constexpr (MJ) {  // one more round trip per tile instead of one per job (C5: one-entry jobs)
     if (tj.nj) first_step_pages(p, pt, q, tj.j0, tj.pd0, tj.pd1, tj.ps0, tj.ps1);
   }
+#else
+  (void)pt;
+#endif
   cur.m = __ballot(tj.nj != 0);
   cur.j = 0;
   cur.njl = 0;
