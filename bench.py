@@ -241,6 +241,29 @@ def e2e_with_apply(eng, tick, G, steps, slot_mask=1, serial=False):
                     + "; PCIe-bound at full batches"}
 
 
+def copyback_schedules(eng, tick, G, steps, slot_mask=1):
+    """The copy-back schedules of DESIGN.md §7, measured warm and in both orders: one warm run grows
+    both apply buffers (device staging and pinned host memory) before anything is timed, then serial,
+    overlapped, overlapped, serial. The headline is the faster schedule (the mean of its two runs);
+    every run is listed, so an order effect shows as a gap between a schedule's two runs."""
+    e2e_with_apply(eng, tick, G, steps=2)  # warm: both buffers grow here, outside the timed runs
+    runs = []
+    for serial in (True, False, False, True):
+        r = e2e_with_apply(eng, tick, G, steps=steps, serial=serial, slot_mask=slot_mask)
+        runs.append({k: r[k] for k in ("schedule", "ms_per_step", "pcie_GBps")})
+    mean = {sch: sum(x["ms_per_step"] for x in runs if x["schedule"] == sch) / 2 for sch in ("serial", "overlapped")}
+    best = min(mean, key=mean.get)
+    out = e2e_with_apply(eng, tick, G, steps=steps, serial=best == "serial", slot_mask=slot_mask)
+    out.update(ms_per_step=mean[best], value=G / (mean[best] / 1e3),
+               pcie_GBps=out["bytes_per_step"] / (mean[best] / 1e3) / 1e9,
+               schedules_ms_per_step=mean, runs=runs,
+               order_spread={sch: abs(runs[0 if sch == "serial" else 1]["ms_per_step"] -
+                                      runs[3 if sch == "serial" else 2]["ms_per_step"]) / mean[sch]
+                             for sch in mean},
+               note=out["note"] + "; headline = the faster schedule, mean of its two runs (warm, both orders)")
+    return out
+
+
 def hand_off(eng, tick, G, steps, slot_mask=1):
     """Ticks with dragonboat's per-step hand-off: after every tick one rg_get_update
     (slot-0 replicas = one node's share; UPDATE_ALL: hard states + appended entries to persist,
@@ -498,11 +521,8 @@ def main():
     errs, drops = int((va["err"] != 0).sum()), int(va["drops"].sum())
     e2e = None
     if not spread:
-        # the copy-back contract: each tick's copy finishes before the next tick, since
-        # copy kernels (blit or SDMA) and tick kernels slow each other down when they share the GPU;
-        # the overlapped schedule is kept beside it as the A/B
-        e2e = e2e_with_apply(eng, lambda: one_step(None), G, steps=max(4, min(args.steps, 12)), serial=True)
-        e2e["overlapped"] = e2e_with_apply(eng, lambda: one_step(None), G, steps=max(4, min(args.steps, 12)))
+        e2e = copyback_schedules(eng, lambda: one_step(None), G, steps=max(4, min(args.steps, 12)))
+        hand_off(eng, lambda: one_step(None), G, steps=2)  # warm: the pinned update buffer grows here
         e2e["hand_off"] = hand_off(eng, lambda: one_step(None), G, steps=max(3, min(args.steps, 8)))
     apply = apply_copyback(eng, torch)
     ing = ingest(eng, G, E, P, steps=max(3, min(args.steps, 8))) if args.ingest and not spread and P else None

@@ -108,12 +108,15 @@ typedef struct rg_config {
   /* Cmd storage: every replica appends its entries' Cmds, each at its own length
    * rounded up to 16 B, to a payload stream mapped onto 4-KiB pages of one engine-wide pool. */
   uint32_t max_cmd_bytes;       /* longest Cmd (raft/state_machine.go:126-145 hands any Cmd []byte back):
-                                   payload_bytes .. 8191; 0 = payload_bytes. payload_bytes is the Cmd
-                                   size the payload kernel's lane groups and the benchmark's synthetic
-                                   Cmds use; longer Cmds take several groups */
+                                   payload_bytes .. 16 MiB (16,777,216); 0 = payload_bytes. payload_bytes
+                                   is the Cmd size the payload kernel's lane groups and the benchmark's
+                                   synthetic Cmds use; longer Cmds take several groups. Terms are < 2^36
+                                   (the Cmd length shares the term word) */
   uint32_t stream_pages;        /* pages one replica's live stream may span (power of two); an append
                                    beyond it is refused like one beyond log_capacity.
-                                   0 = twice a full log of payload_bytes Cmds */
+                                   0 = twice a full log of payload_bytes Cmds, plus room for two of the
+                                   longest Cmds (2·(ceil(max_cmd_bytes / 4096) + 1) pages) when
+                                   max_cmd_bytes > payload_bytes, rounded up to a power of two */
   uint32_t pool_pages;          /* 4-KiB pages in the pool (<= 2^24); 0 = a full log of payload_bytes
                                    Cmds per replica, capped at 2^24. An empty pool poisons the engine:
                                    RG_ERR_POOL in the affected replicas, rg_pool_stats().fail */
@@ -314,14 +317,17 @@ int rg_read_replicas(rg_engine* e, uint32_t first_rid, uint32_t n, rg_replica_vi
  * cleared). */
 int rg_read_msgs(rg_engine* e, uint32_t rid, uint32_t dst, rg_msg_view* out, uint32_t cap, uint64_t* terms);
 /* Log entries first_index .. first_index+n-1 of replica rid (must lie in (marker, last]); payload (if
- * not NULL): entry k's Cmd at payload + k * max_cmd_bytes. */
+ * not NULL, at most n * max_cmd_bytes bytes are written): the Cmds of the application entries, packed
+ * back to back in entry order at their own lengths (out[k].len bytes each; entries with an empty Cmd
+ * and ConfigChange entries take none). */
 int rg_read_entries(rg_engine* e, uint32_t rid, uint64_t first_index, uint32_t n, rg_entry_view* out,
                     uint8_t* payload);
-/* Replace replica rid's state and its log (marker, last]: terms[k], types[k] (RG_ENTRY_*, | RG_ENTRY_EMPTY),
- * payloads = one max_cmd_bytes row per entry of which lens[k] bytes are the Cmd (lens NULL:
- * payload_bytes for every application entry with a payload). The replica's Cmds move to a fresh
- * payload stream (RG_ENOMEM: the page pool is empty; RG_EFULL: longer than stream_pages). Not for a
- * replica whose messages of the last tick are still to be delivered. */
+/* Replace replica rid's state and its log (marker, last]: terms[k] (< 2^36), types[k] (RG_ENTRY_*,
+ * | RG_ENTRY_EMPTY), payloads = the Cmds packed back to back in entry order: an application entry that
+ * is not RG_ENTRY_EMPTY takes lens[k] bytes (lens NULL: payload_bytes), any other entry none; a
+ * ConfigChange entry's lens[k] is its descriptor. The replica's Cmds move to a fresh payload stream
+ * (RG_ENOMEM: the page pool is empty; RG_EFULL: longer than stream_pages). Not for a replica whose
+ * messages of the last tick are still to be delivered. */
 int rg_import_replica(rg_engine* e, uint32_t rid, const rg_replica_view* v, const uint64_t* terms,
                       const uint32_t* types, const uint8_t* payloads, const uint32_t* lens);
 /* Enqueue a message as if `rid_src` had emitted it in the last tick (delivered next tick). */
@@ -389,12 +395,15 @@ int rg_rccl_close(rg_transport* t);
  * RG_EFULL is returned. Synchronous. */
 int rg_apply_committed(rg_engine* e, uint32_t slot_mask, rg_apply_entry* entries, uint8_t* payload, uint64_t cap,
                        uint64_t* n, uint64_t pay_cap, uint64_t* pay_bytes);
-/* Asynchronous, double-buffered copy-back (the same batch as rg_apply_committed): the gather kernel
- * writes the last tick's applied entries straight into engine-owned, host-mapped pinned buffer `buf`
- * (0 or 1) over PCIe, on the engine's stream right after the tick (before the next tick can reuse
- * their log slots): no staging copy and no copy engine contending with the next ticks. Its counts
- * are read back without a host synchronisation when the buffer is large enough from the last use
- * (the buffer grows, with one synchronisation, when it is not). */
+/* Asynchronous, double-buffered copy-back (the same batch as rg_apply_committed) into engine-owned
+ * pinned buffer `buf` (0 or 1). On the engine's stream right after the tick (before a later tick can
+ * reuse the window's log slots and pages): the count and scan kernels, then ONE host synchronisation
+ * for the batch's size (the buffers grow when it exceeds them), then the gather kernel into device
+ * staging. The D2H leg then runs on the engine's copy stream — a copy kernel of a few workgroups
+ * streaming into host-mapped memory (default), the runtime's hipMemcpyAsync
+ * (RAFTGPU_APPLY_MEMCPY=1) or an SDMA engine (RAFTGPU_APPLY_SDMA=1) — so the caller may issue the
+ * next tick before it completes. Whether that overlap pays depends on the platform (DESIGN.md §7,
+ * INTEGRATION.md "Copy-back schedule"). */
 int rg_apply_async(rg_engine* e, uint32_t slot_mask, int buf);
 /* Wait for buffer `buf`'s gather; *entries / *payload (rg_apply_entry.off into it) point into
  * engine-owned pinned memory, valid until the next rg_apply_async into `buf`; *n = the count. */
@@ -418,9 +427,9 @@ int rg_snapshot_events(rg_engine* e, uint32_t slot_mask, rg_snapshot_event* even
  * the snapshot events (rg_snapshot_events) and the reads made ready (rg_read_index_results) — with
  * one host synchronisation for the counts and one D2H copy of all sections. The pointers are
  * engine-owned pinned memory, valid until the next rg_get_update or rg_destroy. slot_mask selects
- * the replicas whose committed entries, snapshot events and reads are reported (the node's slots);
- * the persistence section covers every replica whose log or hard state changed (every replica and
- * its whole log window with RG_UPDATE_FULL_STATE: a checkpoint). Sections not asked for are empty. */
+ * the replicas every section reports (the node's slots): their persistence records (those whose log
+ * or hard state changed; all of them with their whole log window under RG_UPDATE_FULL_STATE: a
+ * checkpoint), committed entries, snapshot events and reads. Sections not asked for are empty. */
 #define RG_UPDATE_PERSIST 1u     /* EntriesToSave + State (rg_persist_collect) */
 #define RG_UPDATE_COMMITTED 2u   /* CommittedEntries for Update (rg_apply_committed) */
 #define RG_UPDATE_SNAPSHOTS 4u   /* snapshot events (rg_snapshot_events) */

@@ -24,6 +24,7 @@ typedef struct {
   uint64_t term;
   uint32_t type, len, crc;
   uint32_t pos; /* payload stream position (16-B chunks) of its Cmd in the replica's log */
+  uint64_t off; /* in an outbox or the proposal staging: byte offset of its Cmd in that arena */
 } ent_t;
 
 typedef struct {
@@ -36,8 +37,8 @@ typedef struct {
   uint32_t emitted[OR_MAX_R]; /* emissions per destination incl. lost ones (loss hash input) */
   msg_t* m;                   /* [R][K_MAX] */
   ent_t* ents;                /* entry arena for Replicate payload copies */
-  uint8_t* pay;
-  size_t n_ents, cap_ents;
+  uint8_t* pay;               /* their Cmds, back to back (ent_t.off) */
+  size_t n_ents, cap_ents, pay_used, pay_cap;
 } outbox_t;
 
 typedef struct {
@@ -51,7 +52,8 @@ typedef struct {
   uint8_t rstate[OR_MAX_R];
   /* log ring: index i in (marker, last] lives at slot i & (L-1) */
   ent_t* log;
-  uint8_t* logpay;
+  uint8_t** cmd;    /* [L] the Cmd bytes of the entry at each ring slot (grown to its longest Cmd) */
+  uint32_t* cmdcap; /* [L] */
   outbox_t ob[2];
   uint32_t g, s; /* group, slot */
   /* apply window of the last step: entries apply_lo .. processed went to the state machine
@@ -72,15 +74,16 @@ typedef struct {
 struct or_engine {
   or_config c;
   uint32_t nrep;
-  uint32_t maxc, pts; /* longest Cmd (the payload row stride), stream pages per replica */
+  uint32_t maxc, pts; /* longest Cmd, stream pages per replica */
   rep_t* reps;
   uint64_t t; /* next tick to run */
   const or_tick_input* in;
   /* caller proposals staged for the next tick (or_propose), per window group */
   uint8_t* stg_slot;  /* [G] target slot, 0xFF none */
   uint32_t* stg_n;    /* [G] entries */
-  ent_t* stg_ents;    /* [G][E] len per entry */
-  uint8_t* stg_pay;   /* [G][E][P] Cmd bytes, zero-padded */
+  ent_t* stg_ents;    /* [G][E] len and arena offset per entry */
+  uint8_t* stg_pay;   /* the staged Cmds, back to back (ent_t.off) */
+  size_t stg_used, stg_cap;
   int staged;
   uint64_t* rd_req;   /* [G*R] ReadIndex contexts staged for the next tick (0 none) */
   int rd_staged;
@@ -142,8 +145,17 @@ static inline uint64_t u64max(uint64_t a, uint64_t b) { return a > b ? a : b; }
 static inline ent_t* log_at(const or_engine* e, const rep_t* r, uint64_t i) {
   return &r->log[i & (e->c.log_capacity - 1)];
 }
-static inline uint8_t* logpay_at(const or_engine* e, const rep_t* r, uint64_t i) {
-  return r->logpay + (size_t)(i & (e->c.log_capacity - 1)) * e->maxc;
+static inline const uint8_t* logpay_at(const or_engine* e, const rep_t* r, uint64_t i) {
+  return r->cmd[i & (e->c.log_capacity - 1)];
+}
+/* the ring slot of index i, made to hold a Cmd of len bytes */
+static uint8_t* logpay_put(const or_engine* e, rep_t* r, uint64_t i, uint32_t len) {
+  const uint64_t k = i & (e->c.log_capacity - 1);
+  if (r->cmdcap[k] < len) {
+    r->cmd[k] = (uint8_t*)realloc(r->cmd[k], len);
+    r->cmdcap[k] = len;
+  }
+  return r->cmd[k];
 }
 /* 16-B chunks a Cmd of len bytes takes in the payload stream */
 static inline uint32_t chunks_of(uint32_t len) { return (len + 15u) >> 4; }
@@ -197,12 +209,33 @@ static int lost(const or_engine* e, const rep_t* r, uint32_t dst, uint32_t n) {
 static outbox_t* cur_ob(const or_engine* e, rep_t* r) { return &r->ob[e->t & 1]; }
 
 static void arena_reserve(const or_engine* e, outbox_t* ob, size_t need) {
+  (void)e;
   if (ob->n_ents + need <= ob->cap_ents) return;
   size_t nc = ob->cap_ents ? ob->cap_ents * 2 : 256;
   while (nc < ob->n_ents + need) nc *= 2;
   ob->ents = (ent_t*)realloc(ob->ents, nc * sizeof(ent_t));
-  if (e->c.payload_bytes) ob->pay = (uint8_t*)realloc(ob->pay, nc * e->maxc);
   ob->cap_ents = nc;
+}
+
+/* room for `bytes` more Cmd bytes in an arena; returns the offset they start at */
+static uint64_t bytes_reserve(uint8_t** buf, size_t* used, size_t* cap, size_t bytes) {
+  if (*used + bytes > *cap) {
+    size_t nc = *cap ? *cap * 2 : 4096;
+    while (nc < *used + bytes) nc *= 2;
+    *buf = (uint8_t*)realloc(*buf, nc);
+    *cap = nc;
+  }
+  uint64_t at = *used;
+  *used += bytes;
+  return at;
+}
+
+/* copy the Cmd of log index i (an entry view en) into the outbox arena: en->off */
+static void ob_put_cmd(outbox_t* ob, ent_t* en, const uint8_t* src) {
+  en->off = 0;
+  if (!(en->type == OR_ENTRY_APP && en->len)) return;
+  en->off = bytes_reserve(&ob->pay, &ob->pay_used, &ob->pay_cap, en->len);
+  memcpy(ob->pay + en->off, src, en->len);
 }
 
 /* raft.send + transport enqueue. Returns the outbox slot or NULL if the message was lost. */
@@ -274,7 +307,7 @@ static int remote_try_update(rep_t* r, uint32_t i, uint64_t idx) {
 }
 
 /* Where the Cmds of an append come from: the entries a Propose message
- * carries (ents / pay, P bytes per entry), or, for a tick-input proposal, the synthetic generator
+ * carries (ents / pay, entry k's Cmd at pay + ents[k].off), or, for a tick-input proposal, the synthetic generator
  * (slab >= 0: Cmd k = or_payload(slab, group, k), len P). NULL source: len-0 no-ops. cc != 0: one
  * ConfigChange entry with that descriptor. */
 typedef struct {
@@ -306,8 +339,8 @@ static int append_entries(or_engine* e, rep_t* r, uint32_t n, const src_t* src) 
     }
     uint32_t len = !src || !P ? 0 : src->ents ? src->ents[k].len : P;
     if (len) {
-      uint8_t* dst = logpay_at(e, r, idx);
-      if (src->ents) memcpy(dst, src->pay + (size_t)k * e->maxc, len);
+      uint8_t* dst = logpay_put(e, r, idx, len);
+      if (src->ents) memcpy(dst, src->pay + src->ents[k].off, len);
       else or_payload(e, (uint32_t)src->slab, (uint32_t)global_group(e, r), k, dst);
       en->len = len;
       en->crc = entry_crc(e, dst, len);
@@ -375,8 +408,9 @@ static void send_replicate(or_engine* e, rep_t* r, uint32_t to) {
     arena_reserve(e, ob, n);
     m->ent_off = (uint32_t)ob->n_ents;
     for (uint32_t k = 0; k < n; ++k) {
-      ob->ents[ob->n_ents + k] = *log_at(e, r, next + k);
-      if (e->c.payload_bytes) memcpy(ob->pay + (ob->n_ents + k) * e->maxc, logpay_at(e, r, next + k), e->maxc);
+      ent_t* en = &ob->ents[ob->n_ents + k];
+      *en = *log_at(e, r, next + k);
+      if (e->c.payload_bytes) ob_put_cmd(ob, en, logpay_at(e, r, next + k));
     }
     ob->n_ents += n;
   }
@@ -488,8 +522,8 @@ static void handle_replicate(or_engine* e, rep_t* r, const msg_in_t* m) {
           en->len = src->len;
           en->pos = r->hw;
           if (src->len && src->type == OR_ENTRY_APP) {
-            uint8_t* dst = logpay_at(e, r, idx);
-            memcpy(dst, m->pay + (size_t)k * e->maxc, src->len);
+            uint8_t* dst = logpay_put(e, r, idx, src->len);
+            memcpy(dst, m->pay + src->off, src->len);
             en->crc = entry_crc(e, dst, src->len);
             if (en->crc != src->crc) r->err |= OR_ERR_CRC;
             r->hw += chunks_of(src->len);
@@ -769,16 +803,13 @@ static void handle_propose(or_engine* e, rep_t* r, const msg_in_t* mi) {
       fm->ent_off = (uint32_t)ob->n_ents;
       for (uint32_t k = 0; k < m->nent; ++k) {
         ent_t* en = &ob->ents[ob->n_ents + k];
-        uint8_t* pd = ob->pay + (ob->n_ents + k) * e->maxc;
         memset(en, 0, sizeof *en);
         en->type = OR_ENTRY_APP;
-        if (mi->ents) {
-          en->len = mi->ents[k].len;
-          memcpy(pd, mi->pay + (size_t)k * e->maxc, e->maxc);
-        } else {
-          en->len = P;
-          or_payload(e, m->src_a, (uint32_t)global_group(e, r), k, pd);
-        }
+        en->len = mi->ents ? mi->ents[k].len : P;
+        if (!en->len) continue;
+        en->off = bytes_reserve(&ob->pay, &ob->pay_used, &ob->pay_cap, en->len);
+        if (mi->ents) memcpy(ob->pay + en->off, mi->pay + mi->ents[k].off, en->len);
+        else or_payload(e, m->src_a, (uint32_t)global_group(e, r), k, ob->pay + en->off);
       }
       ob->n_ents += m->nent;
     }
@@ -940,6 +971,7 @@ static void step_replica(or_engine* e, rep_t* r) {
   memset(ob->n, 0, sizeof ob->n);
   memset(ob->emitted, 0, sizeof ob->emitted);
   ob->n_ents = 0;
+  ob->pay_used = 0;
   rep_t* grp = &e->reps[r->g * R];
   /* 1. inbound messages: source slot ascending, emission order */
   for (uint32_t src = 0; src < R; ++src) {
@@ -950,7 +982,7 @@ static void step_replica(or_engine* e, rep_t* r) {
       msg_in_t mi;
       mi.h = m->h;
       mi.ents = sob->ents + m->ent_off;
-      mi.pay = sob->pay ? sob->pay + (size_t)m->ent_off * e->maxc : NULL;
+      mi.pay = sob->pay;
       handle(e, r, &mi);
     }
   }
@@ -968,7 +1000,7 @@ static void step_replica(or_engine* e, rep_t* r) {
   } else if (e->staged && e->stg_slot[r->g] == r->s) {
     pn = e->stg_n[r->g];
     pents = e->stg_ents + (size_t)r->g * e->c.max_entries_per_msg;
-    ppay = e->stg_pay + (size_t)r->g * e->c.max_entries_per_msg * e->maxc;
+    ppay = e->stg_pay;
   }
   if (pn > 0) {
     msg_in_t mi;
@@ -1069,6 +1101,7 @@ int or_tick(or_engine* e, const or_tick_input* in, int nthreads) {
   if (e->staged) {
     memset(e->stg_slot, 0xFF, e->c.groups);
     memset(e->stg_n, 0, (size_t)e->c.groups * 4);
+    e->stg_used = 0;
     e->staged = 0;
   }
   if (e->rd_staged) {
@@ -1150,10 +1183,10 @@ int or_propose(or_engine* e, const or_proposal* p, size_t n, const uint8_t* payl
         uint64_t j = p[i].first + k, at = (uint64_t)g * E + e->stg_n[g] + k;
         uint32_t len = lens ? lens[j] : 0;
         e->stg_ents[at].len = len;
-        uint8_t* d = e->stg_pay + at * e->maxc;
-        if (P) {
-          memset(d, 0, e->maxc);
-          if (len) memcpy(d, payload + off[j], len);
+        e->stg_ents[at].off = 0;
+        if (P && len) {
+          e->stg_ents[at].off = bytes_reserve(&e->stg_pay, &e->stg_used, &e->stg_cap, len);
+          memcpy(e->stg_pay + e->stg_ents[at].off, payload + off[j], len);
         }
       }
       e->stg_n[g] += p[i].count;
@@ -1181,22 +1214,24 @@ int or_create(const or_config* cfg, or_engine** out) {
   if (c->initial_members >> c->replicas) return -1;
   if (c->join_slots >> c->replicas || (c->initial_members & c->join_slots)) return -1;
   uint32_t maxc = c->max_cmd_bytes ? c->max_cmd_bytes : c->payload_bytes;
-  if (c->payload_bytes ? (maxc < c->payload_bytes || maxc > 8191) : maxc != 0) return -1;
+  if (c->payload_bytes ? (maxc < c->payload_bytes || maxc > OR_MAX_CMD) : maxc != 0) return -1;
   or_engine* e = (or_engine*)calloc(1, sizeof *e);
   e->c = *c;
   e->nrep = c->groups * c->replicas;
   e->maxc = maxc;
-  { /* stream_pages as rg_create sizes it */
+  { /* stream_pages as rg_create sizes it: twice a full log of P-byte Cmds, plus two of the longest */
     uint64_t full = ((uint64_t)c->log_capacity * ((c->payload_bytes + 15) & ~15u) + 4095) / 4096;
+    uint64_t big = maxc > c->payload_bytes ? 2 * (((uint64_t)maxc + 4095) / 4096 + 1) : 0;
     uint32_t pts = 16;
-    while (pts < 2 * full) pts <<= 1;
+    while (pts < 2 * full + big) pts <<= 1;
     e->pts = c->payload_bytes ? (c->stream_pages ? c->stream_pages : pts) : 1;
   }
   e->stg_slot = (uint8_t*)malloc(c->groups);
   memset(e->stg_slot, 0xFF, c->groups);
   e->stg_n = (uint32_t*)calloc(c->groups, 4);
   e->stg_ents = (ent_t*)calloc((size_t)c->groups * c->max_entries_per_msg, sizeof(ent_t));
-  e->stg_pay = (uint8_t*)calloc((size_t)c->groups * c->max_entries_per_msg * (maxc ? maxc : 1), 1);
+  e->stg_pay = NULL;
+  e->stg_used = e->stg_cap = 0;
   e->rd_req = (uint64_t*)calloc((size_t)c->groups * c->replicas, 8);
   e->cc_slot = (uint8_t*)malloc(c->groups);
   memset(e->cc_slot, 0xFF, c->groups);
@@ -1207,10 +1242,16 @@ int or_create(const or_config* cfg, or_engine** out) {
     r->g = i / c->replicas;
     r->s = i % c->replicas;
     r->log = (ent_t*)calloc(c->log_capacity, sizeof(ent_t));
-    if (c->payload_bytes) r->logpay = (uint8_t*)calloc((size_t)c->log_capacity, maxc);
-    /* pre-fault the rings so timed ticks do not pay first-touch page faults */
+    r->cmd = (uint8_t**)calloc(c->log_capacity, sizeof(uint8_t*));
+    r->cmdcap = (uint32_t*)calloc(c->log_capacity, 4);
+    /* pre-fault the ring so timed ticks do not pay first-touch page faults (and give every slot room
+     * for a P-byte Cmd, the benchmark's) */
     memset(r->log, 0, (size_t)c->log_capacity * sizeof(ent_t));
-    if (r->logpay) memset(r->logpay, 0, (size_t)c->log_capacity * maxc);
+    if (c->payload_bytes)
+      for (uint32_t k = 0; k < c->log_capacity; ++k) {
+        r->cmd[k] = (uint8_t*)calloc(c->payload_bytes, 1);
+        r->cmdcap[k] = c->payload_bytes;
+      }
     for (int b = 0; b < 2; ++b)
       r->ob[b].m = (msg_t*)calloc((size_t)c->replicas * c->max_msgs_per_pair, sizeof(msg_t));
   }
@@ -1223,7 +1264,10 @@ void or_destroy(or_engine* e) {
   for (uint32_t i = 0; i < e->nrep; ++i) {
     rep_t* r = &e->reps[i];
     free(r->log);
-    free(r->logpay);
+    if (r->cmd)
+      for (uint32_t k = 0; k < e->c.log_capacity; ++k) free(r->cmd[k]);
+    free(r->cmd);
+    free(r->cmdcap);
     for (int b = 0; b < 2; ++b) {
       free(r->ob[b].m);
       free(r->ob[b].ents);
@@ -1281,6 +1325,7 @@ int or_bootstrap(or_engine* e) {
     for (int b = 0; b < 2; ++b) {
       memset(r->ob[b].n, 0, sizeof r->ob[b].n);
       r->ob[b].n_ents = 0;
+      r->ob[b].pay_used = 0;
     }
   }
   e->t = 0;
@@ -1412,6 +1457,7 @@ int or_import_replica(or_engine* e, uint32_t rid, const or_replica_view* v, cons
   uint32_t P = e->c.payload_bytes;
   r->hw = r->lpg = r->nlpg = 0; /* a fresh payload stream (rg_import_replica) */
   r->fidx = 0;
+  uint64_t src = 0; /* the Cmds come packed back to back, one per entry that has one */
   for (uint64_t i = v->marker + 1; i <= v->last; ++i) {
     uint64_t k = i - v->marker - 1;
     ent_t* en = log_at(e, r, i);
@@ -1421,9 +1467,10 @@ int or_import_replica(or_engine* e, uint32_t rid, const or_replica_view* v, cons
     uint32_t len = lens ? lens[k] : P;
     if (payloads && P && len && en->type == OR_ENTRY_APP && !(types && (types[k] & OR_ENTRY_EMPTY))) {
       en->len = len;
-      memset(logpay_at(e, r, i), 0, e->maxc);
-      memcpy(logpay_at(e, r, i), payloads + k * e->maxc, len);
-      en->crc = entry_crc(e, logpay_at(e, r, i), len);
+      uint8_t* d = logpay_put(e, r, i, len);
+      memcpy(d, payloads + src, len);
+      src += len;
+      en->crc = entry_crc(e, d, len);
       r->hw += chunks_of(len);
     } else {
       en->len = en->type == OR_ENTRY_CONFIG && lens ? lens[k] : 0; /* a ConfigChange keeps its descriptor */
@@ -1448,9 +1495,9 @@ int or_deliver(or_engine* e, uint32_t rid_src, const or_msg_view* m) {
     arena_reserve(e, ob, m->nent);
     mm->ent_off = (uint32_t)ob->n_ents;
     for (uint32_t k = 0; k < m->nent; ++k) {
-      ob->ents[ob->n_ents + k] = *log_at(e, r, m->log_index + 1 + k);
-      if (e->c.payload_bytes)
-        memcpy(ob->pay + (ob->n_ents + k) * e->maxc, logpay_at(e, r, m->log_index + 1 + k), e->maxc);
+      ent_t* en = &ob->ents[ob->n_ents + k];
+      *en = *log_at(e, r, m->log_index + 1 + k);
+      if (e->c.payload_bytes) ob_put_cmd(ob, en, logpay_at(e, r, m->log_index + 1 + k));
     }
     ob->n_ents += m->nent;
   }
@@ -1484,6 +1531,7 @@ int or_get_applied(const or_engine* e, uint32_t rid, uint64_t* index, or_entry_v
   if (rid >= e->nrep) return -1;
   const rep_t* r = &e->reps[rid];
   uint32_t n = 0;
+  uint64_t at = 0; /* payload: the Cmds packed back to back */
   for (uint64_t i = r->apply_lo ? r->apply_lo : 1; i <= r->processed; ++i) {
     const ent_t* en = log_at(e, r, i);
     if (en->type != OR_ENTRY_APP || en->len == 0) continue;
@@ -1496,7 +1544,10 @@ int or_get_applied(const or_engine* e, uint32_t rid, uint64_t* index, or_entry_v
         out[n].crc = en->crc;
         out[n]._pad = 0;
       }
-      if (payload && e->c.payload_bytes) memcpy(payload + (size_t)n * e->maxc, logpay_at(e, r, i), e->maxc);
+      if (payload && e->c.payload_bytes) {
+        memcpy(payload + at, logpay_at(e, r, i), en->len);
+        at += en->len;
+      }
     }
     n++;
   }

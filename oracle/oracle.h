@@ -24,6 +24,7 @@ extern "C" {
 #endif
 
 #define OR_MAX_R 8
+#define OR_MAX_CMD (1u << 24) /* the longest Cmd max_cmd_bytes may name (16 MiB; the engine's MAX_CMD) */
 
 /* raftpb.MessageType numbering as recalled (VERIFY); only the values below are used. */
 enum {
@@ -61,7 +62,7 @@ typedef struct or_config {
                               keeps up); 1: applied moves only by or_notify_applied (NotifyRaftLastApplied) */
   uint32_t initial_members; /* bootstrap membership, bit s = slot s (StartOnDiskReplica's initialMembers);
                                0 = every slot */
-  uint32_t max_cmd_bytes;   /* longest Cmd (payload_bytes .. 8191; 0 = payload_bytes) */
+  uint32_t max_cmd_bytes;   /* longest Cmd (payload_bytes .. OR_MAX_CMD; 0 = payload_bytes) */
   uint32_t stream_pages;    /* the stream capacity rule's window, 4-KiB pages (power of two; 0 = as
                                rg_create sizes it) */
   uint32_t join_slots;      /* slots started with join = true: empty log, term 0, no membership */
@@ -133,10 +134,10 @@ int or_get_msgs(const or_engine* e, uint32_t rid, uint32_t dst, or_msg_view* out
 int or_get_msg_terms(const or_engine* e, uint32_t rid, uint32_t dst, uint32_t k, uint64_t* terms, uint32_t cap);
 /* Log entry at `index` of replica rid (must be in (marker, last]). payload may be NULL (else len bytes). */
 int or_get_entry(const or_engine* e, uint32_t rid, uint64_t index, or_entry_view* out, uint8_t* payload);
-/* Replace a replica's state and log (entries for indices marker+1 .. last). payloads: one row of
- * max_cmd_bytes per entry; lens (NULL = payload_bytes for every application entry with a payload)
- * = the Cmd length of each entry, its first lens[k] bytes of row k. Its payload stream restarts at
- * position 0 (as rg_import_replica's). */
+/* Replace a replica's state and log (entries for indices marker+1 .. last). payloads: the Cmds packed
+ * back to back in entry order; an application entry that is not OR_ENTRY_EMPTY takes lens[k] bytes
+ * (lens NULL: payload_bytes), any other none (a ConfigChange's lens[k] is its descriptor). Its
+ * payload stream restarts at position 0 (as rg_import_replica's). */
 int or_import_replica(or_engine* e, uint32_t rid, const or_replica_view* v,
                       const uint64_t* terms, const uint32_t* types, const uint8_t* payloads,
                       const uint32_t* lens);
@@ -156,8 +157,8 @@ int or_config_change(or_engine* e, uint64_t group, uint32_t slot, uint32_t op, u
  * entries are taken from the sender's current log (indices log_index+1 ..). */
 int or_deliver(or_engine* e, uint32_t rid_src, const or_msg_view* m);
 /* Non-empty application entries replica rid applied in the last step (IOnDiskStateMachine.Update
- * input), in index order. Returns the count; fills up to cap (payload: one max_cmd_bytes row per
- * entry). Any output may be NULL. */
+ * input), in index order. Returns the count; fills up to cap (payload: their Cmds packed back to back
+ * at their own lengths). Any output may be NULL. */
 int or_get_applied(const or_engine* e, uint32_t rid, uint64_t* index, or_entry_view* out, uint8_t* payload,
                    uint32_t cap);
 /* Peer.NotifyRaftLastApplied: the state machine of replica rid has applied through `index`

@@ -158,7 +158,7 @@ def default_config(**kw) -> dict:
 
 
 def max_cmd(cfg: dict) -> int:
-    """The longest Cmd (and payload row stride) of a configuration: max_cmd_bytes, or payload_bytes."""
+    """The longest Cmd of a configuration: max_cmd_bytes, or payload_bytes."""
     return cfg.get("max_cmd_bytes", 0) or cfg["payload_bytes"]
 
 
@@ -271,15 +271,17 @@ class Oracle:
 
     def entry(self, rid, index, with_payload=False):
         ev = EntryView()
-        pay = None
-        if with_payload and self.cfg["payload_bytes"]:
-            pay = (C.c_uint8 * max_cmd(self.cfg))()
-        rc = self.L.or_get_entry(self.h, rid, index, C.byref(ev), pay)
+        rc = self.L.or_get_entry(self.h, rid, index, C.byref(ev), None)
         if rc != 0:
             return None
         d = dict(term=ev.term, type=ev.type, len=ev.len, crc=ev.crc)
-        if pay is not None:
-            d["payload"] = bytes(pay[:ev.len]) if ev.type == 0 else b""  # ConfigChange: len = descriptor
+        if with_payload and self.cfg["payload_bytes"]:
+            if ev.type == 0 and ev.len:  # ConfigChange: len = descriptor, no Cmd
+                pay = (C.c_uint8 * ev.len)()
+                self.L.or_get_entry(self.h, rid, index, C.byref(ev), pay)
+                d["payload"] = bytes(pay)
+            else:
+                d["payload"] = b""
         return d
 
     def applied_entries(self, rid):
@@ -288,12 +290,17 @@ class Oracle:
         n = self.L.or_get_applied(self.h, rid, None, None, None, 0)
         if n <= 0:
             return []
-        P = max_cmd(self.cfg)
         idx = (C.c_uint64 * n)()
         ev = (EntryView * n)()
-        pay = (C.c_uint8 * max(1, n * P))()
+        self.L.or_get_applied(self.h, rid, idx, ev, None, n)
+        tot = sum(ev[k].len for k in range(n))
+        pay = (C.c_uint8 * max(1, tot))()  # the Cmds, packed
         self.L.or_get_applied(self.h, rid, idx, ev, pay, n)
-        return [(idx[k], ev[k].len, ev[k].crc, bytes(pay[k * P:k * P + ev[k].len])) for k in range(n)]
+        out, at = [], 0
+        for k in range(n):
+            out.append((idx[k], ev[k].len, ev[k].crc, bytes(pay[at:at + ev[k].len])))
+            at += ev[k].len
+        return out
 
     def snapshot_event(self, rid):
         """(kind, restored, index, term) of rid's last step (oracle side of rg_snapshot_events)."""

@@ -604,8 +604,9 @@ class Sim:
         P, L = self.cfg["payload_bytes"], self.cfg["log_capacity"]
         self.maxc = self.cfg.get("max_cmd_bytes", 0) or P
         full = (L * ((P + 15) // 16 * 16) + 4095) // 4096
+        big = 2 * ((self.maxc + 4095) // 4096 + 1) if self.maxc > P else 0  # room for two of the longest Cmds
         pts = 16
-        while pts < 2 * full:
+        while pts < 2 * full + big:
             pts <<= 1
         self.pts = (self.cfg.get("stream_pages", 0) or pts) if P else 1
         self.t = 0
@@ -791,7 +792,8 @@ class Sim:
     # -- scenario helpers (KATs): same contract as or_import_replica / or_deliver --
     def import_replica(self, rid, view: dict, terms, types=None, payloads=None, lens=None):
         r = self.reps[rid]
-        P, row = self.cfg["payload_bytes"], self.maxc
+        P = self.cfg["payload_bytes"]
+        at = 0  # the Cmds come packed back to back (application entries with a Cmd)
         for k in ("term", "vote", "leader", "committed", "applied", "processed", "marker", "marker_term",
                   "snap_index", "snap_term", "cap_base", "role", "err", "drops"):
             setattr(r, k, view.get(k, 0))
@@ -813,7 +815,10 @@ class Sim:
             ty = 0 if types is None else types[k] & 0xFF
             ln = P if lens is None else lens[k]
             empty = types is not None and types[k] & 0x100
-            data = payloads[k * row:k * row + ln] if (payloads is not None and P and ty == 0 and not empty) else b""
+            data = b""
+            if payloads is not None and P and ty == 0 and not empty:
+                data = payloads[at:at + ln]
+                at += ln
             r.put(Entry(t, ty, bytes(data), ln if ty == 1 and lens is not None else 0))
         assert r.last == view.get("last", r.last)
         r.remotes = []

@@ -272,6 +272,8 @@ class _Feeds:
             r["rid"] = gm[r["rid"].astype(np.int64)]
             recs.append(r)
             pays.append(p)
+        w = max(p.shape[1] for p in pays)  # row widths follow each engine's batch (engine.row_width)
+        pays = [np.pad(p, ((0, 0), (0, w - p.shape[1]))) for p in pays]
         recs, pays = np.concatenate(recs), np.concatenate(pays)
         order = np.argsort(recs["rid"], kind="stable")  # each replica's entries stay in index order
         return recs[order], pays[order]

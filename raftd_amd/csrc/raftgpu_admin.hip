@@ -83,9 +83,8 @@ hipError_t launch_gather_msgs(const AdminParams& a, uint32_t rid, uint32_t dst, 
   return hipGetLastError();
 }
 
-// one thread per entry: its view, and its Cmd into a row of `row` bytes (read through the stream's pages)
-__global__ void gather_entries_kernel(AdminParams a, uint32_t rid, uint64_t first, uint32_t n, rg_entry_view* out,
-                                      uint8_t* out_pay) {
+// one thread per entry: its view
+__global__ void gather_entries_kernel(AdminParams a, uint32_t rid, uint64_t first, uint32_t n, rg_entry_view* out) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const TickParams& t = a.t;
@@ -101,17 +100,36 @@ __global__ void gather_entries_kernel(AdminParams a, uint32_t rid, uint64_t firs
   v.crc = (w & PAY_BIT) ? crc_of_cmd(inf.x, v.len, t.P, a.zi) : 0u;  // the info word keeps the slot CRC
   v.bank = (uint32_t)bank;
   out[i] = v;
-  if (out_pay && (w & PAY_BIT))
-    for (uint32_t b = 0; b < v.len; ++b) {
-      const uint8_t* src = a.pool + stream_byte(a.pt, a.PTS, q, inf.y + (b >> 4));
-      out_pay[(uint64_t)i * a.row + b] = src[b & 15];
-    }
 }
 
 hipError_t launch_gather_entries(const AdminParams& a, uint32_t rid, uint64_t first, uint32_t n, void* out,
-                                 uint8_t* out_pay, hipStream_t s) {
+                                 hipStream_t s) {
   hipLaunchKernelGGL(gather_entries_kernel, dim3((n + 63) / 64), dim3(64), 0, s, a, rid, first, n,
-                     (rg_entry_view*)out, out_pay);
+                     (rg_entry_view*)out);
+  return hipGetLastError();
+}
+
+// one block per entry: its Cmd's chunks, read through the stream's pages, to out + ao[i] (16-B aligned;
+// ao[i] = ~0: no Cmd)
+__global__ void __launch_bounds__(256) gather_cmds_kernel(AdminParams a, uint32_t rid, uint64_t first,
+                                                          const uint64_t* ao, uint8_t* out) {
+  const uint32_t i = blockIdx.x;
+  if (ao[i] == ~0ull) return;
+  const TickParams& t = a.t;
+  const uint32_t q = q_of(t, rid);
+  const uint64_t slot = (first + i) & (t.L - 1);
+  const uint64_t w = t.tr[slot * t.nrep + q];
+  const uint2 inf = a.info[((w >> 63) * t.nrep + q) * t.L + slot];
+  const uint32_t nc = word_nc(w);
+  for (uint32_t c = threadIdx.x; c < nc; c += blockDim.x)
+    *reinterpret_cast<uint4*>(out + ao[i] + 16ull * c) =
+        *reinterpret_cast<const uint4*>(a.pool + stream_byte(a.pt, a.PTS, q, inf.y + c));
+}
+
+hipError_t launch_gather_cmds(const AdminParams& a, uint32_t rid, uint64_t first, uint32_t n, const uint64_t* ao,
+                              uint8_t* out, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(gather_cmds_kernel, dim3(n), dim3(256), 0, s, a, rid, first, ao, out);
   return hipGetLastError();
 }
 

@@ -32,8 +32,7 @@ __device__ __forceinline__ uint32_t lane_inc_scan(uint32_t v) {
 // chunk t of the run (t < total) belongs to the first candidate whose inc exceeds t (binary search
 // over lanes), and is copied from its stream into out + (base + t) · 16.
 __device__ __forceinline__ void copy_run(const uint8_t* pool, const uint32_t* pt, uint32_t PTS, uint32_t q,
-                                         uint32_t inc, uint32_t sp, uint32_t total, uint8_t* out, uint64_t base,
-                                         bool host) {
+                                         uint32_t inc, uint32_t sp, uint32_t total, uint8_t* out, uint64_t base) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const uint32_t lane = __lane_id();
   for (uint32_t t = lane; t < ((total + 63) & ~63u); t += 64) {
@@ -50,9 +49,7 @@ __device__ __forceinline__ void copy_run(const uint8_t* pool, const uint32_t* pt
     const uint32_t spl = (uint32_t)__shfl((int)sp, (int)(lo < 64 ? lo : 63), 64);
     if (t < total) {
       const u32x4 v = *reinterpret_cast<const u32x4*>(pool + stream_byte(pt, PTS, q, spl + (t - ex)));
-      u32x4* d = reinterpret_cast<u32x4*>(out + (base + t) * 16);
-      if (host) *d = v;
-      else __builtin_nontemporal_store(v, d);
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(out + (base + t) * 16));
     }
   }
 }
@@ -122,7 +119,7 @@ __global__ void __launch_bounds__(256) apply_gather_kernel(ApplyParams a) {
       reinterpret_cast<rg_apply_entry*>(a.out_rec)[k] = r;
     }
     const uint32_t total = (uint32_t)__shfl((int)inc, 63, 64);
-    copy_run(a.pool, a.pt, a.PTS, q, inc, inf.y, total, a.out_pay, cpos, a.out_host != 0);
+    copy_run(a.pool, a.pt, a.PTS, q, inc, inf.y, total, a.out_pay, cpos);
     pos += __builtin_popcountll(mask);
     cpos += total;
   }
@@ -148,6 +145,10 @@ __device__ __forceinline__ uint64_t persist_first(const PersistParams& a, uint32
 __global__ void persist_count_kernel(PersistParams a) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= a.nrep) return;
+  if (!((a.slot_mask >> (q / a.G)) & 1u)) {  // another node's replica: not this hand-off's to persist
+    a.scnt[q] = a.ecnt[q] = a.ccnt[q] = 0;
+    return;
+  }
   const uint64_t n = a.nrep;
   const uint64_t last = a.s64[(uint64_t)S_LAST * n + q], lo = persist_first(a, q);
   const uint32_t ne = lo <= last ? (uint32_t)(last - lo + 1) : 0u;
@@ -229,7 +230,7 @@ __global__ void __launch_bounds__(256) persist_entries_kernel(PersistParams a) {
       reinterpret_cast<rg_persist_entry*>(a.out_ent)[base + (i - lo)] = r;
     }
     const uint32_t total = (uint32_t)__shfl((int)inc, 63, 64);
-    copy_run(a.pool, a.pt, a.PTS, q, inc, inf.y, total, a.out_pay, cpos, false);
+    copy_run(a.pool, a.pt, a.PTS, q, inc, inf.y, total, a.out_pay, cpos);
     cpos += total;
   }
 }

@@ -1,0 +1,136 @@
+// raftgpu_ctl.hip — control_kernel<R> (all Raft logic, one lane per replica) and the
+// resident multi-tick control kernel, one instantiation per translation unit: the build compiles this
+// file once per replica count (-DRG_CTL_R=1..8), so the eight register-heavy instantiations compile in
+// parallel. The step itself is raftgpu_control.h (shared with the CPU harness tests/native/ctl_host.cpp).
+#include "raftgpu_control.h"
+#include "raftgpu_dev.h"
+
+#ifndef RG_CTL_R
+#error "compile raftgpu_ctl.hip with -DRG_CTL_R=<replicas> (raftd_amd/build.py)"
+#endif
+
+namespace rg {
+
+#ifndef RG_CTL_MINWAVES
+#define RG_CTL_MINWAVES 1
+#endif
+#ifndef RG_CTL_BLOCK
+#define RG_CTL_BLOCK 64  // lanes per control workgroup: one wave, so a SIMD starts the next wave as soon as
+                         // its last one ends (r02 A/B vs 256: control 0.122 -> 0.118 ms at 64K x 3, C2 0.043 -> 0.041)
+#endif
+// The parameter block comes by pointer from a device slot the host filled with a stream-ordered
+// copy (DESIGN.md §3 "The control-kernel fault"). Before anything is dereferenced, every lane checks
+// the block's checksum (uniform scalar loads): a stale or torn block becomes a sticky engine error
+// (*perr, a separate kernel argument, reported by the next synchronising call) instead of wild
+// addresses. Ctl reads the fields in place.
+template <int R>
+__global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_MINWAVES) control_kernel(const TickParams* __restrict__ pp,
+                                                                               uint32_t* perr) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  // The checksum: lane i loads word i (one coalesced 424-B wave load, through a laundered pointer so
+  // it stays separate from the step's scalar field reads) and the wave sums the terms with a
+  // butterfly. r03a's volatile chain cost 53 dependent cache-bypassing loads per wave; a chain of
+  // seven s_load_dwordx16 (r03b) still waited seven scalar round trips at the head of every wave.
+  const TickParams* pc = pp;
+  asm volatile("" : "+s"(pc));
+  const uint32_t lane = threadIdx.x & 63u;
+  typedef __attribute__((address_space(1))) const uint64_t gu64;
+  gu64* wv = (gu64*)pc;  // a C cast: the address-space conversion (global_load, not flat_load)
+  uint64_t h = lane < TP_WORDS ? tp_term(wv[lane], lane) : 0ull;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)h, off, 64);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(h >> 32), off, 64);
+    h += ((uint64_t)hi << 32) | lo;
+  }
+  if (h != wv[TP_WORDS]) {
+    if (q == 0) {
+      printf("raftgpu: control_kernel parameter block checksum mismatch (tick %llu): launch skipped\n",
+             (unsigned long long)pp->tick);
+      atomicOr(perr, 1u);
+    }
+    return;
+  }
+  CTickParams& cp = *(CTickParams*)pp;
+  if (q >= cp.nrep) return;
+#ifdef RG_CTL_PROFILE
+  const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memtime();
+  Ctl<R> c(cp, q);
+  c.stamps[0] = t0;
+#else
+  Ctl<R> c(cp, q);
+#endif
+  c.run();
+}
+
+// ---- the resident multi-tick control kernel (metadata-only, one-rank engines). A
+// workgroup holds every replica of 64 groups — wave w is slot w of groups [64·b, 64·b + 64) — so a
+// tick's messages never leave it, and k ticks run in one launch with a workgroup barrier between
+// them instead of a kernel boundary: the state, outboxes and ring words a tick reads were written
+// by this workgroup one tick earlier and are still in its CU's caches. Block i of pp is tick t0 + i
+// (the host seals each); all k checksums are verified before anything is dereferenced.
+__device__ __forceinline__ bool tp_check(const TickParams* pp, uint32_t i) {
+  const TickParams* pc = pp + i;
+  asm volatile("" : "+s"(pc));
+  typedef __attribute__((address_space(1))) const uint64_t gu64;
+  gu64* wv = (gu64*)pc;
+  const uint32_t lane = threadIdx.x & 63u;
+  uint64_t h = lane < TP_WORDS ? tp_term(wv[lane], lane) : 0ull;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)h, off, 64);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(h >> 32), off, 64);
+    h += ((uint64_t)hi << 32) | lo;
+  }
+  return h == wv[TP_WORDS];
+}
+
+template <int R>
+__global__ void __launch_bounds__(64 * R, 1) control_resident_kernel(const TickParams* __restrict__ pp, uint32_t k,
+                                                                     uint32_t* perr) {
+  for (uint32_t i = 0; i < k; ++i)
+    if (!tp_check(pp, i)) {  // the same verdict in every wave: the whole workgroup leaves together
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        printf("raftgpu: control_resident_kernel parameter block %u checksum mismatch: launch skipped\n", i);
+        atomicOr(perr, 1u);
+      }
+      return;
+    }
+  CTickParams* cp = (CTickParams*)pp;
+  const uint32_t G = cp[0].G, w = threadIdx.x >> 6, g = blockIdx.x * 64 + (threadIdx.x & 63u);
+  const uint32_t q = w * G + g;
+  for (uint32_t i = 0; i < k; ++i) {
+    if (g < G) {
+      Ctl<R> c(cp[i], q);
+      c.run();
+    }
+    __syncthreads();  // tick i's outboxes and state, written by this workgroup, before tick i + 1 reads them
+  }
+}
+
+template <>
+hipError_t launch_control_t<RG_CTL_R>(const TickParams* p, uint32_t* perr, uint32_t nrep, hipStream_t s) {
+#ifdef RG_DEV_NO_CONTROL  // development builds of the other kernels only (ISA / resource checks)
+  (void)p; (void)perr; (void)nrep; (void)s;
+  return hipErrorInvalidValue;
+#else
+  hipLaunchKernelGGL(control_kernel<RG_CTL_R>, dim3((nrep + RG_CTL_BLOCK - 1) / RG_CTL_BLOCK), dim3(RG_CTL_BLOCK), 0, s,
+                     p, perr);
+  return hipGetLastError();
+#endif
+}
+
+template <>
+hipError_t launch_control_resident_t<RG_CTL_R>(const TickParams* p, uint32_t k, uint32_t* perr, uint32_t G,
+                                              hipStream_t s) {
+#if defined(RG_DEV_NO_CONTROL) || RG_CTL_R > 4
+  // R > 4: a control wave needs a SIMD of its own (occupancy 1), and a CU has four
+  (void)p; (void)k; (void)perr; (void)G; (void)s;
+  return hipErrorInvalidValue;
+#else
+  hipLaunchKernelGGL(control_resident_kernel<RG_CTL_R>, dim3((G + 63) / 64), dim3(64 * RG_CTL_R), 0, s, p, k, perr);
+  return hipGetLastError();
+#endif
+}
+
+}  // namespace rg

@@ -142,6 +142,7 @@ struct rg_engine {
   hipEvent_t tp_ev[TP_SLOTS / TP_CHUNK] = {};
   bool tp_used[TP_SLOTS / TP_CHUNK] = {};
   uint64_t tp_next = 0;
+  uint32_t tp_corrupt = 0;  // tests (rg_debug_corrupt_params): seal the next n blocks with a wrong checksum
   uint8_t* stage = nullptr;
   uint64_t stage_bytes = 0;
   uint64_t t = 0;
@@ -273,15 +274,10 @@ static void build_crc(rg_engine* e, std::vector<uint32_t>& tab) {
         for (uint32_t i = 0; i < (1u << b); ++i) x = Zi(x);
         tab[CRC_ZI_OFF + (b * 8 + j) * 16 + n] = x;
       }
-  // Z^P (chaining the P-byte segments of a longer Cmd) and the finalisation constants of S·P bytes
+  // Z^P (chaining the P-byte segments of a longer Cmd)
   const uint32_t P = e->c.payload_bytes;
   for (uint32_t j = 0; j < 8; ++j)
     for (uint32_t n = 0; n < 16; ++n) tab[CRC_ZP_OFF + j * 16 + n] = Zn(n << (4 * j), P);
-  uint32_t st = 0xFFFFFFFFu;
-  for (uint32_t S = 1; S <= CRC_CS_MAX; ++S) {
-    st = Zn(st, P);
-    tab[CRC_CS_OFF + S] = st ^ 0xFFFFFFFFu;
-  }
 }
 
 static uint32_t host_crc(const rg_engine* e, const uint8_t* p, size_t n) {
@@ -435,7 +431,7 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if ((N > 1 || c.wire_all) && c.groups >= (1u << 24)) return fail(RG_EINVAL, "groups < 2^24 with ranks > 1");
   const uint32_t maxc = c.max_cmd_bytes ? c.max_cmd_bytes : c.payload_bytes;
   if (c.payload_bytes ? (maxc < c.payload_bytes || maxc > MAX_CMD) : maxc != 0)
-    return fail(RG_EINVAL, "max_cmd_bytes must be in [payload_bytes, 8191] (0 with payload_bytes 0)");
+    return fail(RG_EINVAL, "max_cmd_bytes must be in [payload_bytes, 16 MiB] (0 with payload_bytes 0)");
   if (c.stream_pages && (!pow2(c.stream_pages) || c.stream_pages > (1u << 20)))
     return fail(RG_EINVAL, "stream_pages must be 0 or a power of two <= 2^20");
   if (c.pool_pages > (1u << 24)) return fail(RG_EINVAL, "pool_pages <= 2^24 (64 GiB)");
@@ -456,10 +452,12 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   e->slab_rows = e->wire ? e->nrep : c.groups;  // wire engines: one slab row per replica (bulk_kernel<LG, true>)
   e->J = (c.replicas - 1) * c.max_msgs_per_pair + 2;  // >= appends one step can make
   e->maxc = maxc;
-  {  // payload streams: a replica's window (auto: twice a full log of P-byte Cmds) and the pool
+  {  // payload streams: a replica's window (auto: twice a full log of P-byte Cmds, plus room for two of
+     // the longest Cmds when max_cmd_bytes > P; oracle.c sizes it the same way) and the pool
     const uint64_t full = ((uint64_t)c.log_capacity * ((c.payload_bytes + 15) & ~15u) + PAGE_BYTES - 1) / PAGE_BYTES;
+    const uint64_t big = maxc > c.payload_bytes ? 2 * ((maxc + PAGE_BYTES - 1) / PAGE_BYTES + 1) : 0;
     uint32_t pts = 16;
-    while (pts < 2 * full) pts <<= 1;
+    while (pts < 2 * full + big) pts <<= 1;
     e->PTS = c.payload_bytes ? (c.stream_pages ? c.stream_pages : pts) : 1;
     const uint64_t want = (uint64_t)c.groups * c.replicas * (full + 2);
     e->npages = !c.payload_bytes ? 0 : c.pool_pages ? c.pool_pages : std::min<uint64_t>(want, 1ull << 24);
@@ -1145,6 +1143,10 @@ static int launch_control_slot(rg_engine* e, const TickParams& p) {
   if (k % TP_CHUNK == 0 && e->tp_used[c]) HIPCHK(hipEventSynchronize(e->tp_ev[c]));
   e->h_tp[k] = p;
   seal(e->h_tp[k]);
+  if (e->tp_corrupt) {  // tests only: a torn block, as a stale kernel-argument line would look
+    e->tp_corrupt--;
+    e->h_tp[k].csum ^= 0x100ull;
+  }
   HIPCHK(hipMemcpyAsync(e->d_tp + k, e->h_tp + k, sizeof(TickParams), hipMemcpyHostToDevice, e->stream));
   if (k % TP_CHUNK == TP_CHUNK - 1) {
     HIPCHK(hipEventRecord(e->tp_ev[c], e->stream));
@@ -1305,6 +1307,9 @@ static int tick_graph(rg_engine* e, const rg_tick_input* in, uint32_t k) {
     }
     for (int set = 0; set < 2; ++set) {
       HIPCHK(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+      // every path out of the capture ends it: a failed launch leaves the stream usable
+      // and reports its own error, not a later capture-invalidated one
+      auto capture = [&]() -> hipError_t {
       for (uint32_t i = 0; i < k; ++i) {
         TickParams p = params_at(e, t0 + i);
         p.flags = in->flags;
@@ -1314,18 +1319,27 @@ static int tick_graph(rg_engine* e, const rg_tick_input* in, uint32_t k) {
         p.isolate = in->isolate;
         TickParams* hs = e->g_htp + set * G_MAXK + i;
         TickParams* ds = e->g_dtp + set * G_MAXK + i;
-        HIPCHK(hipMemcpyAsync(ds, hs, sizeof(TickParams), hipMemcpyHostToDevice, e->stream));
-        HIPCHK(launch_control(ds, &e->poolctl->param_err, p.R, p.nrep, e->stream));
-        if (e->c.payload_bytes) {
+        hipError_t r = hipMemcpyAsync(ds, hs, sizeof(TickParams), hipMemcpyHostToDevice, e->stream);
+        if (r == hipSuccess) r = launch_control(ds, &e->poolctl->param_err, p.R, p.nrep, e->stream);
+        if (r == hipSuccess && e->c.payload_bytes) {
           PoolParams pp{};
           pp.nrep = e->nrep; pp.PTS = e->PTS; pp.npages = e->npages;
           pp.s32_out = p.s32_out; pp.s32_in = p.s32_in; pp.pt = e->pt; pp.fring = e->fring; pp.ctl = e->poolctl;
           pp.jcnt = p.jcnt;
-          HIPCHK(launch_pool(pp, e->stream));
-          HIPCHK(launch_bulk(bulk_params_at(e, t0 + i), e->pt, e->stream, e->bulk_grid));
+          r = launch_pool(pp, e->stream);
+          if (r == hipSuccess) r = launch_bulk(bulk_params_at(e, t0 + i), e->pt, e->stream, e->bulk_grid);
         }
+        if (r != hipSuccess) return r;
       }
+      return hipSuccess;
+      };
+      const hipError_t cr = capture();
       hipError_t r = hipStreamEndCapture(e->stream, &e->gg[set]);
+      if (cr != hipSuccess) {
+        if (r == hipSuccess && e->gg[set]) (void)hipGraphDestroy(e->gg[set]);
+        e->gg[set] = nullptr;
+        return fail(RG_EHIP, std::string("rg_tick_device_n: graph capture: ") + hipGetErrorString(cr));
+      }
       if (r != hipSuccess) return fail(RG_EHIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(r));
       HIPCHK(hipGraphInstantiate(&e->gx[set], e->gg[set], nullptr, nullptr, 0));
     }
@@ -1474,13 +1488,35 @@ int rg_read_entries(rg_engine* e, uint32_t rid, uint64_t first, uint32_t n, rg_e
   int rc = rg_read_replicas(e, rid, 1, &v);
   if (rc) return rc;
   if (first <= v.marker || first + n - 1 > v.last) return fail(RG_EINVAL, "index outside (marker, last]");
-  const uint64_t vb = (uint64_t)n * sizeof(rg_entry_view), pb = payload ? (uint64_t)n * e->maxc : 0;
-  rc = stage_reserve(e, vb + pb + 16);
-  if (rc) return rc;
-  HIPCHK(launch_gather_entries(admin(e), rid, first, n, e->stage, payload ? e->stage + vb : nullptr, e->stream));
-  HIPCHK(hipMemcpyAsync(out, e->stage, vb, hipMemcpyDeviceToHost, e->stream));
-  if (payload && pb) HIPCHK(hipMemcpyAsync(payload, e->stage + vb, pb, hipMemcpyDeviceToHost, e->stream));
+  const uint64_t vb = a16((uint64_t)n * sizeof(rg_entry_view));
+  RGCHK(stage_reserve(e, vb + 16));
+  HIPCHK(launch_gather_entries(admin(e), rid, first, n, e->stage, e->stream));
+  HIPCHK(hipMemcpyAsync(out, e->stage, (uint64_t)n * sizeof(rg_entry_view), hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
+  if (!payload) return RG_OK;
+  // the Cmds, packed back to back in entry order at their own lengths: gathered 16-B aligned into
+  // device staging, one D2H copy, then packed on the host
+  std::vector<uint64_t> ao(n, ~0ull);
+  uint64_t tot = 0;
+  for (uint32_t i = 0; i < n; ++i)
+    if (out[i].type == RG_ENTRY_APPLICATION && out[i].len) {
+      ao[i] = tot;
+      tot += a16(out[i].len);
+    }
+  if (!tot) return RG_OK;
+  const uint64_t ob = a16((uint64_t)n * 8);
+  RGCHK(stage_reserve(e, ob + tot + 16));
+  HIPCHK(hipMemcpyAsync(e->stage, ao.data(), (uint64_t)n * 8, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(launch_gather_cmds(admin(e), rid, first, n, (const uint64_t*)e->stage, e->stage + ob, e->stream));
+  std::vector<uint8_t> host(tot);
+  HIPCHK(hipMemcpyAsync(host.data(), e->stage + ob, tot, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  uint64_t at = 0;
+  for (uint32_t i = 0; i < n; ++i)
+    if (ao[i] != ~0ull) {
+      memcpy(payload + at, host.data() + ao[i], out[i].len);
+      at += out[i].len;
+    }
   return RG_OK;
 }
 
@@ -1490,19 +1526,23 @@ int rg_import_replica(rg_engine* e, uint32_t rid, const rg_replica_view* v, cons
   if (int jrc = join(e)) return jrc;
   const uint64_t L = e->c.log_capacity, P = e->c.payload_bytes, row = e->maxc;
   if (v->last < v->marker || v->last - v->marker > L) return fail(RG_EINVAL, "log longer than the ring");
+  if (v->term > TERM_MASK || v->marker_term > TERM_MASK || v->snap_term > TERM_MASK)
+    return fail(RG_EINVAL, "rg_import_replica: term >= 2^36 (the term word's field, DESIGN.md §2)");
   const uint32_t nent = (uint32_t)(v->last - v->marker);
   if (nent && !terms) return fail(RG_EINVAL, "rg_import_replica: null terms");
   std::vector<uint64_t> words(nent);
   std::vector<uint32_t> crcs(nent, 0), pos(nent, 0);
   std::vector<uint8_t> chunks;  // the Cmds back to back, each zero-padded to whole chunks (a fresh stream)
   std::vector<uint8_t> slot;
+  uint64_t src = 0;  // the caller's Cmds are packed back to back (one per entry with a Cmd)
   for (uint32_t k = 0; k < nent; ++k) {
     const uint32_t type = types ? (types[k] & 0xFFu) : RG_ENTRY_APPLICATION;
     const uint32_t len = lens ? lens[k] : (uint32_t)P;
     pos[k] = (uint32_t)(chunks.size() / 16);
+    if (terms[k] > TERM_MASK) return fail(RG_EINVAL, "rg_import_replica: term >= 2^36");
     if (type != RG_ENTRY_APPLICATION) {  // a ConfigChange keeps its descriptor, no Cmd
       const uint32_t cc = lens ? lens[k] : 0u;
-      if (cc > 0x1FFFu) return fail(RG_EINVAL, "rg_import_replica: ConfigChange descriptor out of range");
+      if (cc > 0xFFu) return fail(RG_EINVAL, "rg_import_replica: ConfigChange descriptor out of range");
       words[k] = (terms[k] & TERM_MASK) | TYPE_BIT | cc_bits(cc);
       continue;
     }
@@ -1512,7 +1552,8 @@ int rg_import_replica(rg_engine* e, uint32_t rid, const rg_replica_view* v, cons
     if (hp) {
       const uint64_t S = (len + P - 1) / P;  // the slot CRC: the Cmd zero-padded to S·P bytes
       slot.assign(S * P, 0);
-      memcpy(slot.data(), payloads + (uint64_t)k * row, len);
+      memcpy(slot.data(), payloads + src, len);
+      src += len;
       crcs[k] = host_crc(e, slot.data(), S * P);
       chunks.insert(chunks.end(), slot.begin(), slot.begin() + (len + 15) / 16 * 16);
     }
@@ -1626,6 +1667,7 @@ int rg_persist_collect(rg_engine* e, int full, rg_persist_state* states, uint64_
   PersistParams a{};
   a.G = t.G; a.R = t.R; a.nrep = t.nrep; a.L = t.L; a.P = t.P; a.pl = e->pl;
   a.full = (full || e->t == 0) ? 1u : 0u;  // before the first tick there is no previous state
+  a.slot_mask = ~0u;                         // every replica this engine hosts
   a.s64 = t.s64_in; a.s64_prev = t.s64_out; a.s32 = t.s32_in; a.persist_lo = e->persist_lo;
   a.tr = e->tr; a.info = e->info; a.pool = e->pool; a.pt = e->pt; a.PTS = e->PTS; a.zi = e->crc_tab + CRC_ZI_OFF;
   a.scnt = e->pscnt; a.ecnt = e->pecnt; a.ccnt = e->pccnt; a.soff = e->psoff; a.eoff = e->peoff; a.coff = e->pcoff;
@@ -1823,6 +1865,15 @@ extern "C" int rg_debug_ctl_profile(rg_engine* e, uint32_t* out) {
 }
 #endif
 
+// tests only (not in include/raftgpu.h): the next n control launches get a parameter block whose
+// checksum does not match (the control kernel must skip the tick, the pool and payload stages must
+// not act on its stale rows, and the next rg_sync must report RG_EINVARIANT)
+extern "C" int rg_debug_corrupt_params(rg_engine* e, uint32_t n) {
+  if (!e) return fail(RG_EINVAL, "null engine");
+  e->tp_corrupt = n;
+  return RG_OK;
+}
+
 // tests only (not in include/raftgpu.h): where this process's kernel arguments live.
 // *is_device = 1 device memory, 0 host memory, -1 unknown (the runtime does not track the address)
 extern "C" int rg_debug_kernarg_placement(int32_t device, uint64_t* addr, int32_t* is_device) {
@@ -1933,6 +1984,7 @@ int rg_get_update(rg_engine* e, uint32_t slot_mask, uint32_t flags, rg_update* o
   PersistParams pa{};
   pa.G = t.G; pa.R = t.R; pa.nrep = t.nrep; pa.L = t.L; pa.P = t.P; pa.pl = e->pl;
   pa.full = ((flags & RG_UPDATE_FULL_STATE) || e->t == 0) ? 1u : 0u;
+  pa.slot_mask = slot_mask;  // a node persists its own replicas only (4.3 GB of others' entries)
   pa.s64 = t.s64_in; pa.s64_prev = t.s64_out; pa.s32 = t.s32_in; pa.persist_lo = e->persist_lo;
   pa.tr = e->tr; pa.info = e->info; pa.pool = e->pool; pa.pt = e->pt; pa.PTS = e->PTS; pa.zi = e->crc_tab + CRC_ZI_OFF;
   pa.scnt = e->pscnt; pa.ecnt = e->pecnt; pa.ccnt = e->pccnt; pa.soff = e->psoff; pa.eoff = e->peoff; pa.coff = e->pcoff;

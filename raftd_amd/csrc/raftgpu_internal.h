@@ -15,17 +15,20 @@
 namespace rg {
 
 constexpr uint32_t MAX_R = 8;
-// term-ring / inline-term word: term | cmd_len<<48 | type<<61 | has_payload<<62 | bank<<63
-// (terms < 2^48; cmd_len = the entry's Cmd bytes, 0..max_cmd_bytes (< 8192); has_payload ⇔ an
-// application entry with cmd_len > 0; bank = which of the two info banks holds the entry's
-// {crc, stream position})
+// term-ring / inline-term word: term | cmd_len<<36 | type<<61 | has_payload<<62 | bank<<63
+// (terms < 2^36; cmd_len = the entry's Cmd bytes, 0..max_cmd_bytes (<= MAX_CMD = 16 MiB, a 25-bit
+// field); has_payload ⇔ an application entry with cmd_len > 0; bank = which of the two info banks
+// holds the entry's {crc, stream position}). r01–r03 kept 13 length bits (Cmds of at
+// most 8,191 B); raftd hands any Cmd []byte to Update (raft/state_machine.go:126-145), so r04 moved
+// the field down: 2^36 terms is 2^36 elections of one shard.
 constexpr uint64_t BANK_BIT = 1ull << 63;
 constexpr uint64_t PAY_BIT = 1ull << 62;
 constexpr uint64_t TYPE_BIT = 1ull << 61;
-constexpr uint32_t LEN_SHIFT = 48;
+constexpr uint32_t LEN_SHIFT = 36;
 constexpr uint64_t TERM_MASK = (1ull << LEN_SHIFT) - 1;
-constexpr uint32_t MAX_CMD = 8191;  // the 13-bit length field
-RG_HD_INLINE uint32_t word_len(uint64_t w) { return (uint32_t)(w >> LEN_SHIFT) & 0x1FFFu; }
+constexpr uint32_t LEN_FIELD = (1u << 25) - 1;  // bits 36..60
+constexpr uint32_t MAX_CMD = 1u << 24;           // the longest Cmd rg_config.max_cmd_bytes may name
+RG_HD_INLINE uint32_t word_len(uint64_t w) { return (uint32_t)(w >> LEN_SHIFT) & LEN_FIELD; }
 RG_HD_INLINE uint64_t len_bits(uint32_t len) { return ((uint64_t)len << LEN_SHIFT) | (len ? PAY_BIT : 0ull); }
 // 16-B chunks of the payload stream an entry occupies (0: no Cmd bytes; a ConfigChange has none)
 RG_HD_INLINE uint32_t word_nc(uint64_t w) { return (w & PAY_BIT) ? (word_len(w) + 15u) >> 4 : 0u; }
@@ -308,15 +311,13 @@ constexpr uint32_t CRC_SH_MAX_WORDS = 64 * CRC_SH_STRIDE;
 constexpr uint32_t CRC_ZI_BITS = 10;  // S·P − len < P <= 1024
 constexpr uint32_t CRC_ZI_WORDS = CRC_ZI_BITS * 8 * 16;
 constexpr uint32_t CRC_ZI_OFF = CRC_T_WORDS + CRC_N_WORDS + CRC_SH_MAX_WORDS;
-// ZP [8][16]: Z^P (P zero bytes) on a raw state, to chain the P-byte segments of a Cmd longer than P;
-// CS [S]: the finalisation constant of an S·P-byte message, Z^(S·P)(~0) ^ ~0 (S = 1 .. CRC_CS_MAX)
+// ZP [8][16]: Z^P (P zero bytes) on a raw state, to chain the P-byte segments of a Cmd longer than P
+// (the chain starts from the init value ~0, so no per-length finalisation constant is needed)
 constexpr uint32_t CRC_ZP_OFF = CRC_ZI_OFF + CRC_ZI_WORDS;
 constexpr uint32_t CRC_ZP_WORDS = 8 * 16;
-constexpr uint32_t CRC_CS_OFF = CRC_ZP_OFF + CRC_ZP_WORDS;
-constexpr uint32_t CRC_CS_MAX = 512;  // ceil(MAX_CMD / 16)
 // 16 zero bytes (16-B aligned): where the bulk kernel's idle lanes load from, so a lane past its
 // entry's chunks adds nothing to the lane group's CRC
-constexpr uint32_t CRC_ZERO_OFF = (CRC_CS_OFF + CRC_CS_MAX + 1 + 3) & ~3u;
+constexpr uint32_t CRC_ZERO_OFF = (CRC_ZP_OFF + CRC_ZP_WORDS + 3) & ~3u;
 constexpr uint32_t CRC_TAB_WORDS = CRC_ZERO_OFF + 4;
 
 // CRC-32 of a Cmd of len bytes from its slot CRC (the CRC of the Cmd zero-padded to S·P bytes,
@@ -350,6 +351,15 @@ hipError_t launch_control(const TickParams* p, uint32_t* perr, uint32_t R, uint3
 // k ticks of a metadata-only one-rank engine in one launch (p = k consecutive sealed blocks)
 hipError_t launch_control_resident(const TickParams* p, uint32_t k, uint32_t* perr, uint32_t R, uint32_t G,
                                    hipStream_t s);
+// one instantiation per translation unit (raftgpu_ctl.hip -DRG_CTL_R, raftgpu_bulk.hip -DRG_BULK_W/MJ)
+template <int R>
+hipError_t launch_control_t(const TickParams* p, uint32_t* perr, uint32_t nrep, hipStream_t s);
+template <int R>
+hipError_t launch_control_resident_t(const TickParams* p, uint32_t k, uint32_t* perr, uint32_t G, hipStream_t s);
+template <bool W, bool MJ>
+hipError_t launch_bulk_t(const BulkParams& p, const uint32_t* pt, hipStream_t s, int grid);
+template <bool W, bool MJ>
+int bulk_occupancy_t(uint32_t P);
 hipError_t launch_pool(const PoolParams& p, hipStream_t s);
 // every page free, every replica's stream empty (bootstrap)
 hipError_t launch_pool_reset(uint32_t* fring, uint64_t npages, PoolCtl* ctl, hipStream_t s);
@@ -395,9 +405,8 @@ struct ApplyParams {
   uint64_t* off;            // [nrep + 1] exclusive scan of cnt
   uint64_t* coff;           // [nrep + 1] exclusive scan of ccnt
   uint64_t* bsum;           // scan scratch
-  uint8_t* out_rec;         // [n] rg_apply_entry
+  uint8_t* out_rec;         // [n] rg_apply_entry (device staging)
   uint8_t* out_pay;         // [chunks][16]
-  uint32_t out_host;        // out_* are host-mapped pinned memory: plain (not non-temporal) stores
 };
 hipError_t launch_apply_count(const ApplyParams& a, uint64_t* totals /*[2]: entries, chunks*/, hipStream_t s);
 // snapshot events (raftgpu_apply.hip)
@@ -424,6 +433,7 @@ hipError_t launch_read_gather(const SnapParams& a, hipStream_t s);
 // replica with its whole log window (marker, last] (a checkpoint). Payloads packed (rg_persist_entry.off)
 struct PersistParams {
   uint32_t G, R, nrep, L, P, full;
+  uint32_t slot_mask;        // replicas whose slot bit is set (a node's replicas; rg_persist_collect: all)
   Placement pl;
   const uint64_t* s64;       // current state
   const uint64_t* s64_prev;  // state at the start of the last tick
@@ -471,7 +481,10 @@ hipError_t launch_gather_replicas(const AdminParams& a, uint32_t first_rid, uint
 hipError_t launch_gather_msgs(const AdminParams& a, uint32_t rid, uint32_t dst, void* out_hdr, uint64_t* out_terms,
                               uint32_t* out_cnt, hipStream_t s);
 hipError_t launch_gather_entries(const AdminParams& a, uint32_t rid, uint64_t first, uint32_t n, void* out_views,
-                                 uint8_t* out_pay, hipStream_t s);
+                                 hipStream_t s);
+// the Cmds of entries first .. first+n-1 of rid: entry i's whole chunks to out + ao[i] (ao[i] = ~0: none)
+hipError_t launch_gather_cmds(const AdminParams& a, uint32_t rid, uint64_t first, uint32_t n, const uint64_t* ao,
+                              uint8_t* out, hipStream_t s);
 // import: the view + entry words (term|len|type|pay, bank 0) + slot CRCs + stream positions of a fresh
 // stream (chunk offsets from 0) + the Cmds back to back in whole chunks (nch in all). The replica's
 // old stream pages go back to the pool and its new stream takes ceil(nch / 256) pages (*status = 1

@@ -91,6 +91,19 @@ PERSIST_ENTRY_DTYPE = np.dtype([("index", "<u8"), ("term", "<u8"), ("type", "<u4
                                 ("rid", "<u4"), ("off", "<u8")])
 
 
+ROW_CAP = 65536  # longest max_cmd_bytes shown as fixed-width rows; beyond it rows are as wide as the batch needs
+
+
+def row_width(recs, max_cmd: int) -> int:
+    """Row width of unpack_rows for a batch: max_cmd_bytes up to ROW_CAP (every batch the same shape),
+    else the batch's longest Cmd rounded up to 16 B (a 16-MiB max_cmd_bytes would make every row 16 MiB)."""
+    if max_cmd <= ROW_CAP or not len(recs):
+        return max_cmd if max_cmd <= ROW_CAP else 0
+    app = recs["type"] == 0 if "type" in recs.dtype.names else np.ones(len(recs), bool)
+    m = int(recs["len"][app].max()) if app.any() else 0
+    return (m + 15) // 16 * 16
+
+
 def unpack_rows(recs, packed: np.ndarray, row: int) -> np.ndarray:
     """Packed Cmds (each at recs["off"], recs["len"] bytes) as one zero-padded row of `row` bytes per
     record: the Python view of rg_apply_committed / rg_persist_collect payloads."""
@@ -429,17 +442,21 @@ class Engine:
         if n <= 0:
             return []
         buf = (EntryView * n)()
+        self._check(self.L.rg_read_entries(self.h, rid, first, n, buf, None))
         pay = None
-        P = self.row
-        if with_payload and P:
-            pay = (C.c_uint8 * (n * P))()
-        self._check(self.L.rg_read_entries(self.h, rid, first, n, buf, pay))
-        out = []
-        for k, ev in enumerate(buf):
+        if with_payload and self.row:
+            # rg_read_entries packs the application entries' Cmds back to back at their own lengths (a
+            # ConfigChange entry's len is its descriptor, DESIGN.md §1.4: no Cmd bytes)
+            tot = sum(ev.len for ev in buf if ev.type == 0)
+            pay = (C.c_uint8 * max(tot, 1))()
+            self._check(self.L.rg_read_entries(self.h, rid, first, n, buf, pay))
+        out, at = [], 0
+        for ev in buf:
             d = dict(term=ev.term, type=ev.type, len=ev.len, crc=ev.crc)
             if pay is not None:
-                # a ConfigChange entry's len is its descriptor: no Cmd bytes
-                d["payload"] = bytes(pay[k * P:k * P + ev.len]) if ev.type == 0 else b""
+                ln = ev.len if ev.type == 0 else 0
+                d["payload"] = bytes(pay[at:at + ln])
+                at += ln
             out.append(d)
         return out
 
@@ -561,10 +578,10 @@ class Engine:
 
     def apply_committed(self, slot_mask: int = 0xFF):
         """Committed-entry copy-back of the last tick (rg_apply_committed): a structured array
-        (APPLY_DTYPE: index, group, replica_id, len, crc, rid, off) and the Cmds, one zero-padded row of
-        max_cmd_bytes per entry, as numpy arrays."""
+        (APPLY_DTYPE: index, group, replica_id, len, crc, rid, off) and the Cmds, one zero-padded row per
+        entry (row_width: max_cmd_bytes, or the batch's longest Cmd beyond ROW_CAP), as numpy arrays."""
         recs, packed = self.apply_committed_packed(slot_mask)
-        return recs, unpack_rows(recs, packed, self.row)
+        return recs, unpack_rows(recs, packed, row_width(recs, self.row))
 
     def apply_async(self, slot_mask: int = 0xFF, buf: int = 0):
         """rg_apply_async: gather the last tick's applied entries and start their D2H copy into
@@ -586,11 +603,11 @@ class Engine:
                   else np.zeros(0, np.uint8))
         if not copy:  # views into engine-owned pinned memory: the records and the packed Cmds
             return recs, packed
-        return recs.copy(), unpack_rows(recs, packed, P)
+        return recs.copy(), unpack_rows(recs, packed, row_width(recs, P))
 
     def persist_collect(self, full: bool = False):
         """Host WAL feed of the last tick (rg_persist_collect): (states, entries, payload) numpy
-        arrays — PERSIST_STATE_DTYPE rows, PERSIST_ENTRY_DTYPE rows, one max_cmd_bytes row per entry."""
+        arrays — PERSIST_STATE_DTYPE rows, PERSIST_ENTRY_DTYPE rows, one Cmd row per entry (row_width)."""
         ns, ne, pb = C.c_uint64(), C.c_uint64(), C.c_uint64()
         rc = self.L.rg_persist_collect(self.h, 1 if full else 0, None, 0, C.byref(ns), None, None, 0, C.byref(ne),
                                        0, C.byref(pb))
@@ -603,7 +620,7 @@ class Engine:
                                               en.ctypes.data, packed.ctypes.data, ne.value, C.byref(ne),
                                               packed.size, C.byref(pb)))
         en = en[:ne.value]
-        return st[:ns.value], en, unpack_rows(en, packed[:pb.value], self.row)
+        return st[:ns.value], en, unpack_rows(en, packed[:pb.value], row_width(en, self.row))
 
     def get_update(self, slot_mask: int = 0xFF, flags: int = UPDATE_ALL):
         """rg_get_update: the last tick's whole hand-off in one call. Returns (raw rg_update, dict of

@@ -8,9 +8,9 @@ snapshot's index and term) durable in its LogDB with fsync before the step's mes
 (one ``hipMemcpyAsync`` per array), ``WAL.append`` writes it as one framed, CRC-checked record and
 fsyncs, and the engine may then run the next tick (which delivers the last tick's messages).
 
-Record: ``b"RGWL"``, u32 version, u64 tick, u64 #states, u64 #entries, u32 row bytes (the longest
-Cmd), u32 crc32(body), u64 len(body); body = the state rows, the entry rows, the Cmds, one zero-padded
-row per entry (``PERSIST_STATE_DTYPE`` / ``PERSIST_ENTRY_DTYPE`` little-endian). A torn tail record
+Record: ``b"RGWL"``, u32 version, u64 tick, u64 #states, u64 #entries, u32 row bytes (the record's
+Cmd row width), u32 crc32(body), u64 len(body); body = the state rows, the entry rows, the Cmds, one
+zero-padded row per entry (``PERSIST_STATE_DTYPE`` / ``PERSIST_ENTRY_DTYPE`` little-endian). A torn tail record
 (crash mid-write: short, or failing its CRC) is ignored on replay; a complete record of another
 format version is an error, never silently dropped.
 
@@ -42,9 +42,15 @@ class WAL:
         self.path, self.sync = path, sync
         self.f = open(path, "ab")
 
-    def append(self, tick: int, states, entries, payload, payload_bytes: int):
-        body = states.tobytes() + entries.tobytes() + np.ascontiguousarray(payload).tobytes()
-        self.f.write(HDR.pack(MAGIC, VERSION, tick, len(states), len(entries), payload_bytes,
+    def append(self, tick: int, states, entries, payload, payload_bytes: int | None = None):
+        """payload: one zero-padded Cmd row per entry (Engine.persist_collect); its row width is
+        recorded in the header (payload_bytes, if given, must match it)."""
+        payload = np.ascontiguousarray(payload)
+        row = int(payload.shape[1]) if payload.ndim == 2 else 0
+        if payload_bytes is not None and len(entries) and row not in (payload_bytes, 0):
+            raise ValueError(f"WAL.append: payload rows of {row} B, not {payload_bytes} B")
+        body = states.tobytes() + entries.tobytes() + payload.tobytes()
+        self.f.write(HDR.pack(MAGIC, VERSION, tick, len(states), len(entries), row,
                               zlib.crc32(body), len(body)))
         self.f.write(body)
         self.f.flush()
@@ -147,7 +153,7 @@ def restore(engine, wal_logs: dict, cfg: dict, global_rids, app_applied=None):
     import_replica(rid, view, terms, types, payloads, lens)) from replayed WAL logs. global_rids maps
     the engine's replica ids to global ones (identity for one rank). app_applied(global rid) -> the
     index the replica's state machine has applied (its /LastLogIndex), or None for the commit."""
-    R, P = cfg["replicas"], cfg.get("max_cmd_bytes", 0) or cfg["payload_bytes"]  # the import row stride
+    R = cfg["replicas"]
     for rid, gr in global_rids:
         rl = wal_logs[gr]
         v = restart_view(rl, gr // R, gr % R, cfg, None if app_applied is None else app_applied(gr))
@@ -155,6 +161,7 @@ def restore(engine, wal_logs: dict, cfg: dict, global_rids, app_applied=None):
         terms = [rl.log[i][0] for i in idx]
         # RG_ENTRY_EMPTY: an application entry whose Cmd is empty (a leader's no-op) stays empty
         types = [rl.log[i][1] | (0x100 if rl.log[i][1] == 0 and rl.log[i][2] == 0 else 0) for i in idx]
-        pays = b"".join((rl.log[i][4] if rl.log[i][2] else b"").ljust(P, b"\0") for i in idx) if P else None
+        # rg_import_replica takes the Cmds packed back to back (application entries with a Cmd only)
+        pays = b"".join(rl.log[i][4] for i in idx if rl.log[i][1] == 0 and rl.log[i][2]) if cfg["payload_bytes"] else None
         lens = [rl.log[i][2] for i in idx]
         engine.import_replica(rid, v, terms, types, pays, lens)

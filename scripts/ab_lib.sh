@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 for rep in 1 2; do
   for lib in $LIBS; do
     tag=$(basename $lib .so)_$rep
-    timeout -k 10 150 env RAFTGPU_LIB=$PWD/$lib python bench.py --no-cpu-baseline "$@" > gpurun_out/ab_$tag.log 2>&1 || { tail -5 gpurun_out/ab_$tag.log; exit 1; }
+    timeout -k 10 ${AB_TIMEOUT:-150} env RAFTGPU_LIB=$PWD/$lib python bench.py --no-cpu-baseline "$@" > gpurun_out/ab_$tag.log 2>&1 || { tail -5 gpurun_out/ab_$tag.log; exit 1; }
     python3 -c "
 import json; d=json.loads(open('gpurun_out/ab_$tag.log').read().strip().splitlines()[-1])
 print('$tag', round(d['ms_per_step'],4), {k: round(v,4) for k,v in d['kernels_ms'].items()})"

@@ -6,9 +6,12 @@
  *   rg_create / rg_bootstrap            NewNodeHost + StartOnDiskReplica (raft/raft_manager.go:109,142)
  *   rg_tick (campaign, then plain)      the NodeHost tick loop
  *   rg_propose                          NodeHost.SyncPropose(cmd) (the /raft/update handler's job)
- *   rg_persist_collect                  LogDB SaveRaftState before the messages leave
- *   rg_apply_committed                  IOnDiskStateMachine.Update → POST /UpdateEntries
- *   rg_notify_applied                   NotifyRaftLastApplied once the app answered
+ *   rg_get_update                       Peer.GetUpdate: in one hand-off the entries + State to persist
+ *                                       (LogDB SaveRaftState before the messages leave) and the
+ *                                       committed entries for IOnDiskStateMachine.Update → POST
+ *                                       /UpdateEntries (INTEGRATION.md's per-tick call sequence)
+ *   rg_commit_update(RG_COMMIT_APPLIED) Peer.Commit + NotifyRaftLastApplied once the app answered
+ *   rg_apply_committed / rg_notify_applied  the same through the separate calls (drain phase)
  *   rg_config_change                    SyncRequestDeleteReplica / SyncRequestAddReplica (:165-185)
  *   rg_leader / rg_read_replicas        GetLeaderID / SyncGetShardMembership (raft/members.go:21,30)
  *   rg_destroy                          NodeHost.Close (raft_manager.go:159)
@@ -35,7 +38,8 @@
 #define R 3
 #define TICKS 40
 #define PER_TICK 4 /* Cmds per shard per tick */
-#define MAXC 1500  /* longest Cmd: six 256-B lane groups, up to two pages */
+#define MAXC 1500  /* a usual Cmd: up to six 256-B lane groups, up to two pages */
+#define LONGC 70000 /* about one Cmd in eleven: 8,192 .. LONGC bytes (past r03's 8,191-B ceiling) */
 
 #define CHECK(x)                                                                              \
   do {                                                                                        \
@@ -58,6 +62,7 @@
 static uint32_t make_cmd(uint32_t g, uint32_t t, uint32_t k, uint8_t* out) {
   uint32_t n = (uint32_t)snprintf((char*)out, 256, "put shard=%u tick=%u k=%u;", g, t, k);
   uint32_t len = 1 + (g * 131 + t * 31 + k * 7) % MAXC;
+  if ((g + 3 * t + 5 * k) % 11 == 0) len = 8192 + (g * 977 + t * 131 + k * 17) % (LONGC - 8192);
   if (len < n) len = n;
   for (uint32_t i = n; i < len; ++i) out[i] = (uint8_t)('a' + (g + t + k + i) % 26);
   return len;
@@ -84,7 +89,8 @@ int main(int argc, char** argv) {
   rg_config c;
   memset(&c, 0, sizeof c);
   c.groups = G; c.replicas = R; c.log_capacity = 1024; c.payload_bytes = 256;
-  c.max_cmd_bytes = MAXC;
+  c.max_cmd_bytes = 1u << 20;
+  c.pool_pages = 16384; /* 64 MiB: the long Cmds of 40 ticks stay live (no compaction before 1,000 entries) */
   c.max_entries_per_msg = 16; c.max_msgs_per_pair = 8; c.num_slabs = 2;
   c.election_rtt = 10; c.heartbeat_rtt = 1; c.check_quorum = 1; /* raftd's config (raft_manager.go:92-100) */
   c.snapshot_entries = 1000; c.compaction_overhead = 5; c.seed = 0x5EED; c.ranks = 1;
@@ -125,20 +131,18 @@ int main(int argc, char** argv) {
   /* C-owned buffers for the copy-back and the WAL feed */
   const uint64_t cap = 1u << 16;
   rg_apply_entry* ents = (rg_apply_entry*)malloc(cap * sizeof *ents);
-  const uint64_t pay_cap = cap * 64;
+  const uint64_t pay_cap = cap * 1024;
   uint8_t* pay = (uint8_t*)malloc(pay_cap);
-  rg_persist_state* ps = (rg_persist_state*)malloc(cap * sizeof *ps);
-  rg_persist_entry* pe = (rg_persist_entry*)malloc(cap * sizeof *pe);
-  uint8_t* ppay = (uint8_t*)malloc(pay_cap);
   /* what each replica's state machine received, as a running CRC over (index, Cmd) */
   uint64_t got[G * R];
   uint32_t got_crc[G * R];
   uint64_t last_idx[G * R];
+  uint32_t longest = 0;
   memset(got, 0, sizeof got);
   memset(got_crc, 0, sizeof got_crc);
   memset(last_idx, 0, sizeof last_idx);
 
-  uint8_t* blob = (uint8_t*)malloc(G * PER_TICK * MAXC);
+  uint8_t* blob = (uint8_t*)malloc(G * PER_TICK * LONGC);
   uint32_t lens[G * PER_TICK];
   rg_proposal props[G];
   uint32_t want_crc[G];
@@ -177,26 +181,29 @@ int main(int argc, char** argv) {
         off += n;
       }
     CHECK(tick(e, &in));
-    uint64_t ns = 0, ne = 0, na = 0, pb = 0;
-    CHECK(rg_persist_collect(e, 0, ps, cap, &ns, pe, ppay, cap, &ne, pay_cap, &pb)); /* the shim fsyncs these */
-    for (uint64_t i = 0; i < ne; ++i)  /* a ConfigChange entry's len is its descriptor, no Cmd bytes */
-      EXPECT(pe[i].type != RG_ENTRY_APPLICATION || pe[i].off + pe[i].len <= pb);
-    CHECK(rg_apply_committed(e, 0xFF, ents, pay, cap, &na, pay_cap, &pb));
-    for (uint64_t i = 0; i < na; ++i) {
-      const rg_apply_entry* a = &ents[i];
-      const uint8_t* cmd = pay + a->off;
-      EXPECT(a->off + a->len <= pb);
+    /* Peer.GetUpdate: the whole hand-off of the tick in one call (engine-owned pinned sections) */
+    rg_update u;
+    CHECK(rg_get_update(e, 0xFF, RG_UPDATE_PERSIST | RG_UPDATE_COMMITTED, &u));
+    EXPECT(u.tick == (uint64_t)ticks && u.n_states > 0);
+    for (uint64_t i = 0; i < u.n_entries; ++i) { /* the shim fsyncs these; a ConfigChange's len is its descriptor */
+      const rg_persist_entry* p = &u.entries[i];
+      EXPECT(p->type != RG_ENTRY_APPLICATION || p->off + p->len <= u.entry_payload_bytes);
+      if (p->type == RG_ENTRY_APPLICATION && p->len)
+        EXPECT(p->crc == (uint32_t)crc32(0, u.entry_payload + p->off, p->len));
+    }
+    for (uint64_t i = 0; i < u.n_committed; ++i) { /* IOnDiskStateMachine.Update, per replica */
+      const rg_apply_entry* a = &u.committed[i];
+      const uint8_t* cmd = u.committed_payload + a->off;
+      EXPECT(a->off + a->len <= u.committed_payload_bytes);
       EXPECT(a->crc == (uint32_t)crc32(0, cmd, a->len));
       EXPECT(a->index > last_idx[a->rid]);
       last_idx[a->rid] = a->index;
       got_crc[a->rid] = (uint32_t)crc32(got_crc[a->rid], cmd, a->len);
       got[a->rid]++;
+      if (a->len > longest) longest = a->len;
     }
-    /* the app answered: applied = processed (config changes and no-ops included) */
-    rg_replica_view v[G * R];
-    CHECK(rg_read_replicas(e, 0, G * R, v));
-    for (uint32_t r = 0; r < G * R; ++r) idx[r] = v[r].processed;
-    CHECK(rg_notify_applied(e, rids, idx, G * R));
+    /* Peer.Commit: the app answered, applied = processed (config changes and no-ops included) */
+    CHECK(rg_commit_update(e, &u, RG_COMMIT_APPLIED));
   }
   for (int t = 0; t < 16; ++t) { /* drain: the last Cmds commit everywhere, the re-added follower catches up */
     uint64_t na = 0, pb = 0;
@@ -228,10 +235,15 @@ int main(int argc, char** argv) {
     }
     EXPECT(leaders == 1);
   }
+  EXPECT(longest > 8191); /* Cmds past the old 13-bit length field went through Update */
+  uint64_t pages = 0, free_pages = 0;
+  int pool_failed = 1;
+  CHECK(rg_pool_stats(e, &pages, &free_pages, &pool_failed));
+  EXPECT(!pool_failed && free_pages > 0);
   printf("ABI_C OK%s: %u shards x %u replicas, %llu Cmds per shard applied on every replica, device %.1f MB\n",
          use_wire ? " (wire + RCCL exchange)" : "", G, R, (unsigned long long)want_n[0], rg_device_bytes(e) / 1e6);
   rg_destroy(e);
   if (use_wire) CHECK(rg_rccl_close(&xt));
-  free(ents); free(pay); free(ps); free(pe); free(ppay); free(blob);
+  free(ents); free(pay); free(blob);
   return 0;
 }

@@ -111,7 +111,7 @@ class CtlHost:
             return None
         w = (C.c_uint64 * 1)()
         self.L.ch_read_words(C.c_void_p(self.h), C.c_uint32(rid), C.c_uint64(index), C.c_uint32(1), w)
-        return dict(term=w[0] & ((1 << 48) - 1), type=(w[0] >> 61) & 1)
+        return dict(term=w[0] & ((1 << 36) - 1), type=(w[0] >> 61) & 1)  # raftgpu_internal.h TERM_MASK
 
     def import_replica(self, rid, view: dict, terms, types=None, payloads=None, lens=None):
         from raftd_amd.engine import REPLICA_FIELDS, with_members

@@ -15,7 +15,7 @@ import pytest
 
 from engines import make
 from test_gpu_parity import CHAOS, compare, crc32c_py
-from test_oracle import random_batches
+from test_oracle import BIG_LENS, big_batches, random_batches
 
 pytestmark = pytest.mark.gpu
 
@@ -47,7 +47,7 @@ def check_applied(gpu, ora):
         assert got.get(rid, []) == ora.applied_entries(rid), rid
 
 
-def run_caller(cfg, ticks, seed, make_gpu=None, check_every=1, p_none=0.3, applied=True):
+def run_caller(cfg, ticks, seed, make_gpu=None, check_every=1, p_none=0.3, applied=True, batches_fn=None):
     gpu = make_gpu() if make_gpu else make("gpu", **cfg)
     ora = make("c", **cfg)
     gpu.bootstrap()
@@ -55,7 +55,8 @@ def run_caller(cfg, ticks, seed, make_gpu=None, check_every=1, p_none=0.3, appli
     rng = np.random.default_rng(seed)
     G, R, E, P = ora.G, ora.R, cfg["max_entries_per_msg"], cfg["payload_bytes"]
     for t in range(ticks):
-        batches = random_batches(rng, G, R, E, P, p_none=p_none, maxc=cfg.get("max_cmd_bytes"))
+        batches = (batches_fn(rng, G, R, P) if batches_fn else
+                   random_batches(rng, G, R, E, P, p_none=p_none, maxc=cfg.get("max_cmd_bytes")))
         gpu.propose(batches)
         assert ora.propose(batches) == 0
         camp = (rng.random(G * R) < 0.02).astype(np.uint8)
@@ -92,6 +93,29 @@ def test_caller_long_cmds_chaos(R, P, maxc, pages):
     assert max(lens) > P and {0, 1} <= lens, lens
     st = gpu.pool_stats()
     assert not st["failed"] and 0 < st["free"] < st["total"], st
+
+
+@pytest.mark.parametrize("R,P", [(3, 64), (3, 256), (5, 16)])
+def test_caller_megabyte_cmds_chaos(R, P):
+    """Cmds of 8,191, 8,192, 65,536 and 1 MiB bytes (max_cmd_bytes 1 MiB; r03 refused anything past
+    8,191 B): under message loss, isolation, elections, truncation and snapshots every replica,
+    message, entry (bytes and CRC) and applied batch equals the oracle's, tick by tick."""
+    cfg = dict(CHAOS, groups=4, replicas=R, payload_bytes=P, max_entries_per_msg=8, seed=90 + R,
+               max_cmd_bytes=1 << 20, pool_pages=4 * R * 2048)
+    gpu, _, lens = run_caller(cfg, ticks=60, seed=R * 77 + P, batches_fn=big_batches)
+    assert set(BIG_LENS) <= lens, lens
+    st = gpu.pool_stats()
+    assert not st["failed"], st
+
+
+def test_caller_megabyte_cmds_cluster():
+    """1-MiB Cmds over the wire: forwarded Proposes and Replicates carry them between ranks."""
+    from raftd_amd.cluster import LoopbackCluster
+    cfg = dict(CHAOS, groups=4, replicas=3, payload_bytes=64, max_entries_per_msg=8, seed=17,
+               max_cmd_bytes=1 << 20, pool_pages=2 * 3 * 2048)
+    _, _, lens = run_caller(cfg, ticks=50, seed=5, batches_fn=big_batches,
+                            make_gpu=lambda: LoopbackCluster(ranks=2, **cfg))
+    assert max(lens) == 1 << 20, lens
 
 
 def test_caller_long_cmds_crc32c():

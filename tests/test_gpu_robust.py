@@ -1,0 +1,47 @@
+"""Engine robustness under a corrupt control parameter block.
+
+The control kernel verifies a checksum over its parameter block before it dereferences anything; on
+a mismatch it skips the tick and sets a sticky error. The pool and payload stages that follow it
+must then not act on the skipped tick's stale rows (pool_kernel would free ~2^24 bogus pages,
+bulk_kernel would replay tick t-2's jobs), and rg_sync must report RG_EINVARIANT."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from engines import make
+
+pytestmark = pytest.mark.gpu
+
+
+def test_corrupt_parameter_block_is_reported_and_harmless():
+    from raftd_amd.engine import RgError
+    G, R, E = 64, 3, 8
+    gpu = make("gpu", groups=G, replicas=R, log_capacity=256, payload_bytes=64, max_entries_per_msg=E,
+               snapshot_entries=20, compaction_overhead=3, seed=0xC0)
+    gpu.bootstrap()
+    camp = np.zeros(G * R, np.uint8)
+    camp[0::R] = 1
+    pt, pc = np.zeros(G, np.uint8), np.full(G, E, np.uint32)
+    gpu.tick()
+    gpu.tick(campaign=camp)
+    for _ in range(12):  # steady state with compaction: the stream pages turn over every tick
+        gpu.tick(prop_target=pt, prop_count=pc)
+    gpu.sync()
+    before = gpu.pool_stats()
+    assert not before["failed"]
+    fn = gpu.L.rg_debug_corrupt_params
+    fn.argtypes, fn.restype = [C.c_void_p, C.c_uint32], C.c_int
+    assert fn(gpu.h, 1) == 0
+    gpu.tick(prop_target=pt, prop_count=pc)  # its block fails the checksum
+    with pytest.raises(RgError) as ei:
+        gpu.sync()
+    assert ei.value.code == -5  # RG_EINVARIANT
+    after = gpu.pool_stats()
+    assert not after["failed"]
+    assert after["free"] == before["free"], (before, after)  # the pool stage did not run on stale rows
+    for _ in range(3):  # the engine stays poisoned, and later ticks neither fault nor touch the pool
+        gpu.tick(prop_target=pt, prop_count=pc)
+    with pytest.raises(RgError):
+        gpu.sync()
+    assert gpu.pool_stats()["free"] == before["free"]

@@ -8,6 +8,7 @@ Two identical engines run the same chaos trace (caller Cmds of 0..300 bytes, ele
 loss, an isolated replica that falls behind compaction and is restored by InstallSnapshot, ReadIndex
 requests, apply feedback on); engine A uses the separate calls, engine B rg_get_update."""
 import numpy as np
+import numpy.lib.recfunctions as rfn
 import pytest
 
 from engines import make
@@ -51,9 +52,16 @@ def test_get_update_equals_the_separate_calls():
         rd = a.read_index_results(MASK)
         u, out = b.get_update(MASK)
         assert u.tick == b.t
-        assert out["states"].tobytes() == st.tobytes(), t
-        assert out["entries"].tobytes() == en.tobytes(), t
-        assert np.array_equal(unpack_rows(out["entries"], out["entry_payload"], b.row), rows), t
+        # the persistence section holds the node's replicas only (slot_mask): rg_persist_collect's
+        # records of those replicas, in the same order, with their own offsets
+        keep = ((MASK >> (st["replica_id"].astype(np.int64) - 1)) & 1) == 1
+        ekeep = ((MASK >> (en["rid"].astype(np.int64) % R)) & 1) == 1
+        nooff = [f for f in st.dtype.names if f != "entry_off"]
+        assert rfn.repack_fields(out["states"][nooff]).tobytes() == rfn.repack_fields(st[keep][nooff]).tobytes(), t
+        eo = [f for f in en.dtype.names if f != "off"]
+        assert rfn.repack_fields(out["entries"][eo]).tobytes() == rfn.repack_fields(en[ekeep][eo]).tobytes(), t
+        got = unpack_rows(out["entries"], out["entry_payload"], b.row)
+        assert np.array_equal(got, rows[ekeep]), t
         assert out["committed"].tobytes() == recs.tobytes(), t
         assert np.array_equal(unpack_rows(out["committed"], out["committed_payload"], b.row), arows), t
         assert out["snapshots"].tobytes() == ev.tobytes(), t
@@ -92,3 +100,103 @@ def test_get_update_sections_and_full_state():
     assert full["entries"].tobytes() == en.tobytes()
     assert np.array_equal(unpack_rows(full["entries"], full["entry_payload"], e.row), rows)
     assert len(full["committed"]) == 0
+
+
+def test_get_update_against_oracle():
+    """Every section of rg_get_update checked directly against the C oracle (not only against the
+    engine's own separate calls): persistence records (hard state and rewritten entries with their
+    Cmd bytes) of the node's replicas, committed entries per replica, snapshot events and ready reads;
+    then rg_commit_update(applied) moves the engine as or_notify_applied moves the oracle."""
+    G, R, MASK = 10, 3, 0b101
+    cfg = dict(groups=G, replicas=R, log_capacity=128, payload_bytes=64, max_cmd_bytes=9000, max_entries_per_msg=8,
+               snapshot_entries=20, compaction_overhead=3, drop_ppm=30000, apply_feedback=1, seed=0xA11,
+               pool_pages=G * R * 64)
+    gpu, ora = make("gpu", **cfg), make("c", **cfg)
+    for e in (gpu, ora):
+        e.bootstrap()
+    rng = np.random.default_rng(12)
+    camp = np.zeros(G * R, np.uint8)
+    camp[0::R] = 1
+    mine = [rid for rid in range(G * R) if (MASK >> (rid % R)) & 1]
+    hard = ("term", "vote", "committed", "last", "marker", "snap_index")
+    prev = {rid: ora.replica(rid) for rid in mine}
+    seen = dict(states=0, entries=0, committed=0, snapshots=0, reads=0)
+    for t in range(70):
+        iso = np.zeros(G * R, np.uint8)
+        if 15 <= t < 45:
+            iso[2 * R + 2] = 1  # group 2's slot 2 falls behind compaction, then InstallSnapshot
+        batches = []
+        if t >= 4:
+            for g in range(G):
+                if rng.random() < 0.6:
+                    lens = rng.choice([0, 1, 64, 65, 8192, 9000, int(rng.integers(0, 9001))], int(rng.integers(1, 4)))
+                    batches.append((g, int(rng.integers(0, R)),
+                                    [bytes(rng.integers(0, 256, int(n), dtype=np.uint8)) for n in lens]))
+        reads = [(g, int(rng.integers(0, R)), int(rng.integers(1, 1 << 40))) for g in range(G) if rng.random() < 0.3]
+        for e in (gpu, ora):
+            if batches:
+                e.propose(batches)
+            if t >= 4 and reads:
+                e.read_index(reads)
+            e.tick(campaign=camp if t == 1 else None, isolate=iso)
+        u, out = gpu.get_update(MASK)
+        # persistence: one record per node replica whose log or hard state changed, equal to the oracle
+        got = {int(s["rid"]): s for s in out["states"]}
+        assert set(got) <= set(mine), t
+        for rid in mine:
+            v = ora.replica(rid)
+            if any(v[k] != prev[rid][k] for k in hard):
+                assert rid in got, (t, rid)
+            prev[rid] = v
+        ents = out["entries"]
+        for rid, s in got.items():
+            v = ora.replica(rid)
+            for k, f in (("term", "term"), ("vote", "vote"), ("commit", "committed"), ("last", "last"),
+                         ("marker", "marker"), ("marker_term", "marker_term"), ("snap_index", "snap_index"),
+                         ("snap_term", "snap_term"), ("members", "members"), ("snap_members", "snap_members")):
+                assert int(s[k]) == v[f], (t, rid, k)
+            first, last, lo = int(s["first"]), int(s["last"]), int(s["entry_off"])
+            assert first > v["marker"]
+            for k, i in enumerate(range(first, last + 1)):
+                pe, oe = ents[lo + k], ora.entry(rid, i, with_payload=True)
+                assert (int(pe["index"]), int(pe["term"]), int(pe["type"]), int(pe["len"]), int(pe["crc"])) == \
+                    (i, oe["term"], oe["type"], oe["len"], oe["crc"]), (t, rid, i)
+                if oe["type"] == 0 and oe["len"]:
+                    o = int(pe["off"])
+                    assert bytes(out["entry_payload"][o:o + oe["len"]]) == oe["payload"], (t, rid, i)
+                seen["entries"] += 1
+        seen["states"] += len(got)
+        # committed entries (IOnDiskStateMachine.Update input) per replica
+        com = {}
+        for r in out["committed"]:
+            o, n = int(r["off"]), int(r["len"])
+            com.setdefault(int(r["rid"]), []).append((int(r["index"]), n, int(r["crc"]),
+                                                      bytes(out["committed_payload"][o:o + n])))
+        for rid in range(G * R):
+            assert com.get(rid, []) == (ora.applied_entries(rid) if rid in mine else []), (t, rid)
+        seen["committed"] += len(out["committed"])
+        # snapshot events and ready reads
+        evs = {int(x["rid"]): x for x in out["snapshots"]}
+        rds = {int(x["rid"]): x for x in out["reads"]}
+        for rid in range(G * R):
+            kind, restored, index, term = ora.snapshot_event(rid)
+            if rid in mine and kind:
+                x = evs[rid]
+                assert (int(x["kind"]), int(x["restored"]), int(x["index"]), int(x["term"])) == \
+                    (kind, restored, index, term), (t, rid)
+            else:
+                assert rid not in evs, (t, rid)
+            rr = ora.read_ready(rid)
+            if rid in mine and rr:
+                assert (int(rds[rid]["ctx"]), int(rds[rid]["index"])) == rr, (t, rid)
+            else:
+                assert rid not in rds, (t, rid)
+        seen["snapshots"] += len(evs)
+        seen["reads"] += len(rds)
+        # Peer.Commit: the node's replicas applied what they were handed
+        gpu.commit_update(u, applied=True)
+        for rid in mine:
+            assert ora.notify_applied(rid, ora.replica(rid)["processed"]) == 0
+        for rid in range(G * R):
+            assert gpu.replica(rid) == ora.replica(rid), (t, rid)
+    assert all(v > 0 for v in seen.values()), seen

@@ -103,7 +103,26 @@ def random_batches(rng, G, R, E, P, base=0, p_none=0.3, maxc=None):
     return out
 
 
-def cross_check_caller(seed, G, R, T, **cfg):
+BIG_LENS = (8191, 8192, 65536, 1 << 20)  # the old 13-bit length field's edge, one past it, 64 KiB, 1 MiB
+
+
+def big_batches(rng, G, R, P, base=0, p_none=0.4, nmax=3):
+    """Caller proposals with Cmds far longer than payload_bytes: per group (probability 1 - p_none)
+    1..nmax Cmds whose lengths come from BIG_LENS, the small edge cases (0, 1, P) and uniform
+    [0, 70000] (raftd's Update takes any Cmd []byte, /root/reference/raft/state_machine.go:126-145)."""
+    out = []
+    for g in range(G):
+        if rng.random() < p_none:
+            continue
+        n = int(rng.integers(1, nmax + 1))
+        pool = list(BIG_LENS) + [0, 1, P, int(rng.integers(0, 70001))]
+        lens = [int(x) for x in rng.choice(pool, n)]
+        cmds = [rng.integers(0, 256, ln, dtype=np.uint8).tobytes() for ln in lens]
+        out.append((base + g, int(rng.integers(0, R)), cmds))
+    return out
+
+
+def cross_check_caller(seed, G, R, T, batches=None, **cfg):
     kw = dict(groups=G, replicas=R, payload_bytes=64, max_entries_per_msg=8, log_capacity=64,
               snapshot_entries=20, compaction_overhead=5, drop_ppm=100000, seed=seed)
     kw.update(cfg)
@@ -113,8 +132,9 @@ def cross_check_caller(seed, G, R, T, **cfg):
     rng = np.random.default_rng(seed)
     P = kw["payload_bytes"]
     for t in range(T):
-        batches = random_batches(rng, G, R, kw["max_entries_per_msg"], P, maxc=kw.get("max_cmd_bytes"))
-        assert a.propose(batches) == 0 and b.propose(batches) == 0
+        bt = (batches(rng, G, R, P) if batches else
+              random_batches(rng, G, R, kw["max_entries_per_msg"], P, maxc=kw.get("max_cmd_bytes")))
+        assert a.propose(bt) == 0 and b.propose(bt) == 0
         _, _, camp, iso = random_inputs(rng, G, R, kw["max_entries_per_msg"])
         a.tick(None, None, camp, iso)
         b.tick(None, None, camp, iso)
@@ -167,6 +187,39 @@ def test_long_cmds_c_matches_python(seed, R, P, maxc, pages):
                 import zlib
                 assert e["crc"] == zlib.crc32(e["payload"])
     assert max(lens) > P, lens
+
+
+@pytest.mark.parametrize("seed,R,P", [(0, 3, 64), (1, 5, 256), (2, 2, 16)])
+def test_megabyte_cmds_c_matches_python(seed, R, P):
+    """Cmds of 8,191, 8,192, 65,536 and 1 MiB bytes (max_cmd_bytes 1 MiB, far past r03's 8,191-B
+    ceiling): stored, forwarded, replicated and CRC'd over exactly their length, identically in both
+    restatements, with zlib's CRC-32 of every stored Cmd."""
+    import zlib
+    a = cross_check_caller(700 + seed, G=3, R=R, T=40, batches=big_batches, payload_bytes=P,
+                           max_cmd_bytes=1 << 20)
+    lens = set()
+    for rid in range(a.nrep):
+        v = a.replica(rid)
+        for i in range(v["marker"] + 1, v["last"] + 1):
+            e = a.entry(rid, i, with_payload=True)
+            if e["type"] == 0:
+                lens.add(e["len"])
+                assert len(e["payload"]) == e["len"] and e["crc"] == (zlib.crc32(e["payload"]) if e["len"] else 0)
+    assert {8191, 8192, 65536, 1 << 20} & lens, lens
+    assert max(lens) == 1 << 20, lens
+
+
+def test_cmd_length_limits():
+    """max_cmd_bytes up to 16 MiB is accepted, beyond it refused (rg_create's rule); a Cmd longer than
+    max_cmd_bytes is refused by or_propose."""
+    base = dict(groups=1, replicas=3, payload_bytes=64, max_entries_per_msg=4, log_capacity=64)
+    make("c", max_cmd_bytes=1 << 24, **base)
+    with pytest.raises(Exception):
+        make("c", max_cmd_bytes=(1 << 24) + 1, **base)
+    o = make("c", max_cmd_bytes=1000, **base)
+    o.bootstrap()
+    assert o.propose([(0, 0, [bytes(1001)])]) == -1
+    assert o.propose([(0, 0, [bytes(1000)])]) == 0
 
 
 def lagging_apply(rng, e, nrep, p_notify=0.4):
