@@ -404,6 +404,30 @@ class DistEngine(_Feeds):
         """Whether this rank hosts replica `slot` of global shard `group` (placement)."""
         return rank_of(group, slot, self.N) == self.rank
 
+    def _local(self, group: int, slot: int):
+        """(half engine, its local replica id) of replica `slot` of global shard `group` (hosted here)."""
+        if not self.hosts(group, slot):
+            raise ValueError(f"replica {slot} of shard {group} is hosted by rank {rank_of(group, slot, self.N)}")
+        j = group // self.N
+        h = j // self.cols
+        return self.parts[h].eng, (j - h * self.cols) * self.R + slot
+
+    def replica_of(self, group: int, slot: int) -> dict:
+        """rg_read_replicas of replica `slot` of global shard `group` (hosted by this rank)."""
+        self.drain()
+        e, rid = self._local(group, slot)
+        return e.replica(rid)
+
+    def import_replica_of(self, group: int, slot: int, view, terms, types=None, payloads=None, lens=None):
+        """rg_import_replica of replica `slot` of global shard `group` (hosted by this rank)."""
+        self.drain()
+        e, rid = self._local(group, slot)
+        e.import_replica(rid, view, terms, types, payloads, lens)
+
+    @property
+    def t(self) -> int:
+        return self.eng.t
+
     def propose(self, batches):
         """rg_propose of the batches [(global group, slot, [Cmd bytes])] whose replica is hosted here."""
         per = {}
@@ -631,9 +655,49 @@ class LoopbackCluster(_Feeds):
         k, lr = self.loc[rid_src]
         self.engines[k].deliver(lr, **fields)
 
+    def rank_view(self, rank: int) -> "RankView":
+        """Rank `rank`'s share of this cluster, with a per-rank NodeHost's interface (tests: several
+        NodeHosts over one LoopbackCluster, the driver ticking the cluster once per tick)."""
+        return RankView(self, rank, self.N, self.R)
+
     def leader(self, group):
         """NodeHost.GetLeaderID as the node hosting slot 0 of the group sees it."""
         return self.engines[rank_of(group, 0, self.N)].leader(group)
 
     def sum_committed(self) -> int:
         return sum(e.sum_committed() for e in self.engines)
+
+
+class RankView:
+    """One rank's share of a whole-cluster backend (LoopbackCluster, or the oracle of every shard in
+    tests): the replicas `rank` hosts under the spread placement, addressed by (global shard, slot),
+    as raftd_amd.nodehost.NodeHost uses them. tick() is the backend's, which the driver calls once
+    per tick for all ranks (NodeHost.before_tick / after_tick around it)."""
+
+    def __init__(self, backend, rank: int, ranks: int, replicas: int):
+        self.b, self.rank, self.N, self.R = backend, rank, ranks, replicas
+
+    def hosts(self, group: int, slot: int) -> bool:
+        return rank_of(group, slot, self.N) == self.rank
+
+    def _rid(self, group: int, slot: int) -> int:
+        if not self.hosts(group, slot):
+            raise ValueError(f"replica {slot} of shard {group} is not hosted by rank {self.rank}")
+        return group * self.R + slot
+
+    def replica_of(self, group: int, slot: int) -> dict:
+        return self.b.replica(self._rid(group, slot))
+
+    def import_replica_of(self, group: int, slot: int, view, terms, types=None, payloads=None, lens=None):
+        self.b.import_replica(self._rid(group, slot), view, terms, types, payloads, lens)
+
+    def config_change(self, group: int, slot: int, op: int, target: int):
+        self._rid(group, slot)
+        rc = self.b.config_change(group, slot, op, target)
+        if rc not in (None, 0):
+            raise RuntimeError(f"config_change({group}, {slot}, {op}, {target}): {rc}")
+
+    @property
+    def t(self) -> int:
+        t = getattr(self.b, "t", None)
+        return t if t is not None else self.b.tick_count()

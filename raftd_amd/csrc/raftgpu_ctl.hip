@@ -123,7 +123,7 @@ hipError_t launch_control_t<RG_CTL_R>(const TickParams* p, uint32_t* perr, uint3
 template <>
 hipError_t launch_control_resident_t<RG_CTL_R>(const TickParams* p, uint32_t k, uint32_t* perr, uint32_t G,
                                               hipStream_t s) {
-#if defined(RG_DEV_NO_CONTROL) || RG_CTL_R > 4
+#if defined(RG_DEV_NO_CONTROL) || defined(RG_CTL_NO_RESIDENT) || RG_CTL_R > 4
   // R > 4: a control wave needs a SIMD of its own (occupancy 1), and a CU has four
   (void)p; (void)k; (void)perr; (void)G; (void)s;
   return hipErrorInvalidValue;
