@@ -518,6 +518,14 @@ def main():
     graph = graph_ticks(eng, pt, pc, G) if not spread and not args.wire_all else None
     x_ms = sum(a.elapsed_time(b) for a, b in xev) / args.steps if wire and not pipelined else 0.0
     va = eng.replica_array()  # every replica of this rank's first engine: invariant bits and drops
+    ctl_slow = None
+    fn = getattr(eng.L, "rg_debug_ctl_slow", None)
+    if fn is not None:  # replicas of the last tick whose step left the control fast path
+        import ctypes as C
+        fn.argtypes, fn.restype = [C.c_void_p, C.POINTER(C.c_uint32)], C.c_int
+        n_slow = C.c_uint32()
+        if fn(eng.h, C.byref(n_slow)) == 0:
+            ctl_slow = n_slow.value
     errs, drops = int((va["err"] != 0).sum()), int(va["drops"].sum())
     e2e = None
     if not spread:
@@ -621,6 +629,10 @@ def main():
             "tick_counts": {k: v for k, v in traffic.items() if k not in ("algorithmic_bytes", "bulk_bytes")},
         },
         "kernels_ms": {"control_kernel": ctl_ms, "bulk_kernel": bulk_ms},
+        "control_fast_path": {"enabled": os.environ.get("RAFTGPU_CTL_FAST", "1") != "0",
+                              "slow_replicas_last_tick": ctl_slow,
+                              "note": "control_kernel time = control_fast_kernel (steady-state branches, occupancy 2) + "
+                                      "control_slow_kernel (the full step for the replicas the fast kernel handed off)"},
         "exchange": None if not wire else {
             "mode": (f"pipelined over {args.halves} column halves: one half's all-to-all overlaps the other's "
                      "unpack + tick + pack" if pipelined else "serial: plan + pack + all-to-all + unpack, then tick"),

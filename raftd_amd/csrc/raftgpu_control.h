@@ -103,12 +103,24 @@ RG_FN void sel_set(T (&a)[R], uint32_t f, V val) {
 #endif
 using CTickParams = RG_CONST(const TickParams);
 
-template <int R>
+// FAST = true: the steady-state step (control_fast_kernel, DESIGN.md §3 "Fast path"). It implements the
+// paths a replica takes in steady state — a leader handling ReplicateResp / HeartbeatResp, ticking,
+// appending its synthetic proposal batch and replicating it; a follower appending a uniform Replicate at
+// its log end, committing and answering heartbeats — and ABORTS at every other branch (elections, term
+// changes, rejections, truncation, snapshots, membership changes, reads, caller Cmds, remote messages).
+// An aborted lane stores nothing: the full kernel (FAST = false) re-runs its whole step from the same
+// inputs. Every memory write the fast path made before aborting is one the full step makes too (same
+// decisions on the same inputs: outbox slots, fresh ring words past the old log end, job rows, S_NLPG),
+// or lies where nothing reads it (message slots past the final count, ring slots past the final last,
+// job rows past the final job count). Fewer live values: the fields only the aborted branches touch are
+// copied through at the end instead of living in registers for the whole step.
+template <int R, bool FAST = false>
 struct Ctl {
   // the tick's parameter block, read in place at each use (a device slot the host filled): the
   // fields are reloaded where needed instead of living in registers for the whole step (r02 kept a
   // 368-B copy, 279 SGPR spills at R = 3)
   CTickParams& p;
+  bool aborted = false;  // FAST: the step left the fast path (the full kernel re-runs it)
   uint32_t q, g, s;    // g = local column (indexes every device array)
   uint64_t gg, rid;    // global group and global replica id gg·R + s (RNG keys, loss hash)
   uint32_t gi;         // the global group as an index into this engine's tick-input arrays (< 2^32)
@@ -152,27 +164,37 @@ struct Ctl {
     gi = (uint32_t)pl_input_index(p.pl, gg);
     const uint64_t n = p.nrep;
     const uint64_t* a = p.s64_in + q;
-    term = a[S_TERM * n]; vote = a[S_VOTE * n]; leader = a[S_LEADER * n]; committed = a[S_COMMITTED * n];
-    applied = a[S_APPLIED * n]; last = a[S_LAST * n]; marker = a[S_MARKER * n]; marker_term = a[S_MARKER_TERM * n];
-    snap_index = a[S_SNAP_INDEX * n]; snap_term = a[S_SNAP_TERM * n]; cap_base = a[S_CAP_BASE * n];
-    processed = a[S_PROCESSED * n]; cc_hi = a[S_CC_HI * n];
     const uint32_t* b = p.s32_in + q;
+    term = a[S_TERM * n]; leader = a[S_LEADER * n]; committed = a[S_COMMITTED * n];
+    last = a[S_LAST * n]; marker = a[S_MARKER * n]; marker_term = a[S_MARKER_TERM * n];
+    cap_base = a[S_CAP_BASE * n];
     role = b[S_ROLE * n]; etick = b[S_ETICK * n]; htick = b[S_HTICK * n]; rand_to = b[S_RAND_TO * n];
-    rng_ctr = b[S_RNG_CTR * n]; granted = b[S_GRANTED * n]; responded = b[S_RESPONDED * n];
-    active = b[S_ACTIVE * n]; err = b[S_ERR * n]; drops = b[S_DROPS * n];
-    members = b[S_MEMBERS * n]; snap_members = b[S_SNAP_MEMBERS * n]; cc_pending = b[S_CC_PENDING * n];
+    active = b[S_ACTIVE * n]; drops = b[S_DROPS * n]; members = b[S_MEMBERS * n];
     hw = b[S_HW * n];
+    if constexpr (!FAST) {  // FAST: copied through by store() (no branch of the fast path reads them)
+      vote = a[S_VOTE * n]; applied = a[S_APPLIED * n]; snap_index = a[S_SNAP_INDEX * n];
+      snap_term = a[S_SNAP_TERM * n]; processed = a[S_PROCESSED * n]; cc_hi = a[S_CC_HI * n];
+      rng_ctr = b[S_RNG_CTR * n]; granted = b[S_GRANTED * n]; responded = b[S_RESPONDED * n];
+      err = b[S_ERR * n]; snap_members = b[S_SNAP_MEMBERS * n]; cc_pending = b[S_CC_PENDING * n];
+    } else {
+      vote = applied = snap_index = snap_term = processed = cc_hi = 0;
+      rng_ctr = granted = responded = err = snap_members = cc_pending = 0;
+    }
     sfor<0, R>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       rm[j] = p.rem_in[(0 * R + j) * n + q];
       rn[j] = p.rem_in[(1 * R + j) * n + q];
-      if constexpr (RS_MEM) p.rem_out[(2 * R + j) * n + q] = p.rem_in[(2 * R + j) * n + q];
+      if constexpr (FAST) rs[0] = 0;  // FAST: copied through by store()
+      else if constexpr (RS_MEM) p.rem_out[(2 * R + j) * n + q] = p.rem_in[(2 * R + j) * n + q];
       else rs[j] = p.rem_in[(2 * R + j) * n + q];
       rt[j] = p.rst_in[j * n + q];
     });
     if (last > marker) lt_set(last, *tr_at(last) & TERM_MASK);  // issued early, used after the inbox headers
     last_start = last; sent_hi = 0; rw_lo = ~0ull; rw_hi = 0; marker_start = marker;
     processed_start = processed; restored_at = 0; wlo = ~0ull; took = false;
+    if constexpr (FAST) {
+      if (role == CANDIDATE) abort_();  // every candidate path (votes, fallback) is the full step's
+    }
     // the last step compacted (or restored) below entry fidx: its stream position bounds the pages
     // to release, known now that the step which wrote it has stored its {crc, position} (the bulk
     // kernel). They go back to the pool at the end of this step; the capacity rule keeps lpg until
@@ -199,6 +221,7 @@ struct Ctl {
   // entries per load batch (RG_CTL_BATCH); at R >= 7 the remote arrays leave room for half as many
   static constexpr uint32_t CB = R >= 7 ? (RG_CTL_BATCH > 4 ? 4 : RG_CTL_BATCH) : RG_CTL_BATCH;
   RG_FN uint64_t ri() const { return (uint64_t)gi * R + s; }  // the replica's tick-input index
+  RG_FN void abort_() { aborted = true; }  // FAST: leave the fast path (the full kernel re-runs the step)
   RG_FN uint32_t quorum() const { return (uint32_t)__builtin_popcount(members) / 2 + 1; }  // voting members
   RG_FN bool is_member(uint32_t i) const { return (members >> i) & 1u; }
   RG_FN uint32_t my_id() const { return s + 1; }
@@ -241,6 +264,10 @@ struct Ctl {
   RG_FN void commit_to(uint64_t i) {
     if (i <= committed) return;
     if (i > last) {
+      if constexpr (FAST) {
+        abort_();
+        return;
+      }
       err |= ERR_BEYOND;
       return;
     }
@@ -265,6 +292,10 @@ struct Ctl {
                                       uint64_t hint_high, uint32_t src_a, uint32_t src_b) {
     const uint32_t dst = to - 1;
     if (dst >= (uint32_t)R) {  // unreachable with validated inputs (handle() and unpack check ids)
+      if constexpr (FAST) {
+        abort_();
+        return -1;
+      }
       err |= ERR_WIRE;
       return -1;
     }
@@ -377,9 +408,54 @@ struct Ctl {
     write_entries_(base, e0, n, kind, src, mt, word, aux, li, uspos, ucmd);
     RG_ACC(3, t0);
   }
+  // FAST: the only log write of the fast path — n entries at fresh indices (past every index read or
+  // sent this step: bank 0, nothing to flip), all holding one ring word (a leader's synthetic batch, its
+  // no-op, a follower's uniform Replicate), as one uniform job
+  RG_FN void write_fresh_uniform(uint64_t base, uint32_t n, uint32_t kind, uint32_t src, uint64_t word,
+                                 uint32_t uspos) {
+#ifdef RG_CTL_FASTREP
+    la_n = 0;
+#endif
+    wlo = umin64(wlo, base);
+    const uint32_t ncu = word_nc(word), tot = ncu * n;
+    if (n) lt_set(base + n - 1, word & TERM_MASK);
+    uint64_t* dst = tr_at(base);
+    uint32_t slot = (uint32_t)(base & (p.L - 1));
+    const uint64_t step = p.nrep, wrap = (uint64_t)p.L * p.nrep, wr = word & ~BANK_BIT;
+    for (uint32_t e = 0; e < n; ++e) {
+      *dst = wr;
+      dst += step;
+      if (++slot == p.L) {
+        slot = 0;
+        dst -= wrap;
+      }
+    }
+    const bool uni = ncu <= (p.P >> 4);
+    if (nj < p.J) {
+      const uint64_t n64 = p.nrep, JN = (uint64_t)p.J * n64;
+      uint64_t* j64 = p.job64 + (uint64_t)nj * n64 + q;
+      j64[J_FIRST * JN] = base;
+      j64[J_SPOS * JN] = kind == SRC_RING ? uspos : 0u;
+      j64[J_SMASK * JN] = (word & BANK_BIT) ? (n >= 64 ? ~0ull : (1ull << n) - 1) : 0ull;
+      j64[J_DMASK * JN] = 0;
+      uint32_t* j32 = p.job32 + (uint64_t)nj * n64 + q;
+      j32[J_META * JN] = job_meta(n, 0, kind, uni, uni ? ncu : 0u);
+      j32[J_SRC * JN] = src;
+      j32[J_DPOS * JN] = hw;
+      nj++;
+    }
+    hw += tot;
+  }
+
   RG_FN void write_entries_(uint64_t base, uint32_t e0, uint32_t n, uint32_t kind, uint32_t src,
                             const uint64_t* mt, uint64_t word, uint64_t aux, const uint2* li, uint32_t uspos,
                             bool ucmd) {
+    if constexpr (FAST) {  // the fast path writes through write_fresh_uniform only
+      (void)base; (void)e0; (void)n; (void)kind; (void)src; (void)mt; (void)word; (void)aux; (void)li;
+      (void)uspos; (void)ucmd;
+      abort_();
+      return;
+    } else {
     const uint64_t hi_prot = umax64(last_start, sent_hi);
 #ifdef RG_CTL_FASTREP
     la_n = 0;
@@ -522,6 +598,7 @@ struct Ctl {
       nj++;
     }
     hw += tot;
+    }
   }
 
   RG_FN uint32_t lpg() const { return lpg_; }
@@ -536,6 +613,12 @@ struct Ctl {
   // capacity rule.
   RG_FN bool append_local(uint32_t n, int slab_id, uint32_t rslot = 0, const uint2* li = nullptr,
                           const uint64_t* rmt = nullptr, uint64_t wofs = 0, uint32_t cc = 0, uint64_t cinfo = 0) {
+    if constexpr (FAST) {  // the fast path appends synthetic batches only (caller / forwarded Cmds, changes: full)
+      if (cc || rmt || li) {
+        abort_();
+        return false;
+      }
+    }
     if (last + n > cap_base + p.L) return false;
     const uint64_t base = last + 1;
     if (cc) {  // one ConfigChange entry: no Cmd, the descriptor in its length field
@@ -554,6 +637,14 @@ struct Ctl {
 #endif
     const bool syn = pay && !rmt && (!li || (li[0].x & SYN_OFF));  // generator Cmds: P bytes each
     const uint64_t w = syn ? term | len_bits(p.P) : term;
+    if constexpr (FAST) {
+      if (!plain) {
+        abort_();
+        return false;
+      }
+      if (!pay) write_fresh_uniform(base, n, SRC_NONE, 0, w, 0);
+      else write_fresh_uniform(base, n, SRC_SLAB, (uint32_t)slab_id | (rslot << 16), w, 0);
+    } else
     if (!pay) write_entries(base, 0, n, SRC_NONE, 0, nullptr, w);
     else if (rmt) write_entries(base, 0, n, SRC_WIRE_PROP, n, rmt, w, wofs);
     else if (syn) write_entries(base, 0, n, SRC_SLAB, (uint32_t)slab_id | (rslot << 16), nullptr, w);
@@ -590,6 +681,10 @@ struct Ctl {
     if (st == WAIT || st == SNAPSHOT) return;
     const uint64_t next = RG_GET(rn, to);
     if (next <= marker) {  // compacted: InstallSnapshot
+      if constexpr (FAST) {
+        abort_();
+        return;
+      }
       if (!(active & (1u << to))) return;
       if (snap_index == 0) {
         err |= ERR_EMPTY_SNAP;
@@ -605,6 +700,12 @@ struct Ctl {
     // (at R >= 7 the three extra live registers push the lane past 512 and into scratch: off there)
     const bool fast = R <= 6 && n > 0 && la_n > 0 && next >= la_base && next + n <= la_base + la_n;
     const uint64_t lt = !fast ? term_at(next - 1) : next == la_base ? la_pt : la_word & TERM_MASK;
+    if constexpr (FAST) {  // entries read back from the ring (a lagging follower): the full step's
+      if (n > 0 && !fast) {
+        abort_();
+        return;
+      }
+    }
 #else
     const uint64_t lt = term_at(next - 1);
 #endif
@@ -625,7 +726,7 @@ struct Ctl {
     if (k >= 0 && n > 0) {
       uint64_t* mt = p.mt_out + ((((uint64_t)s * R + to) * p.K + (uint32_t)k) * p.E) * p.G + g;
 #ifdef RG_CTL_FASTREP
-      if (fast) {
+      if (FAST || fast) {
         mt[0] = la_word;  // uniform: one word for every entry
       } else
 #endif
@@ -641,13 +742,21 @@ struct Ctl {
     }
   }
   RG_FN void broadcast_replicate() {
-    for (uint32_t i = 0; i < R; ++i)
+    for (uint32_t i = 0; i < R; ++i) {
       if (i != s && is_member(i)) send_replicate(i);
+      if (FAST && aborted) return;
+    }
   }
   RG_FN void broadcast_heartbeat() {
     // a pending ReadIndex rides on every heartbeat (dragonboat's broadcastHeartbeatMessage attaches
     // readIndex.peepCtx), so a lost read heartbeat or response is retried by the next round
     const uint64_t ctx = p.rdst ? p.rdst[(uint64_t)RI_CTX * p.nrep + q] : 0ull;
+    if constexpr (FAST) {  // a pending read: its confirmation round is the full step's
+      if (ctx) {
+        abort_();
+        return;
+      }
+    }
     for (uint32_t i = 0; i < R; ++i)
       if (i != s && is_member(i)) send(M_HEARTBEAT, i + 1, 0, 0, 0, 0, 0, umin64(RG_GET(rm, i), committed), ctx, 0, 0, 0);
   }
@@ -673,6 +782,29 @@ struct Ctl {
       // a uniform Replicate (local only): every entry carries the word mt[0]
       const bool uni = !remote && ((uint32_t)wofs & RG_UNIFORM) && n > 0;
       const uint64_t uw = uni ? mt0 : 0ull;  // loaded with the header (handle_)
+      if constexpr (FAST) {  // an append at the log end from a uniform Replicate (or an empty one)
+        if (li != last || (n > 0 && !uni) || remote) {
+          abort_();
+          return;
+        }
+        const uint64_t last_new = li + n;
+        if (n > 0) {  // every index is new: no conflict scan (entryLog.getConflictIndex finds li + 1)
+          if (last_new > cap_base + p.L || (p.P && !stream_fits(hw, lpg(), n * word_nc(uw), p.PTS))) {
+            drops++;  // capacity rules (ring, then payload stream): dropped, no reply
+            return;
+          }
+          if (li + 1 <= umax64(last_start, sent_hi)) {
+            abort_();
+            return;
+          }
+          write_fresh_uniform(li + 1, n, SRC_RING, src * p.G + g, uw, (uint32_t)upos);
+          last = last_new;
+        }
+        commit_to(umin64(last_new, mcommit));
+        if (aborted) return;
+        send_simple(M_REPLICATE_RESP, from, 0, last_new);
+        return;
+      }
       uint32_t k0 = n;
       for (uint32_t e = 0; e < n; ++e) {  // entryLog.getConflictIndex
         if (term_at(li + 1 + e) != ((uni ? uw : mt[(uint64_t)e * p.G]) & TERM_MASK)) {
@@ -784,6 +916,12 @@ struct Ctl {
   RG_FN void leader_replicate_resp(uint32_t reject, uint64_t li, uint64_t hint, uint32_t from) {
     const uint32_t f = from - 1;
     if (!is_member(f)) return;  // no remote for it
+    if constexpr (FAST) {  // a rejection walks the remote back (decreaseTo), a snapshot remote: the full step's
+      if (reject || RG_GET(rt, f) == SNAPSHOT) {
+        abort_();
+        return;
+      }
+    }
     active |= 1u << f;
     if (!reject) {
       const uint32_t st0 = RG_GET(rt, f);
@@ -833,6 +971,12 @@ struct Ctl {
   RG_FN void leader_heartbeat_resp(uint32_t from, uint64_t hint) {
     const uint32_t f = from - 1;
     if (!is_member(f)) return;  // no remote for it
+    if constexpr (FAST) {  // a read heartbeat's answer (readIndex.confirm): the full step's
+      if (hint != 0) {
+        abort_();
+        return;
+      }
+    }
     active |= 1u << f;
     if (RG_GET(rt, f) == WAIT) RG_SET(rt, f, (uint32_t)RETRY);
     if (RG_GET(rm, f) < last) send_replicate(f);
@@ -886,8 +1030,16 @@ struct Ctl {
   }
   RG_FN void check_quorum() {
     const uint32_t c = __builtin_popcount((active | (1u << s)) & members);  // leaderHasQuorum
-    active = 0;
-    if (c < quorum()) become_follower(term, 0);
+    if constexpr (FAST) {  // stepping down: the full step's
+      if (c < quorum()) {
+        abort_();
+        return;
+      }
+      active = 0;
+    } else {
+      active = 0;
+      if (c < quorum()) become_follower(term, 0);
+    }
   }
 
   // ---- proposals: nent Cmds (hm = those with a non-empty Cmd, the forwarded header's hint); their
@@ -895,6 +1047,12 @@ struct Ctl {
   // cc != 0: a membership change (one ConfigChange entry)
   RG_FN void handle_propose(uint32_t nent, uint32_t slab_id, uint32_t hop, uint64_t hm, uint32_t rslot,
                             const uint2* li, const uint64_t* rmt, uint64_t wofs, uint32_t cc, uint64_t cinfo) {
+    if constexpr (FAST) {  // forwarding, dropping at a candidate, membership changes: the full step's
+      if (role != LEADER || cc) {
+        abort_();
+        return;
+      }
+    }
     if (role == LEADER) {
       RG_T0(t0);
       const bool dropped = cc && cc_pending;  // one change at a time: an empty entry instead
@@ -903,6 +1061,7 @@ struct Ctl {
         drops++;
         return;
       }
+      if (FAST && aborted) return;
       if (dropped) drops++;        // reportDroppedConfigChange
       else if (cc) cc_pending = 1;  // setPendingConfigChange
       RG_ACC(0, t0);
@@ -923,6 +1082,7 @@ struct Ctl {
       if (etick >= p.ET) {
         etick = 0;
         if (p.CQ) check_quorum();
+        if (FAST && aborted) return;
       }
       htick++;
       if (htick >= p.HT) {
@@ -932,6 +1092,10 @@ struct Ctl {
     } else {
       etick++;
       if (is_member(s) && etick >= rand_to) {  // selfRemoved: no elections
+        if constexpr (FAST) {  // a campaign: the full step's
+          abort_();
+          return;
+        }
         etick = 0;
         handle_node_election();
       }
@@ -997,6 +1161,45 @@ struct Ctl {
     const uint64_t mterm = hw(1);
     const uint32_t type = (uint32_t)(w0 & 0xFF);
     const uint32_t from = (uint32_t)(w0 >> 8) & 0xFF;
+    if constexpr (FAST) {
+      // same-term steady-state traffic only: a term change, a remote message, a vote, a read, a
+      // forwarded proposal or a snapshot leaves the fast path (a candidate never entered it)
+      if (remote || from - 1 >= (uint32_t)R || (mterm != 0 && mterm != term) ||
+          (type == M_REPLICATE && (uint32_t)(w0 >> 32) > p.E)) {
+        abort_();
+        return;
+      }
+      switch (type) {
+        case M_REPLICATE:
+        case M_HEARTBEAT:
+          if (role == LEADER) return;  // a leader ignores them (as the full step's dispatch does)
+          etick = 0;
+          leader = from;
+          if (type == M_REPLICATE) {
+            handle_replicate(w0, hw(2), hw(3), hw(4), from, src, k, remote, hw(7), hw(5), mt0);
+          } else {
+            if (hw(5) || hw(6)) {  // a read heartbeat (its context echoed): the full step's
+              abort_();
+              return;
+            }
+            commit_to(hw(4));
+            if (aborted) return;
+            send_simple(M_HEARTBEAT_RESP, from, 0, 0, 0, 0);
+          }
+          return;
+        case M_REPLICATE_RESP:
+          if (role == LEADER) leader_replicate_resp((uint32_t)(w0 >> 24) & 0xFF, hw(3), hw(5), from);
+          return;
+        case M_HEARTBEAT_RESP:
+          if (role == LEADER) leader_heartbeat_resp(from, hw(5));
+          return;
+        case M_NOOP:
+          return;
+        default:
+          abort_();
+          return;
+      }
+    }
     if (from - 1 >= (uint32_t)R) {  // unreachable: local senders stamp their id, unpack checks remote ones
       err |= ERR_WIRE;
       return;
@@ -1111,6 +1314,7 @@ struct Ctl {
       constexpr int src = decltype(jc)::value;
       if (cnt_pf[src] > p.K) {  // never produced by a sender (unpack_kernel clamps received counts): ERR_WIRE
         RG_OOB("RG_BOUNDS control q=%u src=%u cnt=%u > K=%u\n", q, (uint32_t)src, cnt_pf[src], p.K);
+        if constexpr (FAST) abort_();
         err |= ERR_WIRE;
         cnt_pf[src] = 0;
       }
@@ -1130,7 +1334,7 @@ struct Ctl {
       return false;
     };
     uint32_t cs = 0, ck = 0;
-    bool have = next_msg(0, ~0u, cs, ck);
+    bool have = !(FAST && aborted) && next_msg(0, ~0u, cs, ck);
     Hdr cur{};
     if (have) load_hdr(cs, ck, pl_remote(p.pl, cs, s, g), cur);
     while (have) {
@@ -1142,11 +1346,16 @@ struct Ctl {
       cur = nxt;
       cs = ns;
       ck = nk;
-      have = more;
+      have = more && !(FAST && aborted);
     }
     RG_STAMP(1);
+    if constexpr (FAST) {  // a campaign input, a membership change or a read at this replica: the full step's
+      if (in_camp || (in_cc && (in_cc & 0xFFu) == s) || in_rd) abort_();
+      if (aborted) return;
+    }
     if (in_camp) handle_node_election();
     if (!(p.flags & 1u)) tick();
+    if (FAST && aborted) return;
     RG_STAMP(2);
     if (in_pt == s) {
       const uint32_t n = in_pc;
@@ -1164,6 +1373,7 @@ struct Ctl {
           cinfo = pc.x | ((uint64_t)pc.y << 32);
         }
         handle_propose(n, sl, 0, hm, s, li, nullptr, 0, 0, cinfo);
+        if (FAST && aborted) return;
       }
     }
     {  // 4a: membership change input (rg_config_change)
@@ -1172,12 +1382,32 @@ struct Ctl {
     }
     if (in_rd) handle_read_index(my_id(), in_rd);  // 4b: ReadIndex input (rg_read_index)
     RG_STAMP(3);
+    if constexpr (FAST) {
+      // the fields only the end of the step reads, loaded here (after a compiler barrier, so their
+      // loads are not hoisted to the start of the step and their registers are not held through it)
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__GNUC__)
+      asm volatile("" ::: "memory");
+#endif
+      const uint64_t n = p.nrep;
+      const uint64_t* a = p.s64_in + q;
+      processed = processed_start = a[S_PROCESSED * n];
+      cc_hi = a[S_CC_HI * n];
+      applied = a[S_APPLIED * n];
+      snap_index = a[S_SNAP_INDEX * n];
+    }
     // GetUpdate.CommittedEntries = (processed, committed], then commitUpdate; applied follows unless
     // the state machine reports it (rg_notify_applied); snapshot + compaction on applied
     // the rsm applies the ConfigChange entries it is handed (none past cc_hi)
     for (uint64_t i = umax64(processed_start, restored_at) + 1; i <= umin64(committed, cc_hi); ++i) {
       const uint64_t w = *tr_at(i);
-      if ((w & TYPE_BIT) && word_len(w)) apply_config_change(word_len(w));
+      if ((w & TYPE_BIT) && word_len(w)) {
+        if constexpr (FAST) {  // applying a membership change: the full step's
+          abort_();
+          return;
+        } else {
+          apply_config_change(word_len(w));
+        }
+      }
     }
     processed = committed;
     if (!p.AF) applied = processed;
@@ -1205,6 +1435,22 @@ struct Ctl {
   }
 
   RG_FN void store() {
+    if constexpr (FAST) {  // the fields no fast branch changes: copied through from the step's input state
+      const uint64_t n = p.nrep;
+      const uint64_t* ai = p.s64_in + q;
+      const uint32_t* bi = p.s32_in + q;
+      vote = ai[S_VOTE * n];
+      if (!took) {
+        snap_term = ai[S_SNAP_TERM * n];
+        snap_members = bi[S_SNAP_MEMBERS * n];
+      }
+      rng_ctr = bi[S_RNG_CTR * n]; granted = bi[S_GRANTED * n]; responded = bi[S_RESPONDED * n];
+      err = bi[S_ERR * n]; cc_pending = bi[S_CC_PENDING * n];
+      sfor<0, R>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        p.rem_out[(2 * R + j) * n + q] = p.rem_in[(2 * R + j) * n + q];
+      });
+    }
     const uint64_t n = p.nrep;
     uint64_t* a = p.s64_out + q;
     a[S_TERM * n] = term; a[S_VOTE * n] = vote; a[S_LEADER * n] = leader; a[S_COMMITTED * n] = committed;
@@ -1224,7 +1470,7 @@ struct Ctl {
       constexpr int j = decltype(jc)::value;
       p.rem_out[(0 * R + j) * n + q] = rm[j];
       p.rem_out[(1 * R + j) * n + q] = rn[j];
-      if constexpr (!RS_MEM) p.rem_out[(2 * R + j) * n + q] = rs[j];
+      if constexpr (!RS_MEM && !FAST) p.rem_out[(2 * R + j) * n + q] = rs[j];
       p.rst_out[j * n + q] = (uint8_t)rt[j];
       p.cnt_out[((uint64_t)s * R + j) * p.G + g] = get8(oc, j);
     });

@@ -23,14 +23,12 @@ namespace rg {
 // the block's checksum (uniform scalar loads): a stale or torn block becomes a sticky engine error
 // (*perr, a separate kernel argument, reported by the next synchronising call) instead of wild
 // addresses. Ctl reads the fields in place.
-template <int R>
-__global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_MINWAVES) control_kernel(const TickParams* __restrict__ pp,
-                                                                               uint32_t* perr) {
-  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-  // The checksum: lane i loads word i (one coalesced 424-B wave load, through a laundered pointer so
-  // it stays separate from the step's scalar field reads) and the wave sums the terms with a
-  // butterfly. r03a's volatile chain cost 53 dependent cache-bypassing loads per wave; a chain of
-  // seven s_load_dwordx16 (r03b) still waited seven scalar round trips at the head of every wave.
+// The checksum: lane i loads word i (one coalesced 424-B wave load, through a laundered pointer so
+// it stays separate from the step's scalar field reads) and the wave sums the terms with a
+// butterfly. r03a's volatile chain cost 53 dependent cache-bypassing loads per wave; a chain of
+// seven s_load_dwordx16 (r03b) still waited seven scalar round trips at the head of every wave.
+// On a mismatch the first lane of the launch reports it (sticky *perr) and every wave returns.
+__device__ __forceinline__ bool tp_verify(const TickParams* pp, uint32_t* perr, uint32_t q, const char* kname) {
   const TickParams* pc = pp;
   asm volatile("" : "+s"(pc));
   const uint32_t lane = threadIdx.x & 63u;
@@ -45,12 +43,20 @@ __global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_MINWAVES) control_kernel(
   }
   if (h != wv[TP_WORDS]) {
     if (q == 0) {
-      printf("raftgpu: control_kernel parameter block checksum mismatch (tick %llu): launch skipped\n",
+      printf("raftgpu: %s parameter block checksum mismatch (tick %llu): launch skipped\n", kname,
              (unsigned long long)pp->tick);
       atomicOr(perr, 1u);
     }
-    return;
+    return false;
   }
+  return true;
+}
+
+template <int R>
+__global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_MINWAVES) control_kernel(const TickParams* __restrict__ pp,
+                                                                               uint32_t* perr) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (!tp_verify(pp, perr, q, "control_kernel")) return;
   CTickParams& cp = *(CTickParams*)pp;
   if (q >= cp.nrep) return;
 #ifdef RG_CTL_PROFILE
@@ -60,6 +66,43 @@ __global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_MINWAVES) control_kernel(
 #else
   Ctl<R> c(cp, q);
 #endif
+  c.run();
+}
+
+// ---- the fast path (DESIGN.md §3 "Fast path"): Ctl<R, true> steps every replica through the
+// steady-state branches only and hands a replica whose step leaves them to the slow kernel, which
+// re-runs that replica's whole step with the full Ctl<R> (an aborted fast step stored nothing).
+#ifndef RG_CTL_FAST_WAVES
+#define RG_CTL_FAST_WAVES (RG_CTL_R <= 6 ? 2 : 1)  // R 7, 8: two waves would need scratch
+#endif
+template <int R>
+__global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_FAST_WAVES) control_fast_kernel(
+    const TickParams* __restrict__ pp, uint32_t* perr) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (!tp_verify(pp, perr, q, "control_fast_kernel")) return;
+  CTickParams& cp = *(CTickParams*)pp;
+  if (q == 0) cp.slow_cnt[(cp.tick + 1) & 1] = 0;  // the next tick's counter (its last reader ran before us)
+  if (q >= cp.nrep) return;
+  Ctl<R, true> c(cp, q);
+  c.run();
+  // hand-off: the lane's flag for the slow kernel, and one counter atomic per wave with aborted lanes
+  // (the count is for measurement: rg_debug_ctl_slow)
+  cp.slow_flag[q] = c.aborted ? 1u : 0u;
+  const uint64_t m = __ballot(c.aborted);
+  if (m && (threadIdx.x & 63u) == (uint32_t)__ffsll((long long)m) - 1)
+    atomicAdd(cp.slow_cnt + (cp.tick & 1), (uint32_t)__popcll(m));
+}
+
+// the replicas the fast kernel handed off this tick (a wave without one leaves at once). Lane q steps
+// replica q, as control_kernel does: the affine lane -> replica map keeps its registers the same.
+template <int R>
+__global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_MINWAVES) control_slow_kernel(const TickParams* __restrict__ pp,
+                                                                                    uint32_t* perr) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (!tp_verify(pp, perr, q, "control_slow_kernel")) return;
+  CTickParams& cp = *(CTickParams*)pp;
+  if (q >= cp.nrep || !cp.slow_flag[q]) return;
+  Ctl<R> c(cp, q);
   c.run();
 }
 
@@ -116,6 +159,19 @@ hipError_t launch_control_t<RG_CTL_R>(const TickParams* p, uint32_t* perr, uint3
 #else
   hipLaunchKernelGGL(control_kernel<RG_CTL_R>, dim3((nrep + RG_CTL_BLOCK - 1) / RG_CTL_BLOCK), dim3(RG_CTL_BLOCK), 0, s,
                      p, perr);
+  return hipGetLastError();
+#endif
+}
+
+template <>
+hipError_t launch_control_fast_t<RG_CTL_R>(const TickParams* p, uint32_t* perr, uint32_t nrep, hipStream_t s) {
+#if defined(RG_DEV_NO_CONTROL) || !defined(RG_CTL_FASTREP)  // the fast path builds on the uniform Replicate
+  (void)p; (void)perr; (void)nrep; (void)s;
+  return hipErrorInvalidValue;
+#else
+  const dim3 grid((nrep + RG_CTL_BLOCK - 1) / RG_CTL_BLOCK), block(RG_CTL_BLOCK);
+  hipLaunchKernelGGL(control_fast_kernel<RG_CTL_R>, grid, block, 0, s, p, perr);
+  hipLaunchKernelGGL(control_slow_kernel<RG_CTL_R>, grid, block, 0, s, p, perr);
   return hipGetLastError();
 #endif
 }

@@ -143,6 +143,10 @@ struct rg_engine {
   bool tp_used[TP_SLOTS / TP_CHUNK] = {};
   uint64_t tp_next = 0;
   uint32_t tp_corrupt = 0;  // tests (rg_debug_corrupt_params): seal the next n blocks with a wrong checksum
+  // the control fast path: control_fast_kernel then control_slow_kernel over the replicas it
+  // handed off ([2] counters by tick parity, then the list); RAFTGPU_CTL_FAST=0: control_kernel alone (A/B)
+  uint32_t* slow = nullptr;
+  bool ctl_fast = true;
   uint8_t* stage = nullptr;
   uint64_t stage_bytes = 0;
   uint64_t t = 0;
@@ -353,6 +357,10 @@ static TickParams params_at(rg_engine* e, uint64_t tk) {
   p.prof = e->prof;
   p.info = e->info;
   p.pool = e->poolctl;
+  if (e->ctl_fast) {
+    p.slow_cnt = e->slow;
+    p.slow_flag = e->slow + 2;
+  }
   return p;
 }
 
@@ -486,6 +494,7 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
     if (rc == RG_OK) rc = dalloc(e, &e->jcnt[b], n * 4);
   }
   if (rc == RG_OK) rc = dalloc(e, &e->crc_err, n * 4);
+  if (rc == RG_OK) rc = dalloc(e, &e->slow, (n + 2) * 4);
   if (rc == RG_OK) rc = dalloc(e, &e->slabs, (uint64_t)c.num_slabs * e->slab_rows * E * P);
   if (rc == RG_OK) rc = dalloc(e, &e->slab_info, (uint64_t)c.num_slabs * e->slab_rows * E * sizeof(uint2));
   e->cmd_used.assign(c.num_slabs, 0);
@@ -651,6 +660,7 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   e->bulk_tile = tile;
   if (const char* v = getenv("RAFTGPU_APPLY_MEMCPY")) e->copy_kernel = !(v[0] == '1');
   e->bulk_mj = c.max_entries_per_msg <= 16;
+  if (const char* v = getenv("RAFTGPU_CTL_FAST")) e->ctl_fast = v[0] != '0';
   if (const char* v = getenv("RAFTGPU_BULK_MULTIJOB")) e->bulk_mj = v[0] == '1';
   if (const char* v = getenv("RAFTGPU_APPLY_SDMA"))
     if (v[0] == '1') {
@@ -830,6 +840,7 @@ int rg_bootstrap(rg_engine* e) {
   e->rd_staged = e->rd_reset_pending = false;
   HIPCHK(hipMemsetAsync(e->rdst, 0, (uint64_t)RD_ROWS * e->nrep * 8, e->stream));
   HIPCHK(hipMemsetAsync(e->crc_err, 0, (uint64_t)e->nrep * 4, e->stream));
+  HIPCHK(hipMemsetAsync(e->slow, 0, 8, e->stream));  // the fast path's hand-off counters
   HIPCHK(launch_pool_reset(e->fring, e->npages, e->poolctl, e->stream));  // every stream empty, every page free
   std::fill(e->cmd_used.begin(), e->cmd_used.end(), 0ull);
   std::fill(e->cmd_tick.begin(), e->cmd_tick.end(), ~0ull);
@@ -1152,7 +1163,11 @@ static int launch_control_slot(rg_engine* e, const TickParams& p) {
     HIPCHK(hipEventRecord(e->tp_ev[c], e->stream));
     e->tp_used[c] = true;
   }
-  LAUNCH(launch_control(e->d_tp + k, &e->poolctl->param_err, p.R, p.nrep, e->stream), e->stream, "control_kernel");
+  if (e->ctl_fast)
+    LAUNCH(launch_control_fast(e->d_tp + k, &e->poolctl->param_err, p.R, p.nrep, e->stream), e->stream,
+           "control_fast_kernel / control_slow_kernel");
+  else
+    LAUNCH(launch_control(e->d_tp + k, &e->poolctl->param_err, p.R, p.nrep, e->stream), e->stream, "control_kernel");
   return RG_OK;
 }
 
@@ -1320,7 +1335,9 @@ static int tick_graph(rg_engine* e, const rg_tick_input* in, uint32_t k) {
         TickParams* hs = e->g_htp + set * G_MAXK + i;
         TickParams* ds = e->g_dtp + set * G_MAXK + i;
         hipError_t r = hipMemcpyAsync(ds, hs, sizeof(TickParams), hipMemcpyHostToDevice, e->stream);
-        if (r == hipSuccess) r = launch_control(ds, &e->poolctl->param_err, p.R, p.nrep, e->stream);
+        if (r == hipSuccess)
+          r = e->ctl_fast ? launch_control_fast(ds, &e->poolctl->param_err, p.R, p.nrep, e->stream)
+                          : launch_control(ds, &e->poolctl->param_err, p.R, p.nrep, e->stream);
         if (r == hipSuccess && e->c.payload_bytes) {
           PoolParams pp{};
           pp.nrep = e->nrep; pp.PTS = e->PTS; pp.npages = e->npages;
@@ -1864,6 +1881,18 @@ extern "C" int rg_debug_ctl_profile(rg_engine* e, uint32_t* out) {
   return RG_OK;
 }
 #endif
+
+// measurement / tests (not in include/raftgpu.h): replicas of the last tick whose step left the control
+// fast path and ran in the full kernel (0 with RAFTGPU_CTL_FAST=0)
+extern "C" int rg_debug_ctl_slow(rg_engine* e, uint32_t* n) {
+  if (!e || !n) return fail(RG_EINVAL, "rg_debug_ctl_slow args");
+  if (int jrc = join(e)) return jrc;
+  *n = 0;
+  if (!e->ctl_fast || e->t == 0) return RG_OK;
+  HIPCHK(hipMemcpyAsync(n, e->slow + ((e->t - 1) & 1), 4, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return RG_OK;
+}
 
 // tests only (not in include/raftgpu.h): the next n control launches get a parameter block whose
 // checksum does not match (the control kernel must skip the tick, the pool and payload stages must

@@ -245,6 +245,11 @@ struct TickParams {
   RG_G(uint64_t) rdst;              // [RD_ROWS][nrep] ReadIndex state
   RG_G(const uint2) info;           // [2 banks][nrep][L] {slot crc, stream position} (a freed stream's bound)
   RG_G(PoolCtl) pool;               // sticky param_err on a checksum mismatch
+  // the fast path's hand-off: control_fast_kernel sets slow_flag[q] for a replica whose
+  // step left the fast path (and counts them in slow_cnt[tick & 1], for measurement); control_slow_kernel
+  // re-runs those steps. slow_cnt[(tick + 1) & 1] is zeroed by the fast launch (its readers are done)
+  RG_G(uint32_t) slow_cnt;          // [2] (NULL: no fast path; control_kernel steps every replica)
+  RG_G(uint32_t) slow_flag;         // [nrep]
   uint64_t csum;                    // tp_checksum of every word above (host-computed, checked first)
 };
 // the parameter block's checksum: Σ_i tp_mix(word_i + (i + 1)·φ) mod 2^64 over its words before `csum`
@@ -348,12 +353,17 @@ RG_HD_INLINE uint64_t stream_byte(const uint32_t* pt, uint32_t PTS, uint32_t q, 
 // host-side launchers (raftgpu_kernels.hip)
 // control_kernel<R> over nrep lanes; *p: the tick's parameter block in device memory
 hipError_t launch_control(const TickParams* p, uint32_t* perr, uint32_t R, uint32_t nrep, hipStream_t s);
+// the fast path: control_fast_kernel<R> over every replica, then control_slow_kernel<R> over the replicas
+// it handed off (the parameter block's slow_cnt / slow_flag)
+hipError_t launch_control_fast(const TickParams* p, uint32_t* perr, uint32_t R, uint32_t nrep, hipStream_t s);
 // k ticks of a metadata-only one-rank engine in one launch (p = k consecutive sealed blocks)
 hipError_t launch_control_resident(const TickParams* p, uint32_t k, uint32_t* perr, uint32_t R, uint32_t G,
                                    hipStream_t s);
 // one instantiation per translation unit (raftgpu_ctl.hip -DRG_CTL_R, raftgpu_bulk.hip -DRG_BULK_W/MJ)
 template <int R>
 hipError_t launch_control_t(const TickParams* p, uint32_t* perr, uint32_t nrep, hipStream_t s);
+template <int R>
+hipError_t launch_control_fast_t(const TickParams* p, uint32_t* perr, uint32_t nrep, hipStream_t s);
 template <int R>
 hipError_t launch_control_resident_t(const TickParams* p, uint32_t k, uint32_t* perr, uint32_t G, hipStream_t s);
 template <bool W, bool MJ>

@@ -30,9 +30,9 @@ def make(kind: str, **cfg):
     if kind == "gpu":
         from raftd_amd.engine import Engine
         return Engine(**cfg)
-    if kind in ("ctl", "ctl-asan"):
+    if kind in ("ctl", "ctl-asan", "ctl-fast", "ctl-fast-asan"):
         from native.ctl_host import CtlHost
-        return CtlHost(asan=kind == "ctl-asan", **cfg)
+        return CtlHost(asan=kind.endswith("asan"), fast="fast" in kind, **cfg)
     raise ValueError(kind)
 
 

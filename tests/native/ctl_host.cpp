@@ -14,6 +14,8 @@
 using namespace rg;
 
 struct Host {
+  int fast = 0;             // ch_set_fast: the fast-path step first, the full step for a lane it hands off
+  uint64_t slow_lanes = 0;  // lanes the fast path handed off (all ticks)
   rg_config c;
   uint32_t nrep, J;
   std::vector<uint64_t> s64[2], rem[2], tr, hdr[2], mt[2], job64;
@@ -106,6 +108,9 @@ void* ch_create(const rg_config* c) {
 }
 
 void ch_destroy(void* hh) { delete (Host*)hh; }
+// the fast path (control_fast_kernel + control_slow_kernel on the device): on = 1
+void ch_set_fast(void* hh, int on) { ((Host*)hh)->fast = on; }
+uint64_t ch_slow_lanes(void* hh) { return ((Host*)hh)->slow_lanes; }
 
 // placement math of raftgpu_internal.h, for the CPU cross-check with raftd_amd/cluster.py
 uint64_t ch_pl_group(uint32_t N, uint32_t rank, uint32_t s, uint32_t j) {
@@ -190,11 +195,20 @@ int ch_tick(void* hh, const rg_tick_input* in) {
   if (h->cc_staged) p.cc_in = h->cc.data();
   for (uint32_t q = 0; q < h->nrep; ++q) {
     switch (h->c.replicas) {
-#define RG_CASE(r) \
-  case r: {        \
-    Ctl<r> c(p, q); \
-    c.run();       \
-    break;         \
+#define RG_CASE(r)                 \
+  case r: {                        \
+    bool full = true;              \
+    if (h->fast) {                 \
+      Ctl<r, true> f(p, q);        \
+      f.run();                     \
+      full = f.aborted;            \
+      h->slow_lanes += full;       \
+    }                              \
+    if (full) {                    \
+      Ctl<r> c(p, q);              \
+      c.run();                     \
+    }                              \
+    break;                         \
   }
       RG_CASE(1) RG_CASE(2) RG_CASE(3) RG_CASE(4) RG_CASE(5) RG_CASE(6) RG_CASE(7) RG_CASE(8)
 #undef RG_CASE

@@ -35,7 +35,7 @@ def build(asan: bool = False) -> str:
 
 
 class CtlHost:
-    def __init__(self, asan: bool = False, **cfg):
+    def __init__(self, asan: bool = False, fast: bool = False, **cfg):
         from raftd_amd.engine import Config, MsgView, ReplicaView, default_config  # struct layouts only
         self._MsgView, self._ReplicaView = MsgView, ReplicaView
         self.cfg = default_config(**cfg)
@@ -49,8 +49,17 @@ class CtlHost:
         for k, v in self.cfg.items():
             setattr(c, k, v)
         self.h = self.L.ch_create(C.byref(c))
+        self.L.ch_set_fast.argtypes = [vp, C.c_int]
+        self.L.ch_slow_lanes.argtypes = [vp]
+        self.L.ch_slow_lanes.restype = C.c_uint64
+        self.L.ch_set_fast(C.c_void_p(self.h), 1 if fast else 0)
         self.G, self.R = self.cfg["groups"], self.cfg["replicas"]
         self.nrep = self.G * self.R
+
+    @property
+    def slow_lanes(self) -> int:
+        """Lanes the fast path handed to the full step so far (fast mode)."""
+        return self.L.ch_slow_lanes(C.c_void_p(self.h))
 
     def close(self):
         if self.h:

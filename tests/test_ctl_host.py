@@ -57,6 +57,42 @@ def test_control_step_matches_oracle(R):
     xcheck("ctl", 10 + R, G=5, R=R, T=120)
 
 
+@pytest.mark.parametrize("R", [1, 2, 3, 5, 8])
+def test_fast_path_matches_oracle(R):
+    """The fast-path step (Ctl<R, true>: the steady-state branches, handing every other step to the
+    full Ctl<R>) under chaos — loss, isolation, elections, truncation, snapshots — equals the oracle."""
+    xcheck("ctl-fast", 30 + R, G=5, R=R, T=120)
+
+
+def test_fast_path_membership_and_heavy_loss():
+    xcheck("ctl-fast", 88, G=6, R=5, T=160, drop_ppm=300000, max_msgs_per_pair=4, p_cc=0.05)
+
+
+@pytest.mark.parametrize("R,P", [(3, 256), (5, 64), (3, 0)])
+def test_fast_path_covers_the_steady_state(R, P):
+    """Steady-state leaders with a full batch every tick (the benchmark's workload, snapshots and
+    compaction included): after the election no replica's step leaves the fast path."""
+    G, E = 8, 16
+    kw = dict(groups=G, replicas=R, payload_bytes=P, max_entries_per_msg=E, log_capacity=256,
+              snapshot_entries=100, compaction_overhead=5, seed=9)
+    a, b = make("ctl-fast", **kw), make("c", **kw)
+    for e in (a, b):
+        e.bootstrap()
+    camp = np.zeros(G * R, np.uint8)
+    camp[0::R] = 1
+    pt, pc = np.zeros(G, np.uint8), np.full(G, E, np.uint32)
+    for t in range(60):
+        ins = dict(campaign=camp) if t == 1 else dict(prop_target=pt, prop_count=pc) if t >= 6 else {}
+        if t == 10:
+            slow0 = a.slow_lanes
+        a.tick(**ins)
+        b.tick(**ins)
+        for rid in range(G * R):
+            assert a.replica(rid) == b.replica(rid), (t, rid)
+    assert b.replica(0)["snap_index"] > 0  # the run went through snapshots and compaction
+    assert a.slow_lanes == slow0, a.slow_lanes - slow0
+
+
 def test_control_step_heavy_loss():
     xcheck("ctl", 77, G=6, R=5, T=200, drop_ppm=300000, max_msgs_per_pair=4)
 
@@ -94,6 +130,7 @@ def test_control_step_under_asan():
     code = ("import sys; sys.path[:0] = [%r, %r]; import test_ctl_host as t; "
             "t.xcheck('ctl-asan', 5, G=3, R=3, T=60); t.xcheck('ctl-asan', 6, G=2, R=5, T=60); "
             "t.xcheck('ctl-asan', 7, G=3, R=8, T=80, p_cc=0.08); "
+            "t.xcheck('ctl-fast-asan', 8, G=3, R=3, T=80, p_cc=0.05); t.xcheck('ctl-fast-asan', 9, G=2, R=5, T=60); "
             "import kat_scenarios as K; fx = K.load('kat_check_msgapp.json'); "
             "[K.run_check_msgapp('ctl-asan', fx, c) for c in fx['cases']]; print('ASAN-CLEAN')"
             % (HERE, os.path.dirname(HERE)))

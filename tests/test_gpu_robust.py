@@ -45,3 +45,32 @@ def test_corrupt_parameter_block_is_reported_and_harmless():
     with pytest.raises(RgError):
         gpu.sync()
     assert gpu.pool_stats()["free"] == before["free"]
+
+
+def test_control_fast_path_covers_the_steady_state():
+    """The benchmark's steady state (leaders with full batches every tick, snapshots and compaction)
+    never leaves the control fast path (rg_debug_ctl_slow = 0 per tick after the election), an
+    election does (the full kernel steps the candidates), and every replica equals the oracle."""
+    G, R, E = 512, 3, 64
+    cfg = dict(groups=G, replicas=R, log_capacity=256, payload_bytes=256, max_entries_per_msg=E,
+               snapshot_entries=100, compaction_overhead=5, seed=0x5EED)
+    gpu, ora = make("gpu", **cfg), make("c", **cfg)
+    fn = gpu.L.rg_debug_ctl_slow
+    fn.argtypes, fn.restype = [C.c_void_p, C.POINTER(C.c_uint32)], C.c_int
+    n = C.c_uint32()
+    for e in (gpu, ora):
+        e.bootstrap()
+    camp = np.zeros(G * R, np.uint8)
+    camp[0::R] = 1
+    pt, pc = np.zeros(G, np.uint8), np.full(G, E, np.uint32)
+    slow = []
+    for t in range(40):
+        ins = dict(campaign=camp) if t == 1 else dict(prop_target=pt, prop_count=pc) if t >= 6 else {}
+        gpu.tick(**ins)
+        ora.tick(**ins)
+        assert fn(gpu.h, C.byref(n)) == 0
+        slow.append(n.value)
+    for rid in range(G * R):
+        assert gpu.replica(rid) == ora.replica(rid), rid
+    assert ora.replica(0)["snap_index"] > 0
+    assert slow[1] > 0 and max(slow[12:]) == 0, slow
