@@ -274,6 +274,14 @@ int rg_fill_slabs(rg_engine* e);
  * shard in one tick) — nothing is staged then. The next rg_tick / rg_tick_device takes the staged
  * batches and must not also carry rg_tick_input.prop_target. */
 int rg_propose(rg_engine* e, const rg_proposal* props, size_t n, const uint8_t* payload, const uint32_t* lens);
+/* Register a long-lived host buffer the caller stages Cmds in (hipHostRegister: page-locked until
+ * rg_host_unregister or rg_destroy). An rg_propose whose payload lies inside a registered range and
+ * whose Cmds are packed the way the device arena holds them (every Cmd of a batch but its last a
+ * multiple of 16 B, the batches in few contiguous runs) is copied by DMA straight from it, without
+ * the host copy into pinned staging (DESIGN.md §4 "Ingest"); still copied before return. Ranges may
+ * not overlap. */
+int rg_host_register(rg_engine* e, const void* p, size_t bytes);
+int rg_host_unregister(rg_engine* e, const void* p);
 /* One tick for every replica. Input arrays are host pointers (copied before launch; NULL =
  * none). Synchronous with respect to the host buffers, asynchronous on the device. */
 int rg_tick(rg_engine* e, const rg_tick_input* in);

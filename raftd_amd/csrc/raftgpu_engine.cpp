@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <thread>
 #include <unordered_map>
@@ -54,6 +55,31 @@ static const bool g_sync_debug = [] {
   } while (0)
 
 constexpr uint32_t TP_SLOTS = 128, TP_CHUNK = 32;
+
+// rg_propose's per-batch scratch (kept across calls)
+struct PropScratch {
+  std::vector<uint64_t> ch, by, mk, src, c0;  // chunks, payload bytes, non-empty mask, payload offset, arena chunk
+  std::vector<uint32_t> nc0;                  // chunk count of the first Cmd
+  std::vector<uint8_t> fl;                    // 1 uniform chunk count, 2 flat, 4 last Cmd a multiple of 16 B
+  void resize(size_t n) {
+    for (auto* v : {&ch, &by, &mk, &src, &c0}) v->resize(n);
+    nc0.resize(n);
+    fl.resize(n);
+  }
+};
+
+// f(lo, hi) over [0, n) on T threads (the calling one included)
+template <class F>
+static void par_for(uint64_t T, uint64_t n, F&& f) {
+  if (T <= 1 || n < 2) {
+    f((size_t)0, (size_t)n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (uint64_t t = 1; t < T; ++t) th.emplace_back([&, t] { f((size_t)(n * t / T), (size_t)(n * (t + 1) / T)); });
+  f((size_t)0, (size_t)(n / T));
+  for (auto& x : th) x.join();
+}
 
 struct rg_engine {
   rg_config c{};
@@ -103,7 +129,10 @@ struct rg_engine {
   // rg_propose scratch, kept across calls: per input index this call's additions (validation),
   // the indices set, the callers' Cmd offsets, and per staged Cmd its source offset
   std::vector<uint32_t> padd;
-  std::vector<uint64_t> pset, pboff, psrc;
+  std::vector<uint64_t> pset, pboff;
+  PropScratch ps;                 // per batch of a call (rg_propose)
+  std::vector<size_t> ppiece;     // first batch of each staged piece
+  std::vector<std::pair<uintptr_t, uint64_t>> hreg;  // host ranges registered by rg_host_register
   std::vector<uint64_t> touched;  // input indices set in h_* since the last upload
   bool staged = false, stg_reset_pending = false;
   hipEvent_t stg_ev = nullptr;    // the last upload of h_* (host may rewrite them once it completed)
@@ -715,6 +744,10 @@ void rg_destroy(rg_engine* e) {
     (void)hipStreamSynchronize(e->copy);
     (void)hipStreamDestroy(e->copy);
   }
+  if (!e->hreg.empty()) {  // ranges the caller left registered
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    for (const auto& r : e->hreg) (void)hipHostUnregister((void*)r.first);
+  }
   for (int b = 0; b < 2; ++b) {
     if (e->a_gath[b]) (void)hipEventDestroy(e->a_gath[b]);
     if (e->a_copy[b]) (void)hipEventDestroy(e->a_copy[b]);
@@ -906,6 +939,38 @@ static int cmd_reserve(rg_engine* e, uint64_t need_bytes) {
   return RG_OK;
 }
 
+// [p, p + n) inside one range the caller registered through rg_host_register
+static bool host_registered(const rg_engine* e, const void* p, uint64_t n) {
+  const uintptr_t a = (uintptr_t)p;
+  for (const auto& r : e->hreg)
+    if (a >= r.first && a + n <= r.first + r.second) return true;
+  return false;
+}
+
+int rg_host_register(rg_engine* e, const void* p, size_t bytes) {
+  if (!e || !p || !bytes) return fail(RG_EINVAL, "rg_host_register args");
+  for (const auto& r : e->hreg)
+    if ((uintptr_t)p < r.first + r.second && r.first < (uintptr_t)p + bytes)
+      return fail(RG_EINVAL, "rg_host_register: overlaps a registered range");
+  HIPCHK(hipSetDevice(e->c.device));
+  HIPCHK(hipHostRegister(const_cast<void*>(p), bytes, hipHostRegisterDefault));
+  e->hreg.emplace_back((uintptr_t)p, (uint64_t)bytes);
+  return RG_OK;
+}
+
+int rg_host_unregister(rg_engine* e, const void* p) {
+  if (!e || !p) return fail(RG_EINVAL, "rg_host_unregister args");
+  for (size_t i = 0; i < e->hreg.size(); ++i)
+    if (e->hreg[i].first == (uintptr_t)p) {
+      if (int jrc = join(e)) return jrc;
+      HIPCHK(hipStreamSynchronize(e->stream));  // no copy out of it is still in flight
+      HIPCHK(hipHostUnregister(const_cast<void*>(p)));
+      e->hreg.erase(e->hreg.begin() + i);
+      return RG_OK;
+    }
+  return fail(RG_EINVAL, "rg_host_unregister: not a registered range");
+}
+
 int rg_propose(rg_engine* e, const rg_proposal* props, size_t n, const uint8_t* payload, const uint32_t* lens) {
   if (!e || (n && !props)) return fail(RG_EINVAL, "rg_propose args");
   RGCHK(stage_reset(e));
@@ -962,18 +1027,83 @@ int rg_propose(rg_engine* e, const rg_proposal* props, size_t n, const uint8_t* 
     e->cmd_tick[slab] = e->t;
     e->cmd_used[slab] = 0;
   }
-  // layout: each Cmd at its own length rounded up to 16 B, back to back from cmd_used[slab]
-  uint64_t nstage = 0, chunks = 0;
+  // Layout: each Cmd at its own length rounded up to 16 B, back to back from cmd_used[slab], in batch
+  // order. Per batch (host threads for a large call): its chunks, payload bytes, non-empty mask, the
+  // chunk count all its Cmds share (~0u: none), and whether the caller's packing already is the arena's
+  // (every Cmd but the last a multiple of 16 B: "flat"; the last one too: "aligned").
+  PropScratch& ps = e->ps;
+  ps.resize(n);
+  const bool seq = [&] {  // batches name consecutive Cmds from lens[0]: payload offsets follow batch order
+    uint64_t f = 0;
+    for (size_t i = 0; i < n; ++i) {
+      if (props[i].first != f) return false;
+      f += props[i].count;
+    }
+    return true;
+  }();
+  auto batch_scan = [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) {
+      const rg_proposal& b = props[i];
+      const uint32_t* L = lens + b.first;
+      uint64_t ch = 0, by = 0, mk = 0;
+      const uint32_t nc0 = (L[0] + 15) / 16;
+      bool uni = true, flat = true;
+      for (uint32_t x = 0; x < b.count; ++x) {
+        const uint32_t ln = L[x], nc = (ln + 15) / 16;
+        ch += nc;
+        by += ln;
+        mk |= (uint64_t)(ln != 0) << x;
+        uni &= nc == nc0;
+        if (x + 1 < b.count) flat &= (ln & 15u) == 0;
+      }
+      ps.ch[i] = ch;
+      ps.by[i] = by;
+      ps.mk[i] = mk;
+      ps.nc0[i] = nc0;
+      ps.fl[i] = (uint8_t)((uni ? 1 : 0) | (flat ? 2 : 0) | ((L[b.count - 1] & 15u) == 0 ? 4 : 0));
+    }
+  };
+  const uint64_t T = n < 4096 ? 1 : std::min<uint64_t>({16, std::max(1u, std::thread::hardware_concurrency()), n / 2048});
+  par_for(T, n, batch_scan);
+  uint64_t chunks = 0;
   for (size_t i = 0; i < n; ++i) {
-    nstage += props[i].count;
-    for (uint32_t x = 0; x < props[i].count; ++x) chunks += (lens[props[i].first + x] + 15) / 16;
+    ps.c0[i] = chunks;  // relative to a0 (added below)
+    chunks += ps.ch[i];
+  }
+  // payload offset of each batch: by batch order (seq), else through the prefix over lens
+  if (seq) {
+    uint64_t o = 0;
+    for (size_t i = 0; i < n; ++i) {
+      ps.src[i] = o;
+      o += ps.by[i];
+    }
+  } else {
+    std::vector<uint64_t>& boff = e->pboff;
+    boff.assign(nent + 1, 0);
+    for (uint64_t j = 0; j < nent; ++j) boff[j + 1] = boff[j] + lens[j];
+    for (size_t i = 0; i < n; ++i) ps.src[i] = boff[props[i].first];
   }
   const uint64_t a0 = e->cmd_used[slab];
   if (P && (a0 + chunks) >= SYN_OFF) return fail(RG_EFULL, "rg_propose: a slab's Cmd arena holds at most 32 GiB");
   if (P && chunks) RGCHK(cmd_reserve(e, (a0 + chunks) * 16));
-  // pinned staging: [Cmds, chunk-aligned and zero-padded | info_at u64 | chunk u32 | len u32]
-  const uint64_t cb = chunks * 16, need = cb + nstage * 16 + 64;
-  if (P && nstage) {
+  // the Cmd bytes move by DMA straight from the caller's buffer when it is registered
+  // (rg_host_register) and falls into few runs; otherwise through pinned staging, in pieces whose
+  // H2D copies overlap the host threads' copying of the next pieces
+  const uint64_t cb = chunks * 16;
+  uint64_t runs = 0;
+  bool direct = false;
+  if (P && cb && host_registered(e, payload, nbytes)) {
+    direct = true;
+    for (size_t i = 0; i < n && direct; ++i) {
+      if (!(ps.fl[i] & 2)) direct = false;  // padding inside the batch: not the caller's packing
+      if (i == 0 || !(ps.fl[i - 1] & 4) || ps.src[i] != ps.src[i - 1] + ps.by[i - 1]) ++runs;
+    }
+    if (runs > 1024) direct = false;
+  }
+  // pinned staging: [Cmd bytes (staged path) | per batch: info_at u64, first u64, chunk u32, count u32 | lens u32]
+  const uint64_t sb = direct ? 0 : cb, dsc = n * 24, lb = (nent * 4 + 15) & ~15ull;
+  const uint64_t need = sb + dsc + lb + 64;
+  if (P && n) {
     HIPCHK(hipEventSynchronize(e->prop_ev));  // the last H2D out of h_cmd has completed
     if (need > e->h_cmd_cap) {
       if (e->h_cmd) (void)hipHostFree(e->h_cmd);
@@ -982,7 +1112,7 @@ int rg_propose(rg_engine* e, const rg_proposal* props, size_t n, const uint8_t* 
       if (hipHostMalloc((void**)&e->h_cmd, need * 3 / 2, 0) != hipSuccess) return fail(RG_ENOMEM, "hipHostMalloc");
       e->h_cmd_cap = need * 3 / 2;
     }
-    if (need - cb > e->d_cmd_cap) {
+    if (dsc + lb + 64 > e->d_cmd_cap) {
       HIPCHK(hipStreamSynchronize(e->stream));  // the last stage kernel read the old buffer
       if (e->d_cmd) {
         (void)hipFree(e->d_cmd);
@@ -991,95 +1121,125 @@ int rg_propose(rg_engine* e, const rg_proposal* props, size_t n, const uint8_t* 
         e->d_cmd = nullptr;
       }
       e->d_cmd_cap = 0;
-      RGCHK(dalloc(e, &e->d_cmd, (need - cb) * 3 / 2));
-      e->d_cmd_cap = (need - cb) * 3 / 2;
+      RGCHK(dalloc(e, &e->d_cmd, (dsc + lb + 64) * 3 / 2));
+      e->d_cmd_cap = (dsc + lb + 64) * 3 / 2;
     }
   }
-  std::vector<uint64_t>& boff = e->pboff;
-  boff.assign(nent + 1, 0);
-  for (uint64_t j = 0; j < nent; ++j) boff[j + 1] = boff[j] + lens[j];
-  uint64_t* info_at = (uint64_t*)(e->h_cmd + cb);
-  uint32_t* chunk = (uint32_t*)(info_at + nstage);
-  uint32_t* len = chunk + nstage;
-  std::vector<uint64_t>& srcoff = e->psrc;  // per staged Cmd: its offset in the caller's payload
-  if (P) srcoff.resize(nstage);
-  // pass 1 (serial, tables + descriptors): each Cmd's place in the arena and the shard's batch
-  uint64_t k = 0, at_chunk = 0;
+  uint8_t* arena = P ? e->cmds + slab * e->cmd_cap : nullptr;
+  // the host tables (serial over batches: a shard may come in several batches of one call)
+  uint8_t* hd = e->h_cmd + sb;  // batch descriptors, then lens
+  uint64_t* d_info = (uint64_t*)hd;
+  uint64_t* d_first = d_info + n;
+  uint32_t* d_chunk = (uint32_t*)(d_first + n);
+  uint32_t* d_count = d_chunk + n;
   for (size_t i = 0; i < n; ++i) {
     const rg_proposal& b = props[i];
     const uint64_t gi = b.group - g0;
     const uint32_t j = (uint32_t)(b.group / N - e->pl.col_base);
     const uint64_t row = e->wire ? (uint64_t)b.slot * e->c.groups + j : j;
-    for (uint32_t x = 0; x < b.count; ++x) {
-      const uint32_t at = e->h_pc[gi] + x;  // position in the shard's batch
-      const uint32_t ln = lens[b.first + x];
-      if (ln && P) e->h_hm[gi] |= 1ull << at;
-      if (P) {
-        const uint64_t nc = (ln + 15) / 16;
-        uint2& pc = e->h_pcmd[gi];  // the shard's batch: chunks, contiguity, first arena chunk
-        if (at == 0) {
-          pc = make_uint2(1u << 31, (uint32_t)(a0 + at_chunk));
-          e->pnc[gi] = (uint32_t)nc;
-        } else if (nc != e->pnc[gi] || a0 + at_chunk != pc.y + (uint64_t)at * nc) {
-          pc.x &= ~(1u << 31);
-        }
-        pc.x += (uint32_t)nc;
-        srcoff[k] = boff[b.first + x];
-        info_at[k] = (slab * rows + row) * E + at;
-        chunk[k] = (uint32_t)(a0 + at_chunk);
-        len[k] = ln;
-        at_chunk += nc;
-        ++k;
+    const uint32_t at0 = e->h_pc[gi];  // position of the batch's first Cmd in the shard's batch
+    if (P) {
+      e->h_hm[gi] |= ps.mk[i] << at0;
+      const uint32_t c0 = (uint32_t)(a0 + ps.c0[i]);
+      uint2& pc = e->h_pcmd[gi];  // the shard's batch: chunks, contiguity, first arena chunk
+      if (at0 == 0) {
+        pc = make_uint2(1u << 31, c0);
+        e->pnc[gi] = ps.nc0[i];
       }
+      // contiguous while every Cmd has the first one's chunk count and follows the one before
+      if (!(ps.fl[i] & 1) || ps.nc0[i] != e->pnc[gi] || (uint64_t)c0 != pc.y + (uint64_t)at0 * e->pnc[gi])
+        pc.x &= ~(1u << 31);
+      pc.x += (uint32_t)ps.ch[i];
+      d_info[i] = (slab * rows + row) * E + at0;
+      d_first[i] = b.first;
+      d_chunk[i] = c0;
+      d_count[i] = b.count;
     }
-    if (!e->h_pc[gi]) e->touched.push_back(gi);
+    if (!at0) e->touched.push_back(gi);
     e->h_pt[gi] = (uint8_t)b.slot;
     e->h_pc[gi] += b.count;
   }
-  // pass 2 (the bytes): every Cmd into its chunk-aligned place in pinned staging, zero-padded to its
-  // chunk boundary. Runs of Cmds that are back to back in both buffers (lengths multiples of 16 B,
-  // the common case) move with one memcpy; large calls split over host threads (≈ 1 GiB per tick at
-  // 64K shards x 64 Cmds of 256 B: one thread copies it at host-memcpy speed).
-  if (P && k) {
-    auto copy_range = [&](uint64_t lo, uint64_t hi) {
-      uint64_t r = lo;
-      while (r < hi) {
-        uint64_t q = r, bytes = len[r];
-        while (q + 1 < hi && (len[q] & 15u) == 0 && srcoff[q + 1] == srcoff[q] + len[q] &&
-               chunk[q + 1] == chunk[q] + len[q] / 16) {
-          ++q;
-          bytes += len[q];
-        }
-        uint8_t* d = e->h_cmd + (uint64_t)(chunk[r] - a0) * 16;
-        if (bytes) memcpy(d, payload + srcoff[r], bytes);
-        const uint64_t span = (uint64_t)(chunk[q] - chunk[r]) * 16 + ((len[q] + 15) & ~15u);
-        if (span > bytes) memset(d + bytes, 0, span - bytes);
-        r = q + 1;
+  if (P && n) {
+    uint32_t* hl = (uint32_t*)(hd + dsc);
+    memcpy(hl, lens, nent * 4);
+    if (direct) {
+      // DMA straight from the caller's registered buffer, in stream order after the ticks that read
+      // this slab last (the stage kernel after it zeroes the padding of short Cmds)
+      for (size_t i = 0; i < n;) {
+        size_t j = i;
+        uint64_t by = ps.by[i];
+        while (j + 1 < n && (ps.fl[j] & 4) && ps.src[j + 1] == ps.src[j] + ps.by[j]) by += ps.by[++j];
+        if (by)
+          HIPCHK(hipMemcpyAsync(arena + (a0 + ps.c0[i]) * 16, payload + ps.src[i], by, hipMemcpyHostToDevice, e->stream));
+        i = j + 1;
       }
-    };
-    const uint64_t T = std::min<uint64_t>({16, std::max(1u, std::thread::hardware_concurrency()), 1 + cb / (64ull << 20)});
-    if (T <= 1) {
-      copy_range(0, k);
-    } else {
+    } else if (cb) {
+      // staged: pieces of about 64 MiB of the arena range; T threads copy each piece's batches (a
+      // flat batch with one memcpy, any other Cmd by Cmd), and the H2D copy of a piece is issued as
+      // soon as its batches are in, while the threads go on with the next piece
+      std::vector<size_t>& pb = e->ppiece;  // first batch of each piece
+      pb.clear();
+      for (size_t i = 0; i < n; ++i)
+        if (i == 0 || ps.c0[i] * 16 >= (ps.c0[pb.back()] * 16) + (64ull << 20)) pb.push_back(i);
+      pb.push_back(n);
+      const size_t np = pb.size() - 1;
+      auto copy_batch = [&](size_t i) {
+        const rg_proposal& b = props[i];
+        uint8_t* d = e->h_cmd + ps.c0[i] * 16;
+        const uint8_t* src = payload + ps.src[i];
+        if (ps.fl[i] & 2) {
+          if (ps.by[i]) memcpy(d, src, ps.by[i]);
+          return;
+        }
+        for (uint32_t x = 0; x < b.count; ++x) {
+          const uint32_t ln = lens[b.first + x];
+          if (ln) memcpy(d, src, ln);
+          d += (uint64_t)((ln + 15) / 16) * 16;
+          src += ln;
+        }
+      };
+      const uint64_t TT = std::min<uint64_t>({16, std::max(1u, std::thread::hardware_concurrency()), 1 + cb / (16ull << 20)});
+      std::vector<std::atomic<uint32_t>> done(np);
+      for (auto& d : done) d.store(0);
+      auto worker = [&](uint64_t t) {
+        for (size_t pc = 0; pc < np; ++pc) {
+          const size_t lo = pb[pc], hi = pb[pc + 1], cnt = hi - lo;
+          for (size_t i = lo + cnt * t / TT; i < lo + cnt * (t + 1) / TT; ++i) copy_batch(i);
+          done[pc].fetch_add(1, std::memory_order_release);
+        }
+      };
       std::vector<std::thread> th;
-      for (uint64_t t = 0; t < T; ++t) th.emplace_back(copy_range, k * t / T, k * (t + 1) / T);
+      for (uint64_t t = 1; t < TT; ++t) th.emplace_back(worker, t);
+      // the calling thread copies its share of each piece and issues the piece's H2D copy
+      int herr = 0;
+      for (size_t pc = 0; pc < np; ++pc) {
+        const size_t lo = pb[pc], hi = pb[pc + 1], cnt = hi - lo;
+        for (size_t i = lo; i < lo + cnt / TT; ++i) copy_batch(i);
+        done[pc].fetch_add(1, std::memory_order_release);
+        while (done[pc].load(std::memory_order_acquire) < TT) std::this_thread::yield();
+        const uint64_t b0 = ps.c0[lo] * 16, b1 = hi < n ? ps.c0[hi] * 16 : cb;
+        if (!herr && hipMemcpyAsync(arena + a0 * 16 + b0, e->h_cmd + b0, b1 - b0, hipMemcpyHostToDevice, e->stream) != hipSuccess)
+          herr = 1;
+      }
       for (auto& x : th) x.join();
+      if (herr) return fail(RG_EHIP, "rg_propose: H2D copy of the staged Cmds failed");
     }
-  }
-  if (P && k) {
-    // the Cmd bytes straight into the slab's arena (one H2D copy), then their descriptors
-    if (cb) HIPCHK(hipMemcpyAsync(e->cmds + slab * e->cmd_cap + a0 * 16, e->h_cmd, cb, hipMemcpyHostToDevice, e->stream));
-    HIPCHK(hipMemcpyAsync(e->d_cmd, e->h_cmd + cb, k * 16, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipMemcpyAsync(e->d_cmd, hd, dsc + nent * 4, hipMemcpyHostToDevice, e->stream));
     HIPCHK(hipEventRecord(e->prop_ev, e->stream));
     StageParams sp{};
     sp.slab_info = e->slab_info;
     sp.info_at = (const uint64_t*)e->d_cmd;
-    sp.chunk = (const uint32_t*)(e->d_cmd + k * 8);
-    sp.len = (const uint32_t*)(e->d_cmd + k * 12);
-    sp.n = k;
+    sp.first = sp.info_at + n;
+    sp.chunk = (const uint32_t*)(sp.first + n);
+    sp.count = sp.chunk + n;
+    sp.lens = (const uint32_t*)(e->d_cmd + dsc);
+    sp.arena = arena;
+    sp.n = n;
     LAUNCH(launch_stage_cmds(sp, e->stream), e->stream, "stage_cmds");
     e->cmd_used[slab] = a0 + chunks;
     e->slab_synth &= ~(1ull << slab);
+    // "copied before return": the caller may reuse its buffer
+    if (direct) HIPCHK(hipEventSynchronize(e->prop_ev));
   }
   if (n) e->staged = true;
   return RG_OK;

@@ -382,11 +382,14 @@ hipError_t launch_fill_slabs(uint8_t* slabs, uint2* slab_info, uint32_t slab0, u
                              uint32_t E, uint32_t P, uint64_t seed, const Placement& pl, hipStream_t s);
 // caller proposals (rg_propose): the Cmd bytes reach their slab's arena by one H2D copy; this
 // writes their descriptors slab_info[info_at[e]] = {chunk[e], len[e]}
-struct StageParams {
+struct StageParams {  // rg_propose: one row per batch; the kernel expands the batch's Cmds from lens
   uint2* slab_info;
-  const uint64_t* info_at;  // [n] slab_info index
-  const uint32_t* chunk;    // [n] arena chunk of the Cmd
-  const uint32_t* len;      // [n]
+  const uint64_t* info_at;  // [n] slab_info index of the batch's first Cmd
+  const uint64_t* first;    // [n] index of its first Cmd in lens
+  const uint32_t* chunk;    // [n] arena chunk of its first Cmd (within the slab's arena)
+  const uint32_t* count;    // [n] Cmds (1..64)
+  const uint32_t* lens;     // the call's lens[]
+  uint8_t* arena;           // the slab's Cmd arena (padding of short Cmds zeroed here)
   uint64_t n;
 };
 hipError_t launch_stage_cmds(const StageParams& a, hipStream_t s);

@@ -257,15 +257,25 @@ hipError_t launch_fill_slabs(uint8_t* slabs, uint2* slab_info, uint32_t slab0, u
 // ================================================================== caller proposals (rg_propose)
 // The Cmd bytes themselves reach their slab's arena with one H2D copy (the host lays them out
 // chunk-aligned and zero-padded in pinned staging); this scatters their slab_info descriptors.
-__global__ void stage_cmds_kernel(StageParams a) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * blockDim.x)
-    a.slab_info[a.info_at[i]] = make_uint2(a.chunk[i], a.len[i]);
+// a wave per batch: lane x writes Cmd x's {arena chunk, len} descriptor (chunks by a wave scan of the
+// chunk counts) and zeroes the bytes between its end and its last chunk's end (the slot CRC reads them)
+__global__ void __launch_bounds__(256) stage_cmds_kernel(StageParams a) {
+  const uint64_t b = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= a.n) return;
+  const uint32_t x = threadIdx.x & 63u, cnt = a.count[b];
+  const uint32_t len = x < cnt ? a.lens[a.first[b] + x] : 0u, nc = (len + 15u) >> 4;
+  const uint32_t chunk = a.chunk[b] + wave_excl_scan32(nc);
+  if (x >= cnt) return;
+  a.slab_info[a.info_at[b] + x] = make_uint2(chunk, len);
+  if (len & 15u) {
+    uint8_t* t = a.arena + (uint64_t)chunk * 16 + len;
+    for (uint32_t k = len & 15u; k < 16u; ++k) *t++ = 0;
+  }
 }
 
 hipError_t launch_stage_cmds(const StageParams& a, hipStream_t s) {
   if (!a.n) return hipSuccess;
-  const uint64_t blocks = std::min<uint64_t>((a.n + 255) / 256, 4096);
-  hipLaunchKernelGGL(stage_cmds_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(stage_cmds_kernel, dim3((uint32_t)((a.n + 3) / 4)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -195,7 +195,8 @@ EXPORTS = ["rg_create", "rg_destroy", "rg_bootstrap", "rg_fill_slabs", "rg_tick"
            "rg_apply_committed", "rg_probe_copy", "rg_persist_collect", "rg_snapshot_events", "rg_propose",
            "rg_notify_applied", "rg_apply_async", "rg_apply_wait", "rg_read_index", "rg_read_index_results",
            "rg_config_change", "rg_wire_exchange", "rg_rccl_unique_id", "rg_rccl_open", "rg_rccl_close",
-           "rg_pool_stats", "rg_get_update", "rg_commit_update", "rg_tick_device_n", "rg_digest"]
+           "rg_pool_stats", "rg_get_update", "rg_commit_update", "rg_tick_device_n", "rg_digest",
+           "rg_host_register", "rg_host_unregister"]
 
 _lib = None
 
@@ -238,6 +239,8 @@ def load_library(path: str = LIB_PATH):
         "rg_read_entries": ([vp, u32, u64, u32, C.POINTER(EntryView), vp], i32),
         "rg_import_replica": ([vp, u32, C.POINTER(ReplicaView), vp, vp, vp, vp], i32),
         "rg_propose": ([vp, C.POINTER(Proposal), C.c_size_t, vp, vp], i32),
+        "rg_host_register": ([vp, vp, C.c_size_t], i32),
+        "rg_host_unregister": ([vp, vp], i32),
         "rg_notify_applied": ([vp, vp, vp, C.c_size_t], i32),
         "rg_apply_async": ([vp, u32, i32], i32),
         "rg_read_index": ([vp, C.POINTER(ReadRequest), C.c_size_t], i32),
@@ -354,6 +357,13 @@ class Engine:
         props, lens, blob = pack_proposals(batches)
         self._check(self.L.rg_propose(self.h, props, len(batches), blob.ctypes.data if blob.size else None,
                                       lens.ctypes.data if lens.size else None))
+
+    def host_register(self, ptr: int, nbytes: int):
+        """rg_host_register: page-lock a long-lived host buffer Cmds are staged in (DMA straight from it)."""
+        self._check(self.L.rg_host_register(self.h, ptr, nbytes))
+
+    def host_unregister(self, ptr: int):
+        self._check(self.L.rg_host_unregister(self.h, ptr))
 
     def tick_device(self, prop_target_ptr=0, prop_count_ptr=0, campaign_ptr=0, isolate_ptr=0, flags=0):
         ti = TickInput(prop_target_ptr or None, prop_count_ptr or None, campaign_ptr or None,

@@ -16,7 +16,8 @@ for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
 for r in rows:
     k = r["Kernel_Name"]
-    k = "control" if "control_kernel" in k else "bulk" if "bulk_kernel" in k else None
+    k = ("control_fast" if "control_fast_kernel" in k else "control_slow" if "control_slow_kernel" in k
+         else "control" if "control_kernel" in k else "bulk" if "bulk_kernel" in k else None)
     if k:
         acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in acc.items():

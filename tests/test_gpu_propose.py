@@ -243,3 +243,101 @@ def test_caller_then_synthetic():
             ora.tick()
         compare(gpu, ora, t)
     check_cmds(gpu, ora)
+
+
+def _registered(gpu, cap):
+    """gpu.propose through a buffer registered once (rg_host_register): rg_propose moves a call's Cmds
+    by DMA straight from it when the packing allows, else through pinned staging."""
+    from raftd_amd.engine import pack_proposals
+    buf = np.zeros(cap, np.uint8)
+    gpu.host_register(buf.ctypes.data, cap)
+
+    def propose(batches):
+        props, lens, blob = pack_proposals(batches)
+        assert blob.size <= cap
+        buf[:blob.size] = blob
+        gpu._check(gpu.L.rg_propose(gpu.h, props, len(batches), buf.ctypes.data if blob.size else None,
+                                    lens.ctypes.data if lens.size else None))
+    return propose, buf
+
+
+@pytest.mark.parametrize("R,P", [(3, 64), (3, 256), (5, 16)])
+def test_caller_cmds_registered_buffer(R, P):
+    """Cmds staged from a registered host buffer: ticks whose Cmds are all multiples of 16 B go by DMA
+    straight from it (one run per call), the others (odd lengths inside a batch) through staging;
+    either way every replica, entry (bytes, CRC) and applied batch equals the oracle's."""
+    cfg = dict(CHAOS, groups=4, replicas=R, payload_bytes=P, max_entries_per_msg=8, seed=70 + R,
+               max_cmd_bytes=4 * P)
+    holder = {}
+
+    def make_gpu():
+        g = make("gpu", **cfg)
+        holder["p"], holder["buf"] = _registered(g, 1 << 20)
+        g.propose = holder["p"]
+        return g
+
+    def batches_fn(rng, G, R_, P_):
+        aligned = rng.random() < 0.6
+        out = []
+        for g in range(G):
+            if rng.random() < 0.3:
+                continue
+            n = int(rng.integers(1, 9))
+            if aligned:
+                cmds = [rng.integers(0, 256, 16 * int(rng.integers(0, 3 * P_ // 16 + 2)), dtype=np.uint8).tobytes()
+                        for _ in range(n)]
+            else:
+                cmds = [rng.integers(0, 256, int(rng.integers(0, 2 * P_ + 3)), dtype=np.uint8).tobytes()
+                        for _ in range(n)]
+            out.append((g, int(rng.integers(0, R_)), cmds))
+        return out
+
+    gpu, _, lens = run_caller(cfg, ticks=60, seed=R * 31 + P, make_gpu=make_gpu, batches_fn=batches_fn)
+    assert any(x % 16 for x in lens) and any(x and x % 16 == 0 for x in lens), lens
+    gpu.host_unregister(holder["buf"].ctypes.data)
+
+
+def test_large_call_staged_in_pieces_and_registered():
+    """A call of 8,192 shards x 64 Cmds of 272 B (about 143 MB: three staged pieces, threaded batch
+    scan) and the same from a registered buffer with some 7-B Cmds mixed in: the whole table equals the
+    oracle's (rg_digest)."""
+    from raftd_amd.engine import Proposal
+    G, R, E, P = 8192, 3, 64, 256
+    cfg = dict(groups=G, replicas=R, log_capacity=256, payload_bytes=P, max_entries_per_msg=E, snapshot_entries=0,
+               max_cmd_bytes=512, seed=0x1A6E)
+    gpu, ora = make("gpu", **cfg), make("c", **cfg)
+    for e in (gpu, ora):
+        e.bootstrap()
+    camp = np.zeros(G * R, np.uint8)
+    camp[0::R] = 1
+    for e in (gpu, ora):
+        e.tick()
+        e.tick(campaign=camp)
+        e.tick()
+    rng = np.random.default_rng(5)
+    buf = np.zeros(G * E * 272, np.uint8)
+    gpu.host_register(buf.ctypes.data, buf.nbytes)
+    try:
+        for t in range(4):
+            lens = np.full(G * E, 272, np.uint32)
+            if t >= 2:  # odd lengths: staging; and the last Cmd of some batches odd: direct with more runs
+                lens[rng.integers(0, G * E, 50)] = 7
+                lens[np.arange(G) * E + E - 1] = 9 if t == 3 else 272
+            blob = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+            props = (Proposal * G)()
+            a = np.frombuffer(props, dtype=np.dtype([("group", "<u8"), ("slot", "<u4"), ("count", "<u4"),
+                                                     ("first", "<u8")]))
+            a["group"], a["slot"], a["count"] = np.arange(G), 0, E
+            a["first"] = np.arange(G, dtype=np.uint64) * E
+            src = buf if t % 2 else blob
+            if t % 2:
+                buf[:blob.size] = blob
+            gpu._check(gpu.L.rg_propose(gpu.h, props, G, src.ctypes.data, lens.ctypes.data))
+            cmds = np.split(blob, np.cumsum(lens)[:-1].astype(np.int64))
+            batches = [(g, 0, [c.tobytes() for c in cmds[g * E:(g + 1) * E]]) for g in range(G)]
+            assert ora.propose(batches) == 0
+            gpu.tick()
+            ora.tick()
+            assert gpu.digest() == ora.digest(), t
+    finally:
+        gpu.host_unregister(buf.ctypes.data)
