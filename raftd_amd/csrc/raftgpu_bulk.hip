@@ -95,6 +95,25 @@ __device__ __forceinline__ Job load_job(const BulkParams& p, uint32_t q, uint32_
   return jb;
 }
 
+// bulk_small_kernel's replicas (C5's load: one or two entries per replica per tick): exactly one job,
+// uniform, 1..SMALL_N entries of at most P bytes each, from the sender's stream, a slab or a Cmd arena,
+// and well-formed (set_job's checks for those kinds; anything else stays with bulk_kernel, which
+// flags a malformed job)
+constexpr uint32_t SMALL_N = 4;
+__device__ __forceinline__ bool small_job(const BulkParams& p, uint32_t nj, const Job& jb, uint32_t q, uint32_t nch,
+                                          bool wire) {
+  if (nj != 1) return false;
+  const uint32_t n = jb.meta & 0xFF, e0 = (jb.meta >> 8) & 0xFF, kind = (jb.meta >> 16) & 0xF;
+  const uint32_t ncu = (jb.meta >> 21) & 0x7F;
+  if (!((jb.meta >> 20) & 1u) || e0 >= n || n - e0 > SMALL_N || ncu > nch) return false;
+  if (kind == SRC_RING) return jb.src < p.nrep;
+  if (kind != SRC_SLAB && kind != SRC_CMD) return false;
+  const uint64_t row = wire ? (uint64_t)(jb.src >> 16) * p.G + q % p.G : q % p.G;
+  if ((jb.src & 0xFFFFu) >= p.nslab || row >= (wire ? p.nrep : p.G)) return false;
+  if (kind == SRC_SLAB) return ncu == nch;
+  return (jb.spos + (uint64_t)(n - e0) * ncu) * 16 <= p.cmd_cap;
+}
+
 // ---- software-pipelined payload stream.
 // A wave walks a flat sequence of steps over the jobs of its tiles; one step = epi entries of one
 // uniform job, 16 B per lane. BULK_U steps are in flight at once in a register ring: slot u is
@@ -168,7 +187,11 @@ __device__ __forceinline__ void load_tile(const BulkParams& p, Cursor& cur, Tile
 #else
   (void)pt;
 #endif
-  cur.m = __ballot(tj.nj != 0);
+  bool mine = tj.nj != 0;
+  if constexpr (MJ) {  // the replicas bulk_small_kernel took are done
+    if (p.small && mine && small_job(p, tj.nj, tj.j0, q, p.P >> 4, p.wire_mode != 0)) mine = false;
+  }
+  cur.m = __ballot(mine);
   cur.j = 0;
   cur.njl = 0;
 }
@@ -670,6 +693,114 @@ __global__ void __launch_bounds__(256) RG_BULK_ATTR bulk_kernel(BulkParams p, co
   }
 }
 
+// ---- bulk_small_kernel (MJ engines, before bulk_kernel): the small_job replicas, one entry per
+// lane group. bulk_kernel's cursor is wave-uniform, so a one-entry job fills NCH of its 64 lanes per
+// step (C5: 16 of 64 at P 256) and each job's page ids cost a scalar round trip before its payload
+// load can issue. Here a wave takes a tile of 64 replicas, lists the entries of its small jobs (LDS),
+// and moves EPI entries per step, each lane group with its own replica, page ids and addresses
+// (vector loads), SMALL_U steps in flight.
+#ifndef RG_SMALL_U
+#define RG_SMALL_U 4
+#endif
+constexpr int SMALL_U = RG_SMALL_U;
+
+template <int LG, bool WIRE>
+__global__ void __launch_bounds__(256) bulk_small_kernel(BulkParams p, const uint32_t* __restrict__ pt) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  constexpr uint32_t NCH = 1u << LG, EPI = 64u >> LG, P = 16u << LG;
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  if (p.poolctl->param_err) return;  // stale job tables (a skipped control tick): run nothing
+  const uint32_t shw = CRC_T_WORDS + CRC_N_WORDS + NCH * CRC_SH_STRIDE;
+  for (uint32_t i = threadIdx.x; i < shw; i += blockDim.x) lds[i] = p.crc_tab[i];
+  __syncthreads();
+  const uint32_t lane = lane_id(), c = lane & (NCH - 1), ei = lane >> LG, w = threadIdx.x >> 6;
+  const Crc crc{lds, lds + CRC_T_WORDS, lds + CRC_T_WORDS + CRC_N_WORDS + c * CRC_SH_STRIDE, nullptr};
+  uint8_t* own = reinterpret_cast<uint8_t*>(lds + shw) + w * 64 * SMALL_N;  // this wave's entry list
+  const uint64_t n64 = p.nrep, L = p.L, rows = WIRE ? p.nrep : p.G, PTSM = p.PTS - 1;
+  const uint32_t cols = (p.G + 63) / 64, ntiles = cols * p.R, stride = gridDim.x * (blockDim.x >> 6);
+  for (uint32_t t = rfl(blockIdx.x * (blockDim.x >> 6) + w); t < ntiles; t += stride) {
+    const uint32_t b = t / p.R, s = t - b * p.R, g = b * 64 + lane;
+    const bool valid = g < p.G;
+    const uint32_t q = s * p.G + g;
+    const uint32_t nj = valid ? p.jcnt[q] : 0u;
+    Job jb{};
+    if (nj == 1) jb = load_job(p, q, 0);
+    const bool small = valid && small_job(p, nj, jb, q, NCH, WIRE);
+    const uint32_t e0 = (jb.meta >> 8) & 0xFF, k = small ? (jb.meta & 0xFF) - e0 : 0u;
+    const uint32_t off = wave_excl_scan32(k);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)(off + k), 63);
+    for (uint32_t i = 0; i < k; ++i) own[off + i] = (uint8_t)lane;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (uint32_t base = 0; base < total; base += EPI * SMALL_U) {
+      u32x4 x[SMALL_U];
+      uint32_t want[SMALL_U], dch[SMALL_U], it_q[SMALL_U], it_e[SMALL_U], it_dp[SMALL_U];
+      uint64_t it_first[SMALL_U], it_dm[SMALL_U];
+      bool act[SMALL_U], lead[SMALL_U], chk[SMALL_U];
+#pragma unroll
+      for (int u = 0; u < SMALL_U; ++u) {  // issue: the entry's page ids, then its payload and sender CRC
+        const uint32_t it = base + u * EPI + ei;
+        const bool live = it < total;
+        const uint32_t l = live ? own[it] : 0u;
+        const uint32_t i = it - (uint32_t)__shfl((int)off, (int)l, 64);
+        const uint32_t meta = (uint32_t)__shfl((int)jb.meta, (int)l, 64), src = (uint32_t)__shfl((int)jb.src, (int)l, 64);
+        const uint32_t dpos = (uint32_t)__shfl((int)jb.dpos, (int)l, 64);
+        const uint64_t first = ((uint64_t)(uint32_t)__shfl((int)(jb.first >> 32), (int)l, 64) << 32) |
+                               (uint32_t)__shfl((int)(uint32_t)jb.first, (int)l, 64);
+        const uint64_t spos = ((uint64_t)(uint32_t)__shfl((int)(jb.spos >> 32), (int)l, 64) << 32) |
+                              (uint32_t)__shfl((int)(uint32_t)jb.spos, (int)l, 64);
+        const uint64_t sm = ((uint64_t)(uint32_t)__shfl((int)(jb.sm >> 32), (int)l, 64) << 32) |
+                            (uint32_t)__shfl((int)(uint32_t)jb.sm, (int)l, 64);
+        const uint64_t dm = ((uint64_t)(uint32_t)__shfl((int)(jb.dm >> 32), (int)l, 64) << 32) |
+                            (uint32_t)__shfl((int)(uint32_t)jb.dm, (int)l, 64);
+        const uint32_t ie0 = (meta >> 8) & 0xFF, kind = (meta >> 16) & 0xF, ncu = (meta >> 21) & 0x7F;
+        const uint32_t e = ie0 + i, iq = s * p.G + b * 64 + l;
+        const bool a = live && c < ncu;
+        const bool ring = kind == SRC_RING;
+        // destination: chunk dpos + i·ncu + c of this replica's stream
+        const uint32_t dl = dpos + i * ncu + c;
+        const uint32_t pid = a ? pt[(uint64_t)iq * p.PTS + (vpn_of(dl) & PTSM)] : 0u;
+        dch[u] = pid * PAGE_CH + (dl & (PAGE_CH - 1));
+        const uint8_t* sp;
+        if (ring) {
+          const uint32_t sl = (uint32_t)spos + e * ncu + c;
+          const uint32_t sid = a ? pt[(uint64_t)src * p.PTS + (vpn_of(sl) & PTSM)] : 0u;
+          sp = p.pool + (uint64_t)sid * PAGE_BYTES + ((sl & (PAGE_CH - 1)) << 4);
+        } else {
+          const uint32_t sl16 = src & 0xFFFFu;
+          const uint64_t row = WIRE ? (uint64_t)(src >> 16) * p.G + (b * 64 + l) : (uint64_t)(b * 64 + l);
+          sp = kind == SRC_CMD ? p.cmds + (uint64_t)sl16 * p.cmd_cap + 16ull * ((uint32_t)spos + i * ncu + c)
+                               : p.slabs + (((uint64_t)sl16 * rows + row) * p.E + e) * P + c * 16;
+        }
+        const uint64_t slot = (first + e) & (L - 1);
+        const uint32_t* wp = (ring && a) ? &p.info[(((sm >> e) & 1ull) * n64 + src) * L + slot].x : nullptr;
+        x[u] = a ? *reinterpret_cast<const u32x4*>(sp) : u32x4{0, 0, 0, 0};
+        want[u] = wp ? *wp : 0u;
+        act[u] = a;
+        lead[u] = live && c == 0;
+        chk[u] = ring;
+        it_q[u] = iq;
+        it_e[u] = e;
+        it_dp[u] = dpos + i * ncu;
+        it_first[u] = first;
+        it_dm[u] = dm;
+        (void)rows;
+      }
+#pragma unroll
+      for (int u = 0; u < SMALL_U; ++u) {  // consume: store, CRC, info word, sender-CRC check
+        if (act[u]) __builtin_nontemporal_store(x[u], reinterpret_cast<u32x4*>(p.pool + (uint64_t)dch[u] * 16));
+        uint32_t v = crc.raw16(make_uint4(x[u].x, x[u].y, x[u].z, x[u].w));
+        if constexpr (LG > 0) v = xor_lanes<LG>(crc.shift(v));
+        if (lead[u]) put_info(p, it_q[u], it_first[u], it_dm[u], it_e[u], act[u] ? (p.crc_const ^ v) : 0u, it_dp[u],
+                              chk[u] && act[u], want[u]);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the list is rewritten for the next tile
+  }
+  (void)n64;
+}
+
 static int lg_of(uint32_t P) {
   int lg = 0;
   while ((16u << lg) < P) ++lg;
@@ -697,6 +828,23 @@ static hipError_t with_bulk_w(uint32_t P, F f) {
 template <>
 hipError_t launch_bulk_t<(bool)RG_BULK_W, (bool)RG_BULK_MJ>(const BulkParams& p, const uint32_t* pt, hipStream_t s,
                                                           int grid) {
+#if RG_BULK_MJ
+  if (p.small) {  // the small jobs first, then bulk_kernel for the rest (it skips them)
+    const uint32_t lg = (uint32_t)lg_of(p.P), nch = 1u << lg;
+    const uint32_t tiles = ((p.G + 63) / 64) * p.R;
+    const int sg = (int)std::min<uint32_t>((tiles + 3) / 4, (uint32_t)grid * 2u);
+    const int lds = (int)((CRC_T_WORDS + CRC_N_WORDS + nch * CRC_SH_STRIDE) * 4 + 4 * 64 * SMALL_N);
+    hipError_t r = hipErrorInvalidValue;
+    switch (lg) {
+#define RG_SMALL_CASE(X) \
+  case X: hipLaunchKernelGGL((bulk_small_kernel<X, (bool)RG_BULK_W>), dim3(sg), dim3(256), lds, s, p, pt); r = hipGetLastError(); break;
+      RG_SMALL_CASE(0) RG_SMALL_CASE(1) RG_SMALL_CASE(2) RG_SMALL_CASE(3) RG_SMALL_CASE(4) RG_SMALL_CASE(5) RG_SMALL_CASE(6)
+#undef RG_SMALL_CASE
+      default: break;
+    }
+    if (r != hipSuccess) return r;
+  }
+#endif
   return with_bulk_w<(bool)RG_BULK_W, (bool)RG_BULK_MJ>(p.P, [&](auto k) {
     hipLaunchKernelGGL(k, dim3(grid), dim3(256), bulk_lds_bytes(p.P), s, p, pt);
     return hipGetLastError();

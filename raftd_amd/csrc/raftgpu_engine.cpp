@@ -185,6 +185,7 @@ struct rg_engine {
   // batches carry at most 16 entries (max_entries_per_msg), jobs are small; the 64-entry jobs of
   // full batches run faster without it. RAFTGPU_BULK_MULTIJOB=0/1 overrides (A/B).
   bool bulk_mj = false;
+  bool bulk_small = true;  // MJ engines: bulk_small_kernel takes the small jobs first (RAFTGPU_BULK_SMALL=0: off)
   uint64_t bytes = 0;
   std::vector<void*> allocs;
   // per-launch event timing (rg_timing): bit 0 control_kernel, bit 1 bulk_kernel; a start/end
@@ -425,6 +426,7 @@ static BulkParams bulk_params_at(rg_engine* e, uint64_t tk) {
   b.wire_bytes = e->recv_bytes;
   b.nslab = e->c.num_slabs;
   b.multijob = e->bulk_mj ? 1u : 0u;
+  b.small = e->bulk_mj && e->bulk_small ? 1u : 0u;
   return b;
 }
 
@@ -691,6 +693,7 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   e->bulk_mj = c.max_entries_per_msg <= 16;
   if (const char* v = getenv("RAFTGPU_CTL_FAST")) e->ctl_fast = v[0] != '0';
   if (const char* v = getenv("RAFTGPU_BULK_MULTIJOB")) e->bulk_mj = v[0] == '1';
+  if (const char* v = getenv("RAFTGPU_BULK_SMALL")) e->bulk_small = v[0] != '0';
   if (const char* v = getenv("RAFTGPU_APPLY_SDMA"))
     if (v[0] == '1') {
       std::string why;

@@ -285,6 +285,7 @@ struct BulkParams {
   uint64_t wire_bytes;   // bytes of `wire` in use (job bounds checks)
   uint32_t nslab;
   uint32_t multijob;     // small jobs share a ring pass (bulk_kernel<.., MJ>; the engine's choice)
+  uint32_t small;        // bulk_small_kernel ran first: bulk_kernel skips the replicas it took (small_job)
 };
 
 // pool_kernel (after control, before bulk): frees the stream pages control released, allocates the
