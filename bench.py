@@ -98,13 +98,13 @@ class SelfWire:
         self.wire_bytes = 0
 
     def exchange(self):
-        sizes = self.eng.wire_plan()
+        sizes, rsizes = self.eng.wire_plan_fixed()  # fixed capacity: no host sync
         n = sum(sizes)
         if self.buf is None or self.buf.numel() < n:
             self.eng.sync()
             self.buf = self.torch.empty(max(n, 1 << 20) * 3 // 2, dtype=self.torch.uint8, device="cuda")
         self.eng.wire_pack(self.buf.data_ptr(), self.buf.numel())
-        self.eng.wire_recv(self.buf.data_ptr(), sizes)
+        self.eng.wire_recv(self.buf.data_ptr(), rsizes)
         self.wire_bytes = n
 
     def tick(self, *a, **kw):

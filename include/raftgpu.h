@@ -360,13 +360,28 @@ int rg_last_tick_traffic(rg_engine* e, rg_traffic* out);
  *                                      device buffer buf, are unpacked for the next tick (async);
  *                                      buf must stay valid until that tick has completed on the
  *                                      device (followers read payloads straight out of it).
- * rg_tick fails with RG_EINVAL if a tick after the first runs without rg_wire_recv. */
+ * rg_tick fails with RG_EINVAL if a tick after the first runs without rg_wire_recv.
+ * Two ways to size the regions:
+ *   rg_wire_plan        exact: waits for the plan kernel and returns the bytes each region needs;
+ *                       the transport then has to tell each rank what it receives (a size exchange).
+ *   rg_wire_plan_fixed  fixed capacity, no wait: send_bytes / recv_bytes are capacities both ends of
+ *                       every link already agree on (a rule over numbers both see), so
+ *                       one all-to-all per tick moves the regions. A unit (one replica pair's
+ *                       messages) that does not fit its region is dropped whole — the messages are
+ *                       lost in transit, which Raft tolerates — and counted (rg_wire_dropped); the
+ *                       capacities double past any need above half of them, two exchanges later.
+ *                       They start at the most a region's units could need (K messages of E entries
+ *                       of max_cmd_bytes each), capped at 64 MiB (RAFTGPU_WIRE_CAP0), so a cluster
+ *                       whose worst case fits never drops. */
 int rg_wire_plan(rg_engine* e, uint64_t* send_bytes /*[ranks]*/);
+int rg_wire_plan_fixed(rg_engine* e, uint64_t* send_bytes /*[ranks]*/, uint64_t* recv_bytes /*[ranks]*/);
 int rg_wire_pack(rg_engine* e, void* send_buf, uint64_t send_cap);
 int rg_wire_recv(rg_engine* e, const void* recv_buf, const uint64_t* recv_bytes /*[ranks]*/);
-/* The whole exchange in one call: rg_wire_plan, the region sizes through t->allgather_u64, pack
- * into an engine-owned send buffer, t->alltoallv into an engine-owned receive buffer, and
- * rg_wire_recv. Every rank of the cluster calls it between the same two ticks. A host in any
+/* Messages dropped so far because their unit did not fit a fixed-capacity region. */
+int rg_wire_dropped(rg_engine* e, uint64_t* msgs);
+/* The whole exchange in one call and one collective: rg_wire_plan_fixed, pack into an engine-owned
+ * send buffer, t->alltoallv into an engine-owned receive buffer, and rg_wire_recv — no host sync and
+ * no size exchange. Every rank of the cluster calls it between the same two ticks. A host in any
  * language gets multi-GPU replication from this call plus a transport: the built-in RCCL one
  * (rg_rccl_open) or its own.
  * *sent_bytes (if not NULL) = the bytes this rank sent to other ranks. The transport's callbacks return 0 on success. alltoallv gets device buffers and the engine's
@@ -375,8 +390,9 @@ int rg_wire_recv(rg_engine* e, const void* recv_buf, const uint64_t* recv_bytes 
  * enqueue on `stream` itself, order a stream of its own by events both ways (the RCCL transport),
  * or synchronise `stream` and complete before returning (a host-staged transport). Region r of `send`
  * (send + soff[r], ssize[r] bytes) goes to rank r; region r of `recv`
- * (recv + roff[r], rsize[r] bytes) comes from rank r. allgather_u64 is a host-memory, blocking
- * all-gather of n values per rank: all[r * n + i] = value i of rank r. */
+ * (recv + roff[r], rsize[r] bytes) comes from rank r. allgather_u64 (optional; rg_wire_exchange no
+ * longer calls it) is a host-memory, blocking all-gather of n values per rank: all[r * n + i] = value
+ * i of rank r. */
 typedef struct rg_transport {
   void* user;
   int (*allgather_u64)(void* user, const uint64_t* mine, uint64_t* all, uint32_t n);

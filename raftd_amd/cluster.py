@@ -210,8 +210,8 @@ class _Half:
     them and unpacks before the engine's next tick. With a C transport (exchange="c") start() is
     one rg_wire_exchange call, ordered on the device, and finish() has nothing left to do."""
 
-    def __init__(self, eng, dev, pg, rank, xt=None):
-        self.eng, self.pg, self.rank, self.xt = eng, pg, rank, xt
+    def __init__(self, eng, dev, pg, rank, xt=None, fixed=True):
+        self.eng, self.pg, self.rank, self.xt, self.fixed = eng, pg, rank, xt, fixed
         self.send, self.recv = _Buf(dev), _Buf(dev)
         self.work, self.rsizes, self.sent = None, None, 0
 
@@ -220,15 +220,21 @@ class _Half:
         if self.xt is not None:
             self.sent = e.wire_exchange(self.xt)
             return
-        sizes = e.wire_plan()  # host sync: the tick that produced the messages has completed
+        if self.fixed:
+            # one collective, no host sync: capacities both ends of every link agree on (rg_wire_plan_fixed)
+            sizes, rsizes = e.wire_plan_fixed()
+            biggest = max(sizes + rsizes)  # <= 1 GiB by construction: one all-to-all call on every rank
+        else:
+            sizes = e.wire_plan()  # host sync: the tick that produced the messages has completed
         _, stot = _offsets(sizes)
         self.send.ensure(stot)
         e.wire_pack(self.send.ptr(), self.send.cap())
-        rsizes, biggest = exchange_sizes(sizes, self.pg)
+        if not self.fixed:
+            rsizes, biggest = exchange_sizes(sizes, self.pg)
         _, rtot = _offsets(rsizes)
-        self.recv.ensure(rtot)  # its previous contents were consumed by the tick wire_plan waited for
+        self.recv.ensure(rtot)  # stream order: the tick that reads the old buffer runs before a reuse
         self.work = all_to_all_bytes(self.send.t, sizes, self.recv.t, rsizes, self.pg, async_op=async_op,
-                                     nchunks=a2a_chunks(biggest))
+                                     nchunks=1 if self.fixed else a2a_chunks(biggest))
         self.rsizes, self.sent = rsizes, stot - sizes[self.rank]
 
     def finish(self):

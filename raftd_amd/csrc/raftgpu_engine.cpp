@@ -211,6 +211,15 @@ struct rg_engine {
   uint32_t* rcnt = nullptr;
   std::vector<uint64_t> send_bytes;
   bool planned = false, wire_ready = false;
+  // fixed-capacity exchange (rg_wire_plan_fixed): region bytes per peer, the same at
+  // both ends of a link (the same rule over the same numbers), grown from the exchange two before
+  std::vector<uint64_t> cap_s, cap_r;
+  uint64_t* d_need = nullptr;  // [2][MAX_RANKS]: bytes each sent region asked for (pack), each received one (unpack)
+  uint64_t* h_need = nullptr;  // pinned [4][2][MAX_RANKS], one slot per exchange
+  hipEvent_t need_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  uint64_t nfix = 0;           // fixed-capacity exchanges so far
+  bool fixed = false;          // the planned exchange is fixed-capacity
+  unsigned long long* d_drops = nullptr;  // messages dropped by a full region (cumulative)
   const uint8_t* recv = nullptr;  // receive buffer the next tick's SRC_WIRE jobs read
   uint64_t recv_bytes = 0;         // bytes of it in use (RG_BOUNDS checks)
   // rg_wire_exchange's own buffers (grown on demand; stream order keeps one of each enough: the
@@ -407,6 +416,7 @@ static WireParams wire_params(rg_engine* e) {
   w.usize = e->usize; w.uoff = e->uoff; w.bsum = e->bsum;
   w.rmap = e->rmap; w.rbeg = e->rbeg; w.RU = e->RU;
   w.rhdr = e->rhdr; w.rmt = e->rmt; w.rcnt = e->rcnt;
+  w.sneed = e->d_need; w.rneed = e->d_need ? e->d_need + MAX_RANKS : nullptr; w.drops = e->d_drops;
   return w;
 }
 
@@ -624,6 +634,15 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
     if (rc == RG_OK) rc = dalloc(e, &e->rcnt, R * R * G * 4);
     if (rc == RG_OK && hipHostMalloc((void**)&e->h_bounds, (MAX_RANKS + 1) * 8, 0) != hipSuccess)
       rc = fail(RG_ENOMEM, "hipHostMalloc");
+    if (rc == RG_OK) rc = dalloc(e, &e->d_need, 2 * MAX_RANKS * 8);
+    if (rc == RG_OK) rc = dalloc(e, &e->d_drops, 8);
+    if (rc == RG_OK && hipHostMalloc((void**)&e->h_need, 4 * 2 * MAX_RANKS * 8, 0) != hipSuccess)
+      rc = fail(RG_ENOMEM, "hipHostMalloc");
+    for (int i = 0; i < 4 && rc == RG_OK; ++i)
+      if (hipEventCreateWithFlags(&e->need_ev[i], hipEventDisableTiming) != hipSuccess) rc = fail(RG_EHIP, "event");
+    if (rc == RG_OK && (hipMemset(e->d_need, 0, 2 * MAX_RANKS * 8) != hipSuccess ||
+                        hipMemset(e->d_drops, 0, 8) != hipSuccess))
+      rc = fail(RG_EHIP, "hipMemset");
     if (rc == RG_OK &&
         (hipMemcpy(e->umap, um.data(), um.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
          hipMemcpy(e->rmap, rm.data(), rm.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
@@ -767,6 +786,9 @@ void rg_destroy(rg_engine* e) {
   if (e->h_tp) (void)hipHostFree(e->h_tp);
   for (void* p : e->allocs) (void)hipFree(p);
   if (e->h_bounds) (void)hipHostFree(e->h_bounds);
+  if (e->h_need) (void)hipHostFree(e->h_need);
+  for (hipEvent_t ev : e->need_ev)
+    if (ev) (void)hipEventDestroy(ev);
   for (void* h : {(void*)e->h_pt, (void*)e->h_pc, (void*)e->h_hm, (void*)e->h_cmd, (void*)e->h_pcmd})
     if (h) (void)hipHostFree(h);
   delete e;
@@ -2318,10 +2340,80 @@ int rg_wire_plan(rg_engine* e, uint64_t* send_bytes) {
   HIPCHK(hipStreamSynchronize(e->stream));
   for (uint32_t r = 0; r < N; ++r) {
     const uint64_t units = e->h_ubeg[r + 1] - e->h_ubeg[r], data = (e->h_bounds[r + 1] - e->h_bounds[r]) * 16;
-    e->send_bytes[r] = units ? wire_table_bytes(units) + ((data + 255) & ~255ull) : 0;
+    e->send_bytes[r] = units ? wire_region_min(units) + ((data + 255) & ~255ull) : 0;
     send_bytes[r] = e->send_bytes[r];
   }
   e->planned = true;
+  e->fixed = false;
+  return RG_OK;
+}
+
+// Fixed-capacity regions. A link's region starts at the bytes its units could need
+// (K messages of E entries of max_cmd_bytes each, plus header and table), at most RAFTGPU_WIRE_CAP0
+// (64 MiB) and never more than WIRE_CAP_MAX (one all-to-all call moves it); it doubles past any need
+// above half of it. Both ends apply that rule to the same numbers — the sender to its plan, the
+// receiver to the region header it got — two exchanges late, so neither waits for the other.
+static constexpr uint64_t WIRE_CAP_MAX = 1ull << 30;
+static void wire_caps_init(rg_engine* e) {
+  const uint32_t N = e->pl.N;
+  uint64_t cap0 = 64ull << 20;
+  if (const char* v = getenv("RAFTGPU_WIRE_CAP0")) cap0 = std::max<uint64_t>(strtoull(v, nullptr, 10), 4096);
+  const uint64_t msg = 64 + (uint64_t)e->c.max_entries_per_msg * (16 + (((uint64_t)e->maxc + 15) & ~15ull));
+  auto first = [&](uint64_t units) -> uint64_t {
+    if (!units) return 0;
+    const long double worst = (long double)wire_region_min(units) + (long double)units * e->c.max_msgs_per_pair * msg;
+    const uint64_t c = worst > (long double)cap0 ? cap0 : (uint64_t)worst;
+    return std::min<uint64_t>(WIRE_CAP_MAX, (std::max<uint64_t>(c, wire_region_min(units)) + 255) & ~255ull);
+  };
+  e->cap_s.assign(N, 0);
+  e->cap_r.assign(N, 0);
+  for (uint32_t r = 0; r < N; ++r) {
+    e->cap_s[r] = first(e->h_ubeg[r + 1] - e->h_ubeg[r]);
+    e->cap_r[r] = first(e->h_rbeg[r + 1] - e->h_rbeg[r]);
+  }
+}
+static void wire_cap_grow(uint64_t& cap, uint64_t need) {
+  if (cap && need > cap / 2) cap = std::min<uint64_t>(WIRE_CAP_MAX, std::max<uint64_t>(cap, ((2 * need) + (1ull << 20) - 1) & ~((1ull << 20) - 1)));
+}
+
+int rg_wire_plan_fixed(rg_engine* e, uint64_t* send_bytes, uint64_t* recv_bytes) {
+  if (!e || !send_bytes || !recv_bytes) return fail(RG_EINVAL, "rg_wire_plan_fixed args");
+  const uint32_t N = e->pl.N;
+  if (!e->wire) {
+    for (uint32_t r = 0; r < N; ++r) send_bytes[r] = recv_bytes[r] = 0;
+    return RG_OK;
+  }
+  if (int jrc = join(e)) return jrc;
+  HIPCHK(hipSetDevice(e->c.device));
+  if (e->cap_s.empty()) wire_caps_init(e);
+  if (e->nfix >= 2) {  // the needs of the exchange two before: long complete (a tick has run since)
+    const uint32_t sl = (uint32_t)((e->nfix - 2) % 4);
+    HIPCHK(hipEventSynchronize(e->need_ev[sl]));
+    const uint64_t* hn = e->h_need + (uint64_t)sl * 2 * MAX_RANKS;
+    for (uint32_t r = 0; r < N; ++r) {
+      wire_cap_grow(e->cap_s[r], hn[r]);
+      wire_cap_grow(e->cap_r[r], hn[MAX_RANKS + r]);
+    }
+  }
+  LAUNCH(launch_wire_plan(wire_params(e), e->bounds, e->stream), e->stream, "wire plan");
+  for (uint32_t r = 0; r < N; ++r) {
+    e->send_bytes[r] = send_bytes[r] = e->cap_s[r];
+    recv_bytes[r] = e->cap_r[r];
+  }
+  e->planned = true;
+  e->fixed = true;
+  return RG_OK;
+}
+
+int rg_wire_dropped(rg_engine* e, uint64_t* msgs) {
+  if (!e || !msgs) return fail(RG_EINVAL, "rg_wire_dropped args");
+  *msgs = 0;
+  if (!e->wire) return RG_OK;
+  if (int jrc = join(e)) return jrc;
+  unsigned long long v = 0;
+  HIPCHK(hipMemcpyAsync(&v, e->d_drops, 8, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  *msgs = v;
   return RG_OK;
 }
 
@@ -2333,6 +2425,7 @@ int rg_wire_pack(rg_engine* e, void* send_buf, uint64_t send_cap) {
   uint64_t off = 0;
   for (uint32_t r = 0; r < e->pl.N; ++r) {
     w.send_region[r] = off;
+    w.send_cap[r] = e->fixed ? e->send_bytes[r] : 0;
     off += e->send_bytes[r];
   }
   if (off > send_cap) return fail(RG_EFULL, "rg_wire_pack: send buffer smaller than the planned regions");
@@ -2351,7 +2444,7 @@ int rg_wire_recv(rg_engine* e, const void* recv_buf, const uint64_t* recv_bytes)
   uint64_t off = 0;
   for (uint32_t r = 0; r < e->pl.N; ++r) {
     const uint64_t units = e->h_rbeg[r + 1] - e->h_rbeg[r];
-    if (units ? recv_bytes[r] < wire_table_bytes(units) : recv_bytes[r] != 0)
+    if (units ? recv_bytes[r] < wire_region_min(units) : recv_bytes[r] != 0)
       return fail(RG_EINVAL, "rg_wire_recv: region of rank " + std::to_string(r) + " has the wrong size");
     w.recv_region[r] = off;
     off += recv_bytes[r];
@@ -2360,6 +2453,14 @@ int rg_wire_recv(rg_engine* e, const void* recv_buf, const uint64_t* recv_bytes)
   w.recv = (const uint8_t*)recv_buf;
   w.recv_total = off;
   LAUNCH(launch_wire_unpack(w, e->stream), e->stream, "unpack_kernel");
+  if (e->fixed) {  // this exchange's needs, for the capacity two exchanges on (no wait here)
+    const uint32_t sl = (uint32_t)(e->nfix % 4);
+    HIPCHK(hipMemcpyAsync(e->h_need + (uint64_t)sl * 2 * MAX_RANKS, e->d_need, 2 * MAX_RANKS * 8, hipMemcpyDeviceToHost,
+                          e->stream));
+    HIPCHK(hipEventRecord(e->need_ev[sl], e->stream));
+    e->nfix++;
+    e->fixed = false;
+  }
   e->recv = (const uint8_t*)recv_buf;
   e->recv_bytes = off;
   e->wire_ready = true;
@@ -2419,20 +2520,18 @@ static int xgrow(rg_engine* e, uint8_t** buf, uint64_t* cap, uint64_t need) {
 }
 
 int rg_wire_exchange(rg_engine* e, const rg_transport* t, uint64_t* sent_bytes) {
-  if (!e || !t || !t->allgather_u64 || !t->alltoallv) return fail(RG_EINVAL, "rg_wire_exchange args");
+  if (!e || !t || !t->alltoallv) return fail(RG_EINVAL, "rg_wire_exchange args");
   if (sent_bytes) *sent_bytes = 0;
   if (!e->wire) return RG_OK;
+  // one collective: fixed-capacity regions both ends already agree on (rg_wire_plan_fixed), the
+  // plan's true sizes in-band; no host sync and no size exchange
   const uint32_t N = e->pl.N, me = e->pl.rank;
-  std::vector<uint64_t> ssize(N), soff(N), all((uint64_t)N * N), rsize(N), roff(N);
-  RGCHK(rg_wire_plan(e, ssize.data()));
-  if (t->allgather_u64(t->user, ssize.data(), all.data(), N) != 0)
-    return fail(RG_EHIP, "rg_wire_exchange: transport allgather_u64 failed");
+  std::vector<uint64_t> ssize(N), soff(N), rsize(N), roff(N);
+  RGCHK(rg_wire_plan_fixed(e, ssize.data(), rsize.data()));
   uint64_t st = 0, rt = 0;
   for (uint32_t r = 0; r < N; ++r) {
-    if (all[(uint64_t)me * N + r] != ssize[r]) return fail(RG_EINVAL, "rg_wire_exchange: allgather returned another rank's sizes");
     soff[r] = st;
     st += ssize[r];
-    rsize[r] = all[(uint64_t)r * N + me];
     roff[r] = rt;
     rt += rsize[r];
   }

@@ -29,6 +29,10 @@ struct WireParams {
   uint64_t* bsum;        // scan scratch
   uint8_t* send;         // caller's send buffer
   uint64_t send_region[MAX_RANKS];  // byte offset of each destination's region
+  uint64_t send_cap[MAX_RANKS];     // fixed-capacity exchange: region bytes (0: sized by the plan); units past it are dropped
+  uint64_t* sneed;                  // [N] region bytes the plan asked for, per destination (pack_kernel)
+  uint64_t* rneed;                  // [N] the same, per source, from the received region headers (unpack_kernel)
+  unsigned long long* drops;        // messages dropped because their unit did not fit its region (cumulative)
   // receiver side
   const uint32_t* rmap;  // [RU] receive units, grouped by source rank (each source's send order)
   const uint32_t* rbeg;  // [N+1]
@@ -42,6 +46,9 @@ struct WireParams {
 };
 
 inline uint64_t wire_table_bytes(uint64_t units) { return (units * 8 + 255) & ~255ull; }
+// a region: [256-B header: u64 bytes the sender's plan asked for][unit table][data]
+constexpr uint64_t WIRE_HDR = 256;
+inline uint64_t wire_region_min(uint64_t units) { return units ? WIRE_HDR + wire_table_bytes(units) : 0; }
 
 // plan: usize, the scan, and bounds[r] = uoff[ubeg[r]] (r = 0..N, device) for the region sizes
 hipError_t launch_wire_plan(const WireParams& w, uint64_t* bounds, hipStream_t s);

@@ -8,6 +8,8 @@
 // A *unit* is one (sender slot s, destination slot d, column j) outbox column: up to K messages.
 // Units are listed per destination rank in (s, d, j) order (host-built, identical on the sender
 // and the receiver). A region for one rank is
+//     [256-B header: u64 region bytes the sender's plan asked for (the fixed-capacity exchange sizes
+//      the next regions on it)]
 //     [u64 table: (data offset in 16-B units) << 8 | message count, one per unit, padded to 256 B]
 //     [data: per message a 64-B header, then n 16-B entry records {ring word, slot crc, payload chunk
 //      offset}, then the n Cmds back to back, each rounded up to 16 B — n = the entry count of a
@@ -199,8 +201,24 @@ __global__ void __launch_bounds__(256) pack_kernel(WireParams w) {
     RG_OOB("RG_BOUNDS pack u=%u s=%u d=%u j=%u cnt=%u > K\n", u, s, d, j, c);
     c = 0;
   }
-  if (lane == 0) reinterpret_cast<uint64_t*>(region)[u - u0] = (off16 << 8) | c;
-  uint8_t* out = region + table_bytes(nu) + off16 * 16;
+  const uint64_t tb = table_bytes(nu);
+  if (u == u0 && lane == 0) {  // the header: the bytes this region needs (the receiver sizes the next ones on it)
+    const uint64_t need = 256 + tb + (w.uoff[w.ubeg[r + 1]] - w.uoff[u0]) * 16;
+    reinterpret_cast<uint64_t*>(region)[0] = need;
+    if (w.sneed) w.sneed[r] = need;
+  }
+  // fixed-capacity exchange: a unit whose data would end past the region is dropped whole (its table
+  // entry says no messages; Raft retries, as with a message lost in transit), and counted
+  const uint64_t cap = w.send_cap[r];
+  if (cap && 256 + tb + (off16 + w.usize[u]) * 16 > cap) {
+    if (lane == 0) {
+      reinterpret_cast<uint64_t*>(region + 256)[u - u0] = off16 << 8;
+      if (c && w.drops) atomicAdd(w.drops, (unsigned long long)c);
+    }
+    return;
+  }
+  if (lane == 0) reinterpret_cast<uint64_t*>(region + 256)[u - u0] = (off16 << 8) | c;
+  uint8_t* out = region + 256 + tb + off16 * 16;
   const uint32_t P = w.P;
   for (uint32_t k = 0; k < c; ++k) {
     const uint64_t* hp = w.hdr + (col * w.K + k) * w.G + j;
@@ -281,7 +299,8 @@ __global__ void unpack_kernel(WireParams w) {
   const uint32_t r = find_rank(w.rbeg, w.pl.N, u);
   const uint32_t u0 = w.rbeg[r], nu = w.rbeg[r + 1] - u0;
   const uint8_t* region = w.recv + w.recv_region[r];
-  const uint64_t tv = reinterpret_cast<const uint64_t*>(region)[u - u0];
+  if (u == u0 && w.rneed) w.rneed[r] = reinterpret_cast<const uint64_t*>(region)[0];
+  const uint64_t tv = reinterpret_cast<const uint64_t*>(region + 256)[u - u0];
   uint32_t c = (uint32_t)(tv & 0xFF);
   const uint64_t rend = r + 1 < w.pl.N ? w.recv_region[r + 1] : w.recv_total;
   uint32_t s, d, j;
@@ -293,7 +312,7 @@ __global__ void unpack_kernel(WireParams w) {
            (unsigned long long)(tv >> 8));
     c = 0;
   }
-  const uint8_t* in = region + table_bytes(nu) + (c ? (tv >> 8) * 16 : 0);
+  const uint8_t* in = region + 256 + table_bytes(nu) + (c ? (tv >> 8) * 16 : 0);
   // malformed data (a count or size beyond the region): keep only the messages before it
   uint32_t k = 0;
   for (; k < c; ++k) {

@@ -196,7 +196,7 @@ EXPORTS = ["rg_create", "rg_destroy", "rg_bootstrap", "rg_fill_slabs", "rg_tick"
            "rg_notify_applied", "rg_apply_async", "rg_apply_wait", "rg_read_index", "rg_read_index_results",
            "rg_config_change", "rg_wire_exchange", "rg_rccl_unique_id", "rg_rccl_open", "rg_rccl_close",
            "rg_pool_stats", "rg_get_update", "rg_commit_update", "rg_tick_device_n", "rg_digest",
-           "rg_host_register", "rg_host_unregister"]
+           "rg_host_register", "rg_host_unregister", "rg_wire_plan_fixed", "rg_wire_dropped"]
 
 _lib = None
 
@@ -254,6 +254,8 @@ def load_library(path: str = LIB_PATH):
         "rg_last_tick_traffic": ([vp, C.POINTER(Traffic)], i32),
         "rg_last_error": ([], C.c_char_p),
         "rg_wire_plan": ([vp, C.POINTER(C.c_uint64)], i32),
+        "rg_wire_plan_fixed": ([vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)], i32),
+        "rg_wire_dropped": ([vp, C.POINTER(C.c_uint64)], i32),
         "rg_wire_pack": ([vp, vp, u64], i32),
         "rg_wire_recv": ([vp, vp, C.POINTER(C.c_uint64)], i32),
         "rg_wire_exchange": ([vp, C.POINTER(Transport), C.POINTER(C.c_uint64)], i32),
@@ -558,6 +560,18 @@ class Engine:
         self._check(self.L.rg_wire_plan(self.h, out))
         return list(out)
 
+    def wire_plan_fixed(self):
+        """rg_wire_plan_fixed: (send capacities, receive capacities) per rank, agreed by both ends of
+        every link without a size exchange; no host sync."""
+        so, ro = (C.c_uint64 * self.ranks)(), (C.c_uint64 * self.ranks)()
+        self._check(self.L.rg_wire_plan_fixed(self.h, so, ro))
+        return list(so), list(ro)
+
+    def wire_dropped(self) -> int:
+        v = C.c_uint64()
+        self._check(self.L.rg_wire_dropped(self.h, C.byref(v)))
+        return v.value
+
     def wire_pack(self, send_ptr: int, send_cap: int):
         self._check(self.L.rg_wire_pack(self.h, C.c_void_p(send_ptr or None), send_cap))
 
@@ -566,9 +580,9 @@ class Engine:
         self._check(self.L.rg_wire_recv(self.h, C.c_void_p(recv_ptr or None), rb))
 
     def wire_exchange(self, transport: "Transport") -> int:
-        """rg_wire_exchange: plan, sizes, pack, transport, unpack in one call (the C-ABI path a
-        non-Python host uses; transport = rccl_transport(...) or PyTransport(...).t). Returns the
-        bytes sent to other ranks."""
+        """rg_wire_exchange: fixed-capacity plan, pack, one transport all-to-all, unpack in one call
+        (the C-ABI path a non-Python host uses; transport = rccl_transport(...) or PyTransport(...).t).
+        Returns the bytes sent to other ranks."""
         sent = C.c_uint64()
         self._check(self.L.rg_wire_exchange(self.h, C.byref(transport), C.byref(sent)))
         return sent.value

@@ -204,21 +204,22 @@ def test_malformed_exchange_data_is_dropped():
     def put_u64(buf, at, v):
         buf[at:at + 8].copy_(torch.from_numpy(np.array([v], np.uint64).view(np.uint8)).to(buf.device))
 
+    # a region: [256-B header][unit table][data] (raftgpu_wire.hip)
     def bad_count(k, buf, rsizes):
         for off, n, nu, tb in regions(k, buf, rsizes):
-            tab = buf[off:off + 8 * nu].cpu().numpy().view(np.uint64)
+            tab = buf[off + 256:off + 256 + 8 * nu].cpu().numpy().view(np.uint64)
             busy = [u for u in range(nu) if int(tab[u]) & 0xFF]
             if len(busy) >= 2:  # the first unit with messages claims 255, the next one's data lies at 2^54 B
-                put_u64(buf, off + 8 * busy[0], (int(tab[busy[0]]) & ~0xFF) | 0xFF)
-                put_u64(buf, off + 8 * busy[1], (1 << 58) | (int(tab[busy[1]]) & 0xFF))
+                put_u64(buf, off + 256 + 8 * busy[0], (int(tab[busy[0]]) & ~0xFF) | 0xFF)
+                put_u64(buf, off + 256 + 8 * busy[1], (1 << 58) | (int(tab[busy[1]]) & 0xFF))
                 hits["count"] += 1
 
     def bad_entries(k, buf, rsizes):
         for off, n, nu, tb in regions(k, buf, rsizes):
             reg = buf[off:off + n].cpu().numpy()
-            tab = reg[:8 * nu].view(np.uint64)
+            tab = reg[256:256 + 8 * nu].view(np.uint64)
             for u in range(nu):
-                h = tb + (int(tab[u]) >> 8) * 16
+                h = 256 + tb + (int(tab[u]) >> 8) * 16
                 for _ in range(int(tab[u]) & 0xFF):  # walk the unit's messages
                     w0 = int(reg[h:h + 8].view(np.uint64)[0])
                     if w0 & 0xFF == M_REPLICATE and w0 >> 32:  # the first Replicate claims 2^20 entries
@@ -310,8 +311,91 @@ def test_c_exchange_transport_failures_surface_as_errors():
     with pytest.raises(RgError, match="alltoallv failed"):
         eng.wire_exchange(bad.t)
     assert isinstance(bad.error, RuntimeError)
-    liar = PyTransport(lambda vals: [v + 16 for v in vals], lambda *a: None)
-    liar.nranks = 1
-    with pytest.raises(RgError, match="another rank's sizes"):
-        eng.wire_exchange(liar.t)
     eng.sync()
+
+
+def _copy_transport(calls):
+    """A one-rank Python transport: alltoallv copies the send regions into the receive buffer (after
+    the engine stream, before returning); allgather records that it was called."""
+    import torch
+    from raftd_amd.cluster import _dev_bytes
+    from raftd_amd.engine import PyTransport
+
+    def a2a(send, soff, ssize, recv, roff, rsize, stream):
+        torch.cuda.synchronize()
+        n = sum(ssize)
+        assert n == sum(rsize)
+        if n:
+            _dev_bytes(recv, n, "cuda").copy_(_dev_bytes(send, n, "cuda"))
+        torch.cuda.synchronize()
+
+    t = PyTransport(lambda vals: calls.append(list(vals)) or list(vals), a2a)
+    t.nranks = 1
+    return t
+
+
+def test_exchange_is_one_collective_with_fixed_capacity():
+    """rg_wire_exchange moves fixed-capacity regions with one transport call per tick and never asks
+    for the sizes (no allgather); with the default capacity (the worst case of this configuration
+    fits) nothing is dropped and every tick equals the oracle."""
+    from raftd_amd.engine import Engine
+    cfg = dict(groups=16, replicas=3, seed=95, **CHAOS)
+    eng = Engine(wire_all=1, **cfg)
+    ora = make("c", **cfg)
+    calls = []
+    t = _copy_transport(calls)
+    eng.bootstrap()
+    ora.bootstrap()
+    rng = np.random.default_rng(96)
+    for k in range(50):
+        if k:
+            eng.wire_exchange(t.t)
+        ins = random_inputs(rng, 16, 3, CHAOS["max_entries_per_msg"])
+        eng.tick(*ins)
+        ora.tick(*ins)
+        compare(eng, ora, k)
+    assert calls == [] and t.error is None
+    assert eng.wire_dropped() == 0
+
+
+def test_fixed_capacity_overflow_drops_units_and_grows():
+    """Regions far too small for the traffic (RAFTGPU_WIRE_CAP0 = 4 KiB): the units past a region's
+    end are dropped and counted, the capacity grows from the needs two exchanges later, the drops
+    stop, and the cluster keeps committing with every replica's committed log equal to its leader's
+    (message loss is safe in Raft)."""
+    import os
+    from raftd_amd.engine import Engine
+    G, R, E = 256, 3, 16
+    os.environ["RAFTGPU_WIRE_CAP0"] = "4096"
+    try:
+        eng = Engine(wire_all=1, groups=G, replicas=R, log_capacity=256, payload_bytes=64, max_entries_per_msg=E,
+                     snapshot_entries=0, seed=97)
+        calls = []
+        t = _copy_transport(calls)
+        eng.bootstrap()
+        camp = np.zeros(G * R, np.uint8)
+        camp[0::R] = 1
+        pt, pc = np.zeros(G, np.uint8), np.full(G, E, np.uint32)
+        drops = []
+        for k in range(40):
+            if k:
+                eng.wire_exchange(t.t)
+            eng.tick(*((None, None, camp) if k == 1 else (pt, pc) if k >= 4 else ()))
+            drops.append(eng.wire_dropped())
+        eng.sync()
+    finally:
+        del os.environ["RAFTGPU_WIRE_CAP0"]
+    assert drops[-1] > 0 and drops[-1] == drops[-10], drops  # dropped early, none in the last ten ticks
+    views = eng.replicas()
+    done = 0
+    for g in range(G):
+        vs = views[g * R:(g + 1) * R]
+        c = min(v["committed"] for v in vs)
+        lo = max(v["marker"] for v in vs) + 1
+        if c >= lo:
+            ref = [x["term"] for x in eng.entries(g * R, lo, c - lo + 1)]
+            for s in range(1, R):
+                assert [x["term"] for x in eng.entries(g * R + s, lo, c - lo + 1)] == ref, g
+            done += 1
+        assert max(v["committed"] for v in vs) > 100, g
+    assert done > G // 2
