@@ -156,9 +156,10 @@ struct Ctl {
   uint32_t nj;      // jobs emitted
   uint64_t lt_i = ~0ull, lt_v = 0;  // term_at cache: index lt_i has term lt_v (~0: none)
 
-  RG_FN Ctl(CTickParams& pp, uint32_t qq) : p(pp), q(qq) {
-    s = q / p.G;
-    g = q - s * p.G;
+  RG_FN Ctl(CTickParams& pp, uint32_t qq) : Ctl(pp, qq / pp.G, qq - (qq / pp.G) * pp.G) {}
+  // slot ss of group column g0: the kernels pass a wave-uniform slot (the grid's y index), so every
+  // value derived from s alone (its outbox planes, the sender loop's skip, my_id) stays scalar
+  RG_FN Ctl(CTickParams& pp, uint32_t ss, uint32_t g0) : p(pp), q(ss * pp.G + g0), g(g0), s(ss) {
     gg = pl_group(p.pl, s, g);
     rid = gg * R + s;
     gi = (uint32_t)pl_input_index(p.pl, gg);
@@ -1341,8 +1342,14 @@ struct Ctl {
       uint32_t ns = 0, nk = 0;
       const bool more = next_msg(cs, ck, ns, nk);
       Hdr nxt{};
+#ifdef RG_CTL_FAST_NOPIPE  // experiment: the fast path without the header prefetch (fewer live registers)
+      if (!FAST && more) load_hdr(ns, nk, pl_remote(p.pl, ns, s, g), nxt);
+      handle(cs, ck, pl_remote(p.pl, cs, s, g), cur);
+      if (FAST && more && !aborted) load_hdr(ns, nk, pl_remote(p.pl, ns, s, g), nxt);
+#else
       if (more) load_hdr(ns, nk, pl_remote(p.pl, ns, s, g), nxt);
       handle(cs, ck, pl_remote(p.pl, cs, s, g), cur);
+#endif
       cur = nxt;
       cs = ns;
       ck = nk;

@@ -78,23 +78,30 @@ __global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_MINWAVES) control_kernel(
 template <int R>
 __global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_FAST_WAVES) control_fast_kernel(
     const TickParams* __restrict__ pp, uint32_t* perr) {
-  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (!tp_verify(pp, perr, q, "control_fast_kernel")) return;
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x, s = blockIdx.y;
+  if (!tp_verify(pp, perr, g + s, "control_fast_kernel")) return;
   CTickParams& cp = *(CTickParams*)pp;
-  if (q == 0) cp.slow_cnt[(cp.tick + 1) & 1] = 0;  // the next tick's counter (its last reader ran before us)
-  if (q >= cp.nrep) return;
-  Ctl<R, true> c(cp, q);
+  if (g + s == 0) cp.slow_cnt[(cp.tick + 1) & 1] = 0;  // the next tick's counter (its last reader ran before us)
+  if (g >= cp.G) return;
+#ifdef RG_CTL_PROFILE
+  const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memtime();
+  Ctl<R, true> c(cp, s, g);
+  c.stamps[0] = t0;
+#else
+  Ctl<R, true> c(cp, s, g);
+#endif
   c.run();
   // hand-off: the lane's flag for the slow kernel, and one counter atomic per wave with aborted lanes
   // (the count is for measurement: rg_debug_ctl_slow)
-  cp.slow_flag[q] = c.aborted ? 1u : 0u;
+  cp.slow_flag[c.q] = c.aborted ? 1u : 0u;
   const uint64_t m = __ballot(c.aborted);
   if (m && (threadIdx.x & 63u) == (uint32_t)__ffsll((long long)m) - 1)
     atomicAdd(cp.slow_cnt + (cp.tick & 1), (uint32_t)__popcll(m));
 }
 
 // the replicas the fast kernel handed off this tick (a wave without one leaves at once). Lane q steps
-// replica q, as control_kernel does: the affine lane -> replica map keeps its registers the same.
+// replica q, as control_kernel does (a one-dimensional grid: the full step with a grid-uniform slot
+// index faulted in the full-size C3 test, r04, while this mapping has run every suite since r01).
 template <int R>
 __global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_MINWAVES) control_slow_kernel(const TickParams* __restrict__ pp,
                                                                                     uint32_t* perr) {
@@ -169,9 +176,13 @@ hipError_t launch_control_fast_t<RG_CTL_R>(const TickParams* p, uint32_t* perr, 
   (void)p; (void)perr; (void)nrep; (void)s;
   return hipErrorInvalidValue;
 #else
-  const dim3 grid((nrep + RG_CTL_BLOCK - 1) / RG_CTL_BLOCK), block(RG_CTL_BLOCK);
+  // the fast kernel's grid is (group columns, slots): a wave steps one slot of 64 groups, so its slot
+  // index is scalar (fewer VGPRs, r04); the slow kernel's is the full step's
+  const uint32_t G = nrep / RG_CTL_R;
+  const dim3 grid((G + RG_CTL_BLOCK - 1) / RG_CTL_BLOCK, RG_CTL_R), block(RG_CTL_BLOCK);
   hipLaunchKernelGGL(control_fast_kernel<RG_CTL_R>, grid, block, 0, s, p, perr);
-  hipLaunchKernelGGL(control_slow_kernel<RG_CTL_R>, grid, block, 0, s, p, perr);
+  hipLaunchKernelGGL(control_slow_kernel<RG_CTL_R>, dim3((nrep + RG_CTL_BLOCK - 1) / RG_CTL_BLOCK), block, 0, s, p,
+                     perr);
   return hipGetLastError();
 #endif
 }
