@@ -149,6 +149,35 @@ def all_to_all_bytes(send, send_sizes, recv, recv_sizes, group=None, async_op=Fa
     return None
 
 
+def p2p_regions(send, send_sizes, recv, recv_sizes, group=None, async_op=False, chunk=A2A_CHUNK):
+    """The fixed-capacity exchange's transfer: region r of `send` to rank r and region
+    r of `recv` from rank r as one batch of point-to-point sends and receives (one grouped RCCL call),
+    each piece at most `chunk` bytes (the 1 GiB contract). A link's two ends agree on its size, so
+    they cut it into the same pieces without any rank knowing the others' sizes (an all_to_all's
+    chunk count has to be the same on every rank). The region to this rank itself is a device copy.
+    nccl only; gloo ranks go through all_to_all_bytes."""
+    import torch.distributed as dist
+    me, n = dist.get_rank(group), dist.get_world_size(group)
+    so, _ = _offsets(send_sizes)
+    ro, _ = _offsets(recv_sizes)
+    if send_sizes[me]:
+        recv[ro[me]:ro[me] + recv_sizes[me]].copy_(send[so[me]:so[me] + send_sizes[me]])
+    ops = []
+    for r in range(n):
+        if r == me:
+            continue
+        peer = dist.get_global_rank(group, r) if group is not None else r
+        for lo in range(0, send_sizes[r], chunk):
+            ops.append(dist.P2POp(dist.isend, send[so[r] + lo:so[r] + min(send_sizes[r], lo + chunk)], peer, group))
+        for lo in range(0, recv_sizes[r], chunk):
+            ops.append(dist.P2POp(dist.irecv, recv[ro[r] + lo:ro[r] + min(recv_sizes[r], lo + chunk)], peer, group))
+    h = _Works(dist.batch_isend_irecv(ops) if ops else [])
+    if async_op:
+        return h
+    h.wait()
+    return None
+
+
 def exchange_sizes(send_sizes, group=None):
     """Each rank's outbound region sizes → (the sizes this rank receives from every rank, the
     largest region any rank sends this exchange), by one all_gather of the size rows."""
@@ -220,10 +249,11 @@ class _Half:
         if self.xt is not None:
             self.sent = e.wire_exchange(self.xt)
             return
+        import torch.distributed as dist
         if self.fixed:
-            # one collective, no host sync: capacities both ends of every link agree on (rg_wire_plan_fixed)
+            # one grouped transfer, no host sync: capacities both ends of every link agree on (rg_wire_plan_fixed)
             sizes, rsizes = e.wire_plan_fixed()
-            biggest = max(sizes + rsizes)  # <= 1 GiB by construction: one all-to-all call on every rank
+            biggest = max(sizes + rsizes)  # gloo: host-staged, one call
         else:
             sizes = e.wire_plan()  # host sync: the tick that produced the messages has completed
         _, stot = _offsets(sizes)
@@ -233,8 +263,11 @@ class _Half:
             rsizes, biggest = exchange_sizes(sizes, self.pg)
         _, rtot = _offsets(rsizes)
         self.recv.ensure(rtot)  # stream order: the tick that reads the old buffer runs before a reuse
-        self.work = all_to_all_bytes(self.send.t, sizes, self.recv.t, rsizes, self.pg, async_op=async_op,
-                                     nchunks=1 if self.fixed else a2a_chunks(biggest))
+        if self.fixed and dist.get_backend(self.pg) == "nccl":
+            self.work = p2p_regions(self.send.t, sizes, self.recv.t, rsizes, self.pg, async_op=async_op)
+        else:
+            self.work = all_to_all_bytes(self.send.t, sizes, self.recv.t, rsizes, self.pg, async_op=async_op,
+                                         nchunks=a2a_chunks(biggest))
         self.rsizes, self.sent = rsizes, stot - sizes[self.rank]
 
     def finish(self):

@@ -114,7 +114,10 @@ using CTickParams = RG_CONST(const TickParams);
 // or lies where nothing reads it (message slots past the final count, ring slots past the final last,
 // job rows past the final job count). Fewer live values: the fields only the aborted branches touch are
 // copied through at the end instead of living in registers for the whole step.
-template <int R, bool FAST = false>
+// ROLE (FAST only): -1 = any role; LEADER / FOLLOWER = the role-sorted fast launches (control_fast_kernel):
+// the lane's role is that compile-time constant for the whole step (the fast path never changes a role:
+// every transition aborts), so the other roles' branches compile away.
+template <int R, bool FAST = false, int ROLE = -1>
 struct Ctl {
   // the tick's parameter block, read in place at each use (a device slot the host filled): the
   // fields are reloaded where needed instead of living in registers for the whole step (r02 kept a
@@ -195,6 +198,7 @@ struct Ctl {
     processed_start = processed; restored_at = 0; wlo = ~0ull; took = false;
     if constexpr (FAST) {
       if (role == CANDIDATE) abort_();  // every candidate path (votes, fallback) is the full step's
+      if constexpr (ROLE >= 0) role = ROLE;  // the launch's role (the kernel stepped only those lanes)
     }
     // the last step compacted (or restored) below entry fidx: its stream position bounds the pages
     // to release, known now that the step which wrote it has stored its {crc, position} (the bulk
@@ -1296,6 +1300,17 @@ struct Ctl {
   // ---- the whole step
   uint32_t stamps[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 
+  // the next inbox header is loaded before the current message is handled (one round trip for the
+  // whole inbox), except in the followers' fast step: a follower's inbox is a Replicate and perhaps a
+  // Heartbeat, and without the second header live the step fits three waves per SIMD (r04)
+#if defined(RG_CTL_FAST_NOPIPE)
+  static constexpr bool PIPE = !FAST;
+#elif defined(RG_CTL_FAST_PIPE)
+  static constexpr bool PIPE = true;
+#else
+  static constexpr bool PIPE = !(FAST && ROLE == FOLLOWER);
+#endif
+
   RG_FN void run() {
     // The step's inputs that no step logic feeds — the inbox counts of every sender and the tick
     // inputs — are loaded together up front: the lane then waits one memory latency for all of them
@@ -1342,14 +1357,9 @@ struct Ctl {
       uint32_t ns = 0, nk = 0;
       const bool more = next_msg(cs, ck, ns, nk);
       Hdr nxt{};
-#ifdef RG_CTL_FAST_NOPIPE  // experiment: the fast path without the header prefetch (fewer live registers)
-      if (!FAST && more) load_hdr(ns, nk, pl_remote(p.pl, ns, s, g), nxt);
+      if (PIPE && more) load_hdr(ns, nk, pl_remote(p.pl, ns, s, g), nxt);
       handle(cs, ck, pl_remote(p.pl, cs, s, g), cur);
-      if (FAST && more && !aborted) load_hdr(ns, nk, pl_remote(p.pl, ns, s, g), nxt);
-#else
-      if (more) load_hdr(ns, nk, pl_remote(p.pl, ns, s, g), nxt);
-      handle(cs, ck, pl_remote(p.pl, cs, s, g), cur);
-#endif
+      if (!PIPE && more && !(FAST && aborted)) load_hdr(ns, nk, pl_remote(p.pl, ns, s, g), nxt);
       cur = nxt;
       cs = ns;
       ck = nk;

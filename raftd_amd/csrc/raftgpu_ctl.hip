@@ -73,35 +73,54 @@ __global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_MINWAVES) control_kernel(
 // steady-state branches only and hands a replica whose step leaves them to the slow kernel, which
 // re-runs that replica's whole step with the full Ctl<R> (an aborted fast step stored nothing).
 #ifndef RG_CTL_FAST_WAVES
-#define RG_CTL_FAST_WAVES (RG_CTL_R <= 6 ? 2 : 1)  // R 7, 8: two waves would need scratch
+#define RG_CTL_FAST_WAVES (RG_CTL_R <= 3 ? 3 : 2)  // the most waves per SIMD without scratch (role-sorted)
 #endif
+// The fast path is compiled once per role — Ctl<R, true, LEADER> for leaders, Ctl<R, true, FOLLOWER>
+// for every other replica (followers step, candidates hand off) — and each lane runs its role's
+// step: the two are separate branches, so the kernel holds the larger role's live values instead of
+// both roles' at once (r04: 204 -> 168 VGPRs at R = 3, three waves per SIMD). In steady state a wave's
+// lanes share a role (slot-major lanes, one leader slot per group) and run one branch.
 template <int R>
 __global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_FAST_WAVES) control_fast_kernel(
     const TickParams* __restrict__ pp, uint32_t* perr) {
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x, s = blockIdx.y;
-  if (!tp_verify(pp, perr, g + s, "control_fast_kernel")) return;
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (!tp_verify(pp, perr, q, "control_fast_kernel")) return;
   CTickParams& cp = *(CTickParams*)pp;
-  if (g + s == 0) cp.slow_cnt[(cp.tick + 1) & 1] = 0;  // the next tick's counter (its last reader ran before us)
-  if (g >= cp.G) return;
+  if (q == 0) cp.slow_cnt[(cp.tick + 1) & 1] = 0;  // the next tick's counter (its last reader ran before us)
+  if (q >= cp.nrep) return;
+  bool aborted;
+  if (cp.s32_in[(uint64_t)S_ROLE * cp.nrep + q] == LEADER) {
 #ifdef RG_CTL_PROFILE
-  const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memtime();
-  Ctl<R, true> c(cp, s, g);
-  c.stamps[0] = t0;
+    const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memtime();
+    Ctl<R, true, LEADER> c(cp, q);
+    c.stamps[0] = t0;
 #else
-  Ctl<R, true> c(cp, s, g);
+    Ctl<R, true, LEADER> c(cp, q);
 #endif
-  c.run();
+    c.run();
+    aborted = c.aborted;
+  } else {
+#ifdef RG_CTL_PROFILE
+    const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memtime();
+    Ctl<R, true, FOLLOWER> c(cp, q);
+    c.stamps[0] = t0;
+#else
+    Ctl<R, true, FOLLOWER> c(cp, q);
+#endif
+    c.run();
+    aborted = c.aborted;
+  }
   // hand-off: the lane's flag for the slow kernel, and one counter atomic per wave with aborted lanes
   // (the count is for measurement: rg_debug_ctl_slow)
-  cp.slow_flag[c.q] = c.aborted ? 1u : 0u;
-  const uint64_t m = __ballot(c.aborted);
+  cp.slow_flag[q] = aborted ? 1u : 0u;
+  const uint64_t m = __ballot(aborted);
   if (m && (threadIdx.x & 63u) == (uint32_t)__ffsll((long long)m) - 1)
     atomicAdd(cp.slow_cnt + (cp.tick & 1), (uint32_t)__popcll(m));
 }
 
 // the replicas the fast kernel handed off this tick (a wave without one leaves at once). Lane q steps
 // replica q, as control_kernel does (a one-dimensional grid: the full step with a grid-uniform slot
-// index faulted in the full-size C3 test, r04, while this mapping has run every suite since r01).
+// index, blockIdx.y, faulted in the full-size C3 test in r04; this mapping has run every suite since r01).
 template <int R>
 __global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_MINWAVES) control_slow_kernel(const TickParams* __restrict__ pp,
                                                                                     uint32_t* perr) {
@@ -176,13 +195,9 @@ hipError_t launch_control_fast_t<RG_CTL_R>(const TickParams* p, uint32_t* perr, 
   (void)p; (void)perr; (void)nrep; (void)s;
   return hipErrorInvalidValue;
 #else
-  // the fast kernel's grid is (group columns, slots): a wave steps one slot of 64 groups, so its slot
-  // index is scalar (fewer VGPRs, r04); the slow kernel's is the full step's
-  const uint32_t G = nrep / RG_CTL_R;
-  const dim3 grid((G + RG_CTL_BLOCK - 1) / RG_CTL_BLOCK, RG_CTL_R), block(RG_CTL_BLOCK);
+  const dim3 grid((nrep + RG_CTL_BLOCK - 1) / RG_CTL_BLOCK), block(RG_CTL_BLOCK);
   hipLaunchKernelGGL(control_fast_kernel<RG_CTL_R>, grid, block, 0, s, p, perr);
-  hipLaunchKernelGGL(control_slow_kernel<RG_CTL_R>, dim3((nrep + RG_CTL_BLOCK - 1) / RG_CTL_BLOCK), block, 0, s, p,
-                     perr);
+  hipLaunchKernelGGL(control_slow_kernel<RG_CTL_R>, grid, block, 0, s, p, perr);
   return hipGetLastError();
 #endif
 }

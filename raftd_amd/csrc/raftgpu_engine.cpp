@@ -2350,10 +2350,10 @@ int rg_wire_plan(rg_engine* e, uint64_t* send_bytes) {
 
 // Fixed-capacity regions. A link's region starts at the bytes its units could need
 // (K messages of E entries of max_cmd_bytes each, plus header and table), at most RAFTGPU_WIRE_CAP0
-// (64 MiB) and never more than WIRE_CAP_MAX (one all-to-all call moves it); it doubles past any need
-// above half of it. Both ends apply that rule to the same numbers — the sender to its plan, the
+// (64 MiB) and never more than WIRE_CAP_MAX (4 GiB; transports move a region in pieces of at most
+// 256 MiB); it doubles past any need above half of it. Both ends apply that rule to the same numbers — the sender to its plan, the
 // receiver to the region header it got — two exchanges late, so neither waits for the other.
-static constexpr uint64_t WIRE_CAP_MAX = 1ull << 30;
+static constexpr uint64_t WIRE_CAP_MAX = 4ull << 30;
 static void wire_caps_init(rg_engine* e) {
   const uint32_t N = e->pl.N;
   uint64_t cap0 = 64ull << 20;
