@@ -80,15 +80,9 @@ __global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_MINWAVES) control_kernel(
 // step: the two are separate branches, so the kernel holds the larger role's live values instead of
 // both roles' at once (r04: 204 -> 168 VGPRs at R = 3, three waves per SIMD). In steady state a wave's
 // lanes share a role (slot-major lanes, one leader slot per group) and run one branch.
+// one replica's fast step (its role's instantiation); returns whether it left the fast path
 template <int R>
-__global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_FAST_WAVES) control_fast_kernel(
-    const TickParams* __restrict__ pp, uint32_t* perr) {
-  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (!tp_verify(pp, perr, q, "control_fast_kernel")) return;
-  CTickParams& cp = *(CTickParams*)pp;
-  if (q == 0) cp.slow_cnt[(cp.tick + 1) & 1] = 0;  // the next tick's counter (its last reader ran before us)
-  if (q >= cp.nrep) return;
-  bool aborted;
+__device__ __forceinline__ bool fast_step(CTickParams& cp, uint32_t q) {
   if (cp.s32_in[(uint64_t)S_ROLE * cp.nrep + q] == LEADER) {
 #ifdef RG_CTL_PROFILE
     const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memtime();
@@ -98,25 +92,59 @@ __global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_FAST_WAVES) control_fast_
     Ctl<R, true, LEADER> c(cp, q);
 #endif
     c.run();
-    aborted = c.aborted;
-  } else {
-#ifdef RG_CTL_PROFILE
-    const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memtime();
-    Ctl<R, true, FOLLOWER> c(cp, q);
-    c.stamps[0] = t0;
-#else
-    Ctl<R, true, FOLLOWER> c(cp, q);
-#endif
-    c.run();
-    aborted = c.aborted;
+    return c.aborted;
   }
-  // hand-off: the lane's flag for the slow kernel, and one counter atomic per wave with aborted lanes
-  // (the count is for measurement: rg_debug_ctl_slow)
-  cp.slow_flag[q] = aborted ? 1u : 0u;
+#ifdef RG_CTL_PROFILE
+  const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memtime();
+  Ctl<R, true, FOLLOWER> c(cp, q);
+  c.stamps[0] = t0;
+#else
+  Ctl<R, true, FOLLOWER> c(cp, q);
+#endif
+  c.run();
+  return c.aborted;
+}
+
+// the hand-off count (measurement: rg_debug_ctl_slow): one atomic per wave with aborted lanes
+__device__ __forceinline__ void count_slow(CTickParams& cp, bool aborted) {
   const uint64_t m = __ballot(aborted);
   if (m && (threadIdx.x & 63u) == (uint32_t)__ffsll((long long)m) - 1)
     atomicAdd(cp.slow_cnt + (cp.tick & 1), (uint32_t)__popcll(m));
 }
+
+template <int R>
+__global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_FAST_WAVES) control_fast_kernel(
+    const TickParams* __restrict__ pp, uint32_t* perr) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (!tp_verify(pp, perr, q, "control_fast_kernel")) return;
+  CTickParams& cp = *(CTickParams*)pp;
+  if (q == 0) cp.slow_cnt[(cp.tick + 1) & 1] = 0;  // the next tick's counter (its last reader ran before us)
+  if (q >= cp.nrep) return;
+  const bool aborted = fast_step<R>(cp, q);
+  cp.slow_flag[q] = aborted ? 1u : 0u;  // for control_slow_kernel
+  count_slow(cp, aborted);
+}
+
+// Small engines (a wave or less per SIMD: occupancy buys nothing) run the fallback in the same
+// launch: a lane that leaves the fast path re-runs its step with the full Ctl<R> right away, and the
+// tick saves the slow kernel's launch (C2 shapes: the tick is a few of these latencies).
+#if RG_CTL_R <= 5
+template <int R>
+__global__ void __launch_bounds__(RG_CTL_BLOCK, 1) control_fastfb_kernel(const TickParams* __restrict__ pp,
+                                                                         uint32_t* perr) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (!tp_verify(pp, perr, q, "control_fastfb_kernel")) return;
+  CTickParams& cp = *(CTickParams*)pp;
+  if (q == 0) cp.slow_cnt[(cp.tick + 1) & 1] = 0;
+  if (q >= cp.nrep) return;
+  const bool aborted = fast_step<R>(cp, q);
+  count_slow(cp, aborted);
+  if (aborted) {  // the fast step stored nothing: the full step from the same inputs
+    Ctl<R> c(cp, q);
+    c.run();
+  }
+}
+#endif
 
 // the replicas the fast kernel handed off this tick (a wave without one leaves at once). Lane q steps
 // replica q, as control_kernel does (a one-dimensional grid: the full step with a grid-uniform slot
@@ -170,8 +198,10 @@ __global__ void __launch_bounds__(64 * R, 1) control_resident_kernel(const TickP
   const uint32_t q = w * G + g;
   for (uint32_t i = 0; i < k; ++i) {
     if (g < G) {
-      Ctl<R> c(cp[i], q);
-      c.run();
+      if (fast_step<R>(cp[i], q)) {  // left the fast path (stored nothing): the full step
+        Ctl<R> c(cp[i], q);
+        c.run();
+      }
     }
     __syncthreads();  // tick i's outboxes and state, written by this workgroup, before tick i + 1 reads them
   }
@@ -190,12 +220,20 @@ hipError_t launch_control_t<RG_CTL_R>(const TickParams* p, uint32_t* perr, uint3
 }
 
 template <>
-hipError_t launch_control_fast_t<RG_CTL_R>(const TickParams* p, uint32_t* perr, uint32_t nrep, hipStream_t s) {
+hipError_t launch_control_fast_t<RG_CTL_R>(const TickParams* p, uint32_t* perr, uint32_t nrep, bool fb, hipStream_t s) {
 #if defined(RG_DEV_NO_CONTROL) || !defined(RG_CTL_FASTREP)  // the fast path builds on the uniform Replicate
-  (void)p; (void)perr; (void)nrep; (void)s;
+  (void)p; (void)perr; (void)nrep; (void)fb; (void)s;
   return hipErrorInvalidValue;
 #else
   const dim3 grid((nrep + RG_CTL_BLOCK - 1) / RG_CTL_BLOCK), block(RG_CTL_BLOCK);
+#if RG_CTL_R <= 5  // R 6-8: the fast and the full step together need scratch
+  if (fb) {
+    hipLaunchKernelGGL(control_fastfb_kernel<RG_CTL_R>, grid, block, 0, s, p, perr);
+    return hipGetLastError();
+  }
+#else
+  (void)fb;
+#endif
   hipLaunchKernelGGL(control_fast_kernel<RG_CTL_R>, grid, block, 0, s, p, perr);
   hipLaunchKernelGGL(control_slow_kernel<RG_CTL_R>, grid, block, 0, s, p, perr);
   return hipGetLastError();

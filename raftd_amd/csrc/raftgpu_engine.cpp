@@ -176,6 +176,7 @@ struct rg_engine {
   // handed off ([2] counters by tick parity, then the list); RAFTGPU_CTL_FAST=0: control_kernel alone (A/B)
   uint32_t* slow = nullptr;
   bool ctl_fast = true;
+  bool ctl_fb = false;  // small engines: the fallback runs in the fast kernel's launch (control_fastfb_kernel)
   uint8_t* stage = nullptr;
   uint64_t stage_bytes = 0;
   uint64_t t = 0;
@@ -711,6 +712,9 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if (const char* v = getenv("RAFTGPU_APPLY_MEMCPY")) e->copy_kernel = !(v[0] == '1');
   e->bulk_mj = c.max_entries_per_msg <= 16;
   if (const char* v = getenv("RAFTGPU_CTL_FAST")) e->ctl_fast = v[0] != '0';
+  // at most one wave per SIMD: occupancy buys nothing, and the fallback saves the slow kernel's launch
+  e->ctl_fb = (uint64_t)n <= 64ull * 1024;
+  if (const char* v = getenv("RAFTGPU_CTL_FB")) e->ctl_fb = v[0] == '1';
   if (const char* v = getenv("RAFTGPU_BULK_MULTIJOB")) e->bulk_mj = v[0] == '1';
   if (const char* v = getenv("RAFTGPU_BULK_SMALL")) e->bulk_small = v[0] != '0';
   if (const char* v = getenv("RAFTGPU_APPLY_SDMA"))
@@ -1349,7 +1353,7 @@ static int launch_control_slot(rg_engine* e, const TickParams& p) {
     e->tp_used[c] = true;
   }
   if (e->ctl_fast)
-    LAUNCH(launch_control_fast(e->d_tp + k, &e->poolctl->param_err, p.R, p.nrep, e->stream), e->stream,
+    LAUNCH(launch_control_fast(e->d_tp + k, &e->poolctl->param_err, p.R, p.nrep, e->ctl_fb, e->stream), e->stream,
            "control_fast_kernel / control_slow_kernel");
   else
     LAUNCH(launch_control(e->d_tp + k, &e->poolctl->param_err, p.R, p.nrep, e->stream), e->stream, "control_kernel");
@@ -1521,7 +1525,7 @@ static int tick_graph(rg_engine* e, const rg_tick_input* in, uint32_t k) {
         TickParams* ds = e->g_dtp + set * G_MAXK + i;
         hipError_t r = hipMemcpyAsync(ds, hs, sizeof(TickParams), hipMemcpyHostToDevice, e->stream);
         if (r == hipSuccess)
-          r = e->ctl_fast ? launch_control_fast(ds, &e->poolctl->param_err, p.R, p.nrep, e->stream)
+          r = e->ctl_fast ? launch_control_fast(ds, &e->poolctl->param_err, p.R, p.nrep, e->ctl_fb, e->stream)
                           : launch_control(ds, &e->poolctl->param_err, p.R, p.nrep, e->stream);
         if (r == hipSuccess && e->c.payload_bytes) {
           PoolParams pp{};

@@ -356,7 +356,7 @@ RG_HD_INLINE uint64_t stream_byte(const uint32_t* pt, uint32_t PTS, uint32_t q, 
 hipError_t launch_control(const TickParams* p, uint32_t* perr, uint32_t R, uint32_t nrep, hipStream_t s);
 // the fast path: control_fast_kernel<R> over every replica, then control_slow_kernel<R> over the replicas
 // it handed off (the parameter block's slow_cnt / slow_flag)
-hipError_t launch_control_fast(const TickParams* p, uint32_t* perr, uint32_t R, uint32_t nrep, hipStream_t s);
+hipError_t launch_control_fast(const TickParams* p, uint32_t* perr, uint32_t R, uint32_t nrep, bool fb, hipStream_t s);
 // k ticks of a metadata-only one-rank engine in one launch (p = k consecutive sealed blocks)
 hipError_t launch_control_resident(const TickParams* p, uint32_t k, uint32_t* perr, uint32_t R, uint32_t G,
                                    hipStream_t s);
@@ -364,7 +364,7 @@ hipError_t launch_control_resident(const TickParams* p, uint32_t k, uint32_t* pe
 template <int R>
 hipError_t launch_control_t(const TickParams* p, uint32_t* perr, uint32_t nrep, hipStream_t s);
 template <int R>
-hipError_t launch_control_fast_t(const TickParams* p, uint32_t* perr, uint32_t nrep, hipStream_t s);
+hipError_t launch_control_fast_t(const TickParams* p, uint32_t* perr, uint32_t nrep, bool fb, hipStream_t s);
 template <int R>
 hipError_t launch_control_resident_t(const TickParams* p, uint32_t k, uint32_t* perr, uint32_t G, hipStream_t s);
 template <bool W, bool MJ>

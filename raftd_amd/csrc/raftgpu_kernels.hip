@@ -42,16 +42,16 @@ hipError_t launch_control(const TickParams* p, uint32_t* perr, uint32_t R, uint3
   }
 }
 
-hipError_t launch_control_fast(const TickParams* p, uint32_t* perr, uint32_t R, uint32_t nrep, hipStream_t s) {
+hipError_t launch_control_fast(const TickParams* p, uint32_t* perr, uint32_t R, uint32_t nrep, bool fb, hipStream_t s) {
   switch (R) {
-    case 1: return launch_control_fast_t<1>(p, perr, nrep, s);
-    case 2: return launch_control_fast_t<2>(p, perr, nrep, s);
-    case 3: return launch_control_fast_t<3>(p, perr, nrep, s);
-    case 4: return launch_control_fast_t<4>(p, perr, nrep, s);
-    case 5: return launch_control_fast_t<5>(p, perr, nrep, s);
-    case 6: return launch_control_fast_t<6>(p, perr, nrep, s);
-    case 7: return launch_control_fast_t<7>(p, perr, nrep, s);
-    case 8: return launch_control_fast_t<8>(p, perr, nrep, s);
+    case 1: return launch_control_fast_t<1>(p, perr, nrep, fb, s);
+    case 2: return launch_control_fast_t<2>(p, perr, nrep, fb, s);
+    case 3: return launch_control_fast_t<3>(p, perr, nrep, fb, s);
+    case 4: return launch_control_fast_t<4>(p, perr, nrep, fb, s);
+    case 5: return launch_control_fast_t<5>(p, perr, nrep, fb, s);
+    case 6: return launch_control_fast_t<6>(p, perr, nrep, fb, s);
+    case 7: return launch_control_fast_t<7>(p, perr, nrep, fb, s);
+    case 8: return launch_control_fast_t<8>(p, perr, nrep, fb, s);
     default: return hipErrorInvalidValue;
   }
 }

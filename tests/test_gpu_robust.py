@@ -47,10 +47,13 @@ def test_corrupt_parameter_block_is_reported_and_harmless():
     assert gpu.pool_stats()["free"] == before["free"]
 
 
-def test_control_fast_path_covers_the_steady_state():
+@pytest.mark.parametrize("fb", ["0", "1"])
+def test_control_fast_path_covers_the_steady_state(fb, monkeypatch):
     """The benchmark's steady state (leaders with full batches every tick, snapshots and compaction)
     never leaves the control fast path (rg_debug_ctl_slow = 0 per tick after the election), an
-    election does (the full kernel steps the candidates), and every replica equals the oracle."""
+    election does (the full step runs for the candidates: in control_slow_kernel, fb 0, or in the
+    fast kernel's own launch, fb 1), and every replica equals the oracle."""
+    monkeypatch.setenv("RAFTGPU_CTL_FB", fb)
     G, R, E = 512, 3, 64
     cfg = dict(groups=G, replicas=R, log_capacity=256, payload_bytes=256, max_entries_per_msg=E,
                snapshot_entries=100, compaction_overhead=5, seed=0x5EED)
