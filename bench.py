@@ -645,8 +645,10 @@ def main():
         "kernels_ms": {"control_kernel": ctl_ms, "bulk_kernel": bulk_ms},
         "control_fast_path": {"enabled": os.environ.get("RAFTGPU_CTL_FAST", "1") != "0",
                               "slow_replicas_last_tick": ctl_slow,
-                              "note": "control_kernel time = control_fast_kernel (steady-state branches, occupancy 2) + "
-                                      "control_slow_kernel (the full step for the replicas the fast kernel handed off)"},
+                              "note": "control_kernel time = control_fast_kernel (the steady-state branches, compiled per "
+                                      "role: three waves per SIMD at R <= 3) + control_slow_kernel (the full step for the "
+                                      "replicas the fast kernel handed off); engines of <= 64K replicas run "
+                                      "control_fastfb_kernel instead (the full step inside the same launch)"},
         "exchange": None if not wire else {
             "mode": (f"pipelined over {args.halves} column halves: one half's all-to-all overlaps the other's "
                      "unpack + tick + pack" if pipelined else "serial: plan + pack + all-to-all + unpack, then tick"),

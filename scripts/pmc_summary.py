@@ -26,7 +26,8 @@ def rows(d, pattern):
 
 
 def short(name):
-    for k in ("control_kernel", "bulk_kernel", "bulk_meta_kernel", "tick_kernel", "bootstrap_kernel",
+    for k in ("control_fastfb_kernel", "control_fast_kernel", "control_slow_kernel", "control_kernel",
+              "bulk_small_kernel", "bulk_kernel", "bulk_meta_kernel", "tick_kernel", "bootstrap_kernel",
               "fill_slabs_kernel", "sum_committed_kernel", "traffic_kernel", "unpack_kernel", "pack_kernel",
               "plan_kernel", "scan_reduce_kernel", "scan_blocks_kernel", "scan_apply_kernel", "bounds_kernel",
               "apply_count_kernel", "apply_gather_kernel", "apply_total_kernel", "pool_kernel"):
@@ -35,11 +36,17 @@ def short(name):
     return name[:60]
 
 
-TICK_KERNELS = ("control_kernel", "bulk_kernel", "pool_kernel")
+TICK_KERNELS = ("control_kernel", "control_fast_kernel", "control_fastfb_kernel", "control_slow_kernel",
+                "bulk_kernel", "bulk_small_kernel", "pool_kernel")
+# SKIP_HEAD=h (the bench's bring-up ticks + warm-up): the timed window is the last_n tick launches
+# after the first h (more robust than counting the launches of the runs after the timed region)
+HEAD = int(os.environ["SKIP_HEAD"]) if os.environ.get("SKIP_HEAD") else None
 
 
 def window(k, xs, last_n, skip):
-    """The last_n values before the skipped tail (tick kernels only)."""
+    """The last_n values before the skipped tail (tick kernels only), or after the first SKIP_HEAD."""
+    if HEAD is not None and k in TICK_KERNELS:
+        return xs[HEAD:HEAD + last_n]
     s = skip if k in TICK_KERNELS else 0
     return xs[max(len(xs) - last_n - s, 0):len(xs) - s]
 
