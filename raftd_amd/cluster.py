@@ -351,6 +351,10 @@ class DistEngine(_Feeds):
                                         else [self.stream] * (len(engs) - 1))
         for e, st in zip(engs, self.streams):
             e.set_stream(st.cuda_stream)
+        if exchange == "torch" and dist.get_backend(group) == "nccl":
+            # the exchange is a batch of point-to-point sends and receives (p2p_regions); NCCL wants the
+            # communicator made by a collective of the whole group first
+            dist.barrier(group=group)
         if exchange == "c":
             from .engine import rccl_close, rccl_transport, rccl_unique_id
             if dist.get_backend(group) == "nccl":

@@ -144,7 +144,8 @@ struct Ctl {
   // payload stream: hw = next free chunk. The lowest page held (S_LPG, the capacity
   // rule's base, unchanged during a step) is read where an append needs it
   uint32_t hw;
-  uint32_t lpg_;  // S_LPG at step start (read with the state; the capacity rule's base)
+  uint32_t lpg_;   // S_LPG at step start (read with the state; the capacity rule's base)
+  uint32_t nlpg_;  // S_NLPG out: pages below it are released after this step (pool_kernel)
   // RG_CTL_FASTREP (see the top of this file). The leader's last append
   // of this step when it wrote no protected index: entries
   // [la_base, la_base + la_n) all hold the ring word la_word (bank 0) and term(la_base − 1) = la_pt,
@@ -215,7 +216,8 @@ struct Ctl {
         }
         nlpg = vpn_of(bound);
       }
-      p.s32_out[S_NLPG * n + q] = nlpg;  // for pool_kernel, after this launch
+      nlpg_ = nlpg;  // for pool_kernel, stored with the state (no store before the inbox: the step's
+                     // loads up to its first message can all be in flight together)
     }
 #ifdef RG_CTL_FASTREP
     la_base = la_word = la_pt = 0; la_n = 0; la_pos = 0;
@@ -1483,6 +1485,7 @@ struct Ctl {
     b[S_ACTIVE * n] = active; b[S_ERR * n] = err; b[S_DROPS * n] = drops;
     b[S_MEMBERS * n] = members; b[S_SNAP_MEMBERS * n] = snap_members; b[S_CC_PENDING * n] = cc_pending;
     b[S_HW * n] = hw;  // S_LPG / S_APG: pool_kernel (after this launch)
+    b[S_NLPG * n] = nlpg_;
     sfor<0, R>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       p.rem_out[(0 * R + j) * n + q] = rm[j];
