@@ -106,6 +106,48 @@ def _transport_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def _p2p_worker(rank, world, port, q):
+    """p2p_regions (the fixed-capacity exchange's transfer): every link's size is known to both of its
+    ends without asking (here a formula of the pair), and regions move in pieces of at most 1,000 B."""
+    from raftd_amd.cluster import p2p_regions
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        size = lambda a, b: 0 if (a + b) % 4 == 3 else (a * 997 + b * 613) % 2900 + 1  # noqa: E731
+        sizes = [size(rank, r) for r in range(world)]
+        rsizes = [size(a, rank) for a in range(world)]
+        offs, tot = _offsets(sizes)
+        send = torch.empty(tot + 9, dtype=torch.uint8)
+        for r in range(world):
+            i = torch.arange(sizes[r])
+            send[offs[r]:offs[r] + sizes[r]] = ((rank * 31 + r * 7 + i) % 251).to(torch.uint8)
+        roffs, rtot = _offsets(rsizes)
+        recv = torch.zeros(rtot + 3, dtype=torch.uint8)
+        p2p_regions(send, sizes, recv, rsizes, chunk=1000)
+        ok = True
+        for a in range(world):
+            i = torch.arange(rsizes[a])
+            want = ((a * 31 + rank * 7 + i) % 251).to(torch.uint8)
+            ok &= bool(torch.equal(recv[roffs[a]:roffs[a] + rsizes[a]], want))
+        q.put((rank, ok, rsizes))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_p2p_regions_gloo_world3():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_p2p_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok, _ in res), res
+
+
 def test_transport_gloo_world2():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
