@@ -117,8 +117,12 @@ using CTickParams = RG_CONST(const TickParams);
 // ROLE (FAST only): -1 = any role; LEADER / FOLLOWER = the role-sorted fast launches (control_fast_kernel):
 // the lane's role is that compile-time constant for the whole step (the fast path never changes a role:
 // every transition aborts), so the other roles' branches compile away.
-template <int R, bool FAST = false, int ROLE = -1>
+// LAT (FAST only): the latency build for small engines (control_fastfb_kernel, the resident kernel:
+// a wave or less per SIMD, registers to spare) loads every field with the state up front instead of
+// copying the cold ones through at the end (one round trip fewer on the step's critical path).
+template <int R, bool FAST = false, int ROLE = -1, bool LAT = false>
 struct Ctl {
+  static constexpr bool LEAN = FAST && !LAT;  // cold fields copied through at the end (register-lean)
   // the tick's parameter block, read in place at each use (a device slot the host filled): the
   // fields are reloaded where needed instead of living in registers for the whole step (r02 kept a
   // 368-B copy, 279 SGPR spills at R = 3)
@@ -176,7 +180,7 @@ struct Ctl {
     role = b[S_ROLE * n]; etick = b[S_ETICK * n]; htick = b[S_HTICK * n]; rand_to = b[S_RAND_TO * n];
     active = b[S_ACTIVE * n]; drops = b[S_DROPS * n]; members = b[S_MEMBERS * n];
     hw = b[S_HW * n];
-    if constexpr (!FAST) {  // FAST: copied through by store() (no branch of the fast path reads them)
+    if constexpr (!LEAN) {  // LEAN: copied through by store() (no branch of the fast path reads them)
       vote = a[S_VOTE * n]; applied = a[S_APPLIED * n]; snap_index = a[S_SNAP_INDEX * n];
       snap_term = a[S_SNAP_TERM * n]; processed = a[S_PROCESSED * n]; cc_hi = a[S_CC_HI * n];
       rng_ctr = b[S_RNG_CTR * n]; granted = b[S_GRANTED * n]; responded = b[S_RESPONDED * n];
@@ -189,7 +193,7 @@ struct Ctl {
       constexpr int j = decltype(jc)::value;
       rm[j] = p.rem_in[(0 * R + j) * n + q];
       rn[j] = p.rem_in[(1 * R + j) * n + q];
-      if constexpr (FAST) rs[0] = 0;  // FAST: copied through by store()
+      if constexpr (LEAN) rs[0] = 0;  // LEAN: copied through by store()
       else if constexpr (RS_MEM) p.rem_out[(2 * R + j) * n + q] = p.rem_in[(2 * R + j) * n + q];
       else rs[j] = p.rem_in[(2 * R + j) * n + q];
       rt[j] = p.rst_in[j * n + q];
@@ -1401,7 +1405,7 @@ struct Ctl {
     }
     if (in_rd) handle_read_index(my_id(), in_rd);  // 4b: ReadIndex input (rg_read_index)
     RG_STAMP(3);
-    if constexpr (FAST) {
+    if constexpr (LEAN) {
       // the fields only the end of the step reads, loaded here (after a compiler barrier, so their
       // loads are not hoisted to the start of the step and their registers are not held through it)
 #if defined(__HIP_DEVICE_COMPILE__) || defined(__GNUC__)
@@ -1454,7 +1458,7 @@ struct Ctl {
   }
 
   RG_FN void store() {
-    if constexpr (FAST) {  // the fields no fast branch changes: copied through from the step's input state
+    if constexpr (LEAN) {  // the fields no fast branch changes: copied through from the step's input state
       const uint64_t n = p.nrep;
       const uint64_t* ai = p.s64_in + q;
       const uint32_t* bi = p.s32_in + q;
@@ -1490,7 +1494,7 @@ struct Ctl {
       constexpr int j = decltype(jc)::value;
       p.rem_out[(0 * R + j) * n + q] = rm[j];
       p.rem_out[(1 * R + j) * n + q] = rn[j];
-      if constexpr (!RS_MEM && !FAST) p.rem_out[(2 * R + j) * n + q] = rs[j];
+      if constexpr (!RS_MEM && !LEAN) p.rem_out[(2 * R + j) * n + q] = rs[j];
       p.rst_out[j * n + q] = (uint8_t)rt[j];
       p.cnt_out[((uint64_t)s * R + j) * p.G + g] = get8(oc, j);
     });

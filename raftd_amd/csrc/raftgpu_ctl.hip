@@ -80,26 +80,27 @@ __global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_MINWAVES) control_kernel(
 // step: the two are separate branches, so the kernel holds the larger role's live values instead of
 // both roles' at once (r04: 204 -> 168 VGPRs at R = 3, three waves per SIMD). In steady state a wave's
 // lanes share a role (slot-major lanes, one leader slot per group) and run one branch.
-// one replica's fast step (its role's instantiation); returns whether it left the fast path
-template <int R>
+// one replica's fast step (its role's instantiation); returns whether it left the fast path. LAT: the
+// latency build of small engines (every field loaded up front, Ctl's LAT)
+template <int R, bool LAT = false>
 __device__ __forceinline__ bool fast_step(CTickParams& cp, uint32_t q) {
   if (cp.s32_in[(uint64_t)S_ROLE * cp.nrep + q] == LEADER) {
 #ifdef RG_CTL_PROFILE
     const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memtime();
-    Ctl<R, true, LEADER> c(cp, q);
+    Ctl<R, true, LEADER, LAT> c(cp, q);
     c.stamps[0] = t0;
 #else
-    Ctl<R, true, LEADER> c(cp, q);
+    Ctl<R, true, LEADER, LAT> c(cp, q);
 #endif
     c.run();
     return c.aborted;
   }
 #ifdef RG_CTL_PROFILE
   const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memtime();
-  Ctl<R, true, FOLLOWER> c(cp, q);
+  Ctl<R, true, FOLLOWER, LAT> c(cp, q);
   c.stamps[0] = t0;
 #else
-  Ctl<R, true, FOLLOWER> c(cp, q);
+  Ctl<R, true, FOLLOWER, LAT> c(cp, q);
 #endif
   c.run();
   return c.aborted;
@@ -137,7 +138,7 @@ __global__ void __launch_bounds__(RG_CTL_BLOCK, 1) control_fastfb_kernel(const T
   CTickParams& cp = *(CTickParams*)pp;
   if (q == 0) cp.slow_cnt[(cp.tick + 1) & 1] = 0;
   if (q >= cp.nrep) return;
-  const bool aborted = fast_step<R>(cp, q);
+  const bool aborted = fast_step<R, true>(cp, q);
   count_slow(cp, aborted);
   if (aborted) {  // the fast step stored nothing: the full step from the same inputs
     Ctl<R> c(cp, q);
@@ -198,7 +199,7 @@ __global__ void __launch_bounds__(64 * R, 1) control_resident_kernel(const TickP
   const uint32_t q = w * G + g;
   for (uint32_t i = 0; i < k; ++i) {
     if (g < G) {
-      if (fast_step<R>(cp[i], q)) {  // left the fast path (stored nothing): the full step
+      if (fast_step<R, true>(cp[i], q)) {  // left the fast path (stored nothing): the full step
         Ctl<R> c(cp[i], q);
         c.run();
       }
