@@ -30,9 +30,9 @@ def make(kind: str, **cfg):
     if kind == "gpu":
         from raftd_amd.engine import Engine
         return Engine(**cfg)
-    if kind in ("ctl", "ctl-asan", "ctl-fast", "ctl-fast-asan"):
+    if kind in ("ctl", "ctl-asan", "ctl-fast", "ctl-fast-asan", "ctl-fastlat", "ctl-fastlat-asan"):
         from native.ctl_host import CtlHost
-        return CtlHost(asan=kind.endswith("asan"), fast="fast" in kind, **cfg)
+        return CtlHost(asan=kind.endswith("asan"), fast=2 if "fastlat" in kind else 1 if "fast" in kind else 0, **cfg)
     raise ValueError(kind)
 
 

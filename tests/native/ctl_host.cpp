@@ -175,6 +175,23 @@ static void after_step(Host* h, const TickParams& p) {
     }
   }
 }
+// the product's fast step (control_fast_kernel / control_fastfb_kernel): the role-specialised Ctl,
+// lean (fast mode 1, the large-engine kernel) or the latency build (fast mode 2, small engines)
+extern "C++" {
+template <int R, int ROLE, bool LAT>
+static bool fast_role(const TickParams& p, uint32_t q) {
+  Ctl<R, true, ROLE, LAT> f(p, q);
+  f.run();
+  return f.aborted;
+}
+template <int R, class H>
+static bool fast_step(H* h, const TickParams& p, uint32_t q) {
+  const bool lead = p.s32_in[(uint64_t)S_ROLE * p.nrep + q] == LEADER;
+  if (h->fast == 2) return lead ? fast_role<R, LEADER, true>(p, q) : fast_role<R, FOLLOWER, true>(p, q);
+  return lead ? fast_role<R, LEADER, false>(p, q) : fast_role<R, FOLLOWER, false>(p, q);
+}
+}  // extern "C++"
+
 
 int ch_tick(void* hh, const rg_tick_input* in) {
   Host* h = (Host*)hh;
@@ -199,9 +216,7 @@ int ch_tick(void* hh, const rg_tick_input* in) {
   case r: {                        \
     bool full = true;              \
     if (h->fast) {                 \
-      Ctl<r, true> f(p, q);        \
-      f.run();                     \
-      full = f.aborted;            \
+      full = fast_step<r>(h, p, q); \
       h->slow_lanes += full;       \
     }                              \
     if (full) {                    \

@@ -35,7 +35,9 @@ def build(asan: bool = False) -> str:
 
 
 class CtlHost:
-    def __init__(self, asan: bool = False, fast: bool = False, **cfg):
+    def __init__(self, asan: bool = False, fast: int = 0, **cfg):
+        """fast: 0 the full step; 1 the fast step first (role-specialised, as control_fast_kernel), the
+        full step for a lane it hands off; 2 the same with the small-engine latency build (LAT)."""
         from raftd_amd.engine import Config, MsgView, ReplicaView, default_config  # struct layouts only
         self._MsgView, self._ReplicaView = MsgView, ReplicaView
         self.cfg = default_config(**cfg)
@@ -52,7 +54,7 @@ class CtlHost:
         self.L.ch_set_fast.argtypes = [vp, C.c_int]
         self.L.ch_slow_lanes.argtypes = [vp]
         self.L.ch_slow_lanes.restype = C.c_uint64
-        self.L.ch_set_fast(C.c_void_p(self.h), 1 if fast else 0)
+        self.L.ch_set_fast(C.c_void_p(self.h), int(fast))
         self.G, self.R = self.cfg["groups"], self.cfg["replicas"]
         self.nrep = self.G * self.R
 

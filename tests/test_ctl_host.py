@@ -64,6 +64,13 @@ def test_fast_path_matches_oracle(R):
     xcheck("ctl-fast", 30 + R, G=5, R=R, T=120)
 
 
+@pytest.mark.parametrize("R", [1, 3, 5])
+def test_fast_path_latency_build_matches_oracle(R):
+    """The small-engine latency build of the fast step (Ctl<R, true, role, LAT = true>: every field
+    loaded up front; control_fastfb_kernel and the resident kernel) against the oracle."""
+    xcheck("ctl-fastlat", 50 + R, G=5, R=R, T=120)
+
+
 def test_fast_path_membership_and_heavy_loss():
     xcheck("ctl-fast", 88, G=6, R=5, T=160, drop_ppm=300000, max_msgs_per_pair=4, p_cc=0.05)
 
