@@ -225,9 +225,10 @@ hipError_t launch_pool(const PoolParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-__global__ void pool_reset_kernel(uint32_t* fring, uint64_t npages, PoolCtl* ctl) {
+__global__ void pool_reset_kernel(uint32_t* fring, uint64_t npages, PoolCtl* ctl, uint64_t mul) {
+  // the ring starts as the permutation i -> i * mul mod npages (mul coprime to npages)
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < npages; i += (uint64_t)gridDim.x * blockDim.x)
-    fring[i] = (uint32_t)i;
+    fring[i] = (uint32_t)(mul > 1 ? (i * mul) % npages : i);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     ctl->head = 0;
     ctl->tail = ctl->limit = npages;
@@ -237,7 +238,22 @@ __global__ void pool_reset_kernel(uint32_t* fring, uint64_t npages, PoolCtl* ctl
 }
 
 hipError_t launch_pool_reset(uint32_t* fring, uint64_t npages, PoolCtl* ctl, hipStream_t s) {
-  hipLaunchKernelGGL(pool_reset_kernel, dim3(1024), dim3(256), 0, s, fring, npages, ctl);
+  // The ring starts as the permutation i -> i * 1000003 mod npages (a prime multiplier: a bijection
+  // unless it divides npages), so the pages consecutive replicas take lie ~4 GB apart instead of side
+  // by side: the first snapshot window's payload stage ran 3 % faster so (r04v, per-tick kernel
+  // trace). RAFTGPU_POOL_PERM=<m> overrides the multiplier (1 = the identity, A/B).
+  uint64_t mul = npages % 1000003ull ? 1000003ull : 1000033ull;
+  if (const char* v = getenv("RAFTGPU_POOL_PERM")) mul = strtoull(v, nullptr, 10);
+  {
+    uint64_t a = mul, b = npages;
+    while (b) {
+      const uint64_t t = a % b;
+      a = b;
+      b = t;
+    }
+    if (mul == 0 || a != 1) mul = 1;  // not coprime: the identity
+  }
+  hipLaunchKernelGGL(pool_reset_kernel, dim3(1024), dim3(256), 0, s, fring, npages, ctl, mul);
   return hipGetLastError();
 }
 
