@@ -846,7 +846,8 @@ hipError_t launch_bulk_t<(bool)RG_BULK_W, (bool)RG_BULK_MJ>(const BulkParams& p,
   }
 #endif
   return with_bulk_w<(bool)RG_BULK_W, (bool)RG_BULK_MJ>(p.P, [&](auto k) {
-    hipLaunchKernelGGL(k, dim3(grid), dim3(256), bulk_lds_bytes(p.P), s, p, pt);
+    const uint32_t wg = p.wg_waves >= 1 && p.wg_waves <= 4 ? p.wg_waves : 4u;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(64 * wg), bulk_lds_bytes(p.P), s, p, pt);
     return hipGetLastError();
   });
 }

@@ -186,7 +186,8 @@ struct rg_engine {
   // batches carry at most 16 entries (max_entries_per_msg), jobs are small; the 64-entry jobs of
   // full batches run faster without it. RAFTGPU_BULK_MULTIJOB=0/1 overrides (A/B).
   bool bulk_mj = false;
-  bool bulk_small = true;  // MJ engines: bulk_small_kernel takes the small jobs first (RAFTGPU_BULK_SMALL=0: off)
+  bool bulk_small = true;
+  uint32_t bulk_wg = 4;  // waves per bulk workgroup  // MJ engines: bulk_small_kernel takes the small jobs first (RAFTGPU_BULK_SMALL=0: off)
   uint64_t bytes = 0;
   std::vector<void*> allocs;
   // per-launch event timing (rg_timing): bit 0 control_kernel, bit 1 bulk_kernel; a start/end
@@ -438,6 +439,7 @@ static BulkParams bulk_params_at(rg_engine* e, uint64_t tk) {
   b.nslab = e->c.num_slabs;
   b.multijob = e->bulk_mj ? 1u : 0u;
   b.small = e->bulk_mj && e->bulk_small ? 1u : 0u;
+  b.wg_waves = e->bulk_wg;
   return b;
 }
 
@@ -731,7 +733,14 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
     return fail(RG_EHIP, "page pool reset");
   }
   const uint64_t ntiles = (n + tile - 1) / tile;
-  e->bulk_grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((ntiles + 3) / 4, (uint64_t)std::max(cus, 1) * per_cu));
+  // waves per bulk workgroup (RAFTGPU_BULK_WG, A/B): the tiles of one group block's R slots are
+  // consecutive, so a workgroup of R waves keeps a block's two followers — which read the same
+  // leader entries — on one CU and one XCD's L2
+  e->bulk_wg = 4;
+  if (const char* v = getenv("RAFTGPU_BULK_WG")) e->bulk_wg = std::min(4, std::max(1, atoi(v)));
+  const uint64_t wgw = e->bulk_wg;
+  e->bulk_grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((ntiles + wgw - 1) / wgw,
+                                                               (uint64_t)std::max(cus, 1) * per_cu * 4 / wgw));
   if (const char* gv = getenv("RAFTGPU_BULK_GRID")) {  // measurement override (blocks)
     const int gb = atoi(gv);
     if (gb > 0) e->bulk_grid = gb;

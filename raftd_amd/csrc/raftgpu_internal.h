@@ -286,6 +286,7 @@ struct BulkParams {
   uint32_t nslab;
   uint32_t multijob;     // small jobs share a ring pass (bulk_kernel<.., MJ>; the engine's choice)
   uint32_t small;        // bulk_small_kernel ran first: bulk_kernel skips the replicas it took (small_job)
+  uint32_t wg_waves;     // waves per bulk_kernel workgroup (1..4)
 };
 
 // pool_kernel (after control, before bulk): frees the stream pages control released, allocates the
