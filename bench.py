@@ -67,6 +67,9 @@ def parse():
                     "itself in a one-rank process group): a rehearsal of the multi-GPU step on one GPU")
     ap.add_argument("--halves", type=int, default=2, help="N > 1 spread: engines per rank over disjoint column "
                     "ranges; 2 pipelines one half's all-to-all behind the other half's tick (1 = no overlap)")
+    ap.add_argument("--sizing", choices=["exact", "fixed"], default=None,
+                    help="N > 1, exchange torch: region sizing (default: exact when Cmds travel, fixed for "
+                         "metadata-only engines; DESIGN.md §6)")
     ap.add_argument("--exchange", choices=["torch", "c"], default="torch", help="N > 1 spread: move the regions "
                     "with torch.distributed from Python (default) or with the library's rg_wire_exchange (built-in "
                     "RCCL transport on nccl; each half on its own stream)")
@@ -442,6 +445,7 @@ def main():
     wire = None
     if spread:  # one cluster of world x G groups, replicas spread over the GPUs
         wire = DistEngine(groups=G, halves=args.halves, seed=0x5EED, wire_all=1 if rehearse else 0,
+                          fixed=None if args.sizing is None else args.sizing == "fixed",
                           exchange=args.exchange, **common)
         host, eng = wire, wire.eng  # host: aggregates over the halves; eng: the first half
         Gt = G * world
@@ -653,8 +657,12 @@ def main():
             "mode": (f"pipelined over {args.halves} column halves: one half's all-to-all overlaps the other's "
                      "unpack + tick + pack" if pipelined else "serial: plan + pack + all-to-all + unpack, then tick"),
             "ms_per_step": x_ms if not pipelined else None,
-            "transport": ("rg_wire_exchange (C-ABI, built-in RCCL transport)" if spread and args.exchange == "c"
-                          else "torch.distributed all_to_all_single" if spread else "device copy (one engine)"),
+            "transport": ("rg_wire_exchange (C-ABI, built-in RCCL transport; fixed-capacity regions, one "
+                          "collective)" if spread and args.exchange == "c"
+                          else ("torch.distributed batch_isend_irecv of fixed-capacity regions (no host sync, no "
+                                "size exchange)" if wire.fixed else "torch.distributed all_to_all_single of "
+                                "exactly sized regions (plan host sync + size all-gather)") if spread
+                          else "device copy (one engine)"),
             "bytes_sent_per_step_max_rank": wire_max / K,
             "achieved_GBps_per_rank": ((wire_max / K) / (x_ms / 1e3) / 1e9 if x_ms > 0 else
                                        (wire_max / K) / (wall / K) / 1e9),

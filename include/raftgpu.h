@@ -379,9 +379,13 @@ int rg_wire_pack(rg_engine* e, void* send_buf, uint64_t send_cap);
 int rg_wire_recv(rg_engine* e, const void* recv_buf, const uint64_t* recv_bytes /*[ranks]*/);
 /* Messages dropped so far because their unit did not fit a fixed-capacity region. */
 int rg_wire_dropped(rg_engine* e, uint64_t* msgs);
-/* The whole exchange in one call and one collective: rg_wire_plan_fixed, pack into an engine-owned
- * send buffer, t->alltoallv into an engine-owned receive buffer, and rg_wire_recv — no host sync and
- * no size exchange. Every rank of the cluster calls it between the same two ticks. A host in any
+/* The whole exchange in one call: plan, pack into an engine-owned send buffer, t->alltoallv into an
+ * engine-owned receive buffer, and rg_wire_recv. Sizing: metadata-only engines (or a transport without
+ * allgather_u64) use rg_wire_plan_fixed — one collective, no host sync, no size exchange; engines whose
+ * messages carry Cmds use rg_wire_plan and exchange the sizes through t->allgather_u64, since their
+ * exchanges are bound by the bytes and a fixed capacity moves more of them;
+ * RAFTGPU_WIRE_SIZING=fixed|exact overrides. Every rank of the cluster calls it between the same two
+ * ticks (all with the same sizing). A host in any
  * language gets multi-GPU replication from this call plus a transport: the built-in RCCL one
  * (rg_rccl_open) or its own.
  * *sent_bytes (if not NULL) = the bytes this rank sent to other ranks. The transport's callbacks return 0 on success. alltoallv gets device buffers and the engine's
@@ -390,9 +394,9 @@ int rg_wire_dropped(rg_engine* e, uint64_t* msgs);
  * enqueue on `stream` itself, order a stream of its own by events both ways (the RCCL transport),
  * or synchronise `stream` and complete before returning (a host-staged transport). Region r of `send`
  * (send + soff[r], ssize[r] bytes) goes to rank r; region r of `recv`
- * (recv + roff[r], rsize[r] bytes) comes from rank r. allgather_u64 (optional; rg_wire_exchange no
- * longer calls it) is a host-memory, blocking all-gather of n values per rank: all[r * n + i] = value
- * i of rank r. */
+ * (recv + roff[r], rsize[r] bytes) comes from rank r. allgather_u64 (used by the exact sizing; may be
+ * NULL, which makes the sizing fixed) is a host-memory, blocking all-gather of n values per rank:
+ * all[r * n + i] = value i of rank r. */
 typedef struct rg_transport {
   void* user;
   int (*allgather_u64)(void* user, const uint64_t* mine, uint64_t* all, uint32_t n);

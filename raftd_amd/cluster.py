@@ -325,10 +325,14 @@ class DistEngine(_Feeds):
     tick that produced it. With two halves, step_device() pipelines: while one half's all-to-all
     is on the wire, the other half unpacks, ticks and packs."""
 
-    def __init__(self, groups: int, group=None, halves: int = 1, exchange: str = "torch", **cfg):
+    def __init__(self, groups: int, group=None, halves: int = 1, exchange: str = "torch", fixed=None, **cfg):
         """exchange: "torch" moves the regions with torch.distributed from Python; "c" with the
         library's rg_wire_exchange (RCCL transport on an nccl group, a host-staged one on gloo),
-        each half on a stream of its own so one half's transfer overlaps the other's tick."""
+        each half on a stream of its own so one half's transfer overlaps the other's tick.
+        fixed (torch exchange): size the regions with rg_wire_plan_fixed (no host sync, no size
+        exchange, a transfer moves each link's capacity) instead of rg_wire_plan (exact sizes after a
+        host sync and an all-gather). Default: fixed for metadata-only engines, whose exchanges are
+        latency-bound; exact when Cmds travel, whose exchanges are bound by the bytes."""
         import torch.distributed as dist
         torch = _torch()
         if groups % halves:
@@ -365,7 +369,10 @@ class DistEngine(_Feeds):
             else:
                 self._pyxt = gloo_transport(group, dev)
                 self.xt = self._pyxt.t
-        self.parts = [_Half(e, dev, self.pg, self.rank, self.xt) for e in engs]
+        if fixed is None:
+            fixed = engs[0].cfg["payload_bytes"] == 0
+        self.fixed = bool(fixed)
+        self.parts = [_Half(e, dev, self.pg, self.rank, self.xt, fixed=self.fixed) for e in engs]
         self.eng = engs[0]
         self.cfg, self.R = engs[0].cfg, engs[0].R
         self.async_ok = dist.get_backend(group) == "nccl"

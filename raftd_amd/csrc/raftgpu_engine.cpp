@@ -215,7 +215,7 @@ struct rg_engine {
   bool planned = false, wire_ready = false;
   // fixed-capacity exchange (rg_wire_plan_fixed): region bytes per peer, the same at
   // both ends of a link (the same rule over the same numbers), grown from the exchange two before
-  std::vector<uint64_t> cap_s, cap_r;
+  std::vector<uint64_t> cap_s, cap_r, cap_s0, cap_r0;  // capacities now, and the first ones (their floor)
   uint64_t* d_need = nullptr;  // [2][MAX_RANKS]: bytes each sent region asked for (pack), each received one (unpack)
   uint64_t* h_need = nullptr;  // pinned [4][2][MAX_RANKS], one slot per exchange
   hipEvent_t need_ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -2366,8 +2366,11 @@ int rg_wire_plan(rg_engine* e, uint64_t* send_bytes) {
 // Fixed-capacity regions. A link's region starts at the bytes its units could need
 // (K messages of E entries of max_cmd_bytes each, plus header and table), at most RAFTGPU_WIRE_CAP0
 // (64 MiB) and never more than WIRE_CAP_MAX (4 GiB; transports move a region in pieces of at most
-// 256 MiB); it doubles past any need above half of it. Both ends apply that rule to the same numbers — the sender to its plan, the
-// receiver to the region header it got — two exchanges late, so neither waits for the other.
+// 256 MiB). A transfer moves the whole capacity, so the capacity follows the need closely: 1/16 +
+// 64 KiB above it, grown once a need passes 15/16 of it, shrunk once a need is below half of it, never
+// below the first capacity (a link whose worst case fits it never drops). Both ends apply the rule to
+// the same numbers — the sender to its plan, the receiver to the region header it got — two exchanges
+// late, so neither waits for the other.
 static constexpr uint64_t WIRE_CAP_MAX = 4ull << 30;
 static void wire_caps_init(rg_engine* e) {
   const uint32_t N = e->pl.N;
@@ -2386,9 +2389,23 @@ static void wire_caps_init(rg_engine* e) {
     e->cap_s[r] = first(e->h_ubeg[r + 1] - e->h_ubeg[r]);
     e->cap_r[r] = first(e->h_rbeg[r + 1] - e->h_rbeg[r]);
   }
+  e->cap_s0 = e->cap_s;
+  e->cap_r0 = e->cap_r;
 }
-static void wire_cap_grow(uint64_t& cap, uint64_t need) {
-  if (cap && need > cap / 2) cap = std::min<uint64_t>(WIRE_CAP_MAX, std::max<uint64_t>(cap, ((2 * need) + (1ull << 20) - 1) & ~((1ull << 20) - 1)));
+static void wire_cap_adapt(uint64_t& cap, uint64_t floor, uint64_t need) {
+  if (!cap) return;
+  const uint64_t chunk = 64ull << 10;
+  const uint64_t want = std::min<uint64_t>(WIRE_CAP_MAX, (need + need / 16 + 2 * chunk - 1) & ~(chunk - 1));
+  // A region that dropped units gets half its need again: the drops make catch-up traffic that
+  // grows the need further, and a capacity trailing it by 1/16 kept dropping (rehearsal, warm-up 5:
+  // 6,740 messages lost and 101 ms per step, profiles/r04z).
+  if (need > cap) cap = std::max<uint64_t>(cap, std::min<uint64_t>(WIRE_CAP_MAX, (need + need / 2 + chunk - 1) & ~(chunk - 1)));
+  else if (need > cap - cap / 16) cap = std::max<uint64_t>(cap, want);
+  // Shrinks by at most 1/8 per exchange: the need swings from tick to tick (heartbeat ticks, catch-up
+  // bursts), and cutting the capacity to one quiet tick's need dropped the next busy tick's units
+  // (overflow test: drops until tick 28 of 40).
+  else if (need < cap / 2)
+    cap = std::max<uint64_t>(floor, std::min<uint64_t>(cap, std::max<uint64_t>(want, (cap - cap / 8) & ~(chunk - 1))));
 }
 
 int rg_wire_plan_fixed(rg_engine* e, uint64_t* send_bytes, uint64_t* recv_bytes) {
@@ -2406,8 +2423,8 @@ int rg_wire_plan_fixed(rg_engine* e, uint64_t* send_bytes, uint64_t* recv_bytes)
     HIPCHK(hipEventSynchronize(e->need_ev[sl]));
     const uint64_t* hn = e->h_need + (uint64_t)sl * 2 * MAX_RANKS;
     for (uint32_t r = 0; r < N; ++r) {
-      wire_cap_grow(e->cap_s[r], hn[r]);
-      wire_cap_grow(e->cap_r[r], hn[MAX_RANKS + r]);
+      wire_cap_adapt(e->cap_s[r], e->cap_s0[r], hn[r]);
+      wire_cap_adapt(e->cap_r[r], e->cap_r0[r], hn[MAX_RANKS + r]);
     }
   }
   LAUNCH(launch_wire_plan(wire_params(e), e->bounds, e->stream), e->stream, "wire plan");
@@ -2538,11 +2555,31 @@ int rg_wire_exchange(rg_engine* e, const rg_transport* t, uint64_t* sent_bytes) 
   if (!e || !t || !t->alltoallv) return fail(RG_EINVAL, "rg_wire_exchange args");
   if (sent_bytes) *sent_bytes = 0;
   if (!e->wire) return RG_OK;
-  // one collective: fixed-capacity regions both ends already agree on (rg_wire_plan_fixed), the
-  // plan's true sizes in-band; no host sync and no size exchange
+  // Sizing: fixed capacities — one collective, no host sync — for metadata-only
+  // engines, whose exchanges are latency-bound; exact sizes (the plan's host sync and a size all-gather
+  // through the transport, then a transfer of exactly the planned bytes) when Cmds travel, where the
+  // bytes bound the exchange (r04 rehearsal at 64K x 3: 4.14 ms per step exact, 4.38 ms fixed).
+  // RAFTGPU_WIRE_SIZING=fixed|exact overrides; without allgather_u64 the sizing is fixed.
+  bool fixed = !e->c.payload_bytes || !t->allgather_u64;
+  if (const char* v = getenv("RAFTGPU_WIRE_SIZING")) {
+    if (!strcmp(v, "fixed")) fixed = true;
+    else if (!strcmp(v, "exact") && t->allgather_u64) fixed = false;
+  }
   const uint32_t N = e->pl.N, me = e->pl.rank;
   std::vector<uint64_t> ssize(N), soff(N), rsize(N), roff(N);
-  RGCHK(rg_wire_plan_fixed(e, ssize.data(), rsize.data()));
+  if (fixed) {
+    RGCHK(rg_wire_plan_fixed(e, ssize.data(), rsize.data()));
+  } else {
+    std::vector<uint64_t> all((uint64_t)N * N);
+    RGCHK(rg_wire_plan(e, ssize.data()));
+    if (t->allgather_u64(t->user, ssize.data(), all.data(), N) != 0)
+      return fail(RG_EHIP, "rg_wire_exchange: transport allgather_u64 failed");
+    for (uint32_t r = 0; r < N; ++r) {
+      if (all[(uint64_t)me * N + r] != ssize[r])
+        return fail(RG_EINVAL, "rg_wire_exchange: allgather returned another rank's sizes");
+      rsize[r] = all[(uint64_t)r * N + me];
+    }
+  }
   uint64_t st = 0, rt = 0;
   for (uint32_t r = 0; r < N; ++r) {
     soff[r] = st;

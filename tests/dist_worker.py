@@ -55,7 +55,8 @@ def worker(rank, n, halves, backend, exchange="torch"):
         dist.init_process_group("gloo", rank=rank, world_size=n)
     from raftd_amd.cluster import DistEngine
     extra = dict(wire_all=1) if n == 1 else {}
-    de = DistEngine(groups=G_LOCAL * halves, halves=halves, device=0, exchange=exchange, **CFG, **extra)
+    fixed = {"1": True, "0": False}.get(os.environ.get("DIST_FIXED", ""))  # sizing mode (None: the default)
+    de = DistEngine(groups=G_LOCAL * halves, halves=halves, device=0, exchange=exchange, fixed=fixed, **CFG, **extra)
     if backend == "nccl":
         assert de.async_ok
     de.bootstrap()
