@@ -14,6 +14,7 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdint>
 #include <cstring>
 #include <string>
@@ -106,8 +107,18 @@ int alltoallv(void* user, const void* send, const uint64_t* soff, const uint64_t
   hipStream_t st = (hipStream_t)stream, xs = c->xs;
   if (hipSetDevice(c->device) != hipSuccess) return -1;
   if (hipEventRecord(c->ev_in, st) != hipSuccess || hipStreamWaitEvent(xs, c->ev_in, 0) != hipSuccess) return -1;
+  // the region to this rank itself is a device copy: RCCL's send/receive to self moved a grown
+  // fixed-capacity region at ~25 GB/s (146 ms per step, profiles/r04z_wire_sizing.txt)
+  // (RAFTGPU_RCCL_SELF=rccl sends it through RCCL too: the one-rank tests' way to run the grouped path)
+  const char* sv = getenv("RAFTGPU_RCCL_SELF");
+  const int me = sv && !strcmp(sv, "rccl") ? -1 : c->rank;
+  if (me >= 0 && ssize[me] != rsize[me]) return -1;
+  if (me >= 0 && ssize[me] && hipMemcpyAsync((uint8_t*)recv + roff[me], (const uint8_t*)send + soff[me], ssize[me],
+                                  hipMemcpyDeviceToDevice, xs) != hipSuccess)
+    return -1;
   uint64_t most = 0;
-  for (int r = 0; r < c->nranks; ++r) most = std::max(most, std::max(ssize[r], rsize[r]));
+  for (int r = 0; r < c->nranks; ++r)
+    if (r != me) most = std::max(most, std::max(ssize[r], rsize[r]));
   // piece k of every region in the k-th group; the two ends of a pair agree on its size, and
   // RCCL matches a pair's sends and receives in issue order, so ranks whose largest region is
   // smaller simply issue fewer groups
@@ -116,6 +127,7 @@ int alltoallv(void* user, const void* send, const uint64_t* soff, const uint64_t
     if (a->GroupStart() != 0) return -1;
     bool ok = true;  // a failed Send / Recv still closes the group, or every later call on the comm breaks
     for (int r = 0; r < c->nranks && ok; ++r) {
+      if (r == me) continue;
       const uint64_t o = k * CHUNK;
       if (ssize[r] > o &&
           a->Send((const uint8_t*)send + soff[r] + o, std::min(CHUNK, ssize[r] - o), ncclUint8, r, c->comm, xs) != 0)

@@ -278,10 +278,13 @@ def test_one_rank_rccl_c_exchange():
     _worker(["1", "2", "nccl", "c"], 29538)
 
 
-def test_c_exchange_one_engine_vs_oracle():
+@pytest.mark.parametrize("self_path", ["copy", "rccl"])
+def test_c_exchange_one_engine_vs_oracle(self_path, monkeypatch):
     """A bare engine (no torch.distributed) exchanging through the built-in RCCL transport at
-    world size 1, every plane through the wire: chaos ticks bit-exact against the oracle."""
+    world size 1, every plane through the wire: chaos ticks bit-exact against the oracle. The region
+    to the rank itself is a device copy, or (RAFTGPU_RCCL_SELF=rccl) a grouped RCCL send/receive."""
     from raftd_amd.engine import Engine, rccl_close, rccl_transport, rccl_unique_id
+    monkeypatch.setenv("RAFTGPU_RCCL_SELF", self_path)
     cfg = dict(groups=16, replicas=3, seed=91, **CHAOS)
     eng = Engine(wire_all=1, **cfg)
     ora = make("c", **cfg)
