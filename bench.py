@@ -664,7 +664,7 @@ def main():
                            == "fixed" else "exactly sized regions, plan host sync + size all-gather)")
                           if spread and args.exchange == "c"
                           else ("torch.distributed batch_isend_irecv of fixed-capacity regions (no host sync, no "
-                                "size exchange)" if wire.fixed else "torch.distributed all_to_all_single of "
+                                "size exchange)" if wire.fixed else "torch.distributed batch_isend_irecv of "
                                 "exactly sized regions (plan host sync + size all-gather)") if spread
                           else "device copy (one engine)"),
             "bytes_sent_per_step_max_rank": wire_max / K,

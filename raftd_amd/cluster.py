@@ -150,7 +150,7 @@ def all_to_all_bytes(send, send_sizes, recv, recv_sizes, group=None, async_op=Fa
 
 
 def p2p_regions(send, send_sizes, recv, recv_sizes, group=None, async_op=False, chunk=A2A_CHUNK):
-    """The fixed-capacity exchange's transfer: region r of `send` to rank r and region
+    """The exchange's transfer on nccl, fixed or exactly sized: region r of `send` to rank r and region
     r of `recv` from rank r as one batch of point-to-point sends and receives (one grouped RCCL call),
     each piece at most `chunk` bytes (the 1 GiB contract). A link's two ends agree on its size, so
     they cut it into the same pieces without any rank knowing the others' sizes (an all_to_all's
@@ -263,7 +263,7 @@ class _Half:
             rsizes, biggest = exchange_sizes(sizes, self.pg)
         _, rtot = _offsets(rsizes)
         self.recv.ensure(rtot)  # stream order: the tick that reads the old buffer runs before a reuse
-        if self.fixed and dist.get_backend(self.pg) == "nccl":
+        if dist.get_backend(self.pg) == "nccl":  # the region to this rank: a device copy, not RCCL
             self.work = p2p_regions(self.send.t, sizes, self.recv.t, rsizes, self.pg, async_op=async_op)
         else:
             self.work = all_to_all_bytes(self.send.t, sizes, self.recv.t, rsizes, self.pg, async_op=async_op,

@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 700 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu tests/test_gpu_cluster.py tests/test_nodehost.py > gpurun_out/r04zb_tests.log 2>&1 || { echo tests failed; tail -30 gpurun_out/r04zb_tests.log; exit 1; }
+tail -1 gpurun_out/r04zb_tests.log
+for w in 5 30; do for args in "--sizing exact" "--sizing fixed" "--exchange c --sizing exact"; do timeout -k 10 300 python bench.py --placement spread --wire-all --no-cpu-baseline --steps 10 --warmup $w $args > gpurun_out/r04zb_rehearse.json 2>&1 || { tail -5 gpurun_out/r04zb_rehearse.json; exit 1; }; python3 -c "
+import json; d=json.loads(open('gpurun_out/r04zb_rehearse.json').read().strip().splitlines()[-1]); x=d['exchange']; print('warmup $w $args', round(d['ms_per_step'],3), x['transport'][:80], 'drops', d['drops_total'])" | tee -a gpurun_out/r04zb_sizing.txt; done; done
