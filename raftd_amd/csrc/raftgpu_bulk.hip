@@ -1,6 +1,7 @@
 // raftgpu_bulk.hip — bulk_kernel: the payload stage (entry Cmd copy + CRC-32), one
 // (wire, multi-job) variant per translation unit: the build compiles this file four times
 // (-DRG_BULK_W=0/1 -DRG_BULK_MJ=0/1), each with the seven lane-group sizes.
+#include <cstdlib>
 #include <algorithm>
 #include <type_traits>
 
@@ -832,7 +833,12 @@ hipError_t launch_bulk_t<(bool)RG_BULK_W, (bool)RG_BULK_MJ>(const BulkParams& p,
   if (p.small) {  // the small jobs first, then bulk_kernel for the rest (it skips them)
     const uint32_t lg = (uint32_t)lg_of(p.P), nch = 1u << lg;
     const uint32_t tiles = ((p.G + 63) / 64) * p.R;
-    const int sg = (int)std::min<uint32_t>((tiles + 3) / 4, (uint32_t)grid * 2u);
+    static const uint32_t gmul = [] {  // RAFTGPU_SMALL_GRID: workgroups per bulk-grid slot (A/B)
+      const char* v = getenv("RAFTGPU_SMALL_GRID");
+      const long m = v ? strtol(v, nullptr, 10) : 2;
+      return (uint32_t)(m >= 1 && m <= 64 ? m : 2);
+    }();
+    const int sg = (int)std::min<uint32_t>((tiles + 3) / 4, (uint32_t)grid * gmul);
     const int lds = (int)((CRC_T_WORDS + CRC_N_WORDS + nch * CRC_SH_STRIDE) * 4 + 4 * 64 * SMALL_N);
     hipError_t r = hipErrorInvalidValue;
     switch (lg) {
