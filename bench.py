@@ -78,7 +78,79 @@ def parse():
                     "HBM-resident proposal slabs; reported beside the headline line as `ingest`")
     ap.add_argument("--backend", default="nccl", help="N > 1: nccl (RCCL, default) or gloo (rehearsal: several "
                     "ranks on one GPU with RAFTD_BENCH_DEVICE=0, regions staged through host memory)")
+    ap.add_argument("--dry-run", action="store_true", help="N > 1 launcher check: every rank joins the process "
+                    "group on the CPU (gloo), agrees on the world size and exits without touching a GPU")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` started as ONE process (N > 1, no WORLD_SIZE in the environment): start N
+    fresh child processes of this script, rank r on GPU r (with --backend gloo every rank on GPU 0: the
+    one-GPU rehearsal), rendezvous on 127.0.0.1. This parent makes no GPU call (torch.cuda.device_count
+    does not initialise the device on this image) and never execs: it forwards rank 0's JSON line and
+    exits non-zero if any rank fails (the others are then stopped). Under torch.distributed.run, the
+    driver's N > 1 launcher, every process is already a rank and this is not used."""
+    import signal
+    import subprocess
+    n = args.gpus
+    if not args.dry_run:
+        import torch
+        visible = torch.cuda.device_count()
+        if n > visible and args.backend != "gloo":
+            print(f"bench.py: --gpus {n} but {visible} GPU(s) visible; use --backend gloo to rehearse {n} ranks "
+                  f"on one GPU", file=sys.stderr)
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RAFTD_BENCH_CHILD="1")
+        if args.backend == "gloo" and not args.dry_run:
+            env["RAFTD_BENCH_DEVICE"] = env.get("RAFTD_BENCH_DEVICE", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else None, start_new_session=True))
+    import threading
+    chunks = []
+    reader = threading.Thread(target=lambda: chunks.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    rc = 0
+    while any(p.poll() is None for p in procs):
+        failed = [p for p in procs if p.returncode not in (None, 0)]
+        if failed:  # a failed rank leaves the others waiting in a collective forever: stop them
+            rc = failed[0].returncode
+            for p in procs:
+                if p.poll() is None:
+                    os.killpg(p.pid, signal.SIGTERM)
+            break
+        time.sleep(0.2)
+    for p in procs:
+        p.wait()
+        rc = rc or p.returncode
+    reader.join()
+    sys.stdout.write(b"".join(chunks).decode())
+    sys.stdout.flush()
+    return 1 if rc else 0
+
+
+def dry_run(args, rank, world):
+    """The launcher's check (CPU only): join a gloo group, agree on the world size, print the line rank 0
+    would carry, exit."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    t = torch.tensor([1.0])
+    dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "dry_run": True, "n_gpus": dist.get_world_size(),
+                          "ranks_agreeing": int(t.item()), "backend": args.backend}), flush=True)
+    dist.destroy_process_group()
 
 
 def bring_up(eng, tick, G, R):
@@ -411,8 +483,16 @@ def pmc_traffic(kernel="bulk_kernel", wire=False, spread=False):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+        sys.exit(2)
+    if args.dry_run:
+        dry_run(args, rank, world)
+        return
     local = int(os.environ.get("LOCAL_RANK", "0"))
     local = int(os.environ.get("RAFTD_BENCH_DEVICE", local))
     import torch
@@ -431,6 +511,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(args.backend)
+        world = dist.get_world_size()  # the world the collectives (RCCL with nccl) initialised with
     else:
         torch.cuda.set_device(local)
     from raftd_amd import Engine
@@ -602,6 +683,8 @@ def main():
         "value": group_steps,
         "unit": "group-steps/s",
         "n_gpus": world,
+        "backend": args.backend if dist else None,
+        "ranks_share_one_gpu": bool(dist) and world > 1 and "RAFTD_BENCH_DEVICE" in os.environ,
         "steps": K,
         "warmup": args.warmup,
         "ms_per_step": wall * 1e3 / K,

@@ -32,6 +32,7 @@ for what in ${STEPS:-smoke parity tests bench wire rehearse}; do
     rehearse8) step rehearse8 500 env RAFTD_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
                 --master-addr 127.0.0.1 --master-port 29613 bench.py --gpus 8 --backend gloo --groups 2048 \
                 --steps 4 --warmup 2 ;;
+    launch2) step launch2 600 python bench.py --gpus 2 --backend gloo --no-cpu-baseline --steps 5 --warmup 2 ;;
     rehearse1) step rehearse1 400 env RAFTD_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                 --master-addr 127.0.0.1 --master-port 29612 bench.py --gpus 2 --backend gloo --groups 8192 \
                 --steps 5 --warmup 2 --halves 1 ;;
