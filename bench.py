@@ -68,8 +68,8 @@ def parse():
     ap.add_argument("--halves", type=int, default=2, help="N > 1 spread: engines per rank over disjoint column "
                     "ranges; 2 pipelines one half's all-to-all behind the other half's tick (1 = no overlap)")
     ap.add_argument("--sizing", choices=["exact", "fixed"], default=None,
-                    help="spread placement, either exchange: region sizing (default: exact when Cmds travel, "
-                         "fixed for metadata-only engines; DESIGN.md §6)")
+                    help="spread placement, either exchange: region sizing (default fixed: the all-to-all is the "
+                         "tick's one collective; exact: a plan host sync and a size all-gather first; DESIGN.md §6)")
     ap.add_argument("--exchange", choices=["torch", "c"], default="torch", help="N > 1 spread: move the regions "
                     "with torch.distributed from Python (default) or with the library's rg_wire_exchange (built-in "
                     "RCCL transport on nccl; each half on its own stream)")
@@ -522,8 +522,6 @@ def main():
     spread = placement == "spread" and (world > 1 or rehearse)
     stream = torch.cuda.Stream()  # a real (non-null) stream: the engine launches on it, events time it
     torch.cuda.set_stream(stream)
-    if args.sizing is not None:  # --exchange c: rg_wire_exchange reads the sizing from the environment
-        os.environ["RAFTGPU_WIRE_SIZING"] = args.sizing
     common = dict(replicas=R, log_capacity=args.log_capacity, payload_bytes=P, max_entries_per_msg=E, device=local)
     wire = None
     if spread:  # one cluster of world x G groups, replicas spread over the GPUs
@@ -743,8 +741,8 @@ def main():
                      "unpack + tick + pack" if pipelined else "serial: plan + pack + all-to-all + unpack, then tick"),
             "ms_per_step": x_ms if not pipelined else None,
             "transport": ("rg_wire_exchange (C-ABI, built-in RCCL transport; " +
-                          ("fixed-capacity regions, one collective)" if (args.sizing or ("exact" if P else "fixed"))
-                           == "fixed" else "exactly sized regions, plan host sync + size all-gather)")
+                          ("fixed-capacity regions, one collective)" if wire.fixed
+                           else "exactly sized regions, plan host sync + size all-gather)")
                           if spread and args.exchange == "c"
                           else ("torch.distributed batch_isend_irecv of fixed-capacity regions (no host sync, no "
                                 "size exchange)" if wire.fixed else "torch.distributed batch_isend_irecv of "

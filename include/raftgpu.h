@@ -123,7 +123,9 @@ typedef struct rg_config {
   uint32_t join_slots;          /* slots started by StartOnDiskReplica(join = true) (raft_manager.go:
                                    134-144): empty log, term 0, not a member until a ConfigChange that
                                    adds them reaches them; 0 = none */
-  uint32_t _reserved;
+  uint32_t wire_exact;          /* rg_wire_exchange region sizing: 0 = fixed capacities (one collective per
+                                   tick, no host sync; the default), 1 = exact sizes (a plan host sync and
+                                   a size all-gather through the transport first) */
 } rg_config;
 
 typedef struct rg_replica_view {
@@ -364,15 +366,19 @@ int rg_last_tick_traffic(rg_engine* e, rg_traffic* out);
  * Two ways to size the regions:
  *   rg_wire_plan        exact: waits for the plan kernel and returns the bytes each region needs;
  *                       the transport then has to tell each rank what it receives (a size exchange).
- *   rg_wire_plan_fixed  fixed capacity, no wait: send_bytes / recv_bytes are capacities both ends of
- *                       every link already agree on (a rule over numbers both see), so
- *                       one all-to-all per tick moves the regions. A unit (one replica pair's
- *                       messages) that does not fit its region is dropped whole — the messages are
- *                       lost in transit, which Raft tolerates — and counted (rg_wire_dropped); the
- *                       capacities double past any need above half of them, two exchanges later.
- *                       They start at the most a region's units could need (K messages of E entries
- *                       of max_cmd_bytes each), capped at 64 MiB (RAFTGPU_WIRE_CAP0), so a cluster
- *                       whose worst case fits never drops. */
+ *   rg_wire_plan_fixed  fixed capacity: send_bytes / recv_bytes are capacities both ends of every
+ *                       link already agree on (a rule over numbers both see), so one
+ *                       all-to-all per tick moves the regions and nothing waits for the tick that
+ *                       made the messages. The rule reads the needs of the exchange two before this
+ *                       one: a bounded wait (an event two exchanges old; the host runs at most two
+ *                       exchanges ahead of the device). A unit (one replica pair's messages) that does
+ *                       not fit its region is dropped whole — the messages are lost in transit, which
+ *                       Raft tolerates — and counted (rg_wire_dropped). Capacities start at the most a
+ *                       steady tick can need (a full Replicate plus one header per unit, or the worst
+ *                       case of K messages when smaller; a link whose worst case fits never drops),
+ *                       then follow the largest need of the last 8 exchanges (+1/16): up at once past
+ *                       a need that overflowed, down by at most 1/8 per exchange. A region header whose
+ *                       need is impossible for its link fails the call (RG_EINVARIANT). */
 int rg_wire_plan(rg_engine* e, uint64_t* send_bytes /*[ranks]*/);
 int rg_wire_plan_fixed(rg_engine* e, uint64_t* send_bytes /*[ranks]*/, uint64_t* recv_bytes /*[ranks]*/);
 int rg_wire_pack(rg_engine* e, void* send_buf, uint64_t send_cap);
@@ -380,12 +386,10 @@ int rg_wire_recv(rg_engine* e, const void* recv_buf, const uint64_t* recv_bytes 
 /* Messages dropped so far because their unit did not fit a fixed-capacity region. */
 int rg_wire_dropped(rg_engine* e, uint64_t* msgs);
 /* The whole exchange in one call: plan, pack into an engine-owned send buffer, t->alltoallv into an
- * engine-owned receive buffer, and rg_wire_recv. Sizing: metadata-only engines (or a transport without
- * allgather_u64) use rg_wire_plan_fixed — one collective, no host sync, no size exchange; engines whose
- * messages carry Cmds use rg_wire_plan and exchange the sizes through t->allgather_u64, since their
- * exchanges are bound by the bytes and a fixed capacity moves more of them;
- * RAFTGPU_WIRE_SIZING=fixed|exact overrides. Every rank of the cluster calls it between the same two
- * ticks (all with the same sizing). A host in any
+ * engine-owned receive buffer, and rg_wire_recv. Sizing: rg_wire_plan_fixed — the tick's one
+ * collective, no host sync, no size exchange — unless rg_config.wire_exact is set and the transport has
+ * allgather_u64: then rg_wire_plan, and the sizes go through t->allgather_u64 first. Every rank of the
+ * cluster calls it between the same two ticks (all with the same sizing). A host in any
  * language gets multi-GPU replication from this call plus a transport: the built-in RCCL one
  * (rg_rccl_open) or its own.
  * *sent_bytes (if not NULL) = the bytes this rank sent to other ranks. The transport's callbacks return 0 on success. alltoallv gets device buffers and the engine's

@@ -329,10 +329,10 @@ class DistEngine(_Feeds):
         """exchange: "torch" moves the regions with torch.distributed from Python; "c" with the
         library's rg_wire_exchange (RCCL transport on an nccl group, a host-staged one on gloo),
         each half on a stream of its own so one half's transfer overlaps the other's tick.
-        fixed (torch exchange): size the regions with rg_wire_plan_fixed (no host sync, no size
-        exchange, a transfer moves each link's capacity) instead of rg_wire_plan (exact sizes after a
-        host sync and an all-gather). Default: fixed for metadata-only engines, whose exchanges are
-        latency-bound; exact when Cmds travel, whose exchanges are bound by the bytes."""
+        fixed: size the regions with rg_wire_plan_fixed (no host sync, no size exchange: the all-to-all
+        is the tick's one collective; a transfer moves each link's capacity, which follows its need,
+        DESIGN.md §6) — the default — or, False, with rg_wire_plan (exact sizes after a host sync and a
+        size all-gather; on the C exchange through rg_config.wire_exact)."""
         import torch.distributed as dist
         torch = _torch()
         if groups % halves:
@@ -343,6 +343,8 @@ class DistEngine(_Feeds):
         self.N, self.rank = dist.get_world_size(group), dist.get_rank(group)
         hg = groups // halves
         self.cols = hg
+        self.fixed = True if fixed is None else bool(fixed)
+        cfg = dict(cfg, wire_exact=0 if self.fixed else 1)
         engs = [Engine(groups=hg, ranks=self.N, rank=self.rank, column_base=h * hg, **cfg) for h in range(halves)]
         torch.cuda.set_device(engs[0].cfg["device"])
         self.stream = torch.cuda.current_stream()
@@ -369,9 +371,6 @@ class DistEngine(_Feeds):
             else:
                 self._pyxt = gloo_transport(group, dev)
                 self.xt = self._pyxt.t
-        if fixed is None:
-            fixed = engs[0].cfg["payload_bytes"] == 0
-        self.fixed = bool(fixed)
         self.parts = [_Half(e, dev, self.pg, self.rank, self.xt, fixed=self.fixed) for e in engs]
         self.eng = engs[0]
         self.cfg, self.R = engs[0].cfg, engs[0].R

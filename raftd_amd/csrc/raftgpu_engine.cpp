@@ -215,7 +215,8 @@ struct rg_engine {
   bool planned = false, wire_ready = false;
   // fixed-capacity exchange (rg_wire_plan_fixed): region bytes per peer, the same at
   // both ends of a link (the same rule over the same numbers), grown from the exchange two before
-  std::vector<uint64_t> cap_s, cap_r, cap_s0, cap_r0;  // capacities now, and the first ones (their floor)
+  std::vector<uint64_t> cap_s, cap_r, cap_s0, cap_r0;  // capacities now, and their floors
+  std::vector<uint64_t> win_s, win_r;  // [N][WIRE_WIN] needs of the last exchanges, per link
   uint64_t* d_need = nullptr;  // [2][MAX_RANKS]: bytes each sent region asked for (pack), each received one (unpack)
   uint64_t* h_need = nullptr;  // pinned [4][2][MAX_RANKS], one slot per exchange
   hipEvent_t need_ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -2363,49 +2364,63 @@ int rg_wire_plan(rg_engine* e, uint64_t* send_bytes) {
   return RG_OK;
 }
 
-// Fixed-capacity regions. A link's region starts at the bytes its units could need
-// (K messages of E entries of max_cmd_bytes each, plus header and table), at most RAFTGPU_WIRE_CAP0
-// (64 MiB) and never more than WIRE_CAP_MAX (4 GiB; transports move a region in pieces of at most
-// 256 MiB). A transfer moves the whole capacity, so the capacity follows the need closely: 1/16 +
-// 64 KiB above it, grown once a need passes 15/16 of it, shrunk once a need is below half of it, never
-// below the first capacity (a link whose worst case fits it never drops). Both ends apply the rule to
-// the same numbers — the sender to its plan, the receiver to the region header it got — two exchanges
-// late, so neither waits for the other.
+// Fixed-capacity regions. A transfer moves a link's whole capacity, and no rank may
+// ask another what it needs, so each end of a link (a → b) computes the capacity by the same rule from
+// the same numbers: the bytes the link's region asked for in each exchange (the sender from its plan,
+// the receiver from the region's header), two exchanges late, so neither waits on the current tick.
+// * Start: the worst case (K messages of E entries of max_cmd_bytes per unit) when it is at most
+//   64 MiB — such a link never shrinks below it, so it never drops — else the most the units can need
+//   in a steady tick, a full Replicate plus one more header per unit (at least 64 MiB).
+// * Follow: 1/16 + 64 KiB above the largest need of the last WIRE_WIN exchanges; a need past the
+//   capacity (its units were dropped: lost in transit, counted) takes it to 1.5 × that need at once;
+//   a capacity above the target shrinks by at most 1/8 per exchange (bring-up's small needs do not
+//   undersize it before the load arrives, and a steady load settles 6 % above its need).
+// RAFTGPU_WIRE_CAP0 (tests) caps the start, to exercise the drop-and-grow path.
 static constexpr uint64_t WIRE_CAP_MAX = 4ull << 30;
+static constexpr uint32_t WIRE_WIN = 8;  // exchanges a capacity looks back over
+static constexpr uint64_t WIRE_CAP_SMALL = 64ull << 20;
 static void wire_caps_init(rg_engine* e) {
   const uint32_t N = e->pl.N;
-  uint64_t cap0 = 64ull << 20;
+  uint64_t cap0 = ~0ull;
   if (const char* v = getenv("RAFTGPU_WIRE_CAP0")) cap0 = std::max<uint64_t>(strtoull(v, nullptr, 10), 4096);
   const uint64_t msg = 64 + (uint64_t)e->c.max_entries_per_msg * (16 + (((uint64_t)e->maxc + 15) & ~15ull));
-  auto first = [&](uint64_t units) -> uint64_t {
+  auto first = [&](uint64_t units, uint64_t& floor) -> uint64_t {
+    floor = wire_region_min(units);
     if (!units) return 0;
     const long double worst = (long double)wire_region_min(units) + (long double)units * e->c.max_msgs_per_pair * msg;
-    const uint64_t c = worst > (long double)cap0 ? cap0 : (uint64_t)worst;
-    return std::min<uint64_t>(WIRE_CAP_MAX, (std::max<uint64_t>(c, wire_region_min(units)) + 255) & ~255ull);
+    const long double steady = (long double)wire_region_min(units) + (long double)units * (64 + msg);
+    // a link whose worst case is small keeps it (it never drops: every parity run); a larger one starts
+    // at the steady bound (C3 at N = 8: ~0.4 GB per link instead of K times that)
+    long double c = worst <= (long double)WIRE_CAP_SMALL ? worst
+                                                          : std::max((long double)WIRE_CAP_SMALL, std::min(worst, steady));
+    if (c > (long double)cap0) c = (long double)cap0;
+    if (c > (long double)WIRE_CAP_MAX) c = (long double)WIRE_CAP_MAX;
+    const uint64_t cap = (std::max<uint64_t>((uint64_t)c, wire_region_min(units)) + 255) & ~255ull;
+    if ((long double)cap >= worst) floor = cap;  // the worst case fits: never below it, never a drop
+    return cap;
   };
   e->cap_s.assign(N, 0);
   e->cap_r.assign(N, 0);
+  e->cap_s0.assign(N, 0);
+  e->cap_r0.assign(N, 0);
+  e->win_s.assign((uint64_t)N * WIRE_WIN, 0);
+  e->win_r.assign((uint64_t)N * WIRE_WIN, 0);
   for (uint32_t r = 0; r < N; ++r) {
-    e->cap_s[r] = first(e->h_ubeg[r + 1] - e->h_ubeg[r]);
-    e->cap_r[r] = first(e->h_rbeg[r + 1] - e->h_rbeg[r]);
+    e->cap_s[r] = first(e->h_ubeg[r + 1] - e->h_ubeg[r], e->cap_s0[r]);
+    e->cap_r[r] = first(e->h_rbeg[r + 1] - e->h_rbeg[r], e->cap_r0[r]);
   }
-  e->cap_s0 = e->cap_s;
-  e->cap_r0 = e->cap_r;
 }
-static void wire_cap_adapt(uint64_t& cap, uint64_t floor, uint64_t need) {
+// one exchange's need into the link's window (slot k of WIRE_WIN), then the capacity rule above
+static void wire_cap_adapt(uint64_t& cap, uint64_t floor, uint64_t* win, uint64_t k, uint64_t need) {
   if (!cap) return;
+  win[k % WIRE_WIN] = need;
+  uint64_t peak = 0;
+  for (uint32_t i = 0; i < WIRE_WIN; ++i) peak = std::max(peak, win[i]);
   const uint64_t chunk = 64ull << 10;
-  const uint64_t want = std::min<uint64_t>(WIRE_CAP_MAX, (need + need / 16 + 2 * chunk - 1) & ~(chunk - 1));
-  // A region that dropped units gets half its need again: the drops make catch-up traffic that
-  // grows the need further, and a capacity trailing it by 1/16 kept dropping (rehearsal, warm-up 5:
-  // 6,740 messages lost and 101 ms per step, profiles/r04z).
-  if (need > cap) cap = std::max<uint64_t>(cap, std::min<uint64_t>(WIRE_CAP_MAX, (need + need / 2 + chunk - 1) & ~(chunk - 1)));
-  else if (need > cap - cap / 16) cap = std::max<uint64_t>(cap, want);
-  // Shrinks by at most 1/8 per exchange: the need swings from tick to tick (heartbeat ticks, catch-up
-  // bursts), and cutting the capacity to one quiet tick's need dropped the next busy tick's units
-  // (overflow test: drops until tick 28 of 40).
-  else if (need < cap / 2)
-    cap = std::max<uint64_t>(floor, std::min<uint64_t>(cap, std::max<uint64_t>(want, (cap - cap / 8) & ~(chunk - 1))));
+  const uint64_t target = std::max<uint64_t>(floor, std::min<uint64_t>(WIRE_CAP_MAX, (peak + peak / 16 + 2 * chunk - 1) & ~(chunk - 1)));
+  if (need > cap) cap = std::max<uint64_t>(target, std::min<uint64_t>(WIRE_CAP_MAX, (need + need / 2 + chunk - 1) & ~(chunk - 1)));
+  else if (target > cap) cap = target;
+  else if (target < cap) cap = std::max<uint64_t>(target, std::min<uint64_t>(cap, (cap - cap / 8 + chunk - 1) & ~(chunk - 1)));
 }
 
 int rg_wire_plan_fixed(rg_engine* e, uint64_t* send_bytes, uint64_t* recv_bytes) {
@@ -2418,13 +2433,20 @@ int rg_wire_plan_fixed(rg_engine* e, uint64_t* send_bytes, uint64_t* recv_bytes)
   if (int jrc = join(e)) return jrc;
   HIPCHK(hipSetDevice(e->c.device));
   if (e->cap_s.empty()) wire_caps_init(e);
-  if (e->nfix >= 2) {  // the needs of the exchange two before: long complete (a tick has run since)
-    const uint32_t sl = (uint32_t)((e->nfix - 2) % 4);
+  if (e->nfix >= 2) {
+    // the needs of the exchange two before. A bounded wait: that exchange's unpack sits behind a whole
+    // tick on this stream, so the host never runs more than two exchanges ahead of the device
+    const uint64_t k = e->nfix - 2;
+    const uint32_t sl = (uint32_t)(k % 4);
     HIPCHK(hipEventSynchronize(e->need_ev[sl]));
     const uint64_t* hn = e->h_need + (uint64_t)sl * 2 * MAX_RANKS;
+    for (uint32_t r = 0; r < N; ++r)
+      if (hn[MAX_RANKS + r] == ~0ull)  // unpack_kernel rejected the region header (raftgpu_wire.hip)
+        return fail(RG_EINVARIANT, "rg_wire_plan_fixed: region from rank " + std::to_string(r) +
+                                       " carried an impossible size: the link's capacities can no longer agree");
     for (uint32_t r = 0; r < N; ++r) {
-      wire_cap_adapt(e->cap_s[r], e->cap_s0[r], hn[r]);
-      wire_cap_adapt(e->cap_r[r], e->cap_r0[r], hn[MAX_RANKS + r]);
+      wire_cap_adapt(e->cap_s[r], e->cap_s0[r], &e->win_s[(uint64_t)r * WIRE_WIN], k, hn[r]);
+      wire_cap_adapt(e->cap_r[r], e->cap_r0[r], &e->win_r[(uint64_t)r * WIRE_WIN], k, hn[MAX_RANKS + r]);
     }
   }
   LAUNCH(launch_wire_plan(wire_params(e), e->bounds, e->stream), e->stream, "wire plan");
@@ -2555,16 +2577,11 @@ int rg_wire_exchange(rg_engine* e, const rg_transport* t, uint64_t* sent_bytes) 
   if (!e || !t || !t->alltoallv) return fail(RG_EINVAL, "rg_wire_exchange args");
   if (sent_bytes) *sent_bytes = 0;
   if (!e->wire) return RG_OK;
-  // Sizing: fixed capacities — one collective, no host sync — for metadata-only
-  // engines, whose exchanges are latency-bound; exact sizes (the plan's host sync and a size all-gather
-  // through the transport, then a transfer of exactly the planned bytes) when Cmds travel, where the
-  // bytes bound the exchange (r04 rehearsal at 64K x 3: 4.14 ms per step exact, 4.38 ms fixed).
-  // RAFTGPU_WIRE_SIZING=fixed|exact overrides; without allgather_u64 the sizing is fixed.
-  bool fixed = !e->c.payload_bytes || !t->allgather_u64;
-  if (const char* v = getenv("RAFTGPU_WIRE_SIZING")) {
-    if (!strcmp(v, "fixed")) fixed = true;
-    else if (!strcmp(v, "exact") && t->allgather_u64) fixed = false;
-  }
+  // Sizing: fixed capacities — the one collective of the tick, no host sync, no size
+  // exchange — unless the engine was created with rg_config.wire_exact (and the transport has
+  // allgather_u64): then the plan's host sync and a size all-gather, and a transfer of exactly the
+  // planned bytes.
+  const bool fixed = !e->c.wire_exact || !t->allgather_u64;
   const uint32_t N = e->pl.N, me = e->pl.rank;
   std::vector<uint64_t> ssize(N), soff(N), rsize(N), roff(N);
   if (fixed) {

@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <string>
 
@@ -84,7 +85,16 @@ struct Rccl {
   hipStream_t xs = nullptr;     // transfers
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   uint64_t* d_sizes = nullptr;  // [2][nranks * 64]
+  bool self_rccl = false;       // RAFTGPU_RCCL_SELF=rccl (read at open): the region to self through RCCL too
 };
+
+// a failed transfer says why on stderr (the engine only sees the transport's -1)
+int why(const Rccl* c, const char* what, int rc = 0) {
+  const Api* a = api();
+  fprintf(stderr, "raftgpu rccl transport (rank %d of %d): %s%s%s\n", c->rank, c->nranks, what, rc ? ": " : "",
+          rc && a ? a->GetErrorString((ncclResult_t)rc) : "");
+  return -1;
+}
 
 int allgather_u64(void* user, const uint64_t* mine, uint64_t* all, uint32_t n) {
   Rccl* c = (Rccl*)user;
@@ -110,9 +120,13 @@ int alltoallv(void* user, const void* send, const uint64_t* soff, const uint64_t
   // the region to this rank itself is a device copy: RCCL's send/receive to self moved a grown
   // fixed-capacity region at ~25 GB/s (146 ms per step, profiles/r04z_wire_sizing.txt)
   // (RAFTGPU_RCCL_SELF=rccl sends it through RCCL too: the one-rank tests' way to run the grouped path)
-  const char* sv = getenv("RAFTGPU_RCCL_SELF");
-  const int me = sv && !strcmp(sv, "rccl") ? -1 : c->rank;
-  if (me >= 0 && ssize[me] != rsize[me]) return -1;
+  const int me = c->self_rccl ? -1 : c->rank;
+  if (me >= 0 && ssize[me] != rsize[me]) {
+    char m[160];
+    snprintf(m, sizeof m, "the region to itself is %llu bytes sent but %llu received (sizes disagree)",
+             (unsigned long long)ssize[me], (unsigned long long)rsize[me]);
+    return why(c, m);
+  }
   if (me >= 0 && ssize[me] && hipMemcpyAsync((uint8_t*)recv + roff[me], (const uint8_t*)send + soff[me], ssize[me],
                                   hipMemcpyDeviceToDevice, xs) != hipSuccess)
     return -1;
@@ -124,19 +138,18 @@ int alltoallv(void* user, const void* send, const uint64_t* soff, const uint64_t
   // smaller simply issue fewer groups
   const uint64_t pieces = (most + CHUNK - 1) / CHUNK;
   for (uint64_t k = 0; k < pieces; ++k) {
-    if (a->GroupStart() != 0) return -1;
-    bool ok = true;  // a failed Send / Recv still closes the group, or every later call on the comm breaks
-    for (int r = 0; r < c->nranks && ok; ++r) {
+    if (int rc = a->GroupStart()) return why(c, "ncclGroupStart", rc);
+    int bad = 0;  // a failed Send / Recv still closes the group, or every later call on the comm breaks
+    for (int r = 0; r < c->nranks && !bad; ++r) {
       if (r == me) continue;
       const uint64_t o = k * CHUNK;
-      if (ssize[r] > o &&
-          a->Send((const uint8_t*)send + soff[r] + o, std::min(CHUNK, ssize[r] - o), ncclUint8, r, c->comm, xs) != 0)
-        ok = false;
-      if (ok && rsize[r] > o &&
-          a->Recv((uint8_t*)recv + roff[r] + o, std::min(CHUNK, rsize[r] - o), ncclUint8, r, c->comm, xs) != 0)
-        ok = false;
+      if (ssize[r] > o)
+        bad = a->Send((const uint8_t*)send + soff[r] + o, std::min(CHUNK, ssize[r] - o), ncclUint8, r, c->comm, xs);
+      if (!bad && rsize[r] > o)
+        bad = a->Recv((uint8_t*)recv + roff[r] + o, std::min(CHUNK, rsize[r] - o), ncclUint8, r, c->comm, xs);
     }
-    if (a->GroupEnd() != 0 || !ok) return -1;
+    const int ge = a->GroupEnd();
+    if (bad || ge) return why(c, bad ? "ncclSend / ncclRecv" : "ncclGroupEnd", bad ? bad : ge);
   }
   // the engine stream's next work (unpack) waits for the transfers
   if (hipEventRecord(c->ev_out, xs) != hipSuccess || hipStreamWaitEvent(st, c->ev_out, 0) != hipSuccess) return -1;
@@ -165,6 +178,8 @@ int rg_rccl_open(const uint8_t id[128], int32_t nranks, int32_t rank, int32_t de
   c->nranks = nranks;
   c->rank = rank;
   c->device = device;
+  const char* sv = getenv("RAFTGPU_RCCL_SELF");
+  c->self_rccl = sv && !strcmp(sv, "rccl");
   ncclUniqueId u;
   memcpy(u.internal, id, 128);
   if (hipStreamCreateWithFlags(&c->small, hipStreamNonBlocking) != hipSuccess ||

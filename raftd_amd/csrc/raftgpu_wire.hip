@@ -299,7 +299,14 @@ __global__ void unpack_kernel(WireParams w) {
   const uint32_t r = find_rank(w.rbeg, w.pl.N, u);
   const uint32_t u0 = w.rbeg[r], nu = w.rbeg[r + 1] - u0;
   const uint8_t* region = w.recv + w.recv_region[r];
-  if (u == u0 && w.rneed) w.rneed[r] = reinterpret_cast<const uint64_t*>(region)[0];
+  if (u == u0 && w.rneed) {  // the need the sender's plan put in the header, checked: it comes from another process
+    // and sizes this link's capacity on both ends, so a bad one is reported (~0: the host fails the next
+    // rg_wire_plan_fixed) rather than fed to the capacity rule, where the two ends would then disagree
+    const uint64_t need = reinterpret_cast<const uint64_t*>(region)[0];
+    const uint64_t lo = 256 + ((nu * 8ull + 255) & ~255ull);
+    const uint64_t hi = lo + (uint64_t)nu * w.K * (64 + (uint64_t)w.E * (16 + ((w.maxc + 15ull) & ~15ull)));
+    w.rneed[r] = (need >= lo && need <= hi && !(need & 15)) ? need : ~0ull;
+  }
   const uint64_t tv = reinterpret_cast<const uint64_t*>(region + 256)[u - u0];
   uint32_t c = (uint32_t)(tv & 0xFF);
   const uint64_t rend = r + 1 < w.pl.N ? w.recv_region[r + 1] : w.recv_total;

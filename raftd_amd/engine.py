@@ -36,7 +36,7 @@ class Config(C.Structure):
         ("ranks", C.c_uint32), ("rank", C.c_uint32), ("wire_all", C.c_uint32), ("column_base", C.c_uint32),
         ("crc32c", C.c_uint32), ("apply_feedback", C.c_uint32), ("initial_members", C.c_uint32),
         ("max_cmd_bytes", C.c_uint32), ("stream_pages", C.c_uint32), ("pool_pages", C.c_uint32),
-        ("join_slots", C.c_uint32), ("_cpad", C.c_uint32),
+        ("join_slots", C.c_uint32), ("wire_exact", C.c_uint32),
     ]
 
 
@@ -289,7 +289,7 @@ def default_config(**kw) -> dict:
              max_msgs_per_pair=8, num_slabs=2, election_rtt=10, heartbeat_rtt=1, check_quorum=1,
              snapshot_entries=1000, compaction_overhead=5, drop_ppm=0, device=0, seed=0x5EED,
              ranks=1, rank=0, wire_all=0, column_base=0, crc32c=0, apply_feedback=0,
-             initial_members=0, max_cmd_bytes=0, stream_pages=0, pool_pages=0, join_slots=0)
+             initial_members=0, max_cmd_bytes=0, stream_pages=0, pool_pages=0, join_slots=0, wire_exact=0)
     c.update(kw)
     return c
 
@@ -580,9 +580,9 @@ class Engine:
         self._check(self.L.rg_wire_recv(self.h, C.c_void_p(recv_ptr or None), rb))
 
     def wire_exchange(self, transport: "Transport") -> int:
-        """rg_wire_exchange: fixed-capacity plan, pack, one transport all-to-all, unpack in one call
-        (the C-ABI path a non-Python host uses; transport = rccl_transport(...) or PyTransport(...).t).
-        Returns the bytes sent to other ranks."""
+        """rg_wire_exchange: plan (fixed capacities unless the engine was made with wire_exact=1), pack,
+        one transport all-to-all, unpack in one call (the C-ABI path a non-Python host uses; transport =
+        rccl_transport(...) or PyTransport(...).t). Returns the bytes sent to other ranks."""
         sent = C.c_uint64()
         self._check(self.L.rg_wire_exchange(self.h, C.byref(transport), C.byref(sent)))
         return sent.value

@@ -121,6 +121,18 @@ def test_two_processes_gloo_fixed_capacity():
     assert "dist parity ok" in out.stdout
 
 
+def test_two_processes_capacities_agree_while_growing():
+    """fixed-capacity regions that start at 4 KiB over two processes — units drop, both
+    ends of every link grow its capacity from their own copy of the needs, and in every exchange the
+    capacity a rank sends with equals the one its peer receives with; the drops stop and every
+    shard's committed log is the same on all of its replicas (tests/capacity_worker.py)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29547")
+    out = subprocess.run([sys.executable, "-u", os.path.join(HERE, "capacity_worker.py"), "2"], env=env,
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert "capacity agreement ok" in out.stdout
+
+
 def test_cluster_full_batches():
     cfg = dict(CHAOS, log_capacity=256, max_entries_per_msg=64, snapshot_entries=120, payload_bytes=16)
     run_chaos(3, dict(groups=9, replicas=3, seed=37, **cfg), ticks=120, seed=65, p_camp=0.04)
@@ -353,16 +365,14 @@ def _copy_transport(calls):
 
 
 @pytest.mark.parametrize("sizing", ["fixed", "exact"])
-def test_exchange_is_one_collective_with_fixed_capacity(sizing, monkeypatch):
-    """rg_wire_exchange with fixed-capacity regions (RAFTGPU_WIRE_SIZING=fixed; the default of
-    metadata-only engines) moves them with one transport call per tick and never asks for the sizes
-    (no allgather); with the default capacity (the worst case of this configuration fits) nothing is
-    dropped and every tick equals the oracle. Exact sizing (the default when Cmds travel) asks the
-    transport for the sizes once per exchange."""
+def test_exchange_is_one_collective_with_fixed_capacity(sizing):
+    """rg_wire_exchange with fixed-capacity regions (the default) moves them with one transport call
+    per tick and never asks for the sizes (no allgather); with the default capacity (the worst case of
+    this configuration fits) nothing is dropped and every tick equals the oracle. Exact sizing
+    (rg_config.wire_exact) asks the transport for the sizes once per exchange."""
     from raftd_amd.engine import Engine
-    monkeypatch.setenv("RAFTGPU_WIRE_SIZING", sizing)
     cfg = dict(groups=16, replicas=3, seed=95, **CHAOS)
-    eng = Engine(wire_all=1, **cfg)
+    eng = Engine(wire_all=1, wire_exact=int(sizing == "exact"), **cfg)
     ora = make("c", **cfg)
     calls = []
     t = _copy_transport(calls)
@@ -391,7 +401,6 @@ def test_fixed_capacity_overflow_drops_units_and_grows():
     from raftd_amd.engine import Engine
     G, R, E = 256, 3, 16
     os.environ["RAFTGPU_WIRE_CAP0"] = "4096"
-    os.environ["RAFTGPU_WIRE_SIZING"] = "fixed"
     try:
         eng = Engine(wire_all=1, groups=G, replicas=R, log_capacity=256, payload_bytes=64, max_entries_per_msg=E,
                      snapshot_entries=0, seed=97)
@@ -410,7 +419,6 @@ def test_fixed_capacity_overflow_drops_units_and_grows():
         eng.sync()
     finally:
         del os.environ["RAFTGPU_WIRE_CAP0"]
-        del os.environ["RAFTGPU_WIRE_SIZING"]
     assert drops[-1] > 0 and drops[-1] == drops[-20], drops  # dropped early, none in the last 20 ticks
     views = eng.replicas()
     done = 0
