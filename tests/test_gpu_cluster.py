@@ -336,12 +336,16 @@ def test_c_exchange_transport_failures_surface_as_errors():
     with pytest.raises(RgError, match="alltoallv failed"):
         eng.wire_exchange(bad.t)
     assert isinstance(bad.error, RuntimeError)
-    # exact sizing (the default when Cmds travel): a transport whose size exchange lies is refused
+    eng.sync()
+    # exact sizing (rg_config.wire_exact): a transport whose size exchange lies is refused
+    ex = Engine(wire_all=1, wire_exact=1, **cfg)
+    ex.bootstrap()
+    ex.tick(*random_inputs(np.random.default_rng(94), 8, 3, CHAOS["max_entries_per_msg"]))
     liar = PyTransport(lambda vals: [v + 16 for v in vals], lambda *a: None)
     liar.nranks = 1
     with pytest.raises(RgError, match="another rank's sizes"):
-        eng.wire_exchange(liar.t)
-    eng.sync()
+        ex.wire_exchange(liar.t)
+    ex.sync()
 
 
 def _copy_transport(calls):
