@@ -421,9 +421,11 @@ struct Ctl {
   }
   // FAST: the only log write of the fast path — n entries at fresh indices (past every index read or
   // sent this step: bank 0, nothing to flip), all holding one ring word (a leader's synthetic batch, its
-  // no-op, a follower's uniform Replicate), as one uniform job
+  // no-op, a follower's uniform Replicate from this rank or over the wire), as one uniform job.
+  // spos: a RING job's stream position of entry 0 at the sender, a WIRE job's record offset (the job
+  // write_entries would make for the same entries)
   RG_FN void write_fresh_uniform(uint64_t base, uint32_t n, uint32_t kind, uint32_t src, uint64_t word,
-                                 uint32_t uspos) {
+                                 uint64_t spos) {
 #ifdef RG_CTL_FASTREP
     la_n = 0;
 #endif
@@ -446,7 +448,7 @@ struct Ctl {
       const uint64_t n64 = p.nrep, JN = (uint64_t)p.J * n64;
       uint64_t* j64 = p.job64 + (uint64_t)nj * n64 + q;
       j64[J_FIRST * JN] = base;
-      j64[J_SPOS * JN] = kind == SRC_RING ? uspos : 0u;
+      j64[J_SPOS * JN] = kind == SRC_RING || kind == SRC_WIRE ? spos : 0ull;
       j64[J_SMASK * JN] = (word & BANK_BIT) ? (n >= 64 ? ~0ull : (1ull << n) - 1) : 0ull;
       j64[J_DMASK * JN] = 0;
       uint32_t* j32 = p.job32 + (uint64_t)nj * n64 + q;
@@ -788,13 +790,17 @@ struct Ctl {
       return;
     }
     const uint32_t n = (uint32_t)(w0 >> 32);
+    // a remote Replicate's word 7 is its records' offset in the receive buffer (16-B aligned), with
+    // RG_UNIFORM set by unpack_kernel when every entry record holds the same application ring word
+    const bool runi = remote && ((uint32_t)wofs & RG_UNIFORM) && n > 0;
+    // a uniform Replicate: every entry carries the word mt[0] (local: the sender wrote only that one)
+    const bool uni = !remote && ((uint32_t)wofs & RG_UNIFORM) && n > 0;
+    wofs &= ~(uint64_t)RG_UNIFORM;
     if (term_at(li) == log_term) {
       const uint64_t* mt = (remote ? p.rmt : p.mt_in) + ((((uint64_t)src * R + s) * p.K + k) * p.E) * p.G + g;
-      // a uniform Replicate (local only): every entry carries the word mt[0]
-      const bool uni = !remote && ((uint32_t)wofs & RG_UNIFORM) && n > 0;
-      const uint64_t uw = uni ? mt0 : 0ull;  // loaded with the header (handle_)
+      const uint64_t uw = uni || runi ? mt0 : 0ull;  // loaded with the header (handle_)
       if constexpr (FAST) {  // an append at the log end from a uniform Replicate (or an empty one)
-        if (li != last || (n > 0 && !uni) || remote) {
+        if (li != last || (n > 0 && !uni && !runi) || (uw & TYPE_BIT)) {
           abort_();
           return;
         }
@@ -808,7 +814,8 @@ struct Ctl {
             abort_();
             return;
           }
-          write_fresh_uniform(li + 1, n, SRC_RING, src * p.G + g, uw, (uint32_t)upos);
+          if (remote) write_fresh_uniform(li + 1, n, SRC_WIRE, n, uw, wofs);
+          else write_fresh_uniform(li + 1, n, SRC_RING, src * p.G + g, uw, (uint32_t)upos);
           last = last_new;
         }
         commit_to(umin64(last_new, mcommit));
@@ -1144,19 +1151,19 @@ struct Ctl {
 #endif
   struct Hdr {
     uint64_t w[NB];
-    uint64_t mt0;  // a local Replicate's first inline word (a uniform Replicate needs only it)
+    uint64_t mt0;  // a Replicate's first inline word (a uniform Replicate needs only it)
   };
   RG_FN const uint64_t* hdr_ptr(uint32_t src, uint32_t k, bool remote) const {
     return (remote ? p.rhdr : p.hdr_in) + (((uint64_t)src * R + s) * p.K + k) * p.G + g;
   }
-  // one round trip: the header words and, for a local message, its first inline word (for other
+  // one round trip: the header words and the message's first inline word (for other
   // messages the slot holds stale words, which nothing reads)
   RG_FN void load_hdr(uint32_t src, uint32_t k, bool remote, Hdr& o) const {
     const uint64_t plane = (uint64_t)R * R * p.K * p.G;
     const uint64_t* h = hdr_ptr(src, k, remote);
 #pragma unroll
     for (int x = 0; x < NB; ++x) o.w[x] = h[(uint64_t)x * plane];
-    o.mt0 = remote ? 0ull : p.mt_in[((((uint64_t)src * R + s) * p.K + k) * p.E) * p.G + g];
+    o.mt0 = (remote ? p.rmt : p.mt_in)[((((uint64_t)src * R + s) * p.K + k) * p.E) * p.G + g];
   }
   RG_FN void handle(uint32_t src, uint32_t k, bool remote, const Hdr& hd) {
     RG_T0(t0);
@@ -1173,9 +1180,9 @@ struct Ctl {
     const uint32_t type = (uint32_t)(w0 & 0xFF);
     const uint32_t from = (uint32_t)(w0 >> 8) & 0xFF;
     if constexpr (FAST) {
-      // same-term steady-state traffic only: a term change, a remote message, a vote, a read, a
-      // forwarded proposal or a snapshot leaves the fast path (a candidate never entered it)
-      if (remote || from - 1 >= (uint32_t)R || (mterm != 0 && mterm != term) ||
+      // same-term steady-state traffic only, from this rank or over the wire: a term change, a vote, a
+      // read, a forwarded proposal or a snapshot leaves the fast path (a candidate never entered it)
+      if (from - 1 >= (uint32_t)R || (mterm != 0 && mterm != term) ||
           (type == M_REPLICATE && (uint32_t)(w0 >> 32) > p.E)) {
         abort_();
         return;

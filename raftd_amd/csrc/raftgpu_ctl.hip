@@ -73,7 +73,7 @@ __global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_MINWAVES) control_kernel(
 // steady-state branches only and hands a replica whose step leaves them to the slow kernel, which
 // re-runs that replica's whole step with the full Ctl<R> (an aborted fast step stored nothing).
 #ifndef RG_CTL_FAST_WAVES
-#define RG_CTL_FAST_WAVES (RG_CTL_R <= 3 ? 3 : 2)  // the most waves per SIMD without scratch (role-sorted)
+#define RG_CTL_FAST_WAVES (RG_CTL_R <= 3 ? 3 : RG_CTL_R <= 7 ? 2 : 1)  // the most waves per SIMD without scratch
 #endif
 // The fast path is compiled once per role — Ctl<R, true, LEADER> for leaders, Ctl<R, true, FOLLOWER>
 // for every other replica (followers step, candidates hand off) — and each lane runs its role's

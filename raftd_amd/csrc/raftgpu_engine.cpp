@@ -2498,7 +2498,7 @@ int rg_wire_recv(rg_engine* e, const void* recv_buf, const uint64_t* recv_bytes)
   uint64_t off = 0;
   for (uint32_t r = 0; r < e->pl.N; ++r) {
     const uint64_t units = e->h_rbeg[r + 1] - e->h_rbeg[r];
-    if (units ? recv_bytes[r] < wire_region_min(units) : recv_bytes[r] != 0)
+    if ((units ? recv_bytes[r] < wire_region_min(units) : recv_bytes[r] != 0) || (recv_bytes[r] & 15))
       return fail(RG_EINVAL, "rg_wire_recv: region of rank " + std::to_string(r) + " has the wrong size");
     w.recv_region[r] = off;
     off += recv_bytes[r];

@@ -348,7 +348,7 @@ __global__ void unpack_kernel(WireParams w) {
     }
     // every entry record: an application entry's length <= max_cmd_bytes with the payload bit exactly
     // when non-zero, a ConfigChange no payload and a descriptor; Cmd offsets back to back from 0
-    bool sane = true;
+    bool sane = true, same = n > 0;
     uint32_t tot = 0;
     for (uint32_t e = 0; e < n; ++e) {
       const uint64_t rw = h[8 + 2 * e];
@@ -356,6 +356,7 @@ __global__ void unpack_kernel(WireParams w) {
       sane = sane && ((rw & TYPE_BIT) ? !(rw & PAY_BIT) && ln <= 0x2Fu
                                       : ln <= w.maxc && ((rw & PAY_BIT) != 0) == (ln != 0)) &&
              ofs == tot;
+      same = same && rw == h[8] && !(rw & TYPE_BIT);
       tot += word_nc(rw);
     }
     if (!sane || (uint64_t)(in - w.recv) + 64 + 16ull * (n + tot) > rend) {
@@ -365,7 +366,10 @@ __global__ void unpack_kernel(WireParams w) {
     uint64_t* ho = w.rhdr + (col * w.K + k) * w.G + j;
     for (int x = 0; x < 7; ++x) ho[x * plane] = h[x];
     if (type == M_PROPOSE) ho[4 * plane] = tot;  // its Cmds' stream chunks (the capacity rule's input)
-    ho[7 * plane] = n ? (uint64_t)(in + 64 - w.recv) : h[7];  // entries: word 7 = their records' offset
+    // entries: word 7 = their records' offset (16-B aligned), | RG_UNIFORM for a Replicate whose records
+    // all hold one application ring word (the control kernel's fast path appends it as one uniform job)
+    ho[7 * plane] = n ? (uint64_t)(in + 64 - w.recv) | (type == M_REPLICATE && same ? (uint64_t)RG_UNIFORM : 0ull)
+                      : h[7];
     uint64_t* mo = w.rmt + ((col * w.K + k) * w.E) * w.G + j;  // inline ring words (a Propose: length bits)
     for (uint32_t e = 0; e < n; ++e) mo[(uint64_t)e * w.G] = h[8 + 2 * e] & (type == M_PROPOSE ? ~TERM_MASK & ~BANK_BIT & ~TYPE_BIT : ~0ull);
     in += 64 + 16ull * (n + tot);

@@ -442,3 +442,41 @@ def test_fixed_capacity_overflow_drops_units_and_grows():
     assert done > G // 2
     assert np.mean(np.array(led) > 40) > 0.9, sorted(led)[:20]
     assert np.median([max(views[g * R + s]["committed"] for s in range(R)) for g in range(G)]) > 200
+
+
+@pytest.mark.parametrize("ranks", [3, 1])
+def test_control_fast_path_covers_the_wire_steady_state(ranks):
+    """Replicas spread over ranks (3: every follower on another rank than its leader; 1 with wire_all:
+    every message through the wire): in steady state the followers' Replicates and the leaders'
+    responses arrive over the wire, and no replica leaves the control fast path (unpack_kernel marks a
+    Replicate whose entry records hold one application ring word, which the fast step appends as one
+    uniform WIRE job) — every tick bit-exact with the oracle, entries and payloads included."""
+    import ctypes as C
+    from raftd_amd.cluster import LoopbackCluster
+    G, R, E = 96, 3, 64
+    cfg = dict(replicas=R, log_capacity=256, payload_bytes=256, max_entries_per_msg=E, snapshot_entries=100,
+               compaction_overhead=5, seed=0x5EED)
+    cl = LoopbackCluster(ranks=ranks, groups=G, **cfg, **(dict(wire_all=1) if ranks == 1 else {}))
+    ora = make("c", groups=G, **cfg)
+    fn = cl.engines[0].L.rg_debug_ctl_slow
+    fn.argtypes, fn.restype = [C.c_void_p, C.POINTER(C.c_uint32)], C.c_int
+    n = C.c_uint32()
+    cl.bootstrap()
+    ora.bootstrap()
+    camp = np.zeros(G * R, np.uint8)
+    camp[0::R] = 1
+    pt, pc = np.zeros(G, np.uint8), np.full(G, E, np.uint32)
+    slow = []
+    for t in range(40):
+        ins = (None, None, camp) if t == 1 else (pt, pc) if t >= 6 else ()
+        cl.tick(*ins)
+        ora.tick(*ins)
+        tot = 0
+        for e in cl.engines:
+            assert fn(e.h, C.byref(n)) == 0
+            tot += n.value
+        slow.append(tot)
+        compare(cl, ora, t)
+    check_payloads(cl, ora)
+    assert cl.wire_bytes > 0 and ora.replica(0)["snap_index"] > 0
+    assert slow[1] > 0 and max(slow[12:]) == 0, slow
