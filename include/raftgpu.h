@@ -64,7 +64,10 @@ enum {
   RG_ERR_CONFLICT_COMMITTED = 1, RG_ERR_COMMIT_BEYOND_LAST = 2, RG_ERR_RING_FULL = 4,
   RG_ERR_CRC = 8, RG_ERR_EMPTY_SNAPSHOT = 16,
   RG_ERR_MALFORMED = 32, /* a message with an impossible sender / destination was ignored */
-  RG_ERR_POOL = 64       /* the payload page pool was empty: this replica's appends of a step were lost */
+  RG_ERR_POOL = 64,      /* the payload page pool was empty: this replica's appends of a step were lost */
+  RG_ERR_TERM_LIMIT = 128 /* a campaign at term 2^36 - 1 was refused: terms are 36-bit (the ring word
+                             holds the Cmd length beside the term); the replica stays a
+                             follower at that term. ~6.9e10 elections: unreachable in service */
 };
 #define RG_TICK_NO_LOCALTICK 1u
 

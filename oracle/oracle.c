@@ -611,6 +611,10 @@ static void handle_node_election(or_engine* e, rep_t* r) {
   if (r->role == OR_LEADER) return;
   if (!is_member(r, r->s)) return; /* selfRemoved: no elections */
   if (r->committed > r->applied) return; /* hasConfigChangeToApply */
+  if (r->term >= OR_TERM_MAX) { /* the next term would not fit the ring word's 36-bit field */
+    r->err |= OR_ERR_TERM_LIMIT;
+    return;
+  }
   campaign(e, r);
 }
 

@@ -43,8 +43,10 @@ enum { OR_CC_ADD = 1, OR_CC_REMOVE = 2 };
 #define OR_ENTRY_EMPTY 0x100u /* import: application entry with an empty Cmd (no payload) */
 enum {
   OR_ERR_CONFLICT_COMMITTED = 1, OR_ERR_COMMIT_BEYOND_LAST = 2, OR_ERR_RING_FULL = 4,
-  OR_ERR_CRC = 8, OR_ERR_EMPTY_SNAPSHOT = 16
+  OR_ERR_CRC = 8, OR_ERR_EMPTY_SNAPSHOT = 16,
+  OR_ERR_TERM_LIMIT = 128 /* a campaign at term 2^36 - 1 (the ring word's term field) was refused */
 };
+#define OR_TERM_MAX ((1ull << 36) - 1) /* terms are 36-bit (the GPU ring word's term field) */
 #define OR_TICK_NO_LOCALTICK 1u
 
 typedef struct or_config {

@@ -31,6 +31,8 @@ READ_INDEX, READ_INDEX_RESP = 19, 20
 FOLLOWER, CANDIDATE, LEADER = 0, 1, 2
 RETRY, WAIT, REPL, SNAP = 0, 1, 2, 3
 ERR_CONFLICT, ERR_BEYOND, ERR_RING, ERR_CRC, ERR_EMPTY_SNAP = 1, 2, 4, 8, 16
+ERR_TERM = 128  # a campaign at the last term the ring word holds (2^36 - 1): refused
+TERM_MAX = (1 << 36) - 1
 LEADER_MSGS = (REPLICATE, INSTALL_SNAPSHOT, HEARTBEAT, READ_INDEX_RESP)
 CC_ADD, CC_REMOVE = 1, 2  # membership change ops: descriptor op << 4 | (slot + 1)
 
@@ -491,7 +493,10 @@ class Replica:
             self.tick()
         elif t == ELECTION:
             if role != LEADER and self.s in self.members and not self.committed > self.applied:
-                self.campaign()
+                if self.term >= TERM_MAX:
+                    self.err |= ERR_TERM
+                else:
+                    self.campaign()
         elif t == LEADER_HEARTBEAT:
             if role == LEADER:  # a pending ReadIndex rides on every heartbeat (readIndex.peepCtx)
                 ctx = self.pending_read[0] if self.pending_read is not None else 0

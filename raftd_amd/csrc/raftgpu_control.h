@@ -901,6 +901,10 @@ struct Ctl {
     if (role == LEADER) return;
     if (!is_member(s)) return;        // selfRemoved: no elections
     if (committed > applied) return;  // hasConfigChangeToApply
+    if (term >= TERM_MASK) {          // the next term would not fit the ring word's 36-bit field
+      err |= ERR_TERM;
+      return;
+    }
     campaign();
   }
   RG_FN void handle_request_vote(uint64_t log_term, uint64_t log_index, uint32_t from) {

@@ -83,7 +83,8 @@ constexpr uint32_t RG_UNIFORM = 1;
 enum : uint32_t { RETRY = 0, WAIT = 1, REPLICATE = 2, SNAPSHOT = 3 };
 enum : uint32_t { ENTRY_APP = 0, ENTRY_CONFIG = 1 };
 enum : uint32_t {
-  ERR_CONFLICT = 1, ERR_BEYOND = 2, ERR_RING = 4, ERR_CRC = 8, ERR_EMPTY_SNAP = 16, ERR_WIRE = 32, ERR_POOL = 64
+  ERR_CONFLICT = 1, ERR_BEYOND = 2, ERR_RING = 4, ERR_CRC = 8, ERR_EMPTY_SNAP = 16, ERR_WIRE = 32, ERR_POOL = 64,
+  ERR_TERM = 128  // a campaign at term TERM_MASK (the ring word's 36-bit term field is full) was refused
 };
 // RG_BOUNDS (diagnostic builds): kernels printf and skip any count or offset read from memory that
 // would index outside its buffer (ERR_WIRE in the replica's err word). Product builds check only

@@ -339,7 +339,11 @@ __global__ void unpack_kernel(WireParams w) {
                        type == M_HEARTBEAT || type == M_HEARTBEAT_RESP || type == M_READ_INDEX ||
                        type == M_READ_INDEX_RESP;
     const uint32_t from = (uint32_t)(w0 >> 8) & 0xFF, to = (uint32_t)(w0 >> 16) & 0xFF, nent = (uint32_t)(w0 >> 32);
-    if (!known || from != s + 1 || to != d + 1 || n > w.E ||
+    // terms fit the ring word's 36-bit field (a replica never makes a larger one: rg_import_replica
+    // refuses it, a campaign at the limit is refused, RG_ERR_TERM_LIMIT)
+    const bool terms_ok = h[1] <= TERM_MASK &&
+                          (h[2] <= TERM_MASK || !(type == M_REPLICATE || type == M_REQUEST_VOTE || type == M_INSTALL_SNAPSHOT));
+    if (!known || !terms_ok || from != s + 1 || to != d + 1 || n > w.E ||
         (type == M_PROPOSE && (nent < 1 || nent > w.E || !cc_valid((uint32_t)h[6], w.R))) ||
         (uint64_t)(in - w.recv) + 64 + (uint64_t)n * 16 > rend) {
       RG_OOB("RG_BOUNDS unpack u=%u k=%u type=%u from=%u to=%u n=%u region end %llu\n", u, k, type, from, to, n,

@@ -273,3 +273,22 @@ def _paper_kats():
 
 
 PAPER_KATS = _paper_kats()
+
+
+# ---- the engine's own boundary (not a published table): terms are 36-bit
+TERM_MAX = (1 << 36) - 1
+ERR_TERM_LIMIT = 128
+
+
+def run_term_limit(kind, term):
+    """A follower at `term` campaigns: below the limit it becomes a candidate at term + 1 and asks
+    for votes; at 2^36 - 1 the campaign is refused (RG_ERR_TERM_LIMIT), the replica stays a follower
+    at its term and sends nothing."""
+    e = make(kind, **small_cfg())
+    e.bootstrap()
+    log = [1, 1, 1]
+    e.import_replica(0, view(3, term=term, last=3, committed=3, applied=3, next=[4] * 3), log)
+    e.tick(campaign=np.array([1, 0, 0], np.uint8), flags=NO_TICK)
+    v = e.replica(0)
+    sent = sum(len([m for m in e.msgs(0, d) if m["type"] == RV]) for d in (1, 2))
+    return ROLES[v["role"]], v["term"], v["err"], sent

@@ -168,3 +168,9 @@ def test_control_step_c3_shape():
             for rid in range(0, G * R, 997):
                 assert a.replica(rid) == b.replica(rid), (t, rid)
     assert b.replica(0)["committed"] > 512 and b.replica(0)["marker"] > 0
+
+
+def test_control_step_term_limit():
+    """The 36-bit term boundary on the control step compiled for the CPU, as on the oracles."""
+    assert K.run_term_limit("ctl", K.TERM_MAX - 1) == ("candidate", K.TERM_MAX, 0, 2)
+    assert K.run_term_limit("ctl", K.TERM_MAX) == ("follower", K.TERM_MAX, K.ERR_TERM_LIMIT, 0)

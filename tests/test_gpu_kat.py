@@ -49,3 +49,10 @@ def test_quorum_commit(case):
 def test_paper_kats(name):
     """The etcd paper-test shapes through rg_import_replica / rg_deliver / rg_tick."""
     assert all(K.PAPER_KATS[name]("gpu"))
+
+
+def test_term_limit():
+    """The 36-bit term boundary: the engine refuses a campaign at 2^36 - 1 exactly as the oracles do."""
+    assert K.run_term_limit("gpu", K.TERM_MAX - 1) == ("candidate", K.TERM_MAX, 0, 2)
+    assert K.run_term_limit("gpu", K.TERM_MAX) == ("follower", K.TERM_MAX, K.ERR_TERM_LIMIT, 0)
+    assert K.run_term_limit("c", K.TERM_MAX) == K.run_term_limit("gpu", K.TERM_MAX)

@@ -58,3 +58,9 @@ def test_paper_kats(kind, name):
     """etcd raft paper-test shapes (leader election, candidate fallback, term update, leader and
     follower commit, vote request, CheckQuorum step-down); parity with dragonboat unpinned."""
     assert all(K.PAPER_KATS[name](kind))
+
+
+@pytest.mark.parametrize("kind", KINDS_CPU)
+def test_term_limit(kind):
+    assert K.run_term_limit(kind, K.TERM_MAX - 1) == ("candidate", K.TERM_MAX, 0, 2)
+    assert K.run_term_limit(kind, K.TERM_MAX) == ("follower", K.TERM_MAX, K.ERR_TERM_LIMIT, 0)
