@@ -1131,6 +1131,22 @@ int or_config_change(or_engine* e, uint64_t group, uint32_t slot, uint32_t op, u
   return 0;
 }
 
+int or_compact(or_engine* e, uint64_t group, uint64_t index) {
+  if (group < e->c.group_base || group >= (uint64_t)e->c.group_base + e->c.groups) return -1;
+  const uint32_t g = (uint32_t)(group - e->c.group_base);
+  int n = 0;
+  for (uint32_t s = 0; s < e->c.replicas; ++s) {
+    rep_t* r = &e->reps[g * e->c.replicas + s];
+    const uint64_t c = index < r->snap_index ? index : r->snap_index;
+    if (c <= r->marker) continue;
+    r->marker_term = term_of(e, r, c);
+    r->marker = c;
+    r->fidx = c + 1; /* the next step releases the stream below entry c + 1 */
+    ++n;
+  }
+  return n;
+}
+
 int or_read_index(or_engine* e, const or_read_request* q, size_t n) {
   for (size_t i = 0; i < n; ++i)
     if (q[i].group < e->c.group_base || q[i].group >= (uint64_t)e->c.group_base + e->c.groups ||

@@ -155,6 +155,11 @@ int or_propose(or_engine* e, const or_proposal* p, size_t n, const uint8_t* payl
  * slot `target`, proposed at replica `slot` of shard `group` after that tick's Cmd batch. -1 invalid,
  * -3 a change is already staged for the shard this tick. */
 int or_config_change(or_engine* e, uint64_t group, uint32_t slot, uint32_t op, uint32_t target);
+/* rg_compact: between ticks, compact the log of every replica of global shard `group`
+ * to min(index, its snap_index) when that is above its marker (marker_term = the term there); the
+ * payload stream below it is released by the next tick, as after a snapshot's compaction. Returns the
+ * number of replicas compacted, or -1 for a shard outside the engine. */
+int or_compact(or_engine* e, uint64_t group, uint64_t index);
 /* Append a message to rid_src's most recent outbox so it is delivered next tick. Replicate
  * entries are taken from the sender's current log (indices log_index+1 ..). */
 int or_deliver(or_engine* e, uint32_t rid_src, const or_msg_view* m);

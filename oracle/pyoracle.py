@@ -132,6 +132,7 @@ def lib():
         L.or_propose.argtypes = [vp, C.POINTER(Proposal), C.c_size_t, C.c_void_p, C.c_void_p]
         L.or_notify_applied.argtypes = [vp, u32, u64]
         L.or_config_change.argtypes = [vp, u64, u32, u32, u32]
+        L.or_compact.argtypes = [vp, u64, u64]
         L.or_read_index.argtypes = [vp, C.POINTER(ReadRequest), C.c_size_t]
         L.or_get_read_ready.argtypes = [vp, u32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.or_tick.restype = C.c_int
@@ -352,6 +353,11 @@ class Oracle:
         """(ctx, index) of the read replica rid made ready in the last tick, or None."""
         c, i = C.c_uint64(), C.c_uint64()
         return (c.value, i.value) if self.L.or_get_read_ready(self.h, rid, C.byref(c), C.byref(i)) == 1 else None
+
+    def compact(self, group, index) -> int:
+        """or_compact (rg_compact): compact every replica of global shard `group` to min(index, its
+        snap_index); returns the number compacted, -1 for a shard outside the engine."""
+        return self.L.or_compact(self.h, group, index)
 
     def config_change(self, group, slot, op, target) -> int:
         """Stage a membership change for the next tick (or_config_change): 0, -1 invalid, -3 one

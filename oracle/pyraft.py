@@ -622,6 +622,25 @@ class Sim:
         self.reads = {}   # window rid -> ReadIndex ctx for the next tick
         self.ccs = {}     # window group -> (slot, descriptor) membership change for the next tick
 
+    def compact(self, group, index):
+        """rg_compact between ticks: every replica of `group` compacts to min(index, snap_index) when
+        that is above its marker; the next step releases the stream below (fidx)."""
+        base = self.cfg["group_base"]
+        if not (base <= group < base + self.G):
+            return -1
+        n = 0
+        for s in range(self.R):
+            r = self.reps[(group - base) * self.R + s]
+            c = min(index, r.snap_index)
+            if c <= r.marker:
+                continue
+            mt = r.term_at(c)
+            del r.log[:c - r.marker]
+            r.marker, r.marker_term = c, mt
+            r.fidx = c + 1
+            n += 1
+        return n
+
     def config_change(self, group, slot, op, target):
         base = self.cfg["group_base"]
         if not (base <= group < base + self.G) or slot >= self.R or target >= self.R or op not in (CC_ADD, CC_REMOVE):

@@ -478,5 +478,5 @@ def test_control_fast_path_covers_the_wire_steady_state(ranks):
         slow.append(tot)
         compare(cl, ora, t)
     check_payloads(cl, ora)
-    assert cl.wire_bytes > 0 and ora.replica(0)["snap_index"] > 0
+    assert (cl.wire_bytes > 0 or ranks == 1) and ora.replica(0)["snap_index"] > 0  # 1 rank: regions to itself
     assert slow[1] > 0 and max(slow[12:]) == 0, slow
