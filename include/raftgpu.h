@@ -524,6 +524,14 @@ int rg_config_change(rg_engine* e, uint64_t group, uint32_t slot, uint32_t op, u
  * campaigns (hasConfigChangeToApply: committed > applied) and snapshots (SnapshotEntries applied
  * since the last one). RG_EINVAL (nothing changed) if an index exceeds processed or a rid is bad. */
 int rg_notify_applied(rg_engine* e, const uint32_t* rids, const uint64_t* index, size_t n);
+/* Log compaction for GLOBAL shard `group` between ticks (SURVEY §8b rg_compact; raftd compacts only on
+ * its SnapshotEntries / CompactionOverhead schedule, raft/raft_manager.go:97-98, which the engine runs by
+ * itself — this is the explicit form): every replica of the shard hosted here compacts its log to
+ * min(index, its latest snapshot index) when that is above its marker, exactly as a snapshot's
+ * compaction does (entries at or below it are gone; a follower that needs them gets InstallSnapshot);
+ * the payload stream below is released by the next tick. *compacted (nullable) = replicas compacted.
+ * RG_EINVAL for a shard outside this engine. Synchronises. */
+int rg_compact(rg_engine* e, uint64_t group, uint64_t index, uint32_t* compacted);
 /* Whole-table digest of this engine's replicas: out[0] = the sum over replicas of an
  * fmix64 chain over the replica's rg_replica_view fields (remotes of slots < replicas), out[1] = the
  * sum of a chain over its log entries (marker, last] (term, then type | len << 8 | crc << 32), each

@@ -266,6 +266,29 @@ __global__ void notify_applied_kernel(AdminParams a, const uint32_t* rids, const
   }
 }
 
+// rg_compact: a lane per slot of the shard. Between ticks the next step's input state is
+// s64_in; the marker moves there as a snapshot's compaction moves it at the end of a step, and S_FIDX
+// makes the next step release the payload stream below entry c + 1 ("Release")
+__global__ void compact_kernel(AdminParams a, uint64_t group, uint64_t index, uint32_t* n) {
+  const uint32_t s = threadIdx.x;
+  const TickParams& t = a.t;
+  if (s >= t.R || pl_rank_of(t.pl, group, s) != t.pl.rank) return;
+  const uint64_t j = group / t.pl.N - t.pl.col_base, q = (uint64_t)s * t.G + j, N = t.nrep;
+  uint64_t* s64 = ((uint64_t*)(t.s64_in)) + q;
+  const uint64_t marker = s64[S_MARKER * N], snap = s64[S_SNAP_INDEX * N];
+  const uint64_t c = index < snap ? index : snap;  // snap <= applied <= committed <= last: c is in the ring
+  if (c <= marker) return;
+  s64[S_MARKER_TERM * N] = t.tr[(c & (t.L - 1)) * N + q] & TERM_MASK;
+  s64[S_MARKER * N] = c;
+  s64[S_FIDX * N] = c + 1;
+  atomicAdd(n, 1u);
+}
+
+hipError_t launch_compact(const AdminParams& a, uint64_t group, uint64_t index, uint32_t* n, hipStream_t s) {
+  hipLaunchKernelGGL(compact_kernel, dim3(1), dim3(64), 0, s, a, group, index, n);
+  return hipGetLastError();
+}
+
 hipError_t launch_notify_applied(const AdminParams& a, const uint32_t* rids, const uint64_t* index, uint32_t n,
                                  int pass, uint32_t* bad, hipStream_t s) {
   if (!n) return hipSuccess;

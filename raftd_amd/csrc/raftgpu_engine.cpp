@@ -2333,6 +2333,23 @@ int rg_notify_applied(rg_engine* e, const uint32_t* rids, const uint64_t* index,
   return RG_OK;
 }
 
+int rg_compact(rg_engine* e, uint64_t group, uint64_t index, uint32_t* compacted) {
+  if (!e) return fail(RG_EINVAL, "rg_compact args");
+  const uint32_t N = e->pl.N;
+  const uint64_t g0 = (uint64_t)N * e->pl.col_base, gn = (uint64_t)N * e->c.groups;
+  if (group < g0 || group >= g0 + gn) return fail(RG_EINVAL, "rg_compact: shard outside this engine");
+  if (int jrc = join(e)) return jrc;
+  HIPCHK(hipSetDevice(e->c.device));
+  uint32_t* d = (uint32_t*)e->d_sum;
+  HIPCHK(hipMemsetAsync(d, 0, 4, e->stream));
+  HIPCHK(launch_compact(admin(e), group, index, d, e->stream));
+  uint32_t n = 0;
+  HIPCHK(hipMemcpyAsync(&n, d, 4, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  if (compacted) *compacted = n;
+  return RG_OK;
+}
+
 int rg_global_id(rg_engine* e, uint32_t rid, uint64_t* group, uint64_t* global_rid) {
   if (!e || rid >= e->nrep) return fail(RG_EINVAL, "rg_global_id: bad replica");
   const uint32_t R = e->c.replicas, j = rid / R, s = rid % R;

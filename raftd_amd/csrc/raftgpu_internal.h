@@ -511,6 +511,9 @@ hipError_t launch_scatter_replica(const AdminParams& a, uint32_t rid, const void
 hipError_t launch_deliver(const AdminParams& a, uint32_t rid_src, const void* hdr, uint32_t* status,
                           hipStream_t s);
 // rg_notify_applied: check (pass 0: *bad = number of rids / indices out of range) or set (pass 1) applied
+// rg_compact: every replica of global shard `group` hosted here compacts to min(index, its snap_index)
+// when that is above its marker; *n (device, zeroed by the caller) counts them
+hipError_t launch_compact(const AdminParams& a, uint64_t group, uint64_t index, uint32_t* n, hipStream_t s);
 hipError_t launch_notify_applied(const AdminParams& a, const uint32_t* rids, const uint64_t* index, uint32_t n,
                                  int pass, uint32_t* bad, hipStream_t s);
 // rg_digest: out[0] += Σ view chains, out[1] += Σ log chains (out zeroed by the caller)

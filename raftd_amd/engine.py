@@ -196,7 +196,7 @@ EXPORTS = ["rg_create", "rg_destroy", "rg_bootstrap", "rg_fill_slabs", "rg_tick"
            "rg_notify_applied", "rg_apply_async", "rg_apply_wait", "rg_read_index", "rg_read_index_results",
            "rg_config_change", "rg_wire_exchange", "rg_rccl_unique_id", "rg_rccl_open", "rg_rccl_close",
            "rg_pool_stats", "rg_get_update", "rg_commit_update", "rg_tick_device_n", "rg_digest",
-           "rg_host_register", "rg_host_unregister", "rg_wire_plan_fixed", "rg_wire_dropped"]
+           "rg_host_register", "rg_host_unregister", "rg_wire_plan_fixed", "rg_wire_dropped", "rg_compact"]
 
 _lib = None
 
@@ -245,6 +245,7 @@ def load_library(path: str = LIB_PATH):
         "rg_apply_async": ([vp, u32, i32], i32),
         "rg_read_index": ([vp, C.POINTER(ReadRequest), C.c_size_t], i32),
         "rg_config_change": ([vp, u64, u32, u32, u32], i32),
+        "rg_compact": ([vp, u64, u64, C.POINTER(C.c_uint32)], i32),
         "rg_read_index_results": ([vp, u32, vp, u64, C.POINTER(C.c_uint64)], i32),
         "rg_apply_wait": ([vp, i32, C.POINTER(vp), C.POINTER(vp), C.POINTER(C.c_uint64)], i32),
         "rg_deliver": ([vp, u32, C.POINTER(MsgView)], i32),
@@ -536,6 +537,13 @@ class Engine:
     def read_ready(self, rid):
         """(ctx, index) made ready for local replica rid in the last tick, or None."""
         return self.read_ready_all().get(rid)
+
+    def compact(self, group, index) -> int:
+        """rg_compact: compact every local replica of global shard `group` to min(index, its snap_index);
+        returns how many were compacted."""
+        n = C.c_uint32()
+        self._check(self.L.rg_compact(self.h, group, index, C.byref(n)))
+        return n.value
 
     def notify_applied(self, rids, index):
         """rg_notify_applied (Peer.NotifyRaftLastApplied) for local replicas rids."""

@@ -638,3 +638,38 @@ def test_digest_definition_and_windows():
     s = [sum(x) & ((1 << 64) - 1) for x in zip(*(o.digest() for o in halves))]
     assert tuple(s) == d
     assert whole.replica(0)["snap_index"] > 0  # compaction happened: the log chains start above a marker
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_compact_c_matches_python(seed):
+    """rg_compact's restatement (or_compact / Sim.compact): between ticks random shards compact to a
+    random index — capped at each replica's snapshot index, ignored at or below its marker — and both
+    restatements agree on the count, every replica, message and entry (lagging followers then get
+    InstallSnapshot; the stream below is released by the next step)."""
+    G, R = 4, [3, 5, 3, 2][seed]
+    kw = dict(groups=G, replicas=R, payload_bytes=16, max_entries_per_msg=8, log_capacity=64, snapshot_entries=12,
+              compaction_overhead=5, drop_ppm=100000, seed=700 + seed)
+    a, b = make("c", **kw), make("py", **kw)
+    a.bootstrap()
+    b.bootstrap()
+    rng = np.random.default_rng(seed)
+    moved = 0
+    for t in range(120):
+        for g in range(G):
+            if rng.random() < 0.3:
+                idx = int(rng.integers(0, a.replica(g * R)["committed"] + 6))
+                na, nb = a.compact(g, idx), b.compact(g, idx)
+                assert na == nb, (seed, t, g, idx)
+                moved += na
+        assert a.compact(G, 5) == -1 and b.compact(G, 5) == -1
+        ins = random_inputs(rng, G, R, 8)
+        a.tick(*ins)
+        b.tick(*ins)
+        for rid in range(G * R):
+            va = a.replica(rid)
+            assert va == b.replica(rid), (seed, t, rid)
+            for d in range(R):
+                assert a.msgs(rid, d) == b.msgs(rid, d), (seed, t, rid, d)
+            for i in range(va["marker"] + 1, va["last"] + 1):
+                assert a.entry(rid, i) == b.entry(rid, i), (seed, t, rid, i)
+    assert moved > 10
