@@ -33,6 +33,12 @@ struct Host {
   std::vector<uint16_t> cc;  // membership change staging: slot | descriptor << 8
   bool cc_staged = false;
   uint64_t t = 0;
+  // wire_all (rg_config.wire_all): every plane is remote, so the step reads the remote inbox planes
+  // (rhdr / rmt / rcnt) that unpack_kernel writes on the device; emulate_wire fills them from the last
+  // step's outbox as pack_kernel + unpack_kernel would (the control step's view of the wire)
+  bool wire = false;
+  std::vector<uint64_t> rhdr, rmt;
+  std::vector<uint32_t> rcnt;
 };
 
 static TickParams params(Host* h) {
@@ -47,7 +53,13 @@ static TickParams params(Host* h) {
   p.JS = c.join_slots;
   p.IM = c.initial_members;
   p.info = h->info.data();
-  p.pl = make_placement(1, 0, 0);  // one rank: every plane local
+  p.pl = make_placement(1, 0, h->wire ? 1u : 0u);  // one rank: every plane local, or (wire_all) remote
+  p.wire = h->wire ? 1u : 0u;  // a wire engine's slab rows are per replica
+  if (h->wire) {
+    p.rhdr = h->rhdr.data();
+    p.rmt = h->rmt.data();
+    p.rcnt = h->rcnt.data();
+  }
   const int a = (int)(h->t & 1), b = a ^ 1;
   p.s64_in = h->s64[a].data(); p.s64_out = h->s64[b].data();
   p.s32_in = h->s32[a].data(); p.s32_out = h->s32[b].data();
@@ -97,7 +109,13 @@ void* ch_create(const rg_config* c) {
   h->job64.assign(J64_ROWS * J * n, 0);
   h->job32.assign(J32_ROWS * J * n, 0);
   h->jcnt.assign(n, 0);
-  h->slab_info.assign((size_t)c->num_slabs * G * E, make_uint2(0u, c->payload_bytes));
+  h->wire = c->wire_all != 0;
+  h->slab_info.assign((size_t)c->num_slabs * (h->wire ? n : G) * E, make_uint2(0u, c->payload_bytes));
+  if (h->wire) {
+    h->rhdr.assign(8 * R * R * K * G, 0);
+    h->rmt.assign(R * R * K * E * G, 0);
+    h->rcnt.assign(R * R * G, 0);
+  }
   h->rdst.assign((size_t)RD_ROWS * n, 0);
   h->pt.assign(G, 0xFF);
   h->pc.assign(G, 0);
@@ -175,6 +193,57 @@ static void after_step(Host* h, const TickParams& p) {
     }
   }
 }
+// What pack_kernel + the transfer + unpack_kernel leave for the next step's control kernel when every
+// plane is remote (raftgpu_wire.hip): the remote inbox planes. Headers are copied; a Replicate's inline
+// words expanded per entry (a uniform one's single word repeated); a forwarded Propose's words are its
+// Cmds' length bits from the forwarder's slab row and its header word 4 their stream chunks; word 7 of a
+// message with entries = a 16-B aligned offset of its records in one receive buffer, | RG_UNIFORM for a
+// Replicate whose records all hold one application ring word. The payload bytes themselves (the bulk
+// kernel's input) are not emulated.
+static void emulate_wire(Host* h, const TickParams& p) {
+  const uint64_t G = p.G, R = p.R, K = p.K, E = p.E, n64 = p.nrep, plane = R * R * K * G;
+  const uint32_t maxc = h->c.max_cmd_bytes ? h->c.max_cmd_bytes : h->c.payload_bytes;
+  uint64_t off = 256;
+  for (uint64_t col = 0; col < R * R; ++col) {
+    const uint64_t s = col / R, d = col % R;
+    for (uint64_t j = 0; j < G; ++j) {
+      uint32_t c = s == d ? 0u : p.cnt_in[col * G + j];
+      if (c > K) c = 0;
+      h->rcnt[col * G + j] = c;
+      for (uint32_t k = 0; k < c; ++k) {
+        const uint64_t* hs = p.hdr_in + (col * K + k) * G + j;
+        uint64_t* ho = h->rhdr.data() + (col * K + k) * G + j;
+        const uint64_t w0 = hs[0], w7 = hs[7 * plane];
+        const uint32_t type = (uint32_t)(w0 & 0xFF);
+        const uint32_t n = (type == M_REPLICATE || (type == M_PROPOSE && p.P)) ? (uint32_t)(w0 >> 32) : 0u;
+        const bool uni = type == M_REPLICATE && ((uint32_t)w7 & RG_UNIFORM);
+        const uint64_t* mts = p.mt_in + ((col * K + k) * E) * G + j;
+        uint64_t* mto = h->rmt.data() + ((col * K + k) * E) * G + j;
+        bool same = n > 0;
+        uint64_t first = 0;
+        uint32_t tot = 0;
+        for (uint32_t e = 0; e < n; ++e) {
+          uint64_t word;
+          if (type == M_PROPOSE) {
+            const uint32_t sl = (uint32_t)w7, len = h->slab_info[(((uint64_t)sl * n64) + s * G + j) * E + e].y;
+            word = len_bits(len < maxc ? len : maxc);
+          } else {
+            word = mts[(uni ? 0 : (uint64_t)e) * G];
+          }
+          if (e == 0) first = word;
+          same = same && word == first && !(word & TYPE_BIT);
+          tot += word_nc(word);
+          mto[(uint64_t)e * G] = type == M_PROPOSE ? (word & ~TERM_MASK & ~BANK_BIT & ~TYPE_BIT) : word;
+        }
+        for (int x = 0; x < 7; ++x) ho[x * plane] = hs[x * plane];
+        if (type == M_PROPOSE) ho[4 * plane] = tot;
+        ho[7 * plane] = n ? (off | (type == M_REPLICATE && same ? (uint64_t)RG_UNIFORM : 0ull)) : w7;
+        off += 64 + 16ull * (n + tot);
+      }
+    }
+  }
+}
+
 // the product's fast step (control_fast_kernel / control_fastfb_kernel): the role-specialised Ctl,
 // lean (fast mode 1, the large-engine kernel) or the latency build (fast mode 2, small engines)
 extern "C++" {
@@ -210,6 +279,7 @@ int ch_tick(void* hh, const rg_tick_input* in) {
     p.prop_cmd = h->pcmd.data();
   }
   if (h->cc_staged) p.cc_in = h->cc.data();
+  if (h->wire) emulate_wire(h, p);
   for (uint32_t q = 0; q < h->nrep; ++q) {
     switch (h->c.replicas) {
 #define RG_CASE(r)                 \
@@ -264,7 +334,8 @@ int ch_propose(void* hh, const rg_proposal* props, uint64_t n, const uint32_t* l
     for (uint32_t x = 0; x < b.count; ++x) {
       const uint32_t at = h->pc[b.group] + x, ln = lens[b.first + x];
       if (ln && P) h->hm[b.group] |= 1ull << at;
-      h->slab_info[(slab * h->c.groups + b.group) * E + at] = make_uint2(0u, ln);
+      const uint64_t row = h->wire ? (uint64_t)b.slot * h->c.groups + b.group : b.group;  // wire: per replica
+      h->slab_info[(slab * (h->wire ? h->nrep : h->c.groups) + row) * E + at] = make_uint2(0u, ln);
       if (P) h->pcmd[b.group].x += (ln + 15) / 16;  // not contiguous: the bulk kernel is not emulated
     }
     h->pt[b.group] = (uint8_t)b.slot;

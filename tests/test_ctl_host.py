@@ -25,12 +25,13 @@ def inputs(rng, G, R, emax):
     return pt, pc, camp, iso
 
 
-def xcheck(kind, seed, G, R, T, p_cc=0.0, **cfg):
-    """p_cc: per group and tick, the probability of a membership change."""
+def xcheck(kind, seed, G, R, T, p_cc=0.0, wire_all=0, **cfg):
+    """p_cc: per group and tick, the probability of a membership change. wire_all: the
+    control step reads every message from the remote inbox planes (the harness emulates the wire)."""
     kw = dict(groups=G, replicas=R, payload_bytes=16, max_entries_per_msg=8, log_capacity=64,
               snapshot_entries=20, compaction_overhead=5, drop_ppm=150000, seed=seed)
     kw.update(cfg)
-    a, b = make(kind, **kw), make("c", **kw)
+    a, b = make(kind, wire_all=wire_all, **kw), make("c", **kw)
     a.bootstrap()
     b.bootstrap()
     rng = np.random.default_rng(seed)
@@ -57,6 +58,15 @@ def test_control_step_matches_oracle(R):
     xcheck("ctl", 10 + R, G=5, R=R, T=120)
 
 
+@pytest.mark.parametrize("R", [2, 3, 5, 8])
+@pytest.mark.parametrize("kind", ["ctl", "ctl-fast"])
+def test_control_step_over_the_wire_matches_oracle(kind, R):
+    """Every plane remote (wire_all; the harness emulates pack + unpack): the step's remote-inbox
+    paths — rhdr / rmt / rcnt, uniform WIRE appends on the fast path, records offsets, forwarded
+    Proposes with their length words — equal the oracle, with and without the fast path."""
+    xcheck(kind, 50 + R, G=5, R=R, T=120, wire_all=1, p_cc=0.03 if R > 2 else 0.0)
+
+
 @pytest.mark.parametrize("R", [1, 2, 3, 5, 8])
 def test_fast_path_matches_oracle(R):
     """The fast-path step (Ctl<R, true>: the steady-state branches, handing every other step to the
@@ -75,14 +85,15 @@ def test_fast_path_membership_and_heavy_loss():
     xcheck("ctl-fast", 88, G=6, R=5, T=160, drop_ppm=300000, max_msgs_per_pair=4, p_cc=0.05)
 
 
-@pytest.mark.parametrize("R,P", [(3, 256), (5, 64), (3, 0)])
-def test_fast_path_covers_the_steady_state(R, P):
+@pytest.mark.parametrize("R,P,wire", [(3, 256, 0), (5, 64, 0), (3, 0, 0), (3, 256, 1), (5, 64, 1)])
+def test_fast_path_covers_the_steady_state(R, P, wire):
     """Steady-state leaders with a full batch every tick (the benchmark's workload, snapshots and
-    compaction included): after the election no replica's step leaves the fast path."""
+    compaction included): after the election no replica's step leaves the fast path — with every
+    message over the wire too (wire: the multi-GPU step's inbox)."""
     G, E = 8, 16
     kw = dict(groups=G, replicas=R, payload_bytes=P, max_entries_per_msg=E, log_capacity=256,
               snapshot_entries=100, compaction_overhead=5, seed=9)
-    a, b = make("ctl-fast", **kw), make("c", **kw)
+    a, b = make("ctl-fast", wire_all=wire, **kw), make("c", **kw)
     for e in (a, b):
         e.bootstrap()
     camp = np.zeros(G * R, np.uint8)
@@ -138,6 +149,8 @@ def test_control_step_under_asan():
             "t.xcheck('ctl-asan', 5, G=3, R=3, T=60); t.xcheck('ctl-asan', 6, G=2, R=5, T=60); "
             "t.xcheck('ctl-asan', 7, G=3, R=8, T=80, p_cc=0.08); "
             "t.xcheck('ctl-fast-asan', 8, G=3, R=3, T=80, p_cc=0.05); t.xcheck('ctl-fast-asan', 9, G=2, R=5, T=60); "
+            "t.xcheck('ctl-asan', 11, G=3, R=5, T=60, wire_all=1, p_cc=0.05); "
+            "t.xcheck('ctl-fast-asan', 12, G=3, R=5, T=60, wire_all=1); t.xcheck('ctl-fast-asan', 13, G=2, R=8, T=60, wire_all=1); "
             "import kat_scenarios as K; fx = K.load('kat_check_msgapp.json'); "
             "[K.run_check_msgapp('ctl-asan', fx, c) for c in fx['cases']]; print('ASAN-CLEAN')"
             % (HERE, os.path.dirname(HERE)))
