@@ -256,29 +256,33 @@ def hbm_copy_ceiling(eng, nbytes=2 << 30, reps=10):
 
 def apply_copyback(eng, torch, slot_mask=1):
     """rg_apply_committed after the last timed tick: the entries the node hosting the slot-0
-    replicas hands to /UpdateEntries, gathered on the device and copied back into pinned host
-    buffers. Host wall time of the whole call (count + scan + gather + D2H + sync)."""
+    replicas hands to /UpdateEntries, gathered on the device as runs (a 48-B head per run of
+    consecutive indices, 8 B of {len, crc} per entry) plus the packed Cmds, and copied back into
+    engine-owned pinned memory. Host wall time of the whole call (count + scan + gather + D2H + sync)."""
     import ctypes as C
-    from raftd_amd.engine import APPLY_DTYPE
-    n, pb = C.c_uint64(), C.c_uint64()
-    eng.L.rg_apply_committed(eng.h, slot_mask, None, None, 0, C.byref(n), 0, C.byref(pb))
-    cnt, nbytes = n.value, pb.value
-    if cnt == 0:
-        return None
-    recs = torch.empty(cnt * APPLY_DTYPE.itemsize, dtype=torch.uint8, pin_memory=True)
-    pay = torch.empty(max(nbytes, 16), dtype=torch.uint8, pin_memory=True)
+    from raftd_amd.engine import ApplyBatch
+    b = ApplyBatch()
     best = None
     for _ in range(3):
         t0 = time.perf_counter()
-        rc = eng.L.rg_apply_committed(eng.h, slot_mask, recs.data_ptr(), pay.data_ptr(), cnt, C.byref(n),
-                                      pay.numel(), C.byref(pb))
+        rc = eng.L.rg_apply_committed(eng.h, slot_mask, C.byref(b))
         dt = time.perf_counter() - t0
         if rc < 0:
             return None
         best = dt if best is None else min(best, dt)
-    nb = cnt * APPLY_DTYPE.itemsize + pb.value
-    return {"slot_mask": slot_mask, "entries": cnt, "bytes": nb, "ms": best * 1e3, "GBps": nb / best / 1e9,
-            "note": "count + scan + gather kernels (Cmds packed at their own length), then one hipMemcpyAsync per array into pinned host memory"}
+    if not b.n_entries:
+        return None
+    nb = batch_bytes(b)
+    return {"slot_mask": slot_mask, "entries": b.n_entries, "runs": b.n_runs, "bytes": nb, "ms": best * 1e3,
+            "GBps": nb / best / 1e9,
+            "note": "count + scan + gather kernels (runs + {len, crc} per entry + Cmds packed at their own "
+                    "length), then one hipMemcpyAsync into pinned host memory"}
+
+
+def batch_bytes(b) -> int:
+    """Bytes an rg_apply_batch moves over PCIe: run heads, {len, crc} per entry, Cmds (16-B aligned)."""
+    a16 = lambda x: (x + 15) // 16 * 16  # noqa: E731
+    return a16(b.n_runs * 48) + a16(b.n_entries * 8) + b.payload_bytes
 
 
 def e2e_with_apply(eng, tick, G, steps, slot_mask=1, serial=False):
@@ -287,25 +291,26 @@ def e2e_with_apply(eng, tick, G, steps, slot_mask=1, serial=False):
     D2H copy on the copy stream, double-buffered, so copies overlap the next ticks; the host waits
     for each tick's copy one tick later. Bounded by min(tick rate, PCIe rate)."""
     import torch
-    from raftd_amd.engine import APPLY_DTYPE
     n = nb = 0
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+
+    def done(buf):
+        runs, cmds, pk = eng.apply_wait(buf, copy=False)
+        return len(cmds), ((len(runs) * 48 + 15) // 16 + (len(cmds) * 8 + 15) // 16) * 16 + pk.size
+
     for i in range(steps):
         tick()
         eng.apply_async(slot_mask, i & 1)
         if serial:  # the copy completes before the next tick is issued
-            r, pk = eng.apply_wait(i & 1, copy=False)
-            n += len(r)
-            nb += len(r) * APPLY_DTYPE.itemsize + pk.size
+            a, b = done(i & 1)
+            n, nb = n + a, nb + b
         elif i:
-            r, pk = eng.apply_wait((i - 1) & 1, copy=False)
-            n += len(r)
-            nb += len(r) * APPLY_DTYPE.itemsize + pk.size
+            a, b = done((i - 1) & 1)
+            n, nb = n + a, nb + b
     if not serial:
-        r, pk = eng.apply_wait((steps - 1) & 1, copy=False)
-        n += len(r)
-        nb += len(r) * APPLY_DTYPE.itemsize + pk.size
+        a, b = done((steps - 1) & 1)
+        n, nb = n + a, nb + b
     el = time.perf_counter() - t0
     return {"value": G * steps / el, "unit": "group-steps/s", "steps": steps, "ms_per_step": el * 1e3 / steps,
             "entries_per_step": n / steps, "bytes_per_step": nb / steps, "pcie_GBps": nb / el / 1e9,
@@ -355,8 +360,8 @@ def hand_off(eng, tick, G, steps, slot_mask=1):
         tick()
         if eng.L.rg_get_update(eng.h, slot_mask, UPDATE_ALL, C.byref(u)) != 0:
             raise RuntimeError(f"rg_get_update: {eng.L.rg_last_error().decode()}")
-        ne += u.n_entries + u.n_committed
-        nb += u.entry_payload_bytes + u.committed_payload_bytes
+        ne += u.n_entries + u.committed.n_entries
+        nb += u.entry_payload_bytes + u.committed.payload_bytes
         if eng.L.rg_commit_update(eng.h, C.byref(u), COMMIT_APPLIED) != 0:
             raise RuntimeError(f"rg_commit_update: {eng.L.rg_last_error().decode()}")
     el = time.perf_counter() - t0

@@ -181,19 +181,38 @@ typedef struct rg_traffic {
   uint64_t bulk_bytes;
 } rg_traffic;
 
-/* One entry of the committed-entry copy-back (rg_apply_committed): what dragonboat hands to
- * IOnDiskStateMachine.Update and raftd forwards as {"Index", "Cmd"} to POST /UpdateEntries with
- * headers raftd-node-id = shard, raftd-replica-id = replica (raft/state_machine.go:63-99,126-166). */
-typedef struct rg_apply_entry {
-  uint64_t index;      /* statemachine.Entry.Index */
+/* The committed-entry copy-back (rg_apply_committed / rg_apply_wait / rg_get_update): what dragonboat
+ * hands to IOnDiskStateMachine.Update and raftd forwards as {"Index", "Cmd"} to POST /UpdateEntries
+ * with headers raftd-node-id = shard, raftd-replica-id = replica (raft/state_machine.go:63-99,126-166),
+ * shipped as RANGES: one rg_apply_run per run of consecutive entry indices of one replica, and per
+ * entry only its Cmd's length and CRC (rg_apply_cmd, 8 B). Entry k of run r (0 <= k < r.count) is
+ * Entry.Index r.first + k with length cmds[r.entry + k].len; its Cmd starts at payload + r.off +
+ * the sum over the run's earlier entries of their lengths rounded up to 16 B (Cmds are packed back to
+ * back, each rounded up to 16 B). A replica's runs come in index order, its entries contiguous in
+ * cmds; a replica's window (processed at step start, processed] yields one run unless empty
+ * entries (leader no-ops, config changes) split it. */
+typedef struct rg_apply_run {
   uint64_t group;      /* global shard id (raftd-node-id) */
   uint32_t replica_id; /* raftd-replica-id: slot + 1 */
-  uint32_t len;        /* Cmd bytes, at payload + off */
-  uint32_t crc;        /* CRC-32 of Cmd as stored in the log */
   uint32_t rid;        /* local replica id */
-  uint64_t off;        /* byte offset of the Cmd in the payload buffer (Cmds packed back to back, each
-                          rounded up to 16 B) */
-} rg_apply_entry;
+  uint64_t first;      /* statemachine.Entry.Index of the run's first entry */
+  uint64_t entry;      /* its position in the rg_apply_cmd array */
+  uint64_t off;        /* byte offset of its first Cmd in the payload buffer */
+  uint32_t count;      /* entries in the run (>= 1) */
+  uint32_t _pad;
+} rg_apply_run;
+typedef struct rg_apply_cmd {
+  uint32_t len;        /* Cmd bytes */
+  uint32_t crc;        /* CRC-32 of the Cmd as stored in the log */
+} rg_apply_cmd;
+typedef struct rg_apply_batch {
+  const rg_apply_run* runs;
+  uint64_t n_runs;
+  const rg_apply_cmd* cmds;
+  uint64_t n_entries;
+  const uint8_t* payload;
+  uint64_t payload_bytes;
+} rg_apply_batch;
 
 /* Persistence feed (rg_persist_collect): dragonboat's Update.EntriesToSave + pb.State + snapshot
  * metadata, which it makes durable (LogDB SaveRaftState, fsync) before a step's messages leave. */
@@ -423,13 +442,11 @@ int rg_rccl_close(rg_transport* t);
  * replicas whose slot bit is set in slot_mask applied in the last tick — config changes, leader
  * no-ops and snapshot-restored ranges excluded, as dragonboat's rsm does before Update — grouped
  * by replica in device order (slot by slot, shards ascending within a slot), each replica's
- * entries in index order. Compacted on the device, then copied back by one hipMemcpyAsync
- * per array into entries[cap] and payload[pay_cap] (host memory; pinned is fastest): the Cmds
- * packed back to back, each rounded up to 16 B (rg_apply_entry.off), so only Cmd bytes cross PCIe.
- * *n = the count, *pay_bytes = the payload bytes; if either exceeds its cap nothing is copied and
- * RG_EFULL is returned. Synchronous. */
-int rg_apply_committed(rg_engine* e, uint32_t slot_mask, rg_apply_entry* entries, uint8_t* payload, uint64_t cap,
-                       uint64_t* n, uint64_t pay_cap, uint64_t* pay_bytes);
+ * entries in index order, as runs (rg_apply_run / rg_apply_cmd above). Compacted on the device, then
+ * copied back by one hipMemcpyAsync into engine-owned pinned memory: *out points into it, valid until
+ * the next rg_apply_committed; only run heads, 8 B per entry and the Cmd bytes cross PCIe.
+ * Synchronous. */
+int rg_apply_committed(rg_engine* e, uint32_t slot_mask, rg_apply_batch* out);
 /* Asynchronous, double-buffered copy-back (the same batch as rg_apply_committed) into engine-owned
  * pinned buffer `buf` (0 or 1). On the engine's stream right after the tick (before a later tick can
  * reuse the window's log slots and pages): the count and scan kernels, then ONE host synchronisation
@@ -440,9 +457,9 @@ int rg_apply_committed(rg_engine* e, uint32_t slot_mask, rg_apply_entry* entries
  * next tick before it completes. Whether that overlap pays depends on the platform (DESIGN.md §7,
  * INTEGRATION.md "Copy-back schedule"). */
 int rg_apply_async(rg_engine* e, uint32_t slot_mask, int buf);
-/* Wait for buffer `buf`'s gather; *entries / *payload (rg_apply_entry.off into it) point into
- * engine-owned pinned memory, valid until the next rg_apply_async into `buf`; *n = the count. */
-int rg_apply_wait(rg_engine* e, int buf, const rg_apply_entry** entries, const uint8_t** payload, uint64_t* n);
+/* Wait for buffer `buf`'s gather; *out points into engine-owned pinned memory, valid until the next
+ * rg_apply_async into `buf`. */
+int rg_apply_wait(rg_engine* e, int buf, rg_apply_batch* out);
 /* Host WAL feed: for every replica whose log or hard state changed in the last
  * tick (full != 0, or no tick yet: every replica, whole log window), one rg_persist_state and the
  * entries it rewrote, their Cmds packed (rg_persist_entry.off), gathered on the device and copied back
@@ -479,10 +496,7 @@ typedef struct rg_update {
   uint64_t n_entries;
   const uint8_t* entry_payload;           /* rg_persist_entry.off into it */
   uint64_t entry_payload_bytes;
-  const rg_apply_entry* committed;
-  uint64_t n_committed;
-  const uint8_t* committed_payload;       /* rg_apply_entry.off into it */
-  uint64_t committed_payload_bytes;
+  rg_apply_batch committed;               /* the committed entries, as runs (rg_apply_run) */
   const rg_snapshot_event* snapshots;
   uint64_t n_snapshots;
   const rg_read_ready* reads;

@@ -9,8 +9,13 @@
 // Update()d — into one contiguous batch so that only newly committed data crosses PCIe, in a
 // single hipMemcpyAsync per array.
 //
-// count_kernel   thread per replica: entries to hand over (coalesced term-ring reads, [L][nrep])
-// gather_kernel  wave per replica: ballot-compacted records + 16-B-per-lane payload copies
+// The batch is ranges, not records: one rg_apply_run per run of consecutive indices (group, replica,
+// first index, where its {len, crc} and Cmds start) and 8 B per entry (len, crc) — the index, shard and
+// replica of every entry are implied (r05; r04 shipped a 40-B rg_apply_entry per entry).
+//
+// count_kernel   thread per replica: entries, Cmd chunks and runs to hand over (coalesced [L][nrep] reads)
+// gather_kernel  wave per replica: ballot-compacted {len, crc} + run heads, 16-B-per-lane payload copies
+// runs_kernel    thread per run: its count (the next run of the replica, or the replica's end, minus it)
 #include "../../include/raftgpu.h"
 #include "raftgpu_internal.h"
 
@@ -58,37 +63,45 @@ __global__ void apply_count_kernel(ApplyParams a) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= a.nrep) return;
   const uint32_t s = q / a.G;
-  uint32_t c = 0, cc = 0;
+  uint32_t c = 0, cc = 0, rc = 0;
   if ((a.slot_mask >> s) & 1u) {
     const uint64_t hi = a.s64[(uint64_t)S_PROCESSED * a.nrep + q];
+    bool prev = false;
     for (uint64_t i = a.apply_lo[q] > 0 ? a.apply_lo[q] : 1; i <= hi; ++i) {
       const uint64_t w = a.tr[(i & (a.L - 1)) * a.nrep + q];
-      if (applies(w)) {
+      const bool sel = applies(w);
+      if (sel) {
         c += 1;
         cc += word_nc(w);
+        rc += prev ? 0u : 1u;
       }
+      prev = sel;
     }
   }
   a.cnt[q] = c;
   a.ccnt[q] = cc;
+  a.rcnt[q] = rc;
 }
 
 __global__ void apply_total_kernel(const uint64_t* off, uint32_t n, uint64_t* total) { *total = off[n]; }
-__global__ void totals2_kernel(const uint64_t* a, const uint64_t* b, uint32_t n, uint64_t* out) {
+__global__ void totals3_kernel(const uint64_t* a, const uint64_t* b, const uint64_t* c, uint32_t n, uint64_t* out) {
   out[0] = a[n];
   out[1] = b[n];
+  out[2] = c[n];
 }
 
 hipError_t launch_apply_count(const ApplyParams& a, uint64_t* totals, hipStream_t st) {
   hipLaunchKernelGGL(apply_count_kernel, dim3((a.nrep + 255) / 256), dim3(256), 0, st, a);
   hipError_t r = launch_scan_u32(a.cnt, a.nrep, a.bsum, a.off, st);
   if (r == hipSuccess) r = launch_scan_u32(a.ccnt, a.nrep, a.bsum, a.coff, st);
+  if (r == hipSuccess) r = launch_scan_u32(a.rcnt, a.nrep, a.bsum, a.roff, st);
   if (r != hipSuccess) return r;
-  hipLaunchKernelGGL(totals2_kernel, dim3(1), dim3(1), 0, st, a.off, a.coff, a.nrep, totals);
+  hipLaunchKernelGGL(totals3_kernel, dim3(1), dim3(1), 0, st, a.off, a.coff, a.roff, a.nrep, totals);
   return hipGetLastError();
 }
 
-// wave per replica: ballot-compacted records, then the Cmds of each run of 64 candidates packed
+// wave per replica: ballot-compacted {len, crc}, a run head where a selected entry follows an
+// unselected one (or opens the window), then the Cmds of each stretch of 64 candidates packed
 __global__ void __launch_bounds__(256) apply_gather_kernel(ApplyParams a) {
   const uint32_t lane = __lane_id();
   const uint32_t q = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
@@ -97,36 +110,68 @@ __global__ void __launch_bounds__(256) apply_gather_kernel(ApplyParams a) {
   const uint64_t n64 = a.nrep, L = a.L;
   const uint64_t group = pl_group(a.pl, s, j);
   const uint64_t hi = a.s64[(uint64_t)S_PROCESSED * n64 + q];
-  uint64_t pos = a.off[q], cpos = a.coff[q];
+  uint64_t pos = a.off[q], cpos = a.coff[q], rpos = a.roff[q];
+  uint64_t carry = 0;  // 1: the candidate before this stretch was selected (its run continues)
   for (uint64_t i0 = a.apply_lo[q] > 0 ? a.apply_lo[q] : 1; i0 <= hi; i0 += 64) {
     const uint64_t i = i0 + lane;
     const uint64_t slot = i & (L - 1);
     const uint64_t w = i <= hi ? a.tr[slot * n64 + q] : 0;
     const bool sel = i <= hi && applies(w);
     const uint64_t mask = __ballot(sel);
+    const uint64_t heads = mask & ~((mask << 1) | carry);
     const uint2 inf = sel ? a.info[((w >> 63) * n64 + q) * L + slot] : make_uint2(0u, 0u);
     const uint32_t nc = sel ? word_nc(w) : 0u, inc = lane_inc_scan(nc);
+    const uint64_t below = (1ull << lane) - 1;
     if (sel) {
-      const uint64_t k = pos + __builtin_popcountll(mask & ((1ull << lane) - 1));
-      rg_apply_entry r;
-      r.index = i;
-      r.group = group;
-      r.replica_id = s + 1;
-      r.len = word_len(w);
-      r.crc = crc_of_cmd(inf.x, r.len, a.P, a.zi);  // the info word keeps the slot CRC
-      r.rid = j * a.R + s;
-      r.off = (cpos + inc - nc) * 16;
-      reinterpret_cast<rg_apply_entry*>(a.out_rec)[k] = r;
+      const uint64_t k = pos + __builtin_popcountll(mask & below);
+      rg_apply_cmd c;
+      c.len = word_len(w);
+      c.crc = crc_of_cmd(inf.x, c.len, a.P, a.zi);  // the info word keeps the slot CRC
+      reinterpret_cast<rg_apply_cmd*>(a.out_cmd)[k] = c;
+      if ((heads >> lane) & 1ull) {
+        rg_apply_run r;
+        r.group = group;
+        r.replica_id = s + 1;
+        r.rid = j * a.R + s;
+        r.first = i;
+        r.entry = k;
+        r.off = (cpos + inc - nc) * 16;
+        r.count = 0;  // runs_kernel
+        r._pad = q;   // the replica, for runs_kernel (cleared there)
+        reinterpret_cast<rg_apply_run*>(a.out_run)[rpos + __builtin_popcountll(heads & below)] = r;
+      }
     }
     const uint32_t total = (uint32_t)__shfl((int)inc, 63, 64);
     copy_run(a.pool, a.pt, a.PTS, q, inc, inf.y, total, a.out_pay, cpos);
     pos += __builtin_popcountll(mask);
+    rpos += __builtin_popcountll(heads);
     cpos += total;
+    carry = mask >> 63;
   }
 }
 
-hipError_t launch_apply_gather(const ApplyParams& a, hipStream_t st) {
+// a run's entry count: up to the next run of the same replica, else to the replica's last entry
+__global__ void apply_runs_kernel(ApplyParams a, uint64_t nruns) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nruns) return;
+  rg_apply_run* runs = reinterpret_cast<rg_apply_run*>(a.out_run);
+  const uint32_t q = runs[r]._pad;
+  const uint64_t end = r + 1 < nruns && runs[r + 1]._pad == q ? runs[r + 1].entry : a.off[q + 1];
+  runs[r].count = (uint32_t)(end - runs[r].entry);
+}
+
+__global__ void apply_runs_clear_kernel(ApplyParams a, uint64_t nruns) {  // the scratch replica field
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < nruns) reinterpret_cast<rg_apply_run*>(a.out_run)[r]._pad = 0;
+}
+
+hipError_t launch_apply_gather(const ApplyParams& a, uint64_t nruns, hipStream_t st) {
   hipLaunchKernelGGL(apply_gather_kernel, dim3((a.nrep + 3) / 4), dim3(256), 0, st, a);
+  if (nruns) {
+    const dim3 grid((uint32_t)((nruns + 255) / 256));
+    hipLaunchKernelGGL(apply_runs_kernel, grid, dim3(256), 0, st, a, nruns);
+    hipLaunchKernelGGL(apply_runs_clear_kernel, grid, dim3(256), 0, st, a, nruns);
+  }
   return hipGetLastError();
 }
 

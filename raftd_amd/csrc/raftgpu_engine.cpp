@@ -231,8 +231,8 @@ struct rg_engine {
   uint64_t x_send_cap = 0, x_recv_cap = 0;
   // committed-entry copy-back (raftgpu_apply.hip)
   uint64_t* apply_lo = nullptr;
-  uint32_t *acnt = nullptr, *accnt = nullptr;
-  uint64_t *aoff = nullptr, *acoff = nullptr, *absum = nullptr;
+  uint32_t *acnt = nullptr, *accnt = nullptr, *arcnt = nullptr;
+  uint64_t *aoff = nullptr, *acoff = nullptr, *aroff = nullptr, *absum = nullptr;
   bool copy_kernel = true;  // RAFTGPU_APPLY_MEMCPY=1: the runtime's D2H copy instead (A/B)
   SdmaCopier* sdma = nullptr;  // RAFTGPU_APPLY_SDMA=1: the D2H leg on an SDMA engine (raftgpu_sdma.cpp)
   uint8_t* astage = nullptr;
@@ -242,6 +242,9 @@ struct rg_engine {
   hipStream_t copy = nullptr;
   hipEvent_t a_gath[2] = {nullptr, nullptr}, a_copy[2] = {nullptr, nullptr};
   uint8_t* a_dev[2] = {nullptr, nullptr};
+  uint8_t* ac_host = nullptr;  // rg_apply_committed's pinned batch
+  uint64_t ac_hcap = 0;
+  uint64_t a_tot[2][3] = {};   // rg_apply_async: the batch's entries, chunks, runs per buffer
   uint8_t* a_host[2] = {nullptr, nullptr};
   uint64_t a_dcap[2] = {0, 0}, a_hcap[2] = {0, 0}, a_n[2] = {0, 0};
   bool a_used[2] = {false, false};
@@ -581,6 +584,8 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if (rc == RG_OK) rc = dalloc(e, &e->accnt, n * 4);
   if (rc == RG_OK) rc = dalloc(e, &e->aoff, (n + 1) * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->acoff, (n + 1) * 8);
+  if (rc == RG_OK) rc = dalloc(e, &e->arcnt, n * 4);
+  if (rc == RG_OK) rc = dalloc(e, &e->aroff, (n + 1) * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->absum, ((n + 1023) / 1024 + 1) * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->persist_lo, n * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->snap_ev, n * 8);
@@ -789,6 +794,7 @@ void rg_destroy(rg_engine* e) {
     if (e->a_copy[b]) (void)hipEventDestroy(e->a_copy[b]);
     if (e->a_host[b]) (void)hipHostFree(e->a_host[b]);
   }
+  if (e->ac_host) (void)hipHostFree(e->ac_host);
   if (e->stg_ev) (void)hipEventDestroy(e->stg_ev);
   if (e->rd_ev) (void)hipEventDestroy(e->rd_ev);
   if (e->cc_ev) (void)hipEventDestroy(e->cc_ev);
@@ -1923,34 +1929,58 @@ static ApplyParams apply_params(rg_engine* e, uint32_t slot_mask) {
   a.pool = e->pool; a.pt = e->pt; a.PTS = e->PTS;
   a.zi = e->crc_tab + CRC_ZI_OFF;
   a.cnt = e->acnt; a.ccnt = e->accnt; a.off = e->aoff; a.coff = e->acoff; a.bsum = e->absum;
+  a.rcnt = e->arcnt; a.roff = e->aroff;
   return a;
 }
 
-int rg_apply_committed(rg_engine* e, uint32_t slot_mask, rg_apply_entry* entries, uint8_t* payload, uint64_t cap,
-                       uint64_t* n, uint64_t pay_cap, uint64_t* pay_bytes) {
-  if (!e || !n) return fail(RG_EINVAL, "rg_apply_committed args");
+// the apply staging layout: [runs][cmds][payload], each 16-B aligned (tot: entries, chunks, runs)
+struct ApplyLayout {
+  uint64_t runs, cmds, pay, total;
+};
+static ApplyLayout apply_layout(const uint64_t* tot) {
+  ApplyLayout l;
+  l.runs = 0;
+  l.cmds = a16(tot[2] * sizeof(rg_apply_run));
+  l.pay = l.cmds + a16(tot[0] * sizeof(rg_apply_cmd));
+  l.total = l.pay + tot[1] * 16;
+  return l;
+}
+static void apply_batch(rg_apply_batch* out, const uint8_t* h, const uint64_t* tot, const ApplyLayout& l) {
+  out->runs = (const rg_apply_run*)(h + l.runs);
+  out->n_runs = tot[2];
+  out->cmds = (const rg_apply_cmd*)(h + l.cmds);
+  out->n_entries = tot[0];
+  out->payload = h + l.pay;
+  out->payload_bytes = tot[1] * 16;
+}
+
+int rg_apply_committed(rg_engine* e, uint32_t slot_mask, rg_apply_batch* out) {
+  if (!e || !out) return fail(RG_EINVAL, "rg_apply_committed args");
   if (int jrc = join(e)) return jrc;
+  *out = rg_apply_batch{};
   ApplyParams a = apply_params(e, slot_mask);
   LAUNCH(launch_apply_count(a, (uint64_t*)e->d_sum, e->stream), e->stream, "apply count");
-  uint64_t tot[2] = {0, 0};
-  HIPCHK(hipMemcpyAsync(tot, e->d_sum, 16, hipMemcpyDeviceToHost, e->stream));
+  uint64_t tot[3] = {0, 0, 0};
+  HIPCHK(hipMemcpyAsync(tot, e->d_sum, 24, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
-  *n = tot[0];
-  const uint64_t pb = tot[1] * 16;
-  if (pay_bytes) *pay_bytes = pb;
   if (tot[0] == 0) return RG_OK;
-  if (tot[0] > cap || pb > pay_cap)
-    return fail(RG_EFULL, "rg_apply_committed: " + std::to_string(tot[0]) + " entries / " + std::to_string(pb) +
-                              " payload bytes exceed the buffers");
-  if (!entries || (pb && !payload)) return fail(RG_EINVAL, "rg_apply_committed: null output");
-  const uint64_t rb = a16(tot[0] * sizeof(rg_apply_entry));
-  RGCHK(astage_reserve(e, rb + pb));
-  a.out_rec = e->astage;
-  a.out_pay = e->astage + rb;
-  LAUNCH(launch_apply_gather(a, e->stream), e->stream, "apply gather");
-  HIPCHK(hipMemcpyAsync(entries, a.out_rec, tot[0] * sizeof(rg_apply_entry), hipMemcpyDeviceToHost, e->stream));
-  if (pb) HIPCHK(hipMemcpyAsync(payload, a.out_pay, pb, hipMemcpyDeviceToHost, e->stream));
+  const ApplyLayout l = apply_layout(tot);
+  RGCHK(astage_reserve(e, l.total));
+  if (l.total > e->ac_hcap) {
+    if (e->ac_host) (void)hipHostFree(e->ac_host);
+    e->ac_host = nullptr;
+    e->ac_hcap = 0;
+    const uint64_t nb = std::max<uint64_t>(l.total * 5 / 4, 1 << 20);
+    if (hipHostMalloc((void**)&e->ac_host, nb, 0) != hipSuccess) return fail(RG_ENOMEM, "hipHostMalloc (apply)");
+    e->ac_hcap = nb;
+  }
+  a.out_run = e->astage + l.runs;
+  a.out_cmd = e->astage + l.cmds;
+  a.out_pay = e->astage + l.pay;
+  LAUNCH(launch_apply_gather(a, tot[2], e->stream), e->stream, "apply gather");
+  HIPCHK(hipMemcpyAsync(e->ac_host, e->astage, l.total, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
+  apply_batch(out, e->ac_host, tot, l);
   return RG_OK;
 }
 
@@ -1964,10 +1994,11 @@ int rg_apply_async(rg_engine* e, uint32_t slot_mask, int buf) {
   if (int jrc = join(e)) return jrc;
   ApplyParams a = apply_params(e, slot_mask);
   LAUNCH(launch_apply_count(a, (uint64_t*)e->d_sum, e->stream), e->stream, "apply count");
-  uint64_t tot[2] = {0, 0};
-  HIPCHK(hipMemcpyAsync(tot, e->d_sum, 16, hipMemcpyDeviceToHost, e->stream));
+  uint64_t tot[3] = {0, 0, 0};
+  HIPCHK(hipMemcpyAsync(tot, e->d_sum, 24, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
-  const uint64_t total = tot[0], rb = a16(total * sizeof(rg_apply_entry)), need = rb + tot[1] * 16;
+  const ApplyLayout l = apply_layout(tot);
+  const uint64_t total = tot[0], need = l.total;
   if (need > e->a_dcap[buf] || need > e->a_hcap[buf]) {  // grow: the buffer's last copy must be done
     HIPCHK(hipEventSynchronize(e->a_copy[buf]));
     if (e->sdma) sdma_wait(e->sdma, buf);
@@ -1994,13 +2025,15 @@ int rg_apply_async(rg_engine* e, uint32_t slot_mask, int buf) {
   }
   const bool prev = e->a_used[buf];
   e->a_n[buf] = total;
+  for (int k = 0; k < 3; ++k) e->a_tot[buf][k] = tot[k];
   e->a_used[buf] = true;
   if (total) {
     if (prev && e->sdma) sdma_wait(e->sdma, buf);  // its last copy has read the staging
     else if (prev) HIPCHK(hipStreamWaitEvent(e->stream, e->a_copy[buf], 0));
-    a.out_rec = e->a_dev[buf];
-    a.out_pay = e->a_dev[buf] + rb;
-    LAUNCH(launch_apply_gather(a, e->stream), e->stream, "apply gather");
+    a.out_run = e->a_dev[buf] + l.runs;
+    a.out_cmd = e->a_dev[buf] + l.cmds;
+    a.out_pay = e->a_dev[buf] + l.pay;
+    LAUNCH(launch_apply_gather(a, tot[2], e->stream), e->stream, "apply gather");
   }
   HIPCHK(hipEventRecord(e->a_gath[buf], e->stream));
   if (e->sdma) {  // the DMA engine takes the batch once the gather is done (no shader code on the copy)
@@ -2025,14 +2058,13 @@ int rg_apply_async(rg_engine* e, uint32_t slot_mask, int buf) {
   return RG_OK;
 }
 
-int rg_apply_wait(rg_engine* e, int buf, const rg_apply_entry** entries, const uint8_t** payload, uint64_t* n) {
-  if (!e || buf < 0 || buf > 1 || !n) return fail(RG_EINVAL, "rg_apply_wait args");
+int rg_apply_wait(rg_engine* e, int buf, rg_apply_batch* out) {
+  if (!e || buf < 0 || buf > 1 || !out) return fail(RG_EINVAL, "rg_apply_wait args");
   if (!e->a_used[buf]) return fail(RG_EINVAL, "rg_apply_wait: no rg_apply_async into this buffer");
   if (e->sdma) sdma_wait(e->sdma, buf);
   else HIPCHK(hipEventSynchronize(e->a_copy[buf]));
-  *n = e->a_n[buf];
-  if (entries) *entries = (const rg_apply_entry*)e->a_host[buf];
-  if (payload) *payload = e->a_host[buf] ? e->a_host[buf] + a16(e->a_n[buf] * sizeof(rg_apply_entry)) : nullptr;
+  *out = rg_apply_batch{};
+  if (e->a_n[buf]) apply_batch(out, e->a_host[buf], e->a_tot[buf], apply_layout(e->a_tot[buf]));
   return RG_OK;
 }
 
@@ -2229,16 +2261,17 @@ int rg_get_update(rg_engine* e, uint32_t slot_mask, uint32_t flags, rg_update* o
   HIPCHK(hipMemsetAsync(sum, 0, 64, e->stream));
   if (flags & RG_UPDATE_PERSIST) LAUNCH(launch_persist_count(pa, sum, e->stream), e->stream, "persist count");
   if (flags & RG_UPDATE_COMMITTED) LAUNCH(launch_apply_count(aa, sum + 3, e->stream), e->stream, "apply count");
-  if (flags & RG_UPDATE_SNAPSHOTS) LAUNCH(launch_snap_count(sa, sum + 5, e->stream), e->stream, "snapshot count");
-  if (flags & RG_UPDATE_READS) LAUNCH(launch_read_count(ra, sum + 6, e->stream), e->stream, "read count");
+  if (flags & RG_UPDATE_SNAPSHOTS) LAUNCH(launch_snap_count(sa, sum + 6, e->stream), e->stream, "snapshot count");
+  if (flags & RG_UPDATE_READS) LAUNCH(launch_read_count(ra, sum + 7, e->stream), e->stream, "read count");
   uint64_t tot[8] = {};
   HIPCHK(hipMemcpyAsync(tot, sum, 64, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   // one staging layout for every section, each 16-B aligned
+  const ApplyLayout al = apply_layout(tot + 3);  // committed: entries, chunks, runs
   const uint64_t sb = a16(tot[0] * sizeof(rg_persist_state)), eb = a16(tot[1] * sizeof(rg_persist_entry)),
-                 epb = tot[2] * 16, cb = a16(tot[3] * sizeof(rg_apply_entry)), cpb = tot[4] * 16,
-                 snb = a16(tot[5] * sizeof(rg_snapshot_event)), rdb = a16(tot[6] * sizeof(rg_read_ready));
-  const uint64_t o_e = sb, o_ep = o_e + eb, o_c = o_ep + epb, o_cp = o_c + cb, o_s = o_cp + cpb, o_r = o_s + snb,
+                 epb = tot[2] * 16, cb = al.total,
+                 snb = a16(tot[6] * sizeof(rg_snapshot_event)), rdb = a16(tot[7] * sizeof(rg_read_ready));
+  const uint64_t o_e = sb, o_ep = o_e + eb, o_c = o_ep + epb, o_s = o_c + cb, o_r = o_s + snb,
                  total = o_r + rdb;
   if (total == 0) return RG_OK;
   RGCHK(astage_reserve(e, total));
@@ -2258,15 +2291,16 @@ int rg_get_update(rg_engine* e, uint32_t slot_mask, uint32_t flags, rg_update* o
     LAUNCH(launch_persist_gather(pa, e->stream), e->stream, "persist gather");
   }
   if (tot[3]) {
-    aa.out_rec = d + o_c;
-    aa.out_pay = d + o_cp;
-    LAUNCH(launch_apply_gather(aa, e->stream), e->stream, "apply gather");
+    aa.out_run = d + o_c + al.runs;
+    aa.out_cmd = d + o_c + al.cmds;
+    aa.out_pay = d + o_c + al.pay;
+    LAUNCH(launch_apply_gather(aa, tot[5], e->stream), e->stream, "apply gather");
   }
-  if (tot[5]) {
+  if (tot[6]) {
     sa.out = d + o_s;
     LAUNCH(launch_snap_gather(sa, e->stream), e->stream, "snapshot gather");
   }
-  if (tot[6]) {
+  if (tot[7]) {
     ra.out = d + o_r;
     LAUNCH(launch_read_gather(ra, e->stream), e->stream, "read gather");
   }
@@ -2279,14 +2313,12 @@ int rg_get_update(rg_engine* e, uint32_t slot_mask, uint32_t flags, rg_update* o
   out->n_entries = tot[1];
   out->entry_payload = h + o_ep;
   out->entry_payload_bytes = epb;
-  out->committed = (const rg_apply_entry*)(h + o_c);
-  out->n_committed = tot[3];
-  out->committed_payload = h + o_cp;
-  out->committed_payload_bytes = cpb;
+  out->committed = rg_apply_batch{};
+  if (tot[3]) apply_batch(&out->committed, h + o_c, tot + 3, al);
   out->snapshots = (const rg_snapshot_event*)(h + o_s);
-  out->n_snapshots = tot[5];
+  out->n_snapshots = tot[6];
   out->reads = (const rg_read_ready*)(h + o_r);
-  out->n_reads = tot[6];
+  out->n_reads = tot[7];
   return RG_OK;
 }
 

@@ -402,8 +402,9 @@ hipError_t launch_copy_to_host(const void* src, void* dst, uint64_t bytes, hipSt
 hipError_t launch_sum_committed(const TickParams& p, unsigned long long* out, hipStream_t s);
 hipError_t launch_traffic(const TickParams& p, unsigned long long* out6, hipStream_t s);
 // committed-entry copy-back (raftgpu_apply.hip): after a tick, the application entries each replica
-// applied in it, (apply_lo - 1, applied], gathered for IOnDiskStateMachine.Update; payloads packed
-// back to back, each rounded up to 16 B (rg_apply_entry.off)
+// applied in it, (apply_lo - 1, applied], gathered for IOnDiskStateMachine.Update as runs of
+// consecutive indices (rg_apply_run) + a {len, crc} per entry (rg_apply_cmd); payloads packed back
+// to back, each rounded up to 16 B
 struct ApplyParams {
   uint32_t G, R, nrep, L, P;
   uint32_t slot_mask;       // replicas whose slot bit is set
@@ -418,13 +419,16 @@ struct ApplyParams {
   const uint32_t* zi;       // CRC inverse-shift tables (crc_of_cmd)
   uint32_t* cnt;            // [nrep] entries per replica
   uint32_t* ccnt;           // [nrep] payload chunks per replica
+  uint32_t* rcnt;           // [nrep] runs per replica
   uint64_t* off;            // [nrep + 1] exclusive scan of cnt
   uint64_t* coff;           // [nrep + 1] exclusive scan of ccnt
+  uint64_t* roff;           // [nrep + 1] exclusive scan of rcnt
   uint64_t* bsum;           // scan scratch
-  uint8_t* out_rec;         // [n] rg_apply_entry (device staging)
+  uint8_t* out_run;         // [runs] rg_apply_run (device staging)
+  uint8_t* out_cmd;         // [n] rg_apply_cmd
   uint8_t* out_pay;         // [chunks][16]
 };
-hipError_t launch_apply_count(const ApplyParams& a, uint64_t* totals /*[2]: entries, chunks*/, hipStream_t s);
+hipError_t launch_apply_count(const ApplyParams& a, uint64_t* totals /*[3]: entries, chunks, runs*/, hipStream_t s);
 // snapshot events (raftgpu_apply.hip)
 constexpr uint64_t SNAP_TAKEN_BIT = 1ull << 63;
 struct SnapParams {
@@ -474,7 +478,7 @@ struct PersistParams {
 };
 hipError_t launch_persist_count(const PersistParams& a, uint64_t* totals /*[3]: states, entries, chunks*/, hipStream_t s);
 hipError_t launch_persist_gather(const PersistParams& a, hipStream_t s);
-hipError_t launch_apply_gather(const ApplyParams& a, hipStream_t s);
+hipError_t launch_apply_gather(const ApplyParams& a, uint64_t nruns, hipStream_t s);
 // exclusive scan of n u32 into out[0..n] (out[n] = total); bsum: (n + 1023) / 1024 + 1 words
 hipError_t launch_scan_u32(const uint32_t* in, uint32_t n, uint64_t* bsum, uint64_t* out, hipStream_t s);
 

@@ -74,13 +74,54 @@ class Traffic(C.Structure):
                                           "leader_appended", "algorithmic_bytes", "bulk_bytes")]
 
 
-class ApplyEntry(C.Structure):
-    _fields_ = [("index", C.c_uint64), ("group", C.c_uint64), ("replica_id", C.c_uint32), ("len", C.c_uint32),
-                ("crc", C.c_uint32), ("rid", C.c_uint32), ("off", C.c_uint64)]
+class ApplyBatch(C.Structure):
+    """rg_apply_batch: the committed entries as runs (rg_apply_run) + {len, crc} per entry + the Cmds."""
+    _fields_ = [("runs", C.c_void_p), ("n_runs", C.c_uint64), ("cmds", C.c_void_p), ("n_entries", C.c_uint64),
+                ("payload", C.c_void_p), ("payload_bytes", C.c_uint64)]
 
 
+APPLY_RUN_DTYPE = np.dtype([("group", "<u8"), ("replica_id", "<u4"), ("rid", "<u4"), ("first", "<u8"),
+                            ("entry", "<u8"), ("off", "<u8"), ("count", "<u4"), ("_pad", "<u4")])
+APPLY_CMD_DTYPE = np.dtype([("len", "<u4"), ("crc", "<u4")])
+# one row per entry, expanded on the host from the runs (what the drivers and tests consume)
 APPLY_DTYPE = np.dtype([("index", "<u8"), ("group", "<u8"), ("replica_id", "<u4"), ("len", "<u4"),
                         ("crc", "<u4"), ("rid", "<u4"), ("off", "<u8")])
+
+
+def expand_apply(runs, cmds):
+    """APPLY_DTYPE rows (index, group, replica_id, len, crc, rid, off) from a batch's runs and per-entry
+    {len, crc}: entry k of run r is index r.first + k, its Cmd at r.off + the 16-B-rounded lengths of
+    the run's earlier entries (include/raftgpu.h, rg_apply_run)."""
+    n = len(cmds)
+    out = np.zeros(n, APPLY_DTYPE)
+    if not n:
+        return out
+    cnt = runs["count"].astype(np.int64)
+    rix = np.repeat(np.arange(len(runs)), cnt)
+    k = np.arange(n, dtype=np.int64) - np.repeat(runs["entry"].astype(np.int64), cnt)
+    out["index"] = runs["first"][rix] + k.astype(np.uint64)
+    out["group"] = runs["group"][rix]
+    out["replica_id"] = runs["replica_id"][rix]
+    out["rid"] = runs["rid"][rix]
+    out["len"] = cmds["len"]
+    out["crc"] = cmds["crc"]
+    rounded = (cmds["len"].astype(np.uint64) + 15) // 16 * 16
+    excl = np.cumsum(rounded) - rounded  # exclusive prefix over the whole batch ...
+    start = excl[runs["entry"].astype(np.int64)]  # ... minus the prefix at each run's first entry
+    out["off"] = runs["off"][rix] + excl - start[rix]
+    return out
+
+
+def batch_arrays(b: "ApplyBatch", copy: bool = True):
+    """(runs, cmds, payload) numpy arrays of an rg_apply_batch (views into engine-owned pinned memory
+    unless copy)."""
+    def arr(ptr, n, dt):
+        if not n or not ptr:
+            return np.zeros(0, dt)
+        a = np.frombuffer((C.c_uint8 * (n * dt.itemsize)).from_address(ptr), dtype=dt)
+        return a.copy() if copy else a
+    return (arr(b.runs, b.n_runs, APPLY_RUN_DTYPE), arr(b.cmds, b.n_entries, APPLY_CMD_DTYPE),
+            arr(b.payload, b.payload_bytes, np.dtype(np.uint8)))
 
 
 PERSIST_STATE_DTYPE = np.dtype([("group", "<u8"), ("replica_id", "<u4"), ("rid", "<u4"), ("term", "<u8"),
@@ -159,8 +200,7 @@ class Update(C.Structure):
     """rg_update (include/raftgpu.h): rg_get_update's sections, pointers into engine-owned pinned memory."""
     _fields_ = [("tick", C.c_uint64), ("states", C.c_void_p), ("n_states", C.c_uint64), ("entries", C.c_void_p),
                 ("n_entries", C.c_uint64), ("entry_payload", C.c_void_p), ("entry_payload_bytes", C.c_uint64),
-                ("committed", C.c_void_p), ("n_committed", C.c_uint64), ("committed_payload", C.c_void_p),
-                ("committed_payload_bytes", C.c_uint64), ("snapshots", C.c_void_p), ("n_snapshots", C.c_uint64),
+                ("committed", ApplyBatch), ("snapshots", C.c_void_p), ("n_snapshots", C.c_uint64),
                 ("reads", C.c_void_p), ("n_reads", C.c_uint64), ("slot_mask", C.c_uint32), ("flags", C.c_uint32)]
 
 
@@ -247,7 +287,7 @@ def load_library(path: str = LIB_PATH):
         "rg_config_change": ([vp, u64, u32, u32, u32], i32),
         "rg_compact": ([vp, u64, u64, C.POINTER(C.c_uint32)], i32),
         "rg_read_index_results": ([vp, u32, vp, u64, C.POINTER(C.c_uint64)], i32),
-        "rg_apply_wait": ([vp, i32, C.POINTER(vp), C.POINTER(vp), C.POINTER(C.c_uint64)], i32),
+        "rg_apply_wait": ([vp, i32, vp], i32),
         "rg_deliver": ([vp, u32, C.POINTER(MsgView)], i32),
         "rg_leader": ([vp, u32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_int)], i32),
         "rg_sum_committed": ([vp, C.POINTER(C.c_uint64)], i32),
@@ -264,7 +304,7 @@ def load_library(path: str = LIB_PATH):
         "rg_rccl_open": ([C.c_char_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(Transport)], i32),
         "rg_rccl_close": ([C.POINTER(Transport)], i32),
         "rg_global_id": ([vp, u32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)], i32),
-        "rg_apply_committed": ([vp, u32, vp, vp, u64, C.POINTER(C.c_uint64), u64, C.POINTER(C.c_uint64)], i32),
+        "rg_apply_committed": ([vp, u32, vp], i32),
         "rg_pool_stats": ([vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_int)], i32),
         "rg_get_update": ([vp, u32, u32, C.POINTER(Update)], i32),
         "rg_digest": ([vp, C.POINTER(C.c_uint64)], i32),
@@ -595,18 +635,18 @@ class Engine:
         self._check(self.L.rg_wire_exchange(self.h, C.byref(transport), C.byref(sent)))
         return sent.value
 
+    def apply_batch(self, slot_mask: int = 0xFF):
+        """rg_apply_committed as the C-ABI returns it: (APPLY_RUN_DTYPE runs, APPLY_CMD_DTYPE per entry,
+        packed Cmd bytes), numpy copies."""
+        b = ApplyBatch()
+        self._check(self.L.rg_apply_committed(self.h, slot_mask, C.byref(b)))
+        return batch_arrays(b)
+
     def apply_committed_packed(self, slot_mask: int = 0xFF):
-        """rg_apply_committed as the C-ABI returns it: (APPLY_DTYPE records, packed Cmd bytes, each at
-        its record's off)."""
-        n, pb = C.c_uint64(), C.c_uint64()
-        rc = self.L.rg_apply_committed(self.h, slot_mask, None, None, 0, C.byref(n), 0, C.byref(pb))
-        if rc < 0 and rc != RG_EFULL:
-            self._check(rc)
-        recs = np.zeros(max(n.value, 1), APPLY_DTYPE)
-        pay = np.zeros(max(pb.value, 16), np.uint8)
-        self._check(self.L.rg_apply_committed(self.h, slot_mask, recs.ctypes.data, pay.ctypes.data, n.value,
-                                              C.byref(n), pay.size, C.byref(pb)))
-        return recs[:n.value], pay[:pb.value]
+        """rg_apply_committed: (APPLY_DTYPE rows expanded from the runs, packed Cmd bytes, each at its
+        row's off)."""
+        runs, cmds, pay = self.apply_batch(slot_mask)
+        return expand_apply(runs, cmds), pay
 
     def apply_committed(self, slot_mask: int = 0xFF):
         """Committed-entry copy-back of the last tick (rg_apply_committed): a structured array
@@ -621,21 +661,16 @@ class Engine:
         self._check(self.L.rg_apply_async(self.h, slot_mask, buf))
 
     def apply_wait(self, buf: int = 0, copy: bool = True):
-        """rg_apply_wait: (records, payloads) of buffer `buf` as numpy arrays (copies unless copy=False:
-        then views into engine-owned pinned memory, valid until the next apply_async into `buf`)."""
-        ents, pay, n = C.c_void_p(), C.c_void_p(), C.c_uint64()
-        self._check(self.L.rg_apply_wait(self.h, buf, C.byref(ents), C.byref(pay), C.byref(n)))
-        k, P = n.value, self.row
-        if k == 0:
-            return np.zeros(0, APPLY_DTYPE), np.zeros((0, P), np.uint8)
-        recs = np.ctypeslib.as_array(C.cast(ents, C.POINTER(C.c_uint8)), (k * APPLY_DTYPE.itemsize,)).view(APPLY_DTYPE)
-        last = recs[-1]
-        nbytes = int(last["off"]) + (int(last["len"]) + 15) // 16 * 16
-        packed = (np.ctypeslib.as_array(C.cast(pay, C.POINTER(C.c_uint8)), (max(nbytes, 1),))[:nbytes] if P
-                  else np.zeros(0, np.uint8))
-        if not copy:  # views into engine-owned pinned memory: the records and the packed Cmds
-            return recs, packed
-        return recs.copy(), unpack_rows(recs, packed, row_width(recs, P))
+        """rg_apply_wait: buffer `buf`'s batch. copy: (APPLY_DTYPE rows, Cmd rows) as numpy copies;
+        copy=False: the raw (runs, cmds, packed payload) views into engine-owned pinned memory, valid
+        until the next apply_async into `buf` (no host expansion: the measured path)."""
+        b = ApplyBatch()
+        self._check(self.L.rg_apply_wait(self.h, buf, C.byref(b)))
+        if not copy:
+            return batch_arrays(b, copy=False)
+        runs, cmds, packed = batch_arrays(b)
+        recs = expand_apply(runs, cmds)
+        return recs, unpack_rows(recs, packed, row_width(recs, self.row))
 
     def persist_collect(self, full: bool = False):
         """Host WAL feed of the last tick (rg_persist_collect): (states, entries, payload) numpy
@@ -668,10 +703,12 @@ class Engine:
         out = {"states": arr(u.states, u.n_states, PERSIST_STATE_DTYPE),
                "entries": arr(u.entries, u.n_entries, PERSIST_ENTRY_DTYPE),
                "entry_payload": arr(u.entry_payload, u.entry_payload_bytes, np.dtype(np.uint8)),
-               "committed": arr(u.committed, u.n_committed, APPLY_DTYPE),
-               "committed_payload": arr(u.committed_payload, u.committed_payload_bytes, np.dtype(np.uint8)),
+               "committed": None, "committed_payload": None,
                "snapshots": arr(u.snapshots, u.n_snapshots, SNAPSHOT_EVENT_DTYPE),
                "reads": arr(u.reads, u.n_reads, READ_READY_DTYPE)}
+        runs, cmds, out["committed_payload"] = batch_arrays(u.committed)
+        out["committed"] = expand_apply(runs, cmds)
+        out["committed_runs"] = runs
         return u, out
 
     def commit_update(self, u, applied: bool = True):

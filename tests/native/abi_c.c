@@ -57,6 +57,33 @@
     }                                                                  \
   } while (0)
 
+/* IOnDiskStateMachine.Update from a copy-back batch, the way a cgo shim walks it: per run, entry k is
+ * index first + k, its Cmd at off + the 16-B-rounded lengths before it; each replica's state machine
+ * receives its entries in index order (a running CRC over the Cmds, the count, the longest Cmd) */
+static void consume(const rg_apply_batch* b, uint64_t* got, uint32_t* got_crc, uint64_t* last_idx,
+                    uint32_t* longest) {
+  uint64_t seen = 0;
+  for (uint64_t r = 0; r < b->n_runs; ++r) {
+    const rg_apply_run* run = &b->runs[r];
+    EXPECT(run->count >= 1 && run->entry == seen && run->entry + run->count <= b->n_entries);
+    uint64_t off = run->off;
+    for (uint32_t k = 0; k < run->count; ++k) {
+      const rg_apply_cmd* c = &b->cmds[run->entry + k];
+      const uint8_t* cmd = b->payload + off;
+      EXPECT(off + c->len <= b->payload_bytes);
+      EXPECT(c->crc == (uint32_t)crc32(0, cmd, c->len));
+      EXPECT(run->first + k > last_idx[run->rid]);
+      last_idx[run->rid] = run->first + k;
+      got_crc[run->rid] = (uint32_t)crc32(got_crc[run->rid], cmd, c->len);
+      got[run->rid]++;
+      if (c->len > *longest) *longest = c->len;
+      off += (c->len + 15u) & ~15u;
+    }
+    seen += run->count;
+  }
+  EXPECT(seen == b->n_entries);
+}
+
 /* deterministic Cmd k of shard g at tick t: "put g/t/k" + filler, 1..MAXC bytes (longer than
  * payload_bytes, so Cmds span lane groups and pages) */
 static uint32_t make_cmd(uint32_t g, uint32_t t, uint32_t k, uint8_t* out) {
@@ -128,11 +155,6 @@ int main(int argc, char** argv) {
   in.campaign = NULL;
   for (int t = 0; t < 6; ++t) CHECK(tick(e, &in));
 
-  /* C-owned buffers for the copy-back and the WAL feed */
-  const uint64_t cap = 1u << 16;
-  rg_apply_entry* ents = (rg_apply_entry*)malloc(cap * sizeof *ents);
-  const uint64_t pay_cap = cap * 1024;
-  uint8_t* pay = (uint8_t*)malloc(pay_cap);
   /* what each replica's state machine received, as a running CRC over (index, Cmd) */
   uint64_t got[G * R];
   uint32_t got_crc[G * R];
@@ -191,28 +213,15 @@ int main(int argc, char** argv) {
       if (p->type == RG_ENTRY_APPLICATION && p->len)
         EXPECT(p->crc == (uint32_t)crc32(0, u.entry_payload + p->off, p->len));
     }
-    for (uint64_t i = 0; i < u.n_committed; ++i) { /* IOnDiskStateMachine.Update, per replica */
-      const rg_apply_entry* a = &u.committed[i];
-      const uint8_t* cmd = u.committed_payload + a->off;
-      EXPECT(a->off + a->len <= u.committed_payload_bytes);
-      EXPECT(a->crc == (uint32_t)crc32(0, cmd, a->len));
-      EXPECT(a->index > last_idx[a->rid]);
-      last_idx[a->rid] = a->index;
-      got_crc[a->rid] = (uint32_t)crc32(got_crc[a->rid], cmd, a->len);
-      got[a->rid]++;
-      if (a->len > longest) longest = a->len;
-    }
+    consume(&u.committed, got, got_crc, last_idx, &longest);
     /* Peer.Commit: the app answered, applied = processed (config changes and no-ops included) */
     CHECK(rg_commit_update(e, &u, RG_COMMIT_APPLIED));
   }
   for (int t = 0; t < 16; ++t) { /* drain: the last Cmds commit everywhere, the re-added follower catches up */
-    uint64_t na = 0, pb = 0;
+    rg_apply_batch b;
     CHECK(tick(e, &in));
-    CHECK(rg_apply_committed(e, 0xFF, ents, pay, cap, &na, pay_cap, &pb));
-    for (uint64_t i = 0; i < na; ++i) {
-      got_crc[ents[i].rid] = (uint32_t)crc32(got_crc[ents[i].rid], pay + ents[i].off, ents[i].len);
-      got[ents[i].rid]++;
-    }
+    CHECK(rg_apply_committed(e, 0xFF, &b));
+    consume(&b, got, got_crc, last_idx, &longest);
     rg_replica_view v[G * R];
     CHECK(rg_read_replicas(e, 0, G * R, v));
     for (uint32_t r = 0; r < G * R; ++r) idx[r] = v[r].processed;
@@ -244,6 +253,6 @@ int main(int argc, char** argv) {
          use_wire ? " (wire + RCCL exchange)" : "", G, R, (unsigned long long)want_n[0], rg_device_bytes(e) / 1e6);
   rg_destroy(e);
   if (use_wire) CHECK(rg_rccl_close(&xt));
-  free(ents); free(pay); free(blob);
+  free(blob);
   return 0;
 }

@@ -135,3 +135,24 @@ def test_notify_after_acknowledged_updates(app):
     ap.apply(Eng(), slot_mask=0b010, notify=True)
     assert Eng.notified == ([1, 4, 7, 10], [101, 104, 107, 110])
     ap.close()
+
+
+def test_expand_apply_runs_with_gaps():
+    """expand_apply (the host view of rg_apply_run ranges): entry k of a run is index first + k, its Cmd
+    at the run's off + the 16-B-rounded lengths before it in the run; runs of several replicas."""
+    from raftd_amd.engine import APPLY_CMD_DTYPE, APPLY_RUN_DTYPE, expand_apply
+    cmds = np.zeros(6, APPLY_CMD_DTYPE)
+    cmds["len"] = [5, 16, 17, 1, 300, 2]
+    cmds["crc"] = [1, 2, 3, 4, 5, 6]
+    runs = np.zeros(3, APPLY_RUN_DTYPE)
+    # replica 7: indices 10, 11 then (a no-op at 12) 13; replica 9: 40, 41, 42
+    runs[0] = (3, 2, 7, 10, 0, 0, 2, 0)
+    runs[1] = (3, 2, 7, 13, 2, 32, 1, 0)
+    runs[2] = (4, 1, 9, 40, 3, 80, 3, 0)
+    out = expand_apply(runs, cmds)
+    assert list(out["index"]) == [10, 11, 13, 40, 41, 42]
+    assert list(out["rid"]) == [7, 7, 7, 9, 9, 9]
+    assert list(out["group"]) == [3, 3, 3, 4, 4, 4]
+    assert list(out["off"]) == [0, 16, 32, 80, 96, 400]
+    assert list(out["len"]) == [5, 16, 17, 1, 300, 2] and list(out["crc"]) == [1, 2, 3, 4, 5, 6]
+    assert len(expand_apply(np.zeros(0, APPLY_RUN_DTYPE), np.zeros(0, APPLY_CMD_DTYPE))) == 0

@@ -115,3 +115,32 @@ def test_async_copyback_matches_sync(d2h, monkeypatch):
             assert bytes(got_p[k, :n]) == bytes(want_p[k, :n]), (t, k)
         total += len(want_r)
     assert total > 0
+
+
+def test_apply_batch_ships_runs():
+    """The copy-back is ranges (r05): one rg_apply_run per run of consecutive applied indices, 8 B of
+    {len, crc} per entry. In steady state every replica's window is one run; the runs are maximal (no
+    two runs of a replica touch), their counts tile the per-entry array, and expanding them gives the
+    oracle's applied entries exactly."""
+    G, R, E = 32, 3, 16
+    cfg = dict(groups=G, replicas=R, log_capacity=256, payload_bytes=64, max_entries_per_msg=E, snapshot_entries=0,
+               seed=47)
+    gpu, ora = make("gpu", **cfg), make("c", **cfg)
+    gpu.bootstrap()
+    ora.bootstrap()
+    camp = np.zeros(G * R, np.uint8)
+    camp[0::R] = 1
+    pt, pc = np.zeros(G, np.uint8), np.full(G, E, np.uint32)
+    for t in range(12):
+        ins = (None, None, camp) if t == 1 else (pt, pc) if t >= 4 else ()
+        gpu.tick(*ins)
+        ora.tick(*ins)
+        runs, cmds, pay = gpu.apply_batch()
+        assert int(runs["count"].sum()) == len(cmds)
+        assert np.array_equal(np.cumsum(runs["count"])[:-1] if len(runs) else [], runs["entry"][1:])
+        for a, b in zip(runs[:-1], runs[1:]):  # maximal: a replica's next run starts past a gap
+            assert a["rid"] != b["rid"] or b["first"] > a["first"] + a["count"]
+        if t >= 8:  # steady: every replica applies E entries per tick, one run each
+            assert len(runs) == G * R and np.all(runs["count"] == E), (t, len(runs))
+        recs, rows = gpu.apply_committed()
+        assert sorted(got(recs, rows, lambda rid: rid)) == sorted(expected(ora, range(G * R))), t
