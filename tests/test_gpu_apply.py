@@ -140,7 +140,7 @@ def test_apply_batch_ships_runs():
         assert np.array_equal(np.cumsum(runs["count"])[:-1] if len(runs) else [], runs["entry"][1:])
         for a, b in zip(runs[:-1], runs[1:]):  # maximal: a replica's next run starts past a gap
             assert a["rid"] != b["rid"] or b["first"] > a["first"] + a["count"]
-        if t >= 8:  # steady: every replica applies E entries per tick, one run each
-            assert len(runs) == G * R and np.all(runs["count"] == E), (t, len(runs))
+        if t >= 9:  # steady: every replica's window is one run (followers' windows lag their leader's)
+            assert len(runs) == G * R and np.all(runs["count"] >= E), (t, len(runs), runs["count"])
         recs, rows = gpu.apply_committed()
         assert sorted(got(recs, rows, lambda rid: rid)) == sorted(expected(ora, range(G * R))), t
