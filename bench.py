@@ -735,7 +735,7 @@ def main():
             "tick_counts": {k: v for k, v in traffic.items() if k not in ("algorithmic_bytes", "bulk_bytes")},
         },
         "kernels_ms": {"control_kernel": ctl_ms, "bulk_kernel": bulk_ms},
-        "control_fast_path": {"enabled": os.environ.get("RAFTGPU_CTL_FAST", "1") != "0",
+        "control_fast_path": {"enabled": True,
                               "slow_replicas_last_tick": ctl_slow,
                               "note": "control_kernel time = control_fast_kernel (the steady-state branches, compiled per "
                                       "role: three waves per SIMD at R <= 3) + control_slow_kernel (the full step for the "

@@ -833,11 +833,11 @@ hipError_t launch_bulk_t<(bool)RG_BULK_W, (bool)RG_BULK_MJ>(const BulkParams& p,
   if (p.small) {  // the small jobs first, then bulk_kernel for the rest (it skips them)
     const uint32_t lg = (uint32_t)lg_of(p.P), nch = 1u << lg;
     const uint32_t tiles = ((p.G + 63) / 64) * p.R;
-    static const uint32_t gmul = [] {  // RAFTGPU_SMALL_GRID: workgroups per bulk-grid slot (A/B)
-      const char* v = getenv("RAFTGPU_SMALL_GRID");
-      const long m = v ? strtol(v, nullptr, 10) : 2;
-      return (uint32_t)(m >= 1 && m <= 64 ? m : 2);
-    }();
+#ifdef RG_AB_SMALL_GRID  // A/B variant: workgroups per bulk-grid slot (r04: 2, 4 and 8 tie, 16 loses)
+    constexpr uint32_t gmul = RG_AB_SMALL_GRID;
+#else
+    constexpr uint32_t gmul = 2;
+#endif
     const int sg = (int)std::min<uint32_t>((tiles + 3) / 4, (uint32_t)grid * gmul);
     const int lds = (int)((CRC_T_WORDS + CRC_N_WORDS + nch * CRC_SH_STRIDE) * 4 + 4 * 64 * SMALL_N);
     hipError_t r = hipErrorInvalidValue;

@@ -35,11 +35,18 @@ static int fail(int code, const std::string& msg) {
     if (_e != hipSuccess) return fail(RG_EHIP, std::string(#x) + ": " + hipGetErrorString(_e)); \
   } while (0)
 
-// RAFTGPU_SYNC_DEBUG=1: synchronise after every launch so a fault names its kernel (debug only)
-static const bool g_sync_debug = [] {
-  const char* v = getenv("RAFTGPU_SYNC_DEBUG");
-  return v && *v == '1';
-}();
+// Knobs (r05): the product reads no tuning knob from the environment. The A/B settings of earlier
+// rounds are build-time variants for scripts/build_variant.sh (-DRG_AB_*); only four test hooks are
+// read, once, at rg_create / rg_rccl_open: RAFTGPU_WIRE_CAP0 (start the fixed-capacity regions small),
+// RAFTGPU_CTL_FB (force the control fallback in or out of the fast kernel's launch), RAFTGPU_APPLY_SDMA
+// (the copy-back's D2H leg on an SDMA engine) and RAFTGPU_RCCL_SELF (the RCCL transport's self region
+// through RCCL) — each selects between two product paths the tests run bit-exact.
+// RG_SYNC_DEBUG builds synchronise after every launch so a fault names its kernel (debug only).
+#ifdef RG_SYNC_DEBUG
+static constexpr bool g_sync_debug = true;
+#else
+static constexpr bool g_sync_debug = false;
+#endif
 #define LAUNCH(x, st, name)                                                                          \
   do {                                                                                              \
     HIPCHK(x);                                                                                      \
@@ -712,20 +719,27 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   const uint64_t waves = (uint64_t)std::max(cus, 1) * per_cu * 4;
   uint32_t tile = 64;
   while (tile > 1 && (n + tile - 1) / tile < waves) tile >>= 1;
-  if (const char* tv = getenv("RAFTGPU_BULK_TILE")) {  // measurement override (a power of two, 1..64)
-    const uint32_t t = (uint32_t)atoi(tv);
-    if (pow2(t) && t <= 64) tile = t;
-  }
+#ifdef RG_AB_BULK_TILE  // A/B variant: a fixed tile (a power of two, 1..64)
+  tile = RG_AB_BULK_TILE;
+#endif
   e->bulk_tile = tile;
-  if (const char* v = getenv("RAFTGPU_APPLY_MEMCPY")) e->copy_kernel = !(v[0] == '1');
+#ifdef RG_AB_APPLY_MEMCPY  // A/B variant: the runtime's hipMemcpyAsync for the copy-back's D2H leg
+  e->copy_kernel = false;
+#endif
   e->bulk_mj = c.max_entries_per_msg <= 16;
-  if (const char* v = getenv("RAFTGPU_CTL_FAST")) e->ctl_fast = v[0] != '0';
+#ifdef RG_AB_CTL_FULL  // A/B variant: the full control step for every replica (no fast path)
+  e->ctl_fast = false;
+#endif
   // at most one wave per SIMD: occupancy buys nothing, and the fallback saves the slow kernel's launch
   e->ctl_fb = (uint64_t)n <= 64ull * 1024;
-  if (const char* v = getenv("RAFTGPU_CTL_FB")) e->ctl_fb = v[0] == '1';
-  if (const char* v = getenv("RAFTGPU_BULK_MULTIJOB")) e->bulk_mj = v[0] == '1';
-  if (const char* v = getenv("RAFTGPU_BULK_SMALL")) e->bulk_small = v[0] != '0';
-  if (const char* v = getenv("RAFTGPU_APPLY_SDMA"))
+  if (const char* v = getenv("RAFTGPU_CTL_FB")) e->ctl_fb = v[0] == '1';  // test hook (both paths)
+#ifdef RG_AB_BULK_MULTIJOB  // A/B variant: 0 / 1 forces the bulk kernel's job walk
+  e->bulk_mj = RG_AB_BULK_MULTIJOB;
+#endif
+#ifdef RG_AB_NO_BULK_SMALL  // A/B variant: one-job replicas through bulk_kernel too
+  e->bulk_small = false;
+#endif
+  if (const char* v = getenv("RAFTGPU_APPLY_SDMA"))  // test hook: the SDMA D2H leg
     if (v[0] == '1') {
       std::string why;
       if (sdma_open(c.device, &e->sdma, &why) != 0) {
@@ -739,18 +753,16 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
     return fail(RG_EHIP, "page pool reset");
   }
   const uint64_t ntiles = (n + tile - 1) / tile;
-  // waves per bulk workgroup (RAFTGPU_BULK_WG, A/B): the tiles of one group block's R slots are
-  // consecutive, so a workgroup of R waves keeps a block's two followers — which read the same
-  // leader entries — on one CU and one XCD's L2
+  // waves per bulk workgroup: the tiles of one group block's R slots are consecutive, so a workgroup
+  // of R waves keeps a block's two followers — which read the same leader entries — on one CU and
+  // one XCD's L2 (r04 A/B of 3 and 4 tied)
   e->bulk_wg = 4;
-  if (const char* v = getenv("RAFTGPU_BULK_WG")) e->bulk_wg = std::min(4, std::max(1, atoi(v)));
   const uint64_t wgw = e->bulk_wg;
   e->bulk_grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((ntiles + wgw - 1) / wgw,
                                                                (uint64_t)std::max(cus, 1) * per_cu * 4 / wgw));
-  if (const char* gv = getenv("RAFTGPU_BULK_GRID")) {  // measurement override (blocks)
-    const int gb = atoi(gv);
-    if (gb > 0) e->bulk_grid = gb;
-  }
+#ifdef RG_AB_BULK_GRID  // A/B variant: a fixed bulk grid (blocks)
+  e->bulk_grid = RG_AB_BULK_GRID;
+#endif
   *out = e;
   return RG_OK;
 }

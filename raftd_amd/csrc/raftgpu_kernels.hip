@@ -241,9 +241,11 @@ hipError_t launch_pool_reset(uint32_t* fring, uint64_t npages, PoolCtl* ctl, hip
   // The ring starts as the permutation i -> i * 1000003 mod npages (a prime multiplier: a bijection
   // unless it divides npages), so the pages consecutive replicas take lie ~4 GB apart instead of side
   // by side: the first snapshot window's payload stage ran 3 % faster so (r04v, per-tick kernel
-  // trace). RAFTGPU_POOL_PERM=<m> overrides the multiplier (1 = the identity, A/B).
+  // trace; r04 A/B: 65,537 ties, 4,099 and 257 lose 2-3 %; -DRG_AB_POOL_PERM=<m> builds another).
   uint64_t mul = npages % 1000003ull ? 1000003ull : 1000033ull;
-  if (const char* v = getenv("RAFTGPU_POOL_PERM")) mul = strtoull(v, nullptr, 10);
+#ifdef RG_AB_POOL_PERM
+  mul = RG_AB_POOL_PERM;
+#endif
   {
     uint64_t a = mul, b = npages;
     while (b) {
@@ -418,10 +420,11 @@ __global__ void __launch_bounds__(256) copy_to_host_kernel(const uint8_t* src, u
 
 hipError_t launch_copy_to_host(const void* src, void* dst, uint64_t bytes, hipStream_t s) {
   if (!bytes) return hipSuccess;
-  static const int blocks = [] {
-    const char* v = getenv("RAFTGPU_COPY_WG");  // measurement override
-    return v && atoi(v) > 0 ? atoi(v) : 32;
-  }();
+#ifdef RG_AB_COPY_WG  // A/B variant (r03: 2-16 workgroups lost to 32)
+  constexpr int blocks = RG_AB_COPY_WG;
+#else
+  constexpr int blocks = 32;
+#endif
   hipLaunchKernelGGL(copy_to_host_kernel, dim3(blocks), dim3(256), 0, s, (const uint8_t*)src, (uint8_t*)dst, bytes);
   return hipGetLastError();
 }
