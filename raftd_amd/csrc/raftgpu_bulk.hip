@@ -177,6 +177,17 @@ __device__ __forceinline__ void load_tile(const BulkParams& p, Cursor& cur, Tile
   const bool valid = lane < p.tile && g0 + lane < p.G;
 #endif
   const uint32_t q = cur.qb + lane;
+#ifndef RG_TILE_SLOTMAJOR
+  if constexpr (MJ) {  // a block bulk_small_kernel took whole: nothing to load (C5: every block)
+    if (p.small && !p.rest[(g0 >> 6) * p.R + s]) {
+      tj = TileJobs{};
+      cur.m = 0;
+      cur.j = 0;
+      cur.njl = 0;
+      return;
+    }
+  }
+#endif
   tj.nj = valid ? p.jcnt[q] : 0u;
   tj.j0 = Job{};
   if (tj.nj) tj.j0 = load_job(p, q, 0);
@@ -727,6 +738,9 @@ __global__ void __launch_bounds__(256) bulk_small_kernel(BulkParams p, const uin
     Job jb{};
     if (nj == 1) jb = load_job(p, q, 0);
     const bool small = valid && small_job(p, nj, jb, q, NCH, WIRE);
+    // bulk_kernel skips a block of 64 groups whose replicas with jobs were all taken here
+    const uint64_t left = __ballot(valid && nj != 0 && !small);
+    if (lane == 0) p.rest[t] = left != 0 ? 1u : 0u;
     const uint32_t e0 = (jb.meta >> 8) & 0xFF, k = small ? (jb.meta & 0xFF) - e0 : 0u;
     const uint32_t off = wave_excl_scan32(k);
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)(off + k), 63);

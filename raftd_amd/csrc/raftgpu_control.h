@@ -1186,6 +1186,12 @@ struct Ctl {
     if constexpr (FAST) {
       // same-term steady-state traffic only, from this rank or over the wire: a term change, a vote, a
       // read, a forwarded proposal or a snapshot leaves the fast path (a candidate never entered it)
+#ifdef RG_AB_FAST_NO_REMOTE  // diagnostic variant: r04's fast step, which handed every remote message off
+      if (remote) {
+        abort_();
+        return;
+      }
+#endif
       if (from - 1 >= (uint32_t)R || (mterm != 0 && mterm != term) ||
           (type == M_REPLICATE && (uint32_t)(w0 >> 32) > p.E)) {
         abort_();

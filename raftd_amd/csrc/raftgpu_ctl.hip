@@ -113,14 +113,24 @@ __device__ __forceinline__ void count_slow(CTickParams& cp, bool aborted) {
     atomicAdd(cp.slow_cnt + (cp.tick & 1), (uint32_t)__popcll(m));
 }
 
+// RG_AB_CTL2D (diagnostic variant, never the product): the fast and slow kernels on r04f's (column,
+// slot) grid, the slot index blockIdx.y — the launch geometry of the r04 memory-aperture fault
+// ("The control-kernel fault"). q is still slot · G + column.
+#ifdef RG_AB_CTL2D
+#define RG_CTL_Q (blockIdx.y * ((const TickParams*)pp)->G + blockIdx.x * blockDim.x + threadIdx.x)
+#define RG_CTL_COL_OK(cp) (blockIdx.x * blockDim.x + threadIdx.x < (cp).G)
+#else
+#define RG_CTL_Q (blockIdx.x * blockDim.x + threadIdx.x)
+#define RG_CTL_COL_OK(cp) true
+#endif
 template <int R>
 __global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_FAST_WAVES) control_fast_kernel(
     const TickParams* __restrict__ pp, uint32_t* perr) {
-  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t q = RG_CTL_Q;
   if (!tp_verify(pp, perr, q, "control_fast_kernel")) return;
   CTickParams& cp = *(CTickParams*)pp;
   if (q == 0) cp.slow_cnt[(cp.tick + 1) & 1] = 0;  // the next tick's counter (its last reader ran before us)
-  if (q >= cp.nrep) return;
+  if (q >= cp.nrep || !RG_CTL_COL_OK(cp)) return;
   const bool aborted = fast_step<R>(cp, q);
   cp.slow_flag[q] = aborted ? 1u : 0u;  // for control_slow_kernel
   count_slow(cp, aborted);
@@ -153,11 +163,15 @@ __global__ void __launch_bounds__(RG_CTL_BLOCK, 1) control_fastfb_kernel(const T
 template <int R>
 __global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_MINWAVES) control_slow_kernel(const TickParams* __restrict__ pp,
                                                                                     uint32_t* perr) {
-  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t q = RG_CTL_Q;
   if (!tp_verify(pp, perr, q, "control_slow_kernel")) return;
   CTickParams& cp = *(CTickParams*)pp;
-  if (q >= cp.nrep || !cp.slow_flag[q]) return;
+  if (q >= cp.nrep || !RG_CTL_COL_OK(cp) || !cp.slow_flag[q]) return;
+#ifdef RG_AB_CTL2D
+  Ctl<R> c(cp, blockIdx.y, blockIdx.x * blockDim.x + threadIdx.x);  // the slot a grid-uniform scalar
+#else
   Ctl<R> c(cp, q);
+#endif
   c.run();
 }
 
@@ -235,8 +249,14 @@ hipError_t launch_control_fast_t<RG_CTL_R>(const TickParams* p, uint32_t* perr, 
 #else
   (void)fb;
 #endif
+#ifdef RG_AB_CTL2D
+  const dim3 g2((nrep / RG_CTL_R + RG_CTL_BLOCK - 1) / RG_CTL_BLOCK, RG_CTL_R);
+  hipLaunchKernelGGL(control_fast_kernel<RG_CTL_R>, g2, block, 0, s, p, perr);
+  hipLaunchKernelGGL(control_slow_kernel<RG_CTL_R>, g2, block, 0, s, p, perr);
+#else
   hipLaunchKernelGGL(control_fast_kernel<RG_CTL_R>, grid, block, 0, s, p, perr);
   hipLaunchKernelGGL(control_slow_kernel<RG_CTL_R>, grid, block, 0, s, p, perr);
+#endif
   return hipGetLastError();
 #endif
 }

@@ -238,6 +238,7 @@ struct rg_engine {
   uint64_t x_send_cap = 0, x_recv_cap = 0;
   // committed-entry copy-back (raftgpu_apply.hip)
   uint64_t* apply_lo = nullptr;
+  uint32_t* small_rest = nullptr;  // BulkParams::rest
   uint32_t *acnt = nullptr, *accnt = nullptr, *arcnt = nullptr;
   uint64_t *aoff = nullptr, *acoff = nullptr, *aroff = nullptr, *absum = nullptr;
   bool copy_kernel = true;  // RAFTGPU_APPLY_MEMCPY=1: the runtime's D2H copy instead (A/B)
@@ -450,6 +451,7 @@ static BulkParams bulk_params_at(rg_engine* e, uint64_t tk) {
   b.nslab = e->c.num_slabs;
   b.multijob = e->bulk_mj ? 1u : 0u;
   b.small = e->bulk_mj && e->bulk_small ? 1u : 0u;
+  b.rest = e->small_rest;
   b.wg_waves = e->bulk_wg;
   return b;
 }
@@ -592,6 +594,7 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if (rc == RG_OK) rc = dalloc(e, &e->aoff, (n + 1) * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->acoff, (n + 1) * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->arcnt, n * 4);
+  if (rc == RG_OK) rc = dalloc(e, &e->small_rest, (uint64_t)((c.groups + 63) / 64) * c.replicas * 4);
   if (rc == RG_OK) rc = dalloc(e, &e->aroff, (n + 1) * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->absum, ((n + 1023) / 1024 + 1) * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->persist_lo, n * 8);

@@ -287,6 +287,8 @@ struct BulkParams {
   uint32_t nslab;
   uint32_t multijob;     // small jobs share a ring pass (bulk_kernel<.., MJ>; the engine's choice)
   uint32_t small;        // bulk_small_kernel ran first: bulk_kernel skips the replicas it took (small_job)
+  uint32_t* rest;        // [ceil(G / 64) * R] per 64-group block and slot: 1 if bulk_small_kernel left a
+                         // replica with jobs there (bulk_kernel skips the tiles of a block it took whole)
   uint32_t wg_waves;     // waves per bulk_kernel workgroup (1..4)
 };
 
