@@ -75,6 +75,24 @@ RG_FN void sfor(F&& f) {
   }
 }
 // remote slot f of a per-replica array, with constant indices only (the arrays stay in registers)
+// Diagnostic variants (RG_AB_SV_*): Ctl's slot in one class of uses is laundered through a VGPR
+// move (Ctl::slot_lane), so the compiler treats it as per-lane there (the fault)
+#ifdef RG_AB_SV_SEND
+#define RG_S_SEND slot_lane()
+#else
+#define RG_S_SEND s
+#endif
+#ifdef RG_AB_SV_INBOX
+#define RG_S_INBOX slot_lane()
+#else
+#define RG_S_INBOX s
+#endif
+#ifdef RG_AB_SV_ID
+#define RG_S_ID slot_lane()
+#else
+#define RG_S_ID s
+#endif
+
 template <int R, class T>
 RG_FN T sel_get(const T (&a)[R], uint32_t f) {
   T v = a[0];
@@ -168,8 +186,8 @@ struct Ctl {
   // slot ss of group column g0: the kernels pass a wave-uniform slot (the grid's y index), so every
   // value derived from s alone (its outbox planes, the sender loop's skip, my_id) stays scalar
   RG_FN Ctl(CTickParams& pp, uint32_t ss, uint32_t g0) : p(pp), q(ss * pp.G + g0), g(g0), s(ss) {
-    gg = pl_group(p.pl, s, g);
-    rid = gg * R + s;
+    gg = pl_group(p.pl, RG_S_ID, g);
+    rid = gg * R + RG_S_ID;
     gi = (uint32_t)pl_input_index(p.pl, gg);
     const uint64_t n = p.nrep;
     const uint64_t* a = p.s64_in + q;
@@ -231,11 +249,20 @@ struct Ctl {
 
   // entries per load batch (RG_CTL_BATCH); at R >= 7 the remote arrays leave room for half as many
   static constexpr uint32_t CB = R >= 7 ? (RG_CTL_BATCH > 4 ? 4 : RG_CTL_BATCH) : RG_CTL_BATCH;
-  RG_FN uint64_t ri() const { return (uint64_t)gi * R + s; }  // the replica's tick-input index
+  RG_FN uint64_t ri() const { return (uint64_t)gi * R + RG_S_ID; }  // the replica's tick-input index
   RG_FN void abort_() { aborted = true; }  // FAST: leave the fast path (the full kernel re-runs the step)
   RG_FN uint32_t quorum() const { return (uint32_t)__builtin_popcount(members) / 2 + 1; }  // voting members
   RG_FN bool is_member(uint32_t i) const { return (members >> i) & 1u; }
-  RG_FN uint32_t my_id() const { return s + 1; }
+  // Diagnostic variants (RG_AB_SV_*; DESIGN.md §3, the control-kernel fault): the slot, laundered
+  // through a VGPR move so the compiler treats it as per-lane, in one class of uses at a time
+  RG_FN uint32_t slot_lane() const {
+    uint32_t v = s;
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("v_mov_b32 %0, %0" : "+v"(v));
+#endif
+    return v;
+  }
+  RG_FN uint32_t my_id() const { return RG_S_ID + 1; }
 
   // ---- remotes (compile-time R: selects, no local-memory arrays)
 #define RG_GET(arr, f) sel_get<R>(arr, f)
@@ -320,7 +347,7 @@ struct Ctl {
     }
     oc += 1ull << (8 * dst);
     const uint64_t plane = (uint64_t)R * R * p.K * p.G;
-    uint64_t* h = p.hdr_out + (((uint64_t)s * R + dst) * p.K + k) * p.G + g;
+    uint64_t* h = p.hdr_out + (((uint64_t)RG_S_SEND * R + dst) * p.K + k) * p.G + g;
     h[0 * plane] = (uint64_t)type | ((uint64_t)my_id() << 8) | ((uint64_t)to << 16) | ((uint64_t)reject << 24) |
                    ((uint64_t)nent << 32);
     h[1 * plane] = mterm;
@@ -737,7 +764,7 @@ struct Ctl {
 #endif
     const int k = send(M_REPLICATE, to + 1, 0, 0, n, lt, next - 1, committed, upos, 0, uni, 0);
     if (k >= 0 && n > 0) {
-      uint64_t* mt = p.mt_out + ((((uint64_t)s * R + to) * p.K + (uint32_t)k) * p.E) * p.G + g;
+      uint64_t* mt = p.mt_out + ((((uint64_t)RG_S_SEND * R + to) * p.K + (uint32_t)k) * p.E) * p.G + g;
 #ifdef RG_CTL_FASTREP
       if (FAST || fast) {
         mt[0] = la_word;  // uniform: one word for every entry
@@ -797,7 +824,7 @@ struct Ctl {
     const bool uni = !remote && ((uint32_t)wofs & RG_UNIFORM) && n > 0;
     wofs &= ~(uint64_t)RG_UNIFORM;
     if (term_at(li) == log_term) {
-      const uint64_t* mt = (remote ? p.rmt : p.mt_in) + ((((uint64_t)src * R + s) * p.K + k) * p.E) * p.G + g;
+      const uint64_t* mt = (remote ? p.rmt : p.mt_in) + ((((uint64_t)src * R + RG_S_INBOX) * p.K + k) * p.E) * p.G + g;
       const uint64_t uw = uni || runi ? mt0 : 0ull;  // loaded with the header (handle_)
       if constexpr (FAST) {  // an append at the log end from a uniform Replicate (or an empty one)
         if (li != last || (n > 0 && !uni && !runi) || (uw & TYPE_BIT)) {
@@ -1158,7 +1185,7 @@ struct Ctl {
     uint64_t mt0;  // a Replicate's first inline word (a uniform Replicate needs only it)
   };
   RG_FN const uint64_t* hdr_ptr(uint32_t src, uint32_t k, bool remote) const {
-    return (remote ? p.rhdr : p.hdr_in) + (((uint64_t)src * R + s) * p.K + k) * p.G + g;
+    return (remote ? p.rhdr : p.hdr_in) + (((uint64_t)src * R + RG_S_INBOX) * p.K + k) * p.G + g;
   }
   // one round trip: the header words and the message's first inline word (for other
   // messages the slot holds stale words, which nothing reads)
@@ -1167,7 +1194,7 @@ struct Ctl {
     const uint64_t* h = hdr_ptr(src, k, remote);
 #pragma unroll
     for (int x = 0; x < NB; ++x) o.w[x] = h[(uint64_t)x * plane];
-    o.mt0 = (remote ? p.rmt : p.mt_in)[((((uint64_t)src * R + s) * p.K + k) * p.E) * p.G + g];
+    o.mt0 = (remote ? p.rmt : p.mt_in)[((((uint64_t)src * R + RG_S_INBOX) * p.K + k) * p.E) * p.G + g];
   }
   RG_FN void handle(uint32_t src, uint32_t k, bool remote, const Hdr& hd) {
     RG_T0(t0);
@@ -1264,7 +1291,7 @@ struct Ctl {
         // word 4: the batch's stream chunks | contiguous << 31 | arena chunk << 32 (a remote
         // batch: the chunks unpack_kernel counted)
         if (remote) {
-          const uint64_t* rm = p.rmt + ((((uint64_t)src * R + s) * p.K + k) * p.E) * p.G + g;
+          const uint64_t* rm = p.rmt + ((((uint64_t)src * R + RG_S_INBOX) * p.K + k) * p.E) * p.G + g;
           handle_propose(nent, 0, 1, hw(5), 0, nullptr, rm, w7, (uint32_t)hw(6), hw(4));
         } else {
           const uint64_t row = p.wire ? (uint64_t)src * p.G + g : g;  // the forwarder's slab row (same rank)
@@ -1342,7 +1369,7 @@ struct Ctl {
     sfor<0, R>([&](auto jc) {
       constexpr int src = decltype(jc)::value;
       cnt_pf[src] = (uint32_t)src == s ? 0u
-                    : (pl_remote(p.pl, src, s, g) ? p.rcnt : p.cnt_in)[((uint64_t)src * R + s) * p.G + g];
+                    : (pl_remote(p.pl, src, RG_S_INBOX, g) ? p.rcnt : p.cnt_in)[((uint64_t)src * R + RG_S_INBOX) * p.G + g];
     });
     const uint32_t in_pt = p.prop_target ? p.prop_target[gi] : 0xFFu;
     const uint32_t in_pc = p.prop_target ? p.prop_count[gi] : 0u;
@@ -1375,14 +1402,14 @@ struct Ctl {
     uint32_t cs = 0, ck = 0;
     bool have = !(FAST && aborted) && next_msg(0, ~0u, cs, ck);
     Hdr cur{};
-    if (have) load_hdr(cs, ck, pl_remote(p.pl, cs, s, g), cur);
+    if (have) load_hdr(cs, ck, pl_remote(p.pl, cs, RG_S_INBOX, g), cur);
     while (have) {
       uint32_t ns = 0, nk = 0;
       const bool more = next_msg(cs, ck, ns, nk);
       Hdr nxt{};
-      if (PIPE && more) load_hdr(ns, nk, pl_remote(p.pl, ns, s, g), nxt);
-      handle(cs, ck, pl_remote(p.pl, cs, s, g), cur);
-      if (!PIPE && more && !(FAST && aborted)) load_hdr(ns, nk, pl_remote(p.pl, ns, s, g), nxt);
+      if (PIPE && more) load_hdr(ns, nk, pl_remote(p.pl, ns, RG_S_INBOX, g), nxt);
+      handle(cs, ck, pl_remote(p.pl, cs, RG_S_INBOX, g), cur);
+      if (!PIPE && more && !(FAST && aborted)) load_hdr(ns, nk, pl_remote(p.pl, ns, RG_S_INBOX, g), nxt);
       cur = nxt;
       cs = ns;
       ck = nk;
@@ -1513,7 +1540,7 @@ struct Ctl {
       p.rem_out[(1 * R + j) * n + q] = rn[j];
       if constexpr (!RS_MEM && !LEAN) p.rem_out[(2 * R + j) * n + q] = rs[j];
       p.rst_out[j * n + q] = (uint8_t)rt[j];
-      p.cnt_out[((uint64_t)s * R + j) * p.G + g] = get8(oc, j);
+      p.cnt_out[((uint64_t)RG_S_SEND * R + j) * p.G + g] = get8(oc, j);
     });
     p.jcnt[q] = nj;
     if (p.apply_lo) p.apply_lo[q] = umax64(processed_start, restored_at) + 1;

@@ -167,9 +167,9 @@ __global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_MINWAVES) control_slow_ke
   if (!tp_verify(pp, perr, q, "control_slow_kernel")) return;
   CTickParams& cp = *(CTickParams*)pp;
   if (q >= cp.nrep || !RG_CTL_COL_OK(cp) || !cp.slow_flag[q]) return;
-#ifdef RG_AB_CTL2D
+#if defined(RG_AB_CTL2D) && !defined(RG_AB_CTL2D_Q)
   Ctl<R> c(cp, blockIdx.y, blockIdx.x * blockDim.x + threadIdx.x);  // the slot a grid-uniform scalar
-#else
+#else  // RG_AB_CTL2D_Q: the 2-D launch, the slot derived from q (a per-lane value to the compiler)
   Ctl<R> c(cp, q);
 #endif
   c.run();
