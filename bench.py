@@ -360,16 +360,16 @@ def hand_off(eng, tick, G, steps, slot_mask=1):
         tick()
         if eng.L.rg_get_update(eng.h, slot_mask, UPDATE_ALL, C.byref(u)) != 0:
             raise RuntimeError(f"rg_get_update: {eng.L.rg_last_error().decode()}")
-        ne += u.n_entries + u.committed.n_entries
-        nb += u.entry_payload_bytes + u.committed.payload_bytes
+        ne += u.persist.n_entries + u.committed.n_entries
+        nb += u.persist.payload_bytes + u.committed.payload_bytes
         if eng.L.rg_commit_update(eng.h, C.byref(u), COMMIT_APPLIED) != 0:
             raise RuntimeError(f"rg_commit_update: {eng.L.rg_last_error().decode()}")
     el = time.perf_counter() - t0
     return {"value": G * steps / el, "unit": "group-steps/s", "steps": steps, "ms_per_step": el * 1e3 / steps,
             "entry_rows_per_step": ne / steps, "payload_bytes_per_step": nb / steps,
             "note": "tick + rg_get_update(UPDATE_ALL, slot mask 1) + rg_commit_update(RG_COMMIT_APPLIED) per step: "
-                    "the single GetUpdate / Commit hand-off (entries to persist: every replica of the engine; committed "
-                    "entries, snapshots, reads: the slot-0 replicas), sections read in place from pinned memory; "
+                    "the single GetUpdate / Commit hand-off (the slot-0 replicas' states, entries to persist as term "
+                    "runs + {len, crc}, committed entries as runs, snapshots, reads), sections read in place from pinned memory; "
                     "PCIe-bound at full batches"}
 
 

@@ -214,8 +214,12 @@ typedef struct rg_apply_batch {
   uint64_t payload_bytes;
 } rg_apply_batch;
 
-/* Persistence feed (rg_persist_collect): dragonboat's Update.EntriesToSave + pb.State + snapshot
- * metadata, which it makes durable (LogDB SaveRaftState, fsync) before a step's messages leave. */
+/* Persistence feed (rg_persist_collect, rg_get_update's persist section): dragonboat's
+ * Update.EntriesToSave + pb.State + snapshot metadata, which it makes durable (LogDB SaveRaftState,
+ * fsync) before a step's messages leave. Shipped as ranges: per replica one rg_persist_state; its
+ * entries first..last follow as 8 B each (rg_persist_entry: length and CRC), their terms as runs
+ * (rg_persist_term: term, count), their Cmds packed from payload + payload_off (each rounded up to
+ * 16 B). Entry k of a replica is index first + k, at entries[entry_off + k]. */
 typedef struct rg_persist_state {
   uint64_t group;       /* global shard id */
   uint32_t replica_id;  /* slot + 1 */
@@ -226,13 +230,31 @@ typedef struct rg_persist_state {
                            entries below first, drops those above last and at or below marker */
   uint64_t entry_off;   /* position of this replica's first entry in the entries array */
   uint32_t members, snap_members; /* voting membership now and at the snapshot */
+  uint64_t payload_off; /* byte offset of its first Cmd in the payload */
+  uint64_t term_off;    /* its first term run in the terms array */
+  uint32_t n_terms;     /* its term runs (their counts add up to last - first + 1) */
+  uint32_t _pad;
 } rg_persist_state;
 
+#define RG_PERSIST_CONFIG 0x80000000u /* rg_persist_entry.len: a ConfigChange (the low bits: its descriptor) */
 typedef struct rg_persist_entry {
-  uint64_t index, term;
-  uint32_t type, len, crc, rid; /* an application entry's Cmd: len bytes at payload + off */
-  uint64_t off;
+  uint32_t len;         /* an application entry's Cmd bytes, or RG_PERSIST_CONFIG | descriptor */
+  uint32_t crc;         /* CRC-32 of the Cmd (0 for none) */
 } rg_persist_entry;
+typedef struct rg_persist_term {
+  uint64_t term;
+  uint64_t count;       /* consecutive entries at this term */
+} rg_persist_term;
+typedef struct rg_persist_batch {
+  const rg_persist_state* states;
+  uint64_t n_states;
+  const rg_persist_entry* entries;
+  uint64_t n_entries;
+  const rg_persist_term* terms;
+  uint64_t n_terms;
+  const uint8_t* payload;
+  uint64_t payload_bytes;
+} rg_persist_batch;
 
 /* Snapshot events of the last tick (rg_snapshot_events): where dragonboat's rsm calls the state
  * machine's RecoverFromSnapshot (an InstallSnapshot restored the replica's log) and
@@ -462,13 +484,11 @@ int rg_apply_async(rg_engine* e, uint32_t slot_mask, int buf);
 int rg_apply_wait(rg_engine* e, int buf, rg_apply_batch* out);
 /* Host WAL feed: for every replica whose log or hard state changed in the last
  * tick (full != 0, or no tick yet: every replica, whole log window), one rg_persist_state and the
- * entries it rewrote, their Cmds packed (rg_persist_entry.off), gathered on the device and copied back
- * by one hipMemcpyAsync per array. Make them durable before the next tick delivers the last tick's
- * messages. *n_states / *n_entries / *pay_bytes = the counts; if one exceeds its cap nothing is copied
- * and RG_EFULL is returned. Synchronous. Restart = rg_import_replica of the replayed state. */
-int rg_persist_collect(rg_engine* e, int full, rg_persist_state* states, uint64_t cap_states, uint64_t* n_states,
-                       rg_persist_entry* entries, uint8_t* payload, uint64_t cap_entries, uint64_t* n_entries,
-                       uint64_t pay_cap, uint64_t* pay_bytes);
+ * entries it rewrote as ranges (rg_persist_batch above), gathered on the device and copied back by one
+ * hipMemcpyAsync into engine-owned pinned memory (*out points into it, valid until the next call).
+ * Make them durable before the next tick delivers the last tick's messages. Synchronous. Restart =
+ * rg_import_replica of the replayed state. */
+int rg_persist_collect(rg_engine* e, int full, rg_persist_batch* out);
 /* Snapshot events of the last tick for replicas whose slot bit is set in slot_mask, one per
  * replica in device order (slot by slot, shards ascending within a slot), compacted on the device and copied back by one hipMemcpyAsync. *n = the count;
  * if *n > cap nothing is copied and RG_EFULL is returned. Synchronous. */
@@ -490,12 +510,7 @@ int rg_snapshot_events(rg_engine* e, uint32_t slot_mask, rg_snapshot_event* even
 #define RG_UPDATE_FULL_STATE 16u /* persistence section: every replica, whole log window */
 typedef struct rg_update {
   uint64_t tick;                          /* ticks run when the update was taken */
-  const rg_persist_state* states;
-  uint64_t n_states;
-  const rg_persist_entry* entries;        /* grouped by replica; rg_persist_state.entry_off indexes it */
-  uint64_t n_entries;
-  const uint8_t* entry_payload;           /* rg_persist_entry.off into it */
-  uint64_t entry_payload_bytes;
+  rg_persist_batch persist;               /* states, entries, term runs, Cmds (rg_persist_batch) */
   rg_apply_batch committed;               /* the committed entries, as runs (rg_apply_run) */
   const rg_snapshot_event* snapshots;
   uint64_t n_snapshots;

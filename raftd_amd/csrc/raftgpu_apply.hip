@@ -191,7 +191,7 @@ __global__ void persist_count_kernel(PersistParams a) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= a.nrep) return;
   if (!((a.slot_mask >> (q / a.G)) & 1u)) {  // another node's replica: not this hand-off's to persist
-    a.scnt[q] = a.ecnt[q] = a.ccnt[q] = 0;
+    a.scnt[q] = a.ecnt[q] = a.ccnt[q] = a.tcnt[q] = 0;
     return;
   }
   const uint64_t n = a.nrep;
@@ -200,17 +200,25 @@ __global__ void persist_count_kernel(PersistParams a) {
   const auto diff = [&](uint32_t f) { return a.s64[(uint64_t)f * n + q] != a.s64_prev[(uint64_t)f * n + q]; };
   const bool changed = a.full || ne > 0 || diff(S_TERM) || diff(S_VOTE) || diff(S_COMMITTED) || diff(S_LAST) ||
                        diff(S_MARKER) || diff(S_SNAP_INDEX);
-  uint32_t cc = 0;
-  for (uint64_t i = lo; i <= last; ++i) cc += word_nc(a.tr[(i & (a.L - 1)) * n + q]);
+  uint32_t cc = 0, tc = 0;
+  uint64_t pt = ~0ull;
+  for (uint64_t i = lo; i <= last; ++i) {
+    const uint64_t w = a.tr[(i & (a.L - 1)) * n + q];
+    cc += word_nc(w);
+    tc += (w & TERM_MASK) != pt ? 1u : 0u;  // a term run starts
+    pt = w & TERM_MASK;
+  }
   a.scnt[q] = changed ? 1u : 0u;
   a.ecnt[q] = ne;
   a.ccnt[q] = cc;
+  a.tcnt[q] = tc;
 }
 
 __global__ void persist_total_kernel(const PersistParams a, uint64_t* totals) {
   totals[0] = a.soff[a.nrep];
   totals[1] = a.eoff[a.nrep];
   totals[2] = a.coff[a.nrep];
+  totals[3] = a.toff[a.nrep];
 }
 
 hipError_t launch_persist_count(const PersistParams& a, uint64_t* totals, hipStream_t st) {
@@ -218,6 +226,7 @@ hipError_t launch_persist_count(const PersistParams& a, uint64_t* totals, hipStr
   hipError_t r = launch_scan_u32(a.scnt, a.nrep, a.bsum, a.soff, st);
   if (r == hipSuccess) r = launch_scan_u32(a.ecnt, a.nrep, a.bsum, a.eoff, st);
   if (r == hipSuccess) r = launch_scan_u32(a.ccnt, a.nrep, a.bsum, a.coff, st);
+  if (r == hipSuccess) r = launch_scan_u32(a.tcnt, a.nrep, a.bsum, a.toff, st);
   if (r != hipSuccess) return r;
   hipLaunchKernelGGL(persist_total_kernel, dim3(1), dim3(1), 0, st, a, totals);
   return hipGetLastError();
@@ -245,6 +254,10 @@ __global__ void persist_state_kernel(PersistParams a) {
   r.entry_off = a.eoff[q];
   r.members = a.s32[(uint64_t)S_MEMBERS * n + q];
   r.snap_members = a.s32[(uint64_t)S_SNAP_MEMBERS * n + q];
+  r.payload_off = a.coff[q] * 16;
+  r.term_off = a.toff[q];
+  r.n_terms = a.tcnt[q];
+  r._pad = 0;
   reinterpret_cast<rg_persist_state*>(a.out_state)[a.soff[q]] = r;
 }
 
@@ -256,33 +269,59 @@ __global__ void __launch_bounds__(256) persist_entries_kernel(PersistParams a) {
   const uint64_t n64 = a.nrep, L = a.L;
   const uint64_t lo = persist_first(a, q), hi = a.s64[(uint64_t)S_LAST * n64 + q];
   const uint64_t base = a.eoff[q];
-  uint64_t cpos = a.coff[q];
+  uint64_t cpos = a.coff[q], tpos = a.toff[q];
+  uint64_t prev = ~0ull;  // the term of the entry before this stretch (~0: none yet)
+  rg_persist_term* terms = reinterpret_cast<rg_persist_term*>(a.out_term);
+  (void)s; (void)j;
   for (uint64_t i0 = lo; i0 <= hi; i0 += 64) {
     const uint64_t i = i0 + lane;
     const bool in = i <= hi;
+    const uint32_t nin = (uint32_t)(hi - i0 + 1 < 64 ? hi - i0 + 1 : 64);
     const uint64_t slot = i & (L - 1), w = in ? a.tr[slot * n64 + q] : 0;
     const uint2 inf = in ? a.info[((w >> 63) * n64 + q) * L + slot] : make_uint2(0u, 0u);
     const uint32_t nc = word_nc(w), inc = lane_inc_scan(nc);
+    const uint64_t tm = w & TERM_MASK;
+    // term runs: a head where the term differs from the previous entry's (lane 0: the last stretch's)
+    const uint32_t up = (uint32_t)__shfl_up((int)(uint32_t)tm, 1, 64), uph = (uint32_t)__shfl_up((int)(uint32_t)(tm >> 32), 1, 64);
+    const uint64_t before = lane ? ((uint64_t)uph << 32 | up) : prev;
+    const uint64_t heads = __ballot(in && tm != before);
     if (in) {
       rg_persist_entry r;
-      r.index = i;
-      r.term = w & TERM_MASK;
-      r.type = (uint32_t)((w >> 61) & 1);
-      r.len = (w & (PAY_BIT | TYPE_BIT)) ? word_len(w) : 0u;  // a ConfigChange: its descriptor
-      r.crc = (w & PAY_BIT) ? crc_of_cmd(inf.x, r.len, a.P, a.zi) : 0u;
-      r.rid = j * a.R + s;
-      r.off = (cpos + inc - nc) * 16;
+      r.len = (w & TYPE_BIT) ? (RG_PERSIST_CONFIG | word_len(w)) : (w & PAY_BIT) ? word_len(w) : 0u;
+      r.crc = (w & PAY_BIT) ? crc_of_cmd(inf.x, word_len(w), a.P, a.zi) : 0u;
       reinterpret_cast<rg_persist_entry*>(a.out_ent)[base + (i - lo)] = r;
+      if ((heads >> lane) & 1ull) {  // count: its first entry's position for now (persist_terms_kernel)
+        rg_persist_term t;
+        t.term = tm;
+        t.count = base + (i - lo);
+        terms[tpos + __builtin_popcountll(heads & ((1ull << lane) - 1))] = t;
+      }
     }
     const uint32_t total = (uint32_t)__shfl((int)inc, 63, 64);
     copy_run(a.pool, a.pt, a.PTS, q, inc, inf.y, total, a.out_pay, cpos);
     cpos += total;
+    tpos += __builtin_popcountll(heads);
+    const uint32_t ll = (uint32_t)__shfl((int)(uint32_t)tm, (int)(nin - 1), 64), lh = (uint32_t)__shfl((int)(uint32_t)(tm >> 32), (int)(nin - 1), 64);
+    prev = (uint64_t)lh << 32 | ll;
+  }
+}
+
+// thread per replica: its term runs' counts from their first entries' positions
+__global__ void persist_terms_kernel(PersistParams a) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= a.nrep || !a.tcnt[q]) return;
+  rg_persist_term* t = reinterpret_cast<rg_persist_term*>(a.out_term) + a.toff[q];
+  const uint32_t n = a.tcnt[q];
+  for (uint32_t k = 0; k < n; ++k) {
+    const uint64_t end = k + 1 < n ? t[k + 1].count : a.eoff[q] + a.ecnt[q];
+    t[k].count = end - t[k].count;
   }
 }
 
 hipError_t launch_persist_gather(const PersistParams& a, hipStream_t st) {
   hipLaunchKernelGGL(persist_state_kernel, dim3((a.nrep + 255) / 256), dim3(256), 0, st, a);
   hipLaunchKernelGGL(persist_entries_kernel, dim3((a.nrep + 3) / 4), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(persist_terms_kernel, dim3((a.nrep + 255) / 256), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

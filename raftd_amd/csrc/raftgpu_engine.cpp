@@ -62,6 +62,7 @@ static constexpr bool g_sync_debug = false;
   } while (0)
 
 constexpr uint32_t TP_SLOTS = 128, TP_CHUNK = 32;
+constexpr uint32_t D_SUM_BYTES = 128;  // rg_get_update's section totals (9 u64), digests, counters
 
 // rg_propose's per-batch scratch (kept across calls)
 struct PropScratch {
@@ -168,7 +169,7 @@ struct rg_engine {
   uint32_t* d_prop_count = nullptr;
   uint8_t* d_campaign = nullptr;
   uint8_t* d_isolate = nullptr;
-  unsigned long long* d_sum = nullptr;
+  unsigned long long* d_sum = nullptr;  // D_SUM_BYTES: small totals read back by the host
   // control_kernel's parameter block, passed by pointer (DESIGN.md §3 "The control-kernel fault"):
   // TP_SLOTS device slots, each written by a stream-ordered H2D copy from the pinned host slot of
   // the same index; tp_ev[c] follows the last copy of chunk c, so a host slot is rewritten only
@@ -260,8 +261,10 @@ struct rg_engine {
   uint64_t* persist_lo = nullptr;
   uint64_t* snap_ev = nullptr;  // [nrep] restored_at | SNAP_TAKEN_BIT of the last tick
   uint32_t* prof = nullptr;     // RG_CTL_PROFILE builds: control phase stamps of the last tick
-  uint32_t *pscnt = nullptr, *pecnt = nullptr, *pccnt = nullptr;
-  uint64_t *psoff = nullptr, *peoff = nullptr, *pcoff = nullptr;
+  uint32_t *pscnt = nullptr, *pecnt = nullptr, *pccnt = nullptr, *ptcnt = nullptr;
+  uint64_t *psoff = nullptr, *peoff = nullptr, *pcoff = nullptr, *ptoff = nullptr;
+  uint8_t* pc_host = nullptr;  // rg_persist_collect's pinned batch
+  uint64_t pc_hcap = 0;
   // rg_get_update: count / offset rows of the snapshot and read sections (the committed section
   // uses acnt / aoff, the persistence section pscnt / psoff, so every count runs before any gather),
   // and the pinned host buffer all sections land in
@@ -584,7 +587,7 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if (rc == RG_OK) rc = dalloc(e, &e->d_prop_count, G * N * 4);
   if (rc == RG_OK) rc = dalloc(e, &e->d_campaign, n * N);
   if (rc == RG_OK) rc = dalloc(e, &e->d_isolate, n * N);
-  if (rc == RG_OK) rc = dalloc(e, &e->d_sum, 64);
+  if (rc == RG_OK) rc = dalloc(e, &e->d_sum, D_SUM_BYTES);
   if (rc == RG_OK) rc = dalloc(e, &e->d_tp, (uint64_t)TP_SLOTS * sizeof(TickParams));
   if (rc == RG_OK && hipHostMalloc((void**)&e->h_tp, (uint64_t)TP_SLOTS * sizeof(TickParams), 0) != hipSuccess)
     rc = fail(RG_ENOMEM, "hipHostMalloc (parameter blocks)");
@@ -608,6 +611,8 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if (rc == RG_OK) rc = dalloc(e, &e->psoff, (n + 1) * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->peoff, (n + 1) * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->pcoff, (n + 1) * 8);
+  if (rc == RG_OK) rc = dalloc(e, &e->ptcnt, n * 4);
+  if (rc == RG_OK) rc = dalloc(e, &e->ptoff, (n + 1) * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->uscnt, n * 4);
   if (rc == RG_OK) rc = dalloc(e, &e->urcnt, n * 4);
   if (rc == RG_OK) rc = dalloc(e, &e->usoff, (n + 1) * 8);
@@ -810,6 +815,7 @@ void rg_destroy(rg_engine* e) {
     if (e->a_host[b]) (void)hipHostFree(e->a_host[b]);
   }
   if (e->ac_host) (void)hipHostFree(e->ac_host);
+  if (e->pc_host) (void)hipHostFree(e->pc_host);
   if (e->stg_ev) (void)hipEventDestroy(e->stg_ev);
   if (e->rd_ev) (void)hipEventDestroy(e->rd_ev);
   if (e->cc_ev) (void)hipEventDestroy(e->cc_ev);
@@ -1897,42 +1903,75 @@ static int astage_reserve(rg_engine* e, uint64_t bytes) {
   return RG_OK;
 }
 
-int rg_persist_collect(rg_engine* e, int full, rg_persist_state* states, uint64_t cap_states, uint64_t* n_states,
-                       rg_persist_entry* entries, uint8_t* payload, uint64_t cap_entries, uint64_t* n_entries,
-                       uint64_t pay_cap, uint64_t* pay_bytes) {
-  if (!e || !n_states || !n_entries) return fail(RG_EINVAL, "rg_persist_collect args");
-  if (int jrc = join(e)) return jrc;
+static PersistParams persist_params(rg_engine* e, bool full, uint32_t slot_mask) {
   const TickParams t = params(e);
   PersistParams a{};
   a.G = t.G; a.R = t.R; a.nrep = t.nrep; a.L = t.L; a.P = t.P; a.pl = e->pl;
   a.full = (full || e->t == 0) ? 1u : 0u;  // before the first tick there is no previous state
-  a.slot_mask = ~0u;                         // every replica this engine hosts
+  a.slot_mask = slot_mask;
   a.s64 = t.s64_in; a.s64_prev = t.s64_out; a.s32 = t.s32_in; a.persist_lo = e->persist_lo;
   a.tr = e->tr; a.info = e->info; a.pool = e->pool; a.pt = e->pt; a.PTS = e->PTS; a.zi = e->crc_tab + CRC_ZI_OFF;
-  a.scnt = e->pscnt; a.ecnt = e->pecnt; a.ccnt = e->pccnt; a.soff = e->psoff; a.eoff = e->peoff; a.coff = e->pcoff;
+  a.scnt = e->pscnt; a.ecnt = e->pecnt; a.ccnt = e->pccnt; a.tcnt = e->ptcnt;
+  a.soff = e->psoff; a.eoff = e->peoff; a.coff = e->pcoff; a.toff = e->ptoff;
   a.bsum = e->absum;
+  return a;
+}
+// the persist staging layout: [states][entries][terms][payload], each 16-B aligned (tot: states,
+// entries, chunks, terms)
+struct PersistLayout {
+  uint64_t states, entries, terms, pay, total;
+};
+static PersistLayout persist_layout(const uint64_t* tot) {
+  PersistLayout l;
+  l.states = 0;
+  l.entries = a16(tot[0] * sizeof(rg_persist_state));
+  l.terms = l.entries + a16(tot[1] * sizeof(rg_persist_entry));
+  l.pay = l.terms + a16(tot[3] * sizeof(rg_persist_term));
+  l.total = tot[0] ? l.pay + tot[2] * 16 : 0;
+  return l;
+}
+static void persist_out(PersistParams& a, uint8_t* d, const PersistLayout& l) {
+  a.out_state = d + l.states;
+  a.out_ent = d + l.entries;
+  a.out_term = d + l.terms;
+  a.out_pay = d + l.pay;
+}
+static void persist_batch(rg_persist_batch* out, const uint8_t* h, const uint64_t* tot, const PersistLayout& l) {
+  out->states = (const rg_persist_state*)(h + l.states);
+  out->n_states = tot[0];
+  out->entries = (const rg_persist_entry*)(h + l.entries);
+  out->n_entries = tot[1];
+  out->terms = (const rg_persist_term*)(h + l.terms);
+  out->n_terms = tot[3];
+  out->payload = h + l.pay;
+  out->payload_bytes = tot[2] * 16;
+}
+
+int rg_persist_collect(rg_engine* e, int full, rg_persist_batch* out) {
+  if (!e || !out) return fail(RG_EINVAL, "rg_persist_collect args");
+  if (int jrc = join(e)) return jrc;
+  *out = rg_persist_batch{};
+  PersistParams a = persist_params(e, full != 0, ~0u);  // every replica this engine hosts
   LAUNCH(launch_persist_count(a, (uint64_t*)e->d_sum, e->stream), e->stream, "persist count");
-  uint64_t tot[3] = {0, 0, 0};
-  HIPCHK(hipMemcpyAsync(tot, e->d_sum, 24, hipMemcpyDeviceToHost, e->stream));
+  uint64_t tot[4] = {0, 0, 0, 0};
+  HIPCHK(hipMemcpyAsync(tot, e->d_sum, 32, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
-  *n_states = tot[0];
-  *n_entries = tot[1];
-  const uint64_t pb = tot[2] * 16;
-  if (pay_bytes) *pay_bytes = pb;
-  if (tot[0] > cap_states || tot[1] > cap_entries || pb > pay_cap)
-    return fail(RG_EFULL, "rg_persist_collect: buffers too small");
   if (tot[0] == 0) return RG_OK;
-  if (!states || (tot[1] && !entries) || (pb && !payload)) return fail(RG_EINVAL, "rg_persist_collect: null output");
-  const uint64_t sb = a16(tot[0] * sizeof(rg_persist_state)), eb = a16(tot[1] * sizeof(rg_persist_entry));
-  RGCHK(astage_reserve(e, sb + eb + pb));
-  a.out_state = e->astage;
-  a.out_ent = e->astage + sb;
-  a.out_pay = e->astage + sb + eb;
+  const PersistLayout l = persist_layout(tot);
+  RGCHK(astage_reserve(e, l.total));
+  if (l.total > e->pc_hcap) {
+    if (e->pc_host) (void)hipHostFree(e->pc_host);
+    e->pc_host = nullptr;
+    e->pc_hcap = 0;
+    const uint64_t nb = std::max<uint64_t>(l.total * 5 / 4, 1 << 20);
+    if (hipHostMalloc((void**)&e->pc_host, nb, 0) != hipSuccess) return fail(RG_ENOMEM, "hipHostMalloc (persist)");
+    e->pc_hcap = nb;
+  }
+  persist_out(a, e->astage, l);
   LAUNCH(launch_persist_gather(a, e->stream), e->stream, "persist gather");
-  HIPCHK(hipMemcpyAsync(states, a.out_state, tot[0] * sizeof(rg_persist_state), hipMemcpyDeviceToHost, e->stream));
-  if (tot[1]) HIPCHK(hipMemcpyAsync(entries, a.out_ent, tot[1] * sizeof(rg_persist_entry), hipMemcpyDeviceToHost, e->stream));
-  if (pb) HIPCHK(hipMemcpyAsync(payload, a.out_pay, pb, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(e->pc_host, e->astage, l.total, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
+  persist_batch(out, e->pc_host, tot, l);
   return RG_OK;
 }
 
@@ -2257,15 +2296,11 @@ int rg_get_update(rg_engine* e, uint32_t slot_mask, uint32_t flags, rg_update* o
   out->slot_mask = slot_mask;
   out->flags = flags;
   const TickParams t = params(e);
-  uint64_t* sum = (uint64_t*)e->d_sum;  // [0..2] persist, [3..4] committed, [5] snapshots, [6] reads
-  PersistParams pa{};
-  pa.G = t.G; pa.R = t.R; pa.nrep = t.nrep; pa.L = t.L; pa.P = t.P; pa.pl = e->pl;
-  pa.full = ((flags & RG_UPDATE_FULL_STATE) || e->t == 0) ? 1u : 0u;
-  pa.slot_mask = slot_mask;  // a node persists its own replicas only (4.3 GB of others' entries)
-  pa.s64 = t.s64_in; pa.s64_prev = t.s64_out; pa.s32 = t.s32_in; pa.persist_lo = e->persist_lo;
-  pa.tr = e->tr; pa.info = e->info; pa.pool = e->pool; pa.pt = e->pt; pa.PTS = e->PTS; pa.zi = e->crc_tab + CRC_ZI_OFF;
-  pa.scnt = e->pscnt; pa.ecnt = e->pecnt; pa.ccnt = e->pccnt; pa.soff = e->psoff; pa.eoff = e->peoff; pa.coff = e->pcoff;
-  pa.bsum = e->absum;
+  // [0..3] persist (states, entries, chunks, terms), [4..6] committed (entries, chunks, runs),
+  // [7] snapshots, [8] reads
+  uint64_t* sum = (uint64_t*)e->d_sum;
+  // a node persists its own replicas only (4.3 GB of others' entries)
+  PersistParams pa = persist_params(e, (flags & RG_UPDATE_FULL_STATE) != 0, slot_mask);
   ApplyParams aa = apply_params(e, slot_mask);
   SnapParams sa{};
   sa.G = t.G; sa.R = t.R; sa.nrep = t.nrep; sa.slot_mask = slot_mask; sa.pl = e->pl;
@@ -2273,21 +2308,19 @@ int rg_get_update(rg_engine* e, uint32_t slot_mask, uint32_t flags, rg_update* o
   sa.cnt = e->uscnt; sa.off = e->usoff; sa.bsum = e->absum;
   SnapParams ra = sa;
   ra.cnt = e->urcnt; ra.off = e->uroff;
-  HIPCHK(hipMemsetAsync(sum, 0, 64, e->stream));
+  HIPCHK(hipMemsetAsync(sum, 0, D_SUM_BYTES, e->stream));
   if (flags & RG_UPDATE_PERSIST) LAUNCH(launch_persist_count(pa, sum, e->stream), e->stream, "persist count");
-  if (flags & RG_UPDATE_COMMITTED) LAUNCH(launch_apply_count(aa, sum + 3, e->stream), e->stream, "apply count");
-  if (flags & RG_UPDATE_SNAPSHOTS) LAUNCH(launch_snap_count(sa, sum + 6, e->stream), e->stream, "snapshot count");
-  if (flags & RG_UPDATE_READS) LAUNCH(launch_read_count(ra, sum + 7, e->stream), e->stream, "read count");
-  uint64_t tot[8] = {};
-  HIPCHK(hipMemcpyAsync(tot, sum, 64, hipMemcpyDeviceToHost, e->stream));
+  if (flags & RG_UPDATE_COMMITTED) LAUNCH(launch_apply_count(aa, sum + 4, e->stream), e->stream, "apply count");
+  if (flags & RG_UPDATE_SNAPSHOTS) LAUNCH(launch_snap_count(sa, sum + 7, e->stream), e->stream, "snapshot count");
+  if (flags & RG_UPDATE_READS) LAUNCH(launch_read_count(ra, sum + 8, e->stream), e->stream, "read count");
+  uint64_t tot[D_SUM_BYTES / 8] = {};
+  HIPCHK(hipMemcpyAsync(tot, sum, D_SUM_BYTES, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   // one staging layout for every section, each 16-B aligned
-  const ApplyLayout al = apply_layout(tot + 3);  // committed: entries, chunks, runs
-  const uint64_t sb = a16(tot[0] * sizeof(rg_persist_state)), eb = a16(tot[1] * sizeof(rg_persist_entry)),
-                 epb = tot[2] * 16, cb = al.total,
-                 snb = a16(tot[6] * sizeof(rg_snapshot_event)), rdb = a16(tot[7] * sizeof(rg_read_ready));
-  const uint64_t o_e = sb, o_ep = o_e + eb, o_c = o_ep + epb, o_s = o_c + cb, o_r = o_s + snb,
-                 total = o_r + rdb;
+  const PersistLayout pl = persist_layout(tot);
+  const ApplyLayout al = apply_layout(tot + 4);  // committed: entries, chunks, runs
+  const uint64_t snb = a16(tot[7] * sizeof(rg_snapshot_event)), rdb = a16(tot[8] * sizeof(rg_read_ready));
+  const uint64_t o_c = pl.total, o_s = o_c + al.total, o_r = o_s + snb, total = o_r + rdb;
   if (total == 0) return RG_OK;
   RGCHK(astage_reserve(e, total));
   if (total > e->u_hcap) {
@@ -2300,40 +2333,33 @@ int rg_get_update(rg_engine* e, uint32_t slot_mask, uint32_t flags, rg_update* o
   }
   uint8_t* d = e->astage;
   if (tot[0]) {
-    pa.out_state = d;
-    pa.out_ent = d + o_e;
-    pa.out_pay = d + o_ep;
+    persist_out(pa, d, pl);
     LAUNCH(launch_persist_gather(pa, e->stream), e->stream, "persist gather");
   }
-  if (tot[3]) {
+  if (tot[4]) {
     aa.out_run = d + o_c + al.runs;
     aa.out_cmd = d + o_c + al.cmds;
     aa.out_pay = d + o_c + al.pay;
-    LAUNCH(launch_apply_gather(aa, tot[5], e->stream), e->stream, "apply gather");
+    LAUNCH(launch_apply_gather(aa, tot[6], e->stream), e->stream, "apply gather");
   }
-  if (tot[6]) {
+  if (tot[7]) {
     sa.out = d + o_s;
     LAUNCH(launch_snap_gather(sa, e->stream), e->stream, "snapshot gather");
   }
-  if (tot[7]) {
+  if (tot[8]) {
     ra.out = d + o_r;
     LAUNCH(launch_read_gather(ra, e->stream), e->stream, "read gather");
   }
   HIPCHK(hipMemcpyAsync(e->u_host, d, total, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   uint8_t* h = e->u_host;
-  out->states = (const rg_persist_state*)h;
-  out->n_states = tot[0];
-  out->entries = (const rg_persist_entry*)(h + o_e);
-  out->n_entries = tot[1];
-  out->entry_payload = h + o_ep;
-  out->entry_payload_bytes = epb;
+  if (tot[0]) persist_batch(&out->persist, h, tot, pl);
   out->committed = rg_apply_batch{};
-  if (tot[3]) apply_batch(&out->committed, h + o_c, tot + 3, al);
+  if (tot[4]) apply_batch(&out->committed, h + o_c, tot + 4, al);
   out->snapshots = (const rg_snapshot_event*)(h + o_s);
-  out->n_snapshots = tot[6];
+  out->n_snapshots = tot[7];
   out->reads = (const rg_read_ready*)(h + o_r);
-  out->n_reads = tot[7];
+  out->n_reads = tot[8];
   return RG_OK;
 }
 

@@ -470,15 +470,19 @@ struct PersistParams {
   uint32_t* scnt;            // [nrep] 1 if the replica has a record
   uint32_t* ecnt;            // [nrep] entries to save
   uint32_t* ccnt;            // [nrep] their payload chunks
+  uint32_t* tcnt;            // [nrep] their term runs
   uint64_t* soff;            // [nrep + 1]
   uint64_t* eoff;            // [nrep + 1]
   uint64_t* coff;            // [nrep + 1]
+  uint64_t* toff;            // [nrep + 1]
   uint64_t* bsum;
   uint8_t* out_state;        // [ns] rg_persist_state
-  uint8_t* out_ent;          // [ne] rg_persist_entry
+  uint8_t* out_ent;          // [ne] rg_persist_entry (8 B: len, crc)
+  uint8_t* out_term;         // [nt] rg_persist_term
   uint8_t* out_pay;          // [chunks][16]
 };
-hipError_t launch_persist_count(const PersistParams& a, uint64_t* totals /*[3]: states, entries, chunks*/, hipStream_t s);
+hipError_t launch_persist_count(const PersistParams& a, uint64_t* totals /*[4]: states, entries, chunks, terms*/,
+                                hipStream_t s);
 hipError_t launch_persist_gather(const PersistParams& a, hipStream_t s);
 hipError_t launch_apply_gather(const ApplyParams& a, uint64_t nruns, hipStream_t s);
 // exclusive scan of n u32 into out[0..n] (out[n] = total); bsum: (n + 1023) / 1024 + 1 words

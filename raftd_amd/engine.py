@@ -127,9 +127,60 @@ def batch_arrays(b: "ApplyBatch", copy: bool = True):
 PERSIST_STATE_DTYPE = np.dtype([("group", "<u8"), ("replica_id", "<u4"), ("rid", "<u4"), ("term", "<u8"),
                                 ("vote", "<u8"), ("commit", "<u8"), ("last", "<u8"), ("marker", "<u8"),
                                 ("marker_term", "<u8"), ("snap_index", "<u8"), ("snap_term", "<u8"),
-                                ("first", "<u8"), ("entry_off", "<u8"), ("members", "<u4"), ("snap_members", "<u4")])
+                                ("first", "<u8"), ("entry_off", "<u8"), ("members", "<u4"), ("snap_members", "<u4"),
+                                ("payload_off", "<u8"), ("term_off", "<u8"), ("n_terms", "<u4"), ("_pad", "<u4")])
+PERSIST_CMD_DTYPE = np.dtype([("len", "<u4"), ("crc", "<u4")])  # rg_persist_entry
+PERSIST_TERM_DTYPE = np.dtype([("term", "<u8"), ("count", "<u8")])  # rg_persist_term
+PERSIST_CONFIG = 0x80000000  # RG_PERSIST_CONFIG
+# one row per entry, expanded on the host from the ranges (what wal.py and the tests consume)
 PERSIST_ENTRY_DTYPE = np.dtype([("index", "<u8"), ("term", "<u8"), ("type", "<u4"), ("len", "<u4"), ("crc", "<u4"),
                                 ("rid", "<u4"), ("off", "<u8")])
+
+
+class PersistBatch(C.Structure):
+    """rg_persist_batch: per replica a state record, its entries as {len, crc}, their terms as runs,
+    the Cmds packed."""
+    _fields_ = [("states", C.c_void_p), ("n_states", C.c_uint64), ("entries", C.c_void_p), ("n_entries", C.c_uint64),
+                ("terms", C.c_void_p), ("n_terms", C.c_uint64), ("payload", C.c_void_p), ("payload_bytes", C.c_uint64)]
+
+
+def persist_arrays(b: "PersistBatch", copy: bool = True):
+    """(states, entries, terms, payload) numpy arrays of an rg_persist_batch."""
+    def arr(ptr, n, dt):
+        if not n or not ptr:
+            return np.zeros(0, dt)
+        a = np.frombuffer((C.c_uint8 * (n * dt.itemsize)).from_address(ptr), dtype=dt)
+        return a.copy() if copy else a
+    return (arr(b.states, b.n_states, PERSIST_STATE_DTYPE), arr(b.entries, b.n_entries, PERSIST_CMD_DTYPE),
+            arr(b.terms, b.n_terms, PERSIST_TERM_DTYPE), arr(b.payload, b.payload_bytes, np.dtype(np.uint8)))
+
+
+def expand_persist(states, ents, terms):
+    """PERSIST_ENTRY_DTYPE rows (index, term, type, len, crc, rid, off) from a persist batch's ranges:
+    replica r's entry k is index r.first + k at entries[r.entry_off + k]; its term comes from the
+    runs terms[r.term_off : r.term_off + r.n_terms]; its Cmd at r.payload_off + the 16-B-rounded
+    lengths of the replica's earlier application entries (include/raftgpu.h, rg_persist_state)."""
+    n = len(ents)
+    out = np.zeros(n, PERSIST_ENTRY_DTYPE)
+    if not n:
+        return out
+    fi, la = states["first"], states["last"]  # first > last (first may be ~0): no entries
+    cnt = np.where(fi <= la, la - np.minimum(fi, la) + 1, 0).astype(np.int64)
+    six = np.repeat(np.arange(len(states)), cnt)  # each entry's state record
+    pos = np.arange(n, dtype=np.int64)
+    k = pos - states["entry_off"].astype(np.int64)[six]
+    out["index"] = states["first"][six] + k.astype(np.uint64)
+    out["rid"] = states["rid"][six]
+    out["term"] = np.repeat(terms["term"], terms["count"].astype(np.int64))
+    cfg = (ents["len"] & PERSIST_CONFIG) != 0
+    out["type"] = cfg.astype(np.uint32)
+    out["len"] = ents["len"] & ~np.uint32(PERSIST_CONFIG)
+    out["crc"] = ents["crc"]
+    rounded = np.where(cfg, 0, (ents["len"].astype(np.uint64) + 15) // 16 * 16).astype(np.uint64)
+    excl = np.cumsum(rounded) - rounded
+    first_pos = states["entry_off"].astype(np.int64)[six]
+    out["off"] = states["payload_off"][six] + excl - excl[first_pos]
+    return out
 
 
 ROW_CAP = 65536  # longest max_cmd_bytes shown as fixed-width rows; beyond it rows are as wide as the batch needs
@@ -198,9 +249,7 @@ class Transport(C.Structure):
 
 class Update(C.Structure):
     """rg_update (include/raftgpu.h): rg_get_update's sections, pointers into engine-owned pinned memory."""
-    _fields_ = [("tick", C.c_uint64), ("states", C.c_void_p), ("n_states", C.c_uint64), ("entries", C.c_void_p),
-                ("n_entries", C.c_uint64), ("entry_payload", C.c_void_p), ("entry_payload_bytes", C.c_uint64),
-                ("committed", ApplyBatch), ("snapshots", C.c_void_p), ("n_snapshots", C.c_uint64),
+    _fields_ = [("tick", C.c_uint64), ("persist", PersistBatch), ("committed", ApplyBatch), ("snapshots", C.c_void_p), ("n_snapshots", C.c_uint64),
                 ("reads", C.c_void_p), ("n_reads", C.c_uint64), ("slot_mask", C.c_uint32), ("flags", C.c_uint32)]
 
 
@@ -311,8 +360,7 @@ def load_library(path: str = LIB_PATH):
         "rg_commit_update": ([vp, C.POINTER(Update), u32], i32),
         "rg_probe_copy": ([C.c_int32, u64, C.c_int32, C.POINTER(C.c_double)], i32),
         "rg_snapshot_events": ([vp, u32, vp, u64, C.POINTER(C.c_uint64)], i32),
-        "rg_persist_collect": ([vp, i32, vp, u64, C.POINTER(C.c_uint64), vp, vp, u64, C.POINTER(C.c_uint64), u64,
-                                C.POINTER(C.c_uint64)], i32),
+        "rg_persist_collect": ([vp, i32, vp], i32),
     }
     for name, (args, res) in sig.items():
         if os.environ.get("RAFTGPU_LIB") and not hasattr(L, name):
@@ -675,19 +723,17 @@ class Engine:
     def persist_collect(self, full: bool = False):
         """Host WAL feed of the last tick (rg_persist_collect): (states, entries, payload) numpy
         arrays — PERSIST_STATE_DTYPE rows, PERSIST_ENTRY_DTYPE rows, one Cmd row per entry (row_width)."""
-        ns, ne, pb = C.c_uint64(), C.c_uint64(), C.c_uint64()
-        rc = self.L.rg_persist_collect(self.h, 1 if full else 0, None, 0, C.byref(ns), None, None, 0, C.byref(ne),
-                                       0, C.byref(pb))
-        if rc < 0 and rc != RG_EFULL:
-            self._check(rc)
-        st = np.zeros(max(ns.value, 1), PERSIST_STATE_DTYPE)
-        en = np.zeros(max(ne.value, 1), PERSIST_ENTRY_DTYPE)
-        packed = np.zeros(max(pb.value, 16), np.uint8)
-        self._check(self.L.rg_persist_collect(self.h, 1 if full else 0, st.ctypes.data, ns.value, C.byref(ns),
-                                              en.ctypes.data, packed.ctypes.data, ne.value, C.byref(ne),
-                                              packed.size, C.byref(pb)))
-        en = en[:ne.value]
-        return st[:ns.value], en, unpack_rows(en, packed[:pb.value], row_width(en, self.row))
+        b = PersistBatch()
+        self._check(self.L.rg_persist_collect(self.h, 1 if full else 0, C.byref(b)))
+        st, ents, terms, packed = persist_arrays(b)
+        en = expand_persist(st, ents, terms)
+        return st, en, unpack_rows(en, packed, row_width(en, self.row))
+
+    def persist_batch(self, full: bool = False, copy: bool = True):
+        """rg_persist_collect's ranges as (states, entries {len, crc}, term runs, payload) arrays."""
+        b = PersistBatch()
+        self._check(self.L.rg_persist_collect(self.h, 1 if full else 0, C.byref(b)))
+        return persist_arrays(b, copy)
 
     def get_update(self, slot_mask: int = 0xFF, flags: int = UPDATE_ALL):
         """rg_get_update: the last tick's whole hand-off in one call. Returns (raw rg_update, dict of
@@ -700,10 +746,9 @@ class Engine:
                 return np.zeros(0, dt)
             return np.frombuffer((C.c_uint8 * (n * dt.itemsize)).from_address(ptr), dtype=dt).copy()
 
-        out = {"states": arr(u.states, u.n_states, PERSIST_STATE_DTYPE),
-               "entries": arr(u.entries, u.n_entries, PERSIST_ENTRY_DTYPE),
-               "entry_payload": arr(u.entry_payload, u.entry_payload_bytes, np.dtype(np.uint8)),
-               "committed": None, "committed_payload": None,
+        st, ents, terms, epay = persist_arrays(u.persist)
+        out = {"states": st, "entries": expand_persist(st, ents, terms), "entry_payload": epay,
+               "persist_terms": terms, "committed": None, "committed_payload": None,
                "snapshots": arr(u.snapshots, u.n_snapshots, SNAPSHOT_EVENT_DTYPE),
                "reads": arr(u.reads, u.n_reads, READ_READY_DTYPE)}
         runs, cmds, out["committed_payload"] = batch_arrays(u.committed)

@@ -60,6 +60,37 @@
 /* IOnDiskStateMachine.Update from a copy-back batch, the way a cgo shim walks it: per run, entry k is
  * index first + k, its Cmd at off + the 16-B-rounded lengths before it; each replica's state machine
  * receives its entries in index order (a running CRC over the Cmds, the count, the longest Cmd) */
+/* The WAL writer's walk of a persistence batch (the shim fsyncs these): per replica its entries
+ * first..last, their terms from the runs, each application Cmd at the replica's payload_off + the
+ * rounded lengths before it; a ConfigChange's len is RG_PERSIST_CONFIG | its descriptor. */
+static void persist_walk(const rg_persist_batch* b) {
+  uint64_t seen = 0, tseen = 0;
+  for (uint64_t s = 0; s < b->n_states; ++s) {
+    const rg_persist_state* st = &b->states[s];
+    const uint64_t n = st->first <= st->last ? st->last - st->first + 1 : 0;
+    EXPECT(st->entry_off == seen && st->term_off == tseen);
+    uint64_t cnt = 0, prev = 0;
+    for (uint32_t k = 0; k < st->n_terms; ++k) {
+      const rg_persist_term* t = &b->terms[st->term_off + k];
+      EXPECT(t->count >= 1 && t->term > prev); /* terms only grow along a log */
+      prev = t->term;
+      cnt += t->count;
+    }
+    EXPECT(cnt == n);
+    uint64_t off = st->payload_off;
+    for (uint64_t k = 0; k < n; ++k) {
+      const rg_persist_entry* p = &b->entries[st->entry_off + k];
+      if (p->len & RG_PERSIST_CONFIG) continue;
+      EXPECT(off + p->len <= b->payload_bytes);
+      if (p->len) EXPECT(p->crc == (uint32_t)crc32(0, b->payload + off, p->len));
+      off += (p->len + 15u) & ~15u;
+    }
+    seen += n;
+    tseen += st->n_terms;
+  }
+  EXPECT(seen == b->n_entries && tseen == b->n_terms);
+}
+
 static void consume(const rg_apply_batch* b, uint64_t* got, uint32_t* got_crc, uint64_t* last_idx,
                     uint32_t* longest) {
   uint64_t seen = 0;
@@ -206,13 +237,8 @@ int main(int argc, char** argv) {
     /* Peer.GetUpdate: the whole hand-off of the tick in one call (engine-owned pinned sections) */
     rg_update u;
     CHECK(rg_get_update(e, 0xFF, RG_UPDATE_PERSIST | RG_UPDATE_COMMITTED, &u));
-    EXPECT(u.tick == (uint64_t)ticks && u.n_states > 0);
-    for (uint64_t i = 0; i < u.n_entries; ++i) { /* the shim fsyncs these; a ConfigChange's len is its descriptor */
-      const rg_persist_entry* p = &u.entries[i];
-      EXPECT(p->type != RG_ENTRY_APPLICATION || p->off + p->len <= u.entry_payload_bytes);
-      if (p->type == RG_ENTRY_APPLICATION && p->len)
-        EXPECT(p->crc == (uint32_t)crc32(0, u.entry_payload + p->off, p->len));
-    }
+    EXPECT(u.tick == (uint64_t)ticks && u.persist.n_states > 0);
+    persist_walk(&u.persist);
     consume(&u.committed, got, got_crc, last_idx, &longest);
     /* Peer.Commit: the app answered, applied = processed (config changes and no-ops included) */
     CHECK(rg_commit_update(e, &u, RG_COMMIT_APPLIED));

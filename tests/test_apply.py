@@ -156,3 +156,29 @@ def test_expand_apply_runs_with_gaps():
     assert list(out["off"]) == [0, 16, 32, 80, 96, 400]
     assert list(out["len"]) == [5, 16, 17, 1, 300, 2] and list(out["crc"]) == [1, 2, 3, 4, 5, 6]
     assert len(expand_apply(np.zeros(0, APPLY_RUN_DTYPE), np.zeros(0, APPLY_CMD_DTYPE))) == 0
+
+
+def test_expand_persist_ranges():
+    """expand_persist (the host view of rg_persist_collect's ranges): per replica entries first..last
+    at entry_off, terms from its runs, Cmds at payload_off + the rounded lengths of its earlier
+    application entries (a ConfigChange's len is RG_PERSIST_CONFIG | descriptor, no Cmd bytes); a
+    replica whose state changed without new entries has no rows."""
+    from raftd_amd.engine import (PERSIST_CMD_DTYPE, PERSIST_CONFIG, PERSIST_STATE_DTYPE, PERSIST_TERM_DTYPE,
+                                  expand_persist)
+    st = np.zeros(3, PERSIST_STATE_DTYPE)
+    st["rid"] = [4, 5, 6]
+    st["first"], st["last"] = [20, 2**64 - 1, 7], [23, 8, 8]  # replica 5: a vote only (first > last)
+    st["entry_off"], st["payload_off"], st["term_off"], st["n_terms"] = [0, 4, 4], [0, 64, 64], [0, 2, 2], [2, 0, 1]
+    ents = np.zeros(6, PERSIST_CMD_DTYPE)
+    ents["len"] = [5, PERSIST_CONFIG | 0x23, 0, 33, 16, 1]
+    ents["crc"] = [1, 0, 0, 4, 5, 6]
+    terms = np.zeros(3, PERSIST_TERM_DTYPE)
+    terms["term"], terms["count"] = [3, 4, 7], [1, 3, 2]
+    out = expand_persist(st, ents, terms)
+    assert list(out["index"]) == [20, 21, 22, 23, 7, 8]
+    assert list(out["rid"]) == [4, 4, 4, 4, 6, 6]
+    assert list(out["term"]) == [3, 4, 4, 4, 7, 7]
+    assert list(out["type"]) == [0, 1, 0, 0, 0, 0]
+    assert list(out["len"]) == [5, 0x23, 0, 33, 16, 1]
+    assert list(out["off"]) == [0, 16, 16, 16, 64, 80]
+    assert len(expand_persist(st[1:2], np.zeros(0, PERSIST_CMD_DTYPE), np.zeros(0, PERSIST_TERM_DTYPE))) == 0

@@ -56,7 +56,7 @@ def test_get_update_equals_the_separate_calls():
         # records of those replicas, in the same order, with their own offsets
         keep = ((MASK >> (st["replica_id"].astype(np.int64) - 1)) & 1) == 1
         ekeep = ((MASK >> (en["rid"].astype(np.int64) % R)) & 1) == 1
-        nooff = [f for f in st.dtype.names if f != "entry_off"]
+        nooff = [f for f in st.dtype.names if f not in ("entry_off", "payload_off", "term_off")]
         assert rfn.repack_fields(out["states"][nooff]).tobytes() == rfn.repack_fields(st[keep][nooff]).tobytes(), t
         eo = [f for f in en.dtype.names if f != "off"]
         assert rfn.repack_fields(out["entries"][eo]).tobytes() == rfn.repack_fields(en[ekeep][eo]).tobytes(), t
@@ -157,6 +157,10 @@ def test_get_update_against_oracle():
                 assert int(s[k]) == v[f], (t, rid, k)
             first, last, lo = int(s["first"]), int(s["last"]), int(s["entry_off"])
             assert first > v["marker"]
+            # the terms travel as runs: one per stretch of equal terms, strictly growing, covering first..last
+            runs = out["persist_terms"][int(s["term_off"]):int(s["term_off"]) + int(s["n_terms"])]
+            assert int(runs["count"].sum()) == max(0, last - first + 1), (t, rid)
+            assert np.all(np.diff(runs["term"].astype(np.int64)) > 0) and np.all(runs["count"] > 0), (t, rid)
             for k, i in enumerate(range(first, last + 1)):
                 pe, oe = ents[lo + k], ora.entry(rid, i, with_payload=True)
                 assert (int(pe["index"]), int(pe["term"]), int(pe["type"]), int(pe["len"]), int(pe["crc"])) == \

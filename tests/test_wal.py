@@ -10,7 +10,7 @@ P = 16
 
 def rec(group, slot, term, commit, first, last, marker=0, ents=(), vote=0):
     st = np.zeros(1, PERSIST_STATE_DTYPE)
-    st[0] = (group, slot + 1, 0, term, vote, commit, last, marker, term if marker else 0, marker, 0, first, 0, 7, 7)
+    st[0] = (group, slot + 1, 0, term, vote, commit, last, marker, term if marker else 0, marker, 0, first, 0, 7, 7, 0, 0, 0, 0)
     en = np.zeros(len(ents), PERSIST_ENTRY_DTYPE)
     pay = np.zeros((len(ents), P), np.uint8)
     for k, (i, t, ln) in enumerate(ents):
