@@ -187,3 +187,22 @@ def test_control_step_term_limit():
     """The 36-bit term boundary on the control step compiled for the CPU, as on the oracles."""
     assert K.run_term_limit("ctl", K.TERM_MAX - 1) == ("candidate", K.TERM_MAX, 0, 2)
     assert K.run_term_limit("ctl", K.TERM_MAX) == ("follower", K.TERM_MAX, K.ERR_TERM_LIMIT, 0)
+
+
+def test_control_step_under_msan():
+    """The control step compiled for the CPU under MemorySanitizer (clang's; tests/native/ctl_msan.cpp,
+    a stand-alone driver: MSan needs an instrumented executable): no branch, address or store of the
+    step depends on a value it never initialised — over the steady C3 shape and chaos, every R, the
+    full / fast / latency builds, local and remote inboxes (the control-kernel fault)."""
+    clang = "/opt/rocm/lib/llvm/bin/clang++"
+    if not os.path.exists(clang):
+        pytest.skip("no clang with MemorySanitizer")
+    out = os.path.join(HERE, "native", "build", "ctl_msan")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    subprocess.run([clang, "-fsanitize=memory", "-fsanitize-memory-track-origins=2", "-fno-omit-frame-pointer",
+                    "-O1", "-g", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+                    os.path.join(HERE, "native", "ctl_msan.cpp"), "-o", out], check=True, timeout=900)
+    r = subprocess.run([out], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "MSAN-CLEAN" in r.stdout, r.stderr[-3000:]
+    probe = subprocess.run([out], capture_output=True, text=True, timeout=600, env=dict(os.environ, CTL_MSAN_PROBE="1"))
+    assert probe.returncode != 0 and "use-of-uninitialized-value" in probe.stderr  # the sanitizer is live
