@@ -77,6 +77,9 @@ RG_FN void sfor(F&& f) {
 // remote slot f of a per-replica array, with constant indices only (the arrays stay in registers)
 // Diagnostic variants (RG_AB_SV_*): Ctl's slot in one class of uses is laundered through a VGPR
 // move (Ctl::slot_lane), so the compiler treats it as per-lane there (the fault)
+#ifndef RG_CTL_RELOAD_FAST
+#define RG_CTL_RELOAD_FAST 0
+#endif
 #ifdef RG_AB_SV_SEND
 #define RG_S_SEND slot_lane()
 #else
@@ -144,7 +147,22 @@ struct Ctl {
   // the tick's parameter block, read in place at each use (a device slot the host filled): the
   // fields are reloaded where needed instead of living in registers for the whole step (r02 kept a
   // 368-B copy, 279 SGPR spills at R = 3)
-  CTickParams& p;
+  CTickParams& p_;
+  // P(): the parameter block. In the full step (FAST = false; the fast step too with
+  // RG_CTL_RELOAD_FAST) each use loads the field it needs through a pointer the compiler cannot see
+  // through, so the loads are not hoisted to the kernel entry and no pointer stays live in an SGPR
+  // for the whole step: control_slow_kernel<3> 456 → 66 SGPR spills (into VGPR lanes), <5> 429 → 72.
+  // A field is one scalar-cache hit away at each use. RG_AB_CTL_HOIST: r04's hoisted loads (A/B)
+  RG_FN CTickParams& P() const {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(RG_AB_CTL_HOIST)
+    if constexpr (!FAST || RG_CTL_RELOAD_FAST) {
+      CTickParams* r = &p_;
+      asm volatile("" : "+s"(r));
+      return *r;
+    }
+#endif
+    return p_;
+  }
   bool aborted = false;  // FAST: the step left the fast path (the full kernel re-runs it)
   uint32_t q, g, s;    // g = local column (indexes every device array)
   uint64_t gg, rid;    // global group and global replica id gg·R + s (RNG keys, loss hash)
@@ -185,13 +203,13 @@ struct Ctl {
   RG_FN Ctl(CTickParams& pp, uint32_t qq) : Ctl(pp, qq / pp.G, qq - (qq / pp.G) * pp.G) {}
   // slot ss of group column g0: the kernels pass a wave-uniform slot (the grid's y index), so every
   // value derived from s alone (its outbox planes, the sender loop's skip, my_id) stays scalar
-  RG_FN Ctl(CTickParams& pp, uint32_t ss, uint32_t g0) : p(pp), q(ss * pp.G + g0), g(g0), s(ss) {
-    gg = pl_group(p.pl, RG_S_ID, g);
+  RG_FN Ctl(CTickParams& pp, uint32_t ss, uint32_t g0) : p_(pp), q(ss * pp.G + g0), g(g0), s(ss) {
+    gg = pl_group(P().pl, RG_S_ID, g);
     rid = gg * R + RG_S_ID;
-    gi = (uint32_t)pl_input_index(p.pl, gg);
-    const uint64_t n = p.nrep;
-    const uint64_t* a = p.s64_in + q;
-    const uint32_t* b = p.s32_in + q;
+    gi = (uint32_t)pl_input_index(P().pl, gg);
+    const uint64_t n = P().nrep;
+    const uint64_t* a = P().s64_in + q;
+    const uint32_t* b = P().s32_in + q;
     term = a[S_TERM * n]; leader = a[S_LEADER * n]; committed = a[S_COMMITTED * n];
     last = a[S_LAST * n]; marker = a[S_MARKER * n]; marker_term = a[S_MARKER_TERM * n];
     cap_base = a[S_CAP_BASE * n];
@@ -209,12 +227,12 @@ struct Ctl {
     }
     sfor<0, R>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
-      rm[j] = p.rem_in[(0 * R + j) * n + q];
-      rn[j] = p.rem_in[(1 * R + j) * n + q];
+      rm[j] = P().rem_in[(0 * R + j) * n + q];
+      rn[j] = P().rem_in[(1 * R + j) * n + q];
       if constexpr (LEAN) rs[0] = 0;  // LEAN: copied through by store()
-      else if constexpr (RS_MEM) p.rem_out[(2 * R + j) * n + q] = p.rem_in[(2 * R + j) * n + q];
-      else rs[j] = p.rem_in[(2 * R + j) * n + q];
-      rt[j] = p.rst_in[j * n + q];
+      else if constexpr (RS_MEM) P().rem_out[(2 * R + j) * n + q] = P().rem_in[(2 * R + j) * n + q];
+      else rs[j] = P().rem_in[(2 * R + j) * n + q];
+      rt[j] = P().rst_in[j * n + q];
     });
     if (last > marker) lt_set(last, *tr_at(last) & TERM_MASK);  // issued early, used after the inbox headers
     last_start = last; sent_hi = 0; rw_lo = ~0ull; rw_hi = 0; marker_start = marker;
@@ -233,8 +251,8 @@ struct Ctl {
       if (const uint64_t fi = a[S_FIDX * n]) {
         uint32_t bound = hw;
         if (fi <= last) {
-          const uint64_t sl = fi & (p.L - 1), bank = *tr_at(fi) >> 63;
-          bound = p.info[(bank * n + q) * p.L + sl].y;
+          const uint64_t sl = fi & (P().L - 1), bank = *tr_at(fi) >> 63;
+          bound = P().info[(bank * n + q) * P().L + sl].y;
         }
         nlpg = vpn_of(bound);
       }
@@ -268,17 +286,17 @@ struct Ctl {
 #define RG_GET(arr, f) sel_get<R>(arr, f)
 #define RG_SET(arr, f, val) sel_set<R>(arr, f, val)
   RG_FN uint64_t rs_get(uint32_t f) const {
-    if constexpr (RS_MEM) return p.rem_out[((uint64_t)(2 * R) + f) * p.nrep + q];
+    if constexpr (RS_MEM) return P().rem_out[((uint64_t)(2 * R) + f) * P().nrep + q];
     else return sel_get<R>(rs, f);
   }
   RG_FN void rs_set(uint32_t f, uint64_t v) {
-    if constexpr (RS_MEM) p.rem_out[((uint64_t)(2 * R) + f) * p.nrep + q] = v;
+    if constexpr (RS_MEM) P().rem_out[((uint64_t)(2 * R) + f) * P().nrep + q] = v;
     else sel_set<R>(rs, f, v);
   }
 
   // ---- log (entryLog)
   RG_FN uint64_t* tr_at(uint64_t i) const {
-    return p.tr + (uint64_t)(i & (p.L - 1)) * p.nrep + q;
+    return P().tr + (uint64_t)(i & (P().L - 1)) * P().nrep + q;
   }
   RG_FN uint64_t term_at(uint64_t i) const {
     if (i == marker) return marker_term;
@@ -317,10 +335,10 @@ struct Ctl {
     return (uint32_t)(packed >> (8 * d)) & 0xFF;
   }
   RG_FN bool lost(uint32_t dst, uint32_t n) const {
-    if (p.isolate && (p.isolate[ri()] || p.isolate[(uint64_t)gi * R + dst])) return true;
-    if (p.drop_ppm) {
-      uint64_t h = mix64(p.seed ^ mix64((p.tick << 40) ^ ((uint64_t)rid << 8) ^ dst) ^ (uint64_t)(n + 1));
-      if (h % 1000000ull < p.drop_ppm) return true;
+    if (P().isolate && (P().isolate[ri()] || P().isolate[(uint64_t)gi * R + dst])) return true;
+    if (P().drop_ppm) {
+      uint64_t h = mix64(P().seed ^ mix64((P().tick << 40) ^ ((uint64_t)rid << 8) ^ dst) ^ (uint64_t)(n + 1));
+      if (h % 1000000ull < P().drop_ppm) return true;
     }
     return false;
   }
@@ -341,13 +359,13 @@ struct Ctl {
     const uint32_t n = get8(em, dst);
     em += 1ull << (8 * dst);
     const uint32_t k = get8(oc, dst);
-    if (lost(dst, n) || k >= p.K) {
+    if (lost(dst, n) || k >= P().K) {
       drops++;
       return -1;
     }
     oc += 1ull << (8 * dst);
-    const uint64_t plane = (uint64_t)R * R * p.K * p.G;
-    uint64_t* h = p.hdr_out + (((uint64_t)RG_S_SEND * R + dst) * p.K + k) * p.G + g;
+    const uint64_t plane = (uint64_t)R * R * P().K * P().G;
+    uint64_t* h = P().hdr_out + (((uint64_t)RG_S_SEND * R + dst) * P().K + k) * P().G + g;
     h[0 * plane] = (uint64_t)type | ((uint64_t)my_id() << 8) | ((uint64_t)to << 16) | ((uint64_t)reject << 24) |
                    ((uint64_t)nent << 32);
     h[1 * plane] = mterm;
@@ -375,7 +393,7 @@ struct Ctl {
     etick = htick = 0;
     rng_ctr++;
     uint64_t key = (gg << 32) | ((uint64_t)s << 24) | (uint64_t)(rng_ctr & 0xFFFFFF);
-    rand_to = p.ET + (uint32_t)(mix64(p.seed ^ mix64(key)) % p.ET);
+    rand_to = P().ET + (uint32_t)(mix64(P().seed ^ mix64(key)) % P().ET);
     sfor<0, R>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       rm[j] = (uint32_t)j == s ? last : 0;
@@ -385,7 +403,7 @@ struct Ctl {
     });
     active = 0;
     cc_pending = 0;  // clearPendingConfigChange
-    if (p.rdst) p.rdst[(uint64_t)RI_CTX * p.nrep + q] = 0;  // readIndex.reset
+    if (P().rdst) P().rdst[(uint64_t)RI_CTX * P().nrep + q] = 0;  // readIndex.reset
   }
   RG_FN void become_follower(uint64_t t, uint64_t l) {
     role = FOLLOWER;
@@ -460,25 +478,25 @@ struct Ctl {
     const uint32_t ncu = word_nc(word), tot = ncu * n;
     if (n) lt_set(base + n - 1, word & TERM_MASK);
     uint64_t* dst = tr_at(base);
-    uint32_t slot = (uint32_t)(base & (p.L - 1));
-    const uint64_t step = p.nrep, wrap = (uint64_t)p.L * p.nrep, wr = word & ~BANK_BIT;
+    uint32_t slot = (uint32_t)(base & (P().L - 1));
+    const uint64_t step = P().nrep, wrap = (uint64_t)P().L * P().nrep, wr = word & ~BANK_BIT;
     for (uint32_t e = 0; e < n; ++e) {
       *dst = wr;
       dst += step;
-      if (++slot == p.L) {
+      if (++slot == P().L) {
         slot = 0;
         dst -= wrap;
       }
     }
-    const bool uni = ncu <= (p.P >> 4);
-    if (nj < p.J) {
-      const uint64_t n64 = p.nrep, JN = (uint64_t)p.J * n64;
-      uint64_t* j64 = p.job64 + (uint64_t)nj * n64 + q;
+    const bool uni = ncu <= (P().P >> 4);
+    if (nj < P().J) {
+      const uint64_t n64 = P().nrep, JN = (uint64_t)P().J * n64;
+      uint64_t* j64 = P().job64 + (uint64_t)nj * n64 + q;
       j64[J_FIRST * JN] = base;
       j64[J_SPOS * JN] = kind == SRC_RING || kind == SRC_WIRE ? spos : 0ull;
       j64[J_SMASK * JN] = (word & BANK_BIT) ? (n >= 64 ? ~0ull : (1ull << n) - 1) : 0ull;
       j64[J_DMASK * JN] = 0;
-      uint32_t* j32 = p.job32 + (uint64_t)nj * n64 + q;
+      uint32_t* j32 = P().job32 + (uint64_t)nj * n64 + q;
       j32[J_META * JN] = job_meta(n, 0, kind, uni, uni ? ncu : 0u);
       j32[J_SRC * JN] = src;
       j32[J_DPOS * JN] = hw;
@@ -513,8 +531,8 @@ struct Ctl {
       // 64-bit multiply per entry; masks from the words with single-bit selects. (A lane steps one
       // replica; at occupancy 1 this loop is issue-bound)
       uint64_t* dst = tr_at(base + e0);
-      uint32_t slot = (uint32_t)((base + e0) & (p.L - 1));
-      const uint64_t step = p.nrep, wrap = (uint64_t)p.L * p.nrep;
+      uint32_t slot = (uint32_t)((base + e0) & (P().L - 1));
+      const uint64_t step = P().nrep, wrap = (uint64_t)P().L * P().nrep;
       if (!mt && !li) {  // one word for every entry: a leader's batch of synthetic Cmds, or its no-op
         const uint64_t M = (n - e0 >= 64 ? ~0ull : (1ull << (n - e0)) - 1) << e0;
         sm = (word & BANK_BIT) ? M : 0ull;
@@ -526,7 +544,7 @@ struct Ctl {
         for (uint32_t e = e0; e < n; ++e) {
           *dst = wr;
           dst += step;
-          if (++slot == p.L) {
+          if (++slot == P().L) {
             slot = 0;
             dst -= wrap;
           }
@@ -537,7 +555,7 @@ struct Ctl {
           uint64_t wv[CB];
 #pragma unroll
           for (uint32_t k = 0; k < CB; ++k)
-            wv[k] = word | (e + k >= n ? 0ull : mt ? mt[(uint64_t)(e + k) * p.G] : len_bits(li[e + k].y));
+            wv[k] = word | (e + k >= n ? 0ull : mt ? mt[(uint64_t)(e + k) * P().G] : len_bits(li[e + k].y));
 #pragma unroll
           for (uint32_t k = 0; k < CB; ++k) {
             if (e + k >= n) break;
@@ -551,7 +569,7 @@ struct Ctl {
             tm |= (w & TYPE_BIT) ? bit : 0ull;
             *dst = w & ~BANK_BIT;
             dst += step;
-            if (++slot == p.L) {
+            if (++slot == P().L) {
               slot = 0;
               dst -= wrap;
             }
@@ -571,7 +589,7 @@ struct Ctl {
       for (uint32_t k = 0; k < CB; ++k) {
         const uint64_t idx = base + e + k;
         const bool in = e + k < n;
-        wv[k] = word | (!in ? 0ull : mt ? mt[(uint64_t)(e + k) * p.G] : li ? len_bits(li[e + k].y) : 0ull);
+        wv[k] = word | (!in ? 0ull : mt ? mt[(uint64_t)(e + k) * P().G] : li ? len_bits(li[e + k].y) : 0ull);
         ov[k] = in && idx <= hi_prot ? *tr_at(idx) : 0;
       }
 #pragma unroll
@@ -623,15 +641,15 @@ struct Ctl {
     } else {
       uni = true;  // SRC_SLAB (generator Cmds, P bytes) or SRC_NONE (no Cmd bytes)
     }
-    uni = uni && ncu <= (p.P >> 4);  // the pipelined path moves at most one lane group (P bytes) per entry
-    if (nj < p.J) {
-      const uint64_t n64 = p.nrep, JN = (uint64_t)p.J * n64;
-      uint64_t* j64 = p.job64 + (uint64_t)nj * n64 + q;
+    uni = uni && ncu <= (P().P >> 4);  // the pipelined path moves at most one lane group (P bytes) per entry
+    if (nj < P().J) {
+      const uint64_t n64 = P().nrep, JN = (uint64_t)P().J * n64;
+      uint64_t* j64 = P().job64 + (uint64_t)nj * n64 + q;
       j64[J_FIRST * JN] = base;
       j64[J_SPOS * JN] = spos;
       j64[J_SMASK * JN] = sm;
       j64[J_DMASK * JN] = dm;
-      uint32_t* j32 = p.job32 + (uint64_t)nj * n64 + q;
+      uint32_t* j32 = P().job32 + (uint64_t)nj * n64 + q;
       j32[J_META * JN] = job_meta(n, e0, kind, uni, uni ? ncu : 0u);
       j32[J_SRC * JN] = src;
       j32[J_DPOS * JN] = hw;
@@ -659,7 +677,7 @@ struct Ctl {
         return false;
       }
     }
-    if (last + n > cap_base + p.L) return false;
+    if (last + n > cap_base + P().L) return false;
     const uint64_t base = last + 1;
     if (cc) {  // one ConfigChange entry: no Cmd, the descriptor in its length field
       write_entries(base, 0, 1, SRC_NONE, 0, nullptr, term | TYPE_BIT | cc_bits(cc));
@@ -668,15 +686,15 @@ struct Ctl {
       if (__builtin_popcount(members) == 1) try_commit();  // isSingleNodeQuorum
       return true;
     }
-    const bool pay = slab_id >= 0 && p.P;
-    if (pay && !stream_fits(hw, lpg(), (uint32_t)cinfo & 0x7FFFFFFFu, p.PTS)) return false;
+    const bool pay = slab_id >= 0 && P().P;
+    if (pay && !stream_fits(hw, lpg(), (uint32_t)cinfo & 0x7FFFFFFFu, P().PTS)) return false;
 #ifdef RG_CTL_FASTREP
     const bool plain = base > umax64(last_start, sent_hi);  // no protected index: every bank bit 0
     const uint64_t pt = plain ? term_at(last) : 0;
     const uint32_t pos0 = hw;
 #endif
     const bool syn = pay && !rmt && (!li || (li[0].x & SYN_OFF));  // generator Cmds: P bytes each
-    const uint64_t w = syn ? term | len_bits(p.P) : term;
+    const uint64_t w = syn ? term | len_bits(P().P) : term;
     if constexpr (FAST) {
       if (!plain) {
         abort_();
@@ -735,7 +753,7 @@ struct Ctl {
       send(M_INSTALL_SNAPSHOT, to + 1, 0, 0, 0, snap_term, snap_index, 0, 0, snap_members, 0, 0);
       return;
     }
-    const uint32_t n = next <= last ? (uint32_t)umin64(p.E, last - next + 1) : 0;
+    const uint32_t n = next <= last ? (uint32_t)umin64(P().E, last - next + 1) : 0;
 #ifdef RG_CTL_FASTREP  // the whole message lies in this step's plain append (the steady-state case)
     // (at R >= 7 the three extra live registers push the lane past 512 and into scratch: off there)
     const bool fast = R <= 6 && n > 0 && la_n > 0 && next >= la_base && next + n <= la_base + la_n;
@@ -764,7 +782,7 @@ struct Ctl {
 #endif
     const int k = send(M_REPLICATE, to + 1, 0, 0, n, lt, next - 1, committed, upos, 0, uni, 0);
     if (k >= 0 && n > 0) {
-      uint64_t* mt = p.mt_out + ((((uint64_t)RG_S_SEND * R + to) * p.K + (uint32_t)k) * p.E) * p.G + g;
+      uint64_t* mt = P().mt_out + ((((uint64_t)RG_S_SEND * R + to) * P().K + (uint32_t)k) * P().E) * P().G + g;
 #ifdef RG_CTL_FASTREP
       if (FAST || fast) {
         mt[0] = la_word;  // uniform: one word for every entry
@@ -776,7 +794,7 @@ struct Ctl {
         for (uint32_t k2 = 0; k2 < CB; ++k2) v[k2] = e + k2 < n ? *tr_at(next + e + k2) : 0;
 #pragma unroll
         for (uint32_t k2 = 0; k2 < CB; ++k2)
-          if (e + k2 < n) mt[(uint64_t)(e + k2) * p.G] = v[k2];
+          if (e + k2 < n) mt[(uint64_t)(e + k2) * P().G] = v[k2];
       }
       sent_hi = umax64(sent_hi, next + n - 1);
     }
@@ -790,7 +808,7 @@ struct Ctl {
   RG_FN void broadcast_heartbeat() {
     // a pending ReadIndex rides on every heartbeat (dragonboat's broadcastHeartbeatMessage attaches
     // readIndex.peepCtx), so a lost read heartbeat or response is retried by the next round
-    const uint64_t ctx = p.rdst ? p.rdst[(uint64_t)RI_CTX * p.nrep + q] : 0ull;
+    const uint64_t ctx = P().rdst ? P().rdst[(uint64_t)RI_CTX * P().nrep + q] : 0ull;
     if constexpr (FAST) {  // a pending read: its confirmation round is the full step's
       if (ctx) {
         abort_();
@@ -824,7 +842,7 @@ struct Ctl {
     const bool uni = !remote && ((uint32_t)wofs & RG_UNIFORM) && n > 0;
     wofs &= ~(uint64_t)RG_UNIFORM;
     if (term_at(li) == log_term) {
-      const uint64_t* mt = (remote ? p.rmt : p.mt_in) + ((((uint64_t)src * R + RG_S_INBOX) * p.K + k) * p.E) * p.G + g;
+      const uint64_t* mt = (remote ? P().rmt : P().mt_in) + ((((uint64_t)src * R + RG_S_INBOX) * P().K + k) * P().E) * P().G + g;
       const uint64_t uw = uni || runi ? mt0 : 0ull;  // loaded with the header (handle_)
       if constexpr (FAST) {  // an append at the log end from a uniform Replicate (or an empty one)
         if (li != last || (n > 0 && !uni && !runi) || (uw & TYPE_BIT)) {
@@ -833,7 +851,7 @@ struct Ctl {
         }
         const uint64_t last_new = li + n;
         if (n > 0) {  // every index is new: no conflict scan (entryLog.getConflictIndex finds li + 1)
-          if (last_new > cap_base + p.L || (p.P && !stream_fits(hw, lpg(), n * word_nc(uw), p.PTS))) {
+          if (last_new > cap_base + P().L || (P().P && !stream_fits(hw, lpg(), n * word_nc(uw), P().PTS))) {
             drops++;  // capacity rules (ring, then payload stream): dropped, no reply
             return;
           }
@@ -842,7 +860,7 @@ struct Ctl {
             return;
           }
           if (remote) write_fresh_uniform(li + 1, n, SRC_WIRE, n, uw, wofs);
-          else write_fresh_uniform(li + 1, n, SRC_RING, src * p.G + g, uw, (uint32_t)upos);
+          else write_fresh_uniform(li + 1, n, SRC_RING, src * P().G + g, uw, (uint32_t)upos);
           last = last_new;
         }
         commit_to(umin64(last_new, mcommit));
@@ -852,7 +870,7 @@ struct Ctl {
       }
       uint32_t k0 = n;
       for (uint32_t e = 0; e < n; ++e) {  // entryLog.getConflictIndex
-        if (term_at(li + 1 + e) != ((uni ? uw : mt[(uint64_t)e * p.G]) & TERM_MASK)) {
+        if (term_at(li + 1 + e) != ((uni ? uw : mt[(uint64_t)e * P().G]) & TERM_MASK)) {
           k0 = e;
           break;
         }
@@ -861,13 +879,13 @@ struct Ctl {
       if (k0 < n) {
         const uint64_t ci = li + 1 + k0;
         if (ci > committed) {  // capacity rules (ring, then payload stream): dropped, no reply
-          bool fits = last_new <= cap_base + p.L;
-          if (fits && p.P) {
+          bool fits = last_new <= cap_base + P().L;
+          if (fits && P().P) {
             uint32_t c = 0;
             if (uni) c = (n - k0) * word_nc(uw);
             else
-              for (uint32_t e = k0; e < n; ++e) c += word_nc(mt[(uint64_t)e * p.G]);
-            fits = stream_fits(hw, lpg(), c, p.PTS);
+              for (uint32_t e = k0; e < n; ++e) c += word_nc(mt[(uint64_t)e * P().G]);
+            fits = stream_fits(hw, lpg(), c, P().PTS);
           }
           if (!fits) {
             drops++;
@@ -878,8 +896,8 @@ struct Ctl {
           err |= ERR_CONFLICT;
         } else {
           if (remote) write_entries(li + 1, k0, n, SRC_WIRE, n, mt, 0, wofs);
-          else if (uni) write_entries(li + 1, k0, n, SRC_RING, src * p.G + g, nullptr, uw, 0, nullptr, (uint32_t)upos);
-          else write_entries(li + 1, k0, n, SRC_RING, src * p.G + g, mt, 0);
+          else if (uni) write_entries(li + 1, k0, n, SRC_RING, src * P().G + g, nullptr, uw, 0, nullptr, (uint32_t)upos);
+          else write_entries(li + 1, k0, n, SRC_RING, src * P().G + g, mt, 0);
           last = last_new;
         }
       }
@@ -1029,9 +1047,9 @@ struct Ctl {
     active |= 1u << f;
     if (RG_GET(rt, f) == WAIT) RG_SET(rt, f, (uint32_t)RETRY);
     if (RG_GET(rm, f) < last) send_replicate(f);
-    if (hint != 0 && p.rdst) {  // readIndex.confirm: only read heartbeats carry a context
-      uint64_t* rd = p.rdst + q;
-      const uint64_t n = p.nrep;
+    if (hint != 0 && P().rdst) {  // readIndex.confirm: only read heartbeats carry a context
+      uint64_t* rd = P().rdst + q;
+      const uint64_t n = P().nrep;
       if (rd[RI_CTX * n] == hint) {
         const uint64_t a = rd[RI_ACKS * n] | (1ull << f);
         if ((uint32_t)__builtin_popcount((uint32_t)a & members) >= quorum()) {
@@ -1043,12 +1061,12 @@ struct Ctl {
       }
     }
   }
-  // ---- ReadIndex (Raft thesis §6.4; dragonboat's readIndex), state in p.rdst, not in registers
+  // ---- ReadIndex (Raft thesis §6.4; dragonboat's readIndex), state in P().rdst, not in registers
   RG_FN void read_ready(uint64_t ctx, uint64_t index) {  // addReadyToRead
-    uint64_t* rd = p.rdst + q;
-    rd[RD_CTX * (uint64_t)p.nrep] = ctx;
-    rd[RD_INDEX * (uint64_t)p.nrep] = index;
-    rd[RD_TICK * (uint64_t)p.nrep] = p.tick + 1;
+    uint64_t* rd = P().rdst + q;
+    rd[RD_CTX * (uint64_t)P().nrep] = ctx;
+    rd[RD_INDEX * (uint64_t)P().nrep] = index;
+    rd[RD_TICK * (uint64_t)P().nrep] = P().tick + 1;
   }
   RG_FN void read_confirmed(uint64_t ctx, uint64_t index, uint32_t slot) {
     if (slot == s) read_ready(ctx, index);
@@ -1056,10 +1074,10 @@ struct Ctl {
   }
   RG_FN void handle_read_index(uint32_t from, uint64_t ctx) {
     const uint32_t f = from - 1;
-    if (!p.rdst) return;
+    if (!P().rdst) return;
     if (role == LEADER) {
-      uint64_t* rd = p.rdst + q;
-      const uint64_t n = p.nrep;
+      uint64_t* rd = P().rdst + q;
+      const uint64_t n = P().nrep;
       if (quorum() == 1) {  // isSingleNodeQuorum
         read_confirmed(ctx, committed, f);
       } else if (term_at(committed) != term || rd[RI_CTX * n] != 0) {
@@ -1128,13 +1146,13 @@ struct Ctl {
   RG_FN void tick() {
     if (role == LEADER) {
       etick++;
-      if (etick >= p.ET) {
+      if (etick >= P().ET) {
         etick = 0;
-        if (p.CQ) check_quorum();
+        if (P().CQ) check_quorum();
         if (FAST && aborted) return;
       }
       htick++;
-      if (htick >= p.HT) {
+      if (htick >= P().HT) {
         htick = 0;
         if (role == LEADER) broadcast_heartbeat();
       }
@@ -1185,16 +1203,16 @@ struct Ctl {
     uint64_t mt0;  // a Replicate's first inline word (a uniform Replicate needs only it)
   };
   RG_FN const uint64_t* hdr_ptr(uint32_t src, uint32_t k, bool remote) const {
-    return (remote ? p.rhdr : p.hdr_in) + (((uint64_t)src * R + RG_S_INBOX) * p.K + k) * p.G + g;
+    return (remote ? P().rhdr : P().hdr_in) + (((uint64_t)src * R + RG_S_INBOX) * P().K + k) * P().G + g;
   }
   // one round trip: the header words and the message's first inline word (for other
   // messages the slot holds stale words, which nothing reads)
   RG_FN void load_hdr(uint32_t src, uint32_t k, bool remote, Hdr& o) const {
-    const uint64_t plane = (uint64_t)R * R * p.K * p.G;
+    const uint64_t plane = (uint64_t)R * R * P().K * P().G;
     const uint64_t* h = hdr_ptr(src, k, remote);
 #pragma unroll
     for (int x = 0; x < NB; ++x) o.w[x] = h[(uint64_t)x * plane];
-    o.mt0 = (remote ? p.rmt : p.mt_in)[((((uint64_t)src * R + RG_S_INBOX) * p.K + k) * p.E) * p.G + g];
+    o.mt0 = (remote ? P().rmt : P().mt_in)[((((uint64_t)src * R + RG_S_INBOX) * P().K + k) * P().E) * P().G + g];
   }
   RG_FN void handle(uint32_t src, uint32_t k, bool remote, const Hdr& hd) {
     RG_T0(t0);
@@ -1202,7 +1220,7 @@ struct Ctl {
     RG_ACC(5, t0);
   }
   RG_FN void handle_(uint32_t src, uint32_t k, bool remote, const Hdr& hd) {
-    const uint64_t plane = (uint64_t)R * R * p.K * p.G;
+    const uint64_t plane = (uint64_t)R * R * P().K * P().G;
     const uint64_t* h = hdr_ptr(src, k, remote);
     const uint64_t mt0 = hd.mt0;
     auto hw = [&](int x) -> uint64_t { return x < NB ? hd.w[x < NB ? x : 0] : h[(uint64_t)x * plane]; };
@@ -1220,7 +1238,7 @@ struct Ctl {
       }
 #endif
       if (from - 1 >= (uint32_t)R || (mterm != 0 && mterm != term) ||
-          (type == M_REPLICATE && (uint32_t)(w0 >> 32) > p.E)) {
+          (type == M_REPLICATE && (uint32_t)(w0 >> 32) > P().E)) {
         abort_();
         return;
       }
@@ -1261,21 +1279,21 @@ struct Ctl {
     }
     // unreachable (senders write at most E entries, unpack_kernel keeps only well-formed messages):
     // checked anyway, so that a damaged inbox shows up as ERR_WIRE instead of a wild address
-    if (type == M_REPLICATE && (uint32_t)(w0 >> 32) > p.E) {
+    if (type == M_REPLICATE && (uint32_t)(w0 >> 32) > P().E) {
       RG_OOB("RG_BOUNDS control q=%u src=%u k=%u remote=%d replicate n=%u > E=%u\n", q, src, k, (int)remote,
-             (uint32_t)(w0 >> 32), p.E);
+             (uint32_t)(w0 >> 32), P().E);
       err |= ERR_WIRE;
       return;
     }
     const bool leader_msg =
         type == M_REPLICATE || type == M_INSTALL_SNAPSHOT || type == M_HEARTBEAT || type == M_READ_INDEX_RESP;
     if (mterm != 0 && mterm != term) {
-      if (type == M_REQUEST_VOTE && p.CQ && mterm > term && hw(5) != from && leader != 0 && etick < p.ET)
+      if (type == M_REQUEST_VOTE && P().CQ && mterm > term && hw(5) != from && leader != 0 && etick < P().ET)
         return;
       if (mterm > term) {
         become_follower(mterm, leader_msg ? from : 0);
       } else {
-        if (p.CQ && leader_msg) send_simple(M_NOOP, from);
+        if (P().CQ && leader_msg) send_simple(M_NOOP, from);
         return;
       }
     }
@@ -1284,19 +1302,19 @@ struct Ctl {
         // remote: unpack put their length words in rmt and their records' offset in word 7
         const uint64_t w7 = hw(7);
         const uint32_t nent = (uint32_t)(w0 >> 32);
-        if (nent - 1 >= p.E || (!remote && (uint32_t)w7 >= p.nslab)) {  // unreachable: senders forward
+        if (nent - 1 >= P().E || (!remote && (uint32_t)w7 >= P().nslab)) {  // unreachable: senders forward
           err |= ERR_WIRE;                                               // 1..E entries of a slab
           break;
         }
         // word 4: the batch's stream chunks | contiguous << 31 | arena chunk << 32 (a remote
         // batch: the chunks unpack_kernel counted)
         if (remote) {
-          const uint64_t* rm = p.rmt + ((((uint64_t)src * R + RG_S_INBOX) * p.K + k) * p.E) * p.G + g;
+          const uint64_t* rm = P().rmt + ((((uint64_t)src * R + RG_S_INBOX) * P().K + k) * P().E) * P().G + g;
           handle_propose(nent, 0, 1, hw(5), 0, nullptr, rm, w7, (uint32_t)hw(6), hw(4));
         } else {
-          const uint64_t row = p.wire ? (uint64_t)src * p.G + g : g;  // the forwarder's slab row (same rank)
-          const uint64_t rows = p.wire ? p.nrep : p.G;
-          const uint2* li = p.slab_info + ((uint64_t)(uint32_t)w7 * rows + row) * p.E;
+          const uint64_t row = P().wire ? (uint64_t)src * P().G + g : g;  // the forwarder's slab row (same rank)
+          const uint64_t rows = P().wire ? P().nrep : P().G;
+          const uint2* li = P().slab_info + ((uint64_t)(uint32_t)w7 * rows + row) * P().E;
           handle_propose(nent, (uint32_t)w7, (uint32_t)(w7 >> 32), hw(5), src, li, nullptr, 0, (uint32_t)hw(6), hw(4));
         }
         break;
@@ -1330,7 +1348,7 @@ struct Ctl {
         handle_read_index(from, hw(5));
         break;
       case M_READ_INDEX_RESP:
-        if (role == FOLLOWER && p.rdst) {
+        if (role == FOLLOWER && P().rdst) {
           etick = 0;
           leader = from;
           read_ready(hw(5), hw(3));
@@ -1369,17 +1387,17 @@ struct Ctl {
     sfor<0, R>([&](auto jc) {
       constexpr int src = decltype(jc)::value;
       cnt_pf[src] = (uint32_t)src == s ? 0u
-                    : (pl_remote(p.pl, src, RG_S_INBOX, g) ? p.rcnt : p.cnt_in)[((uint64_t)src * R + RG_S_INBOX) * p.G + g];
+                    : (pl_remote(P().pl, src, RG_S_INBOX, g) ? P().rcnt : P().cnt_in)[((uint64_t)src * R + RG_S_INBOX) * P().G + g];
     });
-    const uint32_t in_pt = p.prop_target ? p.prop_target[gi] : 0xFFu;
-    const uint32_t in_pc = p.prop_target ? p.prop_count[gi] : 0u;
-    const bool in_camp = p.campaign && p.campaign[ri()];
-    const uint32_t in_cc = p.cc_in ? p.cc_in[gi] : 0u;
-    const uint64_t in_rd = p.read_ctx ? p.read_ctx[ri()] : 0ull;
+    const uint32_t in_pt = P().prop_target ? P().prop_target[gi] : 0xFFu;
+    const uint32_t in_pc = P().prop_target ? P().prop_count[gi] : 0u;
+    const bool in_camp = P().campaign && P().campaign[ri()];
+    const uint32_t in_cc = P().cc_in ? P().cc_in[gi] : 0u;
+    const uint64_t in_rd = P().read_ctx ? P().read_ctx[ri()] : 0ull;
     sfor<0, R>([&](auto jc) {
       constexpr int src = decltype(jc)::value;
-      if (cnt_pf[src] > p.K) {  // never produced by a sender (unpack_kernel clamps received counts): ERR_WIRE
-        RG_OOB("RG_BOUNDS control q=%u src=%u cnt=%u > K=%u\n", q, (uint32_t)src, cnt_pf[src], p.K);
+      if (cnt_pf[src] > P().K) {  // never produced by a sender (unpack_kernel clamps received counts): ERR_WIRE
+        RG_OOB("RG_BOUNDS control q=%u src=%u cnt=%u > K=%u\n", q, (uint32_t)src, cnt_pf[src], P().K);
         if constexpr (FAST) abort_();
         err |= ERR_WIRE;
         cnt_pf[src] = 0;
@@ -1402,14 +1420,14 @@ struct Ctl {
     uint32_t cs = 0, ck = 0;
     bool have = !(FAST && aborted) && next_msg(0, ~0u, cs, ck);
     Hdr cur{};
-    if (have) load_hdr(cs, ck, pl_remote(p.pl, cs, RG_S_INBOX, g), cur);
+    if (have) load_hdr(cs, ck, pl_remote(P().pl, cs, RG_S_INBOX, g), cur);
     while (have) {
       uint32_t ns = 0, nk = 0;
       const bool more = next_msg(cs, ck, ns, nk);
       Hdr nxt{};
-      if (PIPE && more) load_hdr(ns, nk, pl_remote(p.pl, ns, RG_S_INBOX, g), nxt);
-      handle(cs, ck, pl_remote(p.pl, cs, RG_S_INBOX, g), cur);
-      if (!PIPE && more && !(FAST && aborted)) load_hdr(ns, nk, pl_remote(p.pl, ns, RG_S_INBOX, g), nxt);
+      if (PIPE && more) load_hdr(ns, nk, pl_remote(P().pl, ns, RG_S_INBOX, g), nxt);
+      handle(cs, ck, pl_remote(P().pl, cs, RG_S_INBOX, g), cur);
+      if (!PIPE && more && !(FAST && aborted)) load_hdr(ns, nk, pl_remote(P().pl, ns, RG_S_INBOX, g), nxt);
       cur = nxt;
       cs = ns;
       ck = nk;
@@ -1421,22 +1439,22 @@ struct Ctl {
       if (aborted) return;
     }
     if (in_camp) handle_node_election();
-    if (!(p.flags & 1u)) tick();
+    if (!(P().flags & 1u)) tick();
     if (FAST && aborted) return;
     RG_STAMP(2);
     if (in_pt == s) {
       const uint32_t n = in_pc;
-      if (n > p.E) {  // rg_tick_device's contract: batches of at most E entries (the host path checks)
+      if (n > P().E) {  // rg_tick_device's contract: batches of at most E entries (the host path checks)
         drops++;
       } else if (n > 0) {
         // caller batch (rg_propose): lengths in slab_info; tick-input batch: synthetic Cmds of P bytes
-        const uint32_t sl = (uint32_t)(p.tick % p.nslab);
-        const uint64_t row = p.wire ? q : g, rows = p.wire ? p.nrep : p.G;
-        const uint64_t hm = !p.P ? 0ull : p.prop_hmask ? p.prop_hmask[gi] : (n >= 64 ? ~0ull : (1ull << n) - 1);
-        const uint2* li = p.prop_hmask && p.P ? p.slab_info + ((uint64_t)sl * rows + row) * p.E : nullptr;
-        uint64_t cinfo = (uint64_t)(n * (p.P >> 4)) | (1ull << 31);  // generator Cmds: P bytes each
-        if (p.prop_cmd) {  // a caller batch: rg_propose's chunk count, contiguity and first arena chunk
-          const uint2 pc = p.prop_cmd[gi];
+        const uint32_t sl = (uint32_t)(P().tick % P().nslab);
+        const uint64_t row = P().wire ? q : g, rows = P().wire ? P().nrep : P().G;
+        const uint64_t hm = !P().P ? 0ull : P().prop_hmask ? P().prop_hmask[gi] : (n >= 64 ? ~0ull : (1ull << n) - 1);
+        const uint2* li = P().prop_hmask && P().P ? P().slab_info + ((uint64_t)sl * rows + row) * P().E : nullptr;
+        uint64_t cinfo = (uint64_t)(n * (P().P >> 4)) | (1ull << 31);  // generator Cmds: P bytes each
+        if (P().prop_cmd) {  // a caller batch: rg_propose's chunk count, contiguity and first arena chunk
+          const uint2 pc = P().prop_cmd[gi];
           cinfo = pc.x | ((uint64_t)pc.y << 32);
         }
         handle_propose(n, sl, 0, hm, s, li, nullptr, 0, 0, cinfo);
@@ -1445,7 +1463,7 @@ struct Ctl {
     }
     {  // 4a: membership change input (rg_config_change)
       const uint32_t v = in_cc;
-      if (v && (v & 0xFFu) == s) handle_propose(1, (uint32_t)(p.tick % p.nslab), 0, 0, s, nullptr, nullptr, 0, v >> 8, 0);
+      if (v && (v & 0xFFu) == s) handle_propose(1, (uint32_t)(P().tick % P().nslab), 0, 0, s, nullptr, nullptr, 0, v >> 8, 0);
     }
     if (in_rd) handle_read_index(my_id(), in_rd);  // 4b: ReadIndex input (rg_read_index)
     RG_STAMP(3);
@@ -1455,8 +1473,8 @@ struct Ctl {
 #if defined(__HIP_DEVICE_COMPILE__) || defined(__GNUC__)
       asm volatile("" ::: "memory");
 #endif
-      const uint64_t n = p.nrep;
-      const uint64_t* a = p.s64_in + q;
+      const uint64_t n = P().nrep;
+      const uint64_t* a = P().s64_in + q;
       processed = processed_start = a[S_PROCESSED * n];
       cc_hi = a[S_CC_HI * n];
       applied = a[S_APPLIED * n];
@@ -1477,13 +1495,13 @@ struct Ctl {
       }
     }
     processed = committed;
-    if (!p.AF) applied = processed;
-    if (p.SE && applied >= snap_index && applied - snap_index >= p.SE) {
+    if (!P().AF) applied = processed;
+    if (P().SE && applied >= snap_index && applied - snap_index >= P().SE) {
       snap_index = applied;
       snap_term = term_at(applied);
       snap_members = members;
       took = true;
-      const uint64_t c = snap_index > p.CO ? snap_index - p.CO : 0;
+      const uint64_t c = snap_index > P().CO ? snap_index - P().CO : 0;
       if (c > marker) {
         marker_term = term_at(c);
         marker = c;
@@ -1496,16 +1514,16 @@ struct Ctl {
     store();
     RG_STAMP(5);
 #if defined(RG_CTL_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
-    if (p.prof)
-      for (int k = 0; k < 12; ++k) p.prof[(uint64_t)k * p.nrep + q] = stamps[k];
+    if (P().prof)
+      for (int k = 0; k < 12; ++k) P().prof[(uint64_t)k * P().nrep + q] = stamps[k];
 #endif
   }
 
   RG_FN void store() {
     if constexpr (LEAN) {  // the fields no fast branch changes: copied through from the step's input state
-      const uint64_t n = p.nrep;
-      const uint64_t* ai = p.s64_in + q;
-      const uint32_t* bi = p.s32_in + q;
+      const uint64_t n = P().nrep;
+      const uint64_t* ai = P().s64_in + q;
+      const uint32_t* bi = P().s32_in + q;
       vote = ai[S_VOTE * n];
       if (!took) {
         snap_term = ai[S_SNAP_TERM * n];
@@ -1515,11 +1533,11 @@ struct Ctl {
       err = bi[S_ERR * n]; cc_pending = bi[S_CC_PENDING * n];
       sfor<0, R>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
-        p.rem_out[(2 * R + j) * n + q] = p.rem_in[(2 * R + j) * n + q];
+        P().rem_out[(2 * R + j) * n + q] = P().rem_in[(2 * R + j) * n + q];
       });
     }
-    const uint64_t n = p.nrep;
-    uint64_t* a = p.s64_out + q;
+    const uint64_t n = P().nrep;
+    uint64_t* a = P().s64_out + q;
     a[S_TERM * n] = term; a[S_VOTE * n] = vote; a[S_LEADER * n] = leader; a[S_COMMITTED * n] = committed;
     a[S_APPLIED * n] = applied; a[S_LAST * n] = last; a[S_MARKER * n] = marker; a[S_MARKER_TERM * n] = marker_term;
     a[S_SNAP_INDEX * n] = snap_index; a[S_SNAP_TERM * n] = snap_term; a[S_CAP_BASE * n] = cap_base;
@@ -1527,7 +1545,7 @@ struct Ctl {
     // compaction or a restore moved the marker: the stream below entry marker + 1 is released by the
     // next step, once this step's bulk kernel has stored that entry's position
     a[S_FIDX * n] = marker != marker_start ? marker + 1 : 0;
-    uint32_t* b = p.s32_out + q;
+    uint32_t* b = P().s32_out + q;
     b[S_ROLE * n] = role; b[S_ETICK * n] = etick; b[S_HTICK * n] = htick; b[S_RAND_TO * n] = rand_to;
     b[S_RNG_CTR * n] = rng_ctr; b[S_GRANTED * n] = granted; b[S_RESPONDED * n] = responded;
     b[S_ACTIVE * n] = active; b[S_ERR * n] = err; b[S_DROPS * n] = drops;
@@ -1536,16 +1554,16 @@ struct Ctl {
     b[S_NLPG * n] = nlpg_;
     sfor<0, R>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
-      p.rem_out[(0 * R + j) * n + q] = rm[j];
-      p.rem_out[(1 * R + j) * n + q] = rn[j];
-      if constexpr (!RS_MEM && !LEAN) p.rem_out[(2 * R + j) * n + q] = rs[j];
-      p.rst_out[j * n + q] = (uint8_t)rt[j];
-      p.cnt_out[((uint64_t)RG_S_SEND * R + j) * p.G + g] = get8(oc, j);
+      P().rem_out[(0 * R + j) * n + q] = rm[j];
+      P().rem_out[(1 * R + j) * n + q] = rn[j];
+      if constexpr (!RS_MEM && !LEAN) P().rem_out[(2 * R + j) * n + q] = rs[j];
+      P().rst_out[j * n + q] = (uint8_t)rt[j];
+      P().cnt_out[((uint64_t)RG_S_SEND * R + j) * P().G + g] = get8(oc, j);
     });
-    p.jcnt[q] = nj;
-    if (p.apply_lo) p.apply_lo[q] = umax64(processed_start, restored_at) + 1;
-    if (p.persist_lo) p.persist_lo[q] = wlo;
-    if (p.snap_ev) p.snap_ev[q] = restored_at | (took ? SNAP_TAKEN_BIT : 0ull);
+    P().jcnt[q] = nj;
+    if (P().apply_lo) P().apply_lo[q] = umax64(processed_start, restored_at) + 1;
+    if (P().persist_lo) P().persist_lo[q] = wlo;
+    if (P().snap_ev) P().snap_ev[q] = restored_at | (took ? SNAP_TAKEN_BIT : 0ull);
   }
 #undef RG_GET
 #undef RG_SET
