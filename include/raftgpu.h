@@ -426,6 +426,11 @@ int rg_last_tick_traffic(rg_engine* e, rg_traffic* out);
 int rg_wire_plan(rg_engine* e, uint64_t* send_bytes /*[ranks]*/);
 int rg_wire_plan_fixed(rg_engine* e, uint64_t* send_bytes /*[ranks]*/, uint64_t* recv_bytes /*[ranks]*/);
 int rg_wire_pack(rg_engine* e, void* send_buf, uint64_t send_cap);
+/* rg_wire_pack with the caller's layout: region r at base + region_off[r] (16-B aligned, inside
+ * base_cap, regions not overlapping). The region to this rank itself can be packed straight into
+ * the place where rg_wire_recv will read it (its receive buffer at that region's offset), so the
+ * transport moves nothing for it — what rg_wire_exchange does. */
+int rg_wire_pack_at(rg_engine* e, void* base, const uint64_t* region_off /*[ranks]*/, uint64_t base_cap);
 int rg_wire_recv(rg_engine* e, const void* recv_buf, const uint64_t* recv_bytes /*[ranks]*/);
 /* Messages dropped so far because their unit did not fit a fixed-capacity region. */
 int rg_wire_dropped(rg_engine* e, uint64_t* msgs);

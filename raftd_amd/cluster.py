@@ -149,16 +149,17 @@ def all_to_all_bytes(send, send_sizes, recv, recv_sizes, group=None, async_op=Fa
     return None
 
 
-def p2p_regions(send, send_sizes, recv, recv_sizes, group=None, async_op=False, chunk=A2A_CHUNK):
+def p2p_regions(send, send_sizes, recv, recv_sizes, group=None, async_op=False, chunk=A2A_CHUNK, send_offs=None):
     """The exchange's transfer on nccl, fixed or exactly sized: region r of `send` to rank r and region
     r of `recv` from rank r as one batch of point-to-point sends and receives (one grouped RCCL call),
     each piece at most `chunk` bytes (the 1 GiB contract). A link's two ends agree on its size, so
     they cut it into the same pieces without any rank knowing the others' sizes (an all_to_all's
     chunk count has to be the same on every rank). The region to this rank itself is a device copy.
-    nccl only; gloo ranks go through all_to_all_bytes."""
+    send_offs: the send regions' offsets in `send` when not consecutive (a region of 0 bytes to this
+    rank: it was packed in place, nothing to copy). nccl only; gloo ranks go through all_to_all_bytes."""
     import torch.distributed as dist
     me, n = dist.get_rank(group), dist.get_world_size(group)
-    so, _ = _offsets(send_sizes)
+    so = list(send_offs) if send_offs is not None else _offsets(send_sizes)[0]
     ro, _ = _offsets(recv_sizes)
     if send_sizes[me]:
         recv[ro[me]:ro[me] + recv_sizes[me]].copy_(send[so[me]:so[me] + send_sizes[me]])
@@ -221,11 +222,19 @@ def gloo_transport(pg, device):
 
     def alltoallv(send, soff, ssize, recv, roff, rsize, stream):
         torch.cuda.synchronize(device)
-        st, rt = sum(ssize), sum(rsize)
-        sb, rb = _dev_bytes(send, st, device), _dev_bytes(recv, rt, device)
-        big = torch.tensor([max(list(ssize) + list(rsize))], dtype=torch.int64)
+        ss, rs = [int(ssize[r]) for r in range(n)], [int(rsize[r]) for r in range(n)]
+        # the regions sit at the offsets given (rg_wire_exchange packs the region to self in place and
+        # the others after the receive regions), staged here in rank order
+        sb = torch.cat([_dev_bytes(send + int(soff[r]), ss[r], device) for r in range(n)])
+        rb = torch.empty(sum(rs), dtype=torch.uint8, device=device)
+        big = torch.tensor([max(ss + rs)], dtype=torch.int64)
         dist.all_reduce(big, op=dist.ReduceOp.MAX, group=pg)  # every rank issues the same chunk count
-        all_to_all_bytes(sb, list(ssize), rb, list(rsize), pg, nchunks=a2a_chunks(int(big.item())))
+        all_to_all_bytes(sb, ss, rb, rs, pg, nchunks=a2a_chunks(int(big.item())))
+        o = 0
+        for r in range(n):
+            if rs[r]:
+                _dev_bytes(recv + int(roff[r]), rs[r], device).copy_(rb[o:o + rs[r]])
+            o += rs[r]
         torch.cuda.synchronize(device)
 
     pt = PyTransport(allgather, alltoallv)
@@ -241,7 +250,7 @@ class _Half:
 
     def __init__(self, eng, dev, pg, rank, xt=None, fixed=True):
         self.eng, self.pg, self.rank, self.xt, self.fixed = eng, pg, rank, xt, fixed
-        self.send, self.recv = _Buf(dev), _Buf(dev)
+        self.send, self.recv = _Buf(dev), _Buf(dev)  # nccl: self.recv holds both (send regions after the receive ones)
         self.work, self.rsizes, self.sent = None, None, 0
 
     def start(self, async_op):
@@ -257,11 +266,30 @@ class _Half:
         else:
             sizes = e.wire_plan()  # host sync: the tick that produced the messages has completed
         _, stot = _offsets(sizes)
-        self.send.ensure(stot)
-        e.wire_pack(self.send.ptr(), self.send.cap())
         if not self.fixed:
             rsizes, biggest = exchange_sizes(sizes, self.pg)
-        _, rtot = _offsets(rsizes)
+        ro, rtot = _offsets(rsizes)
+        me = self.rank
+        if dist.get_backend(self.pg) == "nccl" and sizes[me] == rsizes[me]:
+            # one buffer: the receive regions, then the send regions to the other ranks; the region to
+            # this rank is packed where wire_recv reads it (no self copy; rg_wire_pack_at). Stream order:
+            # the tick that read the old contents runs before the pack and the transfers
+            sbase = (rtot + 255) & ~255
+            so, o = [], sbase
+            for r, n in enumerate(sizes):
+                so.append(ro[r] if r == me else o)
+                o += 0 if r == me else n
+            self.recv.ensure(max(o, 256))
+            e.wire_pack_at(self.recv.ptr(), so, self.recv.cap())
+            ssz = list(sizes)
+            ssz[me] = 0
+            rsz = list(rsizes)
+            rsz[me] = 0
+            self.work = p2p_regions(self.recv.t, ssz, self.recv.t, rsz, self.pg, async_op=async_op, send_offs=so)
+            self.rsizes, self.sent = rsizes, stot - sizes[me]
+            return
+        self.send.ensure(stot)
+        e.wire_pack(self.send.ptr(), self.send.cap())
         self.recv.ensure(rtot)  # stream order: the tick that reads the old buffer runs before a reuse
         if dist.get_backend(self.pg) == "nccl":  # the region to this rank: a device copy, not RCCL
             self.work = p2p_regions(self.send.t, sizes, self.recv.t, rsizes, self.pg, async_op=async_op)

@@ -39,8 +39,9 @@ static int fail(int code, const std::string& msg) {
 // rounds are build-time variants for scripts/build_variant.sh (-DRG_AB_*); only four test hooks are
 // read, once, at rg_create / rg_rccl_open: RAFTGPU_WIRE_CAP0 (start the fixed-capacity regions small),
 // RAFTGPU_CTL_FB (force the control fallback in or out of the fast kernel's launch), RAFTGPU_APPLY_SDMA
-// (the copy-back's D2H leg on an SDMA engine) and RAFTGPU_RCCL_SELF (the RCCL transport's self region
-// through RCCL) — each selects between two product paths the tests run bit-exact.
+// (the copy-back's D2H leg on an SDMA engine) and RAFTGPU_RCCL_SELF (rg_wire_exchange hands the region
+// to self to the transport, which moves it through RCCL, instead of packing it in place) — each
+// selects between two product paths the tests run bit-exact.
 // RG_SYNC_DEBUG builds synchronise after every launch so a fault names its kernel (debug only).
 #ifdef RG_SYNC_DEBUG
 static constexpr bool g_sync_debug = true;
@@ -235,8 +236,9 @@ struct rg_engine {
   uint64_t recv_bytes = 0;         // bytes of it in use (RG_BOUNDS checks)
   // rg_wire_exchange's own buffers (grown on demand; stream order keeps one of each enough: the
   // next exchange is enqueued after the tick that reads the receive buffer)
-  uint8_t *x_send = nullptr, *x_recv = nullptr;
-  uint64_t x_send_cap = 0, x_recv_cap = 0;
+  uint8_t* x_recv = nullptr;  // rg_wire_exchange's buffer: receive regions, then send regions
+  uint64_t x_recv_cap = 0;
+  bool self_via_transport = false;  // RAFTGPU_RCCL_SELF=rccl (tests): no in-place region to self
   // committed-entry copy-back (raftgpu_apply.hip)
   uint64_t* apply_lo = nullptr;
   uint32_t* small_rest = nullptr;  // BulkParams::rest
@@ -747,6 +749,8 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
 #ifdef RG_AB_NO_BULK_SMALL  // A/B variant: one-job replicas through bulk_kernel too
   e->bulk_small = false;
 #endif
+  if (const char* v = getenv("RAFTGPU_RCCL_SELF"))  // test hook: rg_wire_exchange's region to self moves too
+    e->self_via_transport = !strcmp(v, "rccl");
   if (const char* v = getenv("RAFTGPU_APPLY_SDMA"))  // test hook: the SDMA D2H leg
     if (v[0] == '1') {
       std::string why;
@@ -2561,23 +2565,50 @@ int rg_wire_dropped(rg_engine* e, uint64_t* msgs) {
   return RG_OK;
 }
 
-int rg_wire_pack(rg_engine* e, void* send_buf, uint64_t send_cap) {
-  if (!e) return fail(RG_EINVAL, "null engine");
-  if (!e->wire) return RG_OK;
-  if (!e->planned) return fail(RG_EINVAL, "rg_wire_pack before rg_wire_plan");
+// pack region r at base + off[r] (send_bytes[r] bytes; the regions inside cap, not overlapping)
+static int wire_pack_at(rg_engine* e, void* base, const uint64_t* off, uint64_t cap, const char* who) {
+  if (!e->planned) return fail(RG_EINVAL, std::string(who) + " before rg_wire_plan");
   WireParams w = wire_params(e);
-  uint64_t off = 0;
-  for (uint32_t r = 0; r < e->pl.N; ++r) {
-    w.send_region[r] = off;
-    w.send_cap[r] = e->fixed ? e->send_bytes[r] : 0;
-    off += e->send_bytes[r];
+  const uint32_t N = e->pl.N;
+  uint64_t tot = 0;
+  for (uint32_t r = 0; r < N; ++r) {
+    const uint64_t n = e->send_bytes[r];
+    if (!n) continue;
+    if ((off[r] & 15) || off[r] > cap || n > cap - off[r])
+      return fail(RG_EFULL, std::string(who) + ": region of rank " + std::to_string(r) + " outside the buffer");
+    for (uint32_t o = 0; o < r; ++o)
+      if (e->send_bytes[o] && off[o] < off[r] + n && off[r] < off[o] + e->send_bytes[o])
+        return fail(RG_EINVAL, std::string(who) + ": regions of ranks " + std::to_string(o) + " and " +
+                                   std::to_string(r) + " overlap");
+    tot += n;
   }
-  if (off > send_cap) return fail(RG_EFULL, "rg_wire_pack: send buffer smaller than the planned regions");
-  if (off && !send_buf) return fail(RG_EINVAL, "rg_wire_pack: null buffer");
-  w.send = (uint8_t*)send_buf;
+  if (tot && !base) return fail(RG_EINVAL, std::string(who) + ": null buffer");
+  for (uint32_t r = 0; r < N; ++r) {
+    w.send_region[r] = off[r];
+    w.send_cap[r] = e->fixed ? e->send_bytes[r] : 0;
+  }
+  w.send = (uint8_t*)base;
   LAUNCH(launch_wire_pack(w, e->stream), e->stream, "pack_kernel");
   e->planned = false;
   return RG_OK;
+}
+
+int rg_wire_pack(rg_engine* e, void* send_buf, uint64_t send_cap) {
+  if (!e) return fail(RG_EINVAL, "null engine");
+  if (!e->wire) return RG_OK;
+  uint64_t off[MAX_RANKS], o = 0;
+  for (uint32_t r = 0; r < e->pl.N; ++r) {
+    off[r] = o;
+    o += e->send_bytes[r];
+  }
+  if (o > send_cap) return fail(RG_EFULL, "rg_wire_pack: send buffer smaller than the planned regions");
+  return wire_pack_at(e, send_buf, off, send_cap, "rg_wire_pack");
+}
+
+int rg_wire_pack_at(rg_engine* e, void* base, const uint64_t* region_off, uint64_t base_cap) {
+  if (!e || !region_off) return fail(RG_EINVAL, "rg_wire_pack_at args");
+  if (!e->wire) return RG_OK;
+  return wire_pack_at(e, base, region_off, base_cap, "rg_wire_pack_at");
 }
 
 int rg_wire_recv(rg_engine* e, const void* recv_buf, const uint64_t* recv_bytes) {
@@ -2689,18 +2720,32 @@ int rg_wire_exchange(rg_engine* e, const rg_transport* t, uint64_t* sent_bytes) 
   }
   uint64_t st = 0, rt = 0;
   for (uint32_t r = 0; r < N; ++r) {
-    soff[r] = st;
-    st += ssize[r];
     roff[r] = rt;
     rt += rsize[r];
   }
-  RGCHK(xgrow(e, &e->x_send, &e->x_send_cap, std::max<uint64_t>(st, 256)));
-  RGCHK(xgrow(e, &e->x_recv, &e->x_recv_cap, std::max<uint64_t>(rt, 256)));
-  RGCHK(rg_wire_pack(e, e->x_send, e->x_send_cap));
-  if (t->alltoallv(t->user, e->x_send, soff.data(), ssize.data(), e->x_recv, roff.data(), rsize.data(),
+  // One buffer: the receive regions, then the send regions to the other ranks. The region to this
+  // rank is packed where rg_wire_recv reads it (the transport moves 0 bytes for it: no self copy of
+  // a rehearsal's ~2 GB); both ends of that link are this engine, so its send and
+  // receive sizes agree. RAFTGPU_RCCL_SELF=rccl (tests: the transport's grouped path at one rank)
+  // keeps a separate send region for it.
+  const bool alias = !e->self_via_transport && ssize[me] == rsize[me];
+  const uint64_t sbase = (rt + 255) & ~255ull;
+  for (uint32_t r = 0; r < N; ++r) {
+    if (alias && r == me) {
+      soff[r] = roff[r];
+      continue;
+    }
+    soff[r] = sbase + st;
+    st += ssize[r];
+  }
+  RGCHK(xgrow(e, &e->x_recv, &e->x_recv_cap, std::max<uint64_t>(sbase + st, 256)));
+  RGCHK(wire_pack_at(e, e->x_recv, soff.data(), e->x_recv_cap, "rg_wire_exchange"));
+  std::vector<uint64_t> ts(ssize), tr(rsize);
+  if (alias) ts[me] = tr[me] = 0;
+  if (t->alltoallv(t->user, e->x_recv, soff.data(), ts.data(), e->x_recv, roff.data(), tr.data(),
                    (void*)e->stream) != 0)
     return fail(RG_EHIP, "rg_wire_exchange: transport alltoallv failed");
-  if (sent_bytes) *sent_bytes = st - ssize[me];
+  if (sent_bytes) *sent_bytes = st - (alias ? 0 : ssize[me]);
   return rg_wire_recv(e, e->x_recv, rsize.data());
 }
 

@@ -280,7 +280,7 @@ EXPORTS = ["rg_create", "rg_destroy", "rg_bootstrap", "rg_fill_slabs", "rg_tick"
            "rg_set_stream", "rg_sync", "rg_tick_count", "rg_read_replicas", "rg_read_msgs",
            "rg_read_entries", "rg_import_replica", "rg_deliver", "rg_leader", "rg_sum_committed",
            "rg_device_bytes", "rg_last_error", "rg_last_tick_traffic", "rg_join",
-           "rg_timing", "rg_kernel_ms", "rg_wire_plan", "rg_wire_pack", "rg_wire_recv", "rg_global_id",
+           "rg_timing", "rg_kernel_ms", "rg_wire_plan", "rg_wire_pack", "rg_wire_pack_at", "rg_wire_recv", "rg_global_id",
            "rg_apply_committed", "rg_probe_copy", "rg_persist_collect", "rg_snapshot_events", "rg_propose",
            "rg_notify_applied", "rg_apply_async", "rg_apply_wait", "rg_read_index", "rg_read_index_results",
            "rg_config_change", "rg_wire_exchange", "rg_rccl_unique_id", "rg_rccl_open", "rg_rccl_close",
@@ -347,6 +347,7 @@ def load_library(path: str = LIB_PATH):
         "rg_wire_plan_fixed": ([vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)], i32),
         "rg_wire_dropped": ([vp, C.POINTER(C.c_uint64)], i32),
         "rg_wire_pack": ([vp, vp, u64], i32),
+        "rg_wire_pack_at": ([vp, vp, C.POINTER(C.c_uint64), u64], i32),
         "rg_wire_recv": ([vp, vp, C.POINTER(C.c_uint64)], i32),
         "rg_wire_exchange": ([vp, C.POINTER(Transport), C.POINTER(C.c_uint64)], i32),
         "rg_rccl_unique_id": ([C.c_char_p], i32),
@@ -670,6 +671,11 @@ class Engine:
 
     def wire_pack(self, send_ptr: int, send_cap: int):
         self._check(self.L.rg_wire_pack(self.h, C.c_void_p(send_ptr or None), send_cap))
+
+    def wire_pack_at(self, base_ptr: int, region_off, base_cap: int):
+        """rg_wire_pack_at: region r at base + region_off[r]."""
+        ro = (C.c_uint64 * self.ranks)(*region_off)
+        self._check(self.L.rg_wire_pack_at(self.h, C.c_void_p(base_ptr or None), ro, base_cap))
 
     def wire_recv(self, recv_ptr: int, recv_bytes):
         rb = (C.c_uint64 * self.ranks)(*recv_bytes)

@@ -348,19 +348,22 @@ def test_c_exchange_transport_failures_surface_as_errors():
     ex.sync()
 
 
-def _copy_transport(calls):
-    """A one-rank Python transport: alltoallv copies the send regions into the receive buffer (after
-    the engine stream, before returning); allgather records that it was called."""
+def _copy_transport(calls, moved=None):
+    """A one-rank Python transport: alltoallv copies each send region (send + soff[r], ssize[r] bytes)
+    to its receive region (after the engine stream, before returning); allgather records that it was
+    called; `moved` collects the bytes each call was asked to move."""
     import torch
     from raftd_amd.cluster import _dev_bytes
     from raftd_amd.engine import PyTransport
 
     def a2a(send, soff, ssize, recv, roff, rsize, stream):
         torch.cuda.synchronize()
-        n = sum(ssize)
-        assert n == sum(rsize)
-        if n:
-            _dev_bytes(recv, n, "cuda").copy_(_dev_bytes(send, n, "cuda"))
+        assert list(ssize) == list(rsize)
+        for r, n in enumerate(ssize):
+            if n:
+                _dev_bytes(recv + roff[r], n, "cuda").copy_(_dev_bytes(send + soff[r], n, "cuda"))
+        if moved is not None:
+            moved.append(sum(ssize))
         torch.cuda.synchronize()
 
     t = PyTransport(lambda vals: calls.append(list(vals)) or list(vals), a2a)
@@ -378,8 +381,8 @@ def test_exchange_is_one_collective_with_fixed_capacity(sizing):
     cfg = dict(groups=16, replicas=3, seed=95, **CHAOS)
     eng = Engine(wire_all=1, wire_exact=int(sizing == "exact"), **cfg)
     ora = make("c", **cfg)
-    calls = []
-    t = _copy_transport(calls)
+    calls, moved = [], []
+    t = _copy_transport(calls, moved)
     eng.bootstrap()
     ora.bootstrap()
     rng = np.random.default_rng(96)
@@ -392,6 +395,9 @@ def test_exchange_is_one_collective_with_fixed_capacity(sizing):
         compare(eng, ora, k)
     assert t.error is None and eng.wire_dropped() == 0
     assert (calls == []) if sizing == "fixed" else len(calls) == 49
+    # one rank: its only region is the one to itself, packed where the unpack reads it (rg_wire_pack_at),
+    # so the transport is asked to move nothing
+    assert len(moved) == 49 and set(moved) == {0}
 
 
 def test_fixed_capacity_overflow_drops_units_and_grows():
