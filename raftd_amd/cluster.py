@@ -270,7 +270,7 @@ class _Half:
             rsizes, biggest = exchange_sizes(sizes, self.pg)
         ro, rtot = _offsets(rsizes)
         me = self.rank
-        if dist.get_backend(self.pg) == "nccl" and sizes[me] == rsizes[me]:
+        if dist.get_backend(self.pg) == "nccl" and sizes[me] and sizes[me] == rsizes[me]:
             # one buffer: the receive regions, then the send regions to the other ranks; the region to
             # this rank is packed where wire_recv reads it (no self copy; rg_wire_pack_at). Stream order:
             # the tick that read the old contents runs before the pack and the transfers

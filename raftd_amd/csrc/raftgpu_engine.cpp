@@ -2728,7 +2728,7 @@ int rg_wire_exchange(rg_engine* e, const rg_transport* t, uint64_t* sent_bytes) 
   // a rehearsal's ~2 GB); both ends of that link are this engine, so its send and
   // receive sizes agree. RAFTGPU_RCCL_SELF=rccl (tests: the transport's grouped path at one rank)
   // keeps a separate send region for it.
-  const bool alias = !e->self_via_transport && ssize[me] == rsize[me];
+  const bool alias = !e->self_via_transport && ssize[me] && ssize[me] == rsize[me];
   const uint64_t sbase = (rt + 255) & ~255ull;
   for (uint32_t r = 0; r < N; ++r) {
     if (alias && r == me) {
