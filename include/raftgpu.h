@@ -533,12 +533,17 @@ int rg_commit_update(rg_engine* e, const rg_update* u, uint32_t flags);
 /* Stage ReadIndex requests for the next tick (dragonboat's NodeHost.ReadIndex → Peer.ReadIndex): a
  * leader that has committed an entry in its term records its commit index and confirms leadership
  * with one heartbeat round carrying the context; a follower forwards the request to its leader,
- * which answers with a ReadIndexResp once confirmed. One pending request per leader (another is
- * dropped, counted in drops; the shim retries). RG_EINVAL: bad shard / slot, ctx 0, or a replica
+ * which answers with a ReadIndexResp once confirmed. A leader keeps up to RG_READ_QUEUE requests
+ * pending in arrival order (dragonboat's readIndex queue; a context already pending is not added
+ * twice, one more is dropped and counted in drops — the shim retries): when a quorum has confirmed
+ * one, it and every request queued before it become ready at its index, and every regular
+ * heartbeat carries the newest pending context. RG_EINVAL: bad shard / slot, ctx 0, or a replica
  * hosted by another rank (nothing staged). A later request for the same replica in the same tick
  * replaces the earlier one. */
+#define RG_READ_QUEUE 4
 int rg_read_index(rg_engine* e, const rg_read_request* reqs, size_t n);
-/* Reads made ready in the last tick for replicas whose slot bit is set, one per replica at most, in
+/* Reads made ready in the last tick for replicas whose slot bit is set — up to RG_READ_QUEUE per
+ * replica, in the order they became ready (more in one tick are dropped, counted) — replicas in
  * device order; compacted on the device, one hipMemcpyAsync. *n = count; RG_EFULL if > cap. */
 int rg_read_index_results(rg_engine* e, uint32_t slot_mask, rg_read_ready* out, uint64_t cap, uint64_t* n);
 /* Stage a membership change for the next tick: NodeHost.SyncRequestAddReplica (op RG_CC_ADD) /

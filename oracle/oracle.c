@@ -60,10 +60,14 @@ typedef struct {
    * (rsm → IOnDiskStateMachine.Update); a range restored from a snapshot does not */
   uint64_t apply_lo, restored_at;
   int took; /* a snapshot was taken at the end of the last step */
-  /* ReadIndex: the leader's pending request (ctx 0 = none), and the read made ready in a step */
-  uint64_t ri_ctx, ri_index;
-  uint32_t ri_acks, ri_from;
-  uint64_t rd_ctx, rd_index, rd_tick; /* rd_tick = step + 1 when it became ready */
+  /* ReadIndex (dragonboat's readIndex: pending + queue): the leader's pending requests in arrival
+   * order — ctx, the commit index when it arrived, the slots that confirmed it (itself included) and
+   * the requester's slot — and the reads made ready in a step (rd_tick = step + 1) */
+  uint32_t rq_n;
+  uint64_t rq_ctx[OR_RQ], rq_index[OR_RQ];
+  uint32_t rq_acks[OR_RQ], rq_from[OR_RQ];
+  uint32_t rd_n;
+  uint64_t rd_ctx[OR_RQ], rd_index[OR_RQ], rd_tick;
   /* payload stream: the capacity rule's state. hw = next free chunk; lpg = lowest page
    * held; fidx = the step compacted or restored below this entry: its position bounds the pages the
    * next step releases (nlpg, effective once that step ends) */
@@ -275,7 +279,7 @@ static void reset(or_engine* e, rep_t* r, uint64_t t) {
   }
   r->match[r->s] = r->last;
   r->active = 0;
-  r->ri_ctx = 0;     /* readIndex.reset */
+  r->rq_n = 0;       /* readIndex.reset: a new readIndex */
   r->cc_pending = 0; /* clearPendingConfigChange */
 }
 
@@ -429,7 +433,7 @@ static void broadcast_heartbeat(or_engine* e, rep_t* r) {
     h.type = OR_HEARTBEAT;
     h.to = (uint8_t)id_of(i);
     h.commit = u64min(r->match[i], r->committed);
-    h.hint = r->ri_ctx; /* a pending ReadIndex rides on every heartbeat (readIndex.peepCtx) */
+    h.hint = r->rq_n ? r->rq_ctx[r->rq_n - 1] : 0; /* readIndex.peepCtx: the newest pending request */
     send_msg(e, r, &h);
   }
 }
@@ -695,9 +699,17 @@ static void handle_leader_replicate_resp(or_engine* e, rep_t* r, const or_msg_vi
 }
 
 static void read_ready(or_engine* e, rep_t* r, uint64_t ctx, uint64_t index) { /* addReadyToRead */
-  r->rd_ctx = ctx;
-  r->rd_index = index;
-  r->rd_tick = e->t + 1;
+  if (r->rd_tick != e->t + 1) {  /* the first read made ready in this step */
+    r->rd_tick = e->t + 1;
+    r->rd_n = 0;
+  }
+  if (r->rd_n == OR_RQ) { /* the step's ready list is full: dropped (counted) */
+    r->drops++;
+    return;
+  }
+  r->rd_ctx[r->rd_n] = ctx;
+  r->rd_index[r->rd_n] = index;
+  r->rd_n++;
 }
 
 /* the leader's confirmed read goes to its requester: itself, or a follower (ReadIndexResp) */
@@ -721,14 +733,29 @@ static void handle_leader_heartbeat_resp(or_engine* e, rep_t* r, const or_msg_vi
   r->active |= 1u << f;
   if (r->rstate[f] == OR_WAIT) r->rstate[f] = OR_RETRY;
   if (r->match[f] < r->last) send_replicate(e, r, f);
-  if (m->hint != 0 && m->hint == r->ri_ctx) { /* readIndex.confirm */
-    r->ri_acks |= 1u << f;
-    if (popc(r->ri_acks & r->members) >= quorum(r)) {
-      uint64_t ctx = r->ri_ctx;
-      r->ri_ctx = 0;
-      read_confirmed(e, r, ctx, r->ri_index, r->ri_from);
-    }
+  if (m->hint == 0) return;
+  /* readIndex.confirm: the request this heartbeat answered; once a quorum confirmed it, it and every
+   * request queued before it are done, all at its index (dragonboat rewrites v.index = s.index) */
+  uint32_t k = 0;
+  while (k < r->rq_n && r->rq_ctx[k] != m->hint) ++k;
+  if (k == r->rq_n) return;
+  r->rq_acks[k] |= 1u << f;
+  if (popc(r->rq_acks[k] & r->members) < quorum(r)) return;
+  const uint64_t index = r->rq_index[k];
+  uint64_t ctx[OR_RQ];
+  uint32_t from[OR_RQ];
+  for (uint32_t i = 0; i <= k; ++i) {
+    ctx[i] = r->rq_ctx[i];
+    from[i] = r->rq_from[i];
   }
+  for (uint32_t i = k + 1; i < r->rq_n; ++i) { /* the rest move to the front */
+    r->rq_ctx[i - k - 1] = r->rq_ctx[i];
+    r->rq_index[i - k - 1] = r->rq_index[i];
+    r->rq_acks[i - k - 1] = r->rq_acks[i];
+    r->rq_from[i - k - 1] = r->rq_from[i];
+  }
+  r->rq_n -= k + 1;
+  for (uint32_t i = 0; i <= k; ++i) read_confirmed(e, r, ctx[i], index, from[i]);
 }
 
 /* ReadIndex{hint = ctx} from slot m->from (itself, or a follower that forwarded it) */
@@ -737,13 +764,22 @@ static void handle_read_index(or_engine* e, rep_t* r, const or_msg_view* m) {
   if (r->role == OR_LEADER) {
     if (quorum(r) == 1) { /* isSingleNodeQuorum */
       read_confirmed(e, r, m->hint, r->committed, f);
-    } else if (term_of(e, r, r->committed) != r->term || r->ri_ctx != 0) {
-      r->drops++; /* no entry committed in this term yet (thesis §6.4), or a read already pending */
+    } else if (term_of(e, r, r->committed) != r->term) {
+      r->drops++; /* no entry committed in this term yet (thesis §6.4) */
     } else {
-      r->ri_ctx = m->hint;
-      r->ri_index = r->committed;
-      r->ri_acks = 1u << r->s;
-      r->ri_from = f;
+      uint32_t k = 0; /* readIndex.addRequest: a context already pending is not added again */
+      while (k < r->rq_n && r->rq_ctx[k] != m->hint) ++k;
+      if (k == r->rq_n) {
+        if (r->rq_n == OR_RQ) { /* the queue is full: dropped (counted), no heartbeat */
+          r->drops++;
+          return;
+        }
+        r->rq_ctx[k] = m->hint;
+        r->rq_index[k] = r->committed;
+        r->rq_acks[k] = 1u << r->s;
+        r->rq_from[k] = f;
+        r->rq_n++;
+      }
       for (uint32_t i = 0; i < e->c.replicas; ++i) { /* broadcastHeartbeatMessageWithHint */
         if (i == r->s || !is_member(r, i)) continue;
         or_msg_view h;
@@ -1157,13 +1193,15 @@ int or_read_index(or_engine* e, const or_read_request* q, size_t n) {
   return 0;
 }
 
-int or_get_read_ready(const or_engine* e, uint32_t rid, uint64_t* ctx, uint64_t* index) {
+int or_get_read_ready(const or_engine* e, uint32_t rid, uint64_t* ctx, uint64_t* index, uint32_t cap) {
   if (rid >= e->nrep) return -1;
   const rep_t* r = &e->reps[rid];
-  if (r->rd_tick != e->t) return 0; /* not made ready in the last step */
-  if (ctx) *ctx = r->rd_ctx;
-  if (index) *index = r->rd_index;
-  return 1;
+  if (r->rd_tick != e->t) return 0; /* none made ready in the last step */
+  for (uint32_t i = 0; i < r->rd_n && i < cap; ++i) {
+    if (ctx) ctx[i] = r->rd_ctx[i];
+    if (index) index[i] = r->rd_index[i];
+  }
+  return (int)r->rd_n;
 }
 
 int or_propose(or_engine* e, const or_proposal* p, size_t n, const uint8_t* payload, const uint32_t* lens) {
@@ -1454,7 +1492,8 @@ int or_import_replica(or_engine* e, uint32_t rid, const or_replica_view* v, cons
   r->cap_base = v->cap_base;
   r->restored_at = 0;
   r->took = 0;
-  r->ri_ctx = r->rd_tick = 0;
+  r->rq_n = 0;
+  r->rd_tick = 0;
   r->role = v->role;
   r->election_tick = v->election_tick;
   r->heartbeat_tick = v->heartbeat_tick;

@@ -24,6 +24,7 @@ extern "C" {
 #endif
 
 #define OR_MAX_R 8
+#define OR_RQ 4 /* ReadIndex requests a leader holds pending, and reads a replica makes ready per step */
 #define OR_MAX_CMD (1u << 24) /* the longest Cmd max_cmd_bytes may name (16 MiB; the engine's MAX_CMD) */
 
 /* raftpb.MessageType numbering as recalled (VERIFY); only the values below are used. */
@@ -181,9 +182,10 @@ typedef struct or_read_request {
   uint64_t ctx;   /* non-zero request context (dragonboat's SystemCtx) */
 } or_read_request;
 int or_read_index(or_engine* e, const or_read_request* reqs, size_t n);
-/* The read replica rid's last step made ready (ReadyToRead): returns 1 with its ctx and read index
- * (serve it once applied >= index), 0 if none. */
-int or_get_read_ready(const or_engine* e, uint32_t rid, uint64_t* ctx, uint64_t* index);
+/* The reads replica rid's last step made ready (ReadyToRead), in the order they became ready: returns
+ * how many (at most OR_RQ), the first `cap` of them in ctx[] / index[] (serve each once applied >=
+ * its index). */
+int or_get_read_ready(const or_engine* e, uint32_t rid, uint64_t* ctx, uint64_t* index, uint32_t cap);
 /* Snapshot events of rid's last step (the oracle side of rg_snapshot_events): OR_SNAP_* bits. */
 #define OR_SNAP_TAKEN 1
 #define OR_SNAP_RESTORED 2

@@ -134,7 +134,7 @@ def lib():
         L.or_config_change.argtypes = [vp, u64, u32, u32, u32]
         L.or_compact.argtypes = [vp, u64, u64]
         L.or_read_index.argtypes = [vp, C.POINTER(ReadRequest), C.c_size_t]
-        L.or_get_read_ready.argtypes = [vp, u32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.or_get_read_ready.argtypes = [vp, u32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), u32]
         L.or_tick.restype = C.c_int
         L.or_deliver.argtypes = [vp, u32, C.POINTER(MsgView)]
         L.or_payload.argtypes = [vp, u32, u32, u32, C.c_void_p]
@@ -350,9 +350,10 @@ class Oracle:
         return out[0], out[1]
 
     def read_ready(self, rid):
-        """(ctx, index) of the read replica rid made ready in the last tick, or None."""
-        c, i = C.c_uint64(), C.c_uint64()
-        return (c.value, i.value) if self.L.or_get_read_ready(self.h, rid, C.byref(c), C.byref(i)) == 1 else None
+        """[(ctx, index), ...] of the reads replica rid made ready in the last tick, in order."""
+        c, i = (C.c_uint64 * 8)(), (C.c_uint64 * 8)()
+        n = self.L.or_get_read_ready(self.h, rid, c, i, 8)
+        return [(c[k], i[k]) for k in range(n)]
 
     def compact(self, group, index) -> int:
         """or_compact (rg_compact): compact every replica of global shard `group` to min(index, its

@@ -33,6 +33,7 @@ RETRY, WAIT, REPL, SNAP = 0, 1, 2, 3
 ERR_CONFLICT, ERR_BEYOND, ERR_RING, ERR_CRC, ERR_EMPTY_SNAP = 1, 2, 4, 8, 16
 ERR_TERM = 128  # a campaign at the last term the ring word holds (2^36 - 1): refused
 TERM_MAX = (1 << 36) - 1
+RQ = 4  # ReadIndex requests a leader holds pending, reads a replica makes ready per step
 LEADER_MSGS = (REPLICATE, INSTALL_SNAPSHOT, HEARTBEAT, READ_INDEX_RESP)
 CC_ADD, CC_REMOVE = 1, 2  # membership change ops: descriptor op << 4 | (slot + 1)
 
@@ -147,8 +148,8 @@ class Replica:
         self.remotes = []
         self.out = {}
         self.emitted = {}
-        self.pending_read = None  # leader: [ctx, index, acks set, requester slot]
-        self.ready_read = None    # (tick, ctx, index) of the read made ready in a step
+        self.pending_reads = []  # leader, arrival order: [ctx, index, acks set, requester slot]
+        self.ready_reads = None  # (tick, [(ctx, index), ...]) of the reads made ready in a step
         self.members = set(range(sim.R))  # voting membership as applied here
         self.snap_members = set(range(sim.R))
         self.cc_pending = False
@@ -225,7 +226,7 @@ class Replica:
         self.remotes = [Remote(0, self.last + 1) for _ in range(self.sim.R)]
         self.remotes[self.s].match = self.last
         self.active = set()
-        self.pending_read = None
+        self.pending_reads = []  # readIndex.reset
         self.cc_pending = False  # clearPendingConfigChange
 
     def become_follower(self, t, leader):
@@ -333,17 +334,29 @@ class Replica:
             rp.state = RETRY
         if rp.match < self.last:
             self.send_replicate(f)
-        pr = self.pending_read
-        if m["hint"] and pr is not None and m["hint"] == pr[0]:
-            pr[2].add(f)
-            if len(pr[2] & self.members) >= self.quorum:
-                self.pending_read = None
-                self.read_confirmed(pr[0], pr[1], pr[3])
+        # readIndex.confirm: once a quorum confirmed the answered request, it and every request queued
+        # before it are done, all at its index
+        q = self.pending_reads
+        k = next((i for i, pr in enumerate(q) if pr[0] == m["hint"]), None) if m["hint"] else None
+        if k is not None:
+            q[k][2].add(f)
+            if len(q[k][2] & self.members) >= self.quorum:
+                done, self.pending_reads = q[:k + 1], q[k + 1:]
+                for ctx, _, _, slot in done:
+                    self.read_confirmed(ctx, q[k][1], slot)
 
-    # -- ReadIndex (Raft thesis §6.4) --
+    # -- ReadIndex (Raft thesis §6.4; dragonboat's readIndex queue) --
+    def read_ready_add(self, ctx, index):  # addReadyToRead, at most RQ per step
+        if self.ready_reads is None or self.ready_reads[0] != self.sim.t:
+            self.ready_reads = (self.sim.t, [])
+        if len(self.ready_reads[1]) == RQ:
+            self.drops += 1
+        else:
+            self.ready_reads[1].append((ctx, index))
+
     def read_confirmed(self, ctx, index, slot):
         if slot == self.s:
-            self.ready_read = (self.sim.t, ctx, index)
+            self.read_ready_add(ctx, index)
         else:
             self.send(msg(READ_INDEX_RESP, slot + 1, log_index=index, hint=ctx))
 
@@ -352,10 +365,14 @@ class Replica:
         if self.role == LEADER:
             if self.quorum == 1:
                 self.read_confirmed(m["hint"], self.committed, f)
-            elif self.term_at(self.committed) != self.term or self.pending_read is not None:
+            elif self.term_at(self.committed) != self.term:
                 self.drops += 1
             else:
-                self.pending_read = [m["hint"], self.committed, {self.s}, f]
+                if all(pr[0] != m["hint"] for pr in self.pending_reads):  # readIndex.addRequest
+                    if len(self.pending_reads) == RQ:  # the queue is full: dropped, no heartbeat
+                        self.drops += 1
+                        return
+                    self.pending_reads.append([m["hint"], self.committed, {self.s}, f])
                 for i in range(self.sim.R):
                     if i != self.s and i in self.members:
                         self.send(msg(HEARTBEAT, i + 1, commit=min(self.remotes[i].match, self.committed),
@@ -499,7 +516,7 @@ class Replica:
                     self.campaign()
         elif t == LEADER_HEARTBEAT:
             if role == LEADER:  # a pending ReadIndex rides on every heartbeat (readIndex.peepCtx)
-                ctx = self.pending_read[0] if self.pending_read is not None else 0
+                ctx = self.pending_reads[-1][0] if self.pending_reads else 0
                 for i in range(self.sim.R):
                     if i != self.s and i in self.members:
                         self.send(msg(HEARTBEAT, i + 1, commit=min(self.remotes[i].match, self.committed), hint=ctx))
@@ -554,7 +571,7 @@ class Replica:
             if role == FOLLOWER:
                 self.etick = 0
                 self.leader = m["frm"]
-                self.ready_read = (self.sim.t, m["hint"], m["log_index"])
+                self.read_ready_add(m["hint"], m["log_index"])
         elif t == REQUEST_VOTE:
             self.on_request_vote(m)
         elif t == REQUEST_VOTE_RESP:
@@ -660,8 +677,8 @@ class Sim:
         return 0
 
     def read_ready(self, rid):
-        rr = self.reps[rid].ready_read
-        return (rr[1], rr[2]) if rr is not None and rr[0] == self.t - 1 else None
+        rr = self.reps[rid].ready_reads
+        return list(rr[1]) if rr is not None and rr[0] == self.t - 1 else []
 
     def propose(self, batches):
         """Stage caller proposals (group, slot, [cmds]) for the next tick; all or nothing:
@@ -829,7 +846,7 @@ class Sim:
         resp = view.get("responded", 0)
         r.votes = {k: bool(g >> k & 1) for k in range(8) if resp >> k & 1}
         r.active = {k for k in range(8) if view.get("active", 0) >> k & 1}
-        r.pending_read = r.ready_read = None
+        r.pending_reads, r.ready_reads = [], None
         r.members = {k for k in range(8) if view.get("members", (1 << self.R) - 1) >> k & 1}
         r.snap_members = {k for k in range(8) if view.get("snap_members", view.get("members", (1 << self.R) - 1)) >> k & 1}
         r.cc_pending = bool(view.get("cc_pending", 0))

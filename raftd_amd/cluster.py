@@ -706,7 +706,7 @@ class LoopbackCluster(_Feeds):
                 self.engines[k].read_index(b)
 
     def read_ready_all(self) -> dict:
-        """{cluster rid: (ctx, index)} for the reads made ready in the last tick, over all ranks."""
+        """{cluster rid: [(ctx, index), ...]} for the reads made ready in the last tick, over all ranks."""
         back = {kl: r for r, kl in enumerate(self.loc)}
         out = {}
         for k, e in enumerate(self.engines):
@@ -715,8 +715,8 @@ class LoopbackCluster(_Feeds):
         return out
 
     def read_ready(self, rid):
-        """(ctx, index) made ready for cluster replica rid in the last tick, or None."""
-        return self.read_ready_all().get(rid)
+        """[(ctx, index), ...] made ready for cluster replica rid in the last tick."""
+        return self.read_ready_all().get(rid, [])
 
     def propose(self, batches):
         """rg_propose on the rank hosting each batch's replica (global group, slot)."""

@@ -370,7 +370,9 @@ hipError_t launch_snap_gather(const SnapParams& a, hipStream_t st) {
 __global__ void read_count_kernel(SnapParams a) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= a.nrep) return;
-  a.cnt[q] = ((a.slot_mask >> (q / a.G)) & 1u) && a.rdst[(uint64_t)RD_TICK * a.nrep + q] == a.tick ? 1u : 0u;
+  a.cnt[q] = ((a.slot_mask >> (q / a.G)) & 1u) && a.rdst[(uint64_t)RD_TICK * a.nrep + q] == a.tick
+                ? (uint32_t)a.rdst[(uint64_t)RD_N * a.nrep + q]
+                : 0u;
 }
 
 hipError_t launch_read_count(const SnapParams& a, uint64_t* total, hipStream_t st) {
@@ -389,9 +391,11 @@ __global__ void read_gather_kernel(SnapParams a) {
   r.group = pl_group(a.pl, s, j);
   r.replica_id = s + 1;
   r.rid = j * a.R + s;
-  r.ctx = a.rdst[(uint64_t)RD_CTX * a.nrep + q];
-  r.index = a.rdst[(uint64_t)RD_INDEX * a.nrep + q];
-  reinterpret_cast<rg_read_ready*>(a.out)[a.off[q]] = r;
+  for (uint32_t k = 0; k < a.cnt[q]; ++k) {  // in the order they became ready
+    r.ctx = a.rdst[(uint64_t)(RD_CTX + k) * a.nrep + q];
+    r.index = a.rdst[(uint64_t)(RD_INDEX + k) * a.nrep + q];
+    reinterpret_cast<rg_read_ready*>(a.out)[a.off[q] + k] = r;
+  }
 }
 
 hipError_t launch_read_gather(const SnapParams& a, hipStream_t st) {

@@ -403,7 +403,7 @@ struct Ctl {
     });
     active = 0;
     cc_pending = 0;  // clearPendingConfigChange
-    if (P().rdst) P().rdst[(uint64_t)RI_CTX * P().nrep + q] = 0;  // readIndex.reset
+    if (P().rdst) P().rdst[(uint64_t)RQ_N * P().nrep + q] = 0;  // readIndex.reset: a new readIndex
   }
   RG_FN void become_follower(uint64_t t, uint64_t l) {
     role = FOLLOWER;
@@ -806,9 +806,13 @@ struct Ctl {
     }
   }
   RG_FN void broadcast_heartbeat() {
-    // a pending ReadIndex rides on every heartbeat (dragonboat's broadcastHeartbeatMessage attaches
-    // readIndex.peepCtx), so a lost read heartbeat or response is retried by the next round
-    const uint64_t ctx = P().rdst ? P().rdst[(uint64_t)RI_CTX * P().nrep + q] : 0ull;
+    // the newest pending ReadIndex rides on every heartbeat (dragonboat's broadcastHeartbeatMessage
+    // attaches readIndex.peepCtx), so a lost read heartbeat or response is retried by the next round
+    uint64_t ctx = 0;
+    if (P().rdst) {
+      const uint64_t nq = P().rdst[(uint64_t)RQ_N * P().nrep + q];
+      if (nq) ctx = P().rdst[(RQ_CTX + nq - 1) * (uint64_t)P().nrep + q];
+    }
     if constexpr (FAST) {  // a pending read: its confirmation round is the full step's
       if (ctx) {
         abort_();
@@ -1047,26 +1051,52 @@ struct Ctl {
     active |= 1u << f;
     if (RG_GET(rt, f) == WAIT) RG_SET(rt, f, (uint32_t)RETRY);
     if (RG_GET(rm, f) < last) send_replicate(f);
-    if (hint != 0 && P().rdst) {  // readIndex.confirm: only read heartbeats carry a context
-      uint64_t* rd = P().rdst + q;
-      const uint64_t n = P().nrep;
-      if (rd[RI_CTX * n] == hint) {
-        const uint64_t a = rd[RI_ACKS * n] | (1ull << f);
-        if ((uint32_t)__builtin_popcount((uint32_t)a & members) >= quorum()) {
-          rd[RI_CTX * n] = 0;
-          read_confirmed(hint, rd[RI_INDEX * n], (uint32_t)(a >> 32));
-        } else {
-          rd[RI_ACKS * n] = a;
-        }
-      }
+    if (hint != 0 && P().rdst) read_confirm(hint, f);  // only read heartbeats carry a context
+  }
+  // readIndex.confirm: the request this heartbeat answered; once a quorum confirmed it, it and every
+  // request queued before it are done, all at its index (dragonboat rewrites v.index = s.index)
+  RG_FN void read_confirm(uint64_t hint, uint32_t f) {
+    uint64_t* rd = P().rdst + q;
+    const uint64_t n = P().nrep;
+    const uint32_t nq = (uint32_t)rd[RQ_N * n];
+    uint32_t k = 0;
+    while (k < nq && rd[(RQ_CTX + k) * n] != hint) ++k;
+    if (k == nq) return;
+    const uint64_t a = rd[(RQ_ACKS + k) * n] | (1ull << f);
+    if ((uint32_t)__builtin_popcount((uint32_t)a & members) < quorum()) {
+      rd[(RQ_ACKS + k) * n] = a;
+      return;
     }
+    const uint64_t index = rd[(RQ_INDEX + k) * n];
+    uint64_t ctx[RG_RQ], acks[RG_RQ];
+    for (uint32_t i = 0; i <= k; ++i) {
+      ctx[i] = rd[(RQ_CTX + i) * n];
+      acks[i] = rd[(RQ_ACKS + i) * n];
+    }
+    for (uint32_t i = k + 1; i < nq; ++i) {  // the rest move to the front
+      rd[(RQ_CTX + i - k - 1) * n] = rd[(RQ_CTX + i) * n];
+      rd[(RQ_INDEX + i - k - 1) * n] = rd[(RQ_INDEX + i) * n];
+      rd[(RQ_ACKS + i - k - 1) * n] = rd[(RQ_ACKS + i) * n];
+    }
+    rd[RQ_N * n] = nq - k - 1;
+    for (uint32_t i = 0; i <= k; ++i) read_confirmed(ctx[i], index, (uint32_t)(acks[i] >> 32));
   }
   // ---- ReadIndex (Raft thesis §6.4; dragonboat's readIndex), state in P().rdst, not in registers
-  RG_FN void read_ready(uint64_t ctx, uint64_t index) {  // addReadyToRead
+  RG_FN void read_ready(uint64_t ctx, uint64_t index) {  // addReadyToRead, at most RG_RQ per step
     uint64_t* rd = P().rdst + q;
-    rd[RD_CTX * (uint64_t)P().nrep] = ctx;
-    rd[RD_INDEX * (uint64_t)P().nrep] = index;
-    rd[RD_TICK * (uint64_t)P().nrep] = P().tick + 1;
+    const uint64_t n = P().nrep;
+    uint64_t k = rd[RD_N * n];
+    if (rd[RD_TICK * n] != P().tick + 1) {  // the first read made ready in this step
+      rd[RD_TICK * n] = P().tick + 1;
+      k = 0;
+    }
+    if (k == RG_RQ) {  // the step's ready list is full: dropped (counted)
+      drops++;
+      return;
+    }
+    rd[(RD_CTX + k) * n] = ctx;
+    rd[(RD_INDEX + k) * n] = index;
+    rd[RD_N * n] = k + 1;
   }
   RG_FN void read_confirmed(uint64_t ctx, uint64_t index, uint32_t slot) {
     if (slot == s) read_ready(ctx, index);
@@ -1080,12 +1110,22 @@ struct Ctl {
       const uint64_t n = P().nrep;
       if (quorum() == 1) {  // isSingleNodeQuorum
         read_confirmed(ctx, committed, f);
-      } else if (term_at(committed) != term || rd[RI_CTX * n] != 0) {
-        drops++;  // nothing committed in this term yet, or a read already pending
+      } else if (term_at(committed) != term) {
+        drops++;  // nothing committed in this term yet (thesis §6.4)
       } else {
-        rd[RI_CTX * n] = ctx;
-        rd[RI_INDEX * n] = committed;
-        rd[RI_ACKS * n] = (1ull << s) | ((uint64_t)f << 32);
+        const uint32_t nq = (uint32_t)rd[RQ_N * n];
+        uint32_t k = 0;  // readIndex.addRequest: a context already pending is not added again
+        while (k < nq && rd[(RQ_CTX + k) * n] != ctx) ++k;
+        if (k == nq) {
+          if (nq == RG_RQ) {  // the queue is full: dropped (counted), no heartbeat
+            drops++;
+            return;
+          }
+          rd[(RQ_CTX + k) * n] = ctx;
+          rd[(RQ_INDEX + k) * n] = committed;
+          rd[(RQ_ACKS + k) * n] = (1ull << s) | ((uint64_t)f << 32);
+          rd[RQ_N * n] = nq + 1;
+        }
         for (uint32_t i = 0; i < R; ++i)  // broadcastHeartbeatMessageWithHint
           if (i != s && is_member(i)) send(M_HEARTBEAT, i + 1, 0, 0, 0, 0, 0, umin64(RG_GET(rm, i), committed), ctx, 0, 0, 0);
       }

@@ -63,7 +63,8 @@ static constexpr bool g_sync_debug = false;
   } while (0)
 
 constexpr uint32_t TP_SLOTS = 128, TP_CHUNK = 32;
-constexpr uint32_t D_SUM_BYTES = 128;  // rg_get_update's section totals (9 u64), digests, counters
+constexpr uint32_t D_SUM_BYTES = 128;
+static_assert(RG_RQ == RG_READ_QUEUE, "the ReadIndex queue rows and the ABI constant agree");  // rg_get_update's section totals (9 u64), digests, counters
 
 // rg_propose's per-batch scratch (kept across calls)
 struct PropScratch {
@@ -1827,7 +1828,7 @@ int rg_import_replica(rg_engine* e, uint32_t rid, const rg_replica_view* v, cons
   {  // no snapshot event, pending or ready read until it steps (device rows are indexed by q = s·G + g)
     const uint64_t q = (uint64_t)(rid % e->c.replicas) * e->c.groups + rid / e->c.replicas;
     HIPCHK(hipMemsetAsync(e->snap_ev + q, 0, 8, e->stream));
-    HIPCHK(hipMemsetAsync(e->rdst + (uint64_t)RI_CTX * e->nrep + q, 0, 8, e->stream));
+    HIPCHK(hipMemsetAsync(e->rdst + (uint64_t)RQ_N * e->nrep + q, 0, 8, e->stream));
     HIPCHK(hipMemsetAsync(e->rdst + (uint64_t)RD_TICK * e->nrep + q, 0, 8, e->stream));
   }
   uint32_t st = 0;

@@ -76,7 +76,21 @@ enum : uint32_t {
 };
 // ReadIndex state rows ([row][nrep], updated in place by the replica's own lane, touched only on
 // read traffic): the leader's pending request and the read made ready in a step
-enum : uint32_t { RI_CTX, RI_INDEX, RI_ACKS /* acks | requester slot << 32 */, RD_CTX, RD_INDEX, RD_TICK, RD_ROWS };
+// ReadIndex rows (rdst, [RD_ROWS][nrep]; dragonboat's readIndex queue): a leader's pending requests in
+// arrival order (RQ_N of them: ctx, commit index at arrival, acks | requester slot << 32), and the reads
+// a replica made ready in a step (RD_N of them, in order; RD_TICK = step + 1)
+constexpr uint32_t RG_RQ = 4;  // = RG_READ_QUEUE (include/raftgpu.h; checked in raftgpu_engine.cpp)
+enum : uint32_t {
+  RQ_N,
+  RQ_CTX,
+  RQ_INDEX = RQ_CTX + RG_RQ,
+  RQ_ACKS = RQ_INDEX + RG_RQ,
+  RD_TICK = RQ_ACKS + RG_RQ,
+  RD_N,
+  RD_CTX,
+  RD_INDEX = RD_CTX + RG_RQ,
+  RD_ROWS = RD_INDEX + RG_RQ
+};
 enum : uint32_t { FOLLOWER = 0, CANDIDATE = 1, LEADER = 2 };
 // header word 7 of a local Replicate: its n entries all carry the inline word mt[0] (raftgpu_control.h)
 constexpr uint32_t RG_UNIFORM = 1;

@@ -620,12 +620,15 @@ class Engine:
         self._check(self.L.rg_config_change(self.h, group, slot, op, target))
 
     def read_ready_all(self) -> dict:
-        """{local rid: (ctx, index)} for the reads made ready in the last tick."""
-        return {int(r["rid"]): (int(r["ctx"]), int(r["index"])) for r in self.read_index_results()}
+        """{local rid: [(ctx, index), ...]} for the reads made ready in the last tick, in order."""
+        out = {}
+        for r in self.read_index_results():
+            out.setdefault(int(r["rid"]), []).append((int(r["ctx"]), int(r["index"])))
+        return out
 
     def read_ready(self, rid):
-        """(ctx, index) made ready for local replica rid in the last tick, or None."""
-        return self.read_ready_all().get(rid)
+        """[(ctx, index), ...] made ready for local replica rid in the last tick."""
+        return self.read_ready_all().get(rid, [])
 
     def compact(self, group, index) -> int:
         """rg_compact: compact every local replica of global shard `group` to min(index, its snap_index);

@@ -25,6 +25,8 @@ struct Host {
   std::vector<uint8_t> rst[2];
   std::vector<uint2> slab_info;  // [nslab][G][E] {0, len}: synthetic Cmds are P bytes; ch_propose sets lengths
   std::vector<uint64_t> rdst;     // ReadIndex state rows
+  std::vector<uint64_t> rd;       // rg_read_index staging: ctx per (group, slot), 0 = none
+  bool rd_staged = false;
   std::vector<uint8_t> pt;        // rg_propose staging: target slot, count, non-empty mask per group
   std::vector<uint32_t> pc;
   std::vector<uint64_t> hm;
@@ -117,6 +119,7 @@ void* ch_create(const rg_config* c) {
     h->rcnt.assign(R * R * G, 0);
   }
   h->rdst.assign((size_t)RD_ROWS * n, 0);
+  h->rd.assign(n, 0);
   h->pt.assign(G, 0xFF);
   h->pc.assign(G, 0);
   h->hm.assign(G, 0);
@@ -279,6 +282,7 @@ int ch_tick(void* hh, const rg_tick_input* in) {
     p.prop_cmd = h->pcmd.data();
   }
   if (h->cc_staged) p.cc_in = h->cc.data();
+  if (h->rd_staged) p.read_ctx = h->rd.data();
   if (h->wire) emulate_wire(h, p);
   for (uint32_t q = 0; q < h->nrep; ++q) {
     switch (h->c.replicas) {
@@ -313,7 +317,30 @@ int ch_tick(void* hh, const rg_tick_input* in) {
     std::fill(h->cc.begin(), h->cc.end(), (uint16_t)0);
     h->cc_staged = false;
   }
+  if (h->rd_staged) {
+    std::fill(h->rd.begin(), h->rd.end(), 0ull);
+    h->rd_staged = false;
+  }
   return 0;
+}
+
+// = rg_read_index's staging (global replica id g·R + s; the caller validates)
+void ch_read_index(void* hh, uint32_t rid, uint64_t ctx) {
+  Host* h = (Host*)hh;
+  h->rd[rid] = ctx;
+  h->rd_staged = true;
+}
+// the reads replica rid made ready in the last tick (rdst rows, as read_count / read_gather_kernel)
+int ch_read_ready(void* hh, uint32_t rid, uint64_t* ctx, uint64_t* index, uint32_t cap) {
+  Host* h = (Host*)hh;
+  const uint64_t n = h->nrep, q = qof(h, rid);
+  if (h->rdst[RD_TICK * n + q] != h->t) return 0;
+  const uint32_t k = (uint32_t)h->rdst[RD_N * n + q];
+  for (uint32_t i = 0; i < k && i < cap; ++i) {
+    ctx[i] = h->rdst[(RD_CTX + i) * n + q];
+    index[i] = h->rdst[(RD_INDEX + i) * n + q];
+  }
+  return (int)k;
 }
 
 // = rg_config_change's staging (no validation beyond one change per group)

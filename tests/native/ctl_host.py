@@ -144,6 +144,20 @@ class CtlHost:
                          None if ty is None else C.c_void_p(ty.ctypes.data), C.c_int(1 if payloads is not None else 0),
                          None if ln is None else C.c_void_p(ln.ctypes.data))
 
+    def read_index(self, reqs) -> int:
+        """rg_read_index's staging on the CPU harness: [(group, slot, ctx), ...] (the caller validates)."""
+        self.L.ch_read_index.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64]
+        for g, s, ctx in reqs:
+            self.L.ch_read_index(C.c_void_p(self.h), g * self.R + s, ctx)
+        return 0
+
+    def read_ready(self, rid):
+        """[(ctx, index), ...] made ready for replica rid in the last tick."""
+        c, i = (C.c_uint64 * 8)(), (C.c_uint64 * 8)()
+        self.L.ch_read_ready.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint32]
+        n = self.L.ch_read_ready(C.c_void_p(self.h), rid, c, i, 8)
+        return [(c[k], i[k]) for k in range(n)]
+
     def config_change(self, group, slot, op, target) -> int:
         """rg_config_change's staging on the CPU harness (the caller validates)."""
         fn = self.L.ch_config_change

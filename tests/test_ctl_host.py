@@ -25,9 +25,10 @@ def inputs(rng, G, R, emax):
     return pt, pc, camp, iso
 
 
-def xcheck(kind, seed, G, R, T, p_cc=0.0, wire_all=0, **cfg):
+def xcheck(kind, seed, G, R, T, p_cc=0.0, wire_all=0, p_read=0.0, **cfg):
     """p_cc: per group and tick, the probability of a membership change. wire_all: the
-    control step reads every message from the remote inbox planes (the harness emulates the wire)."""
+    control step reads every message from the remote inbox planes (the harness emulates the wire).
+    p_read: per replica and tick, the probability of a ReadIndex request (the ready reads must match)."""
     kw = dict(groups=G, replicas=R, payload_bytes=16, max_entries_per_msg=8, log_capacity=64,
               snapshot_entries=20, compaction_overhead=5, drop_ppm=150000, seed=seed)
     kw.update(cfg)
@@ -40,12 +41,19 @@ def xcheck(kind, seed, G, R, T, p_cc=0.0, wire_all=0, **cfg):
             from test_oracle import random_ccs
             for c in random_ccs(rng, G, R, p_cc):
                 assert b.config_change(*c) == 0 and a.config_change(*c) == 0
+        if p_read:
+            from test_oracle import random_reads
+            reqs = random_reads(rng, G, R, t, p=p_read)
+            a.read_index(reqs)
+            b.read_index(reqs)
         ins = inputs(rng, G, R, kw["max_entries_per_msg"])
         a.tick(*ins)
         b.tick(*ins)
         for rid in range(G * R):
             vb = b.replica(rid)
             assert a.replica(rid) == vb, (seed, t, rid)
+            if p_read:
+                assert a.read_ready(rid) == b.read_ready(rid), (seed, t, rid)
             for d in range(R):
                 assert a.msgs(rid, d) == b.msgs(rid, d), (seed, t, rid, d)
             for i in range(vb["marker"] + 1, vb["last"] + 1):
@@ -109,6 +117,14 @@ def test_fast_path_covers_the_steady_state(R, P, wire):
             assert a.replica(rid) == b.replica(rid), (t, rid)
     assert b.replica(0)["snap_index"] > 0  # the run went through snapshots and compaction
     assert a.slow_lanes == slow0, a.slow_lanes - slow0
+
+
+@pytest.mark.parametrize("R,wire", [(1, 0), (3, 0), (5, 0), (3, 1), (5, 1)])
+@pytest.mark.parametrize("kind", ["ctl", "ctl-fast"])
+def test_control_step_read_index_queue(kind, R, wire):
+    """ReadIndex under chaos with up to RG_READ_QUEUE requests pending per leader (dragonboat's
+    readIndex queue): every state, message and ready read equals the oracle, local and remote inboxes."""
+    xcheck(kind, 70 + R, G=5, R=R, T=120, wire_all=wire, p_read=0.35, heartbeat_rtt=2)
 
 
 def test_control_step_heavy_loss():

@@ -181,7 +181,9 @@ def test_get_update_against_oracle():
         seen["committed"] += len(out["committed"])
         # snapshot events and ready reads
         evs = {int(x["rid"]): x for x in out["snapshots"]}
-        rds = {int(x["rid"]): x for x in out["reads"]}
+        rds = {}
+        for x in out["reads"]:
+            rds.setdefault(int(x["rid"]), []).append((int(x["ctx"]), int(x["index"])))
         for rid in range(G * R):
             kind, restored, index, term = ora.snapshot_event(rid)
             if rid in mine and kind:
@@ -192,7 +194,7 @@ def test_get_update_against_oracle():
                 assert rid not in evs, (t, rid)
             rr = ora.read_ready(rid)
             if rid in mine and rr:
-                assert (int(rds[rid]["ctx"]), int(rds[rid]["index"])) == rr, (t, rid)
+                assert rds[rid] == rr, (t, rid)
             else:
                 assert rid not in rds, (t, rid)
         seen["snapshots"] += len(evs)

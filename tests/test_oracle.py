@@ -291,9 +291,8 @@ def test_read_index_c_matches_python(seed):
                 assert a.msgs(rid, d) == b.msgs(rid, d), (seed, t, rid, d)
             ra = a.read_ready(rid)
             assert ra == b.read_ready(rid), (seed, t, rid)
-            if ra is not None:
-                ready += 1
-                assert ra[1] <= a.replica(rid)["committed"] or a.replica(rid)["role"] != 2
+            ready += len(ra)
+            assert all(ix <= a.replica(rid)["committed"] for _, ix in ra) or a.replica(rid)["role"] != 2
     assert ready > 0
 
 
@@ -422,7 +421,7 @@ def read_heartbeat_drop(o):
     assert o.replica(0)["role"] == 2
     assert o.read_index([(0, 0, 77)]) in (0, None)
     o.tick(isolate=np.array([0, 1, 1], np.uint8))
-    assert o.read_ready(0) is None
+    assert o.read_ready(0) == []
     hint = None
     for _ in range(6):
         o.tick()
@@ -430,7 +429,7 @@ def read_heartbeat_drop(o):
         if hb and hint is None:
             hint = hb[0]["hint"]
         r = o.read_ready(0)
-        if r is not None:
+        if r:
             assert hint == 77  # the regular heartbeat carried the ctx
             return r
     raise AssertionError("the read never became ready")
@@ -440,7 +439,42 @@ def read_heartbeat_drop(o):
 def test_read_index_survives_dropped_heartbeat(kind):
     o = make(kind, groups=1, replicas=3, payload_bytes=16, max_entries_per_msg=8, log_capacity=256,
              snapshot_entries=0, heartbeat_rtt=2, election_rtt=20)
-    assert read_heartbeat_drop(o)[0] == 77
+    assert [c for c, _ in read_heartbeat_drop(o)] == [77]
+
+
+def read_queue(o):
+    """dragonboat's readIndex queue: five reads reach the leader on consecutive ticks while both
+    followers are cut off, so no confirmation round completes. The first four queue up (RG_READ_QUEUE),
+    the fifth is dropped and counted. Once the followers are back, the next regular heartbeat carries
+    the newest pending ctx (readIndex.peepCtx); its confirmation releases that read and every read
+    queued before it, in arrival order, all at its index. Returns (ready reads, drops during the cut)."""
+    o.bootstrap()
+    o.tick()
+    o.tick(campaign=np.array([1, 0, 0], np.uint8))
+    for _ in range(5):
+        o.tick()
+    assert o.replica(0)["role"] == 2
+    d0 = o.replica(0)["drops"]
+    for k in range(5):
+        assert o.read_index([(0, 0, 100 + k)]) in (0, None)
+        o.tick(isolate=np.array([0, 1, 1], np.uint8))
+        assert o.read_ready(0) == []
+    drops = o.replica(0)["drops"] - d0
+    for _ in range(6):
+        o.tick()
+        r = o.read_ready(0)
+        if r:
+            return r, drops
+    raise AssertionError("the queued reads never became ready")
+
+
+@pytest.mark.parametrize("kind", ["c", "py", "ctl"])
+def test_read_index_queue(kind):
+    o = make(kind, groups=1, replicas=3, payload_bytes=16, max_entries_per_msg=8, log_capacity=256,
+             snapshot_entries=0, heartbeat_rtt=2, election_rtt=20)
+    r, drops = read_queue(o)
+    assert [c for c, _ in r] == [100, 101, 102, 103] and len({ix for _, ix in r}) == 1
+    assert drops >= 1  # the fifth request (messages to the cut-off followers may count too)
 
 
 def test_membership_scenario():
