@@ -81,3 +81,16 @@ def test_read_index_errors():
             gpu.read_index(bad)
     gpu.tick()
     assert gpu.read_ready_all() == {}
+
+
+def test_read_index_queue():
+    """dragonboat's readIndex queue on the device: four reads queue while the followers are cut off,
+    a fifth is dropped, and one confirmation releases the four in arrival order at one index — as the
+    oracle does (tests/test_oracle.py::read_queue)."""
+    from test_oracle import read_queue
+    cfg = dict(groups=1, replicas=3, payload_bytes=16, max_entries_per_msg=8, log_capacity=256, snapshot_entries=0,
+               heartbeat_rtt=2, election_rtt=20)
+    gpu, ora = make("gpu", **cfg), make("c", **cfg)
+    got = read_queue(gpu)
+    assert got == read_queue(ora) and [c for c, _ in got[0]] == [100, 101, 102, 103]
+    compare(gpu, ora, -1)
