@@ -1,12 +1,15 @@
 """The multi-tick path (rg_tick_device_n with RG_TICKN_GRAPH): k ticks captured as one
 HIP graph and replayed must equal k rg_tick_device calls bit for bit — every replica view, every
 outbox message and the newest log entries with payload — including ticks whose tick number matters
-(deterministic message loss, randomized election timeouts) and snapshots / compaction."""
+(deterministic message loss, randomized election timeouts) and snapshots / compaction. Both paths
+are also checked against the C oracle directly after every block of ticks (not only
+against single GPU ticks)."""
 import numpy as np
 import pytest
 import torch
 
 from engines import make
+from test_gpu_parity import check_payloads, compare
 
 pytestmark = pytest.mark.gpu
 
@@ -16,24 +19,29 @@ def test_graph_ticks_equal_single_ticks(payload):
     G, R, K = 64, 3, 8
     cfg = dict(groups=G, replicas=R, log_capacity=256, payload_bytes=payload, max_entries_per_msg=16,
                snapshot_entries=40, compaction_overhead=5, drop_ppm=20000, seed=0x6A)
-    a, b = make("gpu", **cfg), make("gpu", **cfg)
+    a, b, ora = make("gpu", **cfg), make("gpu", **cfg), make("c", **cfg)
     camp = np.zeros(G * R, np.uint8)
     camp[0::R] = 1
-    for e in (a, b):
+    for e in (a, b, ora):
         e.bootstrap()
         e.tick()
         e.tick(campaign=camp)
         for _ in range(4):
             e.tick()
-    pt = torch.tensor(np.random.default_rng(3).integers(0, R, G), dtype=torch.uint8, device="cuda")
-    pc = torch.tensor(np.random.default_rng(4).integers(1, 17, G), dtype=torch.int32, device="cuda")
+    pt_np = np.random.default_rng(3).integers(0, R, G).astype(np.uint8)
+    pc_np = np.random.default_rng(4).integers(1, 17, G).astype(np.uint32)
+    pt = torch.tensor(pt_np, dtype=torch.uint8, device="cuda")
+    pc = torch.tensor(pc_np.astype(np.int32), dtype=torch.int32, device="cuda")
     for rep in range(5):
         for _ in range(K):
             a.tick_device(pt.data_ptr(), pc.data_ptr())
+            ora.tick(pt_np, pc_np)
         b.tick_device_n(K, pt.data_ptr(), pc.data_ptr())
         a.sync()
         b.sync()
         assert a.t == b.t
+        compare(b, ora, (rep + 1) * K)  # the graph path against the oracle itself
+        check_payloads(b, ora)
         assert a.replica_array().tobytes() == b.replica_array().tobytes(), rep
         for rid in range(0, G * R, 7):
             for d in range(R):
@@ -70,20 +78,25 @@ def test_resident_ticks_equal_single_ticks(R):
     G, K = 100, 16
     cfg = dict(groups=G, replicas=R, log_capacity=128, payload_bytes=0, max_entries_per_msg=16,
                snapshot_entries=30, compaction_overhead=4, drop_ppm=30000, seed=0x7E5 + R)
-    a, b = make("gpu", **cfg), make("gpu", **cfg)
-    for e in (a, b):
+    a, b, ora = make("gpu", **cfg), make("gpu", **cfg), make("c", **cfg)
+    for e in (a, b, ora):
         e.bootstrap()
     rng = np.random.default_rng(R)
-    pt = torch.tensor(rng.integers(0, R, G), dtype=torch.uint8, device="cuda")
-    pc = torch.tensor(rng.integers(1, 9, G), dtype=torch.int32, device="cuda")
-    iso = torch.tensor((rng.random(G * R) < 0.02).astype(np.uint8), device="cuda")
+    pt_np = rng.integers(0, R, G).astype(np.uint8)
+    pc_np = rng.integers(1, 9, G).astype(np.uint32)
+    iso_np = (rng.random(G * R) < 0.02).astype(np.uint8)
+    pt = torch.tensor(pt_np, dtype=torch.uint8, device="cuda")
+    pc = torch.tensor(pc_np.astype(np.int32), dtype=torch.int32, device="cuda")
+    iso = torch.tensor(iso_np, device="cuda")
     for rep in range(6):
         for _ in range(K):
             a.tick_device(pt.data_ptr(), pc.data_ptr(), 0, iso.data_ptr())
+            ora.tick(pt_np, pc_np, isolate=iso_np)
         b.tick_device_n(K, pt.data_ptr(), pc.data_ptr(), 0, iso.data_ptr(), resident=True)
         a.sync()
         b.sync()
         assert a.t == b.t
+        compare(b, ora, (rep + 1) * K)  # the resident path against the oracle itself
         assert a.replica_array().tobytes() == b.replica_array().tobytes(), rep
         for rid in range(0, G * R, 11):
             for d in range(R):
