@@ -473,6 +473,8 @@ def pmc_traffic(kernel="bulk_kernel", wire=False, spread=False):
     wire — the launch shape of every rank at N > 1)."""
     def mode(f):
         b = os.path.basename(f)
+        if any(t in b for t in ("_c5", "_c2", "_c3", "_c4", "_shape")):
+            return "shape"  # another workload's profile (C2-C5 shapes): never the headline's traffic
         return "spread" if "_spread_" in b else "wire" if "_wire_" in b else "plain"
     want = "spread" if spread else "wire" if wire else "plain"
     files = [f for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_summary.json"))) if mode(f) == want]
