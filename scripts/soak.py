@@ -44,8 +44,23 @@ def draw(rng):
 def run(seed, ticks):
     rng = np.random.default_rng(seed)
     cfg = draw(rng)
+    # the engine under test: one engine (co-located planes), one engine with every message through the
+    # wire (wire_all), or 2-4 engines as ranks of one cluster moving regions by device copies
+    mode = str(rng.choice(["single", "wire_all", "ranks"], p=[0.45, 0.2, 0.35]))
+    if os.environ.get("SOAK_KIND"):
+        mode = "single"
+    ranks = int(rng.integers(2, 5)) if mode == "ranks" else 1
+    if mode == "ranks":
+        cfg["groups"] = max(ranks, cfg["groups"] // ranks * ranks)
+        if "pool_pages" in cfg:
+            cfg["pool_pages"] = cfg["groups"] * cfg["replicas"] * 64
+    if mode == "single":
+        gpu = make(os.environ.get("SOAK_KIND", "gpu"), **cfg)
+    else:
+        from raftd_amd.cluster import LoopbackCluster
+        gpu = LoopbackCluster(ranks=ranks, **dict(cfg, wire_all=1 if mode == "wire_all" else 0))
+    ora = make("c", **cfg)
     G, R, E, P = cfg["groups"], cfg["replicas"], cfg["max_entries_per_msg"], cfg["payload_bytes"]
-    gpu, ora = make(os.environ.get("SOAK_KIND", "gpu"), **cfg), make("c", **cfg)
     gpu.bootstrap()
     ora.bootstrap()
     p_caller, p_cc, p_read = rng.choice([0.0, 0.5, 1.0]), rng.choice([0.0, 0.03]), rng.choice([0.0, 0.2])
@@ -86,10 +101,10 @@ def run(seed, ticks):
             if t % 25 == 24:
                 check_payloads(gpu, ora)
         except AssertionError as ex:
-            print(f"MISMATCH seed {seed} cfg {cfg} p_caller {p_caller} p_cc {p_cc} p_read {p_read}\n{str(ex)[:3000]}",
+            print(f"MISMATCH seed {seed} mode {mode} ranks {ranks} cfg {cfg} p_caller {p_caller} p_cc {p_cc} p_read {p_read}\n{str(ex)[:3000]}",
                   flush=True)
             return False
-    print(f"seed {seed} ok: G {G} R {R} P {P} L {cfg['log_capacity']} E {E} K {cfg['max_msgs_per_pair']} "
+    print(f"seed {seed} ok: {mode} x{ranks} G {G} R {R} P {P} L {cfg['log_capacity']} E {E} K {cfg['max_msgs_per_pair']} "
           f"drop {cfg['drop_ppm']} caller {p_caller} cc {p_cc} reads {reads} maxc {maxc} "
           f"members {cfg.get('initial_members', 0)}", flush=True)
     return True
