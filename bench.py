@@ -11,8 +11,7 @@ slabs) are resident in HBM before the timed region.
 
 roofline: the dominant kernel is bulk_kernel (HBM-bound byte copies + CRC). achieved = its
 algorithmic bytes per launch (rg_traffic.bulk_bytes) / its mean launch duration, timed with HIP
-events recorded on the engine stream around its launches on one tick in ten of the timed region
-(at least two; profiles/r*_pmc_summary.json has the rocprofv3 average of the same command). With
+events recorded on the engine stream around every launch of the timed region. With
 --payload 0 there is no payload stage and the control kernel (the whole tick's algorithmic bytes)
 is reported instead.
 
@@ -46,13 +45,7 @@ METRIC = "raft group-steps/sec & commits/sec, 64K groups×3 replicas, 1/2/4/8 GP
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 XGMI_LINK_GBS = 153.0  # one xGMI link per GPU pair, 7 per GPU (≈153 GB/s each)
 CONTROL_TIMING_STEPS = 4
-TIMING_EVERY = 10  # bulk_kernel launches timed with events: at most one tick in ten of the timed region
-
-
-def timing_every(steps: int) -> int:
-    """Ticks between the timed bulk_kernel launches: one in TIMING_EVERY, and at least two samples in
-    the timed region (each timed tick costs ~0.17 ms of event overhead on this runtime, r04k)."""
-    return max(1, min(TIMING_EVERY, steps // 2))
+TIMING_EVERY = 4  # bulk_kernel launches timed with events: one tick in four of the timed region
 
 
 def parse():
@@ -587,11 +580,10 @@ def main():
                           pc.data_ptr() + 4 * (e.cfg["column_base"] * world if spread else 0))
         return sent
 
-    # the roofline kernel, live: HIP events around bulk_kernel on every `every`-th tick of the timed
-    # region (a timed tick costs ~0.17 ms of event overhead on this runtime: timing every tick made the
-    # step 8% slower, r03d; one in four 3.5 %, r04k / r05p)
-    every = timing_every(args.steps)
-    host.timing(True, bulk_only=True, every=every)
+    # the roofline kernel, live: HIP events around bulk_kernel on every TIMING_EVERY-th tick of the
+    # timed region (each timed event record costs its tick tens of µs on this runtime: timing every
+    # tick made the step 8% slower, r03d)
+    host.timing(True, bulk_only=True, every=TIMING_EVERY)
     wire_bytes = 0
     t0 = time.perf_counter()
     ev0.record(stream)
@@ -737,7 +729,7 @@ def main():
             "frac_of_box_copy_ceiling": achieved / copy_gbs if copy_gbs else None,
             "kernel_ms": rk_ms,
             "launches_timed": kms["bulk"][1],
-            "launches_timed_note": f"HIP events around bulk_kernel on every {every}th tick of the timed region",
+            "launches_timed_note": f"HIP events around bulk_kernel on every {TIMING_EVERY}th tick of the timed region",
             "per": "tick: bulk_kernel launches of every column half summed" if pipelined or (spread and args.halves > 1)
                    else "launch",
             "algorithmic_bytes_per_launch": rk_bytes,
