@@ -548,6 +548,13 @@ def main():
     bring_up(host, step.tick, Gt, R)
     pt = torch.zeros(Gt, dtype=torch.uint8, device="cuda")
     pc = torch.full((Gt,), E, dtype=torch.int32, device="cuda")  # read as uint32 by the kernel
+    # settle into the steady state before the warm-up steps: until every log ring has wrapped once
+    # (L / E ticks: the first pass writes ring slots and stream pages nothing has touched yet, and the
+    # first snapshots and compactions come on it). Measured (scripts/timing_probe.py, r05u): the first
+    # 20 ticks after bring-up run 1.352 ms each, later ones 1.294-1.300 ms
+    settle = min(64, args.log_capacity // max(E, 1) + 8)
+    for _ in range(settle):
+        step.tick_device(pt.data_ptr(), pc.data_ptr())
     for _ in range(max(args.warmup, 1)):
         step.tick_device(pt.data_ptr(), pc.data_ptr())
     traffic = host.last_tick_traffic()  # counts of a steady-state tick (outside the timed region)
@@ -692,6 +699,7 @@ def main():
         "ranks_share_one_gpu": bool(dist) and world > 1 and "RAFTD_BENCH_DEVICE" in os.environ,
         "steps": K,
         "warmup": args.warmup,
+        "settle_ticks": settle,  # steady-state ticks after bring-up, before the warm-up steps
         "ms_per_step": wall * 1e3 / K,
         "higher_is_better": True,
         "scaling": "weak",
