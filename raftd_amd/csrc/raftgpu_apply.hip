@@ -371,7 +371,7 @@ __global__ void read_count_kernel(SnapParams a) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= a.nrep) return;
   a.cnt[q] = ((a.slot_mask >> (q / a.G)) & 1u) && a.rdst[(uint64_t)RD_TICK * a.nrep + q] == a.tick
-                ? (uint32_t)a.rdst[(uint64_t)RD_N * a.nrep + q]
+                ? (uint32_t)min(a.rdst[(uint64_t)RD_N * a.nrep + q], (uint64_t)RG_RQ)
                 : 0u;
 }
 

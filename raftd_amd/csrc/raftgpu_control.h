@@ -810,7 +810,7 @@ struct Ctl {
     // attaches readIndex.peepCtx), so a lost read heartbeat or response is retried by the next round
     uint64_t ctx = 0;
     if (P().rdst) {
-      const uint64_t nq = P().rdst[(uint64_t)RQ_N * P().nrep + q];
+      const uint64_t nq = umin64(P().rdst[(uint64_t)RQ_N * P().nrep + q], RG_RQ);
       if (nq) ctx = P().rdst[(RQ_CTX + nq - 1) * (uint64_t)P().nrep + q];
     }
     if constexpr (FAST) {  // a pending read: its confirmation round is the full step's
@@ -1058,7 +1058,7 @@ struct Ctl {
   RG_FN void read_confirm(uint64_t hint, uint32_t f) {
     uint64_t* rd = P().rdst + q;
     const uint64_t n = P().nrep;
-    const uint32_t nq = (uint32_t)rd[RQ_N * n];
+    const uint32_t nq = (uint32_t)umin64(rd[RQ_N * n], RG_RQ);  // rows written only here: <= RG_RQ
     uint32_t k = 0;
     while (k < nq && rd[(RQ_CTX + k) * n] != hint) ++k;
     if (k == nq) return;
@@ -1085,7 +1085,7 @@ struct Ctl {
   RG_FN void read_ready(uint64_t ctx, uint64_t index) {  // addReadyToRead, at most RG_RQ per step
     uint64_t* rd = P().rdst + q;
     const uint64_t n = P().nrep;
-    uint64_t k = rd[RD_N * n];
+    uint64_t k = umin64(rd[RD_N * n], RG_RQ);
     if (rd[RD_TICK * n] != P().tick + 1) {  // the first read made ready in this step
       rd[RD_TICK * n] = P().tick + 1;
       k = 0;
@@ -1113,7 +1113,7 @@ struct Ctl {
       } else if (term_at(committed) != term) {
         drops++;  // nothing committed in this term yet (thesis §6.4)
       } else {
-        const uint32_t nq = (uint32_t)rd[RQ_N * n];
+        const uint32_t nq = (uint32_t)umin64(rd[RQ_N * n], RG_RQ);
         uint32_t k = 0;  // readIndex.addRequest: a context already pending is not added again
         while (k < nq && rd[(RQ_CTX + k) * n] != ctx) ++k;
         if (k == nq) {
