@@ -8,7 +8,7 @@ requests. After every tick the replica views, every outbox message, the log wind
 CRC) and the reads made ready must equal the oracle's; Cmd bytes are compared on sampled replicas.
 Stops at the first mismatch and prints the round's seed and configuration.
 
-usage: python scripts/soak.py [seconds] [first_seed]
+usage: python scripts/soak.py [seconds] [first_seed] [ticks per configuration, default 200]
 """
 import os
 import sys
@@ -113,9 +113,10 @@ def run(seed, ticks):
 def main():
     budget = float(sys.argv[1]) if len(sys.argv) > 1 else 300.0
     seed = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    ticks = int(sys.argv[3]) if len(sys.argv) > 3 else 200
     t0, n = time.time(), 0
     while time.time() - t0 < budget:
-        if not run(seed, 200):
+        if not run(seed, ticks):
             sys.exit(1)
         seed += 1
         n += 1
