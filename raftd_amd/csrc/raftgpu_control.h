@@ -32,6 +32,9 @@
 #endif
 
 // entries per load batch in the control kernel's term copies (write_entries, send_replicate)
+#ifndef RG_CTL_FULL_BATCH
+#define RG_CTL_FULL_BATCH 2
+#endif
 #ifndef RG_CTL_BATCH
 #define RG_CTL_BATCH 8
 #endif
@@ -141,7 +144,11 @@ using CTickParams = RG_CONST(const TickParams);
 // LAT (FAST only): the latency build for small engines (control_fastfb_kernel, the resident kernel:
 // a wave or less per SIMD, registers to spare) loads every field with the state up front instead of
 // copying the cold ones through at the end (one round trip fewer on the step's critical path).
-template <int R, bool FAST = false, int ROLE = -1, bool LAT = false>
+// SLIM (full step only): load batches of RG_CTL_FULL_BATCH entries instead of RG_CTL_BATCH — the
+// build of control_slow_kernel / control_kernel, whose live values then fit the register file (no
+// VGPR spills at R <= 5); the fallback inside control_fastfb_kernel keeps the wide batches (r05ac: the
+// narrow ones cost C2's fused launch ~2 µs, the storm's slow kernel nothing)
+template <int R, bool FAST = false, int ROLE = -1, bool LAT = false, bool SLIM = false>
 struct Ctl {
   static constexpr bool LEAN = FAST && !LAT;  // cold fields copied through at the end (register-lean)
   // the tick's parameter block, read in place at each use (a device slot the host filled): the
@@ -266,7 +273,8 @@ struct Ctl {
   }
 
   // entries per load batch (RG_CTL_BATCH); at R >= 7 the remote arrays leave room for half as many
-  static constexpr uint32_t CB = R >= 7 ? (RG_CTL_BATCH > 4 ? 4 : RG_CTL_BATCH) : RG_CTL_BATCH;
+  static constexpr uint32_t CB = SLIM ? RG_CTL_FULL_BATCH
+                                      : R >= 7 ? (RG_CTL_BATCH > 4 ? 4 : RG_CTL_BATCH) : RG_CTL_BATCH;
   RG_FN uint64_t ri() const { return (uint64_t)gi * R + RG_S_ID; }  // the replica's tick-input index
   RG_FN void abort_() { aborted = true; }  // FAST: leave the fast path (the full kernel re-runs the step)
   RG_FN uint32_t quorum() const { return (uint32_t)__builtin_popcount(members) / 2 + 1; }  // voting members

@@ -61,10 +61,10 @@ __global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_MINWAVES) control_kernel(
   if (q >= cp.nrep) return;
 #ifdef RG_CTL_PROFILE
   const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memtime();
-  Ctl<R> c(cp, q);
+  Ctl<R, false, -1, false, true> c(cp, q);
   c.stamps[0] = t0;
 #else
-  Ctl<R> c(cp, q);
+  Ctl<R, false, -1, false, true> c(cp, q);
 #endif
   c.run();
 }
@@ -168,9 +168,9 @@ __global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_MINWAVES) control_slow_ke
   CTickParams& cp = *(CTickParams*)pp;
   if (q >= cp.nrep || !RG_CTL_COL_OK(cp) || !cp.slow_flag[q]) return;
 #if defined(RG_AB_CTL2D) && !defined(RG_AB_CTL2D_Q)
-  Ctl<R> c(cp, blockIdx.y, blockIdx.x * blockDim.x + threadIdx.x);  // the slot a grid-uniform scalar
+  Ctl<R, false, -1, false, true> c(cp, blockIdx.y, blockIdx.x * blockDim.x + threadIdx.x);  // the slot a grid-uniform scalar
 #else  // RG_AB_CTL2D_Q: the 2-D launch, the slot derived from q (a per-lane value to the compiler)
-  Ctl<R> c(cp, q);
+  Ctl<R, false, -1, false, true> c(cp, q);
 #endif
   c.run();
 }

@@ -30,9 +30,11 @@ def make(kind: str, **cfg):
     if kind == "gpu":
         from raftd_amd.engine import Engine
         return Engine(**cfg)
-    if kind in ("ctl", "ctl-asan", "ctl-fast", "ctl-fast-asan", "ctl-fastlat", "ctl-fastlat-asan"):
+    if kind in ("ctl", "ctl-asan", "ctl-fast", "ctl-fast-asan", "ctl-fastlat", "ctl-fastlat-asan", "ctl-slim",
+                "ctl-slim-asan"):
         from native.ctl_host import CtlHost
-        return CtlHost(asan=kind.endswith("asan"), fast=2 if "fastlat" in kind else 1 if "fast" in kind else 0, **cfg)
+        fast = 3 if "slim" in kind else 2 if "fastlat" in kind else 1 if "fast" in kind else 0
+        return CtlHost(asan=kind.endswith("asan"), fast=fast, **cfg)
     raise ValueError(kind)
 
 

@@ -14,7 +14,8 @@
 using namespace rg;
 
 struct Host {
-  int fast = 0;             // ch_set_fast: the fast-path step first, the full step for a lane it hands off
+  int fast = 0;             // ch_set_fast: 1 / 2 the fast-path step first (2: its latency build), the full
+                            // step for a lane it hands off; 3 the full step's SLIM build (control_slow_kernel)
   uint64_t slow_lanes = 0;  // lanes the fast path handed off (all ticks)
   rg_config c;
   uint32_t nrep, J;
@@ -286,18 +287,21 @@ int ch_tick(void* hh, const rg_tick_input* in) {
   if (h->wire) emulate_wire(h, p);
   for (uint32_t q = 0; q < h->nrep; ++q) {
     switch (h->c.replicas) {
-#define RG_CASE(r)                 \
-  case r: {                        \
-    bool full = true;              \
-    if (h->fast) {                 \
-      full = fast_step<r>(h, p, q); \
-      h->slow_lanes += full;       \
-    }                              \
-    if (full) {                    \
-      Ctl<r> c(p, q);              \
-      c.run();                     \
-    }                              \
-    break;                         \
+#define RG_CASE(r)                                  \
+  case r: {                                         \
+    bool full = true;                               \
+    if (h->fast == 1 || h->fast == 2) {             \
+      full = fast_step<r>(h, p, q);                 \
+      h->slow_lanes += full;                        \
+    }                                               \
+    if (full && h->fast == 3) {                     \
+      Ctl<r, false, -1, false, true> c(p, q);       \
+      c.run();                                      \
+    } else if (full) {                              \
+      Ctl<r> c(p, q);                               \
+      c.run();                                      \
+    }                                               \
+    break;                                          \
   }
       RG_CASE(1) RG_CASE(2) RG_CASE(3) RG_CASE(4) RG_CASE(5) RG_CASE(6) RG_CASE(7) RG_CASE(8)
 #undef RG_CASE

@@ -65,14 +65,17 @@ def test_kernels_use_no_scratch():
 def test_full_step_keeps_its_pointers_out_of_spill_lanes():
     """The full control step (control_slow_kernel<R>, control_kernel<R>) reloads parameter-block
     fields at each use instead of hoisting ~45 base pointers into SGPRs for the whole step
-    (Ctl::P(), raftgpu_control.h): r04 spilled 429-459 SGPRs into VGPR lanes at R = 3 / 5."""
+    (Ctl::P(), raftgpu_control.h): r04 spilled 429-459 SGPRs into VGPR lanes at R = 3 / 5; and, with the
+    SLIM build's narrower load batches, no VGPR spills up to R = 7 (two remain at R = 8)."""
     from raftd_amd.build import kernel_resources
     res = kernel_resources()
     full = [k for k in res if "control_slow_kernel" in k or "control_kernel" in k]
     assert len(full) == 16
     for k in full:
-        assert int(res[k]["SGPRs Spill"]) < 128, (k, res[k]["SGPRs Spill"])
+        assert int(res[k]["SGPRs Spill"]) < 64, (k, res[k]["SGPRs Spill"])
         assert int(res[k]["ScratchSize [bytes/lane]"]) == 0, k
+        if "ILi8E" not in k:  # R <= 7: the SLIM build's live values fit the register file
+            assert int(res[k]["VGPRs Spill"]) == 0, (k, res[k]["VGPRs Spill"])
 
 
 def test_one_hip_runtime_per_process():

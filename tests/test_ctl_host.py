@@ -66,6 +66,13 @@ def test_control_step_matches_oracle(R):
     xcheck("ctl", 10 + R, G=5, R=R, T=120)
 
 
+@pytest.mark.parametrize("R,wire", [(3, 0), (5, 0), (8, 0), (3, 1), (5, 1)])
+def test_slim_full_step_matches_oracle(R, wire):
+    """The SLIM build of the full step (control_slow_kernel / control_kernel: narrower load batches)
+    under chaos, membership changes and reads, local and remote inboxes."""
+    xcheck("ctl-slim", 110 + R, G=5, R=R, T=120, wire_all=wire, p_cc=0.03 if R > 2 else 0.0, p_read=0.2)
+
+
 @pytest.mark.parametrize("R", [2, 3, 5, 8])
 @pytest.mark.parametrize("kind", ["ctl", "ctl-fast"])
 def test_control_step_over_the_wire_matches_oracle(kind, R):
@@ -167,6 +174,7 @@ def test_control_step_under_asan():
             "t.xcheck('ctl-fast-asan', 8, G=3, R=3, T=80, p_cc=0.05); t.xcheck('ctl-fast-asan', 9, G=2, R=5, T=60); "
             "t.xcheck('ctl-asan', 11, G=3, R=5, T=60, wire_all=1, p_cc=0.05); "
             "t.xcheck('ctl-fast-asan', 12, G=3, R=5, T=60, wire_all=1); t.xcheck('ctl-fast-asan', 13, G=2, R=8, T=60, wire_all=1); "
+            "t.xcheck('ctl-slim-asan', 14, G=3, R=5, T=60, p_cc=0.05, p_read=0.2); "
             "import kat_scenarios as K; fx = K.load('kat_check_msgapp.json'); "
             "[K.run_check_msgapp('ctl-asan', fx, c) for c in fx['cases']]; print('ASAN-CLEAN')"
             % (HERE, os.path.dirname(HERE)))
