@@ -149,23 +149,26 @@ def all_to_all_bytes(send, send_sizes, recv, recv_sizes, group=None, async_op=Fa
     return None
 
 
-def p2p_regions(send, send_sizes, recv, recv_sizes, group=None, async_op=False, chunk=A2A_CHUNK, send_offs=None):
+def p2p_regions(send, send_sizes, recv, recv_sizes, group=None, async_op=False, chunk=A2A_CHUNK, send_offs=None,
+                self_p2p=False):
     """The exchange's transfer on nccl, fixed or exactly sized: region r of `send` to rank r and region
     r of `recv` from rank r as one batch of point-to-point sends and receives (one grouped RCCL call),
     each piece at most `chunk` bytes (the 1 GiB contract). A link's two ends agree on its size, so
     they cut it into the same pieces without any rank knowing the others' sizes (an all_to_all's
     chunk count has to be the same on every rank). The region to this rank itself is a device copy.
     send_offs: the send regions' offsets in `send` when not consecutive (a region of 0 bytes to this
-    rank: it was packed in place, nothing to copy). nccl only; gloo ranks go through all_to_all_bytes."""
+    rank: it was packed in place, nothing to copy). self_p2p (tests): the region to this rank goes through
+    the same point-to-point pieces as the others, so a one-rank group runs the grouped path.
+    nccl only; gloo ranks go through all_to_all_bytes."""
     import torch.distributed as dist
     me, n = dist.get_rank(group), dist.get_world_size(group)
     so = list(send_offs) if send_offs is not None else _offsets(send_sizes)[0]
     ro, _ = _offsets(recv_sizes)
-    if send_sizes[me]:
+    if send_sizes[me] and not self_p2p:
         recv[ro[me]:ro[me] + recv_sizes[me]].copy_(send[so[me]:so[me] + send_sizes[me]])
     ops = []
     for r in range(n):
-        if r == me:
+        if r == me and not self_p2p:
             continue
         peer = dist.get_global_rank(group, r) if group is not None else r
         for lo in range(0, send_sizes[r], chunk):

@@ -9,7 +9,7 @@ sys.path[:0] = [HERE, os.path.dirname(HERE)]
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from raftd_amd.cluster import a2a_chunks, all_to_all_bytes, exchange_sizes  # noqa: E402
+from raftd_amd.cluster import a2a_chunks, all_to_all_bytes, exchange_sizes, p2p_regions  # noqa: E402
 
 torch.cuda.set_device(0)
 dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
@@ -29,5 +29,19 @@ for n, chunk, async_op in ((3_000_001, 1 << 20, False), (3_000_001, 1 << 20, Tru
     assert torch.equal(recv[:n], send[:n]) and bool((recv[n:] == 0).all()), (n, chunk, async_op)
     print(f"ok {n} bytes in {k} calls", flush=True)
     del send, recv
+# the exchange's point-to-point path (cluster.p2p_regions, what DistEngine runs on nccl at N > 1), its
+# region to this rank forced through isend / irecv pieces: a region laid out past the receive regions
+# (send_offs, as _Half packs them), ragged piece counts, sync and async
+for n, chunk, async_op in ((3_000_001, 1 << 20, False), (5_000_000, 1 << 21, True), (16, 1 << 20, False)):
+    base = torch.randint(0, 256, (2 * n + 4096,), dtype=torch.uint8, device="cuda")
+    so = ((n + 255) // 256 * 256 + 512,)  # the send region after the receive area
+    recv = base  # one buffer: receive regions at the front
+    want = base[so[0]:so[0] + n].clone()
+    h = p2p_regions(base, [n], recv, [n], async_op=async_op, chunk=chunk, send_offs=so, self_p2p=True)
+    if h is not None:
+        h.wait()
+    torch.cuda.synchronize()
+    assert torch.equal(recv[:n], want), (n, chunk, async_op)
+    print(f"ok p2p {n} bytes in pieces of {chunk}", flush=True)
 dist.destroy_process_group()
 print("a2a chunks ok", flush=True)

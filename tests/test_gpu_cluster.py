@@ -181,7 +181,9 @@ def test_one_rank_nccl_wire_halves():
 
 def test_chunked_exchange_rccl():
     """all_to_all_bytes through RCCL in pieces of at most A2A_CHUNK bytes per region: exact for
-    ragged, empty and 1.5 GB regions (a single RCCL call corrupted regions above 1 GiB)."""
+    ragged, empty and 1.5 GB regions (a single RCCL call corrupted regions above 1 GiB); and
+    p2p_regions' grouped isend / irecv pieces (DistEngine's N > 1 path) with the send region at its
+    own offset in the shared exchange buffer."""
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29536")
     out = subprocess.run([sys.executable, "-u", os.path.join(HERE, "a2a_worker.py")], env=env,
                          capture_output=True, text=True, timeout=300)
