@@ -251,8 +251,8 @@ class _Half:
     them and unpacks before the engine's next tick. With a C transport (exchange="c") start() is
     one rg_wire_exchange call, ordered on the device, and finish() has nothing left to do."""
 
-    def __init__(self, eng, dev, pg, rank, xt=None, fixed=True):
-        self.eng, self.pg, self.rank, self.xt, self.fixed = eng, pg, rank, xt, fixed
+    def __init__(self, eng, dev, pg, rank, xt=None, fixed=True, p2p_self=False):
+        self.eng, self.pg, self.rank, self.xt, self.fixed, self.p2p_self = eng, pg, rank, xt, fixed, p2p_self
         self.send, self.recv = _Buf(dev), _Buf(dev)  # nccl: self.recv holds both (send regions after the receive ones)
         self.work, self.rsizes, self.sent = None, None, 0
 
@@ -273,7 +273,7 @@ class _Half:
             rsizes, biggest = exchange_sizes(sizes, self.pg)
         ro, rtot = _offsets(rsizes)
         me = self.rank
-        if dist.get_backend(self.pg) == "nccl" and sizes[me] and sizes[me] == rsizes[me]:
+        if dist.get_backend(self.pg) == "nccl" and sizes[me] and sizes[me] == rsizes[me] and not self.p2p_self:
             # one buffer: the receive regions, then the send regions to the other ranks; the region to
             # this rank is packed where wire_recv reads it (no self copy; rg_wire_pack_at). Stream order:
             # the tick that read the old contents runs before the pack and the transfers
@@ -295,7 +295,8 @@ class _Half:
         e.wire_pack(self.send.ptr(), self.send.cap())
         self.recv.ensure(rtot)  # stream order: the tick that reads the old buffer runs before a reuse
         if dist.get_backend(self.pg) == "nccl":  # the region to this rank: a device copy, not RCCL
-            self.work = p2p_regions(self.send.t, sizes, self.recv.t, rsizes, self.pg, async_op=async_op)
+            self.work = p2p_regions(self.send.t, sizes, self.recv.t, rsizes, self.pg, async_op=async_op,
+                                    self_p2p=self.p2p_self)
         else:
             self.work = all_to_all_bytes(self.send.t, sizes, self.recv.t, rsizes, self.pg, async_op=async_op,
                                          nchunks=a2a_chunks(biggest))
@@ -356,14 +357,17 @@ class DistEngine(_Feeds):
     tick that produced it. With two halves, step_device() pipelines: while one half's all-to-all
     is on the wire, the other half unpacks, ticks and packs."""
 
-    def __init__(self, groups: int, group=None, halves: int = 1, exchange: str = "torch", fixed=None, **cfg):
+    def __init__(self, groups: int, group=None, halves: int = 1, exchange: str = "torch", fixed=None,
+                 p2p_self: bool = False, **cfg):
         """exchange: "torch" moves the regions with torch.distributed from Python; "c" with the
         library's rg_wire_exchange (RCCL transport on an nccl group, a host-staged one on gloo),
         each half on a stream of its own so one half's transfer overlaps the other's tick.
         fixed: size the regions with rg_wire_plan_fixed (no host sync, no size exchange: the all-to-all
         is the tick's one collective; a transfer moves each link's capacity, which follows its need,
         DESIGN.md §6) — the default — or, False, with rg_wire_plan (exact sizes after a host sync and a
-        size all-gather; on the C exchange through rg_config.wire_exact)."""
+        size all-gather; on the C exchange through rg_config.wire_exact).
+        p2p_self (tests): on nccl the region to this rank goes through the point-to-point pieces like
+        every other region, so a one-rank group runs the N > 1 transfer path."""
         import torch.distributed as dist
         torch = _torch()
         if groups % halves:
@@ -402,7 +406,7 @@ class DistEngine(_Feeds):
             else:
                 self._pyxt = gloo_transport(group, dev)
                 self.xt = self._pyxt.t
-        self.parts = [_Half(e, dev, self.pg, self.rank, self.xt, fixed=self.fixed) for e in engs]
+        self.parts = [_Half(e, dev, self.pg, self.rank, self.xt, fixed=self.fixed, p2p_self=p2p_self) for e in engs]
         self.eng = engs[0]
         self.cfg, self.R = engs[0].cfg, engs[0].R
         self.async_ok = dist.get_backend(group) == "nccl"

@@ -56,7 +56,9 @@ def worker(rank, n, halves, backend, exchange="torch"):
     from raftd_amd.cluster import DistEngine
     extra = dict(wire_all=1) if n == 1 else {}
     fixed = {"1": True, "0": False}.get(os.environ.get("DIST_FIXED", ""))  # sizing mode (None: the default)
-    de = DistEngine(groups=G_LOCAL * halves, halves=halves, device=0, exchange=exchange, fixed=fixed, **CFG, **extra)
+    p2p_self = os.environ.get("DIST_P2P_SELF") == "1"  # nccl, one rank: the region to self through p2p pieces
+    de = DistEngine(groups=G_LOCAL * halves, halves=halves, device=0, exchange=exchange, fixed=fixed,
+                    p2p_self=p2p_self, **CFG, **extra)
     if backend == "nccl":
         assert de.async_ok
     de.bootstrap()

@@ -168,11 +168,14 @@ def test_two_processes_gloo_halves():
     assert "dist parity ok" in out.stdout
 
 
-def test_one_rank_nccl_wire_halves():
+@pytest.mark.parametrize("p2p_self", [0, 1])
+def test_one_rank_nccl_wire_halves(p2p_self):
     """The RCCL path on the one GPU: a world-size-1 nccl group, every message through the wire,
     two column halves — plain ticks, then pipelined step_device ticks whose exchanges are
-    asynchronous RCCL all_to_all_single calls waited on by the engine stream."""
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29535")
+    asynchronous RCCL transfers waited on by the engine stream. p2p_self: the region to the rank
+    itself goes through the grouped isend / irecv pieces the N > 1 exchange uses (instead of being
+    packed in place), bit-exact with the oracle either way."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29535 + 40 * p2p_self), DIST_P2P_SELF=str(p2p_self))
     out = subprocess.run([sys.executable, "-u", os.path.join(HERE, "dist_worker.py"), "1", "2", "nccl"], env=env,
                          capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
