@@ -223,9 +223,14 @@ def test_control_step_under_msan():
         pytest.skip("no clang with MemorySanitizer")
     out = os.path.join(HERE, "native", "build", "ctl_msan")
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    subprocess.run([clang, "-fsanitize=memory", "-fsanitize-memory-track-origins=2", "-fno-omit-frame-pointer",
-                    "-O1", "-g", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
-                    os.path.join(HERE, "native", "ctl_msan.cpp"), "-o", out], check=True, timeout=900)
+    root = os.path.dirname(HERE)
+    deps = [os.path.join(HERE, "native", f) for f in ("ctl_msan.cpp", "ctl_host.cpp")] + \
+        [os.path.join(root, "raftd_amd", "csrc", f) for f in ("raftgpu_control.h", "raftgpu_internal.h")] + \
+        [os.path.join(root, "include", "raftgpu.h")]
+    if not os.path.exists(out) or any(os.path.getmtime(d) > os.path.getmtime(out) for d in deps):
+        subprocess.run([clang, "-fsanitize=memory", "-fsanitize-memory-track-origins=2", "-fno-omit-frame-pointer",
+                        "-O1", "-g", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+                        os.path.join(HERE, "native", "ctl_msan.cpp"), "-o", out], check=True, timeout=900)
     r = subprocess.run([out], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and "MSAN-CLEAN" in r.stdout, r.stderr[-3000:]
     probe = subprocess.run([out], capture_output=True, text=True, timeout=600, env=dict(os.environ, CTL_MSAN_PROBE="1"))
