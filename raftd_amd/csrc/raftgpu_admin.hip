@@ -184,6 +184,7 @@ __global__ void __launch_bounds__(256) scatter_replica_kernel(AdminParams a, uin
     s64[S_COMMITTED * N] = v.committed; s64[S_APPLIED * N] = v.applied; s64[S_LAST * N] = v.last;
     s64[S_MARKER * N] = v.marker; s64[S_MARKER_TERM * N] = v.marker_term; s64[S_SNAP_INDEX * N] = v.snap_index;
     s64[S_SNAP_TERM * N] = v.snap_term; s64[S_CAP_BASE * N] = v.cap_base; s64[S_PROCESSED * N] = v.processed;
+    s64[S_LAST_TERM * N] = v.last > v.marker ? words[v.last - v.marker - 1] & TERM_MASK : v.marker_term;
     s64[S_FIDX * N] = 0;
     s32[S_ROLE * N] = v.role; s32[S_ETICK * N] = v.election_tick; s32[S_HTICK * N] = v.heartbeat_tick;
     s32[S_RAND_TO * N] = v.rand_timeout; s32[S_RNG_CTR * N] = v.rng_ctr; s32[S_GRANTED * N] = v.granted;

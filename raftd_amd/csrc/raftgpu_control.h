@@ -241,7 +241,11 @@ struct Ctl {
       else rs[j] = P().rem_in[(2 * R + j) * n + q];
       rt[j] = P().rst_in[j * n + q];
     });
-    if (last > marker) lt_set(last, *tr_at(last) & TERM_MASK);  // issued early, used after the inbox headers
+#ifdef RG_AB_LAST_TERM_RING  // A/B variant: the term of `last` from the ring (r04)
+    if (last > marker) lt_set(last, *tr_at(last) & TERM_MASK);
+#else
+    if (last > marker) lt_set(last, a[S_LAST_TERM * n]);  // the state row: no ring read
+#endif
     last_start = last; sent_hi = 0; rw_lo = ~0ull; rw_hi = 0; marker_start = marker;
     processed_start = processed; restored_at = 0; wlo = ~0ull; took = false;
     if constexpr (FAST) {
@@ -1593,6 +1597,7 @@ struct Ctl {
     // compaction or a restore moved the marker: the stream below entry marker + 1 is released by the
     // next step, once this step's bulk kernel has stored that entry's position
     a[S_FIDX * n] = marker != marker_start ? marker + 1 : 0;
+    a[S_LAST_TERM * n] = last > marker ? (lt_i == last ? lt_v : *tr_at(last) & TERM_MASK) : marker_term;
     uint32_t* b = P().s32_out + q;
     b[S_ROLE * n] = role; b[S_ETICK * n] = etick; b[S_HTICK * n] = htick; b[S_RAND_TO * n] = rand_to;
     b[S_RNG_CTR * n] = rng_ctr; b[S_GRANTED * n] = granted; b[S_RESPONDED * n] = responded;

@@ -115,6 +115,8 @@ enum : uint32_t {
   S_SNAP_TERM, S_CAP_BASE, S_PROCESSED,
   S_CC_HI,  // highest index a ConfigChange entry was written to (the apply scan stops there)
   S_FIDX,   // compaction (or a restore) in the last step: the stream below this entry's position is free
+  S_LAST_TERM,  // the term of entry S_LAST (S_MARKER_TERM when the log is empty above the marker): the
+                // step's first term lookup without a ring read (one scattered line per replica at C5)
   S64_ROWS
 };
 enum : uint32_t {

@@ -279,6 +279,7 @@ __global__ void bootstrap_kernel(TickParams p, uint2* info) {
   const uint64_t last = joining ? 0 : R;
   a[S_TERM * n] = joining ? 0 : 1;  // becomeFollower(term, NoLeader): one reset
   a[S_LAST * n] = last;
+  a[S_LAST_TERM * n] = last ? 1 : 0;  // the bootstrap entries are at term 1
   a[S_COMMITTED * n] = last;
   a[S_CC_HI * n] = last;
   b[S_RNG_CTR * n] = 1;

@@ -155,6 +155,7 @@ void ch_bootstrap(void* hh) {  // = bootstrap_kernel
     for (uint32_t f = 0; f < S32_ROWS; ++f) h->s32[0][f * n + q] = 0;
     h->s64[0][S_TERM * n + q] = joining ? 0 : 1;
     h->s64[0][S_LAST * n + q] = last;
+    h->s64[0][S_LAST_TERM * n + q] = last ? 1 : 0;
     h->s64[0][S_COMMITTED * n + q] = last;
     h->s64[0][S_CC_HI * n + q] = last;
     h->s32[0][S_RNG_CTR * n + q] = 1;
@@ -459,6 +460,7 @@ int ch_import(void* hh, uint32_t rid, const rg_replica_view* v, const uint64_t* 
   s64[S_COMMITTED * N] = v->committed; s64[S_APPLIED * N] = v->applied; s64[S_LAST * N] = v->last;
   s64[S_MARKER * N] = v->marker; s64[S_MARKER_TERM * N] = v->marker_term; s64[S_SNAP_INDEX * N] = v->snap_index;
   s64[S_SNAP_TERM * N] = v->snap_term; s64[S_CAP_BASE * N] = v->cap_base; s64[S_PROCESSED * N] = v->processed;
+  s64[S_LAST_TERM * N] = v->last > v->marker ? terms[v->last - v->marker - 1] & TERM_MASK : v->marker_term;
   s32[S_ROLE * N] = v->role; s32[S_ETICK * N] = v->election_tick; s32[S_HTICK * N] = v->heartbeat_tick;
   s32[S_RAND_TO * N] = v->rand_timeout; s32[S_RNG_CTR * N] = v->rng_ctr; s32[S_GRANTED * N] = v->granted;
   s32[S_RESPONDED * N] = v->responded; s32[S_ACTIVE * N] = v->active; s32[S_ERR * N] = v->err;

@@ -26,11 +26,15 @@ def build(asan: bool = False) -> str:
             os.path.join(ROOT, "raftd_amd", "csrc", "raftgpu_internal.h"), os.path.join(ROOT, "include", "raftgpu.h")]
     if os.path.exists(lib) and all(os.path.getmtime(d) <= os.path.getmtime(lib) for d in deps):
         return lib
+    # build into a private file and rename it into place: parallel test workers (pytest -n) that find
+    # the library stale at the same time never load one another's half-written output
+    tmp = f"{lib}.{os.getpid()}.tmp"
     cmd = ["g++", "-O1" if asan else "-O2", "-g", "-std=c++17", "-fPIC", "-shared", "-D__HIP_PLATFORM_AMD__",
-           "-I/opt/rocm/include", *extra, src, "-o", lib]
+           "-I/opt/rocm/include", *extra, src, "-o", tmp]
     if asan:
         cmd[1:1] = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"]
     subprocess.run(cmd, check=True)
+    os.replace(tmp, lib)
     return lib
 
 
