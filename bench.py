@@ -18,8 +18,9 @@ is reported instead.
 N > 1 (default --placement spread, the north star's layout): one process per GPU
 (torch.distributed.run), N x 65,536 groups, replica slot s of group g on GPU (g mod N + off(s)) mod N
 (DESIGN.md §6), so every replica of a group sits on a different GPU, emulating separate nodes.
-Each step = the exchange of the previous tick's cross-GPU messages (plan/pack kernels, one RCCL
-all_to_all_single over xGMI — the only collective — and the unpack kernel) + the tick; with
+Each step = the exchange of the previous tick's cross-GPU messages (plan/pack kernels, one grouped
+RCCL send/recv per peer over xGMI — an all-to-all, the only collective — and the unpack kernel) + the
+tick (the line's `parallelism` / exchange.transport name the transport that ran); with
 --halves 2 (default) each GPU's columns are two engines whose exchanges are pipelined behind each
 other's ticks. Every GPU
 hosts 196,608 replicas, as at N = 1 (weak scaling). --placement colocated keeps every replica of
@@ -81,6 +82,31 @@ def parse():
     ap.add_argument("--dry-run", action="store_true", help="N > 1 launcher check: every rank joins the process "
                     "group on the CPU (gloo), agrees on the world size and exits without touching a GPU")
     return ap.parse_args()
+
+
+def exchange_transport(spread: bool, wire_all: bool, exchange: str, backend: str, fixed: bool):
+    """How the N > 1 step moves its regions, in the words the line's `parallelism` label and
+    `exchange.transport` both use (the label must name the transport that actually ran)."""
+    if not spread:
+        return "device copy (one engine)" if wire_all else None
+    sizing = ("fixed-capacity regions (no host sync, no size exchange)" if fixed
+              else "exactly sized regions (plan host sync + size all-gather)")
+    if exchange == "c":
+        how = ("rg_wire_exchange (C-ABI) with its built-in RCCL transport: one grouped ncclSend / ncclRecv per peer"
+               if backend == "nccl" else "rg_wire_exchange (C-ABI) over a host-staged gloo transport")
+    else:
+        how = ("torch.distributed batch_isend_irecv: one grouped RCCL send / recv per peer" if backend == "nccl"
+               else "torch.distributed all_to_all over gloo, staged through host memory")
+    return f"{how}, {sizing}"
+
+
+def xgmi_bound_ms(bytes_per_step_max_rank: float, world: int):
+    """The per-tick floor the exchange puts on an N-GPU step: the busiest rank's outbound bytes over its
+    N - 1 direct xGMI links (one per peer on an 8-GPU node, XGMI_LINK_GBS each way), the placement
+    spreading a rank's traffic evenly over its peers. None at N = 1 (no link)."""
+    if world < 2:
+        return None
+    return bytes_per_step_max_rank / (min(world - 1, 7) * XGMI_LINK_GBS * 1e9) * 1e3
 
 
 def _free_port() -> int:
@@ -369,7 +395,8 @@ def hand_off(eng, tick, G, steps, slot_mask=1):
             "entry_rows_per_step": ne / steps, "payload_bytes_per_step": nb / steps,
             "note": "tick + rg_get_update(UPDATE_ALL, slot mask 1) + rg_commit_update(RG_COMMIT_APPLIED) per step: "
                     "the single GetUpdate / Commit hand-off (the slot-0 replicas' states, entries to persist as term "
-                    "runs + {len, crc}, committed entries as runs, snapshots, reads), sections read in place from pinned memory; "
+                    "runs + {len, crc} with their Cmds, committed entries as runs + {len, crc} by reference to those "
+                    "Cmds (each Cmd crosses PCIe once), snapshots, reads), sections read in place from pinned memory; "
                     "PCIe-bound at full batches"}
 
 
@@ -590,6 +617,9 @@ def main():
     # the roofline kernel, live: HIP events around bulk_kernel on every TIMING_EVERY-th tick of the
     # timed region (each timed event record costs its tick tens of µs on this runtime: timing every
     # tick made the step 8% slower, r03d)
+    if spread:  # the halves' bulk launches on one timeline: their span per tick (DistEngine.kernel_span_ms)
+        from raftd_amd.engine import timing_epoch
+        timing_epoch(local)
     host.timing(True, bulk_only=True, every=TIMING_EVERY)
     wire_bytes = 0
     t0 = time.perf_counter()
@@ -607,6 +637,7 @@ def main():
     wall = time.perf_counter() - t0
     dev_ms = ev0.elapsed_time(ev1)
     kms = host.kernel_ms()
+    span = host.kernel_span_ms("bulk") if spread else None
     c1 = host.sum_committed()  # before the control-timing steps below
     # control_kernel duration from a few more steps after the timed region (timing both kernels
     # adds two event records per tick, which the timed region does without)
@@ -665,10 +696,12 @@ def main():
         return
     K = args.steps
     group_steps = world * G * K / wall
+    transport = exchange_transport(spread, bool(args.wire_all), args.exchange, args.backend if dist else "none",
+                                   bool(wire.fixed) if spread else True)
     if spread:
         par = (f"{world * G} groups; replica slot s of group g on GPU (g mod {world} + off(s, g div {world})) mod "
                f"{world}, every replica of a group on its own GPU, followers spread evenly over the peers; "
-               f"cross-GPU messages by one RCCL all_to_all_single per tick"
+               f"cross-GPU messages once per tick by {transport}"
                + (f" and column half ({args.halves} halves per GPU, exchange pipelined behind the other half's tick)"
                   if args.halves > 1 else "")
                + (" [rehearsal: one rank, every message through the wire to itself]" if rehearse else ""))
@@ -677,6 +710,9 @@ def main():
     else:
         par = f"groups sharded over {world} GPU(s), replicas co-located (no exchange)"
     bulk_ms = kms["bulk"][0] / max(kms["bulk"][1], 1)
+    bulk_sum_ms = bulk_ms
+    if span and span[1]:  # column halves: the span of their launches per tick, not the sum of the durations
+        bulk_ms = span[0] / span[1]
     ctl_ms = kms["control"][0] / max(kms["control"][1], 1)
     # metadata-only (P = 0): no payload stage is launched, the control kernel is the tick
     meta_only = kms["bulk"][1] == 0
@@ -738,8 +774,9 @@ def main():
             "kernel_ms": rk_ms,
             "launches_timed": kms["bulk"][1],
             "launches_timed_note": f"HIP events around bulk_kernel on every {TIMING_EVERY}th tick of the timed region",
-            "per": "tick: bulk_kernel launches of every column half summed" if pipelined or (spread and args.halves > 1)
-                   else "launch",
+            "per": ("tick: wall-clock span of the column halves' bulk_kernel launches (first start to last end on "
+                    "one timeline, rg_timing_epoch)") if spread and args.halves > 1 else "launch",
+            "bulk_ms_summed_over_halves": bulk_sum_ms if spread and args.halves > 1 else None,
             "algorithmic_bytes_per_launch": rk_bytes,
             "tick_algorithmic_bytes": traffic["algorithmic_bytes"],
             "tick_counts": {k: v for k, v in traffic.items() if k not in ("algorithmic_bytes", "bulk_bytes")},
@@ -755,15 +792,12 @@ def main():
             "mode": (f"pipelined over {args.halves} column halves: one half's all-to-all overlaps the other's "
                      "unpack + tick + pack" if pipelined else "serial: plan + pack + all-to-all + unpack, then tick"),
             "ms_per_step": x_ms if not pipelined else None,
-            "transport": ("rg_wire_exchange (C-ABI, built-in RCCL transport; " +
-                          ("fixed-capacity regions, one collective)" if wire.fixed
-                           else "exactly sized regions, plan host sync + size all-gather)")
-                          if spread and args.exchange == "c"
-                          else ("torch.distributed batch_isend_irecv of fixed-capacity regions (no host sync, no "
-                                "size exchange)" if wire.fixed else "torch.distributed batch_isend_irecv of "
-                                "exactly sized regions (plan host sync + size all-gather)") if spread
-                          else "device copy (one engine)"),
+            "transport": transport,
             "bytes_sent_per_step_max_rank": wire_max / K,
+            "bound_ms": xgmi_bound_ms(wire_max / K, world),
+            "bound_note": "the busiest rank's outbound bytes per step / ((N - 1) xGMI links x "
+                          f"{XGMI_LINK_GBS:.0f} GB/s), traffic spread evenly over the peers (DESIGN.md §6); "
+                          "a step at N > 1 cannot be shorter. None at N = 1",
             "achieved_GBps_per_rank": ((wire_max / K) / (x_ms / 1e3) / 1e9 if x_ms > 0 else
                                        (wire_max / K) / (wall / K) / 1e9),
             "xgmi_peak_GBps_per_rank": min(max(world - 1, 1), 7) * XGMI_LINK_GBS,

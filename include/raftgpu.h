@@ -363,6 +363,15 @@ int rg_timing(rg_engine* e, int enable);
 /* Synchronises, then returns the summed durations (ms) and launch counts since rg_timing(e, 1):
  * index 0 = control_kernel, 1 = bulk_kernel. */
 int rg_kernel_ms(rg_engine* e, double* ms /*[2]*/, uint64_t* launches /*[2]*/);
+/* Measurement across engines (column halves on their own streams): rg_timing_epoch records one
+ * process-wide reference event on `device` (and waits for it); from then on every timed launch of
+ * every engine on that device is also kept as {tick, start, end} in ms after the epoch, so launches
+ * on different streams can be laid on one timeline (the span of overlapping launches, not the sum
+ * of their durations). rg_kernel_events returns up to cap of the kernel's (0 control, 1 bulk)
+ * launches since rg_timing(e, on); *n = how many there are. Synchronises like rg_kernel_ms. */
+int rg_timing_epoch(int device);
+int rg_kernel_events(rg_engine* e, int kernel, uint64_t* ticks, double* start_ms, double* end_ms, uint64_t cap,
+                     uint64_t* n);
 uint64_t rg_tick_count(const rg_engine* e);
 
 int rg_read_replicas(rg_engine* e, uint32_t first_rid, uint32_t n, rg_replica_view* out);
@@ -479,8 +488,9 @@ int rg_apply_committed(rg_engine* e, uint32_t slot_mask, rg_apply_batch* out);
  * reuse the window's log slots and pages): the count and scan kernels, then ONE host synchronisation
  * for the batch's size (the buffers grow when it exceeds them), then the gather kernel into device
  * staging. The D2H leg then runs on the engine's copy stream — a copy kernel of a few workgroups
- * streaming into host-mapped memory (default), the runtime's hipMemcpyAsync
- * (RAFTGPU_APPLY_MEMCPY=1) or an SDMA engine (RAFTGPU_APPLY_SDMA=1) — so the caller may issue the
+ * streaming into host-mapped memory (default), or an SDMA engine (RAFTGPU_APPLY_SDMA=1, the only
+ * runtime hook of the copy-back; the runtime's hipMemcpyAsync is the -DRG_AB_APPLY_MEMCPY build
+ * variant) — so the caller may issue the
  * next tick before it completes. Whether that overlap pays depends on the platform (DESIGN.md §7,
  * INTEGRATION.md "Copy-back schedule"). */
 int rg_apply_async(rg_engine* e, uint32_t slot_mask, int buf);
@@ -513,6 +523,17 @@ int rg_snapshot_events(rg_engine* e, uint32_t slot_mask, rg_snapshot_event* even
 #define RG_UPDATE_READS 8u       /* ReadyToReads (rg_read_index_results) */
 #define RG_UPDATE_ALL 15u
 #define RG_UPDATE_FULL_STATE 16u /* persistence section: every replica, whole log window */
+/* With RG_UPDATE_PERSIST and RG_UPDATE_COMMITTED together the committed section is BY REFERENCE:
+ * runs and {len, crc} only, committed.payload = NULL and payload_bytes = 0. Every committed entry's Cmd
+ * was delivered in this or an earlier persist section of the same replicas (a replica commits only
+ * what it has in its log, and its log writes are persisted in the update of the tick that made them);
+ * the host keeps persisted Cmds until the replica has applied them — dragonboat hands Update its
+ * entries from its own in-memory log the same way. Entry k of a run is its replica's persisted entry
+ * r.first + k; r.off is where its Cmd would sit in a packed payload. Each Cmd then crosses PCIe once
+ * per hand-off stream. Entries of rg_import_replica never pass through a persist section: a host that
+ * imports keeps their Cmds itself (it read them from its WAL). RG_UPDATE_COMMITTED_CMDS ships the Cmds
+ * anyway (and rg_apply_committed / rg_apply_async always do). */
+#define RG_UPDATE_COMMITTED_CMDS 32u
 typedef struct rg_update {
   uint64_t tick;                          /* ticks run when the update was taken */
   rg_persist_batch persist;               /* states, entries, term runs, Cmds (rg_persist_batch) */

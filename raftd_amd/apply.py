@@ -1,7 +1,9 @@
 """raftd's apply path above the engine: committed entries → POST /UpdateEntries.
 
-After every tick the engine copies back only what was newly committed (rg_apply_committed: one
-hipMemcpyAsync per array of the entries each replica applied in the tick). This module turns that
+After every tick the engine copies back only what was newly committed (rg_apply_committed /
+rg_apply_async: count, scan and gather kernels compact the entries each replica applied in the tick
+into runs + {len, crc} + packed Cmds in device staging, and a copy kernel streams that batch into
+host-mapped pinned memory; RAFTGPU_APPLY_SDMA=1 moves it with an SDMA engine instead). This module turns that
 batch into the requests raftd's OnDiskStateMachine makes, byte for byte:
 
 - ``Update`` (/root/reference/raft/state_machine.go:136-166) marshals

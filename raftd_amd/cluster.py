@@ -573,6 +573,19 @@ class DistEngine(_Feeds):
         ks = [p.eng.kernel_ms() for p in self.parts]
         return {k: (sum(x[k][0] for x in ks), ks[0][k][1]) for k in ks[0]}
 
+    def kernel_span_ms(self, kernel: str = "bulk"):
+        """The kernel's wall-clock span per tick over the halves — first launch start to last launch end
+        of the same tick on the epoch timeline (rg_timing_epoch before timing(True)) — summed over the
+        ticks every half timed, and their count. Halves on streams of their own overlap, so the sum of
+        their launch durations overstates the time the tick spent in the kernel; the span does not."""
+        per = {}
+        for p in self.parts:
+            ticks, a, b = p.eng.kernel_events(kernel)
+            for t, x, y in zip(ticks.tolist(), a.tolist(), b.tolist()):
+                per.setdefault(t, []).append((x, y))
+        spans = [max(y for _, y in v) - min(x for x, _ in v) for v in per.values() if len(v) == len(self.parts)]
+        return sum(spans), len(spans)
+
     def last_tick_traffic(self) -> dict:
         ts = [p.eng.last_tick_traffic() for p in self.parts]
         return {k: sum(t[k] for t in ts) for k in ts[0]}

@@ -21,8 +21,8 @@ __global__ void gather_replicas_kernel(AdminParams a, uint32_t first, uint32_t n
   const uint32_t q = q_of(t, first + i);
   const uint64_t N = t.nrep;
   rg_replica_view v;
-  const uint64_t* s64 = t.s64_in + q;
-  const uint32_t* s32 = t.s32_in + q;
+  const uint64_t* s64 = t.s64 + q;
+  const uint32_t* s32 = t.s32 + q;
   v.term = s64[S_TERM * N]; v.vote = s64[S_VOTE * N]; v.leader = s64[S_LEADER * N];
   v.committed = s64[S_COMMITTED * N]; v.applied = s64[S_APPLIED * N]; v.last = s64[S_LAST * N];
   v.marker = s64[S_MARKER * N]; v.marker_term = s64[S_MARKER_TERM * N]; v.snap_index = s64[S_SNAP_INDEX * N];
@@ -36,10 +36,10 @@ __global__ void gather_replicas_kernel(AdminParams a, uint32_t first, uint32_t n
   v._mpad = 0;
   for (uint32_t j = 0; j < RG_MAX_REPLICAS; ++j) {
     const bool in = j < t.R;
-    v.match[j] = in ? t.rem_in[(0 * t.R + j) * N + q] : 0;
-    v.next[j] = in ? t.rem_in[(1 * t.R + j) * N + q] : 0;
-    v.rsnap[j] = in ? t.rem_in[(2 * t.R + j) * N + q] : 0;
-    v.rstate[j] = in ? t.rst_in[j * N + q] : 0;
+    v.match[j] = in ? t.rem[(0 * t.R + j) * N + q] : 0;
+    v.next[j] = in ? t.rem[(1 * t.R + j) * N + q] : 0;
+    v.rsnap[j] = in ? t.rem[(2 * t.R + j) * N + q] : 0;
+    v.rstate[j] = in ? t.rst[j * N + q] : 0;
   }
   out[i] = v;
 }
@@ -144,8 +144,8 @@ __global__ void __launch_bounds__(256) scatter_replica_kernel(AdminParams a, uin
   const uint32_t q = q_of(t, rid);
   const uint64_t N = t.nrep;
   const rg_replica_view& v = *vv;
-  uint32_t* s32 = ((uint32_t*)(t.s32_in)) + q;
-  uint64_t* s64 = ((uint64_t*)(t.s64_in)) + q;
+  uint32_t* s32 = ((uint32_t*)(t.s32)) + q;
+  uint64_t* s64 = ((uint64_t*)(t.s64)) + q;
   __shared__ uint32_t ok;
   const uint32_t np = t.P ? vpn_ceil(nch) : 0u;
   if (threadIdx.x == 0) {
@@ -192,8 +192,8 @@ __global__ void __launch_bounds__(256) scatter_replica_kernel(AdminParams a, uin
     s32[S_DROPS * N] = v.drops;
     s32[S_MEMBERS * N] = v.members; s32[S_SNAP_MEMBERS * N] = v.snap_members; s32[S_CC_PENDING * N] = v.cc_pending;
     s64[S_CC_HI * N] = v.last;  // any imported entry may be a ConfigChange
-    uint64_t* rem = ((uint64_t*)(t.rem_in));
-    uint8_t* rst = ((uint8_t*)(t.rst_in));
+    uint64_t* rem = ((uint64_t*)(t.rem));
+    uint8_t* rst = ((uint8_t*)(t.rst));
     for (uint32_t j = 0; j < t.R; ++j) {
       rem[(0 * t.R + j) * N + q] = v.match[j];
       rem[(1 * t.R + j) * N + q] = v.next[j];
@@ -259,7 +259,7 @@ __global__ void notify_applied_kernel(AdminParams a, const uint32_t* rids, const
     return;
   }
   const uint64_t q = q_of(t, rids[i]), N = t.nrep;
-  uint64_t* s64 = ((uint64_t*)(t.s64_in)) + q;
+  uint64_t* s64 = ((uint64_t*)(t.s64)) + q;
   if (pass == 0) {
     if (index[i] > s64[S_PROCESSED * N]) atomicAdd(bad, 1u);
   } else {
@@ -268,14 +268,14 @@ __global__ void notify_applied_kernel(AdminParams a, const uint32_t* rids, const
 }
 
 // rg_compact: a lane per slot of the shard. Between ticks the next step's input state is
-// s64_in; the marker moves there as a snapshot's compaction moves it at the end of a step, and S_FIDX
+// s64; the marker moves there as a snapshot's compaction moves it at the end of a step, and S_FIDX
 // makes the next step release the payload stream below entry c + 1 ("Release")
 __global__ void compact_kernel(AdminParams a, uint64_t group, uint64_t index, uint32_t* n) {
   const uint32_t s = threadIdx.x;
   const TickParams& t = a.t;
   if (s >= t.R || pl_rank_of(t.pl, group, s) != t.pl.rank) return;
   const uint64_t j = group / t.pl.N - t.pl.col_base, q = (uint64_t)s * t.G + j, N = t.nrep;
-  uint64_t* s64 = ((uint64_t*)(t.s64_in)) + q;
+  uint64_t* s64 = ((uint64_t*)(t.s64)) + q;
   const uint64_t marker = s64[S_MARKER * N], snap = s64[S_SNAP_INDEX * N];
   const uint64_t c = index < snap ? index : snap;  // snap <= applied <= committed <= last: c is in the ring
   if (c <= marker) return;
@@ -315,8 +315,8 @@ __global__ void __launch_bounds__(256) digest_kernel(AdminParams a, unsigned lon
   for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < N; q += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t s = (uint32_t)(q / t.G), g = (uint32_t)(q - (uint64_t)s * t.G);
     const uint64_t gid = pl_group(t.pl, s, g) * t.R + s;
-    const uint64_t* s64 = t.s64_in + q;
-    const uint32_t* s32 = t.s32_in + q;
+    const uint64_t* s64 = t.s64 + q;
+    const uint32_t* s32 = t.s32 + q;
     uint64_t h = dg_mix(gid + 0x9E3779B97F4A7C15ULL);
     for (uint32_t k = 0; k <= S_PROCESSED; ++k) {  // term .. processed, in rg_replica_view order
       const uint32_t row = k <= S_CAP_BASE ? k : S_PROCESSED;
@@ -330,10 +330,10 @@ __global__ void __launch_bounds__(256) digest_kernel(AdminParams a, unsigned lon
       h = dg_mix(h ^ x);
     }
     for (uint32_t j = 0; j < t.R; ++j) {
-      h = dg_mix(h ^ t.rem_in[(0 * t.R + j) * N + q]);
-      h = dg_mix(h ^ t.rem_in[(1 * t.R + j) * N + q]);
-      h = dg_mix(h ^ t.rem_in[(2 * t.R + j) * N + q]);
-      h = dg_mix(h ^ t.rst_in[j * N + q]);
+      h = dg_mix(h ^ t.rem[(0 * t.R + j) * N + q]);
+      h = dg_mix(h ^ t.rem[(1 * t.R + j) * N + q]);
+      h = dg_mix(h ^ t.rem[(2 * t.R + j) * N + q]);
+      h = dg_mix(h ^ t.rst[j * N + q]);
     }
     sa += h;
     const uint64_t marker = s64[S_MARKER * N], last = s64[S_LAST * N];
@@ -372,7 +372,7 @@ __global__ void applied_all_kernel(AdminParams a, uint32_t slot_mask) {
   const TickParams& t = a.t;
   const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, N = t.nrep;
   if (q >= N || !((slot_mask >> (q / t.G)) & 1u)) return;
-  uint64_t* s64 = ((uint64_t*)(t.s64_in)) + q;
+  uint64_t* s64 = ((uint64_t*)(t.s64)) + q;
   s64[S_APPLIED * N] = s64[S_PROCESSED * N];
 }
 

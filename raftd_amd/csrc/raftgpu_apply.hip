@@ -142,7 +142,7 @@ __global__ void __launch_bounds__(256) apply_gather_kernel(ApplyParams a) {
       }
     }
     const uint32_t total = (uint32_t)__shfl((int)inc, 63, 64);
-    copy_run(a.pool, a.pt, a.PTS, q, inc, inf.y, total, a.out_pay, cpos);
+    if (a.out_pay) copy_run(a.pool, a.pt, a.PTS, q, inc, inf.y, total, a.out_pay, cpos);
     pos += __builtin_popcountll(mask);
     rpos += __builtin_popcountll(heads);
     cpos += total;
@@ -197,9 +197,8 @@ __global__ void persist_count_kernel(PersistParams a) {
   const uint64_t n = a.nrep;
   const uint64_t last = a.s64[(uint64_t)S_LAST * n + q], lo = persist_first(a, q);
   const uint32_t ne = lo <= last ? (uint32_t)(last - lo + 1) : 0u;
-  const auto diff = [&](uint32_t f) { return a.s64[(uint64_t)f * n + q] != a.s64_prev[(uint64_t)f * n + q]; };
-  const bool changed = a.full || ne > 0 || diff(S_TERM) || diff(S_VOTE) || diff(S_COMMITTED) || diff(S_LAST) ||
-                       diff(S_MARKER) || diff(S_SNAP_INDEX);
+  // the step recorded whether it wrote entries or changed the hard state (no previous state to diff)
+  const bool changed = a.full || ne > 0 || a.persist_lo[q] != PERSIST_NONE;
   uint32_t cc = 0, tc = 0;
   uint64_t pt = ~0ull;
   for (uint64_t i = lo; i <= last; ++i) {

@@ -56,6 +56,16 @@
 #endif
 
 namespace rg {
+#ifdef RG_X1
+#define RGX(c) true
+#else
+#define RGX(c) (c)
+#endif
+#ifdef RG_X2
+#define RGX2(c) true
+#else
+#define RGX2(c) (c)
+#endif
 
 RG_FN uint64_t mix64(uint64_t z) {
   z ^= z >> 30;
@@ -82,6 +92,13 @@ RG_FN void sfor(F&& f) {
 // move (Ctl::slot_lane), so the compiler treats it as per-lane there (the fault)
 #ifndef RG_CTL_RELOAD_FAST
 #define RG_CTL_RELOAD_FAST 0
+#endif
+// the large-engine fast step (LEAN) reloads the parameter fields too: with the state updated in place
+// its hoisted pointers pushed control_fast_kernel<3> past 168 VGPRs (58 spilled to scratch); reloaded,
+// 145 VGPRs and no scratch. r05's A/B had it neutral at 64K x 3 and C5 (r05l); the LAT build of small
+// engines keeps the hoisted loads (reloading cost C2 ~5 µs there)
+#ifndef RG_CTL_RELOAD_LEAN
+#define RG_CTL_RELOAD_LEAN 1
 #endif
 #ifdef RG_AB_SV_SEND
 #define RG_S_SEND slot_lane()
@@ -150,7 +167,9 @@ using CTickParams = RG_CONST(const TickParams);
 // narrow ones cost C2's fused launch ~2 µs, the storm's slow kernel nothing)
 template <int R, bool FAST = false, int ROLE = -1, bool LAT = false, bool SLIM = false>
 struct Ctl {
-  static constexpr bool LEAN = FAST && !LAT;  // cold fields copied through at the end (register-lean)
+  // LEAN: the fields only the end of the step reads (processed, applied, snapshot index, cc_hi) are
+  // loaded there, not with the state (register-lean); LAT loads them up front
+  static constexpr bool LEAN = FAST && !LAT;
   // the tick's parameter block, read in place at each use (a device slot the host filled): the
   // fields are reloaded where needed instead of living in registers for the whole step (r02 kept a
   // 368-B copy, 279 SGPR spills at R = 3)
@@ -162,7 +181,7 @@ struct Ctl {
   // A field is one scalar-cache hit away at each use. RG_AB_CTL_HOIST: r04's hoisted loads (A/B)
   RG_FN CTickParams& P() const {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(RG_AB_CTL_HOIST)
-    if constexpr (!FAST || RG_CTL_RELOAD_FAST) {
+    if constexpr (!FAST || RG_CTL_RELOAD_FAST || (LEAN && RG_CTL_RELOAD_LEAN)) {
       CTickParams* r = &p_;
       asm volatile("" : "+s"(r));
       return *r;
@@ -182,7 +201,10 @@ struct Ctl {
   // remote match / next / snapshot index; at R = 8 the snapshot indices (touched only on the
   // snapshot path) stay in this step's output rows instead of registers
   static constexpr bool RS_MEM = R >= 8;
-  uint64_t rm[R], rn[R], rs[RS_MEM ? 1 : R];
+  // The fast step neither reads nor writes the snapshot indices: a remote's rsnap is non-zero only in
+  // the SNAPSHOT state, and every SNAPSHOT branch leaves the fast path (rs_get / rs_set below)
+  static constexpr bool RS_REG = !RS_MEM && !FAST;
+  uint64_t rm[R], rn[R], rs[RS_REG ? R : 1];
   uint32_t rt[R];                // remote state
   uint64_t last_start, sent_hi, rw_lo, rw_hi, marker_start;
   uint64_t processed_start, restored_at;  // apply window: entries restored from a snapshot are not Update()d
@@ -206,6 +228,10 @@ struct Ctl {
   uint64_t oc, em;  // per destination: enqueued / emitted counts, 8 bits each
   uint32_t nj;      // jobs emitted
   uint64_t lt_i = ~0ull, lt_v = 0;  // term_at cache: index lt_i has term lt_v (~0: none)
+  // in-place store (FAST): what the step changed, for the fields it cannot compare at the end
+  uint32_t etick0 = 0, drops0 = 0;  // at step start
+  bool fidx0 = false;               // S_FIDX was set (the last step compacted): it is cleared now
+  bool ldv = false, cmv = false;    // leader / committed moved
 
   RG_FN Ctl(CTickParams& pp, uint32_t qq) : Ctl(pp, qq / pp.G, qq - (qq / pp.G) * pp.G) {}
   // slot ss of group column g0: the kernels pass a wave-uniform slot (the grid's y index), so every
@@ -215,31 +241,37 @@ struct Ctl {
     rid = gg * R + RG_S_ID;
     gi = (uint32_t)pl_input_index(P().pl, gg);
     const uint64_t n = P().nrep;
-    const uint64_t* a = P().s64_in + q;
-    const uint32_t* b = P().s32_in + q;
+    const uint64_t* a = P().s64 + q;
+    const uint32_t* b = P().s32 + q;
     term = a[S_TERM * n]; leader = a[S_LEADER * n]; committed = a[S_COMMITTED * n];
     last = a[S_LAST * n]; marker = a[S_MARKER * n]; marker_term = a[S_MARKER_TERM * n];
     cap_base = a[S_CAP_BASE * n];
     role = b[S_ROLE * n]; etick = b[S_ETICK * n]; htick = b[S_HTICK * n]; rand_to = b[S_RAND_TO * n];
     active = b[S_ACTIVE * n]; drops = b[S_DROPS * n]; members = b[S_MEMBERS * n];
     hw = b[S_HW * n];
-    if constexpr (!LEAN) {  // LEAN: copied through by store() (no branch of the fast path reads them)
-      vote = a[S_VOTE * n]; applied = a[S_APPLIED * n]; snap_index = a[S_SNAP_INDEX * n];
-      snap_term = a[S_SNAP_TERM * n]; processed = a[S_PROCESSED * n]; cc_hi = a[S_CC_HI * n];
+    if constexpr (!FAST) {  // the fields no fast branch reads or changes (it aborts first): not loaded there
+      vote = a[S_VOTE * n]; snap_term = a[S_SNAP_TERM * n];
       rng_ctr = b[S_RNG_CTR * n]; granted = b[S_GRANTED * n]; responded = b[S_RESPONDED * n];
       err = b[S_ERR * n]; snap_members = b[S_SNAP_MEMBERS * n]; cc_pending = b[S_CC_PENDING * n];
     } else {
-      vote = applied = snap_index = snap_term = processed = cc_hi = 0;
+      vote = snap_term = 0;
       rng_ctr = granted = responded = err = snap_members = cc_pending = 0;
     }
+    if constexpr (!LEAN) {
+      applied = a[S_APPLIED * n]; snap_index = a[S_SNAP_INDEX * n]; processed = a[S_PROCESSED * n];
+      cc_hi = a[S_CC_HI * n];
+    } else {
+      applied = snap_index = processed = cc_hi = 0;
+    }
+    etick0 = etick;
+    drops0 = drops;
     sfor<0, R>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
-      rm[j] = P().rem_in[(0 * R + j) * n + q];
-      rn[j] = P().rem_in[(1 * R + j) * n + q];
-      if constexpr (LEAN) rs[0] = 0;  // LEAN: copied through by store()
-      else if constexpr (RS_MEM) P().rem_out[(2 * R + j) * n + q] = P().rem_in[(2 * R + j) * n + q];
-      else rs[j] = P().rem_in[(2 * R + j) * n + q];
-      rt[j] = P().rst_in[j * n + q];
+      rm[j] = P().rem[(0 * R + j) * n + q];
+      rn[j] = P().rem[(1 * R + j) * n + q];
+      if constexpr (RS_REG) rs[j] = P().rem[(2 * R + j) * n + q];
+      else rs[0] = 0;  // RS_MEM: read and written in place (rs_get / rs_set); FAST: never touched
+      rt[j] = P().rst[j * n + q];
     });
 #ifdef RG_AB_LAST_TERM_RING  // A/B variant: the term of `last` from the ring (r04)
     if (last > marker) lt_set(last, *tr_at(last) & TERM_MASK);
@@ -260,6 +292,7 @@ struct Ctl {
     {
       uint32_t nlpg = lpg_;
       if (const uint64_t fi = a[S_FIDX * n]) {
+        fidx0 = true;
         uint32_t bound = hw;
         if (fi <= last) {
           const uint64_t sl = fi & (P().L - 1), bank = *tr_at(fi) >> 63;
@@ -297,13 +330,21 @@ struct Ctl {
   // ---- remotes (compile-time R: selects, no local-memory arrays)
 #define RG_GET(arr, f) sel_get<R>(arr, f)
 #define RG_SET(arr, f, val) sel_set<R>(arr, f, val)
+  // FAST: 0 and a no-op. The fast step reaches them only where a remote leaves RETRY for REPLICATE
+  // (respondedTo), whose rsnap is already 0; an aborted fast step must not have written state in place
   RG_FN uint64_t rs_get(uint32_t f) const {
-    if constexpr (RS_MEM) return P().rem_out[((uint64_t)(2 * R) + f) * P().nrep + q];
+    if constexpr (FAST) return 0;
+    else if constexpr (RS_MEM) return P().rem[((uint64_t)(2 * R) + f) * P().nrep + q];
     else return sel_get<R>(rs, f);
   }
   RG_FN void rs_set(uint32_t f, uint64_t v) {
-    if constexpr (RS_MEM) P().rem_out[((uint64_t)(2 * R) + f) * P().nrep + q] = v;
-    else sel_set<R>(rs, f, v);
+    if constexpr (FAST) {
+      (void)f; (void)v;
+    } else if constexpr (RS_MEM) {
+      P().rem[((uint64_t)(2 * R) + f) * P().nrep + q] = v;
+    } else {
+      sel_set<R>(rs, f, v);
+    }
   }
 
   // ---- log (entryLog)
@@ -340,6 +381,7 @@ struct Ctl {
       return;
     }
     committed = i;
+    cmv = true;
   }
 
   // ---- transport
@@ -457,6 +499,7 @@ struct Ctl {
     });
     if (qv > committed && term_at(qv) == term) {
       committed = qv;
+      cmv = true;
       return true;
     }
     return false;
@@ -1299,7 +1342,10 @@ struct Ctl {
         case M_HEARTBEAT:
           if (role == LEADER) return;  // a leader ignores them (as the full step's dispatch does)
           etick = 0;
-          leader = from;
+          if (leader != from) {  // the first message of a new leader in this term
+            leader = from;
+            ldv = true;
+          }
           if (type == M_REPLICATE) {
             handle_replicate(w0, hw(2), hw(3), hw(4), from, src, k, remote, hw(7), hw(5), mt0);
           } else {
@@ -1526,7 +1572,7 @@ struct Ctl {
       asm volatile("" ::: "memory");
 #endif
       const uint64_t n = P().nrep;
-      const uint64_t* a = P().s64_in + q;
+      const uint64_t* a = P().s64 + q;
       processed = processed_start = a[S_PROCESSED * n];
       cc_hi = a[S_CC_HI * n];
       applied = a[S_APPLIED * n];
@@ -1547,6 +1593,7 @@ struct Ctl {
       }
     }
     processed = committed;
+    const bool apv = !P().AF && applied != processed;  // applied moves (the in-place store)
     if (!P().AF) applied = processed;
     if (P().SE && applied >= snap_index && applied - snap_index >= P().SE) {
       snap_index = applied;
@@ -1559,11 +1606,10 @@ struct Ctl {
         marker = c;
       }
     }
+    const bool cbv = cap_base != marker_start;
     cap_base = marker_start;
-    // compaction or a restore moved the marker: the stream below entry marker + 1 is released by the
-    // next step, once this step's bulk kernel has stored that entry's position
     RG_STAMP(4);
-    store();
+    store(apv, cbv);
     RG_STAMP(5);
 #if defined(RG_CTL_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
     if (P().prof)
@@ -1571,51 +1617,90 @@ struct Ctl {
 #endif
   }
 
-  RG_FN void store() {
-    if constexpr (LEAN) {  // the fields no fast branch changes: copied through from the step's input state
-      const uint64_t n = P().nrep;
-      const uint64_t* ai = P().s64_in + q;
-      const uint32_t* bi = P().s32_in + q;
-      vote = ai[S_VOTE * n];
-      if (!took) {
-        snap_term = ai[S_SNAP_TERM * n];
-        snap_members = bi[S_SNAP_MEMBERS * n];
+  // The step's results, written in place. The full step writes every field. The fast step writes only
+  // the fields a fast branch can change, each only when it may have changed this step (apv / cbv:
+  // applied and cap_base moved): term, vote, role, the election timer's bound and RNG, the vote masks,
+  // the error word, the membership, a pending ConfigChange and cc_hi change only on branches that
+  // leave the fast path, and a follower's remotes, heartbeat timer and active mask not at all. In steady
+  // state a follower writes its log end, commit and stream rows, a leader those and its remotes.
+  RG_FN void store(bool apv, bool cbv) {
+    const uint64_t n = P().nrep;
+    uint64_t* a = P().s64 + q;
+    uint32_t* b = P().s32 + q;
+    const bool lmv = last != last_start, mmv = marker != marker_start;
+    // the persistence feed (rg_persist_collect): entries written, else whether the hard state changed
+    uint64_t plo = wlo;
+    if constexpr (FAST) {
+      constexpr bool LD = ROLE == (int)LEADER;
+      if (RGX(!LD && ldv)) a[S_LEADER * n] = leader;
+      if (RGX(cmv)) a[S_COMMITTED * n] = committed;
+      if (RGX(processed != processed_start)) a[S_PROCESSED * n] = processed;
+      if (RGX(apv)) a[S_APPLIED * n] = applied;
+      if (RGX(lmv)) {
+        a[S_LAST * n] = last;
+        b[S_HW * n] = hw;  // S_LPG / S_APG: pool_kernel (after this launch)
       }
-      rng_ctr = bi[S_RNG_CTR * n]; granted = bi[S_GRANTED * n]; responded = bi[S_RESPONDED * n];
-      err = bi[S_ERR * n]; cc_pending = bi[S_CC_PENDING * n];
+      if (RGX(mmv)) {
+        a[S_MARKER * n] = marker;
+        a[S_MARKER_TERM * n] = marker_term;
+      }
+      if (RGX(took)) {
+        a[S_SNAP_INDEX * n] = snap_index;
+        a[S_SNAP_TERM * n] = snap_term;
+        b[S_SNAP_MEMBERS * n] = snap_members;
+      }
+      if (RGX(cbv)) a[S_CAP_BASE * n] = cap_base;
+      // compaction moved the marker: the stream below entry marker + 1 is released by the next step,
+      // once this step's bulk kernel has stored that entry's position
+      if (RGX(mmv || fidx0)) a[S_FIDX * n] = mmv ? marker + 1 : 0;
+      if (RGX(lmv || mmv)) a[S_LAST_TERM * n] = last > marker ? (lt_i == last ? lt_v : *tr_at(last) & TERM_MASK) : marker_term;
+      if (RGX2(LD || etick != etick0)) b[S_ETICK * n] = etick;
+      if (RGX2(drops != drops0)) b[S_DROPS * n] = drops;
+      if (RGX(nlpg_ != lpg_)) b[S_NLPG * n] = nlpg_;  // else S_NLPG = S_LPG already (pool_kernel's last store)
+      if constexpr (LD) {
+        b[S_HTICK * n] = htick;
+        b[S_ACTIVE * n] = active;
+        sfor<0, R>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          P().rem[(0 * R + j) * n + q] = rm[j];
+          P().rem[(1 * R + j) * n + q] = rn[j];
+          P().rst[j * n + q] = (uint8_t)rt[j];
+        });
+      }
+      // term and vote do not change on the fast path
+      if (plo == ~0ull && (cmv || lmv || mmv || took)) plo = PERSIST_HS;
+    } else {
+      if (plo == ~0ull && P().persist_lo &&
+          (a[S_TERM * n] != term || a[S_VOTE * n] != vote || a[S_COMMITTED * n] != committed || lmv || mmv ||
+           a[S_SNAP_INDEX * n] != snap_index))
+        plo = PERSIST_HS;
+      a[S_TERM * n] = term; a[S_VOTE * n] = vote; a[S_LEADER * n] = leader; a[S_COMMITTED * n] = committed;
+      a[S_APPLIED * n] = applied; a[S_LAST * n] = last; a[S_MARKER * n] = marker; a[S_MARKER_TERM * n] = marker_term;
+      a[S_SNAP_INDEX * n] = snap_index; a[S_SNAP_TERM * n] = snap_term; a[S_CAP_BASE * n] = cap_base;
+      a[S_PROCESSED * n] = processed; a[S_CC_HI * n] = cc_hi;
+      a[S_FIDX * n] = mmv ? marker + 1 : 0;
+      a[S_LAST_TERM * n] = last > marker ? (lt_i == last ? lt_v : *tr_at(last) & TERM_MASK) : marker_term;
+      b[S_ROLE * n] = role; b[S_ETICK * n] = etick; b[S_HTICK * n] = htick; b[S_RAND_TO * n] = rand_to;
+      b[S_RNG_CTR * n] = rng_ctr; b[S_GRANTED * n] = granted; b[S_RESPONDED * n] = responded;
+      b[S_ACTIVE * n] = active; b[S_ERR * n] = err; b[S_DROPS * n] = drops;
+      b[S_MEMBERS * n] = members; b[S_SNAP_MEMBERS * n] = snap_members; b[S_CC_PENDING * n] = cc_pending;
+      b[S_HW * n] = hw;
+      b[S_NLPG * n] = nlpg_;
       sfor<0, R>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
-        P().rem_out[(2 * R + j) * n + q] = P().rem_in[(2 * R + j) * n + q];
+        P().rem[(0 * R + j) * n + q] = rm[j];
+        P().rem[(1 * R + j) * n + q] = rn[j];
+        if constexpr (RS_REG) P().rem[(2 * R + j) * n + q] = rs[j];
+        P().rst[j * n + q] = (uint8_t)rt[j];
       });
     }
-    const uint64_t n = P().nrep;
-    uint64_t* a = P().s64_out + q;
-    a[S_TERM * n] = term; a[S_VOTE * n] = vote; a[S_LEADER * n] = leader; a[S_COMMITTED * n] = committed;
-    a[S_APPLIED * n] = applied; a[S_LAST * n] = last; a[S_MARKER * n] = marker; a[S_MARKER_TERM * n] = marker_term;
-    a[S_SNAP_INDEX * n] = snap_index; a[S_SNAP_TERM * n] = snap_term; a[S_CAP_BASE * n] = cap_base;
-    a[S_PROCESSED * n] = processed; a[S_CC_HI * n] = cc_hi;
-    // compaction or a restore moved the marker: the stream below entry marker + 1 is released by the
-    // next step, once this step's bulk kernel has stored that entry's position
-    a[S_FIDX * n] = marker != marker_start ? marker + 1 : 0;
-    a[S_LAST_TERM * n] = last > marker ? (lt_i == last ? lt_v : *tr_at(last) & TERM_MASK) : marker_term;
-    uint32_t* b = P().s32_out + q;
-    b[S_ROLE * n] = role; b[S_ETICK * n] = etick; b[S_HTICK * n] = htick; b[S_RAND_TO * n] = rand_to;
-    b[S_RNG_CTR * n] = rng_ctr; b[S_GRANTED * n] = granted; b[S_RESPONDED * n] = responded;
-    b[S_ACTIVE * n] = active; b[S_ERR * n] = err; b[S_DROPS * n] = drops;
-    b[S_MEMBERS * n] = members; b[S_SNAP_MEMBERS * n] = snap_members; b[S_CC_PENDING * n] = cc_pending;
-    b[S_HW * n] = hw;  // S_LPG / S_APG: pool_kernel (after this launch)
-    b[S_NLPG * n] = nlpg_;
     sfor<0, R>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
-      P().rem_out[(0 * R + j) * n + q] = rm[j];
-      P().rem_out[(1 * R + j) * n + q] = rn[j];
-      if constexpr (!RS_MEM && !LEAN) P().rem_out[(2 * R + j) * n + q] = rs[j];
-      P().rst_out[j * n + q] = (uint8_t)rt[j];
       P().cnt_out[((uint64_t)RG_S_SEND * R + j) * P().G + g] = get8(oc, j);
     });
     P().jcnt[q] = nj;
     if (P().apply_lo) P().apply_lo[q] = umax64(processed_start, restored_at) + 1;
-    if (P().persist_lo) P().persist_lo[q] = wlo;
+    if (P().persist_lo) P().persist_lo[q] = plo;
     if (P().snap_ev) P().snap_ev[q] = restored_at | (took ? SNAP_TAKEN_BIT : 0ull);
   }
 #undef RG_GET

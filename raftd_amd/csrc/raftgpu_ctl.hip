@@ -73,7 +73,7 @@ __global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_MINWAVES) control_kernel(
 // steady-state branches only and hands a replica whose step leaves them to the slow kernel, which
 // re-runs that replica's whole step with the full Ctl<R> (an aborted fast step stored nothing).
 #ifndef RG_CTL_FAST_WAVES
-#define RG_CTL_FAST_WAVES (RG_CTL_R <= 3 ? 3 : RG_CTL_R <= 7 ? 2 : 1)  // the most waves per SIMD without scratch
+#define RG_CTL_FAST_WAVES (RG_CTL_R <= 4 ? 3 : 2)  // the most waves per SIMD without scratch (r06: 145 VGPRs at R 3, 221 at R 8)
 #endif
 // The fast path is compiled once per role — Ctl<R, true, LEADER> for leaders, Ctl<R, true, FOLLOWER>
 // for every other replica (followers step, candidates hand off) — and each lane runs its role's
@@ -84,7 +84,7 @@ __global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_MINWAVES) control_kernel(
 // latency build of small engines (every field loaded up front, Ctl's LAT)
 template <int R, bool LAT = false>
 __device__ __forceinline__ bool fast_step(CTickParams& cp, uint32_t q) {
-  if (cp.s32_in[(uint64_t)S_ROLE * cp.nrep + q] == LEADER) {
+  if (cp.s32[(uint64_t)S_ROLE * cp.nrep + q] == LEADER) {
 #ifdef RG_CTL_PROFILE
     const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memtime();
     Ctl<R, true, LEADER, LAT> c(cp, q);

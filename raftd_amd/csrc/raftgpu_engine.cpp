@@ -96,10 +96,11 @@ struct rg_engine {
   uint32_t nrep = 0, J = 0;
   hipStream_t own = nullptr, stream = nullptr, bulk = nullptr;
   hipEvent_t ctl_done[2] = {nullptr, nullptr}, bulk_done[2] = {nullptr, nullptr};
-  uint64_t* s64[2] = {nullptr, nullptr};
-  uint32_t* s32[2] = {nullptr, nullptr};
-  uint64_t* rem[2] = {nullptr, nullptr};
-  uint8_t* rst[2] = {nullptr, nullptr};
+  // replica state, updated in place by each step (a step writes only the fields it changes)
+  uint64_t* s64 = nullptr;
+  uint32_t* s32 = nullptr;
+  uint64_t* rem = nullptr;
+  uint8_t* rst = nullptr;
   uint64_t* tr = nullptr;
   uint2* info = nullptr;
   // paged payload streams: pool pages, per-replica page tables, the free-id ring and
@@ -183,7 +184,7 @@ struct rg_engine {
   uint64_t tp_next = 0;
   uint32_t tp_corrupt = 0;  // tests (rg_debug_corrupt_params): seal the next n blocks with a wrong checksum
   // the control fast path: control_fast_kernel then control_slow_kernel over the replicas it
-  // handed off ([2] counters by tick parity, then the list); RAFTGPU_CTL_FAST=0: control_kernel alone (A/B)
+  // handed off ([2] counters by tick parity, then the list); build variant -DRG_AB_CTL_FULL: control_kernel alone
   uint32_t* slow = nullptr;
   bool ctl_fast = true;
   bool ctl_fb = false;  // small engines: the fallback runs in the fast kernel's launch (control_fastfb_kernel)
@@ -194,10 +195,10 @@ struct rg_engine {
   uint32_t bulk_tile = 1;
   // small jobs share a bulk ring pass (bulk_kernel<.., MJ = true>): when Replicates and proposal
   // batches carry at most 16 entries (max_entries_per_msg), jobs are small; the 64-entry jobs of
-  // full batches run faster without it. RAFTGPU_BULK_MULTIJOB=0/1 overrides (A/B).
+  // full batches run faster without it. Build variant -DRG_AB_BULK_MULTIJOB=0/1 overrides.
   bool bulk_mj = false;
   bool bulk_small = true;
-  uint32_t bulk_wg = 4;  // waves per bulk workgroup  // MJ engines: bulk_small_kernel takes the small jobs first (RAFTGPU_BULK_SMALL=0: off)
+  uint32_t bulk_wg = 4;  // waves per bulk workgroup; MJ engines: bulk_small_kernel takes the small jobs first (-DRG_AB_NO_BULK_SMALL: off)
   uint64_t bytes = 0;
   std::vector<void*> allocs;
   // per-launch event timing (rg_timing): bit 0 control_kernel, bit 1 bulk_kernel; a start/end
@@ -206,6 +207,9 @@ struct rg_engine {
   uint32_t timing_every = 1;
   std::vector<hipEvent_t> ev_pool, ev_live;
   std::vector<int> ev_kind;  // kernel (0 control, 1 bulk) of each start/end pair in ev_live
+  std::vector<uint64_t> ev_tick;  // the tick of each pair
+  struct KEvent { uint64_t tick; double start, end; };
+  std::vector<KEvent> kev[2];  // timed launches on the process epoch's timeline (rg_timing_epoch)
   double kms[2] = {0, 0};
   uint64_t klaunch[2] = {0, 0};
   uint32_t T0[256];
@@ -245,7 +249,7 @@ struct rg_engine {
   uint32_t* small_rest = nullptr;  // BulkParams::rest
   uint32_t *acnt = nullptr, *accnt = nullptr, *arcnt = nullptr;
   uint64_t *aoff = nullptr, *acoff = nullptr, *aroff = nullptr, *absum = nullptr;
-  bool copy_kernel = true;  // RAFTGPU_APPLY_MEMCPY=1: the runtime's D2H copy instead (A/B)
+  bool copy_kernel = true;  // build variant -DRG_AB_APPLY_MEMCPY: the runtime's D2H copy instead
   SdmaCopier* sdma = nullptr;  // RAFTGPU_APPLY_SDMA=1: the D2H leg on an SDMA engine (raftgpu_sdma.cpp)
   uint8_t* astage = nullptr;
   uint64_t astage_bytes = 0;
@@ -398,10 +402,7 @@ static TickParams params_at(rg_engine* e, uint64_t tk) {
   p.tick = tk;
   p.pl = e->pl;
   const int a = (int)(tk & 1), b = a ^ 1;
-  p.s64_in = e->s64[a]; p.s64_out = e->s64[b];
-  p.s32_in = e->s32[a]; p.s32_out = e->s32[b];
-  p.rem_in = e->rem[a]; p.rem_out = e->rem[b];
-  p.rst_in = e->rst[a]; p.rst_out = e->rst[b];
+  p.s64 = e->s64; p.s32 = e->s32; p.rem = e->rem; p.rst = e->rst;
   p.tr = e->tr;
   p.hdr_in = e->hdr[b]; p.hdr_out = e->hdr[a];
   p.mt_in = e->mt[b]; p.mt_out = e->mt[a];
@@ -536,12 +537,12 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   const uint64_t n = e->nrep, L = c.log_capacity, P = c.payload_bytes, R = c.replicas, K = c.max_msgs_per_pair,
                  E = c.max_entries_per_msg, G = c.groups, J = e->J;
   int rc = RG_OK;
+  rc = dalloc(e, &e->s64, S64_ROWS * n * 8);
+  if (rc == RG_OK) rc = dalloc(e, &e->s32, S32_ROWS * n * 4);
+  if (rc == RG_OK) rc = dalloc(e, &e->rem, 3 * R * n * 8);
+  if (rc == RG_OK) rc = dalloc(e, &e->rst, R * n);
   for (int b = 0; b < 2 && rc == RG_OK; ++b) {
-    rc = dalloc(e, &e->s64[b], S64_ROWS * n * 8);
-    if (rc == RG_OK) rc = dalloc(e, &e->s32[b], S32_ROWS * n * 4);
-    if (rc == RG_OK) rc = dalloc(e, &e->rem[b], 3 * R * n * 8);
-    if (rc == RG_OK) rc = dalloc(e, &e->rst[b], R * n);
-    if (rc == RG_OK) rc = dalloc(e, &e->hdr[b], 8 * R * R * K * G * 8);
+    rc = dalloc(e, &e->hdr[b], 8 * R * R * K * G * 8);
     if (rc == RG_OK) rc = dalloc(e, &e->mt[b], R * R * K * E * G * 8);
     if (rc == RG_OK) rc = dalloc(e, &e->cnt[b], R * R * G * 4);
   }
@@ -750,6 +751,18 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
 #ifdef RG_AB_NO_BULK_SMALL  // A/B variant: one-job replicas through bulk_kernel too
   e->bulk_small = false;
 #endif
+  {  // r05 turned these runtime A/B knobs into build variants (-DRG_AB_*, scripts/build_variant.sh): a script
+     // still setting one would run the same build on both arms of its A/B, so say so once
+    static bool warned = false;
+    static const char* retired[] = {"RAFTGPU_BULK_MULTIJOB", "RAFTGPU_BULK_SMALL", "RAFTGPU_BULK_TILE",
+                                    "RAFTGPU_BULK_GRID", "RAFTGPU_BULK_WG", "RAFTGPU_CTL_FAST", "RAFTGPU_WIRE_SIZING",
+                                    "RAFTGPU_SYNC_DEBUG", "RAFTGPU_SMALL_GRID", "RAFTGPU_APPLY_MEMCPY", "RAFTGPU_POOL_PERM"};
+    for (const char* k : retired)
+      if (!warned && getenv(k)) {
+        fprintf(stderr, "raftgpu: %s is no longer read (a build variant now: scripts/build_variant.sh -DRG_AB_...)\n", k);
+        warned = true;
+      }
+  }
   if (const char* v = getenv("RAFTGPU_RCCL_SELF"))  // test hook: rg_wire_exchange's region to self moves too
     e->self_via_transport = !strcmp(v, "rccl");
   if (const char* v = getenv("RAFTGPU_APPLY_SDMA"))  // test hook: the SDMA D2H leg
@@ -949,10 +962,6 @@ int rg_bootstrap(rg_engine* e) {
   std::fill(e->cmd_used.begin(), e->cmd_used.end(), 0ull);
   std::fill(e->cmd_tick.begin(), e->cmd_tick.end(), ~0ull);
   TickParams p = params(e);
-  p.s64_out = e->s64[0];
-  p.s32_out = e->s32[0];
-  p.rem_out = e->rem[0];
-  p.rst_out = e->rst[0];
   for (int b = 0; b < 2; ++b) HIPCHK(hipMemsetAsync(e->jcnt[b], 0, (uint64_t)e->nrep * 4, e->stream));
   HIPCHK(launch_bootstrap(p, e->info, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
@@ -1328,22 +1337,37 @@ static int timing_event(rg_engine* e, hipStream_t s, int kind) {
     e->ev_pool.pop_back();
   }
   e->ev_live.push_back(ev);
-  if (e->ev_live.size() & 1) e->ev_kind.push_back(kind);
+  if (e->ev_live.size() & 1) {
+    e->ev_kind.push_back(kind);
+    e->ev_tick.push_back(e->t);
+  }
   HIPCHK(hipEventRecord(ev, s));
   return RG_OK;
 }
 
+// rg_timing_epoch: one reference event per process (the device's timeline origin for every engine)
+static hipEvent_t g_epoch = nullptr;
+static int g_epoch_dev = -1;
+
 static int timing_drain(rg_engine* e) {
   HIPCHK(hipStreamSynchronize(e->stream));
   HIPCHK(hipStreamSynchronize(e->bulk));
+  const bool epoch = g_epoch && g_epoch_dev == e->c.device;
   for (size_t i = 0; i + 1 < e->ev_live.size(); i += 2) {
     float ms = 0;
     const int k = e->ev_kind[i / 2];
     HIPCHK(hipEventElapsedTime(&ms, e->ev_live[i], e->ev_live[i + 1]));
     e->kms[k] += ms;
     e->klaunch[k]++;
+    if (epoch) {
+      float a = 0, b = 0;
+      HIPCHK(hipEventElapsedTime(&a, g_epoch, e->ev_live[i]));
+      HIPCHK(hipEventElapsedTime(&b, g_epoch, e->ev_live[i + 1]));
+      e->kev[k].push_back({e->ev_tick[i / 2], (double)a, (double)b});
+    }
   }
   e->ev_kind.clear();
+  e->ev_tick.clear();
   e->ev_pool.insert(e->ev_pool.end(), e->ev_live.begin(), e->ev_live.end());
   e->ev_live.clear();
   return RG_OK;
@@ -1359,6 +1383,37 @@ int rg_timing(rg_engine* e, int enable) {
   e->timing_every = every > 0 ? (uint32_t)every : 1u;
   e->kms[0] = e->kms[1] = 0;
   e->klaunch[0] = e->klaunch[1] = 0;
+  e->kev[0].clear();
+  e->kev[1].clear();
+  return RG_OK;
+}
+
+int rg_timing_epoch(int device) {
+  HIPCHK(hipSetDevice(device));
+  if (g_epoch && g_epoch_dev != device) {
+    (void)hipEventDestroy(g_epoch);
+    g_epoch = nullptr;
+  }
+  if (!g_epoch) HIPCHK(hipEventCreate(&g_epoch));
+  HIPCHK(hipDeviceSynchronize());  // every event recorded later lies after it on the device's timeline
+  HIPCHK(hipEventRecord(g_epoch, nullptr));
+  HIPCHK(hipEventSynchronize(g_epoch));
+  g_epoch_dev = device;
+  return RG_OK;
+}
+
+int rg_kernel_events(rg_engine* e, int kernel, uint64_t* ticks, double* start_ms, double* end_ms, uint64_t cap,
+                     uint64_t* n) {
+  if (!e || !n || kernel < 0 || kernel > 1 || (cap && (!ticks || !start_ms || !end_ms)))
+    return fail(RG_EINVAL, "rg_kernel_events args");
+  if (int rc = timing_drain(e)) return rc;
+  const auto& v = e->kev[kernel];
+  *n = v.size();
+  for (uint64_t i = 0; i < cap && i < v.size(); ++i) {
+    ticks[i] = v[i].tick;
+    start_ms[i] = v[i].start;
+    end_ms[i] = v[i].end;
+  }
   return RG_OK;
 }
 
@@ -1498,7 +1553,7 @@ static int tick_impl(rg_engine* e, const rg_tick_input* in, bool device_ptrs) {
   if (e->c.payload_bytes) {  // stream pages: release what compaction passed, take what this step's appends need
     PoolParams pp{};
     pp.nrep = e->nrep; pp.PTS = e->PTS; pp.npages = e->npages;
-    pp.s32_out = p.s32_out; pp.s32_in = p.s32_in; pp.pt = e->pt; pp.fring = e->fring; pp.ctl = e->poolctl;
+    pp.s32 = p.s32; pp.pt = e->pt; pp.fring = e->fring; pp.ctl = e->poolctl;
     pp.jcnt = p.jcnt;
     LAUNCH(launch_pool(pp, e->stream), e->stream, "pool_kernel");
   }
@@ -1574,7 +1629,7 @@ static int tick_graph(rg_engine* e, const rg_tick_input* in, uint32_t k) {
         if (r == hipSuccess && e->c.payload_bytes) {
           PoolParams pp{};
           pp.nrep = e->nrep; pp.PTS = e->PTS; pp.npages = e->npages;
-          pp.s32_out = p.s32_out; pp.s32_in = p.s32_in; pp.pt = e->pt; pp.fring = e->fring; pp.ctl = e->poolctl;
+          pp.s32 = p.s32; pp.pt = e->pt; pp.fring = e->fring; pp.ctl = e->poolctl;
           pp.jcnt = p.jcnt;
           r = launch_pool(pp, e->stream);
           if (r == hipSuccess) r = launch_bulk(bulk_params_at(e, t0 + i), e->pt, e->stream, e->bulk_grid);
@@ -1914,7 +1969,7 @@ static PersistParams persist_params(rg_engine* e, bool full, uint32_t slot_mask)
   a.G = t.G; a.R = t.R; a.nrep = t.nrep; a.L = t.L; a.P = t.P; a.pl = e->pl;
   a.full = (full || e->t == 0) ? 1u : 0u;  // before the first tick there is no previous state
   a.slot_mask = slot_mask;
-  a.s64 = t.s64_in; a.s64_prev = t.s64_out; a.s32 = t.s32_in; a.persist_lo = e->persist_lo;
+  a.s64 = t.s64; a.s32 = t.s32; a.persist_lo = e->persist_lo;
   a.tr = e->tr; a.info = e->info; a.pool = e->pool; a.pt = e->pt; a.PTS = e->PTS; a.zi = e->crc_tab + CRC_ZI_OFF;
   a.scnt = e->pscnt; a.ecnt = e->pecnt; a.ccnt = e->pccnt; a.tcnt = e->ptcnt;
   a.soff = e->psoff; a.eoff = e->peoff; a.coff = e->pcoff; a.toff = e->ptoff;
@@ -1984,7 +2039,7 @@ static ApplyParams apply_params(rg_engine* e, uint32_t slot_mask) {
   const TickParams t = params(e);
   ApplyParams a{};
   a.G = t.G; a.R = t.R; a.nrep = t.nrep; a.L = t.L; a.P = t.P; a.slot_mask = slot_mask; a.pl = e->pl;
-  a.s64 = t.s64_in; a.apply_lo = e->apply_lo; a.tr = e->tr; a.info = e->info;
+  a.s64 = t.s64; a.apply_lo = e->apply_lo; a.tr = e->tr; a.info = e->info;
   a.pool = e->pool; a.pt = e->pt; a.PTS = e->PTS;
   a.zi = e->crc_tab + CRC_ZI_OFF;
   a.cnt = e->acnt; a.ccnt = e->accnt; a.off = e->aoff; a.coff = e->acoff; a.bsum = e->absum;
@@ -2145,7 +2200,7 @@ int rg_snapshot_events(rg_engine* e, uint32_t slot_mask, rg_snapshot_event* even
   const TickParams t = params(e);
   SnapParams a{};
   a.G = t.G; a.R = t.R; a.nrep = t.nrep; a.slot_mask = slot_mask; a.pl = e->pl;
-  a.s64 = t.s64_in; a.snap_ev = e->snap_ev;
+  a.s64 = t.s64; a.snap_ev = e->snap_ev;
   a.cnt = e->acnt; a.off = e->aoff; a.bsum = e->absum;
   LAUNCH(launch_snap_count(a, (uint64_t*)e->d_sum, e->stream), e->stream, "snapshot count");
   uint64_t total = 0;
@@ -2175,7 +2230,7 @@ extern "C" int rg_debug_ctl_profile(rg_engine* e, uint32_t* out) {
 #endif
 
 // measurement / tests (not in include/raftgpu.h): replicas of the last tick whose step left the control
-// fast path and ran in the full kernel (0 with RAFTGPU_CTL_FAST=0)
+// fast path and ran in the full kernel (0 in the -DRG_AB_CTL_FULL build)
 extern "C" int rg_debug_ctl_slow(rg_engine* e, uint32_t* n) {
   if (!e || !n) return fail(RG_EINVAL, "rg_debug_ctl_slow args");
   if (int jrc = join(e)) return jrc;
@@ -2271,7 +2326,7 @@ int rg_read_index_results(rg_engine* e, uint32_t slot_mask, rg_read_ready* out, 
   const TickParams t = params(e);
   SnapParams a{};
   a.G = t.G; a.R = t.R; a.nrep = t.nrep; a.slot_mask = slot_mask; a.pl = e->pl;
-  a.s64 = t.s64_in; a.rdst = e->rdst; a.tick = e->t;
+  a.s64 = t.s64; a.rdst = e->rdst; a.tick = e->t;
   a.cnt = e->acnt; a.off = e->aoff; a.bsum = e->absum;
   LAUNCH(launch_read_count(a, (uint64_t*)e->d_sum, e->stream), e->stream, "read count");
   uint64_t total = 0;
@@ -2294,7 +2349,12 @@ int rg_read_index_results(rg_engine* e, uint32_t slot_mask, rg_read_ready* out, 
 // synchronisation, every section's gather into one device staging area, one D2H copy, one
 // synchronisation — instead of a count, sync, gather, copy and sync per section
 int rg_get_update(rg_engine* e, uint32_t slot_mask, uint32_t flags, rg_update* out) {
-  if (!e || !out || (flags & ~(RG_UPDATE_ALL | RG_UPDATE_FULL_STATE))) return fail(RG_EINVAL, "rg_get_update args");
+  if (!e || !out || (flags & ~(RG_UPDATE_ALL | RG_UPDATE_FULL_STATE | RG_UPDATE_COMMITTED_CMDS)))
+    return fail(RG_EINVAL, "rg_get_update args");
+  // the committed section by reference: with the persist section in the same hand-off every committed
+  // entry's Cmd has crossed once already (this or an earlier persist section of the same replicas), so
+  // only its run, length and CRC cross again (the hand-off shipped every Cmd twice)
+  const bool by_ref = (flags & RG_UPDATE_PERSIST) && (flags & RG_UPDATE_COMMITTED) && !(flags & RG_UPDATE_COMMITTED_CMDS);
   if (int jrc = join(e)) return jrc;
   *out = rg_update{};
   out->tick = e->t;
@@ -2309,7 +2369,7 @@ int rg_get_update(rg_engine* e, uint32_t slot_mask, uint32_t flags, rg_update* o
   ApplyParams aa = apply_params(e, slot_mask);
   SnapParams sa{};
   sa.G = t.G; sa.R = t.R; sa.nrep = t.nrep; sa.slot_mask = slot_mask; sa.pl = e->pl;
-  sa.s64 = t.s64_in; sa.snap_ev = e->snap_ev; sa.rdst = e->rdst; sa.tick = e->t;
+  sa.s64 = t.s64; sa.snap_ev = e->snap_ev; sa.rdst = e->rdst; sa.tick = e->t;
   sa.cnt = e->uscnt; sa.off = e->usoff; sa.bsum = e->absum;
   SnapParams ra = sa;
   ra.cnt = e->urcnt; ra.off = e->uroff;
@@ -2323,7 +2383,8 @@ int rg_get_update(rg_engine* e, uint32_t slot_mask, uint32_t flags, rg_update* o
   HIPCHK(hipStreamSynchronize(e->stream));
   // one staging layout for every section, each 16-B aligned
   const PersistLayout pl = persist_layout(tot);
-  const ApplyLayout al = apply_layout(tot + 4);  // committed: entries, chunks, runs
+  const uint64_t ctot[3] = {tot[4], by_ref ? 0 : tot[5], tot[6]};
+  const ApplyLayout al = apply_layout(ctot);  // committed: entries, chunks (none by reference), runs
   const uint64_t snb = a16(tot[7] * sizeof(rg_snapshot_event)), rdb = a16(tot[8] * sizeof(rg_read_ready));
   const uint64_t o_c = pl.total, o_s = o_c + al.total, o_r = o_s + snb, total = o_r + rdb;
   if (total == 0) return RG_OK;
@@ -2344,7 +2405,7 @@ int rg_get_update(rg_engine* e, uint32_t slot_mask, uint32_t flags, rg_update* o
   if (tot[4]) {
     aa.out_run = d + o_c + al.runs;
     aa.out_cmd = d + o_c + al.cmds;
-    aa.out_pay = d + o_c + al.pay;
+    aa.out_pay = by_ref ? nullptr : d + o_c + al.pay;
     LAUNCH(launch_apply_gather(aa, tot[6], e->stream), e->stream, "apply gather");
   }
   if (tot[7]) {
@@ -2360,7 +2421,10 @@ int rg_get_update(rg_engine* e, uint32_t slot_mask, uint32_t flags, rg_update* o
   uint8_t* h = e->u_host;
   if (tot[0]) persist_batch(&out->persist, h, tot, pl);
   out->committed = rg_apply_batch{};
-  if (tot[4]) apply_batch(&out->committed, h + o_c, tot + 4, al);
+  if (tot[4]) {
+    apply_batch(&out->committed, h + o_c, ctot, al);
+    if (by_ref) out->committed.payload = nullptr;  // runs' off: where each Cmd would sit, packed
+  }
   out->snapshots = (const rg_snapshot_event*)(h + o_s);
   out->n_snapshots = tot[7];
   out->reads = (const rg_read_ready*)(h + o_r);
@@ -2470,6 +2534,9 @@ int rg_wire_plan(rg_engine* e, uint64_t* send_bytes) {
 //   capacity (its units were dropped: lost in transit, counted) takes it to 1.5 × that need at once;
 //   a capacity above the target shrinks by at most 1/8 per exchange (bring-up's small needs do not
 //   undersize it before the load arrives, and a steady load settles 6 % above its need).
+// * Floor: a large link never shrinks below min(its start, 64 MiB) (with the region's bare
+//   minimum as the floor, ~30 quiet exchanges took it to a few KiB and the next burst was dropped whole
+//   for two exchanges); a link whose worst case fits keeps its start, as before.
 // RAFTGPU_WIRE_CAP0 (tests) caps the start, to exercise the drop-and-grow path.
 static constexpr uint64_t WIRE_CAP_MAX = 4ull << 30;
 static constexpr uint32_t WIRE_WIN = 8;  // exchanges a capacity looks back over
@@ -2492,6 +2559,7 @@ static void wire_caps_init(rg_engine* e) {
     if (c > (long double)WIRE_CAP_MAX) c = (long double)WIRE_CAP_MAX;
     const uint64_t cap = (std::max<uint64_t>((uint64_t)c, wire_region_min(units)) + 255) & ~255ull;
     if ((long double)cap >= worst) floor = cap;  // the worst case fits: never below it, never a drop
+    else floor = std::max<uint64_t>(floor, std::min<uint64_t>(cap, WIRE_CAP_SMALL));  // idle-then-burst headroom
     return cap;
   };
   e->cap_s.assign(N, 0);
@@ -2660,7 +2728,10 @@ int rg_last_tick_traffic(rg_engine* e, rg_traffic* out) {
   if (e->t == 0) return fail(RG_EINVAL, "no tick has run");
   if (int jrc = join(e)) return jrc;
   HIPCHK(hipMemsetAsync(e->d_sum, 0, 64, e->stream));
-  HIPCHK(launch_traffic(params(e), e->d_sum, e->stream));
+  TickParams tp = params(e);  // the last tick's copy jobs: its appended entries
+  tp.job32 = e->job32[(e->t - 1) & 1];
+  tp.jcnt = e->jcnt[(e->t - 1) & 1];
+  HIPCHK(launch_traffic(tp, e->d_sum, e->stream));
   unsigned long long v[8] = {0};
   HIPCHK(hipMemcpyAsync(v, e->d_sum, 64, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));

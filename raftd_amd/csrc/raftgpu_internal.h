@@ -222,14 +222,13 @@ struct TickParams {
   uint32_t JS;             // join slots (rg_config.join_slots): bootstrap with an empty log, no membership
   uint64_t seed, tick;
   Placement pl;
-  RG_G(const uint64_t) s64_in;  // [S64_ROWS][nrep]
-  RG_G(uint64_t) s64_out;
-  RG_G(const uint32_t) s32_in;  // [S32_ROWS][nrep]
-  RG_G(uint32_t) s32_out;
-  RG_G(const uint64_t) rem_in;  // [3][R][nrep]: match, next, rsnap
-  RG_G(uint64_t) rem_out;
-  RG_G(const uint8_t) rst_in;   // [R][nrep]
-  RG_G(uint8_t) rst_out;
+  // replica state, one copy updated in place: a step reads its replica's rows and writes back only
+  // the fields it changed (the fast step: DESIGN.md §3 "In-place state"; r05 and earlier ping-ponged
+  // two copies and copied every unchanged field through)
+  RG_G(uint64_t) s64;           // [S64_ROWS][nrep]
+  RG_G(uint32_t) s32;           // [S32_ROWS][nrep]
+  RG_G(uint64_t) rem;           // [3][R][nrep]: match, next, rsnap
+  RG_G(uint8_t) rst;            // [R][nrep]
   RG_G(uint64_t) tr;            // term ring [L][nrep]
   RG_G(const uint64_t) hdr_in;  // [8][R src][R dst][K][G]
   RG_G(uint64_t) hdr_out;
@@ -243,7 +242,8 @@ struct TickParams {
   RG_G(const uint64_t) rmt;
   RG_G(const uint32_t) rcnt;
   RG_G(uint64_t) apply_lo;      // [nrep] first index this step hands to the state machine (NULL: skip)
-  RG_G(uint64_t) persist_lo;    // [nrep] lowest index written this step, ~0 if none (NULL: skip)
+  RG_G(uint64_t) persist_lo;    // [nrep] lowest index written this step; PERSIST_NONE if none and the hard
+                                //   state is unchanged, PERSIST_HS if none but the hard state changed (NULL: skip)
   RG_G(uint64_t) snap_ev;       // [nrep] restored_at | SNAP_TAKEN_BIT (NULL: skip)
   RG_G(uint32_t) prof;          // RG_CTL_PROFILE builds only: [6][nrep] s_memtime stamps per phase
   RG_G(uint64_t) job64;         // [J64_ROWS][J][nrep]
@@ -313,8 +313,7 @@ struct BulkParams {
 struct PoolParams {
   uint32_t nrep, PTS;
   uint64_t npages;
-  uint32_t* s32_out;           // the step's output state rows (S_HW, S_NLPG written by control)
-  const uint32_t* s32_in;      // S_LPG / S_APG before the step
+  uint32_t* s32;               // state rows: S_HW, S_NLPG (control's) in; S_LPG / S_APG out
   uint32_t* pt;                // [nrep][PTS] page ids
   uint32_t* fring;             // [npages] free page ids
   PoolCtl* ctl;
@@ -444,9 +443,14 @@ struct ApplyParams {
   uint64_t* bsum;           // scan scratch
   uint8_t* out_run;         // [runs] rg_apply_run (device staging)
   uint8_t* out_cmd;         // [n] rg_apply_cmd
-  uint8_t* out_pay;         // [chunks][16]
+  uint8_t* out_pay;         // [chunks][16]; NULL: by reference (no Cmd bytes; rg_get_update with
+                            // RG_UPDATE_PERSIST: the host holds every committed Cmd from a persist section)
 };
 hipError_t launch_apply_count(const ApplyParams& a, uint64_t* totals /*[3]: entries, chunks, runs*/, hipStream_t s);
+// persist_lo of a step that wrote no entry: PERSIST_NONE (hard state unchanged too) or PERSIST_HS (term,
+// vote, commit, last, marker or snapshot index changed). Either is above every log index, so the
+// entry window [persist_lo, last] is empty; with state in place there is no previous copy to diff
+constexpr uint64_t PERSIST_NONE = ~0ull, PERSIST_HS = ~0ull - 1;
 // snapshot events (raftgpu_apply.hip)
 constexpr uint64_t SNAP_TAKEN_BIT = 1ull << 63;
 struct SnapParams {
@@ -474,9 +478,8 @@ struct PersistParams {
   uint32_t slot_mask;        // replicas whose slot bit is set (a node's replicas; rg_persist_collect: all)
   Placement pl;
   const uint64_t* s64;       // current state
-  const uint64_t* s64_prev;  // state at the start of the last tick
   const uint32_t* s32;       // current state (membership)
-  const uint64_t* persist_lo;
+  const uint64_t* persist_lo;  // control's: the lowest index written, or PERSIST_NONE / PERSIST_HS
   const uint64_t* tr;
   const uint2* info;
   const uint8_t* pool;

@@ -98,10 +98,10 @@ __global__ void __launch_bounds__(POOL_BLOCK) pool_kernel(PoolParams pp) {
   const uint64_t n = pp.nrep, PTSM = pp.PTS - 1;
   uint32_t lpg = 0, apg = 0, nlpg = 0, top = 0, f = 0, a = 0;
   if (valid) {
-    lpg = pp.s32_in[S_LPG * n + q];
-    apg = pp.s32_in[S_APG * n + q];
-    nlpg = pp.s32_out[S_NLPG * n + q];
-    top = vpn_ceil(pp.s32_out[S_HW * n + q]);
+    lpg = pp.s32[S_LPG * n + q];
+    apg = pp.s32[S_APG * n + q];
+    nlpg = pp.s32[S_NLPG * n + q];
+    top = vpn_ceil(pp.s32[S_HW * n + q]);
     f = vpn_diff(nlpg, lpg);
     a = vpn_diff(top, apg);
   }
@@ -210,10 +210,10 @@ __global__ void __launch_bounds__(POOL_BLOCK) pool_kernel(PoolParams pp) {
       if (tk[j]) pp.pt[(uint64_t)row[j] * pp.PTS + slot[j]] = v[j];
   }
   if (valid) {
-    pp.s32_out[S_LPG * n + q] = nlpg;
-    pp.s32_out[S_APG * n + q] = ok ? top : apg;
+    pp.s32[S_LPG * n + q] = nlpg;
+    pp.s32[S_APG * n + q] = ok ? top : apg;
     if (!ok) {  // the pool is empty: this replica's appends of the step are not stored; the engine is poisoned
-      pp.s32_out[S_ERR * n + q] |= ERR_POOL;
+      pp.s32[S_ERR * n + q] |= ERR_POOL;
       pp.jcnt[q] = 0;
       atomicOr(&pp.ctl->fail, 1u);
     }
@@ -271,9 +271,9 @@ __global__ void bootstrap_kernel(TickParams p, uint2* info) {
   const uint32_t R = p.R, s = q / p.G, g = q - s * p.G;
   const uint64_t n = p.nrep;
   const bool joining = (p.JS >> s) & 1u;
-  uint64_t* a = p.s64_out + q;
+  uint64_t* a = p.s64 + q;
   for (uint32_t f = 0; f < S64_ROWS; ++f) a[f * n] = 0;
-  uint32_t* b = p.s32_out + q;
+  uint32_t* b = p.s32 + q;
   for (uint32_t f = 0; f < S32_ROWS; ++f) b[f * n] = 0;
   const uint32_t im = (p.IM ? p.IM : (1u << R) - 1u) & ~p.JS;  // initialMembers
   const uint64_t last = joining ? 0 : R;
@@ -288,10 +288,10 @@ __global__ void bootstrap_kernel(TickParams p, uint2* info) {
   const uint64_t key = (pl_group(p.pl, s, g) << 32) | ((uint64_t)s << 24) | 1ull;
   b[S_RAND_TO * n] = p.ET + (uint32_t)(mix64(p.seed ^ mix64(key)) % p.ET);
   for (uint32_t j = 0; j < R; ++j) {  // addNode → setRemote(id, 0, last+1)
-    p.rem_out[(0 * R + j) * n + q] = 0;
-    p.rem_out[(1 * R + j) * n + q] = last + 1;
-    p.rem_out[(2 * R + j) * n + q] = 0;
-    p.rst_out[j * n + q] = RETRY;
+    p.rem[(0 * R + j) * n + q] = 0;
+    p.rem[(1 * R + j) * n + q] = last + 1;
+    p.rem[(2 * R + j) * n + q] = 0;
+    p.rst[j * n + q] = RETRY;
   }
   for (uint32_t i = 1; i <= last; ++i) {
     const uint64_t slot = i & (p.L - 1);
@@ -440,7 +440,7 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t a) {
   return a;
 }
 
-// Σ_g max_s committed, on the state a next tick would read (s64_in). With ranks > 1 the replicas
+// Σ_g max_s committed, on the state a next tick would read (s64). With ranks > 1 the replicas
 // of a column belong to different groups: sum the slot-0 replicas hosted here (each group's slot 0
 // lives on exactly one rank, so the sum over ranks counts every group once).
 __global__ void sum_committed_kernel(TickParams p, unsigned long long* out) {
@@ -448,7 +448,7 @@ __global__ void sum_committed_kernel(TickParams p, unsigned long long* out) {
   const uint32_t ns = p.pl.N > 1 ? 1u : p.R;
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < p.G; g += gridDim.x * blockDim.x) {
     uint64_t m = 0;
-    for (uint32_t s = 0; s < ns; ++s) m = umax64(m, p.s64_in[(uint64_t)S_COMMITTED * p.nrep + (uint64_t)s * p.G + g]);
+    for (uint32_t s = 0; s < ns; ++s) m = umax64(m, p.s64[(uint64_t)S_COMMITTED * p.nrep + (uint64_t)s * p.G + g]);
     acc += m;
   }
   acc = wave_sum64(acc);
@@ -461,14 +461,15 @@ hipError_t launch_sum_committed(const TickParams& p, unsigned long long* out, hi
 }
 
 // Last tick's traffic: leaders, msgs, replicate entries, appended, leader-appended.
-// p is the parameter block a next tick would use: s64_in = current state, s64_out = previous
-// state, cnt_in/hdr_in = the last tick's outbox.
+// p is the parameter block a next tick would use (s64 = current state, cnt_in/hdr_in = the last
+// tick's outbox) with job32 / jcnt pointed at the last tick's copy jobs: a replica's appended
+// entries are its jobs' entry counts (what the bulk kernel moved for it).
 __global__ void traffic_kernel(TickParams p, unsigned long long* out6) {
   uint64_t v[5] = {0, 0, 0, 0, 0};
-  const uint64_t n = p.nrep;
+  const uint64_t n = p.nrep, JN = (uint64_t)p.J * n;
   for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < p.nrep; q += gridDim.x * blockDim.x) {
     const uint32_t s = q / p.G, g = q - s * p.G;
-    const bool ld = p.s32_in[S_ROLE * n + q] == LEADER;
+    const bool ld = p.s32[S_ROLE * n + q] == LEADER;
     v[0] += ld;
     for (uint32_t d = 0; d < p.R; ++d) {
       const uint32_t c = p.cnt_in[((uint64_t)s * p.R + d) * p.G + g];
@@ -478,8 +479,12 @@ __global__ void traffic_kernel(TickParams p, unsigned long long* out6) {
         if ((w0 & 0xFF) == M_REPLICATE) v[2] += w0 >> 32;
       }
     }
-    const uint64_t lc = p.s64_in[S_LAST * n + q], lp = p.s64_out[S_LAST * n + q];
-    const uint64_t app = lc > lp ? lc - lp : 0;
+    uint64_t app = 0;
+    const uint32_t nj = p.jcnt[q] < p.J ? p.jcnt[q] : p.J;
+    for (uint32_t j = 0; j < nj; ++j) {
+      const uint32_t m = p.job32[J_META * JN + (uint64_t)j * n + q];
+      app += (m & 0xFF) - ((m >> 8) & 0xFF);
+    }
     v[3] += app;
     if (ld) v[4] += app;
   }

@@ -254,6 +254,54 @@ class Update(C.Structure):
 
 
 UPDATE_PERSIST, UPDATE_COMMITTED, UPDATE_SNAPSHOTS, UPDATE_READS, UPDATE_ALL, UPDATE_FULL_STATE = 1, 2, 4, 8, 15, 16
+UPDATE_COMMITTED_CMDS = 32  # ship the committed Cmds even with the persist section (no by-reference)
+
+
+class PersistedCmds:
+    """The host's copy of the Cmds an update stream persisted, kept until their replica applied them: what
+    resolves rg_get_update's committed section when it comes by reference (RG_UPDATE_PERSIST together with
+    RG_UPDATE_COMMITTED, include/raftgpu.h). dragonboat hands Update its entries from its own in-memory log
+    the same way. Per replica {index: Cmd bytes}; a state record's window rewrites it (entries at or above
+    its `first` are replaced, those above `last` or at or below `marker` dropped), and an entry handed to
+    the state machine is dropped with everything below it."""
+
+    def __init__(self):
+        self.log = {}
+
+    def persist(self, states, entries, payload):
+        for st in states:
+            rid, first, last, marker = int(st["rid"]), int(st["first"]), int(st["last"]), int(st["marker"])
+            d = self.log.setdefault(rid, {})
+            for i in [i for i in d if i >= first or i > last or i <= marker]:
+                del d[i]
+        for e in entries:
+            if e["type"] == 0:  # application entries (a ConfigChange carries no Cmd)
+                o, n = int(e["off"]), int(e["len"])
+                self.log.setdefault(int(e["rid"]), {})[int(e["index"])] = bytes(payload[o:o + n])
+
+    def resolve(self, runs, cmds):
+        """The packed payload a by-reference committed section stands for: each Cmd at its run's off plus
+        the 16-B-rounded lengths of the run's earlier entries (as rg_apply_committed would ship it)."""
+        if not len(runs):
+            return np.zeros(0, np.uint8)
+        end = max(int(r["off"]) + sum((int(cmds[int(r["entry"]) + k]["len"]) + 15) // 16 * 16
+                                      for k in range(int(r["count"]))) for r in runs)
+        out = np.zeros(end, np.uint8)
+        for r in runs:
+            rid, first, at = int(r["rid"]), int(r["first"]), int(r["off"])
+            d = self.log.get(rid, {})
+            for k in range(int(r["count"])):
+                n = int(cmds[int(r["entry"]) + k]["len"])
+                cmd = d.get(first + k)
+                if cmd is None or len(cmd) != n:
+                    raise KeyError(f"committed entry {first + k} of replica {rid} was never persisted in this "
+                                   f"update stream (RG_UPDATE_COMMITTED_CMDS ships it)")
+                out[at:at + n] = np.frombuffer(cmd, np.uint8)
+                at += (n + 15) // 16 * 16
+            last = first + int(r["count"]) - 1
+            for i in [i for i in d if i <= last]:  # handed to the state machine
+                del d[i]
+        return out
 COMMIT_APPLIED = 1
 
 
@@ -285,9 +333,18 @@ EXPORTS = ["rg_create", "rg_destroy", "rg_bootstrap", "rg_fill_slabs", "rg_tick"
            "rg_notify_applied", "rg_apply_async", "rg_apply_wait", "rg_read_index", "rg_read_index_results",
            "rg_config_change", "rg_wire_exchange", "rg_rccl_unique_id", "rg_rccl_open", "rg_rccl_close",
            "rg_pool_stats", "rg_get_update", "rg_commit_update", "rg_tick_device_n", "rg_digest",
-           "rg_host_register", "rg_host_unregister", "rg_wire_plan_fixed", "rg_wire_dropped", "rg_compact"]
+           "rg_host_register", "rg_host_unregister", "rg_wire_plan_fixed", "rg_wire_dropped", "rg_compact",
+           "rg_timing_epoch", "rg_kernel_events"]
 
 _lib = None
+
+
+def timing_epoch(device: int) -> None:
+    """rg_timing_epoch: the process's reference event on `device`; launches timed afterwards by any
+    engine there carry start / end times on that one timeline (Engine.kernel_events)."""
+    rc = load_library().rg_timing_epoch(int(device))
+    if rc != 0:
+        raise RuntimeError(f"rg_timing_epoch: {load_library().rg_last_error().decode()}")
 
 
 def load_library(path: str = LIB_PATH):
@@ -322,6 +379,8 @@ def load_library(path: str = LIB_PATH):
         "rg_join": ([vp], i32),
         "rg_timing": ([vp, i32], i32),
         "rg_kernel_ms": ([vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64)], i32),
+        "rg_timing_epoch": ([i32], i32),
+        "rg_kernel_events": ([vp, i32, vp, vp, vp, u64, C.POINTER(C.c_uint64)], i32),
         "rg_tick_count": ([vp], u64),
         "rg_read_replicas": ([vp, u32, u32, C.POINTER(ReplicaView)], i32),
         "rg_read_msgs": ([vp, u32, u32, C.POINTER(MsgView), u32, C.POINTER(C.c_uint64)], i32),
@@ -494,6 +553,18 @@ class Engine:
         n = (C.c_uint64 * 2)()
         self._check(self.L.rg_kernel_ms(self.h, ms, n))
         return {"control": (ms[0], n[0]), "bulk": (ms[1], n[1])}
+
+    def kernel_events(self, kernel: str = "bulk"):
+        """Timed launches since timing(True) as {tick, start, end} (ms after the process's
+        rg_timing_epoch): launches of engines on different streams on one timeline."""
+        import numpy as np
+        k = 0 if kernel == "control" else 1
+        n = C.c_uint64()
+        self._check(self.L.rg_kernel_events(self.h, k, None, None, None, 0, C.byref(n)))
+        ticks, a, b = np.zeros(n.value, np.uint64), np.zeros(n.value), np.zeros(n.value)
+        self._check(self.L.rg_kernel_events(self.h, k, ticks.ctypes.data, a.ctypes.data, b.ctypes.data, n.value,
+                                            C.byref(n)))
+        return ticks, a, b
 
     @property
     def t(self) -> int:
@@ -746,7 +817,10 @@ class Engine:
 
     def get_update(self, slot_mask: int = 0xFF, flags: int = UPDATE_ALL):
         """rg_get_update: the last tick's whole hand-off in one call. Returns (raw rg_update, dict of
-        numpy copies: states, entries, entry_payload, committed, committed_payload, snapshots, reads)."""
+        numpy copies: states, entries, entry_payload, committed, committed_payload, snapshots, reads).
+        With the persist and committed sections together the committed Cmds come by reference (each
+        crosses PCIe once) and are resolved from this engine's PersistedCmds (`committed_by_reference`):
+        call it after every tick with the same slot mask, as a daemon's Update loop does."""
         u = Update()
         self._check(self.L.rg_get_update(self.h, slot_mask, flags, C.byref(u)))
 
@@ -761,6 +835,14 @@ class Engine:
                "snapshots": arr(u.snapshots, u.n_snapshots, SNAPSHOT_EVENT_DTYPE),
                "reads": arr(u.reads, u.n_reads, READ_READY_DTYPE)}
         runs, cmds, out["committed_payload"] = batch_arrays(u.committed)
+        by_ref = bool(u.committed.n_entries) and not u.committed.payload
+        if flags & UPDATE_PERSIST:
+            if not hasattr(self, "_persisted"):
+                self._persisted = PersistedCmds()
+            self._persisted.persist(st, out["entries"], epay)
+        if by_ref:
+            out["committed_payload"] = self._persisted.resolve(runs, cmds)
+        out["committed_by_reference"] = by_ref
         out["committed"] = expand_apply(runs, cmds)
         out["committed_runs"] = runs
         return u, out

@@ -20,7 +20,7 @@ for what in ${STEPS:-smoke parity tests bench wire rehearse}; do
     profile) step profile 1000 bash scripts/profile.sh ${PTAG:-r03} ;;
     shapes) step shapes 600 bash scripts/shapes.sh ;;
     copywg) step copywg 900 bash scripts/e2e_copywg.sh ;;
-    mj) step mj 600 bash -c 'for v in 0 1; do RAFTGPU_BULK_MULTIJOB=$v timeout -k 10 200 python bench.py --no-cpu-baseline --steps 20 --warmup 5 > gpurun_out/mj_$v.log 2>&1 || exit 1; RAFTGPU_BULK_MULTIJOB=$v timeout -k 10 200 python bench.py --no-cpu-baseline --groups 1048576 --entries 1 --steps 10 --warmup 3 > gpurun_out/mj_c5_$v.log 2>&1 || exit 1; done' ;;
+    mj) echo "mj: retired (RAFTGPU_BULK_MULTIJOB is a build variant now: scripts/build_variant.sh -DRG_AB_BULK_MULTIJOB=0/1)"; exit 1 ;;
     rehearse_c) step rehearse_c 400 python bench.py --placement spread --wire-all --exchange c --no-cpu-baseline --steps 10 --warmup 3 ;;
     sdma) step sdma 300 env RAFTGPU_APPLY_SDMA=1 python bench.py --steps 12 --warmup 3 --no-cpu-baseline ;;
     wire) step bench_wire 400 python bench.py --wire-all --no-cpu-baseline ;;

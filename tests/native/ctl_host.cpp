@@ -19,11 +19,13 @@ struct Host {
   uint64_t slow_lanes = 0;  // lanes the fast path handed off (all ticks)
   rg_config c;
   uint32_t nrep, J;
-  std::vector<uint64_t> s64[2], rem[2], tr, hdr[2], mt[2], job64;
+  std::vector<uint64_t> s64, rem, tr, hdr[2], mt[2], job64;  // state rows in place, as on the device
   std::vector<uint2> info;        // [2 banks][nrep][L] {crc (0 here), stream position}
   uint32_t PTS = 16;
-  std::vector<uint32_t> s32[2], cnt[2], job32, jcnt;
-  std::vector<uint8_t> rst[2];
+  std::vector<uint32_t> s32, cnt[2], job32, jcnt;
+  std::vector<uint8_t> rst;
+  uint64_t violations = 0;  // ch_violations: state invariants broken after a step, or a fast step that
+                            // handed off after writing state (its in-place rows must be untouched)
   std::vector<uint2> slab_info;  // [nslab][G][E] {0, len}: synthetic Cmds are P bytes; ch_propose sets lengths
   std::vector<uint64_t> rdst;     // ReadIndex state rows
   std::vector<uint64_t> rd;       // rg_read_index staging: ctx per (group, slot), 0 = none
@@ -64,10 +66,7 @@ static TickParams params(Host* h) {
     p.rcnt = h->rcnt.data();
   }
   const int a = (int)(h->t & 1), b = a ^ 1;
-  p.s64_in = h->s64[a].data(); p.s64_out = h->s64[b].data();
-  p.s32_in = h->s32[a].data(); p.s32_out = h->s32[b].data();
-  p.rem_in = h->rem[a].data(); p.rem_out = h->rem[b].data();
-  p.rst_in = h->rst[a].data(); p.rst_out = h->rst[b].data();
+  p.s64 = h->s64.data(); p.s32 = h->s32.data(); p.rem = h->rem.data(); p.rst = h->rst.data();
   p.tr = h->tr.data();
   p.hdr_in = h->hdr[b].data(); p.hdr_out = h->hdr[a].data();
   p.mt_in = h->mt[b].data(); p.mt_out = h->mt[a].data();
@@ -92,11 +91,11 @@ void* ch_create(const rg_config* c) {
   h->J = (c->replicas - 1) * c->max_msgs_per_pair + 2;
   const size_t n = h->nrep, L = c->log_capacity, R = c->replicas, K = c->max_msgs_per_pair,
                E = c->max_entries_per_msg, G = c->groups, J = h->J;
+  h->s64.assign(S64_ROWS * n, 0);
+  h->s32.assign(S32_ROWS * n, 0);
+  h->rem.assign(3 * R * n, 0);
+  h->rst.assign(R * n, 0);
   for (int b = 0; b < 2; ++b) {
-    h->s64[b].assign(S64_ROWS * n, 0);
-    h->s32[b].assign(S32_ROWS * n, 0);
-    h->rem[b].assign(3 * R * n, 0);
-    h->rst[b].assign(R * n, 0);
     h->hdr[b].assign(8 * R * R * K * G, 0);
     h->mt[b].assign(R * R * K * E * G, 0);
     h->cnt[b].assign(R * R * G, 0);
@@ -133,6 +132,7 @@ void ch_destroy(void* hh) { delete (Host*)hh; }
 // the fast path (control_fast_kernel + control_slow_kernel on the device): on = 1
 void ch_set_fast(void* hh, int on) { ((Host*)hh)->fast = on; }
 uint64_t ch_slow_lanes(void* hh) { return ((Host*)hh)->slow_lanes; }
+uint64_t ch_violations(void* hh) { return ((Host*)hh)->violations; }
 
 // placement math of raftgpu_internal.h, for the CPU cross-check with raftd_amd/cluster.py
 uint64_t ch_pl_group(uint32_t N, uint32_t rank, uint32_t s, uint32_t j) {
@@ -151,23 +151,23 @@ void ch_bootstrap(void* hh) {  // = bootstrap_kernel
     const uint32_t s = q / h->c.groups, g = q - s * h->c.groups;
     const bool joining = (JS >> s) & 1u;
     const uint64_t last = joining ? 0 : R;
-    for (uint32_t f = 0; f < S64_ROWS; ++f) h->s64[0][f * n + q] = 0;
-    for (uint32_t f = 0; f < S32_ROWS; ++f) h->s32[0][f * n + q] = 0;
-    h->s64[0][S_TERM * n + q] = joining ? 0 : 1;
-    h->s64[0][S_LAST * n + q] = last;
-    h->s64[0][S_LAST_TERM * n + q] = last ? 1 : 0;
-    h->s64[0][S_COMMITTED * n + q] = last;
-    h->s64[0][S_CC_HI * n + q] = last;
-    h->s32[0][S_RNG_CTR * n + q] = 1;
-    h->s32[0][S_MEMBERS * n + q] = joining ? 0u : im;
-    h->s32[0][S_SNAP_MEMBERS * n + q] = joining ? 0u : im;
+    for (uint32_t f = 0; f < S64_ROWS; ++f) h->s64[f * n + q] = 0;
+    for (uint32_t f = 0; f < S32_ROWS; ++f) h->s32[f * n + q] = 0;
+    h->s64[S_TERM * n + q] = joining ? 0 : 1;
+    h->s64[S_LAST * n + q] = last;
+    h->s64[S_LAST_TERM * n + q] = last ? 1 : 0;
+    h->s64[S_COMMITTED * n + q] = last;
+    h->s64[S_CC_HI * n + q] = last;
+    h->s32[S_RNG_CTR * n + q] = 1;
+    h->s32[S_MEMBERS * n + q] = joining ? 0u : im;
+    h->s32[S_SNAP_MEMBERS * n + q] = joining ? 0u : im;
     const uint64_t key = ((uint64_t)g << 32) | ((uint64_t)s << 24) | 1ull;
-    h->s32[0][S_RAND_TO * n + q] = h->c.election_rtt + (uint32_t)(mix64(h->c.seed ^ mix64(key)) % h->c.election_rtt);
+    h->s32[S_RAND_TO * n + q] = h->c.election_rtt + (uint32_t)(mix64(h->c.seed ^ mix64(key)) % h->c.election_rtt);
     for (uint32_t j = 0; j < R; ++j) {
-      h->rem[0][(0 * R + j) * n + q] = 0;
-      h->rem[0][(1 * R + j) * n + q] = last + 1;
-      h->rem[0][(2 * R + j) * n + q] = 0;
-      h->rst[0][j * n + q] = RETRY;
+      h->rem[(0 * R + j) * n + q] = 0;
+      h->rem[(1 * R + j) * n + q] = last + 1;
+      h->rem[(2 * R + j) * n + q] = 0;
+      h->rst[j * n + q] = RETRY;
     }
     for (uint32_t i = 1; i <= last; ++i) {
       const uint32_t cc = ((im >> (i - 1)) & 1u) ? (CC_ADD << 4 | i) : 0u;
@@ -182,7 +182,7 @@ void ch_bootstrap(void* hh) {  // = bootstrap_kernel
 // from the job's J_DPOS, as the bulk kernel lays them out)
 static void after_step(Host* h, const TickParams& p) {
   const uint64_t n = h->nrep, L = h->c.log_capacity, JN = (uint64_t)h->J * n;
-  uint32_t* so = const_cast<uint32_t*>(p.s32_out);
+  uint32_t* so = const_cast<uint32_t*>(p.s32);
   for (uint64_t q = 0; q < n; ++q) {
     so[S_LPG * n + q] = so[S_NLPG * n + q];
     so[S_APG * n + q] = vpn_ceil(so[S_HW * n + q]);
@@ -258,11 +258,49 @@ static bool fast_role(const TickParams& p, uint32_t q) {
   f.run();
   return f.aborted;
 }
+// replica q's state rows (the in-place state a handed-off fast step must leave untouched)
+struct LaneRows {
+  uint64_t v[S64_ROWS + S32_ROWS + 4 * RG_MAX_REPLICAS];
+  uint32_t n = 0;
+  bool operator!=(const LaneRows& o) const { return n != o.n || memcmp(v, o.v, n * 8) != 0; }
+};
+template <class H>
+static void lane_state(H* h, uint32_t q, LaneRows& o) {
+  const uint64_t n = h->nrep, R = h->c.replicas;
+  o.n = 0;
+  for (uint32_t f = 0; f < S64_ROWS; ++f) o.v[o.n++] = h->s64[f * n + q];
+  for (uint32_t f = 0; f < S32_ROWS; ++f) o.v[o.n++] = h->s32[f * n + q];
+  for (uint32_t j = 0; j < 3 * R; ++j) o.v[o.n++] = h->rem[j * n + q];
+  for (uint32_t j = 0; j < R; ++j) o.v[o.n++] = h->rst[j * n + q];
+}
 template <int R, class H>
 static bool fast_step(H* h, const TickParams& p, uint32_t q) {
-  const bool lead = p.s32_in[(uint64_t)S_ROLE * p.nrep + q] == LEADER;
-  if (h->fast == 2) return lead ? fast_role<R, LEADER, true>(p, q) : fast_role<R, FOLLOWER, true>(p, q);
-  return lead ? fast_role<R, LEADER, false>(p, q) : fast_role<R, FOLLOWER, false>(p, q);
+  const bool lead = p.s32[(uint64_t)S_ROLE * p.nrep + q] == LEADER;
+  LaneRows before, after;
+  lane_state(h, q, before);
+  bool ab;
+  if (h->fast == 2) ab = lead ? fast_role<R, LEADER, true>(p, q) : fast_role<R, FOLLOWER, true>(p, q);
+  else ab = lead ? fast_role<R, LEADER, false>(p, q) : fast_role<R, FOLLOWER, false>(p, q);
+  if (ab) {  // the full step re-runs it from these rows
+    lane_state(h, q, after);
+    if (after != before) h->violations++;
+  }
+  return ab;
+}
+// After every step: S_LAST_TERM caches term(last) (marker_term on an empty log), the pool's
+// bookkeeping left S_NLPG = S_LPG (the fast step's in-place store skips an unchanged S_NLPG), and a remote's
+// snapshot index is 0 outside the SNAPSHOT state (the fast step neither reads nor writes it)
+template <class H>
+static void check_invariants(H* h) {
+  const uint64_t n = h->nrep, R = h->c.replicas, L = h->c.log_capacity;
+  for (uint64_t q = 0; q < n; ++q) {
+    const uint64_t last = h->s64[S_LAST * n + q], marker = h->s64[S_MARKER * n + q];
+    const uint64_t want = last > marker ? h->tr[(last & (L - 1)) * n + q] & TERM_MASK : h->s64[S_MARKER_TERM * n + q];
+    if (h->s64[S_LAST_TERM * n + q] != want) h->violations++;
+    if (h->s32[S_NLPG * n + q] != h->s32[S_LPG * n + q]) h->violations++;
+    for (uint64_t j = 0; j < R; ++j)
+      if (h->rst[j * n + q] != SNAPSHOT && h->rem[(2 * R + j) * n + q] != 0) h->violations++;
+  }
 }
 }  // extern "C++"
 
@@ -310,6 +348,7 @@ int ch_tick(void* hh, const rg_tick_input* in) {
     }
   }
   after_step(h, p);
+  check_invariants(h);
   h->t++;
   if (h->staged) {
     std::fill(h->pt.begin(), h->pt.end(), 0xFF);
@@ -381,7 +420,7 @@ int ch_propose(void* hh, const rg_proposal* props, uint64_t n, const uint32_t* l
 int ch_notify_applied(void* hh, uint32_t rid, uint64_t index) {
   Host* h = (Host*)hh;
   const uint64_t q = qof(h, rid), N = h->nrep;
-  uint64_t* s64 = h->s64[h->t & 1].data() + q;
+  uint64_t* s64 = h->s64.data() + q;
   if (index > s64[S_PROCESSED * N]) return -1;
   s64[S_APPLIED * N] = index;
   return 0;
@@ -391,9 +430,8 @@ int ch_read_replica(void* hh, uint32_t rid, rg_replica_view* v) {
   Host* h = (Host*)hh;
   const uint32_t q = qof(h, rid);
   const uint64_t N = h->nrep;
-  const int a = (int)(h->t & 1);
-  const uint64_t* s64 = h->s64[a].data() + q;
-  const uint32_t* s32 = h->s32[a].data() + q;
+  const uint64_t* s64 = h->s64.data() + q;
+  const uint32_t* s32 = h->s32.data() + q;
   memset(v, 0, sizeof *v);
   v->term = s64[S_TERM * N]; v->vote = s64[S_VOTE * N]; v->leader = s64[S_LEADER * N];
   v->committed = s64[S_COMMITTED * N]; v->applied = s64[S_APPLIED * N]; v->last = s64[S_LAST * N];
@@ -406,10 +444,10 @@ int ch_read_replica(void* hh, uint32_t rid, rg_replica_view* v) {
   v->members = s32[S_MEMBERS * N]; v->snap_members = s32[S_SNAP_MEMBERS * N]; v->cc_pending = s32[S_CC_PENDING * N];
   const uint32_t R = h->c.replicas;
   for (uint32_t j = 0; j < R; ++j) {
-    v->match[j] = h->rem[a][(0 * R + j) * N + q];
-    v->next[j] = h->rem[a][(1 * R + j) * N + q];
-    v->rsnap[j] = h->rem[a][(2 * R + j) * N + q];
-    v->rstate[j] = h->rst[a][j * N + q];
+    v->match[j] = h->rem[(0 * R + j) * N + q];
+    v->next[j] = h->rem[(1 * R + j) * N + q];
+    v->rsnap[j] = h->rem[(2 * R + j) * N + q];
+    v->rstate[j] = h->rst[j * N + q];
   }
   return 0;
 }
@@ -453,9 +491,8 @@ int ch_import(void* hh, uint32_t rid, const rg_replica_view* v, const uint64_t* 
   Host* h = (Host*)hh;
   const uint32_t q = qof(h, rid);
   const uint64_t N = h->nrep;
-  const int a = (int)(h->t & 1);
-  uint64_t* s64 = h->s64[a].data() + q;
-  uint32_t* s32 = h->s32[a].data() + q;
+  uint64_t* s64 = h->s64.data() + q;
+  uint32_t* s32 = h->s32.data() + q;
   s64[S_TERM * N] = v->term; s64[S_VOTE * N] = v->vote; s64[S_LEADER * N] = v->leader;
   s64[S_COMMITTED * N] = v->committed; s64[S_APPLIED * N] = v->applied; s64[S_LAST * N] = v->last;
   s64[S_MARKER * N] = v->marker; s64[S_MARKER_TERM * N] = v->marker_term; s64[S_SNAP_INDEX * N] = v->snap_index;
@@ -470,10 +507,10 @@ int ch_import(void* hh, uint32_t rid, const rg_replica_view* v, const uint64_t* 
   s64[S_FIDX * N] = 0;
   const uint32_t R = h->c.replicas;
   for (uint32_t j = 0; j < R; ++j) {
-    h->rem[a][(0 * R + j) * N + q] = v->match[j];
-    h->rem[a][(1 * R + j) * N + q] = v->next[j];
-    h->rem[a][(2 * R + j) * N + q] = v->rsnap[j];
-    h->rst[a][j * N + q] = v->rstate[j];
+    h->rem[(0 * R + j) * N + q] = v->match[j];
+    h->rem[(1 * R + j) * N + q] = v->next[j];
+    h->rem[(2 * R + j) * N + q] = v->rsnap[j];
+    h->rst[j * N + q] = v->rstate[j];
   }
   uint32_t pos = 0;  // a fresh payload stream from position 0 (rg_import_replica)
   for (uint64_t i = v->marker + 1; i <= v->last; ++i) {

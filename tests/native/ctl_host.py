@@ -58,6 +58,8 @@ class CtlHost:
         self.L.ch_set_fast.argtypes = [vp, C.c_int]
         self.L.ch_slow_lanes.argtypes = [vp]
         self.L.ch_slow_lanes.restype = C.c_uint64
+        self.L.ch_violations.argtypes = [vp]
+        self.L.ch_violations.restype = C.c_uint64
         self.L.ch_set_fast(C.c_void_p(self.h), int(fast))
         self.G, self.R = self.cfg["groups"], self.cfg["replicas"]
         self.nrep = self.G * self.R
@@ -95,6 +97,9 @@ class CtlHost:
                 keep.append(a)
                 setattr(ti, name, a.ctypes.data)
         assert self.L.ch_tick(C.c_void_p(self.h), C.byref(ti)) == 0
+        # the state is updated in place: a handed-off fast step must have left its rows untouched, and
+        # the cached rows (S_LAST_TERM, S_NLPG, remote snapshot indices) must agree with what they cache
+        assert self.L.ch_violations(C.c_void_p(self.h)) == 0, "ctl_host: in-place state invariant broken"
 
     def replica(self, rid) -> dict:
         from raftd_amd.engine import REPLICA_FIELDS

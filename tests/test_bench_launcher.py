@@ -31,3 +31,28 @@ def test_gpus_four_spawns_four_ranks():
 def test_world_size_mismatch_is_an_error():
     r = _run(["--gpus", "2", "--dry-run"], env={"WORLD_SIZE": "3", "RANK": "0"})
     assert r.returncode == 2 and "WORLD_SIZE 3" in r.stderr
+
+
+def test_transport_label_names_the_exchange_that_ran():
+    """the N > 1 line's `parallelism` label and exchange.transport come from one function
+    of --exchange / backend / sizing, so the label cannot name a transport the step did not use."""
+    sys.path.insert(0, ROOT)
+    import bench
+    t = bench.exchange_transport(True, False, "torch", "nccl", True)
+    assert "batch_isend_irecv" in t and "rg_wire_exchange" not in t and "fixed-capacity" in t
+    c = bench.exchange_transport(True, False, "c", "nccl", True)
+    assert "rg_wire_exchange" in c and "ncclSend" in c and "batch_isend_irecv" not in c
+    assert "gloo" in bench.exchange_transport(True, False, "c", "gloo", False)
+    assert "exactly sized" in bench.exchange_transport(True, False, "torch", "nccl", False)
+    assert "gloo" in bench.exchange_transport(True, False, "torch", "gloo", True)
+    assert bench.exchange_transport(False, True, "torch", "nccl", True) == "device copy (one engine)"
+    assert bench.exchange_transport(False, False, "torch", "nccl", True) is None
+
+
+def test_xgmi_bound():
+    """exchange.bound_ms: the busiest rank's bytes over its N - 1 links at XGMI_LINK_GBS each."""
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.xgmi_bound_ms(1.34e9, 1) is None
+    assert abs(bench.xgmi_bound_ms(1.34e9, 2) - 1.34e9 / 153e9 * 1e3) < 1e-9
+    assert abs(bench.xgmi_bound_ms(2.1e9, 8) - 2.1e9 / (7 * 153e9) * 1e3) < 1e-9

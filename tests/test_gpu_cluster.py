@@ -455,6 +455,33 @@ def test_fixed_capacity_overflow_drops_units_and_grows():
     assert np.median([max(views[g * R + s]["committed"] for s in range(R)) for g in range(G)]) > 200
 
 
+def test_fixed_capacity_keeps_a_floor_through_idle():
+    """a large link (its worst case above 64 MiB) starts at the steady bound and shrinks while
+    the load is low, but never below min(its start, 64 MiB). 50 idle exchanges (heartbeats only), then
+    full 64-entry batches of 256-B Cmds (a ~36-MB burst): nothing is dropped and the batches commit."""
+    from raftd_amd.engine import Engine
+    G, R, E = 1024, 3, 64
+    eng = Engine(wire_all=1, groups=G, replicas=R, log_capacity=512, payload_bytes=256, max_entries_per_msg=E,
+                 seed=98)
+    calls = []
+    t = _copy_transport(calls)
+    eng.bootstrap()
+    camp = np.zeros(G * R, np.uint8)
+    camp[0::R] = 1
+    pt, pc = np.zeros(G, np.uint8), np.full(G, E, np.uint32)
+    for k in range(60):  # bring-up, then idle
+        if k:
+            eng.wire_exchange(t.t)
+        eng.tick(*((None, None, camp) if k == 1 else ()))
+    c0 = eng.sum_committed()
+    for k in range(8):  # the burst
+        eng.wire_exchange(t.t)
+        eng.tick(pt, pc)
+    eng.sync()
+    assert t.error is None and eng.wire_dropped() == 0
+    assert eng.sum_committed() - c0 >= G * E * 5
+
+
 @pytest.mark.parametrize("ranks", [3, 1])
 def test_control_fast_path_covers_the_wire_steady_state(ranks):
     """Replicas spread over ranks (3: every follower on another rank than its leader; 1 with wire_all:

@@ -206,3 +206,52 @@ def test_get_update_against_oracle():
         for rid in range(G * R):
             assert gpu.replica(rid) == ora.replica(rid), (t, rid)
     assert all(v > 0 for v in seen.values()), seen
+
+
+def test_committed_section_by_reference():
+    """with the persist section in the same hand-off the committed section carries runs
+    and {len, crc} only (its Cmds crossed PCIe once already, in this or an earlier persist section); the host
+    resolves them from what it persisted. Two engines on one trace: A asks for the Cmds to be shipped
+    (RG_UPDATE_COMMITTED_CMDS), B takes them by reference — the raw section has no payload, and the Cmds B
+    resolves are A's bytes; only the persist section's Cmds crossed for B."""
+    import ctypes as C
+    from raftd_amd.engine import UPDATE_ALL, UPDATE_COMMITTED_CMDS, Update
+    G, R, MASK = 10, 3, 0b001
+    cfg = dict(groups=G, replicas=R, log_capacity=128, payload_bytes=64, max_cmd_bytes=500, max_entries_per_msg=8,
+               snapshot_entries=20, compaction_overhead=3, drop_ppm=20000, seed=0xB1F)
+    a, b = make("gpu", **cfg), make("gpu", **cfg)
+    for e in (a, b):
+        e.bootstrap()
+    rng = np.random.default_rng(21)
+    camp = np.zeros(G * R, np.uint8)
+    camp[0::R] = 1
+    shipped = resolved = 0
+    for t in range(60):
+        batches = []
+        if t >= 4:
+            for g in range(G):
+                if rng.random() < 0.8:
+                    cmds = [bytes(rng.integers(0, 256, int(rng.integers(0, 501)), dtype=np.uint8))
+                            for _ in range(int(rng.integers(1, 5)))]
+                    batches.append((g, int(rng.integers(0, R)), cmds))
+        for e in (a, b):
+            if batches:
+                e.propose(batches)
+            e.tick(campaign=camp if t == 1 else None)
+        ua, oa = a.get_update(MASK, UPDATE_ALL | UPDATE_COMMITTED_CMDS)
+        ub, ob = b.get_update(MASK)
+        assert not oa["committed_by_reference"]
+        assert oa["committed"].tobytes() == ob["committed"].tobytes(), t
+        if len(ob["committed"]):
+            assert ob["committed_by_reference"] and ub.committed.payload is None and ub.committed.payload_bytes == 0
+            assert np.array_equal(unpack_rows(oa["committed"], oa["committed_payload"], a.row),
+                                  unpack_rows(ob["committed"], ob["committed_payload"], b.row)), t
+            shipped += ua.committed.payload_bytes
+            resolved += len(ob["committed"])
+        for e, u in ((a, ua), (b, ub)):
+            e.commit_update(u, applied=True)
+    assert resolved > 200 and shipped > 0
+    # the raw C call: the same flags, no payload pointer, nothing but run heads and {len, crc} for the section
+    u = Update()
+    assert b.L.rg_get_update(b.h, MASK, UPDATE_ALL, C.byref(u)) == 0
+    assert u.committed.payload_bytes == 0
