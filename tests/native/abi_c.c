@@ -57,12 +57,30 @@
     }                                                                  \
   } while (0)
 
-/* IOnDiskStateMachine.Update from a copy-back batch, the way a cgo shim walks it: per run, entry k is
- * index first + k, its Cmd at off + the 16-B-rounded lengths before it; each replica's state machine
- * receives its entries in index order (a running CRC over the Cmds, the count, the longest Cmd) */
+/* The shim's copy of the Cmds it persisted (what it wrote to its WAL), per replica and log index, kept
+ * until the entry is handed to Update: rg_get_update's committed section refers to them when it comes
+ * with the persist section (include/raftgpu.h, RG_UPDATE_COMMITTED_CMDS). A ring of PCAP slots per
+ * replica tagged with the index: a replica's unapplied window never exceeds its log capacity. */
+#define PCAP 1024 /* = rg_config.log_capacity below */
+typedef struct {
+  uint64_t index;
+  uint32_t len;
+  uint8_t* data;
+} pcmd_t;
+static pcmd_t pstore[G * R][PCAP];
+static void pstore_put(uint32_t rid, uint64_t index, const uint8_t* cmd, uint32_t len) {
+  pcmd_t* p = &pstore[rid][index & (PCAP - 1)];
+  free(p->data);
+  p->index = index;
+  p->len = len;
+  p->data = (uint8_t*)malloc(len ? len : 1);
+  memcpy(p->data, cmd, len);
+}
+
 /* The WAL writer's walk of a persistence batch (the shim fsyncs these): per replica its entries
  * first..last, their terms from the runs, each application Cmd at the replica's payload_off + the
- * rounded lengths before it; a ConfigChange's len is RG_PERSIST_CONFIG | its descriptor. */
+ * rounded lengths before it; a ConfigChange's len is RG_PERSIST_CONFIG | its descriptor. Each Cmd is
+ * also kept in pstore (above). */
 static void persist_walk(const rg_persist_batch* b) {
   uint64_t seen = 0, tseen = 0;
   for (uint64_t s = 0; s < b->n_states; ++s) {
@@ -83,6 +101,7 @@ static void persist_walk(const rg_persist_batch* b) {
       if (p->len & RG_PERSIST_CONFIG) continue;
       EXPECT(off + p->len <= b->payload_bytes);
       if (p->len) EXPECT(p->crc == (uint32_t)crc32(0, b->payload + off, p->len));
+      pstore_put(st->rid, st->first + k, b->payload + off, p->len);
       off += (p->len + 15u) & ~15u;
     }
     seen += n;
@@ -91,6 +110,11 @@ static void persist_walk(const rg_persist_batch* b) {
   EXPECT(seen == b->n_entries && tseen == b->n_terms);
 }
 
+/* IOnDiskStateMachine.Update from a copy-back batch, the way a cgo shim walks it: per run, entry k is
+ * index first + k, its Cmd at off + the 16-B-rounded lengths before it — or, when the batch came by
+ * reference (payload NULL: rg_get_update with the persist section), the Cmd the shim persisted for that
+ * replica and index; each replica's state machine receives its entries in index order (a running CRC
+ * over the Cmds, the count, the longest Cmd) */
 static void consume(const rg_apply_batch* b, uint64_t* got, uint32_t* got_crc, uint64_t* last_idx,
                     uint32_t* longest) {
   uint64_t seen = 0;
@@ -100,8 +124,15 @@ static void consume(const rg_apply_batch* b, uint64_t* got, uint32_t* got_crc, u
     uint64_t off = run->off;
     for (uint32_t k = 0; k < run->count; ++k) {
       const rg_apply_cmd* c = &b->cmds[run->entry + k];
-      const uint8_t* cmd = b->payload + off;
-      EXPECT(off + c->len <= b->payload_bytes);
+      const uint8_t* cmd;
+      if (b->payload) {
+        cmd = b->payload + off;
+        EXPECT(off + c->len <= b->payload_bytes);
+      } else {  /* by reference: the Cmd the shim persisted */
+        const pcmd_t* p = &pstore[run->rid][(run->first + k) & (PCAP - 1)];
+        EXPECT(b->payload_bytes == 0 && p->index == run->first + k && p->len == c->len);
+        cmd = p->data;
+      }
       EXPECT(c->crc == (uint32_t)crc32(0, cmd, c->len));
       EXPECT(run->first + k > last_idx[run->rid]);
       last_idx[run->rid] = run->first + k;
@@ -238,6 +269,7 @@ int main(int argc, char** argv) {
     rg_update u;
     CHECK(rg_get_update(e, 0xFF, RG_UPDATE_PERSIST | RG_UPDATE_COMMITTED, &u));
     EXPECT(u.tick == (uint64_t)ticks && u.persist.n_states > 0);
+    EXPECT(u.committed.n_entries == 0 || (u.committed.payload == NULL && u.committed.payload_bytes == 0));
     persist_walk(&u.persist);
     consume(&u.committed, got, got_crc, last_idx, &longest);
     /* Peer.Commit: the app answered, applied = processed (config changes and no-ops included) */
