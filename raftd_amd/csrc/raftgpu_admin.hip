@@ -68,9 +68,11 @@ __global__ void gather_msgs_kernel(AdminParams a, uint32_t rid, uint32_t dst, ui
   const bool uni = type == M_REPLICATE && ((uint32_t)h[7 * plane] & RG_UNIFORM);
   // a Propose's word 4 carries its batch's stream layout (raftgpu_control.h), not a commit index
   const bool prop = type == M_PROPOSE;
+  const uint32_t wm = hdr_words(type);  // the words the type carries; the others read as 0
   for (int w = 0; w < 8; ++w)
-    out_hdr[k * 8 + w] = (uni && w == 5) || (prop && w == 4) ? 0ull
-                                                             : h[w * plane] & (w == 7 && uni ? ~(uint64_t)RG_UNIFORM : ~0ull);
+    out_hdr[k * 8 + w] = (uni && w == 5) || (prop && w == 4) || !((wm >> w) & 1u)
+                             ? 0ull
+                             : h[w * plane] & (w == 7 && uni ? ~(uint64_t)RG_UNIFORM : ~0ull);
   for (uint32_t e = 0; e < t.E; ++e)
     out_terms[(uint64_t)k * t.E + e] =
         (type == M_REPLICATE && e < n) ? (mt[uni ? 0 : (uint64_t)e * t.G] & TERM_MASK) : 0;

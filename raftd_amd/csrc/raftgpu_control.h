@@ -420,15 +420,16 @@ struct Ctl {
     oc += 1ull << (8 * dst);
     const uint64_t plane = (uint64_t)R * R * P().K * P().G;
     uint64_t* h = P().hdr_out + (((uint64_t)RG_S_SEND * R + dst) * P().K + k) * P().G + g;
+    const uint32_t wm = hdr_words(type);  // the words this type carries (a constant at every call site)
     h[0 * plane] = (uint64_t)type | ((uint64_t)my_id() << 8) | ((uint64_t)to << 16) | ((uint64_t)reject << 24) |
                    ((uint64_t)nent << 32);
     h[1 * plane] = mterm;
-    h[2 * plane] = log_term;
-    h[3 * plane] = log_index;
-    h[4 * plane] = commit;
-    h[5 * plane] = hint;
-    h[6 * plane] = hint_high;
-    h[7 * plane] = (uint64_t)src_a | ((uint64_t)src_b << 32);
+    if (wm & 0x04u) h[2 * plane] = log_term;
+    if (wm & 0x08u) h[3 * plane] = log_index;
+    if (wm & 0x10u) h[4 * plane] = commit;
+    if (wm & 0x20u) h[5 * plane] = hint;
+    if (wm & 0x40u) h[6 * plane] = hint_high;
+    if (wm & 0x80u) h[7 * plane] = (uint64_t)src_a | ((uint64_t)src_b << 32);
     return (int)k;
   }
   RG_FN int send_simple(uint32_t type, uint32_t to, uint32_t reject = 0, uint64_t log_index = 0,
@@ -1305,6 +1306,14 @@ struct Ctl {
   RG_FN void load_hdr(uint32_t src, uint32_t k, bool remote, Hdr& o) const {
     const uint64_t plane = (uint64_t)R * R * P().K * P().G;
     const uint64_t* h = hdr_ptr(src, k, remote);
+    if constexpr (FAST && ROLE == (int)LEADER && NB == 8) {
+      // a leader's fast step handles responses only (ids|reject, term, log index, hint: hdr_words);
+      // a Replicate or Heartbeat it ignores, any other type leaves the fast path (its words unread)
+#pragma unroll
+      for (int x = 0; x < NB; ++x) o.w[x] = (0x2Bu >> x) & 1u ? h[(uint64_t)x * plane] : 0ull;
+      o.mt0 = 0;
+      return;
+    }
 #pragma unroll
     for (int x = 0; x < NB; ++x) o.w[x] = h[(uint64_t)x * plane];
     o.mt0 = (remote ? P().rmt : P().mt_in)[((((uint64_t)src * R + RG_S_INBOX) * P().K + k) * P().E) * P().G + g];

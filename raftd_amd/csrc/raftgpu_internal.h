@@ -94,6 +94,19 @@ enum : uint32_t {
 enum : uint32_t { FOLLOWER = 0, CANDIDATE = 1, LEADER = 2 };
 // header word 7 of a local Replicate: its n entries all carry the inline word mt[0] (raftgpu_control.h)
 constexpr uint32_t RG_UNIFORM = 1;
+// The header words a message of each type carries (bit w = word w: 0 type|ids|reject|nent, 1 term,
+// 2 log term, 3 log index, 4 commit, 5 hint, 6 hint high, 7 src): the sender stores only these, the
+// readers load only these, and a message view shows the others as 0. The steady-state types carry
+// half their 64 B (r06: at C5 the outbox planes were a third of the control step's HBM bytes); the
+// rare types carry all eight. Every word a handler of the type reads is in its set.
+RG_HD_INLINE uint32_t hdr_words(uint32_t type) {
+  return type == M_REPLICATE ? 0xBFu          // all but the hint high
+         : type == M_REPLICATE_RESP ? 0x2Bu   // ids|reject, term, log index, hint
+         : type == M_HEARTBEAT ? 0x73u        // ids, term, commit, hint, hint high (a read's context)
+         : type == M_HEARTBEAT_RESP ? 0x63u   // ids, term, hint, hint high (the context echoed)
+         : type == M_NOOP ? 0x03u             // ids, term
+         : 0xFFu;
+}
 enum : uint32_t { RETRY = 0, WAIT = 1, REPLICATE = 2, SNAPSHOT = 3 };
 enum : uint32_t { ENTRY_APP = 0, ENTRY_CONFIG = 1 };
 enum : uint32_t {

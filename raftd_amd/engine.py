@@ -262,8 +262,10 @@ class PersistedCmds:
     resolves rg_get_update's committed section when it comes by reference (RG_UPDATE_PERSIST together with
     RG_UPDATE_COMMITTED, include/raftgpu.h). dragonboat hands Update its entries from its own in-memory log
     the same way. Per replica {index: Cmd bytes}; a state record's window rewrites it (entries at or above
-    its `first` are replaced, those above `last` or at or below `marker` dropped), and an entry handed to
-    the state machine is dropped with everything below it."""
+    its `first` are replaced, those above `last` dropped), an entry handed to the state machine is dropped
+    with everything below it, and once the update is resolved the entries at or below each record's
+    `marker` go too (compacted or restored past: a snapshot in the same step may compact entries that
+    step also committed, so this comes after resolve)."""
 
     def __init__(self):
         self.log = {}
@@ -272,12 +274,19 @@ class PersistedCmds:
         for st in states:
             rid, first, last, marker = int(st["rid"]), int(st["first"]), int(st["last"]), int(st["marker"])
             d = self.log.setdefault(rid, {})
-            for i in [i for i in d if i >= first or i > last or i <= marker]:
+            for i in [i for i in d if i >= first or i > last]:
                 del d[i]
         for e in entries:
             if e["type"] == 0:  # application entries (a ConfigChange carries no Cmd)
                 o, n = int(e["off"]), int(e["len"])
                 self.log.setdefault(int(e["rid"]), {})[int(e["index"])] = bytes(payload[o:o + n])
+
+    def compact(self, states):
+        for st in states:
+            d = self.log.get(int(st["rid"]), {})
+            marker = int(st["marker"])
+            for i in [i for i in d if i <= marker]:
+                del d[i]
 
     def resolve(self, runs, cmds):
         """The packed payload a by-reference committed section stands for: each Cmd at its run's off plus
@@ -842,6 +851,8 @@ class Engine:
             self._persisted.persist(st, out["entries"], epay)
         if by_ref:
             out["committed_payload"] = self._persisted.resolve(runs, cmds)
+        if flags & UPDATE_PERSIST:
+            self._persisted.compact(st)
         out["committed_by_reference"] = by_ref
         out["committed"] = expand_apply(runs, cmds)
         out["committed_runs"] = runs
