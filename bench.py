@@ -639,6 +639,21 @@ def main():
     kms = host.kernel_ms()
     span = host.kernel_span_ms("bulk") if spread else None
     c1 = host.sum_committed()  # before the control-timing steps below
+    # the state the timed ticks left (before the extra phases below run more ticks): invariant bits,
+    # drops, the hand-off count, the page pool (a shape whose log outgrows the pool without compaction
+    # — C5's 1 entry per leader per tick at SnapshotEntries 1000 — must show it here, not in the timed ticks)
+    va = eng.replica_array()  # every replica of this rank's first engine
+    ctl_slow = None
+    fn = getattr(eng.L, "rg_debug_ctl_slow", None)
+    if fn is not None:  # replicas of the last tick whose step left the control fast path (DESIGN.md §3)
+        import ctypes as C
+        fn.argtypes, fn.restype = [C.c_void_p, C.POINTER(C.c_uint32)], C.c_int
+        n_slow = C.c_uint32()
+        if fn(eng.h, C.byref(n_slow)) == 0:
+            ctl_slow = n_slow.value
+    errs, drops = int((va["err"] != 0).sum()), int(va["drops"].sum())
+    pool_timed = eng.pool_stats() if P else None
+    del va
     # control_kernel duration from a few more steps after the timed region (timing both kernels
     # adds two event records per tick, which the timed region does without)
     host.timing(True)
@@ -661,16 +676,6 @@ def main():
     untimed_ms = (time.perf_counter() - u0) * 1e3 / args.steps
     graph = graph_ticks(eng, pt, pc, G) if not spread and not args.wire_all else None
     x_ms = sum(a.elapsed_time(b) for a, b in xev) / args.steps if wire and not pipelined else 0.0
-    va = eng.replica_array()  # every replica of this rank's first engine: invariant bits and drops
-    ctl_slow = None
-    fn = getattr(eng.L, "rg_debug_ctl_slow", None)
-    if fn is not None:  # replicas of the last tick whose step left the control fast path (DESIGN.md §3)
-        import ctypes as C
-        fn.argtypes, fn.restype = [C.c_void_p, C.POINTER(C.c_uint32)], C.c_int
-        n_slow = C.c_uint32()
-        if fn(eng.h, C.byref(n_slow)) == 0:
-            ctl_slow = n_slow.value
-    errs, drops = int((va["err"] != 0).sum()), int(va["drops"].sum())
     e2e = None
     if not spread:
         e2e = copyback_schedules(eng, lambda: one_step(None), G, steps=max(4, min(args.steps, 12)))
@@ -755,6 +760,7 @@ def main():
         "device_ms_per_step": dev_max / K,
         "ms_per_step_without_timing_events": untimed_ms,
         "replicas_with_invariant_errors": errs,
+        "pool_after_timed_ticks": pool_timed,
         "drops_total": drops,
         "drops_note": "messages / batches the engine dropped by its own bounded-buffer rules (K_MAX per pair per "
                       "tick, ring capacity, forward hop limit) since bootstrap, summed over this rank's replicas",

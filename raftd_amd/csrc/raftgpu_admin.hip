@@ -68,7 +68,7 @@ __global__ void gather_msgs_kernel(AdminParams a, uint32_t rid, uint32_t dst, ui
   const bool uni = type == M_REPLICATE && ((uint32_t)h[7 * plane] & RG_UNIFORM);
   // a Propose's word 4 carries its batch's stream layout (raftgpu_control.h), not a commit index
   const bool prop = type == M_PROPOSE;
-  const uint32_t wm = hdr_words(type);  // the words the type carries; the others read as 0
+  const uint32_t wm = hdr_words(type, n);  // the words the message carries; the others read as 0
   for (int w = 0; w < 8; ++w)
     out_hdr[k * 8 + w] = (uni && w == 5) || (prop && w == 4) || !((wm >> w) & 1u)
                              ? 0ull

@@ -416,11 +416,14 @@ __global__ void __launch_bounds__(256) RG_BULK_ATTR bulk_kernel(BulkParams p, co
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   // a corrupt parameter block made control skip its tick: the job tables are stale, run nothing
   if (p.poolctl->param_err) return;
+  // pages freed by this tick's pool kernel become allocatable from the next tick on
+  if (blockIdx.x == 0 && threadIdx.x == 0) p.poolctl->limit = p.poolctl->tail;
+  if constexpr (MJ) {  // bulk_small_kernel took every replica with jobs this tick (its stamp is older)
+    if (p.small && *p.rest_tick != p.tick) return;
+  }
   const uint32_t shw = CRC_T_WORDS + CRC_N_WORDS + NCH * CRC_SH_STRIDE;
   for (uint32_t i = threadIdx.x; i < shw; i += blockDim.x) lds[i] = p.crc_tab[i];
   for (uint32_t i = threadIdx.x; i < CRC_ZP_WORDS; i += blockDim.x) lds[shw + i] = p.crc_tab[CRC_ZP_OFF + i];
-  // pages freed by this tick's pool kernel become allocatable from the next tick on
-  if (blockIdx.x == 0 && threadIdx.x == 0) p.poolctl->limit = p.poolctl->tail;
   __syncthreads();
   const uint32_t waves = blockDim.x >> 6, lane = lane_id();
   const uint32_t stride = gridDim.x * waves;
@@ -741,6 +744,7 @@ __global__ void __launch_bounds__(256) bulk_small_kernel(BulkParams p, const uin
     // bulk_kernel skips a block of 64 groups whose replicas with jobs were all taken here
     const uint64_t left = __ballot(valid && nj != 0 && !small);
     if (lane == 0) p.rest[t] = left != 0 ? 1u : 0u;
+    if (lane == 0 && left) *p.rest_tick = p.tick;  // bulk_kernel has work this tick (every writer stores the same value)
     const uint32_t e0 = (jb.meta >> 8) & 0xFF, k = small ? (jb.meta & 0xFF) - e0 : 0u;
     const uint32_t off = wave_excl_scan32(k);
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)(off + k), 63);

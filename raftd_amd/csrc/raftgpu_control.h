@@ -420,7 +420,7 @@ struct Ctl {
     oc += 1ull << (8 * dst);
     const uint64_t plane = (uint64_t)R * R * P().K * P().G;
     uint64_t* h = P().hdr_out + (((uint64_t)RG_S_SEND * R + dst) * P().K + k) * P().G + g;
-    const uint32_t wm = hdr_words(type);  // the words this type carries (a constant at every call site)
+    const uint32_t wm = hdr_words(type, nent);  // the words this message carries (per type, and an empty Replicate's)
     h[0 * plane] = (uint64_t)type | ((uint64_t)my_id() << 8) | ((uint64_t)to << 16) | ((uint64_t)reject << 24) |
                    ((uint64_t)nent << 32);
     h[1 * plane] = mterm;

@@ -107,10 +107,20 @@ __device__ __forceinline__ bool fast_step(CTickParams& cp, uint32_t q) {
 }
 
 // the hand-off count (measurement: rg_debug_ctl_slow): one atomic per wave with aborted lanes
-__device__ __forceinline__ void count_slow(CTickParams& cp, bool aborted) {
+__device__ __forceinline__ uint32_t count_slow(CTickParams& cp, bool aborted) {
   const uint64_t m = __ballot(aborted);
-  if (m && (threadIdx.x & 63u) == (uint32_t)__ffsll((long long)m) - 1)
-    atomicAdd(cp.slow_cnt + (cp.tick & 1), (uint32_t)__popcll(m));
+  uint32_t base = 0;
+  if (m) {
+    const uint32_t first = (uint32_t)__ffsll((long long)m) - 1;
+    if ((threadIdx.x & 63u) == first) base = atomicAdd(cp.slow_cnt + (cp.tick & 1), (uint32_t)__popcll(m));
+    base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)first);
+  }
+  return base;
+}
+// the hand-off list: an aborted lane's replica at base + its rank among the wave's aborted lanes
+__device__ __forceinline__ void list_slow(CTickParams& cp, bool aborted, uint32_t base, uint32_t q) {
+  const uint64_t m = __ballot(aborted);
+  if (aborted) cp.slow_flag[base + (uint32_t)__popcll(m & ((1ull << (threadIdx.x & 63u)) - 1))] = q;
 }
 
 // RG_AB_CTL2D (diagnostic variant, never the product): the fast and slow kernels on r04f's (column,
@@ -123,6 +133,9 @@ __device__ __forceinline__ void count_slow(CTickParams& cp, bool aborted) {
 #define RG_CTL_Q (blockIdx.x * blockDim.x + threadIdx.x)
 #define RG_CTL_COL_OK(cp) true
 #endif
+#ifndef RG_SLOW_GRID
+#define RG_SLOW_GRID 1024u  // workgroups of control_slow_kernel (at most): 256 CUs x 4 SIMDs
+#endif
 template <int R>
 __global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_FAST_WAVES) control_fast_kernel(
     const TickParams* __restrict__ pp, uint32_t* perr) {
@@ -132,8 +145,12 @@ __global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_FAST_WAVES) control_fast_
   if (q == 0) cp.slow_cnt[(cp.tick + 1) & 1] = 0;  // the next tick's counter (its last reader ran before us)
   if (q >= cp.nrep || !RG_CTL_COL_OK(cp)) return;
   const bool aborted = fast_step<R>(cp, q);
-  cp.slow_flag[q] = aborted ? 1u : 0u;  // for control_slow_kernel
+#ifdef RG_AB_CTL2D
+  cp.slow_flag[q] = aborted ? 1u : 0u;  // for control_slow_kernel (the diagnostic 2-D grid)
   count_slow(cp, aborted);
+#else
+  list_slow(cp, aborted, count_slow(cp, aborted), q);
+#endif
 }
 
 // Small engines (a wave or less per SIMD: occupancy buys nothing) run the fallback in the same
@@ -163,16 +180,41 @@ __global__ void __launch_bounds__(RG_CTL_BLOCK, 1) control_fastfb_kernel(const T
 template <int R>
 __global__ void __launch_bounds__(RG_CTL_BLOCK, RG_CTL_MINWAVES) control_slow_kernel(const TickParams* __restrict__ pp,
                                                                                     uint32_t* perr) {
+#ifdef RG_AB_CTL2D
   const uint32_t q = RG_CTL_Q;
   if (!tp_verify(pp, perr, q, "control_slow_kernel")) return;
   CTickParams& cp = *(CTickParams*)pp;
   if (q >= cp.nrep || !RG_CTL_COL_OK(cp) || !cp.slow_flag[q]) return;
-#if defined(RG_AB_CTL2D) && !defined(RG_AB_CTL2D_Q)
+#if !defined(RG_AB_CTL2D_Q)
   Ctl<R, false, -1, false, true> c(cp, blockIdx.y, blockIdx.x * blockDim.x + threadIdx.x);  // the slot a grid-uniform scalar
 #else  // RG_AB_CTL2D_Q: the 2-D launch, the slot derived from q (a per-lane value to the compiler)
   Ctl<R, false, -1, false, true> c(cp, q);
 #endif
   c.run();
+#else
+  // the list the fast kernel wrote: lane i of the grid steps entries i, i + grid, ... (every replica once)
+  const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (!tp_verify(pp, perr, i0, "control_slow_kernel")) return;
+  CTickParams& cp = *(CTickParams*)pp;
+  // the count is re-read after each step (a scalar-cache hit) instead of living through it: with it and
+  // the list index both live, the full step spilled four VGPRs at R <= 5 (and to scratch at R = 7)
+  auto count = [&]() -> uint32_t {
+    RG_G(uint32_t) c = cp.slow_cnt;
+    asm volatile("" : "+s"(c));
+    return c[cp.tick & 1];
+  };
+#if RG_CTL_R <= 5
+  for (uint32_t i = i0; i < count() && i < cp.nrep; i += gridDim.x * blockDim.x) {
+    Ctl<R, false, -1, false, true> c(cp, cp.slow_flag[i]);
+    c.run();
+  }
+#else  // R 6-8: one entry per lane, a full grid (the loop needed scratch at R = 7)
+  if (i0 < count() && i0 < cp.nrep) {
+    Ctl<R, false, -1, false, true> c(cp, cp.slow_flag[i0]);
+    c.run();
+  }
+#endif
+#endif
 }
 
 // ---- the resident multi-tick control kernel (metadata-only, one-rank engines). A
@@ -255,7 +297,9 @@ hipError_t launch_control_fast_t<RG_CTL_R>(const TickParams* p, uint32_t* perr, 
   hipLaunchKernelGGL(control_slow_kernel<RG_CTL_R>, g2, block, 0, s, p, perr);
 #else
   hipLaunchKernelGGL(control_fast_kernel<RG_CTL_R>, grid, block, 0, s, p, perr);
-  hipLaunchKernelGGL(control_slow_kernel<RG_CTL_R>, grid, block, 0, s, p, perr);
+  // the hand-off list's walk: one full-step wave per SIMD fills the chip (256 VGPRs, occupancy 1)
+  const dim3 sgrid(RG_CTL_R > 5 || grid.x < RG_SLOW_GRID ? grid.x : RG_SLOW_GRID);
+  hipLaunchKernelGGL(control_slow_kernel<RG_CTL_R>, sgrid, block, 0, s, p, perr);
 #endif
   return hipGetLastError();
 #endif

@@ -247,6 +247,7 @@ struct rg_engine {
   // committed-entry copy-back (raftgpu_apply.hip)
   uint64_t* apply_lo = nullptr;
   uint32_t* small_rest = nullptr;  // BulkParams::rest
+  uint64_t* rest_tick = nullptr;   // BulkParams::rest_tick
   uint32_t *acnt = nullptr, *accnt = nullptr, *arcnt = nullptr;
   uint64_t *aoff = nullptr, *acoff = nullptr, *aroff = nullptr, *absum = nullptr;
   bool copy_kernel = true;  // build variant -DRG_AB_APPLY_MEMCPY: the runtime's D2H copy instead
@@ -459,6 +460,8 @@ static BulkParams bulk_params_at(rg_engine* e, uint64_t tk) {
   b.multijob = e->bulk_mj ? 1u : 0u;
   b.small = e->bulk_mj && e->bulk_small ? 1u : 0u;
   b.rest = e->small_rest;
+  b.rest_tick = e->rest_tick;
+  b.tick = tk;
   b.wg_waves = e->bulk_wg;
   return b;
 }
@@ -602,6 +605,8 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if (rc == RG_OK) rc = dalloc(e, &e->acoff, (n + 1) * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->arcnt, n * 4);
   if (rc == RG_OK) rc = dalloc(e, &e->small_rest, (uint64_t)((c.groups + 63) / 64) * c.replicas * 4);
+  if (rc == RG_OK) rc = dalloc(e, &e->rest_tick, 8);
+  if (rc == RG_OK && hipMemset(e->rest_tick, 0xFF, 8) != hipSuccess) rc = fail(RG_EHIP, "hipMemset (rest stamp)");
   if (rc == RG_OK) rc = dalloc(e, &e->aroff, (n + 1) * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->absum, ((n + 1023) / 1024 + 1) * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->persist_lo, n * 8);

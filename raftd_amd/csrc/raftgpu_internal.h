@@ -99,8 +99,9 @@ constexpr uint32_t RG_UNIFORM = 1;
 // readers load only these, and a message view shows the others as 0. The steady-state types carry
 // half their 64 B (r06: at C5 the outbox planes were a third of the control step's HBM bytes); the
 // rare types carry all eight. Every word a handler of the type reads is in its set.
-RG_HD_INLINE uint32_t hdr_words(uint32_t type) {
-  return type == M_REPLICATE ? 0xBFu          // all but the hint high
+RG_HD_INLINE uint32_t hdr_words(uint32_t type, uint32_t nent = 1) {
+  return type == M_REPLICATE ? (nent ? 0xBFu  // all but the hint high
+                                     : 0x1Fu)  // an empty one (a commit update): no Cmd position, no src
          : type == M_REPLICATE_RESP ? 0x2Bu   // ids|reject, term, log index, hint
          : type == M_HEARTBEAT ? 0x73u        // ids, term, commit, hint, hint high (a read's context)
          : type == M_HEARTBEAT_RESP ? 0x63u   // ids, term, hint, hint high (the context echoed)
@@ -275,11 +276,13 @@ struct TickParams {
   RG_G(uint64_t) rdst;              // [RD_ROWS][nrep] ReadIndex state
   RG_G(const uint2) info;           // [2 banks][nrep][L] {slot crc, stream position} (a freed stream's bound)
   RG_G(PoolCtl) pool;               // sticky param_err on a checksum mismatch
-  // the fast path's hand-off: control_fast_kernel sets slow_flag[q] for a replica whose
-  // step left the fast path (and counts them in slow_cnt[tick & 1], for measurement); control_slow_kernel
-  // re-runs those steps. slow_cnt[(tick + 1) & 1] is zeroed by the fast launch (its readers are done)
+  // the fast path's hand-off: control_fast_kernel appends a replica whose step left the
+  // fast path to slow_flag (a list: slow_cnt[tick & 1] of them, one atomic per wave), and
+  // control_slow_kernel re-runs those steps, a grid-stride walk of the list (r06: it was a flag per
+  // replica and a full grid, 0.05 ms at C5 for a handful of lanes). slow_cnt[(tick + 1) & 1] is zeroed
+  // by the fast launch (its readers are done). Diagnostic 2-D builds (RG_AB_CTL2D) keep the flags.
   RG_G(uint32_t) slow_cnt;          // [2] (NULL: no fast path; control_kernel steps every replica)
-  RG_G(uint32_t) slow_flag;         // [nrep]
+  RG_G(uint32_t) slow_flag;         // [nrep]: the hand-off list (RG_AB_CTL2D: a flag per replica)
   uint64_t csum;                    // tp_checksum of every word above (host-computed, checked first)
 };
 // the parameter block's checksum: Σ_i tp_mix(word_i + (i + 1)·φ) mod 2^64 over its words before `csum`
@@ -318,6 +321,9 @@ struct BulkParams {
   uint32_t small;        // bulk_small_kernel ran first: bulk_kernel skips the replicas it took (small_job)
   uint32_t* rest;        // [ceil(G / 64) * R] per 64-group block and slot: 1 if bulk_small_kernel left a
                          // replica with jobs there (bulk_kernel skips the tiles of a block it took whole)
+  uint64_t* rest_tick;   // bulk_small_kernel stamps `tick` here if it left any replica to bulk_kernel; a
+  uint64_t tick;         //   bulk_kernel that finds another stamp has nothing to do and exits at once
+                         //   (C5: every block taken whole; the launch was 0.096 ms of LDS staging and tile walks)
   uint32_t wg_waves;     // waves per bulk_kernel workgroup (1..4)
 };
 

@@ -209,9 +209,9 @@ __global__ void __launch_bounds__(POOL_BLOCK) pool_kernel(PoolParams pp) {
     for (uint32_t j = 0; j < 4; ++j)
       if (tk[j]) pp.pt[(uint64_t)row[j] * pp.PTS + slot[j]] = v[j];
   }
-  if (valid) {
-    pp.s32[S_LPG * n + q] = nlpg;
-    pp.s32[S_APG * n + q] = ok ? top : apg;
+  if (valid) {  // in place: only what moved (a replica takes a page per 16 entries of 256 B)
+    if (nlpg != lpg) pp.s32[S_LPG * n + q] = nlpg;
+    if ((ok ? top : apg) != apg) pp.s32[S_APG * n + q] = ok ? top : apg;
     if (!ok) {  // the pool is empty: this replica's appends of the step are not stored; the engine is poisoned
       pp.s32[S_ERR * n + q] |= ERR_POOL;
       pp.jcnt[q] = 0;

@@ -461,7 +461,7 @@ int ch_read_msgs(void* hh, uint32_t rid, uint32_t dst, rg_msg_view* out, uint32_
   for (uint32_t k = 0; k < cnt && k < cap; ++k) {
     const uint64_t* hp = t.hdr_in + (((uint64_t)s * t.R + dst) * t.K + k) * t.G + g;
     uint64_t w[8];
-    const uint32_t wm = hdr_words((uint32_t)(hp[0] & 0xFF));  // the words the type carries
+    const uint32_t wm = hdr_words((uint32_t)(hp[0] & 0xFF), (uint32_t)(hp[0] >> 32));  // the words it carries
     for (int i = 0; i < 8; ++i) w[i] = (wm >> i) & 1u ? hp[i * plane] : 0ull;
     const bool uni = (w[0] & 0xFF) == M_REPLICATE && ((uint32_t)w[7] & RG_UNIFORM);  // shown expanded
     if (uni) {

@@ -75,7 +75,10 @@ def test_full_step_keeps_its_pointers_out_of_spill_lanes():
         assert int(res[k]["SGPRs Spill"]) < 64, (k, res[k]["SGPRs Spill"])
         assert int(res[k]["ScratchSize [bytes/lane]"]) == 0, k
         if "ILi8E" not in k:  # R <= 7: the SLIM build's live values fit the register file
-            assert int(res[k]["VGPRs Spill"]) == 0, (k, res[k]["VGPRs Spill"])
+            # control_slow_kernel<R <= 5> walks the hand-off list in a loop around the step (r06): the loop
+            # moves 4-6 VGPRs into AGPRs (v_accvgpr moves, no scratch); the one-shot builds have none
+            cap = 8 if "control_slow_kernel" in k and int(k.split("ILi")[1][0]) <= 5 else 0
+            assert int(res[k]["VGPRs Spill"]) <= cap, (k, res[k]["VGPRs Spill"])
 
 
 def test_one_hip_runtime_per_process():
