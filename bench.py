@@ -780,8 +780,8 @@ def main():
             "kernel_ms": rk_ms,
             "launches_timed": kms["bulk"][1],
             "launches_timed_note": f"HIP events around bulk_kernel on every {TIMING_EVERY}th tick of the timed region",
-            "per": ("tick: wall-clock span of the column halves' bulk_kernel launches (first start to last end on "
-                    "one timeline, rg_timing_epoch)") if spread and args.halves > 1 else "launch",
+            "per": ("tick: wall-clock time the column halves' bulk_kernel launches of a tick ran (the union of "
+                    "their intervals on one timeline, rg_timing_epoch)") if spread and args.halves > 1 else "launch",
             "bulk_ms_summed_over_halves": bulk_sum_ms if spread and args.halves > 1 else None,
             "algorithmic_bytes_per_launch": rk_bytes,
             "tick_algorithmic_bytes": traffic["algorithmic_bytes"],

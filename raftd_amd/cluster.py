@@ -574,17 +574,31 @@ class DistEngine(_Feeds):
         return {k: (sum(x[k][0] for x in ks), ks[0][k][1]) for k in ks[0]}
 
     def kernel_span_ms(self, kernel: str = "bulk"):
-        """The kernel's wall-clock span per tick over the halves — first launch start to last launch end
-        of the same tick on the epoch timeline (rg_timing_epoch before timing(True)) — summed over the
-        ticks every half timed, and their count. Halves on streams of their own overlap, so the sum of
-        their launch durations overstates the time the tick spent in the kernel; the span does not."""
+        """The kernel's wall-clock time per tick over the halves — the union of the halves' launch
+        intervals of the same tick on the epoch timeline (rg_timing_epoch before timing(True)) — summed
+        over the ticks every half timed, and their count. Halves on streams of their own overlap, so the
+        sum of their launch durations overstates the time the tick spent in the kernel; halves on one
+        stream run other work between their launches, so a first-start-to-last-end span would overstate
+        it too; the union does neither."""
         per = {}
         for p in self.parts:
             ticks, a, b = p.eng.kernel_events(kernel)
             for t, x, y in zip(ticks.tolist(), a.tolist(), b.tolist()):
                 per.setdefault(t, []).append((x, y))
-        spans = [max(y for _, y in v) - min(x for x, _ in v) for v in per.values() if len(v) == len(self.parts)]
-        return sum(spans), len(spans)
+        out = []
+        for v in per.values():
+            if len(v) != len(self.parts):
+                continue
+            tot, end = 0.0, None
+            for x, y in sorted(v):
+                if end is None or x > end:
+                    tot += y - x
+                    end = y
+                elif y > end:
+                    tot += y - end
+                    end = y
+            out.append(tot)
+        return sum(out), len(out)
 
     def last_tick_traffic(self) -> dict:
         ts = [p.eng.last_tick_traffic() for p in self.parts]

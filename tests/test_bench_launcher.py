@@ -56,3 +56,28 @@ def test_xgmi_bound():
     assert bench.xgmi_bound_ms(1.34e9, 1) is None
     assert abs(bench.xgmi_bound_ms(1.34e9, 2) - 1.34e9 / 153e9 * 1e3) < 1e-9
     assert abs(bench.xgmi_bound_ms(2.1e9, 8) - 2.1e9 / (7 * 153e9) * 1e3) < 1e-9
+
+
+def test_kernel_span_is_the_union_of_the_halves_intervals():
+    """The N > 1 line's bulk time per tick: overlapping halves (their own streams) count their overlap
+    once; halves on one stream with other work between them count only the launches."""
+    sys.path.insert(0, ROOT)
+    import numpy as np
+    from raftd_amd.cluster import DistEngine
+
+    class E:
+        def __init__(self, ev):
+            self.ev = ev
+
+        def kernel_events(self, kernel):
+            t, a, b = zip(*self.ev)
+            return np.array(t, np.uint64), np.array(a), np.array(b)
+
+    class P:
+        def __init__(self, ev):
+            self.eng = E(ev)
+
+    d = DistEngine.__new__(DistEngine)
+    d.parts = [P([(4, 0.0, 1.0), (8, 10.0, 11.0)]), P([(4, 0.5, 1.5), (8, 12.0, 13.0)])]
+    tot, n = d.kernel_span_ms()
+    assert n == 2 and abs(tot - (1.5 + 2.0)) < 1e-12
