@@ -56,7 +56,7 @@ __global__ void gather_msgs_kernel(AdminParams a, uint32_t rid, uint32_t dst, ui
   const TickParams& t = a.t;
   const uint32_t g = rid / t.R, s = rid - g * t.R;
   const uint64_t plane = (uint64_t)t.R * t.R * t.K * t.G;
-  const uint32_t cnt = t.cnt_in[((uint64_t)s * t.R + dst) * t.G + g];
+  const uint32_t cnt = cnt_n(t.cnt_in[((uint64_t)s * t.R + dst) * t.G + g]);
   const uint32_t k = threadIdx.x;
   if (k == 0) *out_cnt = cnt;
   if (k >= cnt || k >= t.K) return;
@@ -228,7 +228,7 @@ __global__ void deliver_kernel(AdminParams a, uint32_t rid, const rg_msg_view* m
   const uint32_t g = rid / t.R, s = rid - g * t.R, q = s * t.G + g;
   const uint32_t dst = m->to - 1;
   uint32_t* cnt = ((uint32_t*)(t.cnt_in)) + ((uint64_t)s * t.R + dst) * t.G + g;
-  const uint32_t k = *cnt;
+  const uint32_t k = cnt_n(*cnt);  // its class bits stay MC_ALL (0): the receiver loads every word
   if (k >= t.K) {
     *status = 1;
     return;
@@ -242,7 +242,7 @@ __global__ void deliver_kernel(AdminParams a, uint32_t rid, const rg_msg_view* m
     uint64_t* mt = ((uint64_t*)(t.mt_in)) + ((((uint64_t)s * t.R + dst) * t.K + k) * t.E) * t.G + g;
     for (uint32_t e = 0; e < m->nent; ++e) mt[(uint64_t)e * t.G] = t.tr[((m->log_index + 1 + e) & (t.L - 1)) * t.nrep + q];
   }
-  *cnt = k + 1;
+  *cnt = (*cnt & ~0xFFu) | (k + 1);
   *status = 0;
 }
 

@@ -226,6 +226,7 @@ struct Ctl {
   uint32_t la_n, la_pos;
 #endif
   uint64_t oc, em;  // per destination: enqueued / emitted counts, 8 bits each
+  uint64_t ocls;    // per destination: the classes of its first four messages (2 bits each, cnt_cls)
   uint32_t nj;      // jobs emitted
   uint64_t lt_i = ~0ull, lt_v = 0;  // term_at cache: index lt_i has term lt_v (~0: none)
   // in-place store (FAST): what the step changed, for the fields it cannot compare at the end
@@ -306,7 +307,7 @@ struct Ctl {
 #ifdef RG_CTL_FASTREP
     la_base = la_word = la_pt = 0; la_n = 0; la_pos = 0;
 #endif
-    oc = 0; em = 0; nj = 0;
+    oc = 0; em = 0; ocls = 0; nj = 0;
   }
 
   // entries per load batch (RG_CTL_BATCH); at R >= 7 the remote arrays leave room for half as many
@@ -418,6 +419,11 @@ struct Ctl {
       return -1;
     }
     oc += 1ull << (8 * dst);
+    // the fast step classifies its messages for the receivers; the full step's (rare: elections,
+    // recoveries) stay MC_ALL, which a receiver always reads correctly (every word)
+    if constexpr (FAST) {
+      if (k < 4) ocls |= (uint64_t)msg_class(type, nent) << (8 * dst + 2 * k);
+    }
     const uint64_t plane = (uint64_t)R * R * P().K * P().G;
     uint64_t* h = P().hdr_out + (((uint64_t)RG_S_SEND * R + dst) * P().K + k) * P().G + g;
     const uint32_t wm = hdr_words(type, nent);  // the words this message carries (per type, and an empty Replicate's)
@@ -1303,15 +1309,21 @@ struct Ctl {
   }
   // one round trip: the header words and the message's first inline word (for other
   // messages the slot holds stale words, which nothing reads)
-  RG_FN void load_hdr(uint32_t src, uint32_t k, bool remote, Hdr& o) const {
+  // cls: the message's class from the count plane (cnt_cls). The fast step loads only that class's words
+  // (and the first inline term only for MC_ALL); the full step loads every word it batches
+  RG_FN void load_hdr(uint32_t src, uint32_t k, bool remote, Hdr& o, uint32_t cls = MC_ALL) const {
     const uint64_t plane = (uint64_t)R * R * P().K * P().G;
     const uint64_t* h = hdr_ptr(src, k, remote);
-    if constexpr (FAST && ROLE == (int)LEADER && NB == 8) {
-      // a leader's fast step handles responses only (ids|reject, term, log index, hint: hdr_words);
-      // a Replicate or Heartbeat it ignores, any other type leaves the fast path (its words unread)
+    if constexpr (FAST && NB == 8) {
+      uint32_t wm = cls_words(cls);
+      // a leader's fast step handles responses only (ids|reject, term, log index, hint); a Replicate or
+      // Heartbeat it ignores, any other type leaves the fast path (its words unread)
+      if constexpr (ROLE == (int)LEADER) wm &= 0x2Bu;
 #pragma unroll
-      for (int x = 0; x < NB; ++x) o.w[x] = (0x2Bu >> x) & 1u ? h[(uint64_t)x * plane] : 0ull;
-      o.mt0 = 0;
+      for (int x = 0; x < NB; ++x) o.w[x] = (wm >> x) & 1u ? h[(uint64_t)x * plane] : 0ull;
+      o.mt0 = ROLE != (int)LEADER && cls == MC_ALL
+                  ? (remote ? P().rmt : P().mt_in)[((((uint64_t)src * R + RG_S_INBOX) * P().K + k) * P().E) * P().G + g]
+                  : 0ull;
       return;
     }
 #pragma unroll
@@ -1503,8 +1515,8 @@ struct Ctl {
     const uint64_t in_rd = P().read_ctx ? P().read_ctx[ri()] : 0ull;
     sfor<0, R>([&](auto jc) {
       constexpr int src = decltype(jc)::value;
-      if (cnt_pf[src] > P().K) {  // never produced by a sender (unpack_kernel clamps received counts): ERR_WIRE
-        RG_OOB("RG_BOUNDS control q=%u src=%u cnt=%u > K=%u\n", q, (uint32_t)src, cnt_pf[src], P().K);
+      if (cnt_n(cnt_pf[src]) > P().K) {  // never produced by a sender (unpack_kernel clamps received counts): ERR_WIRE
+        RG_OOB("RG_BOUNDS control q=%u src=%u cnt=%u > K=%u\n", q, (uint32_t)src, cnt_n(cnt_pf[src]), P().K);
         if constexpr (FAST) abort_();
         err |= ERR_WIRE;
         cnt_pf[src] = 0;
@@ -1516,7 +1528,7 @@ struct Ctl {
     auto next_msg = [&](uint32_t src, uint32_t k, uint32_t& ns, uint32_t& nk) -> bool {
       for (uint32_t x = src, y = k + 1; x < R; ++x, y = 0) {
         if (x == s) continue;
-        if (y < sel_get<R>(cnt_pf, x)) {
+        if (y < cnt_n(sel_get<R>(cnt_pf, x))) {
           ns = x;
           nk = y;
           return true;
@@ -1527,14 +1539,15 @@ struct Ctl {
     uint32_t cs = 0, ck = 0;
     bool have = !(FAST && aborted) && next_msg(0, ~0u, cs, ck);
     Hdr cur{};
-    if (have) load_hdr(cs, ck, pl_remote(P().pl, cs, RG_S_INBOX, g), cur);
+    if (have) load_hdr(cs, ck, pl_remote(P().pl, cs, RG_S_INBOX, g), cur, cnt_cls(sel_get<R>(cnt_pf, cs), ck));
     while (have) {
       uint32_t ns = 0, nk = 0;
       const bool more = next_msg(cs, ck, ns, nk);
       Hdr nxt{};
-      if (PIPE && more) load_hdr(ns, nk, pl_remote(P().pl, ns, RG_S_INBOX, g), nxt);
+      if (PIPE && more) load_hdr(ns, nk, pl_remote(P().pl, ns, RG_S_INBOX, g), nxt, cnt_cls(sel_get<R>(cnt_pf, ns), nk));
       handle(cs, ck, pl_remote(P().pl, cs, RG_S_INBOX, g), cur);
-      if (!PIPE && more && !(FAST && aborted)) load_hdr(ns, nk, pl_remote(P().pl, ns, RG_S_INBOX, g), nxt);
+      if (!PIPE && more && !(FAST && aborted))
+        load_hdr(ns, nk, pl_remote(P().pl, ns, RG_S_INBOX, g), nxt, cnt_cls(sel_get<R>(cnt_pf, ns), nk));
       cur = nxt;
       cs = ns;
       ck = nk;
@@ -1705,7 +1718,7 @@ struct Ctl {
     }
     sfor<0, R>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
-      P().cnt_out[((uint64_t)RG_S_SEND * R + j) * P().G + g] = get8(oc, j);
+      P().cnt_out[((uint64_t)RG_S_SEND * R + j) * P().G + g] = get8(oc, j) | (get8(ocls, j) << 8);
     });
     P().jcnt[q] = nj;
     if (P().apply_lo) P().apply_lo[q] = umax64(processed_start, restored_at) + 1;

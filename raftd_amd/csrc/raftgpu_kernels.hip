@@ -472,7 +472,7 @@ __global__ void traffic_kernel(TickParams p, unsigned long long* out6) {
     const bool ld = p.s32[S_ROLE * n + q] == LEADER;
     v[0] += ld;
     for (uint32_t d = 0; d < p.R; ++d) {
-      const uint32_t c = p.cnt_in[((uint64_t)s * p.R + d) * p.G + g];
+      const uint32_t c = cnt_n(p.cnt_in[((uint64_t)s * p.R + d) * p.G + g]);
       v[1] += c;
       for (uint32_t k = 0; k < c; ++k) {
         const uint64_t w0 = p.hdr_in[(((uint64_t)s * p.R + d) * p.K + k) * p.G + g];

@@ -65,7 +65,7 @@ __global__ void plan_kernel(WireParams w) {
   unit_decode(w.umap[u], s, d, j);
   const uint64_t col = (uint64_t)s * w.R + d;
   const uint64_t plane = (uint64_t)w.R * w.R * w.K * w.G;
-  const uint32_t c = min(w.cnt[col * w.G + j], w.K);
+  const uint32_t c = min(cnt_n(w.cnt[col * w.G + j]), w.K);
   uint32_t sz = 0;
   for (uint32_t k = 0; k < c; ++k) {  // 16-B units: header 4, a record per entry, the Cmd chunks
     const uint64_t* h = w.hdr + (col * w.K + k) * w.G + j;
@@ -196,7 +196,7 @@ __global__ void __launch_bounds__(256) pack_kernel(WireParams w) {
   unit_decode(w.umap[u], s, d, j);
   const uint64_t col = (uint64_t)s * w.R + d, qs = (uint64_t)s * w.G + j, n64 = w.nrep;
   const uint64_t plane = (uint64_t)w.R * w.R * w.K * w.G;
-  uint32_t c = w.cnt[col * w.G + j];
+  uint32_t c = cnt_n(w.cnt[col * w.G + j]);
   if (c > w.K) {
     RG_OOB("RG_BOUNDS pack u=%u s=%u d=%u j=%u cnt=%u > K\n", u, s, d, j, c);
     c = 0;
@@ -321,7 +321,7 @@ __global__ void unpack_kernel(WireParams w) {
   }
   const uint8_t* in = region + 256 + table_bytes(nu) + (c ? (tv >> 8) * 16 : 0);
   // malformed data (a count or size beyond the region): keep only the messages before it
-  uint32_t k = 0;
+  uint32_t k = 0, cls = 0;  // cls: the kept messages' classes (cnt_cls), as the sender's count plane has them
   for (; k < c; ++k) {
     if ((uint64_t)(in - w.recv) + 64 > rend) {
       RG_OOB("RG_BOUNDS unpack u=%u k=%u header beyond region end %llu\n", u, k, (unsigned long long)rend);
@@ -377,8 +377,9 @@ __global__ void unpack_kernel(WireParams w) {
     uint64_t* mo = w.rmt + ((col * w.K + k) * w.E) * w.G + j;  // inline ring words (a Propose: length bits)
     for (uint32_t e = 0; e < n; ++e) mo[(uint64_t)e * w.G] = h[8 + 2 * e] & (type == M_PROPOSE ? ~TERM_MASK & ~BANK_BIT & ~TYPE_BIT : ~0ull);
     in += 64 + 16ull * (n + tot);
+    if (k < 4) cls |= msg_class(type, nent) << (2 * k);
   }
-  w.rcnt[col * w.G + j] = k;
+  w.rcnt[col * w.G + j] = k | (cls << 8);
 }
 
 hipError_t launch_wire_plan(const WireParams& w, uint64_t* bounds, hipStream_t st) {

@@ -212,9 +212,14 @@ static void emulate_wire(Host* h, const TickParams& p) {
   for (uint64_t col = 0; col < R * R; ++col) {
     const uint64_t s = col / R, d = col % R;
     for (uint64_t j = 0; j < G; ++j) {
-      uint32_t c = s == d ? 0u : p.cnt_in[col * G + j];
+      uint32_t c = s == d ? 0u : cnt_n(p.cnt_in[col * G + j]);
       if (c > K) c = 0;
-      h->rcnt[col * G + j] = c;
+      uint32_t cls = 0;  // the kept messages' classes, as unpack_kernel recomputes them
+      for (uint32_t k = 0; k < c && k < 4; ++k) {
+        const uint64_t w0k = p.hdr_in[(col * K + k) * G + j];
+        cls |= msg_class((uint32_t)(w0k & 0xFF), (uint32_t)(w0k >> 32)) << (2 * k);
+      }
+      h->rcnt[col * G + j] = c | (cls << 8);
       for (uint32_t k = 0; k < c; ++k) {
         const uint64_t* hs = p.hdr_in + (col * K + k) * G + j;
         uint64_t* ho = h->rhdr.data() + (col * K + k) * G + j;
@@ -457,7 +462,7 @@ int ch_read_msgs(void* hh, uint32_t rid, uint32_t dst, rg_msg_view* out, uint32_
   TickParams t = params(h);
   const uint32_t g = rid / t.R, s = rid % t.R;
   const uint64_t plane = (uint64_t)t.R * t.R * t.K * t.G;
-  const uint32_t cnt = t.cnt_in[((uint64_t)s * t.R + dst) * t.G + g];
+  const uint32_t cnt = cnt_n(t.cnt_in[((uint64_t)s * t.R + dst) * t.G + g]);
   for (uint32_t k = 0; k < cnt && k < cap; ++k) {
     const uint64_t* hp = t.hdr_in + (((uint64_t)s * t.R + dst) * t.K + k) * t.G + g;
     uint64_t w[8];
@@ -537,7 +542,7 @@ int ch_deliver(void* hh, uint32_t rid, const rg_msg_view* m) {  // = deliver_ker
   const uint32_t g = rid / t.R, s = rid % t.R, q = s * t.G + g;
   const uint32_t dst = m->to - 1;
   uint32_t* cnt = const_cast<uint32_t*>(t.cnt_in) + ((uint64_t)s * t.R + dst) * t.G + g;
-  const uint32_t k = *cnt;
+  const uint32_t k = cnt_n(*cnt);  // its class bits stay MC_ALL (0): the receiver loads every word
   if (k >= t.K) return -3;
   rg_msg_view mm = *m;
   if (mm.from == 0) mm.from = (uint8_t)(s + 1);
@@ -550,7 +555,7 @@ int ch_deliver(void* hh, uint32_t rid, const rg_msg_view* m) {  // = deliver_ker
     uint64_t* mt = const_cast<uint64_t*>(t.mt_in) + ((((uint64_t)s * t.R + dst) * t.K + k) * t.E) * t.G + g;
     for (uint32_t e = 0; e < mm.nent; ++e) mt[(uint64_t)e * t.G] = t.tr[((mm.log_index + 1 + e) & (t.L - 1)) * t.nrep + q];
   }
-  *cnt = k + 1;
+  *cnt = (*cnt & ~0xFFu) | (k + 1);
   return 0;
 }
 
