@@ -1491,6 +1491,7 @@ int or_import_replica(or_engine* e, uint32_t rid, const or_replica_view* v, cons
   r->snap_term = v->snap_term;
   r->cap_base = v->cap_base;
   r->restored_at = 0;
+  r->apply_lo = v->processed + 1; /* nothing to apply until it steps */
   r->took = 0;
   r->rq_n = 0;
   r->rd_tick = 0;

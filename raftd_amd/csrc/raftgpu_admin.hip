@@ -187,7 +187,6 @@ __global__ void __launch_bounds__(256) scatter_replica_kernel(AdminParams a, uin
     s64[S_MARKER * N] = v.marker; s64[S_MARKER_TERM * N] = v.marker_term; s64[S_SNAP_INDEX * N] = v.snap_index;
     s64[S_SNAP_TERM * N] = v.snap_term; s64[S_CAP_BASE * N] = v.cap_base; s64[S_PROCESSED * N] = v.processed;
     s64[S_LAST_TERM * N] = v.last > v.marker ? words[v.last - v.marker - 1] & TERM_MASK : v.marker_term;
-    s64[S_FIDX * N] = 0;
     s32[S_ROLE * N] = v.role; s32[S_ETICK * N] = v.election_tick; s32[S_HTICK * N] = v.heartbeat_tick;
     s32[S_RAND_TO * N] = v.rand_timeout; s32[S_RNG_CTR * N] = v.rng_ctr; s32[S_GRANTED * N] = v.granted;
     s32[S_RESPONDED * N] = v.responded; s32[S_ACTIVE * N] = v.active; s32[S_ERR * N] = v.err;
@@ -270,8 +269,8 @@ __global__ void notify_applied_kernel(AdminParams a, const uint32_t* rids, const
 }
 
 // rg_compact: a lane per slot of the shard. Between ticks the next step's input state is
-// s64; the marker moves there as a snapshot's compaction moves it at the end of a step, and S_FIDX
-// makes the next step release the payload stream below entry c + 1 ("Release")
+// s64; the marker moves there as a snapshot's compaction moves it at the end of a step, and the next
+// step, finding it off cap_base, releases the payload stream below entry c + 1 ("Release")
 __global__ void compact_kernel(AdminParams a, uint64_t group, uint64_t index, uint32_t* n) {
   const uint32_t s = threadIdx.x;
   const TickParams& t = a.t;
@@ -283,7 +282,6 @@ __global__ void compact_kernel(AdminParams a, uint64_t group, uint64_t index, ui
   if (c <= marker) return;
   s64[S_MARKER_TERM * N] = t.tr[(c & (t.L - 1)) * N + q] & TERM_MASK;
   s64[S_MARKER * N] = c;
-  s64[S_FIDX * N] = c + 1;
   atomicAdd(n, 1u);
 }
 

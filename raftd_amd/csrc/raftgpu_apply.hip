@@ -67,7 +67,7 @@ __global__ void apply_count_kernel(ApplyParams a) {
   if ((a.slot_mask >> s) & 1u) {
     const uint64_t hi = a.s64[(uint64_t)S_PROCESSED * a.nrep + q];
     bool prev = false;
-    for (uint64_t i = a.apply_lo[q] > 0 ? a.apply_lo[q] : 1; i <= hi; ++i) {
+    for (uint64_t i = feed_apply_lo(a.feed[q], hi); i <= hi; ++i) {
       const uint64_t w = a.tr[(i & (a.L - 1)) * a.nrep + q];
       const bool sel = applies(w);
       if (sel) {
@@ -112,7 +112,7 @@ __global__ void __launch_bounds__(256) apply_gather_kernel(ApplyParams a) {
   const uint64_t hi = a.s64[(uint64_t)S_PROCESSED * n64 + q];
   uint64_t pos = a.off[q], cpos = a.coff[q], rpos = a.roff[q];
   uint64_t carry = 0;  // 1: the candidate before this stretch was selected (its run continues)
-  for (uint64_t i0 = a.apply_lo[q] > 0 ? a.apply_lo[q] : 1; i0 <= hi; i0 += 64) {
+  for (uint64_t i0 = feed_apply_lo(a.feed[q], hi); i0 <= hi; i0 += 64) {
     const uint64_t i = i0 + lane;
     const uint64_t slot = i & (L - 1);
     const uint64_t w = i <= hi ? a.tr[slot * n64 + q] : 0;
@@ -183,7 +183,7 @@ hipError_t launch_apply_gather(const ApplyParams& a, uint64_t nruns, hipStream_t
 
 __device__ __forceinline__ uint64_t persist_first(const PersistParams& a, uint32_t q) {
   const uint64_t n = a.nrep, marker = a.s64[(uint64_t)S_MARKER * n + q];
-  const uint64_t lo = a.full ? marker + 1 : a.persist_lo[q];
+  const uint64_t lo = a.full ? marker + 1 : feed_persist_lo(a.feed[q], a.s64[(uint64_t)S_LAST * n + q]);
   return lo > marker ? lo : marker + 1;
 }
 
@@ -198,7 +198,7 @@ __global__ void persist_count_kernel(PersistParams a) {
   const uint64_t last = a.s64[(uint64_t)S_LAST * n + q], lo = persist_first(a, q);
   const uint32_t ne = lo <= last ? (uint32_t)(last - lo + 1) : 0u;
   // the step recorded whether it wrote entries or changed the hard state (no previous state to diff)
-  const bool changed = a.full || ne > 0 || a.persist_lo[q] != PERSIST_NONE;
+  const bool changed = a.full || ne > 0 || (a.feed[q] & FEED_PERSIST);
   uint32_t cc = 0, tc = 0;
   uint64_t pt = ~0ull;
   for (uint64_t i = lo; i <= last; ++i) {
@@ -325,13 +325,13 @@ hipError_t launch_persist_gather(const PersistParams& a, hipStream_t st) {
 }
 
 // ================================================================== snapshot events
-// control_kernel leaves snap_ev[q] = restored_at | SNAP_TAKEN_BIT per replica; compact the
+// the step leaves FEED_RESTORED / FEED_TAKEN in feed[q] per replica; compact the
 // non-zero ones (thread per replica, coalesced) into rg_snapshot_event records.
 
 __global__ void snap_count_kernel(SnapParams a) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= a.nrep) return;
-  a.cnt[q] = ((a.slot_mask >> (q / a.G)) & 1u) && a.snap_ev[q] != 0 ? 1u : 0u;
+  a.cnt[q] = ((a.slot_mask >> (q / a.G)) & 1u) && (a.feed[q] & (FEED_RESTORED | FEED_TAKEN)) ? 1u : 0u;
 }
 
 hipError_t launch_snap_count(const SnapParams& a, uint64_t* total, hipStream_t st) {
@@ -345,17 +345,18 @@ hipError_t launch_snap_count(const SnapParams& a, uint64_t* total, hipStream_t s
 __global__ void snap_gather_kernel(SnapParams a) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= a.nrep || !a.cnt[q]) return;
-  const uint64_t n = a.nrep, ev = a.snap_ev[q], restored = ev & ~SNAP_TAKEN_BIT;
+  const uint64_t n = a.nrep, ev = a.feed[q];
+  const uint64_t restored = feed_restored_at(ev, a.s64[(uint64_t)S_PROCESSED * n + q]);
   const uint32_t s = q / a.G, j = q - s * a.G;
   rg_snapshot_event r;
   r.group = pl_group(a.pl, s, j);
   r.replica_id = s + 1;
   r.rid = j * a.R + s;
-  r.kind = (restored ? RG_SNAP_RESTORED : 0u) | ((ev & SNAP_TAKEN_BIT) ? RG_SNAP_TAKEN : 0u);
+  r.kind = (ev & FEED_RESTORED ? RG_SNAP_RESTORED : 0u) | ((ev & FEED_TAKEN) ? RG_SNAP_TAKEN : 0u);
   r._pad = 0;
   r.restored = restored;
-  r.index = (ev & SNAP_TAKEN_BIT) ? a.s64[(uint64_t)S_SNAP_INDEX * n + q] : 0;
-  r.term = (ev & SNAP_TAKEN_BIT) ? a.s64[(uint64_t)S_SNAP_TERM * n + q] : 0;
+  r.index = (ev & FEED_TAKEN) ? a.s64[(uint64_t)S_SNAP_INDEX * n + q] : 0;
+  r.term = (ev & FEED_TAKEN) ? a.s64[(uint64_t)S_SNAP_TERM * n + q] : 0;
   reinterpret_cast<rg_snapshot_event*>(a.out)[a.off[q]] = r;
 }
 

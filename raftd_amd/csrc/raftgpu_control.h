@@ -231,7 +231,6 @@ struct Ctl {
   uint64_t lt_i = ~0ull, lt_v = 0;  // term_at cache: index lt_i has term lt_v (~0: none)
   // in-place store (FAST): what the step changed, for the fields it cannot compare at the end
   uint32_t etick0 = 0, drops0 = 0;  // at step start
-  bool fidx0 = false;               // S_FIDX was set (the last step compacted): it is cleared now
   bool ldv = false, cmv = false;    // leader / committed moved
 
   RG_FN Ctl(CTickParams& pp, uint32_t qq) : Ctl(pp, qq / pp.G, qq - (qq / pp.G) * pp.G) {}
@@ -285,15 +284,16 @@ struct Ctl {
       if (role == CANDIDATE) abort_();  // every candidate path (votes, fallback) is the full step's
       if constexpr (ROLE >= 0) role = ROLE;  // the launch's role (the kernel stepped only those lanes)
     }
-    // the last step compacted (or restored) below entry fidx: its stream position bounds the pages
-    // to release, known now that the step which wrote it has stored its {crc, position} (the bulk
-    // kernel). They go back to the pool at the end of this step; the capacity rule keeps lpg until
+    // the last step compacted (or restored) to the marker (it moved off cap_base, the marker that
+    // step started from; rg_compact moves it the same way between ticks): entry marker + 1's stream
+    // position bounds the pages to release, known now that the step which wrote it has stored its
+    // {crc, position} (the bulk kernel). They go back to the pool at the end of this step; the capacity rule keeps lpg until
     // then, so a page read in this launch is never reassigned in it
     lpg_ = b[S_LPG * n];
     {
       uint32_t nlpg = lpg_;
-      if (const uint64_t fi = a[S_FIDX * n]) {
-        fidx0 = true;
+      if (marker != cap_base) {
+        const uint64_t fi = marker + 1;
         uint32_t bound = hw;
         if (fi <= last) {
           const uint64_t sl = fi & (P().L - 1), bank = *tr_at(fi) >> 63;
@@ -1650,8 +1650,8 @@ struct Ctl {
     uint64_t* a = P().s64 + q;
     uint32_t* b = P().s32 + q;
     const bool lmv = last != last_start, mmv = marker != marker_start;
-    // the persistence feed (rg_persist_collect): entries written, else whether the hard state changed
-    uint64_t plo = wlo;
+    // the persistence feed (rg_persist_collect): entries written (wlo), or whether the hard state changed
+    bool hs;
     if constexpr (FAST) {
       constexpr bool LD = ROLE == (int)LEADER;
       if (RGX(!LD && ldv)) a[S_LEADER * n] = leader;
@@ -1674,7 +1674,6 @@ struct Ctl {
       if (RGX(cbv)) a[S_CAP_BASE * n] = cap_base;
       // compaction moved the marker: the stream below entry marker + 1 is released by the next step,
       // once this step's bulk kernel has stored that entry's position
-      if (RGX(mmv || fidx0)) a[S_FIDX * n] = mmv ? marker + 1 : 0;
       if (RGX(lmv || mmv)) a[S_LAST_TERM * n] = last > marker ? (lt_i == last ? lt_v : *tr_at(last) & TERM_MASK) : marker_term;
       if (RGX2(LD || etick != etick0)) b[S_ETICK * n] = etick;
       if (RGX2(drops != drops0)) b[S_DROPS * n] = drops;
@@ -1690,17 +1689,14 @@ struct Ctl {
         });
       }
       // term and vote do not change on the fast path
-      if (plo == ~0ull && (cmv || lmv || mmv || took)) plo = PERSIST_HS;
+      hs = cmv || lmv || mmv || took;
     } else {
-      if (plo == ~0ull && P().persist_lo &&
-          (a[S_TERM * n] != term || a[S_VOTE * n] != vote || a[S_COMMITTED * n] != committed || lmv || mmv ||
-           a[S_SNAP_INDEX * n] != snap_index))
-        plo = PERSIST_HS;
+      hs = P().feed && (a[S_TERM * n] != term || a[S_VOTE * n] != vote || a[S_COMMITTED * n] != committed ||
+                        lmv || mmv || a[S_SNAP_INDEX * n] != snap_index);
       a[S_TERM * n] = term; a[S_VOTE * n] = vote; a[S_LEADER * n] = leader; a[S_COMMITTED * n] = committed;
       a[S_APPLIED * n] = applied; a[S_LAST * n] = last; a[S_MARKER * n] = marker; a[S_MARKER_TERM * n] = marker_term;
       a[S_SNAP_INDEX * n] = snap_index; a[S_SNAP_TERM * n] = snap_term; a[S_CAP_BASE * n] = cap_base;
       a[S_PROCESSED * n] = processed; a[S_CC_HI * n] = cc_hi;
-      a[S_FIDX * n] = mmv ? marker + 1 : 0;
       a[S_LAST_TERM * n] = last > marker ? (lt_i == last ? lt_v : *tr_at(last) & TERM_MASK) : marker_term;
       b[S_ROLE * n] = role; b[S_ETICK * n] = etick; b[S_HTICK * n] = htick; b[S_RAND_TO * n] = rand_to;
       b[S_RNG_CTR * n] = rng_ctr; b[S_GRANTED * n] = granted; b[S_RESPONDED * n] = responded;
@@ -1721,9 +1717,10 @@ struct Ctl {
       P().cnt_out[((uint64_t)RG_S_SEND * R + j) * P().G + g] = get8(oc, j) | (get8(ocls, j) << 8);
     });
     P().jcnt[q] = nj;
-    if (P().apply_lo) P().apply_lo[q] = umax64(processed_start, restored_at) + 1;
-    if (P().persist_lo) P().persist_lo[q] = plo;
-    if (P().snap_ev) P().snap_ev[q] = restored_at | (took ? SNAP_TAKEN_BIT : 0ull);
+    // a restore moved processed to restored_at > processed_start, and commits only grow after it
+    if (P().feed)
+      P().feed[q] = feed_word(processed, umax64(processed_start, restored_at), last, wlo, wlo != ~0ull || hs,
+                              restored_at != 0, took);
   }
 #undef RG_GET
 #undef RG_SET

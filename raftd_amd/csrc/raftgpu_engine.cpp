@@ -245,7 +245,7 @@ struct rg_engine {
   uint64_t x_recv_cap = 0;
   bool self_via_transport = false;  // RAFTGPU_RCCL_SELF=rccl (tests): no in-place region to self
   // committed-entry copy-back (raftgpu_apply.hip)
-  uint64_t* apply_lo = nullptr;
+  uint64_t* feed = nullptr;  // [nrep] the last tick's hand-off words (feed_word: apply window, persist, snapshots)
   uint32_t* small_rest = nullptr;  // BulkParams::rest
   uint64_t* rest_tick = nullptr;   // BulkParams::rest_tick
   uint32_t *acnt = nullptr, *accnt = nullptr, *arcnt = nullptr;
@@ -266,8 +266,6 @@ struct rg_engine {
   uint64_t a_dcap[2] = {0, 0}, a_hcap[2] = {0, 0}, a_n[2] = {0, 0};
   bool a_used[2] = {false, false};
   // persistence copy-back
-  uint64_t* persist_lo = nullptr;
-  uint64_t* snap_ev = nullptr;  // [nrep] restored_at | SNAP_TAKEN_BIT of the last tick
   uint32_t* prof = nullptr;     // RG_CTL_PROFILE builds: control phase stamps of the last tick
   uint32_t *pscnt = nullptr, *pecnt = nullptr, *pccnt = nullptr, *ptcnt = nullptr;
   uint64_t *psoff = nullptr, *peoff = nullptr, *pcoff = nullptr, *ptoff = nullptr;
@@ -412,9 +410,7 @@ static TickParams params_at(rg_engine* e, uint64_t tk) {
   p.rhdr = e->rhdr; p.rmt = e->rmt; p.rcnt = e->rcnt;
   p.slab_info = e->slab_info;
   p.rdst = e->rdst;
-  p.apply_lo = e->apply_lo;
-  p.persist_lo = e->persist_lo;
-  p.snap_ev = e->snap_ev;
+  p.feed = e->feed;
   p.prof = e->prof;
   p.info = e->info;
   p.pool = e->poolctl;
@@ -490,7 +486,8 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if (!cfg || !out) return fail(RG_EINVAL, "null argument");
   const rg_config& c = *cfg;
   if (c.groups < 1 || c.replicas < 1 || c.replicas > RG_MAX_REPLICAS) return fail(RG_EINVAL, "groups/replicas");
-  if (!pow2(c.log_capacity) || c.log_capacity < 16) return fail(RG_EINVAL, "log_capacity must be a power of two >= 16");
+  if (!pow2(c.log_capacity) || c.log_capacity < 16 || c.log_capacity > (1u << 28))
+    return fail(RG_EINVAL, "log_capacity must be a power of two in [16, 2^28]");
   if (c.payload_bytes && (!pow2(c.payload_bytes) || c.payload_bytes < 16 || c.payload_bytes > 1024))
     return fail(RG_EINVAL, "payload_bytes must be 0 or a power of two in [16, 1024]");
   if (c.max_entries_per_msg < 1 || c.max_entries_per_msg > 64) return fail(RG_EINVAL, "max_entries_per_msg in 1..64");
@@ -598,7 +595,7 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if (rc == RG_OK) rc = dalloc(e, &e->d_tp, (uint64_t)TP_SLOTS * sizeof(TickParams));
   if (rc == RG_OK && hipHostMalloc((void**)&e->h_tp, (uint64_t)TP_SLOTS * sizeof(TickParams), 0) != hipSuccess)
     rc = fail(RG_ENOMEM, "hipHostMalloc (parameter blocks)");
-  if (rc == RG_OK) rc = dalloc(e, &e->apply_lo, n * 8);
+  if (rc == RG_OK) rc = dalloc(e, &e->feed, n * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->acnt, n * 4);
   if (rc == RG_OK) rc = dalloc(e, &e->accnt, n * 4);
   if (rc == RG_OK) rc = dalloc(e, &e->aoff, (n + 1) * 8);
@@ -609,8 +606,6 @@ int rg_create(const rg_config* cfg, rg_engine** out) {
   if (rc == RG_OK && hipMemset(e->rest_tick, 0xFF, 8) != hipSuccess) rc = fail(RG_EHIP, "hipMemset (rest stamp)");
   if (rc == RG_OK) rc = dalloc(e, &e->aroff, (n + 1) * 8);
   if (rc == RG_OK) rc = dalloc(e, &e->absum, ((n + 1023) / 1024 + 1) * 8);
-  if (rc == RG_OK) rc = dalloc(e, &e->persist_lo, n * 8);
-  if (rc == RG_OK) rc = dalloc(e, &e->snap_ev, n * 8);
 #ifdef RG_CTL_PROFILE
   if (rc == RG_OK) rc = dalloc(e, &e->prof, n * 12 * 4);
 #endif
@@ -938,9 +933,7 @@ int rg_bootstrap(rg_engine* e) {
   const uint64_t R = e->c.replicas, G = e->c.groups;
   for (int b = 0; b < 2; ++b) HIPCHK(hipMemsetAsync(e->cnt[b], 0, R * R * G * 4, e->stream));
   if (e->rcnt) HIPCHK(hipMemsetAsync(e->rcnt, 0, R * R * G * 4, e->stream));
-  HIPCHK(hipMemsetAsync(e->apply_lo, 0, (uint64_t)e->nrep * 8, e->stream));
-  HIPCHK(hipMemsetAsync(e->persist_lo, 0xFF, (uint64_t)e->nrep * 8, e->stream));
-  HIPCHK(hipMemsetAsync(e->snap_ev, 0, (uint64_t)e->nrep * 8, e->stream));
+  HIPCHK(hipMemsetAsync(e->feed, 0, (uint64_t)e->nrep * 8, e->stream));
   e->planned = e->wire_ready = false;
   e->recv = nullptr;
   RGCHK(stage_reset(e));
@@ -1887,7 +1880,7 @@ int rg_import_replica(rg_engine* e, uint32_t rid, const rg_replica_view* v, cons
                                 (uint32_t)nch, status, e->stream));
   {  // no snapshot event, pending or ready read until it steps (device rows are indexed by q = s·G + g)
     const uint64_t q = (uint64_t)(rid % e->c.replicas) * e->c.groups + rid / e->c.replicas;
-    HIPCHK(hipMemsetAsync(e->snap_ev + q, 0, 8, e->stream));
+    HIPCHK(hipMemsetAsync(e->feed + q, 0, 8, e->stream));  // nothing to apply or persist either
     HIPCHK(hipMemsetAsync(e->rdst + (uint64_t)RQ_N * e->nrep + q, 0, 8, e->stream));
     HIPCHK(hipMemsetAsync(e->rdst + (uint64_t)RD_TICK * e->nrep + q, 0, 8, e->stream));
   }
@@ -1974,7 +1967,7 @@ static PersistParams persist_params(rg_engine* e, bool full, uint32_t slot_mask)
   a.G = t.G; a.R = t.R; a.nrep = t.nrep; a.L = t.L; a.P = t.P; a.pl = e->pl;
   a.full = (full || e->t == 0) ? 1u : 0u;  // before the first tick there is no previous state
   a.slot_mask = slot_mask;
-  a.s64 = t.s64; a.s32 = t.s32; a.persist_lo = e->persist_lo;
+  a.s64 = t.s64; a.s32 = t.s32; a.feed = e->feed;
   a.tr = e->tr; a.info = e->info; a.pool = e->pool; a.pt = e->pt; a.PTS = e->PTS; a.zi = e->crc_tab + CRC_ZI_OFF;
   a.scnt = e->pscnt; a.ecnt = e->pecnt; a.ccnt = e->pccnt; a.tcnt = e->ptcnt;
   a.soff = e->psoff; a.eoff = e->peoff; a.coff = e->pcoff; a.toff = e->ptoff;
@@ -2044,7 +2037,7 @@ static ApplyParams apply_params(rg_engine* e, uint32_t slot_mask) {
   const TickParams t = params(e);
   ApplyParams a{};
   a.G = t.G; a.R = t.R; a.nrep = t.nrep; a.L = t.L; a.P = t.P; a.slot_mask = slot_mask; a.pl = e->pl;
-  a.s64 = t.s64; a.apply_lo = e->apply_lo; a.tr = e->tr; a.info = e->info;
+  a.s64 = t.s64; a.feed = e->feed; a.tr = e->tr; a.info = e->info;
   a.pool = e->pool; a.pt = e->pt; a.PTS = e->PTS;
   a.zi = e->crc_tab + CRC_ZI_OFF;
   a.cnt = e->acnt; a.ccnt = e->accnt; a.off = e->aoff; a.coff = e->acoff; a.bsum = e->absum;
@@ -2205,7 +2198,7 @@ int rg_snapshot_events(rg_engine* e, uint32_t slot_mask, rg_snapshot_event* even
   const TickParams t = params(e);
   SnapParams a{};
   a.G = t.G; a.R = t.R; a.nrep = t.nrep; a.slot_mask = slot_mask; a.pl = e->pl;
-  a.s64 = t.s64; a.snap_ev = e->snap_ev;
+  a.s64 = t.s64; a.feed = e->feed;
   a.cnt = e->acnt; a.off = e->aoff; a.bsum = e->absum;
   LAUNCH(launch_snap_count(a, (uint64_t*)e->d_sum, e->stream), e->stream, "snapshot count");
   uint64_t total = 0;
@@ -2374,7 +2367,7 @@ int rg_get_update(rg_engine* e, uint32_t slot_mask, uint32_t flags, rg_update* o
   ApplyParams aa = apply_params(e, slot_mask);
   SnapParams sa{};
   sa.G = t.G; sa.R = t.R; sa.nrep = t.nrep; sa.slot_mask = slot_mask; sa.pl = e->pl;
-  sa.s64 = t.s64; sa.snap_ev = e->snap_ev; sa.rdst = e->rdst; sa.tick = e->t;
+  sa.s64 = t.s64; sa.feed = e->feed; sa.rdst = e->rdst; sa.tick = e->t;
   sa.cnt = e->uscnt; sa.off = e->usoff; sa.bsum = e->absum;
   SnapParams ra = sa;
   ra.cnt = e->urcnt; ra.off = e->uroff;

@@ -148,7 +148,6 @@ enum : uint32_t {
   S_TERM, S_VOTE, S_LEADER, S_COMMITTED, S_APPLIED, S_LAST, S_MARKER, S_MARKER_TERM, S_SNAP_INDEX,
   S_SNAP_TERM, S_CAP_BASE, S_PROCESSED,
   S_CC_HI,  // highest index a ConfigChange entry was written to (the apply scan stops there)
-  S_FIDX,   // compaction (or a restore) in the last step: the stream below this entry's position is free
   S_LAST_TERM,  // the term of entry S_LAST (S_MARKER_TERM when the log is empty above the marker): the
                 // step's first term lookup without a ring read (one scattered line per replica at C5)
   S64_ROWS
@@ -275,10 +274,7 @@ struct TickParams {
   RG_G(const uint64_t) rhdr;
   RG_G(const uint64_t) rmt;
   RG_G(const uint32_t) rcnt;
-  RG_G(uint64_t) apply_lo;      // [nrep] first index this step hands to the state machine (NULL: skip)
-  RG_G(uint64_t) persist_lo;    // [nrep] lowest index written this step; PERSIST_NONE if none and the hard
-                                //   state is unchanged, PERSIST_HS if none but the hard state changed (NULL: skip)
-  RG_G(uint64_t) snap_ev;       // [nrep] restored_at | SNAP_TAKEN_BIT (NULL: skip)
+  RG_G(uint64_t) feed;          // [nrep] the step's hand-off word (feed_*, below; NULL: skip)
   RG_G(uint32_t) prof;          // RG_CTL_PROFILE builds only: [6][nrep] s_memtime stamps per phase
   RG_G(uint64_t) job64;         // [J64_ROWS][J][nrep]
   RG_G(uint32_t) job32;         // [J32_ROWS][J][nrep]
@@ -466,7 +462,7 @@ struct ApplyParams {
   uint32_t slot_mask;       // replicas whose slot bit is set
   Placement pl;
   const uint64_t* s64;      // current state (applied)
-  const uint64_t* apply_lo;
+  const uint64_t* feed;     // the last step's hand-off words (its apply window)
   const uint64_t* tr;
   const uint2* info;
   const uint8_t* pool;
@@ -486,17 +482,36 @@ struct ApplyParams {
                             // RG_UPDATE_PERSIST: the host holds every committed Cmd from a persist section)
 };
 hipError_t launch_apply_count(const ApplyParams& a, uint64_t* totals /*[3]: entries, chunks, runs*/, hipStream_t s);
-// persist_lo of a step that wrote no entry: PERSIST_NONE (hard state unchanged too) or PERSIST_HS (term,
-// vote, commit, last, marker or snapshot index changed). Either is above every log index, so the
-// entry window [persist_lo, last] is empty; with state in place there is no previous copy to diff
-constexpr uint64_t PERSIST_NONE = ~0ull, PERSIST_HS = ~0ull - 1;
+// The step's hand-off word per replica (one 8-byte store; rg_get_update reads it with the state rows):
+//   bits 0..31   apply window length n: entries (processed - n, processed] went to the state machine
+//   bits 32..60  persist back b: entries [last - b + 1, last] were written in the step (0: none)
+//   bit 61       a snapshot was restored at processed - n (the apply window starts above it)
+//   bit 62       persist: the step wrote entries or changed the hard state (term, vote, commit, last,
+//                marker or snapshot index) — with state in place there is no previous copy to diff
+//   bit 63       the step took a snapshot
+// All zero (bootstrap, an imported replica until it steps): nothing to apply, persist or report.
+// The lengths fit: a step applies and writes at most log_capacity (<= 2^28) entries.
+constexpr uint64_t FEED_RESTORED = 1ull << 61, FEED_PERSIST = 1ull << 62, FEED_TAKEN = 1ull << 63;
+RG_HD_INLINE uint64_t feed_word(uint64_t processed, uint64_t apply_from, uint64_t last, uint64_t wlo,
+                                bool persist, bool restored, bool took) {
+  return (processed - apply_from) | (wlo <= last ? (last - wlo + 1) << 32 : 0ull) |
+         (restored ? FEED_RESTORED : 0ull) | (persist ? FEED_PERSIST : 0ull) | (took ? FEED_TAKEN : 0ull);
+}
+RG_HD_INLINE uint64_t feed_apply_lo(uint64_t f, uint64_t processed) { return processed - (uint32_t)f + 1; }
+RG_HD_INLINE uint64_t feed_restored_at(uint64_t f, uint64_t processed) {
+  return (f & FEED_RESTORED) ? processed - (uint32_t)f : 0ull;
+}
+// the lowest index written (~0: none, the entry window [lo, last] is empty)
+RG_HD_INLINE uint64_t feed_persist_lo(uint64_t f, uint64_t last) {
+  const uint64_t b = (f >> 32) & ((1ull << 29) - 1);
+  return b ? last - b + 1 : ~0ull;
+}
 // snapshot events (raftgpu_apply.hip)
-constexpr uint64_t SNAP_TAKEN_BIT = 1ull << 63;
 struct SnapParams {
   uint32_t G, R, nrep, slot_mask;
   Placement pl;
-  const uint64_t* s64;      // current state (snap_index, snap_term)
-  const uint64_t* snap_ev;
+  const uint64_t* s64;      // current state (snap_index, snap_term, processed)
+  const uint64_t* feed;     // the last step's hand-off words (FEED_RESTORED / FEED_TAKEN)
   const uint64_t* rdst;     // ReadIndex state (read results)
   uint64_t tick;            // the ticks run so far (a read made ready in the last one has RD_TICK == tick)
   uint32_t* cnt;
@@ -518,7 +533,7 @@ struct PersistParams {
   Placement pl;
   const uint64_t* s64;       // current state
   const uint32_t* s32;       // current state (membership)
-  const uint64_t* persist_lo;  // control's: the lowest index written, or PERSIST_NONE / PERSIST_HS
+  const uint64_t* feed;      // the last step's hand-off words (FEED_PERSIST, the entries written)
   const uint64_t* tr;
   const uint2* info;
   const uint8_t* pool;

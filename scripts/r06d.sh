@@ -1,0 +1,21 @@
+#!/bin/bash
+# r06d: one hand-off word per replica (feed) instead of three rows; no S_FIDX row.
+# rehearsals of the N > 1 step through both exchanges (span-timed bulk).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+STEPS="smoke tests bench" bash scripts/gpu_round.sh || exit 1
+line() {  # line NAME ARGS...
+  local n=$1; shift
+  timeout -k 10 300 python bench.py --no-cpu-baseline "$@" > gpurun_out/r06d_$n.log 2>&1 || { tail -5 gpurun_out/r06d_$n.log; exit 1; }
+  python3 -c "
+import json; d=json.loads([l for l in open('gpurun_out/r06d_$n.log') if l.startswith('{')][-1])
+x=d.get('exchange') or {}
+print('$n', round(d['ms_per_step'],4), 'untimed', round(d['ms_per_step_without_timing_events'],4), {k: round(v,4) for k,v in d['kernels_ms'].items()}, 'frac', round(d['roofline']['frac'],3), 'errs', d['replicas_with_invariant_errors'], 'pool', d.get('pool_after_timed_ticks'), 'bound_ms', x.get('bound_ms'), 'summed', d['roofline'].get('bulk_ms_summed_over_halves'))"
+}
+line c5 --groups 1048576 --entries 1 --steps 10 --warmup 3
+line c2 --groups 4096 --steps 100 --warmup 10
+line c2p0 --groups 4096 --payload 0 --steps 100 --warmup 10
+line rehearse_torch --wire-all --placement spread --steps 10 --warmup 3
+line rehearse_c --wire-all --placement spread --exchange c --steps 10 --warmup 3
+bash scripts/profile.sh r06d_c5 --groups 1048576 --entries 1 --steps 10 --warmup 3 --no-cpu-baseline || exit 1

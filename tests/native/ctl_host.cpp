@@ -510,7 +510,6 @@ int ch_import(void* hh, uint32_t rid, const rg_replica_view* v, const uint64_t* 
   s32[S_DROPS * N] = v->drops;
   s32[S_MEMBERS * N] = v->members; s32[S_SNAP_MEMBERS * N] = v->snap_members; s32[S_CC_PENDING * N] = v->cc_pending;
   s64[S_CC_HI * N] = v->last;  // any imported entry may be a ConfigChange
-  s64[S_FIDX * N] = 0;
   const uint32_t R = h->c.replicas;
   for (uint32_t j = 0; j < R; ++j) {
     h->rem[(0 * R + j) * N + q] = v->match[j];
