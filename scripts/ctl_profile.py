@@ -1,6 +1,6 @@
 """Where control_kernel's time goes: phase stamps of an RG_CTL_PROFILE build at 64K x 3 steady
 state (every leader proposes 64 entries per tick).
-usage: python scripts/ctl_profile.py build_variants/ctlprof.so [groups]"""
+usage: python scripts/ctl_profile.py build_variants/ctlprof.so [groups [payload_bytes]]"""
 import ctypes as C
 import os
 import sys
@@ -12,7 +12,8 @@ import numpy as np  # noqa: E402
 from raftd_amd.engine import Engine  # noqa: E402
 
 G, R, E = int(sys.argv[2]) if len(sys.argv) > 2 else 65536, 3, 64
-eng = Engine(groups=G, replicas=R, log_capacity=2048, payload_bytes=256, max_entries_per_msg=E)
+P = int(sys.argv[3]) if len(sys.argv) > 3 else 256
+eng = Engine(groups=G, replicas=R, log_capacity=2048, payload_bytes=P, max_entries_per_msg=E)
 eng.bootstrap()
 eng.tick()
 camp = np.zeros(G * R, np.uint8)
