@@ -1574,6 +1574,14 @@ int or_notify_applied(or_engine* e, uint32_t rid, uint64_t index) {
 
 /* Snapshot events of replica rid's last step (rg_snapshot_events): returns OR_SNAP_* bits;
  * restored = the index an InstallSnapshot restored the log to, index/term = the snapshot taken. */
+/* the first index replica rid's last step handed to the state machine (its apply window starts
+ * there; tests compare the engine's hand-off word with it) */
+int or_debug_apply_lo(const or_engine* e, uint32_t rid, uint64_t* apply_lo) {
+  if (rid >= e->nrep || !apply_lo) return -1;
+  *apply_lo = e->reps[rid].apply_lo;
+  return 0;
+}
+
 int or_get_snapshot_event(const or_engine* e, uint32_t rid, uint64_t* restored, uint64_t* index, uint64_t* term) {
   if (rid >= e->nrep) return -1;
   const rep_t* r = &e->reps[rid];

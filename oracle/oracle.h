@@ -196,6 +196,8 @@ int or_get_read_ready(const or_engine* e, uint32_t rid, uint64_t* ctx, uint64_t*
  * rg_digest. */
 int or_digest(const or_engine* e, uint64_t out[2]);
 int or_get_snapshot_event(const or_engine* e, uint32_t rid, uint64_t* restored, uint64_t* index, uint64_t* term);
+/* the first index rid's last step handed to the state machine (tests: the engine's hand-off word) */
+int or_debug_apply_lo(const or_engine* e, uint32_t rid, uint64_t* apply_lo);
 /* Proposal payload generator: the synthetic Cmd of a tick-input proposal, len payload_bytes. */
 void or_payload(const or_engine* e, uint32_t slab, uint32_t group, uint32_t entry, uint8_t* out);
 uint32_t or_crc32(const uint8_t* p, size_t n);

@@ -127,6 +127,7 @@ def lib():
         L.or_get_applied.argtypes = [vp, u32, C.c_void_p, C.c_void_p, C.c_void_p, u32]
         L.or_get_snapshot_event.argtypes = [vp, u32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                             C.POINTER(C.c_uint64)]
+        L.or_debug_apply_lo.argtypes = [vp, u32, C.POINTER(C.c_uint64)]
         L.or_import_replica.argtypes = [vp, u32, C.POINTER(ReplicaView), C.c_void_p, C.c_void_p, C.c_void_p,
                                         C.c_void_p]
         L.or_propose.argtypes = [vp, C.POINTER(Proposal), C.c_size_t, C.c_void_p, C.c_void_p]
@@ -302,6 +303,12 @@ class Oracle:
             out.append((idx[k], ev[k].len, ev[k].crc, bytes(pay[at:at + ev[k].len])))
             at += ev[k].len
         return out
+
+    def apply_lo(self, rid):
+        """The first index rid's last step handed to the state machine (its apply window's start)."""
+        v = C.c_uint64()
+        assert self.L.or_debug_apply_lo(self.h, rid, C.byref(v)) == 0
+        return v.value
 
     def snapshot_event(self, rid):
         """(kind, restored, index, term) of rid's last step (oracle side of rg_snapshot_events)."""

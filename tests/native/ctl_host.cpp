@@ -28,6 +28,7 @@ struct Host {
                             // handed off after writing state (its in-place rows must be untouched)
   std::vector<uint2> slab_info;  // [nslab][G][E] {0, len}: synthetic Cmds are P bytes; ch_propose sets lengths
   std::vector<uint64_t> rdst;     // ReadIndex state rows
+  std::vector<uint64_t> feed;     // the step's hand-off words (feed_word), as on the device
   std::vector<uint64_t> rd;       // rg_read_index staging: ctx per (group, slot), 0 = none
   bool rd_staged = false;
   std::vector<uint8_t> pt;        // rg_propose staging: target slot, count, non-empty mask per group
@@ -74,6 +75,7 @@ static TickParams params(Host* h) {
   p.job64 = h->job64.data(); p.job32 = h->job32.data(); p.jcnt = h->jcnt.data();
   p.slab_info = h->slab_info.data();
   p.rdst = h->rdst.data();
+  p.feed = h->feed.data();
   return p;
 }
 
@@ -111,6 +113,7 @@ void* ch_create(const rg_config* c) {
   h->job64.assign(J64_ROWS * J * n, 0);
   h->job32.assign(J32_ROWS * J * n, 0);
   h->jcnt.assign(n, 0);
+  h->feed.assign(n, 0);
   h->wire = c->wire_all != 0;
   h->slab_info.assign((size_t)c->num_slabs * (h->wire ? n : G) * E, make_uint2(0u, c->payload_bytes));
   if (h->wire) {
@@ -504,6 +507,7 @@ int ch_import(void* hh, uint32_t rid, const rg_replica_view* v, const uint64_t* 
   s64[S_MARKER * N] = v->marker; s64[S_MARKER_TERM * N] = v->marker_term; s64[S_SNAP_INDEX * N] = v->snap_index;
   s64[S_SNAP_TERM * N] = v->snap_term; s64[S_CAP_BASE * N] = v->cap_base; s64[S_PROCESSED * N] = v->processed;
   s64[S_LAST_TERM * N] = v->last > v->marker ? terms[v->last - v->marker - 1] & TERM_MASK : v->marker_term;
+  h->feed[q] = 0;  // nothing to apply, persist or report until it steps (rg_import_replica)
   s32[S_ROLE * N] = v->role; s32[S_ETICK * N] = v->election_tick; s32[S_HTICK * N] = v->heartbeat_tick;
   s32[S_RAND_TO * N] = v->rand_timeout; s32[S_RNG_CTR * N] = v->rng_ctr; s32[S_GRANTED * N] = v->granted;
   s32[S_RESPONDED * N] = v->responded; s32[S_ACTIVE * N] = v->active; s32[S_ERR * N] = v->err;
@@ -555,6 +559,22 @@ int ch_deliver(void* hh, uint32_t rid, const rg_msg_view* m) {  // = deliver_ker
     for (uint32_t e = 0; e < mm.nent; ++e) mt[(uint64_t)e * t.G] = t.tr[((mm.log_index + 1 + e) & (t.L - 1)) * t.nrep + q];
   }
   *cnt = (*cnt & ~0xFFu) | (k + 1);
+  return 0;
+}
+
+// replica rid's hand-off word of the last step, decoded as rg_get_update's kernels decode it:
+// {first index applied, restored index (0: none), took a snapshot, persist (entries written or the
+// hard state changed), lowest index written (~0: none)}
+int ch_feed(void* hh, uint32_t rid, uint64_t* out) {
+  Host* h = (Host*)hh;
+  if (rid >= h->nrep) return -1;
+  const uint32_t q = qof(h, rid);
+  const uint64_t n = h->nrep, f = h->feed[q], processed = h->s64[S_PROCESSED * n + q], last = h->s64[S_LAST * n + q];
+  out[0] = feed_apply_lo(f, processed);
+  out[1] = feed_restored_at(f, processed);
+  out[2] = (f & FEED_TAKEN) ? 1 : 0;
+  out[3] = (f & FEED_PERSIST) ? 1 : 0;
+  out[4] = feed_persist_lo(f, last);
   return 0;
 }
 

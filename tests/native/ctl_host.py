@@ -167,6 +167,14 @@ class CtlHost:
         n = self.L.ch_read_ready(C.c_void_p(self.h), rid, c, i, 8)
         return [(c[k], i[k]) for k in range(n)]
 
+    def feed(self, rid) -> dict:
+        """Replica rid's hand-off word of the last step, decoded as the device's rg_get_update kernels
+        decode it (raftgpu_internal.h feed_*)."""
+        out = (C.c_uint64 * 5)()
+        self.L.ch_feed.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
+        assert self.L.ch_feed(C.c_void_p(self.h), rid, out) == 0
+        return dict(apply_lo=out[0], restored=out[1], took=bool(out[2]), persist=bool(out[3]), persist_lo=out[4])
+
     def config_change(self, group, slot, op, target) -> int:
         """rg_config_change's staging on the CPU harness (the caller validates)."""
         fn = self.L.ch_config_change

@@ -52,6 +52,12 @@ def xcheck(kind, seed, G, R, T, p_cc=0.0, wire_all=0, p_read=0.0, **cfg):
         for rid in range(G * R):
             vb = b.replica(rid)
             assert a.replica(rid) == vb, (seed, t, rid)
+            # the step's hand-off word (apply window, snapshot events) decodes to the oracle's
+            f, (kind, restored, _, _) = a.feed(rid), b.snapshot_event(rid)
+            assert (f["apply_lo"], f["restored"], f["took"]) == (b.apply_lo(rid), restored, bool(kind & 1)), \
+                (seed, t, rid, f)
+            if f["persist_lo"] != 2 ** 64 - 1:  # entries written: the word marks the persist bit too
+                assert f["persist"] and f["persist_lo"] <= vb["last"], (seed, t, rid, f)
             if p_read:
                 assert a.read_ready(rid) == b.read_ready(rid), (seed, t, rid)
             for d in range(R):
