@@ -47,6 +47,49 @@ def test_corrupt_parameter_block_is_reported_and_harmless():
     assert gpu.pool_stats()["free"] == before["free"]
 
 
+def test_parameter_blocks_are_copied_once_per_chunk_in_steady_state():
+    """launch_control_slot copies a chunk of 32 parameter blocks at once, speculated for the next ticks
+    with the same inputs, and a tick whose block differs copies its own. Steady ticks then issue one copy
+    per 32 ticks; ticks whose inputs change (no proposals, a campaign) copy their own block. Every
+    replica equals the oracle through both."""
+    G, R, E = 96, 3, 8
+    cfg = dict(groups=G, replicas=R, log_capacity=256, payload_bytes=64, max_entries_per_msg=E,
+               snapshot_entries=40, compaction_overhead=3, seed=0xB10C)
+    gpu, ora = make("gpu", **cfg), make("c", **cfg)
+    fn = gpu.L.rg_debug_param_copies
+    fn.argtypes, fn.restype = [C.c_void_p, C.POINTER(C.c_uint64)], C.c_int
+    n = C.c_uint64()
+
+    def copies():
+        assert fn(gpu.h, C.byref(n)) == 0
+        return n.value
+
+    for e in (gpu, ora):
+        e.bootstrap()
+    camp = np.zeros(G * R, np.uint8)
+    camp[0::R] = 1
+    pt, pc = np.zeros(G, np.uint8), np.full(G, E, np.uint32)
+    for t in range(6):
+        ins = dict(campaign=camp) if t == 1 else {}
+        gpu.tick(**ins)
+        ora.tick(**ins)
+    c0 = copies()
+    for t in range(96):  # steady: the same inputs every tick
+        gpu.tick(prop_target=pt, prop_count=pc)
+        ora.tick(prop_target=pt, prop_count=pc)
+    steady = copies() - c0
+    assert steady <= 96 // 32 + 1, steady
+    c1 = copies()
+    for t in range(24):  # inputs change every other tick: each changed tick copies its own block
+        ins = dict(prop_target=pt, prop_count=pc) if t % 2 else {}
+        gpu.tick(**ins)
+        ora.tick(**ins)
+    assert copies() - c1 >= 10
+    for rid in range(G * R):
+        assert gpu.replica(rid) == ora.replica(rid), rid
+    gpu.sync()
+
+
 @pytest.mark.parametrize("fb", ["0", "1"])
 def test_control_fast_path_covers_the_steady_state(fb, monkeypatch):
     """The benchmark's steady state (leaders with full batches every tick, snapshots and compaction)
