@@ -95,6 +95,9 @@ __global__ void __launch_bounds__(POOL_BLOCK) pool_kernel(PoolParams pp) {
   if (pp.ctl->param_err) return;
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x, lane = lane_id(), w = threadIdx.x >> 6;
   const bool valid = q < pp.nrep;
+  // ids below limit were published by an earlier launch (bulk_kernel) and do not change in this one:
+  // loaded with the state rows, not after the block's reservations (one round trip fewer)
+  const unsigned long long limit = pp.ctl->limit;
   const uint64_t n = pp.nrep, PTSM = pp.PTS - 1;
   uint32_t lpg = 0, apg = 0, nlpg = 0, top = 0, f = 0, a = 0;
   if (valid) {
@@ -125,7 +128,6 @@ __global__ void __launch_bounds__(POOL_BLOCK) pool_kernel(PoolParams pp) {
   }
   __syncthreads();
   const unsigned long long fb = base[0] + wf[w], ab = base[1] + wa[w];
-  const unsigned long long limit = pp.ctl->limit;
   const bool ok = ab + ao + a <= limit;
   // Frees and takes are done by the whole wave, 64 consecutive page-table entries / ring slots per
   // instruction. Lane by lane, a compaction tick's frees (64 pages per replica) touched 64 cache lines
