@@ -3,7 +3,8 @@
 // After each step dragonboat hands a replica's newly committed entries to the state machine
 // (rsm → IOnDiskStateMachine.Update), which raftd forwards as POST /UpdateEntries
 // (/root/reference/raft/state_machine.go:136-166). Here a tick leaves, per replica, the window
-// (apply_lo - 1, applied] it applied (control_kernel; ranges restored from a snapshot excluded:
+// [apply_lo, processed] it handed over, as a length in its hand-off word (feed_word; control_kernel;
+// ranges restored from a snapshot excluded:
 // those reach the application through RecoverFromSnapshot, not Update). These kernels gather the
 // non-empty application entries of that window — config changes and leader no-ops are not
 // Update()d — into one contiguous batch so that only newly committed data crosses PCIe, in a

@@ -454,7 +454,7 @@ hipError_t launch_copy_to_host(const void* src, void* dst, uint64_t bytes, hipSt
 hipError_t launch_sum_committed(const TickParams& p, unsigned long long* out, hipStream_t s);
 hipError_t launch_traffic(const TickParams& p, unsigned long long* out6, hipStream_t s);
 // committed-entry copy-back (raftgpu_apply.hip): after a tick, the application entries each replica
-// applied in it, (apply_lo - 1, applied], gathered for IOnDiskStateMachine.Update as runs of
+// handed over in it, [apply_lo, processed] (feed_apply_lo), gathered for IOnDiskStateMachine.Update as runs of
 // consecutive indices (rg_apply_run) + a {len, crc} per entry (rg_apply_cmd); payloads packed back
 // to back, each rounded up to 16 B
 struct ApplyParams {
